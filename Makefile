@@ -1,0 +1,35 @@
+# libgeoflink_hip.so -- MI355X (gfx950) window-evaluation hot path, plus the test oracle.
+# -ffp-contract=off on host AND device: Java never fuses a*b+c, and the exact prefilters
+# (smax, cell thresholds) must see the same rounding on both sides.
+HIPCC    ?= /opt/rocm/bin/hipcc
+ARCH     ?= gfx950
+HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -ffp-contract=off -fno-fast-math \
+            -Wall -Wno-unused-function -Wno-unused-result -Wno-unused-value
+SRC      := spatialflink_amd/csrc
+OBJDIR   := build/obj
+LIB      := spatialflink_amd/libgeoflink_hip.so
+SOURCES  := $(SRC)/api.cpp $(SRC)/k_points.hip $(SRC)/k_knn.hip $(SRC)/k_range.hip $(SRC)/k_join.hip
+OBJECTS  := $(patsubst $(SRC)/%,$(OBJDIR)/%.o,$(SOURCES))
+HEADERS  := include/geoflink_hip.h $(SRC)/gf_internal.hpp $(SRC)/gf_numerics.hpp
+
+all: $(LIB) oracle
+
+$(OBJDIR)/%.o: $(SRC)/% $(HEADERS)
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
+
+$(LIB): $(OBJECTS)
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(OBJECTS)
+
+oracle:
+	$(MAKE) -s -C oracle
+
+# gfx950 ISA listing for inspection (v_fma_f64 must not appear in the distance paths)
+isa: $(LIB)
+	/opt/rocm/lib/llvm/bin/clang-offload-bundler --list --type=o --input=$(OBJDIR)/k_knn.hip.o
+
+clean:
+	rm -rf build $(LIB)
+	$(MAKE) -s -C oracle clean
+
+.PHONY: all oracle clean isa

@@ -1,0 +1,212 @@
+/*
+ * geoflink_hip.h -- C ABI of libgeoflink_hip.so, the MI355X (gfx950) window-evaluation
+ * hot path of GeoFlink / SpatialFlink (reference: marianaGarcez/SpatialFlink).
+ *
+ * This is the drop-in boundary of BASELINE.json's north star: at each window trigger the
+ * Java operators (UniformGrid, PointStream, RangeQuery, KNNQuery, JoinQuery) hand one
+ * window's points across JNI as SoA buffers (x, y, objID, timestamp) and get the window's
+ * result back.  Every entry point cites the reference code it replaces.  Plain C types only
+ * (no torch, no C++); integer status codes, never exceptions or aborts across the boundary
+ * (the reference's System.exit(1) becomes GF_ERR_LAYERS).  INTEGRATION.md shows the JNI
+ * binding a maintainer adds on the Java side.
+ *
+ * Conventions
+ *  - gf_points buffers are DEVICE pointers (HBM-resident windows).  x and y must be
+ *    16-byte aligned (double2 loads).  gf_window_* upload host windows for callers that
+ *    hold host buffers (JNI DirectByteBuffer / primitive arrays).
+ *  - "async" calls only enqueue on the context's stream; "sync" calls return when results
+ *    are on the host.
+ *  - All arithmetic is IEEE binary64, round-to-nearest, no FMA contraction (Java never
+ *    fuses), so cell IDs, range/join sets and kNN (objID, rank) lists match the reference
+ *    restatement bit for bit.
+ */
+#ifndef GEOFLINK_HIP_H
+#define GEOFLINK_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GF_ABI_VERSION 1
+
+/* status codes */
+#define GF_OK             0
+#define GF_ERR_ARG       -1  /* invalid argument (reference: IllegalArgumentException) */
+#define GF_ERR_CAPACITY  -2  /* output capacity too small; the required count is returned */
+#define GF_ERR_HIP       -3  /* HIP runtime error (see gf_ctx_last_error) */
+#define GF_ERR_NOMEM     -4
+#define GF_ERR_LAYERS    -5  /* candidate layers <= 0 where the reference calls System.exit(1)
+                                (UniformGrid.java:272-276, JoinQuery.java:80) */
+#define GF_ERR_ALIGN     -7  /* x / y not 16-byte aligned */
+
+/* distance metric of JTS Coordinate.distance */
+#define GF_METRIC_SQRT  0    /* Math.sqrt(dx*dx + dy*dy) -- default */
+#define GF_METRIC_HYPOT 1    /* Math.hypot(dx, dy) (fdlibm e_hypot) */
+
+/* kernel ids for gf_ctx_timing */
+#define GF_K_KNN_SCAN    0
+#define GF_K_KNN_SAMPLE  1
+#define GF_K_KNN_SELECT  2
+#define GF_K_RANGE_SCAN  3
+#define GF_K_ASSIGN      4
+#define GF_K_JOIN_PROBE  5
+#define GF_K_COUNT       6
+
+typedef struct gf_ctx gf_ctx;
+
+/* UniformGrid(int n, minX, maxX, minY, maxY) -- UniformGrid.java:74-85 (value type) */
+typedef struct {
+  int32_t n;          /* numGridPartitions */
+  int32_t reserved;
+  double minX, maxX, minY, maxY;
+  double cellLength;  /* (maxX - minX) / n, bounds NOT squared */
+} gf_grid;
+
+/* One window of points as device SoA -- Point(objID, x, y, ts, uGrid), Point.java:91-100 */
+typedef struct {
+  const double* x;
+  const double* y;
+  const int64_t* objID;  /* decimal objID string <-> int64; needed by kNN only */
+  const int64_t* ts;     /* timeStampMillisec; unused by window evaluation */
+  int64_t n;
+} gf_points;
+
+/* Query polygons (host CSR) -- Polygon(List<List<Coordinate>>, UniformGrid), Polygon.java:52-66.
+ * Polygon p owns rings [ring_off[p], ring_off[p+1]); ring j owns vertices
+ * [vert_off[j], vert_off[j+1]).  Ring 0 is the shell; rings are closed (first == last). */
+typedef struct {
+  int32_t npoly;
+  const int32_t* ring_off;
+  const int32_t* vert_off;
+  const double* vx;
+  const double* vy;
+} gf_polygons;
+
+/* ---- library / context ------------------------------------------------------------- */
+int         gf_abi_version(void);
+const char* gf_status_string(int status);
+int         gf_device_count(int* n);
+/* One context per calling thread / Flink subtask; binds `device`, owns scratch + a stream. */
+int         gf_ctx_create(int device, gf_ctx** out);
+void        gf_ctx_destroy(gf_ctx* ctx);
+/* Borrow a caller stream (hipStream_t) -- e.g. torch's current stream; NULL = own stream. */
+int         gf_ctx_set_stream(gf_ctx* ctx, void* hip_stream);
+void*       gf_ctx_stream(gf_ctx* ctx);
+int         gf_ctx_synchronize(gf_ctx* ctx);
+const char* gf_ctx_last_error(gf_ctx* ctx);
+/* Record HIP events around launches of the kernels in `mask` (bit 1 << GF_K_*; 0 = off). */
+int         gf_ctx_set_timing(gf_ctx* ctx, int mask);
+/* Sync, then return the summed kernel time (ms) and launch count for kernel_id; resets it. */
+int         gf_ctx_timing(gf_ctx* ctx, int kernel_id, double* total_ms, int64_t* launches);
+
+/* ---- grid / cell IDs (host) -------------------------------------------------------- */
+int gf_grid_make(int32_t n, double minX, double maxX, double minY, double maxY, gf_grid* out);
+/* getGuaranteedNeighboringLayers / getCandidateNeighboringLayers -- UniformGrid.java:428-445 */
+int gf_grid_layers(const gf_grid* g, double r, int32_t* guaranteed, int32_t* candidate);
+/* assignGridCellID(Coordinate) -- HelperClass.java:104-116 (host scalar form) */
+int gf_cell_of(const gf_grid* g, double x, double y, int32_t* cx, int32_t* cy);
+/* "%05d%05d" -- HelperClass.java:54-57,118-120; returns GF_ERR_CAPACITY if cap too small */
+int gf_format_cell_id(int32_t cx, int32_t cy, char* buf, int32_t cap);
+/* getIntCellIndices -- HelperClass.java:263-276 */
+int gf_parse_cell_id(const char* id, int32_t* cx, int32_t* cy);
+
+/* ---- K1: grid-cell assignment (async) -----------------------------------------------
+ * Replaces HelperClass.assignGridCellID per point at ingest (Point.java:98).  cx/cy are
+ * device int32[n]: cx = (int)Math.floor((x - minX)/cellLength), Java (int) saturation. */
+int gf_assign_cells(gf_ctx* ctx, const gf_grid* g, const gf_points* pts, int32_t* cx, int32_t* cy);
+
+/* ---- K2: bucketing by cell (async) -- the keyBy(gridID) shuffle (PointPointRangeQuery.java:144-148)
+ * perm: device uint32[n], point indices grouped by cell; cell_start: device uint32[n*n + 2],
+ * bucket b = valid cell cy*n + cx, bucket n*n = out-of-grid points.  Order inside a bucket is
+ * unspecified. */
+int gf_bucket_by_cell(gf_ctx* ctx, const gf_grid* g, const gf_points* pts, uint32_t* perm,
+                      uint32_t* cell_start);
+
+/* ---- range queries ----------------------------------------------------------------- */
+typedef struct gf_range_plan gf_range_plan;
+/* PointPointRangeQuery.run(stream, Set<Point> queryPoints, r) -- guaranteed / candidate cell
+ * sets built once (PointPointRangeQuery.java:119-125); qx/qy host arrays. */
+int  gf_range_pp_plan_create(gf_ctx* ctx, const gf_grid* g, const double* qx, const double* qy,
+                             int32_t nq, double r, int approximate, int metric, gf_range_plan** out);
+/* PointPolygonRangeQuery.run(stream, Set<Polygon>, r) -- PointPolygonRangeQuery.java:138-147 */
+int  gf_range_ppoly_plan_create(gf_ctx* ctx, const gf_grid* g, const gf_polygons* polys, double r,
+                                int approximate, int metric, gf_range_plan** out);
+void gf_range_plan_destroy(gf_range_plan* plan);
+/* Window apply (PointPointRangeQuery.java:150-186 / PointPolygonRangeQuery.java:170-204), async.
+ * bitmap: device uint64[(n+63)/64], bit i = point i emitted.  multi_bitmap (nullable): bit i =
+ * point i emitted once per query point (approximate point-point, C cells).  counts: device
+ * int64[2] = {points emitted, size of the emitted multiset}. */
+int  gf_range_run(gf_range_plan* plan, const gf_points* pts, uint64_t* bitmap,
+                  uint64_t* multi_bitmap, int64_t* counts);
+/* Sync: selection bitmap -> ascending point indices (device uint32[cap]). */
+int  gf_bitmap_to_indices(gf_ctx* ctx, const uint64_t* bitmap, int64_t n, uint32_t* idx,
+                          int64_t cap, int64_t* count);
+
+/* ---- kNN ---------------------------------------------------------------------------- */
+typedef struct gf_knn_plan gf_knn_plan;
+/* PointPointKNNQuery.run(stream, queryPoint, r, k) -- PointPointKNNQuery.java:33,132-150 */
+int    gf_knn_pp_plan_create(gf_ctx* ctx, const gf_grid* g, double qx, double qy, double r,
+                             int32_t k, int metric, gf_knn_plan** out);
+void   gf_knn_plan_destroy(gf_knn_plan* plan);
+/* Candidate-buffer capacity (entries); default 1<<20.  Small values force the exact fallback. */
+int    gf_knn_plan_set_capacity(gf_knn_plan* plan, int64_t cap);
+/* Offset added to the window-local point index in results (a shard's first global index). */
+int    gf_knn_plan_set_index_base(gf_knn_plan* plan, int64_t base);
+/* Result record: gf_knn_header followed by double dist[k], int64 objID[k], int64 idx[k]. */
+typedef struct {
+  int32_t status;        /* 0 = final; 1 = needs the exact fallback (see gf_knn_decode) */
+  int32_t n;             /* entries (<= k) */
+  int32_t k;
+  int32_t flags;
+  int64_t candidates;    /* candidates appended by the scan */
+  double threshold;      /* distance threshold the scan used */
+} gf_knn_header;
+size_t gf_knn_result_bytes(int32_t k);
+/* Per-cell heaps + windowAll merge (PointPointKNNQuery.java:159-200, KNNQuery.java:213-272),
+ * async: writes one result record into device memory `result`. */
+int    gf_knn_enqueue(gf_knn_plan* plan, const gf_points* pts, void* result);
+/* Sync: decode a host copy of the record; if it asks for the exact fallback, run it on pts.
+ * Outputs sorted ascending by (dist, objID): rank = position. */
+int    gf_knn_decode(gf_knn_plan* plan, const gf_points* pts, const void* result_host,
+                     int64_t* objID, double* dist, int64_t* idx, int32_t* n_out);
+/* Sync convenience: enqueue + copy + decode. */
+int    gf_knn_run(gf_knn_plan* plan, const gf_points* pts, int64_t* objID, double* dist,
+                  int64_t* idx, int32_t* n_out);
+/* Merge per-shard top-k records (device, `nrec` contiguous records of gf_knn_result_bytes(k))
+ * into one record (async) -- the windowAll funnel across GPUs after an RCCL all-gather. */
+int    gf_knn_merge_dev(gf_ctx* ctx, int32_t k, const void* records, int32_t nrec, void* result);
+/* Host merge of per-shard sorted lists: top-k distinct objIDs by (dist, objID). */
+int    gf_knn_merge_host(int32_t k, int32_t nlists, const int32_t* counts, const int64_t* objID,
+                         const double* dist, const int64_t* idx, int64_t* out_objID,
+                         double* out_dist, int64_t* out_idx, int32_t* n_out);
+
+/* ---- join (sync) --------------------------------------------------------------------
+ * JoinQuery.getReplicatedPointQueryStream + PointPointJoinQuery.windowBased
+ * (JoinQuery.java:73-90, PointPointJoinQuery.java:124-183).  pairs: device uint32[2*cap]
+ * (ordinary idx, query idx), unordered.  *npairs = pairs found; GF_ERR_CAPACITY if > cap. */
+int gf_join_pp(gf_ctx* ctx, const gf_grid* ugrid, const gf_grid* qgrid, const gf_points* ordinary,
+               const gf_points* query, double r, int approximate, int metric, uint32_t* pairs,
+               int64_t cap, int64_t* npairs);
+
+/* ---- host windows -------------------------------------------------------------------- */
+typedef struct gf_window gf_window;
+/* Library-owned device SoA window with pinned staging; upload is async on the ctx stream. */
+int  gf_window_create(gf_ctx* ctx, int64_t capacity, gf_window** out);
+void gf_window_destroy(gf_window* w);
+int  gf_window_upload(gf_window* w, const double* x, const double* y, const int64_t* objID,
+                      const int64_t* ts, int64_t n);
+int  gf_window_points(gf_window* w, gf_points* out);
+
+/* ---- synthetic input (host) ----------------------------------------------------------
+ * java.util.Random(seed): x = minX + nextDouble()*(maxX-minX), then y likewise, per point
+ * (cf. SyntheticGpsSource.java:23,40-41). */
+int gf_synth_uniform(int64_t seed, int64_t n, double minX, double maxX, double minY, double maxY,
+                     double* x, double* y);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GEOFLINK_HIP_H */

@@ -1,0 +1,940 @@
+/*
+ * geoflink_oracle.c -- TEST INFRASTRUCTURE ONLY.  See geoflink_oracle.h.
+ *
+ * Plain-C restatement of the GeoFlink window-evaluation hot path, "reference-shaped":
+ * string cell IDs, string hash sets for the guaranteed/candidate cells, per-cell
+ * java.util.PriorityQueue heaps and the single-threaded windowAll merge.  Parity is
+ * UNPINNED (no reference fixtures exist and no JVM/JTS is available); every function
+ * cites the reference file:line it restates.  Build: oracle/Makefile (gcc -O2
+ * -ffp-contract=off: Java never fuses a*b+c).
+ */
+#include "geoflink_oracle.h"
+
+#include <float.h>
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ------------------------------------------------------------------------------------ */
+/* Java primitives                                                                      */
+/* ------------------------------------------------------------------------------------ */
+
+/* JLS 5.1.3 narrowing double -> int: NaN -> 0, saturate, else round toward zero. */
+int32_t orc_jint(double v) {
+  if (v != v) return 0;
+  if (v >= 2147483647.0) return 2147483647;
+  if (v <= -2147483648.0) return (int32_t)(-2147483647 - 1);
+  return (int32_t)v;
+}
+
+/* UniformGrid(int uniformGridRows, ...) -- UniformGrid.java:74-85: no squaring of bounds */
+int orc_grid_make(int32_t n, double minX, double maxX, double minY, double maxY, orc_grid* g) {
+  if (!g || n <= 0) return ORC_ERR_ARG;
+  g->n = n;
+  g->minX = minX; g->maxX = maxX; g->minY = minY; g->maxY = maxY;
+  g->cellLength = (maxX - minX) / n;
+  return ORC_OK;
+}
+
+/* HelperClass.assignGridCellID -- HelperClass.java:109-110 */
+void orc_cell_of(const orc_grid* g, double x, double y, int32_t* cx, int32_t* cy) {
+  *cx = orc_jint(floor((x - g->minX) / g->cellLength));
+  *cy = orc_jint(floor((y - g->minY) / g->cellLength));
+}
+
+/* String.format("%05d", i) + String.format("%05d", j) -- HelperClass.java:54-57,118-120.
+ * C printf("%05d") renders negatives as Java does ("-0001"). */
+void orc_cell_id(int32_t cx, int32_t cy, char* buf) { sprintf(buf, "%05d%05d", cx, cy); }
+
+/* removeLeadingZeroesFromString -- HelperClass.java:60-63: replaceFirst("^0+(?!$)","") then
+ * Integer.parseInt.  parseInt of the remainder (optional sign, digits). */
+static int32_t parse_java_int(const char* s, size_t len) {
+  size_t i = 0;
+  /* strip leading zeros but keep the last character */
+  while (i + 1 < len && s[i] == '0') i++;
+  int neg = 0;
+  long long v = 0;
+  if (i < len && (s[i] == '-' || s[i] == '+')) { neg = s[i] == '-'; i++; }
+  for (; i < len; i++) v = v * 10 + (s[i] - '0');
+  return (int32_t)(neg ? -v : v);
+}
+
+/* HelperClass.getIntCellIndices -- HelperClass.java:263-276 */
+void orc_parse_cell_id(const char* id, int32_t* cx, int32_t* cy) {
+  size_t len = strlen(id);
+  *cx = parse_java_int(id, len < 5 ? len : 5);
+  *cy = len > 5 ? parse_java_int(id + 5, len - 5) : 0;
+}
+
+void orc_assign_cells(const orc_grid* g, int64_t n, const double* x, const double* y,
+                      int32_t* cx, int32_t* cy) {
+  for (int64_t i = 0; i < n; i++) orc_cell_of(g, x[i], y[i], &cx[i], &cy[i]);
+}
+
+/* UniformGrid.getGuaranteedNeighboringLayers -- UniformGrid.java:428-439 */
+int32_t orc_guaranteed_layers(const orc_grid* g, double r) {
+  double cellDiagonal = g->cellLength * sqrt(2.0);
+  return orc_jint(floor((r / cellDiagonal) - 1));
+}
+
+/* UniformGrid.getCandidateNeighboringLayers -- UniformGrid.java:441-445 */
+int32_t orc_candidate_layers(const orc_grid* g, double r) { return orc_jint(ceil(r / g->cellLength)); }
+
+/* UniformGrid.validKey -- UniformGrid.java:224-229 */
+static int valid_key(const orc_grid* g, int64_t x, int64_t y) {
+  return x >= 0 && y >= 0 && x < g->n && y < g->n;
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* JTS 1.16.1 numerics (restated; third-party, absent from the reference tree)         */
+/* ------------------------------------------------------------------------------------ */
+
+typedef union { double d; uint64_t u; } dbits;
+static uint32_t hi_word(double x) { dbits b; b.d = x; return (uint32_t)(b.u >> 32); }
+static uint32_t lo_word(double x) { dbits b; b.d = x; return (uint32_t)b.u; }
+static double with_hi(double x, uint32_t hi) {
+  dbits b; b.d = x; b.u = ((uint64_t)hi << 32) | (b.u & 0xffffffffULL); return b.d;
+}
+
+/* fdlibm 5.3 e_hypot.c, which JDK 8 StrictMath.hypot (and Math.hypot) executes. */
+double orc_hypot(double x, double y) {
+  double a, b, t1, t2, y1, y2, w;
+  int32_t j, k, ha, hb;
+  ha = (int32_t)(hi_word(x) & 0x7fffffff);
+  hb = (int32_t)(hi_word(y) & 0x7fffffff);
+  if (hb > ha) { a = y; b = x; j = ha; ha = hb; hb = j; } else { a = x; b = y; }
+  a = with_hi(a, (uint32_t)ha);
+  b = with_hi(b, (uint32_t)hb);
+  if ((ha - hb) > 0x3c00000) return a + b; /* x/y > 2**60 */
+  k = 0;
+  if (ha > 0x5f300000) {                  /* a > 2**500 */
+    if (ha >= 0x7ff00000) {               /* Inf or NaN */
+      w = a + b;
+      if (((ha & 0xfffff) | lo_word(a)) == 0) w = a;
+      if (((hb ^ 0x7ff00000) | lo_word(b)) == 0) w = b;
+      return w;
+    }
+    ha -= 0x25800000; hb -= 0x25800000; k += 600;
+    a = with_hi(a, (uint32_t)ha);
+    b = with_hi(b, (uint32_t)hb);
+  }
+  if (hb < 0x20b00000) {                  /* b < 2**-500 */
+    if (hb <= 0x000fffff) {               /* subnormal b or 0 */
+      if ((hb | lo_word(b)) == 0) return a;
+      t1 = with_hi(0.0, 0x7fd00000);      /* t1 = 2^1022 */
+      b *= t1; a *= t1; k -= 1022;
+    } else {
+      ha += 0x25800000; hb += 0x25800000; k -= 600;
+      a = with_hi(a, (uint32_t)ha);
+      b = with_hi(b, (uint32_t)hb);
+    }
+  }
+  w = a - b;
+  if (w > b) {
+    t1 = with_hi(0.0, (uint32_t)ha);
+    t2 = a - t1;
+    w = sqrt(t1 * t1 - (b * (-b) - t2 * (a + t1)));
+  } else {
+    a = a + a;
+    y1 = with_hi(0.0, (uint32_t)hb);
+    y2 = b - y1;
+    t1 = with_hi(0.0, (uint32_t)(ha + 0x00100000));
+    t2 = a - t1;
+    w = sqrt(t1 * y1 - (w * (-w) - (t1 * y2 + t2 * b)));
+  }
+  if (k != 0) {
+    t1 = with_hi(1.0, hi_word(1.0) + ((uint32_t)k << 20));
+    return t1 * w;
+  }
+  return w;
+}
+
+/* JTS Coordinate.distance(c): dx = x - c.x; dy = y - c.y; sqrt or hypot */
+double orc_distance(double x1, double y1, double x2, double y2, int metric) {
+  double dx = x1 - x2, dy = y1 - y2;
+  if (metric == ORC_METRIC_HYPOT) return orc_hypot(dx, dy);
+  return sqrt(dx * dx + dy * dy);
+}
+
+/* JTS algorithm.Distance.pointToSegment(p, A, B) */
+static double point_to_segment(double px, double py, double ax, double ay, double bx, double by,
+                               int metric) {
+  if (ax == bx && ay == by) return orc_distance(px, py, ax, ay, metric);
+  double len2 = (bx - ax) * (bx - ax) + (by - ay) * (by - ay);
+  double r = ((px - ax) * (bx - ax) + (py - ay) * (by - ay)) / len2;
+  if (r <= 0.0) return orc_distance(px, py, ax, ay, metric);
+  if (r >= 1.0) return orc_distance(px, py, bx, by, metric);
+  double s = ((ay - py) * (bx - ax) - (ax - px) * (by - ay)) / len2;
+  return fabs(s) * sqrt(len2);
+}
+
+/* Exact sign of x1*y2 - y1*x2 for the given doubles (what JTS RobustDeterminant.signOfDet2x2
+ * returns).  Products split exactly with fma, the four-term sum grown as a Shewchuk
+ * nonoverlapping expansion; its sign is the sign of the top nonzero component. */
+static void two_sum(double a, double b, double* s, double* e) {
+  double x = a + b, bv = x - a, av = x - bv;
+  *s = x; *e = (a - av) + (b - bv);
+}
+static int sign_det2x2(double x1, double y1, double x2, double y2) {
+  double p1 = x1 * y2, e1 = fma(x1, y2, -p1);
+  double p2 = y1 * x2, e2 = fma(y1, x2, -p2);
+  double terms[4] = {e1, -e2, p1, -p2};
+  double h[4];
+  int m = 1;
+  h[0] = terms[0];
+  for (int t = 1; t < 4; t++) {
+    double q = terms[t];
+    for (int i = 0; i < m; i++) { double s, e; two_sum(q, h[i], &s, &e); h[i] = e; q = s; }
+    h[m++] = q;
+  }
+  for (int i = m - 1; i >= 0; i--) {
+    if (h[i] > 0) return 1;
+    if (h[i] < 0) return -1;
+  }
+  return 0;
+}
+
+#define LOC_INTERIOR 0
+#define LOC_BOUNDARY 1
+#define LOC_EXTERIOR 2
+
+/* JTS RayCrossingCounter.locatePointInRing / countSegment (1.16: RobustDeterminant on the
+ * translated segment). */
+static int locate_in_ring(double px, double py, const double* vx, const double* vy, int32_t nv) {
+  int crossings = 0;
+  for (int32_t i = 1; i < nv; i++) {
+    double p1x = vx[i], p1y = vy[i], p2x = vx[i - 1], p2y = vy[i - 1];
+    if (p1x < px && p2x < px) continue;
+    if (px == p2x && py == p2y) return LOC_BOUNDARY;
+    if (p1y == py && p2y == py) {
+      double minx = p1x, maxx = p2x;
+      if (minx > maxx) { minx = p2x; maxx = p1x; }
+      if (px >= minx && px <= maxx) return LOC_BOUNDARY;
+      continue;
+    }
+    if (((p1y > py) && (p2y <= py)) || ((p2y > py) && (p1y <= py))) {
+      double x1 = p1x - px, y1 = p1y - py, x2 = p2x - px, y2 = p2y - py;
+      int sgn = sign_det2x2(x1, y1, x2, y2);
+      if (sgn == 0) return LOC_BOUNDARY;
+      if (y2 < y1) sgn = -sgn;
+      if (sgn > 0) crossings++;
+    }
+  }
+  return (crossings & 1) ? LOC_INTERIOR : LOC_EXTERIOR;
+}
+
+typedef struct { double minx, maxx, miny, maxy; } env_t;
+static env_t ring_env(const double* vx, const double* vy, int32_t nv) {
+  env_t e = {vx[0], vx[0], vy[0], vy[0]};
+  for (int32_t i = 1; i < nv; i++) {
+    if (vx[i] < e.minx) e.minx = vx[i];
+    if (vx[i] > e.maxx) e.maxx = vx[i];
+    if (vy[i] < e.miny) e.miny = vy[i];
+    if (vy[i] > e.maxy) e.maxy = vy[i];
+  }
+  return e;
+}
+
+/* JTS PointLocator.locateInPolygonRing: envelope test, then ring location */
+static int locate_in_polygon_ring(double px, double py, const double* vx, const double* vy,
+                                  int32_t nv) {
+  env_t e = ring_env(vx, vy, nv);
+  if (px > e.maxx || px < e.minx || py > e.maxy || py < e.miny) return LOC_EXTERIOR;
+  return locate_in_ring(px, py, vx, vy, nv);
+}
+
+/* JTS Envelope.distance(point envelope) */
+static double env_point_distance(env_t e, double px, double py) {
+  if (!(px > e.maxx || px < e.minx || py > e.maxy || py < e.miny)) return 0.0;
+  double dx = 0.0, dy = 0.0;
+  if (e.maxx < px) dx = px - e.maxx; else if (e.minx > px) dx = e.minx - px;
+  if (e.maxy < py) dy = py - e.maxy; else if (e.miny > py) dy = e.miny - py;
+  if (dx == 0.0) return dy;
+  if (dy == 0.0) return dx;
+  return sqrt(dx * dx + dy * dy);
+}
+
+/* JTS DistanceOp(point, polygon).distance(): containment (PointLocator) then facet
+ * distance over shell then holes (computeMinDistanceLinesPoints). */
+double orc_point_polygon_distance(double px, double py, const orc_polygons* P, int32_t p,
+                                  int metric) {
+  int32_t r0 = P->ring_off[p], r1 = P->ring_off[p + 1];
+  /* computeContainmentDistance: PointLocator.locate(pt, poly) != EXTERIOR -> 0.
+   * Deliberate, documented deviation: a NaN x skips the containment test (JTS would feed
+   * NaN into RobustDeterminant's branch ladder, which is not restated). */
+  if (px == px) {
+    int32_t v0 = P->vert_off[r0], nv = P->vert_off[r0 + 1] - v0;
+    int loc = locate_in_polygon_ring(px, py, P->vx + v0, P->vy + v0, nv);
+    if (loc == LOC_BOUNDARY) return 0.0;
+    if (loc == LOC_INTERIOR) {
+      int inside = 1;
+      for (int32_t h = r0 + 1; h < r1; h++) {
+        int32_t hv0 = P->vert_off[h], hnv = P->vert_off[h + 1] - hv0;
+        int hl = locate_in_polygon_ring(px, py, P->vx + hv0, P->vy + hv0, hnv);
+        if (hl == LOC_INTERIOR) { inside = 0; break; }
+        if (hl == LOC_BOUNDARY) return 0.0;
+      }
+      if (inside) return 0.0;
+    }
+  }
+  /* computeFacetDistance -> computeMinDistance(line, pt) per ring */
+  double minDistance = DBL_MAX;
+  for (int32_t rg = r0; rg < r1; rg++) {
+    int32_t v0 = P->vert_off[rg], nv = P->vert_off[rg + 1] - v0;
+    const double* vx = P->vx + v0;
+    const double* vy = P->vy + v0;
+    if (env_point_distance(ring_env(vx, vy, nv), px, py) > minDistance) continue;
+    for (int32_t i = 0; i < nv - 1; i++) {
+      double dist = point_to_segment(px, py, vx[i], vy[i], vx[i + 1], vy[i + 1], metric);
+      if (dist < minDistance) minDistance = dist;
+      if (minDistance <= 0.0) return minDistance;
+    }
+  }
+  return minDistance;
+}
+
+/* DistanceFunctions.getPointPointEuclideanDistance(lon, lat, lon1, lat1) -- :60-63 */
+static double pp_euclid(double lon, double lat, double lon1, double lat1) {
+  double a = lat1 - lat, b = lon1 - lon;
+  return sqrt(a * a + b * b); /* Math.pow(v, 2) == v*v (fdlibm e_pow special case y==2) */
+}
+/* DistanceFunctions.getPointLineStringNearestBBoxBorderMinEuclideanDistance -- :133-146 */
+static double bbox_border(double x, double y, double x1, double y1, double x2, double y2) {
+  if (x1 == x2) return pp_euclid(x, y, x1, y);
+  else if (y1 == y2) return pp_euclid(x, y, x, y1);
+  return 4.9e-324; /* Double.MIN_VALUE */
+}
+/* DistanceFunctions.getPointPolygonBBoxMinEuclideanDistance -- :150-200 */
+double orc_point_bbox_distance(double x, double y, double x1, double y1, double x2, double y2) {
+  if (x <= x1) {
+    if (y <= y1) return pp_euclid(x, y, x1, y1);
+    else if (y >= y2) return pp_euclid(x, y, x1, y2);
+    else return bbox_border(x, y, x1, y1, x1, y2);
+  } else if (x >= x2) {
+    if (y <= y1) return pp_euclid(x, y, x2, y1);
+    else if (y >= y2) return pp_euclid(x, y, x2, y2);
+    else return bbox_border(x, y, x2, y1, x2, y2);
+  } else {
+    if (y <= y1) return bbox_border(x, y, x1, y1, x2, y1);
+    else if (y >= y2) return bbox_border(x, y, x1, y2, x2, y2);
+    else return 0.0;
+  }
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* String hash set (java.util.HashSet<String> stand-in; iteration order never matters)  */
+/* ------------------------------------------------------------------------------------ */
+
+#define KEYLEN 24
+typedef struct {
+  char* keys;      /* cap * KEYLEN, "" = empty slot */
+  int64_t cap, size;
+} strset;
+
+static uint64_t str_hash(const char* s) {
+  uint64_t h = 1469598103934665603ULL;
+  while (*s) { h ^= (unsigned char)*s++; h *= 1099511628211ULL; }
+  return h;
+}
+static void ss_init(strset* s, int64_t hint) {
+  int64_t cap = 16;
+  while (cap < 2 * hint) cap <<= 1;
+  s->keys = (char*)calloc((size_t)cap, KEYLEN);
+  s->cap = cap; s->size = 0;
+}
+static void ss_free(strset* s) { free(s->keys); s->keys = NULL; s->cap = s->size = 0; }
+static int64_t ss_find(const strset* s, const char* k) {
+  uint64_t m = (uint64_t)s->cap - 1, i = str_hash(k) & m;
+  for (;;) {
+    const char* slot = s->keys + i * KEYLEN;
+    if (!slot[0]) return -1;
+    if (!strcmp(slot, k)) return (int64_t)i;
+    i = (i + 1) & m;
+  }
+}
+static int ss_contains(const strset* s, const char* k) { return ss_find(s, k) >= 0; }
+static int64_t ss_add(strset* s, const char* k);
+static void ss_grow(strset* s) {
+  strset t;
+  ss_init(&t, s->cap);
+  for (int64_t i = 0; i < s->cap; i++)
+    if (s->keys[i * KEYLEN]) ss_add(&t, s->keys + i * KEYLEN);
+  free(s->keys);
+  *s = t;
+}
+/* returns slot index (new or existing) */
+static int64_t ss_add(strset* s, const char* k) {
+  if (2 * (s->size + 1) > s->cap) ss_grow(s);
+  uint64_t m = (uint64_t)s->cap - 1, i = str_hash(k) & m;
+  for (;;) {
+    char* slot = s->keys + i * KEYLEN;
+    if (!slot[0]) { strncpy(slot, k, KEYLEN - 1); s->size++; return (int64_t)i; }
+    if (!strcmp(slot, k)) return (int64_t)i;
+    i = (i + 1) & m;
+  }
+}
+static void ss_add_all(strset* dst, const strset* src) {
+  for (int64_t i = 0; i < src->cap; i++)
+    if (src->keys[i * KEYLEN]) ss_add(dst, src->keys + i * KEYLEN);
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* Guaranteed / candidate cell sets -- UniformGrid.java:165-206, 368-411                */
+/* ------------------------------------------------------------------------------------ */
+
+static int64_t lmax(int64_t a, int64_t b) { return a > b ? a : b; }
+static int64_t lmin(int64_t a, int64_t b) { return a < b ? a : b; }
+
+/* getGuaranteedNeighboringCells(r, String queryGridCellID) -- UniformGrid.java:165-190.
+ * Loop bounds are clipped to the grid (validKey rejects everything outside). */
+static void g_cells_of(const orc_grid* g, double r, const char* cellID, strset* out) {
+  int32_t gl = orc_guaranteed_layers(g, r);
+  char id[32];
+  if (gl == 0) {
+    ss_add(out, cellID);
+  } else if (gl > 0) {
+    int32_t qx, qy;
+    orc_parse_cell_id(cellID, &qx, &qy);
+    for (int64_t i = lmax((int64_t)qx - gl, 0); i <= lmin((int64_t)qx + gl, g->n - 1); i++)
+      for (int64_t j = lmax((int64_t)qy - gl, 0); j <= lmin((int64_t)qy + gl, g->n - 1); j++)
+        if (valid_key(g, i, j)) { orc_cell_id((int32_t)i, (int32_t)j, id); ss_add(out, id); }
+  }
+}
+
+/* getCandidateNeighboringCells(r, String, Set G) -- UniformGrid.java:368-395 */
+static void c_cells_of(const orc_grid* g, double r, const char* cellID, const strset* G,
+                       strset* out) {
+  int32_t cl = orc_candidate_layers(g, r);
+  char id[32];
+  if (cl > 0) {
+    int32_t qx, qy;
+    orc_parse_cell_id(cellID, &qx, &qy);
+    for (int64_t i = lmax((int64_t)qx - cl, 0); i <= lmin((int64_t)qx + cl, g->n - 1); i++)
+      for (int64_t j = lmax((int64_t)qy - cl, 0); j <= lmin((int64_t)qy + cl, g->n - 1); j++)
+        if (valid_key(g, i, j)) {
+          orc_cell_id((int32_t)i, (int32_t)j, id);
+          if (!ss_contains(G, id)) ss_add(out, id);
+        }
+  }
+}
+
+int64_t orc_gc_sets_point(const orc_grid* g, double r, int32_t qcx, int32_t qcy,
+                          int32_t* g_cells, int64_t capG, int64_t* nG,
+                          int32_t* c_cells, int64_t capC, int64_t* nC) {
+  char qid[32];
+  strset G, C;
+  orc_cell_id(qcx, qcy, qid);
+  ss_init(&G, 64); ss_init(&C, 64);
+  g_cells_of(g, r, qid, &G);
+  c_cells_of(g, r, qid, &G, &C);
+  *nG = G.size; *nC = C.size;
+  int64_t w = 0;
+  for (int64_t i = 0; i < G.cap && g_cells; i++)
+    if (G.keys[i * KEYLEN] && w < capG) {
+      orc_parse_cell_id(G.keys + i * KEYLEN, &g_cells[2 * w], &g_cells[2 * w + 1]); w++;
+    }
+  w = 0;
+  for (int64_t i = 0; i < C.cap && c_cells; i++)
+    if (C.keys[i * KEYLEN] && w < capC) {
+      orc_parse_cell_id(C.keys + i * KEYLEN, &c_cells[2 * w], &c_cells[2 * w + 1]); w++;
+    }
+  ss_free(&G); ss_free(&C);
+  return ORC_OK;
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* Range queries                                                                        */
+/* ------------------------------------------------------------------------------------ */
+
+static int64_t emit(int64_t* out, int64_t cap, int64_t cnt, int64_t v) {
+  if (cnt < cap) out[cnt] = v;
+  return cnt + 1;
+}
+
+/* PointPointRangeQuery.run, WindowBased -- PointPointRangeQuery.java:111-187 */
+int64_t orc_range_pp(const orc_grid* g, int64_t n, const double* x, const double* y,
+                     int32_t nq, const double* qx, const double* qy, double r,
+                     int approximate, int metric, int64_t* out_idx, int64_t cap) {
+  strset G, C;
+  char id[32];
+  ss_init(&G, 64); ss_init(&C, 64);
+  /* :122-125 -- sets accumulated query by query */
+  for (int32_t q = 0; q < nq; q++) {
+    int32_t cx, cy;
+    strset Gq, Cq;
+    orc_cell_of(g, qx[q], qy[q], &cx, &cy); /* Point(x, y, uGrid), Point.java:60-67 */
+    orc_cell_id(cx, cy, id);
+    ss_init(&Gq, 64);
+    g_cells_of(g, r, id, &Gq);
+    ss_add_all(&G, &Gq);
+    ss_free(&Gq);
+    ss_init(&Cq, 64);
+    c_cells_of(g, r, id, &G, &Cq);
+    ss_add_all(&C, &Cq);
+    ss_free(&Cq);
+  }
+  int64_t cnt = 0;
+  for (int64_t i = 0; i < n; i++) {
+    int32_t cx, cy;
+    orc_cell_of(g, x[i], y[i], &cx, &cy); /* ingest: Point.java:91-100 */
+    orc_cell_id(cx, cy, id);
+    int inG = ss_contains(&G, id);
+    if (!(ss_contains(&C, id) || inG)) continue; /* filter :135-140 */
+    if (inG) { cnt = emit(out_idx, cap, cnt, i); continue; } /* :154-155 */
+    for (int32_t q = 0; q < nq; q++) {                        /* :158-183 */
+      if (approximate) {
+        cnt = emit(out_idx, cap, cnt, i);
+      } else {
+        double d = orc_distance(qx[q], qy[q], x[i], y[i], metric);
+        if (d <= r) { cnt = emit(out_idx, cap, cnt, i); break; }
+      }
+    }
+  }
+  ss_free(&G); ss_free(&C);
+  return cnt;
+}
+
+/* Polygon(List<List<Coordinate>>, UniformGrid) -- Polygon.java:52-66: bbox of the shell
+ * (HelperClass.getBoundingBox :76-80) and gridIDsSet = every cell under the bbox
+ * (HelperClass.assignGridCellID(bBox) :123-143, no validKey). */
+static void polygon_bbox(const orc_polygons* P, int32_t p, double* x1, double* y1,
+                         double* x2, double* y2) {
+  int32_t r0 = P->ring_off[p];
+  int32_t v0 = P->vert_off[r0], nv = P->vert_off[r0 + 1] - v0;
+  env_t e = ring_env(P->vx + v0, P->vy + v0, nv);
+  *x1 = e.minx; *y1 = e.miny; *x2 = e.maxx; *y2 = e.maxy;
+}
+
+/* PointPolygonRangeQuery.run, WindowBased -- PointPolygonRangeQuery.java:134-205 */
+int64_t orc_range_ppoly(const orc_grid* g, int64_t n, const double* x, const double* y,
+                        const orc_polygons* P, double r, int approximate, int metric,
+                        int64_t* out_idx, int64_t cap) {
+  strset G, C;
+  char id[32];
+  ss_init(&G, 64); ss_init(&C, 64);
+  double* bb = (double*)malloc(sizeof(double) * 4 * (size_t)(P->npoly > 0 ? P->npoly : 1));
+  for (int32_t p = 0; p < P->npoly; p++) {
+    double x1, y1, x2, y2;
+    polygon_bbox(P, p, &x1, &y1, &x2, &y2);
+    bb[4 * p] = x1; bb[4 * p + 1] = y1; bb[4 * p + 2] = x2; bb[4 * p + 3] = y2;
+    int32_t xi1, yi1, xi2, yi2;
+    orc_cell_of(g, x1, y1, &xi1, &yi1);
+    orc_cell_of(g, x2, y2, &xi2, &yi2);
+    /* getGuaranteedNeighboringCells(r, Polygon) -- UniformGrid.java:193-206 */
+    strset Gp, Cp;
+    ss_init(&Gp, 64);
+    for (int64_t a = xi1; a <= xi2; a++)
+      for (int64_t b = yi1; b <= yi2; b++) {
+        orc_cell_id((int32_t)a, (int32_t)b, id);
+        g_cells_of(g, r, id, &Gp);
+      }
+    ss_add_all(&G, &Gp);
+    ss_free(&Gp);
+    /* getCandidateNeighboringCells(r, Polygon, G) -- UniformGrid.java:399-411 */
+    ss_init(&Cp, 64);
+    for (int64_t a = xi1; a <= xi2; a++)
+      for (int64_t b = yi1; b <= yi2; b++) {
+        orc_cell_id((int32_t)a, (int32_t)b, id);
+        c_cells_of(g, r, id, &G, &Cp);
+      }
+    ss_add_all(&C, &Cp);
+    ss_free(&Cp);
+  }
+  int64_t cnt = 0;
+  for (int64_t i = 0; i < n; i++) {
+    int32_t cx, cy;
+    orc_cell_of(g, x[i], y[i], &cx, &cy);
+    orc_cell_id(cx, cy, id);
+    int inG = ss_contains(&G, id);
+    if (!(ss_contains(&C, id) || inG)) continue; /* :157-162 */
+    if (inG) { cnt = emit(out_idx, cap, cnt, i); continue; }
+    for (int32_t p = 0; p < P->npoly; p++) { /* :179-201 */
+      double d = approximate
+                     ? orc_point_bbox_distance(x[i], y[i], bb[4 * p], bb[4 * p + 1], bb[4 * p + 2],
+                                               bb[4 * p + 3])
+                     : orc_point_polygon_distance(x[i], y[i], P, p, metric);
+      if (d <= r) { cnt = emit(out_idx, cap, cnt, i); break; }
+    }
+  }
+  free(bb);
+  ss_free(&G); ss_free(&C);
+  return cnt;
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* kNN                                                                                  */
+/* ------------------------------------------------------------------------------------ */
+
+typedef struct { double d; int64_t obj; int64_t idx; } tup; /* Tuple2<Point, Double> */
+
+/* kNN candidates: cell in C u G and d <= r -- PointPointKNNQuery.java:134-150,167-186 */
+static int64_t knn_candidates(const orc_grid* g, int64_t n, const double* x, const double* y,
+                              const int64_t* objID, double qx, double qy, double r, int metric,
+                              tup** out, int64_t** cell_slot, strset* cells_seen) {
+  strset G, C;
+  char id[32];
+  int32_t qcx, qcy;
+  orc_cell_of(g, qx, qy, &qcx, &qcy);
+  orc_cell_id(qcx, qcy, id);
+  ss_init(&G, 64); ss_init(&C, 64);
+  g_cells_of(g, r, id, &G);
+  c_cells_of(g, r, id, &G, &C);
+  tup* c = (tup*)malloc(sizeof(tup) * (size_t)(n > 0 ? n : 1));
+  int64_t* slot = cell_slot ? (int64_t*)malloc(sizeof(int64_t) * (size_t)(n > 0 ? n : 1)) : NULL;
+  int64_t m = 0;
+  for (int64_t i = 0; i < n; i++) {
+    int32_t cx, cy;
+    orc_cell_of(g, x[i], y[i], &cx, &cy);
+    orc_cell_id(cx, cy, id);
+    if (!(ss_contains(&C, id) || ss_contains(&G, id))) continue;
+    double d = orc_distance(qx, qy, x[i], y[i], metric);
+    if (slot) slot[m] = ss_add(cells_seen, id);
+    if (!(d <= r)) {
+      if (slot) { c[m].d = NAN; c[m].obj = objID[i]; c[m].idx = i; m++; }
+      continue;
+    }
+    c[m].d = d; c[m].obj = objID[i]; c[m].idx = i; m++;
+  }
+  ss_free(&G); ss_free(&C);
+  *out = c;
+  if (cell_slot) *cell_slot = slot;
+  return m;
+}
+
+static int cmp_obj_d_idx(const void* a, const void* b) {
+  const tup* p = (const tup*)a; const tup* q = (const tup*)b;
+  if (p->obj != q->obj) return p->obj < q->obj ? -1 : 1;
+  if (p->d != q->d) return p->d < q->d ? -1 : 1;
+  return p->idx < q->idx ? -1 : (p->idx > q->idx);
+}
+static int cmp_d_obj(const void* a, const void* b) {
+  const tup* p = (const tup*)a; const tup* q = (const tup*)b;
+  if (p->d != q->d) return p->d < q->d ? -1 : 1;
+  if (p->obj != q->obj) return p->obj < q->obj ? -1 : 1;
+  return p->idx < q->idx ? -1 : (p->idx > q->idx);
+}
+
+/* Build contract */
+int32_t orc_knn_contract(const orc_grid* g, int64_t n, const double* x, const double* y,
+                         const int64_t* objID, double qx, double qy, double r, int32_t k,
+                         int metric, int64_t* out_objID, double* out_d, int64_t* out_idx) {
+  if (k <= 0) return ORC_ERR_ARG;
+  tup* c;
+  int64_t m = knn_candidates(g, n, x, y, objID, qx, qy, r, metric, &c, NULL, NULL);
+  qsort(c, (size_t)m, sizeof(tup), cmp_obj_d_idx);
+  int64_t u = 0;
+  for (int64_t i = 0; i < m; i++)
+    if (u == 0 || c[u - 1].obj != c[i].obj) c[u++] = c[i];
+  qsort(c, (size_t)u, sizeof(tup), cmp_d_obj);
+  int32_t nout = (int32_t)(u < k ? u : k);
+  for (int32_t i = 0; i < nout; i++) {
+    out_objID[i] = c[i].obj; out_d[i] = c[i].d; out_idx[i] = c[i].idx;
+  }
+  free(c);
+  return nout;
+}
+
+/* ---- java.util.PriorityQueue<Tuple2<Point,Double>> with
+ *      Comparators.inTuplePointDistanceComparator (utils/Comparators.java:14-32) ---- */
+typedef struct { tup* q; int32_t size, cap; } jpq;
+static int jcmp(const tup* a, const tup* b) { /* max-heap on distance */
+  if (a->d > b->d) return -1;
+  else if (a->d == b->d) return 0;
+  return 1;
+}
+static void jpq_init(jpq* p, int32_t cap) {
+  p->cap = cap > 0 ? cap : 1; p->size = 0; p->q = (tup*)malloc(sizeof(tup) * (size_t)p->cap);
+}
+static void jpq_free(jpq* p) { free(p->q); p->q = NULL; }
+static void jpq_sift_up(jpq* p, int32_t k, tup x) {
+  while (k > 0) {
+    int32_t parent = (k - 1) >> 1;
+    tup e = p->q[parent];
+    if (jcmp(&x, &e) >= 0) break;
+    p->q[k] = e; k = parent;
+  }
+  p->q[k] = x;
+}
+static void jpq_sift_down(jpq* p, int32_t k, tup x) {
+  int32_t half = p->size >> 1;
+  while (k < half) {
+    int32_t child = (k << 1) + 1;
+    tup c = p->q[child];
+    int32_t right = child + 1;
+    if (right < p->size && jcmp(&c, &p->q[right]) > 0) c = p->q[child = right];
+    if (jcmp(&x, &c) <= 0) break;
+    p->q[k] = c; k = child;
+  }
+  p->q[k] = x;
+}
+static void jpq_offer(jpq* p, tup e) {
+  if (p->size >= p->cap) { p->cap *= 2; p->q = (tup*)realloc(p->q, sizeof(tup) * (size_t)p->cap); }
+  int32_t i = p->size++;
+  if (i == 0) p->q[0] = e; else jpq_sift_up(p, i, e);
+}
+static tup jpq_poll(jpq* p) {
+  int32_t s = --p->size;
+  tup result = p->q[0];
+  tup x = p->q[s];
+  if (s != 0) jpq_sift_down(p, 0, x);
+  return result;
+}
+/* remove(Object) -> removeAt(indexOf), identity = point index */
+static void jpq_remove_idx(jpq* p, int64_t idx) {
+  int32_t i = -1;
+  for (int32_t j = 0; j < p->size; j++) if (p->q[j].idx == idx) { i = j; break; }
+  if (i < 0) return;
+  int32_t s = --p->size;
+  if (s == i) return;
+  tup moved = p->q[s];
+  jpq_sift_down(p, i, moved);
+  if (p->q[i].idx == moved.idx) jpq_sift_up(p, i, moved);
+}
+
+typedef struct { int64_t* v; int64_t n, cap; } i64set; /* HashSet<String> objIDs (linear) */
+static int i64_contains(const i64set* s, int64_t v) {
+  for (int64_t i = 0; i < s->n; i++) if (s->v[i] == v) return 1;
+  return 0;
+}
+static void i64_add(i64set* s, int64_t v) {
+  if (i64_contains(s, v)) return;
+  if (s->n == s->cap) { s->cap = s->cap ? 2 * s->cap : 64; s->v = (int64_t*)realloc(s->v, 8 * (size_t)s->cap); }
+  s->v[s->n++] = v;
+}
+static void i64_remove(i64set* s, int64_t v) {
+  for (int64_t i = 0; i < s->n; i++) if (s->v[i] == v) { s->v[i] = s->v[--s->n]; return; }
+}
+
+/* PointPointKNNQuery.windowBased apply (:159-192) + KNNQuery.kNNWinAllEvaluationPointStream
+ * (:213-272).  Cells visited in first-appearance order. */
+int32_t orc_knn_reference(const orc_grid* g, int64_t n, const double* x, const double* y,
+                          const int64_t* objID, double qx, double qy, double r, int32_t k,
+                          int metric, int64_t* out_objID, double* out_d, int64_t* out_idx) {
+  if (k <= 0) return ORC_ERR_ARG; /* new PriorityQueue(k<1) throws */
+  strset cells;
+  ss_init(&cells, n + 16); /* sized so it never rehashes: slot indices stay valid */
+  tup* c;
+  int64_t* slot;
+  int64_t m = knn_candidates(g, n, x, y, objID, qx, qy, r, metric, &c, &slot, &cells);
+  /* group by cell slot, first-appearance order */
+  int64_t* first = (int64_t*)malloc(sizeof(int64_t) * (size_t)cells.cap);
+  int64_t* order = (int64_t*)malloc(sizeof(int64_t) * (size_t)(cells.cap));
+  int64_t ncell = 0;
+  for (int64_t i = 0; i < cells.cap; i++) first[i] = -1;
+  for (int64_t i = 0; i < m; i++)
+    if (first[slot[i]] < 0) { first[slot[i]] = ncell; order[ncell++] = slot[i]; }
+  jpq W;
+  i64set objIDs = {0};
+  jpq_init(&W, k);
+  int status = ORC_OK;
+  for (int64_t ci = 0; ci < ncell && status == ORC_OK; ci++) {
+    jpq pq;
+    jpq_init(&pq, k);
+    for (int64_t i = 0; i < m; i++) {
+      if (slot[i] != order[ci]) continue;
+      double d = c[i].d; /* NaN marks d > r (distance already tested) */
+      if (pq.size < k) {
+        if (d == d) jpq_offer(&pq, c[i]);
+      } else if (d == d) {
+        double largest = pq.q[0].d;
+        if (largest > d) { jpq_poll(&pq); jpq_offer(&pq, c[i]); }
+      }
+    }
+    /* merge -- KNNQuery.java:221-268 */
+    for (int32_t t = 0; t < pq.size; t++) {
+      tup cand = pq.q[t];
+      if (W.size < k) {
+        if (!i64_contains(&objIDs, cand.obj)) {
+          jpq_offer(&W, cand); i64_add(&objIDs, cand.obj);
+        } else {
+          for (int32_t e = 0; e < W.size; e++)
+            if (W.q[e].obj == cand.obj && W.q[e].d > cand.d) {
+              jpq_remove_idx(&W, W.q[e].idx); jpq_offer(&W, cand); break;
+            }
+        }
+      } else {
+        double largest = W.q[0].d;
+        if (largest > cand.d) {
+          if (!i64_contains(&objIDs, cand.obj)) {
+            jpq_poll(&W);
+            if (W.size == 0) { status = ORC_ERR_NPE; break; } /* peek() == null -> NPE */
+            i64_remove(&objIDs, W.q[0].obj); /* the reference's bug: removes the NEW peek */
+            jpq_offer(&W, cand); i64_add(&objIDs, cand.obj);
+          } else {
+            for (int32_t e = 0; e < W.size; e++)
+              if (W.q[e].obj == cand.obj && W.q[e].d > cand.d) {
+                jpq_remove_idx(&W, W.q[e].idx); jpq_offer(&W, cand); break;
+              }
+          }
+        }
+      }
+    }
+    jpq_free(&pq);
+  }
+  int32_t nout = W.size;
+  if (status == ORC_OK)
+    for (int32_t i = 0; i < nout; i++) {
+      out_objID[i] = W.q[i].obj; out_d[i] = W.q[i].d; out_idx[i] = W.q[i].idx;
+    }
+  jpq_free(&W);
+  free(objIDs.v); free(first); free(order); free(c); free(slot);
+  ss_free(&cells);
+  return status == ORC_OK ? nout : status;
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* Join -- JoinQuery.getReplicatedPointQueryStream (:73-90) + PointPointJoinQuery (:124-183) */
+/* ------------------------------------------------------------------------------------ */
+
+int64_t orc_join_pp(const orc_grid* ugrid, const orc_grid* qgrid,
+                    int64_t no, const double* ox, const double* oy,
+                    int64_t nq, const double* qx, const double* qy,
+                    double r, int approximate, int metric, int64_t* out_pairs, int64_t cap) {
+  char id[32];
+  int32_t cl = 0;
+  if (!(r == 0)) {
+    cl = orc_candidate_layers(qgrid, r);
+    if (cl <= 0) return ORC_ERR_LAYERS; /* UniformGrid.java:272-276 System.exit(1) */
+  }
+  /* replicate: cell string -> list of query indices */
+  strset cells;
+  ss_init(&cells, 1024);
+  int64_t nrep = 0, repcap = 1024;
+  int64_t* rep_slot = (int64_t*)malloc(8 * (size_t)repcap);
+  int64_t* rep_q = (int64_t*)malloc(8 * (size_t)repcap);
+  for (int64_t q = 0; q < nq; q++) {
+    int64_t i0, i1, j0, j1;
+    if (r == 0) { /* getNeighboringCells: return girdCellsSet (UniformGrid.java:264-266) */
+      i0 = 0; i1 = qgrid->n - 1; j0 = 0; j1 = qgrid->n - 1;
+    } else {
+      int32_t cx, cy, px, py;
+      orc_cell_of(qgrid, qx[q], qy[q], &cx, &cy);
+      orc_cell_id(cx, cy, id);
+      orc_parse_cell_id(id, &px, &py); /* :279 getIntCellIndices(queryCellID) */
+      i0 = lmax((int64_t)px - cl, 0); i1 = lmin((int64_t)px + cl, qgrid->n - 1);
+      j0 = lmax((int64_t)py - cl, 0); j1 = lmin((int64_t)py + cl, qgrid->n - 1);
+    }
+    for (int64_t i = i0; i <= i1; i++)
+      for (int64_t j = j0; j <= j1; j++) {
+        if (!valid_key(qgrid, i, j)) continue;
+        orc_cell_id((int32_t)i, (int32_t)j, id);
+        if (nrep == repcap) {
+          repcap *= 2;
+          rep_slot = (int64_t*)realloc(rep_slot, 8 * (size_t)repcap);
+          rep_q = (int64_t*)realloc(rep_q, 8 * (size_t)repcap);
+        }
+        rep_slot[nrep] = -1; /* slot assigned after all insertions (set may grow) */
+        rep_q[nrep] = q;
+        ss_add(&cells, id);
+        nrep++;
+      }
+  }
+  /* resolve slots now that the set is final; regenerate ids in the same order */
+  {
+    int64_t t = 0;
+    for (int64_t q = 0; q < nq; q++) {
+      int64_t i0, i1, j0, j1;
+      if (r == 0) { i0 = 0; i1 = qgrid->n - 1; j0 = 0; j1 = qgrid->n - 1; }
+      else {
+        int32_t cx, cy, px, py;
+        orc_cell_of(qgrid, qx[q], qy[q], &cx, &cy);
+        orc_cell_id(cx, cy, id);
+        orc_parse_cell_id(id, &px, &py);
+        i0 = lmax((int64_t)px - cl, 0); i1 = lmin((int64_t)px + cl, qgrid->n - 1);
+        j0 = lmax((int64_t)py - cl, 0); j1 = lmin((int64_t)py + cl, qgrid->n - 1);
+      }
+      for (int64_t i = i0; i <= i1; i++)
+        for (int64_t j = j0; j <= j1; j++) {
+          if (!valid_key(qgrid, i, j)) continue;
+          orc_cell_id((int32_t)i, (int32_t)j, id);
+          rep_slot[t++] = ss_find(&cells, id);
+        }
+    }
+  }
+  /* bucket replicated queries by slot (CSR) */
+  int64_t* off = (int64_t*)calloc((size_t)cells.cap + 1, 8);
+  int64_t* lst = (int64_t*)malloc(8 * (size_t)(nrep > 0 ? nrep : 1));
+  for (int64_t t = 0; t < nrep; t++) off[rep_slot[t] + 1]++;
+  for (int64_t s = 0; s < cells.cap; s++) off[s + 1] += off[s];
+  {
+    int64_t* cur = (int64_t*)malloc(8 * (size_t)cells.cap);
+    memcpy(cur, off, 8 * (size_t)cells.cap);
+    for (int64_t t = 0; t < nrep; t++) lst[cur[rep_slot[t]]++] = rep_q[t];
+    free(cur);
+  }
+  /* window join on gridID: JoinFunction.join per co-located pair (:160-175) */
+  int64_t cnt = 0;
+  for (int64_t p = 0; p < no; p++) {
+    int32_t cx, cy;
+    orc_cell_of(ugrid, ox[p], oy[p], &cx, &cy);
+    orc_cell_id(cx, cy, id);
+    int64_t s = ss_find(&cells, id);
+    if (s < 0) continue;
+    for (int64_t t = off[s]; t < off[s + 1]; t++) {
+      int64_t q = lst[t];
+      if (approximate || orc_distance(ox[p], oy[p], qx[q], qy[q], metric) <= r) {
+        if (cnt < cap) { out_pairs[2 * cnt] = p; out_pairs[2 * cnt + 1] = q; }
+        cnt++;
+      }
+    }
+  }
+  free(off); free(lst); free(rep_slot); free(rep_q);
+  ss_free(&cells);
+  return cnt;
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* Generators                                                                           */
+/* ------------------------------------------------------------------------------------ */
+
+/* HelperClass.generateQueryPolygons -- HelperClass.java:387-421 */
+int32_t orc_generate_query_polygons(int32_t numQueryPolygons, double minX, double minY,
+                                    double maxX, double maxY, double* vx, double* vy, int32_t cap) {
+  int gridSize = 100;
+  double polyLength1 = (maxX - minX) / gridSize;
+  double polyLength2 = (maxY - minY) / gridSize;
+  double polyLength = polyLength2 < polyLength1 ? polyLength2 : polyLength1;
+  int32_t count = 0;
+  for (double i = minX; i < maxX; i += polyLength) {
+    if (count >= numQueryPolygons) break;
+    for (double j = minY; j < maxY; j += polyLength) {
+      if (count < cap) {
+        double* px = vx + 5 * count;
+        double* py = vy + 5 * count;
+        px[0] = i;              py[0] = j;
+        px[1] = i + polyLength; py[1] = j;
+        px[2] = i + polyLength; py[2] = j + polyLength;
+        px[3] = i;              py[3] = j + polyLength;
+        px[4] = i;              py[4] = j;
+      }
+      count++;
+    }
+  }
+  return count;
+}
+
+/* java.util.Random(seed): 48-bit LCG, nextDouble() = ((next(26) << 27) + next(27)) * 2^-53 */
+typedef struct { uint64_t seed; } jrandom;
+static void jr_init(jrandom* r, int64_t seed) {
+  r->seed = ((uint64_t)seed ^ 0x5DEECE66DULL) & ((1ULL << 48) - 1);
+}
+static int32_t jr_next(jrandom* r, int bits) {
+  r->seed = (r->seed * 0x5DEECE66DULL + 0xBULL) & ((1ULL << 48) - 1);
+  return (int32_t)(r->seed >> (48 - bits));
+}
+static double jr_next_double(jrandom* r) {
+  int64_t hi = jr_next(r, 26);
+  int64_t lo = jr_next(r, 27);
+  return (double)((hi << 27) + lo) * 0x1.0p-53;
+}
+
+void orc_java_random_points(int64_t seed, int64_t n, double minX, double maxX,
+                            double minY, double maxY, double* x, double* y) {
+  jrandom r;
+  jr_init(&r, seed);
+  for (int64_t i = 0; i < n; i++) {
+    x[i] = minX + jr_next_double(&r) * (maxX - minX);
+    y[i] = minY + jr_next_double(&r) * (maxY - minY);
+  }
+}

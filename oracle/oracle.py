@@ -1,0 +1,234 @@
+"""ctypes + numpy harness for the C oracle -- TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this
+module.  It is the checker: the product path (spatialflink_amd + libgeoflink_hip.so)
+never imports it.  Parity status of the oracle: "parity unpinned" (see
+oracle/geoflink_oracle.h and DESIGN.md).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_SO = os.path.join(_HERE, "liboracle.so")
+
+METRIC_SQRT = 0
+METRIC_HYPOT = 1
+ERR_LAYERS = -5
+ERR_NPE = -6
+
+
+class OrcGrid(C.Structure):
+    _fields_ = [("n", C.c_int32), ("minX", C.c_double), ("maxX", C.c_double),
+                ("minY", C.c_double), ("maxY", C.c_double), ("cellLength", C.c_double)]
+
+
+class OrcPolygons(C.Structure):
+    _fields_ = [("npoly", C.c_int32), ("ring_off", C.c_void_p), ("vert_off", C.c_void_p),
+                ("vx", C.c_void_p), ("vy", C.c_void_p)]
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_SO):
+            build()
+        L = C.CDLL(_SO)
+        P = C.c_void_p
+        d, i32, i64 = C.c_double, C.c_int32, C.c_int64
+        L.orc_grid_make.argtypes = [i32, d, d, d, d, C.POINTER(OrcGrid)]
+        L.orc_jint.argtypes = [d]; L.orc_jint.restype = i32
+        L.orc_cell_id.argtypes = [i32, i32, C.c_char_p]
+        L.orc_parse_cell_id.argtypes = [C.c_char_p, C.POINTER(i32), C.POINTER(i32)]
+        L.orc_assign_cells.argtypes = [C.POINTER(OrcGrid), i64, P, P, P, P]
+        L.orc_guaranteed_layers.argtypes = [C.POINTER(OrcGrid), d]; L.orc_guaranteed_layers.restype = i32
+        L.orc_candidate_layers.argtypes = [C.POINTER(OrcGrid), d]; L.orc_candidate_layers.restype = i32
+        L.orc_distance.argtypes = [d, d, d, d, C.c_int]; L.orc_distance.restype = d
+        L.orc_hypot.argtypes = [d, d]; L.orc_hypot.restype = d
+        L.orc_gc_sets_point.argtypes = [C.POINTER(OrcGrid), d, i32, i32, P, i64, C.POINTER(i64), P, i64, C.POINTER(i64)]
+        L.orc_range_pp.argtypes = [C.POINTER(OrcGrid), i64, P, P, i32, P, P, d, C.c_int, C.c_int, P, i64]
+        L.orc_range_pp.restype = i64
+        L.orc_point_polygon_distance.argtypes = [d, d, C.POINTER(OrcPolygons), i32, C.c_int]
+        L.orc_point_polygon_distance.restype = d
+        L.orc_point_bbox_distance.argtypes = [d, d, d, d, d, d]; L.orc_point_bbox_distance.restype = d
+        L.orc_range_ppoly.argtypes = [C.POINTER(OrcGrid), i64, P, P, C.POINTER(OrcPolygons), d, C.c_int, C.c_int, P, i64]
+        L.orc_range_ppoly.restype = i64
+        for fn in (L.orc_knn_contract, L.orc_knn_reference):
+            fn.argtypes = [C.POINTER(OrcGrid), i64, P, P, P, d, d, d, i32, C.c_int, P, P, P]
+            fn.restype = i32
+        L.orc_join_pp.argtypes = [C.POINTER(OrcGrid), C.POINTER(OrcGrid), i64, P, P, i64, P, P, d, C.c_int, C.c_int, P, i64]
+        L.orc_join_pp.restype = i64
+        L.orc_generate_query_polygons.argtypes = [i32, d, d, d, d, P, P, i32]
+        L.orc_generate_query_polygons.restype = i32
+        L.orc_java_random_points.argtypes = [i64, i64, d, d, d, d, P, P]
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+def _f64(a):
+    return np.ascontiguousarray(a, dtype=np.float64)
+
+
+def grid(n, minX, maxX, minY, maxY):
+    g = OrcGrid()
+    rc = lib().orc_grid_make(int(n), float(minX), float(maxX), float(minY), float(maxY), C.byref(g))
+    assert rc == 0
+    return g
+
+
+def jint(v):
+    return lib().orc_jint(float(v))
+
+
+def cell_id(cx, cy):
+    buf = C.create_string_buffer(32)
+    lib().orc_cell_id(int(cx), int(cy), buf)
+    return buf.value.decode()
+
+
+def parse_cell_id(s):
+    a, b = C.c_int32(), C.c_int32()
+    lib().orc_parse_cell_id(s.encode(), C.byref(a), C.byref(b))
+    return a.value, b.value
+
+
+def assign_cells(g, x, y):
+    x, y = _f64(x), _f64(y)
+    cx = np.empty(len(x), np.int32)
+    cy = np.empty(len(x), np.int32)
+    lib().orc_assign_cells(C.byref(g), len(x), _p(x), _p(y), _p(cx), _p(cy))
+    return cx, cy
+
+
+def layers(g, r):
+    return lib().orc_guaranteed_layers(C.byref(g), float(r)), lib().orc_candidate_layers(C.byref(g), float(r))
+
+
+def distance(x1, y1, x2, y2, metric=METRIC_SQRT):
+    return lib().orc_distance(float(x1), float(y1), float(x2), float(y2), int(metric))
+
+
+def hypot(a, b):
+    return lib().orc_hypot(float(a), float(b))
+
+
+def gc_sets_point(g, r, qcx, qcy):
+    nG, nC = C.c_int64(), C.c_int64()
+    lib().orc_gc_sets_point(C.byref(g), float(r), int(qcx), int(qcy), None, 0, C.byref(nG), None, 0, C.byref(nC))
+    gc = np.empty((max(nG.value, 1), 2), np.int32)
+    cc = np.empty((max(nC.value, 1), 2), np.int32)
+    lib().orc_gc_sets_point(C.byref(g), float(r), int(qcx), int(qcy), _p(gc), nG.value, C.byref(nG), _p(cc), nC.value, C.byref(nC))
+    gs = {tuple(map(int, v)) for v in gc[: nG.value]}
+    cs = {tuple(map(int, v)) for v in cc[: nC.value]}
+    return gs, cs
+
+
+def range_pp(g, x, y, qx, qy, r, approximate=False, metric=METRIC_SQRT):
+    x, y, qx, qy = _f64(x), _f64(y), _f64(np.atleast_1d(qx)), _f64(np.atleast_1d(qy))
+    cap = max(1024, len(x))
+    while True:
+        out = np.empty(cap, np.int64)
+        cnt = lib().orc_range_pp(C.byref(g), len(x), _p(x), _p(y), len(qx), _p(qx), _p(qy), float(r),
+                                 int(approximate), int(metric), _p(out), cap)
+        if cnt <= cap:
+            return out[:cnt]
+        cap = cnt
+
+
+class Polygons:
+    """CSR polygon set for the oracle: list of polygons, each a list of closed rings."""
+
+    def __init__(self, polys):
+        ring_off, vert_off, vx, vy = [0], [0], [], []
+        for poly in polys:
+            for ring in poly:
+                ring = [tuple(map(float, v)) for v in ring]
+                if ring[0] != ring[-1]:
+                    ring.append(ring[0])
+                vx += [v[0] for v in ring]
+                vy += [v[1] for v in ring]
+                vert_off.append(len(vx))
+            ring_off.append(len(vert_off) - 1)
+        self.ring_off = np.array(ring_off, np.int32)
+        self.vert_off = np.array(vert_off, np.int32)
+        self.vx = np.array(vx, np.float64)
+        self.vy = np.array(vy, np.float64)
+        self.c = OrcPolygons(len(polys), _p(self.ring_off).value, _p(self.vert_off).value,
+                             _p(self.vx).value, _p(self.vy).value)
+
+
+def point_polygon_distance(px, py, P: Polygons, p, metric=METRIC_SQRT):
+    return lib().orc_point_polygon_distance(float(px), float(py), C.byref(P.c), int(p), int(metric))
+
+
+def point_bbox_distance(px, py, x1, y1, x2, y2):
+    return lib().orc_point_bbox_distance(*map(float, (px, py, x1, y1, x2, y2)))
+
+
+def range_ppoly(g, x, y, P: Polygons, r, approximate=False, metric=METRIC_SQRT):
+    x, y = _f64(x), _f64(y)
+    cap = max(1024, len(x))
+    out = np.empty(cap, np.int64)
+    cnt = lib().orc_range_ppoly(C.byref(g), len(x), _p(x), _p(y), C.byref(P.c), float(r),
+                                int(approximate), int(metric), _p(out), cap)
+    assert cnt <= cap
+    return out[:cnt]
+
+
+def knn(g, x, y, objID, qx, qy, r, k, metric=METRIC_SQRT, reference_shaped=False):
+    """Returns (status, objID[n], dist[n], idx[n]); contract output is sorted by (d, objID)."""
+    x, y = _f64(x), _f64(y)
+    objID = np.ascontiguousarray(objID, dtype=np.int64)
+    kk = max(int(k), 1)
+    oo = np.empty(kk, np.int64); od = np.empty(kk, np.float64); oi = np.empty(kk, np.int64)
+    fn = lib().orc_knn_reference if reference_shaped else lib().orc_knn_contract
+    n = fn(C.byref(g), len(x), _p(x), _p(y), _p(objID), float(qx), float(qy), float(r), int(k),
+           int(metric), _p(oo), _p(od), _p(oi))
+    if n < 0:
+        return n, None, None, None
+    return 0, oo[:n], od[:n], oi[:n]
+
+
+def join_pp(ugrid, qgrid, ox, oy, qx, qy, r, approximate=False, metric=METRIC_SQRT):
+    """Returns (status, pairs[m,2]) with status < 0 for the reference's System.exit(1)."""
+    ox, oy, qx, qy = _f64(ox), _f64(oy), _f64(qx), _f64(qy)
+    cap = 1 << 16
+    while True:
+        out = np.empty(2 * cap, np.int64)
+        cnt = lib().orc_join_pp(C.byref(ugrid), C.byref(qgrid), len(ox), _p(ox), _p(oy), len(qx), _p(qx),
+                                _p(qy), float(r), int(approximate), int(metric), _p(out), cap)
+        if cnt < 0:
+            return int(cnt), None
+        if cnt <= cap:
+            return 0, out[: 2 * cnt].reshape(-1, 2)
+        cap = int(cnt)
+
+
+def generate_query_polygons(num, minX, minY, maxX, maxY):
+    cap = num + 256
+    vx = np.empty(5 * cap); vy = np.empty(5 * cap)
+    cnt = lib().orc_generate_query_polygons(int(num), float(minX), float(minY), float(maxX), float(maxY),
+                                            _p(vx), _p(vy), cap)
+    assert cnt <= cap
+    return [[list(zip(vx[5 * i:5 * i + 5].tolist(), vy[5 * i:5 * i + 5].tolist()))] for i in range(cnt)]
+
+
+def java_random_points(seed, n, minX, maxX, minY, maxY):
+    x = np.empty(n); y = np.empty(n)
+    lib().orc_java_random_points(int(seed), int(n), float(minX), float(maxX), float(minY), float(maxY), _p(x), _p(y))
+    return x, y

@@ -1,0 +1,20 @@
+"""spatialflink_amd -- MI355X-native window-evaluation hot path of GeoFlink / SpatialFlink.
+
+The Java operators' per-window bodies (range, kNN, join) run as hand-written HIP kernels
+for gfx950 behind the C ABI in include/geoflink_hip.h; this package is the host-side
+mirror of the reference operator API (UniformGrid, Point, Polygon, QueryConfiguration,
+PointPointRangeQuery, PointPolygonRangeQuery, PointPointKNNQuery, PointPointJoinQuery).
+"""
+from . import _lib
+from .spatialIndices import UniformGrid, generateCellIDStr, getIntCellIndices, padLeadingZeroesToInt
+from .spatialObjects import Point, PointWindow, Polygon, PolygonSet
+from .spatialOperators import (KNNResult, PointPointJoinQuery, PointPointKNNQuery, PointPointRangeQuery,
+                               PointPolygonRangeQuery, QueryConfiguration, QueryType, RangeResult, assign_cells,
+                               bucket_by_cell, knn_merge_host, synthetic_uniform)
+
+__all__ = [
+    "UniformGrid", "Point", "Polygon", "PolygonSet", "PointWindow", "QueryType", "QueryConfiguration",
+    "PointPointRangeQuery", "PointPolygonRangeQuery", "PointPointKNNQuery", "PointPointJoinQuery", "RangeResult",
+    "KNNResult", "knn_merge_host", "assign_cells", "bucket_by_cell", "synthetic_uniform", "generateCellIDStr",
+    "getIntCellIndices", "padLeadingZeroesToInt",
+]

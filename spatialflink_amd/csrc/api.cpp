@@ -1,0 +1,1020 @@
+// api.cpp -- C ABI of libgeoflink_hip.so (include/geoflink_hip.h): contexts, plans built once
+// per continuous query (the reference computes its guaranteed / candidate cell sets once per
+// operator, PointPointRangeQuery.java:119-125), and the per-window entry points.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <limits>
+#include <unordered_set>
+#include <vector>
+
+#include "gf_internal.hpp"
+
+using gf::AxisIv;
+using gf::QueryRect;
+
+// ---------------------------------------------------------------------------------------
+// errors, context plumbing
+// ---------------------------------------------------------------------------------------
+namespace gf {
+
+int set_err(gf_ctx* ctx, int code, const std::string& msg) {
+  if (ctx) ctx->last_error = msg;
+  return code;
+}
+
+int hip_err(gf_ctx* ctx, hipError_t e, const char* what) {
+  char buf[512];
+  snprintf(buf, sizeof buf, "%s: %s", what, hipGetErrorString(e));
+  return set_err(ctx, e == hipErrorOutOfMemory ? GF_ERR_NOMEM : GF_ERR_HIP, buf);
+}
+
+int bind(gf_ctx* ctx) {
+  hipError_t e = hipSetDevice(ctx->device);
+  return e == hipSuccess ? GF_OK : hip_err(ctx, e, "hipSetDevice");
+}
+
+void* ctx_scratch(gf_ctx* ctx, size_t bytes, int* status) {
+  *status = GF_OK;
+  if (bytes <= ctx->scratch_bytes) return ctx->scratch;
+  hipStreamSynchronize(ctx->stream);  // scratch may still be in use by queued work
+  if (ctx->scratch) hipFree(ctx->scratch);
+  ctx->scratch = nullptr;
+  ctx->scratch_bytes = 0;
+  size_t sz = std::max(bytes, (size_t)1 << 20);
+  hipError_t e = hipMalloc(&ctx->scratch, sz);
+  if (e != hipSuccess) { *status = hip_err(ctx, e, "hipMalloc(scratch)"); return nullptr; }
+  ctx->scratch_bytes = sz;
+  return ctx->scratch;
+}
+
+void* ctx_pinned(gf_ctx* ctx, size_t bytes, int* status) {
+  *status = GF_OK;
+  if (bytes <= ctx->pinned_bytes) return ctx->pinned;
+  hipStreamSynchronize(ctx->stream);
+  if (ctx->pinned) hipHostFree(ctx->pinned);
+  ctx->pinned = nullptr;
+  ctx->pinned_bytes = 0;
+  size_t sz = std::max(bytes, (size_t)1 << 16);
+  hipError_t e = hipHostMalloc(&ctx->pinned, sz, hipHostMallocDefault);
+  if (e != hipSuccess) { *status = hip_err(ctx, e, "hipHostMalloc"); return nullptr; }
+  ctx->pinned_bytes = sz;
+  return ctx->pinned;
+}
+
+static hipEvent_t take_event(gf_ctx* ctx) {
+  if (!ctx->pool.empty()) {
+    hipEvent_t e = ctx->pool.back();
+    ctx->pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  hipEventCreate(&e);
+  return e;
+}
+
+KTimer::KTimer(gf_ctx* c, int k) : ctx(c), kid(k) {
+  if (!(ctx->timing & (1 << k))) return;
+  a = take_event(ctx);
+  b = take_event(ctx);
+  hipEventRecord(a, ctx->stream);
+}
+KTimer::~KTimer() {
+  if (!a) return;
+  hipEventRecord(b, ctx->stream);
+  ctx->pending.push_back({a, b, kid});
+}
+
+// Carve several aligned buffers out of one scratch allocation.
+struct Arena {
+  size_t off = 0;
+  template <class T>
+  size_t take(size_t count) {
+    size_t o = (off + 255) & ~(size_t)255;
+    off = o + count * sizeof(T);
+    return o;
+  }
+};
+
+// ---------------------------------------------------------------------------------------
+// Exact cell thresholds.  cell(x) = jint(floor((x - mn)/cl)) is monotone non-decreasing in x
+// over the non-NaN doubles (every step is a monotone rounding), so for any integer A the set
+// {x : cell(x) >= A} is an up-set of the double order: a bisection over the ordered bit
+// patterns finds its first element exactly.  The kernels then compare coordinates with
+// these doubles instead of dividing.
+// ---------------------------------------------------------------------------------------
+static uint64_t okey_of(double d) {
+  uint64_t b = dbits(d);
+  return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+}
+static double of_okey(uint64_t k) {
+  uint64_t b = (k >> 63) ? (k & 0x7fffffffffffffffull) : ~k;
+  return from_bits(b);
+}
+
+static double first_at_least(int64_t A, double mn, double cl) {
+  const double nan = std::numeric_limits<double>::quiet_NaN();
+  if (A <= (int64_t)INT32_MIN) return -INFINITY;
+  if (A > (int64_t)INT32_MAX) return nan;
+  if (cell_index(INFINITY, mn, cl) < A) return nan;
+  if (cell_index(-INFINITY, mn, cl) >= A) return -INFINITY;
+  uint64_t lo = okey_of(-INFINITY), hi = okey_of(INFINITY);  // cell(lo) < A <= cell(hi)
+  while (hi - lo > 1) {
+    uint64_t mid = lo + (hi - lo) / 2;
+    if (cell_index(of_okey(mid), mn, cl) >= A) hi = mid; else lo = mid;
+  }
+  return of_okey(hi);
+}
+
+// doubles whose cell index lies in [a, b]
+static AxisIv axis_iv(int64_t a, int64_t b, double mn, double cl) {
+  const double nan = std::numeric_limits<double>::quiet_NaN();
+  if (a > b) return {nan, nan};
+  AxisIv iv;
+  iv.lo = first_at_least(a, mn, cl);
+  iv.hi_excl = first_at_least(b + 1, mn, cl);
+  return iv;
+}
+
+static QueryRect make_qrect(const gf_grid& g, int32_t qcx, int32_t qcy, int32_t gl, int32_t cl) {
+  QueryRect q;
+  const double nan = std::numeric_limits<double>::quiet_NaN();
+  q.minX = g.minX;
+  q.minY = g.minY;
+  const int64_t n1 = g.n - 1;
+  if (cl > 0) {
+    q.cgx = axis_iv(std::max<int64_t>((int64_t)qcx - cl, 0), std::min<int64_t>((int64_t)qcx + cl, n1), g.minX, g.cellLength);
+    q.cgy = axis_iv(std::max<int64_t>((int64_t)qcy - cl, 0), std::min<int64_t>((int64_t)qcy + cl, n1), g.minY, g.cellLength);
+  } else {
+    q.cgx = q.cgy = {nan, nan};
+  }
+  if (gl > 0) {
+    q.gx = axis_iv(std::max<int64_t>((int64_t)qcx - gl, 0), std::min<int64_t>((int64_t)qcx + gl, n1), g.minX, g.cellLength);
+    q.gy = axis_iv(std::max<int64_t>((int64_t)qcy - gl, 0), std::min<int64_t>((int64_t)qcy + gl, n1), g.minY, g.cellLength);
+  } else if (gl == 0) {  // getGuaranteedNeighboringCells adds the query cell itself, no validKey
+    q.gx = axis_iv(qcx, qcx, g.minX, g.cellLength);
+    q.gy = axis_iv(qcy, qcy, g.minY, g.cellLength);
+  } else {
+    q.gx = q.gy = {nan, nan};
+  }
+  q.g_any = (gl >= 0) && !std::isnan(q.gx.lo) && !std::isnan(q.gy.lo);
+  return q;
+}
+
+static bool grid_ok(const gf_grid* g) {
+  return g && g->n > 0 && std::isfinite(g->minX) && std::isfinite(g->minY) && std::isfinite(g->cellLength) &&
+         g->cellLength > 0.0;
+}
+
+static int check_points(gf_ctx* ctx, const gf_points* p) {
+  if (!p || p->n < 0) return set_err(ctx, GF_ERR_ARG, "invalid gf_points");
+  if (p->n > (int64_t)UINT32_MAX) return set_err(ctx, GF_ERR_ARG, "window larger than 2^32-1 points");
+  if (p->n > 0 && (!p->x || !p->y)) return set_err(ctx, GF_ERR_ARG, "null x/y");
+  if ((((uintptr_t)p->x) | ((uintptr_t)p->y)) & 15) return set_err(ctx, GF_ERR_ALIGN, "x/y must be 16-byte aligned");
+  return GF_OK;
+}
+
+static int stream_blocks(gf_ctx* ctx, int64_t items_per_thread_pairs) {
+  int64_t b = (items_per_thread_pairs + kBlock - 1) / kBlock;
+  const int64_t cap = (int64_t)ctx->num_cus * 8;
+  if (b > cap) b = cap;
+  if (b < 1) b = 1;
+  return (int)b;
+}
+
+}  // namespace gf
+
+using namespace gf;
+
+// ---------------------------------------------------------------------------------------
+// library / context
+// ---------------------------------------------------------------------------------------
+extern "C" int gf_abi_version(void) { return GF_ABI_VERSION; }
+
+extern "C" const char* gf_status_string(int s) {
+  switch (s) {
+    case GF_OK: return "ok";
+    case GF_ERR_ARG: return "invalid argument";
+    case GF_ERR_CAPACITY: return "output capacity too small";
+    case GF_ERR_HIP: return "HIP runtime error";
+    case GF_ERR_NOMEM: return "out of device memory";
+    case GF_ERR_LAYERS: return "candidate layers <= 0 (reference: System.exit(1))";
+    case GF_ERR_ALIGN: return "x/y not 16-byte aligned";
+    default: return "unknown status";
+  }
+}
+
+extern "C" int gf_device_count(int* n) {
+  if (!n) return GF_ERR_ARG;
+  int c = 0;
+  hipError_t e = hipGetDeviceCount(&c);
+  *n = (e == hipSuccess) ? c : 0;
+  return e == hipSuccess ? GF_OK : GF_ERR_HIP;
+}
+
+extern "C" int gf_ctx_create(int device, gf_ctx** out) {
+  if (!out) return GF_ERR_ARG;
+  *out = nullptr;
+  int nd = 0;
+  if (hipGetDeviceCount(&nd) != hipSuccess || device < 0 || device >= nd) return GF_ERR_HIP;
+  gf_ctx* ctx = new gf_ctx();
+  ctx->device = device;
+  if (hipSetDevice(device) != hipSuccess) { delete ctx; return GF_ERR_HIP; }
+  if (hipStreamCreateWithFlags(&ctx->own_stream, hipStreamNonBlocking) != hipSuccess) { delete ctx; return GF_ERR_HIP; }
+  ctx->stream = ctx->own_stream;
+  int cus = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
+    ctx->num_cus = cus;
+  *out = ctx;
+  return GF_OK;
+}
+
+extern "C" void gf_ctx_destroy(gf_ctx* ctx) {
+  if (!ctx) return;
+  hipSetDevice(ctx->device);
+  if (ctx->stream) hipStreamSynchronize(ctx->stream);
+  for (auto& e : ctx->pending) { hipEventDestroy(e.a); hipEventDestroy(e.b); }
+  for (auto e : ctx->pool) hipEventDestroy(e);
+  if (ctx->scratch) hipFree(ctx->scratch);
+  if (ctx->pinned) hipHostFree(ctx->pinned);
+  if (ctx->own_stream) hipStreamDestroy(ctx->own_stream);
+  delete ctx;
+}
+
+extern "C" int gf_ctx_set_stream(gf_ctx* ctx, void* s) {
+  if (!ctx) return GF_ERR_ARG;
+  ctx->stream = s ? (hipStream_t)s : ctx->own_stream;
+  return GF_OK;
+}
+extern "C" void* gf_ctx_stream(gf_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
+
+extern "C" int gf_ctx_synchronize(gf_ctx* ctx) {
+  if (!ctx) return GF_ERR_ARG;
+  GF_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+  return GF_OK;
+}
+
+extern "C" const char* gf_ctx_last_error(gf_ctx* ctx) { return ctx ? ctx->last_error.c_str() : "null context"; }
+
+extern "C" int gf_ctx_set_timing(gf_ctx* ctx, int mask) {
+  if (!ctx) return GF_ERR_ARG;
+  ctx->timing = mask;
+  return GF_OK;
+}
+
+extern "C" int gf_ctx_timing(gf_ctx* ctx, int kid, double* total_ms, int64_t* launches) {
+  if (!ctx || kid < 0 || kid >= GF_K_COUNT) return GF_ERR_ARG;
+  int st = bind(ctx);
+  if (st) return st;
+  GF_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+  for (auto& e : ctx->pending) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, e.a, e.b) == hipSuccess) {
+      ctx->acc_ms[e.kid] += ms;
+      ctx->acc_n[e.kid] += 1;
+    }
+    ctx->pool.push_back(e.a);
+    ctx->pool.push_back(e.b);
+  }
+  ctx->pending.clear();
+  if (total_ms) *total_ms = ctx->acc_ms[kid];
+  if (launches) *launches = ctx->acc_n[kid];
+  ctx->acc_ms[kid] = 0.0;
+  ctx->acc_n[kid] = 0;
+  return GF_OK;
+}
+
+// ---------------------------------------------------------------------------------------
+// grid / cell IDs
+// ---------------------------------------------------------------------------------------
+extern "C" int gf_grid_make(int32_t n, double minX, double maxX, double minY, double maxY, gf_grid* out) {
+  if (!out || n <= 0) return GF_ERR_ARG;
+  out->n = n;
+  out->reserved = 0;
+  out->minX = minX; out->maxX = maxX; out->minY = minY; out->maxY = maxY;
+  out->cellLength = (maxX - minX) / n;  // UniformGrid.java:83
+  return grid_ok(out) ? GF_OK : GF_ERR_ARG;
+}
+
+extern "C" int gf_grid_layers(const gf_grid* g, double r, int32_t* gl, int32_t* cl) {
+  if (!g) return GF_ERR_ARG;
+  if (gl) *gl = guaranteed_layers(g->cellLength, r);
+  if (cl) *cl = candidate_layers(g->cellLength, r);
+  return GF_OK;
+}
+
+extern "C" int gf_cell_of(const gf_grid* g, double x, double y, int32_t* cx, int32_t* cy) {
+  if (!g || !cx || !cy) return GF_ERR_ARG;
+  *cx = cell_index(x, g->minX, g->cellLength);
+  *cy = cell_index(y, g->minY, g->cellLength);
+  return GF_OK;
+}
+
+extern "C" int gf_format_cell_id(int32_t cx, int32_t cy, char* buf, int32_t cap) {
+  if (!buf || cap <= 0) return GF_ERR_ARG;
+  int w = snprintf(buf, (size_t)cap, "%05d%05d", cx, cy);
+  return (w >= 0 && w < cap) ? GF_OK : GF_ERR_CAPACITY;
+}
+
+static int32_t parse_java_int(const char* s, size_t len) {
+  size_t i = 0;
+  while (i + 1 < len && s[i] == '0') i++;  // replaceFirst("^0+(?!$)", "")
+  bool neg = false;
+  long long v = 0;
+  if (i < len && (s[i] == '-' || s[i] == '+')) { neg = s[i] == '-'; i++; }
+  for (; i < len; i++) v = v * 10 + (s[i] - '0');
+  return (int32_t)(neg ? -v : v);
+}
+
+extern "C" int gf_parse_cell_id(const char* id, int32_t* cx, int32_t* cy) {
+  if (!id || !cx || !cy) return GF_ERR_ARG;
+  size_t len = strlen(id);
+  if (len < 6) return GF_ERR_ARG;
+  *cx = parse_java_int(id, 5);
+  *cy = parse_java_int(id + 5, len - 5);
+  return GF_OK;
+}
+
+// ---------------------------------------------------------------------------------------
+// K1 / K2
+// ---------------------------------------------------------------------------------------
+extern "C" int gf_assign_cells(gf_ctx* ctx, const gf_grid* g, const gf_points* pts, int32_t* cx, int32_t* cy) {
+  if (!ctx || !grid_ok(g) || !cx || !cy) return set_err(ctx, GF_ERR_ARG, "gf_assign_cells: bad argument");
+  int st = bind(ctx);
+  if (st) return st;
+  if ((st = check_points(ctx, pts))) return st;
+  if (((uintptr_t)cx | (uintptr_t)cy) & 7) return set_err(ctx, GF_ERR_ALIGN, "cx/cy must be 8-byte aligned");
+  GF_HIP_CHECK(ctx, launch_assign(ctx, g, pts, cx, cy));
+  return GF_OK;
+}
+
+extern "C" int gf_bucket_by_cell(gf_ctx* ctx, const gf_grid* g, const gf_points* pts, uint32_t* perm,
+                                 uint32_t* cell_start) {
+  if (!ctx || !grid_ok(g) || !perm || !cell_start) return set_err(ctx, GF_ERR_ARG, "gf_bucket_by_cell: bad argument");
+  int st = bind(ctx);
+  if (st) return st;
+  if ((st = check_points(ctx, pts))) return st;
+  const int64_t bins = (int64_t)g->n * g->n + 1;
+  if (bins >= (int64_t)INT32_MAX) return set_err(ctx, GF_ERR_ARG, "grid too large for bucketing");
+  const int64_t n = pts->n;
+  Arena ar;
+  size_t o_keys = ar.take<uint32_t>(n > 0 ? n : 1);
+  size_t o_hist = ar.take<uint32_t>(bins);
+  size_t o_cur = ar.take<uint32_t>(bins + 1);
+  size_t o_tmp = ar.take<uint32_t>(scan_tmp_elems(bins));
+  char* base = (char*)ctx_scratch(ctx, ar.off, &st);
+  if (st) return st;
+  uint32_t* keys = (uint32_t*)(base + o_keys);
+  uint32_t* hist = (uint32_t*)(base + o_hist);
+  uint32_t* cur = (uint32_t*)(base + o_cur);
+  uint32_t* tmp = (uint32_t*)(base + o_tmp);
+  GF_HIP_CHECK(ctx, hipMemsetAsync(hist, 0, bins * sizeof(uint32_t), ctx->stream));
+  GF_HIP_CHECK(ctx, launch_cell_keys(ctx->stream, g, pts->x, pts->y, n, 0, keys));
+  GF_HIP_CHECK(ctx, launch_histogram(ctx->stream, keys, n, hist));
+  GF_HIP_CHECK(ctx, launch_exclusive_scan(ctx->stream, hist, bins, cell_start, tmp));
+  GF_HIP_CHECK(ctx, hipMemcpyAsync(cur, cell_start, bins * sizeof(uint32_t), hipMemcpyDeviceToDevice, ctx->stream));
+  GF_HIP_CHECK(ctx, launch_scatter(ctx->stream, keys, n, cur, perm));
+  return GF_OK;
+}
+
+// ---------------------------------------------------------------------------------------
+// range plans
+// ---------------------------------------------------------------------------------------
+namespace {
+
+struct Rect { int64_t x0, x1, y0, y1; };
+
+template <class T>
+int upload(gf_ctx* ctx, T** dst, const std::vector<T>& src) {
+  *dst = nullptr;
+  if (src.empty()) return GF_OK;
+  GF_HIP_CHECK(ctx, hipMalloc(dst, src.size() * sizeof(T)));
+  GF_HIP_CHECK(ctx, hipMemcpy(*dst, src.data(), src.size() * sizeof(T), hipMemcpyHostToDevice));
+  return GF_OK;
+}
+
+void add_rect(std::vector<int32_t>& diff, int64_t n, Rect r) {
+  r.x0 = std::max<int64_t>(r.x0, 0); r.y0 = std::max<int64_t>(r.y0, 0);
+  r.x1 = std::min<int64_t>(r.x1, n - 1); r.y1 = std::min<int64_t>(r.y1, n - 1);
+  if (r.x0 > r.x1 || r.y0 > r.y1) return;
+  const int64_t W = n + 1;
+  diff[r.y0 * W + r.x0] += 1;
+  diff[r.y0 * W + r.x1 + 1] -= 1;
+  diff[(r.y1 + 1) * W + r.x0] -= 1;
+  diff[(r.y1 + 1) * W + r.x1 + 1] += 1;
+}
+
+void prefix2d(std::vector<int32_t>& d, int64_t n) {
+  const int64_t W = n + 1;
+  for (int64_t y = 0; y <= n; ++y)
+    for (int64_t x = 1; x <= n; ++x) d[y * W + x] += d[y * W + x - 1];
+  for (int64_t y = 1; y <= n; ++y)
+    for (int64_t x = 0; x <= n; ++x) d[y * W + x] += d[(y - 1) * W + x];
+}
+
+Rect expand(Rect b, int64_t e) { return {b.x0 - e, b.x1 + e, b.y0 - e, b.y1 + e}; }
+
+// Cell classes and candidate lists for a set of query objects with base cell rects B_o
+// (a query point's cell, or every cell under a polygon's bbox -- Polygon.java:62).
+int build_table(gf_range_plan* P, const std::vector<Rect>& base, bool need_lists) {
+  gf_ctx* ctx = P->ctx;
+  const int64_t n = P->grid.n;
+  const int32_t g = P->g_layers, c = P->c_layers;
+  if (n * n > (int64_t)1 << 30) return set_err(ctx, GF_ERR_ARG, "grid too large for a cell table");
+  std::vector<int32_t> dG((n + 1) * (n + 1), 0), dC((n + 1) * (n + 1), 0);
+  std::vector<int32_t> extra;
+  for (const Rect& b : base) {
+    if (g > 0) add_rect(dG, n, expand(b, g));
+    else if (g == 0) {
+      add_rect(dG, n, b);
+      if (b.x0 < 0 || b.y0 < 0 || b.x1 >= n || b.y1 >= n) {  // out-of-grid guaranteed cells
+        auto cl32 = [](int64_t v) { return (int32_t)std::min<int64_t>(std::max<int64_t>(v, INT32_MIN), INT32_MAX); };
+        extra.push_back(cl32(b.x0)); extra.push_back(cl32(b.x1));
+        extra.push_back(cl32(b.y0)); extra.push_back(cl32(b.y1));
+      }
+    }
+    if (c > 0) add_rect(dC, n, expand(b, c));
+  }
+  prefix2d(dG, n);
+  prefix2d(dC, n);
+  std::vector<uint8_t> table(n * n);
+  for (int64_t y = 0; y < n; ++y)
+    for (int64_t x = 0; x < n; ++x) {
+      const int64_t i = y * (n + 1) + x;
+      table[y * n + x] = dG[i] > 0 ? 2 : (dC[i] > 0 ? 1 : 0);
+    }
+  int st;
+  if ((st = upload(ctx, &P->table, table))) return st;
+  P->n_extra = (int32_t)(extra.size() / 4);
+  if ((st = upload(ctx, &P->extra, extra))) return st;
+  if (!need_lists) return GF_OK;
+  // candidate lists over a (c + 2)-cell reach (superset of every object within r)
+  const int64_t reach = (int64_t)std::max(c, 0) + 2;
+  double area = 0;
+  for (const Rect& b : base) {
+    Rect r = expand(b, reach);
+    r.x0 = std::max<int64_t>(r.x0, 0); r.y0 = std::max<int64_t>(r.y0, 0);
+    r.x1 = std::min<int64_t>(r.x1, n - 1); r.y1 = std::min<int64_t>(r.y1, n - 1);
+    if (r.x0 <= r.x1 && r.y0 <= r.y1) area += double(r.x1 - r.x0 + 1) * double(r.y1 - r.y0 + 1);
+  }
+  if (area > 6.4e7) return GF_OK;  // too large: every candidate-cell point tests every object
+  std::vector<int32_t> off(n * n + 1, 0);
+  for (int pass = 0; pass < 2; ++pass) {
+    std::vector<int32_t> cur;
+    std::vector<int32_t> lst;
+    if (pass == 1) {
+      for (int64_t i = 0; i < n * n; ++i) off[i + 1] += off[i];
+      cur.assign(off.begin(), off.end() - 1);
+      lst.resize(off[n * n]);
+    }
+    for (size_t o = 0; o < base.size(); ++o) {
+      Rect r = expand(base[o], reach);
+      r.x0 = std::max<int64_t>(r.x0, 0); r.y0 = std::max<int64_t>(r.y0, 0);
+      r.x1 = std::min<int64_t>(r.x1, n - 1); r.y1 = std::min<int64_t>(r.y1, n - 1);
+      for (int64_t y = r.y0; y <= r.y1; ++y)
+        for (int64_t x = r.x0; x <= r.x1; ++x) {
+          const int64_t cell = y * n + x;
+          if (table[cell] != 1) continue;
+          if (pass == 0) off[cell + 1]++;
+          else lst[cur[cell]++] = (int32_t)o;
+        }
+    }
+    if (pass == 1) {
+      if ((st = upload(ctx, &P->cand_off, off))) return st;
+      if (lst.empty()) lst.push_back(0);
+      if ((st = upload(ctx, &P->cand_list, lst))) return st;
+    }
+  }
+  return GF_OK;
+}
+
+int finish_plan(gf_range_plan* P) {
+  GF_HIP_CHECK(P->ctx, hipMalloc(&P->partials, sizeof(uint64_t) * 2 * (size_t)P->ctx->num_cus * 8));
+  return GF_OK;
+}
+
+}  // namespace
+
+extern "C" void gf_range_plan_destroy(gf_range_plan* P) {
+  if (!P) return;
+  hipSetDevice(P->ctx->device);
+  hipStreamSynchronize(P->ctx->stream);
+  void* bufs[] = {P->table, P->extra, P->cand_off, P->cand_list, P->qx, P->qy, P->ring_off, P->vert_off,
+                  P->vx, P->vy, P->bbox, P->ring_env, P->partials};
+  for (void* b : bufs)
+    if (b) hipFree(b);
+  delete P;
+}
+
+extern "C" int gf_range_pp_plan_create(gf_ctx* ctx, const gf_grid* g, const double* qx, const double* qy,
+                                       int32_t nq, double r, int approximate, int metric, gf_range_plan** out) {
+  if (!ctx || !out || !grid_ok(g) || nq < 0 || (nq > 0 && (!qx || !qy)) || (metric != 0 && metric != 1))
+    return set_err(ctx, GF_ERR_ARG, "gf_range_pp_plan_create: bad argument");
+  *out = nullptr;
+  int st = bind(ctx);
+  if (st) return st;
+  gf_range_plan* P = new gf_range_plan();
+  P->ctx = ctx;
+  P->grid = *g;
+  P->r = r;
+  P->approx = approximate != 0;
+  P->metric = metric;
+  P->nq = nq;
+  P->g_layers = guaranteed_layers(g->cellLength, r);
+  P->c_layers = candidate_layers(g->cellLength, r);
+  const double nan = std::numeric_limits<double>::quiet_NaN();
+  if (nq == 0) {  // nothing is ever guaranteed or candidate
+    P->table_mode = 0;
+    P->qr.cgx = P->qr.cgy = P->qr.gx = P->qr.gy = {nan, nan};
+    P->qr.g_any = 0;
+  } else if (nq == 1) {
+    P->table_mode = 0;
+    const int32_t qcx = cell_index(qx[0], g->minX, g->cellLength), qcy = cell_index(qy[0], g->minY, g->cellLength);
+    P->qr = make_qrect(*g, qcx, qcy, P->g_layers, P->c_layers);
+    P->qx0 = qx[0];
+    P->qy0 = qy[0];
+  } else {
+    P->table_mode = 1;
+    std::vector<Rect> base(nq);
+    for (int32_t q = 0; q < nq; ++q) {
+      const int64_t cx = cell_index(qx[q], g->minX, g->cellLength), cy = cell_index(qy[q], g->minY, g->cellLength);
+      base[q] = {cx, cx, cy, cy};
+    }
+    if ((st = build_table(P, base, !P->approx))) { gf_range_plan_destroy(P); return st; }
+    std::vector<double> vqx(qx, qx + nq), vqy(qy, qy + nq);
+    if ((st = upload(ctx, &P->qx, vqx)) || (st = upload(ctx, &P->qy, vqy))) { gf_range_plan_destroy(P); return st; }
+  }
+  if ((st = finish_plan(P))) { gf_range_plan_destroy(P); return st; }
+  *out = P;
+  return GF_OK;
+}
+
+extern "C" int gf_range_ppoly_plan_create(gf_ctx* ctx, const gf_grid* g, const gf_polygons* polys, double r,
+                                          int approximate, int metric, gf_range_plan** out) {
+  if (!ctx || !out || !grid_ok(g) || !polys || polys->npoly < 0 || (metric != 0 && metric != 1))
+    return set_err(ctx, GF_ERR_ARG, "gf_range_ppoly_plan_create: bad argument");
+  *out = nullptr;
+  int st = bind(ctx);
+  if (st) return st;
+  const int32_t np = polys->npoly;
+  const int32_t nrings = np > 0 ? polys->ring_off[np] : 0;
+  // validate rings: >= 4 vertices, closed (Polygon.createPolygon / JTS LinearRing)
+  for (int32_t p = 0; p < np; ++p)
+    if (polys->ring_off[p + 1] <= polys->ring_off[p]) return set_err(ctx, GF_ERR_ARG, "polygon without a shell");
+  for (int32_t j = 0; j < nrings; ++j) {
+    const int32_t v0 = polys->vert_off[j], v1 = polys->vert_off[j + 1];
+    if (v1 - v0 < 4 || polys->vx[v0] != polys->vx[v1 - 1] || polys->vy[v0] != polys->vy[v1 - 1])
+      return set_err(ctx, GF_ERR_ARG, "ring must be closed with >= 4 vertices");
+  }
+  gf_range_plan* P = new gf_range_plan();
+  P->ctx = ctx;
+  P->grid = *g;
+  P->r = r;
+  P->approx = approximate != 0;
+  P->metric = metric;
+  P->poly = 1;
+  P->table_mode = 1;
+  P->npoly = np;
+  P->nq = np;
+  P->g_layers = guaranteed_layers(g->cellLength, r);
+  P->c_layers = candidate_layers(g->cellLength, r);
+  std::vector<double> bbox(4 * (size_t)std::max(np, 1)), renv(4 * (size_t)std::max(nrings, 1));
+  for (int32_t j = 0; j < nrings; ++j) {
+    const int32_t v0 = polys->vert_off[j], v1 = polys->vert_off[j + 1];
+    double mnx = polys->vx[v0], mxx = mnx, mny = polys->vy[v0], mxy = mny;
+    for (int32_t v = v0 + 1; v < v1; ++v) {
+      mnx = std::min(mnx, polys->vx[v]); mxx = std::max(mxx, polys->vx[v]);
+      mny = std::min(mny, polys->vy[v]); mxy = std::max(mxy, polys->vy[v]);
+    }
+    renv[4 * j] = mnx; renv[4 * j + 1] = mxx; renv[4 * j + 2] = mny; renv[4 * j + 3] = mxy;
+  }
+  std::vector<Rect> base(np);
+  for (int32_t p = 0; p < np; ++p) {
+    const int32_t sh = polys->ring_off[p];  // shell envelope = Polygon.getEnvelopeInternal
+    const double x1 = renv[4 * sh], x2 = renv[4 * sh + 1], y1 = renv[4 * sh + 2], y2 = renv[4 * sh + 3];
+    bbox[4 * p] = x1; bbox[4 * p + 1] = y1; bbox[4 * p + 2] = x2; bbox[4 * p + 3] = y2;
+    base[p] = {cell_index(x1, g->minX, g->cellLength), cell_index(x2, g->minX, g->cellLength),
+               cell_index(y1, g->minY, g->cellLength), cell_index(y2, g->minY, g->cellLength)};
+  }
+  if ((st = build_table(P, base, true))) { gf_range_plan_destroy(P); return st; }
+  const int32_t nverts = nrings > 0 ? polys->vert_off[nrings] : 0;
+  std::vector<int32_t> ro(polys->ring_off, polys->ring_off + np + 1), vo(polys->vert_off, polys->vert_off + nrings + 1);
+  std::vector<double> vx(polys->vx, polys->vx + nverts), vy(polys->vy, polys->vy + nverts);
+  if ((st = upload(ctx, &P->ring_off, ro)) || (st = upload(ctx, &P->vert_off, vo)) || (st = upload(ctx, &P->vx, vx)) ||
+      (st = upload(ctx, &P->vy, vy)) || (st = upload(ctx, &P->bbox, bbox)) || (st = upload(ctx, &P->ring_env, renv))) {
+    gf_range_plan_destroy(P);
+    return st;
+  }
+  if ((st = finish_plan(P))) { gf_range_plan_destroy(P); return st; }
+  *out = P;
+  return GF_OK;
+}
+
+extern "C" int gf_range_run(gf_range_plan* P, const gf_points* pts, uint64_t* bitmap, uint64_t* multi,
+                            int64_t* counts) {
+  if (!P || !bitmap) return GF_ERR_ARG;
+  gf_ctx* ctx = P->ctx;
+  int st = bind(ctx);
+  if (st) return st;
+  if ((st = check_points(ctx, pts))) return st;
+  if (pts->n == 0) {
+    if (counts) GF_HIP_CHECK(ctx, hipMemsetAsync(counts, 0, 2 * sizeof(int64_t), ctx->stream));
+    return GF_OK;
+  }
+  RangeArgs a{};
+  a.x = pts->x; a.y = pts->y; a.n = pts->n;
+  a.bitmap = bitmap; a.multi = multi; a.partials = P->partials;
+  a.nq = P->nq;
+  a.qr = P->qr;
+  a.grid_n = P->grid.n; a.minX = P->grid.minX; a.minY = P->grid.minY; a.cl = P->grid.cellLength;
+  a.table = P->table; a.extra = P->extra; a.n_extra = P->n_extra;
+  a.cand_off = P->cand_off; a.cand_list = P->cand_list;
+  a.approx = P->approx; a.metric = P->metric; a.r = P->r; a.s_r = s_prefilter(P->r, 0);
+  a.qx0 = P->qx0; a.qy0 = P->qy0;
+  a.qx = P->qx; a.qy = P->qy;
+  a.npoly = P->npoly; a.ring_off = P->ring_off; a.vert_off = P->vert_off; a.vx = P->vx; a.vy = P->vy;
+  a.bbox = P->bbox; a.ring_env = P->ring_env;
+  const int blocks = stream_blocks(ctx, (pts->n + 1) / 2);
+  GF_HIP_CHECK(ctx, launch_range(ctx, a, P->table_mode, P->poly, blocks));
+  if (counts) GF_HIP_CHECK(ctx, launch_range_finalize(ctx->stream, P->partials, blocks, counts));
+  return GF_OK;
+}
+
+extern "C" int gf_bitmap_to_indices(gf_ctx* ctx, const uint64_t* bitmap, int64_t n, uint32_t* idx, int64_t cap,
+                                    int64_t* count) {
+  if (!ctx || !bitmap || n < 0 || !count) return set_err(ctx, GF_ERR_ARG, "gf_bitmap_to_indices: bad argument");
+  int st = bind(ctx);
+  if (st) return st;
+  const int64_t words = (n + 63) / 64;
+  Arena ar;
+  size_t o_pc = ar.take<uint32_t>(words + 1);
+  size_t o_off = ar.take<uint32_t>(words + 1);
+  size_t o_tmp = ar.take<uint32_t>(scan_tmp_elems(words));
+  char* base = (char*)ctx_scratch(ctx, ar.off, &st);
+  if (st) return st;
+  uint32_t* pc = (uint32_t*)(base + o_pc);
+  uint32_t* off = (uint32_t*)(base + o_off);
+  uint32_t* tmp = (uint32_t*)(base + o_tmp);
+  GF_HIP_CHECK(ctx, launch_word_popcounts(ctx->stream, bitmap, words, pc));
+  GF_HIP_CHECK(ctx, launch_exclusive_scan(ctx->stream, pc, words, off, tmp));
+  uint32_t total = 0;
+  GF_HIP_CHECK(ctx, hipMemcpyAsync(&total, off + words, sizeof total, hipMemcpyDeviceToHost, ctx->stream));
+  GF_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+  *count = total;
+  if ((int64_t)total > cap) return GF_ERR_CAPACITY;
+  if (total) {
+    if (!idx) return GF_ERR_ARG;
+    GF_HIP_CHECK(ctx, launch_expand_bitmap(ctx->stream, bitmap, words, n, off, idx, cap));
+    GF_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+  }
+  return GF_OK;
+}
+
+// ---------------------------------------------------------------------------------------
+// kNN
+// ---------------------------------------------------------------------------------------
+extern "C" size_t gf_knn_result_bytes(int32_t k) {
+  return sizeof(gf_knn_header) + (size_t)(k > 0 ? k : 0) * (sizeof(double) + 2 * sizeof(int64_t));
+}
+
+extern "C" void gf_knn_plan_destroy(gf_knn_plan* P) {
+  if (!P) return;
+  hipSetDevice(P->ctx->device);
+  hipStreamSynchronize(P->ctx->stream);
+  if (P->st) hipFree(P->st);
+  if (P->cand_d) hipFree(P->cand_d);
+  if (P->cand_i) hipFree(P->cand_i);
+  if (P->tmp_result) hipFree(P->tmp_result);
+  if (P->host_result) hipHostFree(P->host_result);
+  delete P;
+}
+
+static int knn_alloc_candidates(gf_knn_plan* P, int64_t cap) {
+  gf_ctx* ctx = P->ctx;
+  if (P->cand_d) hipFree(P->cand_d);
+  if (P->cand_i) hipFree(P->cand_i);
+  P->cand_d = nullptr;
+  P->cand_i = nullptr;
+  GF_HIP_CHECK(ctx, hipMalloc(&P->cand_d, sizeof(double) * (size_t)cap));
+  GF_HIP_CHECK(ctx, hipMalloc(&P->cand_i, sizeof(uint32_t) * (size_t)cap));
+  P->cap = cap;
+  return GF_OK;
+}
+
+extern "C" int gf_knn_pp_plan_create(gf_ctx* ctx, const gf_grid* g, double qx, double qy, double r, int32_t k,
+                                     int metric, gf_knn_plan** out) {
+  if (!ctx || !out || !grid_ok(g) || k < 1 || k > kMaxK || (metric != 0 && metric != 1))
+    return set_err(ctx, GF_ERR_ARG, "gf_knn_pp_plan_create: bad argument (k must be in [1, 1024])");
+  *out = nullptr;
+  int st = bind(ctx);
+  if (st) return st;
+  gf_knn_plan* P = new gf_knn_plan();
+  P->ctx = ctx;
+  P->grid = *g;
+  P->qx = qx; P->qy = qy; P->r = r; P->k = k; P->metric = metric;
+  const int32_t gl = guaranteed_layers(g->cellLength, r), cl = candidate_layers(g->cellLength, r);
+  const int32_t qcx = cell_index(qx, g->minX, g->cellLength), qcy = cell_index(qy, g->minY, g->cellLength);
+  P->qr = make_qrect(*g, qcx, qcy, gl, cl);  // PointPointKNNQuery.java:134-135
+  auto fail = [&](int s) { gf_knn_plan_destroy(P); return s; };
+  hipError_t e;
+  if ((e = hipMalloc(&P->st, sizeof(KnnState))) != hipSuccess) return fail(hip_err(ctx, e, "hipMalloc(KnnState)"));
+  if ((e = hipMemset(P->st, 0, sizeof(KnnState))) != hipSuccess) return fail(hip_err(ctx, e, "hipMemset"));
+  if ((st = knn_alloc_candidates(P, (int64_t)1 << 20))) return fail(st);
+  if ((e = hipMalloc(&P->tmp_result, gf_knn_result_bytes(k))) != hipSuccess) return fail(hip_err(ctx, e, "hipMalloc"));
+  if ((e = hipHostMalloc(&P->host_result, gf_knn_result_bytes(k), hipHostMallocDefault)) != hipSuccess)
+    return fail(hip_err(ctx, e, "hipHostMalloc"));
+  P->scan_blocks = 0;
+  *out = P;
+  return GF_OK;
+}
+
+extern "C" int gf_knn_plan_set_capacity(gf_knn_plan* P, int64_t cap) {
+  if (!P || cap < 2 || cap > (int64_t)1 << 31) return GF_ERR_ARG;
+  int st = bind(P->ctx);
+  if (st) return st;
+  hipStreamSynchronize(P->ctx->stream);
+  return knn_alloc_candidates(P, cap & ~(int64_t)1);
+}
+
+extern "C" int gf_knn_plan_set_index_base(gf_knn_plan* P, int64_t base) {
+  if (!P || base < 0) return GF_ERR_ARG;
+  P->idx_base = base;
+  return GF_OK;
+}
+
+static int knn_scan_select(gf_knn_plan* P, const gf_points* pts, int64_t begin, int64_t end, int use_state,
+                           void* result) {
+  gf_ctx* ctx = P->ctx;
+  KnnScanArgs s{};
+  s.x = pts->x; s.y = pts->y; s.begin = begin; s.end = end;
+  s.qx = P->qx; s.qy = P->qy; s.qr = P->qr;
+  s.T = P->r; s.s_pre = s_prefilter(P->r, P->metric);
+  s.use_state = use_state; s.metric = P->metric; s.st = P->st;
+  s.cand_d = P->cand_d; s.cand_i = P->cand_i; s.cap = (unsigned long long)P->cap;
+  const int blocks = P->scan_blocks > 0 ? P->scan_blocks : stream_blocks(ctx, ((end - begin) + 1) / 2);
+  GF_HIP_CHECK(ctx, launch_knn_scan(ctx, s, blocks));
+  KnnSelectArgs q{};
+  q.st = P->st; q.cand_d = P->cand_d; q.cand_i = P->cand_i; q.cap = (unsigned long long)P->cap;
+  q.objID = pts->objID; q.use_state = use_state; q.T = P->r; q.r = P->r; q.k = P->k; q.result = result;
+  q.idx_base = P->idx_base;
+  GF_HIP_CHECK(ctx, launch_knn_select(ctx, q));
+  return GF_OK;
+}
+
+extern "C" int gf_knn_enqueue(gf_knn_plan* P, const gf_points* pts, void* result) {
+  if (!P || !result) return GF_ERR_ARG;
+  gf_ctx* ctx = P->ctx;
+  int st = bind(ctx);
+  if (st) return st;
+  if ((st = check_points(ctx, pts))) return st;
+  if (pts->n > 0 && !pts->objID) return set_err(ctx, GF_ERR_ARG, "kNN needs objID");
+  const bool sample = pts->n >= kSampleMinN;
+  if (sample) {
+    KnnSampleArgs s{};
+    s.x = pts->x; s.y = pts->y; s.n = pts->n; s.qx = P->qx; s.qy = P->qy; s.qr = P->qr;
+    s.r = P->r; s.s_r = s_prefilter(P->r, P->metric); s.k = P->k; s.metric = P->metric; s.st = P->st;
+    GF_HIP_CHECK(ctx, launch_knn_sample(ctx, s));
+  }
+  return knn_scan_select(P, pts, 0, pts->n, sample ? 1 : 0, result);
+}
+
+namespace {
+struct Ent { double d; int64_t o, i; };
+void merge_lists(int32_t k, std::vector<Ent>& all, int64_t* oo, double* od, int64_t* oi, int32_t* n_out) {
+  std::sort(all.begin(), all.end(), [](const Ent& a, const Ent& b) {
+    if (a.d != b.d) return a.d < b.d;
+    if (a.o != b.o) return a.o < b.o;
+    return a.i < b.i;
+  });
+  std::unordered_set<int64_t> seen;
+  int32_t n = 0;
+  for (const Ent& e : all) {
+    if (n >= k) break;
+    if (!seen.insert(e.o).second) continue;
+    if (oo) oo[n] = e.o;
+    if (od) od[n] = e.d;
+    if (oi) oi[n] = e.i;
+    ++n;
+  }
+  *n_out = n;
+}
+}  // namespace
+
+extern "C" int gf_knn_merge_host(int32_t k, int32_t nlists, const int32_t* counts, const int64_t* objID,
+                                 const double* dist, const int64_t* idx, int64_t* oo, double* od, int64_t* oi,
+                                 int32_t* n_out) {
+  if (k < 1 || nlists < 0 || !n_out || (nlists > 0 && (!counts || !objID || !dist))) return GF_ERR_ARG;
+  std::vector<Ent> all;
+  int64_t off = 0;
+  for (int32_t l = 0; l < nlists; ++l)
+    for (int32_t j = 0; j < counts[l]; ++j, ++off) all.push_back({dist[off], objID[off], idx ? idx[off] : 0});
+  merge_lists(k, all, oo, od, oi, n_out);
+  return GF_OK;
+}
+
+// exact fallback: T = r over capacity-sized partitions, merged on the host
+static int knn_fallback(gf_knn_plan* P, const gf_points* pts, int64_t* oo, double* od, int64_t* oi, int32_t* n_out) {
+  gf_ctx* ctx = P->ctx;
+  const int64_t part = std::max<int64_t>(2, P->cap & ~(int64_t)1);
+  const size_t rb = gf_knn_result_bytes(P->k);
+  std::vector<Ent> all;
+  for (int64_t lo = 0; lo < pts->n; lo += part) {
+    const int64_t hi = std::min(pts->n, lo + part);
+    int st = knn_scan_select(P, pts, lo, hi, 0, P->tmp_result);
+    if (st) return st;
+    GF_HIP_CHECK(ctx, hipMemcpyAsync(P->host_result, P->tmp_result, rb, hipMemcpyDeviceToHost, ctx->stream));
+    GF_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+    const gf_knn_header* h = (const gf_knn_header*)P->host_result;
+    if (h->status != 0) return set_err(ctx, GF_ERR_HIP, "kNN partition did not converge");
+    const double* d = (const double*)(h + 1);
+    const int64_t* o = (const int64_t*)(d + P->k);
+    const int64_t* i = o + P->k;
+    for (int32_t j = 0; j < h->n; ++j) all.push_back({d[j], o[j], i[j]});
+  }
+  merge_lists(P->k, all, oo, od, oi, n_out);
+  return GF_OK;
+}
+
+extern "C" int gf_knn_decode(gf_knn_plan* P, const gf_points* pts, const void* result_host, int64_t* oo,
+                             double* od, int64_t* oi, int32_t* n_out) {
+  if (!P || !result_host || !n_out) return GF_ERR_ARG;
+  const gf_knn_header* h = (const gf_knn_header*)result_host;
+  if (h->status == 0) {
+    const double* d = (const double*)(h + 1);
+    const int64_t* o = (const int64_t*)(d + h->k);
+    const int64_t* i = o + h->k;
+    for (int32_t j = 0; j < h->n; ++j) {
+      if (oo) oo[j] = o[j];
+      if (od) od[j] = d[j];
+      if (oi) oi[j] = i[j];
+    }
+    *n_out = h->n;
+    return GF_OK;
+  }
+  int st = bind(P->ctx);
+  if (st) return st;
+  if ((st = check_points(P->ctx, pts))) return st;
+  return knn_fallback(P, pts, oo, od, oi, n_out);
+}
+
+extern "C" int gf_knn_run(gf_knn_plan* P, const gf_points* pts, int64_t* oo, double* od, int64_t* oi,
+                          int32_t* n_out) {
+  if (!P || !n_out) return GF_ERR_ARG;
+  gf_ctx* ctx = P->ctx;
+  int st = gf_knn_enqueue(P, pts, P->tmp_result);
+  if (st) return st;
+  GF_HIP_CHECK(ctx, hipMemcpyAsync(P->host_result, P->tmp_result, gf_knn_result_bytes(P->k), hipMemcpyDeviceToHost,
+                                   ctx->stream));
+  GF_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+  return gf_knn_decode(P, pts, P->host_result, oo, od, oi, n_out);
+}
+
+extern "C" int gf_knn_merge_dev(gf_ctx* ctx, int32_t k, const void* records, int32_t nrec, void* result) {
+  if (!ctx || k < 1 || k > kMaxK || nrec < 1 || nrec > 64 || (int64_t)nrec * k > kSortCap || !records || !result)
+    return set_err(ctx, GF_ERR_ARG, "gf_knn_merge_dev: need 1 <= nrec <= 64 and nrec*k <= 4096");
+  int st = bind(ctx);
+  if (st) return st;
+  GF_HIP_CHECK(ctx, launch_knn_merge(ctx, k, records, nrec, result));
+  return GF_OK;
+}
+
+// ---------------------------------------------------------------------------------------
+// join
+// ---------------------------------------------------------------------------------------
+extern "C" int gf_join_pp(gf_ctx* ctx, const gf_grid* ugrid, const gf_grid* qgrid, const gf_points* ord,
+                          const gf_points* qry, double r, int approximate, int metric, uint32_t* pairs, int64_t cap,
+                          int64_t* npairs) {
+  if (!ctx || !grid_ok(ugrid) || !grid_ok(qgrid) || !npairs || (metric != 0 && metric != 1))
+    return set_err(ctx, GF_ERR_ARG, "gf_join_pp: bad argument");
+  int st = bind(ctx);
+  if (st) return st;
+  if ((st = check_points(ctx, ord)) || (st = check_points(ctx, qry))) return st;
+  *npairs = 0;
+  int64_t c;
+  if (r == 0) {
+    c = -1;  // getNeighboringCells: every grid cell (UniformGrid.java:264-266)
+  } else {
+    c = candidate_layers(qgrid->cellLength, r);
+    if (c <= 0) return set_err(ctx, GF_ERR_LAYERS, "candidateNeighboringLayers cannot be 0 or less");
+  }
+  const int64_t no = ord->n, nq = qry->n;
+  if (no == 0 || nq == 0) return GF_OK;
+  const int64_t qn = qgrid->n, W = qn + 2, bins = W * W;
+  if (bins >= (int64_t)INT32_MAX / 2) return set_err(ctx, GF_ERR_ARG, "query grid too large");
+  const int blocks = (int)std::min<int64_t>(std::max<int64_t>((no + kBlock - 1) / kBlock, 1), (int64_t)ctx->num_cus * 8);
+  Arena ar;
+  size_t o_keys = ar.take<uint32_t>(nq), o_qcx = ar.take<int32_t>(nq), o_qcy = ar.take<int32_t>(nq);
+  size_t o_hist = ar.take<uint32_t>(bins), o_off = ar.take<uint32_t>(bins + 1), o_cur = ar.take<uint32_t>(bins);
+  size_t o_tmp = ar.take<uint32_t>(std::max(scan_tmp_elems(bins), scan_tmp_elems(blocks)));
+  size_t o_sqx = ar.take<double>(nq), o_sqy = ar.take<double>(nq);
+  size_t o_sqcx = ar.take<int32_t>(nq), o_sqcy = ar.take<int32_t>(nq), o_sqi = ar.take<uint32_t>(nq);
+  size_t o_cnt = ar.take<uint32_t>(blocks), o_boff = ar.take<uint32_t>(blocks + 1);
+  char* base = (char*)ctx_scratch(ctx, ar.off, &st);
+  if (st) return st;
+  auto U32 = [&](size_t o) { return (uint32_t*)(base + o); };
+  auto I32 = [&](size_t o) { return (int32_t*)(base + o); };
+  auto F64 = [&](size_t o) { return (double*)(base + o); };
+  hipStream_t s = ctx->stream;
+  GF_HIP_CHECK(ctx, hipMemsetAsync(U32(o_hist), 0, bins * sizeof(uint32_t), s));
+  GF_HIP_CHECK(ctx, launch_join_qkeys(s, qry->x, qry->y, nq, qgrid->minX, qgrid->minY, qgrid->cellLength, qgrid->n,
+                                      U32(o_keys), I32(o_qcx), I32(o_qcy)));
+  GF_HIP_CHECK(ctx, launch_histogram(s, U32(o_keys), nq, U32(o_hist)));
+  GF_HIP_CHECK(ctx, launch_exclusive_scan(s, U32(o_hist), bins, U32(o_off), U32(o_tmp)));
+  GF_HIP_CHECK(ctx, hipMemcpyAsync(U32(o_cur), U32(o_off), bins * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
+  GF_HIP_CHECK(ctx, launch_join_qscatter(s, qry->x, qry->y, I32(o_qcx), I32(o_qcy), U32(o_keys), nq, U32(o_cur),
+                                         F64(o_sqx), F64(o_sqy), I32(o_sqcx), I32(o_sqcy), U32(o_sqi)));
+  JoinArgs a{};
+  a.ox = ord->x; a.oy = ord->y; a.no = no;
+  a.u_minX = ugrid->minX; a.u_minY = ugrid->minY; a.u_cl = ugrid->cellLength;
+  a.qn = qgrid->n; a.c = c; a.q_off = U32(o_off);
+  a.sqx = F64(o_sqx); a.sqy = F64(o_sqy); a.sqcx = I32(o_sqcx); a.sqcy = I32(o_sqcy); a.sqidx = U32(o_sqi);
+  a.approx = approximate != 0; a.metric = metric; a.r = r;
+  a.counts = U32(o_cnt); a.offsets = U32(o_boff); a.pairs = pairs;
+  GF_HIP_CHECK(ctx, launch_join_probe(ctx, a, 0, blocks));
+  GF_HIP_CHECK(ctx, launch_exclusive_scan(s, U32(o_cnt), blocks, U32(o_boff), U32(o_tmp)));
+  uint32_t total = 0;
+  GF_HIP_CHECK(ctx, hipMemcpyAsync(&total, U32(o_boff) + blocks, sizeof total, hipMemcpyDeviceToHost, s));
+  GF_HIP_CHECK(ctx, hipStreamSynchronize(s));
+  *npairs = total;
+  if ((int64_t)total > cap) return GF_ERR_CAPACITY;
+  if (total == 0) return GF_OK;
+  if (!pairs) return set_err(ctx, GF_ERR_ARG, "null pairs");
+  GF_HIP_CHECK(ctx, launch_join_probe(ctx, a, 1, blocks));
+  GF_HIP_CHECK(ctx, hipStreamSynchronize(s));
+  return GF_OK;
+}
+
+// ---------------------------------------------------------------------------------------
+// windows, synthetic input
+// ---------------------------------------------------------------------------------------
+extern "C" int gf_window_create(gf_ctx* ctx, int64_t capacity, gf_window** out) {
+  if (!ctx || !out || capacity < 0) return GF_ERR_ARG;
+  int st = bind(ctx);
+  if (st) return st;
+  gf_window* w = new gf_window();
+  w->ctx = ctx;
+  w->capacity = capacity;
+  const size_t n = (size_t)std::max<int64_t>(capacity, 1);
+  if (hipMalloc(&w->x, 8 * n) != hipSuccess || hipMalloc(&w->y, 8 * n) != hipSuccess ||
+      hipMalloc(&w->objID, 8 * n) != hipSuccess || hipMalloc(&w->ts, 8 * n) != hipSuccess) {
+    gf_window_destroy(w);
+    return set_err(ctx, GF_ERR_NOMEM, "gf_window_create: hipMalloc failed");
+  }
+  *out = w;
+  return GF_OK;
+}
+
+extern "C" void gf_window_destroy(gf_window* w) {
+  if (!w) return;
+  hipSetDevice(w->ctx->device);
+  hipStreamSynchronize(w->ctx->stream);
+  if (w->x) hipFree(w->x);
+  if (w->y) hipFree(w->y);
+  if (w->objID) hipFree(w->objID);
+  if (w->ts) hipFree(w->ts);
+  delete w;
+}
+
+extern "C" int gf_window_upload(gf_window* w, const double* x, const double* y, const int64_t* objID,
+                                const int64_t* ts, int64_t n) {
+  if (!w || n < 0 || n > w->capacity || (n > 0 && (!x || !y))) return GF_ERR_ARG;
+  gf_ctx* ctx = w->ctx;
+  int st = bind(ctx);
+  if (st) return st;
+  const size_t b = 8 * (size_t)n;
+  if (n) {
+    GF_HIP_CHECK(ctx, hipMemcpyAsync(w->x, x, b, hipMemcpyHostToDevice, ctx->stream));
+    GF_HIP_CHECK(ctx, hipMemcpyAsync(w->y, y, b, hipMemcpyHostToDevice, ctx->stream));
+    if (objID) GF_HIP_CHECK(ctx, hipMemcpyAsync(w->objID, objID, b, hipMemcpyHostToDevice, ctx->stream));
+    if (ts) GF_HIP_CHECK(ctx, hipMemcpyAsync(w->ts, ts, b, hipMemcpyHostToDevice, ctx->stream));
+  }
+  w->n = n;
+  return GF_OK;
+}
+
+extern "C" int gf_window_points(gf_window* w, gf_points* out) {
+  if (!w || !out) return GF_ERR_ARG;
+  out->x = w->x; out->y = w->y; out->objID = w->objID; out->ts = w->ts; out->n = w->n;
+  return GF_OK;
+}
+
+extern "C" int gf_synth_uniform(int64_t seed, int64_t n, double minX, double maxX, double minY, double maxY, double* x,
+                                double* y) {
+  if (n < 0 || (n > 0 && (!x || !y))) return GF_ERR_ARG;
+  // java.util.Random: 48-bit LCG; nextDouble() = ((next(26) << 27) + next(27)) * 2^-53
+  uint64_t sd = ((uint64_t)seed ^ 0x5DEECE66DULL) & ((1ULL << 48) - 1);
+  auto next = [&](int bits) {
+    sd = (sd * 0x5DEECE66DULL + 0xBULL) & ((1ULL << 48) - 1);
+    return (int64_t)(sd >> (48 - bits));
+  };
+  for (int64_t i = 0; i < n; ++i) {
+    const double u = (double)((next(26) << 27) + next(27)) * 0x1.0p-53;
+    x[i] = minX + u * (maxX - minX);
+    const double v = (double)((next(26) << 27) + next(27)) * 0x1.0p-53;
+    y[i] = minY + v * (maxY - minY);
+  }
+  return GF_OK;
+}

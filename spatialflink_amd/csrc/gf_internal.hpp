@@ -1,0 +1,264 @@
+// gf_internal.hpp -- context, plans and kernel launch interfaces of libgeoflink_hip.so.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../../include/geoflink_hip.h"
+#include "gf_numerics.hpp"
+
+// ---------------------------------------------------------------------------------------
+// context
+// ---------------------------------------------------------------------------------------
+struct gf_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipStream_t own_stream = nullptr;
+  std::string last_error;
+  int timing = 0;  // bitmask of GF_K_* kernels to time
+  struct Ev { hipEvent_t a, b; int kid; };
+  std::vector<Ev> pending;
+  std::vector<hipEvent_t> pool;
+  double acc_ms[GF_K_COUNT] = {};
+  int64_t acc_n[GF_K_COUNT] = {};
+  // grow-only scratch (device) and pinned host staging
+  void* scratch = nullptr;
+  size_t scratch_bytes = 0;
+  void* pinned = nullptr;
+  size_t pinned_bytes = 0;
+  int num_cus = 256;
+};
+
+namespace gf {
+
+int set_err(gf_ctx* ctx, int code, const std::string& msg);
+int hip_err(gf_ctx* ctx, hipError_t e, const char* what);
+void* ctx_scratch(gf_ctx* ctx, size_t bytes, int* status);
+void* ctx_pinned(gf_ctx* ctx, size_t bytes, int* status);
+int bind(gf_ctx* ctx);
+
+#define GF_HIP_CHECK(ctx, call)                                   \
+  do {                                                            \
+    hipError_t _e = (call);                                       \
+    if (_e != hipSuccess) return ::gf::hip_err((ctx), _e, #call); \
+  } while (0)
+
+// RAII event pair around one kernel launch when ctx->timing is on.
+struct KTimer {
+  gf_ctx* ctx;
+  int kid;
+  hipEvent_t a = nullptr, b = nullptr;
+  KTimer(gf_ctx* c, int k);
+  ~KTimer();
+};
+
+// ---------------------------------------------------------------------------------------
+// kernel argument blocks
+// ---------------------------------------------------------------------------------------
+constexpr int kBlock = 256;         // streaming kernels: 4 waves
+constexpr int kSortCap = 4096;      // select kernel: LDS sort capacity
+constexpr int kMaxK = 1024;         // largest k on the device path
+constexpr int kSampleBlocks = 64;   // kNN sample: 64 blocks x 2048 points
+constexpr int kSamplePerBlock = 2048;
+constexpr int64_t kSampleMinN = 1 << 20;
+
+// single-query classification (exact, from host-side cell thresholds)
+struct QueryRect {
+  AxisIv cgx, cgy;   // valid cells within c layers
+  AxisIv gx, gy;     // guaranteed rect (g > 0: valid cells within g; g == 0: the query cell)
+  int g_any;         // g >= 0 and the guaranteed rect is non-empty
+  double minX, minY; // NaN coordinates classify as cell 0 (Java (int)NaN == 0)
+};
+
+// device state of a kNN plan (zeroed at creation)
+struct KnnState {
+  uint32_t hist[kDistBins];
+  uint32_t ticket;
+  uint32_t pad;
+  double T;          // distance threshold chosen by the sample (<= r)
+  double s_pre;      // prefilter bound on dx*dx+dy*dy for T
+  unsigned long long count;  // candidates appended (may exceed capacity)
+};
+
+struct KnnScanArgs {
+  const double* x;
+  const double* y;
+  int64_t begin, end;   // [begin, end), begin even
+  double qx, qy;
+  QueryRect qr;
+  double T, s_pre;      // used when !use_state
+  int use_state;
+  int metric;
+  KnnState* st;
+  double* cand_d;
+  uint32_t* cand_i;
+  unsigned long long cap;
+};
+
+struct KnnSampleArgs {
+  const double* x;
+  const double* y;
+  int64_t n;
+  double qx, qy;
+  QueryRect qr;
+  double r, s_r;
+  int32_t k;
+  int metric;
+  KnnState* st;
+};
+
+struct KnnSelectArgs {
+  KnnState* st;
+  const double* cand_d;
+  const uint32_t* cand_i;
+  unsigned long long cap;
+  const int64_t* objID;
+  int use_state;
+  double T;             // when !use_state
+  double r;
+  int32_t k;
+  int64_t idx_base;     // added to the window-local index in the record
+  void* result;         // gf_knn_header + dist[k] + objID[k] + idx[k]
+};
+
+// range: classification + tester
+struct RangeArgs {
+  const double* x;
+  const double* y;
+  int64_t n;
+  uint64_t* bitmap;
+  uint64_t* multi;           // nullable
+  uint64_t* partials;        // [gridDim.x * 2]: hits, multiset size per block
+  int32_t nq;                // multiplicity for approximate point-point
+  // arithmetic classification (single query point)
+  QueryRect qr;
+  // table classification
+  int32_t grid_n;
+  double minX, minY, cl;
+  const uint8_t* table;      // [n*n]: 0 none, 1 test, 2 accept
+  const int32_t* extra;      // [n_extra*4]: x0, x1, y0, y1 (inclusive) accepted out-of-grid cells
+  int32_t n_extra;
+  const int32_t* cand_off;   // [n*n+1] objects to test per cell (CSR); null => test all
+  const int32_t* cand_list;
+  // tester
+  int approx;
+  int metric;
+  double r, s_r;
+  double qx0, qy0;           // the query point (ARITH mode)
+  const double* qx;          // point-point queries (device)
+  const double* qy;
+  int32_t npoly;
+  const int32_t* ring_off;   // polygons (device)
+  const int32_t* vert_off;
+  const double* vx;
+  const double* vy;
+  const double* bbox;        // [npoly*4] x1, y1, x2, y2 (shell envelope)
+  const double* ring_env;    // [nrings*4] minx, maxx, miny, maxy
+};
+
+// launchers (return hipError_t of the launch)
+hipError_t launch_assign(gf_ctx* ctx, const gf_grid* g, const gf_points* p, int32_t* cx, int32_t* cy);
+hipError_t launch_cell_keys(hipStream_t s, const gf_grid* g, const double* x, const double* y, int64_t n,
+                            int clamp_pad, uint32_t* keys);
+hipError_t launch_histogram(hipStream_t s, const uint32_t* keys, int64_t n, uint32_t* hist);
+hipError_t launch_scatter(hipStream_t s, const uint32_t* keys, int64_t n, uint32_t* cursor, uint32_t* perm);
+// exclusive scan: out[0..L] (out[L] = total); tmp >= scan_tmp_elems(L) uint32
+size_t scan_tmp_elems(int64_t L);
+hipError_t launch_exclusive_scan(hipStream_t s, const uint32_t* in, int64_t L, uint32_t* out, uint32_t* tmp);
+hipError_t launch_word_popcounts(hipStream_t s, const uint64_t* bitmap, int64_t words, uint32_t* pc);
+hipError_t launch_expand_bitmap(hipStream_t s, const uint64_t* bitmap, int64_t words, int64_t n,
+                                const uint32_t* off, uint32_t* idx, int64_t cap);
+
+hipError_t launch_knn_sample(gf_ctx* ctx, const KnnSampleArgs& a);
+hipError_t launch_knn_scan(gf_ctx* ctx, const KnnScanArgs& a, int blocks);
+hipError_t launch_knn_select(gf_ctx* ctx, const KnnSelectArgs& a);
+hipError_t launch_knn_merge(gf_ctx* ctx, int32_t k, const void* records, int32_t nrec, void* result);
+
+hipError_t launch_range(gf_ctx* ctx, const RangeArgs& a, int table_mode, int poly, int blocks);
+hipError_t launch_range_finalize(hipStream_t s, const uint64_t* partials, int blocks, int64_t* counts);
+
+struct JoinArgs {
+  const double* ox;
+  const double* oy;
+  int64_t no;
+  double u_minX, u_minY, u_cl;   // ugrid (ordinary points)
+  int32_t qn;                    // qgrid n (validKey of replicated cells)
+  int64_t c;                     // candidate layers; < 0 => r == 0 (all valid cells)
+  const uint32_t* q_off;         // [(qn+2)^2 + 1] clamped-cell bucket offsets
+  const double* sqx;
+  const double* sqy;
+  const int32_t* sqcx;
+  const int32_t* sqcy;
+  const uint32_t* sqidx;
+  int approx;
+  int metric;
+  double r;
+  uint32_t* counts;              // count pass: per-block pair counts
+  const uint32_t* offsets;       // write pass: per-block output offsets
+  uint32_t* pairs;               // write pass
+};
+hipError_t launch_join_qkeys(hipStream_t s, const double* qx, const double* qy, int64_t nq, double minX,
+                             double minY, double cl, int32_t qn, uint32_t* keys, int32_t* qcx, int32_t* qcy);
+hipError_t launch_join_qscatter(hipStream_t s, const double* qx, const double* qy, const int32_t* qcx,
+                                const int32_t* qcy, const uint32_t* keys, int64_t nq, uint32_t* cursor,
+                                double* sqx, double* sqy, int32_t* sqcx, int32_t* sqcy, uint32_t* sqidx);
+hipError_t launch_join_probe(gf_ctx* ctx, const JoinArgs& a, int write_pass, int blocks);
+
+}  // namespace gf
+
+// plans ---------------------------------------------------------------------------------
+struct gf_range_plan {
+  gf_ctx* ctx = nullptr;
+  gf_grid grid{};
+  double r = 0;
+  int approx = 0, metric = 0, poly = 0, table_mode = 0;
+  int32_t nq = 0, g_layers = 0, c_layers = 0;
+  gf::QueryRect qr{};
+  double qx0 = 0, qy0 = 0;
+  // device buffers (owned)
+  uint8_t* table = nullptr;
+  int32_t* extra = nullptr;
+  int32_t n_extra = 0;
+  int32_t* cand_off = nullptr;
+  int32_t* cand_list = nullptr;
+  double* qx = nullptr;
+  double* qy = nullptr;
+  int32_t npoly = 0;
+  int32_t* ring_off = nullptr;
+  int32_t* vert_off = nullptr;
+  double* vx = nullptr;
+  double* vy = nullptr;
+  double* bbox = nullptr;
+  double* ring_env = nullptr;
+  uint64_t* partials = nullptr;
+  int blocks = 0;
+};
+
+struct gf_knn_plan {
+  gf_ctx* ctx = nullptr;
+  gf_grid grid{};
+  double qx = 0, qy = 0, r = 0;
+  int32_t k = 0;
+  int metric = 0;
+  gf::QueryRect qr{};
+  gf::KnnState* st = nullptr;
+  double* cand_d = nullptr;
+  uint32_t* cand_i = nullptr;
+  int64_t cap = 0;
+  int64_t idx_base = 0;
+  void* tmp_result = nullptr;   // device record used by gf_knn_run / fallback
+  void* host_result = nullptr;  // pinned
+  int scan_blocks = 0;
+};
+
+struct gf_window {
+  gf_ctx* ctx = nullptr;
+  int64_t capacity = 0, n = 0;
+  double* x = nullptr;
+  double* y = nullptr;
+  int64_t* objID = nullptr;
+  int64_t* ts = nullptr;
+};

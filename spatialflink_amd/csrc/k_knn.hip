@@ -1,0 +1,464 @@
+// k_knn.hip -- per-query kNN over one window (PointPointKNNQuery.java:132-201 per-cell heaps +
+// KNNQuery.java:213-272 windowAll merge), restated as a three-kernel pipeline for gfx950:
+//
+//   knn_sample  64 blocks read a strided 128K-point sample, histogram candidate distances
+//               into 4096 log-spaced bins; the last block (atomic ticket) picks T = the upper
+//               edge of the bin holding the sample's k-th candidate (>= the window's k-th
+//               distance, because the sample is a subset).  Skipped for windows < 1M points.
+//   knn_scan    the HBM-bound pass: 16 B/point (x, y), one test per point against the exact
+//               prefilter s = dx*dx+dy*dy <= smax(T); the rare survivors get the exact cell
+//               test (C u G) and are appended (d, idx) with one atomic per wave.
+//   knn_select  one 1024-thread block: LDS histogram of the M candidates, keep the bins up
+//               to the k-th, bitonic-sort (d, objID, idx) in LDS, objID dedupe, first k.
+//
+// Exactness never depends on the sample: if the candidate buffer overflows, or fewer than k
+// distinct objIDs lie below T < r, the record says so and the host re-runs with T = r in
+// capacity-sized partitions (gf_knn_decode).  Output: (d, objID) ascending, min-(d, idx)
+// occurrence per objID.
+#include "gf_internal.hpp"
+
+namespace gf {
+
+__device__ __forceinline__ bool classify_cg(const QueryRect& q, double px, double py) {
+  const double xs = (px == px) ? px : q.minX;  // Java (int)NaN == 0 -> cell 0
+  const double ys = (py == py) ? py : q.minY;
+  const bool inG = q.g_any && in_iv(q.gx, xs) && in_iv(q.gy, ys);
+  return inG || (in_iv(q.cgx, xs) && in_iv(q.cgy, ys));
+}
+
+// kNN candidate: cell in C u G (PointPointKNNQuery.java:145-150) and d <= T (<= r, :170-177).
+template <int METRIC>
+__device__ __forceinline__ bool knn_candidate(double qx, double qy, const QueryRect& qr, double px,
+                                              double py, double sp, double T, double& d) {
+  const double dx = qx - px, dy = qy - py;
+  const double s = dx * dx + dy * dy;
+  if (!(s <= sp)) return false;
+  if (!classify_cg(qr, px, py)) return false;
+  if (METRIC == 0) {
+    d = sqrt(s);  // s <= smax(T)  <=>  sqrt(s) <= T
+    return true;
+  }
+  d = fdlibm_hypot(dx, dy);
+  return d <= T;
+}
+
+__device__ __forceinline__ uint64_t okey(int64_t o) { return (uint64_t)o ^ 0x8000000000000000ull; }
+__device__ __forceinline__ int64_t from_okey(uint64_t k) { return (int64_t)(k ^ 0x8000000000000000ull); }
+
+struct RecView {
+  gf_knn_header* h;
+  double* d;
+  int64_t* o;
+  int64_t* i;
+};
+__host__ __device__ inline RecView rec_view(void* base, int k) {
+  RecView v;
+  v.h = (gf_knn_header*)base;
+  v.d = (double*)(v.h + 1);
+  v.o = (int64_t*)(v.d + k);
+  v.i = v.o + k;
+  return v;
+}
+
+// ---------------------------------------------------------------------------------------
+// sample
+// ---------------------------------------------------------------------------------------
+template <int METRIC>
+__global__ __launch_bounds__(kBlock) void knn_sample_kernel(KnnSampleArgs a) {
+  const int64_t npairs = a.n >> 1;
+  const int64_t stride = npairs / gridDim.x;  // >= kSamplePerBlock/2 since n >= kSampleMinN
+  const int64_t p0 = (int64_t)blockIdx.x * stride;
+  const int64_t bbase = dist_bin_base(a.r);
+  for (int j = threadIdx.x; j < kSamplePerBlock / 2; j += kBlock) {
+    const int64_t i = 2 * (p0 + j);
+    const double2 xv = *reinterpret_cast<const double2*>(a.x + i);
+    const double2 yv = *reinterpret_cast<const double2*>(a.y + i);
+    double d;
+    if (knn_candidate<METRIC>(a.qx, a.qy, a.qr, xv.x, yv.x, a.s_r, a.r, d))
+      atomicAdd(&a.st->hist[dist_bin(d, bbase)], 1u);
+    if (knn_candidate<METRIC>(a.qx, a.qy, a.qr, xv.y, yv.y, a.s_r, a.r, d))
+      atomicAdd(&a.st->hist[dist_bin(d, bbase)], 1u);
+  }
+  // last-arriving block picks the threshold (split-K style ticket, agent-scope fences)
+  __shared__ int s_last;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    const uint32_t t = atomicAdd(&a.st->ticket, 1u);
+    s_last = (t == gridDim.x - 1);
+  }
+  __syncthreads();
+  if (!s_last) return;
+  __threadfence();
+  constexpr int kPer = kDistBins / kBlock;  // 16 bins per thread
+  __shared__ uint32_t wsum[kBlock / 64];
+  __shared__ int s_bin;
+  uint32_t v[kPer];
+  uint32_t s = 0;
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    v[j] = __hip_atomic_load(&a.st->hist[threadIdx.x * kPer + j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s += v[j];
+  }
+  // block exclusive scan (4 waves)
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  uint32_t inc = s;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t t = __shfl_up(inc, off, 64);
+    if (lane >= off) inc += t;
+  }
+  if (lane == 63) wsum[wid] = inc;
+  if (threadIdx.x == 0) s_bin = -1;
+  __syncthreads();
+  uint32_t before = 0;
+  for (int w = 0; w < wid; ++w) before += wsum[w];
+  const uint32_t excl = before + inc - s;
+  const uint32_t k = (uint32_t)a.k;
+  if (excl < k && k <= excl + s) {
+    uint32_t run = excl;
+    for (int j = 0; j < kPer; ++j) {
+      run += v[j];
+      if (run >= k) { s_bin = threadIdx.x * kPer + j; break; }
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double T = a.r;
+    if (s_bin >= 0) {
+      const double up = dist_bin_upper(s_bin, bbase);
+      T = up < a.r ? up : a.r;
+    }
+    a.st->T = T;
+    a.st->s_pre = s_prefilter(T, a.metric);
+    a.st->ticket = 0;
+  }
+  for (int j = threadIdx.x; j < kDistBins; j += kBlock) a.st->hist[j] = 0u;
+}
+
+hipError_t launch_knn_sample(gf_ctx* ctx, const KnnSampleArgs& a) {
+  KTimer t(ctx, GF_K_KNN_SAMPLE);
+  if (a.metric == 0)
+    hipLaunchKernelGGL(knn_sample_kernel<0>, dim3(kSampleBlocks), dim3(kBlock), 0, ctx->stream, a);
+  else
+    hipLaunchKernelGGL(knn_sample_kernel<1>, dim3(kSampleBlocks), dim3(kBlock), 0, ctx->stream, a);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------
+// scan: grid-stride over point pairs, two pairs in flight per lane (64 B of loads)
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ void load_pair(const double* __restrict__ x, const double* __restrict__ y, int64_t p,
+                                          int64_t end, double2& xv, double2& yv) {
+  const int64_t i = 2 * p;
+  if (i + 1 < end) {
+    xv = *reinterpret_cast<const double2*>(x + i);
+    yv = *reinterpret_cast<const double2*>(y + i);
+  } else if (i < end) {
+    xv.x = x[i]; yv.x = y[i];
+    xv.y = NAN; yv.y = NAN;  // NaN never passes the distance prefilter
+  } else {
+    xv.x = xv.y = yv.x = yv.y = NAN;
+  }
+}
+
+__device__ __forceinline__ void wave_append(bool c, double d, uint32_t idx, KnnState* st, double* cand_d,
+                                            uint32_t* cand_i, unsigned long long cap) {
+  const uint64_t m = __ballot(c);
+  if (m == 0) return;
+  const int lane = threadIdx.x & 63;
+  const int leader = __ffsll((unsigned long long)m) - 1;
+  unsigned long long base = 0;
+  if (lane == leader) base = atomicAdd(&st->count, (unsigned long long)__popcll(m));
+  base = __shfl(base, leader, 64);
+  if (c) {
+    const unsigned long long pos = base + (unsigned long long)__popcll(m & ((1ull << lane) - 1ull));
+    if (pos < cap) {
+      cand_d[pos] = d;
+      cand_i[pos] = idx;
+    }
+  }
+}
+
+template <int METRIC>
+__global__ __launch_bounds__(kBlock) void knn_scan_kernel(KnnScanArgs a) {
+  const double sp = a.use_state ? a.st->s_pre : a.s_pre;
+  const double T = a.use_state ? a.st->T : a.T;
+  const int64_t pend = (a.end + 1) >> 1;
+  const int lane = threadIdx.x & 63;
+  const int64_t wstride = (int64_t)gridDim.x * kBlock;
+  int64_t base = (a.begin >> 1) + (int64_t)blockIdx.x * kBlock + (threadIdx.x & ~63);
+  for (; base < pend; base += 2 * wstride) {
+    const int64_t p0 = base + lane, p1 = base + wstride + lane;
+    double2 xa, ya, xb, yb;
+    load_pair(a.x, a.y, p0, a.end, xa, ya);
+    load_pair(a.x, a.y, p1, a.end, xb, yb);
+    double d0 = 0, d1 = 0, d2 = 0, d3 = 0;
+    const bool c0 = knn_candidate<METRIC>(a.qx, a.qy, a.qr, xa.x, ya.x, sp, T, d0);
+    const bool c1 = knn_candidate<METRIC>(a.qx, a.qy, a.qr, xa.y, ya.y, sp, T, d1);
+    const bool c2 = knn_candidate<METRIC>(a.qx, a.qy, a.qr, xb.x, yb.x, sp, T, d2);
+    const bool c3 = knn_candidate<METRIC>(a.qx, a.qy, a.qr, xb.y, yb.y, sp, T, d3);
+    if (__ballot(c0 | c1 | c2 | c3)) {  // wave-uniform, rare once T is tight
+      wave_append(c0, d0, (uint32_t)(2 * p0), a.st, a.cand_d, a.cand_i, a.cap);
+      wave_append(c1, d1, (uint32_t)(2 * p0 + 1), a.st, a.cand_d, a.cand_i, a.cap);
+      wave_append(c2, d2, (uint32_t)(2 * p1), a.st, a.cand_d, a.cand_i, a.cap);
+      wave_append(c3, d3, (uint32_t)(2 * p1 + 1), a.st, a.cand_d, a.cand_i, a.cap);
+    }
+  }
+}
+
+hipError_t launch_knn_scan(gf_ctx* ctx, const KnnScanArgs& a, int blocks) {
+  KTimer t(ctx, GF_K_KNN_SCAN);
+  if (a.metric == 0)
+    hipLaunchKernelGGL(knn_scan_kernel<0>, dim3(blocks), dim3(kBlock), 0, ctx->stream, a);
+  else
+    hipLaunchKernelGGL(knn_scan_kernel<1>, dim3(blocks), dim3(kBlock), 0, ctx->stream, a);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------
+// select / merge: LDS bitonic sort on (d bits, objID key, idx), wave-0 objID dedupe
+// ---------------------------------------------------------------------------------------
+constexpr int kSelThreads = 1024;
+
+__device__ __forceinline__ bool key_gt(const uint64_t* sd, const uint64_t* so, const int64_t* si, int i, int j) {
+  if (sd[i] != sd[j]) return sd[i] > sd[j];
+  if (so[i] != so[j]) return so[i] > so[j];
+  return si[i] > si[j];
+}
+
+__device__ void bitonic_sort(uint64_t* sd, uint64_t* so, int64_t* si, int P) {
+  for (int size = 2; size <= P; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int t = threadIdx.x; t < (P >> 1); t += blockDim.x) {
+        const int i = 2 * stride * (t / stride) + (t & (stride - 1));
+        const int j = i + stride;
+        const bool up = (i & size) == 0;
+        if (key_gt(sd, so, si, i, j) == up) {
+          uint64_t td = sd[i]; sd[i] = sd[j]; sd[j] = td;
+          uint64_t to = so[i]; so[i] = so[j]; so[j] = to;
+          int64_t ti = si[i]; si[i] = si[j]; si[j] = ti;
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+__device__ __forceinline__ int pow2ceil(int v) {
+  int p = 2;
+  while (p < v) p <<= 1;
+  return p;
+}
+
+__device__ void pad_keys(uint64_t* sd, uint64_t* so, int64_t* si, int cnt, int P) {
+  for (int i = cnt + threadIdx.x; i < P; i += blockDim.x) {
+    sd[i] = ~0ull; so[i] = ~0ull; si[i] = INT64_MAX;
+  }
+}
+
+// first k distinct objIDs of the sorted [0, cnt) -> (rd, ro, ri); returns the count (all threads)
+__device__ int dedupe_first_k(const uint64_t* sd, const uint64_t* so, const int64_t* si, int cnt, int k,
+                              uint64_t* rd, uint64_t* ro, int64_t* ri, int* s_n) {
+  if ((threadIdx.x >> 6) == 0) {
+    const int lane = threadIdx.x & 63;
+    int acc = 0;
+    for (int base = 0; base < cnt && acc < k; base += 64) {
+      const int i = base + lane;
+      const bool valid = i < cnt;
+      const uint64_t o = valid ? so[i] : 0ull;
+      bool dup = false;
+      for (int j = 0; j < acc; ++j) dup |= (ro[j] == o);
+      for (int j = 0; j < 64; ++j) {
+        const uint64_t oj = __shfl(o, j, 64);
+        dup |= (j < lane) && (oj == o);
+      }
+      const bool keep = valid && !dup;
+      const uint64_t m = __ballot(keep);
+      const int rank = __popcll(m & ((1ull << lane) - 1ull));
+      if (keep && acc + rank < k) {
+        rd[acc + rank] = sd[i]; ro[acc + rank] = o; ri[acc + rank] = si[i];
+      }
+      const int add = __popcll(m);
+      acc = (acc + add < k) ? acc + add : k;
+    }
+    if (lane == 0) *s_n = acc;
+  }
+  __syncthreads();
+  return *s_n;
+}
+
+__global__ __launch_bounds__(kSelThreads) void knn_select_kernel(KnnSelectArgs a) {
+  __shared__ uint64_t sd[kSortCap], so[kSortCap];
+  __shared__ int64_t si[kSortCap];
+  __shared__ uint64_t rd[kMaxK], ro[kMaxK];
+  __shared__ int64_t ri[kMaxK];
+  __shared__ uint32_t hist[kDistBins];
+  __shared__ uint32_t wsum[kSelThreads / 64];
+  __shared__ int s_cnt, s_n, s_bin;
+  __shared__ uint32_t s_S;
+
+  const int tid = threadIdx.x;
+  const int k = a.k;
+  const unsigned long long count = a.st->count;
+  const bool overflow = count > a.cap;
+  const int64_t M = overflow ? 0 : (int64_t)count;
+  const double T = a.use_state ? a.st->T : a.T;
+  int status = overflow ? 1 : 0;
+  int nres = 0;
+
+  if (!overflow) {
+    // A: histogram of candidate distances over [0, T]
+    for (int i = tid; i < kDistBins; i += kSelThreads) hist[i] = 0u;
+    __syncthreads();
+    const int64_t bbase = dist_bin_base(T);
+    for (int64_t i = tid; i < M; i += kSelThreads) atomicAdd(&hist[dist_bin(a.cand_d[i], bbase)], 1u);
+    __syncthreads();
+    // B: bin holding the k-th candidate (4 bins per thread, block scan)
+    uint32_t v[4], s = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { v[j] = hist[4 * tid + j]; s += v[j]; }
+    const int lane = tid & 63, wid = tid >> 6;
+    uint32_t inc = s;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint32_t t = __shfl_up(inc, off, 64);
+      if (lane >= off) inc += t;
+    }
+    if (lane == 63) wsum[wid] = inc;
+    if (tid == 0) { s_bin = kDistBins - 1; s_S = (uint32_t)M; }
+    __syncthreads();
+    uint32_t before = 0;
+    for (int w = 0; w < wid; ++w) before += wsum[w];
+    const uint32_t excl = before + inc - s;
+    if (excl < (uint32_t)k && (uint32_t)k <= excl + s) {
+      uint32_t run = excl;
+      for (int j = 0; j < 4; ++j) {
+        run += v[j];
+        if (run >= (uint32_t)k) { s_bin = 4 * tid + j; s_S = run; break; }
+      }
+    }
+    __syncthreads();
+    const int bstar = s_bin;
+    bool done = false;
+    // C: fast path -- survivors (bins <= bstar) fit the LDS sort
+    if (s_S <= (uint32_t)kSortCap) {
+      if (tid == 0) s_cnt = 0;
+      __syncthreads();
+      for (int64_t i = tid; i < M; i += kSelThreads) {
+        const double d = a.cand_d[i];
+        if (dist_bin(d, bbase) <= bstar) {
+          const int pos = atomicAdd(&s_cnt, 1);
+          const uint32_t ci = a.cand_i[i];
+          sd[pos] = dbits(d); si[pos] = ci; so[pos] = okey(a.objID[ci]);
+        }
+      }
+      __syncthreads();
+      const int cnt = s_cnt;
+      const int P = pow2ceil(cnt);
+      pad_keys(sd, so, si, cnt, P);
+      __syncthreads();
+      bitonic_sort(sd, so, si, P);
+      nres = dedupe_first_k(sd, so, si, cnt, k, rd, ro, ri, &s_n);
+      done = (nres >= k) || (cnt == M);
+    }
+    // D: general path -- every candidate, chunk by chunk, running top-k-distinct list
+    if (!done) {
+      int nr = 0;
+      const int chunk = kSortCap - k;
+      for (int64_t start = 0; start < M; start += chunk) {
+        const int len = (int)((M - start) < chunk ? (M - start) : chunk);
+        for (int i = tid; i < nr; i += kSelThreads) { sd[i] = rd[i]; so[i] = ro[i]; si[i] = ri[i]; }
+        for (int i = tid; i < len; i += kSelThreads) {
+          const uint32_t ci = a.cand_i[start + i];
+          sd[nr + i] = dbits(a.cand_d[start + i]); si[nr + i] = ci; so[nr + i] = okey(a.objID[ci]);
+        }
+        const int cnt = nr + len;
+        const int P = pow2ceil(cnt);
+        pad_keys(sd, so, si, cnt, P);
+        __syncthreads();
+        bitonic_sort(sd, so, si, P);
+        nr = dedupe_first_k(sd, so, si, cnt, k, rd, ro, ri, &s_n);
+      }
+      nres = nr;
+    }
+    if (nres < k && T < a.r) status = 1;  // fewer than k distinct objIDs below T: exact fallback
+  }
+  RecView out = rec_view(a.result, k);
+  if (status == 0)
+    for (int i = tid; i < nres; i += kSelThreads) {
+      out.d[i] = from_bits(rd[i]); out.o[i] = from_okey(ro[i]); out.i[i] = ri[i] + a.idx_base;
+    }
+  if (tid == 0) {
+    out.h->status = status;
+    out.h->n = status ? 0 : nres;
+    out.h->k = k;
+    out.h->flags = overflow ? 1 : 0;
+    out.h->candidates = (int64_t)count;
+    out.h->threshold = T;
+    a.st->count = 0ull;  // ready for the next window on this stream
+  }
+}
+
+hipError_t launch_knn_select(gf_ctx* ctx, const KnnSelectArgs& a) {
+  KTimer t(ctx, GF_K_KNN_SELECT);
+  hipLaunchKernelGGL(knn_select_kernel, dim3(1), dim3(kSelThreads), 0, ctx->stream, a);
+  return hipGetLastError();
+}
+
+// merge of per-shard records: nrec * k <= kSortCap (checked by the host)
+__global__ __launch_bounds__(kSelThreads) void knn_merge_kernel(int32_t k, const char* records, int32_t nrec,
+                                                                size_t rec_bytes, void* result) {
+  __shared__ uint64_t sd[kSortCap], so[kSortCap];
+  __shared__ int64_t si[kSortCap];
+  __shared__ uint64_t rd[kMaxK], ro[kMaxK];
+  __shared__ int64_t ri[kMaxK];
+  __shared__ int s_off[65], s_n, s_status;
+  const int tid = threadIdx.x;
+  if (tid == 0) {
+    int off = 0, st = 0;
+    for (int r = 0; r < nrec; ++r) {
+      const gf_knn_header* h = (const gf_knn_header*)(records + (size_t)r * rec_bytes);
+      s_off[r] = off;
+      off += h->status == 0 ? h->n : 0;
+      st = h->status > st ? h->status : st;
+    }
+    s_off[nrec] = off;
+    s_status = st;
+  }
+  __syncthreads();
+  for (int r = 0; r < nrec; ++r) {
+    RecView in = rec_view((void*)(records + (size_t)r * rec_bytes), k);
+    const int n = s_off[r + 1] - s_off[r];
+    for (int i = tid; i < n; i += kSelThreads) {
+      sd[s_off[r] + i] = dbits(in.d[i]); so[s_off[r] + i] = okey(in.o[i]); si[s_off[r] + i] = in.i[i];
+    }
+  }
+  const int cnt = s_off[nrec];
+  const int P = pow2ceil(cnt);
+  pad_keys(sd, so, si, cnt, P);
+  __syncthreads();
+  bitonic_sort(sd, so, si, P);
+  const int nres = dedupe_first_k(sd, so, si, cnt, k, rd, ro, ri, &s_n);
+  RecView out = rec_view(result, k);
+  for (int i = tid; i < nres; i += kSelThreads) {
+    out.d[i] = from_bits(rd[i]); out.o[i] = from_okey(ro[i]); out.i[i] = ri[i];
+  }
+  if (tid == 0) {
+    out.h->status = s_status;
+    out.h->n = s_status ? 0 : nres;
+    out.h->k = k;
+    out.h->flags = 0;
+    out.h->candidates = cnt;
+    out.h->threshold = 0.0;
+  }
+}
+
+hipError_t launch_knn_merge(gf_ctx* ctx, int32_t k, const void* records, int32_t nrec, void* result) {
+  const size_t rb = gf_knn_result_bytes(k);
+  hipLaunchKernelGGL(knn_merge_kernel, dim3(1), dim3(kSelThreads), 0, ctx->stream, k, (const char*)records, nrec,
+                     rb, result);
+  return hipGetLastError();
+}
+
+}  // namespace gf

@@ -1,0 +1,90 @@
+"""Multi-GPU evaluation of one window: points sharded by grid-cell column ranges across the
+GPUs of one node (one process per GPU, torch.distributed over RCCL/xGMI).
+
+The reference distributes by keyBy(gridID) (hash of the cell string) over Flink subtasks
+(PointPointRangeQuery.java:144-148) and funnels kNN through a parallelism-1 windowAll
+(PointPointKNNQuery.java:198-200).  Here each rank owns a contiguous band of cell columns;
+range hits need no exchange (concatenate), kNN needs one all-gather of k x (dist, objID, idx)
+records followed by the same deterministic top-k-distinct merge on every rank.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import _lib
+
+
+def column_bands(n_cols: int, world: int, col_counts=None):
+    """Cell-column ranges [lo, hi) per rank.  With a per-column point histogram the bands
+    balance point counts (the bucketing histogram doubles as the load balancer); without
+    one they split the columns evenly."""
+    if col_counts is None:
+        edges = [(r * n_cols) // world for r in range(world + 1)]
+    else:
+        c = np.cumsum(np.asarray(col_counts, np.float64))
+        total = c[-1] if len(c) else 0.0
+        edges = [0]
+        for r in range(1, world):
+            edges.append(int(np.searchsorted(c, total * r / world)) + 1)
+        edges.append(n_cols)
+        for i in range(1, len(edges)):
+            edges[i] = max(edges[i], edges[i - 1])
+    return [(edges[r], edges[r + 1]) for r in range(world)]
+
+
+def band_x_range(grid, lo: int, hi: int):
+    """Coordinate range covering cell columns [lo, hi) (for generating a rank's shard)."""
+    return grid.getMinX() + lo * grid.getCellLength(), grid.getMinX() + hi * grid.getCellLength()
+
+
+def shard_of_columns(cx: np.ndarray, bands) -> np.ndarray:
+    """Rank owning each point's column; out-of-grid columns go to the nearest edge rank."""
+    lows = np.array([b[0] for b in bands])
+    r = np.searchsorted(lows, cx, side="right") - 1
+    return np.clip(r, 0, len(bands) - 1)
+
+
+def merge_knn_records_host(records, k: int):
+    """Top-k-distinct merge of per-shard records (host bytes) -> (objID, dist, idx)."""
+    from .spatialOperators import decode_knn_record, knn_merge_host
+
+    lists = []
+    for raw in records:
+        st, o, d, i = decode_knn_record(raw, k)
+        if st != 0:
+            raise _lib.GeoFlinkError(_lib.GF_ERR_HIP, "shard record needs the exact fallback; decode it first")
+        lists.append((o, d, i))
+    return knn_merge_host(k, lists)
+
+
+def allgather_knn_lists(objID, dist, idx, k: int, group=None):
+    """Any backend (gloo on CPU too): all_gather_object of this rank's sorted list, then the
+    deterministic top-k-distinct merge.  Identical result on every rank."""
+    import torch.distributed as dist_
+
+    world = dist_.get_world_size(group)
+    mine = (np.asarray(objID, np.int64), np.asarray(dist, np.float64), np.asarray(idx, np.int64))
+    gathered = [None] * world
+    dist_.all_gather_object(gathered, mine, group=group)
+    from .spatialOperators import knn_merge_host
+
+    return knn_merge_host(k, gathered)
+
+
+def allgather_knn_records(record, k: int, merged_out, group=None):
+    """RCCL path: all-gather this rank's device kNN record (uint8 tensor of
+    knn_record_bytes(k)) over xGMI, then merge the world's records on the device
+    (gf_knn_merge_dev) into `merged_out`.  Stream-ordered, no host sync."""
+    import ctypes as C  # noqa: F401
+
+    import torch
+    import torch.distributed as dist_
+
+    world = dist_.get_world_size(group)
+    rb = record.numel()
+    gathered = torch.empty(world * rb, dtype=torch.uint8, device=record.device)
+    dist_.all_gather_into_tensor(gathered, record, group=group)
+    ctx = _lib.context(record.device.index)
+    _lib.check(_lib.lib().gf_knn_merge_dev(ctx.handle, int(k), gathered.data_ptr(), world, merged_out.data_ptr()),
+               ctx.handle, "gf_knn_merge_dev")
+    return merged_out

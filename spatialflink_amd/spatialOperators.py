@@ -1,0 +1,404 @@
+"""Spatial operators -- mirrors of GeoFlink.spatialOperators.{range,knn,join} for one window.
+
+The reference builds a Flink DAG per operator and evaluates each window inside a
+WindowFunction.apply; here run() takes the window's points (a PointWindow, device SoA) and
+evaluates that window on the GPU through the C ABI -- the body of apply() is what moved.
+
+  PointPointRangeQuery.run(window, Set<Point>, r)     -- range/PointPointRangeQuery.java:37,111-187
+  PointPolygonRangeQuery.run(window, Set<Polygon>, r) -- range/PointPolygonRangeQuery.java:31,134-205
+  PointPointKNNQuery.run(window, Point, r, k)         -- knn/PointPointKNNQuery.java:33,132-201
+  PointPointJoinQuery.run(ordinary, query, r)         -- join/PointPointJoinQuery.java:24,124-183
+
+Errors follow the reference: unsupported query types raise ValueError ("Not yet support",
+IllegalArgumentException), candidate layers <= 0 raise CandidateLayersError (System.exit(1)).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from enum import Enum
+
+import numpy as np
+
+from . import _lib
+from .spatialIndices import UniformGrid
+from .spatialObjects import Point, PointWindow, Polygon, PolygonSet
+
+
+class QueryType(Enum):
+    """QueryType.java:3-8"""
+    RealTime = 0
+    WindowBased = 1
+    CountBased = 2
+    RealTimeNaive = 3
+
+
+class QueryConfiguration:
+    """QueryConfiguration.java:5-57 (+ distanceMetric: JTS Coordinate.distance variant)."""
+
+    def __init__(self, queryType: QueryType = None):
+        self.queryType = queryType
+        self.windowSize = 0
+        self.slideStep = 0
+        self.allowedLateness = 0
+        self.approximateQuery = False
+        self.distanceMetric = _lib.METRIC_SQRT
+
+    def getQueryType(self): return self.queryType
+    def setQueryType(self, t): self.queryType = t
+    def getWindowSize(self): return self.windowSize
+    def setWindowSize(self, v): self.windowSize = int(v)
+    def getSlideStep(self): return self.slideStep
+    def setSlideStep(self, v): self.slideStep = int(v)
+    def getAllowedLateness(self): return self.allowedLateness
+    def setAllowedLateness(self, v): self.allowedLateness = int(v)
+    def isApproximateQuery(self): return self.approximateQuery
+    def setApproximateQuery(self, v): self.approximateQuery = bool(v)
+
+
+_SUPPORTED = (QueryType.RealTime, QueryType.WindowBased)
+
+
+def _require_supported(conf: QueryConfiguration):
+    # RealTime and WindowBased share the per-point semantics evaluated here (the RealTime
+    # flatMap bodies equal the window apply bodies); the others throw in the reference too.
+    if conf.getQueryType() not in _SUPPORTED:
+        raise ValueError("Not yet support")
+
+
+class SpatialOperator:
+    def __init__(self, conf: QueryConfiguration, index: UniformGrid):
+        self.conf = conf
+        self.index = index
+        self._plans = {}
+
+    def getQueryConfiguration(self):
+        return self.conf
+
+    def getSpatialIndex(self):
+        return self.index
+
+
+# ----------------------------------------------------------------------------------------
+# range
+# ----------------------------------------------------------------------------------------
+@dataclass
+class RangeResult:
+    """Selection bitmap of one window (bit i = point i emitted) plus counts.
+
+    For approximate point-point queries with |Q| > 1 the reference emits candidate-cell
+    points once per query point: `multi` marks those points (multiplicity |Q|)."""
+
+    window: PointWindow
+    bitmap: object          # torch int64 [(n+63)/64] (uint64 words)
+    counts: object          # torch int64 [2]: points emitted, multiset size
+    multi: object = None
+    nq: int = 1
+    ctx: object = None
+
+    def count(self) -> int:
+        return int(self.counts[0].item())
+
+    def multiset_size(self) -> int:
+        return int(self.counts[1].item())
+
+    def indices(self) -> np.ndarray:
+        """Ascending indices of emitted points (each once)."""
+        return bitmap_indices(self.ctx, self.bitmap, self.window.n)
+
+    def multiset_indices(self) -> np.ndarray:
+        idx = self.indices().astype(np.int64)
+        if self.multi is None or self.nq <= 1:
+            return idx
+        m = bitmap_indices(self.ctx, self.multi, self.window.n).astype(np.int64)
+        return np.sort(np.concatenate([idx] + [m] * (self.nq - 1)), kind="stable")
+
+    def points(self, uGrid=None):
+        return [self.window.point(i, uGrid) for i in self.indices()]
+
+
+def bitmap_indices(ctx, bitmap, n) -> np.ndarray:
+    import torch
+
+    cap = max(1, int(n))
+    out = torch.empty(cap, dtype=torch.int32, device=bitmap.device)
+    cnt = C.c_int64()
+    st = _lib.lib().gf_bitmap_to_indices(ctx.handle, bitmap.data_ptr(), int(n), out.data_ptr(), cap, C.byref(cnt))
+    _lib.check(st, ctx.handle, "gf_bitmap_to_indices")
+    return out[: cnt.value].cpu().numpy().view(np.uint32)
+
+
+class _RangeBase(SpatialOperator):
+    def _evaluate(self, plan, window: PointWindow, nq: int) -> RangeResult:
+        import torch
+
+        ctx = _lib.context(window.x.device.index)
+        n = window.n
+        words = max(1, (n + 63) // 64)
+        bitmap = torch.empty(words, dtype=torch.int64, device=window.x.device)
+        multi = torch.empty(words, dtype=torch.int64, device=window.x.device) if nq > 1 else None
+        counts = torch.zeros(2, dtype=torch.int64, device=window.x.device)
+        pts = window.c_struct()
+        st = _lib.lib().gf_range_run(plan, C.byref(pts), bitmap.data_ptr(),
+                                     multi.data_ptr() if multi is not None else None, counts.data_ptr())
+        _lib.check(st, ctx.handle, "gf_range_run")
+        return RangeResult(window, bitmap, counts, multi, nq, ctx)
+
+    def _plan(self, key, create):
+        plan = self._plans.get(key)
+        if plan is None:
+            plan = create()
+            self._plans[key] = plan
+        return plan
+
+    def __del__(self):
+        if _lib._lib is not None:
+            for p in getattr(self, "_plans", {}).values():
+                _lib._lib.gf_range_plan_destroy(p)
+
+
+class PointPointRangeQuery(_RangeBase):
+    """range/PointPointRangeQuery.java -- window-based point-point range query."""
+
+    def run(self, window: PointWindow, queryPointSet, queryRadius: float) -> RangeResult:
+        _require_supported(self.conf)
+        qs = list(queryPointSet)
+        qx = np.array([q.x for q in qs], np.float64)
+        qy = np.array([q.y for q in qs], np.float64)
+        ctx = _lib.context(window.x.device.index)
+        key = (ctx.device, tuple(qx.tolist()), tuple(qy.tolist()), float(queryRadius),
+               bool(self.conf.approximateQuery), int(self.conf.distanceMetric))
+
+        def create():
+            h = C.c_void_p()
+            st = _lib.lib().gf_range_pp_plan_create(ctx.handle, C.byref(self.index.c_grid), qx.ctypes.data,
+                                                    qy.ctypes.data, len(qs), float(queryRadius),
+                                                    int(self.conf.approximateQuery), int(self.conf.distanceMetric),
+                                                    C.byref(h))
+            _lib.check(st, ctx.handle, "gf_range_pp_plan_create")
+            return h
+
+        plan = self._plan(key, create)
+        nq = len(qs) if self.conf.approximateQuery else 1
+        return self._evaluate(plan, window, nq)
+
+
+class PointPolygonRangeQuery(_RangeBase):
+    """range/PointPolygonRangeQuery.java -- window-based point-polygon range query."""
+
+    def run(self, window: PointWindow, queryPolygonSet, queryRadius: float) -> RangeResult:
+        _require_supported(self.conf)
+        polys = list(queryPolygonSet)
+        ctx = _lib.context(window.x.device.index)
+        key = (ctx.device, tuple(id(p) for p in polys), float(queryRadius), bool(self.conf.approximateQuery),
+               int(self.conf.distanceMetric))
+
+        def create():
+            ps = PolygonSet(polys)
+            cs = ps.c_struct()
+            h = C.c_void_p()
+            st = _lib.lib().gf_range_ppoly_plan_create(ctx.handle, C.byref(self.index.c_grid), C.byref(cs),
+                                                       float(queryRadius), int(self.conf.approximateQuery),
+                                                       int(self.conf.distanceMetric), C.byref(h))
+            _lib.check(st, ctx.handle, "gf_range_ppoly_plan_create")
+            return h
+
+        plan = self._plan(key, create)
+        return self._evaluate(plan, window, 1)
+
+
+# ----------------------------------------------------------------------------------------
+# kNN
+# ----------------------------------------------------------------------------------------
+@dataclass
+class KNNResult:
+    """Tuple3<winStart, winEnd, PriorityQueue<Tuple2<Point, Double>>> as sorted arrays:
+    rank i = (objID[i], dist[i]), point index idx[i] in the window."""
+
+    windowStart: int
+    windowEnd: int
+    objID: np.ndarray
+    dist: np.ndarray
+    idx: np.ndarray
+
+    def __len__(self):
+        return len(self.objID)
+
+    def tuples(self):
+        return list(zip(self.objID.tolist(), self.dist.tolist()))
+
+
+def knn_record_bytes(k: int) -> int:
+    return int(_lib.lib().gf_knn_result_bytes(int(k)))
+
+
+def decode_knn_record(raw: bytes, k: int):
+    """Decode a host copy of a device kNN record -> (status, objID, dist, idx)."""
+    h = _lib.GfKnnHeader.from_buffer_copy(raw[: C.sizeof(_lib.GfKnnHeader)])
+    off = C.sizeof(_lib.GfKnnHeader)
+    d = np.frombuffer(raw, np.float64, k, off)
+    o = np.frombuffer(raw, np.int64, k, off + 8 * k)
+    i = np.frombuffer(raw, np.int64, k, off + 16 * k)
+    return h.status, o[: h.n].copy(), d[: h.n].copy(), i[: h.n].copy()
+
+
+class PointPointKNNQuery(SpatialOperator):
+    """knn/PointPointKNNQuery.java -- continuous kNN of one query point within radius r."""
+
+    def plan(self, window_device: int, queryPoint: Point, queryRadius: float, k: int):
+        ctx = _lib.context(window_device)
+        key = (ctx.device, queryPoint.x, queryPoint.y, float(queryRadius), int(k), int(self.conf.distanceMetric))
+        plan = self._plans.get(key)
+        if plan is None:
+            h = C.c_void_p()
+            st = _lib.lib().gf_knn_pp_plan_create(ctx.handle, C.byref(self.index.c_grid), float(queryPoint.x),
+                                                  float(queryPoint.y), float(queryRadius), int(k),
+                                                  int(self.conf.distanceMetric), C.byref(h))
+            _lib.check(st, ctx.handle, "gf_knn_pp_plan_create")
+            self._plans[key] = plan = h
+        return ctx, plan
+
+    def run(self, window: PointWindow, queryPoint: Point, queryRadius: float, k: int) -> KNNResult:
+        _require_supported(self.conf)
+        if k is None or int(k) < 1:
+            raise ValueError("k must be >= 1 (PriorityQueue initialCapacity < 1)")
+        ctx, plan = self.plan(window.x.device.index, queryPoint, queryRadius, k)
+        kk = int(k)
+        oo = np.empty(kk, np.int64); od = np.empty(kk, np.float64); oi = np.empty(kk, np.int64)
+        n = C.c_int32()
+        pts = window.c_struct()
+        st = _lib.lib().gf_knn_run(plan, C.byref(pts), oo.ctypes.data, od.ctypes.data, oi.ctypes.data, C.byref(n))
+        _lib.check(st, ctx.handle, "gf_knn_run")
+        m = n.value
+        return KNNResult(window.start, window.end, oo[:m].copy(), od[:m].copy(), oi[:m].copy())
+
+    def enqueue(self, window: PointWindow, queryPoint: Point, queryRadius: float, k: int, record):
+        """Async: evaluate the window into a device record (torch uint8 tensor of
+        knn_record_bytes(k)); pair with finish() after copying the record to the host."""
+        ctx, plan = self.plan(window.x.device.index, queryPoint, queryRadius, k)
+        pts = window.c_struct()
+        _lib.check(_lib.lib().gf_knn_enqueue(plan, C.byref(pts), record.data_ptr()), ctx.handle, "gf_knn_enqueue")
+
+    def finish(self, window: PointWindow, queryPoint: Point, queryRadius: float, k: int, raw: bytes) -> KNNResult:
+        ctx, plan = self.plan(window.x.device.index, queryPoint, queryRadius, k)
+        kk = int(k)
+        oo = np.empty(kk, np.int64); od = np.empty(kk, np.float64); oi = np.empty(kk, np.int64)
+        n = C.c_int32()
+        buf = C.create_string_buffer(bytes(raw), len(raw))
+        pts = window.c_struct()
+        st = _lib.lib().gf_knn_decode(plan, C.byref(pts), buf, oo.ctypes.data, od.ctypes.data, oi.ctypes.data,
+                                      C.byref(n))
+        _lib.check(st, ctx.handle, "gf_knn_decode")
+        m = n.value
+        return KNNResult(window.start, window.end, oo[:m].copy(), od[:m].copy(), oi[:m].copy())
+
+    def set_capacity(self, window_device, queryPoint, queryRadius, k, cap):
+        ctx, plan = self.plan(window_device, queryPoint, queryRadius, k)
+        _lib.check(_lib.lib().gf_knn_plan_set_capacity(plan, int(cap)), ctx.handle, "set_capacity")
+
+    def __del__(self):
+        if _lib._lib is not None:
+            for p in getattr(self, "_plans", {}).values():
+                _lib._lib.gf_knn_plan_destroy(p)
+
+
+def knn_merge_host(k: int, lists):
+    """Top-k distinct objIDs of several sorted (objID, dist, idx) lists -- the windowAll funnel
+    (KNNQuery.java:213-272) across shards; host code of the library (no GPU needed)."""
+    counts = np.array([len(l[0]) for l in lists], np.int32)
+    o = np.ascontiguousarray(np.concatenate([np.asarray(l[0], np.int64) for l in lists]) if lists else
+                             np.zeros(0, np.int64))
+    d = np.ascontiguousarray(np.concatenate([np.asarray(l[1], np.float64) for l in lists]) if lists else
+                             np.zeros(0, np.float64))
+    i = np.ascontiguousarray(np.concatenate([np.asarray(l[2], np.int64) for l in lists]) if lists else
+                             np.zeros(0, np.int64))
+    oo = np.empty(k, np.int64); od = np.empty(k, np.float64); oi = np.empty(k, np.int64)
+    n = C.c_int32()
+    st = _lib.lib().gf_knn_merge_host(int(k), len(lists), counts.ctypes.data, o.ctypes.data, d.ctypes.data,
+                                      i.ctypes.data, oo.ctypes.data, od.ctypes.data, oi.ctypes.data, C.byref(n))
+    _lib.check(st, None, "gf_knn_merge_host")
+    return oo[: n.value].copy(), od[: n.value].copy(), oi[: n.value].copy()
+
+
+# ----------------------------------------------------------------------------------------
+# join
+# ----------------------------------------------------------------------------------------
+class PointPointJoinQuery(SpatialOperator):
+    """join/PointPointJoinQuery.java -- window-based point-point join.  index1 = uGrid
+    (ordinary stream), index2 = qGrid (query stream, replicated to neighbour cells)."""
+
+    def __init__(self, conf: QueryConfiguration, index1: UniformGrid, index2: UniformGrid = None):
+        super().__init__(conf, index1)
+        self.index2 = index2 if index2 is not None else index1
+
+    def run(self, ordinaryWindow: PointWindow, queryWindow: PointWindow, queryRadius: float) -> np.ndarray:
+        """Returns int64 [m, 2] pairs (ordinary index, query index), sorted."""
+        import torch
+
+        _require_supported(self.conf)
+        ctx = _lib.context(ordinaryWindow.x.device.index)
+        po, pq = ordinaryWindow.c_struct(), queryWindow.c_struct()
+        cap = max(1024, 4 * (ordinaryWindow.n + queryWindow.n))
+        for _ in range(2):
+            pairs = torch.empty(2 * cap, dtype=torch.int32, device=ordinaryWindow.x.device)
+            npairs = C.c_int64()
+            st = _lib.lib().gf_join_pp(ctx.handle, C.byref(self.index.c_grid), C.byref(self.index2.c_grid),
+                                       C.byref(po), C.byref(pq), float(queryRadius), int(self.conf.approximateQuery),
+                                       int(self.conf.distanceMetric), pairs.data_ptr(), cap, C.byref(npairs))
+            if st == _lib.GF_ERR_CAPACITY:
+                cap = int(npairs.value)
+                continue
+            _lib.check(st, ctx.handle, "gf_join_pp")
+            m = int(npairs.value)
+            out = pairs[: 2 * m].cpu().numpy().view(np.uint32).astype(np.int64).reshape(-1, 2)
+            order = np.lexsort((out[:, 1], out[:, 0]))
+            return out[order]
+        raise _lib.GeoFlinkError(_lib.GF_ERR_CAPACITY, "join output kept growing")
+
+
+# ----------------------------------------------------------------------------------------
+# cell assignment / bucketing (the ingest-side pieces of the path)
+# ----------------------------------------------------------------------------------------
+def assign_cells(window: PointWindow, grid: UniformGrid):
+    """K1: HelperClass.assignGridCellID for every point -> (cx, cy) int32 torch tensors."""
+    import torch
+
+    ctx = _lib.context(window.x.device.index)
+    n = window.n
+    cx = torch.empty(max(n, 1), dtype=torch.int32, device=window.x.device)
+    cy = torch.empty(max(n, 1), dtype=torch.int32, device=window.x.device)
+    pts = window.c_struct()
+    _lib.check(_lib.lib().gf_assign_cells(ctx.handle, C.byref(grid.c_grid), C.byref(pts), cx.data_ptr(),
+                                          cy.data_ptr()), ctx.handle, "gf_assign_cells")
+    return cx[:n], cy[:n]
+
+
+def bucket_by_cell(window: PointWindow, grid: UniformGrid):
+    """K2: keyBy(gridID) analogue -> (perm, cell_start) with bucket n*n = out-of-grid."""
+    import torch
+
+    ctx = _lib.context(window.x.device.index)
+    n = window.n
+    g = grid.getNumGridPartitions()
+    perm = torch.empty(max(n, 1), dtype=torch.int32, device=window.x.device)
+    start = torch.empty(g * g + 2, dtype=torch.int32, device=window.x.device)
+    pts = window.c_struct()
+    _lib.check(_lib.lib().gf_bucket_by_cell(ctx.handle, C.byref(grid.c_grid), C.byref(pts), perm.data_ptr(),
+                                            start.data_ptr()), ctx.handle, "gf_bucket_by_cell")
+    return perm[:n], start
+
+
+def synthetic_uniform(seed: int, n: int, minX: float, maxX: float, minY: float, maxY: float):
+    """java.util.Random(seed)-compatible uniform points (SyntheticGpsSource.java:23,40-41)."""
+    x = np.empty(n, np.float64)
+    y = np.empty(n, np.float64)
+    _lib.check(_lib.lib().gf_synth_uniform(int(seed), int(n), float(minX), float(maxX), float(minY), float(maxY),
+                                           x.ctypes.data, y.ctypes.data), None, "gf_synth_uniform")
+    return x, y
+
+
+__all__ = [
+    "QueryType", "QueryConfiguration", "PointPointRangeQuery", "PointPolygonRangeQuery", "PointPointKNNQuery",
+    "PointPointJoinQuery", "RangeResult", "KNNResult", "knn_merge_host", "assign_cells", "bucket_by_cell",
+    "synthetic_uniform", "Point", "Polygon", "PointWindow", "knn_record_bytes", "decode_knn_record",
+]

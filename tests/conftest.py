@@ -1,0 +1,37 @@
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (ROOT, os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests", "golden")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+BEIJING = (115.5, 117.6, 39.6, 41.1)
+QPOINT = (116.414899, 39.920374)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device); run with -m gpu")
+
+
+@pytest.fixture(scope="session")
+def oracle_mod():
+    import oracle
+
+    oracle.build()
+    return oracle
+
+
+@pytest.fixture(scope="session")
+def gpu():
+    """Skip-free on the GPU box: a gpu-marked test must fail loudly if no device is visible."""
+    import torch
+
+    assert torch.cuda.is_available(), "gpu test needs a visible HIP device"
+    import spatialflink_amd._lib as L
+
+    L.lib()
+    return torch.device("cuda", 0)

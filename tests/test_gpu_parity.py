@@ -1,0 +1,396 @@
+"""GPU parity: every hot-path kernel, through the C ABI, against the oracle (C restatement)
+and the committed golden fixtures.  Bit-exact for cells, index/pair sets and kNN
+(objID, rank) lists; kNN distances are compared with rtol 1e-12 (north star) and are in
+fact bit-identical.  Run on an MI355X with `pytest -m gpu`."""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import BEIJING, GOLDEN, QPOINT
+
+pytestmark = pytest.mark.gpu
+
+
+def load(name):
+    return np.load(os.path.join(GOLDEN, name))
+
+
+@pytest.fixture(scope="module")
+def sf(gpu):
+    import spatialflink_amd
+
+    return spatialflink_amd
+
+
+def win(sf, x, y, objID=None):
+    return sf.PointWindow.from_numpy(np.asarray(x, np.float64), np.asarray(y, np.float64), objID)
+
+
+def conf(sf, approximate=False, metric=0):
+    c = sf.QueryConfiguration(sf.QueryType.WindowBased)
+    c.setApproximateQuery(approximate)
+    c.distanceMetric = metric
+    return c
+
+
+# ------------------------------------------------------------------ K1 cell assignment
+@pytest.mark.parametrize("n", [100, 500])
+def test_cells_golden(sf, n):
+    f = load(f"cells_n{n}.npz")
+    g = sf.UniformGrid(n, *BEIJING)
+    cx, cy = sf.assign_cells(win(sf, f["x"], f["y"]), g)
+    np.testing.assert_array_equal(cx.cpu().numpy(), f["cx"])
+    np.testing.assert_array_equal(cy.cpu().numpy(), f["cy"])
+
+
+def test_cells_random_large(sf, oracle_mod):
+    """fp64 division + floor + Java (int) on 1M+ points incl. exact cell boundaries."""
+    g = sf.UniformGrid(1000, *BEIJING)
+    og = oracle_mod.grid(1000, *BEIJING)
+    x0, y0 = oracle_mod.java_random_points(3, 1_000_001, 115.0, 118.2, 39.0, 41.7)
+    cl = og.cellLength
+    bx = 115.5 + np.arange(1001) * cl  # points on (and one ulp around) every cell edge
+    by = 39.6 + np.arange(1001) * cl
+    x = np.concatenate([x0, bx, np.nextafter(bx, -np.inf), np.nextafter(bx, np.inf), [np.nan, np.inf, -1e300]])
+    y = np.concatenate([y0, by, np.nextafter(by, np.inf), np.nextafter(by, -np.inf), [40.0, np.nan, 1e300]])
+    cx, cy = sf.assign_cells(win(sf, x, y), g)
+    ocx, ocy = oracle_mod.assign_cells(og, x, y)
+    np.testing.assert_array_equal(cx.cpu().numpy(), ocx)
+    np.testing.assert_array_equal(cy.cpu().numpy(), ocy)
+
+
+def test_cells_odd_sizes(sf, oracle_mod):
+    g = sf.UniformGrid(100, *BEIJING)
+    og = oracle_mod.grid(100, *BEIJING)
+    for n in (1, 2, 3, 63, 64, 65, 129):
+        x, y = oracle_mod.java_random_points(n, n, *BEIJING)
+        cx, cy = sf.assign_cells(win(sf, x, y), g)
+        ocx, ocy = oracle_mod.assign_cells(og, x, y)
+        np.testing.assert_array_equal(cx.cpu().numpy(), ocx)
+        np.testing.assert_array_equal(cy.cpu().numpy(), ocy)
+
+
+# ------------------------------------------------------------------ K2 bucketing
+def test_bucket_by_cell(sf, oracle_mod):
+    g = sf.UniformGrid(100, *BEIJING)
+    og = oracle_mod.grid(100, *BEIJING)
+    x, y = oracle_mod.java_random_points(9, 200_001, 115.3, 117.8, 39.5, 41.2)
+    perm, start = sf.bucket_by_cell(win(sf, x, y), g)
+    perm = perm.cpu().numpy().view(np.uint32).astype(np.int64)
+    start = start.cpu().numpy().view(np.uint32).astype(np.int64)
+    cx, cy = oracle_mod.assign_cells(og, x, y)
+    valid = (cx >= 0) & (cy >= 0) & (cx < 100) & (cy < 100)
+    key = np.where(valid, cy.astype(np.int64) * 100 + cx, 100 * 100)
+    assert np.array_equal(np.sort(perm), np.arange(len(x)))
+    counts = np.bincount(key, minlength=100 * 100 + 1)
+    np.testing.assert_array_equal(np.diff(start), counts)
+    for b in range(0, 100 * 100 + 1, 97):
+        seg = perm[start[b]:start[b + 1]]
+        assert np.all(key[seg] == b)
+
+
+# ------------------------------------------------------------------ range point-point
+def test_range_pp_golden(sf):
+    f = load("range_pp.npz")
+    g = sf.UniformGrid(100, *BEIJING)
+    w = win(sf, f["x"], f["y"])
+    for qn in ("q1", "q3"):
+        qs = [sf.Point(str(i), a, b, 0, g) for i, (a, b) in enumerate(zip(f[f"{qn}_qx"], f[f"{qn}_qy"]))]
+        for r in (0.5, 0.05, 0.02, 0.0):
+            for ap in (0, 1):
+                res = sf.PointPointRangeQuery(conf(sf, bool(ap)), g).run(w, qs, r)
+                exp = f[f"{qn}_r{r}_a{ap}"]
+                np.testing.assert_array_equal(res.multiset_indices(), exp, err_msg=f"{qn} r={r} ap={ap}")
+                assert res.count() == len(np.unique(exp))
+                assert res.multiset_size() == len(exp)
+
+
+@pytest.mark.parametrize("r,n", [(0.5, 100), (0.05, 100), (0.02, 500), (0.3, 500), (0.0011, 1000)])
+def test_range_pp_large(sf, oracle_mod, r, n):
+    g = sf.UniformGrid(n, *BEIJING)
+    og = oracle_mod.grid(n, *BEIJING)
+    x, y = oracle_mod.java_random_points(17, 1_000_003, 115.4, 117.7, 39.5, 41.2)
+    w = win(sf, x, y)
+    q = sf.Point("q", *QPOINT, 0, g)
+    res = sf.PointPointRangeQuery(conf(sf), g).run(w, [q], r)
+    exp = oracle_mod.range_pp(og, x, y, [QPOINT[0]], [QPOINT[1]], r)
+    np.testing.assert_array_equal(res.indices().astype(np.int64), exp)
+
+
+def test_range_pp_multi_query_large(sf, oracle_mod):
+    g = sf.UniformGrid(100, *BEIJING)
+    og = oracle_mod.grid(100, *BEIJING)
+    x, y = oracle_mod.java_random_points(21, 400_000, *BEIJING)
+    qx, qy = oracle_mod.java_random_points(22, 25, 115.4, 117.7, 39.5, 41.2)
+    w = win(sf, x, y)
+    qs = [sf.Point(str(i), a, b, 0, g) for i, (a, b) in enumerate(zip(qx, qy))]
+    for r in (0.05, 0.11, 0.01):
+        for ap in (False, True):
+            res = sf.PointPointRangeQuery(conf(sf, ap), g).run(w, qs, r)
+            exp = oracle_mod.range_pp(og, x, y, qx, qy, r, ap)
+            np.testing.assert_array_equal(res.multiset_indices(), exp)
+
+
+def test_range_pp_edge_windows(sf, oracle_mod):
+    g = sf.UniformGrid(100, *BEIJING)
+    og = oracle_mod.grid(100, *BEIJING)
+    q = sf.Point("q", *QPOINT, 0, g)
+    op = sf.PointPointRangeQuery(conf(sf), g)
+    # empty window
+    res = op.run(win(sf, np.zeros(0), np.zeros(0)), [q], 0.5)
+    assert res.count() == 0 and len(res.indices()) == 0
+    # every point exactly at the query point / on the r boundary / NaN / inf
+    r = 0.5
+    x = np.array([QPOINT[0], QPOINT[0] + r, QPOINT[0], np.nan, np.inf, 115.5, 117.6, QPOINT[0] - r])
+    y = np.array([QPOINT[1], QPOINT[1], QPOINT[1] + r, 40.0, 40.0, 39.6, 41.1, QPOINT[1]])
+    for n in range(1, len(x) + 1):
+        res = op.run(win(sf, x[:n], y[:n]), [q], r)
+        np.testing.assert_array_equal(res.indices().astype(np.int64),
+                                      oracle_mod.range_pp(og, x[:n], y[:n], [QPOINT[0]], [QPOINT[1]], r))
+
+
+def test_range_query_cell_out_of_grid(sf, oracle_mod):
+    """g == 0 adds the (out-of-grid) query cell without validKey (UniformGrid.java:171-174)."""
+    g = sf.UniformGrid(100, *BEIJING)
+    og = oracle_mod.grid(100, *BEIJING)
+    qx, qy = 115.48, 40.0  # cell -1
+    x, y = oracle_mod.java_random_points(5, 100_000, 115.3, 115.7, 39.8, 40.2)
+    res = sf.PointPointRangeQuery(conf(sf), g).run(win(sf, x, y), [sf.Point("q", qx, qy, 0, g)], 0.05)
+    np.testing.assert_array_equal(res.indices().astype(np.int64), oracle_mod.range_pp(og, x, y, [qx], [qy], 0.05))
+
+
+# ------------------------------------------------------------------ range point-polygon
+def golden_polygons(sf, f, g):
+    polys = []
+    ro, vo, vx, vy = f["ring_off"], f["vert_off"], f["vx"], f["vy"]
+    for p in range(len(ro) - 1):
+        rings = [list(zip(vx[vo[j]:vo[j + 1]], vy[vo[j]:vo[j + 1]])) for j in range(ro[p], ro[p + 1])]
+        polys.append(sf.Polygon(rings, g))
+    return polys
+
+
+def test_range_ppoly_golden(sf):
+    f = load("range_ppoly.npz")
+    g = sf.UniformGrid(100, *BEIJING)
+    polys = golden_polygons(sf, f, g)
+    w = win(sf, f["x"], f["y"])
+    for r in (0.001, 0.05, 0.3):
+        for ap in (0, 1):
+            res = sf.PointPolygonRangeQuery(conf(sf, bool(ap)), g).run(w, polys, r)
+            np.testing.assert_array_equal(res.indices().astype(np.int64), f[f"r{r}_a{ap}"], err_msg=f"r={r} ap={ap}")
+
+
+@pytest.mark.parametrize("n,r", [(100, 0.001), (500, 0.001), (100, 0.05)])
+def test_range_ppoly_generated_1000(sf, oracle_mod, n, r):
+    """C3 shape (1000 generateQueryPolygons squares) at a test-sized window."""
+    g = sf.UniformGrid(n, *BEIJING)
+    og = oracle_mod.grid(n, *BEIJING)
+    raw = oracle_mod.generate_query_polygons(1000, 115.5, 39.6, 117.6, 41.1)
+    polys = [sf.Polygon(p, g) for p in raw]
+    x, y = oracle_mod.java_random_points(31, 150_000, 115.45, 115.75, *BEIJING[2:])
+    w = win(sf, x, y)
+    for ap in (False, True):
+        res = sf.PointPolygonRangeQuery(conf(sf, ap), g).run(w, polys, r)
+        exp = oracle_mod.range_ppoly(og, x, y, oracle_mod.Polygons(raw), r, ap)
+        np.testing.assert_array_equal(res.indices().astype(np.int64), exp)
+
+
+# ------------------------------------------------------------------ kNN
+def check_knn(res, oo, od, oi):
+    np.testing.assert_array_equal(res.objID, oo)
+    np.testing.assert_array_equal(res.idx, oi)
+    np.testing.assert_allclose(res.dist, od, rtol=1e-12, atol=0)
+    np.testing.assert_array_equal(res.dist, od)  # in fact bit-identical
+
+
+def test_knn_golden(sf):
+    f = load("knn.npz")
+    g = sf.UniformGrid(100, *BEIJING)
+    q = sf.Point("q", *QPOINT, 0, g)
+    for tag, ob in (("u", f["objID"]), ("d", f["objID_dup"])):
+        w = win(sf, f["x"], f["y"], ob)
+        for r in (0.5, 0.05, 0.3):
+            for k in (1, 50, 100):
+                res = sf.PointPointKNNQuery(conf(sf), g).run(w, q, r, k)
+                check_knn(res, f[f"{tag}_r{r}_k{k}_obj"], f[f"{tag}_r{r}_k{k}_d"], f[f"{tag}_r{r}_k{k}_idx"])
+
+
+@pytest.mark.parametrize("n,r,k", [(500, 0.5, 50), (500, 0.05, 50), (1000, 0.5, 100), (100, 0.3, 7)])
+def test_knn_large_sampled(sf, oracle_mod, n, r, k):
+    """Windows >= 1M points take the sample -> threshold -> scan -> select path."""
+    g = sf.UniformGrid(n, *BEIJING)
+    og = oracle_mod.grid(n, *BEIJING)
+    N = 2_000_001
+    x, y = oracle_mod.java_random_points(n + k, N, *BEIJING)
+    obj = np.random.default_rng(k).permutation(N).astype(np.int64)
+    q = sf.Point("q", *QPOINT, 0, g)
+    res = sf.PointPointKNNQuery(conf(sf), g).run(win(sf, x, y, obj), q, r, k)
+    st, oo, od, oi = oracle_mod.knn(og, x, y, obj, QPOINT[0], QPOINT[1], r, k)
+    check_knn(res, oo, od, oi)
+
+
+def test_knn_duplicate_objids_sampled(sf, oracle_mod):
+    g = sf.UniformGrid(500, *BEIJING)
+    og = oracle_mod.grid(500, *BEIJING)
+    N = 1_500_000
+    x, y = oracle_mod.java_random_points(77, N, *BEIJING)
+    obj = (np.arange(N) % 997).astype(np.int64)  # each objID ~1500 times (trajectories)
+    q = sf.Point("q", *QPOINT, 0, g)
+    for k in (50, 300):
+        res = sf.PointPointKNNQuery(conf(sf), g).run(win(sf, x, y, obj), q, 0.5, k)
+        st, oo, od, oi = oracle_mod.knn(og, x, y, obj, QPOINT[0], QPOINT[1], 0.5, k)
+        check_knn(res, oo, od, oi)
+
+
+def test_knn_forced_fallback(sf, oracle_mod):
+    """Candidate-buffer overflow -> exact partitioned fallback."""
+    g = sf.UniformGrid(100, *BEIJING)
+    og = oracle_mod.grid(100, *BEIJING)
+    x, y = oracle_mod.java_random_points(8, 300_000, *BEIJING)
+    obj = np.arange(len(x), dtype=np.int64)[::-1].copy()
+    q = sf.Point("q", *QPOINT, 0, g)
+    op = sf.PointPointKNNQuery(conf(sf), g)
+    w = win(sf, x, y, obj)
+    op.set_capacity(w.x.device.index, q, 0.5, 50, 4096)
+    res = op.run(w, q, 0.5, 50)
+    st, oo, od, oi = oracle_mod.knn(og, x, y, obj, QPOINT[0], QPOINT[1], 0.5, 50)
+    check_knn(res, oo, od, oi)
+
+
+def test_knn_ties_broken_by_objid(sf, oracle_mod):
+    """Points at identical distances: ranks follow objID (build contract, Appendix A7)."""
+    g = sf.UniformGrid(100, *BEIJING)
+    og = oracle_mod.grid(100, *BEIJING)
+    base_x, base_y = oracle_mod.java_random_points(4, 2000, 116.3, 116.5, 39.85, 40.0)
+    x = np.repeat(base_x, 8)
+    y = np.repeat(base_y, 8)
+    obj = np.random.default_rng(0).permutation(len(x)).astype(np.int64)
+    q = sf.Point("q", *QPOINT, 0, g)
+    res = sf.PointPointKNNQuery(conf(sf), g).run(win(sf, x, y, obj), q, 0.5, 100)
+    st, oo, od, oi = oracle_mod.knn(og, x, y, obj, QPOINT[0], QPOINT[1], 0.5, 100)
+    check_knn(res, oo, od, oi)
+
+
+def test_knn_hypot_metric(sf, oracle_mod):
+    g = sf.UniformGrid(500, *BEIJING)
+    og = oracle_mod.grid(500, *BEIJING)
+    x, y = oracle_mod.java_random_points(12, 1_200_000, *BEIJING)
+    obj = np.arange(len(x), dtype=np.int64)
+    q = sf.Point("q", *QPOINT, 0, g)
+    res = sf.PointPointKNNQuery(conf(sf, metric=1), g).run(win(sf, x, y, obj), q, 0.5, 50)
+    st, oo, od, oi = oracle_mod.knn(og, x, y, obj, QPOINT[0], QPOINT[1], 0.5, 50, metric=1)
+    check_knn(res, oo, od, oi)
+
+
+def test_knn_edge_windows(sf, oracle_mod):
+    g = sf.UniformGrid(100, *BEIJING)
+    og = oracle_mod.grid(100, *BEIJING)
+    q = sf.Point("q", *QPOINT, 0, g)
+    op = sf.PointPointKNNQuery(conf(sf), g)
+    assert len(op.run(win(sf, np.zeros(0), np.zeros(0), np.zeros(0, np.int64)), q, 0.5, 50)) == 0
+    x = np.array([QPOINT[0], np.nan, QPOINT[0] + 0.5, 117.0, QPOINT[0] + 0.1])
+    y = np.array([QPOINT[1], 40.0, QPOINT[1], 41.0, QPOINT[1]])
+    obj = np.array([5, 4, 3, 2, 1], np.int64)
+    for k in (1, 2, 3, 10):
+        res = op.run(win(sf, x, y, obj), q, 0.5, k)
+        st, oo, od, oi = oracle_mod.knn(og, x, y, obj, QPOINT[0], QPOINT[1], 0.5, k)
+        check_knn(res, oo, od, oi)
+
+
+def test_knn_merge_dev_equals_single_window(sf, oracle_mod):
+    """Per-shard records merged on the device == the whole window (the multi-GPU funnel)."""
+    import torch
+
+    g = sf.UniformGrid(500, *BEIJING)
+    og = oracle_mod.grid(500, *BEIJING)
+    x, y = oracle_mod.java_random_points(55, 400_000, *BEIJING)
+    obj = np.random.default_rng(1).permutation(len(x)).astype(np.int64)
+    q = sf.Point("q", *QPOINT, 0, g)
+    k = 64
+    op = sf.PointPointKNNQuery(conf(sf), g)
+    rb = sf.spatialOperators.knn_record_bytes(k)
+    shards = np.array_split(np.arange(len(x)), 4)
+    recs = torch.zeros(4 * rb, dtype=torch.uint8, device="cuda")
+    for s, ix in enumerate(shards):
+        w = win(sf, x[ix], y[ix], obj[ix])
+        op.enqueue(w, q, 0.5, k, recs[s * rb:(s + 1) * rb])
+    # shard-local indices -> global
+    torch.cuda.synchronize()
+    host = recs.cpu().numpy().tobytes()
+    fixed = bytearray(host)
+    for s, ix in enumerate(shards):
+        st, o, d, i = sf.spatialOperators.decode_knn_record(host[s * rb:(s + 1) * rb], k)
+        assert st == 0
+        i = i + ix[0]
+        off = s * rb + 32 + 16 * k
+        fixed[off:off + 8 * len(i)] = i.astype(np.int64).tobytes()
+    recs_dev = torch.frombuffer(bytearray(fixed), dtype=torch.uint8).cuda()
+    out = torch.zeros(rb, dtype=torch.uint8, device="cuda")
+    import ctypes as C
+    from spatialflink_amd import _lib
+
+    ctx = _lib.context(0)
+    _lib.check(_lib.lib().gf_knn_merge_dev(ctx.handle, k, recs_dev.data_ptr(), 4, out.data_ptr()), ctx.handle, "merge")
+    st, oo2, od2, oi2 = sf.spatialOperators.decode_knn_record(out.cpu().numpy().tobytes(), k)
+    st, oo, od, oi = oracle_mod.knn(og, x, y, obj, QPOINT[0], QPOINT[1], 0.5, k)
+    np.testing.assert_array_equal(oo2, oo)
+    np.testing.assert_array_equal(od2, od)
+    np.testing.assert_array_equal(oi2, oi)
+
+
+def test_knn_deterministic(sf):
+    g = sf.UniformGrid(500, *BEIJING)
+    x, y = sf.synthetic_uniform(42, 2_000_000, *BEIJING)
+    w = win(sf, x, y, np.arange(len(x), dtype=np.int64))
+    q = sf.Point("q", *QPOINT, 0, g)
+    op = sf.PointPointKNNQuery(conf(sf), g)
+    a = op.run(w, q, 0.5, 50)
+    for _ in range(3):
+        b = op.run(w, q, 0.5, 50)
+        np.testing.assert_array_equal(a.objID, b.objID)
+        np.testing.assert_array_equal(a.dist, b.dist)
+
+
+# ------------------------------------------------------------------ join
+def test_join_golden(sf):
+    f = load("join.npz")
+    g = sf.UniformGrid(100, *BEIJING)
+    wo, wq = win(sf, f["ox"], f["oy"]), win(sf, f["qx"], f["qy"])
+    for r in (0.001, 0.05, 0.0):
+        for ap in (0, 1):
+            if r == 0.0 and ap:
+                continue
+            got = sf.PointPointJoinQuery(conf(sf, bool(ap)), g, g).run(wo, wq, r)
+            np.testing.assert_array_equal(got, f[f"r{r}_a{ap}"], err_msg=f"r={r} ap={ap}")
+
+
+@pytest.mark.parametrize("n,r", [(1000, 0.001), (500, 0.01), (100, 0.03)])
+def test_join_large(sf, oracle_mod, n, r):
+    g = sf.UniformGrid(n, *BEIJING)
+    og = oracle_mod.grid(n, *BEIJING)
+    ox, oy = oracle_mod.java_random_points(61, 300_000, 115.4, 117.7, 39.5, 41.2)
+    qx, qy = oracle_mod.java_random_points(62, 30_000, 115.4, 117.7, 39.5, 41.2)
+    got = sf.PointPointJoinQuery(conf(sf), g, g).run(win(sf, ox, oy), win(sf, qx, qy), r)
+    st, pairs = oracle_mod.join_pp(og, og, ox, oy, qx, qy, r)
+    exp = np.array(sorted(map(tuple, pairs.tolist())), np.int64).reshape(-1, 2)
+    np.testing.assert_array_equal(got, exp)
+
+
+def test_join_negative_radius_raises(sf):
+    g = sf.UniformGrid(100, *BEIJING)
+    w = win(sf, [116.0], [40.0])
+    with pytest.raises(sf._lib.CandidateLayersError):
+        sf.PointPointJoinQuery(conf(sf), g, g).run(w, w, -0.5)
+
+
+def test_join_different_query_grid(sf, oracle_mod):
+    ug = sf.UniformGrid(100, *BEIJING)
+    qg = sf.UniformGrid(80, 115.4, 117.8, 39.5, 41.3)
+    oug, oqg = oracle_mod.grid(100, *BEIJING), oracle_mod.grid(80, 115.4, 117.8, 39.5, 41.3)
+    ox, oy = oracle_mod.java_random_points(71, 50_000, *BEIJING)
+    qx, qy = oracle_mod.java_random_points(72, 5_000, *BEIJING)
+    got = sf.PointPointJoinQuery(conf(sf), ug, qg).run(win(sf, ox, oy), win(sf, qx, qy), 0.02)
+    st, pairs = oracle_mod.join_pp(oug, oqg, ox, oy, qx, qy, 0.02)
+    exp = np.array(sorted(map(tuple, pairs.tolist())), np.int64).reshape(-1, 2)
+    np.testing.assert_array_equal(got, exp)

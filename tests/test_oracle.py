@@ -1,0 +1,178 @@
+"""CPU: the oracle (C restatement) against the committed golden fixtures and the
+independent Python restatement.  Parity with the reference is unpinned (no reference
+fixtures exist); these tests pin the oracle to its own cross-checked fixtures and to the
+reference facts that can be derived by reading the Java."""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import BEIJING, GOLDEN, QPOINT
+
+
+def load(name):
+    return np.load(os.path.join(GOLDEN, name))
+
+
+def test_grid_constants(oracle_mod):
+    O = oracle_mod
+    # UniformGrid(int, ...) does not square the bounds: (117.6-115.5)/n in binary64
+    assert O.grid(100, *BEIJING).cellLength == 0.020999999999999942
+    assert O.grid(500, *BEIJING).cellLength == 0.0041999999999999885
+    assert O.grid(1000, *BEIJING).cellLength == 0.0020999999999999942
+
+
+def test_java_random(oracle_mod):
+    x, y = oracle_mod.java_random_points(42, 2, 0.0, 1.0, 0.0, 1.0)
+    # new java.util.Random(42).nextDouble() sequence
+    assert x[0] == 0.7275636800328681 and y[0] == 0.6832234717598454
+
+
+def test_cell_id_format_parse(oracle_mod):
+    O = oracle_mod
+    assert O.cell_id(3, 45) == "0000300045"
+    assert O.cell_id(-1, 5) == "-000100005"   # String.format("%05d", -1)
+    assert O.parse_cell_id("-000100005") == (-1, 5)
+    assert O.parse_cell_id("0000000000") == (0, 0)
+    assert O.parse_cell_id("9999999999") == (99999, 99999)
+
+
+def test_jint(oracle_mod):
+    O = oracle_mod
+    assert O.jint(float("nan")) == 0
+    assert O.jint(1e300) == 2147483647 and O.jint(-1e300) == -2147483648
+    assert O.jint(-0.5) == 0 and O.jint(2.9) == 2
+
+
+def test_layers(oracle_mod):
+    g = oracle_mod.grid(100, *BEIJING)
+    assert oracle_mod.layers(g, 0.5) == (15, 24)
+    assert oracle_mod.layers(g, 0.05) == (0, 3)
+    assert oracle_mod.layers(g, 0.02) == (-1, 1)
+    assert oracle_mod.layers(g, 0.0) == (-1, 0)
+
+
+def test_gc_set_sizes(oracle_mod):
+    g = oracle_mod.grid(100, *BEIJING)
+    qcx, qcy = oracle_mod.assign_cells(g, [QPOINT[0]], [QPOINT[1]])
+    gs, cs = oracle_mod.gc_sets_point(g, 0.5, qcx[0], qcy[0])
+    assert len(gs) == 31 * 31 and not (gs & cs)
+    # g == 0: the query cell itself, no validKey (UniformGrid.java:171-174)
+    gs0, _ = oracle_mod.gc_sets_point(g, 0.05, -3, 7)
+    assert gs0 == {(-3, 7)}
+
+
+def test_generate_query_polygons(oracle_mod):
+    polys = oracle_mod.generate_query_polygons(1000, 115.5, 39.6, 117.6, 41.1)
+    assert len(polys) == 1000  # 10 columns x 100 squares of side 0.015
+    ring = polys[0][0]
+    assert ring[0] == ring[-1] and len(ring) == 5
+    assert abs((ring[1][0] - ring[0][0]) - 0.015) < 1e-15
+
+
+@pytest.mark.parametrize("n", [100, 500])
+def test_cells_golden(oracle_mod, n):
+    f = load(f"cells_n{n}.npz")
+    g = oracle_mod.grid(n, *BEIJING)
+    cx, cy = oracle_mod.assign_cells(g, f["x"], f["y"])
+    np.testing.assert_array_equal(cx, f["cx"])
+    np.testing.assert_array_equal(cy, f["cy"])
+
+
+def test_range_pp_golden(oracle_mod):
+    f = load("range_pp.npz")
+    g = oracle_mod.grid(100, *BEIJING)
+    for qn in ("q1", "q3"):
+        for r in (0.5, 0.05, 0.02, 0.0):
+            for ap in (0, 1):
+                got = oracle_mod.range_pp(g, f["x"], f["y"], f[f"{qn}_qx"], f[f"{qn}_qy"], r, bool(ap))
+                np.testing.assert_array_equal(got, f[f"{qn}_r{r}_a{ap}"])
+
+
+def test_range_ppoly_golden(oracle_mod):
+    f = load("range_ppoly.npz")
+    g = oracle_mod.grid(100, *BEIJING)
+    P = oracle_mod.Polygons([])
+    P.ring_off, P.vert_off, P.vx, P.vy = f["ring_off"], f["vert_off"], f["vx"], f["vy"]
+    P.c = oracle_mod.OrcPolygons(len(P.ring_off) - 1, P.ring_off.ctypes.data, P.vert_off.ctypes.data,
+                                 P.vx.ctypes.data, P.vy.ctypes.data)
+    for r in (0.001, 0.05, 0.3):
+        for ap in (0, 1):
+            got = oracle_mod.range_ppoly(g, f["x"], f["y"], P, r, bool(ap))
+            np.testing.assert_array_equal(got, f[f"r{r}_a{ap}"])
+
+
+def test_knn_golden(oracle_mod):
+    f = load("knn.npz")
+    g = oracle_mod.grid(100, *BEIJING)
+    for r in (0.5, 0.05, 0.3):
+        for k in (1, 50, 100):
+            for tag, ob in (("u", f["objID"]), ("d", f["objID_dup"])):
+                st, oo, od, oi = oracle_mod.knn(g, f["x"], f["y"], ob, QPOINT[0], QPOINT[1], r, k)
+                assert st == 0
+                np.testing.assert_array_equal(oo, f[f"{tag}_r{r}_k{k}_obj"])
+                np.testing.assert_array_equal(od, f[f"{tag}_r{r}_k{k}_d"])
+                np.testing.assert_array_equal(oi, f[f"{tag}_r{r}_k{k}_idx"])
+
+
+def test_knn_reference_shaped_agrees_on_unique_ids(oracle_mod):
+    """With unique objIDs and distinct distances the Java-shaped evaluator (per-cell
+    PriorityQueues + windowAll merge, bug included) returns the contract's set."""
+    f = load("knn.npz")
+    g = oracle_mod.grid(100, *BEIJING)
+    for r in (0.5, 0.05):
+        st, oo, od, oi = oracle_mod.knn(g, f["x"], f["y"], f["objID"], QPOINT[0], QPOINT[1], r, 50,
+                                        reference_shaped=True)
+        assert st == 0
+        ref = sorted(zip(od.tolist(), oo.tolist()))
+        assert ref == list(zip(f[f"u_r{r}_k50_d"].tolist(), f[f"u_r{r}_k50_obj"].tolist()))
+
+
+def test_knn_reference_k1_npe(oracle_mod):
+    """k == 1 throws a NullPointerException in KNNQuery.java:249-251 on the first eviction."""
+    f = load("knn.npz")
+    g = oracle_mod.grid(100, *BEIJING)
+    st, *_ = oracle_mod.knn(g, f["x"], f["y"], f["objID"], QPOINT[0], QPOINT[1], 0.5, 1, reference_shaped=True)
+    assert st == oracle_mod.ERR_NPE
+
+
+def test_join_golden(oracle_mod):
+    f = load("join.npz")
+    g = oracle_mod.grid(100, *BEIJING)
+    for r in (0.001, 0.05, 0.0):
+        for ap in (0, 1):
+            if r == 0.0 and ap:
+                continue
+            st, pairs = oracle_mod.join_pp(g, g, f["ox"], f["oy"], f["qx"], f["qy"], r, bool(ap))
+            assert st == 0
+            got = np.array(sorted(map(tuple, pairs.tolist())), np.int64).reshape(-1, 2)
+            np.testing.assert_array_equal(got, f[f"r{r}_a{ap}"])
+
+
+def test_join_negative_radius_exits(oracle_mod):
+    g = oracle_mod.grid(100, *BEIJING)
+    st, _ = oracle_mod.join_pp(g, g, [116.0], [40.0], [116.0], [40.0], -0.1)
+    assert st == oracle_mod.ERR_LAYERS
+
+
+def test_oracle_vs_pyref_random(oracle_mod):
+    import pyref as P
+
+    g = oracle_mod.grid(37, *BEIJING)
+    pg = P.Grid(37, *BEIJING)
+    x, y = oracle_mod.java_random_points(5, 1500, *BEIJING)
+    for r in (0.2, 0.07):
+        a = oracle_mod.range_pp(g, x, y, [QPOINT[0]], [QPOINT[1]], r)
+        assert a.tolist() == P.range_pp(pg, x.tolist(), y.tolist(), [QPOINT], r)
+
+
+def test_hypot_basics(oracle_mod):
+    O = oracle_mod
+    assert O.hypot(3.0, 4.0) == 5.0
+    assert O.hypot(0.0, 0.0) == 0.0
+    assert O.hypot(float("inf"), float("nan")) == float("inf")
+    assert abs(O.hypot(1e308, 1e308) / np.hypot(1e308, 1e308) - 1) < 1e-15
+    assert O.hypot(1e-310, 3e-310) == np.hypot(1e-310, 3e-310) or abs(O.hypot(1e-310, 3e-310) - np.hypot(1e-310, 3e-310)) <= 5e-324
+    x = np.random.default_rng(1).uniform(-1, 1, (2000, 2))
+    for a, b in x:
+        assert abs(O.hypot(a, b) - np.hypot(a, b)) <= 2 * np.spacing(np.hypot(a, b))
