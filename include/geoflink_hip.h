@@ -92,7 +92,8 @@ int         gf_device_count(int* n);
 /* One context per calling thread / Flink subtask; binds `device`, owns scratch + a stream. */
 int         gf_ctx_create(int device, gf_ctx** out);
 void        gf_ctx_destroy(gf_ctx* ctx);
-/* Borrow a caller stream (hipStream_t) -- e.g. torch's current stream; NULL = own stream. */
+/* Borrow a caller stream (hipStream_t), e.g. torch's current stream; NULL = the HIP null
+ * stream.  A new context starts on its own non-blocking stream (returned by gf_ctx_stream). */
 int         gf_ctx_set_stream(gf_ctx* ctx, void* hip_stream);
 void*       gf_ctx_stream(gf_ctx* ctx);
 int         gf_ctx_synchronize(gf_ctx* ctx);
@@ -153,6 +154,9 @@ int    gf_knn_pp_plan_create(gf_ctx* ctx, const gf_grid* g, double qx, double qy
 void   gf_knn_plan_destroy(gf_knn_plan* plan);
 /* Candidate-buffer capacity (entries); default 1<<20.  Small values force the exact fallback. */
 int    gf_knn_plan_set_capacity(gf_knn_plan* plan, int64_t cap);
+/* Scan-kernel tuning: grid blocks (0 = auto), point pairs per lane per iteration (1..8),
+ * nontemporal loads (0/1).  Results never depend on it. */
+int    gf_knn_plan_set_tuning(gf_knn_plan* plan, int32_t scan_blocks, int32_t unroll, int32_t nontemporal);
 /* Offset added to the window-local point index in results (a shard's first global index). */
 int    gf_knn_plan_set_index_base(gf_knn_plan* plan, int64_t base);
 /* Result record: gf_knn_header followed by double dist[k], int64 objID[k], int64 idx[k]. */

@@ -246,7 +246,7 @@ extern "C" void gf_ctx_destroy(gf_ctx* ctx) {
 
 extern "C" int gf_ctx_set_stream(gf_ctx* ctx, void* s) {
   if (!ctx) return GF_ERR_ARG;
-  ctx->stream = s ? (hipStream_t)s : ctx->own_stream;
+  ctx->stream = (hipStream_t)s;  // NULL is the HIP null stream (what torch's default stream is)
   return GF_OK;
 }
 extern "C" void* gf_ctx_stream(gf_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
@@ -739,6 +739,14 @@ extern "C" int gf_knn_plan_set_capacity(gf_knn_plan* P, int64_t cap) {
   return knn_alloc_candidates(P, cap & ~(int64_t)1);
 }
 
+extern "C" int gf_knn_plan_set_tuning(gf_knn_plan* P, int32_t scan_blocks, int32_t unroll, int32_t nontemporal) {
+  if (!P || scan_blocks < 0 || unroll < 1 || unroll > 8) return GF_ERR_ARG;
+  P->scan_blocks = scan_blocks;
+  P->scan_unroll = unroll;
+  P->scan_nt = nontemporal != 0;
+  return GF_OK;
+}
+
 extern "C" int gf_knn_plan_set_index_base(gf_knn_plan* P, int64_t base) {
   if (!P || base < 0) return GF_ERR_ARG;
   P->idx_base = base;
@@ -755,7 +763,7 @@ static int knn_scan_select(gf_knn_plan* P, const gf_points* pts, int64_t begin, 
   s.use_state = use_state; s.metric = P->metric; s.st = P->st;
   s.cand_d = P->cand_d; s.cand_i = P->cand_i; s.cap = (unsigned long long)P->cap;
   const int blocks = P->scan_blocks > 0 ? P->scan_blocks : stream_blocks(ctx, ((end - begin) + 1) / 2);
-  GF_HIP_CHECK(ctx, launch_knn_scan(ctx, s, blocks));
+  GF_HIP_CHECK(ctx, launch_knn_scan(ctx, s, blocks, P->scan_unroll, P->scan_nt));
   KnnSelectArgs q{};
   q.st = P->st; q.cand_d = P->cand_d; q.cand_i = P->cand_i; q.cap = (unsigned long long)P->cap;
   q.objID = pts->objID; q.use_state = use_state; q.T = P->r; q.r = P->r; q.k = P->k; q.result = result;

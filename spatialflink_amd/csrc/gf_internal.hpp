@@ -61,7 +61,7 @@ struct KTimer {
 constexpr int kBlock = 256;         // streaming kernels: 4 waves
 constexpr int kSortCap = 4096;      // select kernel: LDS sort capacity
 constexpr int kMaxK = 1024;         // largest k on the device path
-constexpr int kSampleBlocks = 64;   // kNN sample: 64 blocks x 2048 points
+constexpr int kSampleBlocks = 128;  // kNN sample: 128 blocks x 2048 points = 256K points
 constexpr int kSamplePerBlock = 2048;
 constexpr int64_t kSampleMinN = 1 << 20;
 
@@ -173,7 +173,7 @@ hipError_t launch_expand_bitmap(hipStream_t s, const uint64_t* bitmap, int64_t w
                                 const uint32_t* off, uint32_t* idx, int64_t cap);
 
 hipError_t launch_knn_sample(gf_ctx* ctx, const KnnSampleArgs& a);
-hipError_t launch_knn_scan(gf_ctx* ctx, const KnnScanArgs& a, int blocks);
+hipError_t launch_knn_scan(gf_ctx* ctx, const KnnScanArgs& a, int blocks, int unroll, int nt);
 hipError_t launch_knn_select(gf_ctx* ctx, const KnnSelectArgs& a);
 hipError_t launch_knn_merge(gf_ctx* ctx, int32_t k, const void* records, int32_t nrec, void* result);
 
@@ -251,7 +251,9 @@ struct gf_knn_plan {
   int64_t idx_base = 0;
   void* tmp_result = nullptr;   // device record used by gf_knn_run / fallback
   void* host_result = nullptr;  // pinned
-  int scan_blocks = 0;
+  int scan_blocks = 0;   // tuning: 0 = auto
+  int scan_unroll = 4;   // point pairs per lane per iteration
+  int scan_nt = 1;       // nontemporal loads
 };
 
 struct gf_window {

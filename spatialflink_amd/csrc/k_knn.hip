@@ -61,26 +61,40 @@ __host__ __device__ inline RecView rec_view(void* base, int k) {
 }
 
 // ---------------------------------------------------------------------------------------
-// sample
+// sample: kSampleBlocks blocks x kSamplePerBlock points, spread evenly over the window.
+// Each thread issues all its loads up front (8 points = 4 x 16-B loads of x and y), bins its
+// candidates into an LDS histogram, and the block flushes only non-zero bins to the global
+// histogram (no same-address global atomic storms).  The last block (ticket) scans it.
 // ---------------------------------------------------------------------------------------
 template <int METRIC>
 __global__ __launch_bounds__(kBlock) void knn_sample_kernel(KnnSampleArgs a) {
+  __shared__ uint32_t lh[kDistBins];
+  __shared__ uint32_t wsum[kBlock / 64];
+  __shared__ int s_last, s_bin;
+  constexpr int kPairs = kSamplePerBlock / 2 / kBlock;  // pairs per thread
+  for (int j = threadIdx.x; j < kDistBins; j += kBlock) lh[j] = 0u;
   const int64_t npairs = a.n >> 1;
   const int64_t stride = npairs / gridDim.x;  // >= kSamplePerBlock/2 since n >= kSampleMinN
   const int64_t p0 = (int64_t)blockIdx.x * stride;
   const int64_t bbase = dist_bin_base(a.r);
-  for (int j = threadIdx.x; j < kSamplePerBlock / 2; j += kBlock) {
-    const int64_t i = 2 * (p0 + j);
-    const double2 xv = *reinterpret_cast<const double2*>(a.x + i);
-    const double2 yv = *reinterpret_cast<const double2*>(a.y + i);
-    double d;
-    if (knn_candidate<METRIC>(a.qx, a.qy, a.qr, xv.x, yv.x, a.s_r, a.r, d))
-      atomicAdd(&a.st->hist[dist_bin(d, bbase)], 1u);
-    if (knn_candidate<METRIC>(a.qx, a.qy, a.qr, xv.y, yv.y, a.s_r, a.r, d))
-      atomicAdd(&a.st->hist[dist_bin(d, bbase)], 1u);
+  double2 xv[kPairs], yv[kPairs];
+#pragma unroll
+  for (int u = 0; u < kPairs; ++u) {
+    const int64_t i = 2 * (p0 + u * kBlock + threadIdx.x);
+    xv[u] = *reinterpret_cast<const double2*>(a.x + i);
+    yv[u] = *reinterpret_cast<const double2*>(a.y + i);
   }
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < kPairs; ++u) {
+    double d;
+    if (knn_candidate<METRIC>(a.qx, a.qy, a.qr, xv[u].x, yv[u].x, a.s_r, a.r, d)) atomicAdd(&lh[dist_bin(d, bbase)], 1u);
+    if (knn_candidate<METRIC>(a.qx, a.qy, a.qr, xv[u].y, yv[u].y, a.s_r, a.r, d)) atomicAdd(&lh[dist_bin(d, bbase)], 1u);
+  }
+  __syncthreads();
+  for (int j = threadIdx.x; j < kDistBins; j += kBlock)
+    if (lh[j]) atomicAdd(&a.st->hist[j], lh[j]);
   // last-arriving block picks the threshold (split-K style ticket, agent-scope fences)
-  __shared__ int s_last;
   __syncthreads();
   if (threadIdx.x == 0) {
     __threadfence();
@@ -91,8 +105,6 @@ __global__ __launch_bounds__(kBlock) void knn_sample_kernel(KnnSampleArgs a) {
   if (!s_last) return;
   __threadfence();
   constexpr int kPer = kDistBins / kBlock;  // 16 bins per thread
-  __shared__ uint32_t wsum[kBlock / 64];
-  __shared__ int s_bin;
   uint32_t v[kPer];
   uint32_t s = 0;
 #pragma unroll
@@ -100,7 +112,6 @@ __global__ __launch_bounds__(kBlock) void knn_sample_kernel(KnnSampleArgs a) {
     v[j] = __hip_atomic_load(&a.st->hist[threadIdx.x * kPer + j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     s += v[j];
   }
-  // block exclusive scan (4 waves)
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   uint32_t inc = s;
 #pragma unroll
@@ -146,14 +157,24 @@ hipError_t launch_knn_sample(gf_ctx* ctx, const KnnSampleArgs& a) {
 }
 
 // ---------------------------------------------------------------------------------------
-// scan: grid-stride over point pairs, two pairs in flight per lane (64 B of loads)
+// scan: grid-stride over point pairs; U pairs per lane per iteration, all loads issued before
+// any use (U x 32 B in flight per lane); NT = nontemporal (streamed-once) loads.
 // ---------------------------------------------------------------------------------------
+typedef double dbl2 __attribute__((ext_vector_type(2)));
+
+template <int NT>
 __device__ __forceinline__ void load_pair(const double* __restrict__ x, const double* __restrict__ y, int64_t p,
                                           int64_t end, double2& xv, double2& yv) {
   const int64_t i = 2 * p;
   if (i + 1 < end) {
-    xv = *reinterpret_cast<const double2*>(x + i);
-    yv = *reinterpret_cast<const double2*>(y + i);
+    if (NT) {
+      const dbl2 a = __builtin_nontemporal_load(reinterpret_cast<const dbl2*>(x + i));
+      const dbl2 b = __builtin_nontemporal_load(reinterpret_cast<const dbl2*>(y + i));
+      xv.x = a.x; xv.y = a.y; yv.x = b.x; yv.y = b.y;
+    } else {
+      xv = *reinterpret_cast<const double2*>(x + i);
+      yv = *reinterpret_cast<const double2*>(y + i);
+    }
   } else if (i < end) {
     xv.x = x[i]; yv.x = y[i];
     xv.y = NAN; yv.y = NAN;  // NaN never passes the distance prefilter
@@ -180,7 +201,24 @@ __device__ __forceinline__ void wave_append(bool c, double d, uint32_t idx, KnnS
   }
 }
 
+// Hot-loop test: prefilter + exact cell class + (hypot) exact distance; no distance is kept
+// live across the loop -- the rare append branch recomputes it from the loaded x, y.
 template <int METRIC>
+__device__ __forceinline__ bool knn_pass(double qx, double qy, const QueryRect& qr, double px, double py,
+                                         double sp, double T) {
+  const double dx = qx - px, dy = qy - py;
+  const double s = dx * dx + dy * dy;
+  if (!(s <= sp)) return false;
+  if (!classify_cg(qr, px, py)) return false;
+  return METRIC == 0 ? true : fdlibm_hypot(dx, dy) <= T;
+}
+template <int METRIC>
+__device__ __forceinline__ double knn_dist(double qx, double qy, double px, double py) {
+  const double dx = qx - px, dy = qy - py;
+  return METRIC == 0 ? sqrt(dx * dx + dy * dy) : fdlibm_hypot(dx, dy);
+}
+
+template <int METRIC, int U, int NT>
 __global__ __launch_bounds__(kBlock) void knn_scan_kernel(KnnScanArgs a) {
   const double sp = a.use_state ? a.st->s_pre : a.s_pre;
   const double T = a.use_state ? a.st->T : a.T;
@@ -188,31 +226,46 @@ __global__ __launch_bounds__(kBlock) void knn_scan_kernel(KnnScanArgs a) {
   const int lane = threadIdx.x & 63;
   const int64_t wstride = (int64_t)gridDim.x * kBlock;
   int64_t base = (a.begin >> 1) + (int64_t)blockIdx.x * kBlock + (threadIdx.x & ~63);
-  for (; base < pend; base += 2 * wstride) {
-    const int64_t p0 = base + lane, p1 = base + wstride + lane;
-    double2 xa, ya, xb, yb;
-    load_pair(a.x, a.y, p0, a.end, xa, ya);
-    load_pair(a.x, a.y, p1, a.end, xb, yb);
-    double d0 = 0, d1 = 0, d2 = 0, d3 = 0;
-    const bool c0 = knn_candidate<METRIC>(a.qx, a.qy, a.qr, xa.x, ya.x, sp, T, d0);
-    const bool c1 = knn_candidate<METRIC>(a.qx, a.qy, a.qr, xa.y, ya.y, sp, T, d1);
-    const bool c2 = knn_candidate<METRIC>(a.qx, a.qy, a.qr, xb.x, yb.x, sp, T, d2);
-    const bool c3 = knn_candidate<METRIC>(a.qx, a.qy, a.qr, xb.y, yb.y, sp, T, d3);
-    if (__ballot(c0 | c1 | c2 | c3)) {  // wave-uniform, rare once T is tight
-      wave_append(c0, d0, (uint32_t)(2 * p0), a.st, a.cand_d, a.cand_i, a.cap);
-      wave_append(c1, d1, (uint32_t)(2 * p0 + 1), a.st, a.cand_d, a.cand_i, a.cap);
-      wave_append(c2, d2, (uint32_t)(2 * p1), a.st, a.cand_d, a.cand_i, a.cap);
-      wave_append(c3, d3, (uint32_t)(2 * p1 + 1), a.st, a.cand_d, a.cand_i, a.cap);
+  for (; base < pend; base += U * wstride) {
+    double2 xv[U], yv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) load_pair<NT>(a.x, a.y, base + u * wstride + lane, a.end, xv[u], yv[u]);
+    uint32_t cm = 0;  // candidate bits, 2 per pair
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      cm |= (uint32_t)knn_pass<METRIC>(a.qx, a.qy, a.qr, xv[u].x, yv[u].x, sp, T) << (2 * u);
+      cm |= (uint32_t)knn_pass<METRIC>(a.qx, a.qy, a.qr, xv[u].y, yv[u].y, sp, T) << (2 * u + 1);
+    }
+    if (__ballot(cm != 0)) {  // wave-uniform, rare once T is tight
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint32_t i0 = (uint32_t)(2 * (base + u * wstride + lane));
+        const bool c0 = (cm >> (2 * u)) & 1u, c1 = (cm >> (2 * u + 1)) & 1u;
+        wave_append(c0, c0 ? knn_dist<METRIC>(a.qx, a.qy, xv[u].x, yv[u].x) : 0.0, i0, a.st, a.cand_d, a.cand_i,
+                    a.cap);
+        wave_append(c1, c1 ? knn_dist<METRIC>(a.qx, a.qy, xv[u].y, yv[u].y) : 0.0, i0 + 1, a.st, a.cand_d,
+                    a.cand_i, a.cap);
+      }
     }
   }
 }
 
-hipError_t launch_knn_scan(gf_ctx* ctx, const KnnScanArgs& a, int blocks) {
+template <int METRIC>
+static void launch_scan_u(gf_ctx* ctx, const KnnScanArgs& a, int blocks, int unroll, int nt) {
+  const dim3 g(blocks), b(kBlock);
+#define GF_SCAN(U, N) hipLaunchKernelGGL((knn_scan_kernel<METRIC, U, N>), g, b, 0, ctx->stream, a)
+  if (nt) {
+    if (unroll <= 1) GF_SCAN(1, 1); else if (unroll == 2) GF_SCAN(2, 1); else if (unroll <= 4) GF_SCAN(4, 1); else GF_SCAN(8, 1);
+  } else {
+    if (unroll <= 1) GF_SCAN(1, 0); else if (unroll == 2) GF_SCAN(2, 0); else if (unroll <= 4) GF_SCAN(4, 0); else GF_SCAN(8, 0);
+  }
+#undef GF_SCAN
+}
+
+hipError_t launch_knn_scan(gf_ctx* ctx, const KnnScanArgs& a, int blocks, int unroll, int nt) {
   KTimer t(ctx, GF_K_KNN_SCAN);
-  if (a.metric == 0)
-    hipLaunchKernelGGL(knn_scan_kernel<0>, dim3(blocks), dim3(kBlock), 0, ctx->stream, a);
-  else
-    hipLaunchKernelGGL(knn_scan_kernel<1>, dim3(blocks), dim3(kBlock), 0, ctx->stream, a);
+  if (a.metric == 0) launch_scan_u<0>(ctx, a, blocks, unroll, nt);
+  else launch_scan_u<1>(ctx, a, blocks, unroll, nt);
   return hipGetLastError();
 }
 
@@ -308,11 +361,30 @@ __global__ __launch_bounds__(kSelThreads) void knn_select_kernel(KnnSelectArgs a
   int nres = 0;
 
   if (!overflow) {
-    // A: histogram of candidate distances over [0, T]
+    // A: stage up to kSortCap candidates in registers (all loads issued at once), then an LDS
+    //    histogram of their distances over [0, T]
+    const bool staged = M <= kSortCap;
+    constexpr int kPer = kSortCap / kSelThreads;  // 4
+    double dv[kPer];
+    uint32_t iv[kPer];
+    if (staged) {
+#pragma unroll
+      for (int j = 0; j < kPer; ++j) {
+        const int64_t i = tid + (int64_t)j * kSelThreads;
+        dv[j] = i < M ? a.cand_d[i] : 0.0;
+        iv[j] = i < M ? a.cand_i[i] : 0u;
+      }
+    }
     for (int i = tid; i < kDistBins; i += kSelThreads) hist[i] = 0u;
     __syncthreads();
     const int64_t bbase = dist_bin_base(T);
-    for (int64_t i = tid; i < M; i += kSelThreads) atomicAdd(&hist[dist_bin(a.cand_d[i], bbase)], 1u);
+    if (staged) {
+#pragma unroll
+      for (int j = 0; j < kPer; ++j)
+        if (tid + (int64_t)j * kSelThreads < M) atomicAdd(&hist[dist_bin(dv[j], bbase)], 1u);
+    } else {
+      for (int64_t i = tid; i < M; i += kSelThreads) atomicAdd(&hist[dist_bin(a.cand_d[i], bbase)], 1u);
+    }
     __syncthreads();
     // B: bin holding the k-th candidate (4 bins per thread, block scan)
     uint32_t v[4], s = 0;
@@ -341,16 +413,26 @@ __global__ __launch_bounds__(kSelThreads) void knn_select_kernel(KnnSelectArgs a
     __syncthreads();
     const int bstar = s_bin;
     bool done = false;
-    // C: fast path -- survivors (bins <= bstar) fit the LDS sort
+    // C: fast path -- survivors (bins <= bstar) fit the LDS sort; objIDs gathered only for them
     if (s_S <= (uint32_t)kSortCap) {
       if (tid == 0) s_cnt = 0;
       __syncthreads();
-      for (int64_t i = tid; i < M; i += kSelThreads) {
-        const double d = a.cand_d[i];
-        if (dist_bin(d, bbase) <= bstar) {
-          const int pos = atomicAdd(&s_cnt, 1);
-          const uint32_t ci = a.cand_i[i];
-          sd[pos] = dbits(d); si[pos] = ci; so[pos] = okey(a.objID[ci]);
+      if (staged) {
+#pragma unroll
+        for (int j = 0; j < kPer; ++j) {
+          if (tid + (int64_t)j * kSelThreads < M && dist_bin(dv[j], bbase) <= bstar) {
+            const int pos = atomicAdd(&s_cnt, 1);
+            sd[pos] = dbits(dv[j]); si[pos] = iv[j]; so[pos] = okey(a.objID[iv[j]]);
+          }
+        }
+      } else {
+        for (int64_t i = tid; i < M; i += kSelThreads) {
+          const double d = a.cand_d[i];
+          if (dist_bin(d, bbase) <= bstar) {
+            const int pos = atomicAdd(&s_cnt, 1);
+            const uint32_t ci = a.cand_i[i];
+            sd[pos] = dbits(d); si[pos] = ci; so[pos] = okey(a.objID[ci]);
+          }
         }
       }
       __syncthreads();

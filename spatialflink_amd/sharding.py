@@ -88,3 +88,15 @@ def allgather_knn_records(record, k: int, merged_out, group=None):
     _lib.check(_lib.lib().gf_knn_merge_dev(ctx.handle, int(k), gathered.data_ptr(), world, merged_out.data_ptr()),
                ctx.handle, "gf_knn_merge_dev")
     return merged_out
+
+
+def join_query_halo(qcx: np.ndarray, band, c: int) -> np.ndarray:
+    """Query points a rank needs for its ordinary band [lo, hi): those whose cell column is
+    within c = ceil(r / cellLength) of the band (the replicated-key neighbourhood,
+    JoinQuery.java:73-90).  c < 0 (r == 0: every cell is a neighbour) -> all of them.
+    Each pair (p, q) is then produced exactly once, by p's owner."""
+    lo, hi = band
+    if c < 0:
+        return np.ones(len(qcx), dtype=bool)
+    qcx = np.asarray(qcx, np.int64)
+    return (qcx >= lo - c) & (qcx <= hi - 1 + c)
