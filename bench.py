@@ -5,7 +5,8 @@ Workload (BASELINE.json configs[1]): continuous kNN, k = 50, radius 0.5 around t
 query point (116.414899, 39.920374), 500 x 500 UniformGrid over Beijing bounds, 10M points
 per window per GPU, synthetic java.util.Random-compatible uniform points.  A step = one
 window evaluated end to end on the device (sample -> scan -> select, plus the RCCL top-k
-all-gather + merge when N > 1), result record copied asynchronously to pinned host memory.
+all-gather + merge when N > 1); the final kernel writes the result record straight into mapped
+pinned host memory (PinnedRecords), so no copy kernel runs per window.
 Windows are device-resident when the timed region starts.
 
 N > 1 (one process per GPU, torchrun): the window is sharded by grid-cell column bands, each
@@ -19,6 +20,7 @@ reference-shaped evaluator, single core, bounded sample).
 from __future__ import annotations
 
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -52,6 +54,7 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=1_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--windows", type=int, default=4, help="distinct resident windows cycled through")
     args = ap.parse_args()
 
     import torch
@@ -69,7 +72,7 @@ def main():
 
     import spatialflink_amd as sf
     from spatialflink_amd import _lib, sharding
-    from spatialflink_amd.spatialOperators import decode_knn_record, knn_record_bytes
+    from spatialflink_amd.spatialOperators import knn_record_bytes
 
     # ---------------- data: this rank's shard of the window ----------------
     grid = sf.UniformGrid(args.grid, *BEIJING)
@@ -79,12 +82,19 @@ def main():
     else:
         lo, hi = sharding.column_bands(args.grid, world)[rank]
         xlo, xhi = sharding.band_x_range(grid, lo, hi)
+    # a ring of distinct windows: consecutive steps never evaluate the same data (the kNN
+    # threshold hint carried from window to window is validated on fresh points every step)
     t = time.perf_counter()
-    x, y = sf.synthetic_uniform(42 + rank, n, xlo, xhi, BEIJING[2], BEIJING[3])
-    obj = np.arange(rank * n, (rank + 1) * n, dtype=np.int64)
-    w = sf.PointWindow.from_numpy(x, y, obj, device=dev.index)
+    wins, host_windows = [], []
+    for j in range(args.windows):
+        x, y = sf.synthetic_uniform(42 + 1000 * rank + j, n, xlo, xhi, BEIJING[2], BEIJING[3])
+        obj = np.arange(rank * n, (rank + 1) * n, dtype=np.int64)
+        wins.append(sf.PointWindow.from_numpy(x, y, obj, device=dev.index))
+        host_windows.append((x, y, obj))
     torch.cuda.synchronize()
-    log(f"[rank {rank}] window shard: {n} points x in [{xlo}, {xhi}) generated+uploaded in {time.perf_counter()-t:.2f}s")
+    log(f"[rank {rank}] {args.windows} window shards x {n} points, x in [{xlo}, {xhi}): "
+        f"generated+uploaded in {time.perf_counter()-t:.2f}s")
+    w = wins[0]
 
     conf = sf.QueryConfiguration(sf.QueryType.WindowBased)
     q = sf.Point("q", QPOINT[0], QPOINT[1], 0, grid)
@@ -93,17 +103,22 @@ def main():
     _lib.check(_lib.lib().gf_knn_plan_set_index_base(plan, rank * n), ctx.handle, "index base")
     rb = knn_record_bytes(args.k)
     slots = torch.zeros(4, rb, dtype=torch.uint8, device=dev)
-    merged = torch.zeros(4, rb, dtype=torch.uint8, device=dev)
     total_steps = args.warmup + args.steps
-    host = torch.empty(total_steps, rb, dtype=torch.uint8, pin_memory=True)
+    host = sf.PinnedRecords(total_steps, args.k)
+    L = _lib.lib()
+    pts = [w_.c_struct() for w_ in wins]
+    pts_ref = [ctypes.byref(p_) for p_ in pts]
+    enqueue = L.gf_knn_enqueue
 
     def step(i):
-        s = i % 4
-        op.enqueue(w, q, args.radius, args.k, slots[s])
-        out = slots[s]
-        if world > 1:
-            out = sharding.allgather_knn_records(slots[s], args.k, merged[s])
-        host[i].copy_(out, non_blocking=True)
+        if world == 1:  # the select kernel writes the final record into pinned host memory
+            st = enqueue(plan, pts_ref[i % args.windows], host.ptr(i))
+            if st:
+                _lib.check(st, ctx.handle, "gf_knn_enqueue")
+        else:  # device record -> RCCL all-gather -> device merge writes the pinned host record
+            s = i % 4
+            _lib.check(enqueue(plan, pts_ref[i % args.windows], slots[s].data_ptr()), ctx.handle, "gf_knn_enqueue")
+            sharding.allgather_knn_records(slots[s], args.k, host.ptr(i))
 
     for i in range(args.warmup):
         step(i)
@@ -131,29 +146,39 @@ def main():
         elapsed = float(tt.item())
 
     # ---------------- validate every timed window's record ----------------
-    raw = host.numpy()
-    first = None
+    per_window = {}
     fallbacks = 0
     for i in range(args.warmup, total_steps):
-        st, o, d, ix = decode_knn_record(raw[i].tobytes(), args.k)
+        st, o, d, ix = host.decode(i)
         if st != 0:
             fallbacks += 1
             continue
-        if first is None:
-            first = (o, d, ix)
+        j = i % args.windows
+        if j in per_window:
+            assert np.array_equal(per_window[j][0], o) and np.array_equal(per_window[j][1], d), "non-deterministic"
         else:
-            assert np.array_equal(first[0], o) and np.array_equal(first[1], d), "non-deterministic window result"
+            per_window[j] = (o, d, ix)
     assert fallbacks == 0, f"{fallbacks} windows needed the exact fallback inside the timed region"
 
-    # per-kernel breakdown (separate, untimed pass)
-    ctx.set_timing((1 << _lib.K_KNN_SCAN) | (1 << _lib.K_KNN_SAMPLE) | (1 << _lib.K_KNN_SELECT))
-    for i in range(10):
-        op.enqueue(w, q, args.radius, args.k, slots[i % 4])
+    # per-kernel breakdown (separate, untimed pass), steady state and cold (no hint: sample each window)
+    kid_all = (1 << _lib.K_KNN_SCAN) | (1 << _lib.K_KNN_SAMPLE) | (1 << _lib.K_KNN_SELECT)
     breakdown = {}
-    for name, kid in (("sample", _lib.K_KNN_SAMPLE), ("scan", _lib.K_KNN_SCAN), ("select", _lib.K_KNN_SELECT)):
-        ms, cnt = ctx.timing(kid)
-        breakdown[name + "_us"] = round(1000.0 * ms / max(cnt, 1), 2)
-    ctx.set_timing(0)
+    for tag, hint in (("", 1), ("cold_", 0)):
+        _lib.check(_lib.lib().gf_knn_plan_set_hint(plan, hint), ctx.handle, "hint")
+        ctx.set_timing(kid_all)
+        for i in range(12):
+            enqueue(plan, pts_ref[i % args.windows], slots[i % 4].data_ptr())
+        for name, kid in (("sample", _lib.K_KNN_SAMPLE), ("scan", _lib.K_KNN_SCAN), ("select", _lib.K_KNN_SELECT)):
+            ms, cnt = ctx.timing(kid)
+            breakdown[tag + name + "_us"] = round(1000.0 * ms / max(cnt, 1), 2)
+        ctx.set_timing(0)
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for i in range(20):
+            enqueue(plan, pts_ref[i % args.windows], slots[i % 4].data_ptr())
+        torch.cuda.synchronize()
+        breakdown[tag + "window_us"] = round(1e6 * (time.perf_counter() - t) / 20, 2)
+    _lib.check(_lib.lib().gf_knn_plan_set_hint(plan, 1), ctx.handle, "hint")
 
     verified = None
     cpu = None
@@ -164,13 +189,17 @@ def main():
         og = O.grid(args.grid, *BEIJING)
         if not args.no_verify:
             t = time.perf_counter()
-            st, oo, od, oi = O.knn(og, x, y, obj, QPOINT[0], QPOINT[1], args.radius, args.k)
-            verified = bool(st == 0 and np.array_equal(oo, first[0]) and np.array_equal(od, first[1])
-                            and np.array_equal(oi, first[2]))
-            log(f"oracle verification over the full window: {verified} ({time.perf_counter()-t:.1f}s)")
+            verified = True
+            for j, (x, y, obj) in enumerate(host_windows):
+                st, oo, od, oi = O.knn(og, x, y, obj, QPOINT[0], QPOINT[1], args.radius, args.k)
+                got = per_window[j]
+                verified &= bool(st == 0 and np.array_equal(oo, got[0]) and np.array_equal(od, got[1])
+                                 and np.array_equal(oi, got[2]))
+            log(f"oracle verification of {len(host_windows)} windows: {verified} ({time.perf_counter()-t:.1f}s)")
             assert verified, "GPU kNN differs from the oracle"
         if not args.no_cpu_baseline:
             S = min(args.cpu_sample, n)
+            x, y, obj = host_windows[0]
             xs, ys, os_ = np.ascontiguousarray(x[:S]), np.ascontiguousarray(y[:S]), np.ascontiguousarray(obj[:S])
             reps, t = 0, time.perf_counter()
             while True:
@@ -202,7 +231,8 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic: java.util.Random-compatible uniform points, Beijing bounds, device-resident windows",
+            "data": (f"synthetic: java.util.Random-compatible uniform points, Beijing bounds, {args.windows} distinct "
+                     "device-resident windows cycled (continuous query)"),
             "config": {
                 "workload": f"knn_k{args.k}_r{args.radius}_{n // 1_000_000}Mpts_per_gpu_grid{args.grid}x{args.grid}",
                 "points_per_window": pts_per_step,

@@ -150,13 +150,16 @@ int  gf_bitmap_to_indices(gf_ctx* ctx, const uint64_t* bitmap, int64_t n, uint32
 typedef struct gf_knn_plan gf_knn_plan;
 /* PointPointKNNQuery.run(stream, queryPoint, r, k) -- PointPointKNNQuery.java:33,132-150 */
 int    gf_knn_pp_plan_create(gf_ctx* ctx, const gf_grid* g, double qx, double qy, double r,
-                             int32_t k, int metric, gf_knn_plan** out);
+                             int32_t k, int metric, gf_knn_plan** out);   /* 1 <= k <= 512 */
 void   gf_knn_plan_destroy(gf_knn_plan* plan);
 /* Candidate-buffer capacity (entries); default 1<<20.  Small values force the exact fallback. */
 int    gf_knn_plan_set_capacity(gf_knn_plan* plan, int64_t cap);
 /* Scan-kernel tuning: grid blocks (0 = auto), point pairs per lane per iteration (1..8),
  * nontemporal loads (0/1).  Results never depend on it. */
 int    gf_knn_plan_set_tuning(gf_knn_plan* plan, int32_t scan_blocks, int32_t unroll, int32_t nontemporal);
+/* Continuous-query threshold hint (default on): each window stores 2 x its k-th distance and
+ * the next window scans only below it (still verified: >= k distinct objIDs or re-evaluate). */
+int    gf_knn_plan_set_hint(gf_knn_plan* plan, int enable);
 /* Offset added to the window-local point index in results (a shard's first global index). */
 int    gf_knn_plan_set_index_base(gf_knn_plan* plan, int64_t base);
 /* Result record: gf_knn_header followed by double dist[k], int64 objID[k], int64 idx[k]. */
@@ -194,6 +197,12 @@ int    gf_knn_merge_host(int32_t k, int32_t nlists, const int32_t* counts, const
 int gf_join_pp(gf_ctx* ctx, const gf_grid* ugrid, const gf_grid* qgrid, const gf_points* ordinary,
                const gf_points* query, double r, int approximate, int metric, uint32_t* pairs,
                int64_t cap, int64_t* npairs);
+
+/* ---- pinned host memory ---------------------------------------------------------------
+ * Mapped, portable host memory: kernels write kNN records straight into it (pass it as the
+ * `result` of gf_knn_enqueue), so no copy kernel runs per window. */
+int  gf_pinned_alloc(size_t bytes, void** ptr);
+void gf_pinned_free(void* ptr);
 
 /* ---- host windows -------------------------------------------------------------------- */
 typedef struct gf_window gf_window;

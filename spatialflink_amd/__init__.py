@@ -8,13 +8,13 @@ PointPointRangeQuery, PointPolygonRangeQuery, PointPointKNNQuery, PointPointJoin
 from . import _lib
 from .spatialIndices import UniformGrid, generateCellIDStr, getIntCellIndices, padLeadingZeroesToInt
 from .spatialObjects import Point, PointWindow, Polygon, PolygonSet
-from .spatialOperators import (KNNResult, PointPointJoinQuery, PointPointKNNQuery, PointPointRangeQuery,
+from .spatialOperators import (KNNResult, PinnedRecords, PointPointJoinQuery, PointPointKNNQuery, PointPointRangeQuery,
                                PointPolygonRangeQuery, QueryConfiguration, QueryType, RangeResult, assign_cells,
                                bucket_by_cell, knn_merge_host, synthetic_uniform)
 
 __all__ = [
     "UniformGrid", "Point", "Polygon", "PolygonSet", "PointWindow", "QueryType", "QueryConfiguration",
     "PointPointRangeQuery", "PointPolygonRangeQuery", "PointPointKNNQuery", "PointPointJoinQuery", "RangeResult",
-    "KNNResult", "knn_merge_host", "assign_cells", "bucket_by_cell", "synthetic_uniform", "generateCellIDStr",
+    "KNNResult", "PinnedRecords", "knn_merge_host", "assign_cells", "bucket_by_cell", "synthetic_uniform", "generateCellIDStr",
     "getIntCellIndices", "padLeadingZeroesToInt",
 ]

@@ -33,9 +33,10 @@ EXPORTS = [
     "gf_ctx_timing", "gf_grid_make", "gf_grid_layers", "gf_cell_of", "gf_format_cell_id", "gf_parse_cell_id",
     "gf_assign_cells", "gf_bucket_by_cell", "gf_range_pp_plan_create", "gf_range_ppoly_plan_create",
     "gf_range_plan_destroy", "gf_range_run", "gf_bitmap_to_indices", "gf_knn_pp_plan_create",
-    "gf_knn_plan_destroy", "gf_knn_plan_set_capacity", "gf_knn_plan_set_index_base", "gf_knn_plan_set_tuning", "gf_knn_result_bytes", "gf_knn_enqueue",
+    "gf_knn_plan_destroy", "gf_knn_plan_set_capacity", "gf_knn_plan_set_index_base", "gf_knn_plan_set_tuning", "gf_knn_plan_set_hint", "gf_knn_result_bytes", "gf_knn_enqueue",
     "gf_knn_decode", "gf_knn_run", "gf_knn_merge_dev", "gf_knn_merge_host", "gf_join_pp", "gf_window_create",
-    "gf_window_destroy", "gf_window_upload", "gf_window_points", "gf_synth_uniform",
+    "gf_window_destroy", "gf_window_upload", "gf_window_points", "gf_synth_uniform", "gf_pinned_alloc",
+    "gf_pinned_free",
 ]
 
 
@@ -119,6 +120,7 @@ def lib():
             "gf_knn_plan_set_capacity": ([P, i64], C.c_int),
             "gf_knn_plan_set_index_base": ([P, i64], C.c_int),
             "gf_knn_plan_set_tuning": ([P, i32, i32, i32], C.c_int),
+            "gf_knn_plan_set_hint": ([P, C.c_int], C.c_int),
             "gf_knn_result_bytes": ([i32], sz),
             "gf_knn_enqueue": ([P, C.POINTER(GfPoints), P], C.c_int),
             "gf_knn_decode": ([P, C.POINTER(GfPoints), P, P, P, P, pi32], C.c_int),
@@ -132,6 +134,8 @@ def lib():
             "gf_window_upload": ([P, P, P, P, P, i64], C.c_int),
             "gf_window_points": ([P, C.POINTER(GfPoints)], C.c_int),
             "gf_synth_uniform": ([i64, i64, d, d, d, d, P, P], C.c_int),
+            "gf_pinned_alloc": ([sz, C.POINTER(P)], C.c_int),
+            "gf_pinned_free": ([P], None),
         }
         for name, (argt, rest) in sig.items():
             fn = getattr(L, name)

@@ -687,6 +687,7 @@ extern "C" void gf_knn_plan_destroy(gf_knn_plan* P) {
   if (P->st) hipFree(P->st);
   if (P->cand_d) hipFree(P->cand_d);
   if (P->cand_i) hipFree(P->cand_i);
+  if (P->cand_o) hipFree(P->cand_o);
   if (P->tmp_result) hipFree(P->tmp_result);
   if (P->host_result) hipHostFree(P->host_result);
   delete P;
@@ -696,10 +697,13 @@ static int knn_alloc_candidates(gf_knn_plan* P, int64_t cap) {
   gf_ctx* ctx = P->ctx;
   if (P->cand_d) hipFree(P->cand_d);
   if (P->cand_i) hipFree(P->cand_i);
+  if (P->cand_o) hipFree(P->cand_o);
   P->cand_d = nullptr;
   P->cand_i = nullptr;
+  P->cand_o = nullptr;
   GF_HIP_CHECK(ctx, hipMalloc(&P->cand_d, sizeof(double) * (size_t)cap));
   GF_HIP_CHECK(ctx, hipMalloc(&P->cand_i, sizeof(uint32_t) * (size_t)cap));
+  GF_HIP_CHECK(ctx, hipMalloc(&P->cand_o, sizeof(int64_t) * (size_t)cap));
   P->cap = cap;
   return GF_OK;
 }
@@ -707,7 +711,7 @@ static int knn_alloc_candidates(gf_knn_plan* P, int64_t cap) {
 extern "C" int gf_knn_pp_plan_create(gf_ctx* ctx, const gf_grid* g, double qx, double qy, double r, int32_t k,
                                      int metric, gf_knn_plan** out) {
   if (!ctx || !out || !grid_ok(g) || k < 1 || k > kMaxK || (metric != 0 && metric != 1))
-    return set_err(ctx, GF_ERR_ARG, "gf_knn_pp_plan_create: bad argument (k must be in [1, 1024])");
+    return set_err(ctx, GF_ERR_ARG, "gf_knn_pp_plan_create: bad argument (k must be in [1, 512])");
   *out = nullptr;
   int st = bind(ctx);
   if (st) return st;
@@ -754,21 +758,35 @@ extern "C" int gf_knn_plan_set_index_base(gf_knn_plan* P, int64_t base) {
 }
 
 static int knn_scan_select(gf_knn_plan* P, const gf_points* pts, int64_t begin, int64_t end, int use_state,
-                           void* result) {
+                           int write_hint, void* result) {
   gf_ctx* ctx = P->ctx;
   KnnScanArgs s{};
-  s.x = pts->x; s.y = pts->y; s.begin = begin; s.end = end;
+  s.x = pts->x; s.y = pts->y; s.objID = pts->objID; s.begin = begin; s.end = end;
   s.qx = P->qx; s.qy = P->qy; s.qr = P->qr;
   s.T = P->r; s.s_pre = s_prefilter(P->r, P->metric);
   s.use_state = use_state; s.metric = P->metric; s.st = P->st;
-  s.cand_d = P->cand_d; s.cand_i = P->cand_i; s.cap = (unsigned long long)P->cap;
-  const int blocks = P->scan_blocks > 0 ? P->scan_blocks : stream_blocks(ctx, ((end - begin) + 1) / 2);
+  s.cand_d = P->cand_d; s.cand_i = P->cand_i; s.cand_o = P->cand_o; s.cap = (unsigned long long)P->cap;
+  int blocks = P->scan_blocks;
+  if (blocks <= 0) {  // 4 blocks per CU measured best for the 1-pair nontemporal loop
+    blocks = stream_blocks(ctx, ((end - begin) + 1) / 2);
+    blocks = std::min(blocks, ctx->num_cus * 4);
+  }
   GF_HIP_CHECK(ctx, launch_knn_scan(ctx, s, blocks, P->scan_unroll, P->scan_nt));
   KnnSelectArgs q{};
-  q.st = P->st; q.cand_d = P->cand_d; q.cand_i = P->cand_i; q.cap = (unsigned long long)P->cap;
-  q.objID = pts->objID; q.use_state = use_state; q.T = P->r; q.r = P->r; q.k = P->k; q.result = result;
-  q.idx_base = P->idx_base;
+  q.st = P->st; q.cand_d = P->cand_d; q.cand_i = P->cand_i; q.cand_o = P->cand_o;
+  q.cap = (unsigned long long)P->cap;
+  q.use_state = use_state; q.T = P->r; q.r = P->r; q.k = P->k; q.result = result;
+  q.write_hint = write_hint; q.idx_base = P->idx_base;
   GF_HIP_CHECK(ctx, launch_knn_select(ctx, q));
+  return GF_OK;
+}
+
+static int knn_launch_sample(gf_knn_plan* P, const gf_points* pts, int use_hint) {
+  KnnSampleArgs s{};
+  s.x = pts->x; s.y = pts->y; s.n = pts->n; s.qx = P->qx; s.qy = P->qy; s.qr = P->qr;
+  s.r = P->r; s.s_r = s_prefilter(P->r, P->metric); s.k = P->k; s.metric = P->metric; s.st = P->st;
+  s.use_hint = use_hint;
+  GF_HIP_CHECK(P->ctx, launch_knn_sample(P->ctx, s));
   return GF_OK;
 }
 
@@ -779,14 +797,20 @@ extern "C" int gf_knn_enqueue(gf_knn_plan* P, const gf_points* pts, void* result
   if (st) return st;
   if ((st = check_points(ctx, pts))) return st;
   if (pts->n > 0 && !pts->objID) return set_err(ctx, GF_ERR_ARG, "kNN needs objID");
-  const bool sample = pts->n >= kSampleMinN;
-  if (sample) {
-    KnnSampleArgs s{};
-    s.x = pts->x; s.y = pts->y; s.n = pts->n; s.qx = P->qx; s.qy = P->qy; s.qr = P->qr;
-    s.r = P->r; s.s_r = s_prefilter(P->r, P->metric); s.k = P->k; s.metric = P->metric; s.st = P->st;
-    GF_HIP_CHECK(ctx, launch_knn_sample(ctx, s));
-  }
-  return knn_scan_select(P, pts, 0, pts->n, sample ? 1 : 0, result);
+  // threshold: previous window's hint (continuous query) or the sample; tiny windows scan to r
+  const bool staged = pts->n >= kSampleMinN;
+  if (staged && (st = knn_launch_sample(P, pts, P->use_hint))) return st;
+  return knn_scan_select(P, pts, 0, pts->n, staged ? 1 : 0, staged && P->use_hint, result);
+}
+
+extern "C" int gf_knn_plan_set_hint(gf_knn_plan* P, int enable) {
+  if (!P) return GF_ERR_ARG;
+  int st = bind(P->ctx);
+  if (st) return st;
+  P->use_hint = enable != 0;
+  GF_HIP_CHECK(P->ctx, hipStreamSynchronize(P->ctx->stream));
+  GF_HIP_CHECK(P->ctx, hipMemset(&P->st->hint_T, 0, sizeof(double)));
+  return GF_OK;
 }
 
 namespace {
@@ -823,19 +847,29 @@ extern "C" int gf_knn_merge_host(int32_t k, int32_t nlists, const int32_t* count
   return GF_OK;
 }
 
-// exact fallback: T = r over capacity-sized partitions, merged on the host
+// Re-evaluation of a flagged window: first the sample path with the hint ignored; if that
+// is still inconclusive, exhaustive T = r over capacity-sized partitions merged on the host.
 static int knn_fallback(gf_knn_plan* P, const gf_points* pts, int64_t* oo, double* od, int64_t* oi, int32_t* n_out) {
   gf_ctx* ctx = P->ctx;
-  const int64_t part = std::max<int64_t>(2, P->cap & ~(int64_t)1);
   const size_t rb = gf_knn_result_bytes(P->k);
+  const gf_knn_header* h = (const gf_knn_header*)P->host_result;
+  auto fetch = [&]() -> int {
+    GF_HIP_CHECK(ctx, hipMemcpyAsync(P->host_result, P->tmp_result, rb, hipMemcpyDeviceToHost, ctx->stream));
+    GF_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+    return GF_OK;
+  };
+  int st;
+  if (pts->n >= kSampleMinN) {
+    if ((st = knn_launch_sample(P, pts, 0)) || (st = knn_scan_select(P, pts, 0, pts->n, 1, P->use_hint, P->tmp_result)) ||
+        (st = fetch()))
+      return st;
+    if (h->status == 0) return gf_knn_decode(P, pts, P->host_result, oo, od, oi, n_out);
+  }
+  const int64_t part = std::max<int64_t>(2, P->cap & ~(int64_t)1);
   std::vector<Ent> all;
   for (int64_t lo = 0; lo < pts->n; lo += part) {
     const int64_t hi = std::min(pts->n, lo + part);
-    int st = knn_scan_select(P, pts, lo, hi, 0, P->tmp_result);
-    if (st) return st;
-    GF_HIP_CHECK(ctx, hipMemcpyAsync(P->host_result, P->tmp_result, rb, hipMemcpyDeviceToHost, ctx->stream));
-    GF_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
-    const gf_knn_header* h = (const gf_knn_header*)P->host_result;
+    if ((st = knn_scan_select(P, pts, lo, hi, 0, 0, P->tmp_result)) || (st = fetch())) return st;
     if (h->status != 0) return set_err(ctx, GF_ERR_HIP, "kNN partition did not converge");
     const double* d = (const double*)(h + 1);
     const int64_t* o = (const int64_t*)(d + P->k);
@@ -958,6 +992,25 @@ extern "C" int gf_join_pp(gf_ctx* ctx, const gf_grid* ugrid, const gf_grid* qgri
 // ---------------------------------------------------------------------------------------
 // windows, synthetic input
 // ---------------------------------------------------------------------------------------
+extern "C" int gf_pinned_alloc(size_t bytes, void** ptr) {
+  if (!ptr || bytes == 0) return GF_ERR_ARG;
+  *ptr = nullptr;
+  // mapped + portable: the same pointer is written by kernels and read by the host
+  hipError_t e = hipHostMalloc(ptr, bytes, hipHostMallocMapped | hipHostMallocPortable);
+  if (e != hipSuccess) return GF_ERR_NOMEM;
+  void* dptr = nullptr;
+  if (hipHostGetDevicePointer(&dptr, *ptr, 0) != hipSuccess || dptr != *ptr) {
+    hipHostFree(*ptr);
+    *ptr = nullptr;
+    return GF_ERR_HIP;  // unified addressing expected on gfx950
+  }
+  return GF_OK;
+}
+
+extern "C" void gf_pinned_free(void* ptr) {
+  if (ptr) hipHostFree(ptr);
+}
+
 extern "C" int gf_window_create(gf_ctx* ctx, int64_t capacity, gf_window** out) {
   if (!ctx || !out || capacity < 0) return GF_ERR_ARG;
   int st = bind(ctx);

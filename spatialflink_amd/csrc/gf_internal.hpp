@@ -60,7 +60,7 @@ struct KTimer {
 // ---------------------------------------------------------------------------------------
 constexpr int kBlock = 256;         // streaming kernels: 4 waves
 constexpr int kSortCap = 4096;      // select kernel: LDS sort capacity
-constexpr int kMaxK = 1024;         // largest k on the device path
+constexpr int kMaxK = 512;          // largest k on the device path
 constexpr int kSampleBlocks = 128;  // kNN sample: 128 blocks x 2048 points = 256K points
 constexpr int kSamplePerBlock = 2048;
 constexpr int64_t kSampleMinN = 1 << 20;
@@ -78,14 +78,16 @@ struct KnnState {
   uint32_t hist[kDistBins];
   uint32_t ticket;
   uint32_t pad;
-  double T;          // distance threshold chosen by the sample (<= r)
+  double T;          // distance threshold of the current window (<= r)
   double s_pre;      // prefilter bound on dx*dx+dy*dy for T
   unsigned long long count;  // candidates appended (may exceed capacity)
+  double hint_T;     // next window's threshold guess (2 x this window's k-th distance); 0 = none
 };
 
 struct KnnScanArgs {
   const double* x;
   const double* y;
+  const int64_t* objID;
   int64_t begin, end;   // [begin, end), begin even
   double qx, qy;
   QueryRect qr;
@@ -95,6 +97,7 @@ struct KnnScanArgs {
   KnnState* st;
   double* cand_d;
   uint32_t* cand_i;
+  int64_t* cand_o;
   unsigned long long cap;
 };
 
@@ -107,6 +110,7 @@ struct KnnSampleArgs {
   double r, s_r;
   int32_t k;
   int metric;
+  int use_hint;         // take st->hint_T when set instead of sampling
   KnnState* st;
 };
 
@@ -114,12 +118,13 @@ struct KnnSelectArgs {
   KnnState* st;
   const double* cand_d;
   const uint32_t* cand_i;
+  const int64_t* cand_o;
   unsigned long long cap;
-  const int64_t* objID;
   int use_state;
   double T;             // when !use_state
   double r;
   int32_t k;
+  int write_hint;       // store 2 x k-th distance as the next window's threshold guess
   int64_t idx_base;     // added to the window-local index in the record
   void* result;         // gf_knn_header + dist[k] + objID[k] + idx[k]
 };
@@ -247,12 +252,14 @@ struct gf_knn_plan {
   gf::KnnState* st = nullptr;
   double* cand_d = nullptr;
   uint32_t* cand_i = nullptr;
+  int64_t* cand_o = nullptr;
   int64_t cap = 0;
+  int use_hint = 1;             // reuse the previous window's k-th distance as the threshold guess
   int64_t idx_base = 0;
   void* tmp_result = nullptr;   // device record used by gf_knn_run / fallback
   void* host_result = nullptr;  // pinned
-  int scan_blocks = 0;   // tuning: 0 = auto
-  int scan_unroll = 4;   // point pairs per lane per iteration
+  int scan_blocks = 0;   // tuning: 0 = auto (4 blocks per CU)
+  int scan_unroll = 1;   // point pairs per lane per iteration (tools/tune_knn.py sweep)
   int scan_nt = 1;       // nontemporal loads
 };
 

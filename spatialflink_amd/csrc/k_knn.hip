@@ -1,20 +1,23 @@
 // k_knn.hip -- per-query kNN over one window (PointPointKNNQuery.java:132-201 per-cell heaps +
 // KNNQuery.java:213-272 windowAll merge), restated as a three-kernel pipeline for gfx950:
 //
-//   knn_sample  64 blocks read a strided 128K-point sample, histogram candidate distances
-//               into 4096 log-spaced bins; the last block (atomic ticket) picks T = the upper
-//               edge of the bin holding the sample's k-th candidate (>= the window's k-th
-//               distance, because the sample is a subset).  Skipped for windows < 1M points.
-//   knn_scan    the HBM-bound pass: 16 B/point (x, y), one test per point against the exact
-//               prefilter s = dx*dx+dy*dy <= smax(T); the rare survivors get the exact cell
-//               test (C u G) and are appended (d, idx) with one atomic per wave.
-//   knn_select  one 1024-thread block: LDS histogram of the M candidates, keep the bins up
-//               to the k-th, bitonic-sort (d, objID, idx) in LDS, objID dedupe, first k.
+//   knn_sample  picks the window's distance threshold T.  Continuous queries: T = the previous
+//               window's hint (2 x its k-th distance) and the kernel exits at once.  Otherwise
+//               128 blocks read a strided 256K-point sample, histogram candidate distances in
+//               LDS (4096 log-spaced bins), flush to a global histogram, and the last block
+//               (atomic ticket) takes the upper edge of the bin holding the sample's k-th
+//               candidate (>= the window's k-th distance: the sample is a subset).
+//   knn_scan    the HBM-bound pass: 16 B/point (x, y), one compare per point against the exact
+//               prefilter s = dx*dx+dy*dy <= smax(T); survivors get the exact cell test (C u G)
+//               and are appended (d, idx, objID) with one atomic per wave.
+//   knn_select  one 1024-thread block: candidates loaded at once, LDS histogram -> bins up to
+//               the k-th -> sort (in one wave's registers when <= 64, else LDS bitonic) ->
+//               objID dedupe -> first k; stores the next window's hint.
 //
-// Exactness never depends on the sample: if the candidate buffer overflows, or fewer than k
-// distinct objIDs lie below T < r, the record says so and the host re-runs with T = r in
-// capacity-sized partitions (gf_knn_decode).  Output: (d, objID) ascending, min-(d, idx)
-// occurrence per objID.
+// Exactness never depends on T: the record is final only if at least k distinct objIDs lie
+// below T (or T == r); otherwise it is flagged and gf_knn_decode re-evaluates the window
+// (sample path, then exhaustive T = r partitions).  Output: (d, objID) ascending, the
+// minimum-(d, idx) occurrence per objID.
 #include "gf_internal.hpp"
 
 namespace gf {
@@ -27,19 +30,20 @@ __device__ __forceinline__ bool classify_cg(const QueryRect& q, double px, doubl
 }
 
 // kNN candidate: cell in C u G (PointPointKNNQuery.java:145-150) and d <= T (<= r, :170-177).
+// The hot test keeps no distance live; the rare append recomputes it from x, y.
 template <int METRIC>
-__device__ __forceinline__ bool knn_candidate(double qx, double qy, const QueryRect& qr, double px,
-                                              double py, double sp, double T, double& d) {
+__device__ __forceinline__ bool knn_pass(double qx, double qy, const QueryRect& qr, double px, double py,
+                                         double sp, double T) {
   const double dx = qx - px, dy = qy - py;
   const double s = dx * dx + dy * dy;
   if (!(s <= sp)) return false;
   if (!classify_cg(qr, px, py)) return false;
-  if (METRIC == 0) {
-    d = sqrt(s);  // s <= smax(T)  <=>  sqrt(s) <= T
-    return true;
-  }
-  d = fdlibm_hypot(dx, dy);
-  return d <= T;
+  return METRIC == 0 ? true : fdlibm_hypot(dx, dy) <= T;  // metric 0: s <= smax(T) <=> sqrt(s) <= T
+}
+template <int METRIC>
+__device__ __forceinline__ double knn_dist(double qx, double qy, double px, double py) {
+  const double dx = qx - px, dy = qy - py;
+  return METRIC == 0 ? sqrt(dx * dx + dy * dy) : fdlibm_hypot(dx, dy);
 }
 
 __device__ __forceinline__ uint64_t okey(int64_t o) { return (uint64_t)o ^ 0x8000000000000000ull; }
@@ -61,16 +65,24 @@ __host__ __device__ inline RecView rec_view(void* base, int k) {
 }
 
 // ---------------------------------------------------------------------------------------
-// sample: kSampleBlocks blocks x kSamplePerBlock points, spread evenly over the window.
-// Each thread issues all its loads up front (8 points = 4 x 16-B loads of x and y), bins its
-// candidates into an LDS histogram, and the block flushes only non-zero bins to the global
-// histogram (no same-address global atomic storms).  The last block (ticket) scans it.
+// sample
 // ---------------------------------------------------------------------------------------
 template <int METRIC>
 __global__ __launch_bounds__(kBlock) void knn_sample_kernel(KnnSampleArgs a) {
   __shared__ uint32_t lh[kDistBins];
   __shared__ uint32_t wsum[kBlock / 64];
   __shared__ int s_last, s_bin;
+  if (a.use_hint) {
+    const double h = a.st->hint_T;
+    if (h > 0.0) {  // continuous query: the previous window's guess; nothing to sample
+      if (blockIdx.x == 0 && threadIdx.x == 0) {
+        const double T = h < a.r ? h : a.r;
+        a.st->T = T;
+        a.st->s_pre = s_prefilter(T, a.metric);
+      }
+      return;
+    }
+  }
   constexpr int kPairs = kSamplePerBlock / 2 / kBlock;  // pairs per thread
   for (int j = threadIdx.x; j < kDistBins; j += kBlock) lh[j] = 0u;
   const int64_t npairs = a.n >> 1;
@@ -87,9 +99,10 @@ __global__ __launch_bounds__(kBlock) void knn_sample_kernel(KnnSampleArgs a) {
   __syncthreads();
 #pragma unroll
   for (int u = 0; u < kPairs; ++u) {
-    double d;
-    if (knn_candidate<METRIC>(a.qx, a.qy, a.qr, xv[u].x, yv[u].x, a.s_r, a.r, d)) atomicAdd(&lh[dist_bin(d, bbase)], 1u);
-    if (knn_candidate<METRIC>(a.qx, a.qy, a.qr, xv[u].y, yv[u].y, a.s_r, a.r, d)) atomicAdd(&lh[dist_bin(d, bbase)], 1u);
+    if (knn_pass<METRIC>(a.qx, a.qy, a.qr, xv[u].x, yv[u].x, a.s_r, a.r))
+      atomicAdd(&lh[dist_bin(knn_dist<METRIC>(a.qx, a.qy, xv[u].x, yv[u].x), bbase)], 1u);
+    if (knn_pass<METRIC>(a.qx, a.qy, a.qr, xv[u].y, yv[u].y, a.s_r, a.r))
+      atomicAdd(&lh[dist_bin(knn_dist<METRIC>(a.qx, a.qy, xv[u].y, yv[u].y), bbase)], 1u);
   }
   __syncthreads();
   for (int j = threadIdx.x; j < kDistBins; j += kBlock)
@@ -157,96 +170,93 @@ hipError_t launch_knn_sample(gf_ctx* ctx, const KnnSampleArgs& a) {
 }
 
 // ---------------------------------------------------------------------------------------
-// scan: grid-stride over point pairs; U pairs per lane per iteration, all loads issued before
-// any use (U x 32 B in flight per lane); NT = nontemporal (streamed-once) loads.
+// scan
 // ---------------------------------------------------------------------------------------
 typedef double dbl2 __attribute__((ext_vector_type(2)));
 
 template <int NT>
-__device__ __forceinline__ void load_pair(const double* __restrict__ x, const double* __restrict__ y, int64_t p,
-                                          int64_t end, double2& xv, double2& yv) {
-  const int64_t i = 2 * p;
-  if (i + 1 < end) {
-    if (NT) {
-      const dbl2 a = __builtin_nontemporal_load(reinterpret_cast<const dbl2*>(x + i));
-      const dbl2 b = __builtin_nontemporal_load(reinterpret_cast<const dbl2*>(y + i));
-      xv.x = a.x; xv.y = a.y; yv.x = b.x; yv.y = b.y;
-    } else {
-      xv = *reinterpret_cast<const double2*>(x + i);
-      yv = *reinterpret_cast<const double2*>(y + i);
-    }
-  } else if (i < end) {
-    xv.x = x[i]; yv.x = y[i];
-    xv.y = NAN; yv.y = NAN;  // NaN never passes the distance prefilter
-  } else {
-    xv.x = xv.y = yv.x = yv.y = NAN;
-  }
+__device__ __forceinline__ dbl2 ld2(const dbl2* p) {
+  if (NT) return __builtin_nontemporal_load(p);
+  return *p;
 }
 
-__device__ __forceinline__ void wave_append(bool c, double d, uint32_t idx, KnnState* st, double* cand_d,
-                                            uint32_t* cand_i, unsigned long long cap) {
+__device__ __forceinline__ void wave_append(bool c, double d, uint32_t idx, const KnnScanArgs& a) {
   const uint64_t m = __ballot(c);
   if (m == 0) return;
   const int lane = threadIdx.x & 63;
   const int leader = __ffsll((unsigned long long)m) - 1;
   unsigned long long base = 0;
-  if (lane == leader) base = atomicAdd(&st->count, (unsigned long long)__popcll(m));
+  if (lane == leader) base = atomicAdd(&a.st->count, (unsigned long long)__popcll(m));
   base = __shfl(base, leader, 64);
   if (c) {
     const unsigned long long pos = base + (unsigned long long)__popcll(m & ((1ull << lane) - 1ull));
-    if (pos < cap) {
-      cand_d[pos] = d;
-      cand_i[pos] = idx;
+    if (pos < a.cap) {
+      a.cand_d[pos] = d;
+      a.cand_i[pos] = idx;
+      a.cand_o[pos] = a.objID[idx];
     }
   }
 }
 
-// Hot-loop test: prefilter + exact cell class + (hypot) exact distance; no distance is kept
-// live across the loop -- the rare append branch recomputes it from the loaded x, y.
-template <int METRIC>
-__device__ __forceinline__ bool knn_pass(double qx, double qy, const QueryRect& qr, double px, double py,
-                                         double sp, double T) {
-  const double dx = qx - px, dy = qy - py;
-  const double s = dx * dx + dy * dy;
-  if (!(s <= sp)) return false;
-  if (!classify_cg(qr, px, py)) return false;
-  return METRIC == 0 ? true : fdlibm_hypot(dx, dy) <= T;
-}
-template <int METRIC>
-__device__ __forceinline__ double knn_dist(double qx, double qy, double px, double py) {
-  const double dx = qx - px, dy = qy - py;
-  return METRIC == 0 ? sqrt(dx * dx + dy * dy) : fdlibm_hypot(dx, dy);
-}
-
-template <int METRIC, int U, int NT>
-__global__ __launch_bounds__(kBlock) void knn_scan_kernel(KnnScanArgs a) {
-  const double sp = a.use_state ? a.st->s_pre : a.s_pre;
-  const double T = a.use_state ? a.st->T : a.T;
-  const int64_t pend = (a.end + 1) >> 1;
-  const int lane = threadIdx.x & 63;
-  const int64_t wstride = (int64_t)gridDim.x * kBlock;
-  int64_t base = (a.begin >> 1) + (int64_t)blockIdx.x * kBlock + (threadIdx.x & ~63);
-  for (; base < pend; base += U * wstride) {
-    double2 xv[U], yv[U];
+// Per-iteration body shared by the unchecked main loop and the checked tail.
+template <int METRIC, int U>
+__device__ __forceinline__ void knn_scan_tile(const KnnScanArgs& a, const dbl2 (&xv)[U], const dbl2 (&yv)[U],
+                                              int64_t p0, int64_t wstride, double sp, double T) {
+  uint32_t cm = 0;  // candidate bits, 2 per pair
 #pragma unroll
-    for (int u = 0; u < U; ++u) load_pair<NT>(a.x, a.y, base + u * wstride + lane, a.end, xv[u], yv[u]);
-    uint32_t cm = 0;  // candidate bits, 2 per pair
+  for (int u = 0; u < U; ++u) {
+    cm |= (uint32_t)knn_pass<METRIC>(a.qx, a.qy, a.qr, xv[u].x, yv[u].x, sp, T) << (2 * u);
+    cm |= (uint32_t)knn_pass<METRIC>(a.qx, a.qy, a.qr, xv[u].y, yv[u].y, sp, T) << (2 * u + 1);
+  }
+  if (__ballot(cm != 0)) {  // wave-uniform, rare once T is tight
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      cm |= (uint32_t)knn_pass<METRIC>(a.qx, a.qy, a.qr, xv[u].x, yv[u].x, sp, T) << (2 * u);
-      cm |= (uint32_t)knn_pass<METRIC>(a.qx, a.qy, a.qr, xv[u].y, yv[u].y, sp, T) << (2 * u + 1);
+      const uint32_t i0 = (uint32_t)(2 * (p0 + u * wstride));
+      const bool c0 = (cm >> (2 * u)) & 1u, c1 = (cm >> (2 * u + 1)) & 1u;
+      wave_append(c0, c0 ? knn_dist<METRIC>(a.qx, a.qy, xv[u].x, yv[u].x) : 0.0, i0, a);
+      wave_append(c1, c1 ? knn_dist<METRIC>(a.qx, a.qy, xv[u].y, yv[u].y) : 0.0, i0 + 1, a);
     }
-    if (__ballot(cm != 0)) {  // wave-uniform, rare once T is tight
+  }
+}
+
+// Main loop: every wave runs the same number of full U-pair tiles with no bounds checks (loads
+// issued back to back from bumped pointers, counted waits); the remainder goes through a
+// checked one-pair-per-lane tail.
+template <int METRIC, int U, int NT>
+__global__ __launch_bounds__(kBlock) void knn_scan_kernel(KnnScanArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wstride = (int64_t)gridDim.x * kBlock;
+  const int64_t pbeg = a.begin >> 1;
+  const int64_t npf = (a.end - a.begin) >> 1;  // complete pairs
+  const int64_t iters = npf / (U * wstride);    // full tiles for every wave
+  const int64_t off = (int64_t)blockIdx.x * kBlock + (threadIdx.x & ~63) + lane;
+  const double sp = a.use_state ? a.st->s_pre : a.s_pre;
+  const double T = a.use_state ? a.st->T : a.T;
+  const dbl2* px = reinterpret_cast<const dbl2*>(a.x) + pbeg + off;
+  const dbl2* py = reinterpret_cast<const dbl2*>(a.y) + pbeg + off;
+  for (int64_t it = 0; it < iters; ++it) {
+    dbl2 xv[U], yv[U];
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const uint32_t i0 = (uint32_t)(2 * (base + u * wstride + lane));
-        const bool c0 = (cm >> (2 * u)) & 1u, c1 = (cm >> (2 * u + 1)) & 1u;
-        wave_append(c0, c0 ? knn_dist<METRIC>(a.qx, a.qy, xv[u].x, yv[u].x) : 0.0, i0, a.st, a.cand_d, a.cand_i,
-                    a.cap);
-        wave_append(c1, c1 ? knn_dist<METRIC>(a.qx, a.qy, xv[u].y, yv[u].y) : 0.0, i0 + 1, a.st, a.cand_d,
-                    a.cand_i, a.cap);
-      }
+    for (int u = 0; u < U; ++u) {
+      xv[u] = ld2<NT>(px + u * wstride);
+      yv[u] = ld2<NT>(py + u * wstride);
     }
+    knn_scan_tile<METRIC, U>(a, xv, yv, pbeg + off + it * U * wstride, wstride, sp, T);
+    px += U * wstride;
+    py += U * wstride;
+  }
+  const int64_t pend = (a.end + 1) >> 1;
+  for (int64_t p = pbeg + iters * U * wstride + off; p - lane < pend; p += wstride) {
+    const int64_t i = 2 * p;
+    dbl2 xv[1], yv[1];
+    if (i + 1 < a.end) {
+      xv[0] = *reinterpret_cast<const dbl2*>(a.x + i);
+      yv[0] = *reinterpret_cast<const dbl2*>(a.y + i);
+    } else {
+      xv[0].x = i < a.end ? a.x[i] : NAN; yv[0].x = i < a.end ? a.y[i] : NAN;
+      xv[0].y = NAN; yv[0].y = NAN;  // NaN never passes the prefilter
+    }
+    knn_scan_tile<METRIC, 1>(a, xv, yv, p, wstride, sp, T);
   }
 }
 
@@ -270,7 +280,7 @@ hipError_t launch_knn_scan(gf_ctx* ctx, const KnnScanArgs& a, int blocks, int un
 }
 
 // ---------------------------------------------------------------------------------------
-// select / merge: LDS bitonic sort on (d bits, objID key, idx), wave-0 objID dedupe
+// select / merge: sort on (d bits, objID key, idx) then objID dedupe
 // ---------------------------------------------------------------------------------------
 constexpr int kSelThreads = 1024;
 
@@ -341,56 +351,97 @@ __device__ int dedupe_first_k(const uint64_t* sd, const uint64_t* so, const int6
   return *s_n;
 }
 
-__global__ __launch_bounds__(kSelThreads) void knn_select_kernel(KnnSelectArgs a) {
-  __shared__ uint64_t sd[kSortCap], so[kSortCap];
-  __shared__ int64_t si[kSortCap];
+// <= 64 entries in one wave's registers: bitonic network over __shfl_xor, then dedupe.
+// Keys are unique (idx), so the compare-exchange needs no tie rule.
+__device__ __forceinline__ bool kless(uint64_t ad, uint64_t ao, int64_t ai, uint64_t bd, uint64_t bo, int64_t bi) {
+  if (ad != bd) return ad < bd;
+  if (ao != bo) return ao < bo;
+  return ai < bi;
+}
+__device__ int wave_sort_dedupe(uint64_t d, uint64_t o, int64_t i, int k, uint64_t* rd, uint64_t* ro, int64_t* ri) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int size = 2; size <= 64; size <<= 1) {
+#pragma unroll
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      const uint64_t pd = __shfl_xor(d, stride, 64), po = __shfl_xor(o, stride, 64);
+      const int64_t pi = __shfl_xor(i, stride, 64);
+      const bool up = (lane & size) == 0;
+      const bool lower = (lane & stride) == 0;
+      const bool plt = kless(pd, po, pi, d, o, i);
+      if ((lower == up) ? plt : !plt) { d = pd; o = po; i = pi; }
+    }
+  }
+  bool dup = false;
+  for (int j = 0; j < 64; ++j) {
+    const uint64_t oj = __shfl(o, j, 64);
+    dup |= (j < lane) && (oj == o);
+  }
+  const bool keep = (d != ~0ull) && !dup;
+  const uint64_t m = __ballot(keep);
+  const int rank = __popcll(m & ((1ull << lane) - 1ull));
+  if (keep && rank < k) { rd[rank] = d; ro[rank] = o; ri[rank] = i; }
+  const int n = __popcll(m);
+  return n < k ? n : k;
+}
+
+// Lean select: 4 waves, 64 KB of LDS.  Up to kSelFast candidates are staged in registers
+// (loaded together with the count: one memory latency), histogrammed in LDS; the survivors up
+// to the k-th bin are sorted in one wave's registers (<= 64) or an LDS bitonic network.
+constexpr int kSelT = 256;
+constexpr int kSelFast = 1024;
+static_assert(kSelFast > kMaxK, "general path needs room for the running list plus a chunk");
+
+__global__ __launch_bounds__(kSelT) void knn_select_kernel(KnnSelectArgs a) {
+  __shared__ uint64_t sd[kSelFast], so[kSelFast];
+  __shared__ int64_t si[kSelFast];
   __shared__ uint64_t rd[kMaxK], ro[kMaxK];
   __shared__ int64_t ri[kMaxK];
   __shared__ uint32_t hist[kDistBins];
-  __shared__ uint32_t wsum[kSelThreads / 64];
+  __shared__ uint32_t wsum[kSelT / 64];
   __shared__ int s_cnt, s_n, s_bin;
   __shared__ uint32_t s_S;
 
   const int tid = threadIdx.x;
+  const int lane = tid & 63, wid = tid >> 6;
   const int k = a.k;
+  constexpr int kPer = kSelFast / kSelT;  // 4
   const unsigned long long count = a.st->count;
+  const double T = a.use_state ? a.st->T : a.T;
+  double dv[kPer];
+  uint32_t iv[kPer];
+  int64_t ov[kPer];
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    const int64_t i = tid + (int64_t)j * kSelT;
+    const bool in = (unsigned long long)i < a.cap;
+    dv[j] = in ? a.cand_d[i] : 0.0;
+    iv[j] = in ? a.cand_i[i] : 0u;
+    ov[j] = in ? a.cand_o[i] : 0;
+  }
+  for (int i = tid; i < kDistBins; i += kSelT) hist[i] = 0u;
   const bool overflow = count > a.cap;
   const int64_t M = overflow ? 0 : (int64_t)count;
-  const double T = a.use_state ? a.st->T : a.T;
   int status = overflow ? 1 : 0;
   int nres = 0;
+  __syncthreads();
 
   if (!overflow) {
-    // A: stage up to kSortCap candidates in registers (all loads issued at once), then an LDS
-    //    histogram of their distances over [0, T]
-    const bool staged = M <= kSortCap;
-    constexpr int kPer = kSortCap / kSelThreads;  // 4
-    double dv[kPer];
-    uint32_t iv[kPer];
-    if (staged) {
-#pragma unroll
-      for (int j = 0; j < kPer; ++j) {
-        const int64_t i = tid + (int64_t)j * kSelThreads;
-        dv[j] = i < M ? a.cand_d[i] : 0.0;
-        iv[j] = i < M ? a.cand_i[i] : 0u;
-      }
-    }
-    for (int i = tid; i < kDistBins; i += kSelThreads) hist[i] = 0u;
-    __syncthreads();
+    const bool staged = M <= kSelFast;
     const int64_t bbase = dist_bin_base(T);
     if (staged) {
 #pragma unroll
       for (int j = 0; j < kPer; ++j)
-        if (tid + (int64_t)j * kSelThreads < M) atomicAdd(&hist[dist_bin(dv[j], bbase)], 1u);
+        if (tid + (int64_t)j * kSelT < M) atomicAdd(&hist[dist_bin(dv[j], bbase)], 1u);
     } else {
-      for (int64_t i = tid; i < M; i += kSelThreads) atomicAdd(&hist[dist_bin(a.cand_d[i], bbase)], 1u);
+      for (int64_t i = tid; i < M; i += kSelT) atomicAdd(&hist[dist_bin(a.cand_d[i], bbase)], 1u);
     }
     __syncthreads();
-    // B: bin holding the k-th candidate (4 bins per thread, block scan)
-    uint32_t v[4], s = 0;
+    // bin holding the k-th candidate: 16 bins per thread, block scan over 4 waves
+    constexpr int kB = kDistBins / kSelT;
+    uint32_t v[kB], s = 0;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) { v[j] = hist[4 * tid + j]; s += v[j]; }
-    const int lane = tid & 63, wid = tid >> 6;
+    for (int j = 0; j < kB; ++j) { v[j] = hist[kB * tid + j]; s += v[j]; }
     uint32_t inc = s;
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {
@@ -398,62 +449,68 @@ __global__ __launch_bounds__(kSelThreads) void knn_select_kernel(KnnSelectArgs a
       if (lane >= off) inc += t;
     }
     if (lane == 63) wsum[wid] = inc;
-    if (tid == 0) { s_bin = kDistBins - 1; s_S = (uint32_t)M; }
+    if (tid == 0) { s_bin = kDistBins - 1; s_S = (uint32_t)M; s_cnt = 0; }
     __syncthreads();
     uint32_t before = 0;
     for (int w = 0; w < wid; ++w) before += wsum[w];
     const uint32_t excl = before + inc - s;
     if (excl < (uint32_t)k && (uint32_t)k <= excl + s) {
       uint32_t run = excl;
-      for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < kB; ++j) {
         run += v[j];
-        if (run >= (uint32_t)k) { s_bin = 4 * tid + j; s_S = run; break; }
+        if (run >= (uint32_t)k) { s_bin = kB * tid + j; s_S = run; break; }
       }
     }
     __syncthreads();
     const int bstar = s_bin;
     bool done = false;
-    // C: fast path -- survivors (bins <= bstar) fit the LDS sort; objIDs gathered only for them
-    if (s_S <= (uint32_t)kSortCap) {
-      if (tid == 0) s_cnt = 0;
-      __syncthreads();
+    if (s_S <= (uint32_t)kSelFast) {  // fast path: survivors (bins <= bstar) fit the sort area
       if (staged) {
 #pragma unroll
         for (int j = 0; j < kPer; ++j) {
-          if (tid + (int64_t)j * kSelThreads < M && dist_bin(dv[j], bbase) <= bstar) {
+          if (tid + (int64_t)j * kSelT < M && dist_bin(dv[j], bbase) <= bstar) {
             const int pos = atomicAdd(&s_cnt, 1);
-            sd[pos] = dbits(dv[j]); si[pos] = iv[j]; so[pos] = okey(a.objID[iv[j]]);
+            sd[pos] = dbits(dv[j]); si[pos] = iv[j]; so[pos] = okey(ov[j]);
           }
         }
       } else {
-        for (int64_t i = tid; i < M; i += kSelThreads) {
+        for (int64_t i = tid; i < M; i += kSelT) {
           const double d = a.cand_d[i];
           if (dist_bin(d, bbase) <= bstar) {
             const int pos = atomicAdd(&s_cnt, 1);
-            const uint32_t ci = a.cand_i[i];
-            sd[pos] = dbits(d); si[pos] = ci; so[pos] = okey(a.objID[ci]);
+            sd[pos] = dbits(d); si[pos] = a.cand_i[i]; so[pos] = okey(a.cand_o[i]);
           }
         }
       }
       __syncthreads();
       const int cnt = s_cnt;
-      const int P = pow2ceil(cnt);
-      pad_keys(sd, so, si, cnt, P);
-      __syncthreads();
-      bitonic_sort(sd, so, si, P);
-      nres = dedupe_first_k(sd, so, si, cnt, k, rd, ro, ri, &s_n);
+      if (cnt <= 64 && k <= 64) {  // one wave, registers only
+        if (wid == 0) {
+          const bool in = lane < cnt;
+          const int r = wave_sort_dedupe(in ? sd[lane] : ~0ull, in ? so[lane] : ~0ull, in ? si[lane] : INT64_MAX, k,
+                                         rd, ro, ri);
+          if (lane == 0) s_n = r;
+        }
+        __syncthreads();
+        nres = s_n;
+      } else {
+        const int P = pow2ceil(cnt);
+        pad_keys(sd, so, si, cnt, P);
+        __syncthreads();
+        bitonic_sort(sd, so, si, P);
+        nres = dedupe_first_k(sd, so, si, cnt, k, rd, ro, ri, &s_n);
+      }
       done = (nres >= k) || (cnt == M);
     }
-    // D: general path -- every candidate, chunk by chunk, running top-k-distinct list
-    if (!done) {
+    if (!done) {  // general path: every candidate, chunk by chunk, running top-k-distinct list
       int nr = 0;
-      const int chunk = kSortCap - k;
+      const int chunk = kSelFast - k;
       for (int64_t start = 0; start < M; start += chunk) {
         const int len = (int)((M - start) < chunk ? (M - start) : chunk);
-        for (int i = tid; i < nr; i += kSelThreads) { sd[i] = rd[i]; so[i] = ro[i]; si[i] = ri[i]; }
-        for (int i = tid; i < len; i += kSelThreads) {
-          const uint32_t ci = a.cand_i[start + i];
-          sd[nr + i] = dbits(a.cand_d[start + i]); si[nr + i] = ci; so[nr + i] = okey(a.objID[ci]);
+        for (int i = tid; i < nr; i += kSelT) { sd[i] = rd[i]; so[i] = ro[i]; si[i] = ri[i]; }
+        for (int i = tid; i < len; i += kSelT) {
+          sd[nr + i] = dbits(a.cand_d[start + i]); si[nr + i] = a.cand_i[start + i];
+          so[nr + i] = okey(a.cand_o[start + i]);
         }
         const int cnt = nr + len;
         const int P = pow2ceil(cnt);
@@ -464,11 +521,11 @@ __global__ __launch_bounds__(kSelThreads) void knn_select_kernel(KnnSelectArgs a
       }
       nres = nr;
     }
-    if (nres < k && T < a.r) status = 1;  // fewer than k distinct objIDs below T: exact fallback
+    if (nres < k && T < a.r) status = 1;  // fewer than k distinct objIDs below T: re-evaluate
   }
   RecView out = rec_view(a.result, k);
   if (status == 0)
-    for (int i = tid; i < nres; i += kSelThreads) {
+    for (int i = tid; i < nres; i += kSelT) {
       out.d[i] = from_bits(rd[i]); out.o[i] = from_okey(ro[i]); out.i[i] = ri[i] + a.idx_base;
     }
   if (tid == 0) {
@@ -479,12 +536,18 @@ __global__ __launch_bounds__(kSelThreads) void knn_select_kernel(KnnSelectArgs a
     out.h->candidates = (int64_t)count;
     out.h->threshold = T;
     a.st->count = 0ull;  // ready for the next window on this stream
+    if (a.write_hint) {
+      double h = 0.0;  // 0: sample the next window
+      if (status == 0 && nres == k) h = 2.0 * from_bits(rd[k - 1]);
+      else if (status == 0) h = a.r;  // fewer than k within r: the next window scans to r as well
+      a.st->hint_T = h;
+    }
   }
 }
 
 hipError_t launch_knn_select(gf_ctx* ctx, const KnnSelectArgs& a) {
   KTimer t(ctx, GF_K_KNN_SELECT);
-  hipLaunchKernelGGL(knn_select_kernel, dim3(1), dim3(kSelThreads), 0, ctx->stream, a);
+  hipLaunchKernelGGL(knn_select_kernel, dim3(1), dim3(kSelT), 0, ctx->stream, a);
   return hipGetLastError();
 }
 

@@ -74,9 +74,8 @@ def allgather_knn_lists(objID, dist, idx, k: int, group=None):
 def allgather_knn_records(record, k: int, merged_out, group=None):
     """RCCL path: all-gather this rank's device kNN record (uint8 tensor of
     knn_record_bytes(k)) over xGMI, then merge the world's records on the device
-    (gf_knn_merge_dev) into `merged_out`.  Stream-ordered, no host sync."""
-    import ctypes as C  # noqa: F401
-
+    (gf_knn_merge_dev) into `merged_out` (a device tensor, or an int address from
+    PinnedRecords.ptr()).  Stream-ordered, no host sync."""
     import torch
     import torch.distributed as dist_
 
@@ -85,7 +84,8 @@ def allgather_knn_records(record, k: int, merged_out, group=None):
     gathered = torch.empty(world * rb, dtype=torch.uint8, device=record.device)
     dist_.all_gather_into_tensor(gathered, record, group=group)
     ctx = _lib.context(record.device.index)
-    _lib.check(_lib.lib().gf_knn_merge_dev(ctx.handle, int(k), gathered.data_ptr(), world, merged_out.data_ptr()),
+    out = merged_out if isinstance(merged_out, int) else merged_out.data_ptr()
+    _lib.check(_lib.lib().gf_knn_merge_dev(ctx.handle, int(k), gathered.data_ptr(), world, out),
                ctx.handle, "gf_knn_merge_dev")
     return merged_out
 

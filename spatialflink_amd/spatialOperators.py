@@ -242,6 +242,39 @@ def decode_knn_record(raw: bytes, k: int):
     return h.status, o[: h.n].copy(), d[: h.n].copy(), i[: h.n].copy()
 
 
+class PinnedRecords:
+    """A ring of kNN records in mapped pinned host memory (gf_pinned_alloc).  Pass
+    `ptr(i)` as the record of enqueue(): the select kernel writes the record straight into
+    host memory, so no copy kernel runs per window; read `raw(i)` after the stream syncs."""
+
+    def __init__(self, count: int, k: int):
+        self.k = int(k)
+        self.count = int(count)
+        self.bytes = knn_record_bytes(k)
+        p = C.c_void_p()
+        _lib.check(_lib.lib().gf_pinned_alloc(self.bytes * self.count, C.byref(p)), None, "gf_pinned_alloc")
+        self._base = p.value
+        self.view = np.ctypeslib.as_array((C.c_uint8 * (self.bytes * self.count)).from_address(self._base))
+        self.view[:] = 0
+
+    def ptr(self, i: int) -> int:
+        return self._base + (i % self.count) * self.bytes
+
+    def raw(self, i: int) -> bytes:
+        j = i % self.count
+        return self.view[j * self.bytes:(j + 1) * self.bytes].tobytes()
+
+    def decode(self, i: int):
+        return decode_knn_record(self.raw(i), self.k)
+
+    def __del__(self):
+        base = getattr(self, "_base", None)
+        if base and _lib._lib is not None:
+            self.view = None
+            _lib._lib.gf_pinned_free(C.c_void_p(base))
+            self._base = None
+
+
 class PointPointKNNQuery(SpatialOperator):
     """knn/PointPointKNNQuery.java -- continuous kNN of one query point within radius r."""
 
@@ -273,11 +306,13 @@ class PointPointKNNQuery(SpatialOperator):
         return KNNResult(window.start, window.end, oo[:m].copy(), od[:m].copy(), oi[:m].copy())
 
     def enqueue(self, window: PointWindow, queryPoint: Point, queryRadius: float, k: int, record):
-        """Async: evaluate the window into a device record (torch uint8 tensor of
-        knn_record_bytes(k)); pair with finish() after copying the record to the host."""
+        """Async: evaluate the window into a record -- a torch uint8 device tensor of
+        knn_record_bytes(k), or an int address from PinnedRecords.ptr() (kernel writes the
+        host record directly); pair with finish() once the record is on the host."""
         ctx, plan = self.plan(window.x.device.index, queryPoint, queryRadius, k)
         pts = window.c_struct()
-        _lib.check(_lib.lib().gf_knn_enqueue(plan, C.byref(pts), record.data_ptr()), ctx.handle, "gf_knn_enqueue")
+        addr = record if isinstance(record, int) else record.data_ptr()
+        _lib.check(_lib.lib().gf_knn_enqueue(plan, C.byref(pts), C.c_void_p(addr)), ctx.handle, "gf_knn_enqueue")
 
     def finish(self, window: PointWindow, queryPoint: Point, queryRadius: float, k: int, raw: bytes) -> KNNResult:
         ctx, plan = self.plan(window.x.device.index, queryPoint, queryRadius, k)

@@ -237,7 +237,7 @@ def test_knn_duplicate_objids_sampled(sf, oracle_mod):
     x, y = oracle_mod.java_random_points(77, N, *BEIJING)
     obj = (np.arange(N) % 997).astype(np.int64)  # each objID ~1500 times (trajectories)
     q = sf.Point("q", *QPOINT, 0, g)
-    for k in (50, 300):
+    for k in (50, 300, 512):  # 512: the largest device k, chunked general select path
         res = sf.PointPointKNNQuery(conf(sf), g).run(win(sf, x, y, obj), q, 0.5, k)
         st, oo, od, oi = oracle_mod.knn(og, x, y, obj, QPOINT[0], QPOINT[1], 0.5, k)
         check_knn(res, oo, od, oi)
@@ -394,3 +394,55 @@ def test_join_different_query_grid(sf, oracle_mod):
     st, pairs = oracle_mod.join_pp(oug, oqg, ox, oy, qx, qy, 0.02)
     exp = np.array(sorted(map(tuple, pairs.tolist())), np.int64).reshape(-1, 2)
     np.testing.assert_array_equal(got, exp)
+
+
+def test_knn_hint_across_windows(sf, oracle_mod):
+    """Continuous query: each window reuses the previous window's threshold hint.  A window
+    whose neighbourhood was emptied (hint too small) must be re-evaluated, still exactly."""
+    g = sf.UniformGrid(500, *BEIJING)
+    og = oracle_mod.grid(500, *BEIJING)
+    q = sf.Point("q", *QPOINT, 0, g)
+    op = sf.PointPointKNNQuery(conf(sf), g)
+    N = 1_100_000
+    for seed in (1, 2, 3, "hole", 4, "sparse", 5):
+        if seed == "hole":  # nothing within 0.02 of the query: the carried hint finds < k points
+            x, y = oracle_mod.java_random_points(99, N, *BEIJING)
+            far = (x - QPOINT[0]) ** 2 + (y - QPOINT[1]) ** 2 > 0.02 ** 2
+            x, y = x[far], y[far]
+        elif seed == "sparse":  # fewer than k candidates within r at all
+            x, y = oracle_mod.java_random_points(98, N, 117.3, 117.6, 40.8, 41.1)
+            x[:20] = QPOINT[0] + np.linspace(0.01, 0.4, 20)
+            y[:20] = QPOINT[1]
+        else:
+            x, y = oracle_mod.java_random_points(seed, N, *BEIJING)
+        obj = np.random.default_rng(7).permutation(len(x)).astype(np.int64)
+        res = op.run(win(sf, x, y, obj), q, 0.5, 50)
+        st, oo, od, oi = oracle_mod.knn(og, x, y, obj, QPOINT[0], QPOINT[1], 0.5, 50)
+        check_knn(res, oo, od, oi)
+
+
+def test_knn_pinned_records_async(sf, oracle_mod):
+    """Several windows enqueued back to back with the record written by the kernel straight
+    into mapped pinned host memory (no copy kernel), decoded after one sync."""
+    import torch
+
+    g = sf.UniformGrid(500, *BEIJING)
+    og = oracle_mod.grid(500, *BEIJING)
+    q = sf.Point("q", *QPOINT, 0, g)
+    op = sf.PointPointKNNQuery(conf(sf), g)
+    N, k = 1_200_000, 64
+    wins, host = [], []
+    for seed in (11, 12, 13):
+        x, y = oracle_mod.java_random_points(seed, N, *BEIJING)
+        obj = np.arange(N, dtype=np.int64) % 400_000  # duplicated objIDs: dedupe in select
+        wins.append(win(sf, x, y, obj))
+        host.append((x, y, obj))
+    rec = sf.PinnedRecords(9, k)
+    for i in range(9):
+        op.enqueue(wins[i % 3], q, 0.5, k, rec.ptr(i))
+    torch.cuda.synchronize()
+    for i in range(9):
+        x, y, obj = host[i % 3]
+        res = op.finish(wins[i % 3], q, 0.5, k, rec.raw(i))
+        st, oo, od, oi = oracle_mod.knn(og, x, y, obj, QPOINT[0], QPOINT[1], 0.5, k)
+        check_knn(res, oo, od, oi)
