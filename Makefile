@@ -24,6 +24,17 @@ $(LIB): $(OBJECTS)
 oracle:
 	$(MAKE) -s -C oracle
 
+# phase-timestamp build for tools/trace_select.py (GF_LIB_PATH selects it); never the product
+TRACE_OBJDIR := build/obj_trace
+TRACE_LIB    := build/libgeoflink_hip_trace.so
+TRACE_OBJECTS := $(patsubst $(SRC)/%,$(TRACE_OBJDIR)/%.o,$(SOURCES))
+$(TRACE_OBJDIR)/%.o: $(SRC)/% $(HEADERS)
+	@mkdir -p $(TRACE_OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -DGF_TRACE -x hip -c $< -o $@
+$(TRACE_LIB): $(TRACE_OBJECTS)
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(TRACE_OBJECTS)
+trace: $(TRACE_LIB)
+
 # gfx950 ISA listing for inspection (v_fma_f64 must not appear in the distance paths)
 isa: $(LIB)
 	/opt/rocm/lib/llvm/bin/clang-offload-bundler --list --type=o --input=$(OBJDIR)/k_knn.hip.o
@@ -32,4 +43,4 @@ clean:
 	rm -rf build $(LIB)
 	$(MAKE) -s -C oracle clean
 
-.PHONY: all oracle clean isa
+.PHONY: all oracle clean isa trace

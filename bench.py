@@ -55,6 +55,10 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--windows", type=int, default=4, help="distinct resident windows cycled through")
+    ap.add_argument("--timing-period", type=int, default=5,
+                    help="HIP events around every N-th launch of the timed kernel (fewer events, less overhead)")
+    ap.add_argument("--pipeline", type=int, default=2, choices=(1, 2),
+                    help="windows in flight: 2 overlaps window i's select with window i+1's scan")
     args = ap.parse_args()
 
     import torch
@@ -101,6 +105,8 @@ def main():
     op = sf.PointPointKNNQuery(conf, grid)
     ctx, plan = op.plan(dev.index, q, args.radius, args.k)
     _lib.check(_lib.lib().gf_knn_plan_set_index_base(plan, rank * n), ctx.handle, "index base")
+    _lib.check(_lib.lib().gf_knn_plan_set_pipeline(plan, args.pipeline), ctx.handle, "pipeline")
+    lag = args.pipeline - 1  # depth 2: window i's record is written by enqueue i+1 (or the flush)
     rb = knn_record_bytes(args.k)
     slots = torch.zeros(4, rb, dtype=torch.uint8, device=dev)
     total_steps = args.warmup + args.steps
@@ -110,35 +116,47 @@ def main():
     pts_ref = [ctypes.byref(p_) for p_ in pts]
     enqueue = L.gf_knn_enqueue
 
-    def step(i):
-        if world == 1:  # the select kernel writes the final record into pinned host memory
+    def exchange(i):  # device record of window i -> RCCL all-gather -> merge into the pinned record
+        sharding.allgather_knn_records(slots[i % 4], args.k, host.ptr(i))
+
+    def step(i, first):
+        if world == 1:  # the select writes the final record straight into pinned host memory
             st = enqueue(plan, pts_ref[i % args.windows], host.ptr(i))
             if st:
                 _lib.check(st, ctx.handle, "gf_knn_enqueue")
-        else:  # device record -> RCCL all-gather -> device merge writes the pinned host record
-            s = i % 4
-            _lib.check(enqueue(plan, pts_ref[i % args.windows], slots[s].data_ptr()), ctx.handle, "gf_knn_enqueue")
-            sharding.allgather_knn_records(slots[s], args.k, host.ptr(i))
+        else:
+            _lib.check(enqueue(plan, pts_ref[i % args.windows], slots[i % 4].data_ptr()), ctx.handle, "enqueue")
+            if i - lag >= first:  # (the previous phase's last window was exchanged by drain)
+                exchange(i - lag)
+
+    def drain(last):
+        _lib.check(L.gf_knn_plan_flush(plan), ctx.handle, "flush")
+        if world > 1 and lag:
+            exchange(last)
 
     for i in range(args.warmup):
-        step(i)
+        step(i, 0)
+    drain(args.warmup - 1)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
 
+    ctx.set_timing_period(args.timing_period)
     ctx.set_timing(1 << _lib.K_KNN_SCAN)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
     for i in range(args.warmup, total_steps):
-        step(i)
+        step(i, args.warmup)
+    drain(total_steps - 1)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     if world > 1:
         dist.barrier()
     scan_ms, scan_n = ctx.timing(_lib.K_KNN_SCAN)
     ctx.set_timing(0)
+    ctx.set_timing_period(1)
     elapsed = t1 - t0
     if world > 1:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -168,6 +186,7 @@ def main():
         ctx.set_timing(kid_all)
         for i in range(12):
             enqueue(plan, pts_ref[i % args.windows], slots[i % 4].data_ptr())
+        L.gf_knn_plan_flush(plan)
         for name, kid in (("sample", _lib.K_KNN_SAMPLE), ("scan", _lib.K_KNN_SCAN), ("select", _lib.K_KNN_SELECT)):
             ms, cnt = ctx.timing(kid)
             breakdown[tag + name + "_us"] = round(1000.0 * ms / max(cnt, 1), 2)
@@ -176,6 +195,7 @@ def main():
         t = time.perf_counter()
         for i in range(20):
             enqueue(plan, pts_ref[i % args.windows], slots[i % 4].data_ptr())
+        L.gf_knn_plan_flush(plan)
         torch.cuda.synchronize()
         breakdown[tag + "window_us"] = round(1e6 * (time.perf_counter() - t) / 20, 2)
     _lib.check(_lib.lib().gf_knn_plan_set_hint(plan, 1), ctx.handle, "hint")
@@ -213,6 +233,20 @@ def main():
                               "evaluator (string cell IDs, HashSet C/G filter, per-cell PriorityQueue, windowAll "
                               "merge), C restatement of the Java operator, 1 thread")}
 
+    traffic, traffic_src = None, None
+    if rank == 0:  # HBM bytes per launch from the committed rocprofv3 PMC pass of this command
+        import glob
+
+        kname = "knn_fused" if args.pipeline == 2 else "knn_scan"
+        for f in sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{kname}_pmc.json")), reverse=True):
+            with open(f) as fh:
+                pm = json.load(fh)
+            if pm.get("points_per_launch", n) == n and "FETCH_SIZE" in pm:
+                traffic = pm["FETCH_SIZE"]["corrected_bytes_per_launch"] + 1024.0 * pm["WRITE_SIZE"]["median_KB"]
+                traffic_src = (os.path.relpath(f, ROOT) + ": rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE passes, "
+                               "median per launch, FETCH_SIZE x2 (gfx950)")
+                break
+
     if rank == 0:
         pts_per_step = world * n
         value = pts_per_step * args.steps / elapsed
@@ -242,18 +276,21 @@ def main():
                 "grid": args.grid,
                 "query_point": list(QPOINT),
                 "parallelism": f"cell-column shards x{world}" + (" + RCCL all-gather top-k" if world > 1 else ""),
+                "windows_in_flight": args.pipeline,
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": "knn_scan",
+                "kernel": "knn_fused (scan of window i + select of window i-1 in block 0)" if args.pipeline == 2
+                else "knn_scan",
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": None,
+                "traffic": traffic,
+                "traffic_source": traffic_src,
                 "bytes_per_launch": bytes_per_launch,
                 "avg_launch_us": round(avg_scan_s * 1e6, 2),
-                "launches": scan_n,
+                "launches_timed": scan_n,
             },
             "cpu_baseline": cpu,
             "breakdown": breakdown,

@@ -100,6 +100,8 @@ int         gf_ctx_synchronize(gf_ctx* ctx);
 const char* gf_ctx_last_error(gf_ctx* ctx);
 /* Record HIP events around launches of the kernels in `mask` (bit 1 << GF_K_*; 0 = off). */
 int         gf_ctx_set_timing(gf_ctx* ctx, int mask);
+/* Time only every period-th launch of each kernel (fewer events in a hot loop); default 1. */
+int         gf_ctx_set_timing_period(gf_ctx* ctx, int period);
 /* Sync, then return the summed kernel time (ms) and launch count for kernel_id; resets it. */
 int         gf_ctx_timing(gf_ctx* ctx, int kernel_id, double* total_ms, int64_t* launches);
 
@@ -162,6 +164,16 @@ int    gf_knn_plan_set_tuning(gf_knn_plan* plan, int32_t scan_blocks, int32_t un
 int    gf_knn_plan_set_hint(gf_knn_plan* plan, int enable);
 /* Offset added to the window-local point index in results (a shard's first global index). */
 int    gf_knn_plan_set_index_base(gf_knn_plan* plan, int64_t base);
+/* Continuous-query pipeline.  depth 1 (default): each enqueue runs sample -> scan -> select,
+ * stream-ordered.  depth 2 (k <= 256): ONE fused launch per window -- blocks 1.. scan window i
+ * with the threshold hint left by window i-2 (two device lanes), block 0 runs window i-1's
+ * select meanwhile.  Window i's record is therefore written by the NEXT enqueue on the plan,
+ * or by gf_knn_plan_flush (stream-ordered on the context stream).  No sample kernel: a cold
+ * or failed hint flags the window (status 1, re-evaluated exactly by gf_knn_decode) and the
+ * threshold adapts (shrinks after an overflow, doubles when fewer than k lie below it).
+ * Results are identical at either depth. */
+int    gf_knn_plan_set_pipeline(gf_knn_plan* plan, int depth);
+int    gf_knn_plan_flush(gf_knn_plan* plan);
 /* Result record: gf_knn_header followed by double dist[k], int64 objID[k], int64 idx[k]. */
 typedef struct {
   int32_t status;        /* 0 = final; 1 = needs the exact fallback (see gf_knn_decode) */
@@ -182,8 +194,9 @@ int    gf_knn_decode(gf_knn_plan* plan, const gf_points* pts, const void* result
 /* Sync convenience: enqueue + copy + decode. */
 int    gf_knn_run(gf_knn_plan* plan, const gf_points* pts, int64_t* objID, double* dist,
                   int64_t* idx, int32_t* n_out);
-/* Merge per-shard top-k records (device, `nrec` contiguous records of gf_knn_result_bytes(k))
- * into one record (async) -- the windowAll funnel across GPUs after an RCCL all-gather. */
+/* Merge per-shard top-k records (device, `nrec` <= 64 contiguous records of
+ * gf_knn_result_bytes(k)) into one record (async) -- the windowAll funnel across GPUs after
+ * an RCCL all-gather.  `result` may be device memory or gf_pinned_alloc memory. */
 int    gf_knn_merge_dev(gf_ctx* ctx, int32_t k, const void* records, int32_t nrec, void* result);
 /* Host merge of per-shard sorted lists: top-k distinct objIDs by (dist, objID). */
 int    gf_knn_merge_host(int32_t k, int32_t nlists, const int32_t* counts, const int64_t* objID,

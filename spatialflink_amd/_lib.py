@@ -11,7 +11,7 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libgeoflink_hip.so")
+LIB_PATH = os.environ.get("GF_LIB_PATH") or os.path.join(_HERE, "libgeoflink_hip.so")
 
 GF_OK = 0
 GF_ERR_ARG = -1
@@ -29,11 +29,12 @@ K_KNN_SCAN, K_KNN_SAMPLE, K_KNN_SELECT, K_RANGE_SCAN, K_ASSIGN, K_JOIN_PROBE = r
 # Every symbol include/geoflink_hip.h declares (checked by tests/test_abi.py).
 EXPORTS = [
     "gf_abi_version", "gf_status_string", "gf_device_count", "gf_ctx_create", "gf_ctx_destroy",
-    "gf_ctx_set_stream", "gf_ctx_stream", "gf_ctx_synchronize", "gf_ctx_last_error", "gf_ctx_set_timing",
+    "gf_ctx_set_stream", "gf_ctx_stream", "gf_ctx_synchronize", "gf_ctx_last_error", "gf_ctx_set_timing", "gf_ctx_set_timing_period",
     "gf_ctx_timing", "gf_grid_make", "gf_grid_layers", "gf_cell_of", "gf_format_cell_id", "gf_parse_cell_id",
     "gf_assign_cells", "gf_bucket_by_cell", "gf_range_pp_plan_create", "gf_range_ppoly_plan_create",
     "gf_range_plan_destroy", "gf_range_run", "gf_bitmap_to_indices", "gf_knn_pp_plan_create",
-    "gf_knn_plan_destroy", "gf_knn_plan_set_capacity", "gf_knn_plan_set_index_base", "gf_knn_plan_set_tuning", "gf_knn_plan_set_hint", "gf_knn_result_bytes", "gf_knn_enqueue",
+    "gf_knn_plan_destroy", "gf_knn_plan_set_capacity", "gf_knn_plan_set_index_base", "gf_knn_plan_set_tuning", "gf_knn_plan_set_hint", "gf_knn_plan_set_pipeline", "gf_knn_plan_flush",
+    "gf_knn_result_bytes", "gf_knn_enqueue",
     "gf_knn_decode", "gf_knn_run", "gf_knn_merge_dev", "gf_knn_merge_host", "gf_join_pp", "gf_window_create",
     "gf_window_destroy", "gf_window_upload", "gf_window_points", "gf_synth_uniform", "gf_pinned_alloc",
     "gf_pinned_free",
@@ -101,6 +102,7 @@ def lib():
             "gf_ctx_synchronize": ([P], C.c_int),
             "gf_ctx_last_error": ([P], C.c_char_p),
             "gf_ctx_set_timing": ([P, C.c_int], C.c_int),
+            "gf_ctx_set_timing_period": ([P, C.c_int], C.c_int),
             "gf_ctx_timing": ([P, C.c_int, pd, pi64], C.c_int),
             "gf_grid_make": ([i32, d, d, d, d, C.POINTER(GfGrid)], C.c_int),
             "gf_grid_layers": ([C.POINTER(GfGrid), d, pi32, pi32], C.c_int),
@@ -121,6 +123,8 @@ def lib():
             "gf_knn_plan_set_index_base": ([P, i64], C.c_int),
             "gf_knn_plan_set_tuning": ([P, i32, i32, i32], C.c_int),
             "gf_knn_plan_set_hint": ([P, C.c_int], C.c_int),
+            "gf_knn_plan_set_pipeline": ([P, C.c_int], C.c_int),
+            "gf_knn_plan_flush": ([P], C.c_int),
             "gf_knn_result_bytes": ([i32], sz),
             "gf_knn_enqueue": ([P, C.POINTER(GfPoints), P], C.c_int),
             "gf_knn_decode": ([P, C.POINTER(GfPoints), P, P, P, P, pi32], C.c_int),
@@ -192,6 +196,9 @@ class Context:
     def set_timing(self, mask: int):
         """mask: bitmask of (1 << K_*) kernels whose launches are bracketed by HIP events."""
         check(lib().gf_ctx_set_timing(self.handle, int(mask)), self.handle, "set_timing")
+
+    def set_timing_period(self, period: int):
+        check(lib().gf_ctx_set_timing_period(self.handle, int(period)), self.handle, "set_timing_period")
 
     def timing(self, kernel_id: int):
         ms, n = C.c_double(), C.c_int64()

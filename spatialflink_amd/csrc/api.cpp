@@ -78,6 +78,7 @@ static hipEvent_t take_event(gf_ctx* ctx) {
 
 KTimer::KTimer(gf_ctx* c, int k) : ctx(c), kid(k) {
   if (!(ctx->timing & (1 << k))) return;
+  if (ctx->timing_period > 1 && (ctx->timing_seq[k]++ % ctx->timing_period) != 0) return;
   a = take_event(ctx);
   b = take_event(ctx);
   hipEventRecord(a, ctx->stream);
@@ -262,6 +263,13 @@ extern "C" const char* gf_ctx_last_error(gf_ctx* ctx) { return ctx ? ctx->last_e
 extern "C" int gf_ctx_set_timing(gf_ctx* ctx, int mask) {
   if (!ctx) return GF_ERR_ARG;
   ctx->timing = mask;
+  return GF_OK;
+}
+
+extern "C" int gf_ctx_set_timing_period(gf_ctx* ctx, int period) {
+  if (!ctx || period < 1) return GF_ERR_ARG;
+  ctx->timing_period = period;
+  for (int64_t& v : ctx->timing_seq) v = 0;
   return GF_OK;
 }
 
@@ -684,26 +692,40 @@ extern "C" void gf_knn_plan_destroy(gf_knn_plan* P) {
   if (!P) return;
   hipSetDevice(P->ctx->device);
   hipStreamSynchronize(P->ctx->stream);
-  if (P->st) hipFree(P->st);
-  if (P->cand_d) hipFree(P->cand_d);
-  if (P->cand_i) hipFree(P->cand_i);
-  if (P->cand_o) hipFree(P->cand_o);
+  for (auto& L : P->lane) {
+    if (L.st) hipFree(L.st);
+    if (L.cand_d) hipFree(L.cand_d);
+    if (L.cand_i) hipFree(L.cand_i);
+    if (L.cand_o) hipFree(L.cand_o);
+  }
   if (P->tmp_result) hipFree(P->tmp_result);
   if (P->host_result) hipHostFree(P->host_result);
   delete P;
 }
 
-static int knn_alloc_candidates(gf_knn_plan* P, int64_t cap) {
+static int knn_alloc_lane(gf_knn_plan* P, int j, int64_t cap) {
   gf_ctx* ctx = P->ctx;
-  if (P->cand_d) hipFree(P->cand_d);
-  if (P->cand_i) hipFree(P->cand_i);
-  if (P->cand_o) hipFree(P->cand_o);
-  P->cand_d = nullptr;
-  P->cand_i = nullptr;
-  P->cand_o = nullptr;
-  GF_HIP_CHECK(ctx, hipMalloc(&P->cand_d, sizeof(double) * (size_t)cap));
-  GF_HIP_CHECK(ctx, hipMalloc(&P->cand_i, sizeof(uint32_t) * (size_t)cap));
-  GF_HIP_CHECK(ctx, hipMalloc(&P->cand_o, sizeof(int64_t) * (size_t)cap));
+  gf_knn_plan::Lane& L = P->lane[j];
+  if (!L.st) {
+    GF_HIP_CHECK(ctx, hipMalloc(&L.st, sizeof(KnnState)));
+    GF_HIP_CHECK(ctx, hipMemset(L.st, 0, sizeof(KnnState)));
+  }
+  if (L.cand_d) hipFree(L.cand_d);
+  if (L.cand_i) hipFree(L.cand_i);
+  if (L.cand_o) hipFree(L.cand_o);
+  L.cand_d = nullptr;
+  L.cand_i = nullptr;
+  L.cand_o = nullptr;
+  GF_HIP_CHECK(ctx, hipMalloc(&L.cand_d, sizeof(double) * (size_t)cap));
+  GF_HIP_CHECK(ctx, hipMalloc(&L.cand_i, sizeof(uint32_t) * (size_t)cap));
+  GF_HIP_CHECK(ctx, hipMalloc(&L.cand_o, sizeof(int64_t) * (size_t)cap));
+  return GF_OK;
+}
+
+static int knn_alloc_candidates(gf_knn_plan* P, int64_t cap) {
+  int st;
+  for (int j = 0; j < 2; ++j)  // lane 1 only once pipelining allocated it
+    if ((j == 0 || P->lane[j].st) && (st = knn_alloc_lane(P, j, cap))) return st;
   P->cap = cap;
   return GF_OK;
 }
@@ -724,8 +746,6 @@ extern "C" int gf_knn_pp_plan_create(gf_ctx* ctx, const gf_grid* g, double qx, d
   P->qr = make_qrect(*g, qcx, qcy, gl, cl);  // PointPointKNNQuery.java:134-135
   auto fail = [&](int s) { gf_knn_plan_destroy(P); return s; };
   hipError_t e;
-  if ((e = hipMalloc(&P->st, sizeof(KnnState))) != hipSuccess) return fail(hip_err(ctx, e, "hipMalloc(KnnState)"));
-  if ((e = hipMemset(P->st, 0, sizeof(KnnState))) != hipSuccess) return fail(hip_err(ctx, e, "hipMemset"));
   if ((st = knn_alloc_candidates(P, (int64_t)1 << 20))) return fail(st);
   if ((e = hipMalloc(&P->tmp_result, gf_knn_result_bytes(k))) != hipSuccess) return fail(hip_err(ctx, e, "hipMalloc"));
   if ((e = hipHostMalloc(&P->host_result, gf_knn_result_bytes(k), hipHostMallocDefault)) != hipSuccess)
@@ -739,6 +759,8 @@ extern "C" int gf_knn_plan_set_capacity(gf_knn_plan* P, int64_t cap) {
   if (!P || cap < 2 || cap > (int64_t)1 << 31) return GF_ERR_ARG;
   int st = bind(P->ctx);
   if (st) return st;
+  int fs = gf_knn_plan_flush(P);
+  if (fs) return fs;
   hipStreamSynchronize(P->ctx->stream);
   return knn_alloc_candidates(P, cap & ~(int64_t)1);
 }
@@ -757,34 +779,50 @@ extern "C" int gf_knn_plan_set_index_base(gf_knn_plan* P, int64_t base) {
   return GF_OK;
 }
 
-static int knn_scan_select(gf_knn_plan* P, const gf_points* pts, int64_t begin, int64_t end, int use_state,
-                           int write_hint, void* result) {
-  gf_ctx* ctx = P->ctx;
+static int scan_blocks_for(gf_knn_plan* P, int64_t n) {
+  int blocks = P->scan_blocks;
+  if (blocks <= 0) {  // 4 blocks per CU measured best for the 1-pair nontemporal loop
+    blocks = stream_blocks(P->ctx, (n + 1) / 2);
+    blocks = std::min(blocks, P->ctx->num_cus * 4);
+  }
+  return blocks;
+}
+
+static KnnScanArgs scan_args(gf_knn_plan* P, int j, const gf_points* pts, int64_t begin, int64_t end, int use_state) {
+  const gf_knn_plan::Lane& L = P->lane[j];
   KnnScanArgs s{};
   s.x = pts->x; s.y = pts->y; s.objID = pts->objID; s.begin = begin; s.end = end;
   s.qx = P->qx; s.qy = P->qy; s.qr = P->qr;
   s.T = P->r; s.s_pre = s_prefilter(P->r, P->metric);
-  s.use_state = use_state; s.metric = P->metric; s.st = P->st;
-  s.cand_d = P->cand_d; s.cand_i = P->cand_i; s.cand_o = P->cand_o; s.cap = (unsigned long long)P->cap;
-  int blocks = P->scan_blocks;
-  if (blocks <= 0) {  // 4 blocks per CU measured best for the 1-pair nontemporal loop
-    blocks = stream_blocks(ctx, ((end - begin) + 1) / 2);
-    blocks = std::min(blocks, ctx->num_cus * 4);
-  }
-  GF_HIP_CHECK(ctx, launch_knn_scan(ctx, s, blocks, P->scan_unroll, P->scan_nt));
+  s.use_state = use_state; s.metric = P->metric; s.st = L.st;
+  s.cand_d = L.cand_d; s.cand_i = L.cand_i; s.cand_o = L.cand_o; s.cap = (unsigned long long)P->cap;
+  return s;
+}
+
+static KnnSelectArgs select_args(gf_knn_plan* P, int j, int use_state, int write_hint, void* result) {
+  const gf_knn_plan::Lane& L = P->lane[j];
   KnnSelectArgs q{};
-  q.st = P->st; q.cand_d = P->cand_d; q.cand_i = P->cand_i; q.cand_o = P->cand_o;
+  q.st = L.st; q.cand_d = L.cand_d; q.cand_i = L.cand_i; q.cand_o = L.cand_o;
   q.cap = (unsigned long long)P->cap;
   q.use_state = use_state; q.T = P->r; q.r = P->r; q.k = P->k; q.result = result;
   q.write_hint = write_hint; q.idx_base = P->idx_base;
-  GF_HIP_CHECK(ctx, launch_knn_select(ctx, q));
+  return q;
+}
+
+// scan + select of points [begin, end) on lane j, stream-ordered
+static int knn_scan_select(gf_knn_plan* P, int j, const gf_points* pts, int64_t begin, int64_t end, int use_state,
+                           int write_hint, void* result) {
+  gf_ctx* ctx = P->ctx;
+  const KnnScanArgs s = scan_args(P, j, pts, begin, end, use_state);
+  GF_HIP_CHECK(ctx, launch_knn_scan(ctx, s, scan_blocks_for(P, end - begin), P->scan_unroll, P->scan_nt));
+  GF_HIP_CHECK(ctx, launch_knn_select(ctx, select_args(P, j, use_state, write_hint, result)));
   return GF_OK;
 }
 
-static int knn_launch_sample(gf_knn_plan* P, const gf_points* pts, int use_hint) {
+static int knn_launch_sample(gf_knn_plan* P, int j, const gf_points* pts, int use_hint) {
   KnnSampleArgs s{};
   s.x = pts->x; s.y = pts->y; s.n = pts->n; s.qx = P->qx; s.qy = P->qy; s.qr = P->qr;
-  s.r = P->r; s.s_r = s_prefilter(P->r, P->metric); s.k = P->k; s.metric = P->metric; s.st = P->st;
+  s.r = P->r; s.s_r = s_prefilter(P->r, P->metric); s.k = P->k; s.metric = P->metric; s.st = P->lane[j].st;
   s.use_hint = use_hint;
   GF_HIP_CHECK(P->ctx, launch_knn_sample(P->ctx, s));
   return GF_OK;
@@ -797,10 +835,55 @@ extern "C" int gf_knn_enqueue(gf_knn_plan* P, const gf_points* pts, void* result
   if (st) return st;
   if ((st = check_points(ctx, pts))) return st;
   if (pts->n > 0 && !pts->objID) return set_err(ctx, GF_ERR_ARG, "kNN needs objID");
-  // threshold: previous window's hint (continuous query) or the sample; tiny windows scan to r
+  if (P->pipeline == 2) {
+    // one fused launch: scan this window on lane j (threshold = the lane's hint), select the
+    // pending previous window on the other lane in block 0
+    const int j = (int)(P->seq++ & 1);
+    // a lane's first window (or hints off): sample the threshold instead of guessing r
+    const bool sample = pts->n >= kSampleMinN && (!P->use_hint || !P->lane_warm[j]);
+    if (sample && (st = knn_launch_sample(P, j, pts, 0))) return st;
+    P->lane_warm[j] = 1;
+    const KnnScanArgs s = scan_args(P, j, pts, 0, pts->n, sample ? 2 : 1);
+    KnnSelectArgs q{};
+    const int has_prev = P->pend_lane >= 0;
+    if (has_prev) q = select_args(P, P->pend_lane, 1, P->use_hint, P->pend_result);
+    GF_HIP_CHECK(ctx, launch_knn_fused(ctx, s, q, has_prev, scan_blocks_for(P, pts->n), P->scan_nt));
+    P->pend_lane = j;
+    P->pend_result = result;
+    return GF_OK;
+  }
+  // threshold: the previous window's hint (continuous query) or the sample; tiny windows
+  // scan to r
   const bool staged = pts->n >= kSampleMinN;
-  if (staged && (st = knn_launch_sample(P, pts, P->use_hint))) return st;
-  return knn_scan_select(P, pts, 0, pts->n, staged ? 1 : 0, staged && P->use_hint, result);
+  if (staged && (st = knn_launch_sample(P, 0, pts, P->use_hint))) return st;
+  return knn_scan_select(P, 0, pts, 0, pts->n, staged ? 1 : 0, staged && P->use_hint, result);
+}
+
+extern "C" int gf_knn_plan_flush(gf_knn_plan* P) {
+  if (!P) return GF_ERR_ARG;
+  if (P->pend_lane < 0) return GF_OK;
+  gf_ctx* ctx = P->ctx;
+  int st = bind(ctx);
+  if (st) return st;
+  GF_HIP_CHECK(ctx, launch_knn_select(ctx, select_args(P, P->pend_lane, 1, P->use_hint, P->pend_result)));
+  P->pend_lane = -1;
+  P->pend_result = nullptr;
+  return GF_OK;
+}
+
+extern "C" int gf_knn_plan_set_pipeline(gf_knn_plan* P, int depth) {
+  if (!P || depth < 1 || depth > 2) return GF_ERR_ARG;
+  gf_ctx* ctx = P->ctx;
+  if (depth == 2 && P->k > 256)
+    return set_err(ctx, GF_ERR_ARG, "gf_knn_plan_set_pipeline: depth 2 needs k <= 256");
+  int st = bind(ctx);
+  if (st || (st = gf_knn_plan_flush(P))) return st;
+  GF_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+  if (depth == 2 && !P->lane[1].st && (st = knn_alloc_lane(P, 1, P->cap))) return st;
+  P->pipeline = depth;
+  P->seq = 0;
+  P->lane_warm[0] = P->lane_warm[1] = 0;
+  return GF_OK;
 }
 
 extern "C" int gf_knn_plan_set_hint(gf_knn_plan* P, int enable) {
@@ -808,8 +891,11 @@ extern "C" int gf_knn_plan_set_hint(gf_knn_plan* P, int enable) {
   int st = bind(P->ctx);
   if (st) return st;
   P->use_hint = enable != 0;
+  if ((st = gf_knn_plan_flush(P))) return st;
   GF_HIP_CHECK(P->ctx, hipStreamSynchronize(P->ctx->stream));
-  GF_HIP_CHECK(P->ctx, hipMemset(&P->st->hint_T, 0, sizeof(double)));
+  for (auto& L : P->lane)
+    if (L.st) GF_HIP_CHECK(P->ctx, hipMemset(&L.st->hint_T, 0, sizeof(double)));
+  P->lane_warm[0] = P->lane_warm[1] = 0;
   return GF_OK;
 }
 
@@ -858,10 +944,11 @@ static int knn_fallback(gf_knn_plan* P, const gf_points* pts, int64_t* oo, doubl
     GF_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
     return GF_OK;
   };
-  int st;
+  int st = gf_knn_plan_flush(P);  // lane 0 is free afterwards
+  if (st) return st;
   if (pts->n >= kSampleMinN) {
-    if ((st = knn_launch_sample(P, pts, 0)) || (st = knn_scan_select(P, pts, 0, pts->n, 1, P->use_hint, P->tmp_result)) ||
-        (st = fetch()))
+    if ((st = knn_launch_sample(P, 0, pts, 0)) ||
+        (st = knn_scan_select(P, 0, pts, 0, pts->n, 1, P->use_hint, P->tmp_result)) || (st = fetch()))
       return st;
     if (h->status == 0) return gf_knn_decode(P, pts, P->host_result, oo, od, oi, n_out);
   }
@@ -869,7 +956,7 @@ static int knn_fallback(gf_knn_plan* P, const gf_points* pts, int64_t* oo, doubl
   std::vector<Ent> all;
   for (int64_t lo = 0; lo < pts->n; lo += part) {
     const int64_t hi = std::min(pts->n, lo + part);
-    if ((st = knn_scan_select(P, pts, lo, hi, 0, 0, P->tmp_result)) || (st = fetch())) return st;
+    if ((st = knn_scan_select(P, 0, pts, lo, hi, 0, 0, P->tmp_result)) || (st = fetch())) return st;
     if (h->status != 0) return set_err(ctx, GF_ERR_HIP, "kNN partition did not converge");
     const double* d = (const double*)(h + 1);
     const int64_t* o = (const int64_t*)(d + P->k);
@@ -907,7 +994,7 @@ extern "C" int gf_knn_run(gf_knn_plan* P, const gf_points* pts, int64_t* oo, dou
   if (!P || !n_out) return GF_ERR_ARG;
   gf_ctx* ctx = P->ctx;
   int st = gf_knn_enqueue(P, pts, P->tmp_result);
-  if (st) return st;
+  if (st || (st = gf_knn_plan_flush(P))) return st;
   GF_HIP_CHECK(ctx, hipMemcpyAsync(P->host_result, P->tmp_result, gf_knn_result_bytes(P->k), hipMemcpyDeviceToHost,
                                    ctx->stream));
   GF_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
@@ -915,8 +1002,8 @@ extern "C" int gf_knn_run(gf_knn_plan* P, const gf_points* pts, int64_t* oo, dou
 }
 
 extern "C" int gf_knn_merge_dev(gf_ctx* ctx, int32_t k, const void* records, int32_t nrec, void* result) {
-  if (!ctx || k < 1 || k > kMaxK || nrec < 1 || nrec > 64 || (int64_t)nrec * k > kSortCap || !records || !result)
-    return set_err(ctx, GF_ERR_ARG, "gf_knn_merge_dev: need 1 <= nrec <= 64 and nrec*k <= 4096");
+  if (!ctx || k < 1 || k > kMaxK || nrec < 1 || nrec > 64 || !records || !result)
+    return set_err(ctx, GF_ERR_ARG, "gf_knn_merge_dev: need 1 <= nrec <= 64 and 1 <= k <= 512");
   int st = bind(ctx);
   if (st) return st;
   GF_HIP_CHECK(ctx, launch_knn_merge(ctx, k, records, nrec, result));

@@ -19,6 +19,8 @@ struct gf_ctx {
   hipStream_t own_stream = nullptr;
   std::string last_error;
   int timing = 0;  // bitmask of GF_K_* kernels to time
+  int timing_period = 1;              // time every period-th launch of each kernel
+  int64_t timing_seq[GF_K_COUNT] = {};
   struct Ev { hipEvent_t a, b; int kid; };
   std::vector<Ev> pending;
   std::vector<hipEvent_t> pool;
@@ -59,7 +61,6 @@ struct KTimer {
 // kernel argument blocks
 // ---------------------------------------------------------------------------------------
 constexpr int kBlock = 256;         // streaming kernels: 4 waves
-constexpr int kSortCap = 4096;      // select kernel: LDS sort capacity
 constexpr int kMaxK = 512;          // largest k on the device path
 constexpr int kSampleBlocks = 128;  // kNN sample: 128 blocks x 2048 points = 256K points
 constexpr int kSamplePerBlock = 2048;
@@ -82,6 +83,7 @@ struct KnnState {
   double s_pre;      // prefilter bound on dx*dx+dy*dy for T
   unsigned long long count;  // candidates appended (may exceed capacity)
   double hint_T;     // next window's threshold guess (2 x this window's k-th distance); 0 = none
+  unsigned long long tr[4];  // GF_TRACE builds only: sample start, scan first start / last end
 };
 
 struct KnnScanArgs {
@@ -180,6 +182,8 @@ hipError_t launch_expand_bitmap(hipStream_t s, const uint64_t* bitmap, int64_t w
 hipError_t launch_knn_sample(gf_ctx* ctx, const KnnSampleArgs& a);
 hipError_t launch_knn_scan(gf_ctx* ctx, const KnnScanArgs& a, int blocks, int unroll, int nt);
 hipError_t launch_knn_select(gf_ctx* ctx, const KnnSelectArgs& a);
+hipError_t launch_knn_fused(gf_ctx* ctx, const KnnScanArgs& a, const KnnSelectArgs& prev, int has_prev,
+                            int scan_blocks, int nt);
 hipError_t launch_knn_merge(gf_ctx* ctx, int32_t k, const void* records, int32_t nrec, void* result);
 
 hipError_t launch_range(gf_ctx* ctx, const RangeArgs& a, int table_mode, int poly, int blocks);
@@ -249,11 +253,21 @@ struct gf_knn_plan {
   int32_t k = 0;
   int metric = 0;
   gf::QueryRect qr{};
-  gf::KnnState* st = nullptr;
-  double* cand_d = nullptr;
-  uint32_t* cand_i = nullptr;
-  int64_t* cand_o = nullptr;
+  // a lane = device state + candidate buffers of one in-flight window.  Lane 1 exists only
+  // at pipeline depth 2 (gf_knn_plan_set_pipeline): window i uses lane i % 2, and its select
+  // runs inside window i+1's fused scan kernel (or at gf_knn_plan_flush).
+  struct Lane {
+    gf::KnnState* st = nullptr;
+    double* cand_d = nullptr;
+    uint32_t* cand_i = nullptr;
+    int64_t* cand_o = nullptr;
+  } lane[2];
   int64_t cap = 0;
+  int pipeline = 1;               // 1: sample -> scan -> select per window; 2: fused
+  uint64_t seq = 0;
+  int pend_lane = -1;             // depth 2: the window whose select has not run yet
+  int lane_warm[2] = {0, 0};      // depth 2: the lane has a hint from an earlier window
+  void* pend_result = nullptr;
   int use_hint = 1;             // reuse the previous window's k-th distance as the threshold guess
   int64_t idx_base = 0;
   void* tmp_result = nullptr;   // device record used by gf_knn_run / fallback

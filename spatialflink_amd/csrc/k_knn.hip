@@ -72,6 +72,9 @@ __global__ __launch_bounds__(kBlock) void knn_sample_kernel(KnnSampleArgs a) {
   __shared__ uint32_t lh[kDistBins];
   __shared__ uint32_t wsum[kBlock / 64];
   __shared__ int s_last, s_bin;
+#ifdef GF_TRACE
+  if (blockIdx.x == 0 && threadIdx.x == 0) a.st->tr[0] = wall_clock64();
+#endif
   if (a.use_hint) {
     const double h = a.st->hint_T;
     if (h > 0.0) {  // continuous query: the previous window's guess; nothing to sample
@@ -221,19 +224,20 @@ __device__ __forceinline__ void knn_scan_tile(const KnnScanArgs& a, const dbl2 (
 
 // Main loop: every wave runs the same number of full U-pair tiles with no bounds checks (loads
 // issued back to back from bumped pointers, counted waits); the remainder goes through a
-// checked one-pair-per-lane tail.
+// checked one-pair-per-lane tail.  `bid` / `nblk`: this block's index among the scanning blocks.
 template <int METRIC, int U, int NT>
-__global__ __launch_bounds__(kBlock) void knn_scan_kernel(KnnScanArgs a) {
+__device__ __forceinline__ void knn_scan_body(const KnnScanArgs& a, double sp, double T, int64_t bid, int64_t nblk) {
   const int lane = threadIdx.x & 63;
-  const int64_t wstride = (int64_t)gridDim.x * kBlock;
+  const int64_t wstride = nblk * kBlock;
   const int64_t pbeg = a.begin >> 1;
   const int64_t npf = (a.end - a.begin) >> 1;  // complete pairs
   const int64_t iters = npf / (U * wstride);    // full tiles for every wave
-  const int64_t off = (int64_t)blockIdx.x * kBlock + (threadIdx.x & ~63) + lane;
-  const double sp = a.use_state ? a.st->s_pre : a.s_pre;
-  const double T = a.use_state ? a.st->T : a.T;
+  const int64_t off = bid * kBlock + (threadIdx.x & ~63) + lane;
   const dbl2* px = reinterpret_cast<const dbl2*>(a.x) + pbeg + off;
   const dbl2* py = reinterpret_cast<const dbl2*>(a.y) + pbeg + off;
+#ifdef GF_TRACE
+  if (threadIdx.x == 0) atomicMin(&a.st->tr[1], (unsigned long long)wall_clock64());
+#endif
   for (int64_t it = 0; it < iters; ++it) {
     dbl2 xv[U], yv[U];
 #pragma unroll
@@ -258,6 +262,17 @@ __global__ __launch_bounds__(kBlock) void knn_scan_kernel(KnnScanArgs a) {
     }
     knn_scan_tile<METRIC, 1>(a, xv, yv, p, wstride, sp, T);
   }
+#ifdef GF_TRACE
+  __syncthreads();
+  if (threadIdx.x == 0) atomicMax(&a.st->tr[2], (unsigned long long)wall_clock64());
+#endif
+}
+
+template <int METRIC, int U, int NT>
+__global__ __launch_bounds__(kBlock) void knn_scan_kernel(KnnScanArgs a) {
+  const double sp = a.use_state ? a.st->s_pre : a.s_pre;
+  const double T = a.use_state ? a.st->T : a.T;
+  knn_scan_body<METRIC, U, NT>(a, sp, T, blockIdx.x, gridDim.x);
 }
 
 template <int METRIC>
@@ -280,85 +295,65 @@ hipError_t launch_knn_scan(gf_ctx* ctx, const KnnScanArgs& a, int blocks, int un
 }
 
 // ---------------------------------------------------------------------------------------
-// select / merge: sort on (d bits, objID key, idx) then objID dedupe
+// select / merge: one 256-thread block (4 waves).  Keys (d bits, objID key, idx): d >= 0 so
+// its IEEE bits order like the values; idx is unique, so keys never tie.
+// Two LDS layouts share the code: SelFull (standalone select / merge kernels: 1024-key sort
+// area, chunked general path) and SelLite (28 KB, block 0 of the fused scan kernel, which
+// must leave room for 4 scanning blocks per CU).  The histogram is dead once the survivors
+// are compacted, so it shares storage with the merge runs and the dedupe hash table.
 // ---------------------------------------------------------------------------------------
-constexpr int kSelThreads = 1024;
+constexpr int kSelT = 256;
+static_assert(kSelT == kBlock, "the fused kernel's select block is a scan-sized block");
 
-__device__ __forceinline__ bool key_gt(const uint64_t* sd, const uint64_t* so, const int64_t* si, int i, int j) {
-  if (sd[i] != sd[j]) return sd[i] > sd[j];
-  if (so[i] != so[j]) return so[i] > so[j];
-  return si[i] > si[j];
-}
+struct SelFull {
+  static constexpr int kCap = 1024, kHBits = 11, kK = kMaxK;
+  uint64_t sd[kCap], so[kCap];
+  int64_t si[kCap];
+  uint64_t rd[kK], ro[kK];  // running / final top-k-distinct list
+  int64_t ri[kK];
+  union {
+    uint32_t hist[kDistBins];
+    struct {
+      uint64_t rund[kSelT], runo[kSelT];
+      int64_t runi[kSelT];
+      uint64_t hkey[1 << kHBits];
+      uint32_t hpos[1 << kHBits];
+    };
+  };
+  uint32_t wsum[kSelT / 64];
+  int s_cnt, s_bin, s_maxpos;
+  uint32_t s_S;
+};
+struct SelLite {
+  static constexpr int kCap = 256, kHBits = 9, kK = 256;
+  uint64_t sd[kCap], so[kCap];
+  int64_t si[kCap];
+  uint64_t rd[kK], ro[kK];
+  int64_t ri[kK];
+  union {
+    uint32_t hist[kDistBins];
+    struct {
+      uint64_t rund[kSelT], runo[kSelT];
+      int64_t runi[kSelT];
+      uint64_t hkey[1 << kHBits];
+      uint32_t hpos[1 << kHBits];
+    };
+  };
+  uint32_t wsum[kSelT / 64];
+  int s_cnt, s_bin, s_maxpos;
+  uint32_t s_S;
+};
+static_assert(SelFull::kCap > kMaxK, "the general path needs room for the running list plus a chunk");
+static_assert(sizeof(SelLite) <= 29 * 1024, "fused kernel: 5 blocks per CU must fit the LDS");
 
-__device__ void bitonic_sort(uint64_t* sd, uint64_t* so, int64_t* si, int P) {
-  for (int size = 2; size <= P; size <<= 1) {
-    for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      for (int t = threadIdx.x; t < (P >> 1); t += blockDim.x) {
-        const int i = 2 * stride * (t / stride) + (t & (stride - 1));
-        const int j = i + stride;
-        const bool up = (i & size) == 0;
-        if (key_gt(sd, so, si, i, j) == up) {
-          uint64_t td = sd[i]; sd[i] = sd[j]; sd[j] = td;
-          uint64_t to = so[i]; so[i] = so[j]; so[j] = to;
-          int64_t ti = si[i]; si[i] = si[j]; si[j] = ti;
-        }
-      }
-      __syncthreads();
-    }
-  }
-}
-
-__device__ __forceinline__ int pow2ceil(int v) {
-  int p = 2;
-  while (p < v) p <<= 1;
-  return p;
-}
-
-__device__ void pad_keys(uint64_t* sd, uint64_t* so, int64_t* si, int cnt, int P) {
-  for (int i = cnt + threadIdx.x; i < P; i += blockDim.x) {
-    sd[i] = ~0ull; so[i] = ~0ull; si[i] = INT64_MAX;
-  }
-}
-
-// first k distinct objIDs of the sorted [0, cnt) -> (rd, ro, ri); returns the count (all threads)
-__device__ int dedupe_first_k(const uint64_t* sd, const uint64_t* so, const int64_t* si, int cnt, int k,
-                              uint64_t* rd, uint64_t* ro, int64_t* ri, int* s_n) {
-  if ((threadIdx.x >> 6) == 0) {
-    const int lane = threadIdx.x & 63;
-    int acc = 0;
-    for (int base = 0; base < cnt && acc < k; base += 64) {
-      const int i = base + lane;
-      const bool valid = i < cnt;
-      const uint64_t o = valid ? so[i] : 0ull;
-      bool dup = false;
-      for (int j = 0; j < acc; ++j) dup |= (ro[j] == o);
-      for (int j = 0; j < 64; ++j) {
-        const uint64_t oj = __shfl(o, j, 64);
-        dup |= (j < lane) && (oj == o);
-      }
-      const bool keep = valid && !dup;
-      const uint64_t m = __ballot(keep);
-      const int rank = __popcll(m & ((1ull << lane) - 1ull));
-      if (keep && acc + rank < k) {
-        rd[acc + rank] = sd[i]; ro[acc + rank] = o; ri[acc + rank] = si[i];
-      }
-      const int add = __popcll(m);
-      acc = (acc + add < k) ? acc + add : k;
-    }
-    if (lane == 0) *s_n = acc;
-  }
-  __syncthreads();
-  return *s_n;
-}
-
-// <= 64 entries in one wave's registers: bitonic network over __shfl_xor, then dedupe.
-// Keys are unique (idx), so the compare-exchange needs no tie rule.
 __device__ __forceinline__ bool kless(uint64_t ad, uint64_t ao, int64_t ai, uint64_t bd, uint64_t bo, int64_t bi) {
   if (ad != bd) return ad < bd;
   if (ao != bo) return ao < bo;
   return ai < bi;
 }
-__device__ int wave_sort_dedupe(uint64_t d, uint64_t o, int64_t i, int k, uint64_t* rd, uint64_t* ro, int64_t* ri) {
+
+// bitonic network over one wave's registers (64 keys, ascending by lane)
+__device__ __forceinline__ void wave_bitonic(uint64_t& d, uint64_t& o, int64_t& i) {
   const int lane = threadIdx.x & 63;
 #pragma unroll
   for (int size = 2; size <= 64; size <<= 1) {
@@ -372,40 +367,178 @@ __device__ int wave_sort_dedupe(uint64_t d, uint64_t o, int64_t i, int k, uint64
       if ((lower == up) ? plt : !plt) { d = pd; o = po; i = pi; }
     }
   }
-  bool dup = false;
-  for (int j = 0; j < 64; ++j) {
-    const uint64_t oj = __shfl(o, j, 64);
-    dup |= (j < lane) && (oj == o);
-  }
-  const bool keep = (d != ~0ull) && !dup;
-  const uint64_t m = __ballot(keep);
-  const int rank = __popcll(m & ((1ull << lane) - 1ull));
-  if (keep && rank < k) { rd[rank] = d; ro[rank] = o; ri[rank] = i; }
-  const int n = __popcll(m);
-  return n < k ? n : k;
 }
 
-// Lean select: 4 waves, 64 KB of LDS.  Up to kSelFast candidates are staged in registers
-// (loaded together with the count: one memory latency), histogrammed in LDS; the survivors up
-// to the k-th bin are sorted in one wave's registers (<= 64) or an LDS bitonic network.
-constexpr int kSelT = 256;
-constexpr int kSelFast = 1024;
-static_assert(kSelFast > kMaxK, "general path needs room for the running list plus a chunk");
+// <= kSelT keys, one per thread (padding: i == INT64_MAX, the largest key) -> L.sd/so/si
+// ascending.  Each wave sorts its 64 in registers; a key's final rank is its lane plus, for
+// every other wave's run, the number of keys below it (binary search in LDS).
+template <class LDS>
+__device__ void sort_regs(LDS& L, uint64_t d, uint64_t o, int64_t i) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  wave_bitonic(d, o, i);
+  L.rund[tid] = d; L.runo[tid] = o; L.runi[tid] = i;
+  __syncthreads();
+  if (i != INT64_MAX) {
+    int rank = lane;
+#pragma unroll
+    for (int v = 0; v < kSelT / 64; ++v) {
+      if (v == w) continue;
+      int lo = 0;  // keys of run v below (d, o, i): 6 halving steps reach 63, one more check 64
+#pragma unroll
+      for (int step = 32; step > 0; step >>= 1) {
+        const int m = 64 * v + lo + step - 1;
+        if (kless(L.rund[m], L.runo[m], L.runi[m], d, o, i)) lo += step;
+      }
+      if (lo == 63 && kless(L.rund[64 * v + 63], L.runo[64 * v + 63], L.runi[64 * v + 63], d, o, i)) lo = 64;
+      rank += lo;
+    }
+    L.sd[rank] = d; L.so[rank] = o; L.si[rank] = i;
+  }
+  __syncthreads();
+}
 
-__global__ __launch_bounds__(kSelT) void knn_select_kernel(KnnSelectArgs a) {
-  __shared__ uint64_t sd[kSelFast], so[kSelFast];
-  __shared__ int64_t si[kSelFast];
-  __shared__ uint64_t rd[kMaxK], ro[kMaxK];
-  __shared__ int64_t ri[kMaxK];
-  __shared__ uint32_t hist[kDistBins];
-  __shared__ uint32_t wsum[kSelT / 64];
-  __shared__ int s_cnt, s_n, s_bin;
-  __shared__ uint32_t s_S;
+template <class LDS>
+__device__ void bitonic_lds(LDS& L, int P) {
+  for (int size = 2; size <= P; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int t = threadIdx.x; t < (P >> 1); t += kSelT) {
+        const int i = 2 * stride * (t / stride) + (t & (stride - 1));
+        const int j = i + stride;
+        const bool up = (i & size) == 0;
+        if (kless(L.sd[j], L.so[j], L.si[j], L.sd[i], L.so[i], L.si[i]) == up) {
+          uint64_t td = L.sd[i]; L.sd[i] = L.sd[j]; L.sd[j] = td;
+          uint64_t to = L.so[i]; L.so[i] = L.so[j]; L.so[j] = to;
+          int64_t ti = L.si[i]; L.si[i] = L.si[j]; L.si[j] = ti;
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
 
+__device__ __forceinline__ int pow2ceil(int v) {
+  int p = 2;
+  while (p < v) p <<= 1;
+  return p;
+}
+
+// sort L.sd/so/si[0, cnt) ascending in place (cnt <= LDS::kCap)
+template <class LDS>
+__device__ void sort_lds(LDS& L, int cnt) {
+  if (cnt <= kSelT) {
+    const int tid = threadIdx.x;
+    const bool in = tid < cnt;
+    const uint64_t d = in ? L.sd[tid] : ~0ull, o = in ? L.so[tid] : ~0ull;
+    const int64_t i = in ? L.si[tid] : INT64_MAX;
+    __syncthreads();  // sort_regs reuses storage the loads above may share
+    sort_regs(L, d, o, i);
+  } else {
+    const int P = pow2ceil(cnt);
+    for (int t = cnt + threadIdx.x; t < P; t += kSelT) { L.sd[t] = ~0ull; L.so[t] = ~0ull; L.si[t] = INT64_MAX; }
+    __syncthreads();
+    bitonic_lds(L, P);
+  }
+}
+
+// Keep the first (lowest-rank) entry of every objID among the ascending L.sd/so/si[0, cnt):
+// an LDS hash table maps objID -> lowest rank (CAS insert, atomicMin), a block prefix over
+// the keep flags places the first k kept entries into L.rd/ro/ri.  Returns their number.
+template <class LDS>
+__device__ int dedupe_topk(LDS& L, int cnt, int k) {
+  constexpr int kH = 1 << LDS::kHBits;
+  constexpr int kR = LDS::kCap / kSelT;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  for (int s = tid; s < kH; s += kSelT) { L.hkey[s] = ~0ull; L.hpos[s] = 0xFFFFFFFFu; }
+  if (tid == 0) L.s_maxpos = 0x7FFFFFFF;
+  __syncthreads();
+  uint32_t slot[kR];
+#pragma unroll
+  for (int r = 0; r < kR; ++r) {
+    const int p = r * kSelT + tid;
+    slot[r] = 0;
+    if (p < cnt) {
+      const uint64_t o = L.so[p];
+      if (o == ~0ull) {  // the table's empty marker is a real objID key (INT64_MAX): own slot
+        atomicMin(&L.s_maxpos, p);
+        slot[r] = kH;
+      } else {
+        uint32_t h = (uint32_t)((o * 0x9E3779B97F4A7C15ull) >> (64 - LDS::kHBits));
+        for (;;) {  // load factor <= 1/2: terminates
+          const unsigned long long prev = atomicCAS((unsigned long long*)&L.hkey[h], ~0ull, o);
+          if (prev == ~0ull || prev == o) break;
+          h = (h + 1) & (kH - 1);
+        }
+        atomicMin(&L.hpos[h], (uint32_t)p);
+        slot[r] = h;
+      }
+    }
+  }
+  __syncthreads();
+  int base = 0;
+#pragma unroll
+  for (int r = 0; r < kR; ++r) {
+    if (r * kSelT < cnt && base < k) {  // block-uniform
+      const int p = r * kSelT + tid;
+      bool keep = false;
+      if (p < cnt) keep = (slot[r] == (uint32_t)kH) ? (L.s_maxpos == p) : (L.hpos[slot[r]] == (uint32_t)p);
+      const uint64_t m = __ballot(keep);
+      if (lane == 0) L.wsum[w] = (uint32_t)__popcll(m);
+      __syncthreads();
+      int before = base;
+      for (int v = 0; v < w; ++v) before += (int)L.wsum[v];
+      const int total = (int)(L.wsum[0] + L.wsum[1] + L.wsum[2] + L.wsum[3]);
+      const int pos = before + __popcll(m & ((1ull << lane) - 1ull));
+      if (keep && pos < k) { L.rd[pos] = L.sd[p]; L.ro[pos] = L.so[p]; L.ri[pos] = L.si[p]; }
+      base += total;
+      __syncthreads();
+    }
+  }
+  return base < k ? base : k;
+}
+
+// wave-aggregated append into the LDS sort area
+template <class LDS>
+__device__ __forceinline__ void lds_push(LDS& L, bool c, uint64_t d, uint64_t o, int64_t i) {
+  const uint64_t m = __ballot(c);
+  if (m == 0) return;
+  const int lane = threadIdx.x & 63;
+  const int leader = __ffsll((unsigned long long)m) - 1;
+  int base = 0;
+  if (lane == leader) base = atomicAdd(&L.s_cnt, __popcll(m));
+  base = __shfl(base, leader, 64);
+  if (c) {
+    const int pos = base + __popcll(m & ((1ull << lane) - 1ull));
+    L.sd[pos] = d; L.so[pos] = o; L.si[pos] = i;
+  }
+}
+
+#ifdef GF_TRACE  // phase timestamps (100 MHz wall clock) after the record, tools/trace_select.py
+#define GF_TR(j) do { if (threadIdx.x == 0) tr[j] = wall_clock64(); } while (0)
+#else
+#define GF_TR(j) do { } while (0)
+#endif
+
+// Select body.  The count and the first LDS::kCap candidates are loaded at once (one memory
+// latency).
+//   M <= 256        sort all of them (register sorts + rank merge), dedupe, done.
+//   otherwise       LDS histogram of log-spaced distance bins -> bin of the k-th -> survivors
+//                   (bins <= it) sorted and deduped.
+//   GENERAL         if that leaves < k distinct (or the survivors overflow the sort area):
+//                   every candidate, chunk by chunk, against a running top-k-distinct list.
+//                   Without it (fused lite select) such a window is flagged for re-evaluation.
+// Next window's threshold guess (write_hint): 2 x the k-th distance; r if fewer than k exist
+// within r; after an overflow the threshold shrunk to fill half the candidate buffer; after
+// too few below T, 2T.  A flagged window is re-evaluated exactly by gf_knn_decode.
+template <class LDS, bool GENERAL>
+__device__ void knn_select_body(const KnnSelectArgs& a, LDS& L) {
   const int tid = threadIdx.x;
   const int lane = tid & 63, wid = tid >> 6;
   const int k = a.k;
-  constexpr int kPer = kSelFast / kSelT;  // 4
+  constexpr int kPer = LDS::kCap / kSelT;
+#ifdef GF_TRACE
+  uint64_t* tr = (uint64_t*)((char*)a.result + sizeof(gf_knn_header) + 24 * (size_t)k);
+#endif
+  GF_TR(0);
   const unsigned long long count = a.st->count;
   const double T = a.use_state ? a.st->T : a.T;
   double dv[kPer];
@@ -419,114 +552,119 @@ __global__ __launch_bounds__(kSelT) void knn_select_kernel(KnnSelectArgs a) {
     iv[j] = in ? a.cand_i[i] : 0u;
     ov[j] = in ? a.cand_o[i] : 0;
   }
-  for (int i = tid; i < kDistBins; i += kSelT) hist[i] = 0u;
   const bool overflow = count > a.cap;
   const int64_t M = overflow ? 0 : (int64_t)count;
-  int status = overflow ? 1 : 0;
+  bool done = overflow;  // an overflowed window is flagged below
   int nres = 0;
-  __syncthreads();
+  GF_TR(1);
 
-  if (!overflow) {
-    const bool staged = M <= kSelFast;
+  if (!overflow && M <= kSelT) {
+    const bool in = tid < M;
+    sort_regs(L, in ? dbits(dv[0]) : ~0ull, in ? okey(ov[0]) : ~0ull, in ? (int64_t)iv[0] : INT64_MAX);
+    GF_TR(4);
+    nres = dedupe_topk(L, (int)M, k);
+    done = true;
+    GF_TR(5);
+  } else if (!overflow) {
+    for (int i = tid; i < kDistBins; i += kSelT) L.hist[i] = 0u;
+    if (tid == 0) { L.s_bin = kDistBins - 1; L.s_S = (uint32_t)M; L.s_cnt = 0; }
+    __syncthreads();
+    const bool staged = M <= LDS::kCap;
     const int64_t bbase = dist_bin_base(T);
     if (staged) {
 #pragma unroll
       for (int j = 0; j < kPer; ++j)
-        if (tid + (int64_t)j * kSelT < M) atomicAdd(&hist[dist_bin(dv[j], bbase)], 1u);
+        if (tid + (int64_t)j * kSelT < M) atomicAdd(&L.hist[dist_bin(dv[j], bbase)], 1u);
     } else {
-      for (int64_t i = tid; i < M; i += kSelT) atomicAdd(&hist[dist_bin(a.cand_d[i], bbase)], 1u);
+      for (int64_t i = tid; i < M; i += kSelT) atomicAdd(&L.hist[dist_bin(a.cand_d[i], bbase)], 1u);
     }
     __syncthreads();
+    GF_TR(2);
     // bin holding the k-th candidate: 16 bins per thread, block scan over 4 waves
     constexpr int kB = kDistBins / kSelT;
     uint32_t v[kB], s = 0;
 #pragma unroll
-    for (int j = 0; j < kB; ++j) { v[j] = hist[kB * tid + j]; s += v[j]; }
+    for (int j = 0; j < kB; ++j) { v[j] = L.hist[kB * tid + j]; s += v[j]; }
     uint32_t inc = s;
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {
       const uint32_t t = __shfl_up(inc, off, 64);
       if (lane >= off) inc += t;
     }
-    if (lane == 63) wsum[wid] = inc;
-    if (tid == 0) { s_bin = kDistBins - 1; s_S = (uint32_t)M; s_cnt = 0; }
+    if (lane == 63) L.wsum[wid] = inc;
     __syncthreads();
     uint32_t before = 0;
-    for (int w = 0; w < wid; ++w) before += wsum[w];
+    for (int w = 0; w < wid; ++w) before += L.wsum[w];
     const uint32_t excl = before + inc - s;
     if (excl < (uint32_t)k && (uint32_t)k <= excl + s) {
       uint32_t run = excl;
       for (int j = 0; j < kB; ++j) {
         run += v[j];
-        if (run >= (uint32_t)k) { s_bin = kB * tid + j; s_S = run; break; }
+        if (run >= (uint32_t)k) { L.s_bin = kB * tid + j; L.s_S = run; break; }
       }
     }
     __syncthreads();
-    const int bstar = s_bin;
-    bool done = false;
-    if (s_S <= (uint32_t)kSelFast) {  // fast path: survivors (bins <= bstar) fit the sort area
+    GF_TR(3);
+    const int bstar = L.s_bin;
+    if (L.s_S <= (uint32_t)LDS::kCap) {  // survivors (bins <= bstar) fit the sort area
       if (staged) {
 #pragma unroll
         for (int j = 0; j < kPer; ++j) {
-          if (tid + (int64_t)j * kSelT < M && dist_bin(dv[j], bbase) <= bstar) {
-            const int pos = atomicAdd(&s_cnt, 1);
-            sd[pos] = dbits(dv[j]); si[pos] = iv[j]; so[pos] = okey(ov[j]);
-          }
+          const bool c = tid + (int64_t)j * kSelT < M && dist_bin(dv[j], bbase) <= bstar;
+          lds_push(L, c, dbits(dv[j]), okey(ov[j]), (int64_t)iv[j]);
         }
       } else {
-        for (int64_t i = tid; i < M; i += kSelT) {
-          const double d = a.cand_d[i];
-          if (dist_bin(d, bbase) <= bstar) {
-            const int pos = atomicAdd(&s_cnt, 1);
-            sd[pos] = dbits(d); si[pos] = a.cand_i[i]; so[pos] = okey(a.cand_o[i]);
-          }
+        for (int64_t i0 = 0; i0 < M; i0 += kSelT) {  // block-uniform trip count
+          const int64_t i = i0 + tid;
+          const double d = i < M ? a.cand_d[i] : 0.0;
+          const bool c = i < M && dist_bin(d, bbase) <= bstar;
+          lds_push(L, c, dbits(d), c ? okey(a.cand_o[i]) : 0ull, c ? (int64_t)a.cand_i[i] : 0);
         }
       }
       __syncthreads();
-      const int cnt = s_cnt;
-      if (cnt <= 64 && k <= 64) {  // one wave, registers only
-        if (wid == 0) {
-          const bool in = lane < cnt;
-          const int r = wave_sort_dedupe(in ? sd[lane] : ~0ull, in ? so[lane] : ~0ull, in ? si[lane] : INT64_MAX, k,
-                                         rd, ro, ri);
-          if (lane == 0) s_n = r;
-        }
-        __syncthreads();
-        nres = s_n;
-      } else {
-        const int P = pow2ceil(cnt);
-        pad_keys(sd, so, si, cnt, P);
-        __syncthreads();
-        bitonic_sort(sd, so, si, P);
-        nres = dedupe_first_k(sd, so, si, cnt, k, rd, ro, ri, &s_n);
-      }
+      GF_TR(4);
+      const int cnt = L.s_cnt;
+#ifdef GF_TRACE
+      if (tid == 0) tr[8] = (uint64_t)cnt;
+#endif
+      sort_lds(L, cnt);
+      nres = dedupe_topk(L, cnt, k);
       done = (nres >= k) || (cnt == M);
+      GF_TR(5);
     }
-    if (!done) {  // general path: every candidate, chunk by chunk, running top-k-distinct list
+    if (GENERAL && !done) {  // every candidate, chunk by chunk, running top-k-distinct list
       int nr = 0;
-      const int chunk = kSelFast - k;
+      const int chunk = LDS::kCap - k;
       for (int64_t start = 0; start < M; start += chunk) {
         const int len = (int)((M - start) < chunk ? (M - start) : chunk);
-        for (int i = tid; i < nr; i += kSelT) { sd[i] = rd[i]; so[i] = ro[i]; si[i] = ri[i]; }
+        for (int i = tid; i < nr; i += kSelT) { L.sd[i] = L.rd[i]; L.so[i] = L.ro[i]; L.si[i] = L.ri[i]; }
         for (int i = tid; i < len; i += kSelT) {
-          sd[nr + i] = dbits(a.cand_d[start + i]); si[nr + i] = a.cand_i[start + i];
-          so[nr + i] = okey(a.cand_o[start + i]);
+          L.sd[nr + i] = dbits(a.cand_d[start + i]); L.si[nr + i] = a.cand_i[start + i];
+          L.so[nr + i] = okey(a.cand_o[start + i]);
         }
-        const int cnt = nr + len;
-        const int P = pow2ceil(cnt);
-        pad_keys(sd, so, si, cnt, P);
         __syncthreads();
-        bitonic_sort(sd, so, si, P);
-        nr = dedupe_first_k(sd, so, si, cnt, k, rd, ro, ri, &s_n);
+        sort_lds(L, nr + len);
+        nr = dedupe_topk(L, nr + len, k);
       }
       nres = nr;
+      done = true;
     }
-    if (nres < k && T < a.r) status = 1;  // fewer than k distinct objIDs below T: re-evaluate
   }
+  // final iff nothing overflowed, every candidate was considered (or k found), and either k
+  // distinct objIDs lie below T or T reached r
+  const bool too_few = done && !overflow && nres < k && T < a.r;
+  const int status = (!done || overflow || too_few) ? 1 : 0;
+  GF_TR(6);
+#ifdef GF_TRACE
+  if (tid == 0) {
+    tr[9] = a.st->tr[0]; tr[10] = a.st->tr[1]; tr[11] = a.st->tr[2];
+    a.st->tr[1] = ~0ull; a.st->tr[2] = 0ull;
+  }
+#endif
   RecView out = rec_view(a.result, k);
   if (status == 0)
     for (int i = tid; i < nres; i += kSelT) {
-      out.d[i] = from_bits(rd[i]); out.o[i] = from_okey(ro[i]); out.i[i] = ri[i] + a.idx_base;
+      out.d[i] = from_bits(L.rd[i]); out.o[i] = from_okey(L.ro[i]); out.i[i] = L.ri[i] + a.idx_base;
     }
   if (tid == 0) {
     out.h->status = status;
@@ -535,14 +673,21 @@ __global__ __launch_bounds__(kSelT) void knn_select_kernel(KnnSelectArgs a) {
     out.h->flags = overflow ? 1 : 0;
     out.h->candidates = (int64_t)count;
     out.h->threshold = T;
-    a.st->count = 0ull;  // ready for the next window on this stream
+    a.st->count = 0ull;  // ready for the lane's next window
     if (a.write_hint) {
-      double h = 0.0;  // 0: sample the next window
-      if (status == 0 && nres == k) h = 2.0 * from_bits(rd[k - 1]);
-      else if (status == 0) h = a.r;  // fewer than k within r: the next window scans to r as well
+      double h;
+      if (status == 0) h = nres == k ? 2.0 * from_bits(L.rd[k - 1]) : a.r;
+      else if (overflow) h = T * sqrt(0.5 * (double)a.cap / (double)count);
+      else if (too_few) h = 2.0 * T;
+      else h = T;
       a.st->hint_T = h;
     }
   }
+}
+
+__global__ __launch_bounds__(kSelT) void knn_select_kernel(KnnSelectArgs a) {
+  __shared__ SelFull L;
+  knn_select_body<SelFull, true>(a, L);
 }
 
 hipError_t launch_knn_select(gf_ctx* ctx, const KnnSelectArgs& a) {
@@ -551,14 +696,50 @@ hipError_t launch_knn_select(gf_ctx* ctx, const KnnSelectArgs& a) {
   return hipGetLastError();
 }
 
-// merge of per-shard records: nrec * k <= kSortCap (checked by the host)
-__global__ __launch_bounds__(kSelThreads) void knn_merge_kernel(int32_t k, const char* records, int32_t nrec,
-                                                                size_t rec_bytes, void* result) {
-  __shared__ uint64_t sd[kSortCap], so[kSortCap];
-  __shared__ int64_t si[kSortCap];
-  __shared__ uint64_t rd[kMaxK], ro[kMaxK];
-  __shared__ int64_t ri[kMaxK];
-  __shared__ int s_off[65], s_n, s_status;
+// Fused continuous-query kernel (pipeline depth 2): blocks 1.. scan window i with the
+// threshold taken from the lane's hint (set by window i-2's select) -- or, for a lane's first
+// window (use_state 2), from the sample kernel launched just before; block 0, dispatched
+// first, runs window i-1's select on the other lane while they stream.  One launch per window.
+template <int METRIC, int NT>
+__global__ __launch_bounds__(kBlock) void knn_fused_kernel(KnnScanArgs a, KnnSelectArgs prev, int has_prev) {
+  __shared__ SelLite L;
+  if (blockIdx.x == 0) {
+    if (has_prev) knn_select_body<SelLite, false>(prev, L);
+    return;
+  }
+  double T, sp;
+  if (a.use_state == 2) {  // cold lane: the sample kernel just set T
+    T = a.st->T;
+    sp = a.st->s_pre;
+  } else {
+    const double h = a.st->hint_T;
+    T = (h > 0.0 && h < a.T) ? h : a.T;  // a.T = r
+    sp = s_prefilter(T, a.metric);
+    if (blockIdx.x == 1 && threadIdx.x == 0) { a.st->T = T; a.st->s_pre = sp; }
+  }
+  knn_scan_body<METRIC, 1, NT>(a, sp, T, blockIdx.x - 1, gridDim.x - 1);
+}
+
+hipError_t launch_knn_fused(gf_ctx* ctx, const KnnScanArgs& a, const KnnSelectArgs& prev, int has_prev,
+                            int scan_blocks, int nt) {
+  KTimer t(ctx, GF_K_KNN_SCAN);
+  const dim3 g(scan_blocks + 1), b(kBlock);
+  if (a.metric == 0) {
+    if (nt) hipLaunchKernelGGL((knn_fused_kernel<0, 1>), g, b, 0, ctx->stream, a, prev, has_prev);
+    else hipLaunchKernelGGL((knn_fused_kernel<0, 0>), g, b, 0, ctx->stream, a, prev, has_prev);
+  } else {
+    if (nt) hipLaunchKernelGGL((knn_fused_kernel<1, 1>), g, b, 0, ctx->stream, a, prev, has_prev);
+    else hipLaunchKernelGGL((knn_fused_kernel<1, 0>), g, b, 0, ctx->stream, a, prev, has_prev);
+  }
+  return hipGetLastError();
+}
+
+// Merge of per-shard records (nrec <= 64): whole records are appended to the running
+// top-k-distinct list while they fit the sort area, then sorted and deduped.
+__global__ __launch_bounds__(kSelT) void knn_merge_kernel(int32_t k, const char* records, int32_t nrec,
+                                                          size_t rec_bytes, void* result) {
+  __shared__ SelFull L;
+  __shared__ int s_off[65], s_status;
   const int tid = threadIdx.x;
   if (tid == 0) {
     int off = 0, st = 0;
@@ -572,36 +753,40 @@ __global__ __launch_bounds__(kSelThreads) void knn_merge_kernel(int32_t k, const
     s_status = st;
   }
   __syncthreads();
-  for (int r = 0; r < nrec; ++r) {
-    RecView in = rec_view((void*)(records + (size_t)r * rec_bytes), k);
-    const int n = s_off[r + 1] - s_off[r];
-    for (int i = tid; i < n; i += kSelThreads) {
-      sd[s_off[r] + i] = dbits(in.d[i]); so[s_off[r] + i] = okey(in.o[i]); si[s_off[r] + i] = in.i[i];
+  int nr = 0, r = 0;
+  while (r < nrec) {  // block-uniform
+    for (int i = tid; i < nr; i += kSelT) { L.sd[i] = L.rd[i]; L.so[i] = L.ro[i]; L.si[i] = L.ri[i]; }
+    int cnt = nr;
+    while (r < nrec && cnt + (s_off[r + 1] - s_off[r]) <= SelFull::kCap) {
+      RecView in = rec_view((void*)(records + (size_t)r * rec_bytes), k);
+      const int n = s_off[r + 1] - s_off[r];
+      for (int i = tid; i < n; i += kSelT) {
+        L.sd[cnt + i] = dbits(in.d[i]); L.so[cnt + i] = okey(in.o[i]); L.si[cnt + i] = in.i[i];
+      }
+      cnt += n;
+      ++r;
     }
+    __syncthreads();
+    sort_lds(L, cnt);
+    nr = dedupe_topk(L, cnt, k);
   }
-  const int cnt = s_off[nrec];
-  const int P = pow2ceil(cnt);
-  pad_keys(sd, so, si, cnt, P);
-  __syncthreads();
-  bitonic_sort(sd, so, si, P);
-  const int nres = dedupe_first_k(sd, so, si, cnt, k, rd, ro, ri, &s_n);
   RecView out = rec_view(result, k);
-  for (int i = tid; i < nres; i += kSelThreads) {
-    out.d[i] = from_bits(rd[i]); out.o[i] = from_okey(ro[i]); out.i[i] = ri[i];
+  for (int i = tid; i < nr; i += kSelT) {
+    out.d[i] = from_bits(L.rd[i]); out.o[i] = from_okey(L.ro[i]); out.i[i] = L.ri[i];
   }
   if (tid == 0) {
     out.h->status = s_status;
-    out.h->n = s_status ? 0 : nres;
+    out.h->n = s_status ? 0 : nr;
     out.h->k = k;
     out.h->flags = 0;
-    out.h->candidates = cnt;
+    out.h->candidates = s_off[nrec];
     out.h->threshold = 0.0;
   }
 }
 
 hipError_t launch_knn_merge(gf_ctx* ctx, int32_t k, const void* records, int32_t nrec, void* result) {
   const size_t rb = gf_knn_result_bytes(k);
-  hipLaunchKernelGGL(knn_merge_kernel, dim3(1), dim3(kSelThreads), 0, ctx->stream, k, (const char*)records, nrec,
+  hipLaunchKernelGGL(knn_merge_kernel, dim3(1), dim3(kSelT), 0, ctx->stream, k, (const char*)records, nrec,
                      rb, result);
   return hipGetLastError();
 }

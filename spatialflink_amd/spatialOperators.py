@@ -327,6 +327,16 @@ class PointPointKNNQuery(SpatialOperator):
         m = n.value
         return KNNResult(window.start, window.end, oo[:m].copy(), od[:m].copy(), oi[:m].copy())
 
+    def set_pipeline(self, window_device, queryPoint, queryRadius, k, depth: int):
+        """depth 2: one fused launch per window; window i's record is written by the next
+        enqueue (its select runs in block 0 of window i+1's scan) or by flush()."""
+        ctx, plan = self.plan(window_device, queryPoint, queryRadius, k)
+        _lib.check(_lib.lib().gf_knn_plan_set_pipeline(plan, int(depth)), ctx.handle, "set_pipeline")
+
+    def flush(self, window_device, queryPoint, queryRadius, k):
+        ctx, plan = self.plan(window_device, queryPoint, queryRadius, k)
+        _lib.check(_lib.lib().gf_knn_plan_flush(plan), ctx.handle, "flush")
+
     def set_capacity(self, window_device, queryPoint, queryRadius, k, cap):
         ctx, plan = self.plan(window_device, queryPoint, queryRadius, k)
         _lib.check(_lib.lib().gf_knn_plan_set_capacity(plan, int(cap)), ctx.handle, "set_capacity")

@@ -446,3 +446,47 @@ def test_knn_pinned_records_async(sf, oracle_mod):
         res = op.finish(wins[i % 3], q, 0.5, k, rec.raw(i))
         st, oo, od, oi = oracle_mod.knn(og, x, y, obj, QPOINT[0], QPOINT[1], 0.5, k)
         check_knn(res, oo, od, oi)
+
+
+@pytest.mark.parametrize("k", [50, 120])
+def test_knn_pipelined(sf, oracle_mod, k):
+    """Depth-2 pipeline: window i's select runs inside window i+1's fused scan kernel; cold
+    starts and a window whose carried hint is too small are re-evaluated at decode; the
+    synchronous API on a pipelined plan."""
+    import torch
+
+    g = sf.UniformGrid(500, *BEIJING)
+    og = oracle_mod.grid(500, *BEIJING)
+    q = sf.Point("q", *QPOINT, 0, g)
+    op = sf.PointPointKNNQuery(conf(sf), g)
+    N = 1_100_000
+    data = []
+    for seed in (21, 22, "hole", 23, 24):
+        if seed == "hole":
+            x, y = oracle_mod.java_random_points(97, N, *BEIJING)
+            far = (x - QPOINT[0]) ** 2 + (y - QPOINT[1]) ** 2 > 0.03 ** 2
+            x, y = x[far], y[far]
+        else:
+            x, y = oracle_mod.java_random_points(seed, N, *BEIJING)
+        obj = np.random.default_rng(3).permutation(len(x)).astype(np.int64)
+        if seed == 23:  # trajectories: every objID three times
+            obj %= len(x) // 3
+        data.append((x, y, obj, win(sf, x, y, obj)))
+    op.set_pipeline(0, q, 0.5, k, 2)
+    order = [0, 1, 0, 1, 3, 4, 2, 3, 4, 0, 2, 2, 1]
+    rec = sf.PinnedRecords(len(order), k)
+    for i, j in enumerate(order):
+        op.enqueue(data[j][3], q, 0.5, k, rec.ptr(i))
+    op.flush(0, q, 0.5, k)
+    torch.cuda.synchronize()
+    for i, j in enumerate(order):
+        x, y, obj, w = data[j]
+        res = op.finish(w, q, 0.5, k, rec.raw(i))
+        st, oo, od, oi = oracle_mod.knn(og, x, y, obj, QPOINT[0], QPOINT[1], 0.5, k)
+        check_knn(res, oo, od, oi)
+    for j in (2, 0, 4):  # synchronous API on a pipelined plan
+        x, y, obj, w = data[j]
+        res = op.run(w, q, 0.5, k)
+        st, oo, od, oi = oracle_mod.knn(og, x, y, obj, QPOINT[0], QPOINT[1], 0.5, k)
+        check_knn(res, oo, od, oi)
+    op.set_pipeline(0, q, 0.5, k, 1)
