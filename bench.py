@@ -57,6 +57,10 @@ def main():
     ap.add_argument("--windows", type=int, default=4, help="distinct resident windows cycled through")
     ap.add_argument("--timing-period", type=int, default=5,
                     help="HIP events around every N-th launch of the timed kernel (fewer events, less overhead)")
+    ap.add_argument("--exchange-batch", type=int, default=8,
+                    help="N > 1: windows whose top-k records share one RCCL all-gather + one merge launch")
+    ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
+                    help="gloo: rehearse the N > 1 path with several ranks on one GPU (not a benchmark)")
     ap.add_argument("--pipeline", type=int, default=2, choices=(1, 2),
                     help="windows in flight: 2 overlaps window i's select with window i+1's scan")
     args = ap.parse_args()
@@ -68,8 +72,11 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        torch.cuda.set_device(local % torch.cuda.device_count())
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
@@ -108,7 +115,8 @@ def main():
     _lib.check(_lib.lib().gf_knn_plan_set_pipeline(plan, args.pipeline), ctx.handle, "pipeline")
     lag = args.pipeline - 1  # depth 2: window i's record is written by enqueue i+1 (or the flush)
     rb = knn_record_bytes(args.k)
-    slots = torch.zeros(4, rb, dtype=torch.uint8, device=dev)
+    B = max(1, args.exchange_batch)
+    slots = torch.zeros(2, B, rb, dtype=torch.uint8, device=dev)  # two groups of B device records
     total_steps = args.warmup + args.steps
     host = sf.PinnedRecords(total_steps, args.k)
     L = _lib.lib()
@@ -116,8 +124,9 @@ def main():
     pts_ref = [ctypes.byref(p_) for p_ in pts]
     enqueue = L.gf_knn_enqueue
 
-    def exchange(i):  # device record of window i -> RCCL all-gather -> merge into the pinned record
-        sharding.allgather_knn_records(slots[i % 4], args.k, host.ptr(i))
+    def exchange(first, lo, hi):  # windows [lo, hi] of one group: one all-gather + one merge launch
+        g = (lo - first) // B
+        sharding.allgather_knn_records_batch(slots[g % 2, : hi - lo + 1], args.k, host.ptr(lo))
 
     def step(i, first):
         if world == 1:  # the select writes the final record straight into pinned host memory
@@ -125,18 +134,22 @@ def main():
             if st:
                 _lib.check(st, ctx.handle, "gf_knn_enqueue")
         else:
-            _lib.check(enqueue(plan, pts_ref[i % args.windows], slots[i % 4].data_ptr()), ctx.handle, "enqueue")
-            if i - lag >= first:  # (the previous phase's last window was exchanged by drain)
-                exchange(i - lag)
+            g, w_ = divmod(i - first, B)
+            _lib.check(enqueue(plan, pts_ref[i % args.windows], slots[g % 2, w_].data_ptr()), ctx.handle, "enqueue")
+            c = i - lag  # this window's record is complete now
+            if c >= first and (c - first) % B == B - 1:
+                exchange(first, c - B + 1, c)
 
-    def drain(last):
+    def drain(first, last):
         _lib.check(L.gf_knn_plan_flush(plan), ctx.handle, "flush")
-        if world > 1 and lag:
-            exchange(last)
+        if world > 1:
+            lo = first + ((last - first) // B) * B
+            if lag or (last - first) % B != B - 1:  # the last group is still pending
+                exchange(first, lo, last)
 
     for i in range(args.warmup):
         step(i, 0)
-    drain(args.warmup - 1)
+    drain(0, args.warmup - 1)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -149,7 +162,7 @@ def main():
     t0 = time.perf_counter()
     for i in range(args.warmup, total_steps):
         step(i, args.warmup)
-    drain(total_steps - 1)
+    drain(args.warmup, total_steps - 1)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     if world > 1:
@@ -159,7 +172,7 @@ def main():
     ctx.set_timing_period(1)
     elapsed = t1 - t0
     if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
 
@@ -185,7 +198,7 @@ def main():
         _lib.check(_lib.lib().gf_knn_plan_set_hint(plan, hint), ctx.handle, "hint")
         ctx.set_timing(kid_all)
         for i in range(12):
-            enqueue(plan, pts_ref[i % args.windows], slots[i % 4].data_ptr())
+            enqueue(plan, pts_ref[i % args.windows], slots[0, i % B].data_ptr())
         L.gf_knn_plan_flush(plan)
         for name, kid in (("sample", _lib.K_KNN_SAMPLE), ("scan", _lib.K_KNN_SCAN), ("select", _lib.K_KNN_SELECT)):
             ms, cnt = ctx.timing(kid)
@@ -194,7 +207,7 @@ def main():
         torch.cuda.synchronize()
         t = time.perf_counter()
         for i in range(20):
-            enqueue(plan, pts_ref[i % args.windows], slots[i % 4].data_ptr())
+            enqueue(plan, pts_ref[i % args.windows], slots[0, i % B].data_ptr())
         L.gf_knn_plan_flush(plan)
         torch.cuda.synchronize()
         breakdown[tag + "window_us"] = round(1e6 * (time.perf_counter() - t) / 20, 2)
@@ -277,6 +290,7 @@ def main():
                 "query_point": list(QPOINT),
                 "parallelism": f"cell-column shards x{world}" + (" + RCCL all-gather top-k" if world > 1 else ""),
                 "windows_in_flight": args.pipeline,
+                "exchange_batch": B if world > 1 else None,
             },
             "roofline": {
                 "bound": "hbm",

@@ -198,6 +198,14 @@ int    gf_knn_run(gf_knn_plan* plan, const gf_points* pts, int64_t* objID, doubl
  * gf_knn_result_bytes(k)) into one record (async) -- the windowAll funnel across GPUs after
  * an RCCL all-gather.  `result` may be device memory or gf_pinned_alloc memory. */
 int    gf_knn_merge_dev(gf_ctx* ctx, int32_t k, const void* records, int32_t nrec, void* result);
+/* Batched: nwin windows in one launch (one block each), so one RCCL all-gather can carry the
+ * records of several windows.  layout GF_MERGE_SHARD_MAJOR: record (shard s, window w) at
+ * index s*nwin + w (an all-gather of each rank's nwin consecutive records);
+ * GF_MERGE_WINDOW_MAJOR: at index w*nrec + s.  `results` receives nwin consecutive records. */
+#define GF_MERGE_SHARD_MAJOR  0
+#define GF_MERGE_WINDOW_MAJOR 1
+int    gf_knn_merge_dev_batch(gf_ctx* ctx, int32_t k, const void* records, int32_t nrec, int32_t nwin,
+                              int32_t layout, void* results);
 /* Host merge of per-shard sorted lists: top-k distinct objIDs by (dist, objID). */
 int    gf_knn_merge_host(int32_t k, int32_t nlists, const int32_t* counts, const int64_t* objID,
                          const double* dist, const int64_t* idx, int64_t* out_objID,

@@ -14,6 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GF_LIB_PATH") or os.path.join(_HERE, "libgeoflink_hip.so")
 
 GF_OK = 0
+GF_MERGE_SHARD_MAJOR, GF_MERGE_WINDOW_MAJOR = 0, 1
 GF_ERR_ARG = -1
 GF_ERR_CAPACITY = -2
 GF_ERR_HIP = -3
@@ -35,7 +36,7 @@ EXPORTS = [
     "gf_range_plan_destroy", "gf_range_run", "gf_bitmap_to_indices", "gf_knn_pp_plan_create",
     "gf_knn_plan_destroy", "gf_knn_plan_set_capacity", "gf_knn_plan_set_index_base", "gf_knn_plan_set_tuning", "gf_knn_plan_set_hint", "gf_knn_plan_set_pipeline", "gf_knn_plan_flush",
     "gf_knn_result_bytes", "gf_knn_enqueue",
-    "gf_knn_decode", "gf_knn_run", "gf_knn_merge_dev", "gf_knn_merge_host", "gf_join_pp", "gf_window_create",
+    "gf_knn_decode", "gf_knn_run", "gf_knn_merge_dev", "gf_knn_merge_dev_batch", "gf_knn_merge_host", "gf_join_pp", "gf_window_create",
     "gf_window_destroy", "gf_window_upload", "gf_window_points", "gf_synth_uniform", "gf_pinned_alloc",
     "gf_pinned_free",
 ]
@@ -130,6 +131,7 @@ def lib():
             "gf_knn_decode": ([P, C.POINTER(GfPoints), P, P, P, P, pi32], C.c_int),
             "gf_knn_run": ([P, C.POINTER(GfPoints), P, P, P, pi32], C.c_int),
             "gf_knn_merge_dev": ([P, i32, P, i32, P], C.c_int),
+            "gf_knn_merge_dev_batch": ([P, i32, P, i32, i32, i32, P], C.c_int),
             "gf_knn_merge_host": ([i32, i32, P, P, P, P, P, P, P, pi32], C.c_int),
             "gf_join_pp": ([P, C.POINTER(GfGrid), C.POINTER(GfGrid), C.POINTER(GfPoints), C.POINTER(GfPoints), d,
                             C.c_int, C.c_int, P, i64, pi64], C.c_int),

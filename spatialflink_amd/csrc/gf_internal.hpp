@@ -184,7 +184,8 @@ hipError_t launch_knn_scan(gf_ctx* ctx, const KnnScanArgs& a, int blocks, int un
 hipError_t launch_knn_select(gf_ctx* ctx, const KnnSelectArgs& a);
 hipError_t launch_knn_fused(gf_ctx* ctx, const KnnScanArgs& a, const KnnSelectArgs& prev, int has_prev,
                             int scan_blocks, int nt);
-hipError_t launch_knn_merge(gf_ctx* ctx, int32_t k, const void* records, int32_t nrec, void* result);
+hipError_t launch_knn_merge(gf_ctx* ctx, int32_t k, const void* records, int32_t nrec, size_t rec_stride,
+                            int32_t nwin, size_t win_stride, void* result, size_t res_stride);
 
 hipError_t launch_range(gf_ctx* ctx, const RangeArgs& a, int table_mode, int poly, int blocks);
 hipError_t launch_range_finalize(hipStream_t s, const uint64_t* partials, int blocks, int64_t* counts);

@@ -736,11 +736,16 @@ hipError_t launch_knn_fused(gf_ctx* ctx, const KnnScanArgs& a, const KnnSelectAr
 
 // Merge of per-shard records (nrec <= 64): whole records are appended to the running
 // top-k-distinct list while they fit the sort area, then sorted and deduped.
+// Block w merges window w: its nrec records start at records + w*win_stride, rec_stride apart;
+// the merged record goes to result + w*res_stride.
 __global__ __launch_bounds__(kSelT) void knn_merge_kernel(int32_t k, const char* records, int32_t nrec,
-                                                          size_t rec_bytes, void* result) {
+                                                          size_t rec_bytes, size_t win_stride, void* result_base,
+                                                          size_t res_stride) {
   __shared__ SelFull L;
   __shared__ int s_off[65], s_status;
   const int tid = threadIdx.x;
+  records += (size_t)blockIdx.x * win_stride;
+  void* result = (char*)result_base + (size_t)blockIdx.x * res_stride;
   if (tid == 0) {
     int off = 0, st = 0;
     for (int r = 0; r < nrec; ++r) {
@@ -784,10 +789,10 @@ __global__ __launch_bounds__(kSelT) void knn_merge_kernel(int32_t k, const char*
   }
 }
 
-hipError_t launch_knn_merge(gf_ctx* ctx, int32_t k, const void* records, int32_t nrec, void* result) {
-  const size_t rb = gf_knn_result_bytes(k);
-  hipLaunchKernelGGL(knn_merge_kernel, dim3(1), dim3(kSelT), 0, ctx->stream, k, (const char*)records, nrec,
-                     rb, result);
+hipError_t launch_knn_merge(gf_ctx* ctx, int32_t k, const void* records, int32_t nrec, size_t rec_stride,
+                            int32_t nwin, size_t win_stride, void* result, size_t res_stride) {
+  hipLaunchKernelGGL(knn_merge_kernel, dim3(nwin), dim3(kSelT), 0, ctx->stream, k, (const char*)records, nrec,
+                     rec_stride, win_stride, result, res_stride);
   return hipGetLastError();
 }
 

@@ -71,6 +71,19 @@ def allgather_knn_lists(objID, dist, idx, k: int, group=None):
     return knn_merge_host(k, gathered)
 
 
+def _all_gather_bytes(out, inp, group):
+    """all_gather_into_tensor; device tensors go through host memory on gloo (CPU rehearsal
+    of the multi-rank path on one GPU), straight over RCCL otherwise."""
+    import torch.distributed as dist_
+
+    if inp.is_cuda and dist_.get_backend(group) == "gloo":
+        tmp = out.cpu()
+        dist_.all_gather_into_tensor(tmp, inp.cpu(), group=group)
+        out.copy_(tmp)
+    else:
+        dist_.all_gather_into_tensor(out, inp, group=group)
+
+
 def allgather_knn_records(record, k: int, merged_out, group=None):
     """RCCL path: all-gather this rank's device kNN record (uint8 tensor of
     knn_record_bytes(k)) over xGMI, then merge the world's records on the device
@@ -82,12 +95,33 @@ def allgather_knn_records(record, k: int, merged_out, group=None):
     world = dist_.get_world_size(group)
     rb = record.numel()
     gathered = torch.empty(world * rb, dtype=torch.uint8, device=record.device)
-    dist_.all_gather_into_tensor(gathered, record, group=group)
+    _all_gather_bytes(gathered, record, group)
     ctx = _lib.context(record.device.index)
     out = merged_out if isinstance(merged_out, int) else merged_out.data_ptr()
     _lib.check(_lib.lib().gf_knn_merge_dev(ctx.handle, int(k), gathered.data_ptr(), world, out),
                ctx.handle, "gf_knn_merge_dev")
     return merged_out
+
+
+def allgather_knn_records_batch(records, k: int, results, group=None):
+    """One RCCL all-gather for several windows: `records` is this rank's [nwin, rb] uint8
+    device tensor (consecutive windows); every rank merges all windows in one launch
+    (gf_knn_merge_dev_batch, shard-major) into `results` -- nwin consecutive records (device
+    tensor or an int address from PinnedRecords.ptr()).  Stream-ordered, no host sync.
+    Batching amortises the collective's latency over nwin windows (xGMI is point to point:
+    small messages are latency-, not bandwidth-bound)."""
+    import torch
+    import torch.distributed as dist_
+
+    world = dist_.get_world_size(group)
+    nwin, rb = records.shape
+    gathered = torch.empty(world * nwin * rb, dtype=torch.uint8, device=records.device)
+    _all_gather_bytes(gathered, records.reshape(-1), group)
+    ctx = _lib.context(records.device.index)
+    out = results if isinstance(results, int) else results.data_ptr()
+    _lib.check(_lib.lib().gf_knn_merge_dev_batch(ctx.handle, int(k), gathered.data_ptr(), world, int(nwin),
+                                                 _lib.GF_MERGE_SHARD_MAJOR, out), ctx.handle, "gf_knn_merge_dev_batch")
+    return results
 
 
 def join_query_halo(qcx: np.ndarray, band, c: int) -> np.ndarray:

@@ -490,3 +490,42 @@ def test_knn_pipelined(sf, oracle_mod, k):
         st, oo, od, oi = oracle_mod.knn(og, x, y, obj, QPOINT[0], QPOINT[1], 0.5, k)
         check_knn(res, oo, od, oi)
     op.set_pipeline(0, q, 0.5, k, 1)
+
+
+@pytest.mark.parametrize("layout", [0, 1])
+def test_knn_merge_dev_batch(sf, oracle_mod, layout):
+    """One batched merge launch over several windows' shard records (both layouts) == each
+    window evaluated whole; shards use index bases so the merged idx is global."""
+    import torch
+
+    from spatialflink_amd import _lib
+
+    g = sf.UniformGrid(500, *BEIJING)
+    og = oracle_mod.grid(500, *BEIJING)
+    q = sf.Point("q", *QPOINT, 0, g)
+    k, S, W = 40, 3, 5
+    rb = sf.spatialOperators.knn_record_bytes(k)
+    recs = torch.zeros(S * W * rb, dtype=torch.uint8, device="cuda")
+    expect = []
+    ops = [sf.PointPointKNNQuery(conf(sf), g) for _ in range(S)]
+    for wi in range(W):
+        x, y = oracle_mod.java_random_points(300 + wi, 240_000, *BEIJING)
+        obj = (np.random.default_rng(wi).permutation(len(x)) % 150_000).astype(np.int64)  # duplicates
+        expect.append(oracle_mod.knn(og, x, y, obj, QPOINT[0], QPOINT[1], 0.5, k))
+        for s, ix in enumerate(np.array_split(np.arange(len(x)), S)):
+            ctx, plan = ops[s].plan(0, q, 0.5, k)
+            _lib.check(_lib.lib().gf_knn_plan_set_index_base(plan, int(ix[0])), ctx.handle, "base")
+            slot = s * W + wi if layout == 0 else wi * S + s
+            ops[s].enqueue(win(sf, x[ix], y[ix], obj[ix]), q, 0.5, k, recs[slot * rb:(slot + 1) * rb])
+    out = torch.zeros(W * rb, dtype=torch.uint8, device="cuda")
+    ctx = _lib.context(0)
+    _lib.check(_lib.lib().gf_knn_merge_dev_batch(ctx.handle, k, recs.data_ptr(), S, W, layout, out.data_ptr()),
+               ctx.handle, "merge batch")
+    raw = out.cpu().numpy().tobytes()
+    for wi in range(W):
+        st, o, d, i = sf.spatialOperators.decode_knn_record(raw[wi * rb:(wi + 1) * rb], k)
+        est, eo, ed, ei = expect[wi]
+        assert st == 0
+        np.testing.assert_array_equal(o, eo)
+        np.testing.assert_array_equal(d, ed)
+        np.testing.assert_array_equal(i, ei)
