@@ -46,7 +46,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--points", type=int, default=10_000_000, help="points per window per GPU")
+    ap.add_argument("--points", type=int, default=None, help="points per window per GPU (kNN default 10M)")
+    ap.add_argument("--workload", default="knn", choices=("knn", "range", "ppoly", "join"),
+                    help="knn = the headline line (BASELINE configs[1]); range/ppoly/join: tools/bench_workloads.py")
     ap.add_argument("--k", type=int, default=50)
     ap.add_argument("--radius", type=float, default=0.5)
     ap.add_argument("--grid", type=int, default=500)
@@ -64,6 +66,14 @@ def main():
     ap.add_argument("--pipeline", type=int, default=2, choices=(1, 2),
                     help="windows in flight: 2 overlaps window i's select with window i+1's scan")
     args = ap.parse_args()
+    if args.workload != "knn":
+        sys.path.insert(0, os.path.join(ROOT, "tools"))
+        import bench_workloads
+
+        bench_workloads.run(args)
+        return
+    if args.points is None:
+        args.points = 10_000_000
 
     import torch
     import torch.distributed as dist
@@ -213,6 +223,38 @@ def main():
         breakdown[tag + "window_us"] = round(1e6 * (time.perf_counter() - t) / 20, 2)
     _lib.check(_lib.lib().gf_knn_plan_set_hint(plan, 1), ctx.handle, "hint")
 
+    # host-buffer boundary (never part of `value`): a window handed over in host memory
+    # (x, y, objID, ts = 32 B/point) is uploaded with gf_window_upload, then evaluated
+    pcie = None
+    if rank == 0 and world == 1:
+        x0, y0, o0 = host_windows[0]
+        ts0 = np.arange(n, dtype=np.int64)
+        hw = ctypes.c_void_p()
+        _lib.check(L.gf_window_create(ctx.handle, n, ctypes.byref(hw)), ctx.handle, "window")
+        pin = ctypes.c_void_p()
+        _lib.check(L.gf_pinned_alloc(32 * n, ctypes.byref(pin)), None, "pinned")
+        pv = np.ctypeslib.as_array((ctypes.c_uint8 * (32 * n)).from_address(pin.value))
+        for j, a in enumerate((x0, y0, o0, ts0)):
+            pv[8 * n * j: 8 * n * (j + 1)] = a.view(np.uint8)
+        res = {}
+        for tag, ptrs in (("pageable", [a.ctypes.data for a in (x0, y0, o0, ts0)]),
+                          ("pinned", [pin.value + 8 * n * j for j in range(4)])):
+            best = 1e9
+            for _ in range(3):
+                torch.cuda.synchronize()
+                t = time.perf_counter()
+                _lib.check(L.gf_window_upload(hw, *ptrs, n), ctx.handle, "upload")
+                torch.cuda.synchronize()
+                best = min(best, time.perf_counter() - t)
+            res[tag] = best
+        L.gf_window_destroy(hw)
+        L.gf_pinned_free(pin)
+        wnd = breakdown.get("window_us", 0.0) * 1e-6
+        pcie = {"bytes_per_window": 32 * n, "upload_pinned_ms": round(1e3 * res["pinned"], 3),
+                "upload_pageable_ms": round(1e3 * res["pageable"], 3),
+                "upload_pinned_GBps": round(32 * n / res["pinned"] / 1e9, 1),
+                "pcie_inclusive_points_per_s": round(n / (res["pinned"] + wnd), 1)}
+
     verified = None
     cpu = None
     if rank == 0 and world == 1:
@@ -308,6 +350,7 @@ def main():
             },
             "cpu_baseline": cpu,
             "breakdown": breakdown,
+            "host_boundary": pcie,
             "verified_vs_oracle": verified,
         }
         print(json.dumps(line), flush=True)
