@@ -53,7 +53,9 @@ extern "C" {
 #define GF_K_RANGE_SCAN  3
 #define GF_K_ASSIGN      4
 #define GF_K_JOIN_PROBE  5
-#define GF_K_COUNT       6
+#define GF_K_RANGE_TEST  6  /* deferred candidate tests of the many-object range plans */
+#define GF_K_JOIN_BUCKET 7  /* ordinary-side bucketing of the join */
+#define GF_K_COUNT       8
 
 typedef struct gf_ctx gf_ctx;
 
@@ -144,6 +146,13 @@ void gf_range_plan_destroy(gf_range_plan* plan);
  * int64[2] = {points emitted, size of the emitted multiset}. */
 int  gf_range_run(gf_range_plan* plan, const gf_points* pts, uint64_t* bitmap,
                   uint64_t* multi_bitmap, int64_t* counts);
+/* Plan diagnostics: in-grid cells by class (none / candidate / guaranteed / candidate cells
+ * accepted untested because closed rectangles cover them); any pointer may be null. */
+int  gf_range_plan_stats(const gf_range_plan* plan, int64_t* none_cells, int64_t* candidate_cells,
+                         int64_t* guaranteed_cells, int64_t* inside_cells);
+/* Tuning: scan blocks (0 = auto, <= 8 per CU); candidate tests: 0 auto, 1 inline in the scan,
+ * 2 deferred to a second kernel over the queued points (table modes). */
+int  gf_range_plan_set_tuning(gf_range_plan* plan, int32_t scan_blocks, int32_t defer_mode);
 /* Sync: selection bitmap -> ascending point indices (device uint32[cap]). */
 int  gf_bitmap_to_indices(gf_ctx* ctx, const uint64_t* bitmap, int64_t n, uint32_t* idx,
                           int64_t cap, int64_t* count);

@@ -4,10 +4,12 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <limits>
+#include <unordered_map>
 #include <unordered_set>
 #include <vector>
 
@@ -425,13 +427,88 @@ void prefix2d(std::vector<int32_t>& d, int64_t n) {
 
 Rect expand(Rect b, int64_t e) { return {b.x0 - e, b.x1 + e, b.y0 - e, b.y1 + e}; }
 
+// Candidate cells covered by closed regions at distance 0 from each of their points (axis-
+// aligned rectangle polygons; every bbox in approximate mode) become kInside (3) and are
+// accepted untested.  A cell's exact coordinate range is the closed box
+// [X_c, prev(X_{c+1})] x [Y_c, prev(Y_{c+1})] (X_c = first_at_least(c)).  Cells inside one
+// region are marked directly; a cell the regions only partly overlap is split at the regions'
+// edges into closed sub-boxes, and is covered iff every sub-box lies in some region -- so
+// cells straddling the shared edge of two adjacent squares count too.
+void mark_inside(gf_range_plan* P, std::vector<uint8_t>& table, const std::vector<std::array<double, 4>>& regs) {
+  const gf_grid& g = P->grid;
+  const int64_t n = g.n;
+  std::vector<double> XT(n + 1), YT(n + 1);
+  for (int64_t c = 0; c <= n; ++c) {
+    XT[c] = first_at_least(c, g.minX, g.cellLength);
+    YT[c] = first_at_least(c, g.minY, g.cellLength);
+  }
+  auto hi = [](const std::vector<double>& T, int64_t c) {  // largest double of cell c
+    return std::isnan(T[c + 1]) ? INFINITY : std::nextafter(T[c + 1], -INFINITY);
+  };
+  // cells of [lo, hi] (overlapping: o0..o1; wholly inside: i0..i1)
+  auto span = [&](const std::vector<double>& T, double lo, double up, double mn, int64_t& o0, int64_t& o1,
+                  int64_t& i0, int64_t& i1) {
+    o0 = std::max<int64_t>(cell_index(lo, mn, g.cellLength), 0);
+    o1 = std::min<int64_t>(cell_index(up, mn, g.cellLength), n - 1);
+    i0 = o0;
+    i1 = o1;
+    while (i0 <= i1 && !(T[i0] >= lo)) ++i0;
+    while (i1 >= i0 && !(hi(T, i1) <= up)) --i1;
+  };
+  std::unordered_map<int64_t, std::vector<int32_t>> partial;
+  for (size_t k = 0; k < regs.size(); ++k) {
+    const auto& b = regs[k];
+    int64_t ox0, ox1, ix0, ix1, oy0, oy1, iy0, iy1;
+    span(XT, b[0], b[2], g.minX, ox0, ox1, ix0, ix1);
+    span(YT, b[1], b[3], g.minY, oy0, oy1, iy0, iy1);
+    for (int64_t y = oy0; y <= oy1; ++y)
+      for (int64_t x = ox0; x <= ox1; ++x) {
+        const int64_t cell = y * n + x;
+        if (table[cell] != 1) continue;
+        const bool in = x >= ix0 && x <= ix1 && y >= iy0 && y <= iy1;
+        if (in) table[cell] = 3;
+        else partial[cell].push_back((int32_t)k);
+      }
+  }
+  for (auto& kv : partial) {
+    const int64_t cell = kv.first;
+    if (table[cell] != 1 || kv.second.size() < 2) continue;  // one partial region never covers
+    const int64_t cx = cell % n, cy = cell / n;
+    const double x0 = XT[cx], x1 = hi(XT, cx), y0 = YT[cy], y1 = hi(YT, cy);
+    std::vector<double> xs{x0, x1}, ys{y0, y1};
+    for (int32_t k : kv.second) {
+      const auto& b = regs[k];
+      if (b[0] > x0 && b[0] < x1) xs.push_back(b[0]);
+      if (b[2] > x0 && b[2] < x1) xs.push_back(b[2]);
+      if (b[1] > y0 && b[1] < y1) ys.push_back(b[1]);
+      if (b[3] > y0 && b[3] < y1) ys.push_back(b[3]);
+    }
+    std::sort(xs.begin(), xs.end());
+    xs.erase(std::unique(xs.begin(), xs.end()), xs.end());
+    std::sort(ys.begin(), ys.end());
+    ys.erase(std::unique(ys.begin(), ys.end()), ys.end());
+    bool covered = true;
+    for (size_t i = 0; covered && i + 1 < xs.size(); ++i)
+      for (size_t j = 0; covered && j + 1 < ys.size(); ++j) {
+        bool any = false;
+        for (int32_t k : kv.second) {
+          const auto& b = regs[k];
+          if (b[0] <= xs[i] && xs[i + 1] <= b[2] && b[1] <= ys[j] && ys[j + 1] <= b[3]) { any = true; break; }
+        }
+        covered = any;
+      }
+    if (covered) table[cell] = 3;
+  }
+}
+
 // Cell classes and candidate lists for a set of query objects with base cell rects B_o
 // (a query point's cell, or every cell under a polygon's bbox -- Polygon.java:62).
-int build_table(gf_range_plan* P, const std::vector<Rect>& base, bool need_lists) {
+int build_table(gf_range_plan* P, const std::vector<Rect>& base, bool need_lists,
+                const std::vector<std::array<double, 4>>* inside = nullptr) {
   gf_ctx* ctx = P->ctx;
   const int64_t n = P->grid.n;
   const int32_t g = P->g_layers, c = P->c_layers;
-  if (n * n > (int64_t)1 << 30) return set_err(ctx, GF_ERR_ARG, "grid too large for a cell table");
+  if (n * n > (int64_t)1 << 30 || n > 16384) return set_err(ctx, GF_ERR_ARG, "grid too large for a cell table");
   std::vector<int32_t> dG((n + 1) * (n + 1), 0), dC((n + 1) * (n + 1), 0);
   std::vector<int32_t> extra;
   for (const Rect& b : base) {
@@ -454,8 +531,40 @@ int build_table(gf_range_plan* P, const std::vector<Rect>& base, bool need_lists
       const int64_t i = y * (n + 1) + x;
       table[y * n + x] = dG[i] > 0 ? 2 : (dC[i] > 0 ? 1 : 0);
     }
+  if (inside && P->r >= 0.0)
+    mark_inside(P, table, *inside);
+  for (uint8_t v : table) P->cls_cells[v & 3]++;
+  std::vector<uint32_t> rows(n);
+  for (int64_t y = 0; y < n; ++y) {
+    int64_t lo = n, hi = -1;
+    for (int64_t x = 0; x < n; ++x)
+      if (table[y * n + x]) { lo = std::min(lo, x); hi = std::max(hi, x); }
+    rows[y] = hi < 0 ? 0xffffu : (uint32_t)lo | ((uint32_t)hi << 16);  // empty: lo 65535 > hi 0
+  }
+  std::vector<uint32_t> rowoff(n);
+  std::vector<uint8_t> spans;
+  for (int64_t y = 0; y < n; ++y) {
+    rowoff[y] = (uint32_t)spans.size();
+    const int64_t lo = rows[y] & 0xffffu, hi = rows[y] >> 16;
+    for (int64_t x = lo; x <= hi; ++x) spans.push_back(table[y * n + x]);
+  }
+  P->span_bytes = (int64_t)spans.size();
+  while (spans.size() % 4) spans.push_back(0);
+  if (spans.empty()) spans.assign(4, 0);
   int st;
-  if ((st = upload(ctx, &P->table, table))) return st;
+  if ((st = upload(ctx, &P->table, table)) || (st = upload(ctx, &P->rows, rows)) ||
+      (st = upload(ctx, &P->rowoff, rowoff)) || (st = upload(ctx, &P->spans, spans)))
+    return st;
+  if (n <= 2048) {  // division-free cells in the scan (thresholds staged in LDS)
+    std::vector<double> xt(n + 1), yt(n + 1);
+    for (int64_t c = 0; c <= n; ++c) {
+      xt[c] = first_at_least(c, P->grid.minX, P->grid.cellLength);
+      yt[c] = first_at_least(c, P->grid.minY, P->grid.cellLength);
+    }
+    P->x_lo = xt[0]; P->x_hi = xt[n]; P->y_lo = yt[0]; P->y_hi = yt[n];
+    if ((st = upload(ctx, &P->xt, xt)) || (st = upload(ctx, &P->yt, yt))) return st;
+  }
+
   P->n_extra = (int32_t)(extra.size() / 4);
   if ((st = upload(ctx, &P->extra, extra))) return st;
   if (!need_lists) return GF_OK;
@@ -485,7 +594,7 @@ int build_table(gf_range_plan* P, const std::vector<Rect>& base, bool need_lists
       for (int64_t y = r.y0; y <= r.y1; ++y)
         for (int64_t x = r.x0; x <= r.x1; ++x) {
           const int64_t cell = y * n + x;
-          if (table[cell] != 1) continue;
+          if (table[cell] != 1 && table[cell] != 3) continue;
           if (pass == 0) off[cell + 1]++;
           else lst[cur[cell]++] = (int32_t)o;
         }
@@ -499,10 +608,17 @@ int build_table(gf_range_plan* P, const std::vector<Rect>& base, bool need_lists
   return GF_OK;
 }
 
+// row-span class tables up to this size are staged in LDS by every scan block
+constexpr int64_t kSpanLdsBytes = 32768;
+
+// scan blocks (<= 8 per CU) + deferred-test blocks (8 per CU) of per-block partial counts
 int finish_plan(gf_range_plan* P) {
-  GF_HIP_CHECK(P->ctx, hipMalloc(&P->partials, sizeof(uint64_t) * 2 * (size_t)P->ctx->num_cus * 8));
+  GF_HIP_CHECK(P->ctx, hipMalloc(&P->partials, sizeof(uint64_t) * 2 * (size_t)P->ctx->num_cus * 16));
+  GF_HIP_CHECK(P->ctx, hipMalloc(&P->queue_count, sizeof(uint32_t) * (size_t)P->ctx->num_cus * 8));
   return GF_OK;
 }
+
+
 
 }  // namespace
 
@@ -511,7 +627,8 @@ extern "C" void gf_range_plan_destroy(gf_range_plan* P) {
   hipSetDevice(P->ctx->device);
   hipStreamSynchronize(P->ctx->stream);
   void* bufs[] = {P->table, P->extra, P->cand_off, P->cand_list, P->qx, P->qy, P->ring_off, P->vert_off,
-                  P->vx, P->vy, P->bbox, P->ring_env, P->partials};
+                  P->vx, P->vy, P->bbox, P->ring_env, P->partials, P->queue, P->queue_count, P->queue_xy, P->rows, P->xt, P->yt,
+                  P->rowoff, P->spans};
   for (void* b : bufs)
     if (b) hipFree(b);
   delete P;
@@ -607,7 +724,28 @@ extern "C" int gf_range_ppoly_plan_create(gf_ctx* ctx, const gf_grid* g, const g
     base[p] = {cell_index(x1, g->minX, g->cellLength), cell_index(x2, g->minX, g->cellLength),
                cell_index(y1, g->minY, g->cellLength), cell_index(y2, g->minY, g->cellLength)};
   }
-  if ((st = build_table(P, base, true))) { gf_range_plan_destroy(P); return st; }
+  // regions at distance 0 from each of their points: approximate mode -> every bbox;
+  // exact mode -> shells that are axis-aligned rectangles without holes
+  std::vector<std::array<double, 4>> inside;
+  for (int32_t p = 0; p < np; ++p) {
+    const double x1 = bbox[4 * p], y1 = bbox[4 * p + 1], x2 = bbox[4 * p + 2], y2 = bbox[4 * p + 3];
+    if (!(x1 < x2 && y1 < y2)) continue;
+    bool rect = P->approx != 0;
+    if (!rect && polys->ring_off[p + 1] - polys->ring_off[p] == 1) {
+      const int32_t v0 = polys->vert_off[polys->ring_off[p]], v1 = polys->vert_off[polys->ring_off[p] + 1];
+      int corners = 0;
+      rect = (v1 - v0 == 5);
+      for (int32_t v = v0; rect && v < v1; ++v) {
+        const double X = polys->vx[v], Y = polys->vy[v];
+        rect = (X == x1 || X == x2) && (Y == y1 || Y == y2);
+        if (rect && v > v0) rect = (X == polys->vx[v - 1]) != (Y == polys->vy[v - 1]);  // one axis moves
+        if (rect && v < v1 - 1) corners |= 1 << ((X == x2) + 2 * (Y == y2));
+      }
+      rect = rect && corners == 15;
+    }
+    if (rect) inside.push_back({x1, y1, x2, y2});
+  }
+  if ((st = build_table(P, base, true, &inside))) { gf_range_plan_destroy(P); return st; }
   const int32_t nverts = nrings > 0 ? polys->vert_off[nrings] : 0;
   std::vector<int32_t> ro(polys->ring_off, polys->ring_off + np + 1), vo(polys->vert_off, polys->vert_off + nrings + 1);
   std::vector<double> vx(polys->vx, polys->vx + nverts), vy(polys->vy, polys->vy + nverts);
@@ -638,16 +776,69 @@ extern "C" int gf_range_run(gf_range_plan* P, const gf_points* pts, uint64_t* bi
   a.nq = P->nq;
   a.qr = P->qr;
   a.grid_n = P->grid.n; a.minX = P->grid.minX; a.minY = P->grid.minY; a.cl = P->grid.cellLength;
-  a.table = P->table; a.extra = P->extra; a.n_extra = P->n_extra;
+  a.table = P->table; a.rows = P->rows; a.extra = P->extra; a.n_extra = P->n_extra;
+  a.rowoff = P->rowoff; a.spans = P->spans; a.span_bytes = (int32_t)std::min<int64_t>(P->span_bytes, INT32_MAX);
+  a.span_lds = P->span_bytes <= kSpanLdsBytes;
+  a.xt = P->xt; a.yt = P->yt; a.x_lo = P->x_lo; a.x_hi = P->x_hi; a.y_lo = P->y_lo; a.y_hi = P->y_hi;
+  a.inv_cl = 1.0 / P->grid.cellLength;
   a.cand_off = P->cand_off; a.cand_list = P->cand_list;
   a.approx = P->approx; a.metric = P->metric; a.r = P->r; a.s_r = s_prefilter(P->r, 0);
   a.qx0 = P->qx0; a.qy0 = P->qy0;
   a.qx = P->qx; a.qy = P->qy;
   a.npoly = P->npoly; a.ring_off = P->ring_off; a.vert_off = P->vert_off; a.vx = P->vx; a.vy = P->vy;
   a.bbox = P->bbox; a.ring_env = P->ring_env;
-  const int blocks = stream_blocks(ctx, (pts->n + 1) / 2);
+  // every wave should run >= 2 pipeline stages of kRangeU tiles (range_kernel); at most 4
+  // blocks per CU (the sweep in tools/bench_workloads.py: 1024 blocks best at 10M points)
+  int blocks = (int)std::min<int64_t>(std::max<int64_t>(pts->n / (4 * 128 * 2 * 2), 1), (int64_t)ctx->num_cus * 4);
+  if (P->scan_blocks > 0) blocks = P->scan_blocks;
+  blocks = std::min(blocks, 2048);  // range_test_kernel's segment prefix (kMaxSegs)
+  // Deferred tests pay a second launch; inline tests stall the waves holding candidate lanes.
+  // Auto: defer while candidate cells are more than 5% of the non-none cells.
+  const int64_t live = P->cls_cells[1] + P->cls_cells[2] + P->cls_cells[3];
+  const bool can_defer = P->table_mode && (P->poly || !P->approx);
+  const bool defer = can_defer && (P->defer_mode == 2 || (P->defer_mode == 0 && P->cls_cells[1] * 20 > live));
+  if (defer) {
+    // a scan block visits at most 2 points per thread per grid sweep
+    const int64_t tstride = (int64_t)blocks * kBlock * 2;
+    a.seg_cap = 2 * kBlock * ((pts->n + tstride - 1) / tstride);
+    const int64_t need = a.seg_cap * blocks;
+    if (P->queue_cap < need) {
+      GF_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+      if (P->queue) GF_HIP_CHECK(ctx, hipFree(P->queue));
+      if (P->queue_xy) GF_HIP_CHECK(ctx, hipFree(P->queue_xy));
+      P->queue = nullptr;
+      P->queue_xy = nullptr;
+      P->queue_cap = 0;
+      GF_HIP_CHECK(ctx, hipMalloc(&P->queue, sizeof(uint32_t) * (size_t)need));
+      GF_HIP_CHECK(ctx, hipMalloc(&P->queue_xy, 2 * sizeof(double) * (size_t)need));
+      P->queue_cap = need;
+    }
+    a.queue = P->queue;
+    a.queue_xy = P->queue_xy;
+    a.queue_count = P->queue_count;
+    a.test_blocks = ctx->num_cus * 8;
+  }
   GF_HIP_CHECK(ctx, launch_range(ctx, a, P->table_mode, P->poly, blocks));
-  if (counts) GF_HIP_CHECK(ctx, launch_range_finalize(ctx->stream, P->partials, blocks, counts));
+  if (counts)
+    GF_HIP_CHECK(ctx, launch_range_finalize(ctx->stream, P->partials, blocks + (defer ? a.test_blocks : 0), counts));
+  return GF_OK;
+}
+
+extern "C" int gf_range_plan_stats(const gf_range_plan* P, int64_t* none_cells, int64_t* candidate_cells,
+                                   int64_t* guaranteed_cells, int64_t* inside_cells) {
+  if (!P) return GF_ERR_ARG;
+  if (none_cells) *none_cells = P->cls_cells[0];
+  if (candidate_cells) *candidate_cells = P->cls_cells[1];
+  if (guaranteed_cells) *guaranteed_cells = P->cls_cells[2];
+  if (inside_cells) *inside_cells = P->cls_cells[3];
+  return GF_OK;
+}
+
+extern "C" int gf_range_plan_set_tuning(gf_range_plan* P, int32_t scan_blocks, int32_t defer_mode) {
+  if (!P || scan_blocks < 0 || scan_blocks > P->ctx->num_cus * 8 || defer_mode < 0 || defer_mode > 2)
+    return GF_ERR_ARG;
+  P->scan_blocks = scan_blocks;
+  P->defer_mode = defer_mode;
   return GF_OK;
 }
 

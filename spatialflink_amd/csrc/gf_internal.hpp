@@ -145,7 +145,16 @@ struct RangeArgs {
   // table classification
   int32_t grid_n;
   double minX, minY, cl;
-  const uint8_t* table;      // [n*n]: 0 none, 1 test, 2 accept
+  const uint8_t* table;      // [n*n]: 0 none, 1 test, 2 accept, 3 inside (accept unless NaN)
+  const uint32_t* rows;      // [n] first | last << 16 column of a non-none class per row
+  const uint32_t* rowoff;    // [n] offset of each row's span in `spans`
+  const uint8_t* spans;      // class table restricted to the row spans (concatenated)
+  int32_t span_bytes;
+  int32_t span_lds;          // spans small enough to stage in LDS
+  const double* xt;          // [n+1] exact thresholds first_at_least(c) per axis (n <= 2048; else null)
+  const double* yt;
+  double x_lo, x_hi, y_lo, y_hi;  // xt[0], xt[n], yt[0], yt[n]
+  double inv_cl;
   const int32_t* extra;      // [n_extra*4]: x0, x1, y0, y1 (inclusive) accepted out-of-grid cells
   int32_t n_extra;
   const int32_t* cand_off;   // [n*n+1] objects to test per cell (CSR); null => test all
@@ -164,6 +173,12 @@ struct RangeArgs {
   const double* vy;
   const double* bbox;        // [npoly*4] x1, y1, x2, y2 (shell envelope)
   const double* ring_env;    // [nrings*4] minx, maxx, miny, maxy
+  // deferred candidate tests (table modes): scan appends, range_test_kernel drains
+  uint32_t* queue;           // [blocks * seg_cap] point indices, a segment per scan block; null => inline
+  uint32_t* queue_count;     // [blocks] entries per segment
+  double* queue_xy;          // [2 * blocks * seg_cap] the queued points' coordinates
+  int64_t seg_cap;           // points one scan block visits at most
+  int test_blocks;
 };
 
 // launchers (return hipError_t of the launch)
@@ -230,6 +245,13 @@ struct gf_range_plan {
   double qx0 = 0, qy0 = 0;
   // device buffers (owned)
   uint8_t* table = nullptr;
+  uint32_t* rows = nullptr;
+  uint32_t* rowoff = nullptr;
+  uint8_t* spans = nullptr;
+  int64_t span_bytes = 0;
+  double* xt = nullptr;            // exact cell thresholds (table modes, n <= 2048)
+  double* yt = nullptr;
+  double x_lo = 0, x_hi = 0, y_lo = 0, y_hi = 0;
   int32_t* extra = nullptr;
   int32_t n_extra = 0;
   int32_t* cand_off = nullptr;
@@ -245,6 +267,13 @@ struct gf_range_plan {
   double* ring_env = nullptr;
   uint64_t* partials = nullptr;
   int blocks = 0;
+  uint32_t* queue = nullptr;       // deferred candidate tests (grown to blocks x seg_cap)
+  double* queue_xy = nullptr;
+  int64_t queue_cap = 0;
+  uint32_t* queue_count = nullptr; // [num_cus * 8] per-segment counts
+  int64_t cls_cells[4] = {0, 0, 0, 0};  // in-grid cells per class (diagnostics)
+  int32_t scan_blocks = 0;         // tuning: 0 = auto
+  int32_t defer_mode = 0;          // tuning: 0 auto, 1 test inline, 2 defer
 };
 
 struct gf_knn_plan {

@@ -158,21 +158,83 @@ __device__ double point_bbox_distance(double x, double y, const double* bb) {
 }
 
 // ---------------- classification --------------------------------------------------------
-constexpr int kNone = 0, kTest = 1, kAccept = 2;
+// kInside: a candidate cell lying wholly inside a closed region whose every point is at
+// distance 0 (an axis-aligned rectangle polygon, or any polygon's bbox in approximate mode);
+// accepted without a test for non-NaN coordinates (d = 0 <= r, r >= 0).
+constexpr int kNone = 0, kTest = 1, kAccept = 2, kInside = 3;
+
+// Table modes: rows[cy] packs the first / last column of row cy whose class is not kNone
+// (staged in LDS), so points of a row outside that span never touch the n*n class table (a
+// per-point L2 gather: at 10M points the L2 request rate, not HBM, bounded the scan).
+// Two phases so that a wave's table gathers overlap: cell_slot() computes the cell (-1 when
+// outside the grid, -2 when outside its row's span) without touching memory; the caller then
+// issues every gather of the iteration (an unconditional load from a clamped address: a load
+// under a branch would be waited on inside the branch) and only then finishes the classes.
+// Exact cell of an in-grid coordinate without a division: c = trunc((v - mn) / cl) computed
+// with 1/cl is within one of the exact cell (relative error ~2^-52 on values < n <= 2048), and
+// the exact per-axis thresholds T[c] = first_at_least(c) (host-built, staged in LDS) fix it.
+__device__ __forceinline__ int32_t fast_cell(double v, double mn, double inv_cl, const double* T, int32_t n) {
+  int32_t c = (int32_t)((v - mn) * inv_cl);
+  c = c < 0 ? 0 : (c > n - 1 ? n - 1 : c);
+  return c - (v < T[c] ? 1 : 0) + (v >= T[c + 1] ? 1 : 0);
+}
+
+// Block-local copies of the plan's lookup tables (LDS).
+struct RangeLds {
+  const uint32_t* rows;    // [n] span of row cy: first | last << 16 non-none column
+  const uint32_t* rowoff;  // [n] offset of row cy's span in `spans`
+  const uint8_t* spans;    // the class table restricted to the row spans (null: use a.table)
+  const double* tx;        // [n+1] exact thresholds per axis (null: divide)
+  const double* ty;
+};
 
 template <int TABLE>
-__device__ __forceinline__ int classify(const RangeArgs& a, double px, double py, int32_t& cell) {
+__device__ __forceinline__ int32_t cell_slot(const RangeArgs& a, const RangeLds& L, double px, double py) {
+  if (!TABLE) return 0;
+#ifdef GF_EXP_NOCELL
+  if (px > 1e300) return 5;
+  return -2;
+#endif
+  const int32_t n = a.grid_n;
+  int32_t cx, cy;
+  if (L.tx) {
+    // in grid on both axes <=> T[0] <= v < T[n] (NaN fails: it takes the slow path below)
+    if (!(px >= a.x_lo && px < a.x_hi && py >= a.y_lo && py < a.y_hi)) return -1;
+    cx = fast_cell(px, a.minX, a.inv_cl, L.tx, n);
+    cy = fast_cell(py, a.minY, a.inv_cl, L.ty, n);
+  } else {
+    cx = cell_index(px, a.minX, a.cl);
+    cy = cell_index(py, a.minY, a.cl);
+    if (!(cx >= 0 && cy >= 0 && cx < n && cy < n)) return -1;
+  }
+  const uint32_t span = L.rows[cy];
+  const int32_t lo = (int32_t)(span & 0xffffu);
+  if (cx < lo || cx > (int32_t)(span >> 16)) return -2;
+  return L.spans ? (int32_t)L.rowoff[cy] + (cx - lo) : cy * n + cx;
+}
+__device__ __forceinline__ int table_load(const RangeArgs& a, const RangeLds& L, int32_t slot) {
+  if (L.spans) return L.spans[slot < 0 ? 0 : slot];
+  return a.table[slot < 0 ? 0 : slot];
+}
+template <int TABLE>
+__device__ __forceinline__ int classify_finish(const RangeArgs& a, double px, double py, int32_t slot, int tv) {
   if (!TABLE) {
     const double xs = (px == px) ? px : a.qr.minX;
     const double ys = (py == py) ? py : a.qr.minY;
     if (a.qr.g_any && in_iv(a.qr.gx, xs) && in_iv(a.qr.gy, ys)) return kAccept;
     return (in_iv(a.qr.cgx, xs) && in_iv(a.qr.cgy, ys)) ? kTest : kNone;
   }
+  if (slot >= 0) {
+    if (tv != kInside) return tv;
+    return (px == px && py == py) ? kAccept : kTest;  // NaN lands in cell 0 (Java (int)NaN == 0)
+  }
+  if (slot == -2) return kNone;
   const int32_t cx = cell_index(px, a.minX, a.cl);
   const int32_t cy = cell_index(py, a.minY, a.cl);
-  if (cx >= 0 && cy >= 0 && cx < a.grid_n && cy < a.grid_n) {
-    cell = cy * a.grid_n + cx;
-    return a.table[cell];
+  const int32_t n = a.grid_n;
+  if (cx >= 0 && cy >= 0 && cx < n && cy < n) {  // only NaN coordinates get here in grid
+    const int c = a.table[cy * n + cx];
+    return c == kInside ? kTest : c;
   }
   for (int e = 0; e < a.n_extra; ++e) {
     const int32_t* r = a.extra + 4 * e;
@@ -181,9 +243,27 @@ __device__ __forceinline__ int classify(const RangeArgs& a, double px, double py
   return kNone;
 }
 
-// candidate-cell test: exists object within r (first hit wins, emitted once)
+// Envelope prune for the exact point-polygon test.  The computed point-polygon distance of a
+// point outside the (closed) shell envelope is a min of computed point-segment distances, each
+// within ~16 eps x (coordinate scale) of a true distance >= the true envelope distance; the
+// margin (1e-12 relative to the coordinates, 1e-9 relative to r) exceeds that by orders of
+// magnitude, so a pruned polygon could never have tested <= r.
+__device__ __forceinline__ bool env_far(const double* bb, double px, double py, double r) {
+  const double dx = px < bb[0] ? bb[0] - px : (px > bb[2] ? px - bb[2] : 0.0);
+  const double dy = py < bb[1] ? bb[1] - py : (py > bb[3] ? py - bb[3] : 0.0);
+  const double scale = fabs(px) + fabs(py) + fabs(bb[0]) + fabs(bb[1]) + fabs(bb[2]) + fabs(bb[3]);
+  const double rm = r + r * 1e-9 + scale * 1e-12;
+  return dx > rm || dy > rm || dx * dx + dy * dy > rm * rm;
+}
+__device__ __forceinline__ bool env_holds(const double* bb, double px, double py) {
+  return px >= bb[0] && px <= bb[2] && py >= bb[1] && py <= bb[3];
+}
+
+// candidate-cell test: exists object within r (first hit wins, emitted once).  The answer is
+// an existential over the cell's object list, so visiting order is free: polygons whose
+// envelope holds the point go first, polygons whose envelope is farther than r are skipped.
 template <int TABLE, int POLY>
-__device__ __forceinline__ bool test_point(const RangeArgs& a, double px, double py, int32_t cell) {
+__device__ __forceinline__ bool test_point(const RangeArgs& a, double px, double py) {
   if (!POLY && !TABLE) {  // single query point: exact s <= smax(r) for the sqrt metric
     const double dx = a.qx0 - px, dy = a.qy0 - py;
     if (a.metric == 0) return dx * dx + dy * dy <= a.s_r;
@@ -192,111 +272,392 @@ __device__ __forceinline__ bool test_point(const RangeArgs& a, double px, double
   int32_t b = 0, e = POLY ? a.npoly : a.nq;
   const int32_t* lst = nullptr;
   if (a.cand_off) {
+    const int32_t cell = cell_index(py, a.minY, a.cl) * a.grid_n + cell_index(px, a.minX, a.cl);
     b = a.cand_off[cell];
     e = a.cand_off[cell + 1];
     lst = a.cand_list;
   }
-  for (int32_t t = b; t < e; ++t) {
-    const int32_t o = lst ? lst[t] : t;
-    if (POLY) {
-      const double d = a.approx ? point_bbox_distance(px, py, a.bbox + 4 * o) : point_polygon_distance(px, py, a, o);
-      if (d <= a.r) return true;
-    } else {
-      if (distance(a.qx[o], a.qy[o], px, py, a.metric) <= a.r) return true;
+  if (!POLY) {
+    for (int32_t t = b; t < e; ++t) {
+      const int32_t o = lst ? lst[t] : t;
+      const double dx = a.qx[o] - px, dy = a.qy[o] - py;
+      if (a.metric == 0 ? (dx * dx + dy * dy <= a.s_r) : (fdlibm_hypot(dx, dy) <= a.r)) return true;
     }
+    return false;
+  }
+  if (a.approx) {
+    for (int32_t t = b; t < e; ++t) {
+      const int32_t o = lst ? lst[t] : t;
+      if (point_bbox_distance(px, py, a.bbox + 4 * o) <= a.r) return true;
+    }
+    return false;
+  }
+  const bool finite = px == px && py == py;
+  if (finite) {
+    for (int32_t t = b; t < e; ++t) {  // pass 1: envelopes holding the point (usually a hit)
+      const int32_t o = lst ? lst[t] : t;
+      if (env_holds(a.bbox + 4 * o, px, py) && point_polygon_distance(px, py, a, o) <= a.r) return true;
+    }
+  }
+  for (int32_t t = b; t < e; ++t) {  // pass 2: the rest, envelope-pruned
+    const int32_t o = lst ? lst[t] : t;
+    const double* bb = a.bbox + 4 * o;
+    if (finite && (env_holds(bb, px, py) || env_far(bb, px, py, a.r))) continue;
+    if (point_polygon_distance(px, py, a, o) <= a.r) return true;
   }
   return false;
 }
 
-__device__ __forceinline__ uint64_t spread32(uint32_t v) {
-  uint64_t x = v;
-  x = (x | (x << 16)) & 0x0000FFFF0000FFFFull;
-  x = (x | (x << 8)) & 0x00FF00FF00FF00FFull;
-  x = (x | (x << 4)) & 0x0F0F0F0F0F0F0F0Full;
-  x = (x | (x << 2)) & 0x3333333333333333ull;
-  x = (x | (x << 1)) & 0x5555555555555555ull;
-  return x;
-}
 
-template <int TABLE, int POLY>
-__device__ __forceinline__ void eval_point(const RangeArgs& a, double px, double py, bool valid, bool& hit,
-                                           bool& multi) {
+// DEFER: candidate-cell points are not tested inline (a wave would serialise on its slowest
+// lane's object list) but appended to a queue that range_test_kernel drains densely.
+template <int TABLE, int POLY, int DEFER>
+__device__ __forceinline__ void eval_point(const RangeArgs& a, double px, double py, int cls, bool valid, bool& hit,
+                                           bool& multi, bool& defer) {
   hit = false;
   multi = false;
+  defer = false;
   if (!valid) return;
-  int32_t cell = 0;
-  const int cls = classify<TABLE>(a, px, py, cell);
   if (cls == kAccept) {
     hit = true;
   } else if (cls == kTest) {
     if (!POLY && a.approx) {  // approximate point-point: emitted once per query point
       hit = true;
       multi = a.nq > 1;
+    } else if (DEFER) {
+      defer = true;
     } else {
-      hit = test_point<TABLE, POLY>(a, px, py, cell);
+      hit = test_point<TABLE, POLY>(a, px, py);
     }
   }
 }
 
-template <int TABLE, int POLY>
-__global__ __launch_bounds__(kBlock) void range_kernel(RangeArgs a) {
-  const int64_t npairs = (a.n + 1) >> 1;
-  const int64_t words = (a.n + 63) >> 6;
+// Per-block queue segments: a wave reserves slots with one LDS atomic (a single global
+// counter would serialise ~10^5 wave atomics on one L2 line).
+__device__ __forceinline__ void queue_append(bool c, uint32_t idx, double px, double py, const RangeArgs& a,
+                                             uint32_t* lcount) {
+#ifdef GF_EXP_NOAPPEND
+  return;
+#endif
+  const uint64_t m = __ballot(c);
+  if (m == 0) return;
   const int lane = threadIdx.x & 63;
+  const int leader = __ffsll((unsigned long long)m) - 1;
+  uint32_t base = 0;
+  if (lane == leader) base = atomicAdd(lcount, (uint32_t)__popcll(m));
+  base = __shfl(base, leader, 64);
+  if (c) {
+    const size_t pos = (size_t)blockIdx.x * a.seg_cap + base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+    a.queue[pos] = idx;
+    a.queue_xy[2 * pos] = px;  // the test kernel reads the coordinates back contiguously
+    a.queue_xy[2 * pos + 1] = py;
+  }
+}
+
+// One wave-tile = 128 consecutive points = bitmap words w, w+1: lane l evaluates points
+// t + l and t + 64 + l, so the two ballots ARE the two words (one 16-B store by lane 0).
+template <int TABLE, int POLY, int DEFER, bool FULL>
+__device__ __forceinline__ void range_tile(const RangeArgs& a, int64_t t, double x0, double y0, double x1, double y1,
+                                           int c0, int c1, uint64_t& hits, uint64_t& mult, uint32_t* lcount) {
+  const int lane = threadIdx.x & 63;
+  const int64_t i0 = t + lane, i1 = t + 64 + lane;
+  const bool v0 = FULL || i0 < a.n, v1 = FULL || i1 < a.n;
+  bool h0, h1, m0, m1, d0, d1;
+  eval_point<TABLE, POLY, DEFER>(a, x0, y0, c0, v0, h0, m0, d0);
+  eval_point<TABLE, POLY, DEFER>(a, x1, y1, c1, v1, h1, m1, d1);
+  const uint64_t b0 = __ballot(h0), b1 = __ballot(h1);
+  const int64_t w = t >> 6;
+  if (lane == 0) {  // the caller's bitmap is only 8-B aligned
+    a.bitmap[w] = b0;
+    if (FULL || t + 64 < a.n) a.bitmap[w + 1] = b1;
+  }
+  if (a.multi) {
+    const uint64_t e0 = __ballot(m0), e1 = __ballot(m1);
+    if (lane == 0) {
+      a.multi[w] = e0;
+      if (FULL || t + 64 < a.n) a.multi[w + 1] = e1;
+    }
+    mult += (uint64_t)(__popcll(e0) + __popcll(e1));
+  }
+  if (DEFER) {
+    queue_append(d0, (uint32_t)i0, x0, y0, a, lcount);
+    queue_append(d1, (uint32_t)i1, x1, y1, a, lcount);
+  }
+  hits += (uint64_t)(__popcll(b0) + __popcll(b1));
+}
+
+// Main loop: every wave runs the same number of full U-tile iterations with unchecked
+// nontemporal 16-B loads (x, y are read once); the remainder goes through the checked tail.
+// All U tiles are classified (the table-mode cell-class gathers are independent loads that
+// overlap) before any tile stores, so U tiles' latencies overlap instead of adding up.
+// U tiles of one wave: coordinates of points t_u + lane and t_u + 64 + lane.  Loads clamp
+// the index to n - 1, so tiles past the end (the pipeline's last prefetch, a partial last
+// tile) read valid memory and are masked afterwards.
+template <int U>
+struct RangeBuf {
+  double xa[U], ya[U], xb[U], yb[U];
+};
+template <int U>
+__device__ __forceinline__ void range_load(RangeBuf<U>& b, const RangeArgs& a, int64_t t, int64_t tstride) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t last = (uint32_t)(a.n - 1);
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t tu = t + u * tstride;
+    const uint32_t i0 = tu + lane < a.n ? (uint32_t)(tu + lane) : last;
+    const uint32_t i1 = tu + 64 + lane < a.n ? (uint32_t)(tu + 64 + lane) : last;
+    b.xa[u] = __builtin_nontemporal_load(a.x + i0);
+    b.xb[u] = __builtin_nontemporal_load(a.x + i1);
+    b.ya[u] = __builtin_nontemporal_load(a.y + i0);
+    b.yb[u] = __builtin_nontemporal_load(a.y + i1);
+  }
+}
+
+// One pipeline stage: classify the U tiles of `cur` (issuing the class-table gathers first),
+// then issue the loads of `nxt`, then finish -- so the gathers are waited on (vmcnt is in
+// order) while the next stage's tiles stay in flight.
+template <int TABLE, int POLY, int DEFER, int U>
+__device__ __forceinline__ void range_stage(const RangeArgs& a, const RangeLds& L, const RangeBuf<U>& cur, int64_t t, RangeBuf<U>& nxt,
+                                            int64_t tn, int64_t tstride, uint64_t& hits, uint64_t& mult,
+                                            uint32_t* lcount) {
+  int32_t s0[U], s1[U];
+  int c0[U], c1[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    s0[u] = cell_slot<TABLE>(a, L, cur.xa[u], cur.ya[u]);
+    s1[u] = cell_slot<TABLE>(a, L, cur.xb[u], cur.yb[u]);
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    c0[u] = TABLE ? table_load(a, L, s0[u]) : 0;
+    c1[u] = TABLE ? table_load(a, L, s1[u]) : 0;
+  }
+  range_load<U>(nxt, a, tn, tstride);
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    c0[u] = classify_finish<TABLE>(a, cur.xa[u], cur.ya[u], s0[u], c0[u]);
+    c1[u] = classify_finish<TABLE>(a, cur.xb[u], cur.yb[u], s1[u], c1[u]);
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t tu = t + u * tstride;
+#ifndef GF_EXP_ONETILE
+    if (tu + 128 <= a.n)
+      range_tile<TABLE, POLY, DEFER, true>(a, tu, cur.xa[u], cur.ya[u], cur.xb[u], cur.yb[u], c0[u], c1[u], hits,
+                                           mult, lcount);
+    else
+#endif
+    if (tu < a.n)
+      range_tile<TABLE, POLY, DEFER, false>(a, tu, cur.xa[u], cur.ya[u], cur.xb[u], cur.yb[u], c0[u], c1[u], hits,
+                                            mult, lcount);
+  }
+}
+
+#ifndef GF_RANGE_WAVES
+#define GF_RANGE_WAVES 1
+#endif
+template <int TABLE, int POLY, int DEFER, int U>
+__global__ __launch_bounds__(kBlock, GF_RANGE_WAVES) void range_kernel(RangeArgs a) {
+  const int64_t tstride = (int64_t)gridDim.x * (kBlock / 64) * 128;       // points per grid sweep
+  const int64_t t0 = ((int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * 128;
   uint64_t hits = 0, mult = 0;
-  for (int64_t base = (int64_t)blockIdx.x * kBlock + (threadIdx.x & ~63); base < npairs;
-       base += (int64_t)gridDim.x * kBlock) {
-    const int64_t i = 2 * (base + lane);
-    double2 xv, yv;
-    const bool v0 = i < a.n, v1 = i + 1 < a.n;
-    if (v1) {
-      xv = *reinterpret_cast<const double2*>(a.x + i);
-      yv = *reinterpret_cast<const double2*>(a.y + i);
-    } else if (v0) {
-      xv.x = a.x[i]; yv.x = a.y[i]; xv.y = yv.y = 0.0;
-    } else {
-      xv.x = xv.y = yv.x = yv.y = 0.0;
-    }
-    bool h0, h1, m0, m1;
-    eval_point<TABLE, POLY>(a, xv.x, yv.x, v0, h0, m0);
-    eval_point<TABLE, POLY>(a, xv.y, yv.y, v1, h1, m1);
-    const uint64_t b0 = __ballot(h0), b1 = __ballot(h1);
-    const int64_t w = base >> 5;  // 128 points per wave = 2 words
-    if (lane < 2 && w + lane < words) {
-      const uint32_t s0 = lane ? (uint32_t)(b0 >> 32) : (uint32_t)b0;
-      const uint32_t s1 = lane ? (uint32_t)(b1 >> 32) : (uint32_t)b1;
-      a.bitmap[w + lane] = spread32(s0) | (spread32(s1) << 1);
-    }
-    if (a.multi) {
-      const uint64_t c0 = __ballot(m0), c1 = __ballot(m1);
-      if (lane < 2 && w + lane < words) {
-        const uint32_t s0 = lane ? (uint32_t)(c0 >> 32) : (uint32_t)c0;
-        const uint32_t s1 = lane ? (uint32_t)(c1 >> 32) : (uint32_t)c1;
-        a.multi[w + lane] = spread32(s0) | (spread32(s1) << 1);
+  __shared__ uint32_t lcount;
+  // TABLE: LDS = rows[n] | rowoff[n] | (fast cells) 2 x (n+1) thresholds | (small) spans
+  extern __shared__ uint32_t lds[];
+  RangeLds L{nullptr, nullptr, nullptr, nullptr, nullptr};
+  if (DEFER || TABLE) {
+    if (threadIdx.x == 0) lcount = 0u;
+    if (TABLE) {
+      const int n = a.grid_n;
+      uint32_t* lr = lds;
+      uint32_t* lo = lds + n;
+      for (int j = threadIdx.x; j < n; j += kBlock) {
+        lr[j] = a.rows[j];
+        lo[j] = a.rowoff[j];
       }
-      mult += (uint64_t)(__popcll(c0) + __popcll(c1));
+      L.rows = lr;
+      L.rowoff = lo;
+      char* tail = reinterpret_cast<char*>(lds + ((2 * n + 1) & ~1));
+      if (a.xt) {
+        double* lt = reinterpret_cast<double*>(tail);
+        for (int j = threadIdx.x; j <= n; j += kBlock) {
+          lt[j] = a.xt[j];
+          lt[n + 1 + j] = a.yt[j];
+        }
+        L.tx = lt;
+        L.ty = lt + n + 1;
+        tail += 2 * sizeof(double) * (n + 1);
+      }
+      if (a.span_lds) {
+        uint32_t* ls = reinterpret_cast<uint32_t*>(tail);
+        const uint32_t* gs = reinterpret_cast<const uint32_t*>(a.spans);
+        for (int j = threadIdx.x; j < (a.span_bytes + 3) / 4; j += kBlock) ls[j] = gs[j];
+        L.spans = reinterpret_cast<const uint8_t*>(ls);
+      }
     }
-    hits += (uint64_t)(__popcll(b0) + __popcll(b1));
+    __syncthreads();
+  }
+  // this wave's tiles t0 + k * tstride, k < K; stages of U tiles, run in pairs (buffers A, B
+  // alternate, so no register copies -- and no wait -- sit on the loop's back edge)
+  const int64_t K = t0 < a.n ? (a.n - t0 + tstride - 1) / tstride : 0;
+  const int64_t pairs = (K + 2 * U - 1) / (2 * U);
+  const int64_t sstride = U * tstride;
+  RangeBuf<U> A, B;
+  if (pairs > 0) range_load<U>(A, a, t0, tstride);
+  for (int64_t p = 0; p < pairs; ++p) {
+    const int64_t ta = t0 + 2 * p * sstride;
+    range_stage<TABLE, POLY, DEFER, U>(a, L, A, ta, B, ta + sstride, tstride, hits, mult, &lcount);
+    range_stage<TABLE, POLY, DEFER, U>(a, L, B, ta + sstride, A, ta + 2 * sstride, tstride, hits, mult, &lcount);
   }
   // per-block partial counts (plain stores; summed by range_finalize)
   __shared__ uint64_t sh[kBlock / 64], sm[kBlock / 64];
   const int wid = threadIdx.x >> 6;
-  if (lane == 0) { sh[wid] = hits; sm[wid] = mult; }
+  if ((threadIdx.x & 63) == 0) { sh[wid] = hits; sm[wid] = mult; }
   __syncthreads();
   if (threadIdx.x == 0) {
     uint64_t th = 0, tm = 0;
     for (int w = 0; w < kBlock / 64; ++w) { th += sh[w]; tm += sm[w]; }
     a.partials[2 * blockIdx.x] = th;
     a.partials[2 * blockIdx.x + 1] = th + tm * (uint64_t)(a.nq > 1 ? a.nq - 1 : 0);
+    if (DEFER) a.queue_count[blockIdx.x] = lcount;
   }
 }
 
+// One candidate object of a queued point: within r?  (envelope-pruned for exact polygons)
+template <int POLY>
+__device__ __forceinline__ bool test_object(const RangeArgs& a, double px, double py, int32_t o) {
+  if (!POLY) {
+    const double dx = a.qx[o] - px, dy = a.qy[o] - py;
+    return a.metric == 0 ? (dx * dx + dy * dy <= a.s_r) : (fdlibm_hypot(dx, dy) <= a.r);
+  }
+  if (a.approx) return point_bbox_distance(px, py, a.bbox + 4 * o) <= a.r;
+  if (px == px && py == py && env_far(a.bbox + 4 * o, px, py, a.r)) return false;
+  return point_polygon_distance(px, py, a, o) <= a.r;
+}
+
+// Drains the candidate queue (the scan blocks' segments).  A queued point is a group of 8
+// lanes that test the point's candidate objects in parallel (8 at a time, stopping once one
+// hits), so the dependent chain per point is one object test, not the list length; and the
+// entries of all segments are dealt out over the whole grid (a block-local prefix of the
+// segment counts in LDS) so the queue is drained in one round of dependent loads.  Hits are
+// OR-ed into the bitmap the scan wrote (stream-ordered after it); partials go to slots
+// [part_base + block].
+constexpr int kTestGroup = 8;
+constexpr int kMaxSegs = 2048;  // scan blocks <= 8 per CU
+template <int POLY>
+__global__ __launch_bounds__(kBlock) void range_test_kernel(RangeArgs a, int part_base) {
+  __shared__ uint32_t pre[kMaxSegs + 1];
+  __shared__ uint32_t wsum[kBlock / 64];
+  const int lane = threadIdx.x & 63, g = lane & (kTestGroup - 1);
+  constexpr int kGroups = kBlock / kTestGroup;
+  const int grp = threadIdx.x / kTestGroup;
+  const uint64_t gmask = ((1ull << kTestGroup) - 1) << (lane & ~(kTestGroup - 1));
+  // exclusive prefix of the segment counts (kMaxSegs / kBlock = 8 per thread)
+  constexpr int kPer = kMaxSegs / kBlock;
+  uint32_t v[kPer], sum = 0;
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    const int sgi = threadIdx.x * kPer + j;
+    v[j] = sgi < part_base ? a.queue_count[sgi] : 0u;
+    sum += v[j];
+  }
+  uint32_t inc = sum;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t t = __shfl_up(inc, off, 64);
+    if (lane >= off) inc += t;
+  }
+  if (lane == 63) wsum[threadIdx.x >> 6] = inc;
+  __syncthreads();
+  uint32_t run = inc - sum;
+  for (int w = 0; w < (int)(threadIdx.x >> 6); ++w) run += wsum[w];
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    pre[threadIdx.x * kPer + j] = run;
+    run += v[j];
+  }
+  if (threadIdx.x == kBlock - 1) pre[kMaxSegs] = run;
+  __syncthreads();
+  const uint32_t total = pre[kMaxSegs];
+  uint64_t hits = 0;
+  for (uint32_t e0 = blockIdx.x * kGroups; e0 < total; e0 += gridDim.x * kGroups) {  // block-uniform
+    const uint32_t e = e0 + grp;
+    const bool valid = e < total;
+    size_t pos = 0;
+    double px = 0.0, py = 0.0;
+    int32_t b = 0, end = 0;
+    if (valid) {
+      int lo = 0, hi = kMaxSegs;  // last segment with pre[seg] <= e
+      while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (pre[mid] <= e) lo = mid; else hi = mid;
+      }
+      pos = (size_t)lo * a.seg_cap + (e - pre[lo]);
+      px = a.queue_xy[2 * pos];
+      py = a.queue_xy[2 * pos + 1];
+      end = POLY ? a.npoly : a.nq;
+      if (a.cand_off) {
+        const int32_t cell = cell_index(py, a.minY, a.cl) * a.grid_n + cell_index(px, a.minX, a.cl);
+        b = a.cand_off[cell];
+        end = a.cand_off[cell + 1];
+      }
+    }
+    bool hit = false;
+    for (int32_t t = b + g;; t += kTestGroup) {
+      const uint64_t hb = __ballot(hit);  // all lanes: the loop is wave-uniform
+      const bool mine = t < end && !(hb & gmask);
+      if (!__ballot(mine)) break;  // every group of the wave is done
+      if (mine) hit = test_object<POLY>(a, px, py, a.cand_off ? a.cand_list[t] : t);
+    }
+    const bool ghit = (__ballot(hit) & gmask) != 0;
+    if (valid && g == 0 && ghit) {
+      const uint32_t i = a.queue[pos];
+      atomicOr((unsigned long long*)&a.bitmap[i >> 6], 1ull << (i & 63));
+      ++hits;
+    }
+  }
+  __shared__ uint64_t sh[kBlock];
+  sh[threadIdx.x] = hits;
+  __syncthreads();
+  for (int s = kBlock / 2; s > 0; s >>= 1) {
+    if (threadIdx.x < s) sh[threadIdx.x] += sh[threadIdx.x + s];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    a.partials[2 * (part_base + blockIdx.x)] = sh[0];
+    a.partials[2 * (part_base + blockIdx.x) + 1] = sh[0];
+  }
+}
+
+#ifndef GF_RANGE_U
+#define GF_RANGE_U 2
+#endif
+constexpr int kRangeU = GF_RANGE_U;  // tiles (of 128 points per wave) per main-loop iteration
+
 hipError_t launch_range(gf_ctx* ctx, const RangeArgs& a, int table_mode, int poly, int blocks) {
-  KTimer t(ctx, GF_K_RANGE_SCAN);
   const dim3 g(blocks), b(kBlock);
-  if (!table_mode && !poly) hipLaunchKernelGGL((range_kernel<0, 0>), g, b, 0, ctx->stream, a);
-  else if (table_mode && !poly) hipLaunchKernelGGL((range_kernel<1, 0>), g, b, 0, ctx->stream, a);
-  else hipLaunchKernelGGL((range_kernel<1, 1>), g, b, 0, ctx->stream, a);
+  const bool defer = a.queue != nullptr;
+  const size_t lds = table_mode ? sizeof(uint32_t) * (size_t)((2 * a.grid_n + 1) & ~1) +
+                                      (a.xt ? 2 * sizeof(double) * (size_t)(a.grid_n + 1) : 0) +
+                                      (a.span_lds ? (size_t)((a.span_bytes + 3) & ~3) : 0)
+                                : 0;
+  {
+    KTimer t(ctx, GF_K_RANGE_SCAN);
+    if (!table_mode && !poly) hipLaunchKernelGGL((range_kernel<0, 0, 0, kRangeU>), g, b, 0, ctx->stream, a);
+    else if (!poly) {
+      if (defer) hipLaunchKernelGGL((range_kernel<1, 0, 1, kRangeU>), g, b, lds, ctx->stream, a);
+      else hipLaunchKernelGGL((range_kernel<1, 0, 0, kRangeU>), g, b, lds, ctx->stream, a);
+    } else {
+      if (defer) hipLaunchKernelGGL((range_kernel<1, 1, 1, kRangeU>), g, b, lds, ctx->stream, a);
+      else hipLaunchKernelGGL((range_kernel<1, 1, 0, kRangeU>), g, b, lds, ctx->stream, a);
+    }
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  if (!defer) return hipSuccess;
+  KTimer t(ctx, GF_K_RANGE_TEST);
+  if (poly) hipLaunchKernelGGL(range_test_kernel<1>, dim3(a.test_blocks), b, 0, ctx->stream, a, blocks);
+  else hipLaunchKernelGGL(range_test_kernel<0>, dim3(a.test_blocks), b, 0, ctx->stream, a, blocks);
   return hipGetLastError();
 }
 
@@ -311,7 +672,9 @@ __global__ __launch_bounds__(kBlock) void range_finalize_kernel(const uint64_t* 
     if (threadIdx.x < s) { sh[threadIdx.x] += sh[threadIdx.x + s]; sm[threadIdx.x] += sm[threadIdx.x + s]; }
     __syncthreads();
   }
-  if (threadIdx.x == 0) { counts[0] = (int64_t)sh[0]; counts[1] = (int64_t)sm[0]; }
+  if (threadIdx.x == 0) {
+    if (counts) { counts[0] = (int64_t)sh[0]; counts[1] = (int64_t)sm[0]; }
+  }
 }
 
 hipError_t launch_range_finalize(hipStream_t s, const uint64_t* partials, int blocks, int64_t* counts) {

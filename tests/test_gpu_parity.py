@@ -196,6 +196,76 @@ def test_range_ppoly_generated_1000(sf, oracle_mod, n, r):
         np.testing.assert_array_equal(res.indices().astype(np.int64), exp)
 
 
+def _ulps(v, k):
+    for _ in range(abs(k)):
+        v = np.nextafter(v, np.inf if k > 0 else -np.inf)
+    return float(v)
+
+
+def test_range_ppoly_inside_cells_and_edges(sf, oracle_mod):
+    """Exact-mode shortcuts of the point-polygon plan: candidate cells wholly inside an
+    axis-aligned rectangle are accepted untested (kInside), candidate points go through the
+    deferred queue with envelope pruning.  Rectangles whose edges sit on / a few ulps off
+    cell boundaries, a rectangle with a hole (not kInside), a diamond, a triangle; points on
+    edges, at cell thresholds, NaN."""
+    n = 100
+    g = sf.UniformGrid(n, *BEIJING)
+    og = oracle_mod.grid(n, *BEIJING)
+    cl = (BEIJING[1] - BEIJING[0]) / n
+    bx = lambda c, k=0: _ulps(BEIJING[0] + c * cl, k)
+    by = lambda c, k=0: _ulps(BEIJING[2] + c * cl, k)
+    raw = []
+    for i, (k0, k1) in enumerate([(0, 0), (1, -1), (-1, 1), (2, -3), (-2, 2)]):
+        x1, x2, y1, y2 = bx(10 + 7 * i, k0), bx(14 + 7 * i, k1), by(20, k0), by(25, k1)
+        raw.append([[(x1, y1), (x2, y1), (x2, y2), (x1, y2), (x1, y1)]])
+    # rectangle with a rectangular hole
+    raw.append([[(bx(50), by(30)), (bx(56), by(30)), (bx(56), by(36)), (bx(50), by(36)), (bx(50), by(30))],
+                [(bx(52), by(32)), (bx(54), by(32)), (bx(54), by(34)), (bx(52), by(34)), (bx(52), by(32))]])
+    # diamond and triangle
+    cx0, cy0, h = bx(70), by(40), 3 * cl
+    raw.append([[(cx0, cy0 - h), (cx0 + h, cy0), (cx0, cy0 + h), (cx0 - h, cy0), (cx0, cy0 - h)]])
+    raw.append([[(bx(80), by(10)), (bx(88), by(10)), (bx(84), by(18)), (bx(80), by(10))]])
+    # rectangle given clockwise, starting at another corner
+    raw.append([[(bx(30, 1), by(50)), (bx(30, 1), by(46)), (bx(26), by(46)), (bx(26), by(50)), (bx(30, 1), by(50))]])
+    # adjacent rectangles sharing an edge inside a cell (their union covers it), and a pair
+    # separated by a 2-ulp gap (never covered)
+    mid, m2 = bx(40) + 0.4 * cl, bx(46) + 0.6 * cl
+    for (a0, a1, b0, b1) in [(bx(40), mid, mid, bx(44)), (bx(46), m2, _ulps(m2, 2), bx(50))]:
+        raw.append([[(a0, by(20)), (a1, by(20)), (a1, by(24)), (a0, by(24)), (a0, by(20))]])
+        raw.append([[(b0, by(20)), (b1, by(20)), (b1, by(24)), (b0, by(24)), (b0, by(20))]])
+    polys = [sf.Polygon(p, g) for p in raw]
+    x, y = oracle_mod.java_random_points(77, 300_000, BEIJING[0], bx(92), BEIJING[2], by(60))
+    ex, ey = [], []
+    for p in raw:
+        for ring in p:
+            for (ax, ay), (bx_, by_) in zip(ring[:-1], ring[1:]):
+                for t in np.linspace(0.0, 1.0, 9):
+                    ex.append(ax + t * (bx_ - ax))
+                    ey.append(ay + t * (by_ - ay))
+                for k in (-2, -1, 1, 2):
+                    ex.append(_ulps(ax, k))
+                    ey.append(ay)
+                    ex.append(ax)
+                    ey.append(_ulps(ay, k))
+    for c in range(8, 60):
+        for k in (-1, 0, 1):
+            ex.append(bx(c, k))
+            ey.append(by(22, 0) + 0.0003)
+            ex.append(bx(12) + 0.0002)
+            ey.append(by(c, k))
+    ex += [np.nan, bx(12), np.nan, bx(52) + 1e-4, _ulps(m2, 1), m2, _ulps(m2, 2), mid]
+    ey += [by(22), np.nan, np.nan, by(33), by(22), by(22), by(22), by(22)]
+    x = np.concatenate([np.asarray(ex), x])
+    y = np.concatenate([np.asarray(ey), y])
+    w = win(sf, x, y)
+    for r in (0.0, 0.0005, 0.001, 0.02):
+        for ap in (False, True):
+            res = sf.PointPolygonRangeQuery(conf(sf, ap), g).run(w, polys, r)
+            exp = oracle_mod.range_ppoly(og, x, y, oracle_mod.Polygons(raw), r, ap)
+            np.testing.assert_array_equal(res.indices().astype(np.int64), exp, err_msg=f"r={r} ap={ap}")
+            assert res.count() == len(exp)
+
+
 # ------------------------------------------------------------------ kNN
 def check_knn(res, oo, od, oi):
     np.testing.assert_array_equal(res.objID, oo)

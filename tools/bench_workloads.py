@@ -59,7 +59,9 @@ def bench_range(args, polygons=False):
 
     L = _lib.lib()
     sizes = [args.points] if args.points else ([10_000_000] if polygons else [1_000_000, 10_000_000])
-    for n in sizes:
+    sweep = [int(b) for b in str(args.range_blocks).split(",")]
+    dsweep = [int(b) for b in str(args.range_defer).split(",")]
+    for n, blocks, dmode in [(n, b, d) for n in sizes for b in sweep for d in dsweep]:
         grid_n = 500 if polygons else 100
         grid = sf.UniformGrid(grid_n, *BEIJING)
         og = O.grid(grid_n, *BEIJING)
@@ -81,6 +83,9 @@ def bench_range(args, polygons=False):
             h = C.c_void_p()
             _lib.check(L.gf_range_pp_plan_create(ctx.handle, C.byref(grid.c_grid), qx.ctypes.data, qy.ctypes.data, 1,
                                                  r, 0, 0, C.byref(h)), ctx.handle, "plan")
+        _lib.check(L.gf_range_plan_set_tuning(h, blocks, dmode), ctx.handle, "tuning")
+        cells = [C.c_int64() for _ in range(4)]
+        _lib.check(L.gf_range_plan_stats(h, *[C.byref(c) for c in cells]), ctx.handle, "stats")
         words = (n + 63) // 64
         bitmaps = torch.empty(nwin, words, dtype=torch.int64, device="cuda")
         counts = torch.zeros(nwin, 2, dtype=torch.int64, device="cuda")
@@ -96,33 +101,39 @@ def bench_range(args, polygons=False):
             step(i)
         torch.cuda.synchronize()
         ctx.set_timing_period(5)
-        ctx.set_timing(1 << _lib.K_RANGE_SCAN)
+        ctx.set_timing((1 << _lib.K_RANGE_SCAN) | (1 << _lib.K_RANGE_TEST))
         t0 = time.perf_counter()
         for i in range(args.steps):
             step(i)
         torch.cuda.synchronize()
         elapsed = time.perf_counter() - t0
         ms, cnt = ctx.timing(_lib.K_RANGE_SCAN)
+        tms, tcnt = ctx.timing(_lib.K_RANGE_TEST)
         ctx.set_timing(0)
         ctx.set_timing_period(1)
-        # parity spot check of window 0 against the oracle (1M-point windows only; 10M polygon
-        # windows are covered by the GPU parity tests at smaller sizes)
-        verified = None
+        # parity spot check of window 0 against the oracle: range results are per point, so the
+        # first min(n, 1M) points of the window are checked against the oracle run on them alone
         hits = int(counts[0, 0].item())
-        if n <= 1_000_000:
-            x, y, _ = wins[0]
-            exp = (O.range_ppoly(og, x, y, O.Polygons(raw), r) if polygons
-                   else O.range_pp(og, x, y, [QPOINT[0]], [QPOINT[1]], r))
-            got = sf.spatialOperators.bitmap_indices(ctx, bitmaps[0], n).astype(np.int64)
-            verified = bool(np.array_equal(got, exp))
+        m = min(n, 1_000_000)
+        x, y, _ = wins[0]
+        exp = (O.range_ppoly(og, x[:m], y[:m], O.Polygons(raw), r) if polygons
+               else O.range_pp(og, x[:m], y[:m], [QPOINT[0]], [QPOINT[1]], r))
+        got = sf.spatialOperators.bitmap_indices(ctx, bitmaps[0], n).astype(np.int64)
+        verified = bool(np.array_equal(got[got < m], exp))
         L.gf_range_plan_destroy(h)
-        avg = ms / 1000.0 / max(cnt, 1)
+        avg_scan = ms / 1000.0 / max(cnt, 1)
+        avg_test = tms / 1000.0 / tcnt if tcnt else 0.0
+        avg = avg_scan + avg_test
         wl = (f"ppoly_{len(polys)}polys_r{r}_{n // 1_000_000}Mpts_grid{grid_n}" if polygons
               else f"range_pp_r{r}_{n // 1_000_000}Mpts_grid{grid_n}")
         _line("point-polygon range" if polygons else "point-point range", n * args.steps / elapsed, "points/s",
-              args.steps, args.warmup, elapsed, "range_kernel", 16.0 * n + n / 8.0, avg,
+              args.steps, args.warmup, elapsed,
+              "range_kernel + range_test_kernel" if tcnt else "range_kernel", 16.0 * n + n / 8.0, avg,
               {"config": {"workload": wl, "points_per_window": n, "grid": grid_n, "radius": r,
-                          "hits_window0": hits}, "verified_vs_oracle": verified})
+                          "hits_window0": hits, "scan_blocks": blocks, "defer_mode": dmode,
+                          "cells_none_candidate_guaranteed_inside": [c.value for c in cells]},
+               "breakdown": {"scan_us": round(avg_scan * 1e6, 2), "test_us": round(avg_test * 1e6, 2)},
+               "verified_vs_oracle": verified, "verified_sample": f"first {m} points of window 0"})
 
 
 def bench_join(args):
