@@ -100,6 +100,11 @@ int         gf_ctx_set_stream(gf_ctx* ctx, void* hip_stream);
 void*       gf_ctx_stream(gf_ctx* ctx);
 int         gf_ctx_synchronize(gf_ctx* ctx);
 const char* gf_ctx_last_error(gf_ctx* ctx);
+/* Context flags (testing / tuning).  GF_FLAG_JOIN_LEGACY: 1 = gf_join_pp probes the query
+ * buckets from global memory in input order instead of the row-bucketed LDS path. */
+#define GF_FLAG_JOIN_LEGACY 1
+int gf_ctx_set_flag(gf_ctx* ctx, int flag, int value);
+
 /* Record HIP events around launches of the kernels in `mask` (bit 1 << GF_K_*; 0 = off). */
 int         gf_ctx_set_timing(gf_ctx* ctx, int mask);
 /* Time only every period-th launch of each kernel (fewer events in a hot loop); default 1. */

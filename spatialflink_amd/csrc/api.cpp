@@ -262,6 +262,12 @@ extern "C" int gf_ctx_synchronize(gf_ctx* ctx) {
 
 extern "C" const char* gf_ctx_last_error(gf_ctx* ctx) { return ctx ? ctx->last_error.c_str() : "null context"; }
 
+extern "C" int gf_ctx_set_flag(gf_ctx* ctx, int flag, int value) {
+  if (!ctx) return GF_ERR_ARG;
+  if (flag == GF_FLAG_JOIN_LEGACY) { ctx->join_legacy = value != 0; return GF_OK; }
+  return set_err(ctx, GF_ERR_ARG, "gf_ctx_set_flag: unknown flag");
+}
+
 extern "C" int gf_ctx_set_timing(gf_ctx* ctx, int mask) {
   if (!ctx) return GF_ERR_ARG;
   ctx->timing = mask;
@@ -607,6 +613,9 @@ int build_table(gf_range_plan* P, const std::vector<Rect>& base, bool need_lists
   }
   return GF_OK;
 }
+
+// dynamic LDS of a join probe task (2 x 512-thread blocks per CU)
+constexpr int kJoinLdsBudget = 76 * 1024;
 
 // row-span class tables up to this size are staged in LDS by every scan block
 constexpr int64_t kSpanLdsBytes = 32768;
@@ -1248,6 +1257,17 @@ extern "C" int gf_join_pp(gf_ctx* ctx, const gf_grid* ugrid, const gf_grid* qgri
   size_t o_sqx = ar.take<double>(nq), o_sqy = ar.take<double>(nq);
   size_t o_sqcx = ar.take<int32_t>(nq), o_sqcy = ar.take<int32_t>(nq), o_sqi = ar.take<uint32_t>(nq);
   size_t o_cnt = ar.take<uint32_t>(blocks), o_boff = ar.take<uint32_t>(blocks + 1);
+  // row-bucketed path (k_join.hip): bucket the ordinary side by cell row, probe per task
+  const bool rowpath = c >= 0 && 2 * c + 1 <= kJoinMaxRows && qn <= 8192 && !ctx->join_legacy;
+  const int64_t max_tasks = no / kJoinTask + qn + 1;
+  const int sblocks = (int)std::min<int64_t>(std::max<int64_t>(no / 8192, 1), (int64_t)ctx->num_cus * 4);
+  const int64_t mat = rowpath ? qn * sblocks : 1;
+  size_t o_rmat = ar.take<uint32_t>(mat), o_rmats = ar.take<uint32_t>(mat + 1), o_roff = ar.take<uint32_t>(qn + 1);
+  size_t o_rtask = ar.take<uint32_t>(qn), o_toff = ar.take<uint32_t>(qn + 1);
+  size_t o_tcnt = ar.take<uint32_t>(rowpath ? max_tasks : 1), o_tpo = ar.take<uint32_t>(rowpath ? max_tasks + 1 : 1);
+  size_t o_btmp = ar.take<uint32_t>(std::max(scan_tmp_elems(mat), scan_tmp_elems(max_tasks)));
+  size_t o_soxy = ar.take<double>(rowpath ? 2 * no : 1), o_soidx = ar.take<uint32_t>(rowpath ? no : 1);
+  size_t o_pcnt = ar.take<uint8_t>(rowpath ? no : 1);
   char* base = (char*)ctx_scratch(ctx, ar.off, &st);
   if (st) return st;
   auto U32 = [&](size_t o) { return (uint32_t*)(base + o); };
@@ -1262,6 +1282,39 @@ extern "C" int gf_join_pp(gf_ctx* ctx, const gf_grid* ugrid, const gf_grid* qgri
   GF_HIP_CHECK(ctx, hipMemcpyAsync(U32(o_cur), U32(o_off), bins * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
   GF_HIP_CHECK(ctx, launch_join_qscatter(s, qry->x, qry->y, I32(o_qcx), I32(o_qcy), U32(o_keys), nq, U32(o_cur),
                                          F64(o_sqx), F64(o_sqy), I32(o_sqcx), I32(o_sqcy), U32(o_sqi)));
+  if (rowpath) {
+    auto R32 = [&](size_t o) { return (uint32_t*)(base + o); };
+    JoinRowArgs j{};
+    j.ox = ord->x; j.oy = ord->y; j.no = no;
+    j.u_minX = ugrid->minX; j.u_minY = ugrid->minY; j.u_cl = ugrid->cellLength;
+    j.qn = (int32_t)qn; j.c = c; j.q_off = U32(o_off);
+    j.sqx = F64(o_sqx); j.sqy = F64(o_sqy); j.sqcx = I32(o_sqcx); j.sqcy = I32(o_sqcy); j.sqidx = U32(o_sqi);
+    j.approx = approximate != 0; j.metric = metric; j.r = r; j.s_r = s_prefilter(r, 0);
+    j.row_mat = R32(o_rmat); j.row_mat_scan = R32(o_rmats); j.row_off_w = R32(o_roff); j.row_off = R32(o_roff);
+    j.row_tasks = R32(o_rtask);
+    j.task_off = R32(o_toff); j.soxy = (double*)(base + o_soxy); j.soidx = R32(o_soidx);
+    j.pcnt = (uint8_t*)(base + o_pcnt);
+    j.task_cnt = R32(o_tcnt); j.task_pair_off = R32(o_tpo); j.pairs = pairs;
+    j.lds_budget = kJoinLdsBudget;
+    GF_HIP_CHECK(ctx, launch_join_rows(ctx, j, 0, sblocks));
+    GF_HIP_CHECK(ctx, launch_exclusive_scan(s, j.row_mat, mat, j.row_mat_scan, R32(o_btmp)));
+    GF_HIP_CHECK(ctx, launch_join_rows(ctx, j, 1, sblocks));
+    GF_HIP_CHECK(ctx, launch_join_rows(ctx, j, 2, sblocks));
+    GF_HIP_CHECK(ctx, launch_exclusive_scan(s, j.row_tasks, qn, R32(o_toff), R32(o_btmp)));
+    const int pblocks = (int)max_tasks;
+    GF_HIP_CHECK(ctx, launch_join_rows(ctx, j, 3, pblocks));
+    GF_HIP_CHECK(ctx, launch_exclusive_scan(s, j.task_cnt, max_tasks, R32(o_tpo), R32(o_btmp)));
+    uint32_t total = 0;
+    GF_HIP_CHECK(ctx, hipMemcpyAsync(&total, R32(o_tpo) + max_tasks, sizeof total, hipMemcpyDeviceToHost, s));
+    GF_HIP_CHECK(ctx, hipStreamSynchronize(s));
+    *npairs = total;
+    if ((int64_t)total > cap) return GF_ERR_CAPACITY;
+    if (total == 0) return GF_OK;
+    if (!pairs) return set_err(ctx, GF_ERR_ARG, "null pairs");
+    GF_HIP_CHECK(ctx, launch_join_rows(ctx, j, 4, pblocks));
+    GF_HIP_CHECK(ctx, hipStreamSynchronize(s));
+    return GF_OK;
+  }
   JoinArgs a{};
   a.ox = ord->x; a.oy = ord->y; a.no = no;
   a.u_minX = ugrid->minX; a.u_minY = ugrid->minY; a.u_cl = ugrid->cellLength;

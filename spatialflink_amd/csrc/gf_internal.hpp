@@ -32,6 +32,7 @@ struct gf_ctx {
   void* pinned = nullptr;
   size_t pinned_bytes = 0;
   int num_cus = 256;
+  int join_legacy = 0;  // testing: force the original (unbucketed) join probe
 };
 
 namespace gf {
@@ -231,6 +232,41 @@ hipError_t launch_join_qscatter(hipStream_t s, const double* qx, const double* q
                                 const int32_t* qcy, const uint32_t* keys, int64_t nq, uint32_t* cursor,
                                 double* sqx, double* sqy, int32_t* sqcx, int32_t* sqcy, uint32_t* sqidx);
 hipError_t launch_join_probe(gf_ctx* ctx, const JoinArgs& a, int write_pass, int blocks);
+
+// row-bucketed join (c >= 0): see k_join.hip
+constexpr int kJoinTask = 8192;      // ordinary points per probe task (one row)
+constexpr int kJoinThreads = 1024;
+constexpr int kJoinMaxRows = 16;     // staged query rows (2c+1) per task
+struct JoinRowArgs {
+  const double* ox;
+  const double* oy;
+  int64_t no;
+  double u_minX, u_minY, u_cl;
+  int32_t qn;
+  int64_t c;
+  const uint32_t* q_off;
+  const double* sqx;
+  const double* sqy;
+  const int32_t* sqcx;
+  const int32_t* sqcy;
+  const uint32_t* sqidx;
+  int approx, metric;
+  double r, s_r;            // s_r = smax(r): exact squared-distance bound for metric 0
+  uint32_t* row_mat;        // [qn * nblk] per-block row histograms (row-major)
+  uint32_t* row_mat_scan;   // [qn * nblk + 1] its exclusive scan: run start per (row, block)
+  uint32_t* row_off_w;      // [qn+1] row starts (written by the finish kernel)
+  const uint32_t* row_off;  // same buffer, read by the probe
+  uint32_t* row_tasks;      // [qn]
+  const uint32_t* task_off; // [qn+1]
+  double* soxy;             // [2*no] row-bucketed ordinary xy
+  uint32_t* soidx;          // [no]
+  uint8_t* pcnt;            // [no] count pass: pairs per bucketed point (255 = saturated)
+  uint32_t* task_cnt;       // count pass: pairs per task
+  const uint32_t* task_pair_off;  // write pass: output offset per task
+  uint32_t* pairs;
+  int lds_budget;
+};
+hipError_t launch_join_rows(gf_ctx* ctx, const JoinRowArgs& a, int stage, int blocks);
 
 }  // namespace gf
 

@@ -157,4 +157,360 @@ hipError_t launch_join_probe(gf_ctx* ctx, const JoinArgs& a, int write_pass, int
   return hipGetLastError();
 }
 
+// =======================================================================================
+// Row-bucketed join (the default path when c >= 0).  The ordinary points are bucketed by
+// their cell row (counting sort over qn rows, block-local LDS histograms, one global atomic
+// per block and row to reserve a run), then processed as tasks of <= kJoinTask points of one
+// row: a task stages the query buckets of rows cy-c .. cy+c (u16 bucket offsets + xy) in LDS
+// and tests each ordinary point against the (2c+1) bucket runs around its cell -- all LDS.
+// A task whose rows do not fit the LDS budget probes the same runs from global memory.
+// Counts pass -> scan over tasks -> write pass; pair order inside a task is unspecified.
+// =======================================================================================
+constexpr int kRowMax = 8192;  // rows staged as LDS histograms by the bucketing kernels
+#ifndef GF_JOIN_BATCH
+#define GF_JOIN_BATCH 4
+#endif
+constexpr int kJoinBatch = GF_JOIN_BATCH;  // candidates of one row loaded together in the probe
+
+// Bucketing: block b owns the contiguous input chunk b; its row histogram goes to column b of
+// the row-major matrix M[row][block] (plain stores).  The exclusive scan of M (flattened) is
+// then, for every (row, block), the start of that block's run of the row -- no contended
+// atomics, and the order inside a row is the block order.
+__device__ __forceinline__ void chunk_of(int64_t no, int64_t& beg, int64_t& end) {
+  const int64_t chunk = (no + gridDim.x - 1) / gridDim.x;
+  beg = (int64_t)blockIdx.x * chunk;
+  end = beg + chunk < no ? beg + chunk : no;
+  if (beg > no) beg = no;
+}
+
+// kBucketU points per thread are loaded before any is used (the loop is latency-bound
+// otherwise: one HBM round trip per point per wave)
+constexpr int kBucketU = 8;
+
+__global__ __launch_bounds__(kBlock) void join_orow_hist_kernel(JoinRowArgs a, uint32_t* __restrict__ M) {
+  __shared__ uint32_t h[kRowMax];
+  int64_t beg, end;
+  chunk_of(a.no, beg, end);
+  for (int j = threadIdx.x; j < a.qn; j += kBlock) h[j] = 0u;
+  __syncthreads();
+  for (int64_t i0 = beg + threadIdx.x; i0 < end; i0 += kBlock * kBucketU) {
+    double x[kBucketU], y[kBucketU];
+#pragma unroll
+    for (int u = 0; u < kBucketU; ++u) {
+      const int64_t i = i0 + u * kBlock;
+      x[u] = i < end ? __builtin_nontemporal_load(a.ox + i) : NAN;
+      y[u] = i < end ? __builtin_nontemporal_load(a.oy + i) : NAN;
+    }
+#pragma unroll
+    for (int u = 0; u < kBucketU; ++u) {
+      if (!(x[u] == x[u])) {  // NaN (or past the end): cell 0 per Java, but i may be past the end
+        if (i0 + u * kBlock >= end) continue;
+      }
+      const int32_t cx = cell_index(x[u], a.u_minX, a.u_cl);
+      const int32_t cy = cell_index(y[u], a.u_minY, a.u_cl);
+      if (cx >= 0 && cy >= 0 && cx < a.qn && cy < a.qn) atomicAdd(&h[cy], 1u);
+    }
+  }
+  __syncthreads();
+  for (int j = threadIdx.x; j < a.qn; j += kBlock) M[(size_t)j * gridDim.x + blockIdx.x] = h[j];
+}
+
+__global__ __launch_bounds__(kBlock) void join_orow_scatter_kernel(JoinRowArgs a, const uint32_t* __restrict__ Ms) {
+  __shared__ uint32_t h[kRowMax];
+  int64_t beg, end;
+  chunk_of(a.no, beg, end);
+  for (int j = threadIdx.x; j < a.qn; j += kBlock) h[j] = Ms[(size_t)j * gridDim.x + blockIdx.x];
+  __syncthreads();
+  for (int64_t i0 = beg + threadIdx.x; i0 < end; i0 += kBlock * kBucketU) {
+    double x[kBucketU], y[kBucketU];
+#pragma unroll
+    for (int u = 0; u < kBucketU; ++u) {
+      const int64_t i = i0 + u * kBlock;
+      x[u] = i < end ? __builtin_nontemporal_load(a.ox + i) : 0.0;
+      y[u] = i < end ? __builtin_nontemporal_load(a.oy + i) : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < kBucketU; ++u) {
+      const int64_t i = i0 + u * kBlock;
+      if (i >= end) continue;
+      const int32_t cx = cell_index(x[u], a.u_minX, a.u_cl);
+      const int32_t cy = cell_index(y[u], a.u_minY, a.u_cl);
+      if (cx >= 0 && cy >= 0 && cx < a.qn && cy < a.qn) {
+        const uint32_t pos = atomicAdd(&h[cy], 1u);
+        reinterpret_cast<double2*>(a.soxy)[pos] = make_double2(x[u], y[u]);
+        a.soidx[pos] = (uint32_t)i;
+      }
+    }
+  }
+}
+
+// row_off[j] = Ms[j][0] (row starts), row_off[qn] = total; tasks per row
+__global__ __launch_bounds__(kBlock) void join_rows_finish_kernel(const uint32_t* __restrict__ Ms, int32_t qn,
+                                                                  int32_t nblk, uint32_t total_idx,
+                                                                  uint32_t* __restrict__ row_off,
+                                                                  uint32_t* __restrict__ row_tasks) {
+  for (int j = blockIdx.x * kBlock + threadIdx.x; j <= qn; j += gridDim.x * kBlock) {
+    const uint32_t b = Ms[j < qn ? (size_t)j * nblk : total_idx];
+    row_off[j] = b;
+    if (j < qn) {
+      const uint32_t e = Ms[j + 1 < qn ? (size_t)(j + 1) * nblk : total_idx];
+      row_tasks[j] = (e - b + kJoinTask - 1) / kJoinTask;
+    }
+  }
+}
+
+template <int NT>
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* total, uint32_t* wsum) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  uint32_t inc = v;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t t = __shfl_up(inc, off, 64);
+    if (lane >= off) inc += t;
+  }
+  if (lane == 63) wsum[wid] = inc;
+  __syncthreads();
+  uint32_t before = 0, tot = 0;
+  for (int w = 0; w < NT / 64; ++w) {
+    if (w < wid) before += wsum[w];
+    tot += wsum[w];
+  }
+  *total = tot;
+  __syncthreads();
+  return before + inc - v;
+}
+
+// View of one staged query row: bucket kx (0..W-1) holds points [off(kx), off(kx+1)).
+// LDS mode: u16 bucket offsets relative to gbase at byte offset loff of the dynamic LDS, the
+// row's xy pairs at byte offset lxy (offsets, not pointers, so the loads stay ds_read).
+struct QRow {
+  int32_t ry;      // clamped row index in [-1, qn]
+  uint32_t gbase;  // global index of the row's first point (sorted query arrays)
+  uint32_t loff;
+  uint32_t lxy;
+};
+
+// Candidates of ordinary point (px, py) in cell (cx, cy) among the staged rows.  EMIT writes
+// its pairs from `pos`; returns the number of pairs.
+template <bool EMIT>
+__device__ __forceinline__ uint32_t join_row_point(const JoinRowArgs& a, const char* lds, const QRow* rows, int nrows,
+                                                   double px, double py, int32_t cx, int32_t cy, uint32_t pidx,
+                                                   uint64_t pos) {
+  const int32_t W = a.qn + 2, c = (int32_t)a.c, qn = a.qn;
+  const int32_t kb = (cx - c < -1 ? -1 : cx - c) + 1, ke = (cx + c > qn ? qn : cx + c) + 2;
+  const bool fast_ok = !a.approx && a.metric == 0;
+  uint32_t cnt = 0;
+  for (int j = 0; j < nrows; ++j) {
+    const QRow R = rows[j];
+    const bool in_lds = R.loff != 0xffffffffu;
+    uint32_t tb, te, t_lo, t_hi;  // candidate run; [t_lo, t_hi) holds the interior buckets
+    if (in_lds) {
+      const uint16_t* lo16 = reinterpret_cast<const uint16_t*>(lds + R.loff);
+      tb = lo16[kb]; te = lo16[ke]; t_lo = lo16[1]; t_hi = lo16[W - 1];
+    } else {
+      const uint32_t* qo = a.q_off + (size_t)(R.ry + 1) * W;
+      tb = qo[kb] - R.gbase; te = qo[ke] - R.gbase; t_lo = qo[1] - R.gbase; t_hi = qo[W - 1] - R.gbase;
+    }
+    const bool brow = R.ry < 0 || R.ry >= qn;  // clamped row: true cells differ
+    uint32_t t = tb;
+    if (fast_ok && in_lds && !brow && te > tb && tb >= t_lo && te <= t_hi) {
+      // interior LDS run: kJoinBatch candidates loaded together (independent ds_read_b128)
+      const double2* lxy = reinterpret_cast<const double2*>(lds + R.lxy);
+      for (; t < te; t += kJoinBatch) {
+        double2 q[kJoinBatch];
+#pragma unroll
+        for (int k = 0; k < kJoinBatch; ++k) q[k] = lxy[t + k < te ? t + k : t];
+#pragma unroll
+        for (int k = 0; k < kJoinBatch; ++k) {
+          const double dx = px - q[k].x, dy = py - q[k].y;
+          if (t + k < te && dx * dx + dy * dy <= a.s_r) {  // s <= smax(r) <=> sqrt(s) <= r
+            if (EMIT) {
+              a.pairs[2 * (pos + cnt)] = pidx;
+              a.pairs[2 * (pos + cnt) + 1] = a.sqidx[R.gbase + t + k];
+            }
+            ++cnt;
+          }
+        }
+      }
+      continue;
+    }
+    for (; t < te; ++t) {
+      const uint32_t gi = R.gbase + t;
+      if (brow || t < t_lo || t >= t_hi) {  // clamped bucket: Chebyshev test on the true cell
+        const int64_t ddx = (int64_t)a.sqcx[gi] - cx, ddy = (int64_t)a.sqcy[gi] - cy;
+        if (ddx > c || ddx < -c || ddy > c || ddy < -c) continue;
+      }
+      if (!a.approx) {
+        double qx, qy;
+        if (in_lds) {
+          const double2 q = reinterpret_cast<const double2*>(lds + R.lxy)[t];
+          qx = q.x; qy = q.y;
+        } else {
+          qx = a.sqx[gi]; qy = a.sqy[gi];
+        }
+        const double dx = px - qx, dy = py - qy;
+        if (a.metric == 0 ? !(dx * dx + dy * dy <= a.s_r) : !(fdlibm_hypot(dx, dy) <= a.r)) continue;
+      }
+      if (EMIT) {
+        a.pairs[2 * (pos + cnt)] = pidx;
+        a.pairs[2 * (pos + cnt) + 1] = a.sqidx[gi];
+      }
+      ++cnt;
+    }
+  }
+  return cnt;
+}
+
+// Count pass (WRITE = 0): pairs per ordinary point (u8, saturating) and per task.  Write pass:
+// per-point counts -> block scan per round -> one emitting traversal.
+template <int WRITE>
+__global__ __launch_bounds__(kJoinThreads) __attribute__((amdgpu_waves_per_eu(8)))  // 2 blocks per CU
+void join_row_probe_kernel(JoinRowArgs a) {
+  extern __shared__ char lds[];
+  __shared__ uint32_t wsum[kJoinThreads / 64];
+  __shared__ int32_t s_row, s_fit;
+  __shared__ uint32_t s_beg, s_end;
+  __shared__ QRow rows[kJoinMaxRows];
+  const uint32_t ntask = a.task_off[a.qn];
+  const uint32_t task = blockIdx.x;
+  if (task >= ntask) {
+    if (!WRITE && threadIdx.x == 0) a.task_cnt[task] = 0u;
+    return;
+  }
+  const int64_t W = (int64_t)a.qn + 2, c = a.c, qn = a.qn;
+  if (threadIdx.x == 0) {
+    int lo = 0, hi = a.qn;  // row = last j with task_off[j] <= task
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (a.task_off[mid] <= task) lo = mid; else hi = mid;
+    }
+    const uint32_t k = task - a.task_off[lo];
+    const uint32_t rb = a.row_off[lo], re = a.row_off[lo + 1];
+    s_row = lo;
+    s_beg = rb + k * kJoinTask;
+    s_end = rb + (k + 1) * kJoinTask < re ? rb + (k + 1) * kJoinTask : re;
+    // staged rows and their LDS footprint
+    const int64_t r0 = lo - c < -1 ? -1 : lo - c, r1 = lo + c > qn ? qn : lo + c;
+    size_t need = 0;
+    bool fit = (r1 - r0 + 1) <= kJoinMaxRows;
+    for (int64_t ry = r0; fit && ry <= r1; ++ry) {
+      const uint32_t b = a.q_off[(ry + 1) * W], e = a.q_off[(ry + 1) * W + W];
+      fit = (e - b) < 65536u;
+      need += ((size_t)(W + 1) * 2 + 15) / 16 * 16 + (size_t)(e - b) * 16;
+    }
+    s_fit = fit && need <= (size_t)a.lds_budget;
+  }
+  __syncthreads();
+  const int32_t cy = s_row;
+  const int64_t r0 = cy - c < -1 ? -1 : cy - c, r1 = cy + c > qn ? qn : cy + c;
+  const int nrows = (int)(r1 - r0 + 1);
+  // stage (or describe) the rows
+  size_t off = 0;
+  for (int j = 0; j < nrows && j < kJoinMaxRows; ++j) {
+    const int64_t ry = r0 + j;
+    const uint32_t* qo = a.q_off + (ry + 1) * W;
+    const uint32_t b = qo[0], e = qo[W];
+    if (s_fit) {
+      const uint32_t o16 = (uint32_t)off;
+      uint16_t* lo16 = reinterpret_cast<uint16_t*>(lds + off);
+      off += ((size_t)(W + 1) * 2 + 15) / 16 * 16;
+      const uint32_t oxy = (uint32_t)off;
+      double2* lxy = reinterpret_cast<double2*>(lds + off);
+      off += (size_t)(e - b) * 16;
+      for (int64_t t = threadIdx.x; t <= W; t += kJoinThreads) lo16[t] = (uint16_t)(qo[t] - b);
+      for (uint32_t t = threadIdx.x; t < e - b; t += kJoinThreads) lxy[t] = make_double2(a.sqx[b + t], a.sqy[b + t]);
+      if (threadIdx.x == 0) rows[j] = QRow{(int32_t)ry, b, o16, oxy};
+    } else if (threadIdx.x == 0) {
+      rows[j] = QRow{(int32_t)ry, b, 0xffffffffu, 0u};
+    }
+  }
+  __syncthreads();
+  const uint32_t beg = s_beg, end = s_end;
+  uint64_t run = WRITE ? a.task_pair_off[task] : 0;
+  uint32_t total_cnt = 0;
+  // Rounds of kJoinThreads points, in pairs with two register buffers: the next round's point
+  // loads are in flight while a round is processed (no copies on the loop's back edge).
+  // WRITE: every thread walks the same number of rounds (block scan per round).
+  struct Pt {
+    double x, y;
+    uint32_t idx, cnt;
+  };
+  auto load = [&](uint32_t s0, Pt& p) {
+    const uint32_t i = s0 + threadIdx.x;
+    p.x = p.y = 0.0;
+    p.idx = 0u;
+    p.cnt = 0u;
+    if (i < end) {
+      const double2 v = reinterpret_cast<const double2*>(a.soxy)[i];
+      p.x = v.x;
+      p.y = v.y;
+      if (WRITE) {
+        p.idx = a.soidx[i];
+        p.cnt = a.pcnt[i];
+      }
+    }
+  };
+  auto round = [&](uint32_t s0, const Pt& p) {
+    const uint32_t i = s0 + threadIdx.x;
+    const bool valid = i < end;
+    const int32_t cx = valid ? cell_index(p.x, a.u_minX, a.u_cl) : 0;
+    if (!WRITE) {
+      const uint32_t cnt = valid ? join_row_point<false>(a, lds, rows, nrows, p.x, p.y, cx, cy, 0, 0) : 0u;
+      if (valid) a.pcnt[i] = (uint8_t)(cnt < 255u ? cnt : 255u);
+      total_cnt += cnt;
+    } else {
+      uint32_t cnt = p.cnt;
+      if (cnt == 255u) cnt = join_row_point<false>(a, lds, rows, nrows, p.x, p.y, cx, cy, 0, 0);
+      uint32_t tot;
+      const uint32_t ex = block_excl_scan<kJoinThreads>(cnt, &tot, wsum);
+      if (valid && cnt) join_row_point<true>(a, lds, rows, nrows, p.x, p.y, cx, cy, p.idx, run + ex);
+      run += tot;
+    }
+  };
+  Pt A, B;
+  load(beg, A);
+  for (uint32_t s = beg; s < end; s += 2 * kJoinThreads) {
+    load(s + kJoinThreads, B);
+    round(s, A);
+    load(s + 2 * kJoinThreads, A);
+    if (s + kJoinThreads < end) round(s + kJoinThreads, B);
+  }
+  if (!WRITE) {
+    uint32_t tot;
+    block_excl_scan<kJoinThreads>(total_cnt, &tot, wsum);
+    if (threadIdx.x == 0) a.task_cnt[task] = tot;
+  }
+}
+
+hipError_t launch_join_rows(gf_ctx* ctx, const JoinRowArgs& a, int stage, int blocks) {
+  hipStream_t s = ctx->stream;
+  switch (stage) {
+    case 0: {
+      KTimer t(ctx, GF_K_JOIN_BUCKET);
+      hipLaunchKernelGGL(join_orow_hist_kernel, dim3(blocks), dim3(kBlock), 0, s, a, a.row_mat);
+      break;
+    }
+    case 1: {
+      KTimer t(ctx, GF_K_JOIN_BUCKET);
+      hipLaunchKernelGGL(join_orow_scatter_kernel, dim3(blocks), dim3(kBlock), 0, s, a, a.row_mat_scan);
+      break;
+    }
+    case 2:  // blocks = the bucketing grid size
+      hipLaunchKernelGGL(join_rows_finish_kernel, dim3((a.qn + 1 + kBlock - 1) / kBlock), dim3(kBlock), 0, s,
+                         a.row_mat_scan, a.qn, blocks, (uint32_t)((size_t)a.qn * blocks), a.row_off_w, a.row_tasks);
+      break;
+    case 3: {
+      KTimer t(ctx, GF_K_JOIN_PROBE);
+      hipLaunchKernelGGL(join_row_probe_kernel<0>, dim3(blocks), dim3(kJoinThreads), a.lds_budget, s, a);
+      break;
+    }
+    case 4: {
+      KTimer t(ctx, GF_K_JOIN_PROBE);
+      hipLaunchKernelGGL(join_row_probe_kernel<1>, dim3(blocks), dim3(kJoinThreads), a.lds_budget, s, a);
+      break;
+    }
+  }
+  return hipGetLastError();
+}
+
 }  // namespace gf

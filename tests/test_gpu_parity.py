@@ -466,6 +466,51 @@ def test_join_different_query_grid(sf, oracle_mod):
     np.testing.assert_array_equal(got, exp)
 
 
+@pytest.mark.parametrize("n,r,qn,qbox", [(100, 0.001, 100, None), (100, 0.05, 100, None),
+                                          (200, 0.012, 150, (115.3, 117.9, 39.4, 41.4)),
+                                          (100, 0.05, 100, (115.45, 117.65, 39.55, 41.15))])
+def test_join_row_path_edges(sf, oracle_mod, n, r, qn, qbox):
+    """Row-bucketed join vs the legacy probe vs the oracle: points outside the grid on both
+    sides (clamped query rows / columns need the true-cell test), NaN coordinates, a
+    query grid different from the ordinary grid, c = 1..3."""
+    from spatialflink_amd import _lib
+
+    ug = sf.UniformGrid(n, *BEIJING)
+    qgb = qbox or BEIJING
+    qg = sf.UniformGrid(qn, *qgb)
+    oug, oqg = oracle_mod.grid(n, *BEIJING), oracle_mod.grid(qn, *qgb)
+    ox, oy = oracle_mod.java_random_points(81, 120_000, 115.3, 117.8, 39.4, 41.3)
+    qx, qy = oracle_mod.java_random_points(82, 40_000, 115.3, 117.8, 39.4, 41.3)
+    ox[:3] = np.nan
+    qy[5:8] = np.nan
+    qx[10:40] = BEIJING[0] - np.linspace(0, 0.02, 30)  # just left of the grid
+    qy[40:70] = BEIJING[3] + np.linspace(0, 0.02, 30)  # just above
+    st, pairs = oracle_mod.join_pp(oug, oqg, ox, oy, qx, qy, r)
+    exp = np.array(sorted(map(tuple, pairs.tolist())), np.int64).reshape(-1, 2)
+    ctx = _lib.context(0)
+    for legacy in (0, 1):
+        _lib.check(_lib.lib().gf_ctx_set_flag(ctx.handle, _lib.FLAG_JOIN_LEGACY, legacy), ctx.handle, "flag")
+        try:
+            got = sf.PointPointJoinQuery(conf(sf), ug, qg).run(win(sf, ox, oy), win(sf, qx, qy), r)
+        finally:
+            _lib.lib().gf_ctx_set_flag(ctx.handle, _lib.FLAG_JOIN_LEGACY, 0)
+        np.testing.assert_array_equal(got, exp, err_msg=f"legacy={legacy}")
+
+
+def test_join_dense_rows_fall_back_to_global(sf, oracle_mod):
+    """A query row too dense to stage in LDS (every query point in one cell row) takes the
+    task's global-memory probe; a single dense cell as well."""
+    g = sf.UniformGrid(1000, *BEIJING)
+    og = oracle_mod.grid(1000, *BEIJING)
+    ox, oy = oracle_mod.java_random_points(91, 200_000, 115.5, 117.6, 40.0, 40.01)
+    qx, qy = oracle_mod.java_random_points(92, 60_000, 115.5, 117.6, 40.002, 40.004)
+    qx[:20_000] = 116.0 + 1e-7 * np.arange(20_000)
+    st, pairs = oracle_mod.join_pp(og, og, ox, oy, qx, qy, 0.001)
+    exp = np.array(sorted(map(tuple, pairs.tolist())), np.int64).reshape(-1, 2)
+    got = sf.PointPointJoinQuery(conf(sf), g, g).run(win(sf, ox, oy), win(sf, qx, qy), 0.001)
+    np.testing.assert_array_equal(got, exp)
+
+
 def test_knn_hint_across_windows(sf, oracle_mod):
     """Continuous query: each window reuses the previous window's threshold hint.  A window
     whose neighbourhood was emptied (hint too small) must be re-evaluated, still exactly."""

@@ -164,7 +164,7 @@ def bench_join(args):
     for i in range(args.warmup):
         step(i)
     torch.cuda.synchronize()
-    ctx.set_timing(1 << _lib.K_JOIN_PROBE)
+    ctx.set_timing((1 << _lib.K_JOIN_PROBE) | (1 << _lib.K_JOIN_BUCKET))
     t0 = time.perf_counter()
     total_pairs = 0
     for i in range(args.steps):
@@ -173,6 +173,7 @@ def bench_join(args):
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     ms, cnt = ctx.timing(_lib.K_JOIN_PROBE)
+    bms, bcnt = ctx.timing(_lib.K_JOIN_BUCKET)
     ctx.set_timing(0)
     avg = ms / 1000.0 / max(cnt, 1)
     pp = total_pairs / args.steps
@@ -180,6 +181,9 @@ def bench_join(args):
           "join_probe (count + write passes, per launch)", 16.0 * no + 8.0 * pp / 2, avg,
           {"config": {"workload": f"join_pp_{no // 1_000_000}Mx{nq / 1e6:g}M_r{r}_grid1000", "ordinary": no,
                       "query": nq, "radius": r, "pairs_per_window": pp},
+           "breakdown": {"probe_us_per_launch": round(avg * 1e6, 2), "probe_launches_per_window": cnt / args.steps,
+                         "bucket_us_per_launch": round(bms * 1000.0 / max(bcnt, 1), 2),
+                         "bucket_launches_per_window": bcnt / args.steps},
            "pairs_per_s": round(pp * args.steps / elapsed, 1)})
 
 
