@@ -55,7 +55,8 @@ extern "C" {
 #define GF_K_JOIN_PROBE  5
 #define GF_K_RANGE_TEST  6  /* deferred candidate tests of the many-object range plans */
 #define GF_K_JOIN_BUCKET 7  /* ordinary-side bucketing of the join */
-#define GF_K_COUNT       8
+#define GF_K_KNN_MERGE   8  /* top-k record merges (shards, sliding-window panes) */
+#define GF_K_COUNT       9
 
 typedef struct gf_ctx gf_ctx;
 
@@ -224,6 +225,42 @@ int    gf_knn_merge_dev_batch(gf_ctx* ctx, int32_t k, const void* records, int32
 int    gf_knn_merge_host(int32_t k, int32_t nlists, const int32_t* counts, const int64_t* objID,
                          const double* dist, const int64_t* idx, int64_t* out_objID,
                          double* out_dist, int64_t* out_idx, int32_t* n_out);
+
+/* ---- sliding-window kNN: pane engine ------------------------------------------------
+ * PointPointKNNQuery.windowBased with SlidingProcessingTimeWindows.of(size, slide)
+ * (PointPointKNNQuery.java:158,198-200; KNNQuery.java:213-272).  The reference re-evaluates
+ * every window from scratch (each point size/slide times); here the stream is cut into panes
+ * of gcd(size, slide) ms, each pane is evaluated ONCE on `plan` into a device record ring, and
+ * a window's record is the top-k-distinct merge of its panes' records -- identical to
+ * evaluating the window whole.  Pane p holds timestamps [p*pane_ms, (p+1)*pane_ms) (Flink
+ * window assignment, offset 0); window [e - size, e) closes with the pane ending at e for every
+ * multiple e of slide, and fires only if it holds a point.  Result idx = the point's position
+ * in the pushed stream (panes concatenated in push order). */
+typedef struct gf_knn_sliding gf_knn_sliding;
+/* size / gcd(size, slide) <= 64.  The plan's pipeline depth applies (depth 2: one fused launch
+ * per pane). */
+int  gf_knn_sliding_create(gf_knn_plan* plan, int64_t size_ms, int64_t slide_ms, gf_knn_sliding** out);
+void gf_knn_sliding_destroy(gf_knn_sliding* s);
+/* pane length, panes per window / per slide, and how many of the latest panes the engine keeps
+ * (their device buffers are borrowed and must stay valid while in the ring) */
+int  gf_knn_sliding_geometry(const gf_knn_sliding* s, int64_t* pane_ms, int32_t* panes_per_window,
+                             int32_t* panes_per_slide, int32_t* ring_panes);
+/* Async.  Push pane `pane_index` (consecutive indices; an empty pane is pushed with n = 0).  If
+ * a window closes with it, *closed = 1, *window_end = its end (ms), and its record is written
+ * to window_result (device or gf_pinned_alloc memory) -- at depth 2 by the next push or flush. */
+int  gf_knn_sliding_push(gf_knn_sliding* s, int64_t pane_index, const gf_points* pane, void* window_result,
+                         int32_t* closed, int64_t* window_end);
+int  gf_knn_sliding_flush(gf_knn_sliding* s);
+/* Sync: decode a host copy of a window record; a flagged record (a pane needed the exact
+ * fallback) is re-evaluated pane by pane (the panes must still be in the ring). */
+int  gf_knn_sliding_decode(gf_knn_sliding* s, int64_t window_end, const void* result_host, int64_t* objID,
+                           double* dist, int64_t* idx, int32_t* n_out);
+
+/* Async window assembler for a batch in timestamp order (processing-time ingestion):
+ * bounds (device int64[npanes + 1]) [j] = first i with ts[i] >= (first_pane + j) * pane_ms, so
+ * pane first_pane + j is the slice [bounds[j], bounds[j+1]).  ts must be non-decreasing. */
+int  gf_pane_bounds(gf_ctx* ctx, const int64_t* ts, int64_t n, int64_t pane_ms, int64_t first_pane, int32_t npanes,
+                    int64_t* bounds);
 
 /* ---- join (sync) --------------------------------------------------------------------
  * JoinQuery.getReplicatedPointQueryStream + PointPointJoinQuery.windowBased

@@ -999,13 +999,14 @@ static KnnScanArgs scan_args(gf_knn_plan* P, int j, const gf_points* pts, int64_
   return s;
 }
 
-static KnnSelectArgs select_args(gf_knn_plan* P, int j, int use_state, int write_hint, void* result) {
+static KnnSelectArgs select_args(gf_knn_plan* P, int j, int use_state, int write_hint, void* result,
+                                 int64_t idx_base) {
   const gf_knn_plan::Lane& L = P->lane[j];
   KnnSelectArgs q{};
   q.st = L.st; q.cand_d = L.cand_d; q.cand_i = L.cand_i; q.cand_o = L.cand_o;
   q.cap = (unsigned long long)P->cap;
   q.use_state = use_state; q.T = P->r; q.r = P->r; q.k = P->k; q.result = result;
-  q.write_hint = write_hint; q.idx_base = P->idx_base;
+  q.write_hint = write_hint; q.idx_base = idx_base;
   return q;
 }
 
@@ -1015,7 +1016,7 @@ static int knn_scan_select(gf_knn_plan* P, int j, const gf_points* pts, int64_t 
   gf_ctx* ctx = P->ctx;
   const KnnScanArgs s = scan_args(P, j, pts, begin, end, use_state);
   GF_HIP_CHECK(ctx, launch_knn_scan(ctx, s, scan_blocks_for(P, end - begin), P->scan_unroll, P->scan_nt));
-  GF_HIP_CHECK(ctx, launch_knn_select(ctx, select_args(P, j, use_state, write_hint, result)));
+  GF_HIP_CHECK(ctx, launch_knn_select(ctx, select_args(P, j, use_state, write_hint, result, P->idx_base)));
   return GF_OK;
 }
 
@@ -1046,10 +1047,11 @@ extern "C" int gf_knn_enqueue(gf_knn_plan* P, const gf_points* pts, void* result
     const KnnScanArgs s = scan_args(P, j, pts, 0, pts->n, sample ? 2 : 1);
     KnnSelectArgs q{};
     const int has_prev = P->pend_lane >= 0;
-    if (has_prev) q = select_args(P, P->pend_lane, 1, P->use_hint, P->pend_result);
+    if (has_prev) q = select_args(P, P->pend_lane, 1, P->use_hint, P->pend_result, P->pend_idx_base);
     GF_HIP_CHECK(ctx, launch_knn_fused(ctx, s, q, has_prev, scan_blocks_for(P, pts->n), P->scan_nt));
     P->pend_lane = j;
     P->pend_result = result;
+    P->pend_idx_base = P->idx_base;  // the index base in force when this window was enqueued
     return GF_OK;
   }
   // threshold: the previous window's hint (continuous query) or the sample; tiny windows
@@ -1065,7 +1067,8 @@ extern "C" int gf_knn_plan_flush(gf_knn_plan* P) {
   gf_ctx* ctx = P->ctx;
   int st = bind(ctx);
   if (st) return st;
-  GF_HIP_CHECK(ctx, launch_knn_select(ctx, select_args(P, P->pend_lane, 1, P->use_hint, P->pend_result)));
+  GF_HIP_CHECK(ctx, launch_knn_select(ctx, select_args(P, P->pend_lane, 1, P->use_hint, P->pend_result,
+                                                       P->pend_idx_base)));
   P->pend_lane = -1;
   P->pend_result = nullptr;
   return GF_OK;

@@ -195,6 +195,9 @@ hipError_t launch_word_popcounts(hipStream_t s, const uint64_t* bitmap, int64_t 
 hipError_t launch_expand_bitmap(hipStream_t s, const uint64_t* bitmap, int64_t words, int64_t n,
                                 const uint32_t* off, uint32_t* idx, int64_t cap);
 
+hipError_t launch_pane_bounds(hipStream_t s, const int64_t* ts, int64_t n, int64_t pane_ms, int64_t first_pane,
+                              int32_t nb, int64_t* bounds);
+
 hipError_t launch_knn_sample(gf_ctx* ctx, const KnnSampleArgs& a);
 hipError_t launch_knn_scan(gf_ctx* ctx, const KnnScanArgs& a, int blocks, int unroll, int nt);
 hipError_t launch_knn_select(gf_ctx* ctx, const KnnSelectArgs& a);
@@ -202,6 +205,12 @@ hipError_t launch_knn_fused(gf_ctx* ctx, const KnnScanArgs& a, const KnnSelectAr
                             int scan_blocks, int nt);
 hipError_t launch_knn_merge(gf_ctx* ctx, int32_t k, const void* records, int32_t nrec, size_t rec_stride,
                             int32_t nwin, size_t win_stride, void* result, size_t res_stride);
+// records of one merge given as a pointer list (kernel argument; the panes of a sliding window)
+constexpr int kMaxMergeRecs = 64;
+struct KnnRecList {
+  const char* rec[kMaxMergeRecs];
+};
+hipError_t launch_knn_merge_list(gf_ctx* ctx, int32_t k, const KnnRecList& list, int32_t nrec, void* result);
 
 hipError_t launch_range(gf_ctx* ctx, const RangeArgs& a, int table_mode, int poly, int blocks);
 hipError_t launch_range_finalize(hipStream_t s, const uint64_t* partials, int blocks, int64_t* counts);
@@ -334,6 +343,7 @@ struct gf_knn_plan {
   int pend_lane = -1;             // depth 2: the window whose select has not run yet
   int lane_warm[2] = {0, 0};      // depth 2: the lane has a hint from an earlier window
   void* pend_result = nullptr;
+  int64_t pend_idx_base = 0;      // depth 2: idx_base of the pending window (set at its enqueue)
   int use_hint = 1;             // reuse the previous window's k-th distance as the threshold guess
   int64_t idx_base = 0;
   void* tmp_result = nullptr;   // device record used by gf_knn_run / fallback

@@ -734,22 +734,31 @@ hipError_t launch_knn_fused(gf_ctx* ctx, const KnnScanArgs& a, const KnnSelectAr
   return hipGetLastError();
 }
 
-// Merge of per-shard records (nrec <= 64): whole records are appended to the running
-// top-k-distinct list while they fit the sort area, then sorted and deduped.
-// Block w merges window w: its nrec records start at records + w*win_stride, rec_stride apart;
-// the merged record goes to result + w*res_stride.
-__global__ __launch_bounds__(kSelT) void knn_merge_kernel(int32_t k, const char* records, int32_t nrec,
-                                                          size_t rec_bytes, size_t win_stride, void* result_base,
-                                                          size_t res_stride) {
+// Merge of per-shard / per-pane records (nrec <= 64): whole records are appended to the
+// running top-k-distinct list while they fit the sort area, then sorted and deduped.
+// Top-k-distinct of a union = top-k-distinct of the parts' top-k-distinct lists, so the
+// merged record equals evaluating the union directly.  The record source is a functor:
+// strided (all-gathered shard records, batched over windows) or a pointer list (the panes of
+// a sliding window, which wrap around the sliding engine's record ring).
+struct StridedRecs {
+  const char* base;
+  size_t stride;
+  __device__ const char* operator()(int r) const { return base + (size_t)r * stride; }
+};
+struct ListRecs {
+  const KnnRecList* l;
+  __device__ const char* operator()(int r) const { return l->rec[r]; }
+};
+
+template <class Src>
+__device__ void knn_merge_body(int32_t k, const Src& src, int32_t nrec, void* result) {
   __shared__ SelFull L;
-  __shared__ int s_off[65], s_status;
+  __shared__ int s_off[kMaxMergeRecs + 1], s_status;
   const int tid = threadIdx.x;
-  records += (size_t)blockIdx.x * win_stride;
-  void* result = (char*)result_base + (size_t)blockIdx.x * res_stride;
   if (tid == 0) {
     int off = 0, st = 0;
     for (int r = 0; r < nrec; ++r) {
-      const gf_knn_header* h = (const gf_knn_header*)(records + (size_t)r * rec_bytes);
+      const gf_knn_header* h = (const gf_knn_header*)src(r);
       s_off[r] = off;
       off += h->status == 0 ? h->n : 0;
       st = h->status > st ? h->status : st;
@@ -763,7 +772,7 @@ __global__ __launch_bounds__(kSelT) void knn_merge_kernel(int32_t k, const char*
     for (int i = tid; i < nr; i += kSelT) { L.sd[i] = L.rd[i]; L.so[i] = L.ro[i]; L.si[i] = L.ri[i]; }
     int cnt = nr;
     while (r < nrec && cnt + (s_off[r + 1] - s_off[r]) <= SelFull::kCap) {
-      RecView in = rec_view((void*)(records + (size_t)r * rec_bytes), k);
+      RecView in = rec_view((void*)src(r), k);
       const int n = s_off[r + 1] - s_off[r];
       for (int i = tid; i < n; i += kSelT) {
         L.sd[cnt + i] = dbits(in.d[i]); L.so[cnt + i] = okey(in.o[i]); L.si[cnt + i] = in.i[i];
@@ -789,10 +798,32 @@ __global__ __launch_bounds__(kSelT) void knn_merge_kernel(int32_t k, const char*
   }
 }
 
+// Block w merges window w: its nrec records start at records + w*win_stride, rec_stride apart;
+// the merged record goes to result + w*res_stride.
+__global__ __launch_bounds__(kSelT) void knn_merge_kernel(int32_t k, const char* records, int32_t nrec,
+                                                          size_t rec_stride, size_t win_stride, void* result_base,
+                                                          size_t res_stride) {
+  const StridedRecs src{records + (size_t)blockIdx.x * win_stride, rec_stride};
+  knn_merge_body(k, src, nrec, (char*)result_base + (size_t)blockIdx.x * res_stride);
+}
+
+__global__ __launch_bounds__(kSelT) void knn_merge_list_kernel(int32_t k, KnnRecList list, int32_t nrec,
+                                                               void* result) {
+  const ListRecs src{&list};
+  knn_merge_body(k, src, nrec, result);
+}
+
 hipError_t launch_knn_merge(gf_ctx* ctx, int32_t k, const void* records, int32_t nrec, size_t rec_stride,
                             int32_t nwin, size_t win_stride, void* result, size_t res_stride) {
+  KTimer t(ctx, GF_K_KNN_MERGE);
   hipLaunchKernelGGL(knn_merge_kernel, dim3(nwin), dim3(kSelT), 0, ctx->stream, k, (const char*)records, nrec,
                      rec_stride, win_stride, result, res_stride);
+  return hipGetLastError();
+}
+
+hipError_t launch_knn_merge_list(gf_ctx* ctx, int32_t k, const KnnRecList& list, int32_t nrec, void* result) {
+  KTimer t(ctx, GF_K_KNN_MERGE);
+  hipLaunchKernelGGL(knn_merge_list_kernel, dim3(1), dim3(kSelT), 0, ctx->stream, k, list, nrec, result);
   return hipGetLastError();
 }
 

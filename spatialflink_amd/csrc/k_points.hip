@@ -52,6 +52,32 @@ hipError_t launch_assign(gf_ctx* ctx, const gf_grid* g, const gf_points* p, int3
 }
 
 // ---------------------------------------------------------------------------------------
+// Pane boundaries of a time-ordered batch (the sliding-window assembler): bounds[j] = first i
+// with ts[i] >= (first_pane + j) * pane_ms, i.e. floor(ts / pane_ms) >= first_pane + j.  One
+// lane per boundary, binary search over the (non-decreasing) timestamps.
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void pane_bounds_kernel(const int64_t* __restrict__ ts, int64_t n, int64_t pane_ms,
+                                                         int64_t first_pane, int32_t nb, int64_t* __restrict__ bounds) {
+  const int32_t j = blockIdx.x * 64 + threadIdx.x;
+  if (j >= nb) return;
+  const int64_t target = (first_pane + j) * pane_ms;
+  int64_t lo = 0, hi = n;
+  while (lo < hi) {
+    const int64_t mid = lo + ((hi - lo) >> 1);
+    if (ts[mid] < target) lo = mid + 1;
+    else hi = mid;
+  }
+  bounds[j] = lo;
+}
+
+hipError_t launch_pane_bounds(hipStream_t s, const int64_t* ts, int64_t n, int64_t pane_ms, int64_t first_pane,
+                              int32_t nb, int64_t* bounds) {
+  hipLaunchKernelGGL(pane_bounds_kernel, dim3((nb + 63) / 64), dim3(64), 0, s, ts, n, pane_ms, first_pane, nb,
+                     bounds);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------
 // K2 building blocks.  Bucket key of a point:
 //   clamp_pad == 0: valid cell -> cy*n + cx, out-of-grid -> n*n            (gf_bucket_by_cell)
 // ---------------------------------------------------------------------------------------

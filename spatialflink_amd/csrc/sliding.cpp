@@ -1,0 +1,234 @@
+// sliding.cpp -- pane engine for sliding-window kNN (BASELINE configs[4]).
+//
+// The reference evaluates every sliding window from scratch: PointPointKNNQuery.windowBased
+// keys the stream by cell and applies SlidingProcessingTimeWindows.of(size, slide) twice --
+// per-cell heaps, then the windowAll merge (PointPointKNNQuery.java:158-200,
+// KNNQuery.java:213-272) -- so every point is scanned size/slide times.  Here the stream is cut
+// into panes of gcd(size, slide) ms: each pane is scanned ONCE (the fused kNN scan/select, one
+// launch per pane) into a top-k record kept in a device ring, and a window's result is the
+// top-k-distinct merge of its panes' records (one 256-thread merge launch).  Top-k-distinct of
+// a union = top-k-distinct of the parts' top-k-distinct lists, so the window record equals
+// evaluating the window whole -- bit for bit, including the (d, objID) order and idx.
+//
+// Flink window assignment (TimeWindow.getWindowStartWithOffset, offset 0): an element with
+// timestamp t lies in pane floor(t / pane); window [e - size, e) closes when the pane ending
+// at e is complete, for every e that is a multiple of slide; a window with no element never
+// fires.
+#include <algorithm>
+#include <climits>
+#include <numeric>
+#include <vector>
+
+#include "gf_internal.hpp"
+
+using namespace gf;
+
+struct gf_knn_sliding {
+  gf_knn_plan* plan = nullptr;
+  int64_t size_ms = 0, slide_ms = 0, pane_ms = 0;
+  int32_t W = 0;   // panes per window
+  int32_t S = 0;   // panes per slide
+  int32_t R = 0;   // ring slots (panes kept: borrowed buffers must stay alive that long)
+  size_t rb = 0;
+  char* recs = nullptr;  // device ring of R pane records
+  struct Pane {
+    int64_t index = LLONG_MIN;
+    gf_points pts{};
+    int64_t base = 0;    // stream position of the pane's first point (idx of results)
+  };
+  std::vector<Pane> ring;
+  bool started = false;
+  int64_t last = 0;      // last pushed pane index
+  int64_t pos = 0;       // stream position of the next pane's first point
+  // depth 2: a closed window whose last pane's select has not run yet
+  bool pend = false;
+  int64_t pend_last = 0;
+  void* pend_result = nullptr;
+};
+
+namespace {
+
+int64_t floor_mod(int64_t a, int64_t m) {
+  const int64_t r = a % m;
+  return r < 0 ? r + m : r;
+}
+int64_t floor_div(int64_t a, int64_t m) { return (a - floor_mod(a, m)) / m; }
+
+gf_knn_sliding::Pane& slot(gf_knn_sliding* s, int64_t p) { return s->ring[(size_t)floor_mod(p, s->R)]; }
+char* rec_of(gf_knn_sliding* s, int64_t p) { return s->recs + (size_t)floor_mod(p, s->R) * s->rb; }
+
+// the window ending with pane p: panes [p - W + 1, p]
+bool window_has_points(gf_knn_sliding* s, int64_t p) {
+  for (int64_t q = p - s->W + 1; q <= p; ++q) {
+    const gf_knn_sliding::Pane& pn = slot(s, q);
+    if (pn.index == q && pn.pts.n > 0) return true;
+  }
+  return false;
+}
+
+int merge_window(gf_knn_sliding* s, int64_t p, void* result) {
+  KnnRecList l{};
+  int n = 0;
+  for (int64_t q = p - s->W + 1; q <= p; ++q) {
+    const gf_knn_sliding::Pane& pn = slot(s, q);
+    if (pn.index == q && pn.pts.n > 0) l.rec[n++] = rec_of(s, q);
+  }
+  gf_ctx* ctx = s->plan->ctx;
+  GF_HIP_CHECK(ctx, launch_knn_merge_list(ctx, s->plan->k, l, n, result));
+  return GF_OK;
+}
+
+bool closes_window(const gf_knn_sliding* s, int64_t p) { return floor_mod(p + 1, s->S) == 0; }
+
+}  // namespace
+
+extern "C" int gf_knn_sliding_create(gf_knn_plan* plan, int64_t size_ms, int64_t slide_ms, gf_knn_sliding** out) {
+  if (!plan || !out || size_ms <= 0 || slide_ms <= 0) return GF_ERR_ARG;
+  *out = nullptr;
+  gf_ctx* ctx = plan->ctx;
+  const int64_t pane = std::gcd(size_ms, slide_ms);
+  const int64_t W = size_ms / pane, S = slide_ms / pane;
+  if (W > kMaxMergeRecs)
+    return set_err(ctx, GF_ERR_ARG, "gf_knn_sliding_create: size / gcd(size, slide) must be <= 64 panes");
+  int st = bind(ctx);
+  if (st) return st;
+  gf_knn_sliding* s = new gf_knn_sliding();
+  s->plan = plan;
+  s->size_ms = size_ms; s->slide_ms = slide_ms; s->pane_ms = pane;
+  s->W = (int32_t)W; s->S = (int32_t)S;
+  s->R = (int32_t)(2 * W + S + 2);  // a window's panes + those pushed before its record is read
+  s->rb = gf_knn_result_bytes(plan->k);
+  s->ring.resize((size_t)s->R);
+  hipError_t e = hipMalloc(&s->recs, s->rb * (size_t)s->R);
+  if (e != hipSuccess) {
+    delete s;
+    return hip_err(ctx, e, "hipMalloc");
+  }
+  *out = s;
+  return GF_OK;
+}
+
+extern "C" void gf_knn_sliding_destroy(gf_knn_sliding* s) {
+  if (!s) return;
+  hipSetDevice(s->plan->ctx->device);
+  hipStreamSynchronize(s->plan->ctx->stream);
+  if (s->recs) hipFree(s->recs);
+  delete s;
+}
+
+extern "C" int gf_knn_sliding_geometry(const gf_knn_sliding* s, int64_t* pane_ms, int32_t* panes_per_window,
+                                       int32_t* panes_per_slide, int32_t* ring_panes) {
+  if (!s) return GF_ERR_ARG;
+  if (pane_ms) *pane_ms = s->pane_ms;
+  if (panes_per_window) *panes_per_window = s->W;
+  if (panes_per_slide) *panes_per_slide = s->S;
+  if (ring_panes) *ring_panes = s->R;
+  return GF_OK;
+}
+
+extern "C" int gf_knn_sliding_push(gf_knn_sliding* s, int64_t pane_index, const gf_points* pane, void* window_result,
+                                   int32_t* closed, int64_t* window_end) {
+  if (!s || !pane || !closed) return GF_ERR_ARG;
+  gf_knn_plan* P = s->plan;
+  gf_ctx* ctx = P->ctx;
+  *closed = 0;
+  if (s->started && pane_index != s->last + 1)
+    return set_err(ctx, GF_ERR_ARG, "gf_knn_sliding_push: panes must be pushed consecutively (empty panes with n = 0)");
+  if (pane->n < 0) return set_err(ctx, GF_ERR_ARG, "gf_knn_sliding_push: negative n");
+  int st = bind(ctx);
+  if (st) return st;
+  gf_knn_sliding::Pane& pn = slot(s, pane_index);
+  pn.index = pane_index;
+  pn.pts = *pane;
+  pn.base = s->pos;
+  if (pane->n > 0) {
+    P->idx_base = s->pos;
+    // depth 2: the fused launch also selects the previous non-empty pane into its ring slot
+    if ((st = gf_knn_enqueue(P, pane, rec_of(s, pane_index)))) return st;
+  } else if ((st = gf_knn_plan_flush(P))) {
+    return st;
+  }
+  s->pos += pane->n;
+  s->started = true;
+  s->last = pane_index;
+  // every record of a pane before this one is complete (stream order); this pane's too unless
+  // its select is still pending (depth 2)
+  if (s->pend) {
+    s->pend = false;
+    if ((st = merge_window(s, s->pend_last, s->pend_result))) return st;
+  }
+  if (closes_window(s, pane_index) && window_has_points(s, pane_index)) {
+    if (!window_result) return set_err(ctx, GF_ERR_ARG, "gf_knn_sliding_push: a window closes, result is null");
+    *closed = 1;
+    if (window_end) *window_end = (pane_index + 1) * s->pane_ms;
+    if (P->pend_lane >= 0) {
+      s->pend = true;
+      s->pend_last = pane_index;
+      s->pend_result = window_result;
+    } else if ((st = merge_window(s, pane_index, window_result))) {
+      return st;
+    }
+  }
+  return GF_OK;
+}
+
+extern "C" int gf_knn_sliding_flush(gf_knn_sliding* s) {
+  if (!s) return GF_ERR_ARG;
+  int st = bind(s->plan->ctx);
+  if (st || (st = gf_knn_plan_flush(s->plan))) return st;
+  if (s->pend) {
+    s->pend = false;
+    return merge_window(s, s->pend_last, s->pend_result);
+  }
+  return GF_OK;
+}
+
+extern "C" int gf_pane_bounds(gf_ctx* ctx, const int64_t* ts, int64_t n, int64_t pane_ms, int64_t first_pane,
+                              int32_t npanes, int64_t* bounds) {
+  if (!ctx || pane_ms <= 0 || npanes < 0 || n < 0 || !bounds || (n > 0 && !ts))
+    return set_err(ctx, GF_ERR_ARG, "gf_pane_bounds: bad argument");
+  int st = bind(ctx);
+  if (st) return st;
+  GF_HIP_CHECK(ctx, launch_pane_bounds(ctx->stream, ts, n, pane_ms, first_pane, npanes + 1, bounds));
+  return GF_OK;
+}
+
+extern "C" int gf_knn_sliding_decode(gf_knn_sliding* s, int64_t window_end, const void* result_host, int64_t* oo,
+                                     double* od, int64_t* oi, int32_t* n_out) {
+  if (!s || !result_host || !n_out) return GF_ERR_ARG;
+  gf_knn_plan* P = s->plan;
+  const gf_knn_header* h = (const gf_knn_header*)result_host;
+  if (h->status == 0) return gf_knn_decode(P, nullptr, result_host, oo, od, oi, n_out);
+  // a pane overflowed its candidate buffer or its threshold guess failed: evaluate each pane of
+  // the window exactly (the plan's decode fallback) and merge on the host
+  const int64_t p = floor_div(window_end, s->pane_ms) - 1;
+  int st = gf_knn_sliding_flush(s);
+  if (st) return st;
+  std::vector<int32_t> counts;
+  std::vector<int64_t> o, i;
+  std::vector<double> d;
+  const int32_t k = P->k;
+  std::vector<int64_t> to(k), ti(k);
+  std::vector<double> td(k);
+  const int64_t saved_base = P->idx_base;
+  for (int64_t q = p - s->W + 1; q <= p; ++q) {
+    const gf_knn_sliding::Pane& pn = slot(s, q);
+    if (pn.index != q) {
+      P->idx_base = saved_base;
+      return set_err(P->ctx, GF_ERR_ARG, "gf_knn_sliding_decode: the window's panes left the ring");
+    }
+    if (pn.pts.n == 0) continue;
+    int32_t m = 0;
+    P->idx_base = pn.base;
+    if ((st = gf_knn_run(P, &pn.pts, to.data(), td.data(), ti.data(), &m))) {
+      P->idx_base = saved_base;
+      return st;
+    }
+    counts.push_back(m);
+    o.insert(o.end(), to.begin(), to.begin() + m);
+    d.insert(d.end(), td.begin(), td.begin() + m);
+    i.insert(i.end(), ti.begin(), ti.begin() + m);
+  }
+  P->idx_base = saved_base;
+  return gf_knn_merge_host(k, (int32_t)counts.size(), counts.data(), o.data(), d.data(), i.data(), oo, od, oi, n_out);
+}

@@ -187,10 +187,239 @@ def bench_join(args):
            "pairs_per_s": round(pp * args.steps / elapsed, 1)})
 
 
+def bench_sliding(args):
+    """C5: sliding-window kNN, k = 100, 1000 x 1000 grid, 100M points per window, size/slide = 2
+    (panes of 50M points), r = 0.5 around the README query point.  A step = one slide: one pane
+    pushed through the pane engine (one fused scan/select launch) and one window record merged
+    from its two panes.  value = window points / s (each window holds 100M points; the
+    reference re-evaluates all of them per window, the engine scans each pane once).  N > 1:
+    strong scaling -- the window's points are split across ranks by cell-column bands, each
+    rank runs its own pane engine on its band and the window records of B consecutive windows
+    are all-gathered over RCCL and merged in one launch."""
+    import torch
+    import torch.distributed as dist
+
+    import spatialflink_amd as sf
+    from spatialflink_amd import _lib, sharding
+    from spatialflink_amd.spatialOperators import knn_record_bytes
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local % torch.cuda.device_count())
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.cuda.current_device()
+    L = _lib.lib()
+    k = args.k if args.k != 50 else 100
+    grid_n = args.grid if args.grid != 500 else 1000
+    window_pts = args.points or 100_000_000
+    W = 2                                     # size / slide
+    pane_pts = window_pts // W // world       # this rank's share of one pane
+    pane_pts -= pane_pts % 2
+    npanes = max(3, args.windows)             # distinct device-resident panes cycled
+    grid = sf.UniformGrid(grid_n, *BEIJING)
+    if world == 1:
+        xlo, xhi = BEIJING[0], BEIJING[1]
+    else:
+        lo, hi = sharding.column_bands(grid_n, world)[rank]
+        xlo, xhi = sharding.band_x_range(grid, lo, hi)
+    t = time.perf_counter()
+    panes, host = [], []
+    for j in range(npanes):
+        x, y = sf.synthetic_uniform(4242 + 1000 * rank + j, pane_pts, xlo, xhi, BEIJING[2], BEIJING[3])
+        obj = np.arange(pane_pts, dtype=np.int64) + (rank * npanes + j) * pane_pts
+        panes.append(sf.PointWindow.from_numpy(x, y, obj, device=dev))
+        host.append((x, y, obj))
+    torch.cuda.synchronize()
+    print(f"[rank {rank}] {npanes} panes x {pane_pts} points generated+uploaded in {time.perf_counter() - t:.1f}s",
+          file=sys.stderr, flush=True)
+    conf = sf.QueryConfiguration(sf.QueryType.WindowBased)
+    q = sf.Point("q", QPOINT[0], QPOINT[1], 0, grid)
+    op = sf.PointPointKNNQuery(conf, grid)
+    ctx, plan = op.plan(dev, q, args.radius, k)
+    _lib.check(L.gf_knn_plan_set_pipeline(plan, args.pipeline), ctx.handle, "pipeline")
+    size_ms, slide_ms = 2000, 1000
+    eng = C.c_void_p()
+    _lib.check(L.gf_knn_sliding_create(plan, size_ms, slide_ms, C.byref(eng)), ctx.handle, "sliding")
+    rb = knn_record_bytes(k)
+    B = max(1, args.exchange_batch)
+    total = args.warmup + args.steps
+    recs = torch.zeros(total, rb, dtype=torch.uint8, device=dev)   # rank-local window records
+    merged = sf.PinnedRecords(total, k) if world > 1 else None
+    out = merged if world > 1 else sf.PinnedRecords(total, k)
+    pts = [p.c_struct() for p in panes]
+    closed, wend = C.c_int32(), C.c_int64()
+    lag = 1 if args.pipeline == 2 else 0
+    push = L.gf_knn_sliding_push
+
+    def exchange(lo, hi):  # windows [lo, hi]: one all-gather + one merge launch
+        sharding.allgather_knn_records_batch(recs[lo:hi + 1], k, out.ptr(lo))
+
+    def step(i, first):
+        dst = recs[i].data_ptr() if world > 1 else out.ptr(i)
+        st = push(eng, i, C.byref(pts[i % npanes]), C.c_void_p(dst), C.byref(closed), C.byref(wend))
+        if st:
+            _lib.check(st, ctx.handle, "gf_knn_sliding_push")
+        if world > 1:
+            c = i - lag
+            if c >= first and (c - first) % B == B - 1:
+                exchange(c - B + 1, c)
+
+    def drain(first, last):
+        _lib.check(L.gf_knn_sliding_flush(eng), ctx.handle, "flush")
+        if world > 1:
+            lo = first + ((last - first) // B) * B
+            if lag or (last - first) % B != B - 1:
+                exchange(lo, last)
+
+    for i in range(args.warmup):
+        step(i, 0)
+    drain(0, args.warmup - 1)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    ctx.set_timing_period(args.timing_period)
+    ctx.set_timing((1 << _lib.K_KNN_SCAN) | (1 << _lib.K_KNN_MERGE))
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for i in range(args.warmup, total):
+        step(i, args.warmup)
+    drain(args.warmup, total - 1)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    scan_ms, scan_n = ctx.timing(_lib.K_KNN_SCAN)
+    merge_ms, merge_n = ctx.timing(_lib.K_KNN_MERGE)
+    ctx.set_timing(0)
+    ctx.set_timing_period(1)
+    elapsed = t1 - t0
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+
+    # every timed window record is final (no fallback) and deterministic per distinct window
+    # (engine idx = stream position; window i starts at pane i-1, position (i-1) * pane_pts)
+    per = {}
+    for i in range(max(1, args.warmup), total):
+        st, o, d, ix = out.decode(i)
+        assert st == 0, f"window {i} needed the exact fallback inside the timed region"
+        key = ((i - 1) % npanes, i % npanes)
+        rel = ix - (i - 1) * pane_pts
+        if key in per:
+            assert all(np.array_equal(u, v) for u, v in zip(per[key], (o, d, rel))), "non-deterministic"
+        else:
+            per[key] = (o, d, rel)
+
+    # parity (N = 1): each distinct window == the same plan's whole-window evaluation of the two
+    # panes concatenated (the reference's from-scratch evaluation; gf_knn_run is oracle-checked in
+    # tests/), and the first window == the oracle; plus the from-scratch time for comparison
+    verified, scratch_us = None, None
+    if world == 1:
+        op2 = sf.PointPointKNNQuery(conf, grid)
+        ctx2, plan2 = op2.plan(dev, q, args.radius, k)
+        verified = True
+        for (a, b), (o, d, ix) in sorted(per.items()):
+            wa, wb = panes[a], panes[b]
+            cat = sf.PointWindow(torch.cat([wa.x, wb.x]), torch.cat([wa.y, wb.y]), torch.cat([wa.objID, wb.objID]),
+                                 torch.cat([wa.timeStampMillisec, wb.timeStampMillisec]))
+            res = op2.run(cat, q, args.radius, k)
+            verified &= bool(np.array_equal(res.objID, o) and np.array_equal(res.dist, d)
+                             and np.array_equal(res.idx, ix))
+            if scratch_us is None:  # the from-scratch alternative: one 100M-point evaluation per window
+                _lib.check(L.gf_knn_plan_set_pipeline(plan2, args.pipeline), ctx2.handle, "pipeline")
+                tmp = torch.zeros(8, rb, dtype=torch.uint8, device=dev)
+                cs = cat.c_struct()
+                for it in range(3):
+                    L.gf_knn_enqueue(plan2, C.byref(cs), C.c_void_p(tmp[it].data_ptr()))
+                L.gf_knn_plan_flush(plan2)
+                torch.cuda.synchronize()
+                ts_ = time.perf_counter()
+                for it in range(8):
+                    L.gf_knn_enqueue(plan2, C.byref(cs), C.c_void_p(tmp[it].data_ptr()))
+                L.gf_knn_plan_flush(plan2)
+                torch.cuda.synchronize()
+                scratch_us = 1e6 * (time.perf_counter() - ts_) / 8
+            del cat
+        assert verified, "pane-merged windows differ from whole-window evaluation"
+        if not args.no_verify:
+            sys.path.insert(0, os.path.join(ROOT, "oracle"))
+            import oracle as O
+
+            (a, b), (o, d, ix) = sorted(per.items())[0]
+            X = np.concatenate([host[a][0], host[b][0]]); Y = np.concatenate([host[a][1], host[b][1]])
+            OB = np.concatenate([host[a][2], host[b][2]])
+            t = time.perf_counter()
+            st, eo, ed, ei = O.knn(O.grid(grid_n, *BEIJING), X, Y, OB, QPOINT[0], QPOINT[1], args.radius, k)
+            verified &= bool(st == 0 and np.array_equal(eo, o) and np.array_equal(ed, d) and np.array_equal(ei, ix))
+            print(f"oracle check of one {len(X)}-point window: {verified} ({time.perf_counter() - t:.1f}s)",
+                  file=sys.stderr, flush=True)
+            assert verified, "pane-merged window differs from the oracle"
+
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle as O
+
+        S = min(args.cpu_sample, pane_pts)
+        x, y, obj = host[0]
+        xs, ys, os_ = (np.ascontiguousarray(a[:S]) for a in (x, y, obj))
+        og = O.grid(grid_n, *BEIJING)
+        reps, t = 0, time.perf_counter()
+        while True:
+            O.knn(og, xs, ys, os_, QPOINT[0], QPOINT[1], args.radius, k, reference_shaped=True)
+            reps += 1
+            if time.perf_counter() - t >= args.cpu_seconds:
+                break
+        ct = time.perf_counter() - t
+        cpu = {"value": round(reps * S / ct, 1), "unit": "window points/s", "cores": 1, "kind": "port",
+               "sample": (f"first {S} points of a window x {reps} reps ({ct:.1f}s): oracle's reference-shaped "
+                          "evaluator (string cell IDs, HashSet C/G filter, per-cell PriorityQueue, windowAll merge), "
+                          "1 thread; the reference evaluates every window from scratch")}
+    if rank == 0:
+        avg = scan_ms / 1000.0 / max(scan_n, 1)
+        steps = args.steps
+        d = {"metric": "points/sec per window (sliding-window kNN k=100)", "value": round(window_pts * steps / elapsed, 1),
+             "unit": "window points/s", "n_gpus": world, "steps": steps, "warmup": args.warmup,
+             "ms_per_step": round(1000.0 * elapsed / steps, 4), "higher_is_better": True,
+             "scaling": "strong" if world > 1 else "weak", "vs_baseline": None, "dtype": "f64",
+             "data": f"synthetic: java.util.Random-compatible uniform points, Beijing bounds, {npanes} distinct "
+                     "device-resident panes cycled",
+             "config": {"workload": f"sliding_knn_k{k}_r{args.radius}_{window_pts // 1_000_000}Mpts_grid{grid_n}",
+                        "window_points": window_pts, "size_over_slide": W, "pane_points_per_gpu": pane_pts,
+                        "k": k, "radius": args.radius, "grid": grid_n, "windows_in_flight": args.pipeline,
+                        "parallelism": f"cell-column shards x{world}" + (" + RCCL all-gather top-k" if world > 1 else ""),
+                        "exchange_batch": B if world > 1 else None},
+             "roofline": {"bound": "hbm", "kernel": "knn_fused (scan of pane i + select of pane i-1)",
+                          "achieved": round(16.0 * pane_pts / avg / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                          "frac": round(16.0 * pane_pts / avg / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
+                          "bytes_per_launch": 16.0 * pane_pts, "avg_launch_us": round(avg * 1e6, 2),
+                          "launches_timed": scan_n},
+             "scanned_points_per_s": round(pane_pts * world * steps / elapsed, 1),
+             "breakdown": {"merge_us": round(1000.0 * merge_ms / max(merge_n, 1), 2),
+                           "from_scratch_window_us": round(scratch_us, 2) if scratch_us else None},
+             "cpu_baseline": cpu, "verified_vs_whole_window_and_oracle": verified}
+        print(json.dumps(d), flush=True)
+    L.gf_knn_sliding_destroy(eng)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def run(args):
     if args.workload in ("range", "ppoly"):
         bench_range(args, polygons=args.workload == "ppoly")
     elif args.workload == "join":
         bench_join(args)
+    elif args.workload == "sliding":
+        bench_sliding(args)
     else:
         raise SystemExit(f"unknown workload {args.workload}")
