@@ -233,8 +233,8 @@ int    gf_knn_merge_host(int32_t k, int32_t nlists, const int32_t* counts, const
  * of gcd(size, slide) ms, each pane is evaluated ONCE on `plan` into a device record ring, and
  * a window's record is the top-k-distinct merge of its panes' records -- identical to
  * evaluating the window whole.  Pane p holds timestamps [p*pane_ms, (p+1)*pane_ms) (Flink
- * window assignment, offset 0); window [e - size, e) closes with the pane ending at e for every
- * multiple e of slide, and fires only if it holds a point.  Result idx = the point's position
+ * window assignment, offset 0); window [s, s + size), s a multiple of slide, closes with the
+ * pane ending at s + size, and fires only if it holds a point.  Result idx = the point's position
  * in the pushed stream (panes concatenated in push order). */
 typedef struct gf_knn_sliding gf_knn_sliding;
 /* size / gcd(size, slide) <= 64.  The plan's pipeline depth applies (depth 2: one fused launch

@@ -93,6 +93,10 @@ def lib():
             raise ImportError(
                 f"{LIB_PATH} is missing: build it with `make` (or __graft_entry__.build()). "
                 "There is no CPU fallback for the window-evaluation path.")
+        # torch first: it ships its own libamdhip64 (same soname); whichever loads first serves the
+        # process, and torch must get the runtime it was built against
+        import torch  # noqa: F401
+
         L = C.CDLL(LIB_PATH)
         P, i32, i64, d, sz = C.c_void_p, C.c_int32, C.c_int64, C.c_double, C.c_size_t
         pi32, pi64, pd = C.POINTER(i32), C.POINTER(i64), C.POINTER(d)

@@ -11,9 +11,8 @@
 // evaluating the window whole -- bit for bit, including the (d, objID) order and idx.
 //
 // Flink window assignment (TimeWindow.getWindowStartWithOffset, offset 0): an element with
-// timestamp t lies in pane floor(t / pane); window [e - size, e) closes when the pane ending
-// at e is complete, for every e that is a multiple of slide; a window with no element never
-// fires.
+// timestamp t lies in pane floor(t / pane); window [s, s + size) (s a multiple of slide) closes
+// when the pane ending at s + size is complete; a window with no element never fires.
 #include <algorithm>
 #include <climits>
 #include <numeric>
@@ -38,6 +37,7 @@ struct gf_knn_sliding {
   };
   std::vector<Pane> ring;
   bool started = false;
+  int64_t first = 0;     // first pushed pane index (earlier panes are empty)
   int64_t last = 0;      // last pushed pane index
   int64_t pos = 0;       // stream position of the next pane's first point
   // depth 2: a closed window whose last pane's select has not run yet
@@ -78,7 +78,9 @@ int merge_window(gf_knn_sliding* s, int64_t p, void* result) {
   return GF_OK;
 }
 
-bool closes_window(const gf_knn_sliding* s, int64_t p) { return floor_mod(p + 1, s->S) == 0; }
+// windows start at multiples of slide, so they end at e = start + size: pane p closes one iff
+// (p + 1) * pane - size is a multiple of slide, i.e. (p + 1 - W) mod S == 0
+bool closes_window(const gf_knn_sliding* s, int64_t p) { return floor_mod(p + 1 - s->W, s->S) == 0; }
 
 }  // namespace
 
@@ -149,6 +151,7 @@ extern "C" int gf_knn_sliding_push(gf_knn_sliding* s, int64_t pane_index, const 
     return st;
   }
   s->pos += pane->n;
+  if (!s->started) s->first = pane_index;
   s->started = true;
   s->last = pane_index;
   // every record of a pane before this one is complete (stream order); this pane's too unless
@@ -212,6 +215,7 @@ extern "C" int gf_knn_sliding_decode(gf_knn_sliding* s, int64_t window_end, cons
   std::vector<double> td(k);
   const int64_t saved_base = P->idx_base;
   for (int64_t q = p - s->W + 1; q <= p; ++q) {
+    if (q < s->first) continue;  // before the stream: empty
     const gf_knn_sliding::Pane& pn = slot(s, q);
     if (pn.index != q) {
       P->idx_base = saved_base;

@@ -64,7 +64,8 @@ class SlidingWindows:
         return np.floor_divide(np.asarray(ts, np.int64), self.pane)
 
     def closes(self, pane_index: int) -> bool:
-        return (pane_index + 1) % self.panes_per_slide == 0
+        """Windows start at multiples of slide: pane p ends one iff (p+1)*pane - size is one."""
+        return (pane_index + 1 - self.panes_per_window) % self.panes_per_slide == 0
 
     def window_of_last_pane(self, pane_index: int):
         end = (pane_index + 1) * self.pane
@@ -174,6 +175,7 @@ class SlidingKNNQuery:
         self.closed = []             # (window_end, record slot, first pane)
         self.nclosed = 0
         self.pending = False         # depth 2: the newest closed window's record is not written yet
+        self.ready = []              # decoded KNNResults not yet returned by results()
         self.stream = _PaneStream(self.geo)
 
     # -- panes ---------------------------------------------------------------------------
@@ -202,6 +204,10 @@ class SlidingKNNQuery:
             self.closed.append((end.value, slot, p - self.geo.panes_per_window + 1))
             self.nclosed += 1
             self.pending = self.depth == 2 and not empty
+        # a flagged record is re-evaluated from its panes, which the engine keeps for `ring`
+        # panes only: decode before the oldest undecoded window's panes leave the ring
+        if self.closed and p - self.closed[0][2] >= self.ring - 2:
+            self._collect()
 
     def push(self, batch: PointWindow):
         for p, pane in self.stream.feed(batch):
@@ -223,25 +229,26 @@ class SlidingKNNQuery:
 
     def results(self):
         """KNNResults of the windows fired so far whose records are complete (syncs)."""
+        self._collect()
+        out, self.ready = self.ready, []
+        return out
+
+    def _collect(self):
         import torch
 
         torch.cuda.synchronize(self.ctx.device)
         ready = self.closed[:-1] if self.pending else self.closed
         self.closed = self.closed[len(ready):]
-        out = []
         for end, slot, first in ready:
-            base = self.panes[first][1] if first in self.panes else None
+            base = self.panes[first][1] if first in self.panes else self._base_of(first)
             oo = np.empty(self.k, np.int64); od = np.empty(self.k, np.float64); oi = np.empty(self.k, np.int64)
             n = C.c_int32()
             buf = C.create_string_buffer(self.records.raw(slot), self.records.bytes)
             st = _lib.lib().gf_knn_sliding_decode(self.handle, int(end), buf, oo.ctypes.data, od.ctypes.data,
                                                   oi.ctypes.data, C.byref(n))
             _lib.check(st, self.ctx.handle, "gf_knn_sliding_decode")
-            if base is None:
-                base = self._base_of(first)
             m = n.value
-            out.append(KNNResult(end - self.geo.size, end, oo[:m].copy(), od[:m].copy(), oi[:m] - base))
-        return out
+            self.ready.append(KNNResult(end - self.geo.size, end, oo[:m].copy(), od[:m].copy(), oi[:m] - base))
 
     def _base_of(self, first):
         for q, (_, pos) in self.panes.items():

@@ -53,6 +53,7 @@ def conf(sf):
 
 @pytest.mark.parametrize("size,slide,k,depth,n,cap", [
     (3000, 1000, 50, 2, 900_000, None),
+    (3000, 1000, 50, 1, 900_000, None),
     (4000, 2000, 120, 1, 700_000, None),
     (5000, 3000, 7, 2, 600_000, None),
     (2000, 1000, 50, 2, 400_000, 64),      # every pane overflows: pane-by-pane exact decode
@@ -79,7 +80,8 @@ def test_sliding_knn_matches_oracle(sf, oracle_mod, size, slide, k, depth, n, ca
         assert st == 0
         np.testing.assert_array_equal(r.objID, eo)
         np.testing.assert_array_equal(r.dist, ed)
-        np.testing.assert_array_equal(r.idx, ei)
+        np.testing.assert_array_equal(r.idx, ei, err_msg=f"window {r.windowStart}..{r.windowEnd} points {m.sum()} "
+                                      f"before {np.count_nonzero(ts < r.windowStart)} panes {sorted(op.panes.items())[:3]}")
 
 
 def test_pane_bounds_kernel(sf, oracle_mod):

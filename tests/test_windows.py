@@ -25,7 +25,7 @@ def test_window_assignment_matches_panes(size, slide):
     # a window closes with the pane ending at its end
     for p in range(-20, 40):
         s, e = g.window_of_last_pane(p)
-        assert g.closes(p) == (e % slide == 0)
+        assert g.closes(p) == (s % slide == 0)
         assert e - s == size
 
 
