@@ -1030,6 +1030,13 @@ static int knn_launch_sample(gf_knn_plan* P, int j, const gf_points* pts, int us
 }
 
 extern "C" int gf_knn_enqueue(gf_knn_plan* P, const gf_points* pts, void* result) {
+  int merged = 0;
+  return gf::knn_enqueue_merge(P, pts, result, nullptr, &merged);
+}
+
+int gf::knn_enqueue_merge(gf_knn_plan* P, const gf_points* pts, void* result, const KnnMergeArgs* merge,
+                          int* merged) {
+  *merged = 0;
   if (!P || !result) return GF_ERR_ARG;
   gf_ctx* ctx = P->ctx;
   int st = bind(ctx);
@@ -1048,7 +1055,10 @@ extern "C" int gf_knn_enqueue(gf_knn_plan* P, const gf_points* pts, void* result
     KnnSelectArgs q{};
     const int has_prev = P->pend_lane >= 0;
     if (has_prev) q = select_args(P, P->pend_lane, 1, P->use_hint, P->pend_result, P->pend_idx_base);
-    GF_HIP_CHECK(ctx, launch_knn_fused(ctx, s, q, has_prev, scan_blocks_for(P, pts->n), P->scan_nt));
+    const bool fold = merge && merge->nrec > 0 && has_prev && P->k <= kFusedMergeMaxK;
+    GF_HIP_CHECK(ctx, launch_knn_fused(ctx, s, q, has_prev, scan_blocks_for(P, pts->n), P->scan_nt,
+                                       fold ? merge : nullptr));
+    *merged = fold ? 1 : 0;
     P->pend_lane = j;
     P->pend_result = result;
     P->pend_idx_base = P->idx_base;  // the index base in force when this window was enqueued

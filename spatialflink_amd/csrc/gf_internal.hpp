@@ -201,8 +201,7 @@ hipError_t launch_pane_bounds(hipStream_t s, const int64_t* ts, int64_t n, int64
 hipError_t launch_knn_sample(gf_ctx* ctx, const KnnSampleArgs& a);
 hipError_t launch_knn_scan(gf_ctx* ctx, const KnnScanArgs& a, int blocks, int unroll, int nt);
 hipError_t launch_knn_select(gf_ctx* ctx, const KnnSelectArgs& a);
-hipError_t launch_knn_fused(gf_ctx* ctx, const KnnScanArgs& a, const KnnSelectArgs& prev, int has_prev,
-                            int scan_blocks, int nt);
+
 hipError_t launch_knn_merge(gf_ctx* ctx, int32_t k, const void* records, int32_t nrec, size_t rec_stride,
                             int32_t nwin, size_t win_stride, void* result, size_t res_stride);
 // records of one merge given as a pointer list (kernel argument; the panes of a sliding window)
@@ -211,6 +210,18 @@ struct KnnRecList {
   const char* rec[kMaxMergeRecs];
 };
 hipError_t launch_knn_merge_list(gf_ctx* ctx, int32_t k, const KnnRecList& list, int32_t nrec, void* result);
+// a window merge folded into block 0 of the next fused launch (after the select it waits for)
+constexpr int kFusedMergeMaxK = 128;
+struct KnnMergeArgs {
+  int32_t nrec;   // 0 = none
+  void* result;
+  KnnRecList list;
+};
+hipError_t launch_knn_fused(gf_ctx* ctx, const KnnScanArgs& a, const KnnSelectArgs& prev, int has_prev,
+                            int scan_blocks, int nt, const KnnMergeArgs* merge);
+// gf_knn_enqueue with an optional window merge for the fused launch; *merged = 1 if it was
+// folded in (depth 2, a pending select, k <= kFusedMergeMaxK), else the caller launches it
+int knn_enqueue_merge(gf_knn_plan* P, const gf_points* pts, void* result, const KnnMergeArgs* merge, int* merged);
 
 hipError_t launch_range(gf_ctx* ctx, const RangeArgs& a, int table_mode, int poly, int blocks);
 hipError_t launch_range_finalize(hipStream_t s, const uint64_t* partials, int blocks, int64_t* counts);

@@ -696,44 +696,6 @@ hipError_t launch_knn_select(gf_ctx* ctx, const KnnSelectArgs& a) {
   return hipGetLastError();
 }
 
-// Fused continuous-query kernel (pipeline depth 2): blocks 1.. scan window i with the
-// threshold taken from the lane's hint (set by window i-2's select) -- or, for a lane's first
-// window (use_state 2), from the sample kernel launched just before; block 0, dispatched
-// first, runs window i-1's select on the other lane while they stream.  One launch per window.
-template <int METRIC, int NT>
-__global__ __launch_bounds__(kBlock) void knn_fused_kernel(KnnScanArgs a, KnnSelectArgs prev, int has_prev) {
-  __shared__ SelLite L;
-  if (blockIdx.x == 0) {
-    if (has_prev) knn_select_body<SelLite, false>(prev, L);
-    return;
-  }
-  double T, sp;
-  if (a.use_state == 2) {  // cold lane: the sample kernel just set T
-    T = a.st->T;
-    sp = a.st->s_pre;
-  } else {
-    const double h = a.st->hint_T;
-    T = (h > 0.0 && h < a.T) ? h : a.T;  // a.T = r
-    sp = s_prefilter(T, a.metric);
-    if (blockIdx.x == 1 && threadIdx.x == 0) { a.st->T = T; a.st->s_pre = sp; }
-  }
-  knn_scan_body<METRIC, 1, NT>(a, sp, T, blockIdx.x - 1, gridDim.x - 1);
-}
-
-hipError_t launch_knn_fused(gf_ctx* ctx, const KnnScanArgs& a, const KnnSelectArgs& prev, int has_prev,
-                            int scan_blocks, int nt) {
-  KTimer t(ctx, GF_K_KNN_SCAN);
-  const dim3 g(scan_blocks + 1), b(kBlock);
-  if (a.metric == 0) {
-    if (nt) hipLaunchKernelGGL((knn_fused_kernel<0, 1>), g, b, 0, ctx->stream, a, prev, has_prev);
-    else hipLaunchKernelGGL((knn_fused_kernel<0, 0>), g, b, 0, ctx->stream, a, prev, has_prev);
-  } else {
-    if (nt) hipLaunchKernelGGL((knn_fused_kernel<1, 1>), g, b, 0, ctx->stream, a, prev, has_prev);
-    else hipLaunchKernelGGL((knn_fused_kernel<1, 0>), g, b, 0, ctx->stream, a, prev, has_prev);
-  }
-  return hipGetLastError();
-}
-
 // Merge of per-shard / per-pane records (nrec <= 64): whole records are appended to the
 // running top-k-distinct list while they fit the sort area, then sorted and deduped.
 // Top-k-distinct of a union = top-k-distinct of the parts' top-k-distinct lists, so the
@@ -750,9 +712,10 @@ struct ListRecs {
   __device__ const char* operator()(int r) const { return l->rec[r]; }
 };
 
-template <class Src>
-__device__ void knn_merge_body(int32_t k, const Src& src, int32_t nrec, void* result) {
-  __shared__ SelFull L;
+// LDS: SelFull (merge kernels, any k) or SelLite (block 0 of the fused kernel, k <= 128 so the
+// running list plus one whole record fit its 256-key sort area).
+template <class LDS, class Src>
+__device__ void knn_merge_body(int32_t k, const Src& src, int32_t nrec, void* result, LDS& L) {
   __shared__ int s_off[kMaxMergeRecs + 1], s_status;
   const int tid = threadIdx.x;
   if (tid == 0) {
@@ -771,7 +734,7 @@ __device__ void knn_merge_body(int32_t k, const Src& src, int32_t nrec, void* re
   while (r < nrec) {  // block-uniform
     for (int i = tid; i < nr; i += kSelT) { L.sd[i] = L.rd[i]; L.so[i] = L.ro[i]; L.si[i] = L.ri[i]; }
     int cnt = nr;
-    while (r < nrec && cnt + (s_off[r + 1] - s_off[r]) <= SelFull::kCap) {
+    while (r < nrec && cnt + (s_off[r + 1] - s_off[r]) <= LDS::kCap) {
       RecView in = rec_view((void*)src(r), k);
       const int n = s_off[r + 1] - s_off[r];
       for (int i = tid; i < n; i += kSelT) {
@@ -798,19 +761,70 @@ __device__ void knn_merge_body(int32_t k, const Src& src, int32_t nrec, void* re
   }
 }
 
+// Fused continuous-query kernel (pipeline depth 2): blocks 1.. scan window i with the
+// threshold taken from the lane's hint (set by window i-2's select) -- or, for a lane's first
+// window (use_state 2), from the sample kernel launched just before; block 0, dispatched
+// first, runs window i-1's select on the other lane while they stream.  One launch per window.
+// Sliding windows: with m.nrec > 0, block 0 then merges the window that closed with window i-1
+// (its pane records, the one just written included) into m.result -- no separate merge launch.
+template <int METRIC, int NT>
+__global__ __launch_bounds__(kBlock) void knn_fused_kernel(KnnScanArgs a, KnnSelectArgs prev, int has_prev,
+                                                           KnnMergeArgs m) {
+  __shared__ SelLite L;
+  if (blockIdx.x == 0) {
+    if (has_prev) knn_select_body<SelLite, false>(prev, L);
+    if (m.nrec > 0) {
+      __threadfence();  // the select's record stores, before the block reads them back
+      __syncthreads();
+      const ListRecs src{&m.list};
+      knn_merge_body(prev.k, src, m.nrec, m.result, L);
+    }
+    return;
+  }
+  double T, sp;
+  if (a.use_state == 2) {  // cold lane: the sample kernel just set T
+    T = a.st->T;
+    sp = a.st->s_pre;
+  } else {
+    const double h = a.st->hint_T;
+    T = (h > 0.0 && h < a.T) ? h : a.T;  // a.T = r
+    sp = s_prefilter(T, a.metric);
+    if (blockIdx.x == 1 && threadIdx.x == 0) { a.st->T = T; a.st->s_pre = sp; }
+  }
+  knn_scan_body<METRIC, 1, NT>(a, sp, T, blockIdx.x - 1, gridDim.x - 1);
+}
+
+hipError_t launch_knn_fused(gf_ctx* ctx, const KnnScanArgs& a, const KnnSelectArgs& prev, int has_prev,
+                            int scan_blocks, int nt, const KnnMergeArgs* merge) {
+  KTimer t(ctx, GF_K_KNN_SCAN);
+  const dim3 g(scan_blocks + 1), b(kBlock);
+  KnnMergeArgs m{};
+  if (merge && has_prev) m = *merge;
+  if (a.metric == 0) {
+    if (nt) hipLaunchKernelGGL((knn_fused_kernel<0, 1>), g, b, 0, ctx->stream, a, prev, has_prev, m);
+    else hipLaunchKernelGGL((knn_fused_kernel<0, 0>), g, b, 0, ctx->stream, a, prev, has_prev, m);
+  } else {
+    if (nt) hipLaunchKernelGGL((knn_fused_kernel<1, 1>), g, b, 0, ctx->stream, a, prev, has_prev, m);
+    else hipLaunchKernelGGL((knn_fused_kernel<1, 0>), g, b, 0, ctx->stream, a, prev, has_prev, m);
+  }
+  return hipGetLastError();
+}
+
 // Block w merges window w: its nrec records start at records + w*win_stride, rec_stride apart;
 // the merged record goes to result + w*res_stride.
 __global__ __launch_bounds__(kSelT) void knn_merge_kernel(int32_t k, const char* records, int32_t nrec,
                                                           size_t rec_stride, size_t win_stride, void* result_base,
                                                           size_t res_stride) {
+  __shared__ SelFull L;
   const StridedRecs src{records + (size_t)blockIdx.x * win_stride, rec_stride};
-  knn_merge_body(k, src, nrec, (char*)result_base + (size_t)blockIdx.x * res_stride);
+  knn_merge_body(k, src, nrec, (char*)result_base + (size_t)blockIdx.x * res_stride, L);
 }
 
 __global__ __launch_bounds__(kSelT) void knn_merge_list_kernel(int32_t k, KnnRecList list, int32_t nrec,
                                                                void* result) {
+  __shared__ SelFull L;
   const ListRecs src{&list};
-  knn_merge_body(k, src, nrec, result);
+  knn_merge_body(k, src, nrec, result, L);
 }
 
 hipError_t launch_knn_merge(gf_ctx* ctx, int32_t k, const void* records, int32_t nrec, size_t rec_stride,

@@ -66,15 +66,20 @@ bool window_has_points(gf_knn_sliding* s, int64_t p) {
   return false;
 }
 
-int merge_window(gf_knn_sliding* s, int64_t p, void* result) {
-  KnnRecList l{};
-  int n = 0;
+KnnMergeArgs window_merge(gf_knn_sliding* s, int64_t p, void* result) {
+  KnnMergeArgs m{};
+  m.result = result;
   for (int64_t q = p - s->W + 1; q <= p; ++q) {
     const gf_knn_sliding::Pane& pn = slot(s, q);
-    if (pn.index == q && pn.pts.n > 0) l.rec[n++] = rec_of(s, q);
+    if (pn.index == q && pn.pts.n > 0) m.list.rec[m.nrec++] = rec_of(s, q);
   }
+  return m;
+}
+
+int merge_window(gf_knn_sliding* s, int64_t p, void* result) {
+  const KnnMergeArgs m = window_merge(s, p, result);
   gf_ctx* ctx = s->plan->ctx;
-  GF_HIP_CHECK(ctx, launch_knn_merge_list(ctx, s->plan->k, l, n, result));
+  GF_HIP_CHECK(ctx, launch_knn_merge_list(ctx, s->plan->k, m.list, m.nrec, result));
   return GF_OK;
 }
 
@@ -143,10 +148,13 @@ extern "C" int gf_knn_sliding_push(gf_knn_sliding* s, int64_t pane_index, const 
   pn.index = pane_index;
   pn.pts = *pane;
   pn.base = s->pos;
+  int merged = 0;
   if (pane->n > 0) {
     P->idx_base = s->pos;
     // depth 2: the fused launch also selects the previous non-empty pane into its ring slot
-    if ((st = gf_knn_enqueue(P, pane, rec_of(s, pane_index)))) return st;
+    // and, k <= 128, merges the window pending on that pane in the same block
+    const KnnMergeArgs m = s->pend ? window_merge(s, s->pend_last, s->pend_result) : KnnMergeArgs{};
+    if ((st = knn_enqueue_merge(P, pane, rec_of(s, pane_index), s->pend ? &m : nullptr, &merged))) return st;
   } else if ((st = gf_knn_plan_flush(P))) {
     return st;
   }
@@ -158,7 +166,7 @@ extern "C" int gf_knn_sliding_push(gf_knn_sliding* s, int64_t pane_index, const 
   // its select is still pending (depth 2)
   if (s->pend) {
     s->pend = false;
-    if ((st = merge_window(s, s->pend_last, s->pend_result))) return st;
+    if (!merged && (st = merge_window(s, s->pend_last, s->pend_result))) return st;
   }
   if (closes_window(s, pane_index) && window_has_points(s, pane_index)) {
     if (!window_result) return set_err(ctx, GF_ERR_ARG, "gf_knn_sliding_push: a window closes, result is null");
