@@ -324,7 +324,7 @@ def bench_sliding(args):
     # panes concatenated (the reference's from-scratch evaluation; gf_knn_run is oracle-checked in
     # tests/), and the first window == the oracle; plus the from-scratch time for comparison
     verified, scratch_us = None, None
-    if world == 1:
+    if world == 1 and not args.no_verify:
         op2 = sf.PointPointKNNQuery(conf, grid)
         ctx2, plan2 = op2.plan(dev, q, args.radius, k)
         verified = True
@@ -385,6 +385,17 @@ def bench_sliding(args):
                "sample": (f"first {S} points of a window x {reps} reps ({ct:.1f}s): oracle's reference-shaped "
                           "evaluator (string cell IDs, HashSet C/G filter, per-cell PriorityQueue, windowAll merge), "
                           "1 thread; the reference evaluates every window from scratch")}
+    traffic, traffic_src = None, None
+    if rank == 0:  # HBM bytes per pane launch from the committed rocprofv3 PMC passes
+        import glob
+
+        for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_sliding_knn_fused_pmc.json")), reverse=True):
+            with open(f) as fh:
+                pm = json.load(fh)
+            if pm.get("points_per_launch") == pane_pts:
+                traffic = pm["traffic_bytes_per_launch"]
+                traffic_src = os.path.relpath(f, ROOT) + ": rocprofv3 FETCH_SIZE (x2, gfx950) + WRITE_SIZE, median per launch"
+                break
     if rank == 0:
         avg = scan_ms / 1000.0 / max(scan_n, 1)
         steps = args.steps
@@ -401,7 +412,8 @@ def bench_sliding(args):
                         "exchange_batch": B if world > 1 else None},
              "roofline": {"bound": "hbm", "kernel": "knn_fused (scan of pane i + select of pane i-1)",
                           "achieved": round(16.0 * pane_pts / avg / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                          "frac": round(16.0 * pane_pts / avg / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
+                          "frac": round(16.0 * pane_pts / avg / 1e9 / HBM_PEAK_GBS, 4), "traffic": traffic,
+                          "traffic_source": traffic_src,
                           "bytes_per_launch": 16.0 * pane_pts, "avg_launch_us": round(avg * 1e6, 2),
                           "launches_timed": scan_n},
              "scanned_points_per_s": round(pane_pts * world * steps / elapsed, 1),
