@@ -56,7 +56,8 @@ extern "C" {
 #define GF_K_RANGE_TEST  6  /* deferred candidate tests of the many-object range plans */
 #define GF_K_JOIN_BUCKET 7  /* ordinary-side bucketing of the join */
 #define GF_K_KNN_MERGE   8  /* top-k record merges (shards, sliding-window panes) */
-#define GF_K_COUNT       9
+#define GF_K_CSV_PARSE   9  /* CSV ingest: the per-line parse kernel */
+#define GF_K_COUNT       10
 
 typedef struct gf_ctx gf_ctx;
 
@@ -261,6 +262,35 @@ int  gf_knn_sliding_decode(gf_knn_sliding* s, int64_t window_end, const void* re
  * pane first_pane + j is the slice [bounds[j], bounds[j+1]).  ts must be non-decreasing. */
 int  gf_pane_bounds(gf_ctx* ctx, const int64_t* ts, int64_t n, int64_t pane_ms, int64_t first_pane, int32_t npanes,
                     int64_t* bounds);
+
+/* ---- CSV / TSV ingest ----------------------------------------------------------------
+ * Deserialization.CSVTSVToTSpatial(uGrid, dateFormat, delimiter, csvTsvSchemaAttr).map
+ * (Deserialization.java:291-325) over a chunk of text lines, on the device.  Per line: '"'
+ * removed, fields split on `delimiter` with the surrounding whitespace (split("\\s*" + delimiter
+ * + "\\s*")), objID = Long.valueOf(field[objid_field]) (decimal objIDs only: the SoA carries
+ * them as int64), ts = Long.valueOf(field[time_field]), x / y = Double.valueOf(...) correctly
+ * rounded; with `grid`, the cell of Point(objID, x, y, ts, uGrid) (Point.java:98) as well. */
+typedef struct {
+  char delimiter;          /* ',' ';' '\t' ... (one character) */
+  char reserved[3];
+  int32_t objid_field;     /* csvTsvSchemaAttr.get(0) */
+  int32_t time_field;      /* csvTsvSchemaAttr.get(1) */
+  int32_t x_field;         /* csvTsvSchemaAttr.get(2) */
+  int32_t y_field;         /* csvTsvSchemaAttr.get(3) */
+} gf_csv_schema;
+#define GF_CSV_OK              0
+#define GF_CSV_NUMBER_FORMAT   1  /* Long.valueOf / Double.valueOf throw NumberFormatException */
+#define GF_CSV_UNSUPPORTED     2  /* valid Java literal the device path does not take: hexadecimal, or
+                                     > 19 significant digits within 1e-19 of a rounding boundary */
+#define GF_CSV_MISSING_FIELD   3  /* the reference's List.get throws IndexOutOfBoundsException */
+#define GF_CSV_EMPTY_LINE      4  /* an empty line (a trailing newline at the end is fine) */
+/* Sync.  text: device bytes [len], 16-byte aligned, complete lines separated by '\n' ("\r\n"
+ * accepted; the last line may lack its '\n').  Outputs: device arrays of capacity cap (cx, cy
+ * nullable, need grid).  *n_out = lines.  GF_ERR_CAPACITY if lines > cap (*n_out = lines);
+ * GF_ERR_ARG on a bad line: *bad_line = its 0-based index, *bad_kind = GF_CSV_*. */
+int gf_csv_parse(gf_ctx* ctx, const char* text, int64_t len, const gf_csv_schema* schema, const gf_grid* grid,
+                 double* x, double* y, int64_t* objID, int64_t* ts, int32_t* cx, int32_t* cy, int64_t cap,
+                 int64_t* n_out, int64_t* bad_line, int32_t* bad_kind);
 
 /* ---- join (sync) --------------------------------------------------------------------
  * JoinQuery.getReplicatedPointQueryStream + PointPointJoinQuery.windowBased

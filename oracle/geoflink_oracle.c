@@ -938,3 +938,156 @@ void orc_java_random_points(int64_t seed, int64_t n, double minX, double maxX,
     y[i] = minY + jr_next_double(&r) * (maxY - minY);
   }
 }
+
+/* ------------------------------------------------------------------------------------
+ * CSV / TSV ingest -- Deserialization.CSVTSVToTSpatial.map (Deserialization.java:314-322):
+ *   strArrayList = Arrays.asList(str.replace("\"", "").split("\\s*" + delimiter + "\\s*"));
+ *   objID = Long.valueOf-able decimal (kept as int64 here), time = Long.valueOf,
+ *   x, y = Double.valueOf (JDK FloatingDecimal: trim, Java literal grammar, correctly rounded;
+ *   glibc strtod is correctly rounded too).  Lines come from Flink's TextInputFormat: split
+ *   on '\n', a trailing '\r' dropped.
+ * ------------------------------------------------------------------------------------ */
+static int orc_java_s(char c) { return c == ' ' || c == '\t' || c == '\n' || c == '\x0B' || c == '\f' || c == '\r'; }
+
+/* String.split(regex "\s*D\s*") with limit 0: returns field count, fields as [fb, fe) */
+static int orc_java_split(const char* s, int n, char D, int* fb, int* fe, int maxf) {
+  int nf = 0, start = 0, pos = 0;
+  while (pos < n) {
+    int p, mb = -1, me = -1;
+    for (p = pos; p < n; ++p) {  /* leftmost match */
+      int q = p;
+      while (q < n && orc_java_s(s[q])) ++q;
+      if (orc_java_s(D)) {
+        int r, has = 0;
+        for (r = p; r < q; ++r) has |= s[r] == D;
+        if (q > p && has) { mb = p; me = q; break; }
+      } else if (q < n && s[q] == D) {
+        int r = q + 1;
+        while (r < n && orc_java_s(s[r])) ++r;
+        mb = p; me = r;
+        break;
+      }
+    }
+    if (mb < 0) break;
+    if (nf < maxf) { fb[nf] = start; fe[nf] = mb; }
+    ++nf;
+    start = me;
+    pos = me;
+  }
+  if (nf < maxf) { fb[nf] = start; fe[nf] = n; }
+  ++nf;
+  while (nf > 0 && nf <= maxf && fe[nf - 1] == fb[nf - 1]) --nf;  /* trailing empty strings removed */
+  return nf;
+}
+
+/* Long.valueOf: [+-]digits, no whitespace, overflow -> NumberFormatException */
+static int orc_java_long(const char* s, int n, int64_t* out) {
+  int i = 0, neg = 0;
+  uint64_t v = 0, lim;
+  if (n == 0) return 1;
+  if (s[0] == '-' || s[0] == '+') { neg = s[0] == '-'; i = 1; }
+  if (i == n) return 1;
+  lim = neg ? 9223372036854775808ull : 9223372036854775807ull;
+  for (; i < n; ++i) {
+    uint64_t d;
+    if (s[i] < '0' || s[i] > '9') return 1;
+    d = (uint64_t)(s[i] - '0');
+    if (v > (lim - d) / 10) return 1;
+    v = v * 10 + d;
+  }
+  *out = neg ? (int64_t)(0ull - v) : (int64_t)v;
+  return 0;
+}
+
+static int orc_isdig(char c) { return c >= '0' && c <= '9'; }
+static int orc_ishex(char c) { return orc_isdig(c) || (c >= 'a' && c <= 'f') || (c >= 'A' && c <= 'F'); }
+
+/* Double.valueOf: 0 ok, 1 NumberFormatException; *hex = 1 for a hexadecimal literal */
+static int orc_java_double(const char* s0, int n, double* out, int* hex) {
+  char buf[512];
+  int b = 0, e = n, i, neg = 0, nd = 0;
+  *hex = 0;
+  while (b < e && (unsigned char)s0[b] <= ' ') ++b;  /* String.trim() */
+  while (e > b && (unsigned char)s0[e - 1] <= ' ') --e;
+  if (e - b <= 0 || e - b >= (int)sizeof(buf)) return 1;
+  memcpy(buf, s0 + b, (size_t)(e - b));
+  n = e - b;
+  buf[n] = 0;
+  i = 0;
+  if (buf[0] == '+' || buf[0] == '-') { neg = buf[0] == '-'; i = 1; }
+  if (!strcmp(buf + i, "NaN")) { *out = NAN; return 0; }
+  if (!strcmp(buf + i, "Infinity")) { *out = neg ? -INFINITY : INFINITY; return 0; }
+  if (n > 0 && (buf[n - 1] == 'f' || buf[n - 1] == 'F' || buf[n - 1] == 'd' || buf[n - 1] == 'D')) buf[--n] = 0;
+  if (buf[i] == '0' && (buf[i + 1] == 'x' || buf[i + 1] == 'X')) {  /* 0x h* [. h*] p [+-] d+ */
+    int j = i + 2, nh = 0;
+    while (orc_ishex(buf[j])) { ++j; ++nh; }
+    if (buf[j] == '.') { ++j; while (orc_ishex(buf[j])) { ++j; ++nh; } }
+    if (!nh || (buf[j] != 'p' && buf[j] != 'P')) return 1;
+    ++j;
+    if (buf[j] == '+' || buf[j] == '-') ++j;
+    if (!orc_isdig(buf[j])) return 1;
+    while (orc_isdig(buf[j])) ++j;
+    if (j != n) return 1;
+    *hex = 1;
+    *out = strtod(buf, NULL);
+    return 0;
+  }
+  {
+    int j = i;
+    while (orc_isdig(buf[j])) { ++j; ++nd; }
+    if (buf[j] == '.') { ++j; while (orc_isdig(buf[j])) { ++j; ++nd; } }
+    if (!nd) return 1;
+    if (buf[j] == 'e' || buf[j] == 'E') {
+      ++j;
+      if (buf[j] == '+' || buf[j] == '-') ++j;
+      if (!orc_isdig(buf[j])) return 1;
+      while (orc_isdig(buf[j])) ++j;
+    }
+    if (j != n) return 1;
+  }
+  *out = strtod(buf, NULL);
+  return 0;
+}
+
+int64_t orc_csv_parse(const char* text, int64_t len, char delim, const int32_t* want, double* x, double* y,
+                      int64_t* objID, int64_t* ts, int64_t cap, int64_t* bad_line, int32_t* bad_kind) {
+  int64_t pos = 0, line = 0;
+  char* buf = NULL;
+  int bufcap = 0;
+  *bad_line = -1;
+  *bad_kind = 0;
+  while (pos < len) {
+    int64_t e = pos, le;
+    int n = 0, nf, k, kind = 0, fb[64], fe[64], hex = 0;
+    while (e < len && text[e] != '\n') ++e;
+    le = e;
+    if (le > pos && text[le - 1] == '\r') --le;
+    if (le - pos + 1 > bufcap) { bufcap = (int)(le - pos + 1) * 2; buf = (char*)realloc(buf, (size_t)bufcap); }
+    for (int64_t i = pos; i < le; ++i)
+      if (text[i] != '"') buf[n++] = text[i];  /* str.replace("\"", "") */
+    if (le == pos) kind = 4;
+    else {
+      nf = orc_java_split(buf, n, delim, fb, fe, 64);
+      for (k = 0; k < 4 && !kind; ++k)
+        if (want[k] >= nf || want[k] >= 64) kind = 3;
+      if (!kind) {
+        int64_t o = 0, t = 0;
+        double vx = 0, vy = 0;
+        int hx = 0, hy = 0;
+        if (orc_java_long(buf + fb[want[0]], fe[want[0]] - fb[want[0]], &o) ||
+            orc_java_long(buf + fb[want[1]], fe[want[1]] - fb[want[1]], &t) ||
+            orc_java_double(buf + fb[want[2]], fe[want[2]] - fb[want[2]], &vx, &hx) ||
+            orc_java_double(buf + fb[want[3]], fe[want[3]] - fb[want[3]], &vy, &hy))
+          kind = 1;
+        hex = hx || hy;
+        if (!kind && line < cap) { x[line] = vx; y[line] = vy; objID[line] = o; ts[line] = t; }
+        if (!kind && hex) kind = 2;  /* valid Java; reported so tests can pin the device's answer */
+      }
+    }
+    if (kind && *bad_line < 0) { *bad_line = line; *bad_kind = kind; }
+    ++line;
+    pos = e + 1;
+  }
+  free(buf);
+  return line;
+}

@@ -140,6 +140,13 @@ int32_t orc_generate_query_polygons(int32_t numQueryPolygons, double minX, doubl
 void orc_java_random_points(int64_t seed, int64_t n, double minX, double maxX,
                             double minY, double maxY, double* x, double* y);
 
+/* Deserialization.CSVTSVToTSpatial.map over the lines of text (Deserialization.java:314-322):
+ * want = csvTsvSchemaAttr (objID, time, x, y field indices).  Returns the line count (rows past
+ * cap are not written); the first bad line and its kind (1 NumberFormatException, 2 hexadecimal
+ * literal -- valid Java, value still written --, 3 missing field, 4 empty line) or -1. */
+int64_t orc_csv_parse(const char* text, int64_t len, char delim, const int32_t* want, double* x, double* y,
+                      int64_t* objID, int64_t* ts, int64_t cap, int64_t* bad_line, int32_t* bad_kind);
+
 #ifdef __cplusplus
 }
 #endif

@@ -72,6 +72,8 @@ def lib():
         L.orc_generate_query_polygons.argtypes = [i32, d, d, d, d, P, P, i32]
         L.orc_generate_query_polygons.restype = i32
         L.orc_java_random_points.argtypes = [i64, i64, d, d, d, d, P, P]
+        L.orc_csv_parse.argtypes = [C.c_char_p, i64, C.c_char, P, P, P, P, P, i64, C.POINTER(i64), C.POINTER(i32)]
+        L.orc_csv_parse.restype = i64
         _lib = L
     return _lib
 
@@ -232,3 +234,13 @@ def java_random_points(seed, n, minX, maxX, minY, maxY):
     x = np.empty(n); y = np.empty(n)
     lib().orc_java_random_points(int(seed), int(n), float(minX), float(maxX), float(minY), float(maxY), _p(x), _p(y))
     return x, y
+
+
+def csv_parse(text: bytes, delim: str, want):
+    """Deserialization.CSVTSVToTSpatial.map per line -> (x, y, objID, ts, bad_line, bad_kind)."""
+    w = np.asarray(want, np.int32)
+    bl, bk = C.c_int64(), C.c_int32()
+    n = lib().orc_csv_parse(text, len(text), delim.encode(), _p(w), None, None, None, None, 0, C.byref(bl), C.byref(bk))
+    x = np.zeros(n); y = np.zeros(n); o = np.zeros(n, np.int64); t = np.zeros(n, np.int64)
+    lib().orc_csv_parse(text, len(text), delim.encode(), _p(w), _p(x), _p(y), _p(o), _p(t), n, C.byref(bl), C.byref(bk))
+    return x, y, o, t, bl.value, bk.value

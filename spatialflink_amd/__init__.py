@@ -11,10 +11,11 @@ from .spatialObjects import Point, PointWindow, Polygon, PolygonSet
 from .spatialOperators import (KNNResult, PinnedRecords, PointPointJoinQuery, PointPointKNNQuery, PointPointRangeQuery,
                                PointPolygonRangeQuery, QueryConfiguration, QueryType, RangeResult, assign_cells,
                                bucket_by_cell, knn_merge_host, synthetic_uniform)
+from .spatialStreams import Deserialization
 from .windows import SlidingKNNQuery, SlidingRangeQuery, SlidingWindows
 
 __all__ = [
-    "SlidingWindows", "SlidingKNNQuery", "SlidingRangeQuery",
+    "SlidingWindows", "SlidingKNNQuery", "SlidingRangeQuery", "Deserialization",
     "UniformGrid", "Point", "Polygon", "PolygonSet", "PointWindow", "QueryType", "QueryConfiguration",
     "PointPointRangeQuery", "PointPolygonRangeQuery", "PointPointKNNQuery", "PointPointJoinQuery", "RangeResult",
     "KNNResult", "PinnedRecords", "knn_merge_host", "assign_cells", "bucket_by_cell", "synthetic_uniform", "generateCellIDStr",

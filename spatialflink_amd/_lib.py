@@ -27,7 +27,7 @@ METRIC_HYPOT = 1
 
 FLAG_JOIN_LEGACY = 1
 (K_KNN_SCAN, K_KNN_SAMPLE, K_KNN_SELECT, K_RANGE_SCAN, K_ASSIGN, K_JOIN_PROBE, K_RANGE_TEST, K_JOIN_BUCKET,
- K_KNN_MERGE) = range(9)
+ K_KNN_MERGE, K_CSV_PARSE) = range(10)
 
 # Every symbol include/geoflink_hip.h declares (checked by tests/test_abi.py).
 EXPORTS = [
@@ -40,7 +40,8 @@ EXPORTS = [
     "gf_knn_result_bytes", "gf_knn_enqueue",
     "gf_knn_decode", "gf_knn_run", "gf_knn_merge_dev", "gf_knn_merge_dev_batch", "gf_knn_merge_host",
     "gf_knn_sliding_create", "gf_knn_sliding_destroy", "gf_knn_sliding_geometry", "gf_knn_sliding_push",
-    "gf_knn_sliding_flush", "gf_knn_sliding_decode", "gf_pane_bounds", "gf_join_pp", "gf_window_create",
+    "gf_knn_sliding_flush", "gf_knn_sliding_decode", "gf_pane_bounds", "gf_csv_parse", "gf_join_pp",
+    "gf_window_create",
     "gf_window_destroy", "gf_window_upload", "gf_window_points", "gf_synth_uniform", "gf_pinned_alloc",
     "gf_pinned_free",
 ]
@@ -151,6 +152,7 @@ def lib():
             "gf_knn_sliding_flush": ([P], C.c_int),
             "gf_knn_sliding_decode": ([P, i64, P, P, P, P, pi32], C.c_int),
             "gf_pane_bounds": ([P, P, i64, i64, i64, i32, P], C.c_int),
+            "gf_csv_parse": ([P, P, i64, P, C.POINTER(GfGrid), P, P, P, P, P, P, i64, pi64, pi64, pi32], C.c_int),
             "gf_join_pp": ([P, C.POINTER(GfGrid), C.POINTER(GfGrid), C.POINTER(GfPoints), C.POINTER(GfPoints), d,
                             C.c_int, C.c_int, P, i64, pi64], C.c_int),
             "gf_window_create": ([P, i64, C.POINTER(P)], C.c_int),

@@ -1,0 +1,89 @@
+// csv.cpp -- host side of the GPU CSV/TSV ingest (k_csv.hip): Deserialization.CSVTSVToTSpatial
+// (Deserialization.java:291-325) over a chunk of HBM-resident text.
+//
+//   count newlines per 64 KB segment -> exclusive scan -> (sync: line count, capacity check)
+//   -> newline positions -> one lane per line parse + cell -> (sync: first bad line, if any)
+#include <cstring>
+#include <string>
+
+#include "gf_internal.hpp"
+
+using namespace gf;
+
+extern "C" int gf_csv_parse(gf_ctx* ctx, const char* text, int64_t len, const gf_csv_schema* sc, const gf_grid* g,
+                            double* x, double* y, int64_t* objID, int64_t* ts, int32_t* cx, int32_t* cy, int64_t cap,
+                            int64_t* n_out, int64_t* bad_line, int32_t* bad_kind) {
+  if (!ctx || !sc || !n_out || len < 0 || (len > 0 && !text) || !x || !y || !objID || !ts || (!cx) != (!cy) ||
+      (cx && !g) || sc->objid_field < 0 || sc->time_field < 0 || sc->x_field < 0 || sc->y_field < 0)
+    return set_err(ctx, GF_ERR_ARG, "gf_csv_parse: bad argument");
+  if (g && !(g->n > 0 && g->cellLength > 0)) return set_err(ctx, GF_ERR_ARG, "gf_csv_parse: bad grid");
+  if ((uintptr_t)text & 15) return set_err(ctx, GF_ERR_ALIGN, "gf_csv_parse: text must be 16-byte aligned");
+  int st = bind(ctx);
+  if (st) return st;
+  *n_out = 0;
+  if (bad_line) *bad_line = -1;
+  if (bad_kind) *bad_kind = GF_CSV_OK;
+  if (len == 0) return GF_OK;
+  const int64_t nseg = (len + kCsvSeg - 1) / kCsvSeg;
+  if (nseg >= (int64_t)INT32_MAX) return set_err(ctx, GF_ERR_ARG, "gf_csv_parse: text too large");
+  // scratch: counts | offsets | scan tmp | error | tail bytes
+  size_t o_cnt = 0, o_off = o_cnt + sizeof(uint32_t) * (size_t)(nseg + 1);
+  size_t o_tmp = o_off + sizeof(uint32_t) * (size_t)(nseg + 1);
+  size_t o_err = (o_tmp + sizeof(uint32_t) * scan_tmp_elems(nseg) + 15) & ~(size_t)15;
+  size_t o_nl = o_err + 64;
+  // the newline array is sized after the count; reserve a first guess (one line per 32 B)
+  char* base = (char*)ctx_scratch(ctx, o_nl + sizeof(int64_t) * (size_t)(len / 32 + 2), &st);
+  if (st) return st;
+  uint32_t* pinned = (uint32_t*)ctx_pinned(ctx, 16, &st);
+  if (st) return st;
+  auto count = [&]() -> int {
+    GF_HIP_CHECK(ctx, launch_csv_count(ctx->stream, text, len, nseg, (uint32_t*)(base + o_cnt)));
+    GF_HIP_CHECK(ctx, launch_exclusive_scan(ctx->stream, (uint32_t*)(base + o_cnt), nseg, (uint32_t*)(base + o_off),
+                                            (uint32_t*)(base + o_tmp)));
+    return GF_OK;
+  };
+  if ((st = count())) return st;
+  GF_HIP_CHECK(ctx, hipMemcpyAsync(pinned, (uint32_t*)(base + o_off) + nseg, sizeof(uint32_t), hipMemcpyDeviceToHost,
+                                   ctx->stream));
+  GF_HIP_CHECK(ctx, hipMemcpyAsync((char*)pinned + 4, text + len - 1, 1, hipMemcpyDeviceToHost, ctx->stream));
+  GF_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+  const int64_t newlines = pinned[0];
+  const int64_t lines = newlines + (((char*)pinned)[4] != '\n' ? 1 : 0);
+  *n_out = lines;
+  if (lines > cap) return set_err(ctx, GF_ERR_CAPACITY, "gf_csv_parse: more lines than capacity");
+  if ((size_t)newlines > (size_t)(len / 32 + 2)) {  // short lines: a larger scratch (it may move: recount)
+    char* nb = (char*)ctx_scratch(ctx, o_nl + sizeof(int64_t) * (size_t)(newlines + 1), &st);
+    if (st) return st;
+    if (nb != base) {
+      base = nb;
+      if ((st = count())) return st;
+    }
+  }
+  const uint32_t* offs = (const uint32_t*)(base + o_off);
+  int64_t* nl = (int64_t*)(base + o_nl);
+  CsvErr* err = (CsvErr*)(base + o_err);
+  GF_HIP_CHECK(ctx, hipMemsetAsync(err, 0xFF, sizeof(CsvErr), ctx->stream));
+  GF_HIP_CHECK(ctx, launch_csv_index(ctx->stream, text, len, nseg, offs, nl));
+  CsvArgs a{};
+  a.text = text; a.len = len; a.nl = nl; a.newlines = newlines; a.lines = lines;
+  a.delim = sc->delimiter;
+  a.want[0] = sc->objid_field; a.want[1] = sc->time_field; a.want[2] = sc->x_field; a.want[3] = sc->y_field;
+  a.x = x; a.y = y; a.objID = objID; a.ts = ts; a.cx = cx; a.cy = cy;
+  if (g) { a.minX = g->minX; a.minY = g->minY; a.cl = g->cellLength; }
+  a.err = err;
+  GF_HIP_CHECK(ctx, launch_csv_parse(ctx, a));
+  CsvErr he{};
+  GF_HIP_CHECK(ctx, hipMemcpyAsync(pinned, err, sizeof(CsvErr), hipMemcpyDeviceToHost, ctx->stream));
+  GF_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+  std::memcpy(&he, pinned, sizeof(CsvErr));
+  if (he.line != ~0ull) {
+    if (bad_line) *bad_line = (int64_t)he.line;
+    if (bad_kind) *bad_kind = he.kind;
+    static const char* what[] = {"ok", "NumberFormatException", "unsupported numeric literal (hexadecimal, or > 19 "
+                                 "significant digits at a rounding boundary)", "missing field (IndexOutOfBounds)",
+                                 "empty line"};
+    const int k = he.kind >= 0 && he.kind <= 4 ? he.kind : 1;
+    return set_err(ctx, GF_ERR_ARG, "gf_csv_parse: line " + std::to_string(he.line) + ": " + what[k]);
+  }
+  return GF_OK;
+}

@@ -195,6 +195,36 @@ hipError_t launch_word_popcounts(hipStream_t s, const uint64_t* bitmap, int64_t 
 hipError_t launch_expand_bitmap(hipStream_t s, const uint64_t* bitmap, int64_t words, int64_t n,
                                 const uint32_t* off, uint32_t* idx, int64_t cap);
 
+// CSV ingest (k_csv.hip)
+constexpr int64_t kCsvSeg = 64 * 1024;  // text bytes per count / index block
+enum { kCsvOk = 0, kCsvNumberFormat = 1, kCsvUnsupported = 2, kCsvMissingField = 3, kCsvEmptyLine = 4 };
+struct CsvErr {
+  unsigned long long line;  // first bad line (~0 = none)
+  int kind;
+  int pad;
+};
+struct CsvArgs {
+  const char* text;
+  int64_t len;
+  const int64_t* nl;    // newline positions
+  int64_t newlines;
+  int64_t lines;        // newlines + (unterminated last line)
+  char delim;
+  int32_t want[4];      // field index of objID, time, x, y (csvTsvSchemaAttr)
+  double* x;
+  double* y;
+  int64_t* objID;
+  int64_t* ts;
+  int32_t* cx;          // nullable: fused cell assignment
+  int32_t* cy;
+  double minX, minY, cl;
+  CsvErr* err;
+};
+hipError_t launch_csv_count(hipStream_t st, const char* text, int64_t len, int64_t nseg, uint32_t* counts);
+hipError_t launch_csv_index(hipStream_t st, const char* text, int64_t len, int64_t nseg, const uint32_t* seg_off,
+                            int64_t* nl);
+hipError_t launch_csv_parse(gf_ctx* ctx, const CsvArgs& a);
+
 hipError_t launch_pane_bounds(hipStream_t s, const int64_t* ts, int64_t n, int64_t pane_ms, int64_t first_pane,
                               int32_t nb, int64_t* bounds);
 

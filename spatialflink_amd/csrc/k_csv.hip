@@ -1,0 +1,233 @@
+// k_csv.hip -- GPU CSV/TSV ingest: Deserialization.CSVTSVToTSpatial.map
+// (Deserialization.java:291-325) for a whole chunk of text lines at once, fused with
+// HelperClass.assignGridCellID (Point.java:98).  Three kernels over HBM-resident text:
+//
+//   csv_count   newline bytes per 64 KB segment (16-B loads, SWAR byte compare)
+//   csv_index   the newline positions, in order (block-wide prefix of per-thread counts)
+//   csv_parse   one lane per line: quotes dropped, fields split on the delimiter with the
+//               surrounding whitespace (the reference's split("\\s*" + delim + "\\s*")),
+//               Long.valueOf(objID, time), Double.valueOf(x, y) correctly rounded on the device
+//               (gf_decimal.hpp), cell (cx, cy), SoA stores.
+#include "gf_decimal.hpp"
+#include "gf_internal.hpp"
+
+namespace gf {
+
+__device__ const uint64_t kPow5Dev[] = {GF_POW5_TABLE};
+
+// bytes equal to '\n' in a 64-bit word: high bit of each matching byte (exact, no carries)
+__device__ __forceinline__ uint64_t nl_bytes(uint64_t x) {
+  const uint64_t y = x ^ 0x0A0A0A0A0A0A0A0Aull;
+  const uint64_t t = (y & 0x7F7F7F7F7F7F7F7Full) + 0x7F7F7F7F7F7F7F7Full;
+  return ~(t | y | 0x7F7F7F7F7F7F7F7Full);
+}
+// 16-bit mask of '\n' bytes in 16 bytes (bit b = byte b)
+__device__ __forceinline__ uint32_t nl_mask16(uint64_t lo, uint64_t hi) {
+  uint32_t m = 0;
+  const uint64_t a = nl_bytes(lo), b = nl_bytes(hi);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    m |= (uint32_t)((a >> (8 * k + 7)) & 1ull) << k;
+    m |= (uint32_t)((b >> (8 * k + 7)) & 1ull) << (k + 8);
+  }
+  return m;
+}
+
+// this thread's 16 bytes at [off, off + 16) of the segment (bytewise past len)
+__device__ __forceinline__ uint32_t chunk_mask(const char* text, int64_t len, int64_t off) {
+  if (off + 16 <= len) {
+    const uint4 v = *reinterpret_cast<const uint4*>(text + off);
+    return nl_mask16(((uint64_t)v.y << 32) | v.x, ((uint64_t)v.w << 32) | v.z);
+  }
+  uint32_t m = 0;
+  for (int k = 0; k < 16 && off + k < len; ++k) m |= (uint32_t)(text[off + k] == '\n') << k;
+  return m;
+}
+
+__global__ __launch_bounds__(kBlock) void csv_count_kernel(const char* __restrict__ text, int64_t len,
+                                                           uint32_t* __restrict__ counts) {
+  const int64_t s0 = (int64_t)blockIdx.x * kCsvSeg;
+  const int64_t s1 = s0 + kCsvSeg < len ? s0 + kCsvSeg : len;
+  uint32_t c = 0;
+  for (int64_t off = s0 + 16 * threadIdx.x; off < s1; off += 16 * kBlock) c += __popc(chunk_mask(text, len, off));
+  __shared__ uint32_t ws[kBlock / 64];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) counts[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
+}
+
+__global__ __launch_bounds__(kBlock) void csv_index_kernel(const char* __restrict__ text, int64_t len,
+                                                           const uint32_t* __restrict__ seg_off,
+                                                           int64_t* __restrict__ nl) {
+  const int64_t s0 = (int64_t)blockIdx.x * kCsvSeg;
+  const int64_t s1 = s0 + kCsvSeg < len ? s0 + kCsvSeg : len;
+  __shared__ uint32_t ws[kBlock / 64];
+  uint32_t base = seg_off[blockIdx.x];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int64_t it = s0; it < s1; it += 16 * kBlock) {  // block-uniform trip count
+    const int64_t off = it + 16 * threadIdx.x;
+    const uint32_t m = off < s1 ? chunk_mask(text, len, off) : 0u;
+    const uint32_t c = __popc(m);
+    uint32_t inc = c;  // inclusive wave prefix
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t t = __shfl_up(inc, o, 64);
+      if (lane >= o) inc += t;
+    }
+    if (lane == 63) ws[w] = inc;
+    __syncthreads();
+    uint32_t wbase = 0, tot = 0;
+#pragma unroll
+    for (int v = 0; v < kBlock / 64; ++v) {
+      wbase += v < w ? ws[v] : 0u;
+      tot += ws[v];
+    }
+    uint32_t pos = base + wbase + inc - c;
+    for (uint32_t mm = m; mm; mm &= mm - 1) nl[pos++] = off + __ffs(mm) - 1;
+    base += tot;
+    __syncthreads();
+  }
+}
+
+struct GBytes {
+  const char* p;
+  __device__ char operator()(int64_t i) const { return p[i]; }
+};
+
+__device__ __forceinline__ bool java_s(char c) {  // regex \s: [ \t\n\x0B\f\r]
+  return c == ' ' || c == '\t' || c == '\n' || c == '\x0B' || c == '\f' || c == '\r';
+}
+
+// Field ranges of the wanted columns of line [b, e).  Returns the number of fields.
+__device__ int split_line(const GBytes& s, int64_t b, int64_t e, char d, const int32_t* want, Field* got) {
+  const bool wsd = java_s(d);
+  int field = 0;
+  int64_t fs = b;
+  auto close = [&](int64_t fe, bool last) {
+    int64_t x0 = fs, x1 = fe;
+    if (!wsd) {  // whitespace next to a delimiter belongs to the delimiter
+      if (field > 0)
+        while (x0 < x1 && (java_s(s(x0)) || s(x0) == '"')) ++x0;
+      if (!last)
+        while (x1 > x0 && (java_s(s(x1 - 1)) || s(x1 - 1) == '"')) --x1;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (want[k] == field) got[k] = Field{x0, x1};
+    ++field;
+  };
+  if (!wsd) {
+    for (int64_t i = b; i < e; ++i)
+      if (s(i) == d) {
+        close(i, false);
+        fs = i + 1;
+      }
+  } else {  // a run of whitespace (quotes are transparent) holding a delimiter is one separator
+    int64_t i = b;
+    while (i < e) {
+      const char c = s(i);
+      if (java_s(c) || c == '"') {
+        int64_t j = i;
+        bool hd = false;
+        while (j < e && (java_s(s(j)) || s(j) == '"')) {
+          hd |= s(j) == d;
+          ++j;
+        }
+        if (hd) {
+          close(i, false);
+          fs = j;
+        }
+        i = j;
+      } else {
+        ++i;
+      }
+    }
+  }
+  close(e, true);
+  return field;
+}
+
+__global__ __launch_bounds__(kBlock) void csv_parse_kernel(CsvArgs a) {
+  const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (j >= a.lines) return;
+  const GBytes s{a.text};
+  const int64_t b = j == 0 ? 0 : a.nl[j - 1] + 1;
+  int64_t e = j < a.newlines ? a.nl[j] : a.len;
+  if (e > b && s(e - 1) == '\r') --e;  // TextInputFormat drops the '\r' of "\r\n"
+  int err = kCsvOk;
+  Field f[4] = {{0, 0}, {0, 0}, {0, 0}, {0, 0}};
+  int64_t obj = 0, ts = 0;
+  double x = 0.0, y = 0.0;
+  if (e <= b) {
+    err = kCsvEmptyLine;
+  } else {
+    const int nf = split_line(s, b, e, a.delim, a.want, f);
+    int st = kNumOk;
+    if (a.want[0] >= nf || a.want[1] >= nf || a.want[2] >= nf || a.want[3] >= nf) err = kCsvMissingField;
+    else if ((st = parse_java_long(s, f[0], &obj)) || (st = parse_java_long(s, f[1], &ts)) ||
+             (st = parse_java_double(s, f[2], kPow5Dev, &x)) || (st = parse_java_double(s, f[3], kPow5Dev, &y)))
+      err = st == kNumUnsupported ? kCsvUnsupported : kCsvNumberFormat;
+  }
+  if (err != kCsvOk) {
+    atomicMin(&a.err->line, (unsigned long long)j);
+    return;
+  }
+  a.x[j] = x;
+  a.y[j] = y;
+  a.objID[j] = obj;
+  a.ts[j] = ts;
+  if (a.cx) {
+    a.cx[j] = cell_index(x, a.minX, a.cl);
+    a.cy[j] = cell_index(y, a.minY, a.cl);
+  }
+}
+
+// error kind of the first bad line (re-derived by a one-lane pass over that line)
+__global__ void csv_error_kernel(CsvArgs a) {
+  const unsigned long long j = a.err->line;
+  if (j == ~0ull || threadIdx.x != 0) return;
+  const GBytes s{a.text};
+  const int64_t b = j == 0 ? 0 : a.nl[j - 1] + 1;
+  int64_t e = (int64_t)j < a.newlines ? a.nl[j] : a.len;
+  if (e > b && s(e - 1) == '\r') --e;
+  int kind = kCsvEmptyLine;
+  if (e > b) {
+    Field f[4] = {{0, 0}, {0, 0}, {0, 0}, {0, 0}};
+    const int nf = split_line(s, b, e, a.delim, a.want, f);
+    int64_t v;
+    double d;
+    int st = kNumOk;
+    if (a.want[0] >= nf || a.want[1] >= nf || a.want[2] >= nf || a.want[3] >= nf) kind = kCsvMissingField;
+    else if ((st = parse_java_long(s, f[0], &v)) || (st = parse_java_long(s, f[1], &v)) ||
+             (st = parse_java_double(s, f[2], kPow5Dev, &d)) || (st = parse_java_double(s, f[3], kPow5Dev, &d)))
+      kind = st == kNumUnsupported ? kCsvUnsupported : kCsvNumberFormat;
+    else
+      kind = kCsvOk;
+  }
+  a.err->kind = kind;
+}
+
+hipError_t launch_csv_count(hipStream_t st, const char* text, int64_t len, int64_t nseg, uint32_t* counts) {
+  hipLaunchKernelGGL(csv_count_kernel, dim3((unsigned)nseg), dim3(kBlock), 0, st, text, len, counts);
+  return hipGetLastError();
+}
+
+hipError_t launch_csv_index(hipStream_t st, const char* text, int64_t len, int64_t nseg, const uint32_t* seg_off,
+                            int64_t* nl) {
+  hipLaunchKernelGGL(csv_index_kernel, dim3((unsigned)nseg), dim3(kBlock), 0, st, text, len, seg_off, nl);
+  return hipGetLastError();
+}
+
+hipError_t launch_csv_parse(gf_ctx* ctx, const CsvArgs& a) {
+  KTimer t(ctx, GF_K_CSV_PARSE);
+  if (a.lines > 0) {
+    const unsigned blocks = (unsigned)((a.lines + kBlock - 1) / kBlock);
+    hipLaunchKernelGGL(csv_parse_kernel, dim3(blocks), dim3(kBlock), 0, ctx->stream, a);
+  }
+  hipLaunchKernelGGL(csv_error_kernel, dim3(1), dim3(64), 0, ctx->stream, a);
+  return hipGetLastError();
+}
+
+}  // namespace gf

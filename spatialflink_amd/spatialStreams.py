@@ -1,0 +1,92 @@
+"""Ingest -- mirror of GeoFlink.spatialStreams.Deserialization for the CSV/TSV point stream
+(Deserialization.CSVTSVToTSpatial, Deserialization.java:291-325), run on the GPU.
+
+The reference maps each text line to a Point with String.split + Long.valueOf +
+Double.valueOf and assigns its grid cell in the Point constructor (Point.java:98).  Here a whole
+chunk of lines (device bytes, or host bytes uploaded once) becomes the window's SoA in one call:
+gf_csv_parse (k_csv.hip) finds the lines, splits the fields with the reference's
+"\\s*delim\\s*" rule, parses the numbers correctly rounded on the device and writes x, y,
+objID, ts and the cells (cx, cy) -- no per-point host work.  A bad line raises ValueError naming
+it (the reference's map throws NumberFormatException / IndexOutOfBoundsException).
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib
+from .spatialObjects import PointWindow
+
+
+class GfCsvSchema(C.Structure):
+    _fields_ = [("delimiter", C.c_char), ("reserved", C.c_char * 3), ("objid_field", C.c_int32),
+                ("time_field", C.c_int32), ("x_field", C.c_int32), ("y_field", C.c_int32)]
+
+
+CSV_KINDS = {0: "ok", 1: "NumberFormatException", 2: "unsupported numeric literal", 3: "missing field",
+             4: "empty line"}
+
+
+def device_text(text, device=None):
+    """bytes / bytearray / numpy uint8 -> a 16-byte-aligned device uint8 tensor (torch allocations
+    are 256-B aligned); a device uint8 tensor is returned as is."""
+    import torch
+
+    if isinstance(text, torch.Tensor):
+        return text
+    arr = np.frombuffer(bytes(text), np.uint8) if not isinstance(text, np.ndarray) else text
+    dev = torch.device("cuda", torch.cuda.current_device() if device is None else device)
+    return torch.from_numpy(np.ascontiguousarray(arr)).to(dev)
+
+
+class Deserialization:
+    class CSVTSVToTSpatial:
+        """CSVTSVToTSpatial(uGrid, dateFormat, delimiter, csvTsvSchemaAttr) -- csvTsvSchemaAttr
+        lists the field indices of objID, timestamp, x, y (Deserialization.java:314-322).
+        dateFormat is unused by the reference's map (the time field is Long.valueOf)."""
+
+        def __init__(self, uGrid=None, dateFormat=None, delimiter=",", csvTsvSchemaAttr=(0, 1, 2, 3)):
+            if len(delimiter) != 1:
+                raise ValueError("single-character delimiters only")
+            self.uGrid = uGrid
+            self.delimiter = delimiter
+            a = list(csvTsvSchemaAttr)
+            self.schema = GfCsvSchema(delimiter.encode(), b"\0\0\0", a[0], a[1], a[2], a[3])
+
+        def parse(self, text, device=None, capacity=None) -> PointWindow:
+            """All lines of `text` -> one PointWindow (extra: cx, cy when a grid is set)."""
+            import torch
+
+            t = device_text(text, device)
+            dev = t.device
+            ctx = _lib.context(dev.index)
+            n = int(t.numel())
+            cap = capacity if capacity is not None else max(1, n // 8 + 1)
+            L = _lib.lib()
+            nout, bl, bk = C.c_int64(), C.c_int64(), C.c_int32()
+            while True:
+                x = torch.empty(cap, dtype=torch.float64, device=dev)
+                y = torch.empty(cap, dtype=torch.float64, device=dev)
+                o = torch.empty(cap, dtype=torch.int64, device=dev)
+                ts = torch.empty(cap, dtype=torch.int64, device=dev)
+                cx = torch.empty(cap, dtype=torch.int32, device=dev) if self.uGrid is not None else None
+                cy = torch.empty(cap, dtype=torch.int32, device=dev) if self.uGrid is not None else None
+                st = L.gf_csv_parse(ctx.handle, C.c_void_p(t.data_ptr()), n, C.byref(self.schema),
+                                    C.byref(self.uGrid.c_grid) if self.uGrid is not None else None,
+                                    x.data_ptr(), y.data_ptr(), o.data_ptr(), ts.data_ptr(),
+                                    cx.data_ptr() if cx is not None else None,
+                                    cy.data_ptr() if cy is not None else None, cap, C.byref(nout), C.byref(bl),
+                                    C.byref(bk))
+                if st == _lib.GF_ERR_CAPACITY:
+                    cap = nout.value
+                    continue
+                if st == _lib.GF_ERR_ARG and bl.value >= 0:
+                    raise ValueError(f"line {bl.value}: {CSV_KINDS.get(bk.value, bk.value)}")
+                _lib.check(st, ctx.handle, "gf_csv_parse")
+                break
+            m = nout.value
+            w = PointWindow(x[:m], y[:m], o[:m], ts[:m])
+            if cx is not None:
+                w.extra["cx"], w.extra["cy"] = cx[:m], cy[:m]
+            return w
