@@ -1053,23 +1053,29 @@ int64_t orc_csv_parse(const char* text, int64_t len, char delim, const int32_t* 
                       int64_t* objID, int64_t* ts, int64_t cap, int64_t* bad_line, int32_t* bad_kind) {
   int64_t pos = 0, line = 0;
   char* buf = NULL;
-  int bufcap = 0;
+  int bufcap = 0, *fidx = NULL;
   *bad_line = -1;
   *bad_kind = 0;
   while (pos < len) {
     int64_t e = pos, le;
-    int n = 0, nf, k, kind = 0, fb[64], fe[64], hex = 0;
+    int n = 0, nf, k, kind = 0, hex = 0, *fb, *fe;
     while (e < len && text[e] != '\n') ++e;
     le = e;
     if (le > pos && text[le - 1] == '\r') --le;
-    if (le - pos + 1 > bufcap) { bufcap = (int)(le - pos + 1) * 2; buf = (char*)realloc(buf, (size_t)bufcap); }
+    if (le - pos + 1 > bufcap) {
+      bufcap = (int)(le - pos + 1) * 2;
+      buf = (char*)realloc(buf, (size_t)bufcap);
+      fidx = (int*)realloc(fidx, sizeof(int) * 2 * (size_t)(bufcap + 2));
+    }
+    fb = fidx;
+    fe = fidx + bufcap + 2;
     for (int64_t i = pos; i < le; ++i)
       if (text[i] != '"') buf[n++] = text[i];  /* str.replace("\"", "") */
     if (le == pos) kind = 4;
     else {
-      nf = orc_java_split(buf, n, delim, fb, fe, 64);
+      nf = orc_java_split(buf, n, delim, fb, fe, bufcap + 2);
       for (k = 0; k < 4 && !kind; ++k)
-        if (want[k] >= nf || want[k] >= 64) kind = 3;
+        if (want[k] >= nf) kind = 3;
       if (!kind) {
         int64_t o = 0, t = 0;
         double vx = 0, vy = 0;
@@ -1089,5 +1095,6 @@ int64_t orc_csv_parse(const char* text, int64_t len, char delim, const int32_t* 
     pos = e + 1;
   }
   free(buf);
+  free(fidx);
   return line;
 }

@@ -197,6 +197,7 @@ hipError_t launch_expand_bitmap(hipStream_t s, const uint64_t* bitmap, int64_t w
 
 // CSV ingest (k_csv.hip)
 constexpr int64_t kCsvSeg = 64 * 1024;  // text bytes per count / index block
+constexpr int kCsvLds = 24 * 1024;      // parse: a block's 256 lines staged in LDS when they fit
 enum { kCsvOk = 0, kCsvNumberFormat = 1, kCsvUnsupported = 2, kCsvMissingField = 3, kCsvEmptyLine = 4 };
 struct CsvErr {
   unsigned long long line;  // first bad line (~0 = none)

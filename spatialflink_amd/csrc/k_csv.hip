@@ -100,8 +100,16 @@ __device__ __forceinline__ bool java_s(char c) {  // regex \s: [ \t\n\x0B\f\r]
   return c == ' ' || c == '\t' || c == '\n' || c == '\x0B' || c == '\f' || c == '\r';
 }
 
+// the bytes of a block's lines staged in LDS: text position i lives at p[i - base]
+struct LBytes {
+  const char* p;
+  int64_t base;
+  __device__ char operator()(int64_t i) const { return p[i - base]; }
+};
+
 // Field ranges of the wanted columns of line [b, e).  Returns the number of fields.
-__device__ int split_line(const GBytes& s, int64_t b, int64_t e, char d, const int32_t* want, Field* got) {
+template <class Src>
+__device__ int split_line(const Src& s, int64_t b, int64_t e, char d, const int32_t* want, Field* got) {
   const bool wsd = java_s(d);
   int field = 0;
   int64_t fs = b;
@@ -149,10 +157,8 @@ __device__ int split_line(const GBytes& s, int64_t b, int64_t e, char d, const i
   return field;
 }
 
-__global__ __launch_bounds__(kBlock) void csv_parse_kernel(CsvArgs a) {
-  const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (j >= a.lines) return;
-  const GBytes s{a.text};
+template <class Src>
+__device__ __forceinline__ void parse_line(const CsvArgs& a, const Src& s, int64_t j) {
   const int64_t b = j == 0 ? 0 : a.nl[j - 1] + 1;
   int64_t e = j < a.newlines ? a.nl[j] : a.len;
   if (e > b && s(e - 1) == '\r') --e;  // TextInputFormat drops the '\r' of "\r\n"
@@ -181,6 +187,32 @@ __global__ __launch_bounds__(kBlock) void csv_parse_kernel(CsvArgs a) {
   if (a.cx) {
     a.cx[j] = cell_index(x, a.minX, a.cl);
     a.cy[j] = cell_index(y, a.minY, a.cl);
+  }
+}
+
+// A block takes 256 consecutive lines.  Their bytes are contiguous: when they fit kCsvLds they
+// are staged in LDS with coalesced 16-B loads first, so the per-byte reads of the split/parse
+// state machines (a dependent chain per lane) hit LDS instead of waiting on L2 one byte at a time.
+__global__ __launch_bounds__(kBlock) void csv_parse_kernel(CsvArgs a) {
+  __shared__ __attribute__((aligned(16))) char lds[kCsvLds];
+  const int64_t L0 = (int64_t)blockIdx.x * kBlock;
+  const int64_t L1 = L0 + kBlock < a.lines ? L0 + kBlock : a.lines;  // exclusive
+  const int64_t b0 = L0 == 0 ? 0 : a.nl[L0 - 1] + 1;
+  const int64_t b1 = L1 - 1 < a.newlines ? a.nl[L1 - 1] : a.len;     // the last line's '\n' (or end)
+  const int64_t a0 = b0 & ~(int64_t)15;
+  const int64_t j = L0 + threadIdx.x;
+  if (b1 - a0 <= kCsvLds) {  // block-uniform
+    for (int64_t off = a0 + 16 * threadIdx.x; off < b1; off += 16 * kBlock) {
+      if (off + 16 <= a.len) {
+        *reinterpret_cast<uint4*>(lds + (off - a0)) = *reinterpret_cast<const uint4*>(a.text + off);
+      } else {
+        for (int k = 0; k < 16 && off + k < a.len; ++k) lds[off - a0 + k] = a.text[off + k];
+      }
+    }
+    __syncthreads();
+    if (j < L1) parse_line(a, LBytes{lds, a0}, j);
+  } else if (j < L1) {
+    parse_line(a, GBytes{a.text}, j);
   }
 }
 

@@ -426,6 +426,114 @@ def bench_sliding(args):
         dist.destroy_process_group()
 
 
+def bench_csv(args):
+    """C1 ingest: 1M-line CSV window (objID, ts, x, y; shortest round-trip doubles, the way Java's
+    Double.toString prints them) device-resident as text -> gf_csv_parse (SoA + 100x100 cells),
+    then the C1 point-point range query on the parsed window.  value = lines/s of the whole
+    text -> range-hits step; the parse kernel's roofline counts text bytes + 40 B/point out."""
+    import torch
+
+    import spatialflink_amd as sf
+    from spatialflink_amd import _lib
+    from spatialflink_amd.spatialStreams import GfCsvSchema, device_text
+
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    from csv_gen import make_csv
+
+    n = args.points or 1_000_000
+    L = _lib.lib()
+    ctx = _lib.context(0)
+    grid = sf.UniformGrid(100, *BEIJING)
+    texts = []
+    for j in range(2):
+        text, px, py, po, pt = make_csv(n, seed=31 + j)
+        texts.append((text, px, py, po, device_text(text)))
+    nbytes = len(texts[0][0])
+    sc = GfCsvSchema(b",", b"\0\0\0", 0, 1, 2, 3)
+    x = torch.empty(n, dtype=torch.float64, device="cuda"); y = torch.empty_like(x)
+    o = torch.empty(n, dtype=torch.int64, device="cuda"); ts = torch.empty_like(o)
+    cx = torch.empty(n, dtype=torch.int32, device="cuda"); cy = torch.empty_like(cx)
+    nout, bl, bk = C.c_int64(), C.c_int64(), C.c_int32()
+    qx = np.array([QPOINT[0]]); qy = np.array([QPOINT[1]])
+    h = C.c_void_p()
+    _lib.check(L.gf_range_pp_plan_create(ctx.handle, C.byref(grid.c_grid), qx.ctypes.data, qy.ctypes.data, 1,
+                                         args.radius, 0, 0, C.byref(h)), ctx.handle, "plan")
+    words = (n + 63) // 64
+    bitmap = torch.empty(words, dtype=torch.int64, device="cuda")
+    counts = torch.zeros(2, dtype=torch.int64, device="cuda")
+    pts = sf.PointWindow(x, y, o, ts).c_struct()
+
+    def parse(i):
+        t = texts[i % 2][4]
+        _lib.check(L.gf_csv_parse(ctx.handle, C.c_void_p(t.data_ptr()), t.numel(), C.byref(sc), C.byref(grid.c_grid),
+                                  x.data_ptr(), y.data_ptr(), o.data_ptr(), ts.data_ptr(), cx.data_ptr(), cy.data_ptr(),
+                                  n, C.byref(nout), C.byref(bl), C.byref(bk)), ctx.handle, "gf_csv_parse")
+
+    def step(i):
+        parse(i)
+        _lib.check(L.gf_range_run(h, C.byref(pts), bitmap.data_ptr(), None, counts.data_ptr()), ctx.handle, "range")
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    ctx.set_timing((1 << _lib.K_CSV_PARSE) | (1 << _lib.K_RANGE_SCAN))
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(i)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    pms, pcnt = ctx.timing(_lib.K_CSV_PARSE)
+    rms, rcnt = ctx.timing(_lib.K_RANGE_SCAN)
+    ctx.set_timing(0)
+    # ingest alone
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    for i in range(args.steps):
+        parse(i)
+    torch.cuda.synchronize()
+    ingest_s = (time.perf_counter() - t1) / args.steps
+    # parity: the last parsed window (texts[(steps-1) % 2]) bit-exact vs the oracle, and its range hits
+    j = (args.steps - 1) % 2
+    parse(j)
+    text = texts[j][0]
+    ex, ey, eo, et, ebl, ebk = O.csv_parse(text, ",", [0, 1, 2, 3])
+    verified = bool(ebl == -1 and np.array_equal(x.cpu().numpy().view(np.int64), ex.view(np.int64))
+                    and np.array_equal(y.cpu().numpy().view(np.int64), ey.view(np.int64))
+                    and np.array_equal(o.cpu().numpy(), eo) and np.array_equal(ts.cpu().numpy(), et))
+    og = O.grid(100, *BEIJING)
+    ecx, ecy = O.assign_cells(og, ex, ey)
+    verified &= bool(np.array_equal(cx.cpu().numpy(), ecx) and np.array_equal(cy.cpu().numpy(), ecy))
+    _lib.check(L.gf_range_run(h, C.byref(pts), bitmap.data_ptr(), None, counts.data_ptr()), ctx.handle, "range")
+    got = sf.spatialOperators.bitmap_indices(ctx, bitmap, n).astype(np.int64)
+    verified &= bool(np.array_equal(got, O.range_pp(og, ex, ey, [QPOINT[0]], [QPOINT[1]], args.radius)))
+    L.gf_range_plan_destroy(h)
+    cpu = None
+    if not args.no_cpu_baseline:  # the oracle's restatement of the reference's per-line map, 1 thread
+        reps, tc = 0, time.perf_counter()
+        while True:
+            O.csv_parse(text, ",", [0, 1, 2, 3])
+            reps += 1
+            if time.perf_counter() - tc >= min(args.cpu_seconds, 10.0):
+                break
+        ct = time.perf_counter() - tc
+        cpu = {"value": round(reps * n / ct, 1), "unit": "lines/s", "cores": 1, "kind": "port",
+               "sample": f"the {n}-line window x {reps} ({ct:.1f}s): oracle orc_csv_parse (quote removal, Java split "
+                         "rule, Long.valueOf, strtod), 1 thread -- ingest only"}
+    avg_parse = pms / 1000.0 / max(pcnt, 1)
+    _line("CSV ingest + point-point range", n * args.steps / elapsed, "lines/s", args.steps, args.warmup, elapsed,
+          "csv_parse_kernel", float(nbytes + 40 * n), avg_parse,
+          {"config": {"workload": f"csv_{n // 1_000_000}Mlines_range_r{args.radius}_grid100", "lines": n,
+                      "text_bytes": nbytes, "radius": args.radius},
+           "breakdown": {"parse_kernel_us": round(avg_parse * 1e6, 2),
+                         "range_kernel_us": round(rms * 1000.0 / max(rcnt, 1), 2),
+                         "ingest_call_us": round(ingest_s * 1e6, 2),
+                         "ingest_lines_per_s": round(n / ingest_s, 1),
+                         "ingest_text_GBps": round(nbytes / ingest_s / 1e9, 2)},
+           "cpu_baseline": cpu, "verified_vs_oracle": verified})
+
+
 def run(args):
     if args.workload in ("range", "ppoly"):
         bench_range(args, polygons=args.workload == "ppoly")
@@ -433,5 +541,7 @@ def run(args):
         bench_join(args)
     elif args.workload == "sliding":
         bench_sliding(args)
+    elif args.workload == "csv":
+        bench_csv(args)
     else:
         raise SystemExit(f"unknown workload {args.workload}")
