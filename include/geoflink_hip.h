@@ -169,6 +169,13 @@ typedef struct gf_knn_plan gf_knn_plan;
 /* PointPointKNNQuery.run(stream, queryPoint, r, k) -- PointPointKNNQuery.java:33,132-150 */
 int    gf_knn_pp_plan_create(gf_ctx* ctx, const gf_grid* g, double qx, double qy, double r,
                              int32_t k, int metric, gf_knn_plan** out);   /* 1 <= k <= 512 */
+/* PointPolygonKNNQuery.run(stream, queryPolygon, r, k) -- knn/PointPolygonKNNQuery.java:245-317:
+ * kNN of the window's points to ONE query polygon (polys->npoly == 1): candidates have their cell
+ * in C u G of the polygon's bbox cells and d <= r, d = JTS point-polygon distance (0 inside) or,
+ * approximate, DistanceFunctions.getPointPolygonBBoxMinEuclideanDistance.  Same records, decode
+ * and contract as point queries ((d, objID) order, one entry per objID); pipeline depth 1. */
+int    gf_knn_ppoly_plan_create(gf_ctx* ctx, const gf_grid* g, const gf_polygons* polys, double r, int32_t k,
+                                int approximate, int metric, gf_knn_plan** out);
 void   gf_knn_plan_destroy(gf_knn_plan* plan);
 /* Candidate-buffer capacity (entries); default 1<<20.  Small values force the exact fallback. */
 int    gf_knn_plan_set_capacity(gf_knn_plan* plan, int64_t cap);

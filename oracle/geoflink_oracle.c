@@ -635,6 +635,60 @@ int32_t orc_knn_contract(const orc_grid* g, int64_t n, const double* x, const do
   return nout;
 }
 
+/* PointPolygonKNNQuery.windowBased -- knn/PointPolygonKNNQuery.java:245-317: cell filter with the
+ * polygon's guaranteed / candidate sets (UniformGrid.java:193-206,399-411, as orc_range_ppoly),
+ * d = JTS point-polygon distance (DistanceFunctions.java:33-36) or, approximate, the bbox
+ * distance (:150-200); d <= r; then the build contract of orc_knn_contract (one entry per objID,
+ * (d, objID) order, first k). */
+int32_t orc_knn_ppoly_contract(const orc_grid* g, int64_t n, const double* x, const double* y,
+                               const int64_t* objID, const orc_polygons* P, double r, int32_t k,
+                               int approximate, int metric, int64_t* out_objID, double* out_d,
+                               int64_t* out_idx) {
+  strset G, C;
+  char id[32];
+  double x1, y1, x2, y2;
+  int32_t xi1, yi1, xi2, yi2;
+  if (k <= 0 || P->npoly != 1) return ORC_ERR_ARG;
+  ss_init(&G, 64); ss_init(&C, 64);
+  polygon_bbox(P, 0, &x1, &y1, &x2, &y2);
+  orc_cell_of(g, x1, y1, &xi1, &yi1);
+  orc_cell_of(g, x2, y2, &xi2, &yi2);
+  for (int64_t a = xi1; a <= xi2; a++)
+    for (int64_t b = yi1; b <= yi2; b++) {
+      orc_cell_id((int32_t)a, (int32_t)b, id);
+      g_cells_of(g, r, id, &G);
+    }
+  for (int64_t a = xi1; a <= xi2; a++)
+    for (int64_t b = yi1; b <= yi2; b++) {
+      orc_cell_id((int32_t)a, (int32_t)b, id);
+      c_cells_of(g, r, id, &G, &C);
+    }
+  tup* c = (tup*)malloc(sizeof(tup) * (size_t)(n > 0 ? n : 1));
+  int64_t m = 0;
+  for (int64_t i = 0; i < n; i++) {
+    int32_t cx, cy;
+    orc_cell_of(g, x[i], y[i], &cx, &cy);
+    orc_cell_id(cx, cy, id);
+    if (!(ss_contains(&C, id) || ss_contains(&G, id))) continue; /* :279-284 */
+    double d = approximate ? orc_point_bbox_distance(x[i], y[i], x1, y1, x2, y2)
+                           : orc_point_polygon_distance(x[i], y[i], P, 0, metric);
+    if (!(d <= r)) continue;
+    c[m].d = d; c[m].obj = objID[i]; c[m].idx = i; m++;
+  }
+  ss_free(&G); ss_free(&C);
+  qsort(c, (size_t)m, sizeof(tup), cmp_obj_d_idx);
+  int64_t u = 0;
+  for (int64_t i = 0; i < m; i++)
+    if (u == 0 || c[u - 1].obj != c[i].obj) c[u++] = c[i];
+  qsort(c, (size_t)u, sizeof(tup), cmp_d_obj);
+  int32_t nout = (int32_t)(u < k ? u : k);
+  for (int32_t i = 0; i < nout; i++) {
+    out_objID[i] = c[i].obj; out_d[i] = c[i].d; out_idx[i] = c[i].idx;
+  }
+  free(c);
+  return nout;
+}
+
 /* ---- java.util.PriorityQueue<Tuple2<Point,Double>> with
  *      Comparators.inTuplePointDistanceComparator (utils/Comparators.java:14-32) ---- */
 typedef struct { tup* q; int32_t size, cap; } jpq;

@@ -140,6 +140,13 @@ int32_t orc_generate_query_polygons(int32_t numQueryPolygons, double minX, doubl
 void orc_java_random_points(int64_t seed, int64_t n, double minX, double maxX,
                             double minY, double maxY, double* x, double* y);
 
+/* PointPolygonKNNQuery.windowBased -- knn/PointPolygonKNNQuery.java:245-317, one query polygon
+ * (P->npoly == 1), build contract as orc_knn_contract.  Returns the count or ORC_ERR_ARG. */
+int32_t orc_knn_ppoly_contract(const orc_grid* g, int64_t n, const double* x, const double* y,
+                               const int64_t* objID, const orc_polygons* P, double r, int32_t k,
+                               int approximate, int metric, int64_t* out_objID, double* out_d,
+                               int64_t* out_idx);
+
 /* Deserialization.CSVTSVToTSpatial.map over the lines of text (Deserialization.java:314-322):
  * want = csvTsvSchemaAttr (objID, time, x, y field indices).  Returns the line count (rows past
  * cap are not written); the first bad line and its kind (1 NumberFormatException, 2 hexadecimal

@@ -72,6 +72,9 @@ def lib():
         L.orc_generate_query_polygons.argtypes = [i32, d, d, d, d, P, P, i32]
         L.orc_generate_query_polygons.restype = i32
         L.orc_java_random_points.argtypes = [i64, i64, d, d, d, d, P, P]
+        L.orc_knn_ppoly_contract.argtypes = [C.POINTER(OrcGrid), i64, P, P, P, C.POINTER(OrcPolygons), d, i32,
+                                             C.c_int, C.c_int, P, P, P]
+        L.orc_knn_ppoly_contract.restype = i32
         L.orc_csv_parse.argtypes = [C.c_char_p, i64, C.c_char, P, P, P, P, P, i64, C.POINTER(i64), C.POINTER(i32)]
         L.orc_csv_parse.restype = i64
         _lib = L
@@ -244,3 +247,14 @@ def csv_parse(text: bytes, delim: str, want):
     x = np.zeros(n); y = np.zeros(n); o = np.zeros(n, np.int64); t = np.zeros(n, np.int64)
     lib().orc_csv_parse(text, len(text), delim.encode(), _p(w), _p(x), _p(y), _p(o), _p(t), n, C.byref(bl), C.byref(bk))
     return x, y, o, t, bl.value, bk.value
+
+
+def knn_ppoly(g, x, y, objID, P: "Polygons", r, k, approximate=False, metric=METRIC_SQRT):
+    """PointPolygonKNNQuery (one query polygon) -> (n, objID, dist, idx), build contract."""
+    x, y, objID = _f64(x), _f64(y), np.ascontiguousarray(objID, np.int64)
+    oo = np.zeros(k, np.int64); od = np.zeros(k); oi = np.zeros(k, np.int64)
+    m = lib().orc_knn_ppoly_contract(C.byref(g), len(x), _p(x), _p(y), _p(objID), C.byref(P.c), float(r), int(k),
+                                     int(approximate), int(metric), _p(oo), _p(od), _p(oi))
+    if m < 0:
+        raise ValueError(f"orc_knn_ppoly_contract: {m}")
+    return m, oo[:m], od[:m], oi[:m]

@@ -9,13 +9,14 @@ from . import _lib
 from .spatialIndices import UniformGrid, generateCellIDStr, getIntCellIndices, padLeadingZeroesToInt
 from .spatialObjects import Point, PointWindow, Polygon, PolygonSet
 from .spatialOperators import (KNNResult, PinnedRecords, PointPointJoinQuery, PointPointKNNQuery, PointPointRangeQuery,
+                               PointPolygonKNNQuery,
                                PointPolygonRangeQuery, QueryConfiguration, QueryType, RangeResult, assign_cells,
                                bucket_by_cell, knn_merge_host, synthetic_uniform)
 from .spatialStreams import Deserialization
 from .windows import SlidingKNNQuery, SlidingRangeQuery, SlidingWindows
 
 __all__ = [
-    "SlidingWindows", "SlidingKNNQuery", "SlidingRangeQuery", "Deserialization",
+    "SlidingWindows", "SlidingKNNQuery", "SlidingRangeQuery", "Deserialization", "PointPolygonKNNQuery",
     "UniformGrid", "Point", "Polygon", "PolygonSet", "PointWindow", "QueryType", "QueryConfiguration",
     "PointPointRangeQuery", "PointPolygonRangeQuery", "PointPointKNNQuery", "PointPointJoinQuery", "RangeResult",
     "KNNResult", "PinnedRecords", "knn_merge_host", "assign_cells", "bucket_by_cell", "synthetic_uniform", "generateCellIDStr",

@@ -900,6 +900,8 @@ extern "C" void gf_knn_plan_destroy(gf_knn_plan* P) {
   }
   if (P->tmp_result) hipFree(P->tmp_result);
   if (P->host_result) hipHostFree(P->host_result);
+  for (void* q : {(void*)P->ring_off, (void*)P->vert_off, (void*)P->vx, (void*)P->vy, (void*)P->ring_env})
+    if (q) hipFree(q);
   delete P;
 }
 
@@ -951,6 +953,76 @@ extern "C" int gf_knn_pp_plan_create(gf_ctx* ctx, const gf_grid* g, double qx, d
   if ((e = hipHostMalloc(&P->host_result, gf_knn_result_bytes(k), hipHostMallocDefault)) != hipSuccess)
     return fail(hip_err(ctx, e, "hipHostMalloc"));
   P->scan_blocks = 0;
+  *out = P;
+  return GF_OK;
+}
+
+// PointPolygonKNNQuery.run(stream, queryPolygon, r, k) -- knn/PointPolygonKNNQuery.java:245-317:
+// the C u G cells of the polygon's bbox cells (UniformGrid.java:193-206,399-411) as one rect
+// pair (valid cells within c of the bbox rect; for g == 0 the bbox cells themselves, no
+// validKey), the polygon on the device for the exact JTS distance.
+extern "C" int gf_knn_ppoly_plan_create(gf_ctx* ctx, const gf_grid* g, const gf_polygons* poly, double r,
+                                        int32_t k, int approximate, int metric, gf_knn_plan** out) {
+  if (!ctx || !out || !grid_ok(g) || !poly || poly->npoly != 1 || k < 1 || k > kMaxK || (metric != 0 && metric != 1))
+    return set_err(ctx, GF_ERR_ARG, "gf_knn_ppoly_plan_create: bad argument (one polygon, 1 <= k <= 512)");
+  *out = nullptr;
+  const int32_t nrings = poly->ring_off[1] - poly->ring_off[0];
+  if (poly->ring_off[0] != 0 || nrings < 1) return set_err(ctx, GF_ERR_ARG, "polygon without a shell");
+  for (int32_t j = 0; j < nrings; ++j) {
+    const int32_t v0 = poly->vert_off[j], v1 = poly->vert_off[j + 1];
+    if (v1 - v0 < 4 || poly->vx[v0] != poly->vx[v1 - 1] || poly->vy[v0] != poly->vy[v1 - 1])
+      return set_err(ctx, GF_ERR_ARG, "ring must be closed with >= 4 vertices");
+  }
+  int st = gf_knn_pp_plan_create(ctx, g, 0.0, 0.0, r, k, metric, out);
+  if (st) return st;
+  gf_knn_plan* P = *out;
+  *out = nullptr;
+  P->poly = 1;
+  P->approx = approximate != 0;
+  std::vector<double> renv(4 * (size_t)nrings);
+  for (int32_t j = 0; j < nrings; ++j) {
+    const int32_t v0 = poly->vert_off[j], v1 = poly->vert_off[j + 1];
+    double mnx = poly->vx[v0], mxx = mnx, mny = poly->vy[v0], mxy = mny;
+    for (int32_t v = v0 + 1; v < v1; ++v) {
+      mnx = std::min(mnx, poly->vx[v]); mxx = std::max(mxx, poly->vx[v]);
+      mny = std::min(mny, poly->vy[v]); mxy = std::max(mxy, poly->vy[v]);
+    }
+    renv[4 * j] = mnx; renv[4 * j + 1] = mxx; renv[4 * j + 2] = mny; renv[4 * j + 3] = mxy;
+  }
+  P->bbox[0] = renv[0]; P->bbox[1] = renv[2]; P->bbox[2] = renv[1]; P->bbox[3] = renv[3];  // shell envelope
+  const int32_t gl = guaranteed_layers(g->cellLength, r), cl = candidate_layers(g->cellLength, r);
+  const int64_t bx0 = cell_index(P->bbox[0], g->minX, g->cellLength), bx1 = cell_index(P->bbox[2], g->minX, g->cellLength);
+  const int64_t by0 = cell_index(P->bbox[1], g->minY, g->cellLength), by1 = cell_index(P->bbox[3], g->minY, g->cellLength);
+  const double nan = std::numeric_limits<double>::quiet_NaN();
+  const int64_t n1 = g->n - 1;
+  QueryRect q;
+  q.minX = g->minX;
+  q.minY = g->minY;
+  if (cl > 0) {
+    q.cgx = axis_iv(std::max<int64_t>(bx0 - cl, 0), std::min<int64_t>(bx1 + cl, n1), g->minX, g->cellLength);
+    q.cgy = axis_iv(std::max<int64_t>(by0 - cl, 0), std::min<int64_t>(by1 + cl, n1), g->minY, g->cellLength);
+  } else {
+    q.cgx = q.cgy = {nan, nan};
+  }
+  if (gl > 0) {
+    q.gx = axis_iv(std::max<int64_t>(bx0 - gl, 0), std::min<int64_t>(bx1 + gl, n1), g->minX, g->cellLength);
+    q.gy = axis_iv(std::max<int64_t>(by0 - gl, 0), std::min<int64_t>(by1 + gl, n1), g->minY, g->cellLength);
+  } else if (gl == 0) {  // the bbox cells themselves, without validKey
+    q.gx = axis_iv(bx0, bx1, g->minX, g->cellLength);
+    q.gy = axis_iv(by0, by1, g->minY, g->cellLength);
+  } else {
+    q.gx = q.gy = {nan, nan};
+  }
+  q.g_any = (gl >= 0) && !std::isnan(q.gx.lo) && !std::isnan(q.gy.lo);
+  P->qr = q;
+  const int32_t nverts = poly->vert_off[nrings];
+  std::vector<int32_t> ro = {0, nrings}, vo(poly->vert_off, poly->vert_off + nrings + 1);
+  std::vector<double> vx(poly->vx, poly->vx + nverts), vy(poly->vy, poly->vy + nverts);
+  if ((st = upload(ctx, &P->ring_off, ro)) || (st = upload(ctx, &P->vert_off, vo)) || (st = upload(ctx, &P->vx, vx)) ||
+      (st = upload(ctx, &P->vy, vy)) || (st = upload(ctx, &P->ring_env, renv))) {
+    gf_knn_plan_destroy(P);
+    return st;
+  }
   *out = P;
   return GF_OK;
 }
@@ -1010,10 +1082,29 @@ static KnnSelectArgs select_args(gf_knn_plan* P, int j, int use_state, int write
   return q;
 }
 
+static KnnPolyArgs poly_args(gf_knn_plan* P, int j, const gf_points* pts, int64_t begin, int64_t end, int use_state,
+                             int use_hint) {
+  const gf_knn_plan::Lane& L = P->lane[j];
+  KnnPolyArgs a{};
+  a.x = pts->x; a.y = pts->y; a.objID = pts->objID; a.begin = begin; a.end = end;
+  a.qr = P->qr;
+  a.poly = PolyView{P->ring_off, P->vert_off, P->vx, P->vy, P->ring_env, P->metric};
+  for (int i = 0; i < 4; ++i) a.bbox[i] = P->bbox[i];
+  a.approx = P->approx; a.r = P->r; a.k = P->k; a.use_state = use_state; a.use_hint = use_hint;
+  a.st = L.st; a.cand_d = L.cand_d; a.cand_i = L.cand_i; a.cand_o = L.cand_o; a.cap = (unsigned long long)P->cap;
+  return a;
+}
+
 // scan + select of points [begin, end) on lane j, stream-ordered
 static int knn_scan_select(gf_knn_plan* P, int j, const gf_points* pts, int64_t begin, int64_t end, int use_state,
                            int write_hint, void* result) {
   gf_ctx* ctx = P->ctx;
+  if (P->poly) {
+    const KnnPolyArgs a = poly_args(P, j, pts, begin, end, use_state, 0);
+    GF_HIP_CHECK(ctx, launch_knn_poly_scan(ctx, a, scan_blocks_for(P, (end - begin + 1) / 2)));
+    GF_HIP_CHECK(ctx, launch_knn_select(ctx, select_args(P, j, use_state, write_hint, result, P->idx_base)));
+    return GF_OK;
+  }
   const KnnScanArgs s = scan_args(P, j, pts, begin, end, use_state);
   GF_HIP_CHECK(ctx, launch_knn_scan(ctx, s, scan_blocks_for(P, end - begin), P->scan_unroll, P->scan_nt));
   GF_HIP_CHECK(ctx, launch_knn_select(ctx, select_args(P, j, use_state, write_hint, result, P->idx_base)));
@@ -1021,6 +1112,10 @@ static int knn_scan_select(gf_knn_plan* P, int j, const gf_points* pts, int64_t 
 }
 
 static int knn_launch_sample(gf_knn_plan* P, int j, const gf_points* pts, int use_hint) {
+  if (P->poly) {
+    GF_HIP_CHECK(P->ctx, launch_knn_poly_sample(P->ctx, poly_args(P, j, pts, 0, pts->n, 1, use_hint)));
+    return GF_OK;
+  }
   KnnSampleArgs s{};
   s.x = pts->x; s.y = pts->y; s.n = pts->n; s.qx = P->qx; s.qy = P->qy; s.qr = P->qr;
   s.r = P->r; s.s_r = s_prefilter(P->r, P->metric); s.k = P->k; s.metric = P->metric; s.st = P->lane[j].st;
@@ -1089,6 +1184,8 @@ extern "C" int gf_knn_plan_set_pipeline(gf_knn_plan* P, int depth) {
   gf_ctx* ctx = P->ctx;
   if (depth == 2 && P->k > 256)
     return set_err(ctx, GF_ERR_ARG, "gf_knn_plan_set_pipeline: depth 2 needs k <= 256");
+  if (depth == 2 && P->poly)
+    return set_err(ctx, GF_ERR_ARG, "gf_knn_plan_set_pipeline: polygon queries run at depth 1");
   int st = bind(ctx);
   if (st || (st = gf_knn_plan_flush(P))) return st;
   GF_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));

@@ -117,6 +117,37 @@ struct KnnSampleArgs {
   KnnState* st;
 };
 
+// one polygon set in device memory (CSR: polygon -> rings -> vertices; rings closed)
+struct PolyView {
+  const int32_t* ring_off;
+  const int32_t* vert_off;
+  const double* vx;
+  const double* vy;
+  const double* ring_env;  // [nrings*4] minx, maxx, miny, maxy
+  int metric;
+};
+
+// polygon-query kNN (PointPolygonKNNQuery): scan / sample arguments
+struct KnnPolyArgs {
+  const double* x;
+  const double* y;
+  const int64_t* objID;
+  int64_t begin, end;   // points [begin, end)
+  QueryRect qr;         // C u G of the polygon's bbox cells
+  PolyView poly;        // the query polygon (index 0)
+  double bbox[4];       // shell envelope x1, y1, x2, y2
+  int approx;           // bbox distance (DistanceFunctions.java:150-200) instead of JTS
+  double r;
+  int32_t k;
+  int use_state;        // scan: T = st->T (set by the sample); else T = r
+  int use_hint;         // sample: take st->hint_T when set
+  KnnState* st;
+  double* cand_d;
+  uint32_t* cand_i;
+  int64_t* cand_o;
+  unsigned long long cap;
+};
+
 struct KnnSelectArgs {
   KnnState* st;
   const double* cand_d;
@@ -233,6 +264,8 @@ hipError_t launch_knn_sample(gf_ctx* ctx, const KnnSampleArgs& a);
 hipError_t launch_knn_scan(gf_ctx* ctx, const KnnScanArgs& a, int blocks, int unroll, int nt);
 hipError_t launch_knn_select(gf_ctx* ctx, const KnnSelectArgs& a);
 
+hipError_t launch_knn_poly_sample(gf_ctx* ctx, const KnnPolyArgs& a);
+hipError_t launch_knn_poly_scan(gf_ctx* ctx, const KnnPolyArgs& a, int blocks);
 hipError_t launch_knn_merge(gf_ctx* ctx, int32_t k, const void* records, int32_t nrec, size_t rec_stride,
                             int32_t nwin, size_t win_stride, void* result, size_t res_stride);
 // records of one merge given as a pointer list (kernel argument; the panes of a sliding window)
@@ -393,6 +426,14 @@ struct gf_knn_plan {
   int scan_blocks = 0;   // tuning: 0 = auto (4 blocks per CU)
   int scan_unroll = 1;   // point pairs per lane per iteration (tools/tune_knn.py sweep)
   int scan_nt = 1;       // nontemporal loads
+  // polygon query (gf_knn_ppoly_plan_create): device copy of the polygon, depth 1 only
+  int poly = 0, approx = 0;
+  int32_t* ring_off = nullptr;
+  int32_t* vert_off = nullptr;
+  double* vx = nullptr;
+  double* vy = nullptr;
+  double* ring_env = nullptr;
+  double bbox[4] = {0, 0, 0, 0};
 };
 
 struct gf_window {

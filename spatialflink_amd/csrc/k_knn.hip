@@ -18,6 +18,7 @@
 // below T (or T == r); otherwise it is flagged and gf_knn_decode re-evaluates the window
 // (sample path, then exhaustive T = r partitions).  Output: (d, objID) ascending, the
 // minimum-(d, idx) occurrence per objID.
+#include "gf_geom.hpp"
 #include "gf_internal.hpp"
 
 namespace gf {
@@ -67,11 +68,70 @@ __host__ __device__ inline RecView rec_view(void* base, int k) {
 // ---------------------------------------------------------------------------------------
 // sample
 // ---------------------------------------------------------------------------------------
+// The sample kernels' common end: flush the block's LDS histogram, and the last-arriving block
+// (atomic ticket) sets T = the upper edge of the bin holding the sample's k-th candidate.
+__device__ void sample_finish(KnnState* st, uint32_t* lh, int32_t k, double r, int metric, int64_t bbase) {
+  __shared__ uint32_t wsum[kBlock / 64];
+  __shared__ int s_last, s_bin;
+  __syncthreads();
+  for (int j = threadIdx.x; j < kDistBins; j += kBlock)
+    if (lh[j]) atomicAdd(&st->hist[j], lh[j]);
+  // last-arriving block picks the threshold (split-K style ticket, agent-scope fences)
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    const uint32_t t = atomicAdd(&st->ticket, 1u);
+    s_last = (t == gridDim.x - 1);
+  }
+  __syncthreads();
+  if (!s_last) return;
+  __threadfence();
+  constexpr int kPer = kDistBins / kBlock;  // 16 bins per thread
+  uint32_t v[kPer];
+  uint32_t s = 0;
+#pragma unroll
+  for (int j = 0; j < kPer; ++j) {
+    v[j] = __hip_atomic_load(&st->hist[threadIdx.x * kPer + j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s += v[j];
+  }
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  uint32_t inc = s;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t t = __shfl_up(inc, off, 64);
+    if (lane >= off) inc += t;
+  }
+  if (lane == 63) wsum[wid] = inc;
+  if (threadIdx.x == 0) s_bin = -1;
+  __syncthreads();
+  uint32_t before = 0;
+  for (int w = 0; w < wid; ++w) before += wsum[w];
+  const uint32_t excl = before + inc - s;
+  const uint32_t kk = (uint32_t)k;
+  if (excl < kk && kk <= excl + s) {
+    uint32_t run = excl;
+    for (int j = 0; j < kPer; ++j) {
+      run += v[j];
+      if (run >= kk) { s_bin = threadIdx.x * kPer + j; break; }
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double T = r;
+    if (s_bin >= 0) {
+      const double up = dist_bin_upper(s_bin, bbase);
+      T = up < r ? up : r;
+    }
+    st->T = T;
+    st->s_pre = s_prefilter(T, metric);
+    st->ticket = 0;
+  }
+  for (int j = threadIdx.x; j < kDistBins; j += kBlock) st->hist[j] = 0u;
+}
+
 template <int METRIC>
 __global__ __launch_bounds__(kBlock) void knn_sample_kernel(KnnSampleArgs a) {
   __shared__ uint32_t lh[kDistBins];
-  __shared__ uint32_t wsum[kBlock / 64];
-  __shared__ int s_last, s_bin;
 #ifdef GF_TRACE
   if (blockIdx.x == 0 && threadIdx.x == 0) a.st->tr[0] = wall_clock64();
 #endif
@@ -107,60 +167,7 @@ __global__ __launch_bounds__(kBlock) void knn_sample_kernel(KnnSampleArgs a) {
     if (knn_pass<METRIC>(a.qx, a.qy, a.qr, xv[u].y, yv[u].y, a.s_r, a.r))
       atomicAdd(&lh[dist_bin(knn_dist<METRIC>(a.qx, a.qy, xv[u].y, yv[u].y), bbase)], 1u);
   }
-  __syncthreads();
-  for (int j = threadIdx.x; j < kDistBins; j += kBlock)
-    if (lh[j]) atomicAdd(&a.st->hist[j], lh[j]);
-  // last-arriving block picks the threshold (split-K style ticket, agent-scope fences)
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __threadfence();
-    const uint32_t t = atomicAdd(&a.st->ticket, 1u);
-    s_last = (t == gridDim.x - 1);
-  }
-  __syncthreads();
-  if (!s_last) return;
-  __threadfence();
-  constexpr int kPer = kDistBins / kBlock;  // 16 bins per thread
-  uint32_t v[kPer];
-  uint32_t s = 0;
-#pragma unroll
-  for (int j = 0; j < kPer; ++j) {
-    v[j] = __hip_atomic_load(&a.st->hist[threadIdx.x * kPer + j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s += v[j];
-  }
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  uint32_t inc = s;
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const uint32_t t = __shfl_up(inc, off, 64);
-    if (lane >= off) inc += t;
-  }
-  if (lane == 63) wsum[wid] = inc;
-  if (threadIdx.x == 0) s_bin = -1;
-  __syncthreads();
-  uint32_t before = 0;
-  for (int w = 0; w < wid; ++w) before += wsum[w];
-  const uint32_t excl = before + inc - s;
-  const uint32_t k = (uint32_t)a.k;
-  if (excl < k && k <= excl + s) {
-    uint32_t run = excl;
-    for (int j = 0; j < kPer; ++j) {
-      run += v[j];
-      if (run >= k) { s_bin = threadIdx.x * kPer + j; break; }
-    }
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    double T = a.r;
-    if (s_bin >= 0) {
-      const double up = dist_bin_upper(s_bin, bbase);
-      T = up < a.r ? up : a.r;
-    }
-    a.st->T = T;
-    a.st->s_pre = s_prefilter(T, a.metric);
-    a.st->ticket = 0;
-  }
-  for (int j = threadIdx.x; j < kDistBins; j += kBlock) a.st->hist[j] = 0u;
+  sample_finish(a.st, lh, a.k, a.r, a.metric, bbase);
 }
 
 hipError_t launch_knn_sample(gf_ctx* ctx, const KnnSampleArgs& a) {
@@ -676,7 +683,7 @@ __device__ void knn_select_body(const KnnSelectArgs& a, LDS& L) {
     a.st->count = 0ull;  // ready for the lane's next window
     if (a.write_hint) {
       double h;
-      if (status == 0) h = nres == k ? 2.0 * from_bits(L.rd[k - 1]) : a.r;
+      if (status == 0) h = nres == k ? fmax(2.0 * from_bits(L.rd[k - 1]), 4.9e-324) : a.r;
       else if (overflow) h = T * sqrt(0.5 * (double)a.cap / (double)count);
       else if (too_few) h = 2.0 * T;
       else h = T;
@@ -838,6 +845,84 @@ hipError_t launch_knn_merge(gf_ctx* ctx, int32_t k, const void* records, int32_t
 hipError_t launch_knn_merge_list(gf_ctx* ctx, int32_t k, const KnnRecList& list, int32_t nrec, void* result) {
   KTimer t(ctx, GF_K_KNN_MERGE);
   hipLaunchKernelGGL(knn_merge_list_kernel, dim3(1), dim3(kSelT), 0, ctx->stream, k, list, nrec, result);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------
+// Polygon-query kNN -- PointPolygonKNNQuery.windowBased (knn/PointPolygonKNNQuery.java:245-317):
+// a point is a candidate iff its cell is in C u G of the polygon (UniformGrid.java:193-206,
+// 399-411, the bbox cells as query cells) and d(p, P) <= T, d = JTS point-polygon distance
+// (DistanceFunctions.java:33-36) or, approximate, the bbox distance (:150-200).  The envelope
+// prefilter (env_far) skips the exact distance only where no rounding could bring it under T.
+// T: the continuous-query hint or a 256K-point sample's k-th distance (as for point queries);
+// the candidates then go through the same select (dedupe by objID, (d, objID) order).
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ bool poly_pass(const KnnPolyArgs& a, double px, double py, double T, double& d) {
+  if (!classify_cg(a.qr, px, py)) return false;
+  if (px == px && py == py && env_far(a.bbox, px, py, T)) return false;
+  d = a.approx ? point_bbox_distance(px, py, a.bbox) : polygon_distance(px, py, a.poly, 0);
+  return d <= T;
+}
+
+__global__ __launch_bounds__(kBlock) void knn_poly_sample_kernel(KnnPolyArgs a) {
+  __shared__ uint32_t lh[kDistBins];
+  if (a.use_hint) {
+    const double h = a.st->hint_T;
+    if (h > 0.0) {
+      if (blockIdx.x == 0 && threadIdx.x == 0) a.st->T = h < a.r ? h : a.r;
+      return;
+    }
+  }
+  for (int j = threadIdx.x; j < kDistBins; j += kBlock) lh[j] = 0u;
+  __syncthreads();
+  const int64_t n = a.end - a.begin;
+  const int64_t stride = n / gridDim.x;  // >= kSamplePerBlock (n >= kSampleMinN)
+  const int64_t p0 = a.begin + (int64_t)blockIdx.x * stride;
+  const int64_t bbase = dist_bin_base(a.r);
+  for (int u = threadIdx.x; u < kSamplePerBlock; u += kBlock) {
+    const double px = a.x[p0 + u], py = a.y[p0 + u];
+    double d;
+    if (poly_pass(a, px, py, a.r, d)) atomicAdd(&lh[dist_bin(d, bbase)], 1u);
+  }
+  sample_finish(a.st, lh, a.k, a.r, a.poly.metric, bbase);
+}
+
+__global__ __launch_bounds__(kBlock) void knn_poly_scan_kernel(KnnPolyArgs a) {
+  const double T = a.use_state ? a.st->T : a.r;
+  const int lane = threadIdx.x & 63;
+  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  for (int64_t i = a.begin + (int64_t)blockIdx.x * kBlock + threadIdx.x; i - lane < a.end; i += stride) {
+    const bool in = i < a.end;
+    const double px = in ? __builtin_nontemporal_load(a.x + i) : 0.0;
+    const double py = in ? __builtin_nontemporal_load(a.y + i) : 0.0;
+    double d = 0.0;
+    const bool c = in && poly_pass(a, px, py, T, d);
+    const uint64_t m = __ballot(c);
+    if (m == 0) continue;
+    const int leader = __ffsll((unsigned long long)m) - 1;
+    unsigned long long base = 0;
+    if (lane == leader) base = atomicAdd(&a.st->count, (unsigned long long)__popcll(m));
+    base = __shfl(base, leader, 64);
+    if (c) {
+      const unsigned long long pos = base + (unsigned long long)__popcll(m & ((1ull << lane) - 1ull));
+      if (pos < a.cap) {
+        a.cand_d[pos] = d;
+        a.cand_i[pos] = (uint32_t)i;
+        a.cand_o[pos] = a.objID[i];
+      }
+    }
+  }
+}
+
+hipError_t launch_knn_poly_sample(gf_ctx* ctx, const KnnPolyArgs& a) {
+  KTimer t(ctx, GF_K_KNN_SAMPLE);
+  hipLaunchKernelGGL(knn_poly_sample_kernel, dim3(kSampleBlocks), dim3(kBlock), 0, ctx->stream, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_knn_poly_scan(gf_ctx* ctx, const KnnPolyArgs& a, int blocks) {
+  KTimer t(ctx, GF_K_KNN_SCAN);
+  hipLaunchKernelGGL(knn_poly_scan_kernel, dim3(blocks), dim3(kBlock), 0, ctx->stream, a);
   return hipGetLastError();
 }
 

@@ -347,6 +347,29 @@ class PointPointKNNQuery(SpatialOperator):
                 _lib._lib.gf_knn_plan_destroy(p)
 
 
+class PointPolygonKNNQuery(PointPointKNNQuery):
+    """knn/PointPolygonKNNQuery.java -- continuous kNN of the window's points to one query
+    polygon within r (JTS point-polygon distance, 0 inside; approximate: the bbox distance).
+    Same run / enqueue / finish API as PointPointKNNQuery with a Polygon as the query."""
+
+    def plan(self, window_device: int, queryPolygon: Polygon, queryRadius: float, k: int):
+        ctx = _lib.context(window_device)
+        key = (ctx.device, id(queryPolygon), float(queryRadius), int(k), int(self.conf.distanceMetric),
+               bool(self.conf.isApproximateQuery()))
+        plan = self._plans.get(key)
+        if plan is None:
+            ps = PolygonSet([queryPolygon])
+            cs = ps.c_struct()
+            h = C.c_void_p()
+            st = _lib.lib().gf_knn_ppoly_plan_create(ctx.handle, C.byref(self.index.c_grid), C.byref(cs),
+                                                     float(queryRadius), int(k), int(self.conf.isApproximateQuery()),
+                                                     int(self.conf.distanceMetric), C.byref(h))
+            _lib.check(st, ctx.handle, "gf_knn_ppoly_plan_create")
+            self._plans[key] = plan = h
+            self._keep = getattr(self, "_keep", []) + [queryPolygon]
+        return ctx, plan
+
+
 def knn_merge_host(k: int, lists):
     """Top-k distinct objIDs of several sorted (objID, dist, idx) lists -- the windowAll funnel
     (KNNQuery.java:213-272) across shards; host code of the library (no GPU needed)."""

@@ -1,0 +1,93 @@
+"""GPU parity of the polygon-query kNN (PointPolygonKNNQuery, gf_knn_ppoly_plan_create) against
+the oracle's restatement (orc_knn_ppoly_contract): (objID, rank) lists, distances and indices
+bit-exact; exact JTS distance and approximate bbox distance; g > 0, g == 0 and g < 0 layer
+cases; polygons with holes, partly outside the grid; continuous windows (threshold hint) and
+the exact fallback."""
+import numpy as np
+import pytest
+
+from conftest import BEIJING, QPOINT
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def sf(gpu):
+    import spatialflink_amd
+
+    return spatialflink_amd
+
+
+def square(cx, cy, h):
+    return [(cx - h, cy - h), (cx + h, cy - h), (cx + h, cy + h), (cx - h, cy + h), (cx - h, cy - h)]
+
+
+POLYS = {
+    "square": [square(QPOINT[0], QPOINT[1], 0.01)],
+    "generated": [[(115.5, 39.6), (115.515, 39.6), (115.515, 39.615), (115.5, 39.615), (115.5, 39.6)]],
+    "holed": [[(116.30, 39.85), (116.55, 39.80), (116.50, 40.05), (116.40, 39.95), (116.32, 40.02), (116.30, 39.85)],
+              square(116.42, 39.90, 0.02)],
+    "outside": [square(115.49, 40.0, 0.03)],
+}
+
+
+def conf(sf, approximate=False, metric=0):
+    c = sf.QueryConfiguration(sf.QueryType.WindowBased)
+    c.setApproximateQuery(approximate)
+    c.distanceMetric = metric
+    return c
+
+
+def run_case(sf, oracle_mod, poly, n, r, k, approximate=False, metric=0, seed=5, grid_n=500, cap=None):
+    g = sf.UniformGrid(grid_n, *BEIJING)
+    og = oracle_mod.grid(grid_n, *BEIJING)
+    x, y = oracle_mod.java_random_points(seed, n, 115.4, 117.7, 39.5, 41.2)
+    obj = (np.random.default_rng(seed).permutation(n) % max(1, n // 2)).astype(np.int64)  # duplicates
+    P = sf.Polygon(poly, g)
+    op = sf.PointPolygonKNNQuery(conf(sf, approximate, metric), g)
+    if cap:
+        op.set_capacity(0, P, r, k, cap)
+    w = sf.PointWindow.from_numpy(x, y, obj)
+    res = op.run(w, P, r, k)
+    m, eo, ed, ei = oracle_mod.knn_ppoly(og, x, y, obj, oracle_mod.Polygons([P.rings]), r, k, approximate, metric)
+    np.testing.assert_array_equal(res.objID, eo)
+    np.testing.assert_array_equal(res.dist.view(np.int64), ed.view(np.int64))
+    np.testing.assert_array_equal(res.idx, ei)
+    return op, P, res
+
+
+@pytest.mark.parametrize("name", list(POLYS))
+@pytest.mark.parametrize("r,k", [(0.5, 50), (0.01, 20), (0.003, 7)])
+def test_polyknn_small(sf, oracle_mod, name, r, k):
+    run_case(sf, oracle_mod, POLYS[name], 300_000, r, k)
+
+
+@pytest.mark.parametrize("name,approx,metric,k", [("square", False, 0, 50), ("holed", False, 1, 120),
+                                                   ("holed", True, 0, 50), ("generated", False, 0, 1)])
+def test_polyknn_sampled(sf, oracle_mod, name, approx, metric, k):
+    """>= 1M points: the sample kernel picks the threshold."""
+    run_case(sf, oracle_mod, POLYS[name], 1_200_000, 0.5, k, approx, metric, seed=11)
+
+
+def test_polyknn_continuous_and_fallback(sf, oracle_mod):
+    g = sf.UniformGrid(500, *BEIJING)
+    og = oracle_mod.grid(500, *BEIJING)
+    P = sf.Polygon(POLYS["holed"], g)
+    op = sf.PointPolygonKNNQuery(conf(sf), g)
+    OP = oracle_mod.Polygons([P.rings])
+    for seed in (21, 22, 23):  # the hint carried from window to window
+        x, y = oracle_mod.java_random_points(seed, 1_100_000, *BEIJING)
+        obj = np.arange(len(x), dtype=np.int64)
+        res = op.run(sf.PointWindow.from_numpy(x, y, obj), P, 0.2, 60)
+        m, eo, ed, ei = oracle_mod.knn_ppoly(og, x, y, obj, OP, 0.2, 60)
+        np.testing.assert_array_equal(res.objID, eo)
+        np.testing.assert_array_equal(res.dist, ed)
+    run_case(sf, oracle_mod, POLYS["square"], 400_000, 0.5, 50, cap=64)  # every scan overflows
+
+
+def test_polyknn_rejects_pipeline_depth_2(sf, oracle_mod):
+    g = sf.UniformGrid(100, *BEIJING)
+    P = sf.Polygon(POLYS["square"], g)
+    op = sf.PointPolygonKNNQuery(conf(sf), g)
+    with pytest.raises(ValueError):
+        op.set_pipeline(0, P, 0.5, 10, 2)
