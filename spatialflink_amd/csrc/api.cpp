@@ -900,7 +900,8 @@ extern "C" void gf_knn_plan_destroy(gf_knn_plan* P) {
   }
   if (P->tmp_result) hipFree(P->tmp_result);
   if (P->host_result) hipHostFree(P->host_result);
-  for (void* q : {(void*)P->ring_off, (void*)P->vert_off, (void*)P->vx, (void*)P->vy, (void*)P->ring_env})
+  for (void* q : {(void*)P->ring_off, (void*)P->vert_off, (void*)P->vx, (void*)P->vy, (void*)P->ring_env,
+                  (void*)P->maybe_i[0], (void*)P->maybe_i[1]})
     if (q) hipFree(q);
   delete P;
 }
@@ -1092,7 +1093,21 @@ static KnnPolyArgs poly_args(gf_knn_plan* P, int j, const gf_points* pts, int64_
   for (int i = 0; i < 4; ++i) a.bbox[i] = P->bbox[i];
   a.approx = P->approx; a.r = P->r; a.k = P->k; a.use_state = use_state; a.use_hint = use_hint;
   a.st = L.st; a.cand_d = L.cand_d; a.cand_i = L.cand_i; a.cand_o = L.cand_o; a.cap = (unsigned long long)P->cap;
+  a.maybe_i = P->maybe_i[j];
   return a;
+}
+
+// the polygon scan's prefilter-survivor buffers (cap entries per lane)
+static int poly_buffers(gf_knn_plan* P) {
+  if (P->maybe_cap >= P->cap) return GF_OK;
+  GF_HIP_CHECK(P->ctx, hipStreamSynchronize(P->ctx->stream));
+  for (auto& m : P->maybe_i) {
+    if (m) hipFree(m);
+    m = nullptr;
+    GF_HIP_CHECK(P->ctx, hipMalloc(&m, sizeof(uint32_t) * (size_t)P->cap));
+  }
+  P->maybe_cap = P->cap;
+  return GF_OK;
 }
 
 // scan + select of points [begin, end) on lane j, stream-ordered
@@ -1100,6 +1115,8 @@ static int knn_scan_select(gf_knn_plan* P, int j, const gf_points* pts, int64_t 
                            int write_hint, void* result) {
   gf_ctx* ctx = P->ctx;
   if (P->poly) {
+    int st = poly_buffers(P);
+    if (st) return st;
     const KnnPolyArgs a = poly_args(P, j, pts, begin, end, use_state, 0);
     GF_HIP_CHECK(ctx, launch_knn_poly_scan(ctx, a, scan_blocks_for(P, (end - begin + 1) / 2)));
     GF_HIP_CHECK(ctx, launch_knn_select(ctx, select_args(P, j, use_state, write_hint, result, P->idx_base)));

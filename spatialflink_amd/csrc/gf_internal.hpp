@@ -85,6 +85,7 @@ struct KnnState {
   unsigned long long count;  // candidates appended (may exceed capacity)
   double hint_T;     // next window's threshold guess (2 x this window's k-th distance); 0 = none
   unsigned long long tr[4];  // GF_TRACE builds only: sample start, scan first start / last end
+  unsigned long long maybe;  // polygon queries: points past the cheap prefilter (refined next)
 };
 
 struct KnnScanArgs {
@@ -146,6 +147,7 @@ struct KnnPolyArgs {
   uint32_t* cand_i;
   int64_t* cand_o;
   unsigned long long cap;
+  uint32_t* maybe_i;    // scan -> refine: indices past the prefilter (cap entries)
 };
 
 struct KnnSelectArgs {
@@ -265,7 +267,7 @@ hipError_t launch_knn_scan(gf_ctx* ctx, const KnnScanArgs& a, int blocks, int un
 hipError_t launch_knn_select(gf_ctx* ctx, const KnnSelectArgs& a);
 
 hipError_t launch_knn_poly_sample(gf_ctx* ctx, const KnnPolyArgs& a);
-hipError_t launch_knn_poly_scan(gf_ctx* ctx, const KnnPolyArgs& a, int blocks);
+hipError_t launch_knn_poly_scan(gf_ctx* ctx, const KnnPolyArgs& a, int blocks);  // prefilter + refine
 hipError_t launch_knn_merge(gf_ctx* ctx, int32_t k, const void* records, int32_t nrec, size_t rec_stride,
                             int32_t nwin, size_t win_stride, void* result, size_t res_stride);
 // records of one merge given as a pointer list (kernel argument; the panes of a sliding window)
@@ -434,6 +436,8 @@ struct gf_knn_plan {
   double* vy = nullptr;
   double* ring_env = nullptr;
   double bbox[4] = {0, 0, 0, 0};
+  uint32_t* maybe_i[2] = {nullptr, nullptr};  // per lane, cap entries
+  int64_t maybe_cap = 0;
 };
 
 struct gf_window {

@@ -681,6 +681,7 @@ __device__ void knn_select_body(const KnnSelectArgs& a, LDS& L) {
     out.h->candidates = (int64_t)count;
     out.h->threshold = T;
     a.st->count = 0ull;  // ready for the lane's next window
+    a.st->maybe = 0ull;
     if (a.write_hint) {
       double h;
       if (status == 0) h = nres == k ? fmax(2.0 * from_bits(L.rd[k - 1]), 4.9e-324) : a.r;
@@ -887,16 +888,75 @@ __global__ __launch_bounds__(kBlock) void knn_poly_sample_kernel(KnnPolyArgs a) 
   sample_finish(a.st, lh, a.k, a.r, a.poly.metric, bbase);
 }
 
+// Scan: the cheap prefilter only (cell class + envelope) -- no call to the polygon distance in
+// the streaming loop, so the kernel keeps a streaming register footprint; survivors' indices go
+// to maybe_i (one atomic per wave) and the refine kernel computes their exact distances.
+__device__ __forceinline__ bool poly_maybe(const KnnPolyArgs& a, double px, double py, double T) {
+  if (!classify_cg(a.qr, px, py)) return false;
+  return !(px == px && py == py && env_far(a.bbox, px, py, T));
+}
+
+__device__ __forceinline__ void maybe_append(const KnnPolyArgs& a, bool c, int64_t i) {
+  const uint64_t m = __ballot(c);
+  if (m == 0) return;
+  const int lane = threadIdx.x & 63;
+  const int leader = __ffsll((unsigned long long)m) - 1;
+  unsigned long long base = 0;
+  if (lane == leader) base = atomicAdd(&a.st->maybe, (unsigned long long)__popcll(m));
+  base = __shfl(base, leader, 64);
+  if (c) {
+    const unsigned long long pos = base + (unsigned long long)__popcll(m & ((1ull << lane) - 1ull));
+    if (pos < a.cap) a.maybe_i[pos] = (uint32_t)i;
+  }
+}
+
+// Two points per lane per iteration from 16-B loads of x and y (begin is even, x / y 16-B
+// aligned), like the point scan; the odd last point in a checked tail.
 __global__ __launch_bounds__(kBlock) void knn_poly_scan_kernel(KnnPolyArgs a) {
   const double T = a.use_state ? a.st->T : a.r;
   const int lane = threadIdx.x & 63;
   const int64_t stride = (int64_t)gridDim.x * kBlock;
-  for (int64_t i = a.begin + (int64_t)blockIdx.x * kBlock + threadIdx.x; i - lane < a.end; i += stride) {
-    const bool in = i < a.end;
-    const double px = in ? __builtin_nontemporal_load(a.x + i) : 0.0;
-    const double py = in ? __builtin_nontemporal_load(a.y + i) : 0.0;
+  const int64_t pb = a.begin >> 1, pe = a.end >> 1;  // complete pairs [pb, pe)
+  for (int64_t p = pb + (int64_t)blockIdx.x * kBlock + threadIdx.x; p - lane < pe; p += stride) {
+    const bool in = p < pe;
+    dbl2 xv = {0.0, 0.0}, yv = {0.0, 0.0};
+    if (in) {
+      xv = __builtin_nontemporal_load(reinterpret_cast<const dbl2*>(a.x) + p);
+      yv = __builtin_nontemporal_load(reinterpret_cast<const dbl2*>(a.y) + p);
+    }
+    const bool c0 = in && poly_maybe(a, xv.x, yv.x, T);
+    const bool c1 = in && poly_maybe(a, xv.y, yv.y, T);
+    if (__ballot(c0 || c1) == 0) continue;  // wave-uniform
+    maybe_append(a, c0, 2 * p);
+    maybe_append(a, c1, 2 * p + 1);
+  }
+  if ((a.end & 1) && blockIdx.x == 0 && threadIdx.x < 64) {  // the odd last point, one wave
+    const int64_t i = a.end - 1;
+    maybe_append(a, lane == 0 && poly_maybe(a, a.x[i], a.y[i], T), i);
+  }
+}
+
+// Refine: exact distance of each prefilter survivor; d <= T -> (d, idx, objID) candidates.  A
+// maybe-list past capacity marks the window overflowed (count > cap) for the select.
+__global__ __launch_bounds__(kBlock) void knn_poly_refine_kernel(KnnPolyArgs a) {
+  const double T = a.use_state ? a.st->T : a.r;
+  const unsigned long long nm = a.st->maybe;
+  if (nm > a.cap) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&a.st->count, nm);
+    return;
+  }
+  const int lane = threadIdx.x & 63;
+  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  for (int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x; j - lane < (int64_t)nm; j += stride) {
+    const bool in = j < (int64_t)nm;
+    const int64_t i = in ? (int64_t)a.maybe_i[j] : 0;
     double d = 0.0;
-    const bool c = in && poly_pass(a, px, py, T, d);
+    bool c = false;
+    if (in) {
+      const double px = a.x[i], py = a.y[i];
+      d = a.approx ? point_bbox_distance(px, py, a.bbox) : polygon_distance(px, py, a.poly, 0);
+      c = d <= T;
+    }
     const uint64_t m = __ballot(c);
     if (m == 0) continue;
     const int leader = __ffsll((unsigned long long)m) - 1;
@@ -921,8 +981,11 @@ hipError_t launch_knn_poly_sample(gf_ctx* ctx, const KnnPolyArgs& a) {
 }
 
 hipError_t launch_knn_poly_scan(gf_ctx* ctx, const KnnPolyArgs& a, int blocks) {
-  KTimer t(ctx, GF_K_KNN_SCAN);
-  hipLaunchKernelGGL(knn_poly_scan_kernel, dim3(blocks), dim3(kBlock), 0, ctx->stream, a);
+  {
+    KTimer t(ctx, GF_K_KNN_SCAN);
+    hipLaunchKernelGGL(knn_poly_scan_kernel, dim3(blocks), dim3(kBlock), 0, ctx->stream, a);
+  }
+  hipLaunchKernelGGL(knn_poly_refine_kernel, dim3(256), dim3(kBlock), 0, ctx->stream, a);
   return hipGetLastError();
 }
 

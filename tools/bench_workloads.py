@@ -534,6 +534,65 @@ def bench_csv(args):
            "cpu_baseline": cpu, "verified_vs_oracle": verified})
 
 
+def bench_polyknn(args):
+    """Polygon-query kNN (PointPolygonKNNQuery.java:245-317, §8f row 4): k = 50, r = 0.5, a
+    0.02-degree square around the README query point, 500 x 500 grid, 10M points per window,
+    continuous query over a ring of distinct windows (threshold hint carried), depth 1."""
+    import torch
+
+    import spatialflink_amd as sf
+    from spatialflink_amd import _lib
+
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+
+    n = args.points or 10_000_000
+    L = _lib.lib()
+    grid = sf.UniformGrid(500, *BEIJING)
+    h = 0.01
+    ring = [(QPOINT[0] - h, QPOINT[1] - h), (QPOINT[0] + h, QPOINT[1] - h), (QPOINT[0] + h, QPOINT[1] + h),
+            (QPOINT[0] - h, QPOINT[1] + h), (QPOINT[0] - h, QPOINT[1] - h)]
+    P = sf.Polygon([ring], grid)
+    wins = _windows(sf, n, 4, 61)
+    op = sf.PointPolygonKNNQuery(sf.QueryConfiguration(sf.QueryType.WindowBased), grid)
+    ctx, plan = op.plan(0, P, args.radius, args.k)
+    recs = sf.PinnedRecords(args.warmup + args.steps, args.k)
+    pts = [w[2].c_struct() for w in wins]
+
+    def step(i):
+        _lib.check(L.gf_knn_enqueue(plan, C.byref(pts[i % 4]), C.c_void_p(recs.ptr(i))), ctx.handle, "enqueue")
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    ctx.set_timing((1 << _lib.K_KNN_SCAN) | (1 << _lib.K_KNN_SAMPLE) | (1 << _lib.K_KNN_SELECT))
+    t0 = time.perf_counter()
+    for i in range(args.warmup, args.warmup + args.steps):
+        step(i)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    sms, scnt = ctx.timing(_lib.K_KNN_SCAN)
+    pms, pcnt = ctx.timing(_lib.K_KNN_SAMPLE)
+    lms, lcnt = ctx.timing(_lib.K_KNN_SELECT)
+    ctx.set_timing(0)
+    fallbacks = sum(1 for i in range(args.warmup, args.warmup + args.steps) if recs.decode(i)[0] != 0)
+    verified = None
+    if not args.no_verify:  # the first window against the oracle
+        x, y, w = wins[args.warmup % 4]
+        st, o, d, ix = recs.decode(args.warmup)
+        m, eo, ed, ei = O.knn_ppoly(O.grid(500, *BEIJING), x, y, np.arange(n, dtype=np.int64),
+                                    O.Polygons([P.rings]), args.radius, args.k)
+        verified = bool(st == 0 and np.array_equal(o, eo) and np.array_equal(d, ed) and np.array_equal(ix, ei))
+    avg = sms / 1000.0 / max(scnt, 1)
+    _line("polygon-query kNN k=%d" % args.k, n * args.steps / elapsed, "points/s", args.steps, args.warmup, elapsed,
+          "knn_poly_scan", 16.0 * n, avg,
+          {"config": {"workload": f"knn_ppoly_k{args.k}_r{args.radius}_{n // 1_000_000}Mpts_grid500_square0.02",
+                      "points_per_window": n, "k": args.k, "radius": args.radius},
+           "breakdown": {"scan_us": round(avg * 1e6, 2), "sample_us": round(1000 * pms / max(pcnt, 1), 2),
+                         "select_us": round(1000 * lms / max(lcnt, 1), 2)},
+           "fallback_windows": fallbacks, "verified_vs_oracle": verified})
+
+
 def run(args):
     if args.workload in ("range", "ppoly"):
         bench_range(args, polygons=args.workload == "ppoly")
@@ -543,5 +602,7 @@ def run(args):
         bench_sliding(args)
     elif args.workload == "csv":
         bench_csv(args)
+    elif args.workload == "polyknn":
+        bench_polyknn(args)
     else:
         raise SystemExit(f"unknown workload {args.workload}")
