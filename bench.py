@@ -65,7 +65,8 @@ def main():
                     help="N > 1: windows whose top-k records share one RCCL all-gather + one merge launch")
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                     help="gloo: rehearse the N > 1 path with several ranks on one GPU (not a benchmark)")
-    ap.add_argument("--pipeline", type=int, default=2, choices=(1, 2),
+    ap.add_argument("--scan-blocks", type=int, default=0, help="kNN scan grid (0 = auto: 4 blocks per CU)")
+    ap.add_argument("--pipeline", type=int, default=2, choices=(1, 2, 3),
                     help="windows in flight: 2 overlaps window i's select with window i+1's scan")
     args = ap.parse_args()
     if args.workload != "knn":
@@ -125,7 +126,11 @@ def main():
     ctx, plan = op.plan(dev.index, q, args.radius, args.k)
     _lib.check(_lib.lib().gf_knn_plan_set_index_base(plan, rank * n), ctx.handle, "index base")
     _lib.check(_lib.lib().gf_knn_plan_set_pipeline(plan, args.pipeline), ctx.handle, "pipeline")
-    lag = args.pipeline - 1  # depth 2: window i's record is written by enqueue i+1 (or the flush)
+    if args.scan_blocks:
+        _lib.check(_lib.lib().gf_knn_plan_set_tuning(plan, args.scan_blocks, 1, 1), ctx.handle, "tuning")
+    lag = args.pipeline - 1  # depth d: window i's record is written by enqueue i+d-1 (or the flush)
+    if world > 1 and args.pipeline == 3:
+        raise SystemExit("--pipeline 3 is single-GPU only (the exchange runs on the context stream)")
     rb = knn_record_bytes(args.k)
     B = max(1, args.exchange_batch)
     slots = torch.zeros(2, B, rb, dtype=torch.uint8, device=dev)  # two groups of B device records
@@ -294,7 +299,7 @@ def main():
     if rank == 0:  # HBM bytes per launch from the committed rocprofv3 PMC pass of this command
         import glob
 
-        kname = "knn_fused" if args.pipeline == 2 else "knn_scan"
+        kname = "knn_fused" if args.pipeline >= 2 else "knn_scan"
         for f in sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{kname}_pmc.json")), reverse=True):
             with open(f) as fh:
                 pm = json.load(fh)
@@ -338,7 +343,7 @@ def main():
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": "knn_fused (scan of window i + select of window i-1 in block 0)" if args.pipeline == 2
+                "kernel": "knn_fused (scan of window i + select of window i-1 in block 0)" if args.pipeline >= 2
                 else "knn_scan",
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS,

@@ -194,7 +194,11 @@ int    gf_knn_plan_set_index_base(gf_knn_plan* plan, int64_t base);
  * or by gf_knn_plan_flush (stream-ordered on the context stream).  No sample kernel: a cold
  * or failed hint flags the window (status 1, re-evaluated exactly by gf_knn_decode) and the
  * threshold adapts (shrinks after an overflow, doubles when fewer than k lie below it).
- * Results are identical at either depth. */
+ * depth 3 (k <= 256): window i's fused launch selects window i-2; odd windows launch on a
+ * second (non-blocking) stream, so consecutive launches overlap.  Window buffers must be
+ * complete before their enqueue (no cross-stream wait is inserted); gf_knn_plan_flush joins
+ * the second stream back into the context stream.  The sliding engine rejects depth 3.
+ * Results are identical at every depth. */
 int    gf_knn_plan_set_pipeline(gf_knn_plan* plan, int depth);
 int    gf_knn_plan_flush(gf_knn_plan* plan);
 /* Result record: gf_knn_header followed by double dist[k], int64 objID[k], int64 idx[k]. */

@@ -244,6 +244,10 @@ extern "C" void gf_ctx_destroy(gf_ctx* ctx) {
   if (ctx->scratch) hipFree(ctx->scratch);
   if (ctx->pinned) hipHostFree(ctx->pinned);
   if (ctx->own_stream) hipStreamDestroy(ctx->own_stream);
+  if (ctx->aux) {
+    hipStreamSynchronize(ctx->aux);
+    hipStreamDestroy(ctx->aux);
+  }
   delete ctx;
 }
 
@@ -257,6 +261,7 @@ extern "C" void* gf_ctx_stream(gf_ctx* ctx) { return ctx ? (void*)ctx->stream : 
 extern "C" int gf_ctx_synchronize(gf_ctx* ctx) {
   if (!ctx) return GF_ERR_ARG;
   GF_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+  if (ctx->aux) GF_HIP_CHECK(ctx, hipStreamSynchronize(ctx->aux));
   return GF_OK;
 }
 
@@ -286,6 +291,7 @@ extern "C" int gf_ctx_timing(gf_ctx* ctx, int kid, double* total_ms, int64_t* la
   int st = bind(ctx);
   if (st) return st;
   GF_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+  if (ctx->aux) GF_HIP_CHECK(ctx, hipStreamSynchronize(ctx->aux));
   for (auto& e : ctx->pending) {
     float ms = 0.f;
     if (hipEventElapsedTime(&ms, e.a, e.b) == hipSuccess) {
@@ -927,7 +933,7 @@ static int knn_alloc_lane(gf_knn_plan* P, int j, int64_t cap) {
 
 static int knn_alloc_candidates(gf_knn_plan* P, int64_t cap) {
   int st;
-  for (int j = 0; j < 2; ++j)  // lane 1 only once pipelining allocated it
+  for (int j = 0; j < 4; ++j)  // lanes 1.. only once pipelining allocated them
     if ((j == 0 || P->lane[j].st) && (st = knn_alloc_lane(P, j, cap))) return st;
   P->cap = cap;
   return GF_OK;
@@ -1155,6 +1161,38 @@ int gf::knn_enqueue_merge(gf_knn_plan* P, const gf_points* pts, void* result, co
   if (st) return st;
   if ((st = check_points(ctx, pts))) return st;
   if (pts->n > 0 && !pts->objID) return set_err(ctx, GF_ERR_ARG, "kNN needs objID");
+  if (P->pipeline == 3) {
+    // window k scans on lane k % 4 and selects window k-2 in block 0; odd windows launch on the
+    // aux stream, so consecutive windows' kernels overlap (ramp-up of one under the tail of the
+    // other) while every dependency -- window k-2's candidates, lane k % 4's last select (in
+    // kernel k-2) and its hint -- stays on the same stream.  Window buffers must be complete
+    // when enqueued (no cross-stream wait is inserted for them).
+    const uint64_t kseq = P->seq++;
+    const int j = (int)(kseq & 3);
+    hipStream_t main = ctx->stream;
+    ctx->stream = (kseq & 1) ? ctx->aux : main;
+    int rc = GF_OK;
+    do {
+      const bool sample = pts->n >= kSampleMinN && (!P->use_hint || !P->lane_warm3[j]);
+      if (sample && (rc = knn_launch_sample(P, j, pts, 0))) break;
+      P->lane_warm3[j] = 1;
+      const KnnScanArgs s = scan_args(P, j, pts, 0, pts->n, sample ? 2 : 1);
+      KnnSelectArgs q{};
+      int has_prev = 0;
+      if (P->npq > 0 && P->pq[0].seq + 2 == kseq) {
+        const gf_knn_plan::Pend e = P->pq[0];
+        q = select_args(P, e.lane, 1, P->use_hint, e.result, e.idx_base);
+        has_prev = 1;
+        P->pq[0] = P->pq[1];
+        --P->npq;
+      }
+      hipError_t he = launch_knn_fused(ctx, s, q, has_prev, scan_blocks_for(P, pts->n), P->scan_nt, merge);
+      if (he != hipSuccess) { rc = hip_err(ctx, he, "launch_knn_fused"); break; }
+      P->pq[P->npq++] = gf_knn_plan::Pend{j, result, P->idx_base, kseq};
+    } while (0);
+    ctx->stream = main;
+    return rc;
+  }
   if (P->pipeline == 2) {
     // one fused launch: scan this window on lane j (threshold = the lane's hint), select the
     // pending previous window on the other lane in block 0
@@ -1185,6 +1223,27 @@ int gf::knn_enqueue_merge(gf_knn_plan* P, const gf_points* pts, void* result, co
 
 extern "C" int gf_knn_plan_flush(gf_knn_plan* P) {
   if (!P) return GF_ERR_ARG;
+  if (P->pipeline == 3) {
+    if (P->npq == 0) return GF_OK;
+    gf_ctx* ctx = P->ctx;
+    int st = bind(ctx);
+    if (st) return st;
+    hipStream_t main = ctx->stream;
+    for (int e = 0; e < P->npq; ++e) {
+      const gf_knn_plan::Pend& w = P->pq[e];
+      ctx->stream = (w.seq & 1) ? ctx->aux : main;
+      hipError_t he = launch_knn_select(ctx, select_args(P, w.lane, 1, P->use_hint, w.result, w.idx_base));
+      ctx->stream = main;
+      if (he != hipSuccess) return hip_err(ctx, he, "launch_knn_select");
+    }
+    P->npq = 0;
+    // every window of the plan is complete in the context stream's order from here on
+    hipEvent_t ev = take_event(ctx);
+    GF_HIP_CHECK(ctx, hipEventRecord(ev, ctx->aux));
+    GF_HIP_CHECK(ctx, hipStreamWaitEvent(main, ev, 0));
+    ctx->pool.push_back(ev);
+    return GF_OK;
+  }
   if (P->pend_lane < 0) return GF_OK;
   gf_ctx* ctx = P->ctx;
   int st = bind(ctx);
@@ -1197,19 +1256,24 @@ extern "C" int gf_knn_plan_flush(gf_knn_plan* P) {
 }
 
 extern "C" int gf_knn_plan_set_pipeline(gf_knn_plan* P, int depth) {
-  if (!P || depth < 1 || depth > 2) return GF_ERR_ARG;
+  if (!P || depth < 1 || depth > 3) return GF_ERR_ARG;
   gf_ctx* ctx = P->ctx;
-  if (depth == 2 && P->k > 256)
-    return set_err(ctx, GF_ERR_ARG, "gf_knn_plan_set_pipeline: depth 2 needs k <= 256");
-  if (depth == 2 && P->poly)
+  if (depth >= 2 && P->k > 256)
+    return set_err(ctx, GF_ERR_ARG, "gf_knn_plan_set_pipeline: depth 2 / 3 needs k <= 256");
+  if (depth >= 2 && P->poly)
     return set_err(ctx, GF_ERR_ARG, "gf_knn_plan_set_pipeline: polygon queries run at depth 1");
   int st = bind(ctx);
   if (st || (st = gf_knn_plan_flush(P))) return st;
   GF_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
-  if (depth == 2 && !P->lane[1].st && (st = knn_alloc_lane(P, 1, P->cap))) return st;
+  if (ctx->aux) GF_HIP_CHECK(ctx, hipStreamSynchronize(ctx->aux));
+  for (int j = 1; j < (depth == 3 ? 4 : depth); ++j)
+    if (!P->lane[j].st && (st = knn_alloc_lane(P, j, P->cap))) return st;
+  if (depth == 3 && !ctx->aux) GF_HIP_CHECK(ctx, hipStreamCreateWithFlags(&ctx->aux, hipStreamNonBlocking));
   P->pipeline = depth;
   P->seq = 0;
   P->lane_warm[0] = P->lane_warm[1] = 0;
+  for (int& w : P->lane_warm3) w = 0;
+  P->npq = 0;
   return GF_OK;
 }
 

@@ -33,6 +33,7 @@ struct gf_ctx {
   size_t pinned_bytes = 0;
   int num_cus = 256;
   int join_legacy = 0;  // testing: force the original (unbucketed) join probe
+  hipStream_t aux = nullptr;  // kNN depth 3: odd windows' launches (created on first use)
 };
 
 namespace gf {
@@ -413,7 +414,7 @@ struct gf_knn_plan {
     double* cand_d = nullptr;
     uint32_t* cand_i = nullptr;
     int64_t* cand_o = nullptr;
-  } lane[2];
+  } lane[4];  // depth 3 uses four
   int64_t cap = 0;
   int pipeline = 1;               // 1: sample -> scan -> select per window; 2: fused
   uint64_t seq = 0;
@@ -421,6 +422,16 @@ struct gf_knn_plan {
   int lane_warm[2] = {0, 0};      // depth 2: the lane has a hint from an earlier window
   void* pend_result = nullptr;
   int64_t pend_idx_base = 0;      // depth 2: idx_base of the pending window (set at its enqueue)
+  // depth 3: windows whose select has not run yet (seq k-1, k-2), oldest first
+  struct Pend {
+    int lane;
+    void* result;
+    int64_t idx_base;
+    uint64_t seq;
+  };
+  Pend pq[2];
+  int npq = 0;
+  int lane_warm3[4] = {0, 0, 0, 0};
   int use_hint = 1;             // reuse the previous window's k-th distance as the threshold guess
   int64_t idx_base = 0;
   void* tmp_result = nullptr;   // device record used by gf_knn_run / fallback

@@ -142,6 +142,7 @@ extern "C" int gf_knn_sliding_push(gf_knn_sliding* s, int64_t pane_index, const 
   if (s->started && pane_index != s->last + 1)
     return set_err(ctx, GF_ERR_ARG, "gf_knn_sliding_push: panes must be pushed consecutively (empty panes with n = 0)");
   if (pane->n < 0) return set_err(ctx, GF_ERR_ARG, "gf_knn_sliding_push: negative n");
+  if (P->pipeline > 2) return set_err(ctx, GF_ERR_ARG, "gf_knn_sliding_push: the pane engine runs at pipeline depth <= 2");
   int st = bind(ctx);
   if (st) return st;
   gf_knn_sliding::Pane& pn = slot(s, pane_index);

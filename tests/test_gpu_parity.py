@@ -563,9 +563,10 @@ def test_knn_pinned_records_async(sf, oracle_mod):
         check_knn(res, oo, od, oi)
 
 
-@pytest.mark.parametrize("k", [50, 120])
-def test_knn_pipelined(sf, oracle_mod, k):
-    """Depth-2 pipeline: window i's select runs inside window i+1's fused scan kernel; cold
+@pytest.mark.parametrize("k,depth", [(50, 2), (120, 2), (50, 3), (120, 3)])
+def test_knn_pipelined(sf, oracle_mod, k, depth):
+    """Depth-2 pipeline: window i's select runs inside window i+1's fused scan kernel (depth 3:
+    inside window i+2's, odd windows on a second stream); cold
     starts and a window whose carried hint is too small are re-evaluated at decode; the
     synchronous API on a pipelined plan."""
     import torch
@@ -587,7 +588,7 @@ def test_knn_pipelined(sf, oracle_mod, k):
         if seed == 23:  # trajectories: every objID three times
             obj %= len(x) // 3
         data.append((x, y, obj, win(sf, x, y, obj)))
-    op.set_pipeline(0, q, 0.5, k, 2)
+    op.set_pipeline(0, q, 0.5, k, depth)
     order = [0, 1, 0, 1, 3, 4, 2, 3, 4, 0, 2, 2, 1]
     rec = sf.PinnedRecords(len(order), k)
     for i, j in enumerate(order):
@@ -644,3 +645,35 @@ def test_knn_merge_dev_batch(sf, oracle_mod, layout):
         np.testing.assert_array_equal(o, eo)
         np.testing.assert_array_equal(d, ed)
         np.testing.assert_array_equal(i, ei)
+
+
+def test_join_dense_spot_and_capacity(sf, oracle_mod):
+    """Many pairs per point around a dense spot == the oracle; a too-small capacity returns
+    GF_ERR_CAPACITY with the exact count."""
+    import ctypes as C
+
+    import torch
+
+    from spatialflink_amd import _lib
+
+    g = sf.UniformGrid(1000, *BEIJING)
+    og = oracle_mod.grid(1000, *BEIJING)
+    x, y = oracle_mod.java_random_points(71, 600_000, *BEIJING)
+    qx, qy = oracle_mod.java_random_points(72, 60_000, *BEIJING)
+    # a dense spot: many pairs per point (more than the LDS pair slots)
+    qx[:2000] = 116.4 + 1e-5 * np.arange(2000) % 3e-4
+    qy[:2000] = 40.0
+    x[:3000] = 116.4001
+    y[:3000] = 40.0
+    st, exp = oracle_mod.join_pp(og, og, x, y, qx, qy, 0.001)
+    exp = exp[np.lexsort((exp[:, 1], exp[:, 0]))]
+    op = sf.PointPointJoinQuery(conf(sf), g)
+    ctx = _lib.context(0)
+    wo, wq = win(sf, x, y), win(sf, qx, qy)
+    np.testing.assert_array_equal(op.run(wo, wq, 0.001), exp)
+    pairs = torch.empty(2 * 100, dtype=torch.int32, device="cuda")
+    n = C.c_int64()
+    po, pq = wo.c_struct(), wq.c_struct()
+    st = _lib.lib().gf_join_pp(ctx.handle, C.byref(g.c_grid), C.byref(g.c_grid), C.byref(po), C.byref(pq), 0.001, 0, 0,
+                               pairs.data_ptr(), 100, C.byref(n))
+    assert st == _lib.GF_ERR_CAPACITY and n.value == len(exp)
