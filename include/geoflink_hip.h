@@ -101,6 +101,9 @@ void        gf_ctx_destroy(gf_ctx* ctx);
 int         gf_ctx_set_stream(gf_ctx* ctx, void* hip_stream);
 void*       gf_ctx_stream(gf_ctx* ctx);
 int         gf_ctx_synchronize(gf_ctx* ctx);
+/* Make the context stream wait for everything enqueued so far on the context's second stream
+ * (kNN pipeline depth 3 launches odd windows there); no-op when it has none.  Host does not block. */
+int         gf_ctx_join(gf_ctx* ctx);
 const char* gf_ctx_last_error(gf_ctx* ctx);
 /* Context flags (testing / tuning).  GF_FLAG_JOIN_LEGACY: 1 = gf_join_pp probes the query
  * buckets from global memory in input order instead of the row-bucketed LDS path. */

@@ -258,6 +258,18 @@ extern "C" int gf_ctx_set_stream(gf_ctx* ctx, void* s) {
 }
 extern "C" void* gf_ctx_stream(gf_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
 
+extern "C" int gf_ctx_join(gf_ctx* ctx) {
+  if (!ctx) return GF_ERR_ARG;
+  if (!ctx->aux) return GF_OK;
+  int st = bind(ctx);
+  if (st) return st;
+  hipEvent_t ev = take_event(ctx);
+  GF_HIP_CHECK(ctx, hipEventRecord(ev, ctx->aux));
+  GF_HIP_CHECK(ctx, hipStreamWaitEvent(ctx->stream, ev, 0));
+  ctx->pool.push_back(ev);
+  return GF_OK;
+}
+
 extern "C" int gf_ctx_synchronize(gf_ctx* ctx) {
   if (!ctx) return GF_ERR_ARG;
   GF_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
@@ -1173,9 +1185,9 @@ int gf::knn_enqueue_merge(gf_knn_plan* P, const gf_points* pts, void* result, co
     ctx->stream = (kseq & 1) ? ctx->aux : main;
     int rc = GF_OK;
     do {
-      const bool sample = pts->n >= kSampleMinN && (!P->use_hint || !P->lane_warm3[j]);
+      const bool sample = pts->n >= kSampleMinN && (!P->use_hint || !P->lane_warm[j]);
       if (sample && (rc = knn_launch_sample(P, j, pts, 0))) break;
-      P->lane_warm3[j] = 1;
+      P->lane_warm[j] = 1;
       const KnnScanArgs s = scan_args(P, j, pts, 0, pts->n, sample ? 2 : 1);
       KnnSelectArgs q{};
       int has_prev = 0;
@@ -1238,11 +1250,7 @@ extern "C" int gf_knn_plan_flush(gf_knn_plan* P) {
     }
     P->npq = 0;
     // every window of the plan is complete in the context stream's order from here on
-    hipEvent_t ev = take_event(ctx);
-    GF_HIP_CHECK(ctx, hipEventRecord(ev, ctx->aux));
-    GF_HIP_CHECK(ctx, hipStreamWaitEvent(main, ev, 0));
-    ctx->pool.push_back(ev);
-    return GF_OK;
+    return gf_ctx_join(ctx);
   }
   if (P->pend_lane < 0) return GF_OK;
   gf_ctx* ctx = P->ctx;
@@ -1271,8 +1279,7 @@ extern "C" int gf_knn_plan_set_pipeline(gf_knn_plan* P, int depth) {
   if (depth == 3 && !ctx->aux) GF_HIP_CHECK(ctx, hipStreamCreateWithFlags(&ctx->aux, hipStreamNonBlocking));
   P->pipeline = depth;
   P->seq = 0;
-  P->lane_warm[0] = P->lane_warm[1] = 0;
-  for (int& w : P->lane_warm3) w = 0;
+  for (int& w : P->lane_warm) w = 0;
   P->npq = 0;
   return GF_OK;
 }
@@ -1286,7 +1293,7 @@ extern "C" int gf_knn_plan_set_hint(gf_knn_plan* P, int enable) {
   GF_HIP_CHECK(P->ctx, hipStreamSynchronize(P->ctx->stream));
   for (auto& L : P->lane)
     if (L.st) GF_HIP_CHECK(P->ctx, hipMemset(&L.st->hint_T, 0, sizeof(double)));
-  P->lane_warm[0] = P->lane_warm[1] = 0;
+  for (int& w : P->lane_warm) w = 0;
   return GF_OK;
 }
 

@@ -419,7 +419,7 @@ struct gf_knn_plan {
   int pipeline = 1;               // 1: sample -> scan -> select per window; 2: fused
   uint64_t seq = 0;
   int pend_lane = -1;             // depth 2: the window whose select has not run yet
-  int lane_warm[2] = {0, 0};      // depth 2: the lane has a hint from an earlier window
+  int lane_warm[4] = {0, 0, 0, 0};  // depth 2 / 3: the lane has a hint from an earlier window
   void* pend_result = nullptr;
   int64_t pend_idx_base = 0;      // depth 2: idx_base of the pending window (set at its enqueue)
   // depth 3: windows whose select has not run yet (seq k-1, k-2), oldest first
@@ -431,7 +431,6 @@ struct gf_knn_plan {
   };
   Pend pq[2];
   int npq = 0;
-  int lane_warm3[4] = {0, 0, 0, 0};
   int use_hint = 1;             // reuse the previous window's k-th distance as the threshold guess
   int64_t idx_base = 0;
   void* tmp_result = nullptr;   // device record used by gf_knn_run / fallback

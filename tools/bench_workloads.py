@@ -243,7 +243,8 @@ def bench_sliding(args):
     q = sf.Point("q", QPOINT[0], QPOINT[1], 0, grid)
     op = sf.PointPointKNNQuery(conf, grid)
     ctx, plan = op.plan(dev, q, args.radius, k)
-    _lib.check(L.gf_knn_plan_set_pipeline(plan, args.pipeline), ctx.handle, "pipeline")
+    depth = min(args.pipeline, 2)  # the pane engine runs at depth <= 2
+    _lib.check(L.gf_knn_plan_set_pipeline(plan, depth), ctx.handle, "pipeline")
     size_ms, slide_ms = 2000, 1000
     eng = C.c_void_p()
     _lib.check(L.gf_knn_sliding_create(plan, size_ms, slide_ms, C.byref(eng)), ctx.handle, "sliding")
@@ -255,7 +256,7 @@ def bench_sliding(args):
     out = merged if world > 1 else sf.PinnedRecords(total, k)
     pts = [p.c_struct() for p in panes]
     closed, wend = C.c_int32(), C.c_int64()
-    lag = 1 if args.pipeline == 2 else 0
+    lag = 1 if depth == 2 else 0
     push = L.gf_knn_sliding_push
 
     def exchange(lo, hi):  # windows [lo, hi]: one all-gather + one merge launch
@@ -407,7 +408,7 @@ def bench_sliding(args):
                      "device-resident panes cycled",
              "config": {"workload": f"sliding_knn_k{k}_r{args.radius}_{window_pts // 1_000_000}Mpts_grid{grid_n}",
                         "window_points": window_pts, "size_over_slide": W, "pane_points_per_gpu": pane_pts,
-                        "k": k, "radius": args.radius, "grid": grid_n, "windows_in_flight": args.pipeline,
+                        "k": k, "radius": args.radius, "grid": grid_n, "windows_in_flight": depth,
                         "parallelism": f"cell-column shards x{world}" + (" + RCCL all-gather top-k" if world > 1 else ""),
                         "exchange_batch": B if world > 1 else None},
              "roofline": {"bound": "hbm", "kernel": "knn_fused (scan of pane i + select of pane i-1)",
