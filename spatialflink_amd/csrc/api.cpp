@@ -1462,10 +1462,9 @@ extern "C" int gf_join_pp(gf_ctx* ctx, const gf_grid* ugrid, const gf_grid* qgri
   const int64_t mat = rowpath ? qn * sblocks : 1;
   size_t o_rmat = ar.take<uint32_t>(mat), o_rmats = ar.take<uint32_t>(mat + 1), o_roff = ar.take<uint32_t>(qn + 1);
   size_t o_rtask = ar.take<uint32_t>(qn), o_toff = ar.take<uint32_t>(qn + 1);
-  size_t o_tcnt = ar.take<uint32_t>(rowpath ? max_tasks : 1), o_tpo = ar.take<uint32_t>(rowpath ? max_tasks + 1 : 1);
-  size_t o_btmp = ar.take<uint32_t>(std::max(scan_tmp_elems(mat), scan_tmp_elems(max_tasks)));
+  size_t o_gcnt = ar.take<unsigned long long>(1);
+  size_t o_btmp = ar.take<uint32_t>(std::max(scan_tmp_elems(mat), scan_tmp_elems(qn)));
   size_t o_soxy = ar.take<double>(rowpath ? 2 * no : 1), o_soidx = ar.take<uint32_t>(rowpath ? no : 1);
-  size_t o_pcnt = ar.take<uint8_t>(rowpath ? no : 1);
   char* base = (char*)ctx_scratch(ctx, ar.off, &st);
   if (st) return st;
   auto U32 = [&](size_t o) { return (uint32_t*)(base + o); };
@@ -1491,26 +1490,24 @@ extern "C" int gf_join_pp(gf_ctx* ctx, const gf_grid* ugrid, const gf_grid* qgri
     j.row_mat = R32(o_rmat); j.row_mat_scan = R32(o_rmats); j.row_off_w = R32(o_roff); j.row_off = R32(o_roff);
     j.row_tasks = R32(o_rtask);
     j.task_off = R32(o_toff); j.soxy = (double*)(base + o_soxy); j.soidx = R32(o_soidx);
-    j.pcnt = (uint8_t*)(base + o_pcnt);
-    j.task_cnt = R32(o_tcnt); j.task_pair_off = R32(o_tpo); j.pairs = pairs;
+    j.gcount = (unsigned long long*)(base + o_gcnt);
+    j.pairs = pairs;
+    j.cap = pairs ? (uint64_t)cap : 0;
+    j.pairs_aligned = ((uintptr_t)pairs & 7) == 0;
     j.lds_budget = kJoinLdsBudget;
+    GF_HIP_CHECK(ctx, hipMemsetAsync(j.gcount, 0, sizeof(unsigned long long), s));
     GF_HIP_CHECK(ctx, launch_join_rows(ctx, j, 0, sblocks));
     GF_HIP_CHECK(ctx, launch_exclusive_scan(s, j.row_mat, mat, j.row_mat_scan, R32(o_btmp)));
     GF_HIP_CHECK(ctx, launch_join_rows(ctx, j, 1, sblocks));
     GF_HIP_CHECK(ctx, launch_join_rows(ctx, j, 2, sblocks));
     GF_HIP_CHECK(ctx, launch_exclusive_scan(s, j.row_tasks, qn, R32(o_toff), R32(o_btmp)));
-    const int pblocks = (int)max_tasks;
-    GF_HIP_CHECK(ctx, launch_join_rows(ctx, j, 3, pblocks));
-    GF_HIP_CHECK(ctx, launch_exclusive_scan(s, j.task_cnt, max_tasks, R32(o_tpo), R32(o_btmp)));
-    uint32_t total = 0;
-    GF_HIP_CHECK(ctx, hipMemcpyAsync(&total, R32(o_tpo) + max_tasks, sizeof total, hipMemcpyDeviceToHost, s));
+    // one pass: pairs are stored as they are found (past `cap` only counted)
+    GF_HIP_CHECK(ctx, launch_join_rows(ctx, j, 3, (int)max_tasks));
+    unsigned long long total = 0;
+    GF_HIP_CHECK(ctx, hipMemcpyAsync(&total, j.gcount, sizeof total, hipMemcpyDeviceToHost, s));
     GF_HIP_CHECK(ctx, hipStreamSynchronize(s));
-    *npairs = total;
-    if ((int64_t)total > cap) return GF_ERR_CAPACITY;
-    if (total == 0) return GF_OK;
-    if (!pairs) return set_err(ctx, GF_ERR_ARG, "null pairs");
-    GF_HIP_CHECK(ctx, launch_join_rows(ctx, j, 4, pblocks));
-    GF_HIP_CHECK(ctx, hipStreamSynchronize(s));
+    *npairs = (int64_t)total;
+    if ((int64_t)total > cap || (total > 0 && !pairs)) return GF_ERR_CAPACITY;
     return GF_OK;
   }
   JoinArgs a{};

@@ -347,12 +347,17 @@ struct JoinRowArgs {
   const uint32_t* task_off; // [qn+1]
   double* soxy;             // [2*no] row-bucketed ordinary xy
   uint32_t* soidx;          // [no]
-  uint8_t* pcnt;            // [no] count pass: pairs per bucketed point (255 = saturated)
-  uint32_t* task_cnt;       // count pass: pairs per task
-  const uint32_t* task_pair_off;  // write pass: output offset per task
-  uint32_t* pairs;
+  unsigned long long* gcount;  // pairs found (one atomic per probe round)
+  uint32_t* pairs;          // [2 * cap] (ordinary idx, query idx)
+  uint64_t cap;
+  int pairs_aligned;        // pairs is 8-byte aligned: one 8-byte store per pair
   int lds_budget;
 };
+constexpr int kJoinReg = 3;  // pairs per ordinary point kept in registers by the probe
+// LDS bytes of one staged query row with m points: u16 bucket offsets, xy, query indices
+__host__ __device__ inline size_t join_row_lds_bytes(int64_t W, uint32_t m) {
+  return ((size_t)(W + 1) * 2 + 15) / 16 * 16 + (size_t)m * 16 + ((size_t)m * 4 + 15) / 16 * 16;
+}
 hipError_t launch_join_rows(gf_ctx* ctx, const JoinRowArgs& a, int stage, int blocks);
 
 }  // namespace gf

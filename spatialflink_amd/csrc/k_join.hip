@@ -170,7 +170,10 @@ constexpr int kRowMax = 8192;  // rows staged as LDS histograms by the bucketing
 #ifndef GF_JOIN_BATCH
 #define GF_JOIN_BATCH 4
 #endif
-constexpr int kJoinBatch = GF_JOIN_BATCH;  // candidates of one row loaded together in the probe
+constexpr int kJoinBatch = GF_JOIN_BATCH;
+#ifndef GF_JOIN_PTS
+#define GF_JOIN_PTS 1  // ordinary points per thread per probe round (one output reservation)
+#endif  // candidates of one row loaded together in the probe
 
 // Bucketing: block b owns the contiguous input chunk b; its row histogram goes to column b of
 // the row-major matrix M[row][block] (plain stores).  The exclusive scan of M (flattened) is
@@ -282,23 +285,25 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* total,
 
 // View of one staged query row: bucket kx (0..W-1) holds points [off(kx), off(kx+1)).
 // LDS mode: u16 bucket offsets relative to gbase at byte offset loff of the dynamic LDS, the
-// row's xy pairs at byte offset lxy (offsets, not pointers, so the loads stay ds_read).
+// row's xy pairs at byte offset lxy and its query indices at lidx (offsets, not pointers, so
+// the loads stay ds_read).
 struct QRow {
   int32_t ry;      // clamped row index in [-1, qn]
   uint32_t gbase;  // global index of the row's first point (sorted query arrays)
-  uint32_t loff;
+  uint32_t loff;   // 0xffffffff: the row is read from global memory
   uint32_t lxy;
+  uint32_t lidx;
 };
 
-// Candidates of ordinary point (px, py) in cell (cx, cy) among the staged rows.  EMIT writes
-// its pairs from `pos`; returns the number of pairs.
-template <bool EMIT>
+// Candidates of ordinary point (px, py) in cell (cx, cy) among the staged rows: calls
+// hit(query index) for every pair, in a fixed order; returns the number of pairs.
+// EXACT0: the plan is exact with metric 0 (squared-distance prefilter only, no hypot code).
+template <bool EXACT0, class Hit>
 __device__ __forceinline__ uint32_t join_row_point(const JoinRowArgs& a, const char* lds, const QRow* rows, int nrows,
-                                                   double px, double py, int32_t cx, int32_t cy, uint32_t pidx,
-                                                   uint64_t pos) {
+                                                   double px, double py, int32_t cx, int32_t cy, Hit&& hit) {
   const int32_t W = a.qn + 2, c = (int32_t)a.c, qn = a.qn;
   const int32_t kb = (cx - c < -1 ? -1 : cx - c) + 1, ke = (cx + c > qn ? qn : cx + c) + 2;
-  const bool fast_ok = !a.approx && a.metric == 0;
+  const bool fast_ok = EXACT0;
   uint32_t cnt = 0;
   for (int j = 0; j < nrows; ++j) {
     const QRow R = rows[j];
@@ -316,6 +321,7 @@ __device__ __forceinline__ uint32_t join_row_point(const JoinRowArgs& a, const c
     if (fast_ok && in_lds && !brow && te > tb && tb >= t_lo && te <= t_hi) {
       // interior LDS run: kJoinBatch candidates loaded together (independent ds_read_b128)
       const double2* lxy = reinterpret_cast<const double2*>(lds + R.lxy);
+      const uint32_t* lix = reinterpret_cast<const uint32_t*>(lds + R.lidx);
       for (; t < te; t += kJoinBatch) {
         double2 q[kJoinBatch];
 #pragma unroll
@@ -324,10 +330,7 @@ __device__ __forceinline__ uint32_t join_row_point(const JoinRowArgs& a, const c
         for (int k = 0; k < kJoinBatch; ++k) {
           const double dx = px - q[k].x, dy = py - q[k].y;
           if (t + k < te && dx * dx + dy * dy <= a.s_r) {  // s <= smax(r) <=> sqrt(s) <= r
-            if (EMIT) {
-              a.pairs[2 * (pos + cnt)] = pidx;
-              a.pairs[2 * (pos + cnt) + 1] = a.sqidx[R.gbase + t + k];
-            }
+            hit(lix[t + k]);
             ++cnt;
           }
         }
@@ -340,7 +343,7 @@ __device__ __forceinline__ uint32_t join_row_point(const JoinRowArgs& a, const c
         const int64_t ddx = (int64_t)a.sqcx[gi] - cx, ddy = (int64_t)a.sqcy[gi] - cy;
         if (ddx > c || ddx < -c || ddy > c || ddy < -c) continue;
       }
-      if (!a.approx) {
+      if (EXACT0 || !a.approx) {
         double qx, qy;
         if (in_lds) {
           const double2 q = reinterpret_cast<const double2*>(lds + R.lxy)[t];
@@ -349,34 +352,43 @@ __device__ __forceinline__ uint32_t join_row_point(const JoinRowArgs& a, const c
           qx = a.sqx[gi]; qy = a.sqy[gi];
         }
         const double dx = px - qx, dy = py - qy;
-        if (a.metric == 0 ? !(dx * dx + dy * dy <= a.s_r) : !(fdlibm_hypot(dx, dy) <= a.r)) continue;
+        if (EXACT0 || a.metric == 0 ? !(dx * dx + dy * dy <= a.s_r) : !(fdlibm_hypot(dx, dy) <= a.r)) continue;
       }
-      if (EMIT) {
-        a.pairs[2 * (pos + cnt)] = pidx;
-        a.pairs[2 * (pos + cnt) + 1] = a.sqidx[gi];
-      }
+      hit(in_lds ? reinterpret_cast<const uint32_t*>(lds + R.lidx)[t] : a.sqidx[gi]);
       ++cnt;
     }
   }
   return cnt;
 }
 
-// Count pass (WRITE = 0): pairs per ordinary point (u8, saturating) and per task.  Write pass:
-// per-point counts -> block scan per round -> one emitting traversal.
-template <int WRITE>
+// Pair slot `pos` of the output (dropped past the capacity: the caller sees the total).
+__device__ __forceinline__ void join_put(const JoinRowArgs& a, uint64_t pos, uint32_t p, uint32_t q) {
+  if (pos >= a.cap) return;
+  if (a.pairs_aligned)
+    reinterpret_cast<uint2*>(a.pairs)[pos] = make_uint2(p, q);
+  else {
+    a.pairs[2 * pos] = p;
+    a.pairs[2 * pos + 1] = q;
+  }
+}
+
+// One pass per task: a round = kJoinThreads x 2 ordinary points.  Each thread probes its two
+// points keeping the first kJoinReg query indices of each in registers, a block scan places
+// every thread's pairs, ONE global atomic per round reserves the round's output run, and the
+// pairs are stored from registers (a point with more than kJoinReg pairs is probed again for
+// the rest -- rare; the order of its pairs is the probe order both times).
+template <bool EXACT0>
 __global__ __launch_bounds__(kJoinThreads) __attribute__((amdgpu_waves_per_eu(8)))  // 2 blocks per CU
 void join_row_probe_kernel(JoinRowArgs a) {
   extern __shared__ char lds[];
   __shared__ uint32_t wsum[kJoinThreads / 64];
   __shared__ int32_t s_row, s_fit;
   __shared__ uint32_t s_beg, s_end;
+  __shared__ uint64_t s_base;
   __shared__ QRow rows[kJoinMaxRows];
   const uint32_t ntask = a.task_off[a.qn];
   const uint32_t task = blockIdx.x;
-  if (task >= ntask) {
-    if (!WRITE && threadIdx.x == 0) a.task_cnt[task] = 0u;
-    return;
-  }
+  if (task >= ntask) return;
   const int64_t W = (int64_t)a.qn + 2, c = a.c, qn = a.qn;
   if (threadIdx.x == 0) {
     int lo = 0, hi = a.qn;  // row = last j with task_off[j] <= task
@@ -396,7 +408,7 @@ void join_row_probe_kernel(JoinRowArgs a) {
     for (int64_t ry = r0; fit && ry <= r1; ++ry) {
       const uint32_t b = a.q_off[(ry + 1) * W], e = a.q_off[(ry + 1) * W + W];
       fit = (e - b) < 65536u;
-      need += ((size_t)(W + 1) * 2 + 15) / 16 * 16 + (size_t)(e - b) * 16;
+      need += join_row_lds_bytes(W, e - b);
     }
     s_fit = fit && need <= (size_t)a.lds_budget;
   }
@@ -417,69 +429,101 @@ void join_row_probe_kernel(JoinRowArgs a) {
       const uint32_t oxy = (uint32_t)off;
       double2* lxy = reinterpret_cast<double2*>(lds + off);
       off += (size_t)(e - b) * 16;
+      const uint32_t oix = (uint32_t)off;
+      uint32_t* lix = reinterpret_cast<uint32_t*>(lds + off);
+      off += ((size_t)(e - b) * 4 + 15) / 16 * 16;
       for (int64_t t = threadIdx.x; t <= W; t += kJoinThreads) lo16[t] = (uint16_t)(qo[t] - b);
-      for (uint32_t t = threadIdx.x; t < e - b; t += kJoinThreads) lxy[t] = make_double2(a.sqx[b + t], a.sqy[b + t]);
-      if (threadIdx.x == 0) rows[j] = QRow{(int32_t)ry, b, o16, oxy};
+      for (uint32_t t = threadIdx.x; t < e - b; t += kJoinThreads) {
+        lxy[t] = make_double2(a.sqx[b + t], a.sqy[b + t]);
+        lix[t] = a.sqidx[b + t];
+      }
+      if (threadIdx.x == 0) rows[j] = QRow{(int32_t)ry, b, o16, oxy, oix};
     } else if (threadIdx.x == 0) {
-      rows[j] = QRow{(int32_t)ry, b, 0xffffffffu, 0u};
+      rows[j] = QRow{(int32_t)ry, b, 0xffffffffu, 0u, 0u};
     }
   }
   __syncthreads();
   const uint32_t beg = s_beg, end = s_end;
-  uint64_t run = WRITE ? a.task_pair_off[task] : 0;
-  uint32_t total_cnt = 0;
-  // Rounds of kJoinThreads points, in pairs with two register buffers: the next round's point
-  // loads are in flight while a round is processed (no copies on the loop's back edge).
-  // WRITE: every thread walks the same number of rounds (block scan per round).
   struct Pt {
     double x, y;
-    uint32_t idx, cnt;
+    uint32_t idx;
+    bool valid;
   };
-  auto load = [&](uint32_t s0, Pt& p) {
-    const uint32_t i = s0 + threadIdx.x;
+  auto load = [&](uint32_t i, Pt& p) {
+    p.valid = i < end;
     p.x = p.y = 0.0;
     p.idx = 0u;
-    p.cnt = 0u;
-    if (i < end) {
+    if (p.valid) {
       const double2 v = reinterpret_cast<const double2*>(a.soxy)[i];
       p.x = v.x;
       p.y = v.y;
-      if (WRITE) {
-        p.idx = a.soidx[i];
-        p.cnt = a.pcnt[i];
-      }
+      p.idx = a.soidx[i];
     }
   };
-  auto round = [&](uint32_t s0, const Pt& p) {
-    const uint32_t i = s0 + threadIdx.x;
-    const bool valid = i < end;
-    const int32_t cx = valid ? cell_index(p.x, a.u_minX, a.u_cl) : 0;
-    if (!WRITE) {
-      const uint32_t cnt = valid ? join_row_point<false>(a, lds, rows, nrows, p.x, p.y, cx, cy, 0, 0) : 0u;
-      if (valid) a.pcnt[i] = (uint8_t)(cnt < 255u ? cnt : 255u);
-      total_cnt += cnt;
-    } else {
-      uint32_t cnt = p.cnt;
-      if (cnt == 255u) cnt = join_row_point<false>(a, lds, rows, nrows, p.x, p.y, cx, cy, 0, 0);
-      uint32_t tot;
-      const uint32_t ex = block_excl_scan<kJoinThreads>(cnt, &tot, wsum);
-      if (valid && cnt) join_row_point<true>(a, lds, rows, nrows, p.x, p.y, cx, cy, p.idx, run + ex);
-      run += tot;
+  struct Hits {
+    uint32_t n = 0, h0 = 0, h1 = 0, h2 = 0;  // kJoinReg = 3 (no dynamic register indexing)
+  };
+  auto probe = [&](const Pt& p, Hits& H) {
+    if (!p.valid) return;
+    const int32_t cx = cell_index(p.x, a.u_minX, a.u_cl);
+    join_row_point<EXACT0>(a, lds, rows, nrows, p.x, p.y, cx, cy, [&](uint32_t q) {
+      const uint32_t n = H.n;  // selects, not an indexed array (which would live in scratch)
+      H.h0 = n == 0 ? q : H.h0;
+      H.h1 = n == 1 ? q : H.h1;
+      H.h2 = n == 2 ? q : H.h2;
+      H.n = n + 1;
+    });
+  };
+  auto emit = [&](const Pt& p, const Hits& H, uint64_t pos) {
+    if (H.n > 0) join_put(a, pos, p.idx, H.h0);
+    if (H.n > 1) join_put(a, pos + 1, p.idx, H.h1);
+    if (H.n > 2) join_put(a, pos + 2, p.idx, H.h2);
+    if (H.n > kJoinReg) {  // the rest: probe again, skipping the first kJoinReg pairs
+      uint32_t m = 0;
+      const int32_t cx = cell_index(p.x, a.u_minX, a.u_cl);
+      join_row_point<EXACT0>(a, lds, rows, nrows, p.x, p.y, cx, cy, [&](uint32_t q) {
+        if (m >= kJoinReg) join_put(a, pos + m, p.idx, q);
+        ++m;
+      });
     }
   };
-  Pt A, B;
-  load(beg, A);
+#if GF_JOIN_PTS == 2
+  Pt A0, A1;
+  load(beg + threadIdx.x, A0);
+  load(beg + kJoinThreads + threadIdx.x, A1);
   for (uint32_t s = beg; s < end; s += 2 * kJoinThreads) {
-    load(s + kJoinThreads, B);
-    round(s, A);
-    load(s + 2 * kJoinThreads, A);
-    if (s + kJoinThreads < end) round(s + kJoinThreads, B);
-  }
-  if (!WRITE) {
+    Pt B0, B1;  // next round's points in flight while this round is probed
+    load(s + 2 * kJoinThreads + threadIdx.x, B0);
+    load(s + 3 * kJoinThreads + threadIdx.x, B1);
+    Hits H0, H1;
+    probe(A0, H0);
+    probe(A1, H1);
     uint32_t tot;
-    block_excl_scan<kJoinThreads>(total_cnt, &tot, wsum);
-    if (threadIdx.x == 0) a.task_cnt[task] = tot;
+    const uint32_t ex = block_excl_scan<kJoinThreads>(H0.n + H1.n, &tot, wsum);
+    if (threadIdx.x == 0) s_base = tot ? atomicAdd(a.gcount, (unsigned long long)tot) : 0ull;
+    __syncthreads();
+    const uint64_t base = s_base + ex;
+    emit(A0, H0, base);
+    emit(A1, H1, base + H0.n);
+    A0 = B0;
+    A1 = B1;
   }
+#else
+  Pt A;
+  load(beg + threadIdx.x, A);
+  for (uint32_t s = beg; s < end; s += kJoinThreads) {
+    Pt B;  // the next round's point in flight while this round is probed
+    load(s + kJoinThreads + threadIdx.x, B);
+    Hits H;
+    probe(A, H);
+    uint32_t tot;
+    const uint32_t ex = block_excl_scan<kJoinThreads>(H.n, &tot, wsum);
+    if (threadIdx.x == 0) s_base = tot ? atomicAdd(a.gcount, (unsigned long long)tot) : 0ull;
+    __syncthreads();
+    emit(A, H, s_base + ex);
+    A = B;
+  }
+#endif
 }
 
 hipError_t launch_join_rows(gf_ctx* ctx, const JoinRowArgs& a, int stage, int blocks) {
@@ -501,12 +545,10 @@ hipError_t launch_join_rows(gf_ctx* ctx, const JoinRowArgs& a, int stage, int bl
       break;
     case 3: {
       KTimer t(ctx, GF_K_JOIN_PROBE);
-      hipLaunchKernelGGL(join_row_probe_kernel<0>, dim3(blocks), dim3(kJoinThreads), a.lds_budget, s, a);
-      break;
-    }
-    case 4: {
-      KTimer t(ctx, GF_K_JOIN_PROBE);
-      hipLaunchKernelGGL(join_row_probe_kernel<1>, dim3(blocks), dim3(kJoinThreads), a.lds_budget, s, a);
+      if (!a.approx && a.metric == 0)
+        hipLaunchKernelGGL(join_row_probe_kernel<true>, dim3(blocks), dim3(kJoinThreads), a.lds_budget, s, a);
+      else
+        hipLaunchKernelGGL(join_row_probe_kernel<false>, dim3(blocks), dim3(kJoinThreads), a.lds_budget, s, a);
       break;
     }
   }

@@ -677,3 +677,11 @@ def test_join_dense_spot_and_capacity(sf, oracle_mod):
     st = _lib.lib().gf_join_pp(ctx.handle, C.byref(g.c_grid), C.byref(g.c_grid), C.byref(po), C.byref(pq), 0.001, 0, 0,
                                pairs.data_ptr(), 100, C.byref(n))
     assert st == _lib.GF_ERR_CAPACITY and n.value == len(exp)
+    # an output buffer that is only 4-byte aligned (two 4-byte stores per pair)
+    big = torch.zeros(2 * len(exp) + 2, dtype=torch.int32, device="cuda")
+    st = _lib.lib().gf_join_pp(ctx.handle, C.byref(g.c_grid), C.byref(g.c_grid), C.byref(po), C.byref(pq), 0.001, 0, 0,
+                               big.data_ptr() + 4, len(exp), C.byref(n))
+    assert st == 0 and n.value == len(exp)
+    got = big[1:1 + 2 * len(exp)].cpu().numpy().view(np.uint32).astype(np.int64).reshape(-1, 2)
+    np.testing.assert_array_equal(got[np.lexsort((got[:, 1], got[:, 0]))], exp)
+    assert big[0].item() == 0 and big[-1].item() == 0  # nothing written outside the buffer

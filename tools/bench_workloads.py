@@ -178,7 +178,7 @@ def bench_join(args):
     avg = ms / 1000.0 / max(cnt, 1)
     pp = total_pairs / args.steps
     _line("point-point join", (no + nq) * args.steps / elapsed, "points/s", args.steps, args.warmup, elapsed,
-          "join_probe (count + write passes, per launch)", 16.0 * no + 8.0 * pp / 2, avg,
+          "join_row_probe (single pass: row-bucketed ordinary xy + idx in, pairs out)", 20.0 * no + 8.0 * pp, avg,
           {"config": {"workload": f"join_pp_{no // 1_000_000}Mx{nq / 1e6:g}M_r{r}_grid1000", "ordinary": no,
                       "query": nq, "radius": r, "pairs_per_window": pp},
            "breakdown": {"probe_us_per_launch": round(avg * 1e6, 2), "probe_launches_per_window": cnt / args.steps,
