@@ -1462,7 +1462,13 @@ extern "C" int gf_join_pp(gf_ctx* ctx, const gf_grid* ugrid, const gf_grid* qgri
   const int64_t mat = rowpath ? qn * sblocks : 1;
   size_t o_rmat = ar.take<uint32_t>(mat), o_rmats = ar.take<uint32_t>(mat + 1), o_roff = ar.take<uint32_t>(qn + 1);
   size_t o_rtask = ar.take<uint32_t>(qn), o_toff = ar.take<uint32_t>(qn + 1);
-  size_t o_gcnt = ar.take<unsigned long long>(1);
+  size_t o_gcnt = ar.take<unsigned long long>(2);  // overflow count, total
+  // task output regions, sized from the last join's pairs per point (x1.25 + one round)
+  const double ppp = ctx->join_ppp > 0 ? ctx->join_ppp : 1.0;
+  int64_t tcap = (int64_t)std::ceil(1.25 * ppp * kJoinTask) + 2 * kJoinThreads;
+  tcap = std::max<int64_t>(tcap, kJoinTask);
+  tcap = std::min<int64_t>(tcap, std::max<int64_t>(kJoinTask, ((int64_t)1 << 31) / 8 / std::max<int64_t>(max_tasks, 1)));
+  size_t o_tpairs = ar.take<uint64_t>(rowpath ? max_tasks * tcap : 1), o_tcnt = ar.take<uint32_t>(rowpath ? max_tasks : 1);
   size_t o_btmp = ar.take<uint32_t>(std::max(scan_tmp_elems(mat), scan_tmp_elems(qn)));
   size_t o_soxy = ar.take<double>(rowpath ? 2 * no : 1), o_soidx = ar.take<uint32_t>(rowpath ? no : 1);
   char* base = (char*)ctx_scratch(ctx, ar.off, &st);
@@ -1490,23 +1496,32 @@ extern "C" int gf_join_pp(gf_ctx* ctx, const gf_grid* ugrid, const gf_grid* qgri
     j.row_mat = R32(o_rmat); j.row_mat_scan = R32(o_rmats); j.row_off_w = R32(o_roff); j.row_off = R32(o_roff);
     j.row_tasks = R32(o_rtask);
     j.task_off = R32(o_toff); j.soxy = (double*)(base + o_soxy); j.soidx = R32(o_soidx);
-    j.gcount = (unsigned long long*)(base + o_gcnt);
+    unsigned long long* cnt2 = (unsigned long long*)(base + o_gcnt);
+    j.tpairs = (uint2*)(base + o_tpairs);
+    j.task_cap = (uint32_t)tcap;
+    j.task_cnt = R32(o_tcnt);
+    j.ovf_count = cnt2;
     j.pairs = pairs;
-    j.cap = pairs ? (uint64_t)cap : 0;
+    j.cap = pairs ? (uint64_t)std::max<int64_t>(cap, 0) : 0;
     j.pairs_aligned = ((uintptr_t)pairs & 7) == 0;
     j.lds_budget = kJoinLdsBudget;
-    GF_HIP_CHECK(ctx, hipMemsetAsync(j.gcount, 0, sizeof(unsigned long long), s));
+    GF_HIP_CHECK(ctx, hipMemsetAsync(cnt2, 0, sizeof(unsigned long long), s));
     GF_HIP_CHECK(ctx, launch_join_rows(ctx, j, 0, sblocks));
     GF_HIP_CHECK(ctx, launch_exclusive_scan(s, j.row_mat, mat, j.row_mat_scan, R32(o_btmp)));
     GF_HIP_CHECK(ctx, launch_join_rows(ctx, j, 1, sblocks));
     GF_HIP_CHECK(ctx, launch_join_rows(ctx, j, 2, sblocks));
     GF_HIP_CHECK(ctx, launch_exclusive_scan(s, j.row_tasks, qn, R32(o_toff), R32(o_btmp)));
-    // one pass: pairs are stored as they are found (past `cap` only counted)
+    // one probe pass into the task regions (+ overflow), then one packing launch
     GF_HIP_CHECK(ctx, launch_join_rows(ctx, j, 3, (int)max_tasks));
+    JoinCompactArgs k{};
+    k.tpairs = j.tpairs; k.task_cap = j.task_cap; k.task_cnt = j.task_cnt; k.ntask = (uint32_t)max_tasks;
+    k.ovf_count = cnt2; k.pairs = pairs; k.cap = j.cap; k.pairs_aligned = j.pairs_aligned; k.total = cnt2 + 1;
+    GF_HIP_CHECK(ctx, launch_join_compact(ctx, k));
     unsigned long long total = 0;
-    GF_HIP_CHECK(ctx, hipMemcpyAsync(&total, j.gcount, sizeof total, hipMemcpyDeviceToHost, s));
+    GF_HIP_CHECK(ctx, hipMemcpyAsync(&total, cnt2 + 1, sizeof total, hipMemcpyDeviceToHost, s));
     GF_HIP_CHECK(ctx, hipStreamSynchronize(s));
     *npairs = (int64_t)total;
+    ctx->join_ppp = (double)total / (double)no;
     if ((int64_t)total > cap || (total > 0 && !pairs)) return GF_ERR_CAPACITY;
     return GF_OK;
   }

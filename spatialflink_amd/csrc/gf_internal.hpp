@@ -33,6 +33,7 @@ struct gf_ctx {
   size_t pinned_bytes = 0;
   int num_cus = 256;
   int join_legacy = 0;  // testing: force the original (unbucketed) join probe
+  double join_ppp = 0.0;  // pairs per ordinary point of the last join (sizes the task regions)
   hipStream_t aux = nullptr;  // kNN depth 3: odd windows' launches (created on first use)
 };
 
@@ -347,12 +348,44 @@ struct JoinRowArgs {
   const uint32_t* task_off; // [qn+1]
   double* soxy;             // [2*no] row-bucketed ordinary xy
   uint32_t* soidx;          // [no]
-  unsigned long long* gcount;  // pairs found (one atomic per probe round)
-  uint32_t* pairs;          // [2 * cap] (ordinary idx, query idx)
+  // output: task t writes its pairs to the private region tpairs[t * task_cap ...]; a round
+  // that does not fit goes to the overflow: the caller's buffer filled from its END (pair i
+  // of the overflow at slot cap-1-i), one atomic on ovf_count per such round
+  uint2* tpairs;
+  uint32_t task_cap;
+  uint32_t* task_cnt;       // [max_tasks] pairs in each task's region
+  unsigned long long* ovf_count;
+  uint32_t* pairs;          // caller's [2 * cap]
   uint64_t cap;
-  int pairs_aligned;        // pairs is 8-byte aligned: one 8-byte store per pair
+  int pairs_aligned;        // 8-byte aligned: one 8-byte store per pair
   int lds_budget;
 };
+// Dense output [0, total): the task regions packed in task order, then the overflow moved
+// down from the buffer's end.  *total = pairs found (also when > cap: nothing is then valid).
+struct JoinCompactArgs {
+  const uint2* tpairs;
+  uint32_t task_cap;
+  const uint32_t* task_cnt;
+  uint32_t ntask;
+  const unsigned long long* ovf_count;
+  uint32_t* pairs;
+  uint64_t cap;
+  int pairs_aligned;
+  unsigned long long* total;
+};
+__device__ __forceinline__ void join_store(uint32_t* pairs, int aligned, uint64_t pos, uint2 v) {
+  if (aligned) {
+    reinterpret_cast<uint2*>(pairs)[pos] = v;
+  } else {
+    pairs[2 * pos] = v.x;
+    pairs[2 * pos + 1] = v.y;
+  }
+}
+__device__ __forceinline__ uint2 join_load(const uint32_t* pairs, int aligned, uint64_t pos) {
+  if (aligned) return reinterpret_cast<const uint2*>(pairs)[pos];
+  return make_uint2(pairs[2 * pos], pairs[2 * pos + 1]);
+}
+hipError_t launch_join_compact(gf_ctx* ctx, const JoinCompactArgs& a);
 constexpr int kJoinReg = 3;  // pairs per ordinary point kept in registers by the probe
 // LDS bytes of one staged query row with m points: u16 bucket offsets, xy, query indices
 __host__ __device__ inline size_t join_row_lds_bytes(int64_t W, uint32_t m) {

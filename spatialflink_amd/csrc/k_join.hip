@@ -171,9 +171,7 @@ constexpr int kRowMax = 8192;  // rows staged as LDS histograms by the bucketing
 #define GF_JOIN_BATCH 4
 #endif
 constexpr int kJoinBatch = GF_JOIN_BATCH;
-#ifndef GF_JOIN_PTS
-#define GF_JOIN_PTS 1  // ordinary points per thread per probe round (one output reservation)
-#endif  // candidates of one row loaded together in the probe
+  // candidates of one row loaded together in the probe
 
 // Bucketing: block b owns the contiguous input chunk b; its row histogram goes to column b of
 // the row-major matrix M[row][block] (plain stores).  The exclusive scan of M (flattened) is
@@ -361,22 +359,28 @@ __device__ __forceinline__ uint32_t join_row_point(const JoinRowArgs& a, const c
   return cnt;
 }
 
-// Pair slot `pos` of the output (dropped past the capacity: the caller sees the total).
-__device__ __forceinline__ void join_put(const JoinRowArgs& a, uint64_t pos, uint32_t p, uint32_t q) {
-  if (pos >= a.cap) return;
-  if (a.pairs_aligned)
-    reinterpret_cast<uint2*>(a.pairs)[pos] = make_uint2(p, q);
-  else {
-    a.pairs[2 * pos] = p;
-    a.pairs[2 * pos + 1] = q;
+// Output sinks of the probe: a task's private region (capacity checked by the caller), and
+// the overflow, stored from the END of the caller's buffer (dropped past cap; still counted).
+struct RegionSink {
+  uint2* out;
+  __device__ void operator()(uint64_t pos, uint32_t p, uint32_t q) const { out[pos] = make_uint2(p, q); }
+};
+struct OverflowSink {
+  uint32_t* pairs;
+  uint64_t cap;
+  int aligned;
+  __device__ void operator()(uint64_t pos, uint32_t p, uint32_t q) const {
+    if (pos < cap) join_store(pairs, aligned, cap - 1 - pos, make_uint2(p, q));
   }
-}
+};
 
-// One pass per task: a round = kJoinThreads x 2 ordinary points.  Each thread probes its two
-// points keeping the first kJoinReg query indices of each in registers, a block scan places
-// every thread's pairs, ONE global atomic per round reserves the round's output run, and the
-// pairs are stored from registers (a point with more than kJoinReg pairs is probed again for
-// the rest -- rare; the order of its pairs is the probe order both times).
+// One pass per task: a round = kJoinThreads ordinary points.  Each thread probes its point
+// keeping the first kJoinReg query indices in registers, a block scan places every thread's
+// pairs, and the round's run goes to the task's private output region at a block-uniform
+// running offset -- no global atomics (one same-address device atomic per round serialises
+// the whole grid: measured 4x slower than two passes).  A point with more than kJoinReg pairs
+// is probed again for the rest (rare; same probe order both times).  A round that no longer
+// fits the region goes to the overflow region.  join_compact_kernel packs the regions.
 template <bool EXACT0>
 __global__ __launch_bounds__(kJoinThreads) __attribute__((amdgpu_waves_per_eu(8)))  // 2 blocks per CU
 void join_row_probe_kernel(JoinRowArgs a) {
@@ -388,7 +392,10 @@ void join_row_probe_kernel(JoinRowArgs a) {
   __shared__ QRow rows[kJoinMaxRows];
   const uint32_t ntask = a.task_off[a.qn];
   const uint32_t task = blockIdx.x;
-  if (task >= ntask) return;
+  if (task >= ntask) {
+    if (threadIdx.x == 0) a.task_cnt[task] = 0u;
+    return;
+  }
   const int64_t W = (int64_t)a.qn + 2, c = a.c, qn = a.qn;
   if (threadIdx.x == 0) {
     int lo = 0, hi = a.qn;  // row = last j with task_off[j] <= task
@@ -474,41 +481,21 @@ void join_row_probe_kernel(JoinRowArgs a) {
       H.n = n + 1;
     });
   };
-  auto emit = [&](const Pt& p, const Hits& H, uint64_t pos) {
-    if (H.n > 0) join_put(a, pos, p.idx, H.h0);
-    if (H.n > 1) join_put(a, pos + 1, p.idx, H.h1);
-    if (H.n > 2) join_put(a, pos + 2, p.idx, H.h2);
+  auto emit = [&](const Pt& p, const Hits& H, const auto& put, uint64_t pos) {
+    if (H.n > 0) put(pos, p.idx, H.h0);
+    if (H.n > 1) put(pos + 1, p.idx, H.h1);
+    if (H.n > 2) put(pos + 2, p.idx, H.h2);
     if (H.n > kJoinReg) {  // the rest: probe again, skipping the first kJoinReg pairs
       uint32_t m = 0;
       const int32_t cx = cell_index(p.x, a.u_minX, a.u_cl);
       join_row_point<EXACT0>(a, lds, rows, nrows, p.x, p.y, cx, cy, [&](uint32_t q) {
-        if (m >= kJoinReg) join_put(a, pos + m, p.idx, q);
+        if (m >= kJoinReg) put(pos + m, p.idx, q);
         ++m;
       });
     }
   };
-#if GF_JOIN_PTS == 2
-  Pt A0, A1;
-  load(beg + threadIdx.x, A0);
-  load(beg + kJoinThreads + threadIdx.x, A1);
-  for (uint32_t s = beg; s < end; s += 2 * kJoinThreads) {
-    Pt B0, B1;  // next round's points in flight while this round is probed
-    load(s + 2 * kJoinThreads + threadIdx.x, B0);
-    load(s + 3 * kJoinThreads + threadIdx.x, B1);
-    Hits H0, H1;
-    probe(A0, H0);
-    probe(A1, H1);
-    uint32_t tot;
-    const uint32_t ex = block_excl_scan<kJoinThreads>(H0.n + H1.n, &tot, wsum);
-    if (threadIdx.x == 0) s_base = tot ? atomicAdd(a.gcount, (unsigned long long)tot) : 0ull;
-    __syncthreads();
-    const uint64_t base = s_base + ex;
-    emit(A0, H0, base);
-    emit(A1, H1, base + H0.n);
-    A0 = B0;
-    A1 = B1;
-  }
-#else
+  uint2* const region = a.tpairs + (size_t)task * a.task_cap;
+  uint32_t used = 0;  // block-uniform
   Pt A;
   load(beg + threadIdx.x, A);
   for (uint32_t s = beg; s < end; s += kJoinThreads) {
@@ -518,12 +505,61 @@ void join_row_probe_kernel(JoinRowArgs a) {
     probe(A, H);
     uint32_t tot;
     const uint32_t ex = block_excl_scan<kJoinThreads>(H.n, &tot, wsum);
-    if (threadIdx.x == 0) s_base = tot ? atomicAdd(a.gcount, (unsigned long long)tot) : 0ull;
-    __syncthreads();
-    emit(A, H, s_base + ex);
+    if (used + tot <= a.task_cap) {
+      emit(A, H, RegionSink{region}, used + ex);
+      used += tot;
+    } else {  // overflow (dense spots): one atomic for the round
+      if (threadIdx.x == 0) s_base = atomicAdd(a.ovf_count, (unsigned long long)tot);
+      __syncthreads();
+      emit(A, H, OverflowSink{a.pairs, a.cap, a.pairs_aligned}, s_base + ex);
+    }
     A = B;
   }
-#endif
+  if (threadIdx.x == 0) a.task_cnt[task] = used;
+}
+
+// Block t < ntask: its output offset = sum of task_cnt[0..t) (a block reduction over <= a few
+// thousand L2-resident counts -- no separate scan launches), then a coalesced copy of the
+// region to [off, off + n).  Blocks >= ntask move the overflow, which sits at
+// [cap - n_ovf, cap), down to [T, T + n_ovf) (T = sum of all regions): the part of it already
+// inside the target stays, the rest fills the target's remainder (disjoint ranges, and
+// disjoint from [0, T) whenever T + n_ovf <= cap -- otherwise the call fails with the total).
+__global__ __launch_bounds__(kBlock) void join_compact_kernel(JoinCompactArgs a) {
+  __shared__ unsigned long long part[kBlock / 64];
+  const uint32_t t = blockIdx.x < a.ntask ? blockIdx.x : a.ntask;
+  unsigned long long sum = 0;
+  for (uint32_t i = threadIdx.x; i < t; i += kBlock) sum += a.task_cnt[i];
+  for (int o = 32; o > 0; o >>= 1) sum += __shfl_down(sum, o, 64);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = sum;
+  __syncthreads();
+  unsigned long long off = 0;
+  for (int w = 0; w < kBlock / 64; ++w) off += part[w];
+  if (blockIdx.x < a.ntask) {
+    const uint32_t n = a.task_cnt[blockIdx.x];
+    const uint2* src = a.tpairs + (size_t)blockIdx.x * a.task_cap;
+    for (uint32_t i = threadIdx.x; i < n; i += kBlock)
+      if (off + i < a.cap) join_store(a.pairs, a.pairs_aligned, off + i, src[i]);
+    return;
+  }
+  const unsigned long long nov = *a.ovf_count, T = off;
+  if (blockIdx.x == a.ntask && threadIdx.x == 0) *a.total = T + nov;
+  if (nov == 0 || T + nov > a.cap) return;
+  const uint64_t lo = a.cap - nov;  // overflow source [lo, cap), target [T, T + nov)
+  uint64_t src0, dst0, n;
+  if (lo >= T + nov) {
+    src0 = lo; dst0 = T; n = nov;
+  } else {  // [lo, T + nov) is already in place
+    src0 = T + nov; dst0 = T; n = lo - T;
+  }
+  for (uint64_t i = (uint64_t)(blockIdx.x - a.ntask) * kBlock + threadIdx.x; i < n;
+       i += (uint64_t)(gridDim.x - a.ntask) * kBlock)
+    join_store(a.pairs, a.pairs_aligned, dst0 + i, join_load(a.pairs, a.pairs_aligned, src0 + i));
+}
+
+hipError_t launch_join_compact(gf_ctx* ctx, const JoinCompactArgs& a) {
+  KTimer t(ctx, GF_K_JOIN_PROBE);
+  hipLaunchKernelGGL(join_compact_kernel, dim3(a.ntask + 64), dim3(kBlock), 0, ctx->stream, a);
+  return hipGetLastError();
 }
 
 hipError_t launch_join_rows(gf_ctx* ctx, const JoinRowArgs& a, int stage, int blocks) {
