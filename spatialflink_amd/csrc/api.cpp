@@ -1515,7 +1515,7 @@ extern "C" int gf_join_pp(gf_ctx* ctx, const gf_grid* ugrid, const gf_grid* qgri
     GF_HIP_CHECK(ctx, launch_join_rows(ctx, j, 3, (int)max_tasks));
     JoinCompactArgs k{};
     k.tpairs = j.tpairs; k.task_cap = j.task_cap; k.task_cnt = j.task_cnt; k.ntask = (uint32_t)max_tasks;
-    k.ovf_count = cnt2; k.pairs = pairs; k.cap = j.cap; k.pairs_aligned = j.pairs_aligned; k.total = cnt2 + 1;
+    k.ovf_count = cnt2; k.sqidx = j.sqidx; k.pairs = pairs; k.cap = j.cap; k.pairs_aligned = j.pairs_aligned; k.total = cnt2 + 1;
     GF_HIP_CHECK(ctx, launch_join_compact(ctx, k));
     unsigned long long total = 0;
     GF_HIP_CHECK(ctx, hipMemcpyAsync(&total, cnt2 + 1, sizeof total, hipMemcpyDeviceToHost, s));

@@ -361,13 +361,15 @@ struct JoinRowArgs {
   int lds_budget;
 };
 // Dense output [0, total): the task regions packed in task order, then the overflow moved
-// down from the buffer's end.  *total = pairs found (also when > cap: nothing is then valid).
+// down from the buffer's end; the probe stores (ordinary idx, query slot), the packing maps
+// the slot to the query index.  *total = pairs found (also when > cap: nothing is then valid).
 struct JoinCompactArgs {
   const uint2* tpairs;
   uint32_t task_cap;
   const uint32_t* task_cnt;
   uint32_t ntask;
   const unsigned long long* ovf_count;
+  const uint32_t* sqidx;    // query slot -> query index
   uint32_t* pairs;
   uint64_t cap;
   int pairs_aligned;
@@ -387,9 +389,9 @@ __device__ __forceinline__ uint2 join_load(const uint32_t* pairs, int aligned, u
 }
 hipError_t launch_join_compact(gf_ctx* ctx, const JoinCompactArgs& a);
 constexpr int kJoinReg = 3;  // pairs per ordinary point kept in registers by the probe
-// LDS bytes of one staged query row with m points: u16 bucket offsets, xy, query indices
+// LDS bytes of one staged query row with m points: u16 bucket offsets, xy
 __host__ __device__ inline size_t join_row_lds_bytes(int64_t W, uint32_t m) {
-  return ((size_t)(W + 1) * 2 + 15) / 16 * 16 + (size_t)m * 16 + ((size_t)m * 4 + 15) / 16 * 16;
+  return ((size_t)(W + 1) * 2 + 15) / 16 * 16 + (size_t)m * 16;
 }
 hipError_t launch_join_rows(gf_ctx* ctx, const JoinRowArgs& a, int stage, int blocks);
 

@@ -260,41 +260,21 @@ __global__ __launch_bounds__(kBlock) void join_rows_finish_kernel(const uint32_t
   }
 }
 
-template <int NT>
-__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* total, uint32_t* wsum) {
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  uint32_t inc = v;
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const uint32_t t = __shfl_up(inc, off, 64);
-    if (lane >= off) inc += t;
-  }
-  if (lane == 63) wsum[wid] = inc;
-  __syncthreads();
-  uint32_t before = 0, tot = 0;
-  for (int w = 0; w < NT / 64; ++w) {
-    if (w < wid) before += wsum[w];
-    tot += wsum[w];
-  }
-  *total = tot;
-  __syncthreads();
-  return before + inc - v;
-}
-
 // View of one staged query row: bucket kx (0..W-1) holds points [off(kx), off(kx+1)).
 // LDS mode: u16 bucket offsets relative to gbase at byte offset loff of the dynamic LDS, the
-// row's xy pairs at byte offset lxy and its query indices at lidx (offsets, not pointers, so
-// the loads stay ds_read).
+// row's xy pairs at byte offset lxy (offsets, not pointers, so the loads stay ds_read).
 struct QRow {
   int32_t ry;      // clamped row index in [-1, qn]
   uint32_t gbase;  // global index of the row's first point (sorted query arrays)
   uint32_t loff;   // 0xffffffff: the row is read from global memory
   uint32_t lxy;
-  uint32_t lidx;
 };
 
 // Candidates of ordinary point (px, py) in cell (cx, cy) among the staged rows: calls
-// hit(query index) for every pair, in a fixed order; returns the number of pairs.
+// hit(slot) for every pair, in a fixed order, where slot = the query point's position in the
+// cell-sorted query arrays; returns the number of pairs.  The slot -> query index lookup
+// (sqidx) is left to join_compact_kernel, where the gathers are independent of each other
+// (inside the probe loop each one stalls the candidate walk that follows it).
 // EXACT0: the plan is exact with metric 0 (squared-distance prefilter only, no hypot code).
 template <bool EXACT0, class Hit>
 __device__ __forceinline__ uint32_t join_row_point(const JoinRowArgs& a, const char* lds, const QRow* rows, int nrows,
@@ -319,7 +299,6 @@ __device__ __forceinline__ uint32_t join_row_point(const JoinRowArgs& a, const c
     if (fast_ok && in_lds && !brow && te > tb && tb >= t_lo && te <= t_hi) {
       // interior LDS run: kJoinBatch candidates loaded together (independent ds_read_b128)
       const double2* lxy = reinterpret_cast<const double2*>(lds + R.lxy);
-      const uint32_t* lix = reinterpret_cast<const uint32_t*>(lds + R.lidx);
       for (; t < te; t += kJoinBatch) {
         double2 q[kJoinBatch];
 #pragma unroll
@@ -328,7 +307,7 @@ __device__ __forceinline__ uint32_t join_row_point(const JoinRowArgs& a, const c
         for (int k = 0; k < kJoinBatch; ++k) {
           const double dx = px - q[k].x, dy = py - q[k].y;
           if (t + k < te && dx * dx + dy * dy <= a.s_r) {  // s <= smax(r) <=> sqrt(s) <= r
-            hit(lix[t + k]);
+            hit(R.gbase + t + k);
             ++cnt;
           }
         }
@@ -352,7 +331,7 @@ __device__ __forceinline__ uint32_t join_row_point(const JoinRowArgs& a, const c
         const double dx = px - qx, dy = py - qy;
         if (EXACT0 || a.metric == 0 ? !(dx * dx + dy * dy <= a.s_r) : !(fdlibm_hypot(dx, dy) <= a.r)) continue;
       }
-      hit(in_lds ? reinterpret_cast<const uint32_t*>(lds + R.lidx)[t] : a.sqidx[gi]);
+      hit(gi);
       ++cnt;
     }
   }
@@ -374,22 +353,35 @@ struct OverflowSink {
   }
 };
 
+struct JoinProbeHdr {
+  int32_t row, fit;
+  uint32_t beg, end;
+  uint32_t used;     // pairs placed in the task's region so far (wave reservations)
+  uint32_t fit_end;  // end of the last reservation that fit the region
+  QRow rows[kJoinMaxRows];
+};
+constexpr int kJoinHdrBytes = (int)((sizeof(JoinProbeHdr) + 15) / 16 * 16);
+
 // One pass per task: a round = kJoinThreads ordinary points.  Each thread probes its point
-// keeping the first kJoinReg query indices in registers, a block scan places every thread's
-// pairs, and the round's run goes to the task's private output region at a block-uniform
-// running offset -- no global atomics (one same-address device atomic per round serialises
-// the whole grid: measured 4x slower than two passes).  A point with more than kJoinReg pairs
+// keeping the first kJoinReg query slots in registers; each wave reserves its pairs' run in the
+// task's private output region with one LDS atomic -- no block barrier and no global atomic in
+// the loop.  A point with more than kJoinReg pairs
 // is probed again for the rest (rare; same probe order both times).  A round that no longer
 // fits the region goes to the overflow region.  join_compact_kernel packs the regions.
 template <bool EXACT0>
 __global__ __launch_bounds__(kJoinThreads) __attribute__((amdgpu_waves_per_eu(8)))  // 2 blocks per CU
 void join_row_probe_kernel(JoinRowArgs a) {
-  extern __shared__ char lds[];
-  __shared__ uint32_t wsum[kJoinThreads / 64];
-  __shared__ int32_t s_row, s_fit;
-  __shared__ uint32_t s_beg, s_end;
-  __shared__ uint64_t s_base;
-  __shared__ QRow rows[kJoinMaxRows];
+  // every LDS variable lives in the dynamic region, header first: static __shared__ would sit
+  // in front of it and shift its base off 16 B, and each misaligned ds_read_b128 of the staged
+  // rows is then replayed (measured: the probe ran 4x slower with a 408-byte static block)
+  extern __shared__ __attribute__((aligned(16))) char lds_base[];
+  JoinProbeHdr& hd = *reinterpret_cast<JoinProbeHdr*>(lds_base);
+  char* const lds = lds_base + kJoinHdrBytes;
+  int32_t& s_row = hd.row;
+  int32_t& s_fit = hd.fit;
+  uint32_t& s_beg = hd.beg;
+  uint32_t& s_end = hd.end;
+  QRow* const rows = hd.rows;
   const uint32_t ntask = a.task_off[a.qn];
   const uint32_t task = blockIdx.x;
   if (task >= ntask) {
@@ -398,6 +390,8 @@ void join_row_probe_kernel(JoinRowArgs a) {
   }
   const int64_t W = (int64_t)a.qn + 2, c = a.c, qn = a.qn;
   if (threadIdx.x == 0) {
+    hd.used = 0u;
+    hd.fit_end = 0u;
     int lo = 0, hi = a.qn;  // row = last j with task_off[j] <= task
     while (hi - lo > 1) {
       const int mid = (lo + hi) >> 1;
@@ -418,6 +412,11 @@ void join_row_probe_kernel(JoinRowArgs a) {
       need += join_row_lds_bytes(W, e - b);
     }
     s_fit = fit && need <= (size_t)a.lds_budget;
+#ifdef GF_EXP_J4
+    if (task % 500 == 7)
+      printf("task %u row %d rows %d..%d need %lu fit %d budget %d W %ld c %ld\n", task, lo, (int)r0, (int)r1,
+             (unsigned long)need, (int)s_fit, a.lds_budget, (long)W, (long)c);
+#endif
   }
   __syncthreads();
   const int32_t cy = s_row;
@@ -436,17 +435,11 @@ void join_row_probe_kernel(JoinRowArgs a) {
       const uint32_t oxy = (uint32_t)off;
       double2* lxy = reinterpret_cast<double2*>(lds + off);
       off += (size_t)(e - b) * 16;
-      const uint32_t oix = (uint32_t)off;
-      uint32_t* lix = reinterpret_cast<uint32_t*>(lds + off);
-      off += ((size_t)(e - b) * 4 + 15) / 16 * 16;
       for (int64_t t = threadIdx.x; t <= W; t += kJoinThreads) lo16[t] = (uint16_t)(qo[t] - b);
-      for (uint32_t t = threadIdx.x; t < e - b; t += kJoinThreads) {
-        lxy[t] = make_double2(a.sqx[b + t], a.sqy[b + t]);
-        lix[t] = a.sqidx[b + t];
-      }
-      if (threadIdx.x == 0) rows[j] = QRow{(int32_t)ry, b, o16, oxy, oix};
+      for (uint32_t t = threadIdx.x; t < e - b; t += kJoinThreads) lxy[t] = make_double2(a.sqx[b + t], a.sqy[b + t]);
+      if (threadIdx.x == 0) rows[j] = QRow{(int32_t)ry, b, o16, oxy};
     } else if (threadIdx.x == 0) {
-      rows[j] = QRow{(int32_t)ry, b, 0xffffffffu, 0u, 0u};
+      rows[j] = QRow{(int32_t)ry, b, 0xffffffffu, 0u};
     }
   }
   __syncthreads();
@@ -495,7 +488,7 @@ void join_row_probe_kernel(JoinRowArgs a) {
     }
   };
   uint2* const region = a.tpairs + (size_t)task * a.task_cap;
-  uint32_t used = 0;  // block-uniform
+  const uint32_t lane = threadIdx.x & 63;
   Pt A;
   load(beg + threadIdx.x, A);
   for (uint32_t s = beg; s < end; s += kJoinThreads) {
@@ -503,27 +496,42 @@ void join_row_probe_kernel(JoinRowArgs a) {
     load(s + kJoinThreads + threadIdx.x, B);
     Hits H;
     probe(A, H);
-    uint32_t tot;
-    const uint32_t ex = block_excl_scan<kJoinThreads>(H.n, &tot, wsum);
-    if (used + tot <= a.task_cap) {
-      emit(A, H, RegionSink{region}, used + ex);
-      used += tot;
-    } else {  // overflow (dense spots): one atomic for the round
-      if (threadIdx.x == 0) s_base = atomicAdd(a.ovf_count, (unsigned long long)tot);
-      __syncthreads();
-      emit(A, H, OverflowSink{a.pairs, a.cap, a.pairs_aligned}, s_base + ex);
+    // wave-level placement, no block barrier in the loop: a wave prefix sum, then one LDS
+    // atomic per wave reserves its run in the task's region (pair order is unspecified)
+    uint32_t inc = H.n;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t t = __shfl_up(inc, o, 64);
+      if (lane >= (uint32_t)o) inc += t;
+    }
+    const uint32_t wt = __shfl(inc, 63, 64), ex = inc - H.n;
+    if (wt) {
+      uint32_t wb = 0;
+      if (lane == 0) wb = atomicAdd(&hd.used, wt);
+      wb = __shfl(wb, 0, 64);
+      if (wb + wt <= a.task_cap) {
+        if (lane == 0) atomicMax(&hd.fit_end, wb + wt);
+        emit(A, H, RegionSink{region}, wb + ex);
+      } else {  // overflow (dense spots): one device atomic per wave
+        unsigned long long ob = 0;
+        if (lane == 0) ob = atomicAdd(a.ovf_count, (unsigned long long)wt);
+        ob = ((unsigned long long)__shfl((uint32_t)(ob >> 32), 0, 64) << 32) | __shfl((uint32_t)ob, 0, 64);
+        emit(A, H, OverflowSink{a.pairs, a.cap, a.pairs_aligned}, ob + ex);
+      }
     }
     A = B;
   }
-  if (threadIdx.x == 0) a.task_cnt[task] = used;
+  __syncthreads();
+  if (threadIdx.x == 0) a.task_cnt[task] = hd.fit_end;
 }
 
 // Block t < ntask: its output offset = sum of task_cnt[0..t) (a block reduction over <= a few
 // thousand L2-resident counts -- no separate scan launches), then a coalesced copy of the
-// region to [off, off + n).  Blocks >= ntask move the overflow, which sits at
-// [cap - n_ovf, cap), down to [T, T + n_ovf) (T = sum of all regions): the part of it already
-// inside the target stays, the rest fills the target's remainder (disjoint ranges, and
-// disjoint from [0, T) whenever T + n_ovf <= cap -- otherwise the call fails with the total).
+// region to [off, off + n) with each pair's query slot mapped to the query index.  Blocks >=
+// ntask handle the overflow, which sits at [cap - n_ovf, cap): its pair i goes to T + i (T =
+// sum of all regions); where [T, T + n_ovf) overlaps the source the pairs are mapped in place,
+// the rest of the target takes the source's remainder (every position read and written by one
+// thread; disjoint from [0, T) whenever T + n_ovf <= cap -- otherwise the call fails anyway).
 __global__ __launch_bounds__(kBlock) void join_compact_kernel(JoinCompactArgs a) {
   __shared__ unsigned long long part[kBlock / 64];
   const uint32_t t = blockIdx.x < a.ntask ? blockIdx.x : a.ntask;
@@ -537,23 +545,25 @@ __global__ __launch_bounds__(kBlock) void join_compact_kernel(JoinCompactArgs a)
   if (blockIdx.x < a.ntask) {
     const uint32_t n = a.task_cnt[blockIdx.x];
     const uint2* src = a.tpairs + (size_t)blockIdx.x * a.task_cap;
-    for (uint32_t i = threadIdx.x; i < n; i += kBlock)
-      if (off + i < a.cap) join_store(a.pairs, a.pairs_aligned, off + i, src[i]);
+    for (uint32_t i = threadIdx.x; i < n; i += kBlock) {
+      if (off + i >= a.cap) break;
+      const uint2 v = src[i];
+      join_store(a.pairs, a.pairs_aligned, off + i, make_uint2(v.x, a.sqidx[v.y]));
+    }
     return;
   }
   const unsigned long long nov = *a.ovf_count, T = off;
   if (blockIdx.x == a.ntask && threadIdx.x == 0) *a.total = T + nov;
   if (nov == 0 || T + nov > a.cap) return;
   const uint64_t lo = a.cap - nov;  // overflow source [lo, cap), target [T, T + nov)
-  uint64_t src0, dst0, n;
-  if (lo >= T + nov) {
-    src0 = lo; dst0 = T; n = nov;
-  } else {  // [lo, T + nov) is already in place
-    src0 = T + nov; dst0 = T; n = lo - T;
+  const bool apart = lo >= T + nov;
+  for (uint64_t i = (uint64_t)(blockIdx.x - a.ntask) * kBlock + threadIdx.x; i < nov;
+       i += (uint64_t)(gridDim.x - a.ntask) * kBlock) {
+    const uint64_t dst = T + i;
+    const uint64_t src = apart ? lo + i : (dst < lo ? T + nov + i : dst);
+    const uint2 v = join_load(a.pairs, a.pairs_aligned, src);
+    join_store(a.pairs, a.pairs_aligned, dst, make_uint2(v.x, a.sqidx[v.y]));
   }
-  for (uint64_t i = (uint64_t)(blockIdx.x - a.ntask) * kBlock + threadIdx.x; i < n;
-       i += (uint64_t)(gridDim.x - a.ntask) * kBlock)
-    join_store(a.pairs, a.pairs_aligned, dst0 + i, join_load(a.pairs, a.pairs_aligned, src0 + i));
 }
 
 hipError_t launch_join_compact(gf_ctx* ctx, const JoinCompactArgs& a) {
@@ -582,9 +592,11 @@ hipError_t launch_join_rows(gf_ctx* ctx, const JoinRowArgs& a, int stage, int bl
     case 3: {
       KTimer t(ctx, GF_K_JOIN_PROBE);
       if (!a.approx && a.metric == 0)
-        hipLaunchKernelGGL(join_row_probe_kernel<true>, dim3(blocks), dim3(kJoinThreads), a.lds_budget, s, a);
+        hipLaunchKernelGGL(join_row_probe_kernel<true>, dim3(blocks), dim3(kJoinThreads), a.lds_budget + kJoinHdrBytes,
+                           s, a);
       else
-        hipLaunchKernelGGL(join_row_probe_kernel<false>, dim3(blocks), dim3(kJoinThreads), a.lds_budget, s, a);
+        hipLaunchKernelGGL(join_row_probe_kernel<false>, dim3(blocks), dim3(kJoinThreads), a.lds_budget + kJoinHdrBytes,
+                           s, a);
       break;
     }
   }

@@ -305,6 +305,8 @@ __device__ __forceinline__ void range_stage(const RangeArgs& a, const RangeLds& 
   }
 }
 
+// dynamic-LDS header of range_kernel: lcount, pad, sh[kBlock/64], sm[kBlock/64] (16 B multiple)
+constexpr int kRangeHdrWords = 4 + 2 * 2 * (kBlock / 64);
 #ifndef GF_RANGE_WAVES
 #define GF_RANGE_WAVES 1
 #endif
@@ -313,9 +315,14 @@ __global__ __launch_bounds__(kBlock, GF_RANGE_WAVES) void range_kernel(RangeArgs
   const int64_t tstride = (int64_t)gridDim.x * (kBlock / 64) * 128;       // points per grid sweep
   const int64_t t0 = ((int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * 128;
   uint64_t hits = 0, mult = 0;
-  __shared__ uint32_t lcount;
-  // TABLE: LDS = rows[n] | rowoff[n] | (fast cells) 2 x (n+1) thresholds | (small) spans
-  extern __shared__ uint32_t lds[];
+  // LDS = 16-byte header (lcount) | TABLE: rows[n] | rowoff[n] | (fast cells) 2 x (n+1)
+  // thresholds | (small) spans.  No static __shared__: it would shift the dynamic base off
+  // 8 B and every fp64 threshold read (ds_read_b64) would be replayed as misaligned.
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds_base[];
+  uint32_t& lcount = lds_base[0];
+  uint64_t* const sh = reinterpret_cast<uint64_t*>(lds_base + 4);  // [kBlock / 64] hits
+  uint64_t* const sm = sh + kBlock / 64;                           // [kBlock / 64] multiplicity
+  uint32_t* const lds = lds_base + kRangeHdrWords;
   RangeLds L{nullptr, nullptr, nullptr, nullptr, nullptr};
   if (DEFER || TABLE) {
     if (threadIdx.x == 0) lcount = 0u;
@@ -362,7 +369,6 @@ __global__ __launch_bounds__(kBlock, GF_RANGE_WAVES) void range_kernel(RangeArgs
     range_stage<TABLE, POLY, DEFER, U>(a, L, B, ta + sstride, A, ta + 2 * sstride, tstride, hits, mult, &lcount);
   }
   // per-block partial counts (plain stores; summed by range_finalize)
-  __shared__ uint64_t sh[kBlock / 64], sm[kBlock / 64];
   const int wid = threadIdx.x >> 6;
   if ((threadIdx.x & 63) == 0) { sh[wid] = hits; sm[wid] = mult; }
   __syncthreads();
@@ -489,13 +495,13 @@ constexpr int kRangeU = GF_RANGE_U;  // tiles (of 128 points per wave) per main-
 hipError_t launch_range(gf_ctx* ctx, const RangeArgs& a, int table_mode, int poly, int blocks) {
   const dim3 g(blocks), b(kBlock);
   const bool defer = a.queue != nullptr;
-  const size_t lds = table_mode ? sizeof(uint32_t) * (size_t)((2 * a.grid_n + 1) & ~1) +
-                                      (a.xt ? 2 * sizeof(double) * (size_t)(a.grid_n + 1) : 0) +
-                                      (a.span_lds ? (size_t)((a.span_bytes + 3) & ~3) : 0)
-                                : 0;
+  const size_t lds = 4 * kRangeHdrWords + (table_mode ? sizeof(uint32_t) * (size_t)((2 * a.grid_n + 1) & ~1) +
+                                           (a.xt ? 2 * sizeof(double) * (size_t)(a.grid_n + 1) : 0) +
+                                           (a.span_lds ? (size_t)((a.span_bytes + 3) & ~3) : 0)
+                                     : 0);
   {
     KTimer t(ctx, GF_K_RANGE_SCAN);
-    if (!table_mode && !poly) hipLaunchKernelGGL((range_kernel<0, 0, 0, kRangeU>), g, b, 0, ctx->stream, a);
+    if (!table_mode && !poly) hipLaunchKernelGGL((range_kernel<0, 0, 0, kRangeU>), g, b, lds, ctx->stream, a);
     else if (!poly) {
       if (defer) hipLaunchKernelGGL((range_kernel<1, 0, 1, kRangeU>), g, b, lds, ctx->stream, a);
       else hipLaunchKernelGGL((range_kernel<1, 0, 0, kRangeU>), g, b, lds, ctx->stream, a);
