@@ -1456,7 +1456,13 @@ extern "C" int gf_join_pp(gf_ctx* ctx, const gf_grid* ugrid, const gf_grid* qgri
   size_t o_sqcx = ar.take<int32_t>(nq), o_sqcy = ar.take<int32_t>(nq), o_sqi = ar.take<uint32_t>(nq);
   size_t o_cnt = ar.take<uint32_t>(blocks), o_boff = ar.take<uint32_t>(blocks + 1);
   // row-bucketed path (k_join.hip): bucket the ordinary side by cell row, probe per task
-  const bool rowpath = c >= 0 && 2 * c + 1 <= kJoinMaxRows && qn <= 8192 && !ctx->join_legacy;
+  const bool rowpath = c >= 0 && 2 * c + 1 <= kJoinMaxRows && qn + 2 <= 8192 && !ctx->join_legacy;
+  // query side of the row path: row bucketing + per-row column sort (no global atomics)
+  const int qblk = (int)std::min<int64_t>(std::min<int64_t>(std::max<int64_t>(nq / 4096, 1), (int64_t)ctx->num_cus * 2), W);
+  const int64_t qmat = rowpath ? W * qblk : 1;
+  size_t o_qmat = ar.take<uint32_t>(qmat), o_qmats = ar.take<uint32_t>(qmat + 1);
+  size_t o_txy = ar.take<double>(rowpath ? 2 * nq : 1), o_tc = ar.take<int32_t>(rowpath ? 2 * nq : 1);
+  size_t o_tidx = ar.take<uint32_t>(rowpath ? nq : 1);
   const int64_t max_tasks = no / kJoinTask + qn + 1;
   const int sblocks = (int)std::min<int64_t>(std::max<int64_t>(no / 8192, 1), (int64_t)ctx->num_cus * 4);
   const int64_t mat = rowpath ? qn * sblocks : 1;
@@ -1477,14 +1483,28 @@ extern "C" int gf_join_pp(gf_ctx* ctx, const gf_grid* ugrid, const gf_grid* qgri
   auto I32 = [&](size_t o) { return (int32_t*)(base + o); };
   auto F64 = [&](size_t o) { return (double*)(base + o); };
   hipStream_t s = ctx->stream;
-  GF_HIP_CHECK(ctx, hipMemsetAsync(U32(o_hist), 0, bins * sizeof(uint32_t), s));
-  GF_HIP_CHECK(ctx, launch_join_qkeys(s, qry->x, qry->y, nq, qgrid->minX, qgrid->minY, qgrid->cellLength, qgrid->n,
-                                      U32(o_keys), I32(o_qcx), I32(o_qcy)));
-  GF_HIP_CHECK(ctx, launch_histogram(s, U32(o_keys), nq, U32(o_hist)));
-  GF_HIP_CHECK(ctx, launch_exclusive_scan(s, U32(o_hist), bins, U32(o_off), U32(o_tmp)));
-  GF_HIP_CHECK(ctx, hipMemcpyAsync(U32(o_cur), U32(o_off), bins * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
-  GF_HIP_CHECK(ctx, launch_join_qscatter(s, qry->x, qry->y, I32(o_qcx), I32(o_qcy), U32(o_keys), nq, U32(o_cur),
-                                         F64(o_sqx), F64(o_sqy), I32(o_sqcx), I32(o_sqcy), U32(o_sqi)));
+  if (rowpath) {
+    JoinQueryArgs q{};
+    q.qx = qry->x; q.qy = qry->y; q.nq = nq;
+    q.minX = qgrid->minX; q.minY = qgrid->minY; q.cl = qgrid->cellLength; q.qn = (int32_t)qn; q.nblk = qblk;
+    q.qmat = U32(o_qmat); q.qmat_scan = U32(o_qmats);
+    q.txy = F64(o_txy); q.tc = I32(o_tc); q.tidx = U32(o_tidx);
+    q.q_off = U32(o_off); q.sqx = F64(o_sqx); q.sqy = F64(o_sqy); q.sqcx = I32(o_sqcx); q.sqcy = I32(o_sqcy);
+    q.sqidx = U32(o_sqi);
+    GF_HIP_CHECK(ctx, launch_join_qrows(ctx, q, 0));
+    GF_HIP_CHECK(ctx, launch_exclusive_scan(s, q.qmat, qmat, q.qmat_scan, U32(o_tmp)));
+    GF_HIP_CHECK(ctx, launch_join_qrows(ctx, q, 1));
+    GF_HIP_CHECK(ctx, launch_join_qrows(ctx, q, 2));
+  } else {
+    GF_HIP_CHECK(ctx, hipMemsetAsync(U32(o_hist), 0, bins * sizeof(uint32_t), s));
+    GF_HIP_CHECK(ctx, launch_join_qkeys(s, qry->x, qry->y, nq, qgrid->minX, qgrid->minY, qgrid->cellLength,
+                                        qgrid->n, U32(o_keys), I32(o_qcx), I32(o_qcy)));
+    GF_HIP_CHECK(ctx, launch_histogram(s, U32(o_keys), nq, U32(o_hist)));
+    GF_HIP_CHECK(ctx, launch_exclusive_scan(s, U32(o_hist), bins, U32(o_off), U32(o_tmp)));
+    GF_HIP_CHECK(ctx, hipMemcpyAsync(U32(o_cur), U32(o_off), bins * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
+    GF_HIP_CHECK(ctx, launch_join_qscatter(s, qry->x, qry->y, I32(o_qcx), I32(o_qcy), U32(o_keys), nq, U32(o_cur),
+                                           F64(o_sqx), F64(o_sqy), I32(o_sqcx), I32(o_sqcy), U32(o_sqi)));
+  }
   if (rowpath) {
     auto R32 = [&](size_t o) { return (uint32_t*)(base + o); };
     JoinRowArgs j{};

@@ -394,6 +394,27 @@ __host__ __device__ inline size_t join_row_lds_bytes(int64_t W, uint32_t m) {
   return ((size_t)(W + 1) * 2 + 15) / 16 * 16 + (size_t)m * 16;
 }
 hipError_t launch_join_rows(gf_ctx* ctx, const JoinRowArgs& a, int stage, int blocks);
+// row path, query side: cell-sorted query arrays + q_off without global atomics
+struct JoinQueryArgs {
+  const double* qx;
+  const double* qy;
+  int64_t nq;
+  double minX, minY, cl;
+  int32_t qn;
+  int32_t nblk;            // bucketing grid
+  uint32_t* qmat;          // [(qn+2) * nblk] per-block row histograms (row-major)
+  uint32_t* qmat_scan;     // [(qn+2) * nblk + 1]
+  double* txy;             // [2*nq] row-bucketed xy
+  int32_t* tc;             // [2*nq] row-bucketed (cx, cy)
+  uint32_t* tidx;          // [nq]
+  uint32_t* q_off;         // [(qn+2)^2 + 1]
+  double* sqx;
+  double* sqy;
+  int32_t* sqcx;
+  int32_t* sqcy;
+  uint32_t* sqidx;
+};
+hipError_t launch_join_qrows(gf_ctx* ctx, const JoinQueryArgs& a, int stage);
 
 }  // namespace gf
 

@@ -245,6 +245,103 @@ __global__ __launch_bounds__(kBlock) void join_orow_scatter_kernel(JoinRowArgs a
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Query side of the row path: the same cell order as the histogram + scan + atomic scatter
+// of the legacy path (q_off[(ky)*W + kx] = first point of clamped cell (kx, ky)), built
+// without global atomics: row histograms in LDS -> one scan -> row scatter -> one block per
+// row counting-sorts its points by clamped column in LDS and writes that row of q_off.
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ int32_t clamp_key(int32_t c, int32_t qn) { return (c < -1 ? -1 : (c > qn ? qn : c)) + 1; }
+
+__global__ __launch_bounds__(kBlock) void join_qrow_hist_kernel(JoinQueryArgs a, uint32_t* __restrict__ M) {
+  __shared__ uint32_t h[kRowMax];
+  int64_t beg, end;
+  chunk_of(a.nq, beg, end);
+  const int32_t W = a.qn + 2;
+  for (int j = threadIdx.x; j < W; j += kBlock) h[j] = 0u;
+  __syncthreads();
+  for (int64_t i = beg + threadIdx.x; i < end; i += kBlock)
+    atomicAdd(&h[clamp_key(cell_index(a.qy[i], a.minY, a.cl), a.qn)], 1u);
+  __syncthreads();
+  for (int j = threadIdx.x; j < W; j += kBlock) M[(size_t)j * gridDim.x + blockIdx.x] = h[j];
+}
+
+__global__ __launch_bounds__(kBlock) void join_qrow_scatter_kernel(JoinQueryArgs a, const uint32_t* __restrict__ Ms) {
+  __shared__ uint32_t h[kRowMax];
+  int64_t beg, end;
+  chunk_of(a.nq, beg, end);
+  const int32_t W = a.qn + 2;
+  for (int j = threadIdx.x; j < W; j += kBlock) h[j] = Ms[(size_t)j * gridDim.x + blockIdx.x];
+  __syncthreads();
+  for (int64_t i = beg + threadIdx.x; i < end; i += kBlock) {
+    const double x = a.qx[i], y = a.qy[i];
+    const int32_t cx = cell_index(x, a.minX, a.cl), cy = cell_index(y, a.minY, a.cl);
+    const uint32_t pos = atomicAdd(&h[clamp_key(cy, a.qn)], 1u);
+    reinterpret_cast<double2*>(a.txy)[pos] = make_double2(x, y);
+    reinterpret_cast<int2*>(a.tc)[pos] = make_int2(cx, cy);
+    a.tidx[pos] = (uint32_t)i;
+  }
+}
+
+// one block per clamped row ky: column histogram + scan in LDS, q_off row, scatter in the row
+__global__ __launch_bounds__(kBlock) void join_qrow_sort_kernel(JoinQueryArgs a, const uint32_t* __restrict__ Ms,
+                                                                uint32_t total_idx) {
+  __shared__ uint32_t h[kRowMax];
+  __shared__ uint32_t wsum[kBlock / 64];
+  const int32_t W = a.qn + 2, ky = blockIdx.x;
+  const uint32_t rb = Ms[(size_t)ky * a.nblk], re = ky + 1 < W ? Ms[(size_t)(ky + 1) * a.nblk] : Ms[total_idx];
+  for (int j = threadIdx.x; j < W; j += kBlock) h[j] = 0u;
+  __syncthreads();
+  for (uint32_t i = rb + threadIdx.x; i < re; i += kBlock)
+    atomicAdd(&h[clamp_key(reinterpret_cast<const int2*>(a.tc)[i].x, a.qn)], 1u);
+  __syncthreads();
+  // exclusive scan of h[0..W) in place: each thread owns a contiguous span of columns
+  const int per = (W + kBlock - 1) / kBlock, j0 = threadIdx.x * per;
+  uint32_t run = 0;
+  for (int j = j0; j < j0 + per && j < W; ++j) run += h[j];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  uint32_t inc = run;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t t = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += t;
+  }
+  if (lane == 63) wsum[wid] = inc;
+  __syncthreads();
+  uint32_t before = inc - run;
+  for (int w = 0; w < wid; ++w) before += wsum[w];
+  for (int j = j0; j < j0 + per && j < W; ++j) {
+    const uint32_t c = h[j];
+    h[j] = rb + before;  // now the cell's cursor (absolute position)
+    a.q_off[(size_t)ky * W + j] = rb + before;
+    before += c;
+  }
+  if (ky == W - 1 && threadIdx.x == 0) a.q_off[(size_t)W * W] = re;
+  __syncthreads();
+  for (uint32_t i = rb + threadIdx.x; i < re; i += kBlock) {
+    const int2 cc = reinterpret_cast<const int2*>(a.tc)[i];
+    const uint32_t pos = atomicAdd(&h[clamp_key(cc.x, a.qn)], 1u);
+    const double2 v = reinterpret_cast<const double2*>(a.txy)[i];
+    a.sqx[pos] = v.x;
+    a.sqy[pos] = v.y;
+    a.sqcx[pos] = cc.x;
+    a.sqcy[pos] = cc.y;
+    a.sqidx[pos] = a.tidx[i];
+  }
+}
+
+hipError_t launch_join_qrows(gf_ctx* ctx, const JoinQueryArgs& a, int stage) {
+  hipStream_t s = ctx->stream;
+  KTimer t(ctx, GF_K_JOIN_BUCKET);
+  if (stage == 0)
+    hipLaunchKernelGGL(join_qrow_hist_kernel, dim3(a.nblk), dim3(kBlock), 0, s, a, a.qmat);
+  else if (stage == 1)
+    hipLaunchKernelGGL(join_qrow_scatter_kernel, dim3(a.nblk), dim3(kBlock), 0, s, a, a.qmat_scan);
+  else
+    hipLaunchKernelGGL(join_qrow_sort_kernel, dim3(a.qn + 2), dim3(kBlock), 0, s, a, a.qmat_scan,
+                       (uint32_t)((size_t)(a.qn + 2) * a.nblk));
+  return hipGetLastError();
+}
+
 // row_off[j] = Ms[j][0] (row starts), row_off[qn] = total; tasks per row
 __global__ __launch_bounds__(kBlock) void join_rows_finish_kernel(const uint32_t* __restrict__ Ms, int32_t qn,
                                                                   int32_t nblk, uint32_t total_idx,
