@@ -260,8 +260,14 @@ __global__ __launch_bounds__(kBlock) void join_qrow_hist_kernel(JoinQueryArgs a,
   const int32_t W = a.qn + 2;
   for (int j = threadIdx.x; j < W; j += kBlock) h[j] = 0u;
   __syncthreads();
-  for (int64_t i = beg + threadIdx.x; i < end; i += kBlock)
-    atomicAdd(&h[clamp_key(cell_index(a.qy[i], a.minY, a.cl), a.qn)], 1u);
+  for (int64_t i0 = beg + threadIdx.x; i0 < end; i0 += kBlock * kBucketU) {
+    double y[kBucketU];  // all loads in flight before the first use
+#pragma unroll
+    for (int u = 0; u < kBucketU; ++u) y[u] = i0 + u * kBlock < end ? a.qy[i0 + u * kBlock] : 0.0;
+#pragma unroll
+    for (int u = 0; u < kBucketU; ++u)
+      if (i0 + u * kBlock < end) atomicAdd(&h[clamp_key(cell_index(y[u], a.minY, a.cl), a.qn)], 1u);
+  }
   __syncthreads();
   for (int j = threadIdx.x; j < W; j += kBlock) M[(size_t)j * gridDim.x + blockIdx.x] = h[j];
 }
@@ -273,13 +279,24 @@ __global__ __launch_bounds__(kBlock) void join_qrow_scatter_kernel(JoinQueryArgs
   const int32_t W = a.qn + 2;
   for (int j = threadIdx.x; j < W; j += kBlock) h[j] = Ms[(size_t)j * gridDim.x + blockIdx.x];
   __syncthreads();
-  for (int64_t i = beg + threadIdx.x; i < end; i += kBlock) {
-    const double x = a.qx[i], y = a.qy[i];
-    const int32_t cx = cell_index(x, a.minX, a.cl), cy = cell_index(y, a.minY, a.cl);
-    const uint32_t pos = atomicAdd(&h[clamp_key(cy, a.qn)], 1u);
-    reinterpret_cast<double2*>(a.txy)[pos] = make_double2(x, y);
-    reinterpret_cast<int2*>(a.tc)[pos] = make_int2(cx, cy);
-    a.tidx[pos] = (uint32_t)i;
+  for (int64_t i0 = beg + threadIdx.x; i0 < end; i0 += kBlock * kBucketU) {
+    double x[kBucketU], y[kBucketU];
+#pragma unroll
+    for (int u = 0; u < kBucketU; ++u) {
+      const int64_t i = i0 + u * kBlock;
+      x[u] = i < end ? a.qx[i] : 0.0;
+      y[u] = i < end ? a.qy[i] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < kBucketU; ++u) {
+      const int64_t i = i0 + u * kBlock;
+      if (i >= end) continue;
+      const int32_t cx = cell_index(x[u], a.minX, a.cl), cy = cell_index(y[u], a.minY, a.cl);
+      const uint32_t pos = atomicAdd(&h[clamp_key(cy, a.qn)], 1u);
+      reinterpret_cast<double2*>(a.txy)[pos] = make_double2(x[u], y[u]);
+      reinterpret_cast<int2*>(a.tc)[pos] = make_int2(cx, cy);
+      a.tidx[pos] = (uint32_t)i;
+    }
   }
 }
 
@@ -292,8 +309,14 @@ __global__ __launch_bounds__(kBlock) void join_qrow_sort_kernel(JoinQueryArgs a,
   const uint32_t rb = Ms[(size_t)ky * a.nblk], re = ky + 1 < W ? Ms[(size_t)(ky + 1) * a.nblk] : Ms[total_idx];
   for (int j = threadIdx.x; j < W; j += kBlock) h[j] = 0u;
   __syncthreads();
-  for (uint32_t i = rb + threadIdx.x; i < re; i += kBlock)
-    atomicAdd(&h[clamp_key(reinterpret_cast<const int2*>(a.tc)[i].x, a.qn)], 1u);
+  for (uint32_t i0 = rb + threadIdx.x; i0 < re; i0 += kBlock * 4) {
+    int32_t cx[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) cx[u] = i0 + u * kBlock < re ? a.tc[2 * (i0 + u * kBlock)] : 0;
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (i0 + u * kBlock < re) atomicAdd(&h[clamp_key(cx[u], a.qn)], 1u);
+  }
   __syncthreads();
   // exclusive scan of h[0..W) in place: each thread owns a contiguous span of columns
   const int per = (W + kBlock - 1) / kBlock, j0 = threadIdx.x * per;
@@ -317,15 +340,27 @@ __global__ __launch_bounds__(kBlock) void join_qrow_sort_kernel(JoinQueryArgs a,
   }
   if (ky == W - 1 && threadIdx.x == 0) a.q_off[(size_t)W * W] = re;
   __syncthreads();
-  for (uint32_t i = rb + threadIdx.x; i < re; i += kBlock) {
-    const int2 cc = reinterpret_cast<const int2*>(a.tc)[i];
-    const uint32_t pos = atomicAdd(&h[clamp_key(cc.x, a.qn)], 1u);
-    const double2 v = reinterpret_cast<const double2*>(a.txy)[i];
-    a.sqx[pos] = v.x;
-    a.sqy[pos] = v.y;
-    a.sqcx[pos] = cc.x;
-    a.sqcy[pos] = cc.y;
-    a.sqidx[pos] = a.tidx[i];
+  for (uint32_t i0 = rb + threadIdx.x; i0 < re; i0 += kBlock * 4) {
+    int2 cc[4];
+    double2 v[4];
+    uint32_t ix[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const uint32_t i = i0 + u * kBlock < re ? i0 + u * kBlock : rb;
+      cc[u] = reinterpret_cast<const int2*>(a.tc)[i];
+      v[u] = reinterpret_cast<const double2*>(a.txy)[i];
+      ix[u] = a.tidx[i];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (i0 + u * kBlock >= re) continue;
+      const uint32_t pos = atomicAdd(&h[clamp_key(cc[u].x, a.qn)], 1u);
+      a.sqx[pos] = v[u].x;
+      a.sqy[pos] = v[u].y;
+      a.sqcx[pos] = cc[u].x;
+      a.sqcy[pos] = cc[u].y;
+      a.sqidx[pos] = ix[u];
+    }
   }
 }
 
