@@ -639,19 +639,37 @@ __device__ void knn_select_body(const KnnSelectArgs& a, LDS& L) {
       done = (nres >= k) || (cnt == M);
       GF_TR(5);
     }
-    if (GENERAL && !done) {  // every candidate, chunk by chunk, running top-k-distinct list
+    if (GENERAL && !done) {
+      // every candidate, 256 at a time, against a running top-k-distinct list: once the list
+      // holds k entries only keys below its k-th can change it, so a round usually adds a few
+      // keys and the sort stays on the register path (many equal distances -- points inside a
+      // query polygon all have d = 0 -- used to cost full LDS bitonic sorts of 1024 keys)
       int nr = 0;
-      const int chunk = LDS::kCap - k;
-      for (int64_t start = 0; start < M; start += chunk) {
-        const int len = (int)((M - start) < chunk ? (M - start) : chunk);
+      uint64_t md = ~0ull, mo = ~0ull;
+      int64_t mi = INT64_MAX;
+      for (int64_t i0 = 0; i0 < M; i0 += kSelT) {  // block-uniform trip count
         for (int i = tid; i < nr; i += kSelT) { L.sd[i] = L.rd[i]; L.so[i] = L.ro[i]; L.si[i] = L.ri[i]; }
-        for (int i = tid; i < len; i += kSelT) {
-          L.sd[nr + i] = dbits(a.cand_d[start + i]); L.si[nr + i] = a.cand_i[start + i];
-          L.so[nr + i] = okey(a.cand_o[start + i]);
+        if (tid == 0) L.s_cnt = nr;
+        __syncthreads();
+        const int64_t i = i0 + tid;
+        bool c = i < M;
+        uint64_t d = 0, o = 0;
+        int64_t ix = 0;
+        if (c) {
+          d = dbits(a.cand_d[i]);
+          o = okey(a.cand_o[i]);
+          ix = (int64_t)a.cand_i[i];
+          c = nr < k || kless(d, o, ix, md, mo, mi);
+        }
+        lds_push(L, c, d, o, ix);
+        __syncthreads();
+        const int cnt = L.s_cnt;
+        if (cnt > nr) {  // block-uniform
+          sort_lds(L, cnt);
+          nr = dedupe_topk(L, cnt, k);
+          if (nr == k) { md = L.rd[k - 1]; mo = L.ro[k - 1]; mi = L.ri[k - 1]; }
         }
         __syncthreads();
-        sort_lds(L, nr + len);
-        nr = dedupe_topk(L, nr + len, k);
       }
       nres = nr;
       done = true;
