@@ -1391,6 +1391,16 @@ extern "C" int gf_knn_run(gf_knn_plan* P, const gf_points* pts, int64_t* oo, dou
                           int32_t* n_out) {
   if (!P || !n_out) return GF_ERR_ARG;
   gf_ctx* ctx = P->ctx;
+  if (P->pipeline == 3 && ctx->aux) {
+    // the synchronous call may get a window the caller produced on the context stream just
+    // now: order the second stream after it (nothing to overlap with in a synchronous call)
+    int bs = bind(ctx);
+    if (bs) return bs;
+    hipEvent_t ev = take_event(ctx);
+    GF_HIP_CHECK(ctx, hipEventRecord(ev, ctx->stream));
+    GF_HIP_CHECK(ctx, hipStreamWaitEvent(ctx->aux, ev, 0));
+    ctx->pool.push_back(ev);
+  }
   int st = gf_knn_enqueue(P, pts, P->tmp_result);
   if (st || (st = gf_knn_plan_flush(P))) return st;
   GF_HIP_CHECK(ctx, hipMemcpyAsync(P->host_result, P->tmp_result, gf_knn_result_bytes(P->k), hipMemcpyDeviceToHost,

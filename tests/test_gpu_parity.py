@@ -605,6 +605,15 @@ def test_knn_pipelined(sf, oracle_mod, k, depth):
         res = op.run(w, q, 0.5, k)
         st, oo, od, oi = oracle_mod.knn(og, x, y, obj, QPOINT[0], QPOINT[1], 0.5, k)
         check_knn(res, oo, od, oi)
+    for j0, j1 in ((0, 1), (3, 4), (1, 2)):  # windows built by torch right before the call
+        (x0, y0, o0, w0), (x1, y1, o1, w1) = data[j0], data[j1]
+        w = sf.PointWindow(torch.cat([w0.x, w1.x]), torch.cat([w0.y, w1.y]), torch.cat([w0.objID, w1.objID + 10**7]),
+                           torch.cat([w0.timeStampMillisec, w1.timeStampMillisec]))
+        res = op.run(w, q, 0.5, k)
+        del w
+        st, oo, od, oi = oracle_mod.knn(og, np.concatenate([x0, x1]), np.concatenate([y0, y1]),
+                                        np.concatenate([o0, o1 + 10**7]), QPOINT[0], QPOINT[1], 0.5, k)
+        check_knn(res, oo, od, oi)
     op.set_pipeline(0, q, 0.5, k, 1)
 
 

@@ -15,6 +15,8 @@ tools/gpu_step.sh wl_polyknn 300 python -u bench.py --workload polyknn --steps 3
 for w in range ppoly join csv polyknn; do
   tools/gpu_step.sh st_$w 300 rocprofv3 --kernel-trace --stats -d $O/$w -o $w --output-format csv -- python -u bench.py --workload $w --steps 5 --warmup 1 --no-verify --no-cpu-baseline
 done
+tools/gpu_step.sh st_knn 300 rocprofv3 --kernel-trace --stats -d $O/knn -o knn --output-format csv -- python -u bench.py --steps 200 --warmup 10 --no-verify --no-cpu-baseline
 tools/gpu_step.sh st_sliding 300 rocprofv3 --kernel-trace --stats -d $O/sliding -o sliding --output-format csv -- python -u bench.py --workload sliding --steps 6 --warmup 2 --no-verify --no-cpu-baseline
+python tools/trace_interval.py $O/knn/knn_kernel_trace.csv knn_fused 20 > $O/knn_interval.txt || true
 grep -h '^{' gpurun_out/wl_*.log > $O/lines.jsonl || true
 wc -l $O/lines.jsonl
