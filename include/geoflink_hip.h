@@ -104,6 +104,10 @@ int         gf_ctx_synchronize(gf_ctx* ctx);
 /* Make the context stream wait for everything enqueued so far on the context's second stream
  * (kNN pipeline depth 3 launches odd windows there); no-op when it has none.  Host does not block. */
 int         gf_ctx_join(gf_ctx* ctx);
+/* The converse: make the second stream wait for everything enqueued so far on the context
+ * stream.  Call it after producing a window on the context stream and before a depth-3
+ * gf_knn_enqueue of it (gf_window_upload and gf_knn_run do it themselves). */
+int         gf_ctx_fork(gf_ctx* ctx);
 const char* gf_ctx_last_error(gf_ctx* ctx);
 /* Context flags (testing / tuning).  GF_FLAG_JOIN_LEGACY: 1 = gf_join_pp probes the query
  * buckets from global memory in input order instead of the row-bucketed LDS path. */
@@ -199,8 +203,8 @@ int    gf_knn_plan_set_index_base(gf_knn_plan* plan, int64_t base);
  * threshold adapts (shrinks after an overflow, doubles when fewer than k lie below it).
  * depth 3 (k <= 256): window i's fused launch selects window i-2; odd windows launch on a
  * second (non-blocking) stream, so consecutive launches overlap.  Window buffers must be
- * complete before their enqueue (no cross-stream wait is inserted); gf_knn_plan_flush joins
- * the second stream back into the context stream.  The sliding engine rejects depth 3.
+ * complete before their enqueue: no cross-stream wait is inserted for them (gf_ctx_fork after
+ * producing one on the context stream); gf_knn_plan_flush joins the second stream back.  The sliding engine rejects depth 3.
  * Results are identical at every depth. */
 int    gf_knn_plan_set_pipeline(gf_knn_plan* plan, int depth);
 int    gf_knn_plan_flush(gf_knn_plan* plan);

@@ -32,7 +32,7 @@ FLAG_JOIN_LEGACY = 1
 # Every symbol include/geoflink_hip.h declares (checked by tests/test_abi.py).
 EXPORTS = [
     "gf_abi_version", "gf_status_string", "gf_device_count", "gf_ctx_create", "gf_ctx_destroy",
-    "gf_ctx_set_stream", "gf_ctx_stream", "gf_ctx_synchronize", "gf_ctx_join", "gf_ctx_last_error", "gf_ctx_set_timing", "gf_ctx_set_timing_period", "gf_ctx_set_flag",
+    "gf_ctx_set_stream", "gf_ctx_stream", "gf_ctx_synchronize", "gf_ctx_join", "gf_ctx_fork", "gf_ctx_last_error", "gf_ctx_set_timing", "gf_ctx_set_timing_period", "gf_ctx_set_flag",
     "gf_ctx_timing", "gf_grid_make", "gf_grid_layers", "gf_cell_of", "gf_format_cell_id", "gf_parse_cell_id",
     "gf_assign_cells", "gf_bucket_by_cell", "gf_range_pp_plan_create", "gf_range_ppoly_plan_create",
     "gf_range_plan_destroy", "gf_range_run", "gf_range_plan_stats", "gf_range_plan_set_tuning", "gf_bitmap_to_indices", "gf_knn_pp_plan_create",
@@ -112,6 +112,7 @@ def lib():
             "gf_ctx_stream": ([P], P),
             "gf_ctx_synchronize": ([P], C.c_int),
             "gf_ctx_join": ([P], C.c_int),
+            "gf_ctx_fork": ([P], C.c_int),
             "gf_ctx_last_error": ([P], C.c_char_p),
             "gf_ctx_set_timing": ([P, C.c_int], C.c_int),
             "gf_ctx_set_flag": ([P, C.c_int, C.c_int], C.c_int),

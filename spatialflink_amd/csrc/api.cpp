@@ -270,6 +270,18 @@ extern "C" int gf_ctx_join(gf_ctx* ctx) {
   return GF_OK;
 }
 
+extern "C" int gf_ctx_fork(gf_ctx* ctx) {
+  if (!ctx) return GF_ERR_ARG;
+  if (!ctx->aux) return GF_OK;
+  int st = bind(ctx);
+  if (st) return st;
+  hipEvent_t ev = take_event(ctx);
+  GF_HIP_CHECK(ctx, hipEventRecord(ev, ctx->stream));
+  GF_HIP_CHECK(ctx, hipStreamWaitEvent(ctx->aux, ev, 0));
+  ctx->pool.push_back(ev);
+  return GF_OK;
+}
+
 extern "C" int gf_ctx_synchronize(gf_ctx* ctx) {
   if (!ctx) return GF_ERR_ARG;
   GF_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
@@ -1391,17 +1403,11 @@ extern "C" int gf_knn_run(gf_knn_plan* P, const gf_points* pts, int64_t* oo, dou
                           int32_t* n_out) {
   if (!P || !n_out) return GF_ERR_ARG;
   gf_ctx* ctx = P->ctx;
-  if (P->pipeline == 3 && ctx->aux) {
-    // the synchronous call may get a window the caller produced on the context stream just
-    // now: order the second stream after it (nothing to overlap with in a synchronous call)
-    int bs = bind(ctx);
-    if (bs) return bs;
-    hipEvent_t ev = take_event(ctx);
-    GF_HIP_CHECK(ctx, hipEventRecord(ev, ctx->stream));
-    GF_HIP_CHECK(ctx, hipStreamWaitEvent(ctx->aux, ev, 0));
-    ctx->pool.push_back(ev);
-  }
-  int st = gf_knn_enqueue(P, pts, P->tmp_result);
+  // the synchronous call may get a window the caller produced on the context stream just now:
+  // order the second stream after it (nothing to overlap with in a synchronous call)
+  int st = P->pipeline == 3 ? gf_ctx_fork(ctx) : GF_OK;
+  if (st) return st;
+  st = gf_knn_enqueue(P, pts, P->tmp_result);
   if (st || (st = gf_knn_plan_flush(P))) return st;
   GF_HIP_CHECK(ctx, hipMemcpyAsync(P->host_result, P->tmp_result, gf_knn_result_bytes(P->k), hipMemcpyDeviceToHost,
                                    ctx->stream));
@@ -1640,7 +1646,7 @@ extern "C" int gf_window_upload(gf_window* w, const double* x, const double* y, 
     if (ts) GF_HIP_CHECK(ctx, hipMemcpyAsync(w->ts, ts, b, hipMemcpyHostToDevice, ctx->stream));
   }
   w->n = n;
-  return GF_OK;
+  return gf_ctx_fork(ctx);  // a depth-3 plan may read the window from the second stream
 }
 
 extern "C" int gf_window_points(gf_window* w, gf_points* out) {
