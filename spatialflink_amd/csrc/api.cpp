@@ -798,6 +798,9 @@ extern "C" int gf_range_ppoly_plan_create(gf_ctx* ctx, const gf_grid* g, const g
   return GF_OK;
 }
 
+#ifndef GF_TEST_BPC
+#define GF_TEST_BPC 4  // range_test_kernel blocks per CU (4: 28 us vs 31-32 us at 8 or 2, C3)
+#endif
 extern "C" int gf_range_run(gf_range_plan* P, const gf_points* pts, uint64_t* bitmap, uint64_t* multi,
                             int64_t* counts) {
   if (!P || !bitmap) return GF_ERR_ARG;
@@ -855,7 +858,7 @@ extern "C" int gf_range_run(gf_range_plan* P, const gf_points* pts, uint64_t* bi
     a.queue = P->queue;
     a.queue_xy = P->queue_xy;
     a.queue_count = P->queue_count;
-    a.test_blocks = ctx->num_cus * 8;
+    a.test_blocks = ctx->num_cus * GF_TEST_BPC;
   }
   GF_HIP_CHECK(ctx, launch_range(ctx, a, P->table_mode, P->poly, blocks));
   if (counts)

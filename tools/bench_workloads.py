@@ -26,15 +26,78 @@ QPOINT = (116.414899, 39.920374)
 HBM_PEAK_GBS = 8000.0
 
 
-def _windows(sf, n, count, seed0, dev=0):
+def _dist(args):
+    """One process per GPU (torchrun env): (world, rank, device index).  Weak scaling: every
+    rank holds the configuration's per-GPU share of points in its cell-column band."""
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local % torch.cuda.device_count())
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
+    else:
+        torch.cuda.set_device(0)
+    return world, rank, torch.cuda.current_device()
+
+
+def _sync(world):
+    import torch
+    import torch.distributed as dist
+
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+
+
+def _reduce(v, world, args, dev, op="max"):
+    """max (elapsed) / min (verified flags) over ranks."""
+    if world == 1:
+        return v
+    import torch
+    import torch.distributed as dist
+
+    t = torch.tensor([float(v)], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.MIN)
+    return float(t.item())
+
+
+def _reduce_sum(v, world, args, dev):
+    import torch
+    import torch.distributed as dist
+
+    t = torch.tensor([float(v)], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
+    dist.all_reduce(t)
+    return float(t.item())
+
+
+def _band(sf, grid, grid_n, world, rank):
+    """x range of this rank's cell-column band (the whole grid at N = 1)."""
+    from spatialflink_amd import sharding
+
+    if world == 1:
+        return BEIJING[0], BEIJING[1]
+    lo, hi = sharding.column_bands(grid_n, world)[rank]
+    return sharding.band_x_range(grid, lo, hi)
+
+
+def _windows(sf, n, count, seed0, dev=0, xr=None):
     wins = []
+    xlo, xhi = xr or (BEIJING[0], BEIJING[1])
     for j in range(count):
-        x, y = sf.synthetic_uniform(seed0 + j, n, *BEIJING)
+        x, y = sf.synthetic_uniform(seed0 + j, n, xlo, xhi, BEIJING[2], BEIJING[3])
         wins.append((x, y, sf.PointWindow.from_numpy(x, y, np.arange(n, dtype=np.int64), device=dev)))
     return wins
 
 
-def _line(workload, value, unit, steps, warmup, elapsed, kernel, bytes_per_launch, avg_s, extra):
+def _line(workload, value, unit, steps, warmup, elapsed, kernel, bytes_per_launch, avg_s, extra, rank=0):
+    if rank != 0:
+        return
     achieved = bytes_per_launch / avg_s / 1e9 if avg_s > 0 else None
     d = {"metric": f"points/sec per window ({workload})", "value": round(value, 1), "unit": unit, "n_gpus": 1,
          "steps": steps, "warmup": warmup, "ms_per_step": round(1000.0 * elapsed / steps, 4),
@@ -49,6 +112,10 @@ def _line(workload, value, unit, steps, warmup, elapsed, kernel, bytes_per_launc
 
 
 def bench_range(args, polygons=False):
+    """C1 / C3 range windows.  N > 1: weak scaling -- each rank holds the per-GPU window share
+    (1M / 10M points) in its cell-column band and evaluates it with the full query set (query
+    points / polygons replicated); hits need no exchange (each point is owned by one rank), so
+    there is no collective in the data path.  value = points of all ranks / max elapsed."""
     import torch
 
     import spatialflink_amd as sf
@@ -57,6 +124,7 @@ def bench_range(args, polygons=False):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
 
+    world, rank, dev = _dist(args)
     L = _lib.lib()
     sizes = [args.points] if args.points else ([10_000_000] if polygons else [1_000_000, 10_000_000])
     sweep = [int(b) for b in str(args.range_blocks).split(",")]
@@ -66,9 +134,8 @@ def bench_range(args, polygons=False):
         grid = sf.UniformGrid(grid_n, *BEIJING)
         og = O.grid(grid_n, *BEIJING)
         nwin = 4
-        wins = _windows(sf, n, nwin, 7)
-        conf = sf.QueryConfiguration(sf.QueryType.WindowBased)
-        ctx = _lib.context(0)
+        wins = _windows(sf, n, nwin, 7 + 1000 * rank, dev, _band(sf, grid, grid_n, world, rank))
+        ctx = _lib.context(dev)
         r = 0.001 if polygons else args.radius
         if polygons:
             raw = O.generate_query_polygons(1000, BEIJING[0], BEIJING[2], BEIJING[1], BEIJING[3])
@@ -87,8 +154,8 @@ def bench_range(args, polygons=False):
         cells = [C.c_int64() for _ in range(4)]
         _lib.check(L.gf_range_plan_stats(h, *[C.byref(c) for c in cells]), ctx.handle, "stats")
         words = (n + 63) // 64
-        bitmaps = torch.empty(nwin, words, dtype=torch.int64, device="cuda")
-        counts = torch.zeros(nwin, 2, dtype=torch.int64, device="cuda")
+        bitmaps = torch.empty(nwin, words, dtype=torch.int64, device=dev)
+        counts = torch.zeros(nwin, 2, dtype=torch.int64, device=dev)
         pts = [w[2].c_struct() for w in wins]
 
         def step(i):
@@ -99,59 +166,90 @@ def bench_range(args, polygons=False):
 
         for i in range(args.warmup):
             step(i)
-        torch.cuda.synchronize()
+        _sync(world)
         ctx.set_timing_period(5)
         ctx.set_timing((1 << _lib.K_RANGE_SCAN) | (1 << _lib.K_RANGE_TEST))
+        _sync(world)
         t0 = time.perf_counter()
         for i in range(args.steps):
             step(i)
         torch.cuda.synchronize()
         elapsed = time.perf_counter() - t0
+        if world > 1:
+            import torch.distributed as dist
+
+            dist.barrier()
+        elapsed = _reduce(elapsed, world, args, dev)
         ms, cnt = ctx.timing(_lib.K_RANGE_SCAN)
         tms, tcnt = ctx.timing(_lib.K_RANGE_TEST)
         ctx.set_timing(0)
         ctx.set_timing_period(1)
         # parity spot check of window 0 against the oracle: range results are per point, so the
         # first min(n, 1M) points of the window are checked against the oracle run on them alone
+        # (on every rank: its shard's hits are exactly the oracle's hits of those points)
         hits = int(counts[0, 0].item())
         m = min(n, 1_000_000)
         x, y, _ = wins[0]
-        exp = (O.range_ppoly(og, x[:m], y[:m], O.Polygons(raw), r) if polygons
-               else O.range_pp(og, x[:m], y[:m], [QPOINT[0]], [QPOINT[1]], r))
-        got = sf.spatialOperators.bitmap_indices(ctx, bitmaps[0], n).astype(np.int64)
-        verified = bool(np.array_equal(got[got < m], exp))
+        verified = None
+        if not args.no_verify:
+            exp = (O.range_ppoly(og, x[:m], y[:m], O.Polygons(raw), r) if polygons
+                   else O.range_pp(og, x[:m], y[:m], [QPOINT[0]], [QPOINT[1]], r))
+            got = sf.spatialOperators.bitmap_indices(ctx, bitmaps[0], n).astype(np.int64)
+            verified = bool(_reduce(float(np.array_equal(got[got < m], exp)), world, args, dev, op="min"))
         L.gf_range_plan_destroy(h)
         avg_scan = ms / 1000.0 / max(cnt, 1)
         avg_test = tms / 1000.0 / tcnt if tcnt else 0.0
         avg = avg_scan + avg_test
         wl = (f"ppoly_{len(polys)}polys_r{r}_{n // 1_000_000}Mpts_grid{grid_n}" if polygons
               else f"range_pp_r{r}_{n // 1_000_000}Mpts_grid{grid_n}")
-        _line("point-polygon range" if polygons else "point-point range", n * args.steps / elapsed, "points/s",
-              args.steps, args.warmup, elapsed,
+        if world > 1:
+            wl += f"_per_gpu_x{world}"
+        _line("point-polygon range" if polygons else "point-point range", world * n * args.steps / elapsed,
+              "points/s", args.steps, args.warmup, elapsed,
               "range_kernel + range_test_kernel" if tcnt else "range_kernel", 16.0 * n + n / 8.0, avg,
-              {"config": {"workload": wl, "points_per_window": n, "grid": grid_n, "radius": r,
-                          "hits_window0": hits, "scan_blocks": blocks, "defer_mode": dmode,
+              {"n_gpus": world,
+               "config": {"workload": wl, "points_per_window": n * world, "points_per_gpu": n, "grid": grid_n,
+                          "radius": r, "hits_window0": hits, "scan_blocks": blocks, "defer_mode": dmode,
+                          "parallelism": f"cell-column shards x{world} (no collective)",
                           "cells_none_candidate_guaranteed_inside": [c.value for c in cells]},
                "breakdown": {"scan_us": round(avg_scan * 1e6, 2), "test_us": round(avg_test * 1e6, 2)},
-               "verified_vs_oracle": verified, "verified_sample": f"first {m} points of window 0"})
+               "verified_vs_oracle": verified, "verified_sample": f"first {m} points of window 0 on every rank"},
+              rank=rank)
 
 
 def bench_join(args):
+    """C4 join.  N > 1: weak scaling, grid-partitioned -- each rank holds 10M ordinary points of
+    its cell-column band; the query side (1M per GPU, the same global set on every rank) is
+    replicated with a c-column halo (sharding.join_query_halo), so every pair is produced once,
+    by its ordinary point's owner, with no collective in the data path."""
     import torch
 
     import spatialflink_amd as sf
-    from spatialflink_amd import _lib
+    from spatialflink_amd import _lib, sharding
 
+    world, rank, dev = _dist(args)
     L = _lib.lib()
     no = args.points or 10_000_000
     nq = max(1, no // 10)
-    grid = sf.UniformGrid(1000, *BEIJING)
-    ctx = _lib.context(0)
-    ow = _windows(sf, no, 2, 11)
-    qw = _windows(sf, nq, 2, 21)
+    grid_n = 1000
+    grid = sf.UniformGrid(grid_n, *BEIJING)
+    ctx = _lib.context(dev)
+    ow = _windows(sf, no, 2, 11 + 1000 * rank, dev, _band(sf, grid, grid_n, world, rank))
     r = 0.001
-    cap = 4 * (no + nq)
-    pairs = torch.empty(2 * cap, dtype=torch.int32, device="cuda")
+    if world == 1:
+        qw = _windows(sf, nq, 2, 21, dev)
+    else:
+        band = sharding.column_bands(grid_n, world)[rank]
+        c = int(np.ceil(r / grid.getCellLength()))
+        qw = []
+        for j in range(2):
+            x, y = sf.synthetic_uniform(21 + j, nq * world, *BEIJING)
+            keep = sharding.join_query_halo(np.floor((x - BEIJING[0]) / grid.getCellLength()), band, c)
+            xs, ys = np.ascontiguousarray(x[keep]), np.ascontiguousarray(y[keep])
+            qw.append((xs, ys, sf.PointWindow.from_numpy(xs, ys, np.flatnonzero(keep).astype(np.int64), device=dev)))
+    nq_rank = len(qw[0][0])
+    cap = 4 * (no + nq_rank)
+    pairs = torch.empty(2 * cap, dtype=torch.int32, device=dev)
     npairs = C.c_int64()
     po = [w[2].c_struct() for w in ow]
     pq = [w[2].c_struct() for w in qw]
@@ -163,8 +261,9 @@ def bench_join(args):
 
     for i in range(args.warmup):
         step(i)
-    torch.cuda.synchronize()
+    _sync(world)
     ctx.set_timing((1 << _lib.K_JOIN_PROBE) | (1 << _lib.K_JOIN_BUCKET))
+    _sync(world)
     t0 = time.perf_counter()
     total_pairs = 0
     for i in range(args.steps):
@@ -172,19 +271,28 @@ def bench_join(args):
         total_pairs += npairs.value
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.barrier()
+    elapsed = _reduce(elapsed, world, args, dev)
     ms, cnt = ctx.timing(_lib.K_JOIN_PROBE)
     bms, bcnt = ctx.timing(_lib.K_JOIN_BUCKET)
     ctx.set_timing(0)
     avg = ms / 1000.0 / max(cnt, 1)
     pp = total_pairs / args.steps
-    _line("point-point join", (no + nq) * args.steps / elapsed, "points/s", args.steps, args.warmup, elapsed,
+    pp_all = pp if world == 1 else _reduce_sum(pp, world, args, dev)
+    wl = f"join_pp_{no // 1_000_000}Mx{nq / 1e6:g}M_r{r}_grid1000" + (f"_per_gpu_x{world}" if world > 1 else "")
+    _line("point-point join", world * (no + nq) * args.steps / elapsed, "points/s", args.steps, args.warmup, elapsed,
           "join_row_probe (single pass: row-bucketed ordinary xy + idx in, pairs out)", 20.0 * no + 8.0 * pp, avg,
-          {"config": {"workload": f"join_pp_{no // 1_000_000}Mx{nq / 1e6:g}M_r{r}_grid1000", "ordinary": no,
-                      "query": nq, "radius": r, "pairs_per_window": pp},
+          {"n_gpus": world,
+           "config": {"workload": wl, "ordinary": no * world, "query": nq * world, "radius": r,
+                      "pairs_per_window": pp_all, "query_per_rank_with_halo": nq_rank,
+                      "parallelism": f"cell-column shards x{world}, query halo c columns (no collective)"},
            "breakdown": {"probe_us_per_launch": round(avg * 1e6, 2), "probe_launches_per_window": cnt / args.steps,
                          "bucket_us_per_launch": round(bms * 1000.0 / max(bcnt, 1), 2),
                          "bucket_launches_per_window": bcnt / args.steps},
-           "pairs_per_s": round(pp * args.steps / elapsed, 1)})
+           "pairs_per_s": round(pp_all * args.steps / elapsed, 1)}, rank=rank)
 
 
 def bench_sliding(args):
