@@ -318,6 +318,23 @@ int gf_join_pp(gf_ctx* ctx, const gf_grid* ugrid, const gf_grid* qgrid, const gf
                const gf_points* query, double r, int approximate, int metric, uint32_t* pairs,
                int64_t cap, int64_t* npairs);
 
+/* Point-polygon window join: JoinQuery.getReplicatedPolygonQueryStream + PointPolygonJoinQuery
+ * .windowBased (JoinQuery.java:93-115, PointPolygonJoinQuery.java:154-213).  Polygon q is
+ * replicated to its own G_q u C_q keys (UniformGrid.java:193-206,399-411) on qgrid; point p
+ * (key on ugrid, which must equal qgrid here) pairs with q if approximate or the JTS distance
+ * (DistanceFunctions.java:33-36) is <= r.  The plan is the replicated polygon side (reusable
+ * while the polygon set is unchanged); gf_range_plan_destroy frees it.  Run (sync): pairs =
+ * device uint32[2*cap] (point idx, polygon idx), unordered; *npairs = pairs found,
+ * GF_ERR_CAPACITY if > cap (pairs may be null with cap 0 to count). */
+int gf_join_ppoly_plan_create(gf_ctx* ctx, const gf_grid* qgrid, const gf_polygons* polys, double r,
+                              int approximate, int metric, gf_range_plan** out);
+int gf_join_ppoly_run(gf_range_plan* plan, const gf_grid* ugrid, const gf_points* points, uint32_t* pairs,
+                      int64_t cap, int64_t* npairs);
+/* One-shot: plan create + run + destroy (a polygon stream's window). */
+int gf_join_ppoly(gf_ctx* ctx, const gf_grid* ugrid, const gf_grid* qgrid, const gf_points* points,
+                  const gf_polygons* polys, double r, int approximate, int metric, uint32_t* pairs,
+                  int64_t cap, int64_t* npairs);
+
 /* ---- pinned host memory ---------------------------------------------------------------
  * Mapped, portable host memory: kernels write kNN records straight into it (pass it as the
  * `result` of gf_knn_enqueue), so no copy kernel runs per window. */

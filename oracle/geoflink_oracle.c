@@ -938,6 +938,91 @@ int64_t orc_join_pp(const orc_grid* ugrid, const orc_grid* qgrid,
   return cnt;
 }
 
+/* PointPolygonJoinQuery.windowBased -- PointPolygonJoinQuery.java:154-213, with the query
+ * polygons replicated by JoinQuery.getReplicatedPolygonQueryStream (JoinQuery.java:93-115):
+ * polygon q goes to every key of getGuaranteedNeighboringCells(r, q) (UniformGrid.java:193-206)
+ * and of getCandidateNeighboringCells(r, q, G_q) (:399-411) -- its OWN G, not a global one.
+ * The window join on gridID pairs point p (key = p.gridID on ugrid) with each replica whose key
+ * equals it; JoinFunction.join keeps (p, q) if approximate or getDistance(p, q) <= r
+ * (DistanceFunctions.java:33-36).  A polygon's keys form a set, so a pair appears at most once.
+ * Pairs come out grouped by point, polygons in replication order. */
+int64_t orc_join_ppoly(const orc_grid* ugrid, const orc_grid* qgrid, int64_t no, const double* ox,
+                       const double* oy, const orc_polygons* P, double r, int approximate, int metric,
+                       int64_t* out_pairs, int64_t cap) {
+  char id[32];
+  strset cells; /* every replicated key */
+  ss_init(&cells, 1024);
+  int64_t nrep = 0, repcap = 1024;
+  char* rep_key = (char*)malloc(KEYLEN * (size_t)repcap);
+  int64_t* rep_q = (int64_t*)malloc(8 * (size_t)repcap);
+  for (int32_t q = 0; q < P->npoly; q++) {
+    double x1, y1, x2, y2;
+    polygon_bbox(P, q, &x1, &y1, &x2, &y2);
+    int32_t xi1, yi1, xi2, yi2;
+    orc_cell_of(qgrid, x1, y1, &xi1, &yi1); /* Polygon.gridIDsSet: cells under the bbox */
+    orc_cell_of(qgrid, x2, y2, &xi2, &yi2);
+    strset Gq, Cq;
+    ss_init(&Gq, 64);
+    ss_init(&Cq, 64);
+    for (int64_t a = xi1; a <= xi2; a++)
+      for (int64_t b = yi1; b <= yi2; b++) {
+        orc_cell_id((int32_t)a, (int32_t)b, id);
+        g_cells_of(qgrid, r, id, &Gq);
+      }
+    for (int64_t a = xi1; a <= xi2; a++)
+      for (int64_t b = yi1; b <= yi2; b++) {
+        orc_cell_id((int32_t)a, (int32_t)b, id);
+        c_cells_of(qgrid, r, id, &Gq, &Cq);
+      }
+    const strset* sets[2] = {&Gq, &Cq};
+    for (int k = 0; k < 2; k++)
+      for (int64_t i = 0; i < sets[k]->cap; i++) {
+        const char* key = sets[k]->keys + i * KEYLEN;
+        if (!key[0]) continue;
+        if (nrep == repcap) {
+          repcap *= 2;
+          rep_key = (char*)realloc(rep_key, KEYLEN * (size_t)repcap);
+          rep_q = (int64_t*)realloc(rep_q, 8 * (size_t)repcap);
+        }
+        memcpy(rep_key + nrep * KEYLEN, key, KEYLEN);
+        rep_q[nrep++] = q;
+        ss_add(&cells, key);
+      }
+    ss_free(&Gq);
+    ss_free(&Cq);
+  }
+  /* bucket the replicas by key slot (CSR), replication order kept inside a key */
+  int64_t* off = (int64_t*)calloc((size_t)cells.cap + 1, 8);
+  int64_t* slot = (int64_t*)malloc(8 * (size_t)(nrep > 0 ? nrep : 1));
+  int64_t* lst = (int64_t*)malloc(8 * (size_t)(nrep > 0 ? nrep : 1));
+  for (int64_t t = 0; t < nrep; t++) { slot[t] = ss_find(&cells, rep_key + t * KEYLEN); off[slot[t] + 1]++; }
+  for (int64_t s2 = 0; s2 < cells.cap; s2++) off[s2 + 1] += off[s2];
+  {
+    int64_t* cur = (int64_t*)malloc(8 * (size_t)(cells.cap > 0 ? cells.cap : 1));
+    memcpy(cur, off, 8 * (size_t)cells.cap);
+    for (int64_t t = 0; t < nrep; t++) lst[cur[slot[t]]++] = rep_q[t];
+    free(cur);
+  }
+  int64_t cnt = 0;
+  for (int64_t p = 0; p < no; p++) {
+    int32_t cx, cy;
+    orc_cell_of(ugrid, ox[p], oy[p], &cx, &cy);
+    orc_cell_id(cx, cy, id);
+    int64_t s2 = ss_find(&cells, id);
+    if (s2 < 0) continue;
+    for (int64_t t = off[s2]; t < off[s2 + 1]; t++) {
+      int64_t q = lst[t];
+      if (approximate || orc_point_polygon_distance(ox[p], oy[p], P, (int32_t)q, metric) <= r) {
+        if (cnt < cap) { out_pairs[2 * cnt] = p; out_pairs[2 * cnt + 1] = q; }
+        cnt++;
+      }
+    }
+  }
+  free(off); free(slot); free(lst); free(rep_key); free(rep_q);
+  ss_free(&cells);
+  return cnt;
+}
+
 /* ------------------------------------------------------------------------------------ */
 /* Generators                                                                           */
 /* ------------------------------------------------------------------------------------ */

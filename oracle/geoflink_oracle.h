@@ -125,6 +125,9 @@ int32_t orc_knn_reference(const orc_grid* g, int64_t n, const double* x, const d
  * ugrid assigns ordinary points, qgrid assigns and replicates query points.
  * Writes pairs (ordinary idx, query idx) as out_pairs[2*i], out_pairs[2*i+1].
  * Returns pair count (may exceed cap) or ORC_ERR_LAYERS. */
+int64_t orc_join_ppoly(const orc_grid* ugrid, const orc_grid* qgrid, int64_t no, const double* ox,
+                       const double* oy, const orc_polygons* P, double r, int approximate, int metric,
+                       int64_t* out_pairs, int64_t cap);
 int64_t orc_join_pp(const orc_grid* ugrid, const orc_grid* qgrid,
                     int64_t no, const double* ox, const double* oy,
                     int64_t nq, const double* qx, const double* qy,

@@ -69,6 +69,9 @@ def lib():
             fn.restype = i32
         L.orc_join_pp.argtypes = [C.POINTER(OrcGrid), C.POINTER(OrcGrid), i64, P, P, i64, P, P, d, C.c_int, C.c_int, P, i64]
         L.orc_join_pp.restype = i64
+        L.orc_join_ppoly.argtypes = [C.POINTER(OrcGrid), C.POINTER(OrcGrid), i64, P, P, C.POINTER(OrcPolygons), d,
+                                     C.c_int, C.c_int, P, i64]
+        L.orc_join_ppoly.restype = i64
         L.orc_generate_query_polygons.argtypes = [i32, d, d, d, d, P, P, i32]
         L.orc_generate_query_polygons.restype = i32
         L.orc_java_random_points.argtypes = [i64, i64, d, d, d, d, P, P]
@@ -221,6 +224,19 @@ def join_pp(ugrid, qgrid, ox, oy, qx, qy, r, approximate=False, metric=METRIC_SQ
             return int(cnt), None
         if cnt <= cap:
             return 0, out[: 2 * cnt].reshape(-1, 2)
+        cap = int(cnt)
+
+
+def join_ppoly(ugrid, qgrid, ox, oy, P: Polygons, r, approximate=False, metric=METRIC_SQRT):
+    """Point-polygon window join (orc_join_ppoly): pairs[m, 2] = (point index, polygon index)."""
+    ox, oy = _f64(ox), _f64(oy)
+    cap = 1 << 16
+    while True:
+        out = np.empty(2 * cap, np.int64)
+        cnt = lib().orc_join_ppoly(C.byref(ugrid), C.byref(qgrid), len(ox), _p(ox), _p(oy), C.byref(P.c), float(r),
+                                   int(approximate), int(metric), _p(out), cap)
+        if cnt <= cap:
+            return out[: 2 * cnt].reshape(-1, 2)
         cap = int(cnt)
 
 

@@ -3,20 +3,21 @@
 The Java operators' per-window bodies (range, kNN, join) run as hand-written HIP kernels
 for gfx950 behind the C ABI in include/geoflink_hip.h; this package is the host-side
 mirror of the reference operator API (UniformGrid, Point, Polygon, QueryConfiguration,
-PointPointRangeQuery, PointPolygonRangeQuery, PointPointKNNQuery, PointPointJoinQuery).
+PointPointRangeQuery, PointPolygonRangeQuery, PointPointKNNQuery, PointPointJoinQuery,
+PointPolygonKNNQuery, PointPolygonJoinQuery).
 """
 from . import _lib
 from .spatialIndices import UniformGrid, generateCellIDStr, getIntCellIndices, padLeadingZeroesToInt
 from .spatialObjects import Point, PointWindow, Polygon, PolygonSet
 from .spatialOperators import (KNNResult, PinnedRecords, PointPointJoinQuery, PointPointKNNQuery, PointPointRangeQuery,
-                               PointPolygonKNNQuery,
+                               PointPolygonJoinQuery, PointPolygonKNNQuery,
                                PointPolygonRangeQuery, QueryConfiguration, QueryType, RangeResult, assign_cells,
                                bucket_by_cell, knn_merge_host, synthetic_uniform)
 from .spatialStreams import Deserialization
 from .windows import SlidingKNNQuery, SlidingRangeQuery, SlidingWindows
 
 __all__ = [
-    "SlidingWindows", "SlidingKNNQuery", "SlidingRangeQuery", "Deserialization", "PointPolygonKNNQuery",
+    "SlidingWindows", "SlidingKNNQuery", "SlidingRangeQuery", "Deserialization", "PointPolygonKNNQuery", "PointPolygonJoinQuery",
     "UniformGrid", "Point", "Polygon", "PolygonSet", "PointWindow", "QueryType", "QueryConfiguration",
     "PointPointRangeQuery", "PointPolygonRangeQuery", "PointPointKNNQuery", "PointPointJoinQuery", "RangeResult",
     "KNNResult", "PinnedRecords", "knn_merge_host", "assign_cells", "bucket_by_cell", "synthetic_uniform", "generateCellIDStr",

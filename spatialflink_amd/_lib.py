@@ -42,6 +42,7 @@ EXPORTS = [
     "gf_knn_decode", "gf_knn_run", "gf_knn_merge_dev", "gf_knn_merge_dev_batch", "gf_knn_merge_host",
     "gf_knn_sliding_create", "gf_knn_sliding_destroy", "gf_knn_sliding_geometry", "gf_knn_sliding_push",
     "gf_knn_sliding_flush", "gf_knn_sliding_decode", "gf_pane_bounds", "gf_csv_parse", "gf_join_pp",
+    "gf_join_ppoly_plan_create", "gf_join_ppoly_run", "gf_join_ppoly",
     "gf_window_create",
     "gf_window_destroy", "gf_window_upload", "gf_window_points", "gf_synth_uniform", "gf_pinned_alloc",
     "gf_pinned_free",
@@ -160,6 +161,11 @@ def lib():
             "gf_csv_parse": ([P, P, i64, P, C.POINTER(GfGrid), P, P, P, P, P, P, i64, pi64, pi64, pi32], C.c_int),
             "gf_join_pp": ([P, C.POINTER(GfGrid), C.POINTER(GfGrid), C.POINTER(GfPoints), C.POINTER(GfPoints), d,
                             C.c_int, C.c_int, P, i64, pi64], C.c_int),
+            "gf_join_ppoly_plan_create": ([P, C.POINTER(GfGrid), C.POINTER(GfPolygons), d, C.c_int, C.c_int,
+                                           C.POINTER(P)], C.c_int),
+            "gf_join_ppoly_run": ([P, C.POINTER(GfGrid), C.POINTER(GfPoints), P, i64, pi64], C.c_int),
+            "gf_join_ppoly": ([P, C.POINTER(GfGrid), C.POINTER(GfGrid), C.POINTER(GfPoints), C.POINTER(GfPolygons), d,
+                               C.c_int, C.c_int, P, i64, pi64], C.c_int),
             "gf_window_create": ([P, i64, C.POINTER(P)], C.c_int),
             "gf_window_destroy": ([P], None),
             "gf_window_upload": ([P, P, P, P, P, i64], C.c_int),

@@ -540,7 +540,7 @@ void mark_inside(gf_range_plan* P, std::vector<uint8_t>& table, const std::vecto
 // Cell classes and candidate lists for a set of query objects with base cell rects B_o
 // (a query point's cell, or every cell under a polygon's bbox -- Polygon.java:62).
 int build_table(gf_range_plan* P, const std::vector<Rect>& base, bool need_lists,
-                const std::vector<std::array<double, 4>>* inside = nullptr) {
+                const std::vector<std::array<double, 4>>* inside = nullptr, bool lists_all = false) {
   gf_ctx* ctx = P->ctx;
   const int64_t n = P->grid.n;
   const int32_t g = P->g_layers, c = P->c_layers;
@@ -630,7 +630,7 @@ int build_table(gf_range_plan* P, const std::vector<Rect>& base, bool need_lists
       for (int64_t y = r.y0; y <= r.y1; ++y)
         for (int64_t x = r.x0; x <= r.x1; ++x) {
           const int64_t cell = y * n + x;
-          if (table[cell] != 1 && table[cell] != 3) continue;
+          if (lists_all ? table[cell] == 0 : (table[cell] != 1 && table[cell] != 3)) continue;
           if (pass == 0) off[cell + 1]++;
           else lst[cur[cell]++] = (int32_t)o;
         }
@@ -667,7 +667,7 @@ extern "C" void gf_range_plan_destroy(gf_range_plan* P) {
   hipStreamSynchronize(P->ctx->stream);
   void* bufs[] = {P->table, P->extra, P->cand_off, P->cand_list, P->qx, P->qy, P->ring_off, P->vert_off,
                   P->vx, P->vy, P->bbox, P->ring_env, P->partials, P->queue, P->queue_count, P->queue_xy, P->rows, P->xt, P->yt,
-                  P->rowoff, P->spans};
+                  P->rowoff, P->spans, P->brect, P->jecnt, P->jecand, P->jbtot, P->jtotal};
   for (void* b : bufs)
     if (b) hipFree(b);
   delete P;
@@ -716,10 +716,14 @@ extern "C" int gf_range_pp_plan_create(gf_ctx* ctx, const gf_grid* g, const doub
   return GF_OK;
 }
 
-extern "C" int gf_range_ppoly_plan_create(gf_ctx* ctx, const gf_grid* g, const gf_polygons* polys, double r,
-                                          int approximate, int metric, gf_range_plan** out) {
+namespace {
+// join != 0: a point-polygon join plan -- cell lists for every non-none cell (guaranteed ones
+// too: the join tests every co-located pair), no inside-cell marking, per-polygon bbox cells.
+int ppoly_plan_create(gf_ctx* ctx, const gf_grid* g, const gf_polygons* polys, double r, int approximate, int metric,
+                      int join, gf_range_plan** out) {
   if (!ctx || !out || !grid_ok(g) || !polys || polys->npoly < 0 || (metric != 0 && metric != 1))
-    return set_err(ctx, GF_ERR_ARG, "gf_range_ppoly_plan_create: bad argument");
+    return set_err(ctx, GF_ERR_ARG, join ? "gf_join_ppoly_plan_create: bad argument"
+                                         : "gf_range_ppoly_plan_create: bad argument");
   *out = nullptr;
   int st = bind(ctx);
   if (st) return st;
@@ -784,7 +788,19 @@ extern "C" int gf_range_ppoly_plan_create(gf_ctx* ctx, const gf_grid* g, const g
     }
     if (rect) inside.push_back({x1, y1, x2, y2});
   }
-  if ((st = build_table(P, base, true, &inside))) { gf_range_plan_destroy(P); return st; }
+  P->join = join;
+  if ((st = build_table(P, base, true, join ? nullptr : &inside, join != 0))) { gf_range_plan_destroy(P); return st; }
+  if (join) {
+    std::vector<int32_t> br(4 * (size_t)std::max(np, 1), 0);
+    auto cl32 = [](int64_t v) { return (int32_t)std::min<int64_t>(std::max<int64_t>(v, INT32_MIN), INT32_MAX); };
+    for (int32_t p = 0; p < np; ++p) {
+      br[4 * p] = cl32(base[p].x0); br[4 * p + 1] = cl32(base[p].x1);
+      br[4 * p + 2] = cl32(base[p].y0); br[4 * p + 3] = cl32(base[p].y1);
+    }
+    if ((st = upload(ctx, &P->brect, br))) { gf_range_plan_destroy(P); return st; }
+    GF_HIP_CHECK(ctx, hipMalloc(&P->jbtot, sizeof(uint32_t) * (size_t)ctx->num_cus * 8));
+    GF_HIP_CHECK(ctx, hipMalloc(&P->jtotal, sizeof(unsigned long long)));
+  }
   const int32_t nverts = nrings > 0 ? polys->vert_off[nrings] : 0;
   std::vector<int32_t> ro(polys->ring_off, polys->ring_off + np + 1), vo(polys->vert_off, polys->vert_off + nrings + 1);
   std::vector<double> vx(polys->vx, polys->vx + nverts), vy(polys->vy, polys->vy + nverts);
@@ -797,21 +813,23 @@ extern "C" int gf_range_ppoly_plan_create(gf_ctx* ctx, const gf_grid* g, const g
   *out = P;
   return GF_OK;
 }
+}  // namespace
+
+extern "C" int gf_range_ppoly_plan_create(gf_ctx* ctx, const gf_grid* g, const gf_polygons* polys, double r,
+                                          int approximate, int metric, gf_range_plan** out) {
+  return ppoly_plan_create(ctx, g, polys, r, approximate, metric, 0, out);
+}
+
+extern "C" int gf_join_ppoly_plan_create(gf_ctx* ctx, const gf_grid* qgrid, const gf_polygons* polys, double r,
+                                         int approximate, int metric, gf_range_plan** out) {
+  return ppoly_plan_create(ctx, qgrid, polys, r, approximate, metric, 1, out);
+}
 
 #ifndef GF_TEST_BPC
 #define GF_TEST_BPC 4  // range_test_kernel blocks per CU (4: 28 us vs 31-32 us at 8 or 2, C3)
 #endif
-extern "C" int gf_range_run(gf_range_plan* P, const gf_points* pts, uint64_t* bitmap, uint64_t* multi,
-                            int64_t* counts) {
-  if (!P || !bitmap) return GF_ERR_ARG;
-  gf_ctx* ctx = P->ctx;
-  int st = bind(ctx);
-  if (st) return st;
-  if ((st = check_points(ctx, pts))) return st;
-  if (pts->n == 0) {
-    if (counts) GF_HIP_CHECK(ctx, hipMemsetAsync(counts, 0, 2 * sizeof(int64_t), ctx->stream));
-    return GF_OK;
-  }
+namespace {
+RangeArgs range_args(const gf_range_plan* P, const gf_points* pts, uint64_t* bitmap, uint64_t* multi) {
   RangeArgs a{};
   a.x = pts->x; a.y = pts->y; a.n = pts->n;
   a.bitmap = bitmap; a.multi = multi; a.partials = P->partials;
@@ -829,41 +847,118 @@ extern "C" int gf_range_run(gf_range_plan* P, const gf_points* pts, uint64_t* bi
   a.qx = P->qx; a.qy = P->qy;
   a.npoly = P->npoly; a.ring_off = P->ring_off; a.vert_off = P->vert_off; a.vx = P->vx; a.vy = P->vy;
   a.bbox = P->bbox; a.ring_env = P->ring_env;
+  a.brect = P->brect; a.g_layers = P->g_layers; a.c_layers = P->c_layers;
+  return a;
+}
+
+// the deferred-test queue: one segment per scan block, each large enough for every point the
+// block visits (a scan block visits at most 2 points per thread per grid sweep)
+int ensure_queue(gf_range_plan* P, RangeArgs& a, int blocks, bool with_counts) {
+  gf_ctx* ctx = P->ctx;
+  const int64_t tstride = (int64_t)blocks * kBlock * 2;
+  a.seg_cap = 2 * kBlock * ((a.n + tstride - 1) / tstride);
+  const int64_t need = a.seg_cap * blocks;
+  if (P->queue_cap < need || (with_counts && !P->jecnt)) {
+    GF_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+    void* old[] = {P->queue, P->queue_xy, P->jecnt, P->jecand};
+    for (void* b : old)
+      if (b) GF_HIP_CHECK(ctx, hipFree(b));
+    P->queue = nullptr;
+    P->queue_xy = nullptr;
+    P->jecnt = nullptr;
+    P->jecand = nullptr;
+    P->queue_cap = 0;
+    const int64_t cap = need;
+    GF_HIP_CHECK(ctx, hipMalloc(&P->queue, sizeof(uint32_t) * (size_t)cap));
+    GF_HIP_CHECK(ctx, hipMalloc(&P->queue_xy, 2 * sizeof(double) * (size_t)cap));
+    if (with_counts) {
+      GF_HIP_CHECK(ctx, hipMalloc(&P->jecnt, sizeof(uint32_t) * (size_t)cap));
+      GF_HIP_CHECK(ctx, hipMalloc(&P->jecand, 2 * sizeof(uint32_t) * (size_t)cap));
+    }
+    P->queue_cap = cap;
+  }
+  a.queue = P->queue;
+  a.queue_xy = P->queue_xy;
+  a.queue_count = P->queue_count;
+  return GF_OK;
+}
+
+int scan_blocks_range(const gf_range_plan* P, int64_t n) {
   // every wave should run >= 2 pipeline stages of kRangeU tiles (range_kernel); at most 4
   // blocks per CU (the sweep in tools/bench_workloads.py: 1024 blocks best at 10M points)
-  int blocks = (int)std::min<int64_t>(std::max<int64_t>(pts->n / (4 * 128 * 2 * 2), 1), (int64_t)ctx->num_cus * 4);
+  int blocks = (int)std::min<int64_t>(std::max<int64_t>(n / (4 * 128 * 2 * 2), 1), (int64_t)P->ctx->num_cus * 4);
   if (P->scan_blocks > 0) blocks = P->scan_blocks;
-  blocks = std::min(blocks, 2048);  // range_test_kernel's segment prefix (kMaxSegs)
+  return std::min(blocks, 2048);  // range_test_kernel's segment prefix (kMaxSegs)
+}
+}  // namespace
+
+extern "C" int gf_range_run(gf_range_plan* P, const gf_points* pts, uint64_t* bitmap, uint64_t* multi,
+                            int64_t* counts) {
+  if (!P || !bitmap) return GF_ERR_ARG;
+  if (P->join) return set_err(P->ctx, GF_ERR_ARG, "gf_range_run: a join plan (use gf_join_ppoly_run)");
+  gf_ctx* ctx = P->ctx;
+  int st = bind(ctx);
+  if (st) return st;
+  if ((st = check_points(ctx, pts))) return st;
+  if (pts->n == 0) {
+    if (counts) GF_HIP_CHECK(ctx, hipMemsetAsync(counts, 0, 2 * sizeof(int64_t), ctx->stream));
+    return GF_OK;
+  }
+  RangeArgs a = range_args(P, pts, bitmap, multi);
+  const int blocks = scan_blocks_range(P, pts->n);
   // Deferred tests pay a second launch; inline tests stall the waves holding candidate lanes.
   // Auto: defer while candidate cells are more than 5% of the non-none cells.
   const int64_t live = P->cls_cells[1] + P->cls_cells[2] + P->cls_cells[3];
   const bool can_defer = P->table_mode && (P->poly || !P->approx);
   const bool defer = can_defer && (P->defer_mode == 2 || (P->defer_mode == 0 && P->cls_cells[1] * 20 > live));
   if (defer) {
-    // a scan block visits at most 2 points per thread per grid sweep
-    const int64_t tstride = (int64_t)blocks * kBlock * 2;
-    a.seg_cap = 2 * kBlock * ((pts->n + tstride - 1) / tstride);
-    const int64_t need = a.seg_cap * blocks;
-    if (P->queue_cap < need) {
-      GF_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
-      if (P->queue) GF_HIP_CHECK(ctx, hipFree(P->queue));
-      if (P->queue_xy) GF_HIP_CHECK(ctx, hipFree(P->queue_xy));
-      P->queue = nullptr;
-      P->queue_xy = nullptr;
-      P->queue_cap = 0;
-      GF_HIP_CHECK(ctx, hipMalloc(&P->queue, sizeof(uint32_t) * (size_t)need));
-      GF_HIP_CHECK(ctx, hipMalloc(&P->queue_xy, 2 * sizeof(double) * (size_t)need));
-      P->queue_cap = need;
-    }
-    a.queue = P->queue;
-    a.queue_xy = P->queue_xy;
-    a.queue_count = P->queue_count;
+    if ((st = ensure_queue(P, a, blocks, false))) return st;
     a.test_blocks = ctx->num_cus * GF_TEST_BPC;
   }
   GF_HIP_CHECK(ctx, launch_range(ctx, a, P->table_mode, P->poly, blocks));
   if (counts)
     GF_HIP_CHECK(ctx, launch_range_finalize(ctx->stream, P->partials, blocks + (defer ? a.test_blocks : 0), counts));
   return GF_OK;
+}
+
+extern "C" int gf_join_ppoly_run(gf_range_plan* P, const gf_grid* ugrid, const gf_points* pts, uint32_t* pairs,
+                                 int64_t cap, int64_t* npairs) {
+  if (!P || !npairs || cap < 0 || !grid_ok(ugrid)) return GF_ERR_ARG;
+  gf_ctx* ctx = P->ctx;
+  if (!P->join) return set_err(ctx, GF_ERR_ARG, "gf_join_ppoly_run: not a join plan (gf_join_ppoly_plan_create)");
+  const gf_grid& q = P->grid;
+  if (ugrid->n != q.n || ugrid->minX != q.minX || ugrid->maxX != q.maxX || ugrid->minY != q.minY ||
+      ugrid->maxY != q.maxY || ugrid->cellLength != q.cellLength)
+    return set_err(ctx, GF_ERR_ARG, "gf_join_ppoly_run: the point grid must equal the polygon grid");
+  int st = bind(ctx);
+  if (st) return st;
+  if ((st = check_points(ctx, pts))) return st;
+  *npairs = 0;
+  if (pts->n == 0 || P->npoly == 0) return GF_OK;
+  if (pts->n > (int64_t)UINT32_MAX) return set_err(ctx, GF_ERR_ARG, "gf_join_ppoly_run: window too large");
+  RangeArgs a = range_args(P, pts, nullptr, nullptr);
+  const int blocks = scan_blocks_range(P, pts->n);
+  if ((st = ensure_queue(P, a, blocks, true))) return st;
+  const int jblocks = blocks;  // one count/write block per scan block (its queue segment)
+  GF_HIP_CHECK(ctx, launch_join_ppoly(ctx, a, blocks, jblocks, P->jecnt, P->jecand, P->jbtot, P->jtotal, pairs,
+                                      pairs ? cap : 0, pairs && ((uintptr_t)pairs % 8 == 0)));
+  unsigned long long total = 0;
+  GF_HIP_CHECK(ctx, hipMemcpyAsync(&total, P->jtotal, sizeof total, hipMemcpyDeviceToHost, ctx->stream));
+  GF_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+  *npairs = (int64_t)total;
+  if ((int64_t)total > cap || (total > 0 && !pairs)) return GF_ERR_CAPACITY;
+  return GF_OK;
+}
+
+extern "C" int gf_join_ppoly(gf_ctx* ctx, const gf_grid* ugrid, const gf_grid* qgrid, const gf_points* pts,
+                             const gf_polygons* polys, double r, int approximate, int metric, uint32_t* pairs,
+                             int64_t cap, int64_t* npairs) {
+  gf_range_plan* P = nullptr;
+  int st = gf_join_ppoly_plan_create(ctx, qgrid, polys, r, approximate, metric, &P);
+  if (st) return st;
+  st = gf_join_ppoly_run(P, ugrid, pts, pairs, cap, npairs);
+  gf_range_plan_destroy(P);
+  return st;
 }
 
 extern "C" int gf_range_plan_stats(const gf_range_plan* P, int64_t* none_cells, int64_t* candidate_cells,

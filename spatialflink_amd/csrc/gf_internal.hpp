@@ -215,6 +215,9 @@ struct RangeArgs {
   double* queue_xy;          // [2 * blocks * seg_cap] the queued points' coordinates
   int64_t seg_cap;           // points one scan block visits at most
   int test_blocks;
+  // point-polygon join: bbox cells per polygon (x0, x1, y0, y1) and the layer counts
+  const int32_t* brect;
+  int32_t g_layers, c_layers;
 };
 
 // launchers (return hipError_t of the launch)
@@ -292,6 +295,8 @@ hipError_t launch_knn_fused(gf_ctx* ctx, const KnnScanArgs& a, const KnnSelectAr
 int knn_enqueue_merge(gf_knn_plan* P, const gf_points* pts, void* result, const KnnMergeArgs* merge, int* merged);
 
 hipError_t launch_range(gf_ctx* ctx, const RangeArgs& a, int table_mode, int poly, int blocks);
+hipError_t launch_join_ppoly(gf_ctx* ctx, const RangeArgs& a, int blocks, int jblocks, uint32_t* ecnt, uint32_t* ecand,
+                             uint32_t* btot, unsigned long long* total, uint32_t* pairs, int64_t cap, int aligned);
 hipError_t launch_range_finalize(hipStream_t s, const uint64_t* partials, int blocks, int64_t* counts);
 
 struct JoinArgs {
@@ -458,6 +463,13 @@ struct gf_range_plan {
   int64_t cls_cells[4] = {0, 0, 0, 0};  // in-grid cells per class (diagnostics)
   int32_t scan_blocks = 0;         // tuning: 0 = auto
   int32_t defer_mode = 0;          // tuning: 0 auto, 1 test inline, 2 defer
+  // point-polygon join plans (gf_join_ppoly_plan_create)
+  int join = 0;
+  int32_t* brect = nullptr;        // [npoly * 4] bbox cells x0, x1, y0, y1
+  uint32_t* jecnt = nullptr;       // [queue_cap] pairs per queued point
+  uint32_t* jecand = nullptr;      // [queue_cap * 2] their first polygon indices
+  uint32_t* jbtot = nullptr;       // [num_cus * 8] pairs per join block
+  unsigned long long* jtotal = nullptr;
 };
 
 struct gf_knn_plan {

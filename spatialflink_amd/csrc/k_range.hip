@@ -170,6 +170,10 @@ __device__ __forceinline__ void eval_point(const RangeArgs& a, double px, double
   multi = false;
   defer = false;
   if (!valid) return;
+  if (DEFER == 2) {  // point-polygon join: every point whose key some polygon replicates to
+    defer = cls != kNone;
+    return;
+  }
   if (cls == kAccept) {
     hit = true;
   } else if (cls == kTest) {
@@ -219,7 +223,7 @@ __device__ __forceinline__ void range_tile(const RangeArgs& a, int64_t t, double
   eval_point<TABLE, POLY, DEFER>(a, x1, y1, c1, v1, h1, m1, d1);
   const uint64_t b0 = __ballot(h0), b1 = __ballot(h1);
   const int64_t w = t >> 6;
-  if (lane == 0) {  // the caller's bitmap is only 8-B aligned
+  if (DEFER != 2 && lane == 0) {  // the caller's bitmap is only 8-B aligned
     a.bitmap[w] = b0;
     if (FULL || t + 64 < a.n) a.bitmap[w + 1] = b1;
   }
@@ -491,6 +495,169 @@ __global__ __launch_bounds__(kBlock) void range_test_kernel(RangeArgs a, int par
 #define GF_RANGE_U 2
 #endif
 constexpr int kRangeU = GF_RANGE_U;  // tiles (of 128 points per wave) per main-loop iteration
+
+// =======================================================================================
+// Point-polygon window join (PointPolygonJoinQuery.java:154-213).  Polygon q is replicated to
+// its keys K_q = G_q u C_q (JoinQuery.java:93-115): with B_q its bbox cells (Polygon.gridIDsSet),
+//   K_q = (g == 0 ? B_q : {}) u (c > 0 ? valid cells within Chebyshev c of B_q : {})
+// (G_q for g > 0 lies inside the c-neighbourhood since g < c).  Point p pairs with q iff p's
+// cell is in K_q and (approximate or JTS distance(p, q) <= r).  The scan (range_kernel with
+// DEFER == 2) queues every point whose cell is in some K_q; the two passes below walk each
+// queued point's cell list (CSR superset) with the exact key test -- count, then write at
+// block-scanned offsets.  Pairs are grouped by queued point; order otherwise unspecified.
+// =======================================================================================
+constexpr int kJoinKeep = 2;  // pairs per queued point kept by the count pass for the write pass
+struct JoinPolyOut {
+  uint32_t* ecnt;             // [queued entries] pairs per entry (count pass -> write pass)
+  uint32_t* ecand;            // [queued entries * kJoinKeep] the first pairs' polygon indices
+  uint32_t* btot;             // [gridDim.x] pairs per block
+  unsigned long long* total;  // pairs of the window
+  uint32_t* pairs;            // caller's (point index, polygon index) pairs
+  int64_t cap;
+  int aligned;
+};
+
+// Block b takes scan block b's queue segment (equal point ranges -> balanced segments), one
+// lane per queued point, so the per-point set-up (queue loads, cell, list bounds) is done
+// once, not by a group of lanes.  A lane walks its cell's polygon list 4 at a time (list and
+// bbox-cell loads batched before the tests: the walk is a chain of dependent loads otherwise).
+// Count pass: pairs per point (+ the first kJoinKeep polygon indices) and per block; write
+// pass: block offset = sum of the earlier blocks' counts, a block scan per round of kBlock
+// points, then the kept pairs are stored (points with more pairs walk their list again).
+__device__ __forceinline__ uint32_t block_scan_excl(uint32_t v, uint32_t* total, uint32_t* ws) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  uint32_t inc = v;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t t = __shfl_up(inc, off, 64);
+    if (lane >= off) inc += t;
+  }
+  if (lane == 63) ws[wid] = inc;
+  __syncthreads();
+  uint32_t before = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < kBlock / 64; ++w) {
+    before += w < wid ? ws[w] : 0u;
+    tot += ws[w];
+  }
+  *total = tot;
+  __syncthreads();
+  return before + inc - v;
+}
+
+// the polygons of (px, py)'s list that pair with it, in list order: sink(rank, q)
+template <class Sink>
+__device__ __forceinline__ uint32_t join_ppoly_walk(const RangeArgs& a, double px, double py, Sink&& sink) {
+  const int32_t cx = cell_index(px, a.minX, a.cl), cy = cell_index(py, a.minY, a.cl);
+  int32_t lb = 0, le = a.npoly;
+  const bool list = a.cand_off && cx >= 0 && cy >= 0 && cx < a.grid_n && cy < a.grid_n;
+  if (list) {
+    const int32_t cell = cy * a.grid_n + cx;
+    lb = a.cand_off[cell];
+    le = a.cand_off[cell + 1];
+  }
+  uint32_t n = 0;
+  for (int32_t t = lb; t < le; t += 4) {
+    int32_t q[4];
+    int4 br[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) q[u] = t + u < le ? (list ? a.cand_list[t + u] : t + u) : -1;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) br[u] = reinterpret_cast<const int4*>(a.brect)[q[u] < 0 ? 0 : q[u]];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (q[u] < 0) continue;
+      // p's key in K_q (see above), on the loaded bbox cells
+      const int4 b = br[u];
+      bool key = a.g_layers == 0 && cx >= b.x && cx <= b.y && cy >= b.z && cy <= b.w;
+      const int64_t c = a.c_layers;
+      key = key || (c > 0 && cx >= 0 && cy >= 0 && cx < a.grid_n && cy < a.grid_n && (int64_t)cx >= (int64_t)b.x - c &&
+                    (int64_t)cx <= (int64_t)b.y + c && (int64_t)cy >= (int64_t)b.z - c && (int64_t)cy <= (int64_t)b.w + c);
+      if (key && (a.approx || test_object<1>(a, px, py, q[u]))) sink(n++, q[u]);
+    }
+  }
+  return n;
+}
+
+template <int WRITE>
+__global__ __launch_bounds__(kBlock) void join_ppoly_kernel(RangeArgs a, JoinPolyOut o) {
+  __shared__ uint32_t ws[kBlock / 64];
+  __shared__ unsigned long long part[kBlock / 64];
+  const int lane = threadIdx.x & 63;
+  const uint32_t cnt = a.queue_count[blockIdx.x];
+  const size_t base = (size_t)blockIdx.x * a.seg_cap;
+  unsigned long long run = 0;
+  if (WRITE) {  // this block's output offset: sum of the earlier blocks' totals
+    unsigned long long sum = 0;
+    for (uint32_t i = threadIdx.x; i < blockIdx.x; i += kBlock) sum += o.btot[i];
+    for (int off = 32; off > 0; off >>= 1) sum += __shfl_down(sum, off, 64);
+    if (lane == 0) part[threadIdx.x >> 6] = sum;
+    __syncthreads();
+#pragma unroll
+    for (int w = 0; w < kBlock / 64; ++w) run += part[w];
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) *o.total = run + o.btot[blockIdx.x];
+  }
+  uint32_t bsum = 0;
+  for (uint32_t i0 = 0; i0 < cnt; i0 += kBlock) {  // block-uniform
+    const uint32_t i = i0 + threadIdx.x;
+    const bool valid = i < cnt;
+    const size_t pos = base + i;
+    if (WRITE) {
+      const uint32_t c = valid ? o.ecnt[pos] : 0u;
+      uint32_t tot;
+      const uint32_t ex = block_scan_excl(c, &tot, ws);
+      const unsigned long long at0 = run + ex;
+      run += tot;
+      if (c == 0) continue;
+      const uint32_t pidx = a.queue[pos];
+      auto put = [&](uint32_t k, int32_t q) {
+        if ((int64_t)(at0 + k) < o.cap) join_store(o.pairs, o.aligned, at0 + k, make_uint2(pidx, (uint32_t)q));
+      };
+      if (c <= (uint32_t)kJoinKeep) {
+        for (uint32_t k = 0; k < c; ++k) put(k, (int32_t)o.ecand[pos * kJoinKeep + k]);
+      } else {
+        join_ppoly_walk(a, a.queue_xy[2 * pos], a.queue_xy[2 * pos + 1], put);
+      }
+      continue;
+    }
+    if (!valid) continue;
+    const uint32_t n = join_ppoly_walk(a, a.queue_xy[2 * pos], a.queue_xy[2 * pos + 1], [&](uint32_t k, int32_t q) {
+      if (k < (uint32_t)kJoinKeep) o.ecand[pos * kJoinKeep + k] = (uint32_t)q;
+    });
+    o.ecnt[pos] = n;
+    bsum += n;
+  }
+  if (!WRITE) {
+    for (int off = 32; off > 0; off >>= 1) bsum += __shfl_down(bsum, off, 64);
+    if (lane == 0) ws[threadIdx.x >> 6] = bsum;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      uint32_t t = 0;
+#pragma unroll
+      for (int w = 0; w < kBlock / 64; ++w) t += ws[w];
+      o.btot[blockIdx.x] = t;
+    }
+  }
+}
+
+hipError_t launch_join_ppoly(gf_ctx* ctx, const RangeArgs& a, int blocks, int jblocks, uint32_t* ecnt, uint32_t* ecand,
+                             uint32_t* btot, unsigned long long* total, uint32_t* pairs, int64_t cap, int aligned) {
+  const size_t lds = 4 * kRangeHdrWords + sizeof(uint32_t) * (size_t)((2 * a.grid_n + 1) & ~1) +
+                     (a.xt ? 2 * sizeof(double) * (size_t)(a.grid_n + 1) : 0) +
+                     (a.span_lds ? (size_t)((a.span_bytes + 3) & ~3) : 0);
+  {
+    KTimer t(ctx, GF_K_RANGE_SCAN);
+    hipLaunchKernelGGL((range_kernel<1, 1, 2, kRangeU>), dim3(blocks), dim3(kBlock), lds, ctx->stream, a);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  KTimer t(ctx, GF_K_RANGE_TEST);
+  JoinPolyOut o{ecnt, ecand, btot, total, pairs, cap, aligned};
+  (void)jblocks;  // one block per scan block's queue segment
+  hipLaunchKernelGGL(join_ppoly_kernel<0>, dim3(blocks), dim3(kBlock), 0, ctx->stream, a, o);
+  hipLaunchKernelGGL(join_ppoly_kernel<1>, dim3(blocks), dim3(kBlock), 0, ctx->stream, a, o);
+  return hipGetLastError();
+}
 
 hipError_t launch_range(gf_ctx* ctx, const RangeArgs& a, int table_mode, int poly, int blocks) {
   const dim3 g(blocks), b(kBlock);

@@ -8,6 +8,7 @@ evaluates that window on the GPU through the C ABI -- the body of apply() is wha
   PointPolygonRangeQuery.run(window, Set<Polygon>, r) -- range/PointPolygonRangeQuery.java:31,134-205
   PointPointKNNQuery.run(window, Point, r, k)         -- knn/PointPointKNNQuery.java:33,132-201
   PointPointJoinQuery.run(ordinary, query, r)         -- join/PointPointJoinQuery.java:24,124-183
+  PointPolygonJoinQuery.run(points, polygons, r)      -- join/PointPolygonJoinQuery.java:154-213
 
 Errors follow the reference: unsupported query types raise ValueError ("Not yet support",
 IllegalArgumentException), candidate layers <= 0 raise CandidateLayersError (System.exit(1)).
@@ -424,6 +425,57 @@ class PointPointJoinQuery(SpatialOperator):
         raise _lib.GeoFlinkError(_lib.GF_ERR_CAPACITY, "join output kept growing")
 
 
+class PointPolygonJoinQuery(_RangeBase):
+    """join/PointPolygonJoinQuery.java -- window-based join of a point stream with a polygon
+    stream (PointPolygonJoinQuery.java:154-213; polygons replicated to their own guaranteed +
+    candidate cells, JoinQuery.java:93-115).  index1 = uGrid (points), index2 = qGrid
+    (polygons); the device path requires the two grids to be equal.  The replicated polygon
+    side is a plan, cached while the same polygon objects come back (a static query set);
+    a polygon stream's new window builds a new one."""
+
+    def __init__(self, conf: QueryConfiguration, index1: UniformGrid, index2: UniformGrid = None):
+        super().__init__(conf, index1)
+        self.index2 = index2 if index2 is not None else index1
+
+    def run(self, pointWindow: PointWindow, queryPolygons, queryRadius: float) -> np.ndarray:
+        """Returns int64 [m, 2] pairs (point index, polygon index), sorted."""
+        import torch
+
+        _require_supported(self.conf)
+        polys = list(queryPolygons)
+        ctx = _lib.context(pointWindow.x.device.index)
+        key = (ctx.device, tuple(id(p) for p in polys), float(queryRadius), bool(self.conf.approximateQuery),
+               int(self.conf.distanceMetric))
+
+        def create():
+            ps = PolygonSet(polys)  # keeps the CSR arrays alive during the call
+            cs = ps.c_struct()
+            h = C.c_void_p()
+            _lib.check(_lib.lib().gf_join_ppoly_plan_create(ctx.handle, C.byref(self.index2.c_grid), C.byref(cs),
+                                                            float(queryRadius), int(self.conf.approximateQuery),
+                                                            int(self.conf.distanceMetric), C.byref(h)),
+                       ctx.handle, "gf_join_ppoly_plan_create")
+            return h
+
+        plan = self._plan(key, create)
+        pts = pointWindow.c_struct()
+        cap = max(1024, 2 * pointWindow.n)
+        for _ in range(2):
+            pairs = torch.empty(2 * cap, dtype=torch.int32, device=pointWindow.x.device)
+            npairs = C.c_int64()
+            st = _lib.lib().gf_join_ppoly_run(plan, C.byref(self.index.c_grid), C.byref(pts), pairs.data_ptr(), cap,
+                                              C.byref(npairs))
+            if st == _lib.GF_ERR_CAPACITY:
+                cap = int(npairs.value)
+                continue
+            _lib.check(st, ctx.handle, "gf_join_ppoly_run")
+            m = int(npairs.value)
+            out = pairs[: 2 * m].cpu().numpy().view(np.uint32).astype(np.int64).reshape(-1, 2)
+            order = np.lexsort((out[:, 1], out[:, 0]))
+            return out[order]
+        raise _lib.GeoFlinkError(_lib.GF_ERR_CAPACITY, "join output kept growing")
+
+
 # ----------------------------------------------------------------------------------------
 # cell assignment / bucketing (the ingest-side pieces of the path)
 # ----------------------------------------------------------------------------------------
@@ -467,6 +519,6 @@ def synthetic_uniform(seed: int, n: int, minX: float, maxX: float, minY: float, 
 
 __all__ = [
     "QueryType", "QueryConfiguration", "PointPointRangeQuery", "PointPolygonRangeQuery", "PointPointKNNQuery",
-    "PointPointJoinQuery", "RangeResult", "KNNResult", "knn_merge_host", "assign_cells", "bucket_by_cell",
+    "PointPointJoinQuery", "PointPolygonJoinQuery", "RangeResult", "KNNResult", "knn_merge_host", "assign_cells", "bucket_by_cell",
     "synthetic_uniform", "Point", "Polygon", "PointWindow", "knn_record_bytes", "decode_knn_record",
 ]

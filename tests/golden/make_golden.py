@@ -115,8 +115,42 @@ def main():
             rec[f"r{r}_a{ap}"] = np.array(got, np.int64).reshape(-1, 2)
     np.savez(os.path.join(HERE, "join.npz"), **rec)
     out["join"] = len(rec)
+    out["join_ppoly"] = make_join_ppoly()
     print("fixtures written:", out)
 
 
+def join_ppoly_polygons():
+    """The range_ppoly set plus a square straddling the grid's lower-left corner (bbox cells
+    outside the grid: keys without validKey when g == 0)."""
+    polys = O.generate_query_polygons(40, 115.5, 39.6, 117.6, 41.1)
+    polys.append([[(116.0, 40.0), (116.3, 40.1), (116.1, 40.5), (116.0, 40.0)],
+                  [(116.05, 40.05), (116.15, 40.1), (116.1, 40.2), (116.05, 40.05)]])
+    polys.append([[(116.5, 40.3), (116.9, 40.3), (116.9, 40.7), (116.7, 40.45), (116.5, 40.7), (116.5, 40.3)]])
+    polys.append([[(115.45, 39.55), (115.53, 39.55), (115.53, 39.63), (115.45, 39.63), (115.45, 39.55)]])
+    return polys
+
+
+def make_join_ppoly():
+    """PointPolygonJoinQuery fixtures: C oracle == pyref before anything is written."""
+    g = O.grid(100, *BEIJING)
+    pg = P.Grid(100, *BEIJING)
+    x, y = window(42, 3000, g)
+    polys = join_ppoly_polygons()
+    PP = O.Polygons(polys)
+    rec = {"x": x, "y": y, "ring_off": PP.ring_off, "vert_off": PP.vert_off, "vx": PP.vx, "vy": PP.vy}
+    for r in (0.001, 0.05, 0.3, 0.0):
+        for ap in (0, 1):
+            a = O.join_ppoly(g, g, x, y, PP, r, bool(ap))
+            got = sorted(map(tuple, a.tolist()))
+            ref = P.join_ppoly(pg, pg, x.tolist(), y.tolist(), polys, r, bool(ap))
+            assert got == ref, (r, ap, len(got), len(ref))
+            rec[f"r{r}_a{ap}"] = np.array(got, np.int64).reshape(-1, 2)
+    np.savez(os.path.join(HERE, "join_ppoly.npz"), **rec)
+    return len(rec)
+
+
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:] == ["join_ppoly"]:
+        print("fixtures written:", {"join_ppoly": make_join_ppoly()})
+    else:
+        main()

@@ -7,6 +7,7 @@ inputs only (pure-Python loops).  Follows the same reference files:
   PointPointRangeQuery.java:111-187; PointPolygonRangeQuery.java:134-205;
   PointPointKNNQuery.java:132-201 + KNNQuery.java:213-272 (build contract, A7);
   JoinQuery.java:73-90 + PointPointJoinQuery.java:124-183;
+  JoinQuery.java:93-115 + PointPolygonJoinQuery.java:154-213;
   JTS 1.16.1 DistanceOp / Distance.pointToSegment / RayCrossingCounter (restated).
 Exact orientation signs use fractions.Fraction (not the oracle's expansion arithmetic).
 Metric: sqrt(dx*dx + dy*dy) only.
@@ -320,3 +321,31 @@ def join_pp(ugrid, qgrid, oxs, oys, qxs, qys, r, approximate=False):
             if approximate or dist(x, y, qxs[q], qys[q]) <= r:
                 out.append((p, q))
     return out
+
+
+def join_ppoly(ugrid, qgrid, xs, ys, polys, r, approximate=False):
+    """PointPolygonJoinQuery.windowBased: polygon q replicated to its own G_q u C_q
+    (getReplicatedPolygonQueryStream), point p joined on its gridID, kept if approximate or
+    getDistance(p, q) <= r.  Returns sorted (point, polygon) pairs."""
+    polys = [[_close(rg) for rg in p] for p in polys]
+    buckets = {}
+    for q, p in enumerate(polys):
+        sx = [v[0] for v in p[0]]
+        sy = [v[1] for v in p[0]]
+        x1, y1 = qgrid.cell(min(sx), min(sy))
+        x2, y2 = qgrid.cell(max(sx), max(sy))
+        ids = [cell_id(a, b) for a in range(x1, x2 + 1) for b in range(y1, y2 + 1)]
+        Gq = set()
+        for cid in ids:
+            Gq |= g_set(qgrid, r, cid)
+        Cq = set()
+        for cid in ids:
+            Cq |= c_set(qgrid, r, cid, Gq)
+        for k in Gq | Cq:
+            buckets.setdefault(k, []).append(q)
+    out = []
+    for i, (x, y) in enumerate(zip(xs, ys)):
+        for q in buckets.get(cell_id(*ugrid.cell(x, y)), ()):
+            if approximate or point_polygon_distance(x, y, polys[q]) <= r:
+                out.append((i, q))
+    return sorted(out)

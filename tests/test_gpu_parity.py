@@ -694,3 +694,85 @@ def test_join_dense_spot_and_capacity(sf, oracle_mod):
     got = big[1:1 + 2 * len(exp)].cpu().numpy().view(np.uint32).astype(np.int64).reshape(-1, 2)
     np.testing.assert_array_equal(got[np.lexsort((got[:, 1], got[:, 0]))], exp)
     assert big[0].item() == 0 and big[-1].item() == 0  # nothing written outside the buffer
+
+
+# ------------------------------------------------------------------ point-polygon join
+def test_join_ppoly_golden(sf):
+    f = load("join_ppoly.npz")
+    g = sf.UniformGrid(100, *BEIJING)
+    polys = golden_polygons(sf, f, g)
+    w = win(sf, f["x"], f["y"])
+    for r in (0.001, 0.05, 0.3, 0.0):
+        for ap in (0, 1):
+            got = sf.PointPolygonJoinQuery(conf(sf, bool(ap)), g, g).run(w, polys, r)
+            np.testing.assert_array_equal(got, f[f"r{r}_a{ap}"], err_msg=f"r={r} ap={ap}")
+
+
+@pytest.mark.parametrize("n,r,metric", [(500, 0.001, 0), (100, 0.05, 0), (500, 0.01, 1), (1000, 0.004, 0)])
+def test_join_ppoly_generated_1000(sf, oracle_mod, n, r, metric):
+    """C3's 1000 query polygons as the polygon side of the join, test-sized point window."""
+    g = sf.UniformGrid(n, *BEIJING)
+    og = oracle_mod.grid(n, *BEIJING)
+    raw = oracle_mod.generate_query_polygons(1000, 115.5, 39.6, 117.6, 41.1)
+    polys = [sf.Polygon(p, g) for p in raw]
+    x, y = oracle_mod.java_random_points(33, 200_000, 115.45, 115.75, *BEIJING[2:])
+    w = win(sf, x, y)
+    for ap in (False, True):
+        got = sf.PointPolygonJoinQuery(conf(sf, ap, metric), g, g).run(w, polys, r)
+        exp = oracle_mod.join_ppoly(og, og, x, y, oracle_mod.Polygons(raw), r, ap, metric)
+        exp = np.array(sorted(map(tuple, exp.tolist())), np.int64).reshape(-1, 2)
+        assert len(exp) > 0
+        np.testing.assert_array_equal(got, exp, err_msg=f"approximate={ap}")
+
+
+def test_join_ppoly_capacity_empty_and_grid_mismatch(sf, oracle_mod):
+    import ctypes as C
+
+    import torch
+    from spatialflink_amd import _lib
+
+    g = sf.UniformGrid(100, *BEIJING)
+    og = oracle_mod.grid(100, *BEIJING)
+    raw = oracle_mod.generate_query_polygons(100, 115.5, 39.6, 117.6, 41.1)
+    polys = [sf.Polygon(p, g) for p in raw]
+    x, y = oracle_mod.java_random_points(35, 50_000, *BEIJING)
+    w = win(sf, x, y)
+    exp = oracle_mod.join_ppoly(og, og, x, y, oracle_mod.Polygons(raw), 0.05)
+    ctx = _lib.context(0)
+    L = _lib.lib()
+    ps = sf.PolygonSet(polys)
+    cs = ps.c_struct()
+    h = C.c_void_p()
+    _lib.check(L.gf_join_ppoly_plan_create(ctx.handle, C.byref(g.c_grid), C.byref(cs), 0.05, 0, 0, C.byref(h)),
+               ctx.handle, "plan")
+    try:
+        pts = w.c_struct()
+        npairs = C.c_int64()
+        # counting call (no buffer), then a too-small buffer, then the right size
+        assert L.gf_join_ppoly_run(h, C.byref(g.c_grid), C.byref(pts), None, 0, C.byref(npairs)) == _lib.GF_ERR_CAPACITY
+        assert npairs.value == len(exp)
+        small = torch.empty(2 * 10, dtype=torch.int32, device="cuda")
+        assert L.gf_join_ppoly_run(h, C.byref(g.c_grid), C.byref(pts), small.data_ptr(), 10,
+                                   C.byref(npairs)) == _lib.GF_ERR_CAPACITY
+        assert npairs.value == len(exp)
+        full = torch.empty(2 * len(exp), dtype=torch.int32, device="cuda")
+        assert L.gf_join_ppoly_run(h, C.byref(g.c_grid), C.byref(pts), full.data_ptr(), len(exp), C.byref(npairs)) == 0
+        got = full.cpu().numpy().view(np.uint32).astype(np.int64).reshape(-1, 2)
+        assert sorted(map(tuple, got.tolist())) == sorted(map(tuple, exp.tolist()))
+        # empty window
+        e = win(sf, np.zeros(0), np.zeros(0)).c_struct()
+        assert L.gf_join_ppoly_run(h, C.byref(g.c_grid), C.byref(e), full.data_ptr(), 4, C.byref(npairs)) == 0
+        assert npairs.value == 0
+        # the point grid must equal the polygon grid; a range plan is not a join plan
+        g2 = sf.UniformGrid(101, *BEIJING)
+        assert L.gf_join_ppoly_run(h, C.byref(g2.c_grid), C.byref(pts), full.data_ptr(), 4,
+                                   C.byref(npairs)) == _lib.GF_ERR_ARG
+    finally:
+        L.gf_range_plan_destroy(h)
+    # the one-shot entry point
+    npairs = C.c_int64()
+    full = torch.empty(2 * len(exp), dtype=torch.int32, device="cuda")
+    pts = w.c_struct()
+    assert L.gf_join_ppoly(ctx.handle, C.byref(g.c_grid), C.byref(g.c_grid), C.byref(pts), C.byref(cs), 0.05, 0, 0,
+                           full.data_ptr(), len(exp), C.byref(npairs)) == 0
+    assert npairs.value == len(exp)

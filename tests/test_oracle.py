@@ -176,3 +176,42 @@ def test_hypot_basics(oracle_mod):
     x = np.random.default_rng(1).uniform(-1, 1, (2000, 2))
     for a, b in x:
         assert abs(O.hypot(a, b) - np.hypot(a, b)) <= 2 * np.spacing(np.hypot(a, b))
+
+
+def _fixture_polygons(oracle_mod, f):
+    P = oracle_mod.Polygons([])
+    P.ring_off, P.vert_off, P.vx, P.vy = f["ring_off"], f["vert_off"], f["vx"], f["vy"]
+    P.c = oracle_mod.OrcPolygons(len(P.ring_off) - 1, P.ring_off.ctypes.data, P.vert_off.ctypes.data,
+                                 P.vx.ctypes.data, P.vy.ctypes.data)
+    return P
+
+
+def test_join_ppoly_golden(oracle_mod):
+    """PointPolygonJoinQuery (JoinQuery.java:93-115, PointPolygonJoinQuery.java:154-213): the
+    fixture was cross-checked against tests/golden/pyref.py when written."""
+    f = load("join_ppoly.npz")
+    g = oracle_mod.grid(100, *BEIJING)
+    P = _fixture_polygons(oracle_mod, f)
+    for r in (0.001, 0.05, 0.3, 0.0):
+        for ap in (0, 1):
+            got = oracle_mod.join_ppoly(g, g, f["x"], f["y"], P, r, bool(ap))
+            got = np.array(sorted(map(tuple, got.tolist())), np.int64).reshape(-1, 2)
+            np.testing.assert_array_equal(got, f[f"r{r}_a{ap}"], err_msg=f"r={r} ap={ap}")
+
+
+def test_join_ppoly_own_guaranteed_set(oracle_mod):
+    """A polygon's candidate keys exclude only its OWN guaranteed cells (the replicated stream
+    is per polygon), unlike the range query's global G: with two overlapping polygons every
+    key of each is replicated, so a point in a cell guaranteed for one polygon still pairs with
+    the other when within r."""
+    import pyref as PR
+
+    g = oracle_mod.grid(50, *BEIJING)
+    pg = PR.Grid(50, *BEIJING)
+    polys = [[[(116.0, 40.0), (116.2, 40.0), (116.2, 40.2), (116.0, 40.2), (116.0, 40.0)]],
+             [[(116.25, 40.0), (116.4, 40.0), (116.4, 40.2), (116.25, 40.0)]]]
+    x, y = oracle_mod.java_random_points(9, 3000, 115.9, 116.5, 39.9, 40.3)
+    for r in (0.05, 0.13):
+        got = sorted(map(tuple, oracle_mod.join_ppoly(g, g, x, y, oracle_mod.Polygons(polys), r).tolist()))
+        assert got == PR.join_ppoly(pg, pg, x.tolist(), y.tolist(), polys, r)
+        assert {q for _, q in got} == {0, 1}

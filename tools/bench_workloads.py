@@ -295,6 +295,91 @@ def bench_join(args):
            "pairs_per_s": round(pp_all * args.steps / elapsed, 1)}, rank=rank)
 
 
+def bench_pjoin(args):
+    """Point-polygon window join (PointPolygonJoinQuery): the C3 shapes --
+    the 1000 generateQueryPolygons squares as the polygon side, 10M points per window, 500 x 500
+    grid, r = 0.001.  A step = one window: scan (every point whose cell some polygon replicates
+    to is queued) + count pass + write pass + the pair count read back (sync).  N > 1: weak
+    scaling, points sharded by cell-column bands, polygons replicated, no collective."""
+    import torch
+
+    import spatialflink_amd as sf
+    from spatialflink_amd import _lib
+
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+
+    world, rank, dev = _dist(args)
+    L = _lib.lib()
+    n = args.points or 10_000_000
+    grid_n = 500
+    grid = sf.UniformGrid(grid_n, *BEIJING)
+    og = O.grid(grid_n, *BEIJING)
+    nwin = 4
+    wins = _windows(sf, n, nwin, 17 + 1000 * rank, dev, _band(sf, grid, grid_n, world, rank))
+    ctx = _lib.context(dev)
+    r = 0.001
+    raw = O.generate_query_polygons(1000, BEIJING[0], BEIJING[2], BEIJING[1], BEIJING[3])
+    polys = [sf.Polygon(rings, grid) for rings in raw]
+    ps = sf.PolygonSet(polys)
+    cs = ps.c_struct()
+    h = C.c_void_p()
+    _lib.check(L.gf_join_ppoly_plan_create(ctx.handle, C.byref(grid.c_grid), C.byref(cs), r, 0, 0, C.byref(h)),
+               ctx.handle, "plan")
+    cap = max(1 << 20, n // 4)
+    pairs = torch.empty(2 * cap, dtype=torch.int32, device=dev)
+    npairs = C.c_int64()
+    pts = [w[2].c_struct() for w in wins]
+    counts = [0] * nwin
+
+    def step(i):
+        _lib.check(L.gf_join_ppoly_run(h, C.byref(grid.c_grid), C.byref(pts[i % nwin]), pairs.data_ptr(), cap,
+                                       C.byref(npairs)), ctx.handle, "gf_join_ppoly_run")
+        counts[i % nwin] = npairs.value
+
+    for i in range(args.warmup):
+        step(i)
+    _sync(world)
+    ctx.set_timing((1 << _lib.K_RANGE_SCAN) | (1 << _lib.K_RANGE_TEST))
+    _sync(world)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(i)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.barrier()
+    elapsed = _reduce(elapsed, world, args, dev)
+    ms, cnt = ctx.timing(_lib.K_RANGE_SCAN)
+    tms, tcnt = ctx.timing(_lib.K_RANGE_TEST)
+    ctx.set_timing(0)
+    verified = None
+    if not args.no_verify:  # first 1M points of window 0 (pairs are per point) vs the oracle
+        step(0)
+        m = min(n, 1_000_000)
+        got = pairs[: 2 * npairs.value].cpu().numpy().view(np.uint32).astype(np.int64).reshape(-1, 2)
+        got = sorted(map(tuple, got[got[:, 0] < m].tolist()))
+        x, y, _ = wins[0]
+        exp = sorted(map(tuple, O.join_ppoly(og, og, x[:m], y[:m], O.Polygons(raw), r).tolist()))
+        verified = bool(_reduce(float(got == exp), world, args, dev, op="min"))
+    L.gf_range_plan_destroy(h)
+    avg_scan = ms / 1000.0 / max(cnt, 1)
+    avg_test = tms / 1000.0 / max(tcnt, 1)
+    pp = float(np.mean(counts))
+    wl = f"join_ppoly_{len(polys)}polys_r{r}_{n // 1_000_000}Mpts_grid{grid_n}" + (f"_per_gpu_x{world}" if world > 1 else "")
+    _line("point-polygon join", world * n * args.steps / elapsed, "points/s", args.steps, args.warmup, elapsed,
+          "range_kernel (join queue) + join_ppoly count/write", 16.0 * n + 8.0 * pp, avg_scan + avg_test,
+          {"n_gpus": world,
+           "config": {"workload": wl, "points_per_window": n * world, "points_per_gpu": n, "grid": grid_n, "radius": r,
+                      "polygons": len(polys), "pairs_per_window_rank0": pp,
+                      "parallelism": f"cell-column shards x{world} (no collective)"},
+           "breakdown": {"scan_us": round(avg_scan * 1e6, 2), "count_write_us": round(avg_test * 1e6, 2)},
+           "verified_vs_oracle": verified, "verified_sample": f"first {min(n, 1_000_000)} points of window 0"},
+          rank=rank)
+
+
 def bench_sliding(args):
     """C5: sliding-window kNN, k = 100, 1000 x 1000 grid, 100M points per window, size/slide = 2
     (panes of 50M points), r = 0.5 around the README query point.  A step = one slide: one pane
@@ -707,6 +792,8 @@ def run(args):
         bench_range(args, polygons=args.workload == "ppoly")
     elif args.workload == "join":
         bench_join(args)
+    elif args.workload == "pjoin":
+        bench_pjoin(args)
     elif args.workload == "sliding":
         bench_sliding(args)
     elif args.workload == "csv":
