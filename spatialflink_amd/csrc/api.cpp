@@ -667,7 +667,7 @@ extern "C" void gf_range_plan_destroy(gf_range_plan* P) {
   hipStreamSynchronize(P->ctx->stream);
   void* bufs[] = {P->table, P->extra, P->cand_off, P->cand_list, P->qx, P->qy, P->ring_off, P->vert_off,
                   P->vx, P->vy, P->bbox, P->ring_env, P->partials, P->queue, P->queue_count, P->queue_xy, P->rows, P->xt, P->yt,
-                  P->rowoff, P->spans, P->brect, P->jecnt, P->jecand, P->jbtot, P->jtotal};
+                  P->rowoff, P->spans, P->brect, P->rect, P->jecnt, P->jecand, P->jbtot, P->jtotal};
   for (void* b : bufs)
     if (b) hipFree(b);
   delete P;
@@ -770,11 +770,12 @@ int ppoly_plan_create(gf_ctx* ctx, const gf_grid* g, const gf_polygons* polys, d
   // regions at distance 0 from each of their points: approximate mode -> every bbox;
   // exact mode -> shells that are axis-aligned rectangles without holes
   std::vector<std::array<double, 4>> inside;
+  std::vector<uint8_t> rectf((size_t)std::max(np, 1), 0);
   for (int32_t p = 0; p < np; ++p) {
     const double x1 = bbox[4 * p], y1 = bbox[4 * p + 1], x2 = bbox[4 * p + 2], y2 = bbox[4 * p + 3];
     if (!(x1 < x2 && y1 < y2)) continue;
-    bool rect = P->approx != 0;
-    if (!rect && polys->ring_off[p + 1] - polys->ring_off[p] == 1) {
+    bool rect = false;
+    if (polys->ring_off[p + 1] - polys->ring_off[p] == 1) {
       const int32_t v0 = polys->vert_off[polys->ring_off[p]], v1 = polys->vert_off[polys->ring_off[p] + 1];
       int corners = 0;
       rect = (v1 - v0 == 5);
@@ -786,7 +787,8 @@ int ppoly_plan_create(gf_ctx* ctx, const gf_grid* g, const gf_polygons* polys, d
       }
       rect = rect && corners == 15;
     }
-    if (rect) inside.push_back({x1, y1, x2, y2});
+    rectf[p] = rect;
+    if (rect || P->approx) inside.push_back({x1, y1, x2, y2});
   }
   P->join = join;
   if ((st = build_table(P, base, true, join ? nullptr : &inside, join != 0))) { gf_range_plan_destroy(P); return st; }
@@ -805,7 +807,8 @@ int ppoly_plan_create(gf_ctx* ctx, const gf_grid* g, const gf_polygons* polys, d
   std::vector<int32_t> ro(polys->ring_off, polys->ring_off + np + 1), vo(polys->vert_off, polys->vert_off + nrings + 1);
   std::vector<double> vx(polys->vx, polys->vx + nverts), vy(polys->vy, polys->vy + nverts);
   if ((st = upload(ctx, &P->ring_off, ro)) || (st = upload(ctx, &P->vert_off, vo)) || (st = upload(ctx, &P->vx, vx)) ||
-      (st = upload(ctx, &P->vy, vy)) || (st = upload(ctx, &P->bbox, bbox)) || (st = upload(ctx, &P->ring_env, renv))) {
+      (st = upload(ctx, &P->vy, vy)) || (st = upload(ctx, &P->bbox, bbox)) || (st = upload(ctx, &P->ring_env, renv)) ||
+      (st = upload(ctx, &P->rect, rectf))) {
     gf_range_plan_destroy(P);
     return st;
   }
@@ -846,7 +849,7 @@ RangeArgs range_args(const gf_range_plan* P, const gf_points* pts, uint64_t* bit
   a.qx0 = P->qx0; a.qy0 = P->qy0;
   a.qx = P->qx; a.qy = P->qy;
   a.npoly = P->npoly; a.ring_off = P->ring_off; a.vert_off = P->vert_off; a.vx = P->vx; a.vy = P->vy;
-  a.bbox = P->bbox; a.ring_env = P->ring_env;
+  a.bbox = P->bbox; a.ring_env = P->ring_env; a.rect = P->rect;
   a.brect = P->brect; a.g_layers = P->g_layers; a.c_layers = P->c_layers;
   return a;
 }
@@ -873,7 +876,7 @@ int ensure_queue(gf_range_plan* P, RangeArgs& a, int blocks, bool with_counts) {
     GF_HIP_CHECK(ctx, hipMalloc(&P->queue_xy, 2 * sizeof(double) * (size_t)cap));
     if (with_counts) {
       GF_HIP_CHECK(ctx, hipMalloc(&P->jecnt, sizeof(uint32_t) * (size_t)cap));
-      GF_HIP_CHECK(ctx, hipMalloc(&P->jecand, 2 * sizeof(uint32_t) * (size_t)cap));
+      GF_HIP_CHECK(ctx, hipMalloc(&P->jecand, 4 * sizeof(uint32_t) * (size_t)cap));  // kJoinKeep
     }
     P->queue_cap = cap;
   }

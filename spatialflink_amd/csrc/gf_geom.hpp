@@ -92,7 +92,14 @@ static __device__ inline double env_point_distance(const double* e, double px, d
 // DistanceOp(point, polygon): containment (shell, holes), then min facet distance
 static __device__ __noinline__ double polygon_distance(double px, double py, const PolyView& a, int p) {
   const int r0 = a.ring_off[p], r1 = a.ring_off[p + 1];
-  if (px == px) {  // NaN x: containment skipped (documented; matches the oracle)
+  if (a.rect && a.rect[p]) {
+    // one-ring axis-aligned rectangle: PointLocator's interior-or-boundary is exactly the
+    // closed box (every orientation sign against an axis-aligned edge is a plain comparison);
+    // outside it, the same facet loop as below (a NaN coordinate fails the box and lands there
+    // too, as it does on the general path)
+    const double* e = a.ring_env + 4 * r0;
+    if (px >= e[0] && px <= e[1] && py >= e[2] && py <= e[3]) return 0.0;
+  } else if (px == px) {  // NaN x: containment skipped (documented; matches the oracle)
     const int v0 = a.vert_off[r0], nv = a.vert_off[r0 + 1] - v0;
     const int loc = locate_in_ring(px, py, a.vx + v0, a.vy + v0, nv, a.ring_env + 4 * r0);
     if (loc == kLocBoundary) return 0.0;

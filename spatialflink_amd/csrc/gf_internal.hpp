@@ -128,6 +128,7 @@ struct PolyView {
   const double* vy;
   const double* ring_env;  // [nrings*4] minx, maxx, miny, maxy
   int metric;
+  const uint8_t* rect;     // [npoly] 1: one-ring axis-aligned rectangle (nullable)
 };
 
 // polygon-query kNN (PointPolygonKNNQuery): scan / sample arguments
@@ -215,6 +216,7 @@ struct RangeArgs {
   double* queue_xy;          // [2 * blocks * seg_cap] the queued points' coordinates
   int64_t seg_cap;           // points one scan block visits at most
   int test_blocks;
+  const uint8_t* rect;       // [npoly] axis-aligned rectangle shells without holes (nullable)
   // point-polygon join: bbox cells per polygon (x0, x1, y0, y1) and the layer counts
   const int32_t* brect;
   int32_t g_layers, c_layers;
@@ -466,8 +468,9 @@ struct gf_range_plan {
   // point-polygon join plans (gf_join_ppoly_plan_create)
   int join = 0;
   int32_t* brect = nullptr;        // [npoly * 4] bbox cells x0, x1, y0, y1
+  uint8_t* rect = nullptr;         // [npoly] 1: axis-aligned rectangle shell, no holes
   uint32_t* jecnt = nullptr;       // [queue_cap] pairs per queued point
-  uint32_t* jecand = nullptr;      // [queue_cap * 2] their first polygon indices
+  uint32_t* jecand = nullptr;      // [queue_cap * 4] their first polygon indices (kJoinKeep)
   uint32_t* jbtot = nullptr;       // [num_cus * 8] pairs per join block
   unsigned long long* jtotal = nullptr;
 };

@@ -21,7 +21,7 @@ namespace gf {
 
 // DistanceOp(point, polygon) of polygon p of the plan's set (gf_geom.hpp)
 __device__ __forceinline__ double point_polygon_distance(double px, double py, const RangeArgs& a, int p) {
-  return polygon_distance(px, py, PolyView{a.ring_off, a.vert_off, a.vx, a.vy, a.ring_env, a.metric}, p);
+  return polygon_distance(px, py, PolyView{a.ring_off, a.vert_off, a.vx, a.vy, a.ring_env, a.metric, a.rect}, p);
 }
 
 // ---------------- classification --------------------------------------------------------
@@ -506,7 +506,8 @@ constexpr int kRangeU = GF_RANGE_U;  // tiles (of 128 points per wave) per main-
 // queued point's cell list (CSR superset) with the exact key test -- count, then write at
 // block-scanned offsets.  Pairs are grouped by queued point; order otherwise unspecified.
 // =======================================================================================
-constexpr int kJoinKeep = 2;  // pairs per queued point kept by the count pass for the write pass
+constexpr int kJoinKeep = 4;  // pairs per queued point kept by the count pass for the write pass (a corner point of
+                              // four adjacent squares has 4; more re-walk the list in the write pass)
 struct JoinPolyOut {
   uint32_t* ecnt;             // [queued entries] pairs per entry (count pass -> write pass)
   uint32_t* ecand;            // [queued entries * kJoinKeep] the first pairs' polygon indices
@@ -586,6 +587,9 @@ __global__ __launch_bounds__(kBlock) void join_ppoly_kernel(RangeArgs a, JoinPol
   const int lane = threadIdx.x & 63;
   const uint32_t cnt = a.queue_count[blockIdx.x];
   const size_t base = (size_t)blockIdx.x * a.seg_cap;
+#ifdef GF_EXP_J4
+  if (threadIdx.x == 0 && (blockIdx.x % 256) == 0) printf("block %u cnt %u seg_cap %lld\n", blockIdx.x, cnt, (long long)a.seg_cap);
+#endif
   unsigned long long run = 0;
   if (WRITE) {  // this block's output offset: sum of the earlier blocks' totals
     unsigned long long sum = 0;
@@ -621,6 +625,9 @@ __global__ __launch_bounds__(kBlock) void join_ppoly_kernel(RangeArgs a, JoinPol
       continue;
     }
     if (!valid) continue;
+#ifdef GF_EXP_J3
+    if (pos < (size_t)-1) { o.ecnt[pos] = 0; continue; }
+#endif
     const uint32_t n = join_ppoly_walk(a, a.queue_xy[2 * pos], a.queue_xy[2 * pos + 1], [&](uint32_t k, int32_t q) {
       if (k < (uint32_t)kJoinKeep) o.ecand[pos * kJoinKeep + k] = (uint32_t)q;
     });
