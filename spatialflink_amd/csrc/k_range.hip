@@ -647,6 +647,121 @@ __global__ __launch_bounds__(kBlock) void join_ppoly_kernel(RangeArgs a, JoinPol
   }
 }
 
+// Count pass.  Phase A, one lane per queued point: walk the cell list with the key test, the
+// envelope prune and -- for rectangles -- the closed-box test; every other surviving pair needs
+// the exact JTS distance and goes to a block worklist in LDS.  Phase B: the whole block
+// computes the worklist's distances densely (a lane-per-point walk would run each wave's
+// distance calls once per lane that needs one).  A point whose pairs overflow the worklist is
+// recounted by its own full walk.  Ranks inside a point come from LDS atomics (pair order is
+// unspecified); the set equals join_ppoly_walk's.
+constexpr int kJoinWork = 4 * kBlock;  // worklist entries per round
+__global__ __launch_bounds__(kBlock) void join_ppoly_count_kernel(RangeArgs a, JoinPolyOut o) {
+  __shared__ uint32_t ws[kBlock / 64];
+  __shared__ uint32_t pcnt[kBlock];
+  __shared__ uint8_t slow[kBlock];
+  __shared__ double2 pxy[kBlock];
+  __shared__ uint16_t wl_slot[kJoinWork];
+  __shared__ int32_t wl_poly[kJoinWork];
+  __shared__ uint32_t wl_n;
+  const int lane = threadIdx.x & 63;
+  const uint32_t cnt = a.queue_count[blockIdx.x];
+  const size_t base = (size_t)blockIdx.x * a.seg_cap;
+  uint32_t bsum = 0;
+  for (uint32_t i0 = 0; i0 < cnt; i0 += kBlock) {  // block-uniform
+    const uint32_t i = i0 + threadIdx.x;
+    const bool valid = i < cnt;
+    const size_t pos = base + i;
+    if (threadIdx.x == 0) wl_n = 0u;
+    slow[threadIdx.x] = 0;
+    __syncthreads();
+    uint32_t n = 0;  // pairs found without the exact distance
+    bool over = false;
+    double px = 0.0, py = 0.0;
+    if (valid) {
+      px = a.queue_xy[2 * pos];
+      py = a.queue_xy[2 * pos + 1];
+      pxy[threadIdx.x] = make_double2(px, py);
+      const bool finite = px == px && py == py;
+      const int32_t cx = cell_index(px, a.minX, a.cl), cy = cell_index(py, a.minY, a.cl);
+      int32_t lb = 0, le = a.npoly;
+      const bool list = a.cand_off && cx >= 0 && cy >= 0 && cx < a.grid_n && cy < a.grid_n;
+      if (list) {
+        const int32_t cell = cy * a.grid_n + cx;
+        lb = a.cand_off[cell];
+        le = a.cand_off[cell + 1];
+      }
+      for (int32_t t = lb; t < le; t += 4) {
+        int32_t q[4];
+        int4 br[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) q[u] = t + u < le ? (list ? a.cand_list[t + u] : t + u) : -1;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) br[u] = reinterpret_cast<const int4*>(a.brect)[q[u] < 0 ? 0 : q[u]];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          if (q[u] < 0) continue;
+          const int4 b = br[u];
+          bool key = a.g_layers == 0 && cx >= b.x && cx <= b.y && cy >= b.z && cy <= b.w;
+          const int64_t c = a.c_layers;
+          key = key || (c > 0 && cx >= 0 && cy >= 0 && cx < a.grid_n && cy < a.grid_n &&
+                        (int64_t)cx >= (int64_t)b.x - c && (int64_t)cx <= (int64_t)b.y + c &&
+                        (int64_t)cy >= (int64_t)b.z - c && (int64_t)cy <= (int64_t)b.w + c);
+          if (!key) continue;
+          bool hit = a.approx != 0;
+          if (!hit) {
+            const double* bb = a.bbox + 4 * q[u];
+            if (finite && env_far(bb, px, py, a.r)) continue;
+            // rectangle shell: inside the closed box <=> distance 0 (<= r: keys exist only for r > 0)
+            hit = a.rect && a.rect[q[u]] && env_holds(bb, px, py);
+          }
+          if (hit) {
+            if (n < (uint32_t)kJoinKeep) o.ecand[pos * kJoinKeep + n] = (uint32_t)q[u];
+            ++n;
+          } else {
+            const uint32_t w = atomicAdd(&wl_n, 1u);
+            if (w < (uint32_t)kJoinWork) { wl_slot[w] = (uint16_t)threadIdx.x; wl_poly[w] = q[u]; }
+            else over = true;
+          }
+        }
+      }
+    }
+    pcnt[threadIdx.x] = n;
+    if (over) slow[threadIdx.x] = 1;
+    __syncthreads();
+    const uint32_t nw = wl_n < (uint32_t)kJoinWork ? wl_n : (uint32_t)kJoinWork;
+    for (uint32_t w = threadIdx.x; w < nw; w += kBlock) {  // phase B: dense exact distances
+      const uint32_t sl = wl_slot[w];
+      if (slow[sl]) continue;
+      const double2 v = pxy[sl];
+      const int32_t q = wl_poly[w];
+      if (point_polygon_distance(v.x, v.y, a, q) <= a.r) {
+        const uint32_t rk = atomicAdd(&pcnt[sl], 1u);
+        if (rk < (uint32_t)kJoinKeep) o.ecand[(base + i0 + sl) * kJoinKeep + rk] = (uint32_t)q;
+      }
+    }
+    __syncthreads();
+    uint32_t total = pcnt[threadIdx.x];
+    if (over)  // worklist overflow: this point's own full walk
+      total = join_ppoly_walk(a, px, py, [&](uint32_t k, int32_t q) {
+        if (k < (uint32_t)kJoinKeep) o.ecand[pos * kJoinKeep + k] = (uint32_t)q;
+      });
+    if (valid) {
+      o.ecnt[pos] = total;
+      bsum += total;
+    }
+    __syncthreads();  // pcnt / slow / worklist reused by the next round
+  }
+  for (int off = 32; off > 0; off >>= 1) bsum += __shfl_down(bsum, off, 64);
+  if (lane == 0) ws[threadIdx.x >> 6] = bsum;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t t = 0;
+#pragma unroll
+    for (int w = 0; w < kBlock / 64; ++w) t += ws[w];
+    o.btot[blockIdx.x] = t;
+  }
+}
+
 hipError_t launch_join_ppoly(gf_ctx* ctx, const RangeArgs& a, int blocks, int jblocks, uint32_t* ecnt, uint32_t* ecand,
                              uint32_t* btot, unsigned long long* total, uint32_t* pairs, int64_t cap, int aligned) {
   const size_t lds = 4 * kRangeHdrWords + sizeof(uint32_t) * (size_t)((2 * a.grid_n + 1) & ~1) +
@@ -661,7 +776,11 @@ hipError_t launch_join_ppoly(gf_ctx* ctx, const RangeArgs& a, int blocks, int jb
   KTimer t(ctx, GF_K_RANGE_TEST);
   JoinPolyOut o{ecnt, ecand, btot, total, pairs, cap, aligned};
   (void)jblocks;  // one block per scan block's queue segment
+#ifdef GF_EXP_JLANE
   hipLaunchKernelGGL(join_ppoly_kernel<0>, dim3(blocks), dim3(kBlock), 0, ctx->stream, a, o);
+#else
+  hipLaunchKernelGGL(join_ppoly_count_kernel, dim3(blocks), dim3(kBlock), 0, ctx->stream, a, o);
+#endif
   hipLaunchKernelGGL(join_ppoly_kernel<1>, dim3(blocks), dim3(kBlock), 0, ctx->stream, a, o);
   return hipGetLastError();
 }

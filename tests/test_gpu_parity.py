@@ -776,3 +776,26 @@ def test_join_ppoly_capacity_empty_and_grid_mismatch(sf, oracle_mod):
     assert L.gf_join_ppoly(ctx.handle, C.byref(g.c_grid), C.byref(g.c_grid), C.byref(pts), C.byref(cs), 0.05, 0, 0,
                            full.data_ptr(), len(exp), C.byref(npairs)) == 0
     assert npairs.value == len(exp)
+
+
+def test_join_ppoly_dense_overlap_worklist_overflow(sf, oracle_mod):
+    """60 overlapping triangles (not rectangles: every pair needs the exact JTS distance) over
+    the same spot: a block round's exact-distance worklist overflows and points are recounted
+    by their own walk; plus a polygon with a hole."""
+    g = sf.UniformGrid(200, *BEIJING)
+    og = oracle_mod.grid(200, *BEIJING)
+    raw = []
+    for k in range(60):
+        d = 0.0004 * k
+        raw.append([[(116.0 + d, 40.0), (116.08 + d, 40.01), (116.03, 40.07 + d), (116.0 + d, 40.0)]])
+    raw.append([[(116.0, 39.98), (116.12, 39.98), (116.12, 40.1), (116.0, 40.1), (116.0, 39.98)],
+                [(116.02, 40.0), (116.05, 40.0), (116.05, 40.03), (116.02, 40.03), (116.02, 40.0)]])
+    polys = [sf.Polygon(p, g) for p in raw]
+    x, y = oracle_mod.java_random_points(37, 60_000, 115.98, 116.15, 39.97, 40.12)
+    w = win(sf, x, y)
+    for r in (0.002, 0.02):
+        got = sf.PointPolygonJoinQuery(conf(sf), g, g).run(w, polys, r)
+        exp = oracle_mod.join_ppoly(og, og, x, y, oracle_mod.Polygons(raw), r)
+        exp = np.array(sorted(map(tuple, exp.tolist())), np.int64).reshape(-1, 2)
+        assert len(exp) > 100_000
+        np.testing.assert_array_equal(got, exp, err_msg=f"r={r}")
