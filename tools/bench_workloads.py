@@ -76,6 +76,10 @@ def _reduce_sum(v, world, args, dev):
     return float(t.item())
 
 
+def _cpu_line(value, unit, sample):
+    return {"value": round(value, 1), "unit": unit, "cores": 1, "kind": "port", "sample": sample}
+
+
 def _band(sf, grid, grid_n, world, rank):
     """x range of this rank's cell-column band (the whole grid at N = 1)."""
     from spatialflink_amd import sharding
@@ -190,10 +194,16 @@ def bench_range(args, polygons=False):
         hits = int(counts[0, 0].item())
         m = min(n, 1_000_000)
         x, y, _ = wins[0]
-        verified = None
+        verified, cpu = None, None
         if not args.no_verify:
+            tc = time.perf_counter()
             exp = (O.range_ppoly(og, x[:m], y[:m], O.Polygons(raw), r) if polygons
                    else O.range_pp(og, x[:m], y[:m], [QPOINT[0]], [QPOINT[1]], r))
+            tc = time.perf_counter() - tc
+            if world == 1 and not args.no_cpu_baseline:
+                cpu = _cpu_line(m / tc, "points/s", f"first {m} points of window 0, 1 pass ({tc:.2f}s): oracle's "
+                                "reference-shaped evaluator (string cell IDs, HashSet G/C filter, per-point JTS "
+                                "distance loop), C restatement of the Java operator, 1 thread")
             got = sf.spatialOperators.bitmap_indices(ctx, bitmaps[0], n).astype(np.int64)
             verified = bool(_reduce(float(np.array_equal(got[got < m], exp)), world, args, dev, op="min"))
         L.gf_range_plan_destroy(h)
@@ -213,7 +223,8 @@ def bench_range(args, polygons=False):
                           "parallelism": f"cell-column shards x{world} (no collective)",
                           "cells_none_candidate_guaranteed_inside": [c.value for c in cells]},
                "breakdown": {"scan_us": round(avg_scan * 1e6, 2), "test_us": round(avg_test * 1e6, 2)},
-               "verified_vs_oracle": verified, "verified_sample": f"first {m} points of window 0 on every rank"},
+               "verified_vs_oracle": verified, "verified_sample": f"first {m} points of window 0 on every rank",
+               **({"cpu_baseline": cpu} if cpu else {})},
               rank=rank)
 
 
@@ -282,6 +293,31 @@ def bench_join(args):
     avg = ms / 1000.0 / max(cnt, 1)
     pp = total_pairs / args.steps
     pp_all = pp if world == 1 else _reduce_sum(pp, world, args, dev)
+    # parity + CPU baseline (N = 1): pairs of the first 1M ordinary points of window 0 against
+    # the whole query window == the oracle's reference-shaped join of those points (pairs are
+    # per ordinary point), timed
+    verified, cpu = None, None
+    if world == 1 and not args.no_verify:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle as O
+
+        step(0)
+        m = min(no, 1_000_000)
+        got = pairs[: 2 * npairs.value].cpu().numpy().view(np.uint32).astype(np.int64).reshape(-1, 2)
+        got = got[got[:, 0] < m]
+        og = O.grid(grid_n, *BEIJING)
+        (x, y, _), (qx, qy, _) = ow[0], qw[0]
+        tc = time.perf_counter()
+        st, exp = O.join_pp(og, og, x[:m], y[:m], qx, qy, r)
+        tc = time.perf_counter() - tc
+        order = np.lexsort((got[:, 1], got[:, 0]))
+        eo = np.lexsort((exp[:, 1], exp[:, 0]))
+        verified = bool(st == 0 and np.array_equal(got[order], exp[eo]))
+        if not args.no_cpu_baseline:
+            cpu = _cpu_line((m + len(qx)) / tc, "points/s", f"first {m} ordinary points of window 0 x the {len(qx)} "
+                            f"query points, 1 pass ({tc:.2f}s): oracle's reference-shaped join (query points "
+                            "replicated to string keys, hash join on gridID, distance per co-located pair), "
+                            "C restatement, 1 thread")
     wl = f"join_pp_{no // 1_000_000}Mx{nq / 1e6:g}M_r{r}_grid1000" + (f"_per_gpu_x{world}" if world > 1 else "")
     _line("point-point join", world * (no + nq) * args.steps / elapsed, "points/s", args.steps, args.warmup, elapsed,
           "join_row_probe (single pass: row-bucketed ordinary xy + idx in, pairs out)", 20.0 * no + 8.0 * pp, avg,
@@ -292,7 +328,10 @@ def bench_join(args):
            "breakdown": {"probe_us_per_launch": round(avg * 1e6, 2), "probe_launches_per_window": cnt / args.steps,
                          "bucket_us_per_launch": round(bms * 1000.0 / max(bcnt, 1), 2),
                          "bucket_launches_per_window": bcnt / args.steps},
-           "pairs_per_s": round(pp_all * args.steps / elapsed, 1)}, rank=rank)
+           "pairs_per_s": round(pp_all * args.steps / elapsed, 1), "verified_vs_oracle": verified,
+           **({"verified_sample": f"pairs of the first {min(no, 1_000_000)} ordinary points of window 0"}
+              if verified is not None else {}),
+           **({"cpu_baseline": cpu} if cpu else {})}, rank=rank)
 
 
 def bench_pjoin(args):
@@ -355,14 +394,21 @@ def bench_pjoin(args):
     ms, cnt = ctx.timing(_lib.K_RANGE_SCAN)
     tms, tcnt = ctx.timing(_lib.K_RANGE_TEST)
     ctx.set_timing(0)
-    verified = None
+    verified, cpu = None, None
     if not args.no_verify:  # first 1M points of window 0 (pairs are per point) vs the oracle
         step(0)
         m = min(n, 1_000_000)
         got = pairs[: 2 * npairs.value].cpu().numpy().view(np.uint32).astype(np.int64).reshape(-1, 2)
         got = sorted(map(tuple, got[got[:, 0] < m].tolist()))
         x, y, _ = wins[0]
-        exp = sorted(map(tuple, O.join_ppoly(og, og, x[:m], y[:m], O.Polygons(raw), r).tolist()))
+        tc = time.perf_counter()
+        exp = O.join_ppoly(og, og, x[:m], y[:m], O.Polygons(raw), r)
+        tc = time.perf_counter() - tc
+        exp = sorted(map(tuple, exp.tolist()))
+        if world == 1 and not args.no_cpu_baseline:
+            cpu = _cpu_line(m / tc, "points/s", f"first {m} points of window 0 x the 1000 polygons, 1 pass ({tc:.2f}s): "
+                            "oracle's reference-shaped join (polygons replicated to string keys, hash join on "
+                            "gridID, JTS distance per co-located pair), C restatement, 1 thread")
         verified = bool(_reduce(float(got == exp), world, args, dev, op="min"))
     L.gf_range_plan_destroy(h)
     avg_scan = ms / 1000.0 / max(cnt, 1)
@@ -376,7 +422,8 @@ def bench_pjoin(args):
                       "polygons": len(polys), "pairs_per_window_rank0": pp,
                       "parallelism": f"cell-column shards x{world} (no collective)"},
            "breakdown": {"scan_us": round(avg_scan * 1e6, 2), "count_write_us": round(avg_test * 1e6, 2)},
-           "verified_vs_oracle": verified, "verified_sample": f"first {min(n, 1_000_000)} points of window 0"},
+           "verified_vs_oracle": verified, "verified_sample": f"first {min(n, 1_000_000)} points of window 0",
+           **({"cpu_baseline": cpu} if cpu else {})},
           rank=rank)
 
 
