@@ -675,12 +675,28 @@ __global__ __launch_bounds__(kBlock) void join_compact_kernel(JoinCompactArgs a)
   unsigned long long off = 0;
   for (int w = 0; w < kBlock / 64; ++w) off += part[w];
   if (blockIdx.x < a.ntask) {
-    const uint32_t n = a.task_cnt[blockIdx.x];
+    const uint32_t n0 = a.task_cnt[blockIdx.x];
+    const uint32_t n = off >= a.cap ? 0u : (uint32_t)(off + n0 > a.cap ? a.cap - off : n0);  // capacity clip
     const uint2* src = a.tpairs + (size_t)blockIdx.x * a.task_cap;
-    for (uint32_t i = threadIdx.x; i < n; i += kBlock) {
-      if (off + i >= a.cap) break;
-      const uint2 v = src[i];
-      join_store(a.pairs, a.pairs_aligned, off + i, make_uint2(v.x, a.sqidx[v.y]));
+    // kCompactU pairs per thread in flight: the region loads, then the slot -> index gathers,
+    // then the stores (one at a time, each gather stalled the loop on its L2 round trip: 87 -> 67 us
+    // per 10M x 1M window)
+    constexpr int kCompactU = 4;
+    for (uint32_t i0 = threadIdx.x; i0 < n; i0 += kBlock * kCompactU) {
+      uint2 v[kCompactU];
+      uint32_t q[kCompactU];
+#pragma unroll
+      for (int u = 0; u < kCompactU; ++u) {
+        const uint32_t i = i0 + u * kBlock;
+        v[u] = src[i < n ? i : i0];
+      }
+#pragma unroll
+      for (int u = 0; u < kCompactU; ++u) q[u] = a.sqidx[v[u].y];
+#pragma unroll
+      for (int u = 0; u < kCompactU; ++u) {
+        const uint32_t i = i0 + u * kBlock;
+        if (i < n) join_store(a.pairs, a.pairs_aligned, off + i, make_uint2(v[u].x, q[u]));
+      }
     }
     return;
   }
