@@ -1581,7 +1581,10 @@ extern "C" int gf_join_pp(gf_ctx* ctx, const gf_grid* ugrid, const gf_grid* qgri
   size_t o_txy = ar.take<double>(rowpath ? 2 * nq : 1), o_tc = ar.take<int32_t>(rowpath ? 2 * nq : 1);
   size_t o_tidx = ar.take<uint32_t>(rowpath ? nq : 1);
   const int64_t max_tasks = no / kJoinTask + qn + 1;
-  const int sblocks = (int)std::min<int64_t>(std::max<int64_t>(no / 8192, 1), (int64_t)ctx->num_cus * 4);
+#ifndef GF_JOIN_SBPC
+#define GF_JOIN_SBPC 4  // ordinary-side bucketing blocks per CU
+#endif
+  const int sblocks = (int)std::min<int64_t>(std::max<int64_t>(no / 8192, 1), (int64_t)ctx->num_cus * GF_JOIN_SBPC);
   const int64_t mat = rowpath ? qn * sblocks : 1;
   size_t o_rmat = ar.take<uint32_t>(mat), o_rmats = ar.take<uint32_t>(mat + 1), o_roff = ar.take<uint32_t>(qn + 1);
   size_t o_rtask = ar.take<uint32_t>(qn), o_toff = ar.take<uint32_t>(qn + 1);
