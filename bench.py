@@ -51,6 +51,8 @@ def main():
                     help="knn = the headline line (BASELINE configs[1]); range/ppoly/join/pjoin/sliding/csv/polyknn: tools/bench_workloads.py")
     ap.add_argument("--range-blocks", default="0", help="range/ppoly scan blocks, comma list = sweep (0 = auto)")
     ap.add_argument("--range-defer", default="0", help="range/ppoly candidate tests: 0 auto, 1 inline, 2 deferred (list = sweep)")
+    ap.add_argument("--range-streams", type=int, default=2,
+                    help="range/ppoly: consecutive windows alternate over this many contexts (HIP streams)")
     ap.add_argument("--k", type=int, default=50)
     ap.add_argument("--radius", type=float, default=0.5)
     ap.add_argument("--grid", type=int, default=500)
