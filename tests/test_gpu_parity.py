@@ -799,3 +799,47 @@ def test_join_ppoly_dense_overlap_worklist_overflow(sf, oracle_mod):
         exp = np.array(sorted(map(tuple, exp.tolist())), np.int64).reshape(-1, 2)
         assert len(exp) > 100_000
         np.testing.assert_array_equal(got, exp, err_msg=f"r={r}")
+
+
+def test_range_windows_in_flight_on_two_contexts(sf, oracle_mod):
+    """Consecutive windows alternating over two contexts (two HIP streams, two plans), as the
+    bench's --range-streams 2 runs them: every window's hits == the oracle's."""
+    import ctypes as C
+
+    import torch
+    from spatialflink_amd import _lib
+
+    L = _lib.lib()
+    g = sf.UniformGrid(100, *BEIJING)
+    og = oracle_mod.grid(100, *BEIJING)
+    qx, qy = np.array([QPOINT[0]]), np.array([QPOINT[1]])
+    ctxs = [_lib.Context(0), _lib.Context(0)]
+    plans = []
+    for c in ctxs:
+        h = C.c_void_p()
+        _lib.check(L.gf_range_pp_plan_create(c.handle, C.byref(g.c_grid), qx.ctypes.data, qy.ctypes.data, 1, 0.3, 0, 0,
+                                             C.byref(h)), c.handle, "plan")
+        plans.append(h)
+    try:
+        wins, exps = [], []
+        for j in range(6):
+            x, y = oracle_mod.java_random_points(70 + j, 300_000, *BEIJING)
+            wins.append(win(sf, x, y))
+            exps.append(oracle_mod.range_pp(og, x, y, qx, qy, 0.3))
+        torch.cuda.synchronize()
+        n = 300_000
+        bitmaps = torch.zeros(6, (n + 63) // 64, dtype=torch.int64, device="cuda")
+        counts = torch.zeros(6, 2, dtype=torch.int64, device="cuda")
+        pts = [w.c_struct() for w in wins]
+        for j in range(6):
+            _lib.check(L.gf_range_run(plans[j % 2], C.byref(pts[j]), bitmaps[j].data_ptr(), None, counts[j].data_ptr()),
+                       ctxs[j % 2].handle, "gf_range_run")
+        for c in ctxs:
+            c.synchronize()
+        for j in range(6):
+            got = sf.spatialOperators.bitmap_indices(ctxs[0], bitmaps[j], n).astype(np.int64)
+            np.testing.assert_array_equal(got, exps[j], err_msg=f"window {j}")
+            assert int(counts[j, 0].item()) == len(exps[j])
+    finally:
+        for h in plans:
+            L.gf_range_plan_destroy(h)
