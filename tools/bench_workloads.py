@@ -855,13 +855,19 @@ def bench_polyknn(args):
     lms, lcnt = ctx.timing(_lib.K_KNN_SELECT)
     ctx.set_timing(0)
     fallbacks = sum(1 for i in range(args.warmup, args.warmup + args.steps) if recs.decode(i)[0] != 0)
-    verified = None
+    verified, cpu = None, None
     if not args.no_verify:  # the first window against the oracle
         x, y, w = wins[args.warmup % 4]
         st, o, d, ix = recs.decode(args.warmup)
+        tc = time.perf_counter()
         m, eo, ed, ei = O.knn_ppoly(O.grid(500, *BEIJING), x, y, np.arange(n, dtype=np.int64),
                                     O.Polygons([P.rings]), args.radius, args.k)
+        tc = time.perf_counter() - tc
         verified = bool(st == 0 and np.array_equal(o, eo) and np.array_equal(d, ed) and np.array_equal(ix, ei))
+        if not args.no_cpu_baseline:
+            cpu = _cpu_line(n / tc, "points/s", f"the whole {n}-point window, 1 pass ({tc:.2f}s): oracle's C "
+                            "restatement of PointPolygonKNNQuery (polygon G/C cell filter, JTS point-polygon "
+                            "distance, bounded k-heap), 1 thread")
     avg = sms / 1000.0 / max(scnt, 1)
     _line("polygon-query kNN k=%d" % args.k, n * args.steps / elapsed, "points/s", args.steps, args.warmup, elapsed,
           "knn_poly_scan", 16.0 * n, avg,
@@ -869,7 +875,8 @@ def bench_polyknn(args):
                       "points_per_window": n, "k": args.k, "radius": args.radius},
            "breakdown": {"scan_us": round(avg * 1e6, 2), "sample_us": round(1000 * pms / max(pcnt, 1), 2),
                          "select_us": round(1000 * lms / max(lcnt, 1), 2)},
-           "fallback_windows": fallbacks, "verified_vs_oracle": verified})
+           "fallback_windows": fallbacks, "verified_vs_oracle": verified,
+           **({"cpu_baseline": cpu} if cpu else {})})
 
 
 def run(args):
