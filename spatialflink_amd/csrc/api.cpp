@@ -598,6 +598,14 @@ int build_table(gf_range_plan* P, const std::vector<Rect>& base, bool need_lists
       yt[c] = first_at_least(c, P->grid.minY, P->grid.cellLength);
     }
     P->x_lo = xt[0]; P->x_hi = xt[n]; P->y_lo = yt[0]; P->y_hi = yt[n];
+    int64_t clo = n, chi = -1;  // union of the row spans (columns holding any class)
+    for (int64_t y = 0; y < n; ++y)
+      if ((rows[y] & 0xffffu) <= (rows[y] >> 16)) {
+        clo = std::min<int64_t>(clo, rows[y] & 0xffffu);
+        chi = std::max<int64_t>(chi, rows[y] >> 16);
+      }
+    P->sx_lo = chi < 0 ? xt[n] : xt[clo];  // empty: sx_lo == sx_hi, every x fails
+    P->sx_hi = chi < 0 ? xt[n] : xt[chi + 1];
     if ((st = upload(ctx, &P->xt, xt)) || (st = upload(ctx, &P->yt, yt))) return st;
   }
 
@@ -843,6 +851,7 @@ RangeArgs range_args(const gf_range_plan* P, const gf_points* pts, uint64_t* bit
   a.rowoff = P->rowoff; a.spans = P->spans; a.span_bytes = (int32_t)std::min<int64_t>(P->span_bytes, INT32_MAX);
   a.span_lds = P->span_bytes <= kSpanLdsBytes;
   a.xt = P->xt; a.yt = P->yt; a.x_lo = P->x_lo; a.x_hi = P->x_hi; a.y_lo = P->y_lo; a.y_hi = P->y_hi;
+  a.sx_lo = P->sx_lo; a.sx_hi = P->sx_hi;
   a.inv_cl = 1.0 / P->grid.cellLength;
   a.cand_off = P->cand_off; a.cand_list = P->cand_list;
   a.approx = P->approx; a.metric = P->metric; a.r = P->r; a.s_r = s_prefilter(P->r, 0);

@@ -191,6 +191,7 @@ struct RangeArgs {
   const double* xt;          // [n+1] exact thresholds first_at_least(c) per axis (n <= 2048; else null)
   const double* yt;
   double x_lo, x_hi, y_lo, y_hi;  // xt[0], xt[n], yt[0], yt[n]
+  double sx_lo, sx_hi;       // xt[first], xt[last + 1] over every row's span: x outside => no class
   double inv_cl;
   const int32_t* extra;      // [n_extra*4]: x0, x1, y0, y1 (inclusive) accepted out-of-grid cells
   int32_t n_extra;
@@ -443,6 +444,7 @@ struct gf_range_plan {
   double* xt = nullptr;            // exact cell thresholds (table modes, n <= 2048)
   double* yt = nullptr;
   double x_lo = 0, x_hi = 0, y_lo = 0, y_hi = 0;
+  double sx_lo = 0, sx_hi = 0;
   int32_t* extra = nullptr;
   int32_t n_extra = 0;
   int32_t* cand_off = nullptr;

@@ -67,6 +67,9 @@ __device__ __forceinline__ int32_t cell_slot(const RangeArgs& a, const RangeLds&
   if (L.tx) {
     // in grid on both axes <=> T[0] <= v < T[n] (NaN fails: it takes the slow path below)
     if (!(px >= a.x_lo && px < a.x_hi && py >= a.y_lo && py < a.y_hi)) return -1;
+    // in grid, column outside every row's span (T[lo] <= x < T[hi + 1] <=> lo <= cx <= hi):
+    // those lanes skip the threshold / span LDS reads
+    if (!(px >= a.sx_lo && px < a.sx_hi)) return -2;
     cx = fast_cell(px, a.minX, a.inv_cl, L.tx, n);
     cy = fast_cell(py, a.minY, a.inv_cl, L.ty, n);
   } else {
