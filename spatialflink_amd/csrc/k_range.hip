@@ -193,23 +193,34 @@ __device__ __forceinline__ void eval_point(const RangeArgs& a, double px, double
 
 // Per-block queue segments: a wave reserves slots with one LDS atomic (a single global
 // counter would serialise ~10^5 wave atomics on one L2 line).
-__device__ __forceinline__ void queue_append(bool c, uint32_t idx, double px, double py, const RangeArgs& a,
-                                             uint32_t* lcount) {
+// Both halves of a wave-tile with ONE LDS reservation (the reservation's atomic return and
+// the broadcast are the latency a queueing tile pays): slots [base, base + |m0|) for the first
+// half, then [base + |m0|, base + |m0| + |m1|) for the second.
+__device__ __forceinline__ void queue_append2(bool c0, uint32_t i0, double x0, double y0, bool c1, uint32_t i1,
+                                              double x1, double y1, const RangeArgs& a, uint32_t* lcount) {
 #ifdef GF_EXP_NOAPPEND
   return;
 #endif
-  const uint64_t m = __ballot(c);
-  if (m == 0) return;
+  const uint64_t m0 = __ballot(c0), m1 = __ballot(c1);
+  if ((m0 | m1) == 0) return;
   const int lane = threadIdx.x & 63;
-  const int leader = __ffsll((unsigned long long)m) - 1;
+  const uint32_t n0 = (uint32_t)__popcll(m0);
   uint32_t base = 0;
-  if (lane == leader) base = atomicAdd(lcount, (uint32_t)__popcll(m));
-  base = __shfl(base, leader, 64);
-  if (c) {
-    const size_t pos = (size_t)blockIdx.x * a.seg_cap + base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-    a.queue[pos] = idx;
-    a.queue_xy[2 * pos] = px;  // the test kernel reads the coordinates back contiguously
-    a.queue_xy[2 * pos + 1] = py;
+  if (lane == 0) base = atomicAdd(lcount, n0 + (uint32_t)__popcll(m1));
+  base = __shfl(base, 0, 64);
+  const uint64_t below = (1ull << lane) - 1ull;
+  const size_t seg = (size_t)blockIdx.x * a.seg_cap + base;
+  if (c0) {
+    const size_t pos = seg + (uint32_t)__popcll(m0 & below);
+    a.queue[pos] = i0;
+    a.queue_xy[2 * pos] = x0;
+    a.queue_xy[2 * pos + 1] = y0;
+  }
+  if (c1) {
+    const size_t pos = seg + n0 + (uint32_t)__popcll(m1 & below);
+    a.queue[pos] = i1;
+    a.queue_xy[2 * pos] = x1;
+    a.queue_xy[2 * pos + 1] = y1;
   }
 }
 
@@ -238,10 +249,7 @@ __device__ __forceinline__ void range_tile(const RangeArgs& a, int64_t t, double
     }
     mult += (uint64_t)(__popcll(e0) + __popcll(e1));
   }
-  if (DEFER) {
-    queue_append(d0, (uint32_t)i0, x0, y0, a, lcount);
-    queue_append(d1, (uint32_t)i1, x1, y1, a, lcount);
-  }
+  if (DEFER) queue_append2(d0, (uint32_t)i0, x0, y0, d1, (uint32_t)i1, x1, y1, a, lcount);
   hits += (uint64_t)(__popcll(b0) + __popcll(b1));
 }
 
