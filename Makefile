@@ -45,10 +45,3 @@ clean:
 	$(MAKE) -s -C oracle clean
 
 .PHONY: all oracle clean isa trace
-
-# experiment builds: explibs/<NAME>/libgeoflink_hip.so with -D<NAME> (select with GF_LIB_PATH)
-EXP_NAMES ?= GF_EXP_NOCELL GF_EXP_NOAPPEND
-exp:
-	@for e in $(EXP_NAMES); do mkdir -p explibs/$$e && \
-	  $(HIPCC) $(HIPFLAGS) -D$$e -shared -o explibs/$$e/libgeoflink_hip.so -x hip $(SOURCES) || exit 1; done
-.PHONY: exp

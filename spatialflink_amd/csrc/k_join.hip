@@ -544,11 +544,6 @@ void join_row_probe_kernel(JoinRowArgs a) {
       need += join_row_lds_bytes(W, e - b);
     }
     s_fit = fit && need <= (size_t)a.lds_budget;
-#ifdef GF_EXP_J4
-    if (task % 500 == 7)
-      printf("task %u row %d rows %d..%d need %lu fit %d budget %d W %ld c %ld\n", task, lo, (int)r0, (int)r1,
-             (unsigned long)need, (int)s_fit, a.lds_budget, (long)W, (long)c);
-#endif
   }
   __syncthreads();
   const int32_t cy = s_row;

@@ -58,10 +58,6 @@ struct RangeLds {
 template <int TABLE>
 __device__ __forceinline__ int32_t cell_slot(const RangeArgs& a, const RangeLds& L, double px, double py) {
   if (!TABLE) return 0;
-#ifdef GF_EXP_NOCELL
-  if (px > 1e300) return 5;
-  return -2;
-#endif
   const int32_t n = a.grid_n;
   int32_t cx, cy;
   if (L.tx) {
@@ -198,9 +194,6 @@ __device__ __forceinline__ void eval_point(const RangeArgs& a, double px, double
 // half, then [base + |m0|, base + |m0| + |m1|) for the second.
 __device__ __forceinline__ void queue_append2(bool c0, uint32_t i0, double x0, double y0, bool c1, uint32_t i1,
                                               double x1, double y1, const RangeArgs& a, uint32_t* lcount) {
-#ifdef GF_EXP_NOAPPEND
-  return;
-#endif
   const uint64_t m0 = __ballot(c0), m1 = __ballot(c1);
   if ((m0 | m1) == 0) return;
   const int lane = threadIdx.x & 63;
@@ -308,13 +301,10 @@ __device__ __forceinline__ void range_stage(const RangeArgs& a, const RangeLds& 
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     const int64_t tu = t + u * tstride;
-#ifndef GF_EXP_ONETILE
     if (tu + 128 <= a.n)
       range_tile<TABLE, POLY, DEFER, true>(a, tu, cur.xa[u], cur.ya[u], cur.xb[u], cur.yb[u], c0[u], c1[u], hits,
                                            mult, lcount);
-    else
-#endif
-    if (tu < a.n)
+    else if (tu < a.n)
       range_tile<TABLE, POLY, DEFER, false>(a, tu, cur.xa[u], cur.ya[u], cur.xb[u], cur.yb[u], c0[u], c1[u], hits,
                                             mult, lcount);
   }
@@ -530,12 +520,8 @@ struct JoinPolyOut {
 };
 
 // Block b takes scan block b's queue segment (equal point ranges -> balanced segments), one
-// lane per queued point, so the per-point set-up (queue loads, cell, list bounds) is done
-// once, not by a group of lanes.  A lane walks its cell's polygon list 4 at a time (list and
-// bbox-cell loads batched before the tests: the walk is a chain of dependent loads otherwise).
-// Count pass: pairs per point (+ the first kJoinKeep polygon indices) and per block; write
-// pass: block offset = sum of the earlier blocks' counts, a block scan per round of kBlock
-// points, then the kept pairs are stored (points with more pairs walk their list again).
+// lane per queued point.  A lane walks its cell's polygon list 4 at a time (list and bbox-cell
+// loads batched before the tests: the walk is a chain of dependent loads otherwise).
 __device__ __forceinline__ uint32_t block_scan_excl(uint32_t v, uint32_t* total, uint32_t* ws) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   uint32_t inc = v;
@@ -591,18 +577,17 @@ __device__ __forceinline__ uint32_t join_ppoly_walk(const RangeArgs& a, double p
   return n;
 }
 
-template <int WRITE>
-__global__ __launch_bounds__(kBlock) void join_ppoly_kernel(RangeArgs a, JoinPolyOut o) {
+// Write pass: block offset = sum of the earlier blocks' counts (count pass), a block scan per
+// round of kBlock queued points, then the kept pairs are stored (a point with more than
+// kJoinKeep pairs walks its list again).
+__global__ __launch_bounds__(kBlock) void join_ppoly_write_kernel(RangeArgs a, JoinPolyOut o) {
   __shared__ uint32_t ws[kBlock / 64];
   __shared__ unsigned long long part[kBlock / 64];
   const int lane = threadIdx.x & 63;
   const uint32_t cnt = a.queue_count[blockIdx.x];
   const size_t base = (size_t)blockIdx.x * a.seg_cap;
-#ifdef GF_EXP_J4
-  if (threadIdx.x == 0 && (blockIdx.x % 256) == 0) printf("block %u cnt %u seg_cap %lld\n", blockIdx.x, cnt, (long long)a.seg_cap);
-#endif
   unsigned long long run = 0;
-  if (WRITE) {  // this block's output offset: sum of the earlier blocks' totals
+  {  // this block's output offset: sum of the earlier blocks' totals
     unsigned long long sum = 0;
     for (uint32_t i = threadIdx.x; i < blockIdx.x; i += kBlock) sum += o.btot[i];
     for (int off = 32; off > 0; off >>= 1) sum += __shfl_down(sum, off, 64);
@@ -612,48 +597,24 @@ __global__ __launch_bounds__(kBlock) void join_ppoly_kernel(RangeArgs a, JoinPol
     for (int w = 0; w < kBlock / 64; ++w) run += part[w];
     if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) *o.total = run + o.btot[blockIdx.x];
   }
-  uint32_t bsum = 0;
   for (uint32_t i0 = 0; i0 < cnt; i0 += kBlock) {  // block-uniform
     const uint32_t i = i0 + threadIdx.x;
     const bool valid = i < cnt;
     const size_t pos = base + i;
-    if (WRITE) {
-      const uint32_t c = valid ? o.ecnt[pos] : 0u;
-      uint32_t tot;
-      const uint32_t ex = block_scan_excl(c, &tot, ws);
-      const unsigned long long at0 = run + ex;
-      run += tot;
-      if (c == 0) continue;
-      const uint32_t pidx = a.queue[pos];
-      auto put = [&](uint32_t k, int32_t q) {
-        if ((int64_t)(at0 + k) < o.cap) join_store(o.pairs, o.aligned, at0 + k, make_uint2(pidx, (uint32_t)q));
-      };
-      if (c <= (uint32_t)kJoinKeep) {
-        for (uint32_t k = 0; k < c; ++k) put(k, (int32_t)o.ecand[pos * kJoinKeep + k]);
-      } else {
-        join_ppoly_walk(a, a.queue_xy[2 * pos], a.queue_xy[2 * pos + 1], put);
-      }
-      continue;
-    }
-    if (!valid) continue;
-#ifdef GF_EXP_J3
-    if (pos < (size_t)-1) { o.ecnt[pos] = 0; continue; }
-#endif
-    const uint32_t n = join_ppoly_walk(a, a.queue_xy[2 * pos], a.queue_xy[2 * pos + 1], [&](uint32_t k, int32_t q) {
-      if (k < (uint32_t)kJoinKeep) o.ecand[pos * kJoinKeep + k] = (uint32_t)q;
-    });
-    o.ecnt[pos] = n;
-    bsum += n;
-  }
-  if (!WRITE) {
-    for (int off = 32; off > 0; off >>= 1) bsum += __shfl_down(bsum, off, 64);
-    if (lane == 0) ws[threadIdx.x >> 6] = bsum;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      uint32_t t = 0;
-#pragma unroll
-      for (int w = 0; w < kBlock / 64; ++w) t += ws[w];
-      o.btot[blockIdx.x] = t;
+    const uint32_t c = valid ? o.ecnt[pos] : 0u;
+    uint32_t tot;
+    const uint32_t ex = block_scan_excl(c, &tot, ws);
+    const unsigned long long at0 = run + ex;
+    run += tot;
+    if (c == 0) continue;
+    const uint32_t pidx = a.queue[pos];
+    auto put = [&](uint32_t k, int32_t q) {
+      if ((int64_t)(at0 + k) < o.cap) join_store(o.pairs, o.aligned, at0 + k, make_uint2(pidx, (uint32_t)q));
+    };
+    if (c <= (uint32_t)kJoinKeep) {
+      for (uint32_t k = 0; k < c; ++k) put(k, (int32_t)o.ecand[pos * kJoinKeep + k]);
+    } else {
+      join_ppoly_walk(a, a.queue_xy[2 * pos], a.queue_xy[2 * pos + 1], put);
     }
   }
 }
@@ -787,12 +748,8 @@ hipError_t launch_join_ppoly(gf_ctx* ctx, const RangeArgs& a, int blocks, int jb
   KTimer t(ctx, GF_K_RANGE_TEST);
   JoinPolyOut o{ecnt, ecand, btot, total, pairs, cap, aligned};
   (void)jblocks;  // one block per scan block's queue segment
-#ifdef GF_EXP_JLANE
-  hipLaunchKernelGGL(join_ppoly_kernel<0>, dim3(blocks), dim3(kBlock), 0, ctx->stream, a, o);
-#else
   hipLaunchKernelGGL(join_ppoly_count_kernel, dim3(blocks), dim3(kBlock), 0, ctx->stream, a, o);
-#endif
-  hipLaunchKernelGGL(join_ppoly_kernel<1>, dim3(blocks), dim3(kBlock), 0, ctx->stream, a, o);
+  hipLaunchKernelGGL(join_ppoly_write_kernel, dim3(blocks), dim3(kBlock), 0, ctx->stream, a, o);
   return hipGetLastError();
 }
 

@@ -114,6 +114,18 @@ class PolygonSet:
         return _lib.GfPolygons(len(self.polygons), self.ring_off.ctypes.data, self.vert_off.ctypes.data,
                                self.vx.ctypes.data, self.vy.ctypes.data)
 
+    def digest(self) -> bytes:
+        """Content key of the set (ring layout + every vertex bit pattern): device plans are
+        cached by it, so a new polygon list with the same geometry reuses a plan and any other
+        geometry never does (object ids are recycled by CPython, contents are not)."""
+        import hashlib
+
+        h = hashlib.blake2b(digest_size=20)
+        for a in (self.ring_off, self.vert_off, self.vx, self.vy):
+            h.update(np.int64(a.size).tobytes())
+            h.update(np.ascontiguousarray(a).tobytes())
+        return h.digest()
+
 
 @dataclass
 class PointWindow:

@@ -16,6 +16,7 @@ IllegalArgumentException), candidate layers <= 0 raise CandidateLayersError (Sys
 from __future__ import annotations
 
 import ctypes as C
+from collections import OrderedDict
 from dataclasses import dataclass
 from enum import Enum
 
@@ -67,11 +68,48 @@ def _require_supported(conf: QueryConfiguration):
         raise ValueError("Not yet support")
 
 
+class _PlanCache:
+    """Device plans of one operator, keyed by query CONTENTS (coordinates, polygon digest,
+    radius, flags) and bounded: the least recently used plan beyond `limit` is destroyed, so a
+    query stream (a new polygon set per window) does not leak one device plan per window."""
+
+    def __init__(self, destroy_name: str, limit: int = 16):
+        self._destroy_name = destroy_name
+        self.limit = int(limit)
+        self._d = OrderedDict()
+
+    def get(self, key):
+        plan = self._d.get(key)
+        if plan is not None:
+            self._d.move_to_end(key)
+        return plan
+
+    def put(self, key, plan):
+        self._d[key] = plan
+        while len(self._d) > self.limit:
+            _, old = self._d.popitem(last=False)
+            self._destroy(old)
+
+    def _destroy(self, plan):
+        if _lib._lib is not None:
+            getattr(_lib._lib, self._destroy_name)(plan)
+
+    def __len__(self):
+        return len(self._d)
+
+    def close(self):
+        while self._d:
+            _, p = self._d.popitem(last=False)
+            self._destroy(p)
+
+
 class SpatialOperator:
+    _destroy_name = "gf_range_plan_destroy"
+
     def __init__(self, conf: QueryConfiguration, index: UniformGrid):
         self.conf = conf
         self.index = index
-        self._plans = {}
+        self._plans = _PlanCache(self._destroy_name)
 
     def getQueryConfiguration(self):
         return self.conf
@@ -149,13 +187,13 @@ class _RangeBase(SpatialOperator):
         plan = self._plans.get(key)
         if plan is None:
             plan = create()
-            self._plans[key] = plan
+            self._plans.put(key, plan)
         return plan
 
     def __del__(self):
-        if _lib._lib is not None:
-            for p in getattr(self, "_plans", {}).values():
-                _lib._lib.gf_range_plan_destroy(p)
+        plans = getattr(self, "_plans", None)
+        if plans is not None:
+            plans.close()
 
 
 class PointPointRangeQuery(_RangeBase):
@@ -189,13 +227,12 @@ class PointPolygonRangeQuery(_RangeBase):
 
     def run(self, window: PointWindow, queryPolygonSet, queryRadius: float) -> RangeResult:
         _require_supported(self.conf)
-        polys = list(queryPolygonSet)
+        ps = PolygonSet(queryPolygonSet)
         ctx = _lib.context(window.x.device.index)
-        key = (ctx.device, tuple(id(p) for p in polys), float(queryRadius), bool(self.conf.approximateQuery),
+        key = (ctx.device, ps.digest(), float(queryRadius), bool(self.conf.approximateQuery),
                int(self.conf.distanceMetric))
 
         def create():
-            ps = PolygonSet(polys)
             cs = ps.c_struct()
             h = C.c_void_p()
             st = _lib.lib().gf_range_ppoly_plan_create(ctx.handle, C.byref(self.index.c_grid), C.byref(cs),
@@ -279,6 +316,8 @@ class PinnedRecords:
 class PointPointKNNQuery(SpatialOperator):
     """knn/PointPointKNNQuery.java -- continuous kNN of one query point within radius r."""
 
+    _destroy_name = "gf_knn_plan_destroy"
+
     def plan(self, window_device: int, queryPoint: Point, queryRadius: float, k: int):
         ctx = _lib.context(window_device)
         key = (ctx.device, queryPoint.x, queryPoint.y, float(queryRadius), int(k), int(self.conf.distanceMetric))
@@ -289,7 +328,8 @@ class PointPointKNNQuery(SpatialOperator):
                                                   float(queryPoint.y), float(queryRadius), int(k),
                                                   int(self.conf.distanceMetric), C.byref(h))
             _lib.check(st, ctx.handle, "gf_knn_pp_plan_create")
-            self._plans[key] = plan = h
+            self._plans.put(key, h)
+            plan = h
         return ctx, plan
 
     def run(self, window: PointWindow, queryPoint: Point, queryRadius: float, k: int) -> KNNResult:
@@ -343,9 +383,9 @@ class PointPointKNNQuery(SpatialOperator):
         _lib.check(_lib.lib().gf_knn_plan_set_capacity(plan, int(cap)), ctx.handle, "set_capacity")
 
     def __del__(self):
-        if _lib._lib is not None:
-            for p in getattr(self, "_plans", {}).values():
-                _lib._lib.gf_knn_plan_destroy(p)
+        plans = getattr(self, "_plans", None)
+        if plans is not None:
+            plans.close()
 
 
 class PointPolygonKNNQuery(PointPointKNNQuery):
@@ -355,19 +395,19 @@ class PointPolygonKNNQuery(PointPointKNNQuery):
 
     def plan(self, window_device: int, queryPolygon: Polygon, queryRadius: float, k: int):
         ctx = _lib.context(window_device)
-        key = (ctx.device, id(queryPolygon), float(queryRadius), int(k), int(self.conf.distanceMetric),
+        ps = PolygonSet([queryPolygon])
+        key = (ctx.device, ps.digest(), float(queryRadius), int(k), int(self.conf.distanceMetric),
                bool(self.conf.isApproximateQuery()))
         plan = self._plans.get(key)
         if plan is None:
-            ps = PolygonSet([queryPolygon])
             cs = ps.c_struct()
             h = C.c_void_p()
             st = _lib.lib().gf_knn_ppoly_plan_create(ctx.handle, C.byref(self.index.c_grid), C.byref(cs),
                                                      float(queryRadius), int(k), int(self.conf.isApproximateQuery()),
                                                      int(self.conf.distanceMetric), C.byref(h))
             _lib.check(st, ctx.handle, "gf_knn_ppoly_plan_create")
-            self._plans[key] = plan = h
-            self._keep = getattr(self, "_keep", []) + [queryPolygon]
+            self._plans.put(key, h)
+            plan = h
         return ctx, plan
 
 
@@ -430,8 +470,8 @@ class PointPolygonJoinQuery(_RangeBase):
     stream (PointPolygonJoinQuery.java:154-213; polygons replicated to their own guaranteed +
     candidate cells, JoinQuery.java:93-115).  index1 = uGrid (points), index2 = qGrid
     (polygons); the device path requires the two grids to be equal.  The replicated polygon
-    side is a plan, cached while the same polygon objects come back (a static query set);
-    a polygon stream's new window builds a new one."""
+    side is a plan, cached by the polygons' contents (a static query set reuses it; a polygon
+    stream's window with new geometry builds a new one, the cache keeps the 16 most recent)."""
 
     def __init__(self, conf: QueryConfiguration, index1: UniformGrid, index2: UniformGrid = None):
         super().__init__(conf, index1)
@@ -442,13 +482,12 @@ class PointPolygonJoinQuery(_RangeBase):
         import torch
 
         _require_supported(self.conf)
-        polys = list(queryPolygons)
+        ps = PolygonSet(queryPolygons)  # keeps the CSR arrays alive during the call
         ctx = _lib.context(pointWindow.x.device.index)
-        key = (ctx.device, tuple(id(p) for p in polys), float(queryRadius), bool(self.conf.approximateQuery),
+        key = (ctx.device, ps.digest(), float(queryRadius), bool(self.conf.approximateQuery),
                int(self.conf.distanceMetric))
 
         def create():
-            ps = PolygonSet(polys)  # keeps the CSR arrays alive during the call
             cs = ps.c_struct()
             h = C.c_void_p()
             _lib.check(_lib.lib().gf_join_ppoly_plan_create(ctx.handle, C.byref(self.index2.c_grid), C.byref(cs),

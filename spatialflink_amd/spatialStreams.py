@@ -35,7 +35,8 @@ def device_text(text, device=None):
 
     if isinstance(text, torch.Tensor):
         return text
-    arr = np.frombuffer(bytes(text), np.uint8) if not isinstance(text, np.ndarray) else text
+    # bytearray: a writable buffer (torch.from_numpy of a read-only array is undefined behaviour)
+    arr = np.frombuffer(bytearray(text), np.uint8) if not isinstance(text, np.ndarray) else text
     dev = torch.device("cuda", torch.cuda.current_device() if device is None else device)
     return torch.from_numpy(np.ascontiguousarray(arr)).to(dev)
 

@@ -310,9 +310,16 @@ class SlidingRangeQuery:
             self._pane(p, pane)
 
     def flush(self):
+        """End of input (Flink's final watermark): the pane being filled, then empty panes until
+        every window holding a point has fired -- as SlidingKNNQuery.flush."""
         last = self.stream.close()
         if last is not None:
             self._pane(*last)
+        if self.last_pane is not None:
+            g = self.geo
+            last_start = (self.last_pane * g.pane // g.slide) * g.slide
+            for p in range(self.last_pane + 1, (last_start + g.size) // g.pane):
+                self._one(p, None)
 
     def results(self):
         out, self.fired = self.fired, []

@@ -830,6 +830,8 @@ def test_range_windows_in_flight_on_two_contexts(sf, oracle_mod):
         n = 300_000
         bitmaps = torch.zeros(6, (n + 63) // 64, dtype=torch.int64, device="cuda")
         counts = torch.zeros(6, 2, dtype=torch.int64, device="cuda")
+        # the raw contexts run on their own non-blocking streams: order them after torch's fills
+        torch.cuda.synchronize()
         pts = [w.c_struct() for w in wins]
         for j in range(6):
             _lib.check(L.gf_range_run(plans[j % 2], C.byref(pts[j]), bitmaps[j].data_ptr(), None, counts[j].data_ptr()),
