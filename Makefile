@@ -8,8 +8,8 @@ HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -ffp-contract=off -fno-f
 SRC      := spatialflink_amd/csrc
 OBJDIR   := build/obj
 LIB      := spatialflink_amd/libgeoflink_hip.so
-SOURCES  := $(SRC)/api.cpp $(SRC)/sliding.cpp $(SRC)/csv.cpp $(SRC)/k_points.hip $(SRC)/k_knn.hip \
-            $(SRC)/k_range.hip $(SRC)/k_join.hip $(SRC)/k_csv.hip
+SOURCES  := $(SRC)/api.cpp $(SRC)/sliding.cpp $(SRC)/csv.cpp $(SRC)/objid.cpp $(SRC)/k_points.hip $(SRC)/k_knn.hip \
+            $(SRC)/k_range.hip $(SRC)/k_join.hip $(SRC)/k_csv.hip $(SRC)/k_objid.hip
 OBJECTS  := $(patsubst $(SRC)/%,$(OBJDIR)/%.o,$(SOURCES))
 HEADERS  := include/geoflink_hip.h $(SRC)/gf_internal.hpp $(SRC)/gf_numerics.hpp $(SRC)/gf_decimal.hpp $(SRC)/gf_pow5.hpp $(SRC)/gf_geom.hpp
 

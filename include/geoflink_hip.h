@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define GF_ABI_VERSION 1
+#define GF_ABI_VERSION 2
 
 /* status codes */
 #define GF_OK             0
@@ -69,11 +69,26 @@ typedef struct {
   double cellLength;  /* (maxX - minX) / n, bounds NOT squared */
 } gf_grid;
 
+/* ---- objID keys ----------------------------------------------------------------------
+ * The reference's objID is a String (Point.objID, Point.java:41-47; the CSV ingest keeps the
+ * field as is, Deserialization.java:317 `String strOId`) and the kNN merge dedupes by
+ * String.equals (KNNQuery.java:232-251).  gf_points.objID carries one int64 KEY per point,
+ * injective over Strings:
+ *   - a String that is exactly Long.toString(v) of a v in [-2^62, 2^62) -- "7", "-12"; not
+ *     "007", "+7", " 7", "-0" -- has key v;
+ *   - every other String has key INT64_MIN + id, its id in a gf_objid_dict -- assigned in first-
+ *     occurrence order per batch, so keys never depend on scheduling.
+ * Equal keys <=> equal Strings (keys of one dictionary).  The kNN contract's ties are broken by
+ * key, so dictionary Strings order before numeric ones. */
+#define GF_OBJID_NUMERIC_MIN (-(INT64_C(1) << 62))  /* keys below: dictionary Strings */
+#define GF_OBJID_NUMERIC_END (INT64_C(1) << 62)     /* keys at or above: never produced */
+typedef struct gf_objid_dict gf_objid_dict;
+
 /* One window of points as device SoA -- Point(objID, x, y, ts, uGrid), Point.java:91-100 */
 typedef struct {
   const double* x;
   const double* y;
-  const int64_t* objID;  /* decimal objID string <-> int64; needed by kNN only */
+  const int64_t* objID;  /* objID keys (above); needed by kNN only */
   const int64_t* ts;     /* timeStampMillisec; unused by window evaluation */
   int64_t n;
 } gf_points;
@@ -281,13 +296,30 @@ int  gf_knn_sliding_decode(gf_knn_sliding* s, int64_t window_end, const void* re
 int  gf_pane_bounds(gf_ctx* ctx, const int64_t* ts, int64_t n, int64_t pane_ms, int64_t first_pane, int32_t npanes,
                     int64_t* bounds);
 
+/* ---- objID dictionaries ----------------------------------------------------------------
+ * Device hash table + byte arena of the non-canonical objID Strings of a stream of windows.
+ * gf_csv_parse uses the context's default dictionary (gf_ctx_objid_dict, owned by the
+ * context); a JNI shim maps Point.objID Strings with gf_objid_intern and decodes result keys
+ * (kNN objIDs) with gf_objid_decode.  Not thread-safe: one dictionary per calling thread. */
+int  gf_objid_dict_create(gf_ctx* ctx, gf_objid_dict** out);
+void gf_objid_dict_destroy(gf_objid_dict* d);
+int  gf_ctx_objid_dict(gf_ctx* ctx, gf_objid_dict** out);
+int  gf_objid_dict_size(const gf_objid_dict* d, int64_t* n);
+/* Sync: keys of n host Strings, String i = bytes[offs[i], offs[i+1]) (offs: n+1 entries). */
+int  gf_objid_intern(gf_objid_dict* d, const char* bytes, const int64_t* offs, int64_t n, int64_t* keys);
+/* Sync: the Strings of n keys, String i = buf[offs[i], offs[i+1]) (offs: n+1 entries);
+ * GF_ERR_CAPACITY when cap is too small (offs[n] = the bytes needed). */
+int  gf_objid_decode(gf_objid_dict* d, const int64_t* keys, int64_t n, char* buf, int64_t cap, int64_t* offs);
+
 /* ---- CSV / TSV ingest ----------------------------------------------------------------
  * Deserialization.CSVTSVToTSpatial(uGrid, dateFormat, delimiter, csvTsvSchemaAttr).map
  * (Deserialization.java:291-325) over a chunk of text lines, on the device.  Per line: '"'
  * removed, fields split on `delimiter` with the surrounding whitespace (split("\\s*" + delimiter
- * + "\\s*")), objID = Long.valueOf(field[objid_field]) (decimal objIDs only: the SoA carries
- * them as int64), ts = Long.valueOf(field[time_field]), x / y = Double.valueOf(...) correctly
- * rounded; with `grid`, the cell of Point(objID, x, y, ts, uGrid) (Point.java:98) as well. */
+ * + "\\s*")), objID = the String field[objid_field] as its key (objID keys above; any String,
+ * whitespace kept), ts = Long.valueOf(field[time_field]), x / y = Double.valueOf(...) correctly
+ * rounded; with `grid`, the cell of Point(objID, x, y, ts, uGrid) (Point.java:98) as well.
+ * Fields are read in the reference's order (objID, time, x, y): the first missing or
+ * malformed one names the line's error. */
 typedef struct {
   char delimiter;          /* ',' ';' '\t' ... (one character) */
   char reserved[3];
@@ -299,7 +331,8 @@ typedef struct {
 #define GF_CSV_OK              0
 #define GF_CSV_NUMBER_FORMAT   1  /* Long.valueOf / Double.valueOf throw NumberFormatException */
 #define GF_CSV_UNSUPPORTED     2  /* valid Java literal the device path does not take: hexadecimal, or
-                                     > 19 significant digits within 1e-19 of a rounding boundary */
+                                     > 19 significant digits within 1e-19 of a rounding boundary;
+                                     or an objID field of 1 MiB or more */
 #define GF_CSV_MISSING_FIELD   3  /* the reference's List.get throws IndexOutOfBoundsException */
 #define GF_CSV_EMPTY_LINE      4  /* an empty line (a trailing newline at the end is fine) */
 /* Sync.  text: device bytes [len], 16-byte aligned, complete lines separated by '\n' ("\r\n"
@@ -309,6 +342,10 @@ typedef struct {
 int gf_csv_parse(gf_ctx* ctx, const char* text, int64_t len, const gf_csv_schema* schema, const gf_grid* grid,
                  double* x, double* y, int64_t* objID, int64_t* ts, int32_t* cx, int32_t* cy, int64_t cap,
                  int64_t* n_out, int64_t* bad_line, int32_t* bad_kind);
+/* As gf_csv_parse, objID keys from `dict` (NULL: the context's default dictionary). */
+int gf_csv_parse_dict(gf_ctx* ctx, gf_objid_dict* dict, const char* text, int64_t len, const gf_csv_schema* schema,
+                      const gf_grid* grid, double* x, double* y, int64_t* objID, int64_t* ts, int32_t* cx, int32_t* cy,
+                      int64_t cap, int64_t* n_out, int64_t* bad_line, int32_t* bad_kind);
 
 /* ---- join (sync) --------------------------------------------------------------------
  * JoinQuery.getReplicatedPointQueryStream + PointPointJoinQuery.windowBased

@@ -1081,10 +1081,13 @@ void orc_java_random_points(int64_t seed, int64_t n, double minX, double maxX,
 /* ------------------------------------------------------------------------------------
  * CSV / TSV ingest -- Deserialization.CSVTSVToTSpatial.map (Deserialization.java:314-322):
  *   strArrayList = Arrays.asList(str.replace("\"", "").split("\\s*" + delimiter + "\\s*"));
- *   objID = Long.valueOf-able decimal (kept as int64 here), time = Long.valueOf,
- *   x, y = Double.valueOf (JDK FloatingDecimal: trim, Java literal grammar, correctly rounded;
- *   glibc strtod is correctly rounded too).  Lines come from Flink's TextInputFormat: split
- *   on '\n', a trailing '\r' dropped.
+ *   String strOId = get(objid)   (the field itself: any String, whitespace kept, :317)
+ *   long time = Long.valueOf(get(time))     (:318)
+ *   double x = Double.valueOf(get(x)), y = Double.valueOf(get(y))   (:319-320; JDK
+ *   FloatingDecimal: trim, Java literal grammar, correctly rounded; glibc strtod is correctly
+ *   rounded too).  Evaluated in that order: the first get() past the fields
+ *   (IndexOutOfBoundsException) or malformed number (NumberFormatException) is the error.
+ *   Lines come from Flink's TextInputFormat: split on '\n', a trailing '\r' dropped.
  * ------------------------------------------------------------------------------------ */
 static int orc_java_s(char c) { return c == ' ' || c == '\t' || c == '\n' || c == '\x0B' || c == '\f' || c == '\r'; }
 
@@ -1189,15 +1192,19 @@ static int orc_java_double(const char* s0, int n, double* out, int* hex) {
 }
 
 int64_t orc_csv_parse(const char* text, int64_t len, char delim, const int32_t* want, double* x, double* y,
-                      int64_t* objID, int64_t* ts, int64_t cap, int64_t* bad_line, int32_t* bad_kind) {
-  int64_t pos = 0, line = 0;
+                      char* oid, int64_t oid_cap, int64_t* oid_off, int64_t* oid_len, int64_t* ts, int64_t cap,
+                      int64_t* bad_line, int32_t* bad_kind) {
+  int64_t pos = 0, line = 0, ob = 0;
   char* buf = NULL;
   int bufcap = 0, *fidx = NULL;
   *bad_line = -1;
   *bad_kind = 0;
   while (pos < len) {
     int64_t e = pos, le;
-    int n = 0, nf, k, kind = 0, hex = 0, *fb, *fe;
+    int n = 0, nf = 0, kind = 0, *fb, *fe;
+    int64_t t = 0;
+    double vx = 0, vy = 0;
+    int hx = 0, hy = 0;
     while (e < len && text[e] != '\n') ++e;
     le = e;
     if (le > pos && text[le - 1] == '\r') --le;
@@ -1210,29 +1217,31 @@ int64_t orc_csv_parse(const char* text, int64_t len, char delim, const int32_t* 
     fe = fidx + bufcap + 2;
     for (int64_t i = pos; i < le; ++i)
       if (text[i] != '"') buf[n++] = text[i];  /* str.replace("\"", "") */
+    if (oid_off && line < cap) oid_off[line] = ob;
     if (le == pos) kind = 4;
     else {
       nf = orc_java_split(buf, n, delim, fb, fe, bufcap + 2);
-      for (k = 0; k < 4 && !kind; ++k)
-        if (want[k] >= nf) kind = 3;
-      if (!kind) {
-        int64_t o = 0, t = 0;
-        double vx = 0, vy = 0;
-        int hx = 0, hy = 0;
-        if (orc_java_long(buf + fb[want[0]], fe[want[0]] - fb[want[0]], &o) ||
-            orc_java_long(buf + fb[want[1]], fe[want[1]] - fb[want[1]], &t) ||
-            orc_java_double(buf + fb[want[2]], fe[want[2]] - fb[want[2]], &vx, &hx) ||
-            orc_java_double(buf + fb[want[3]], fe[want[3]] - fb[want[3]], &vy, &hy))
-          kind = 1;
-        hex = hx || hy;
-        if (!kind && line < cap) { x[line] = vx; y[line] = vy; objID[line] = o; ts[line] = t; }
-        if (!kind && hex) kind = 2;  /* valid Java; reported so tests can pin the device's answer */
+      if (want[0] >= nf) kind = 3;                                   /* get(objid) */
+      else {
+        const int ol = fe[want[0]] - fb[want[0]];
+        if (oid && ob + ol <= oid_cap) memcpy(oid + ob, buf + fb[want[0]], (size_t)ol);
+        ob += ol;
       }
+      if (!kind && want[1] >= nf) kind = 3;                          /* Long.valueOf(get(time)) */
+      if (!kind && orc_java_long(buf + fb[want[1]], fe[want[1]] - fb[want[1]], &t)) kind = 1;
+      if (!kind && want[2] >= nf) kind = 3;                          /* Double.valueOf(get(x)) */
+      if (!kind && orc_java_double(buf + fb[want[2]], fe[want[2]] - fb[want[2]], &vx, &hx)) kind = 1;
+      if (!kind && want[3] >= nf) kind = 3;                          /* Double.valueOf(get(y)) */
+      if (!kind && orc_java_double(buf + fb[want[3]], fe[want[3]] - fb[want[3]], &vy, &hy)) kind = 1;
+      if (!kind && line < cap) { x[line] = vx; y[line] = vy; ts[line] = t; }
+      if (!kind && (hx || hy)) kind = 2;  /* valid Java; reported so tests can pin the device's answer */
     }
     if (kind && *bad_line < 0) { *bad_line = line; *bad_kind = kind; }
     ++line;
     pos = e + 1;
   }
+  if (oid_off && line <= cap) oid_off[line] = ob;
+  *oid_len = ob;
   free(buf);
   free(fidx);
   return line;

@@ -154,8 +154,11 @@ int32_t orc_knn_ppoly_contract(const orc_grid* g, int64_t n, const double* x, co
  * want = csvTsvSchemaAttr (objID, time, x, y field indices).  Returns the line count (rows past
  * cap are not written); the first bad line and its kind (1 NumberFormatException, 2 hexadecimal
  * literal -- valid Java, value still written --, 3 missing field, 4 empty line) or -1. */
+/* objID Strings: line i's String = oid[oid_off[i], oid_off[i+1]) (quotes removed, whitespace
+ * kept); *oid_len = bytes needed (strings written only while they fit oid_cap). */
 int64_t orc_csv_parse(const char* text, int64_t len, char delim, const int32_t* want, double* x, double* y,
-                      int64_t* objID, int64_t* ts, int64_t cap, int64_t* bad_line, int32_t* bad_kind);
+                      char* oid, int64_t oid_cap, int64_t* oid_off, int64_t* oid_len, int64_t* ts, int64_t cap,
+                      int64_t* bad_line, int32_t* bad_kind);
 
 #ifdef __cplusplus
 }

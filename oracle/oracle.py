@@ -78,7 +78,8 @@ def lib():
         L.orc_knn_ppoly_contract.argtypes = [C.POINTER(OrcGrid), i64, P, P, P, C.POINTER(OrcPolygons), d, i32,
                                              C.c_int, C.c_int, P, P, P]
         L.orc_knn_ppoly_contract.restype = i32
-        L.orc_csv_parse.argtypes = [C.c_char_p, i64, C.c_char, P, P, P, P, P, i64, C.POINTER(i64), C.POINTER(i32)]
+        L.orc_csv_parse.argtypes = [C.c_char_p, i64, C.c_char, P, P, P, C.c_char_p, i64, P, C.POINTER(i64), P, i64,
+                                    C.POINTER(i64), C.POINTER(i32)]
         L.orc_csv_parse.restype = i64
         _lib = L
     return _lib
@@ -256,12 +257,18 @@ def java_random_points(seed, n, minX, maxX, minY, maxY):
 
 
 def csv_parse(text: bytes, delim: str, want):
-    """Deserialization.CSVTSVToTSpatial.map per line -> (x, y, objID, ts, bad_line, bad_kind)."""
+    """Deserialization.CSVTSVToTSpatial.map per line -> (x, y, objID Strings as a list of bytes,
+    ts, bad_line, bad_kind)."""
     w = np.asarray(want, np.int32)
-    bl, bk = C.c_int64(), C.c_int32()
-    n = lib().orc_csv_parse(text, len(text), delim.encode(), _p(w), None, None, None, None, 0, C.byref(bl), C.byref(bk))
-    x = np.zeros(n); y = np.zeros(n); o = np.zeros(n, np.int64); t = np.zeros(n, np.int64)
-    lib().orc_csv_parse(text, len(text), delim.encode(), _p(w), _p(x), _p(y), _p(o), _p(t), n, C.byref(bl), C.byref(bk))
+    bl, bk, ol = C.c_int64(), C.c_int32(), C.c_int64()
+    n = lib().orc_csv_parse(text, len(text), delim.encode(), _p(w), None, None, None, 0, None, C.byref(ol), None, 0,
+                            C.byref(bl), C.byref(bk))
+    x = np.zeros(n); y = np.zeros(n); t = np.zeros(n, np.int64); off = np.zeros(n + 1, np.int64)
+    ob = C.create_string_buffer(max(1, ol.value))
+    lib().orc_csv_parse(text, len(text), delim.encode(), _p(w), _p(x), _p(y), ob, ol.value, _p(off), C.byref(ol), _p(t),
+                        n, C.byref(bl), C.byref(bk))
+    raw = ob.raw
+    o = [raw[off[i]:off[i + 1]] for i in range(n)]
     return x, y, o, t, bl.value, bk.value
 
 

@@ -8,7 +8,7 @@ PointPolygonKNNQuery, PointPolygonJoinQuery).
 """
 from . import _lib
 from .spatialIndices import UniformGrid, generateCellIDStr, getIntCellIndices, padLeadingZeroesToInt
-from .spatialObjects import Point, PointWindow, Polygon, PolygonSet
+from .spatialObjects import ObjIdDict, Point, PointWindow, Polygon, PolygonSet
 from .spatialOperators import (KNNResult, PinnedRecords, PointPointJoinQuery, PointPointKNNQuery, PointPointRangeQuery,
                                PointPolygonJoinQuery, PointPolygonKNNQuery,
                                PointPolygonRangeQuery, QueryConfiguration, QueryType, RangeResult, assign_cells,
@@ -18,7 +18,7 @@ from .windows import SlidingKNNQuery, SlidingRangeQuery, SlidingWindows
 
 __all__ = [
     "SlidingWindows", "SlidingKNNQuery", "SlidingRangeQuery", "Deserialization", "PointPolygonKNNQuery", "PointPolygonJoinQuery",
-    "UniformGrid", "Point", "Polygon", "PolygonSet", "PointWindow", "QueryType", "QueryConfiguration",
+    "UniformGrid", "ObjIdDict", "Point", "Polygon", "PolygonSet", "PointWindow", "QueryType", "QueryConfiguration",
     "PointPointRangeQuery", "PointPolygonRangeQuery", "PointPointKNNQuery", "PointPointJoinQuery", "RangeResult",
     "KNNResult", "PinnedRecords", "knn_merge_host", "assign_cells", "bucket_by_cell", "synthetic_uniform", "generateCellIDStr",
     "getIntCellIndices", "padLeadingZeroesToInt",

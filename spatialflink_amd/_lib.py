@@ -14,6 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("GF_LIB_PATH") or os.path.join(_HERE, "libgeoflink_hip.so")
 
 GF_OK = 0
+OBJID_NUMERIC_MIN, OBJID_NUMERIC_END = -(1 << 62), 1 << 62
 GF_MERGE_SHARD_MAJOR, GF_MERGE_WINDOW_MAJOR = 0, 1
 GF_ERR_ARG = -1
 GF_ERR_CAPACITY = -2
@@ -41,7 +42,9 @@ EXPORTS = [
     "gf_knn_result_bytes", "gf_knn_enqueue",
     "gf_knn_decode", "gf_knn_run", "gf_knn_merge_dev", "gf_knn_merge_dev_batch", "gf_knn_merge_host",
     "gf_knn_sliding_create", "gf_knn_sliding_destroy", "gf_knn_sliding_geometry", "gf_knn_sliding_push",
-    "gf_knn_sliding_flush", "gf_knn_sliding_decode", "gf_pane_bounds", "gf_csv_parse", "gf_join_pp",
+    "gf_knn_sliding_flush", "gf_knn_sliding_decode", "gf_pane_bounds", "gf_csv_parse", "gf_csv_parse_dict",
+    "gf_objid_dict_create", "gf_objid_dict_destroy", "gf_ctx_objid_dict", "gf_objid_dict_size", "gf_objid_intern",
+    "gf_objid_decode", "gf_join_pp",
     "gf_join_ppoly_plan_create", "gf_join_ppoly_run", "gf_join_ppoly",
     "gf_window_create",
     "gf_window_destroy", "gf_window_upload", "gf_window_points", "gf_synth_uniform", "gf_pinned_alloc",
@@ -159,6 +162,14 @@ def lib():
             "gf_knn_sliding_decode": ([P, i64, P, P, P, P, pi32], C.c_int),
             "gf_pane_bounds": ([P, P, i64, i64, i64, i32, P], C.c_int),
             "gf_csv_parse": ([P, P, i64, P, C.POINTER(GfGrid), P, P, P, P, P, P, i64, pi64, pi64, pi32], C.c_int),
+            "gf_csv_parse_dict": ([P, P, P, i64, P, C.POINTER(GfGrid), P, P, P, P, P, P, i64, pi64, pi64, pi32],
+                                  C.c_int),
+            "gf_objid_dict_create": ([P, C.POINTER(P)], C.c_int),
+            "gf_objid_dict_destroy": ([P], None),
+            "gf_ctx_objid_dict": ([P, C.POINTER(P)], C.c_int),
+            "gf_objid_dict_size": ([P, pi64], C.c_int),
+            "gf_objid_intern": ([P, C.c_char_p, P, i64, P], C.c_int),
+            "gf_objid_decode": ([P, P, i64, P, i64, P], C.c_int),
             "gf_join_pp": ([P, C.POINTER(GfGrid), C.POINTER(GfGrid), C.POINTER(GfPoints), C.POINTER(GfPoints), d,
                             C.c_int, C.c_int, P, i64, pi64], C.c_int),
             "gf_join_ppoly_plan_create": ([P, C.POINTER(GfGrid), C.POINTER(GfPolygons), d, C.c_int, C.c_int,

@@ -3,6 +3,7 @@
 //
 //   count newlines per 64 KB segment -> exclusive scan -> (sync: line count, capacity check)
 //   -> newline positions -> one lane per line parse + cell -> (sync: first bad line, if any)
+//   -> objID Strings that are not canonical decimals -> dictionary keys (objid.cpp)
 #include <cstring>
 #include <string>
 
@@ -13,13 +14,22 @@ using namespace gf;
 extern "C" int gf_csv_parse(gf_ctx* ctx, const char* text, int64_t len, const gf_csv_schema* sc, const gf_grid* g,
                             double* x, double* y, int64_t* objID, int64_t* ts, int32_t* cx, int32_t* cy, int64_t cap,
                             int64_t* n_out, int64_t* bad_line, int32_t* bad_kind) {
+  return gf_csv_parse_dict(ctx, nullptr, text, len, sc, g, x, y, objID, ts, cx, cy, cap, n_out, bad_line, bad_kind);
+}
+
+extern "C" int gf_csv_parse_dict(gf_ctx* ctx, gf_objid_dict* dict, const char* text, int64_t len,
+                                 const gf_csv_schema* sc, const gf_grid* g, double* x, double* y, int64_t* objID,
+                                 int64_t* ts, int32_t* cx, int32_t* cy, int64_t cap, int64_t* n_out, int64_t* bad_line,
+                                 int32_t* bad_kind) {
   if (!ctx || !sc || !n_out || len < 0 || (len > 0 && !text) || !x || !y || !objID || !ts || (!cx) != (!cy) ||
       (cx && !g) || sc->objid_field < 0 || sc->time_field < 0 || sc->x_field < 0 || sc->y_field < 0)
     return set_err(ctx, GF_ERR_ARG, "gf_csv_parse: bad argument");
   if (g && !(g->n > 0 && g->cellLength > 0)) return set_err(ctx, GF_ERR_ARG, "gf_csv_parse: bad grid");
   if ((uintptr_t)text & 15) return set_err(ctx, GF_ERR_ALIGN, "gf_csv_parse: text must be 16-byte aligned");
+  if (dict && dict->ctx != ctx) return set_err(ctx, GF_ERR_ARG, "gf_csv_parse: dictionary of another context");
   int st = bind(ctx);
   if (st) return st;
+  if (!dict && (st = ctx_dict(ctx, &dict))) return st;
   *n_out = 0;
   if (bad_line) *bad_line = -1;
   if (bad_kind) *bad_kind = GF_CSV_OK;
@@ -34,7 +44,7 @@ extern "C" int gf_csv_parse(gf_ctx* ctx, const char* text, int64_t len, const gf
   // the newline array is sized after the count; reserve a first guess (one line per 32 B)
   char* base = (char*)ctx_scratch(ctx, o_nl + sizeof(int64_t) * (size_t)(len / 32 + 2), &st);
   if (st) return st;
-  uint32_t* pinned = (uint32_t*)ctx_pinned(ctx, 16, &st);
+  uint32_t* pinned = (uint32_t*)ctx_pinned(ctx, 64, &st);
   if (st) return st;
   auto count = [&]() -> int {
     GF_HIP_CHECK(ctx, launch_csv_count(ctx->stream, text, len, nseg, (uint32_t*)(base + o_cnt)));
@@ -59,6 +69,10 @@ extern "C" int gf_csv_parse(gf_ctx* ctx, const char* text, int64_t len, const gf
       if ((st = count())) return st;
     }
   }
+  if (lines > (int64_t)UINT32_MAX) return set_err(ctx, GF_ERR_ARG, "gf_csv_parse: more than 2^32-1 lines");
+  // the dictionary worklist: at most one String per line
+  if ((st = dict_reserve_batch(dict, (uint64_t)lines, (uint64_t)lines))) return st;
+  GF_HIP_CHECK(ctx, hipMemsetAsync(dict->counters + 2, 0, 2 * sizeof(unsigned long long), ctx->stream));
   const uint32_t* offs = (const uint32_t*)(base + o_off);
   int64_t* nl = (int64_t*)(base + o_nl);
   CsvErr* err = (CsvErr*)(base + o_err);
@@ -71,11 +85,17 @@ extern "C" int gf_csv_parse(gf_ctx* ctx, const char* text, int64_t len, const gf
   a.x = x; a.y = y; a.objID = objID; a.ts = ts; a.cx = cx; a.cy = cy;
   if (g) { a.minX = g->minX; a.minY = g->minY; a.cl = g->cellLength; }
   a.err = err;
+  a.dict_work = (DictWork*)dict->work[0];
+  a.dict_n = (uint32_t*)(dict->counters + 2);
+  a.dict_bytes = dict->counters + 3;
   GF_HIP_CHECK(ctx, launch_csv_parse(ctx, a));
   CsvErr he{};
+  unsigned long long dn[2] = {0, 0};
   GF_HIP_CHECK(ctx, hipMemcpyAsync(pinned, err, sizeof(CsvErr), hipMemcpyDeviceToHost, ctx->stream));
+  GF_HIP_CHECK(ctx, hipMemcpyAsync((char*)pinned + 32, dict->counters + 2, sizeof dn, hipMemcpyDeviceToHost, ctx->stream));
   GF_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
   std::memcpy(&he, pinned, sizeof(CsvErr));
+  std::memcpy(dn, (char*)pinned + 32, sizeof dn);
   if (he.line != ~0ull) {
     if (bad_line) *bad_line = (int64_t)he.line;
     if (bad_kind) *bad_kind = he.kind;
@@ -84,6 +104,12 @@ extern "C" int gf_csv_parse(gf_ctx* ctx, const char* text, int64_t len, const gf
                                  "empty line"};
     const int k = he.kind >= 0 && he.kind <= 4 ? he.kind : 1;
     return set_err(ctx, GF_ERR_ARG, "gf_csv_parse: line " + std::to_string(he.line) + ": " + what[k]);
+  }
+  // objID Strings that are not canonical decimals: keys from the dictionary (ids in line order)
+  const uint32_t nw = (uint32_t)dn[0];
+  if (nw > 0) {
+    if ((st = dict_reserve_table(dict, nw, dn[1]))) return st;
+    if ((st = dict_run(dict, text, 1, nw, (uint64_t)lines, objID))) return st;
   }
   return GF_OK;
 }

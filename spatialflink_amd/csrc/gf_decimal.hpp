@@ -60,6 +60,47 @@ GF_DHD inline int parse_java_long(const Src& s, Field f, int64_t* out) {
   return kNumOk;
 }
 
+// objID keys (include/geoflink_hip.h, "objID keys"): the reference keeps the objID field as
+// the String itself (Deserialization.java:317 strOId), so every distinct String must get its
+// own key.  The numeric fast path takes a field only when the String IS Long.toString(v) of a
+// v in [-2^62, 2^62) -- no sign '+', no leading zero, not "-0" -- so "7" -> 7 while "007",
+// "+7", " 7" and "abc" go to the dictionary (keys INT64_MIN + id, below -2^62).
+constexpr int64_t kObjKeyNumLo = -(int64_t(1) << 62);
+constexpr int64_t kObjKeyNumHi = int64_t(1) << 62;  // exclusive
+template <class Src>
+GF_DHD inline bool canonical_objid_key(const Src& s, Field f, int64_t* out) {
+  int64_t i = f.b;
+  auto next = [&](int64_t j) {  // first non-quote position >= j
+    while (j < f.e && s(j) == '"') ++j;
+    return j;
+  };
+  i = next(i);
+  if (i >= f.e) return false;
+  bool neg = false;
+  if (s(i) == '-') {
+    neg = true;
+    i = next(i + 1);
+    if (i >= f.e) return false;
+  }
+  if (s(i) == '0') {  // "0" alone; "-0", "00", "05" are not Long.toString output
+    if (neg) return false;
+    if (next(i + 1) < f.e) return false;
+    *out = 0;
+    return true;
+  }
+  uint64_t v = 0;
+  int nd = 0;
+  for (; i < f.e; i = next(i + 1)) {
+    const char c = s(i);
+    if (c < '0' || c > '9' || ++nd > 19) return false;
+    v = v * 10 + (uint64_t)(c - '0');
+  }
+  if (nd == 0) return false;
+  if (neg ? v > (uint64_t)1 << 62 : v >= (uint64_t)1 << 62) return false;
+  *out = neg ? (int64_t)(0ull - v) : (int64_t)v;
+  return true;
+}
+
 GF_DHD inline int clz64(uint64_t x) { return __builtin_clzll(x); }
 
 // Eisel-Lemire for binary64 (w != 0): the correctly rounded bits of w * 10^q.

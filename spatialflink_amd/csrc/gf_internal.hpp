@@ -35,6 +35,33 @@ struct gf_ctx {
   int join_legacy = 0;  // testing: force the original (unbucketed) join probe
   double join_ppp = 0.0;  // pairs per ordinary point of the last join (sizes the task regions)
   hipStream_t aux = nullptr;  // kNN depth 3: odd windows' launches (created on first use)
+  gf_objid_dict* dict = nullptr;  // the context's default objID dictionary (created on first use)
+};
+
+// objID dictionary (objid.cpp): device hash table + arena, batch buffers, host mirror for decode
+struct gf_objid_dict {
+  gf_ctx* ctx = nullptr;
+  void* slots = nullptr;          // gf::DictSlot[cap]
+  uint64_t cap = 0;               // power of two
+  char* arena = nullptr;
+  uint64_t arena_cap = 0;
+  unsigned long long* counters = nullptr;  // [0] arena bytes used, [1] pending count, [2] csv count, [3] csv bytes
+  unsigned long long* idmap = nullptr;
+  uint64_t idmap_cap = 0;
+  int64_t size = 0;               // ids assigned
+  uint32_t round = 2;
+  void* work[3] = {nullptr, nullptr, nullptr};  // gf::DictWork: the batch, two pending lists
+  uint64_t work_cap = 0;
+  uint32_t* slot_of = nullptr;
+  uint32_t* flag = nullptr;
+  uint32_t* rank = nullptr;
+  uint32_t* tmp = nullptr;
+  uint64_t line_cap = 0;
+  char* src = nullptr;            // host intern: uploaded Strings
+  uint64_t src_cap = 0;
+  // host mirror of idmap / arena, extended on demand by gf_objid_decode
+  std::vector<unsigned long long> h_idmap;
+  std::vector<char> h_arena;
 };
 
 namespace gf {
@@ -236,6 +263,50 @@ hipError_t launch_word_popcounts(hipStream_t s, const uint64_t* bitmap, int64_t 
 hipError_t launch_expand_bitmap(hipStream_t s, const uint64_t* bitmap, int64_t words, int64_t n,
                                 const uint32_t* off, uint32_t* idx, int64_t cap);
 
+// objID dictionary (k_objid.hip, objid.cpp)
+constexpr int kDictLenBits = 20;  // slot meta = arena offset << 20 | String length
+constexpr uint64_t kDictLenMask = (1ull << kDictLenBits) - 1;
+struct DictSlot {                 // 32 B
+  unsigned long long tag;         // 0 = empty, else hash | 1
+  unsigned long long meta;        // arena offset << kDictLenBits | length
+  long long id;                   // -1 until the batch's id pass
+  unsigned int first;             // smallest batch position mapping here (new slots)
+  unsigned int round;             // probe round that created it (0 = being created)
+};
+struct DictWork {                 // one String of a batch: source bytes [b, b + n), '"' skipped if quotes
+  int64_t b;
+  int32_t n;
+  uint32_t line;                  // batch position
+};
+struct DictDev {
+  DictSlot* slots;
+  uint64_t mask;
+  char* arena;
+  unsigned long long* arena_used;
+  unsigned long long* idmap;      // [id] = meta
+};
+struct DictBatch {
+  const char* src;
+  int quotes;
+  const DictWork* work;
+  uint32_t nwork;
+  DictWork* pend_out;
+  uint32_t* npend_out;
+  uint32_t* slot_of;              // [lines]
+  uint32_t* flag;                 // [lines + 1]
+  const uint32_t* rank;           // [lines + 1]
+  uint32_t round, round0;
+  int64_t id_base;
+  int64_t* keys;                  // [lines]
+};
+hipError_t launch_dict(hipStream_t st, int stage, const DictDev& d, const DictBatch& B);
+hipError_t launch_dict_rehash(hipStream_t st, const DictDev& d, int64_t n);
+int dict_reserve_batch(gf_objid_dict* d, uint64_t nwork, uint64_t lines);
+int dict_reserve_table(gf_objid_dict* d, uint64_t more, uint64_t bytes);
+// keys of the batch in d->work[0] -> keys[line] (sync)
+int dict_run(gf_objid_dict* d, const char* src, int quotes, uint32_t nwork, uint64_t lines, int64_t* keys);
+int ctx_dict(gf_ctx* ctx, gf_objid_dict** out);  // the context's default dictionary
+
 // CSV ingest (k_csv.hip)
 constexpr int64_t kCsvSeg = 64 * 1024;  // text bytes per count / index block
 constexpr int kCsvLds = 24 * 1024;      // parse: a block's 256 lines staged in LDS when they fit
@@ -261,6 +332,10 @@ struct CsvArgs {
   int32_t* cy;
   double minX, minY, cl;
   CsvErr* err;
+  // objID fields that are not canonical decimals (gf_decimal.hpp): queued for the dictionary
+  DictWork* dict_work;           // [lines]
+  uint32_t* dict_n;
+  unsigned long long* dict_bytes;  // sum of their raw lengths (arena bound)
 };
 hipError_t launch_csv_count(hipStream_t st, const char* text, int64_t len, int64_t nseg, uint32_t* counts);
 hipError_t launch_csv_index(hipStream_t st, const char* text, int64_t len, int64_t nseg, const uint32_t* seg_off,

@@ -6,8 +6,9 @@
 //   csv_index   the newline positions, in order (block-wide prefix of per-thread counts)
 //   csv_parse   one lane per line: quotes dropped, fields split on the delimiter with the
 //               surrounding whitespace (the reference's split("\\s*" + delim + "\\s*")),
-//               Long.valueOf(objID, time), Double.valueOf(x, y) correctly rounded on the device
-//               (gf_decimal.hpp), cell (cx, cy), SoA stores.
+//               the objID String as its key (canonical decimals directly, the rest queued for
+//               the dictionary, k_objid.hip), Long.valueOf(time), Double.valueOf(x, y) correctly
+//               rounded on the device (gf_decimal.hpp), cell (cx, cy), SoA stores.
 #include "gf_decimal.hpp"
 #include "gf_internal.hpp"
 
@@ -157,42 +158,63 @@ __device__ int split_line(const Src& s, int64_t b, int64_t e, char d, const int3
   return field;
 }
 
+// One line, in the reference's order: strOId = get(objid) (any String: canonical decimals become
+// their key here, the rest is queued for the dictionary), time = Long.valueOf(get(time)),
+// x = Double.valueOf(get(x)), y = Double.valueOf(get(y)); the first missing field
+// (IndexOutOfBounds) or malformed number (NumberFormatException) is the line's error.
+struct LineOut {
+  int64_t obj, ts;
+  double x, y;
+  bool dict;        // objID is not a canonical decimal: f_obj goes to the dictionary
+  Field f_obj;
+};
 template <class Src>
-__device__ __forceinline__ void parse_line(const CsvArgs& a, const Src& s, int64_t j) {
+__device__ __forceinline__ int eval_line(const CsvArgs& a, const Src& s, int64_t j, LineOut* o) {
   const int64_t b = j == 0 ? 0 : a.nl[j - 1] + 1;
   int64_t e = j < a.newlines ? a.nl[j] : a.len;
   if (e > b && s(e - 1) == '\r') --e;  // TextInputFormat drops the '\r' of "\r\n"
-  int err = kCsvOk;
+  if (e <= b) return kCsvEmptyLine;
   Field f[4] = {{0, 0}, {0, 0}, {0, 0}, {0, 0}};
-  int64_t obj = 0, ts = 0;
-  double x = 0.0, y = 0.0;
-  if (e <= b) {
-    err = kCsvEmptyLine;
-  } else {
-    const int nf = split_line(s, b, e, a.delim, a.want, f);
-    int st = kNumOk;
-    if (a.want[0] >= nf || a.want[1] >= nf || a.want[2] >= nf || a.want[3] >= nf) err = kCsvMissingField;
-    else if ((st = parse_java_long(s, f[0], &obj)) || (st = parse_java_long(s, f[1], &ts)) ||
-             (st = parse_java_double(s, f[2], kPow5Dev, &x)) || (st = parse_java_double(s, f[3], kPow5Dev, &y)))
-      err = st == kNumUnsupported ? kCsvUnsupported : kCsvNumberFormat;
-  }
-  if (err != kCsvOk) {
+  const int nf = split_line(s, b, e, a.delim, a.want, f);
+  if (a.want[0] >= nf) return kCsvMissingField;
+  o->dict = !canonical_objid_key(s, f[0], &o->obj);
+  o->f_obj = f[0];
+  if (o->dict && f[0].e - f[0].b > (int64_t)kDictLenMask) return kCsvUnsupported;
+  int st;
+  if (a.want[1] >= nf) return kCsvMissingField;
+  if ((st = parse_java_long(s, f[1], &o->ts))) return st == kNumUnsupported ? kCsvUnsupported : kCsvNumberFormat;
+  if (a.want[2] >= nf) return kCsvMissingField;
+  if ((st = parse_java_double(s, f[2], kPow5Dev, &o->x))) return st == kNumUnsupported ? kCsvUnsupported : kCsvNumberFormat;
+  if (a.want[3] >= nf) return kCsvMissingField;
+  if ((st = parse_java_double(s, f[3], kPow5Dev, &o->y))) return st == kNumUnsupported ? kCsvUnsupported : kCsvNumberFormat;
+  return kCsvOk;
+}
+
+// parse + store line j; returns true when its objID needs the dictionary (*w filled)
+template <class Src>
+__device__ __forceinline__ bool parse_line(const CsvArgs& a, const Src& s, int64_t j, DictWork* w) {
+  LineOut o{0, 0, 0.0, 0.0, false, {0, 0}};
+  if (eval_line(a, s, j, &o) != kCsvOk) {
     atomicMin(&a.err->line, (unsigned long long)j);
-    return;
+    return false;
   }
-  a.x[j] = x;
-  a.y[j] = y;
-  a.objID[j] = obj;
-  a.ts[j] = ts;
+  a.x[j] = o.x;
+  a.y[j] = o.y;
+  a.ts[j] = o.ts;
+  if (!o.dict) a.objID[j] = o.obj;
   if (a.cx) {
-    a.cx[j] = cell_index(x, a.minX, a.cl);
-    a.cy[j] = cell_index(y, a.minY, a.cl);
+    a.cx[j] = cell_index(o.x, a.minX, a.cl);
+    a.cy[j] = cell_index(o.y, a.minY, a.cl);
   }
+  if (o.dict) *w = DictWork{o.f_obj.b, (int32_t)(o.f_obj.e - o.f_obj.b), (uint32_t)j};
+  return o.dict;
 }
 
 // A block takes 256 consecutive lines.  Their bytes are contiguous: when they fit kCsvLds they
 // are staged in LDS with coalesced 16-B loads first, so the per-byte reads of the split/parse
 // state machines (a dependent chain per lane) hit LDS instead of waiting on L2 one byte at a time.
+// Dictionary objIDs are queued with one atomic per wave (the queue order is free: ids follow
+// line order, k_objid.hip).
 __global__ __launch_bounds__(kBlock) void csv_parse_kernel(CsvArgs a) {
   __shared__ __attribute__((aligned(16))) char lds[kCsvLds];
   const int64_t L0 = (int64_t)blockIdx.x * kBlock;
@@ -201,6 +223,8 @@ __global__ __launch_bounds__(kBlock) void csv_parse_kernel(CsvArgs a) {
   const int64_t b1 = L1 - 1 < a.newlines ? a.nl[L1 - 1] : a.len;     // the last line's '\n' (or end)
   const int64_t a0 = b0 & ~(int64_t)15;
   const int64_t j = L0 + threadIdx.x;
+  DictWork w{0, 0, 0};
+  bool need = false;
   if (b1 - a0 <= kCsvLds) {  // block-uniform
     for (int64_t off = a0 + 16 * threadIdx.x; off < b1; off += 16 * kBlock) {
       if (off + 16 <= a.len) {
@@ -210,9 +234,23 @@ __global__ __launch_bounds__(kBlock) void csv_parse_kernel(CsvArgs a) {
       }
     }
     __syncthreads();
-    if (j < L1) parse_line(a, LBytes{lds, a0}, j);
+    if (j < L1) need = parse_line(a, LBytes{lds, a0}, j, &w);
   } else if (j < L1) {
-    parse_line(a, GBytes{a.text}, j);
+    need = parse_line(a, GBytes{a.text}, j, &w);
+  }
+  const uint64_t m = __ballot(need);
+  if (m) {
+    const int lane = threadIdx.x & 63;
+    unsigned long long nb = need ? (unsigned long long)w.n : 0ull;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) nb += __shfl_xor(nb, o, 64);
+    uint32_t base = 0;
+    if (lane == 0) {
+      base = atomicAdd(a.dict_n, (uint32_t)__popcll(m));
+      atomicAdd(a.dict_bytes, nb);
+    }
+    base = __shfl(base, 0, 64);
+    if (need) a.dict_work[base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = w;
   }
 }
 
@@ -220,25 +258,8 @@ __global__ __launch_bounds__(kBlock) void csv_parse_kernel(CsvArgs a) {
 __global__ void csv_error_kernel(CsvArgs a) {
   const unsigned long long j = a.err->line;
   if (j == ~0ull || threadIdx.x != 0) return;
-  const GBytes s{a.text};
-  const int64_t b = j == 0 ? 0 : a.nl[j - 1] + 1;
-  int64_t e = (int64_t)j < a.newlines ? a.nl[j] : a.len;
-  if (e > b && s(e - 1) == '\r') --e;
-  int kind = kCsvEmptyLine;
-  if (e > b) {
-    Field f[4] = {{0, 0}, {0, 0}, {0, 0}, {0, 0}};
-    const int nf = split_line(s, b, e, a.delim, a.want, f);
-    int64_t v;
-    double d;
-    int st = kNumOk;
-    if (a.want[0] >= nf || a.want[1] >= nf || a.want[2] >= nf || a.want[3] >= nf) kind = kCsvMissingField;
-    else if ((st = parse_java_long(s, f[0], &v)) || (st = parse_java_long(s, f[1], &v)) ||
-             (st = parse_java_double(s, f[2], kPow5Dev, &d)) || (st = parse_java_double(s, f[3], kPow5Dev, &d)))
-      kind = st == kNumUnsupported ? kCsvUnsupported : kCsvNumberFormat;
-    else
-      kind = kCsvOk;
-  }
-  a.err->kind = kind;
+  LineOut o{0, 0, 0.0, 0.0, false, {0, 0}};
+  a.err->kind = eval_line(a, GBytes{a.text}, (int64_t)j, &o);
 }
 
 hipError_t launch_csv_count(hipStream_t st, const char* text, int64_t len, int64_t nseg, uint32_t* counts) {

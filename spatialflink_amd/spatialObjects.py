@@ -3,10 +3,12 @@ batch that crosses the C ABI at each window trigger.
 
 A PointWindow is the device-resident struct-of-arrays form of a window's Iterable<Point>:
 x, y (float64, 16-B aligned), objID and timeStampMillisec (int64), as torch CUDA tensors.
-objID strings are carried as their int64 decimal value.
+objID Strings (Point.objID) are carried as int64 keys (include/geoflink_hip.h "objID keys"):
+a canonical decimal String is its value, any other String its id in an ObjIdDict.
 """
 from __future__ import annotations
 
+import ctypes as C
 from dataclasses import dataclass, field
 from typing import Optional
 
@@ -14,6 +16,79 @@ import numpy as np
 
 from . import _lib
 from .spatialIndices import UniformGrid, generateCellIDStr
+
+
+class ObjIdDict:
+    """gf_objid_dict: String objIDs <-> int64 keys.  ObjIdDict.default(device) is the device
+    context's dictionary, the one the CSV ingest uses; keys of one dictionary are equal iff
+    their Strings are."""
+
+    _defaults = {}
+
+    def __init__(self, device: int = 0, handle=None, owned=True):
+        self.device = int(device)
+        self.ctx = _lib.context(self.device)
+        if handle is None:
+            h = C.c_void_p()
+            _lib.check(_lib.lib().gf_objid_dict_create(self.ctx.handle, C.byref(h)), self.ctx.handle,
+                       "gf_objid_dict_create")
+            handle = h
+        self.handle = handle
+        self.owned = owned
+
+    @classmethod
+    def default(cls, device: int = 0) -> "ObjIdDict":
+        ctx = _lib.context(int(device))
+        key = id(ctx)
+        d = cls._defaults.get(key)
+        if d is None:
+            h = C.c_void_p()
+            _lib.check(_lib.lib().gf_ctx_objid_dict(ctx.handle, C.byref(h)), ctx.handle, "gf_ctx_objid_dict")
+            d = cls(device, h, owned=False)
+            cls._defaults[key] = d
+        return d
+
+    def size(self) -> int:
+        n = C.c_int64()
+        _lib.check(_lib.lib().gf_objid_dict_size(self.handle, C.byref(n)), None, "gf_objid_dict_size")
+        return n.value
+
+    def intern(self, objids) -> np.ndarray:
+        """keys of Strings (str or bytes; str is UTF-8 encoded) -> int64[n]"""
+        bs = [o.encode() if isinstance(o, str) else bytes(o) for o in objids]
+        offs = np.zeros(len(bs) + 1, np.int64)
+        offs[1:] = np.cumsum([len(b) for b in bs])
+        blob = b"".join(bs)
+        keys = np.empty(len(bs), np.int64)
+        _lib.check(_lib.lib().gf_objid_intern(self.handle, blob, offs.ctypes.data, len(bs), keys.ctypes.data),
+                   self.ctx.handle, "gf_objid_intern")
+        return keys
+
+    def decode_bytes(self, keys):
+        """int64 keys -> list of bytes (the Strings' UTF-8)"""
+        k = np.ascontiguousarray(np.asarray(keys, np.int64))
+        offs = np.zeros(len(k) + 1, np.int64)
+        cap = 64 * len(k) + 64
+        for _ in range(2):
+            buf = C.create_string_buffer(cap)
+            st = _lib.lib().gf_objid_decode(self.handle, k.ctypes.data, len(k), buf, cap, offs.ctypes.data)
+            if st == _lib.GF_ERR_CAPACITY:
+                cap = int(offs[-1])
+                continue
+            _lib.check(st, self.ctx.handle, "gf_objid_decode")
+            raw = buf.raw
+            return [raw[offs[i]:offs[i + 1]] for i in range(len(k))]
+        raise _lib.GeoFlinkError(_lib.GF_ERR_CAPACITY, "gf_objid_decode")
+
+    def decode(self, keys):
+        """int64 keys -> list of str"""
+        return [b.decode("utf-8", "surrogateescape") for b in self.decode_bytes(keys)]
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h and getattr(self, "owned", False) and _lib._lib is not None:
+            _lib._lib.gf_objid_dict_destroy(h)
+            self.handle = None
 
 
 class Point:
@@ -138,6 +213,7 @@ class PointWindow:
     start: int = 0
     end: int = 0
     extra: dict = field(default_factory=dict)
+    objid_dict: Optional[ObjIdDict] = None   # the dictionary of its non-numeric objID keys
 
     @property
     def n(self) -> int:
@@ -155,12 +231,29 @@ class PointWindow:
         return cls(t(x, np.float64), t(y, np.float64), t(objID, np.int64), t(ts, np.int64), start, end)
 
     @classmethod
-    def from_points(cls, points, device=None, start=0, end=0):
+    def from_points(cls, points, device=None, start=0, end=0, objid_dict: Optional[ObjIdDict] = None):
+        """Points with String (or int) objIDs; Strings are mapped to keys by `objid_dict`
+        (default: the device context's dictionary)."""
+        import torch
+
+        points = list(points)
+        dev = torch.cuda.current_device() if device is None else device
+        d = objid_dict or ObjIdDict.default(dev)
         x = np.array([p.x for p in points], np.float64)
         y = np.array([p.y for p in points], np.float64)
-        o = np.array([int(p.objID) for p in points], np.int64)
+        o = d.intern([str(p.objID) if p.objID is not None else "null" for p in points])
         ts = np.array([p.timeStampMillisec for p in points], np.int64)
-        return cls.from_numpy(x, y, o, ts, device, start, end)
+        w = cls.from_numpy(x, y, o, ts, device, start, end)
+        w.objid_dict = d
+        return w
+
+    def objid_strings(self, keys=None):
+        """Strings of objID keys (default: every point's)."""
+        import torch
+
+        k = self.objID.cpu().numpy() if keys is None else np.asarray(keys, np.int64)
+        d = self.objid_dict or ObjIdDict.default(self.x.device.index if self.x.is_cuda else torch.cuda.current_device())
+        return d.decode(k)
 
     def c_struct(self) -> _lib.GfPoints:
         for t in (self.x, self.y):
@@ -171,5 +264,5 @@ class PointWindow:
 
     def point(self, i: int, uGrid: Optional[UniformGrid] = None) -> Point:
         i = int(i)
-        return Point(str(int(self.objID[i])), float(self.x[i]), float(self.y[i]), int(self.timeStampMillisec[i]),
-                     uGrid)
+        return Point(self.objid_strings([int(self.objID[i])])[0], float(self.x[i]), float(self.y[i]),
+                     int(self.timeStampMillisec[i]), uGrid)

@@ -6,7 +6,9 @@ Double.valueOf and assigns its grid cell in the Point constructor (Point.java:98
 chunk of lines (device bytes, or host bytes uploaded once) becomes the window's SoA in one call:
 gf_csv_parse (k_csv.hip) finds the lines, splits the fields with the reference's
 "\\s*delim\\s*" rule, parses the numbers correctly rounded on the device and writes x, y,
-objID, ts and the cells (cx, cy) -- no per-point host work.  A bad line raises ValueError naming
+objID keys (the objID field is a String, :317 -- canonical decimals are their value, any other
+String goes through the device dictionary, k_objid.hip), ts and the cells (cx, cy) -- no
+per-point host work.  A bad line raises ValueError naming
 it (the reference's map throws NumberFormatException / IndexOutOfBoundsException).
 """
 from __future__ import annotations
@@ -16,7 +18,7 @@ import ctypes as C
 import numpy as np
 
 from . import _lib
-from .spatialObjects import PointWindow
+from .spatialObjects import ObjIdDict, PointWindow
 
 
 class GfCsvSchema(C.Structure):
@@ -55,13 +57,15 @@ class Deserialization:
             a = list(csvTsvSchemaAttr)
             self.schema = GfCsvSchema(delimiter.encode(), b"\0\0\0", a[0], a[1], a[2], a[3])
 
-        def parse(self, text, device=None, capacity=None) -> PointWindow:
-            """All lines of `text` -> one PointWindow (extra: cx, cy when a grid is set)."""
+        def parse(self, text, device=None, capacity=None, objid_dict: ObjIdDict = None) -> PointWindow:
+            """All lines of `text` -> one PointWindow (extra: cx, cy when a grid is set).  objID
+            Strings become keys of `objid_dict` (default: the device context's dictionary)."""
             import torch
 
             t = device_text(text, device)
             dev = t.device
             ctx = _lib.context(dev.index)
+            d = objid_dict or ObjIdDict.default(dev.index)
             n = int(t.numel())
             cap = capacity if capacity is not None else max(1, n // 8 + 1)
             L = _lib.lib()
@@ -73,7 +77,7 @@ class Deserialization:
                 ts = torch.empty(cap, dtype=torch.int64, device=dev)
                 cx = torch.empty(cap, dtype=torch.int32, device=dev) if self.uGrid is not None else None
                 cy = torch.empty(cap, dtype=torch.int32, device=dev) if self.uGrid is not None else None
-                st = L.gf_csv_parse(ctx.handle, C.c_void_p(t.data_ptr()), n, C.byref(self.schema),
+                st = L.gf_csv_parse_dict(ctx.handle, d.handle, C.c_void_p(t.data_ptr()), n, C.byref(self.schema),
                                     C.byref(self.uGrid.c_grid) if self.uGrid is not None else None,
                                     x.data_ptr(), y.data_ptr(), o.data_ptr(), ts.data_ptr(),
                                     cx.data_ptr() if cx is not None else None,
@@ -87,7 +91,7 @@ class Deserialization:
                 _lib.check(st, ctx.handle, "gf_csv_parse")
                 break
             m = nout.value
-            w = PointWindow(x[:m], y[:m], o[:m], ts[:m])
+            w = PointWindow(x[:m], y[:m], o[:m], ts[:m], objid_dict=d)
             if cx is not None:
                 w.extra["cx"], w.extra["cy"] = cx[:m], cy[:m]
             return w

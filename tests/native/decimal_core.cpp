@@ -23,3 +23,7 @@ extern "C" int core_parse_long(const char* s, int64_t len, int64_t* out) {
 extern "C" void core_parse_many(const char* buf, const int64_t* off, int64_t n, double* out, int32_t* st) {
   for (int64_t j = 0; j < n; ++j) st[j] = core_parse_double(buf + off[j], off[j + 1] - off[j], out + j);
 }
+// objID fast path: 1 + key when the String is a canonical decimal key, 0 when it needs the dictionary
+extern "C" int core_objid_key(const char* s, int64_t len, int64_t* out) {
+  return gf::canonical_objid_key(Str{s}, gf::Field{0, len}, out) ? 1 : 0;
+}

@@ -22,7 +22,7 @@ def header_symbols():
 
 def test_library_loads():
     L = _lib.lib()
-    assert L.gf_abi_version() == 1
+    assert L.gf_abi_version() == 2
 
 
 def test_exports_match_header():

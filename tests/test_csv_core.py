@@ -136,3 +136,24 @@ def test_java_long(core):
     for s in ["", "-", "9223372036854775808", "-9223372036854775809", "1.0", " 1", "1 ", "1e3"]:
         v = C.c_int64()
         assert core.core_parse_long(s.encode(), len(s), C.byref(v)) == BAD, s
+
+
+def test_objid_canonical_keys(core):
+    """objID Strings (Deserialization.java:317) take the numeric key only when the String is
+    Long.toString(v) of v in [-2^62, 2^62) (quotes are removed before the split): the key map is
+    injective over Strings -- "7" and "007" / "+7" / " 7" / "-0" never share a key."""
+    core.core_objid_key.argtypes = [C.c_char_p, C.c_int64, C.POINTER(C.c_int64)]
+    rng = random.Random(3)
+    cases = ["0", "7", "-7", "-0", "00", "007", "+7", " 7", "7 ", "", "-", "abc", "1e3", "12a",
+             str(2**62 - 1), str(2**62), str(-(2**62)), str(-(2**62) - 1), str(2**63 - 1), "9" * 19, "9" * 20,
+             '"7"', '7"', '"-"12']
+    cases += [str(rng.randint(-2**63, 2**63 - 1)) for _ in range(2000)]
+    cases += [str(rng.randint(-10**6, 10**6)) for _ in range(2000)]
+    for s in cases:
+        v = C.c_int64()
+        ok = core.core_objid_key(s.encode(), len(s), C.byref(v))
+        t = s.replace('"', "")
+        canon = t.lstrip("-").isdigit() and str(int(t)) == t and -(2**62) <= int(t) < 2**62
+        assert ok == canon, s
+        if ok:
+            assert v.value == int(t), s
