@@ -57,7 +57,9 @@ extern "C" {
 #define GF_K_JOIN_BUCKET 7  /* ordinary-side bucketing of the join */
 #define GF_K_KNN_MERGE   8  /* top-k record merges (shards, sliding-window panes) */
 #define GF_K_CSV_PARSE   9  /* CSV ingest: the per-line parse kernel */
-#define GF_K_COUNT       10
+#define GF_K_BUCKET      10 /* K2 bucketing by cell (gf_bucket_by_cell) */
+#define GF_K_JOIN_COMPACT 11 /* join: packing of the probe's task regions */
+#define GF_K_COUNT       12
 
 typedef struct gf_ctx gf_ctx;
 
@@ -154,8 +156,9 @@ int gf_assign_cells(gf_ctx* ctx, const gf_grid* g, const gf_points* pts, int32_t
 
 /* ---- K2: bucketing by cell (async) -- the keyBy(gridID) shuffle (PointPointRangeQuery.java:144-148)
  * perm: device uint32[n], point indices grouped by cell; cell_start: device uint32[n*n + 2],
- * bucket b = valid cell cy*n + cx, bucket n*n = out-of-grid points.  Order inside a bucket is
- * unspecified. */
+ * bucket b = valid cell cy*n + cx, bucket n*n = out-of-grid points: bucket b is
+ * perm[cell_start[b] .. cell_start[b+1]).  Stable: inside a bucket the points keep their input
+ * order (Flink's per-key window buffer iterates in arrival order), so the result is unique. */
 int gf_bucket_by_cell(gf_ctx* ctx, const gf_grid* g, const gf_points* pts, uint32_t* perm,
                       uint32_t* cell_start);
 

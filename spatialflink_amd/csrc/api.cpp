@@ -407,23 +407,48 @@ extern "C" int gf_bucket_by_cell(gf_ctx* ctx, const gf_grid* g, const gf_points*
   const int64_t bins = (int64_t)g->n * g->n + 1;
   if (bins >= (int64_t)INT32_MAX) return set_err(ctx, GF_ERR_ARG, "grid too large for bucketing");
   const int64_t n = pts->n;
+  if (n == 0) {
+    GF_HIP_CHECK(ctx, hipMemsetAsync(cell_start, 0, sizeof(uint32_t) * (size_t)(bins + 1), ctx->stream));
+    return GF_OK;
+  }
+  int bits = 1;
+  while (((int64_t)1 << bits) < bins) ++bits;
+  const int passes = (bits + kRadixBits - 1) / kRadixBits;
+  // >= ~4K points per wave-chunk, <= 2 blocks per CU (the digit matrix is 2048 x wave-chunks)
+  const int blocks = (int)std::min<int64_t>(std::max<int64_t>(n / (4 * 4096), 1), (int64_t)ctx->num_cus * 2);
+  const int64_t mat = (int64_t)kRadixDigits * blocks * (kBlock / 64);
   Arena ar;
-  size_t o_keys = ar.take<uint32_t>(n > 0 ? n : 1);
-  size_t o_hist = ar.take<uint32_t>(bins);
-  size_t o_cur = ar.take<uint32_t>(bins + 1);
-  size_t o_tmp = ar.take<uint32_t>(scan_tmp_elems(bins));
+  size_t o_k[2] = {ar.take<uint32_t>(n), ar.take<uint32_t>(n)};
+  size_t o_v[2] = {ar.take<uint32_t>(n), ar.take<uint32_t>(n)};
+  size_t o_k0 = ar.take<uint32_t>(n);  // pass 0's keys (stored by its histogram)
+  size_t o_m = ar.take<uint32_t>(mat), o_ms = ar.take<uint32_t>(mat + 1), o_h = ar.take<uint32_t>(bins);
+  size_t o_tmp = ar.take<uint32_t>(std::max(scan_tmp_elems(mat), scan_tmp_elems(bins)));
   char* base = (char*)ctx_scratch(ctx, ar.off, &st);
   if (st) return st;
-  uint32_t* keys = (uint32_t*)(base + o_keys);
-  uint32_t* hist = (uint32_t*)(base + o_hist);
-  uint32_t* cur = (uint32_t*)(base + o_cur);
-  uint32_t* tmp = (uint32_t*)(base + o_tmp);
-  GF_HIP_CHECK(ctx, hipMemsetAsync(hist, 0, bins * sizeof(uint32_t), ctx->stream));
-  GF_HIP_CHECK(ctx, launch_cell_keys(ctx->stream, g, pts->x, pts->y, n, 0, keys));
-  GF_HIP_CHECK(ctx, launch_histogram(ctx->stream, keys, n, hist));
-  GF_HIP_CHECK(ctx, launch_exclusive_scan(ctx->stream, hist, bins, cell_start, tmp));
-  GF_HIP_CHECK(ctx, hipMemcpyAsync(cur, cell_start, bins * sizeof(uint32_t), hipMemcpyDeviceToDevice, ctx->stream));
-  GF_HIP_CHECK(ctx, launch_scatter(ctx->stream, keys, n, cur, perm));
+  auto U32 = [&](size_t o) { return (uint32_t*)(base + o); };
+  RadixArgs a{};
+  a.x = pts->x; a.y = pts->y; a.n = n;
+  a.minX = g->minX; a.minY = g->minY; a.cl = g->cellLength; a.gn = g->n;
+  uint32_t* k0 = U32(o_k0);
+  for (int p = 0; p < passes; ++p) {
+    a.kin = p == 0 ? nullptr : U32(o_k[(p - 1) & 1]);
+    a.vin = p == 0 ? nullptr : U32(o_v[(p - 1) & 1]);
+    a.kout = p == 0 ? k0 : U32(o_k[p & 1]);
+    a.shift = p * kRadixBits;
+    a.M = U32(o_m);
+    a.Ms = U32(o_ms);
+    GF_HIP_CHECK(ctx, launch_radix(ctx, 0, a, blocks));  // pass 0: keys -> k0
+    GF_HIP_CHECK(ctx, launch_exclusive_scan(ctx->stream, U32(o_m), mat, U32(o_ms), U32(o_tmp)));
+    if (p == 0) a.kin = k0;  // the scatter reads the stored keys, index = position
+    a.kout = U32(o_k[p & 1]);
+    a.vout = p == passes - 1 ? perm : U32(o_v[p & 1]);
+    GF_HIP_CHECK(ctx, launch_radix(ctx, 1, a, blocks));
+  }
+  // bucket sizes from the sorted keys' runs, then their exclusive scan = cell_start[0 .. bins]
+  GF_HIP_CHECK(ctx, hipMemsetAsync(U32(o_h), 0, sizeof(uint32_t) * (size_t)bins, ctx->stream));
+  a.M = U32(o_h);
+  GF_HIP_CHECK(ctx, launch_radix(ctx, 2, a, blocks));
+  GF_HIP_CHECK(ctx, launch_exclusive_scan(ctx->stream, U32(o_h), bins, cell_start, U32(o_tmp)));
   return GF_OK;
 }
 

@@ -252,10 +252,26 @@ struct RangeArgs {
 
 // launchers (return hipError_t of the launch)
 hipError_t launch_assign(gf_ctx* ctx, const gf_grid* g, const gf_points* p, int32_t* cx, int32_t* cy);
-hipError_t launch_cell_keys(hipStream_t s, const gf_grid* g, const double* x, const double* y, int64_t n,
-                            int clamp_pad, uint32_t* keys);
 hipError_t launch_histogram(hipStream_t s, const uint32_t* keys, int64_t n, uint32_t* hist);
-hipError_t launch_scatter(hipStream_t s, const uint32_t* keys, int64_t n, uint32_t* cursor, uint32_t* perm);
+// K2: stable LSD radix bucketing (k_points.hip)
+constexpr int kRadixBits = 11;
+constexpr int kRadixDigits = 1 << kRadixBits;
+struct RadixArgs {
+  const double* x;          // pass 0 input (kin == null): keys from the cells of x, y
+  const double* y;
+  int64_t n;
+  double minX, minY, cl;
+  int32_t gn;
+  const uint32_t* kin;      // later passes: keys, point indices
+  const uint32_t* vin;
+  uint32_t* kout;
+  uint32_t* vout;
+  int shift;                // digit = (key >> shift) & (kRadixDigits - 1)
+  uint32_t* M;              // stage 0: [kRadixDigits][wave chunks]; stage 2: bucket sizes (zeroed)
+  const uint32_t* Ms;       // stage 1: the exclusive scan of M
+};
+// stage 0 histogram, 1 scatter, 2 bucket sizes of the sorted kout
+hipError_t launch_radix(gf_ctx* ctx, int stage, const RadixArgs& a, int blocks);
 // exclusive scan: out[0..L] (out[L] = total); tmp >= scan_tmp_elems(L) uint32
 size_t scan_tmp_elems(int64_t L);
 hipError_t launch_exclusive_scan(hipStream_t s, const uint32_t* in, int64_t L, uint32_t* out, uint32_t* tmp);

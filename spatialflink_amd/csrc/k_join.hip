@@ -710,7 +710,7 @@ __global__ __launch_bounds__(kBlock) void join_compact_kernel(JoinCompactArgs a)
 }
 
 hipError_t launch_join_compact(gf_ctx* ctx, const JoinCompactArgs& a) {
-  KTimer t(ctx, GF_K_JOIN_PROBE);
+  KTimer t(ctx, GF_K_JOIN_COMPACT);
   hipLaunchKernelGGL(join_compact_kernel, dim3(a.ntask + 64), dim3(kBlock), 0, ctx->stream, a);
   return hipGetLastError();
 }

@@ -1,5 +1,6 @@
-// k_points.hip -- per-point kernels: K1 cell assignment, K2 bucketing by cell (histogram,
-// exclusive scan, scatter), and selection-bitmap -> index expansion.  gfx950, wave64.
+// k_points.hip -- per-point kernels: K1 cell assignment, K2 bucketing by cell (stable LSD
+// radix sort: per-wave LDS histograms, wave-ballot ranking), exclusive scan, and selection-
+// bitmap -> index expansion.  gfx950, wave64.
 #include "gf_internal.hpp"
 
 namespace gf {
@@ -78,30 +79,147 @@ hipError_t launch_pane_bounds(hipStream_t s, const int64_t* ts, int64_t n, int64
 }
 
 // ---------------------------------------------------------------------------------------
-// K2 building blocks.  Bucket key of a point:
-//   clamp_pad == 0: valid cell -> cy*n + cx, out-of-grid -> n*n            (gf_bucket_by_cell)
+// K2: bucketing by cell -- the keyBy(gridID) shuffle (PointPointRangeQuery.java:144-148): a
+// stable LSD radix sort of the points' bucket keys (valid cell -> cy*n + cx, out-of-grid ->
+// n*n), kRadixBits per pass, so every bucket lists its points in input (arrival) order -- the
+// order Flink's per-key window buffer iterates -- and the result never depends on scheduling.
+//   radix_hist     per WAVE-chunk LDS histograms of the pass's digit (no global atomics)
+//   (scan)         of the digit-major matrix M[digit][wave-chunk] -> every wave-chunk's
+//                  first output slot per digit
+//   radix_scatter  each wave walks its chunk 64 points at a time: the lanes sharing a digit are
+//                  found with kRadixBits ballots, their rank = popcount below, and one LDS
+//                  atomic per (step, digit) on the wave's own cursors places the run -- no block
+//                  barrier, no global atomic, stable by construction.
+// Pass 0's histogram reads x, y (16 B/point) and stores the keys; every scatter reads (key,
+// index) -- pass 0's index is the position itself.
+// Afterwards: bucket sizes from the sorted keys' run boundaries -> exclusive scan = cell_start.
 // ---------------------------------------------------------------------------------------
-__global__ __launch_bounds__(kBlock) void cell_keys_kernel(const double* __restrict__ x,
-                                                           const double* __restrict__ y, int64_t n,
-                                                           double minX, double minY, double cl,
-                                                           int32_t gn, uint32_t* __restrict__ keys) {
-  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
-    const int32_t cx = cell_index(x[i], minX, cl);
-    const int32_t cy = cell_index(y[i], minY, cl);
-    const bool valid = cx >= 0 && cy >= 0 && cx < gn && cy < gn;
-    keys[i] = valid ? (uint32_t)cy * (uint32_t)gn + (uint32_t)cx : (uint32_t)gn * (uint32_t)gn;
+__device__ __forceinline__ uint32_t bucket_key(double x, double y, const RadixArgs& a) {
+  const int32_t cx = cell_index(x, a.minX, a.cl), cy = cell_index(y, a.minY, a.cl);
+  const bool valid = cx >= 0 && cy >= 0 && cx < a.gn && cy < a.gn;
+  return valid ? (uint32_t)cy * (uint32_t)a.gn + (uint32_t)cx : (uint32_t)a.gn * (uint32_t)a.gn;
+}
+
+// wave-chunk w of the nw = gridDim.x * waves_per_block chunks: [beg, end)
+__device__ __forceinline__ void wave_chunk(int64_t n, int64_t& beg, int64_t& end, int& w) {
+  const int64_t nw = (int64_t)gridDim.x * (kBlock / 64);
+  w = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+  const int64_t chunk = (n + nw - 1) / nw;
+  beg = (int64_t)w * chunk;
+  end = beg + chunk < n ? beg + chunk : n;
+  if (beg > n) beg = n;
+}
+
+constexpr int kRadixU = 8;  // 64-point steps whose loads are in flight together
+
+// FIRST: the key from x, y (histogram of pass 0, which also stores the keys); otherwise
+// (key, index) from the previous pass -- pass 0's scatter has vin == null: index = position
+template <bool FIRST>
+__device__ __forceinline__ void radix_load(const RadixArgs& a, int64_t i, int64_t end, uint32_t& k, uint32_t& v) {
+  if (i < end) {
+    if (FIRST) {
+      k = bucket_key(__builtin_nontemporal_load(a.x + i), __builtin_nontemporal_load(a.y + i), a);
+    } else {
+      k = a.kin[i];
+    }
+    v = a.vin ? a.vin[i] : (uint32_t)i;
+  } else {
+    k = 0u;
+    v = 0u;
   }
 }
 
-hipError_t launch_cell_keys(hipStream_t s, const gf_grid* g, const double* x, const double* y, int64_t n,
-                            int /*clamp_pad*/, uint32_t* keys) {
-  if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(cell_keys_kernel, dim3(stream_blocks(n, kBlock)), dim3(kBlock), 0, s, x, y, n,
-                     g->minX, g->minY, g->cellLength, g->n, keys);
+template <bool FIRST>
+__global__ __launch_bounds__(kBlock) void radix_hist_kernel(RadixArgs a) {
+  __shared__ uint32_t h[kBlock / 64][kRadixDigits];
+  const int wl = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (int j = lane; j < kRadixDigits; j += 64) h[wl][j] = 0u;
+  int64_t beg, end;
+  int w;
+  wave_chunk(a.n, beg, end, w);
+  for (int64_t i0 = beg + lane; i0 < end; i0 += 64 * kRadixU) {
+    uint32_t k[kRadixU], v[kRadixU];
+#pragma unroll
+    for (int u = 0; u < kRadixU; ++u) radix_load<FIRST>(a, i0 + 64 * u, end, k[u], v[u]);
+#pragma unroll
+    for (int u = 0; u < kRadixU; ++u)
+      if (i0 + 64 * u < end) {
+        atomicAdd(&h[wl][(k[u] >> a.shift) & (kRadixDigits - 1)], 1u);
+        if (FIRST) a.kout[i0 + 64 * u] = k[u];  // pass 0's scatter reads the keys, not x, y
+      }
+  }
+  const int64_t nw = (int64_t)gridDim.x * (kBlock / 64);
+  for (int j = lane; j < kRadixDigits; j += 64) a.M[(size_t)j * nw + w] = h[wl][j];
+}
+
+__global__ __launch_bounds__(kBlock) void radix_scatter_kernel(RadixArgs a) {
+  __shared__ uint32_t cur[kBlock / 64][kRadixDigits];
+  const int wl = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  int64_t beg, end;
+  int w;
+  wave_chunk(a.n, beg, end, w);
+  const int64_t nw = (int64_t)gridDim.x * (kBlock / 64);
+  for (int j = lane; j < kRadixDigits; j += 64) cur[wl][j] = a.Ms[(size_t)j * nw + w];
+  const uint64_t below = (1ull << lane) - 1ull;
+  for (int64_t s0 = beg; s0 < end; s0 += 64 * kRadixU) {  // wave-uniform
+    uint32_t k[kRadixU], v[kRadixU];
+#pragma unroll
+    for (int u = 0; u < kRadixU; ++u) radix_load<false>(a, s0 + 64 * u + lane, end, k[u], v[u]);
+#pragma unroll
+    for (int u = 0; u < kRadixU; ++u) {
+      const bool valid = s0 + 64 * u + lane < end;
+      const uint32_t d = (k[u] >> a.shift) & (kRadixDigits - 1);
+      uint64_t peers = __ballot(valid);
+#pragma unroll
+      for (int b = 0; b < kRadixBits; ++b) {
+        const uint64_t bal = __ballot((d >> b) & 1u);
+        peers &= ((d >> b) & 1u) ? bal : ~bal;
+      }
+      const uint32_t rank = (uint32_t)__popcll(peers & below);
+      uint32_t base = 0;
+      if (valid && rank == 0) base = atomicAdd(&cur[wl][d], (uint32_t)__popcll(peers));
+      const int leader = valid ? __ffsll((unsigned long long)peers) - 1 : lane;
+      base = __shfl(base, leader, 64);
+      if (valid) {
+        a.kout[base + rank] = k[u];
+        a.vout[base + rank] = v[u];
+      }
+    }
+  }
+}
+
+// bucket sizes from the sorted keys: +(run end) at the last point of a run, -(run start) at
+// its first (two atomics per non-empty bucket; hist zeroed before)
+__global__ __launch_bounds__(kBlock) void radix_runs_kernel(const uint32_t* __restrict__ keys, int64_t n,
+                                                            uint32_t* __restrict__ hist) {
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
+    const uint32_t k = keys[i];
+    if (i == 0 || keys[i - 1] != k) atomicSub(&hist[k], (uint32_t)i);
+    if (i == n - 1 || keys[i + 1] != k) atomicAdd(&hist[k], (uint32_t)(i + 1));
+  }
+}
+
+hipError_t launch_radix(gf_ctx* ctx, int stage, const RadixArgs& a, int blocks) {
+  hipStream_t s = ctx->stream;
+  KTimer t(ctx, GF_K_BUCKET);
+  switch (stage) {
+    case 0:  // kin == null: pass 0, keys from x, y stored to kout
+      if (!a.kin) hipLaunchKernelGGL(radix_hist_kernel<true>, dim3(blocks), dim3(kBlock), 0, s, a);
+      else hipLaunchKernelGGL(radix_hist_kernel<false>, dim3(blocks), dim3(kBlock), 0, s, a);
+      break;
+    case 1:
+      hipLaunchKernelGGL(radix_scatter_kernel, dim3(blocks), dim3(kBlock), 0, s, a);
+      break;
+    default:
+      if (a.n > 0)
+        hipLaunchKernelGGL(radix_runs_kernel, dim3(stream_blocks(a.n, kBlock)), dim3(kBlock), 0, s, a.kout, a.n,
+                           a.M);
+      break;
+  }
   return hipGetLastError();
 }
 
-// Global-atomic histogram (bins up to n*n+1 do not fit LDS for the large grids).
+// Global-atomic histogram / scatter (the legacy join path's query side)
 __global__ __launch_bounds__(kBlock) void histogram_kernel(const uint32_t* __restrict__ keys, int64_t n,
                                                            uint32_t* __restrict__ hist) {
   for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock)
@@ -111,21 +229,6 @@ __global__ __launch_bounds__(kBlock) void histogram_kernel(const uint32_t* __res
 hipError_t launch_histogram(hipStream_t s, const uint32_t* keys, int64_t n, uint32_t* hist) {
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(histogram_kernel, dim3(stream_blocks(n, kBlock)), dim3(kBlock), 0, s, keys, n, hist);
-  return hipGetLastError();
-}
-
-__global__ __launch_bounds__(kBlock) void scatter_kernel(const uint32_t* __restrict__ keys, int64_t n,
-                                                         uint32_t* __restrict__ cursor,
-                                                         uint32_t* __restrict__ perm) {
-  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
-    const uint32_t pos = atomicAdd(&cursor[keys[i]], 1u);
-    perm[pos] = (uint32_t)i;
-  }
-}
-
-hipError_t launch_scatter(hipStream_t s, const uint32_t* keys, int64_t n, uint32_t* cursor, uint32_t* perm) {
-  if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(scatter_kernel, dim3(stream_blocks(n, kBlock)), dim3(kBlock), 0, s, keys, n, cursor, perm);
   return hipGetLastError();
 }
 

@@ -72,22 +72,54 @@ def test_cells_odd_sizes(sf, oracle_mod):
 
 
 # ------------------------------------------------------------------ K2 bucketing
-def test_bucket_by_cell(sf, oracle_mod):
-    g = sf.UniformGrid(100, *BEIJING)
-    og = oracle_mod.grid(100, *BEIJING)
-    x, y = oracle_mod.java_random_points(9, 200_001, 115.3, 117.8, 39.5, 41.2)
+def bucket_expected(oracle_mod, og, gn, x, y):
+    """keyBy(gridID) restated: bucket = valid cell cy*n + cx (out-of-grid last), points of a
+    bucket in arrival order (a stable sort of the keys) -- the exact permutation."""
+    cx, cy = oracle_mod.assign_cells(og, x, y)
+    valid = (cx >= 0) & (cy >= 0) & (cx < gn) & (cy < gn)
+    key = np.where(valid, cy.astype(np.int64) * gn + cx, gn * gn)
+    perm = np.argsort(key, kind="stable")
+    start = np.searchsorted(key[perm], np.arange(gn * gn + 2), side="left")
+    return perm, start
+
+
+@pytest.mark.parametrize("gn,n,box,clustered", [
+    (100, 200_001, (115.3, 117.8, 39.5, 41.2), False),     # 14-bit keys: 2 passes, out-of-grid points
+    (1000, 1_500_000, BEIJING, False),                      # 20-bit keys: 2 passes
+    (2048, 700_000, BEIJING, True),                         # 23-bit keys: 3 passes, hot spots
+    (7, 5_000, BEIJING, True),                              # 1 pass
+    (500, 1, BEIJING, False), (500, 63, BEIJING, False), (500, 4097, BEIJING, True),
+])
+def test_bucket_by_cell_exact(sf, oracle_mod, gn, n, box, clustered):
+    g = sf.UniformGrid(gn, *BEIJING)
+    og = oracle_mod.grid(gn, *BEIJING)
+    x, y = oracle_mod.java_random_points(9 + gn, n, *box)
+    if clustered:  # Gaussian hot spots, sigma 0.01 deg: most points in a few cells
+        rng = np.random.default_rng(gn)
+        c = rng.integers(0, 4, n)
+        cxs, cys = np.array([116.0, 116.4, 117.1, 115.9]), np.array([39.9, 40.3, 40.0, 40.8])
+        h = rng.random(n) < 0.8
+        x = np.where(h, cxs[c] + 0.01 * rng.standard_normal(n), x)
+        y = np.where(h, cys[c] + 0.01 * rng.standard_normal(n), y)
     perm, start = sf.bucket_by_cell(win(sf, x, y), g)
     perm = perm.cpu().numpy().view(np.uint32).astype(np.int64)
     start = start.cpu().numpy().view(np.uint32).astype(np.int64)
-    cx, cy = oracle_mod.assign_cells(og, x, y)
-    valid = (cx >= 0) & (cy >= 0) & (cx < 100) & (cy < 100)
-    key = np.where(valid, cy.astype(np.int64) * 100 + cx, 100 * 100)
-    assert np.array_equal(np.sort(perm), np.arange(len(x)))
-    counts = np.bincount(key, minlength=100 * 100 + 1)
-    np.testing.assert_array_equal(np.diff(start), counts)
-    for b in range(0, 100 * 100 + 1, 97):
-        seg = perm[start[b]:start[b + 1]]
-        assert np.all(key[seg] == b)
+    ep, es = bucket_expected(oracle_mod, og, gn, x, y)
+    np.testing.assert_array_equal(perm, ep)
+    np.testing.assert_array_equal(start, es)
+
+
+def test_bucket_by_cell_empty_and_repeatable(sf, oracle_mod):
+    g = sf.UniformGrid(50, *BEIJING)
+    import torch
+    w = sf.PointWindow(torch.empty(0, dtype=torch.float64, device="cuda"), torch.empty(0, dtype=torch.float64, device="cuda"),
+                       torch.empty(0, dtype=torch.int64, device="cuda"), torch.empty(0, dtype=torch.int64, device="cuda"))
+    perm, start = sf.bucket_by_cell(w, g)
+    assert start.cpu().numpy().sum() == 0 and start.numel() == 50 * 50 + 2
+    x, y = oracle_mod.java_random_points(4, 333_333, *BEIJING)
+    a = sf.bucket_by_cell(win(sf, x, y), g)[0].cpu().numpy()
+    b = sf.bucket_by_cell(win(sf, x, y), g)[0].cpu().numpy()
+    np.testing.assert_array_equal(a, b)
 
 
 # ------------------------------------------------------------------ range point-point

@@ -778,9 +778,11 @@ def bench_csv(args):
     parse(j)
     text = texts[j][0]
     ex, ey, eo, et, ebl, ebk = O.csv_parse(text, ",", [0, 1, 2, 3])
+    # objIDs: the keys decode to the oracle's Strings exactly (numeric Strings are their own key)
     verified = bool(ebl == -1 and np.array_equal(x.cpu().numpy().view(np.int64), ex.view(np.int64))
                     and np.array_equal(y.cpu().numpy().view(np.int64), ey.view(np.int64))
-                    and np.array_equal(o.cpu().numpy(), eo) and np.array_equal(ts.cpu().numpy(), et))
+                    and sf.ObjIdDict.default(0).decode_bytes(o.cpu().numpy()) == eo
+                    and np.array_equal(ts.cpu().numpy(), et))
     og = O.grid(100, *BEIJING)
     ecx, ecy = O.assign_cells(og, ex, ey)
     verified &= bool(np.array_equal(cx.cpu().numpy(), ecx) and np.array_equal(cy.cpu().numpy(), ecy))
@@ -879,6 +881,68 @@ def bench_polyknn(args):
            **({"cpu_baseline": cpu} if cpu else {})})
 
 
+def bench_bucket(args):
+    """K2 bucketing by cell (north-star subsystem 2, the keyBy(gridID) shuffle,
+    PointPointRangeQuery.java:144-148): gf_bucket_by_cell over 10M-point windows of the C2 grid
+    (500 x 500).  A step = one window: the stable radix passes + bucket offsets.  Algorithmic
+    bytes: x, y in (16 B/point) + the permutation out (4 B/point) + cell_start (4 B/bucket); the
+    passes move 28 B/point more (keys, indices) -- the roofline counts only the former."""
+    import torch
+
+    import spatialflink_amd as sf
+    from spatialflink_amd import _lib
+
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+
+    n = args.points or 10_000_000
+    grid_n = args.grid
+    L = _lib.lib()
+    grid = sf.UniformGrid(grid_n, *BEIJING)
+    nwin = 4
+    wins = _windows(sf, n, nwin, 91)
+    ctx = _lib.context(0)
+    perm = torch.empty(n, dtype=torch.int32, device="cuda")
+    start = torch.empty(grid_n * grid_n + 2, dtype=torch.int32, device="cuda")
+    pts = [w[2].c_struct() for w in wins]
+
+    def step(i):
+        _lib.check(L.gf_bucket_by_cell(ctx.handle, C.byref(grid.c_grid), C.byref(pts[i % nwin]), perm.data_ptr(),
+                                       start.data_ptr()), ctx.handle, "gf_bucket_by_cell")
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    ctx.set_timing(1 << _lib.K_BUCKET)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(i)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    ms, cnt = ctx.timing(_lib.K_BUCKET)
+    ctx.set_timing(0)
+    verified = None
+    if not args.no_verify:  # the exact permutation (stable: arrival order inside a bucket)
+        step(0)
+        x, y, _ = wins[0]
+        og = O.grid(grid_n, *BEIJING)
+        cx, cy = O.assign_cells(og, x, y)
+        valid = (cx >= 0) & (cy >= 0) & (cx < grid_n) & (cy < grid_n)
+        key = np.where(valid, cy.astype(np.int64) * grid_n + cx, grid_n * grid_n)
+        ep = np.argsort(key, kind="stable")
+        verified = bool(np.array_equal(perm.cpu().numpy().view(np.uint32).astype(np.int64), ep))
+    per_window = elapsed / args.steps
+    bytes_alg = 20.0 * n + 4.0 * (grid_n * grid_n + 2)
+    _line("K2 bucketing by cell", n * args.steps / elapsed, "points/s", args.steps, args.warmup, elapsed,
+          "radix hist + scatter passes (gf_bucket_by_cell)", bytes_alg, per_window,
+          {"config": {"workload": f"bucket_by_cell_{n // 1_000_000}Mpts_grid{grid_n}", "points_per_window": n,
+                      "grid": grid_n},
+           "breakdown": {"kernel_us_per_window": round(1000.0 * ms / max(args.steps, 1), 2),
+                         "launches_per_window": cnt / args.steps,
+                         "achieved_basis": "algorithmic bytes / whole call (all passes + scans)"},
+           "verified_vs_oracle": verified})
+
+
 def run(args):
     if args.workload in ("range", "ppoly"):
         bench_range(args, polygons=args.workload == "ppoly")
@@ -892,5 +956,7 @@ def run(args):
         bench_csv(args)
     elif args.workload == "polyknn":
         bench_polyknn(args)
+    elif args.workload == "bucket":
+        bench_bucket(args)
     else:
         raise SystemExit(f"unknown workload {args.workload}")
