@@ -8,6 +8,7 @@
  * cites the reference file:line it restates.  Build: oracle/Makefile (gcc -O2
  * -ffp-contract=off: Java never fuses a*b+c).
  */
+#define _POSIX_C_SOURCE 200809L
 #include "geoflink_oracle.h"
 
 #include <float.h>
@@ -760,44 +761,38 @@ static void i64_remove(i64set* s, int64_t v) {
   for (int64_t i = 0; i < s->n; i++) if (s->v[i] == v) { s->v[i] = s->v[--s->n]; return; }
 }
 
-/* PointPointKNNQuery.windowBased apply (:159-192) + KNNQuery.kNNWinAllEvaluationPointStream
- * (:213-272).  Cells visited in first-appearance order. */
-int32_t orc_knn_reference(const orc_grid* g, int64_t n, const double* x, const double* y,
-                          const int64_t* objID, double qx, double qy, double r, int32_t k,
-                          int metric, int64_t* out_objID, double* out_d, int64_t* out_idx) {
-  if (k <= 0) return ORC_ERR_ARG; /* new PriorityQueue(k<1) throws */
-  strset cells;
-  ss_init(&cells, n + 16); /* sized so it never rehashes: slot indices stay valid */
-  tup* c;
-  int64_t* slot;
-  int64_t m = knn_candidates(g, n, x, y, objID, qx, qy, r, metric, &c, &slot, &cells);
-  /* group by cell slot, first-appearance order */
-  int64_t* first = (int64_t*)malloc(sizeof(int64_t) * (size_t)cells.cap);
-  int64_t* order = (int64_t*)malloc(sizeof(int64_t) * (size_t)(cells.cap));
-  int64_t ncell = 0;
-  for (int64_t i = 0; i < cells.cap; i++) first[i] = -1;
-  for (int64_t i = 0; i < m; i++)
-    if (first[slot[i]] < 0) { first[slot[i]] = ncell; order[ncell++] = slot[i]; }
+/* Per-cell apply of PointPointKNNQuery.windowBased (:159-192) on one cell's candidates in
+ * arrival order: a bounded max-heap of (Point, d) over d <= r, replaced iff peek.d > d.  The
+ * heap (array order) is written to out[0 .. return). */
+static int32_t knn_cell_apply(const tup* c, int64_t m, int32_t k, tup* out) {
+  jpq pq;
+  jpq_init(&pq, k);
+  for (int64_t i = 0; i < m; i++) {
+    double d = c[i].d; /* NaN marks d > r (distance already tested) */
+    if (pq.size < k) {
+      if (d == d) jpq_offer(&pq, c[i]);
+    } else if (d == d) {
+      double largest = pq.q[0].d;
+      if (largest > d) { jpq_poll(&pq); jpq_offer(&pq, c[i]); }
+    }
+  }
+  int32_t n = pq.size;
+  memcpy(out, pq.q, sizeof(tup) * (size_t)n);
+  jpq_free(&pq);
+  return n;
+}
+
+/* KNNQuery.kNNWinAllEvaluationPointStream (:213-272): merge the per-cell heaps (cells in the
+ * given order) into one k-heap with the objID set, its eviction bug included. */
+static int32_t knn_winall_merge(const tup* heaps, const int64_t* heap_off, int64_t ncell, int32_t k,
+                                int64_t* out_objID, double* out_d, int64_t* out_idx) {
   jpq W;
   i64set objIDs = {0};
   jpq_init(&W, k);
   int status = ORC_OK;
   for (int64_t ci = 0; ci < ncell && status == ORC_OK; ci++) {
-    jpq pq;
-    jpq_init(&pq, k);
-    for (int64_t i = 0; i < m; i++) {
-      if (slot[i] != order[ci]) continue;
-      double d = c[i].d; /* NaN marks d > r (distance already tested) */
-      if (pq.size < k) {
-        if (d == d) jpq_offer(&pq, c[i]);
-      } else if (d == d) {
-        double largest = pq.q[0].d;
-        if (largest > d) { jpq_poll(&pq); jpq_offer(&pq, c[i]); }
-      }
-    }
-    /* merge -- KNNQuery.java:221-268 */
-    for (int32_t t = 0; t < pq.size; t++) {
-      tup cand = pq.q[t];
+    for (int64_t t = heap_off[ci]; t < heap_off[ci + 1]; t++) {
+      tup cand = heaps[t];
       if (W.size < k) {
         if (!i64_contains(&objIDs, cand.obj)) {
           jpq_offer(&W, cand); i64_add(&objIDs, cand.obj);
@@ -824,7 +819,6 @@ int32_t orc_knn_reference(const orc_grid* g, int64_t n, const double* x, const d
         }
       }
     }
-    jpq_free(&pq);
   }
   int32_t nout = W.size;
   if (status == ORC_OK)
@@ -832,9 +826,201 @@ int32_t orc_knn_reference(const orc_grid* g, int64_t n, const double* x, const d
       out_objID[i] = W.q[i].obj; out_d[i] = W.q[i].d; out_idx[i] = W.q[i].idx;
     }
   jpq_free(&W);
-  free(objIDs.v); free(first); free(order); free(c); free(slot);
-  ss_free(&cells);
+  free(objIDs.v);
   return status == ORC_OK ? nout : status;
+}
+
+/* PointPointKNNQuery.windowBased apply (:159-192) + KNNQuery.kNNWinAllEvaluationPointStream
+ * (:213-272).  Cells visited in first-appearance order; each cell's candidates in arrival
+ * order (the keyed window buffer), grouped by a stable counting sort on the cell slot. */
+int32_t orc_knn_reference(const orc_grid* g, int64_t n, const double* x, const double* y,
+                          const int64_t* objID, double qx, double qy, double r, int32_t k,
+                          int metric, int64_t* out_objID, double* out_d, int64_t* out_idx) {
+  if (k <= 0) return ORC_ERR_ARG; /* new PriorityQueue(k<1) throws */
+  strset cells;
+  ss_init(&cells, n + 16); /* sized so it never rehashes: slot indices stay valid */
+  tup* c;
+  int64_t* slot;
+  int64_t m = knn_candidates(g, n, x, y, objID, qx, qy, r, metric, &c, &slot, &cells);
+  /* cell rank in first-appearance order, then a stable counting sort of the candidates */
+  int64_t* rank = (int64_t*)malloc(sizeof(int64_t) * (size_t)cells.cap);
+  int64_t ncell = 0;
+  for (int64_t i = 0; i < cells.cap; i++) rank[i] = -1;
+  for (int64_t i = 0; i < m; i++)
+    if (rank[slot[i]] < 0) rank[slot[i]] = ncell++;
+  int64_t* off = (int64_t*)calloc((size_t)ncell + 1, sizeof(int64_t));
+  for (int64_t i = 0; i < m; i++) off[rank[slot[i]] + 1]++;
+  for (int64_t ci = 0; ci < ncell; ci++) off[ci + 1] += off[ci];
+  tup* grouped = (tup*)malloc(sizeof(tup) * (size_t)(m > 0 ? m : 1));
+  int64_t* cur = (int64_t*)malloc(sizeof(int64_t) * (size_t)(ncell > 0 ? ncell : 1));
+  for (int64_t ci = 0; ci < ncell; ci++) cur[ci] = off[ci];
+  for (int64_t i = 0; i < m; i++) grouped[cur[rank[slot[i]]]++] = c[i];
+  /* per-cell heaps, concatenated in cell order */
+  tup* heaps = (tup*)malloc(sizeof(tup) * (size_t)(m > 0 ? m : 1));
+  int64_t* hoff = (int64_t*)malloc(sizeof(int64_t) * (size_t)(ncell + 1));
+  hoff[0] = 0;
+  for (int64_t ci = 0; ci < ncell; ci++)
+    hoff[ci + 1] = hoff[ci] + knn_cell_apply(grouped + off[ci], off[ci + 1] - off[ci], k, heaps + hoff[ci]);
+  int32_t st = knn_winall_merge(heaps, hoff, ncell, k, out_objID, out_d, out_idx);
+  free(rank); free(off); free(grouped); free(cur); free(heaps); free(hoff); free(c); free(slot);
+  ss_free(&cells);
+  return st;
+}
+
+/* ---- the same operator on T host threads, shaped as Flink runs it with parallelism T
+ * (conf/geoflink-conf.yml:55; keyBy(gridID) over subtasks, PointPointKNNQuery.java:144-158):
+ *   source subtasks   contiguous point ranges: cell-ID string, HashSet C/G filter, JTS distance;
+ *                     each candidate goes to key subtask hash(gridID) % T (the shuffle)
+ *   key subtasks      group their candidates by cell string (arrival order kept: sources are
+ *                     drained in order), per-cell bounded heap (:159-192)
+ *   windowAll         one thread merges every cell's heap (KNNQuery.java:213-272), cells in
+ *                     first-appearance order -- so the result equals orc_knn_reference. */
+#include <pthread.h>
+
+typedef struct { tup t; uint64_t h; int32_t cx, cy; } cand_t;
+typedef struct { cand_t* v; int64_t n, cap; } cvec;
+static void cvec_push(cvec* a, cand_t c) {
+  if (a->n == a->cap) { a->cap = a->cap ? 2 * a->cap : 1024; a->v = (cand_t*)realloc(a->v, sizeof(cand_t) * (size_t)a->cap); }
+  a->v[a->n++] = c;
+}
+typedef struct { int64_t first; int64_t off, cnt; const tup* h; } cellrun;
+typedef struct {
+  int T, tid;
+  const orc_grid* g;
+  int64_t n;
+  const double *x, *y;
+  const int64_t* objID;
+  double qx, qy, r;
+  int32_t k;
+  int metric;
+  const strset *G, *C;
+  cvec* out;            /* [T * T]: out[src * T + dst] */
+  /* key phase results */
+  tup* heaps;
+  cellrun* runs;
+  int64_t nruns;
+  pthread_barrier_t* bar;
+} mt_arg;
+
+static void* knn_mt_worker(void* p) {
+  mt_arg* a = (mt_arg*)p;
+  const int T = a->T, t = a->tid;
+  char id[32];
+  /* source subtask: points [lo, hi) */
+  const int64_t lo = a->n * t / T, hi = a->n * (t + 1) / T;
+  for (int64_t i = lo; i < hi; i++) {
+    int32_t cx, cy;
+    orc_cell_of(a->g, a->x[i], a->y[i], &cx, &cy);
+    orc_cell_id(cx, cy, id);
+    if (!(ss_contains(a->C, id) || ss_contains(a->G, id))) continue;
+    double d = orc_distance(a->qx, a->qy, a->x[i], a->y[i], a->metric);
+    cand_t c;
+    c.t.d = d <= a->r ? d : NAN; c.t.obj = a->objID[i]; c.t.idx = i;
+    c.h = str_hash(id); c.cx = cx; c.cy = cy;
+    cvec_push(&a->out[(int64_t)t * T + (int64_t)(c.h % (uint64_t)T)], c);
+  }
+  pthread_barrier_wait(a->bar);
+  /* key subtask t: its candidates from every source, in source (= arrival) order */
+  int64_t m = 0;
+  for (int s = 0; s < T; s++) m += a->out[(int64_t)s * T + t].n;
+  strset keys;
+  ss_init(&keys, m + 16);
+  int64_t* rank = (int64_t*)malloc(sizeof(int64_t) * (size_t)keys.cap);
+  for (int64_t i = 0; i < keys.cap; i++) rank[i] = -1;
+  int64_t* slot = (int64_t*)malloc(sizeof(int64_t) * (size_t)(m > 0 ? m : 1));
+  cellrun* runs = (cellrun*)malloc(sizeof(cellrun) * (size_t)(m > 0 ? m : 1));
+  int64_t nr = 0, j = 0;
+  for (int s = 0; s < T; s++) {
+    const cvec* v = &a->out[(int64_t)s * T + t];
+    for (int64_t i = 0; i < v->n; i++, j++) {
+      orc_cell_id(v->v[i].cx, v->v[i].cy, id);
+      int64_t sl = ss_add(&keys, id);
+      if (rank[sl] < 0) { rank[sl] = nr; runs[nr].first = v->v[i].t.idx; runs[nr].cnt = 0; nr++; }
+      slot[j] = rank[sl];
+      runs[slot[j]].cnt++;
+    }
+  }
+  int64_t acc = 0;
+  for (int64_t ri = 0; ri < nr; ri++) { runs[ri].off = acc; acc += runs[ri].cnt; runs[ri].cnt = 0; }
+  tup* grouped = (tup*)malloc(sizeof(tup) * (size_t)(m > 0 ? m : 1));
+  j = 0;
+  for (int s = 0; s < T; s++) {
+    const cvec* v = &a->out[(int64_t)s * T + t];
+    for (int64_t i = 0; i < v->n; i++, j++) {
+      cellrun* R = &runs[slot[j]];
+      grouped[R->off + R->cnt++] = v->v[i].t;
+    }
+  }
+  /* per-cell heaps: heap of run ri replaces its candidates at the same offset */
+  a->heaps = (tup*)malloc(sizeof(tup) * (size_t)(m > 0 ? m : 1));
+  for (int64_t ri = 0; ri < nr; ri++) {
+    int32_t h = knn_cell_apply(grouped + runs[ri].off, runs[ri].cnt, a->k, a->heaps + runs[ri].off);
+    runs[ri].cnt = h;
+    runs[ri].h = a->heaps + runs[ri].off;
+  }
+  a->runs = runs;
+  a->nruns = nr;
+  free(grouped); free(slot); free(rank);
+  ss_free(&keys);
+  return NULL;
+}
+
+static int cmp_run_first(const void* p, const void* q) {
+  const cellrun* a = *(const cellrun* const*)p; const cellrun* b = *(const cellrun* const*)q;
+  return a->first < b->first ? -1 : (a->first > b->first);
+}
+
+int32_t orc_knn_reference_mt(const orc_grid* g, int64_t n, const double* x, const double* y,
+                             const int64_t* objID, double qx, double qy, double r, int32_t k,
+                             int metric, int nthreads, int64_t* out_objID, double* out_d, int64_t* out_idx) {
+  if (k <= 0) return ORC_ERR_ARG;
+  const int T = nthreads < 1 ? 1 : nthreads;
+  strset G, C;
+  char id[32];
+  int32_t qcx, qcy;
+  orc_cell_of(g, qx, qy, &qcx, &qcy);
+  orc_cell_id(qcx, qcy, id);
+  ss_init(&G, 64); ss_init(&C, 64);
+  g_cells_of(g, r, id, &G);
+  c_cells_of(g, r, id, &G, &C);
+  cvec* out = (cvec*)calloc((size_t)T * (size_t)T, sizeof(cvec));
+  mt_arg* args = (mt_arg*)calloc((size_t)T, sizeof(mt_arg));
+  pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * (size_t)T);
+  pthread_barrier_t bar;
+  pthread_barrier_init(&bar, NULL, (unsigned)T);
+  for (int t = 0; t < T; t++) {
+    mt_arg* a = &args[t];
+    a->T = T; a->tid = t; a->g = g; a->n = n; a->x = x; a->y = y; a->objID = objID;
+    a->qx = qx; a->qy = qy; a->r = r; a->k = k; a->metric = metric; a->G = &G; a->C = &C;
+    a->out = out; a->bar = &bar;
+    if (t > 0) pthread_create(&th[t], NULL, knn_mt_worker, a);
+  }
+  knn_mt_worker(&args[0]);
+  for (int t = 1; t < T; t++) pthread_join(th[t], NULL);
+  pthread_barrier_destroy(&bar);
+  /* windowAll: every cell's heap, cells in first-appearance order */
+  int64_t ncell = 0, total = 0;
+  for (int t = 0; t < T; t++) ncell += args[t].nruns;
+  cellrun** order = (cellrun**)malloc(sizeof(cellrun*) * (size_t)(ncell > 0 ? ncell : 1));
+  int64_t w = 0;
+  for (int t = 0; t < T; t++)
+    for (int64_t ri = 0; ri < args[t].nruns; ri++) order[w++] = &args[t].runs[ri];
+  qsort(order, (size_t)ncell, sizeof(cellrun*), cmp_run_first);
+  for (int64_t ci = 0; ci < ncell; ci++) total += order[ci]->cnt;
+  tup* heaps = (tup*)malloc(sizeof(tup) * (size_t)(total > 0 ? total : 1));
+  int64_t* hoff = (int64_t*)malloc(sizeof(int64_t) * (size_t)(ncell + 1));
+  hoff[0] = 0;
+  for (int64_t ci = 0; ci < ncell; ci++) {
+    const cellrun* R = order[ci];
+    memcpy(heaps + hoff[ci], R->h, sizeof(tup) * (size_t)R->cnt);
+    hoff[ci + 1] = hoff[ci] + R->cnt;
+  }
+  int32_t st = knn_winall_merge(heaps, hoff, ncell, k, out_objID, out_d, out_idx);
+  for (int t = 0; t < T; t++) { free(args[t].heaps); free(args[t].runs); }
+  for (int64_t i = 0; i < (int64_t)T * T; i++) free(out[i].v);
+  free(out); free(args); free(th); free(order); free(heaps); free(hoff);
+  ss_free(&G); ss_free(&C);
+  return st;
 }
 
 /* ------------------------------------------------------------------------------------ */

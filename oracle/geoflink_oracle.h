@@ -121,6 +121,21 @@ int32_t orc_knn_reference(const orc_grid* g, int64_t n, const double* x, const d
                           const int64_t* objID, double qx, double qy, double r, int32_t k,
                           int metric, int64_t* out_objID, double* out_d, int64_t* out_idx);
 
+/* orc_knn_reference on nthreads host threads, shaped as Flink runs the operator with
+ * parallelism nthreads: source subtasks (contiguous point ranges: cell-ID string, HashSet C/G
+ * filter, JTS distance) -> keyBy(gridID) hash shuffle -> key subtasks (per-cell bounded heaps)
+ * -> one windowAll merge.  Same result as orc_knn_reference (the CPU baseline's all-core line). */
+int32_t orc_knn_reference_mt(const orc_grid* g, int64_t n, const double* x, const double* y,
+                             const int64_t* objID, double qx, double qy, double r, int32_t k,
+                             int metric, int nthreads, int64_t* out_objID, double* out_d, int64_t* out_idx);
+
+/* An optimised C kNN (build contract, = orc_knn_contract): OpenMP over point ranges, integer
+ * Chebyshev cell test, squared-distance prefilter against each thread's running k-th distance,
+ * per-thread bounded top-k-distinct heap, one merge.  The CPU baseline's second line. */
+int32_t orc_knn_scan_omp(const orc_grid* g, int64_t n, const double* x, const double* y,
+                         const int64_t* objID, double qx, double qy, double r, int32_t k,
+                         int metric, int nthreads, int64_t* out_objID, double* out_d, int64_t* out_idx);
+
 /* Window-based point-point join -- JoinQuery.java:73-90 + PointPointJoinQuery.java:124-183.
  * ugrid assigns ordinary points, qgrid assigns and replicates query points.
  * Writes pairs (ordinary idx, query idx) as out_pairs[2*i], out_pairs[2*i+1].

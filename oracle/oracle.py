@@ -67,6 +67,9 @@ def lib():
         for fn in (L.orc_knn_contract, L.orc_knn_reference):
             fn.argtypes = [C.POINTER(OrcGrid), i64, P, P, P, d, d, d, i32, C.c_int, P, P, P]
             fn.restype = i32
+        for fn in (L.orc_knn_reference_mt, L.orc_knn_scan_omp):
+            fn.argtypes = [C.POINTER(OrcGrid), i64, P, P, P, d, d, d, i32, C.c_int, C.c_int, P, P, P]
+            fn.restype = i32
         L.orc_join_pp.argtypes = [C.POINTER(OrcGrid), C.POINTER(OrcGrid), i64, P, P, i64, P, P, d, C.c_int, C.c_int, P, i64]
         L.orc_join_pp.restype = i64
         L.orc_join_ppoly.argtypes = [C.POINTER(OrcGrid), C.POINTER(OrcGrid), i64, P, P, C.POINTER(OrcPolygons), d,
@@ -211,6 +214,36 @@ def knn(g, x, y, objID, qx, qy, r, k, metric=METRIC_SQRT, reference_shaped=False
     if n < 0:
         return n, None, None, None
     return 0, oo[:n], od[:n], oi[:n]
+
+
+def knn_mt(g, x, y, objID, qx, qy, r, k, nthreads, metric=METRIC_SQRT, optimized=False):
+    """CPU baselines on nthreads host threads: the reference-shaped evaluator shaped as Flink's
+    parallel operator (orc_knn_reference_mt, = knn(reference_shaped=True)) or the optimised
+    OpenMP scan (orc_knn_scan_omp, = knn()).  Returns (status, objID, dist, idx)."""
+    x, y = _f64(x), _f64(y)
+    objID = np.ascontiguousarray(objID, dtype=np.int64)
+    kk = max(int(k), 1)
+    oo = np.empty(kk, np.int64); od = np.empty(kk, np.float64); oi = np.empty(kk, np.int64)
+    fn = lib().orc_knn_scan_omp if optimized else lib().orc_knn_reference_mt
+    n = fn(C.byref(g), len(x), _p(x), _p(y), _p(objID), float(qx), float(qy), float(r), int(k), int(metric),
+           int(nthreads), _p(oo), _p(od), _p(oi))
+    if n < 0:
+        return n, None, None, None
+    return 0, oo[:n], od[:n], oi[:n]
+
+
+def host_cpu():
+    """(nproc, lscpu model name) of this host."""
+    model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return os.cpu_count() or 1, model
 
 
 def join_pp(ugrid, qgrid, ox, oy, qx, qy, r, approximate=False, metric=METRIC_SQRT):

@@ -215,3 +215,25 @@ def test_join_ppoly_own_guaranteed_set(oracle_mod):
         got = sorted(map(tuple, oracle_mod.join_ppoly(g, g, x, y, oracle_mod.Polygons(polys), r).tolist()))
         assert got == PR.join_ppoly(pg, pg, x.tolist(), y.tolist(), polys, r)
         assert {q for _, q in got} == {0, 1}
+
+
+@pytest.mark.parametrize("r,k,dup", [(0.5, 50, False), (0.05, 20, True), (0.3, 300, True), (0.5, 1, False),
+                                     (0.002, 50, False)])
+def test_cpu_baselines_match(oracle_mod, r, k, dup):
+    """The bench's multi-core CPU baselines compute the same results as the single-thread
+    oracle: the Flink-shaped parallel evaluator == the reference-shaped one (per-cell heaps +
+    windowAll merge, bug included), the OpenMP scan == the build contract."""
+    og = oracle_mod.grid(500, *BEIJING)
+    x, y = oracle_mod.java_random_points(17, 200_000, 115.4, 117.7, 39.5, 41.2)
+    obj = ((np.arange(len(x)) * 7919) % (60_000 if dup else len(x))).astype(np.int64)
+    ref = oracle_mod.knn(og, x, y, obj, QPOINT[0], QPOINT[1], r, k, reference_shaped=True)
+    con = oracle_mod.knn(og, x, y, obj, QPOINT[0], QPOINT[1], r, k)
+    for T in (1, 3, 8):
+        mt = oracle_mod.knn_mt(og, x, y, obj, QPOINT[0], QPOINT[1], r, k, T)
+        assert mt[0] == ref[0]
+        if ref[0] == 0:
+            for a, b in zip(mt[1:], ref[1:]):
+                np.testing.assert_array_equal(a, b)
+        om = oracle_mod.knn_mt(og, x, y, obj, QPOINT[0], QPOINT[1], r, k, T, optimized=True)
+        for a, b in zip(om, con):
+            np.testing.assert_array_equal(a, b)
