@@ -70,7 +70,9 @@ def cpu_baselines(args, O, og, window, gpu_result, n):
     q = (QPOINT[0], QPOINT[1], args.radius, args.k)
     reps, t, res = _timed_reps(lambda: O.knn_mt(og, x, y, obj, *q, threads), budget)
     go, gd, gi = gpu_result
-    agree = bool(res[0] == 0 and np.array_equal(res[1], go) and np.array_equal(res[2], gd))
+    # the reference's result is its PriorityQueue in heap order: compare as (d, objID)-sorted
+    o_ = np.lexsort((res[1], res[2])) if res[0] == 0 else None
+    agree = bool(res[0] == 0 and np.array_equal(res[1][o_], go) and np.array_equal(res[2][o_], gd))
     S = min(args.cpu_sample, n)
     xs, ys, os_ = (np.ascontiguousarray(a[:S]) for a in (x, y, obj))
     reps1, t1, _ = _timed_reps(lambda: O.knn(og, xs, ys, os_, *q, reference_shaped=True), budget)
@@ -110,6 +112,8 @@ def main():
     ap.add_argument("--range-defer", default="0", help="range/ppoly candidate tests: 0 auto, 1 inline, 2 deferred (list = sweep)")
     ap.add_argument("--range-streams", type=int, default=2,
                     help="range/ppoly: consecutive windows alternate over this many contexts (HIP streams)")
+    ap.add_argument("--no-indices", action="store_true",
+                    help="range/ppoly: leave the index list out of the step (bitmap + counts only; ablation)")
     ap.add_argument("--k", type=int, default=50)
     ap.add_argument("--radius", type=float, default=0.5)
     ap.add_argument("--grid", type=int, default=500)

@@ -175,7 +175,8 @@ void gf_range_plan_destroy(gf_range_plan* plan);
 /* Window apply (PointPointRangeQuery.java:150-186 / PointPolygonRangeQuery.java:170-204), async.
  * bitmap: device uint64[(n+63)/64], bit i = point i emitted.  multi_bitmap (nullable): bit i =
  * point i emitted once per query point (approximate point-point, C cells).  counts: device
- * int64[2] = {points emitted, size of the emitted multiset}. */
+ * int64[2] = {points emitted, size of the emitted multiset}, summed by the last block of the
+ * window's last kernel (no extra launch). */
 int  gf_range_run(gf_range_plan* plan, const gf_points* pts, uint64_t* bitmap,
                   uint64_t* multi_bitmap, int64_t* counts);
 /* Plan diagnostics: in-grid cells by class (none / candidate / guaranteed / candidate cells
@@ -188,6 +189,11 @@ int  gf_range_plan_set_tuning(gf_range_plan* plan, int32_t scan_blocks, int32_t 
 /* Sync: selection bitmap -> ascending point indices (device uint32[cap]). */
 int  gf_bitmap_to_indices(gf_ctx* ctx, const uint64_t* bitmap, int64_t n, uint32_t* idx,
                           int64_t cap, int64_t* count);
+/* Async, one launch: the same indices (those past cap are not written) and their count into
+ * device int64 *count -- enqueue it after gf_range_run so a window's step ends with the index
+ * list the Java collector emits (PointPointRangeQuery.java:150-186) without a host sync. */
+int  gf_bitmap_to_indices_async(gf_ctx* ctx, const uint64_t* bitmap, int64_t n, uint32_t* idx,
+                                int64_t cap, int64_t* count);
 
 /* ---- kNN ---------------------------------------------------------------------------- */
 typedef struct gf_knn_plan gf_knn_plan;

@@ -240,6 +240,8 @@ extern "C" void gf_ctx_destroy(gf_ctx* ctx) {
   hipSetDevice(ctx->device);
   if (ctx->stream) hipStreamSynchronize(ctx->stream);
   if (ctx->dict) gf_objid_dict_destroy(ctx->dict);
+  if (ctx->expand_ticket) hipFree(ctx->expand_ticket);
+  if (ctx->expand_status) hipFree(ctx->expand_status);
   for (auto& e : ctx->pending) { hipEventDestroy(e.a); hipEventDestroy(e.b); }
   for (auto e : ctx->pool) hipEventDestroy(e);
   if (ctx->scratch) hipFree(ctx->scratch);
@@ -686,7 +688,10 @@ constexpr int64_t kSpanLdsBytes = 32768;
 
 // scan blocks (<= 8 per CU) + deferred-test blocks (8 per CU) of per-block partial counts
 int finish_plan(gf_range_plan* P) {
-  GF_HIP_CHECK(P->ctx, hipMalloc(&P->partials, sizeof(uint64_t) * 2 * (size_t)P->ctx->num_cus * 16));
+  // partials of <= kRangeMaxParts blocks (scan <= 8 per CU + deferred tests), then the ticket
+  if (P->ctx->num_cus * 16 > gf::kRangeMaxParts) return set_err(P->ctx, GF_ERR_ARG, "too many CUs for the partials");
+  GF_HIP_CHECK(P->ctx, hipMalloc(&P->partials, sizeof(uint64_t) * (gf::kRangeTicketSlot + 1)));
+  GF_HIP_CHECK(P->ctx, hipMemset(P->partials + gf::kRangeTicketSlot, 0, sizeof(uint64_t)));
   GF_HIP_CHECK(P->ctx, hipMalloc(&P->queue_count, sizeof(uint32_t) * (size_t)P->ctx->num_cus * 8));
   return GF_OK;
 }
@@ -953,9 +958,9 @@ extern "C" int gf_range_run(gf_range_plan* P, const gf_points* pts, uint64_t* bi
     if ((st = ensure_queue(P, a, blocks, false))) return st;
     a.test_blocks = ctx->num_cus * GF_TEST_BPC;
   }
+  // the counts are summed by the last block of the window's last kernel (no finalize launch)
+  a.counts = counts;
   GF_HIP_CHECK(ctx, launch_range(ctx, a, P->table_mode, P->poly, blocks));
-  if (counts)
-    GF_HIP_CHECK(ctx, launch_range_finalize(ctx->stream, P->partials, blocks + (defer ? a.test_blocks : 0), counts));
   return GF_OK;
 }
 
@@ -1044,6 +1049,35 @@ extern "C" int gf_bitmap_to_indices(gf_ctx* ctx, const uint64_t* bitmap, int64_t
     GF_HIP_CHECK(ctx, launch_expand_bitmap(ctx->stream, bitmap, words, n, off, idx, cap));
     GF_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
   }
+  return GF_OK;
+}
+
+extern "C" int gf_bitmap_to_indices_async(gf_ctx* ctx, const uint64_t* bitmap, int64_t n, uint32_t* idx, int64_t cap,
+                                          int64_t* count) {
+  if (!ctx || !bitmap || n < 0 || n > (int64_t)UINT32_MAX || !count || cap < 0 || (cap > 0 && !idx))
+    return set_err(ctx, GF_ERR_ARG, "gf_bitmap_to_indices_async: bad argument");
+  int st = bind(ctx);
+  if (st) return st;
+  const int64_t words = (n + 63) / 64, blocks = (words + kBlock - 1) / kBlock;
+  if (!ctx->expand_ticket) {
+    GF_HIP_CHECK(ctx, hipMalloc(&ctx->expand_ticket, sizeof(unsigned long long)));
+    GF_HIP_CHECK(ctx, hipMemset(ctx->expand_ticket, 0, sizeof(unsigned long long)));
+  }
+  if (ctx->expand_status_cap < blocks) {  // epoch 0 is never used, so zeroed words read "not ready"
+    GF_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+    if (ctx->expand_status) GF_HIP_CHECK(ctx, hipFree(ctx->expand_status));
+    ctx->expand_status = nullptr;
+    const int64_t cap_b = std::max<int64_t>(blocks, 1024);
+    GF_HIP_CHECK(ctx, hipMalloc(&ctx->expand_status, sizeof(unsigned long long) * (size_t)cap_b));
+    GF_HIP_CHECK(ctx, hipMemset(ctx->expand_status, 0, sizeof(unsigned long long) * (size_t)cap_b));
+    ctx->expand_status_cap = cap_b;
+  }
+  ExpandState es{ctx->expand_ticket, ctx->expand_base, ctx->expand_status, 0};
+  ctx->expand_epoch = (ctx->expand_epoch + 1) & 0x3FFFFFFu;
+  if (ctx->expand_epoch == 0) ctx->expand_epoch = 1;
+  es.epoch = ctx->expand_epoch;
+  GF_HIP_CHECK(ctx, launch_expand_bitmap_async(ctx->stream, bitmap, words, n, idx, cap, count, es));
+  ctx->expand_base += (unsigned long long)(words > 0 ? blocks : 0);
   return GF_OK;
 }
 

@@ -36,6 +36,12 @@ struct gf_ctx {
   double join_ppp = 0.0;  // pairs per ordinary point of the last join (sizes the task regions)
   hipStream_t aux = nullptr;  // kNN depth 3: odd windows' launches (created on first use)
   gf_objid_dict* dict = nullptr;  // the context's default objID dictionary (created on first use)
+  // gf_bitmap_to_indices_async: block tickets + look-back status (grown on demand)
+  unsigned long long* expand_ticket = nullptr;
+  unsigned long long expand_base = 0;
+  unsigned long long* expand_status = nullptr;
+  int64_t expand_status_cap = 0;
+  uint32_t expand_epoch = 0;
 };
 
 // objID dictionary (objid.cpp): device hash table + arena, batch buffers, host mirror for decode
@@ -195,6 +201,10 @@ struct KnnSelectArgs {
   void* result;         // gf_knn_header + dist[k] + objID[k] + idx[k]
 };
 
+// partials: [kRangeMaxParts] (hits, multiset size) pairs, then the finalisation ticket
+constexpr int kRangeMaxParts = 4096;
+constexpr int kRangeTicketSlot = 2 * kRangeMaxParts;
+
 // range: classification + tester
 struct RangeArgs {
   const double* x;
@@ -203,6 +213,12 @@ struct RangeArgs {
   uint64_t* bitmap;
   uint64_t* multi;           // nullable
   uint64_t* partials;        // [gridDim.x * 2]: hits, multiset size per block
+  // nullable: the window's counts, summed by the last block of its last kernel.  Its ticket
+  // sits right after the partials (kRangeTicketSlot) and the partial count follows from the
+  // grid, so only this pointer is added to the arguments: every extra argument the scan keeps
+  // live through its loop costs SGPRs (spilled into VGPR lanes, the 10M-point scan ran 2x slower
+  // with the ticket and part count as arguments too)
+  int64_t* counts;
   int32_t nq;                // multiplicity for approximate point-point
   // arithmetic classification (single query point)
   QueryRect qr;
@@ -278,6 +294,15 @@ hipError_t launch_exclusive_scan(hipStream_t s, const uint32_t* in, int64_t L, u
 hipError_t launch_word_popcounts(hipStream_t s, const uint64_t* bitmap, int64_t words, uint32_t* pc);
 hipError_t launch_expand_bitmap(hipStream_t s, const uint64_t* bitmap, int64_t words, int64_t n,
                                 const uint32_t* off, uint32_t* idx, int64_t cap);
+// single-pass compaction state (per context): block tickets and look-back status words
+struct ExpandState {
+  unsigned long long* ticket;  // grows across launches; this launch's blocks take [base, base + blocks)
+  unsigned long long base;
+  unsigned long long* status;  // [blocks] epoch-tagged aggregate / inclusive prefix
+  uint32_t epoch;
+};
+hipError_t launch_expand_bitmap_async(hipStream_t s, const uint64_t* bitmap, int64_t words, int64_t n, uint32_t* idx,
+                                      int64_t cap, int64_t* count, const ExpandState& st);
 
 // objID dictionary (k_objid.hip, objid.cpp)
 constexpr int kDictLenBits = 20;  // slot meta = arena offset << 20 | String length
@@ -391,7 +416,6 @@ int knn_enqueue_merge(gf_knn_plan* P, const gf_points* pts, void* result, const 
 hipError_t launch_range(gf_ctx* ctx, const RangeArgs& a, int table_mode, int poly, int blocks);
 hipError_t launch_join_ppoly(gf_ctx* ctx, const RangeArgs& a, int blocks, int jblocks, uint32_t* ecnt, uint32_t* ecand,
                              uint32_t* btot, unsigned long long* total, uint32_t* pairs, int64_t cap, int aligned);
-hipError_t launch_range_finalize(hipStream_t s, const uint64_t* partials, int blocks, int64_t* counts);
 
 struct JoinArgs {
   const double* ox;

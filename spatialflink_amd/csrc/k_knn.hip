@@ -76,16 +76,17 @@ __device__ void sample_finish(KnnState* st, uint32_t* lh, int32_t k, double r, i
   __syncthreads();
   for (int j = threadIdx.x; j < kDistBins; j += kBlock)
     if (lh[j]) atomicAdd(&st->hist[j], lh[j]);
-  // last-arriving block picks the threshold (split-K style ticket, agent-scope fences)
+  // last-arriving block picks the threshold (ticket).  No fences (Guideline 16, R1): the
+  // histogram adds are agent-scope atomics (performed at the memory side), every wave drains
+  // them before the barrier, the last block reads the bins with agent-scope (sc1) loads.
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
-    __threadfence();
     const uint32_t t = atomicAdd(&st->ticket, 1u);
     s_last = (t == gridDim.x - 1);
   }
   __syncthreads();
   if (!s_last) return;
-  __threadfence();
   constexpr int kPer = kDistBins / kBlock;  // 16 bins per thread
   uint32_t v[kPer];
   uint32_t s = 0;
@@ -124,7 +125,7 @@ __device__ void sample_finish(KnnState* st, uint32_t* lh, int32_t k, double r, i
     }
     st->T = T;
     st->s_pre = s_prefilter(T, metric);
-    st->ticket = 0;
+    __hip_atomic_store(&st->ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   for (int j = threadIdx.x; j < kDistBins; j += kBlock) st->hist[j] = 0u;
 }

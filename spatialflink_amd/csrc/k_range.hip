@@ -310,6 +310,46 @@ __device__ __forceinline__ void range_stage(const RangeArgs& a, const RangeLds& 
   }
 }
 
+// The window's counts without a finalize launch: the last block of the window's last kernel to
+// finish (atomic ticket) sums the partials of every block and resets the ticket for the next
+// window.  Hand-off without fences (cdna_hip_programming.md Guideline 16, R1): each partial is
+// stored write-through (agent-scope atomic store = sc1) and drained (s_waitcnt vmcnt(0)) by the
+// storing lane before its ticket add; the last block reads them with agent-scope (sc1) loads.
+// (__threadfence() here is an L2 write-back per block: it doubled the 10M-point scan.)
+__device__ __forceinline__ void store_partial(uint64_t* p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void finalize_counts(const RangeArgs& a, int nparts, uint32_t* flag, uint64_t* wsum) {
+  uint32_t* ticket = reinterpret_cast<uint32_t*>(a.partials + kRangeTicketSlot);
+  if (threadIdx.x == 0) {  // the lane that stored this block's partials
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    *flag = atomicAdd(ticket, 1u) == gridDim.x - 1 ? 1u : 0u;
+  }
+  __syncthreads();
+  if (!*flag) return;
+  uint64_t h = 0, m = 0;
+  for (int b = threadIdx.x; b < nparts; b += kBlock) {
+    h += __hip_atomic_load(&a.partials[2 * b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    m += __hip_atomic_load(&a.partials[2 * b + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    h += __shfl_xor(h, o, 64);
+    m += __shfl_xor(m, o, 64);
+  }
+  const int w = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) { wsum[2 * w] = h; wsum[2 * w + 1] = m; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t th = 0, tm = 0;
+    for (int v = 0; v < kBlock / 64; ++v) { th += wsum[2 * v]; tm += wsum[2 * v + 1]; }
+    a.counts[0] = (int64_t)th;
+    a.counts[1] = (int64_t)tm;
+    __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 // dynamic-LDS header of range_kernel: lcount, pad, sh[kBlock/64], sm[kBlock/64] (16 B multiple)
 constexpr int kRangeHdrWords = 4 + 2 * 2 * (kBlock / 64);
 #ifndef GF_RANGE_WAVES
@@ -380,10 +420,13 @@ __global__ __launch_bounds__(kBlock, GF_RANGE_WAVES) void range_kernel(RangeArgs
   if (threadIdx.x == 0) {
     uint64_t th = 0, tm = 0;
     for (int w = 0; w < kBlock / 64; ++w) { th += sh[w]; tm += sm[w]; }
-    a.partials[2 * blockIdx.x] = th;
-    a.partials[2 * blockIdx.x + 1] = th + tm * (uint64_t)(a.nq > 1 ? a.nq - 1 : 0);
+    store_partial(&a.partials[2 * blockIdx.x], th);
+    store_partial(&a.partials[2 * blockIdx.x + 1], th + tm * (uint64_t)(a.nq > 1 ? a.nq - 1 : 0));
     if (DEFER) a.queue_count[blockIdx.x] = lcount;
   }
+  // no deferred tests follow: this kernel's last block sums the window's counts (sh / sm are
+  // free again after the partials, lds_base[1] is header padding)
+  if (!DEFER && a.counts) finalize_counts(a, gridDim.x, &lds_base[1], sh);
 }
 
 // One candidate object of a queued point: within r?  (envelope-pruned for exact polygons)
@@ -409,6 +452,7 @@ constexpr int kTestGroup = 8;
 constexpr int kMaxSegs = 2048;  // scan blocks <= 8 per CU
 template <int POLY>
 __global__ __launch_bounds__(kBlock) void range_test_kernel(RangeArgs a, int part_base) {
+  __shared__ uint64_t wsum_fin[2 * (kBlock / 64)];
   __shared__ uint32_t pre[kMaxSegs + 1];
   __shared__ uint32_t wsum[kBlock / 64];
   const int lane = threadIdx.x & 63, g = lane & (kTestGroup - 1);
@@ -487,9 +531,11 @@ __global__ __launch_bounds__(kBlock) void range_test_kernel(RangeArgs a, int par
     __syncthreads();
   }
   if (threadIdx.x == 0) {
-    a.partials[2 * (part_base + blockIdx.x)] = sh[0];
-    a.partials[2 * (part_base + blockIdx.x) + 1] = sh[0];
+    store_partial(&a.partials[2 * (part_base + blockIdx.x)], sh[0]);
+    store_partial(&a.partials[2 * (part_base + blockIdx.x) + 1], sh[0]);
   }
+  __shared__ uint32_t s_flag;
+  if (a.counts) finalize_counts(a, part_base + gridDim.x, &s_flag, reinterpret_cast<uint64_t*>(wsum_fin));
 }
 
 #ifndef GF_RANGE_U
@@ -777,27 +823,6 @@ hipError_t launch_range(gf_ctx* ctx, const RangeArgs& a, int table_mode, int pol
   KTimer t(ctx, GF_K_RANGE_TEST);
   if (poly) hipLaunchKernelGGL(range_test_kernel<1>, dim3(a.test_blocks), b, 0, ctx->stream, a, blocks);
   else hipLaunchKernelGGL(range_test_kernel<0>, dim3(a.test_blocks), b, 0, ctx->stream, a, blocks);
-  return hipGetLastError();
-}
-
-__global__ __launch_bounds__(kBlock) void range_finalize_kernel(const uint64_t* __restrict__ partials, int blocks,
-                                                                int64_t* counts) {
-  uint64_t h = 0, m = 0;
-  for (int b = threadIdx.x; b < blocks; b += kBlock) { h += partials[2 * b]; m += partials[2 * b + 1]; }
-  __shared__ uint64_t sh[kBlock], sm[kBlock];
-  sh[threadIdx.x] = h; sm[threadIdx.x] = m;
-  __syncthreads();
-  for (int s = kBlock / 2; s > 0; s >>= 1) {
-    if (threadIdx.x < s) { sh[threadIdx.x] += sh[threadIdx.x + s]; sm[threadIdx.x] += sm[threadIdx.x + s]; }
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) {
-    if (counts) { counts[0] = (int64_t)sh[0]; counts[1] = (int64_t)sm[0]; }
-  }
-}
-
-hipError_t launch_range_finalize(hipStream_t s, const uint64_t* partials, int blocks, int64_t* counts) {
-  hipLaunchKernelGGL(range_finalize_kernel, dim3(1), dim3(kBlock), 0, s, partials, blocks, counts);
   return hipGetLastError();
 }
 

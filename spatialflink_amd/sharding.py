@@ -32,6 +32,48 @@ def column_bands(n_cols: int, world: int, col_counts=None):
     return [(edges[r], edges[r + 1]) for r in range(world)]
 
 
+def work_bands(n_cols: int, world: int, col_points, col_candidates=None, candidate_cost: float = 0.0):
+    """Bands balanced by WORK, not points: every point costs its 16-B scan, a point the plan
+    queues for the exact test (a candidate-cell point of a polygon set, C3) costs
+    `candidate_cost` scans more.  Without candidates this is column_bands(col_points)."""
+    w = np.asarray(col_points, np.float64)
+    if col_candidates is not None:
+        w = w + candidate_cost * np.asarray(col_candidates, np.float64)
+    return column_bands(n_cols, world, w)
+
+
+def candidate_columns(grid, cx, cy, bboxes, r):
+    """Per-column count of the points that lie in a cell touched by some query object's bbox
+    expanded by r (the cells a range / join plan tests exactly) -- the candidate term of
+    work_bands.  bboxes: [m, 4] (x1, y1, x2, y2)."""
+    n = grid.getNumGridPartitions()
+    cl = grid.getCellLength()
+    hit = np.zeros((n, n), dtype=bool)
+    for x1, y1, x2, y2 in np.asarray(bboxes, np.float64):
+        a0 = max(int(np.floor((x1 - r - grid.getMinX()) / cl)), 0)
+        a1 = min(int(np.floor((x2 + r - grid.getMinX()) / cl)), n - 1)
+        b0 = max(int(np.floor((y1 - r - grid.getMinY()) / cl)), 0)
+        b1 = min(int(np.floor((y2 + r - grid.getMinY()) / cl)), n - 1)
+        if a0 <= a1 and b0 <= b1:
+            hit[b0:b1 + 1, a0:a1 + 1] = True
+    cx = np.asarray(cx, np.int64)
+    cy = np.asarray(cy, np.int64)
+    ok = (cx >= 0) & (cy >= 0) & (cx < n) & (cy < n)
+    cand = np.zeros(len(cx), dtype=bool)
+    cand[ok] = hit[cy[ok], cx[ok]]
+    return np.bincount(cx[cand], minlength=n)[:n]
+
+
+def shard_order(cx, bands):
+    """A window's points grouped by owning rank, arrival order kept inside a shard:
+    (perm, offsets) with shard s = perm[offsets[s]:offsets[s+1]] (global point indices) -- a
+    rank's window is that slice, and its kNN index base is offsets[s] in the permuted order."""
+    owner = shard_of_columns(np.asarray(cx, np.int64), bands)
+    perm = np.argsort(owner, kind="stable")
+    offsets = np.searchsorted(owner[perm], np.arange(len(bands) + 1), side="left")
+    return perm, offsets
+
+
 def band_x_range(grid, lo: int, hi: int):
     """Coordinate range covering cell columns [lo, hi) (for generating a rank's shard)."""
     return grid.getMinX() + lo * grid.getCellLength(), grid.getMinX() + hi * grid.getCellLength()
@@ -103,13 +145,10 @@ def allgather_knn_records(record, k: int, merged_out, group=None):
     return merged_out
 
 
-def allgather_knn_records_batch(records, k: int, results, group=None):
-    """One RCCL all-gather for several windows: `records` is this rank's [nwin, rb] uint8
-    device tensor (consecutive windows); every rank merges all windows in one launch
-    (gf_knn_merge_dev_batch, shard-major) into `results` -- nwin consecutive records (device
-    tensor or an int address from PinnedRecords.ptr()).  Stream-ordered, no host sync.
-    Batching amortises the collective's latency over nwin windows (xGMI is point to point:
-    small messages are latency-, not bandwidth-bound)."""
+def gather_records_batch(records, group=None):
+    """The collective of allgather_knn_records_batch: this rank's [nwin, rb] uint8 records ->
+    the world's, shard-major ([world * nwin * rb]: rank s's window w at (s * nwin + w) * rb) --
+    the layout gf_knn_merge_dev_batch(GF_MERGE_SHARD_MAJOR) reads.  CPU tensors over gloo too."""
     import torch
     import torch.distributed as dist_
 
@@ -117,6 +156,31 @@ def allgather_knn_records_batch(records, k: int, results, group=None):
     nwin, rb = records.shape
     gathered = torch.empty(world * nwin * rb, dtype=torch.uint8, device=records.device)
     _all_gather_bytes(gathered, records.reshape(-1), group)
+    return gathered
+
+
+def encode_knn_record(k: int, objID, dist, idx, status: int = 0, candidates: int = 0, threshold: float = 0.0):
+    """Host bytes of a kNN result record (gf_knn_header + dist[k] + objID[k] + idx[k]) -- the
+    inverse of spatialOperators.decode_knn_record (for host-side shards and tests)."""
+    n = len(objID)
+    h = _lib.GfKnnHeader(int(status), n, int(k), 0, int(candidates), float(threshold))
+    d = np.zeros(k, np.float64); o = np.zeros(k, np.int64); i = np.zeros(k, np.int64)
+    d[:n] = dist; o[:n] = objID; i[:n] = idx
+    return bytes(h) + d.tobytes() + o.tobytes() + i.tobytes()
+
+
+def allgather_knn_records_batch(records, k: int, results, group=None):
+    """One RCCL all-gather for several windows: `records` is this rank's [nwin, rb] uint8
+    device tensor (consecutive windows); every rank merges all windows in one launch
+    (gf_knn_merge_dev_batch, shard-major) into `results` -- nwin consecutive records (device
+    tensor or an int address from PinnedRecords.ptr()).  Stream-ordered, no host sync.
+    Batching amortises the collective's latency over nwin windows (xGMI is point to point:
+    small messages are latency-, not bandwidth-bound)."""
+    import torch.distributed as dist_
+
+    world = dist_.get_world_size(group)
+    nwin = records.shape[0]
+    gathered = gather_records_batch(records, group)
     ctx = _lib.context(records.device.index)
     out = results if isinstance(results, int) else results.data_ptr()
     _lib.check(_lib.lib().gf_knn_merge_dev_batch(ctx.handle, int(k), gathered.data_ptr(), world, int(nwin),

@@ -877,3 +877,50 @@ def test_range_windows_in_flight_on_two_contexts(sf, oracle_mod):
     finally:
         for h in plans:
             L.gf_range_plan_destroy(h)
+
+
+@pytest.mark.parametrize("n", [1, 63, 64, 65, 1_000_000, 10_000_001])
+def test_bitmap_to_indices_async(sf, n):
+    """One-launch async expansion == the synchronous one (ascending indices, count on the
+    device, indices past cap not written), on random bitmaps of every density."""
+    import ctypes as C
+
+    import torch
+    from spatialflink_amd import _lib
+
+    ctx = _lib.context(0)
+    L = _lib.lib()
+    rng = np.random.default_rng(n)
+    words = (n + 63) // 64
+    for dens in (0.0, 0.01, 0.5, 1.0):
+        bits = rng.random(words * 64) < dens
+        bits[n:] = False
+        bm = torch.from_numpy(np.packbits(bits.reshape(-1, 8)[:, ::-1]).view(np.int64).copy()).cuda()
+        exp = np.flatnonzero(bits)
+        for cap in (len(exp), max(len(exp) // 2, 0)):
+            idx = torch.full((max(cap, 1),), -1, dtype=torch.int32, device="cuda")
+            cnt = torch.full((1,), -7, dtype=torch.int64, device="cuda")
+            _lib.check(L.gf_bitmap_to_indices_async(ctx.handle, bm.data_ptr(), n, idx.data_ptr(), cap, cnt.data_ptr()),
+                       ctx.handle, "async")
+            assert int(cnt.item()) == len(exp)
+            got = idx.cpu().numpy().view(np.uint32).astype(np.int64)[:cap]
+            np.testing.assert_array_equal(got, exp[:cap])
+
+
+def test_range_counts_folded_in_kernel(sf, oracle_mod):
+    """The window's counts come from the last block of the window's last kernel (ticket):
+    consecutive windows on one plan, inline and deferred candidate tests, every count right."""
+    g = sf.UniformGrid(500, *BEIJING)
+    og = oracle_mod.grid(500, *BEIJING)
+    raw = oracle_mod.generate_query_polygons(200, BEIJING[0], BEIJING[2], BEIJING[1], BEIJING[3])
+    polys = [sf.Polygon(rings, g) for rings in raw]
+    op = sf.PointPolygonRangeQuery(conf(sf), g)
+    qop = sf.PointPointRangeQuery(conf(sf), g)
+    q = sf.Point("q", *QPOINT, 0, g)
+    for j in range(5):
+        x, y = oracle_mod.java_random_points(500 + j, 400_000 + 77 * j, *BEIJING)
+        w = win(sf, x, y)
+        res = op.run(w, polys, 0.002)
+        assert res.count() == len(oracle_mod.range_ppoly(og, x, y, oracle_mod.Polygons(raw), 0.002))
+        res = qop.run(w, [q], 0.3)
+        assert res.count() == len(oracle_mod.range_pp(og, x, y, [QPOINT[0]], [QPOINT[1]], 0.3))

@@ -1,0 +1,162 @@
+"""GPU: the multi-GPU decomposition through the PRODUCT kernels, on one device.  A window is
+cut into 8 cell-column shards (sharding.column_bands / work_bands, as 8 ranks would hold it);
+every shard runs the real plans -- kNN records with their index base, range / point-polygon
+range bitmaps, joins with the c-column query halo -- and the shard results are combined the
+way the N > 1 path does it: kNN records in the shard-major layout of an all-gather, merged by
+gf_knn_merge_dev_batch; range hits / join pairs concatenated (no collective).  Every combined
+result is compared with the oracle on the whole window (C3 / C4 / C5 shapes at test size).
+Anchors: PointPointKNNQuery.java:198-200 (windowAll funnel), JoinQuery.java:80-87 (query
+replication), PointPointRangeQuery.java:144-148 (keyBy(gridID) over subtasks)."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from conftest import BEIJING, QPOINT
+
+pytestmark = pytest.mark.gpu
+SHARDS = 8
+
+
+@pytest.fixture(scope="module")
+def sf(gpu):
+    import spatialflink_amd
+
+    return spatialflink_amd
+
+
+def conf(sf):
+    return sf.QueryConfiguration(sf.QueryType.WindowBased)
+
+
+def shards_of(sf, oracle_mod, grid_n, x, y, weights=None):
+    og = oracle_mod.grid(grid_n, *BEIJING)
+    cx, cy = oracle_mod.assign_cells(og, x, y)
+    from spatialflink_amd import sharding
+
+    counts = np.bincount(np.clip(cx, 0, grid_n - 1), minlength=grid_n)
+    bands = sharding.column_bands(grid_n, SHARDS, counts if weights is None else weights)
+    perm, off = sharding.shard_order(cx, bands)
+    return og, cx, cy, bands, perm, off
+
+
+@pytest.mark.parametrize("grid_n,n,k,r,nwin,depth", [
+    (1000, 1_600_000, 100, 0.5, 3, 1),      # C5 shape (k = 100, 1000 x 1000), 3 windows per exchange
+    (500, 9_000_000, 50, 0.5, 1, 2),        # C2 shape, plans at pipeline depth 2 (>= 1M points per shard)
+    (500, 600_000, 20, 0.05, 2, 1),         # small radius: most shards hold no candidate
+])
+def test_knn_shards_merged_on_device(sf, oracle_mod, grid_n, n, k, r, nwin, depth):
+    import torch
+    from spatialflink_amd import _lib
+
+    L = _lib.lib()
+    g = sf.UniformGrid(grid_n, *BEIJING)
+    q = sf.Point("q", *QPOINT, 0, g)
+    rb = sf.spatialOperators.knn_record_bytes(k)
+    recs = torch.zeros(SHARDS, nwin, rb, dtype=torch.uint8, device="cuda")  # rank-major = all-gather layout
+    wins = []
+    for w in range(nwin):
+        x, y = oracle_mod.java_random_points(300 + w, n, 115.45, 117.65, 39.55, 41.15)
+        obj = np.random.default_rng(w).permutation(n).astype(np.int64) % (n // 2)  # repeated objIDs
+        og, cx, cy, bands, perm, off = shards_of(sf, oracle_mod, grid_n, x, y)
+        wins.append((x, y, obj, og, perm))
+        for s in range(SHARDS):
+            ix = perm[off[s]:off[s + 1]]
+            op = sf.PointPointKNNQuery(conf(sf), g)  # one plan per "rank"
+            ctx, plan = op.plan(0, q, r, k)
+            _lib.check(L.gf_knn_plan_set_index_base(plan, int(off[s])), ctx.handle, "index base")
+            _lib.check(L.gf_knn_plan_set_pipeline(plan, depth), ctx.handle, "pipeline")
+            pw = sf.PointWindow.from_numpy(x[ix], y[ix], obj[ix])
+            op.enqueue(pw, q, r, k, recs[s, w])
+            op.flush(0, q, r, k)
+            torch.cuda.synchronize()
+            del op
+    out = torch.zeros(nwin, rb, dtype=torch.uint8, device="cuda")
+    ctx = _lib.context(0)
+    _lib.check(L.gf_knn_merge_dev_batch(ctx.handle, k, recs.data_ptr(), SHARDS, nwin, _lib.GF_MERGE_SHARD_MAJOR,
+                                        out.data_ptr()), ctx.handle, "gf_knn_merge_dev_batch")
+    host = out.cpu().numpy()
+    for w, (x, y, obj, og, perm) in enumerate(wins):
+        st, o, d, i = sf.spatialOperators.decode_knn_record(host[w].tobytes(), k)
+        assert st == 0
+        est, eo, ed, ei = oracle_mod.knn(og, x, y, obj, QPOINT[0], QPOINT[1], r, k)
+        np.testing.assert_array_equal(o, eo)
+        np.testing.assert_array_equal(d, ed)
+        np.testing.assert_array_equal(perm[i], ei)  # index base = the shard's offset in the permuted window
+
+
+def test_range_pp_shards_concatenated(sf, oracle_mod):
+    """C1 shape: 100 x 100 grid, per-shard plans, hits concatenated == the whole window."""
+    g = sf.UniformGrid(100, *BEIJING)
+    x, y = oracle_mod.java_random_points(71, 1_000_000, 115.4, 117.7, 39.5, 41.2)
+    og, cx, cy, bands, perm, off = shards_of(sf, oracle_mod, 100, x, y)
+    q = sf.Point("q", *QPOINT, 0, g)
+    for r in (0.5, 0.05):
+        got = []
+        for s in range(SHARDS):
+            ix = perm[off[s]:off[s + 1]]
+            res = sf.PointPointRangeQuery(conf(sf), g).run(sf.PointWindow.from_numpy(x[ix], y[ix]), [q], r)
+            got.append(ix[res.indices().astype(np.int64)])
+        got = np.sort(np.concatenate(got))
+        np.testing.assert_array_equal(got, oracle_mod.range_pp(og, x, y, [QPOINT[0]], [QPOINT[1]], r))
+
+
+def test_ppoly_shards_balanced_by_work(sf, oracle_mod):
+    """C3 shape: the 1000 generateQueryPolygons squares, 500 x 500 grid; bands balanced by
+    candidate work (work_bands: the squares sit in the first ~37 columns, so the first band is
+    narrow); per-shard hits concatenated == the whole window."""
+    from spatialflink_amd import sharding
+
+    g = sf.UniformGrid(500, *BEIJING)
+    og = oracle_mod.grid(500, *BEIJING)
+    raw = oracle_mod.generate_query_polygons(1000, BEIJING[0], BEIJING[2], BEIJING[1], BEIJING[3])
+    polys = [sf.Polygon(rings, g) for rings in raw]
+    x, y = oracle_mod.java_random_points(72, 1_500_000, *BEIJING)
+    cx, cy = oracle_mod.assign_cells(og, x, y)
+    r = 0.001
+    bb = [(p.boundingBox[0][0], p.boundingBox[0][1], p.boundingBox[1][0], p.boundingBox[1][1]) for p in polys]
+    cand = sharding.candidate_columns(g, cx, cy, bb, r)
+    pts = np.bincount(np.clip(cx, 0, 499), minlength=500)
+    bands = sharding.work_bands(500, SHARDS, pts, cand, candidate_cost=8.0)
+    work = pts + 8.0 * cand
+    per = [work[a:b].sum() for a, b in bands]
+    assert max(per) <= 1.25 * (work.sum() / SHARDS)     # balanced by work
+    assert bands[0][1] - bands[0][0] < 500 // SHARDS      # the polygon band is narrower
+    perm, off = sharding.shard_order(cx, bands)
+    got = []
+    for s in range(SHARDS):
+        ix = perm[off[s]:off[s + 1]]
+        res = sf.PointPolygonRangeQuery(conf(sf), g).run(sf.PointWindow.from_numpy(x[ix], y[ix]), polys, r)
+        got.append(ix[res.indices().astype(np.int64)])
+    got = np.sort(np.concatenate(got))
+    np.testing.assert_array_equal(got, oracle_mod.range_ppoly(og, x, y, oracle_mod.Polygons(raw), r))
+
+
+@pytest.mark.parametrize("r", [0.001, 0.004])
+def test_join_shards_with_query_halo(sf, oracle_mod, r):
+    """C4 shape: 1000 x 1000 grid, ordinary side sharded by columns, query side replicated with
+    a c-column halo: every pair is produced once, by its ordinary point's shard."""
+    from spatialflink_amd import sharding
+
+    g = sf.UniformGrid(1000, *BEIJING)
+    og = oracle_mod.grid(1000, *BEIJING)
+    x, y = oracle_mod.java_random_points(81, 1_000_000, *BEIJING)
+    qx, qy = oracle_mod.java_random_points(82, 100_000, *BEIJING)
+    cx, _ = oracle_mod.assign_cells(og, x, y)
+    qcx, _ = oracle_mod.assign_cells(og, qx, qy)
+    c = oracle_mod.layers(og, r)[1]
+    bands = sharding.column_bands(1000, SHARDS, np.bincount(np.clip(cx, 0, 999), minlength=1000))
+    perm, off = sharding.shard_order(cx, bands)
+    got = []
+    for s in range(SHARDS):
+        ix = perm[off[s]:off[s + 1]]
+        qi = np.flatnonzero(sharding.join_query_halo(qcx, bands[s], c))
+        pairs = sf.PointPointJoinQuery(conf(sf), g, g).run(sf.PointWindow.from_numpy(x[ix], y[ix]),
+                                                          sf.PointWindow.from_numpy(qx[qi], qy[qi]), r)
+        got.append(np.stack([ix[pairs[:, 0]], qi[pairs[:, 1]]], 1))
+    got = np.concatenate(got)
+    got = got[np.lexsort((got[:, 1], got[:, 0]))]
+    st, exp = oracle_mod.join_pp(og, og, x, y, qx, qy, r)
+    assert st == 0 and len(exp) > 1000
+    exp = exp[np.lexsort((exp[:, 1], exp[:, 0]))]
+    np.testing.assert_array_equal(got, exp)

@@ -1,7 +1,10 @@
-"""CPU, world_size 2 (gloo): the multi-GPU decomposition -- cell-column shards, concatenated
-range hits, all-gathered kNN top-k merge, halo-replicated join -- reproduces the
-single-window result.  The per-shard evaluator here is the oracle (no GPU in this
-container); the GPU per-shard kernels are covered by tests/test_gpu_parity.py."""
+"""CPU, world_size 2 (gloo): the host side of the multi-GPU decomposition -- cell-column band
+arithmetic, the kNN record exchange (sharding.gather_records_batch: the same all_gather of
+[nwin, rb] byte records the RCCL path runs, here over gloo on CPU tensors, decoded in the
+shard-major layout gf_knn_merge_dev_batch reads, merged with the library's host merge),
+concatenated range hits and the halo-replicated join.  The shard results fed in are the
+oracle's (no GPU here); the product kernels per shard and the device merge are covered by
+tests/test_gpu_sharding.py on the GPU."""
 import os
 import socket
 
@@ -44,10 +47,36 @@ def _worker(rank, world, port, ret):
         own = sharding.shard_of_columns(cx, bands) == rank
         idx = np.nonzero(own)[0]
 
-        # kNN: per-shard top-k (global indices), all-gather, merge
+        # kNN: per-shard top-k records of 3 windows (global indices) in ONE all-gather of byte
+        # records, decoded shard-major, merged per window
+        import torch
+        from spatialflink_amd.spatialOperators import decode_knn_record, knn_merge_host, knn_record_bytes
+
         for r, k in ((0.5, 50), (0.05, 20), (0.3, 200)):
-            st, o, d, i = O.knn(og, x[idx], y[idx], obj[idx], QPOINT[0], QPOINT[1], r, k)
-            mo, md, mi = sharding.allgather_knn_lists(o, d, idx[i], k)
+            rb = knn_record_bytes(k)
+            nwin = 3
+            recs = torch.zeros(nwin, rb, dtype=torch.uint8)
+            for w in range(nwin):
+                sel = idx[w:]  # windows differ: drop the first w points of the shard
+                st, o, d, i = O.knn(og, x[sel], y[sel], obj[sel], QPOINT[0], QPOINT[1], r, k)
+                recs[w] = torch.frombuffer(bytearray(sharding.encode_knn_record(k, o, d, sel[i])), dtype=torch.uint8)
+            gathered = sharding.gather_records_batch(recs).numpy()
+            assert gathered.size == world * nwin * rb
+            for w in range(nwin):
+                lists = []
+                for s_ in range(world):  # record (shard s, window w) at (s * nwin + w) * rb
+                    st, o, d, i = decode_knn_record(gathered[(s_ * nwin + w) * rb:(s_ * nwin + w + 1) * rb].tobytes(), k)
+                    assert st == 0
+                    lists.append((o, d, i))
+                mo, md, mi = knn_merge_host(k, lists)
+                keep = np.ones(len(x), bool)
+                for s_ in range(world):  # the window: every rank dropped its own first w points
+                    keep[np.nonzero(sharding.shard_of_columns(cx, bands) == s_)[0][:w]] = False
+                al = np.nonzero(keep)[0]
+                st, fo, fd, fi = O.knn(og, x[al], y[al], obj[al], QPOINT[0], QPOINT[1], r, k)
+                assert np.array_equal(mo, fo) and np.array_equal(md, fd) and np.array_equal(mi, al[fi]), (r, k, w)
+            mo, md, mi = sharding.allgather_knn_lists(*O.knn(og, x[idx], y[idx], obj[idx], QPOINT[0], QPOINT[1], r, k)[1:3],
+                                                      idx[O.knn(og, x[idx], y[idx], obj[idx], QPOINT[0], QPOINT[1], r, k)[3]], k)
             st, fo, fd, fi = O.knn(og, x, y, obj, QPOINT[0], QPOINT[1], r, k)
             assert np.array_equal(mo, fo) and np.array_equal(md, fd) and np.array_equal(mi, fi), (r, k)
 

@@ -137,7 +137,9 @@ def bench_range(args, polygons=False):
         grid_n = 500 if polygons else 100
         grid = sf.UniformGrid(grid_n, *BEIJING)
         og = O.grid(grid_n, *BEIJING)
-        nwin = 4
+        # enough distinct windows that their x, y (16 B/point) exceed the 256 MB Infinity Cache:
+        # every window is then read from HBM, not from the last window's residue
+        nwin = max(4, -(-384 * 2**20 // (16 * n)))
         wins = _windows(sf, n, nwin, 7 + 1000 * rank, dev, _band(sf, grid, grid_n, world, rank))
         ctx = _lib.context(dev)
         r = 0.001 if polygons else args.radius
@@ -176,16 +178,24 @@ def bench_range(args, polygons=False):
         words = (n + 63) // 64
         bitmaps = torch.empty(nwin, words, dtype=torch.int64, device=dev)
         counts = torch.zeros(nwin, 2, dtype=torch.int64, device=dev)
+        # the step ends with the window's ascending index list on the device (what the Java
+        # collector emits), produced by one async expansion launch after the scan
+        idx = torch.empty(4, n, dtype=torch.int32, device=dev)
+        icount = torch.zeros(nwin, dtype=torch.int64, device=dev)
         pts = [w[2].c_struct() for w in wins]
 
         nstreams = len(plans)
 
         def step(i):
             j = i % nwin
+            c = ctxs[i % nstreams].handle
             st = L.gf_range_run(plans[i % nstreams], C.byref(pts[j]), bitmaps[j].data_ptr(), None,
                                 counts[j].data_ptr())
+            if not st and not args.no_indices:
+                st = L.gf_bitmap_to_indices_async(c, bitmaps[j].data_ptr(), n, idx[i % 4].data_ptr(), n,
+                                                  icount[j].data_ptr())
             if st:
-                _lib.check(st, ctxs[i % nstreams].handle, "gf_range_run")
+                _lib.check(st, c, "gf_range_run")
 
         def sync_all():
             for c in ctxs:
@@ -221,6 +231,7 @@ def bench_range(args, polygons=False):
         # first min(n, 1M) points of the window are checked against the oracle run on them alone
         # (on every rank: its shard's hits are exactly the oracle's hits of those points)
         hits = int(counts[0, 0].item())
+        assert args.no_indices or int(icount[0].item()) == hits, "index list / counts disagree"
         m = min(n, 1_000_000)
         x, y, _ = wins[0]
         verified, cpu = None, None
@@ -252,11 +263,13 @@ def bench_range(args, polygons=False):
             wl += f"_per_gpu_x{world}"
         _line("point-polygon range" if polygons else "point-point range", world * n * args.steps / elapsed,
               "points/s", args.steps, args.warmup, elapsed,
-              "range_kernel + range_test_kernel" if tcnt else "range_kernel", 16.0 * n + n / 8.0, avg,
+              "range_kernel + range_test_kernel" if tcnt else "range_kernel", 16.0 * n + n / 8.0 + 4.0 * hits, avg,
               {"n_gpus": world,
                "config": {"workload": wl, "points_per_window": n * world, "points_per_gpu": n, "grid": grid_n,
                           "radius": r, "hits_window0": hits, "scan_blocks": blocks, "defer_mode": dmode,
-                          "windows_in_flight": nstreams,
+                          "windows_in_flight": nstreams, "distinct_windows": nwin,
+                          "window_set_MB": round(16.0 * n * nwin / 2**20, 1),
+                          "step": "gf_range_run (bitmap + counts) + gf_bitmap_to_indices_async (index list)",
                           "parallelism": f"cell-column shards x{world} (no collective)",
                           "cells_none_candidate_guaranteed_inside": [c.value for c in cells]},
                "breakdown": {"scan_us": round(avg_scan * 1e6, 2), "test_us": round(avg_test * 1e6, 2),
