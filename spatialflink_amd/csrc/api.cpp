@@ -67,6 +67,19 @@ void* ctx_pinned(gf_ctx* ctx, size_t bytes, int* status) {
   return ctx->pinned;
 }
 
+// One device scalar -> host through the pinned staging, then a stream sync (a pageable
+// destination is copied by a staged blit, ~50 us per call in the join's rocprofv3 trace).
+template <class T>
+static int read_scalar_sync(gf_ctx* ctx, const void* dev, T* out) {
+  int st = GF_OK;
+  T* h = (T*)ctx_pinned(ctx, sizeof(T), &st);
+  if (!h) return st;
+  GF_HIP_CHECK(ctx, hipMemcpyAsync(h, dev, sizeof(T), hipMemcpyDeviceToHost, ctx->stream));
+  GF_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+  *out = *h;
+  return GF_OK;
+}
+
 static hipEvent_t take_event(gf_ctx* ctx) {
   if (!ctx->pool.empty()) {
     hipEvent_t e = ctx->pool.back();
@@ -680,9 +693,6 @@ int build_table(gf_range_plan* P, const std::vector<Rect>& base, bool need_lists
   return GF_OK;
 }
 
-// dynamic LDS of a join probe task (2 x 512-thread blocks per CU)
-constexpr int kJoinLdsBudget = 76 * 1024;
-
 // row-span class tables up to this size are staged in LDS by every scan block
 constexpr int64_t kSpanLdsBytes = 32768;
 
@@ -986,8 +996,7 @@ extern "C" int gf_join_ppoly_run(gf_range_plan* P, const gf_grid* ugrid, const g
   GF_HIP_CHECK(ctx, launch_join_ppoly(ctx, a, blocks, jblocks, P->jecnt, P->jecand, P->jbtot, P->jtotal, pairs,
                                       pairs ? cap : 0, pairs && ((uintptr_t)pairs % 8 == 0)));
   unsigned long long total = 0;
-  GF_HIP_CHECK(ctx, hipMemcpyAsync(&total, P->jtotal, sizeof total, hipMemcpyDeviceToHost, ctx->stream));
-  GF_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+  if ((st = read_scalar_sync(ctx, P->jtotal, &total))) return st;
   *npairs = (int64_t)total;
   if ((int64_t)total > cap || (total > 0 && !pairs)) return GF_ERR_CAPACITY;
   return GF_OK;
@@ -1040,8 +1049,7 @@ extern "C" int gf_bitmap_to_indices(gf_ctx* ctx, const uint64_t* bitmap, int64_t
   GF_HIP_CHECK(ctx, launch_word_popcounts(ctx->stream, bitmap, words, pc));
   GF_HIP_CHECK(ctx, launch_exclusive_scan(ctx->stream, pc, words, off, tmp));
   uint32_t total = 0;
-  GF_HIP_CHECK(ctx, hipMemcpyAsync(&total, off + words, sizeof total, hipMemcpyDeviceToHost, ctx->stream));
-  GF_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+  if (int e = read_scalar_sync(ctx, off + words, &total)) return e;
   *count = total;
   if ((int64_t)total > cap) return GF_ERR_CAPACITY;
   if (total) {
@@ -1649,7 +1657,8 @@ extern "C" int gf_join_pp(gf_ctx* ctx, const gf_grid* ugrid, const gf_grid* qgri
   size_t o_qmat = ar.take<uint32_t>(qmat), o_qmats = ar.take<uint32_t>(qmat + 1);
   size_t o_txy = ar.take<double>(rowpath ? 2 * nq : 1), o_tc = ar.take<int32_t>(rowpath ? 2 * nq : 1);
   size_t o_tidx = ar.take<uint32_t>(rowpath ? nq : 1);
-  const int64_t max_tasks = no / kJoinTask + qn + 1;
+  // probe grid / task slots: >= the tasks (sum of ceil(row / kJoinTask)) + 8, a multiple of 8
+  const int64_t max_tasks = (no / kJoinTask + qn + 1 + 8 + 7) / 8 * 8;
 #ifndef GF_JOIN_SBPC
 #define GF_JOIN_SBPC 4  // ordinary-side bucketing blocks per CU
 #endif
@@ -1713,7 +1722,7 @@ extern "C" int gf_join_pp(gf_ctx* ctx, const gf_grid* ugrid, const gf_grid* qgri
     j.pairs = pairs;
     j.cap = pairs ? (uint64_t)std::max<int64_t>(cap, 0) : 0;
     j.pairs_aligned = ((uintptr_t)pairs & 7) == 0;
-    j.lds_budget = kJoinLdsBudget;
+    j.lds_budget = join_probe_budget(nq, qn, c);
     GF_HIP_CHECK(ctx, hipMemsetAsync(cnt2, 0, sizeof(unsigned long long), s));
     GF_HIP_CHECK(ctx, launch_join_rows(ctx, j, 0, sblocks));
     GF_HIP_CHECK(ctx, launch_exclusive_scan(s, j.row_mat, mat, j.row_mat_scan, R32(o_btmp)));
@@ -1727,8 +1736,7 @@ extern "C" int gf_join_pp(gf_ctx* ctx, const gf_grid* ugrid, const gf_grid* qgri
     k.ovf_count = cnt2; k.sqidx = j.sqidx; k.pairs = pairs; k.cap = j.cap; k.pairs_aligned = j.pairs_aligned; k.total = cnt2 + 1;
     GF_HIP_CHECK(ctx, launch_join_compact(ctx, k));
     unsigned long long total = 0;
-    GF_HIP_CHECK(ctx, hipMemcpyAsync(&total, cnt2 + 1, sizeof total, hipMemcpyDeviceToHost, s));
-    GF_HIP_CHECK(ctx, hipStreamSynchronize(s));
+    if (int e = read_scalar_sync(ctx, cnt2 + 1, &total)) return e;
     *npairs = (int64_t)total;
     ctx->join_ppp = (double)total / (double)no;
     if ((int64_t)total > cap || (total > 0 && !pairs)) return GF_ERR_CAPACITY;
@@ -1744,8 +1752,7 @@ extern "C" int gf_join_pp(gf_ctx* ctx, const gf_grid* ugrid, const gf_grid* qgri
   GF_HIP_CHECK(ctx, launch_join_probe(ctx, a, 0, blocks));
   GF_HIP_CHECK(ctx, launch_exclusive_scan(s, U32(o_cnt), blocks, U32(o_boff), U32(o_tmp)));
   uint32_t total = 0;
-  GF_HIP_CHECK(ctx, hipMemcpyAsync(&total, U32(o_boff) + blocks, sizeof total, hipMemcpyDeviceToHost, s));
-  GF_HIP_CHECK(ctx, hipStreamSynchronize(s));
+  if (int e = read_scalar_sync(ctx, U32(o_boff) + blocks, &total)) return e;
   *npairs = total;
   if ((int64_t)total > cap) return GF_ERR_CAPACITY;
   if (total == 0) return GF_OK;

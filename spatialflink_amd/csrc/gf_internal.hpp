@@ -445,8 +445,8 @@ hipError_t launch_join_qscatter(hipStream_t s, const double* qx, const double* q
 hipError_t launch_join_probe(gf_ctx* ctx, const JoinArgs& a, int write_pass, int blocks);
 
 // row-bucketed join (c >= 0): see k_join.hip
-constexpr int kJoinTask = 8192;      // ordinary points per probe task (one row)
-constexpr int kJoinThreads = 1024;
+constexpr int kJoinTask = 8192;      // ordinary points per probe task (part of one row)
+constexpr int kJoinThreads = 1024;   // two probe blocks per CU when the staged rows fit 80 KB
 constexpr int kJoinMaxRows = 16;     // staged query rows (2c+1) per task
 struct JoinRowArgs {
   const double* ox;
@@ -517,6 +517,8 @@ __host__ __device__ inline size_t join_row_lds_bytes(int64_t W, uint32_t m) {
   return ((size_t)(W + 1) * 2 + 15) / 16 * 16 + (size_t)m * 16;
 }
 hipError_t launch_join_rows(gf_ctx* ctx, const JoinRowArgs& a, int stage, int blocks);
+// LDS budget of the probe's staged query rows for nq query points on a qn x qn grid, 2c+1 rows
+int join_probe_budget(int64_t nq, int32_t qn, int64_t c);
 // row path, query side: cell-sorted query arrays + q_off without global atomics
 struct JoinQueryArgs {
   const double* qx;

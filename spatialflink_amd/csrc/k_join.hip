@@ -167,11 +167,6 @@ hipError_t launch_join_probe(gf_ctx* ctx, const JoinArgs& a, int write_pass, int
 // Counts pass -> scan over tasks -> write pass; pair order inside a task is unspecified.
 // =======================================================================================
 constexpr int kRowMax = 8192;  // rows staged as LDS histograms by the bucketing kernels
-#ifndef GF_JOIN_BATCH
-#define GF_JOIN_BATCH 4
-#endif
-constexpr int kJoinBatch = GF_JOIN_BATCH;
-  // candidates of one row loaded together in the probe
 
 // Bucketing: block b owns the contiguous input chunk b; its row histogram goes to column b of
 // the row-major matrix M[row][block] (plain stores).  The exclusive scan of M (flattened) is
@@ -402,160 +397,215 @@ struct QRow {
   uint32_t lxy;
 };
 
-// Candidates of ordinary point (px, py) in cell (cx, cy) among the staged rows: calls
-// hit(slot) for every pair, in a fixed order, where slot = the query point's position in the
-// cell-sorted query arrays; returns the number of pairs.  The slot -> query index lookup
-// (sqidx) is left to join_compact_kernel, where the gathers are independent of each other
-// (inside the probe loop each one stalls the candidate walk that follows it).
-// EXACT0: the plan is exact with metric 0 (squared-distance prefilter only, no hypot code).
-template <bool EXACT0, class Hit>
-__device__ __forceinline__ uint32_t join_row_point(const JoinRowArgs& a, const char* lds, const QRow* rows, int nrows,
-                                                   double px, double py, int32_t cx, int32_t cy, Hit&& hit) {
-  const int32_t W = a.qn + 2, c = (int32_t)a.c, qn = a.qn;
-  const int32_t kb = (cx - c < -1 ? -1 : cx - c) + 1, ke = (cx + c > qn ? qn : cx + c) + 2;
-  const bool fast_ok = EXACT0;
-  uint32_t cnt = 0;
-  for (int j = 0; j < nrows; ++j) {
-    const QRow R = rows[j];
-    const bool in_lds = R.loff != 0xffffffffu;
-    uint32_t tb, te, t_lo, t_hi;  // candidate run; [t_lo, t_hi) holds the interior buckets
-    if (in_lds) {
-      const uint16_t* lo16 = reinterpret_cast<const uint16_t*>(lds + R.loff);
-      tb = lo16[kb]; te = lo16[ke]; t_lo = lo16[1]; t_hi = lo16[W - 1];
-    } else {
-      const uint32_t* qo = a.q_off + (size_t)(R.ry + 1) * W;
-      tb = qo[kb] - R.gbase; te = qo[ke] - R.gbase; t_lo = qo[1] - R.gbase; t_hi = qo[W - 1] - R.gbase;
-    }
-    const bool brow = R.ry < 0 || R.ry >= qn;  // clamped row: true cells differ
-    uint32_t t = tb;
-    if (fast_ok && in_lds && !brow && te > tb && tb >= t_lo && te <= t_hi) {
-      // interior LDS run: kJoinBatch candidates loaded together (independent ds_read_b128)
-      const double2* lxy = reinterpret_cast<const double2*>(lds + R.lxy);
-      for (; t < te; t += kJoinBatch) {
-        double2 q[kJoinBatch];
-#pragma unroll
-        for (int k = 0; k < kJoinBatch; ++k) q[k] = lxy[t + k < te ? t + k : t];
-#pragma unroll
-        for (int k = 0; k < kJoinBatch; ++k) {
-          const double dx = px - q[k].x, dy = py - q[k].y;
-          if (t + k < te && dx * dx + dy * dy <= a.s_r) {  // s <= smax(r) <=> sqrt(s) <= r
-            hit(R.gbase + t + k);
-            ++cnt;
-          }
-        }
-      }
-      continue;
-    }
-    for (; t < te; ++t) {
-      const uint32_t gi = R.gbase + t;
-      if (brow || t < t_lo || t >= t_hi) {  // clamped bucket: Chebyshev test on the true cell
-        const int64_t ddx = (int64_t)a.sqcx[gi] - cx, ddy = (int64_t)a.sqcy[gi] - cy;
-        if (ddx > c || ddx < -c || ddy > c || ddy < -c) continue;
-      }
-      if (EXACT0 || !a.approx) {
-        double qx, qy;
-        if (in_lds) {
-          const double2 q = reinterpret_cast<const double2*>(lds + R.lxy)[t];
-          qx = q.x; qy = q.y;
-        } else {
-          qx = a.sqx[gi]; qy = a.sqy[gi];
-        }
-        const double dx = px - qx, dy = py - qy;
-        if (EXACT0 || a.metric == 0 ? !(dx * dx + dy * dy <= a.s_r) : !(fdlibm_hypot(dx, dy) <= a.r)) continue;
-      }
-      hit(gi);
-      ++cnt;
-    }
-  }
-  return cnt;
-}
-
-// Output sinks of the probe: a task's private region (capacity checked by the caller), and
-// the overflow, stored from the END of the caller's buffer (dropped past cap; still counted).
-struct RegionSink {
-  uint2* out;
-  __device__ void operator()(uint64_t pos, uint32_t p, uint32_t q) const { out[pos] = make_uint2(p, q); }
-};
-struct OverflowSink {
-  uint32_t* pairs;
-  uint64_t cap;
-  int aligned;
-  __device__ void operator()(uint64_t pos, uint32_t p, uint32_t q) const {
-    if (pos < cap) join_store(pairs, aligned, cap - 1 - pos, make_uint2(p, q));
-  }
-};
-
 struct JoinProbeHdr {
   int32_t row, fit;
+  uint32_t need;     // staged bytes of the task's query rows
   uint32_t beg, end;
   uint32_t used;     // pairs placed in the task's region so far (wave reservations)
   uint32_t fit_end;  // end of the last reservation that fit the region
+  uint32_t wsum[kJoinThreads / 64];
   QRow rows[kJoinMaxRows];
 };
 constexpr int kJoinHdrBytes = (int)((sizeof(JoinProbeHdr) + 15) / 16 * 16);
+constexpr int kJoinWaveBuf = 128;  // pairs a wave collects in LDS before one coalesced flush
+static_assert(kJoinTask <= 8192, "local index packed in 13 bits");
+// u16 column keys, later (same bytes) the wave pair buffers
+constexpr size_t kJoinUnionBytes = 2 * kJoinTask > kJoinWaveBuf * 8 * (kJoinThreads / 64)
+                                       ? 2 * kJoinTask : kJoinWaveBuf * 8 * (kJoinThreads / 64);
 
-// One pass per task: a round = kJoinThreads ordinary points.  Each thread probes its point
-// keeping the first kJoinReg query slots in registers; each wave reserves its pairs' run in the
-// task's private output region with one LDS atomic -- no block barrier and no global atomic in
-// the loop.  A point with more than kJoinReg pairs
-// is probed again for the rest (rare; same probe order both times).  A round that no longer
-// fits the region goes to the overflow region.  join_compact_kernel packs the regions.
-template <bool EXACT0>
-__global__ __launch_bounds__(kJoinThreads) __attribute__((amdgpu_waves_per_eu(8)))  // 2 blocks per CU
-void join_row_probe_kernel(JoinRowArgs a) {
-  // every LDS variable lives in the dynamic region, header first: static __shared__ would sit
-  // in front of it and shift its base off 16 B, and each misaligned ds_read_b128 of the staged
-  // rows is then replayed (measured: the probe ran 4x slower with a 408-byte static block)
+// Dynamic LDS of the probe: header | staged rows (budget) | sorted (column << 13 | local index)
+// u32 per point | column keys / wave pair buffers | column histogram [qn + 1]
+static size_t join_probe_lds_fixed(int32_t qn) {
+  return kJoinHdrBytes + 4 * (size_t)kJoinTask + kJoinUnionBytes + 4 * ((size_t)qn + 1);
+}
+static size_t join_probe_lds_bytes(int lds_budget, int32_t qn) { return join_probe_lds_fixed(qn) + (size_t)lds_budget; }
+
+// Two blocks per CU (80 KB each of the 160 KB LDS) when the expected staged rows fit: 2c+1 rows
+// of 1.15 x the mean row + 64 points (C4: 3 x 1000-point rows = 59 KB); otherwise one block
+// with the rest of the 160 KB.  A task whose rows exceed the budget reads them from global
+// memory (same results, slower).
+int join_probe_budget(int64_t nq, int32_t qn, int64_t c) {
+  const int64_t W = (int64_t)qn + 2;
+  const double mean = (double)nq / (double)(qn > 0 ? qn : 1);
+  const size_t need = (size_t)(2 * c + 1) * join_row_lds_bytes(W, (uint32_t)(mean + 4.0 * std::sqrt(mean) + 16.0));
+  const size_t fixed = join_probe_lds_fixed(qn);
+  const size_t half = 80 * 1024, full = 160 * 1024;
+  if (fixed < half && need <= half - fixed) return (int)(half - fixed);
+  return fixed < full ? (int)(full - fixed) : 0;
+}
+
+// Wave-uniform value (the compiler cannot prove it): one readfirstlane, so the loops that use
+// it run on scalar registers.
+__device__ __forceinline__ uint32_t join_uni(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+__device__ __forceinline__ int32_t join_uni(int32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+
+struct JoinLane {  // this lane's ordinary point
+  double px, py;
+  int32_t cx, cy;
+  uint32_t pidx;
+};
+
+// The wave's pair buffer in LDS: hits are appended in ballot order (one mbcnt per hit round,
+// the count stays in a scalar register); past kJoinWaveBuf - 64 the wave reserves a run in the
+// task's region (one LDS atomic) -- or, when the region is full, in the overflow at the end of
+// the caller's buffer (one device atomic) -- and copies the buffer out with coalesced stores.
+struct JoinWaveBuf {
+  uint2* buf;
+  uint32_t cnt;
+  __device__ __forceinline__ void flush(const JoinRowArgs& a, JoinProbeHdr& hd, uint2* region) {
+    const uint32_t lane = threadIdx.x & 63;
+    uint32_t wb = 0;
+    if (lane == 0) wb = atomicAdd(&hd.used, cnt);
+    wb = join_uni(wb);
+    if (wb + cnt <= a.task_cap) {
+      if (lane == 0) atomicMax(&hd.fit_end, wb + cnt);
+      for (uint32_t i = lane; i < cnt; i += 64) region[wb + i] = buf[i];
+    } else {
+      unsigned long long ob = 0;
+      if (lane == 0) ob = atomicAdd(a.ovf_count, (unsigned long long)cnt);
+      ob = ((unsigned long long)join_uni((uint32_t)(ob >> 32)) << 32) | join_uni((uint32_t)ob);
+      for (uint32_t i = lane; i < cnt; i += 64)
+        if (ob + i < a.cap) join_store(a.pairs, a.pairs_aligned, a.cap - 1 - (ob + i), buf[i]);
+    }
+    cnt = 0;
+  }
+  // one round's hits: hit i of this lane (candidate q[i]) goes after all hits of rounds < i
+  template <int R>
+  __device__ __forceinline__ void push(const bool (&hit)[R], uint32_t p, const uint32_t (&q)[R], const JoinRowArgs& a,
+                                       JoinProbeHdr& hd, uint2* region) {
+    uint64_t m[R];
+    uint64_t any = 0;
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      m[i] = __ballot(hit[i]);
+      any |= m[i];
+    }
+    if (any == 0) return;
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      if (m[i] == 0) continue;
+      if (hit[i])
+        buf[cnt + __builtin_amdgcn_mbcnt_hi((uint32_t)(m[i] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m[i], 0u))] =
+            make_uint2(p, q[i]);
+      cnt += (uint32_t)__popcll(m[i]);
+      if (cnt > kJoinWaveBuf - 64) flush(a, hd, region);
+    }
+  }
+};
+
+// One lane's candidates [tb, te) of one query row (relative to the row's first point gb): the
+// lanes walk their own runs together, two candidates per round, until every run is done (the
+// exit is a ballot, so the loop and the pair count stay wave-uniform).  Column-sorted lanes
+// share columns, so most lanes of a round read the same few LDS addresses.  SLOW: the run
+// touches a clamped bucket or row, so each candidate's true cell is checked (Chebyshev <= c).
+template <int MODE, bool LDS, bool SLOW>
+__device__ __forceinline__ void join_lane_run(const JoinRowArgs& a, const double2* lxy, uint32_t gb, uint32_t tb,
+                                              uint32_t te, const JoinLane& ln, JoinWaveBuf& wbuf, JoinProbeHdr& hd,
+                                              uint2* region) {
+  const uint32_t len = te - tb;
+  auto test = [&](bool act, uint32_t t, double2 q) {
+    bool in = act;
+    if constexpr (SLOW) {
+      if (act) {
+        const int64_t ddx = (int64_t)a.sqcx[gb + t] - ln.cx, ddy = (int64_t)a.sqcy[gb + t] - ln.cy;
+        in = ddx <= a.c && ddx >= -a.c && ddy <= a.c && ddy >= -a.c;
+      }
+    }
+    const double dx = ln.px - q.x, dy = ln.py - q.y;
+    bool ok;
+    if constexpr (MODE == 0) ok = dx * dx + dy * dy <= a.s_r;  // s <= smax(r) <=> sqrt(s) <= r
+    else ok = a.approx || (a.metric == 0 ? dx * dx + dy * dy <= a.s_r : fdlibm_hypot(dx, dy) <= a.r);
+    return in && ok;
+  };
+  constexpr int R = 4;  // candidates per round: their loads are in flight together
+  for (uint32_t k = 0; __ballot(k < len) != 0; k += R) {
+    bool act[R], hit[R];
+    uint32_t t[R], q[R];
+    double2 v[R];
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      act[i] = k + i < len;
+      t[i] = tb + (act[i] ? k + i : 0u);
+      q[i] = gb + t[i];
+    }
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      if constexpr (LDS) {  // a stale slot for a finished lane reads in-bounds LDS, masked below
+        v[i] = lxy[t[i]];
+      } else {
+        v[i] = make_double2(0.0, 0.0);
+        if (act[i]) v[i] = make_double2(a.sqx[q[i]], a.sqy[q[i]]);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < R; ++i) hit[i] = test(act[i], t[i], v[i]);
+    wbuf.push<R>(hit, ln.pidx, q, a, hd, region);
+  }
+}
+
+// One block per task = <= kJoinTask ordinary points of one cell row.  The 2c+1 query rows
+// around it are staged in LDS (u16 bucket offsets per column + xy), then the task's points are
+// counting-sorted by column in LDS.  A wave takes 64 consecutive points of that order and, per
+// staged row, each lane walks its own candidate run (the buckets cx-c .. cx+c of that row = the
+// replicated-key match, true cell within Chebyshev c) with the exact distance test.  Sorting
+// makes the lanes' runs overlap, so the per-round LDS reads hit few distinct addresses, and
+// the rounds per row are the longest run among ~8 columns instead of the union of all of them.
+// Pairs go through the wave's LDS buffer into the task's private region in coalesced runs;
+// join_compact_kernel packs the regions.
+template <int MODE>  // 0: exact, metric 0 (squared-distance bound); 1: approximate or hypot
+__global__ __launch_bounds__(kJoinThreads) void join_row_probe_kernel(JoinRowArgs a) {
+  // every LDS variable lives in the dynamic region, header first (a static __shared__ block in
+  // front would shift the dynamic base off 16 B: misaligned ds_read_b128 of the staged xy)
   extern __shared__ __attribute__((aligned(16))) char lds_base[];
   JoinProbeHdr& hd = *reinterpret_cast<JoinProbeHdr*>(lds_base);
   char* const lds = lds_base + kJoinHdrBytes;
-  int32_t& s_row = hd.row;
-  int32_t& s_fit = hd.fit;
-  uint32_t& s_beg = hd.beg;
-  uint32_t& s_end = hd.end;
   QRow* const rows = hd.rows;
+  // XCD-aware task order: workgroups go round-robin to the 8 XCDs, so XCD x gets the
+  // consecutive tasks [x * per, (x + 1) * per) -- neighbouring row tasks stage the same query
+  // rows, and they now meet in the same L2.  The grid is >= ntask + 8 (host); slots past ntask
+  // are zeroed by the block of the same index.
   const uint32_t ntask = a.task_off[a.qn];
-  const uint32_t task = blockIdx.x;
-  if (task >= ntask) {
-    if (threadIdx.x == 0) a.task_cnt[task] = 0u;
-    return;
-  }
+  if (blockIdx.x >= ntask && threadIdx.x == 0) a.task_cnt[blockIdx.x] = 0u;
+  const uint32_t per = (ntask + 7) / 8;
+  const uint32_t task = (blockIdx.x & 7u) * per + (blockIdx.x >> 3);
+  if ((blockIdx.x >> 3) >= per || task >= ntask) return;
   const int64_t W = (int64_t)a.qn + 2, c = a.c, qn = a.qn;
+  // the task's row: the one j with task_off[j] <= task < task_off[j+1] (a parallel search --
+  // one round of loads, where a serial binary search costs ~10 dependent ones)
   if (threadIdx.x == 0) {
     hd.used = 0u;
     hd.fit_end = 0u;
-    int lo = 0, hi = a.qn;  // row = last j with task_off[j] <= task
-    while (hi - lo > 1) {
-      const int mid = (lo + hi) >> 1;
-      if (a.task_off[mid] <= task) lo = mid; else hi = mid;
-    }
-    const uint32_t k = task - a.task_off[lo];
-    const uint32_t rb = a.row_off[lo], re = a.row_off[lo + 1];
-    s_row = lo;
-    s_beg = rb + k * kJoinTask;
-    s_end = rb + (k + 1) * kJoinTask < re ? rb + (k + 1) * kJoinTask : re;
-    // staged rows and their LDS footprint
-    const int64_t r0 = lo - c < -1 ? -1 : lo - c, r1 = lo + c > qn ? qn : lo + c;
-    size_t need = 0;
-    bool fit = (r1 - r0 + 1) <= kJoinMaxRows;
-    for (int64_t ry = r0; fit && ry <= r1; ++ry) {
-      const uint32_t b = a.q_off[(ry + 1) * W], e = a.q_off[(ry + 1) * W + W];
-      fit = (e - b) < 65536u;
-      need += join_row_lds_bytes(W, e - b);
-    }
-    s_fit = fit && need <= (size_t)a.lds_budget;
+    hd.need = 0u;
+    hd.fit = 1;
   }
+  for (int j = threadIdx.x; j < a.qn; j += kJoinThreads)
+    if (a.task_off[j] <= task && task < a.task_off[j + 1]) hd.row = j;
   __syncthreads();
-  const int32_t cy = s_row;
+  const int32_t cy = hd.row;
   const int64_t r0 = cy - c < -1 ? -1 : cy - c, r1 = cy + c > qn ? qn : cy + c;
   const int nrows = (int)(r1 - r0 + 1);
-  // stage (or describe) the rows
+  if (threadIdx.x == 0) {
+    // the row's tasks split it evenly (10000 points: 2 x 5000, not 8192 + 1808)
+    const uint32_t k = task - a.task_off[cy], nt = a.task_off[cy + 1] - a.task_off[cy];
+    const uint32_t rb = a.row_off[cy], re = a.row_off[cy + 1], size = (re - rb + nt - 1) / nt;
+    hd.beg = rb + k * size;
+    hd.end = rb + (k + 1) * size < re ? rb + (k + 1) * size : re;
+  }
+  if ((int)threadIdx.x < nrows && nrows <= kJoinMaxRows) {  // staged bytes of every query row
+    const uint32_t* qo = a.q_off + (r0 + threadIdx.x + 1) * W;
+    const uint32_t m = qo[W] - qo[0];
+    if (m >= 65536u) hd.fit = 0;
+    atomicAdd(&hd.need, (uint32_t)join_row_lds_bytes(W, m < 65536u ? m : 65536u));
+  }
+  __syncthreads();
+  const bool fit = hd.fit && nrows <= kJoinMaxRows && hd.need <= (uint32_t)a.lds_budget;
+  // stage (or describe) the query rows
   size_t off = 0;
-  for (int j = 0; j < nrows && j < kJoinMaxRows; ++j) {
+  for (int j = 0; j < nrows; ++j) {
     const int64_t ry = r0 + j;
     const uint32_t* qo = a.q_off + (ry + 1) * W;
     const uint32_t b = qo[0], e = qo[W];
-    if (s_fit) {
+    if (fit) {
       const uint32_t o16 = (uint32_t)off;
       uint16_t* lo16 = reinterpret_cast<uint16_t*>(lds + off);
       off += ((size_t)(W + 1) * 2 + 15) / 16 * 16;
@@ -569,85 +619,110 @@ void join_row_probe_kernel(JoinRowArgs a) {
       rows[j] = QRow{(int32_t)ry, b, 0xffffffffu, 0u};
     }
   }
+  // the task's points, counting-sorted by column: column per point (u16), column histogram ->
+  // exclusive scan (cursors) -> sorted (column << 13 | local index)
+  uint32_t* const lsort = reinterpret_cast<uint32_t*>(lds + a.lds_budget);
+  uint16_t* const lcx = reinterpret_cast<uint16_t*>(lsort + kJoinTask);
+  uint32_t* const hist = reinterpret_cast<uint32_t*>(lcx + kJoinTask);  // [qn + 1]
+  const uint32_t beg = hd.beg, cnt = hd.end - hd.beg;
+  for (int j = threadIdx.x; j <= a.qn; j += kJoinThreads) hist[j] = 0u;
   __syncthreads();
-  const uint32_t beg = s_beg, end = s_end;
-  struct Pt {
-    double x, y;
-    uint32_t idx;
-    bool valid;
-  };
-  auto load = [&](uint32_t i, Pt& p) {
-    p.valid = i < end;
-    p.x = p.y = 0.0;
-    p.idx = 0u;
-    if (p.valid) {
-      const double2 v = reinterpret_cast<const double2*>(a.soxy)[i];
-      p.x = v.x;
-      p.y = v.y;
-      p.idx = a.soidx[i];
+  {
+    constexpr int PER = kJoinTask / kJoinThreads;  // all loads in flight before the first use
+    double xs[PER];
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const uint32_t i = threadIdx.x + u * kJoinThreads;
+      xs[u] = i < cnt ? a.soxy[2 * (size_t)(beg + i)] : 0.0;
     }
-  };
-  struct Hits {
-    uint32_t n = 0, h0 = 0, h1 = 0, h2 = 0;  // kJoinReg = 3 (no dynamic register indexing)
-  };
-  auto probe = [&](const Pt& p, Hits& H) {
-    if (!p.valid) return;
-    const int32_t cx = cell_index(p.x, a.u_minX, a.u_cl);
-    join_row_point<EXACT0>(a, lds, rows, nrows, p.x, p.y, cx, cy, [&](uint32_t q) {
-      const uint32_t n = H.n;  // selects, not an indexed array (which would live in scratch)
-      H.h0 = n == 0 ? q : H.h0;
-      H.h1 = n == 1 ? q : H.h1;
-      H.h2 = n == 2 ? q : H.h2;
-      H.n = n + 1;
-    });
-  };
-  auto emit = [&](const Pt& p, const Hits& H, const auto& put, uint64_t pos) {
-    if (H.n > 0) put(pos, p.idx, H.h0);
-    if (H.n > 1) put(pos + 1, p.idx, H.h1);
-    if (H.n > 2) put(pos + 2, p.idx, H.h2);
-    if (H.n > kJoinReg) {  // the rest: probe again, skipping the first kJoinReg pairs
-      uint32_t m = 0;
-      const int32_t cx = cell_index(p.x, a.u_minX, a.u_cl);
-      join_row_point<EXACT0>(a, lds, rows, nrows, p.x, p.y, cx, cy, [&](uint32_t q) {
-        if (m >= kJoinReg) put(pos + m, p.idx, q);
-        ++m;
-      });
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const uint32_t i = threadIdx.x + u * kJoinThreads;
+      if (i < cnt) {
+        const int32_t cx = cell_index(xs[u], a.u_minX, a.u_cl);  // in [0, qn): bucketed points are in grid
+        lcx[i] = (uint16_t)cx;
+        atomicAdd(&hist[cx], 1u);
+      }
     }
-  };
-  uint2* const region = a.tpairs + (size_t)task * a.task_cap;
-  const uint32_t lane = threadIdx.x & 63;
-  Pt A;
-  load(beg + threadIdx.x, A);
-  for (uint32_t s = beg; s < end; s += kJoinThreads) {
-    Pt B;  // the next round's point in flight while this round is probed
-    load(s + kJoinThreads + threadIdx.x, B);
-    Hits H;
-    probe(A, H);
-    // wave-level placement, no block barrier in the loop: a wave prefix sum, then one LDS
-    // atomic per wave reserves its run in the task's region (pair order is unspecified)
-    uint32_t inc = H.n;
+  }
+  __syncthreads();
+  {  // exclusive scan of hist[0 .. qn) in place (each thread a contiguous run of columns)
+    uint32_t* const wsum = hd.wsum;
+    const int per = (a.qn + kJoinThreads - 1) / kJoinThreads, j0 = threadIdx.x * per;
+    uint32_t run = 0;
+    for (int j = j0; j < j0 + per && j < a.qn; ++j) run += hist[j];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    uint32_t inc = run;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
       const uint32_t t = __shfl_up(inc, o, 64);
-      if (lane >= (uint32_t)o) inc += t;
+      if (lane >= o) inc += t;
     }
-    const uint32_t wt = __shfl(inc, 63, 64), ex = inc - H.n;
-    if (wt) {
-      uint32_t wb = 0;
-      if (lane == 0) wb = atomicAdd(&hd.used, wt);
-      wb = __shfl(wb, 0, 64);
-      if (wb + wt <= a.task_cap) {
-        if (lane == 0) atomicMax(&hd.fit_end, wb + wt);
-        emit(A, H, RegionSink{region}, wb + ex);
-      } else {  // overflow (dense spots): one device atomic per wave
-        unsigned long long ob = 0;
-        if (lane == 0) ob = atomicAdd(a.ovf_count, (unsigned long long)wt);
-        ob = ((unsigned long long)__shfl((uint32_t)(ob >> 32), 0, 64) << 32) | __shfl((uint32_t)ob, 0, 64);
-        emit(A, H, OverflowSink{a.pairs, a.cap, a.pairs_aligned}, ob + ex);
+    if (lane == 63) wsum[wid] = inc;
+    __syncthreads();
+    uint32_t before = inc - run;
+    for (int w = 0; w < wid; ++w) before += wsum[w];
+    for (int j = j0; j < j0 + per && j < a.qn; ++j) {
+      const uint32_t v = hist[j];
+      hist[j] = before;
+      before += v;
+    }
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < cnt; i += kJoinThreads) {
+    const uint32_t cx = lcx[i];
+    lsort[atomicAdd(&hist[cx], 1u)] = cx << 13 | i;
+  }
+  __syncthreads();  // lcx is dead from here: its space holds the wave buffers
+
+  const uint32_t lane = threadIdx.x & 63;
+  const int32_t qnn = a.qn, cc = (int32_t)c;
+  uint2* const region = a.tpairs + (size_t)task * a.task_cap;
+  JoinWaveBuf wbuf{reinterpret_cast<uint2*>(lcx) + (threadIdx.x >> 6) * kJoinWaveBuf, 0u};
+  // the next wave-step's points are fetched before this step's candidates are walked
+  struct Pt {
+    double2 v;
+    uint32_t idx, e;
+  };
+  auto fetch = [&](uint32_t s) {
+    Pt p{make_double2(0.0, 0.0), 0u, 0u};
+    if (s + lane < cnt) {
+      p.e = lsort[s + lane];
+      p.v = reinterpret_cast<const double2*>(a.soxy)[beg + (p.e & 8191u)];
+      p.idx = a.soidx[beg + (p.e & 8191u)];
+    }
+    return p;
+  };
+  Pt nxt = fetch((threadIdx.x >> 6) * 64);
+  for (uint32_t s = (threadIdx.x >> 6) * 64; s < cnt; s += kJoinThreads) {  // wave-uniform
+    const bool valid = s + lane < cnt;
+    const Pt cur = nxt;
+    nxt = fetch(s + kJoinThreads);
+    const JoinLane ln{cur.v.x, cur.v.y, valid ? (int32_t)(cur.e >> 13) : 0, cy, cur.idx};
+    const int32_t kb = (ln.cx - cc < -1 ? -1 : ln.cx - cc) + 1, ke = (ln.cx + cc > qnn ? qnn : ln.cx + cc) + 2;
+    for (int j = 0; j < nrows; ++j) {
+      const QRow R = rows[j];
+      const int32_t ry = join_uni(R.ry);
+      const uint32_t gb = join_uni(R.gbase);
+      const bool brow = ry < 0 || ry >= qnn;  // clamped row: the true cells differ
+      if (join_uni(R.loff) != 0xffffffffu) {
+        const uint16_t* lo16 = reinterpret_cast<const uint16_t*>(lds + join_uni(R.loff));
+        const double2* lxy = reinterpret_cast<const double2*>(lds + join_uni(R.lxy));
+        const uint32_t tb = valid ? lo16[kb] : 0u, te = valid ? lo16[ke] : 0u;
+        // clamped buckets 0 (column -1) and W-1 (column qn): [0, lo16[1]) and [lo16[W-1], ...)
+        const bool slow = te > tb && (brow || kb == 0 || ke == (int32_t)W);
+        if (__ballot(slow) != 0) join_lane_run<MODE, true, true>(a, lxy, gb, tb, te, ln, wbuf, hd, region);
+        else join_lane_run<MODE, true, false>(a, lxy, gb, tb, te, ln, wbuf, hd, region);
+      } else {
+        const uint32_t* qo = a.q_off + (size_t)(ry + 1) * W;
+        const uint32_t tb = valid ? qo[kb] - gb : 0u, te = valid ? qo[ke] - gb : 0u;
+        const bool slow = te > tb && (brow || kb == 0 || ke == (int32_t)W);
+        if (__ballot(slow) != 0) join_lane_run<MODE, false, true>(a, nullptr, gb, tb, te, ln, wbuf, hd, region);
+        else join_lane_run<MODE, false, false>(a, nullptr, gb, tb, te, ln, wbuf, hd, region);
       }
     }
-    A = B;
   }
+  if (wbuf.cnt > 0) wbuf.flush(a, hd, region);
   __syncthreads();
   if (threadIdx.x == 0) a.task_cnt[task] = hd.fit_end;
 }
@@ -734,12 +809,11 @@ hipError_t launch_join_rows(gf_ctx* ctx, const JoinRowArgs& a, int stage, int bl
       break;
     case 3: {
       KTimer t(ctx, GF_K_JOIN_PROBE);
+      const size_t lds = join_probe_lds_bytes(a.lds_budget, a.qn);
       if (!a.approx && a.metric == 0)
-        hipLaunchKernelGGL(join_row_probe_kernel<true>, dim3(blocks), dim3(kJoinThreads), a.lds_budget + kJoinHdrBytes,
-                           s, a);
+        hipLaunchKernelGGL(join_row_probe_kernel<0>, dim3(blocks), dim3(kJoinThreads), lds, s, a);
       else
-        hipLaunchKernelGGL(join_row_probe_kernel<false>, dim3(blocks), dim3(kJoinThreads), a.lds_budget + kJoinHdrBytes,
-                           s, a);
+        hipLaunchKernelGGL(join_row_probe_kernel<1>, dim3(blocks), dim3(kJoinThreads), lds, s, a);
       break;
     }
   }
