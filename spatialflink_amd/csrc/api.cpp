@@ -1650,7 +1650,7 @@ extern "C" int gf_join_pp(gf_ctx* ctx, const gf_grid* ugrid, const gf_grid* qgri
   size_t o_sqcx = ar.take<int32_t>(nq), o_sqcy = ar.take<int32_t>(nq), o_sqi = ar.take<uint32_t>(nq);
   size_t o_cnt = ar.take<uint32_t>(blocks), o_boff = ar.take<uint32_t>(blocks + 1);
   // row-bucketed path (k_join.hip): bucket the ordinary side by cell row, probe per task
-  const bool rowpath = c >= 0 && 2 * c + 1 <= kJoinMaxRows && qn + 2 <= 8192 && !ctx->join_legacy;
+  const bool rowpath = c >= 0 && 2 * c + 1 <= kJoinMaxRows && qn + 8 <= 8192 && !ctx->join_legacy;
   // query side of the row path: row bucketing + per-row column sort (no global atomics)
   const int qblk = (int)std::min<int64_t>(std::min<int64_t>(std::max<int64_t>(nq / 4096, 1), (int64_t)ctx->num_cus * 2), W);
   const int64_t qmat = rowpath ? W * qblk : 1;
@@ -1660,7 +1660,7 @@ extern "C" int gf_join_pp(gf_ctx* ctx, const gf_grid* ugrid, const gf_grid* qgri
   // probe grid / task slots: >= the tasks (sum of ceil(row / kJoinTask)) + 8, a multiple of 8
   const int64_t max_tasks = (no / kJoinTask + qn + 1 + 8 + 7) / 8 * 8;
 #ifndef GF_JOIN_SBPC
-#define GF_JOIN_SBPC 4  // ordinary-side bucketing blocks per CU
+#define GF_JOIN_SBPC 1  // ordinary-side bucketing blocks per CU (1024 threads, one tile buffer each)
 #endif
   const int sblocks = (int)std::min<int64_t>(std::max<int64_t>(no / 8192, 1), (int64_t)ctx->num_cus * GF_JOIN_SBPC);
   const int64_t mat = rowpath ? qn * sblocks : 1;
@@ -1673,7 +1673,8 @@ extern "C" int gf_join_pp(gf_ctx* ctx, const gf_grid* ugrid, const gf_grid* qgri
   tcap = std::max<int64_t>(tcap, kJoinTask);
   tcap = std::min<int64_t>(tcap, std::max<int64_t>(kJoinTask, ((int64_t)1 << 31) / 8 / std::max<int64_t>(max_tasks, 1)));
   size_t o_tpairs = ar.take<uint64_t>(rowpath ? max_tasks * tcap : 1), o_tcnt = ar.take<uint32_t>(rowpath ? max_tasks : 1);
-  size_t o_btmp = ar.take<uint32_t>(std::max(scan_tmp_elems(mat), scan_tmp_elems(qn)));
+  size_t o_tkoff = ar.take<uint32_t>(rowpath ? max_tasks + 1 : 1);
+  size_t o_btmp = ar.take<uint32_t>(std::max({scan_tmp_elems(mat), scan_tmp_elems(qn), scan_tmp_elems(max_tasks)}));
   size_t o_soxy = ar.take<double>(rowpath ? 2 * no : 1), o_soidx = ar.take<uint32_t>(rowpath ? no : 1);
   char* base = (char*)ctx_scratch(ctx, ar.off, &st);
   if (st) return st;
@@ -1731,9 +1732,11 @@ extern "C" int gf_join_pp(gf_ctx* ctx, const gf_grid* ugrid, const gf_grid* qgri
     GF_HIP_CHECK(ctx, launch_exclusive_scan(s, j.row_tasks, qn, R32(o_toff), R32(o_btmp)));
     // one probe pass into the task regions (+ overflow), then one packing launch
     GF_HIP_CHECK(ctx, launch_join_rows(ctx, j, 3, (int)max_tasks));
+    GF_HIP_CHECK(ctx, launch_exclusive_scan(s, j.task_cnt, max_tasks, R32(o_tkoff), R32(o_btmp)));
     JoinCompactArgs k{};
-    k.tpairs = j.tpairs; k.task_cap = j.task_cap; k.task_cnt = j.task_cnt; k.ntask = (uint32_t)max_tasks;
-    k.ovf_count = cnt2; k.sqidx = j.sqidx; k.pairs = pairs; k.cap = j.cap; k.pairs_aligned = j.pairs_aligned; k.total = cnt2 + 1;
+    k.tpairs = j.tpairs; k.task_cap = j.task_cap; k.task_cnt = j.task_cnt; k.task_off = R32(o_tkoff);
+    k.ntask = (uint32_t)max_tasks;
+    k.ovf_count = cnt2; k.pairs = pairs; k.cap = j.cap; k.pairs_aligned = j.pairs_aligned; k.total = cnt2 + 1;
     GF_HIP_CHECK(ctx, launch_join_compact(ctx, k));
     unsigned long long total = 0;
     if (int e = read_scalar_sync(ctx, cnt2 + 1, &total)) return e;

@@ -483,16 +483,17 @@ struct JoinRowArgs {
   int pairs_aligned;        // 8-byte aligned: one 8-byte store per pair
   int lds_budget;
 };
-// Dense output [0, total): the task regions packed in task order, then the overflow moved
-// down from the buffer's end; the probe stores (ordinary idx, query slot), the packing maps
-// the slot to the query index.  *total = pairs found (also when > cap: nothing is then valid).
+// Dense output [0, total): the task regions packed in task order (offsets = exclusive scan
+// of task_cnt, task_off[ntask] = their sum), then the overflow moved down from the buffer's
+// end.  The probe already stores (ordinary idx, query idx).  *total = pairs found (also when
+// > cap: nothing is then valid).
 struct JoinCompactArgs {
   const uint2* tpairs;
   uint32_t task_cap;
   const uint32_t* task_cnt;
+  const uint32_t* task_off;  // [ntask + 1]
   uint32_t ntask;
   const unsigned long long* ovf_count;
-  const uint32_t* sqidx;    // query slot -> query index
   uint32_t* pairs;
   uint64_t cap;
   int pairs_aligned;

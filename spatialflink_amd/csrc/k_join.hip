@@ -183,24 +183,28 @@ __device__ __forceinline__ void chunk_of(int64_t no, int64_t& beg, int64_t& end)
 // otherwise: one HBM round trip per point per wave)
 constexpr int kBucketU = 8;
 
-__global__ __launch_bounds__(kBlock) void join_orow_hist_kernel(JoinRowArgs a, uint32_t* __restrict__ M) {
+constexpr int kScatThreads = 1024;
+constexpr int kScatTile = 4096;
+constexpr int kScatPer = kScatTile / kScatThreads;
+
+__global__ __launch_bounds__(kScatThreads) void join_orow_hist_kernel(JoinRowArgs a, uint32_t* __restrict__ M) {
   __shared__ uint32_t h[kRowMax];
   int64_t beg, end;
   chunk_of(a.no, beg, end);
-  for (int j = threadIdx.x; j < a.qn; j += kBlock) h[j] = 0u;
+  for (int j = threadIdx.x; j < a.qn; j += kScatThreads) h[j] = 0u;
   __syncthreads();
-  for (int64_t i0 = beg + threadIdx.x; i0 < end; i0 += kBlock * kBucketU) {
+  for (int64_t i0 = beg + threadIdx.x; i0 < end; i0 += kScatThreads * kBucketU) {
     double x[kBucketU], y[kBucketU];
 #pragma unroll
     for (int u = 0; u < kBucketU; ++u) {
-      const int64_t i = i0 + u * kBlock;
+      const int64_t i = i0 + u * kScatThreads;
       x[u] = i < end ? __builtin_nontemporal_load(a.ox + i) : NAN;
       y[u] = i < end ? __builtin_nontemporal_load(a.oy + i) : NAN;
     }
 #pragma unroll
     for (int u = 0; u < kBucketU; ++u) {
       if (!(x[u] == x[u])) {  // NaN (or past the end): cell 0 per Java, but i may be past the end
-        if (i0 + u * kBlock >= end) continue;
+        if (i0 + u * kScatThreads >= end) continue;
       }
       const int32_t cx = cell_index(x[u], a.u_minX, a.u_cl);
       const int32_t cy = cell_index(y[u], a.u_minY, a.u_cl);
@@ -208,35 +212,100 @@ __global__ __launch_bounds__(kBlock) void join_orow_hist_kernel(JoinRowArgs a, u
     }
   }
   __syncthreads();
-  for (int j = threadIdx.x; j < a.qn; j += kBlock) M[(size_t)j * gridDim.x + blockIdx.x] = h[j];
+  for (int j = threadIdx.x; j < a.qn; j += kScatThreads) M[(size_t)j * gridDim.x + blockIdx.x] = h[j];
 }
 
-__global__ __launch_bounds__(kBlock) void join_orow_scatter_kernel(JoinRowArgs a, const uint32_t* __restrict__ Ms) {
-  __shared__ uint32_t h[kRowMax];
+// Write-combining row scatter.  Stores straight from the registers put every lane of a wave
+// into a different row: 64 separate 16 B + 4 B writes per store instruction, each a partial
+// line that reaches HBM on its own (rocprofv3 r02: WRITE_SIZE 2.5x the bytes, 208 us).  Here a
+// block takes its chunk in tiles of kScatTile points: cells -> LDS row histogram -> scan ->
+// the tile's points placed row-contiguously in LDS (with their destination) -> written out in
+// that order, so consecutive lanes write consecutive slots of one row (runs of ~tile/qn
+// points) and successive tiles extend the same runs.  Destinations: the block's run start of
+// each row (scan of the histogram matrix, as before) advanced tile by tile.
+
+size_t join_scatter_lds_bytes(int32_t qn) {
+  return (size_t)kScatTile * (16 + 4 + 4) + 2 * 4 * (size_t)qn + 4 * (kScatThreads / 64);
+}
+
+__global__ __launch_bounds__(kScatThreads) void join_orow_scatter_kernel(JoinRowArgs a, const uint32_t* __restrict__ Ms) {
+  extern __shared__ __attribute__((aligned(16))) char sm[];
+  double2* const sxy = reinterpret_cast<double2*>(sm);
+  uint32_t* const sidx = reinterpret_cast<uint32_t*>(sxy + kScatTile);
+  uint32_t* const sdst = sidx + kScatTile;
+  uint32_t* const th = sdst + kScatTile;  // [qn] tile counts -> starts -> ends
+  uint32_t* const gd = th + a.qn;         // [qn] next global slot of the row (tile-local: minus start)
+  uint32_t* const wsum = gd + a.qn;
+  const int qn = a.qn;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   int64_t beg, end;
   chunk_of(a.no, beg, end);
-  for (int j = threadIdx.x; j < a.qn; j += kBlock) h[j] = Ms[(size_t)j * gridDim.x + blockIdx.x];
+  for (int r = threadIdx.x; r < qn; r += kScatThreads) {
+    gd[r] = Ms[(size_t)r * gridDim.x + blockIdx.x];
+    th[r] = 0u;
+  }
   __syncthreads();
-  for (int64_t i0 = beg + threadIdx.x; i0 < end; i0 += kBlock * kBucketU) {
-    double x[kBucketU], y[kBucketU];
+  const int per = (qn + kScatThreads - 1) / kScatThreads, r0 = threadIdx.x * per;
+  for (int64_t t0 = beg; t0 < end; t0 += kScatTile) {
+    double x[kScatPer], y[kScatPer];
+    int32_t row[kScatPer];
 #pragma unroll
-    for (int u = 0; u < kBucketU; ++u) {
-      const int64_t i = i0 + u * kBlock;
+    for (int u = 0; u < kScatPer; ++u) {
+      const int64_t i = t0 + threadIdx.x + u * kScatThreads;
       x[u] = i < end ? __builtin_nontemporal_load(a.ox + i) : 0.0;
       y[u] = i < end ? __builtin_nontemporal_load(a.oy + i) : 0.0;
     }
 #pragma unroll
-    for (int u = 0; u < kBucketU; ++u) {
-      const int64_t i = i0 + u * kBlock;
-      if (i >= end) continue;
+    for (int u = 0; u < kScatPer; ++u) {
+      const int64_t i = t0 + threadIdx.x + u * kScatThreads;
       const int32_t cx = cell_index(x[u], a.u_minX, a.u_cl);
       const int32_t cy = cell_index(y[u], a.u_minY, a.u_cl);
-      if (cx >= 0 && cy >= 0 && cx < a.qn && cy < a.qn) {
-        const uint32_t pos = atomicAdd(&h[cy], 1u);
-        reinterpret_cast<double2*>(a.soxy)[pos] = make_double2(x[u], y[u]);
-        a.soidx[pos] = (uint32_t)i;
-      }
+      row[u] = i < end && cx >= 0 && cy >= 0 && cx < qn && cy < qn ? cy : -1;
+      if (row[u] >= 0) atomicAdd(&th[row[u]], 1u);
     }
+    __syncthreads();
+    // exclusive scan of the tile counts (a contiguous run of rows per thread); gd becomes
+    // (next global slot - tile start) so that slot + gd is the destination
+    uint32_t run = 0;
+    for (int r = r0; r < r0 + per && r < qn; ++r) run += th[r];
+    uint32_t inc = run;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t t = __shfl_up(inc, o, 64);
+      if (lane >= o) inc += t;
+    }
+    if (lane == 63) wsum[wid] = inc;
+    __syncthreads();
+    uint32_t before = inc - run;
+    for (int w = 0; w < wid; ++w) before += wsum[w];
+    uint32_t kept = 0;
+    for (int w = 0; w < kScatThreads / 64; ++w) kept += wsum[w];
+    for (int r = r0; r < r0 + per && r < qn; ++r) {
+      const uint32_t v = th[r];
+      th[r] = before;
+      gd[r] -= before;
+      before += v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < kScatPer; ++u) {
+      if (row[u] < 0) continue;
+      const uint32_t slot = atomicAdd(&th[row[u]], 1u);
+      sxy[slot] = make_double2(x[u], y[u]);
+      sidx[slot] = (uint32_t)(t0 + threadIdx.x + u * kScatThreads);
+      sdst[slot] = gd[row[u]] + slot;
+    }
+    __syncthreads();
+    for (uint32_t k = threadIdx.x; k < kept; k += kScatThreads) {
+      const uint32_t d = sdst[k];
+      reinterpret_cast<double2*>(a.soxy)[d] = sxy[k];
+      a.soidx[d] = sidx[k];
+    }
+    for (int r = r0; r < r0 + per && r < qn; ++r) {  // th[r] = tile end of the row
+      gd[r] += th[r];
+      th[r] = 0u;
+    }
+    __syncthreads();
   }
 }
 
@@ -457,15 +526,21 @@ struct JoinWaveBuf {
     uint32_t wb = 0;
     if (lane == 0) wb = atomicAdd(&hd.used, cnt);
     wb = join_uni(wb);
+    // the query slot becomes the query index here (an L2 gather of the sorted query side)
     if (wb + cnt <= a.task_cap) {
       if (lane == 0) atomicMax(&hd.fit_end, wb + cnt);
-      for (uint32_t i = lane; i < cnt; i += 64) region[wb + i] = buf[i];
+      for (uint32_t i = lane; i < cnt; i += 64) {
+        const uint2 v = buf[i];
+        region[wb + i] = make_uint2(v.x, a.sqidx[v.y]);
+      }
     } else {
       unsigned long long ob = 0;
       if (lane == 0) ob = atomicAdd(a.ovf_count, (unsigned long long)cnt);
       ob = ((unsigned long long)join_uni((uint32_t)(ob >> 32)) << 32) | join_uni((uint32_t)ob);
-      for (uint32_t i = lane; i < cnt; i += 64)
-        if (ob + i < a.cap) join_store(a.pairs, a.pairs_aligned, a.cap - 1 - (ob + i), buf[i]);
+      for (uint32_t i = lane; i < cnt; i += 64) {
+        const uint2 v = buf[i];
+        if (ob + i < a.cap) join_store(a.pairs, a.pairs_aligned, a.cap - 1 - (ob + i), make_uint2(v.x, a.sqidx[v.y]));
+      }
     }
     cnt = 0;
   }
@@ -735,42 +810,29 @@ __global__ __launch_bounds__(kJoinThreads) void join_row_probe_kernel(JoinRowArg
 // the rest of the target takes the source's remainder (every position read and written by one
 // thread; disjoint from [0, T) whenever T + n_ovf <= cap -- otherwise the call fails anyway).
 __global__ __launch_bounds__(kBlock) void join_compact_kernel(JoinCompactArgs a) {
-  __shared__ unsigned long long part[kBlock / 64];
-  const uint32_t t = blockIdx.x < a.ntask ? blockIdx.x : a.ntask;
-  unsigned long long sum = 0;
-  for (uint32_t i = threadIdx.x; i < t; i += kBlock) sum += a.task_cnt[i];
-  for (int o = 32; o > 0; o >>= 1) sum += __shfl_down(sum, o, 64);
-  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = sum;
-  __syncthreads();
-  unsigned long long off = 0;
-  for (int w = 0; w < kBlock / 64; ++w) off += part[w];
-  if (blockIdx.x < a.ntask) {
+  const uint64_t T = a.task_off[a.ntask];
+  if (blockIdx.x < a.ntask) {  // block b copies task b's region to its offset (capacity clipped)
+    const uint64_t off = a.task_off[blockIdx.x];
     const uint32_t n0 = a.task_cnt[blockIdx.x];
-    const uint32_t n = off >= a.cap ? 0u : (uint32_t)(off + n0 > a.cap ? a.cap - off : n0);  // capacity clip
+    const uint32_t n = off >= a.cap ? 0u : (uint32_t)(off + n0 > a.cap ? a.cap - off : n0);
     const uint2* src = a.tpairs + (size_t)blockIdx.x * a.task_cap;
-    // kCompactU pairs per thread in flight: the region loads, then the slot -> index gathers,
-    // then the stores (one at a time, each gather stalled the loop on its L2 round trip: 87 -> 67 us
-    // per 10M x 1M window)
-    constexpr int kCompactU = 4;
+    constexpr int kCompactU = 4;  // region loads in flight before the stores
     for (uint32_t i0 = threadIdx.x; i0 < n; i0 += kBlock * kCompactU) {
       uint2 v[kCompactU];
-      uint32_t q[kCompactU];
 #pragma unroll
       for (int u = 0; u < kCompactU; ++u) {
         const uint32_t i = i0 + u * kBlock;
         v[u] = src[i < n ? i : i0];
       }
 #pragma unroll
-      for (int u = 0; u < kCompactU; ++u) q[u] = a.sqidx[v[u].y];
-#pragma unroll
       for (int u = 0; u < kCompactU; ++u) {
         const uint32_t i = i0 + u * kBlock;
-        if (i < n) join_store(a.pairs, a.pairs_aligned, off + i, make_uint2(v[u].x, q[u]));
+        if (i < n) join_store(a.pairs, a.pairs_aligned, off + i, v[u]);
       }
     }
     return;
   }
-  const unsigned long long nov = *a.ovf_count, T = off;
+  const unsigned long long nov = *a.ovf_count;
   if (blockIdx.x == a.ntask && threadIdx.x == 0) *a.total = T + nov;
   if (nov == 0 || T + nov > a.cap) return;
   const uint64_t lo = a.cap - nov;  // overflow source [lo, cap), target [T, T + nov)
@@ -779,8 +841,7 @@ __global__ __launch_bounds__(kBlock) void join_compact_kernel(JoinCompactArgs a)
        i += (uint64_t)(gridDim.x - a.ntask) * kBlock) {
     const uint64_t dst = T + i;
     const uint64_t src = apart ? lo + i : (dst < lo ? T + nov + i : dst);
-    const uint2 v = join_load(a.pairs, a.pairs_aligned, src);
-    join_store(a.pairs, a.pairs_aligned, dst, make_uint2(v.x, a.sqidx[v.y]));
+    join_store(a.pairs, a.pairs_aligned, dst, join_load(a.pairs, a.pairs_aligned, src));
   }
 }
 
@@ -795,12 +856,13 @@ hipError_t launch_join_rows(gf_ctx* ctx, const JoinRowArgs& a, int stage, int bl
   switch (stage) {
     case 0: {
       KTimer t(ctx, GF_K_JOIN_BUCKET);
-      hipLaunchKernelGGL(join_orow_hist_kernel, dim3(blocks), dim3(kBlock), 0, s, a, a.row_mat);
+      hipLaunchKernelGGL(join_orow_hist_kernel, dim3(blocks), dim3(kScatThreads), 0, s, a, a.row_mat);
       break;
     }
     case 1: {
       KTimer t(ctx, GF_K_JOIN_BUCKET);
-      hipLaunchKernelGGL(join_orow_scatter_kernel, dim3(blocks), dim3(kBlock), 0, s, a, a.row_mat_scan);
+      hipLaunchKernelGGL(join_orow_scatter_kernel, dim3(blocks), dim3(kScatThreads), join_scatter_lds_bytes(a.qn), s,
+                         a, a.row_mat_scan);
       break;
     }
     case 2:  // blocks = the bucketing grid size

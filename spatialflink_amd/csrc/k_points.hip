@@ -233,7 +233,8 @@ hipError_t launch_histogram(hipStream_t s, const uint32_t* keys, int64_t n, uint
 }
 
 // ---------------------------------------------------------------------------------------
-// Exclusive scan of uint32 (reduce-then-scan, 3 launches).  Tile = 1024 threads x 4 items.
+// Exclusive scan of uint32 with the total at out[L] (reduce-then-scan, 3 launches; one
+// single-block launch up to 8 tiles).  Tile = 1024 threads x 4 items.
 // Wave-level inclusive scans with __shfl_up (64 lanes), wave totals through LDS.
 // ---------------------------------------------------------------------------------------
 constexpr int kScanThreads = 1024;
@@ -312,25 +313,47 @@ __global__ __launch_bounds__(kScanThreads) void scan_apply_kernel(const uint32_t
   for (int j = 0; j < kScanItems; ++j) {
     if (base + j < L) out[base + j] = run;
     run += v[j];
+    if (base + j == L - 1) out[L] = run;  // the total
   }
 }
 
-__global__ void scan_total_kernel(const uint32_t* __restrict__ in, int64_t L, uint32_t* __restrict__ out) {
-  // out[L] = out[L-1] + in[L-1]
-  if (L > 0) out[L] = out[L - 1] + in[L - 1];
-  else out[0] = 0u;
+// single block, any L: the tiles in sequence with a carried prefix, the total at out[L] -- one
+// launch where the 3-kernel scan is launch-bound (row / task counts of a few thousand)
+__global__ __launch_bounds__(kScanThreads) void scan_small_kernel(const uint32_t* __restrict__ in, int64_t L,
+                                                                  uint32_t* __restrict__ out) {
+  uint32_t carry = 0;
+  for (int64_t b = 0; b < L; b += kScanTile) {
+    const int64_t base = b + (int64_t)threadIdx.x * kScanItems;
+    uint32_t v[kScanItems];
+    uint32_t s = 0;
+#pragma unroll
+    for (int j = 0; j < kScanItems; ++j) {
+      v[j] = base + j < L ? in[base + j] : 0u;
+      s += v[j];
+    }
+    uint32_t total;
+    uint32_t run = carry + block_excl_scan(s, &total);
+#pragma unroll
+    for (int j = 0; j < kScanItems; ++j) {
+      if (base + j < L) out[base + j] = run;
+      run += v[j];
+    }
+    carry += total;
+  }
+  if (threadIdx.x == 0) out[L] = carry;
 }
 
 size_t scan_tmp_elems(int64_t L) { return (size_t)((L + kScanTile - 1) / kScanTile + 1); }
 
 hipError_t launch_exclusive_scan(hipStream_t s, const uint32_t* in, int64_t L, uint32_t* out, uint32_t* tmp) {
   const int64_t nt = (L + kScanTile - 1) / kScanTile;
-  if (nt > 0) {
-    hipLaunchKernelGGL(scan_reduce_kernel, dim3((unsigned)nt), dim3(kScanThreads), 0, s, in, L, tmp);
-    hipLaunchKernelGGL(scan_sums_kernel, dim3(1), dim3(kScanThreads), 0, s, tmp, nt);
-    hipLaunchKernelGGL(scan_apply_kernel, dim3((unsigned)nt), dim3(kScanThreads), 0, s, in, L, tmp, out);
+  if (nt <= 8) {
+    hipLaunchKernelGGL(scan_small_kernel, dim3(1), dim3(kScanThreads), 0, s, in, L, out);
+    return hipGetLastError();
   }
-  hipLaunchKernelGGL(scan_total_kernel, dim3(1), dim3(1), 0, s, in, L, out);
+  hipLaunchKernelGGL(scan_reduce_kernel, dim3((unsigned)nt), dim3(kScanThreads), 0, s, in, L, tmp);
+  hipLaunchKernelGGL(scan_sums_kernel, dim3(1), dim3(kScanThreads), 0, s, tmp, nt);
+  hipLaunchKernelGGL(scan_apply_kernel, dim3((unsigned)nt), dim3(kScanThreads), 0, s, in, L, tmp, out);
   return hipGetLastError();
 }
 
