@@ -246,15 +246,26 @@ __global__ __launch_bounds__(kScatThreads) void join_orow_scatter_kernel(JoinRow
   }
   __syncthreads();
   const int per = (qn + kScatThreads - 1) / kScatThreads, r0 = threadIdx.x * per;
+  // the next tile's coordinates are loaded while this tile goes through its LDS phases
+  double xn[kScatPer], yn[kScatPer];
+  auto load_tile = [&](int64_t t0) {
+#pragma unroll
+    for (int u = 0; u < kScatPer; ++u) {
+      const int64_t i = t0 + threadIdx.x + u * kScatThreads;
+      xn[u] = i < end ? __builtin_nontemporal_load(a.ox + i) : 0.0;
+      yn[u] = i < end ? __builtin_nontemporal_load(a.oy + i) : 0.0;
+    }
+  };
+  load_tile(beg);
   for (int64_t t0 = beg; t0 < end; t0 += kScatTile) {
     double x[kScatPer], y[kScatPer];
     int32_t row[kScatPer];
 #pragma unroll
     for (int u = 0; u < kScatPer; ++u) {
-      const int64_t i = t0 + threadIdx.x + u * kScatThreads;
-      x[u] = i < end ? __builtin_nontemporal_load(a.ox + i) : 0.0;
-      y[u] = i < end ? __builtin_nontemporal_load(a.oy + i) : 0.0;
+      x[u] = xn[u];
+      y[u] = yn[u];
     }
+    if (t0 + kScatTile < end) load_tile(t0 + kScatTile);
 #pragma unroll
     for (int u = 0; u < kScatPer; ++u) {
       const int64_t i = t0 + threadIdx.x + u * kScatThreads;

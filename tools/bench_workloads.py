@@ -370,13 +370,17 @@ def bench_join(args):
                             "replicated to string keys, hash join on gridID, distance per co-located pair), "
                             "C restatement, 1 thread")
     wl = f"join_pp_{no // 1_000_000}Mx{nq / 1e6:g}M_r{r}_grid1000" + (f"_per_gpu_x{world}" if world > 1 else "")
+    # roofline over the WHOLE window (every join kernel: both bucketings, probe, packing): the
+    # algorithmic bytes are the two sides' xy read once and the pairs written once
     _line("point-point join", world * (no + nq) * args.steps / elapsed, "points/s", args.steps, args.warmup, elapsed,
-          "join_row_probe (single pass: row-bucketed ordinary xy + idx in, pairs out)", 20.0 * no + 8.0 * pp, avg,
+          "window (query + ordinary row bucketing, join_row_probe, packing): xy of both sides in once, pairs out once",
+          16.0 * (no + nq_rank) + 8.0 * pp, elapsed / args.steps,
           {"n_gpus": world,
            "config": {"workload": wl, "ordinary": no * world, "query": nq * world, "radius": r,
                       "pairs_per_window": pp_all, "query_per_rank_with_halo": nq_rank,
                       "parallelism": f"cell-column shards x{world}, query halo c columns (no collective)"},
            "breakdown": {"probe_us_per_launch": round(avg * 1e6, 2), "probe_launches_per_window": cnt / args.steps,
+                         "probe_GBps_row_bucketed_in_pairs_out": round((20.0 * no + 8.0 * pp) / avg / 1e9, 1) if avg > 0 else None,
                          "bucket_us_per_launch": round(bms * 1000.0 / max(bcnt, 1), 2),
                          "bucket_launches_per_window": bcnt / args.steps},
            "pairs_per_s": round(pp_all * args.steps / elapsed, 1), "verified_vs_oracle": verified,
