@@ -121,6 +121,8 @@ def main():
                     help="CPU baseline budget, split over its three lines (rank 0, N=1)")
     ap.add_argument("--cpu-sample", type=int, default=1_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--clustered", action="store_true",
+                    help="BASELINE.md section 3 clustered variant: 80%% of the points in 8 Gaussian hot spots (sigma 0.01)")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--windows", type=int, default=4, help="distinct resident windows cycled through")
     ap.add_argument("--timing-period", type=int, default=5,
@@ -134,11 +136,12 @@ def main():
                     help="windows in flight: 2 overlaps window i's select with window i+1's scan; 3 also "
                          "overlaps consecutive windows' launches on two streams")
     args = ap.parse_args()
-    if args.workload != "knn":
-        sys.path.insert(0, os.path.join(ROOT, "tools"))
-        import bench_workloads
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import bench_workloads as W
 
-        bench_workloads.run(args)
+    W.CLUSTERED = args.clustered
+    if args.workload != "knn":
+        W.run(args)
         return
     if args.points is None:
         args.points = 10_000_000
@@ -176,7 +179,7 @@ def main():
     t = time.perf_counter()
     wins, host_windows = [], []
     for j in range(args.windows):
-        x, y = sf.synthetic_uniform(42 + 1000 * rank + j, n, xlo, xhi, BEIJING[2], BEIJING[3])
+        x, y = W.gen_points(sf, 42 + 1000 * rank + j, n, xlo, xhi)
         obj = np.arange(rank * n, (rank + 1) * n, dtype=np.int64)
         wins.append(sf.PointWindow.from_numpy(x, y, obj, device=dev.index))
         host_windows.append((x, y, obj))
@@ -299,37 +302,78 @@ def main():
         breakdown[tag + "window_us"] = round(1e6 * (time.perf_counter() - t) / 20, 2)
     _lib.check(_lib.lib().gf_knn_plan_set_hint(plan, 1), ctx.handle, "hint")
 
-    # host-buffer boundary (never part of `value`): a window handed over in host memory
-    # (x, y, objID, ts = 32 B/point) is uploaded with gf_window_upload, then evaluated
+    # host-buffer boundary (never part of `value`): windows handed over in host memory.  kNN
+    # reads x, y, objID (24 B/point; ts is never uploaded).  Single-upload times (pinned and
+    # pageable), then the host-resident pipeline: NH distinct pinned host windows streamed
+    # through two gf_windows -- upload(i+1) on the window's copy stream overlaps evaluate(i)
     pcie = None
     if rank == 0 and world == 1:
-        x0, y0, o0 = host_windows[0]
-        ts0 = np.arange(n, dtype=np.int64)
-        hw = ctypes.c_void_p()
-        _lib.check(L.gf_window_create(ctx.handle, n, ctypes.byref(hw)), ctx.handle, "window")
-        pin = ctypes.c_void_p()
-        _lib.check(L.gf_pinned_alloc(32 * n, ctypes.byref(pin)), None, "pinned")
-        pv = np.ctypeslib.as_array((ctypes.c_uint8 * (32 * n)).from_address(pin.value))
-        for j, a in enumerate((x0, y0, o0, ts0)):
-            pv[8 * n * j: 8 * n * (j + 1)] = a.view(np.uint8)
+        bpp = 24
+        NH = 3
+        pins, hws = [], []
+        for j in range(NH):
+            pin = ctypes.c_void_p()
+            _lib.check(L.gf_pinned_alloc(bpp * n, ctypes.byref(pin)), None, "pinned")
+            pv = np.ctypeslib.as_array((ctypes.c_uint8 * (bpp * n)).from_address(pin.value))
+            for c_, a_ in enumerate(host_windows[j % args.windows]):
+                pv[8 * n * c_: 8 * n * (c_ + 1)] = a_.view(np.uint8)
+            pins.append(pin)
+        for _ in range(2):
+            hw = ctypes.c_void_p()
+            _lib.check(L.gf_window_create(ctx.handle, n, ctypes.byref(hw)), ctx.handle, "window")
+            hws.append(hw)
+        cols = lambda j: [pins[j].value + 8 * n * c_ for c_ in range(3)] + [None]  # noqa: E731
         res = {}
-        for tag, ptrs in (("pageable", [a.ctypes.data for a in (x0, y0, o0, ts0)]),
-                          ("pinned", [pin.value + 8 * n * j for j in range(4)])):
+        x0, y0, o0 = host_windows[0]
+        for tag, ptrs in (("pageable", [x0.ctypes.data, y0.ctypes.data, o0.ctypes.data, None]), ("pinned", cols(0))):
             best = 1e9
             for _ in range(3):
                 torch.cuda.synchronize()
                 t = time.perf_counter()
-                _lib.check(L.gf_window_upload(hw, *ptrs, n), ctx.handle, "upload")
+                _lib.check(L.gf_window_upload(hws[0], *ptrs, n), ctx.handle, "upload")
+                gp = _lib.GfPoints()
+                _lib.check(L.gf_window_points(hws[0], ctypes.byref(gp)), ctx.handle, "points")
                 torch.cuda.synchronize()
                 best = min(best, time.perf_counter() - t)
             res[tag] = best
-        L.gf_window_destroy(hw)
-        L.gf_pinned_free(pin)
+
+        def host_pipeline(steps):
+            _lib.check(L.gf_window_upload(hws[0], *cols(0), n), ctx.handle, "upload")
+            for i in range(steps):
+                if i + 1 < steps:  # next window's copy, behind everything enqueued so far
+                    _lib.check(L.gf_window_upload(hws[(i + 1) % 2], *cols((i + 1) % NH), n), ctx.handle, "upload")
+                gp = _lib.GfPoints()
+                _lib.check(L.gf_window_points(hws[i % 2], ctypes.byref(gp)), ctx.handle, "points")
+                _lib.check(enqueue(plan, ctypes.byref(gp), slots[0, i % B].data_ptr()), ctx.handle, "enqueue")
+            _lib.check(L.gf_knn_plan_flush(plan), ctx.handle, "flush")
+
+        host_pipeline(4)
+        torch.cuda.synchronize()
+        hsteps = 12
+        t = time.perf_counter()
+        host_pipeline(hsteps)
+        torch.cuda.synchronize()
+        hpipe = (time.perf_counter() - t) / hsteps
+        # the pipeline's last records == the device-resident results of the same windows
+        for i in range(max(0, hsteps - B), hsteps):
+            st_, o_, d_, _ = sf.spatialOperators.decode_knn_record(slots[0, i % B].cpu().numpy().tobytes(), args.k)
+            ref = per_window.get((i % NH) % args.windows) if (i % NH) < args.windows else None
+            if ref is not None:
+                assert st_ == 0 and np.array_equal(ref[0], o_) and np.array_equal(ref[1], d_), "host-resident mismatch"
+        for hw in hws:
+            L.gf_window_destroy(hw)
+        for pin in pins:
+            L.gf_pinned_free(pin)
         wnd = breakdown.get("window_us", 0.0) * 1e-6
-        pcie = {"bytes_per_window": 32 * n, "upload_pinned_ms": round(1e3 * res["pinned"], 3),
+        pcie = {"bytes_per_window": bpp * n, "columns": "x, y, objID (ts not uploaded)",
+                "upload_pinned_ms": round(1e3 * res["pinned"], 3),
                 "upload_pageable_ms": round(1e3 * res["pageable"], 3),
-                "upload_pinned_GBps": round(32 * n / res["pinned"] / 1e9, 1),
-                "pcie_inclusive_points_per_s": round(n / (res["pinned"] + wnd), 1)}
+                "upload_pinned_GBps": round(bpp * n / res["pinned"] / 1e9, 1),
+                "serial_upload_then_evaluate_points_per_s": round(n / (res["pinned"] + wnd), 1),
+                "host_resident_pipelined_points_per_s": round(n / hpipe, 1),
+                "host_resident_pipelined_ms_per_window": round(1e3 * hpipe, 3),
+                "host_resident_note": (f"{NH} distinct pinned host windows streamed through 2 device windows: "
+                                       "upload(i+1) on the window's copy stream overlaps evaluate(i); PCIe-bound")}
 
     verified = None
     cpu = None
@@ -388,10 +432,11 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": (f"synthetic: java.util.Random-compatible uniform points, Beijing bounds, {args.windows} distinct "
+            "data": (W.data_desc().replace(", device-resident", "") + f", {args.windows} distinct "
                      "device-resident windows cycled (continuous query)"),
             "config": {
-                "workload": f"knn_k{args.k}_r{args.radius}_{n // 1_000_000}Mpts_per_gpu_grid{args.grid}x{args.grid}",
+                "workload": f"knn_k{args.k}_r{args.radius}_{n // 1_000_000}Mpts_per_gpu_grid{args.grid}x{args.grid}"
+                            + ("_clustered" if args.clustered else ""),
                 "points_per_window": pts_per_step,
                 "points_per_gpu": n,
                 "k": args.k,

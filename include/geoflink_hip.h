@@ -389,7 +389,16 @@ void gf_pinned_free(void* ptr);
 
 /* ---- host windows -------------------------------------------------------------------- */
 typedef struct gf_window gf_window;
-/* Library-owned device SoA window with pinned staging; upload is async on the ctx stream. */
+/* Library-owned device SoA window (reused across windows: create once per plan / operator).
+ * gf_window_upload copies on the window's own stream, after the work already enqueued on the
+ * context (which may still read the old contents) and without blocking work enqueued later:
+ * with two windows, upload(i+1) overlaps the evaluation of window i.  Pass NULL for columns
+ * the query does not read (range / join: x, y = 16 B per point; kNN: x, y, objID; ts is never
+ * read by window evaluation).  Host buffers from gf_pinned_alloc copy asynchronously at PCIe
+ * rate; pageable ones are staged by the runtime.
+ * gf_window_points MUST be called after each upload and before the evaluation that reads the
+ * window: it orders the context's streams after the copy.  Columns not uploaded come back
+ * NULL (a kNN plan then reports GF_ERR_ARG). */
 int  gf_window_create(gf_ctx* ctx, int64_t capacity, gf_window** out);
 void gf_window_destroy(gf_window* w);
 int  gf_window_upload(gf_window* w, const double* x, const double* y, const int64_t* objID,

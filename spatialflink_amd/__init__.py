@@ -12,7 +12,8 @@ from .spatialObjects import ObjIdDict, Point, PointWindow, Polygon, PolygonSet
 from .spatialOperators import (KNNResult, PinnedRecords, PointPointJoinQuery, PointPointKNNQuery, PointPointRangeQuery,
                                PointPolygonJoinQuery, PointPolygonKNNQuery,
                                PointPolygonRangeQuery, QueryConfiguration, QueryType, RangeResult, assign_cells,
-                               bucket_by_cell, knn_merge_host, synthetic_uniform)
+                               bucket_by_cell, knn_merge_host, synthetic_uniform,
+                               synthetic_clustered)
 from .spatialStreams import Deserialization
 from .windows import SlidingKNNQuery, SlidingRangeQuery, SlidingWindows
 
@@ -20,6 +21,6 @@ __all__ = [
     "SlidingWindows", "SlidingKNNQuery", "SlidingRangeQuery", "Deserialization", "PointPolygonKNNQuery", "PointPolygonJoinQuery",
     "UniformGrid", "ObjIdDict", "Point", "Polygon", "PolygonSet", "PointWindow", "QueryType", "QueryConfiguration",
     "PointPointRangeQuery", "PointPolygonRangeQuery", "PointPointKNNQuery", "PointPointJoinQuery", "RangeResult",
-    "KNNResult", "PinnedRecords", "knn_merge_host", "assign_cells", "bucket_by_cell", "synthetic_uniform", "generateCellIDStr",
+    "KNNResult", "PinnedRecords", "knn_merge_host", "assign_cells", "bucket_by_cell", "synthetic_uniform", "synthetic_clustered", "generateCellIDStr",
     "getIntCellIndices", "padLeadingZeroesToInt",
 ]

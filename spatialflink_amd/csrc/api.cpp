@@ -1671,7 +1671,9 @@ extern "C" int gf_join_pp(gf_ctx* ctx, const gf_grid* ugrid, const gf_grid* qgri
   const double ppp = ctx->join_ppp > 0 ? ctx->join_ppp : 1.0;
   int64_t tcap = (int64_t)std::ceil(1.25 * ppp * kJoinTask) + 2 * kJoinThreads;
   tcap = std::max<int64_t>(tcap, kJoinTask);
-  tcap = std::min<int64_t>(tcap, std::max<int64_t>(kJoinTask, ((int64_t)1 << 31) / 8 / std::max<int64_t>(max_tasks, 1)));
+  // regions of all tasks <= 8 GiB (1G pairs: their u32 offsets cannot wrap); denser windows spill
+  // to the overflow run
+  tcap = std::min<int64_t>(tcap, std::max<int64_t>(kJoinTask, ((int64_t)1 << 33) / 8 / std::max<int64_t>(max_tasks, 1)));
   size_t o_tpairs = ar.take<uint64_t>(rowpath ? max_tasks * tcap : 1), o_tcnt = ar.take<uint32_t>(rowpath ? max_tasks : 1);
   size_t o_tkoff = ar.take<uint32_t>(rowpath ? max_tasks + 1 : 1);
   size_t o_btmp = ar.take<uint32_t>(std::max({scan_tmp_elems(mat), scan_tmp_elems(qn), scan_tmp_elems(max_tasks)}));
@@ -1796,9 +1798,13 @@ extern "C" int gf_window_create(gf_ctx* ctx, int64_t capacity, gf_window** out) 
   w->capacity = capacity;
   const size_t n = (size_t)std::max<int64_t>(capacity, 1);
   if (hipMalloc(&w->x, 8 * n) != hipSuccess || hipMalloc(&w->y, 8 * n) != hipSuccess ||
-      hipMalloc(&w->objID, 8 * n) != hipSuccess || hipMalloc(&w->ts, 8 * n) != hipSuccess) {
+      hipMalloc(&w->objID, 8 * n) != hipSuccess || hipMalloc(&w->ts, 8 * n) != hipSuccess ||
+      hipStreamCreateWithFlags(&w->copy, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&w->ready, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&w->fence_main, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&w->fence_aux, hipEventDisableTiming) != hipSuccess) {
     gf_window_destroy(w);
-    return set_err(ctx, GF_ERR_NOMEM, "gf_window_create: hipMalloc failed");
+    return set_err(ctx, GF_ERR_NOMEM, "gf_window_create: device allocation failed");
   }
   *out = w;
   return GF_OK;
@@ -1807,11 +1813,17 @@ extern "C" int gf_window_create(gf_ctx* ctx, int64_t capacity, gf_window** out) 
 extern "C" void gf_window_destroy(gf_window* w) {
   if (!w) return;
   hipSetDevice(w->ctx->device);
+  if (w->copy) hipStreamSynchronize(w->copy);
   hipStreamSynchronize(w->ctx->stream);
+  if (w->ctx->aux) hipStreamSynchronize(w->ctx->aux);
   if (w->x) hipFree(w->x);
   if (w->y) hipFree(w->y);
   if (w->objID) hipFree(w->objID);
   if (w->ts) hipFree(w->ts);
+  if (w->ready) hipEventDestroy(w->ready);
+  if (w->fence_main) hipEventDestroy(w->fence_main);
+  if (w->fence_aux) hipEventDestroy(w->fence_aux);
+  if (w->copy) hipStreamDestroy(w->copy);
   delete w;
 }
 
@@ -1821,20 +1833,42 @@ extern "C" int gf_window_upload(gf_window* w, const double* x, const double* y, 
   gf_ctx* ctx = w->ctx;
   int st = bind(ctx);
   if (st) return st;
-  const size_t b = 8 * (size_t)n;
-  if (n) {
-    GF_HIP_CHECK(ctx, hipMemcpyAsync(w->x, x, b, hipMemcpyHostToDevice, ctx->stream));
-    GF_HIP_CHECK(ctx, hipMemcpyAsync(w->y, y, b, hipMemcpyHostToDevice, ctx->stream));
-    if (objID) GF_HIP_CHECK(ctx, hipMemcpyAsync(w->objID, objID, b, hipMemcpyHostToDevice, ctx->stream));
-    if (ts) GF_HIP_CHECK(ctx, hipMemcpyAsync(w->ts, ts, b, hipMemcpyHostToDevice, ctx->stream));
+  // the copy waits for everything already enqueued on the context (evaluations of the old
+  // contents), not for what is enqueued after this call
+  GF_HIP_CHECK(ctx, hipEventRecord(w->fence_main, ctx->stream));
+  GF_HIP_CHECK(ctx, hipStreamWaitEvent(w->copy, w->fence_main, 0));
+  if (ctx->aux) {
+    GF_HIP_CHECK(ctx, hipEventRecord(w->fence_aux, ctx->aux));
+    GF_HIP_CHECK(ctx, hipStreamWaitEvent(w->copy, w->fence_aux, 0));
   }
+  const size_t b = 8 * (size_t)n;
+  if (n) {  // only the columns given: range / join read x, y (16 B per point), kNN adds objID
+    GF_HIP_CHECK(ctx, hipMemcpyAsync(w->x, x, b, hipMemcpyHostToDevice, w->copy));
+    GF_HIP_CHECK(ctx, hipMemcpyAsync(w->y, y, b, hipMemcpyHostToDevice, w->copy));
+    if (objID) GF_HIP_CHECK(ctx, hipMemcpyAsync(w->objID, objID, b, hipMemcpyHostToDevice, w->copy));
+    if (ts) GF_HIP_CHECK(ctx, hipMemcpyAsync(w->ts, ts, b, hipMemcpyHostToDevice, w->copy));
+  }
+  GF_HIP_CHECK(ctx, hipEventRecord(w->ready, w->copy));
+  w->has_objid = objID != nullptr;
+  w->has_ts = ts != nullptr;
+  w->pending = true;
   w->n = n;
-  return gf_ctx_fork(ctx);  // a depth-3 plan may read the window from the second stream
+  return GF_OK;
 }
 
 extern "C" int gf_window_points(gf_window* w, gf_points* out) {
   if (!w || !out) return GF_ERR_ARG;
-  out->x = w->x; out->y = w->y; out->objID = w->objID; out->ts = w->ts; out->n = w->n;
+  if (w->pending) {  // work enqueued on the context from here on sees the uploaded contents
+    gf_ctx* ctx = w->ctx;
+    int st = bind(ctx);
+    if (st) return st;
+    GF_HIP_CHECK(ctx, hipStreamWaitEvent(ctx->stream, w->ready, 0));
+    if ((st = gf_ctx_fork(ctx))) return st;  // a depth-3 plan may read the window from the second stream
+    w->pending = false;
+  }
+  out->x = w->x; out->y = w->y; out->n = w->n;
+  out->objID = w->has_objid ? w->objID : nullptr;
+  out->ts = w->has_ts ? w->ts : nullptr;
   return GF_OK;
 }
 

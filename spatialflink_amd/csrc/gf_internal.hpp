@@ -653,4 +653,11 @@ struct gf_window {
   double* y = nullptr;
   int64_t* objID = nullptr;
   int64_t* ts = nullptr;
+  bool has_objid = false, has_ts = false;  // columns of the last upload
+  // uploads run on the window's own copy stream: they wait for the work already enqueued on
+  // the context's streams (which may still read the previous contents), and gf_window_points
+  // makes the context's streams wait for the copy -- so upload(i+1) overlaps evaluate(i)
+  hipStream_t copy = nullptr;
+  hipEvent_t ready = nullptr, fence_main = nullptr, fence_aux = nullptr;
+  bool pending = false;
 };

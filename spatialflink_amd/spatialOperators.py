@@ -556,8 +556,37 @@ def synthetic_uniform(seed: int, n: int, minX: float, maxX: float, minY: float, 
     return x, y
 
 
+def synthetic_clustered(seed: int, n: int, minX: float, maxX: float, minY: float, maxY: float, centers=None,
+                        n_centers: int = 8, sigma: float = 0.01, frac: float = 0.8):
+    """The clustered variant of the synthetic source: a fraction `frac`
+    of the points from Gaussian hot spots N(centre, sigma^2) (sigma in degrees), the rest
+    uniform; `centers` (list of (x, y)) come first, the remaining of `n_centers` are uniform in
+    the bounds.  Points falling outside the bounds are drawn again, so every point is inside.
+    numpy PCG64(seed): deterministic, host-side (input generation, not the evaluated path)."""
+    rng = np.random.default_rng(seed)
+    cs = [tuple(c) for c in (centers or [])][:n_centers]
+    while len(cs) < n_centers:
+        cs.append((rng.uniform(minX, maxX), rng.uniform(minY, maxY)))
+    cx = np.array([c[0] for c in cs], np.float64)
+    cy = np.array([c[1] for c in cs], np.float64)
+    x = np.empty(n, np.float64)
+    y = np.empty(n, np.float64)
+    todo = np.arange(n)
+    while len(todo):
+        m = len(todo)
+        hot = rng.random(m) < frac
+        k = rng.integers(0, len(cs), m)
+        xv = np.where(hot, cx[k] + sigma * rng.standard_normal(m), rng.uniform(minX, maxX, m))
+        yv = np.where(hot, cy[k] + sigma * rng.standard_normal(m), rng.uniform(minY, maxY, m))
+        ok = (xv >= minX) & (xv < maxX) & (yv >= minY) & (yv < maxY)
+        x[todo[ok]] = xv[ok]
+        y[todo[ok]] = yv[ok]
+        todo = todo[~ok]
+    return x, y
+
+
 __all__ = [
-    "QueryType", "QueryConfiguration", "PointPointRangeQuery", "PointPolygonRangeQuery", "PointPointKNNQuery",
+    "synthetic_clustered", "QueryType", "QueryConfiguration", "PointPointRangeQuery", "PointPolygonRangeQuery", "PointPointKNNQuery",
     "PointPointJoinQuery", "PointPolygonJoinQuery", "RangeResult", "KNNResult", "knn_merge_host", "assign_cells", "bucket_by_cell",
     "synthetic_uniform", "Point", "Polygon", "PointWindow", "knn_record_bytes", "decode_knn_record",
 ]

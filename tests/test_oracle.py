@@ -237,3 +237,17 @@ def test_cpu_baselines_match(oracle_mod, r, k, dup):
         om = oracle_mod.knn_mt(og, x, y, obj, QPOINT[0], QPOINT[1], r, k, T, optimized=True)
         for a, b in zip(om, con):
             np.testing.assert_array_equal(a, b)
+
+
+def test_synthetic_clustered_deterministic_and_in_bounds():
+    import spatialflink_amd as sf
+
+    a = sf.synthetic_clustered(3, 50_000, *BEIJING, centers=[QPOINT])
+    b = sf.synthetic_clustered(3, 50_000, *BEIJING, centers=[QPOINT])
+    np.testing.assert_array_equal(a[0], b[0])
+    np.testing.assert_array_equal(a[1], b[1])
+    x, y = a
+    assert (x >= BEIJING[0]).all() and (x < BEIJING[1]).all() and (y >= BEIJING[2]).all() and (y < BEIJING[3]).all()
+    # 80% in 8 spots of sigma 0.01: the spot on the query point holds ~10% within 3 sigma
+    near = np.hypot(x - QPOINT[0], y - QPOINT[1]) < 0.03
+    assert 0.08 < near.mean() < 0.12

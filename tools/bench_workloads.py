@@ -90,11 +90,35 @@ def _band(sf, grid, grid_n, world, rank):
     return sharding.band_x_range(grid, lo, hi)
 
 
+# --clustered: the BASELINE.md section 3 variant -- 80% of the points in 8 Gaussian hot spots
+# (sigma 0.01 deg), the first on the query point, the other 7 fixed (the same for every window
+# and both join sides, so the hot spots of the two sides overlap)
+CLUSTERED = False
+
+
+def hot_spots():
+    r = np.random.default_rng(2024)
+    return [QPOINT] + [(r.uniform(BEIJING[0], BEIJING[1]), r.uniform(BEIJING[2], BEIJING[3])) for _ in range(7)]
+
+
+def gen_points(sf, seed, n, xlo, xhi):
+    if not CLUSTERED:
+        return sf.synthetic_uniform(seed, n, xlo, xhi, BEIJING[2], BEIJING[3])
+    cs = [c for c in hot_spots() if xlo <= c[0] < xhi] or None
+    return sf.synthetic_clustered(seed, n, xlo, xhi, BEIJING[2], BEIJING[3], centers=cs, n_centers=len(cs or [0]) or 1)
+
+
+def data_desc():
+    return ("synthetic: clustered -- 80% in 8 Gaussian hot spots (sigma 0.01 deg, one on the query point), 20% "
+            "uniform, Beijing bounds, device-resident" if CLUSTERED else
+            "synthetic: java.util.Random-compatible uniform points, Beijing bounds, device-resident")
+
+
 def _windows(sf, n, count, seed0, dev=0, xr=None):
     wins = []
     xlo, xhi = xr or (BEIJING[0], BEIJING[1])
     for j in range(count):
-        x, y = sf.synthetic_uniform(seed0 + j, n, xlo, xhi, BEIJING[2], BEIJING[3])
+        x, y = gen_points(sf, seed0 + j, n, xlo, xhi)
         wins.append((x, y, sf.PointWindow.from_numpy(x, y, np.arange(n, dtype=np.int64), device=dev)))
     return wins
 
@@ -106,7 +130,7 @@ def _line(workload, value, unit, steps, warmup, elapsed, kernel, bytes_per_launc
     d = {"metric": f"points/sec per window ({workload})", "value": round(value, 1), "unit": unit, "n_gpus": 1,
          "steps": steps, "warmup": warmup, "ms_per_step": round(1000.0 * elapsed / steps, 4),
          "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
-         "data": "synthetic: java.util.Random-compatible uniform points, Beijing bounds, device-resident",
+         "data": data_desc(),
          "roofline": {"bound": "hbm", "kernel": kernel, "achieved": round(achieved, 1) if achieved else None,
                       "peak": HBM_PEAK_GBS, "unit": "GB/s",
                       "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
@@ -305,7 +329,7 @@ def bench_join(args):
         c = int(np.ceil(r / grid.getCellLength()))
         qw = []
         for j in range(2):
-            x, y = sf.synthetic_uniform(21 + j, nq * world, *BEIJING)
+            x, y = gen_points(sf, 21 + j, nq * world, BEIJING[0], BEIJING[1])
             keep = sharding.join_query_halo(np.floor((x - BEIJING[0]) / grid.getCellLength()), band, c)
             xs, ys = np.ascontiguousarray(x[keep]), np.ascontiguousarray(y[keep])
             qw.append((xs, ys, sf.PointWindow.from_numpy(xs, ys, np.flatnonzero(keep).astype(np.int64), device=dev)))
@@ -320,6 +344,19 @@ def bench_join(args):
         _lib.check(L.gf_join_pp(ctx.handle, C.byref(grid.c_grid), C.byref(grid.c_grid), C.byref(po[i % 2]),
                                 C.byref(pq[i % 2]), r, 0, 0, pairs.data_ptr(), cap, C.byref(npairs)),
                    ctx.handle, "gf_join_pp")
+
+    # output capacity: sized from a counting call on each window (clustered inputs produce
+    # hundreds of pairs per point in the hot spots), outside the timed region
+    for i in range(2):
+        st = L.gf_join_pp(ctx.handle, C.byref(grid.c_grid), C.byref(grid.c_grid), C.byref(po[i]), C.byref(pq[i]), r,
+                          0, 0, None, 0, C.byref(npairs))
+        if st not in (0, _lib.GF_ERR_CAPACITY):
+            _lib.check(st, ctx.handle, "gf_join_pp (count)")
+        if npairs.value > cap:
+            cap = int(1.05 * npairs.value) + 1024
+    if 2 * cap > pairs.numel():
+        del pairs
+        pairs = torch.empty(2 * cap, dtype=torch.int32, device=dev)
 
     for i in range(args.warmup):
         step(i)
@@ -369,7 +406,8 @@ def bench_join(args):
                             f"query points, 1 pass ({tc:.2f}s): oracle's reference-shaped join (query points "
                             "replicated to string keys, hash join on gridID, distance per co-located pair), "
                             "C restatement, 1 thread")
-    wl = f"join_pp_{no // 1_000_000}Mx{nq / 1e6:g}M_r{r}_grid1000" + (f"_per_gpu_x{world}" if world > 1 else "")
+    wl = f"join_pp_{no // 1_000_000}Mx{nq / 1e6:g}M_r{r}_grid1000" + (f"_per_gpu_x{world}" if world > 1 else "") + (
+        "_clustered" if CLUSTERED else "")
     # roofline over the WHOLE window (every join kernel: both bucketings, probe, packing): the
     # algorithmic bytes are the two sides' xy read once and the pairs written once
     _line("point-point join", world * (no + nq) * args.steps / elapsed, "points/s", args.steps, args.warmup, elapsed,
