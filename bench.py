@@ -105,7 +105,7 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--points", type=int, default=None, help="points per window per GPU (kNN default 10M)")
-    ap.add_argument("--workload", default="knn", choices=("knn", "range", "ppoly", "join", "pjoin", "sliding", "csv", "polyknn", "bucket"),
+    ap.add_argument("--workload", default="knn", choices=("knn", "range", "ppoly", "join", "pjoin", "sliding", "csv", "geojson", "polyknn", "bucket"),
                     help="knn = the headline line (BASELINE configs[1]); range/ppoly/join/pjoin/sliding/csv/polyknn/"
                          "bucket: tools/bench_workloads.py")
     ap.add_argument("--range-blocks", default="0", help="range/ppoly scan blocks, comma list = sweep (0 = auto)")

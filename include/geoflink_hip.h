@@ -83,7 +83,8 @@ typedef struct {
  * Equal keys <=> equal Strings (keys of one dictionary).  The kNN contract's ties are broken by
  * key, so dictionary Strings order before numeric ones. */
 #define GF_OBJID_NUMERIC_MIN (-(INT64_C(1) << 62))  /* keys below: dictionary Strings */
-#define GF_OBJID_NUMERIC_END (INT64_C(1) << 62)     /* keys at or above: never produced */
+#define GF_OBJID_NUMERIC_END (INT64_C(1) << 62)     /* keys at or above: only GF_OBJID_NULL */
+#define GF_OBJID_NULL INT64_MAX  /* a null objID (GeoJSON feature without the objID property) */
 typedef struct gf_objid_dict gf_objid_dict;
 
 /* One window of points as device SoA -- Point(objID, x, y, ts, uGrid), Point.java:91-100 */
@@ -355,6 +356,33 @@ int gf_csv_parse(gf_ctx* ctx, const char* text, int64_t len, const gf_csv_schema
 int gf_csv_parse_dict(gf_ctx* ctx, gf_objid_dict* dict, const char* text, int64_t len, const gf_csv_schema* schema,
                       const gf_grid* grid, double* x, double* y, int64_t* objID, int64_t* ts, int32_t* cx, int32_t* cy,
                       int64_t cap, int64_t* n_out, int64_t* bad_line, int32_t* bad_kind);
+
+/* ---- GeoJSON ingest ------------------------------------------------------------------
+ * Deserialization.GeoJSONToTSpatial(uGrid, dateFormat, propertyTimeStamp, propertyObjID).map
+ * (Deserialization.java:149-211) over a chunk of lines, one JSON object per line: the Kafka
+ * key/value record {"key":..,"value":{Feature}} (the object under "value" is the feature) or a
+ * bare Feature (Serialization.PointToGeoJSONOutputSchema's output).  Per line, in the reference's
+ * order: x, y = the geometry's first coordinate (geometry.getCoordinate(): "coordinates" of
+ * "geometry", first number pair, descending nested arrays); then from "properties" (absent or not
+ * an object: objID null, ts 0): ts from `time_property` -- date_format 0: Long.parseLong of the
+ * node's text (a JSON integer; anything else throws NumberFormatException: GF_CSV_NUMBER_FORMAT),
+ * date_format 1: the string value parsed as SimpleDateFormat("yyyy-MM-dd HH:mm:ss") (lenient
+ * field rollover) in a fixed UTC offset (tz_offset_minutes; DST not modelled), unparsable -> 0;
+ * objID from `objid_property` -- node.toString() without '"': a string's content, an integer's
+ * digits ("-0" -> "0"), true / false / null as text; absent -> GF_OBJID_NULL.  The last of
+ * duplicate keys wins (Jackson ObjectNode).  GF_CSV_UNSUPPORTED: strings with escapes where a
+ * value is taken, non-integer or structured objID values, years before 1583 (Julian calendar),
+ * property names longer than 63 bytes. */
+typedef struct {
+  const char* objid_property;   /* propertyObjID (host C string); NULL: objID always null */
+  const char* time_property;    /* propertyTimeStamp; NULL: ts always 0 */
+  int32_t date_format;          /* 0: integer milliseconds; 1: "yyyy-MM-dd HH:mm:ss" */
+  int32_t tz_offset_minutes;    /* date_format 1: offset of the reference JVM's default zone */
+} gf_geojson_schema;
+/* Same conventions as gf_csv_parse_dict (device text, outputs, capacity, first bad line). */
+int gf_geojson_parse(gf_ctx* ctx, gf_objid_dict* dict, const char* text, int64_t len, const gf_geojson_schema* schema,
+                     const gf_grid* grid, double* x, double* y, int64_t* objID, int64_t* ts, int32_t* cx,
+                     int32_t* cy, int64_t cap, int64_t* n_out, int64_t* bad_line, int32_t* bad_kind);
 
 /* ---- join (sync) --------------------------------------------------------------------
  * JoinQuery.getReplicatedPointQueryStream + PointPointJoinQuery.windowBased

@@ -305,6 +305,118 @@ def csv_parse(text: bytes, delim: str, want):
     return x, y, o, t, bl.value, bk.value
 
 
+# ---------------------------------------------------------------------------------------------
+# GeoJSON point ingest -- Deserialization.GeoJSONToTSpatial.map (Deserialization.java:149-211),
+# restated over Python's json module (a JSON parser independent of the device scanner):
+#   geometry = readGeoJSON(value) -- the geometry's first coordinate (:170-178, :203/:207);
+#   time: dateFormat null -> Long.parseLong(String.valueOf(node)) (:190; a non-integer node throws
+#         NumberFormatException), else dateFormat.parse(node.textValue()).getTime() (:187; a
+#         ParseException leaves time 0, :193);
+#   objID: node.toString().replaceAll("\"", "") (:197) -- a string's content, an integer's digits,
+#          true / false / null as text; absent properties / objID -> null.
+# Kinds as gf_geojson_parse: 1 NumberFormatException, 2 outside the restated subset (escaped
+# strings, non-integer objIDs, dates before 1583), 3 malformed / no coordinates, 4 empty line.
+# ---------------------------------------------------------------------------------------------
+def _jdate(v: str, tz_off_min: int):
+    import calendar
+    import re
+
+    m = re.match(r"(\d+)-(\d+)-(\d+) (\d+):(\d+):(\d+)", v)
+    if not m:
+        return 0, 0                       # ParseException: time stays 0
+    f = [int(g) for g in m.groups()]
+    if any(len(g) >= 10 for g in m.groups()):  # int overflow territory of the lenient calendar
+        return None, 2
+    y = f[0] + (f[1] - 1) // 12           # SimpleDateFormat is lenient: fields roll over
+    mo = (f[1] - 1) % 12 + 1
+    if y < 1 or y > 9999:
+        return None, 2
+    secs = calendar.timegm((y, mo, 1, 0, 0, 0)) + (f[2] - 1) * 86400 + f[3] * 3600 + f[4] * 60 + f[5]
+    if secs < -12219292800:               # before 1582-10-15: Java's Julian calendar
+        return None, 2
+    return secs * 1000 - tz_off_min * 60000, 0
+
+
+def _geojson_line(line: bytes, prop_obj, prop_ts, date_fmt, tz_off_min):
+    import json
+
+    if line.endswith(b"\r"):
+        line = line[:-1]
+    if not line:
+        return None, 4
+    try:
+        d = json.loads(line)
+    except ValueError:
+        return None, 3
+    if not isinstance(d, dict):
+        return None, 3
+    feat = d["value"] if isinstance(d.get("value"), dict) else d
+    geom = feat.get("geometry")
+    if not isinstance(geom, dict) or not isinstance(geom.get("coordinates"), list):
+        return None, 3
+    c = geom["coordinates"]
+    while c and isinstance(c[0], list):
+        c = c[0]
+    if len(c) < 2:
+        return None, 3
+    num = lambda v: isinstance(v, (int, float)) and not isinstance(v, bool)  # noqa: E731
+    if not (num(c[0]) and num(c[1])):
+        return None, 1
+    x, y = float(c[0]), float(c[1])
+    ts, obj = 0, None
+    props = feat.get("properties")
+    if isinstance(props, dict):
+        if prop_ts is not None and prop_ts in props:
+            v = props[prop_ts]
+            if date_fmt == 0:
+                if not (isinstance(v, int) and not isinstance(v, bool)) or not -(1 << 63) <= v < (1 << 63):
+                    return None, 1
+                ts = v
+            else:
+                if not isinstance(v, str):
+                    return None, 1
+                if b"\\" in line:
+                    return None, 2
+                t, k = _jdate(v, tz_off_min)
+                if k:
+                    return None, k
+                ts = t
+        if prop_obj is not None and prop_obj in props:
+            v = props[prop_obj]
+            if isinstance(v, bool):
+                obj = b"true" if v else b"false"
+            elif v is None:
+                obj = b"null"
+            elif isinstance(v, int):
+                obj = str(v).encode()
+            elif isinstance(v, str):
+                if b"\\" in line:
+                    return None, 2
+                obj = v.encode("utf-8", "surrogateescape")
+            else:
+                return None, 2
+    return (x, y, ts, obj), 0
+
+
+def geojson_parse(text: bytes, prop_obj=None, prop_ts=None, date_fmt=0, tz_off_min=0):
+    """GeoJSONToTSpatial.map per line -> (x, y, objID Strings as bytes or None, ts, bad_line,
+    bad_kind); bad lines contribute zeros."""
+    lines = text.split(b"\n")
+    if lines and lines[-1] == b"" and text.endswith(b"\n"):
+        lines = lines[:-1]
+    n = len(lines)
+    x = np.zeros(n); y = np.zeros(n); t = np.zeros(n, np.int64); o = [None] * n
+    bad_line, bad_kind = -1, 0
+    for i, ln in enumerate(lines):
+        r, k = _geojson_line(ln, prop_obj, prop_ts, date_fmt, tz_off_min)
+        if k:
+            if bad_line < 0:
+                bad_line, bad_kind = i, k
+            continue
+        x[i], y[i], t[i], o[i] = r
+    return x, y, o, t, bad_line, bad_kind
+
+
 def knn_ppoly(g, x, y, objID, P: "Polygons", r, k, approximate=False, metric=METRIC_SQRT):
     """PointPolygonKNNQuery (one query polygon) -> (n, objID, dist, idx), build contract."""
     x, y, objID = _f64(x), _f64(y), np.ascontiguousarray(objID, np.int64)

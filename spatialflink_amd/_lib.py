@@ -15,6 +15,7 @@ LIB_PATH = os.environ.get("GF_LIB_PATH") or os.path.join(_HERE, "libgeoflink_hip
 
 GF_OK = 0
 OBJID_NUMERIC_MIN, OBJID_NUMERIC_END = -(1 << 62), 1 << 62
+OBJID_NULL = (1 << 63) - 1  # GeoJSON feature without the objID property
 GF_MERGE_SHARD_MAJOR, GF_MERGE_WINDOW_MAJOR = 0, 1
 GF_ERR_ARG = -1
 GF_ERR_CAPACITY = -2
@@ -42,7 +43,7 @@ EXPORTS = [
     "gf_knn_result_bytes", "gf_knn_enqueue",
     "gf_knn_decode", "gf_knn_run", "gf_knn_merge_dev", "gf_knn_merge_dev_batch", "gf_knn_merge_host",
     "gf_knn_sliding_create", "gf_knn_sliding_destroy", "gf_knn_sliding_geometry", "gf_knn_sliding_push",
-    "gf_knn_sliding_flush", "gf_knn_sliding_decode", "gf_pane_bounds", "gf_csv_parse", "gf_csv_parse_dict",
+    "gf_knn_sliding_flush", "gf_knn_sliding_decode", "gf_pane_bounds", "gf_csv_parse", "gf_csv_parse_dict", "gf_geojson_parse",
     "gf_objid_dict_create", "gf_objid_dict_destroy", "gf_ctx_objid_dict", "gf_objid_dict_size", "gf_objid_intern",
     "gf_objid_decode", "gf_join_pp",
     "gf_join_ppoly_plan_create", "gf_join_ppoly_run", "gf_join_ppoly",
@@ -163,6 +164,8 @@ def lib():
             "gf_knn_sliding_decode": ([P, i64, P, P, P, P, pi32], C.c_int),
             "gf_pane_bounds": ([P, P, i64, i64, i64, i32, P], C.c_int),
             "gf_csv_parse": ([P, P, i64, P, C.POINTER(GfGrid), P, P, P, P, P, P, i64, pi64, pi64, pi32], C.c_int),
+            "gf_geojson_parse": ([P, P, P, i64, P, C.POINTER(GfGrid), P, P, P, P, P, P, i64, pi64, pi64, pi32],
+                                 C.c_int),
             "gf_csv_parse_dict": ([P, P, P, i64, P, C.POINTER(GfGrid), P, P, P, P, P, P, i64, pi64, pi64, pi32],
                                   C.c_int),
             "gf_objid_dict_create": ([P, C.POINTER(P)], C.c_int),

@@ -17,12 +17,12 @@ extern "C" int gf_csv_parse(gf_ctx* ctx, const char* text, int64_t len, const gf
   return gf_csv_parse_dict(ctx, nullptr, text, len, sc, g, x, y, objID, ts, cx, cy, cap, n_out, bad_line, bad_kind);
 }
 
-extern "C" int gf_csv_parse_dict(gf_ctx* ctx, gf_objid_dict* dict, const char* text, int64_t len,
-                                 const gf_csv_schema* sc, const gf_grid* g, double* x, double* y, int64_t* objID,
-                                 int64_t* ts, int32_t* cx, int32_t* cy, int64_t cap, int64_t* n_out, int64_t* bad_line,
-                                 int32_t* bad_kind) {
-  if (!ctx || !sc || !n_out || len < 0 || (len > 0 && !text) || !x || !y || !objID || !ts || (!cx) != (!cy) ||
-      (cx && !g) || sc->objid_field < 0 || sc->time_field < 0 || sc->x_field < 0 || sc->y_field < 0)
+// The line pipeline shared by the CSV/TSV and GeoJSON ingest: `proto` carries the format's
+// fields (delimiter + schema, or the GeoJSON properties); the rest is filled here.
+static int parse_text_lines(gf_ctx* ctx, gf_objid_dict* dict, const char* text, int64_t len, const CsvArgs& proto,
+                            const gf_grid* g, double* x, double* y, int64_t* objID, int64_t* ts, int32_t* cx,
+                            int32_t* cy, int64_t cap, int64_t* n_out, int64_t* bad_line, int32_t* bad_kind) {
+  if (!n_out || len < 0 || (len > 0 && !text) || !x || !y || !objID || !ts || (!cx) != (!cy) || (cx && !g))
     return set_err(ctx, GF_ERR_ARG, "gf_csv_parse: bad argument");
   if (g && !(g->n > 0 && g->cellLength > 0)) return set_err(ctx, GF_ERR_ARG, "gf_csv_parse: bad grid");
   if ((uintptr_t)text & 15) return set_err(ctx, GF_ERR_ALIGN, "gf_csv_parse: text must be 16-byte aligned");
@@ -78,10 +78,8 @@ extern "C" int gf_csv_parse_dict(gf_ctx* ctx, gf_objid_dict* dict, const char* t
   CsvErr* err = (CsvErr*)(base + o_err);
   GF_HIP_CHECK(ctx, hipMemsetAsync(err, 0xFF, sizeof(CsvErr), ctx->stream));
   GF_HIP_CHECK(ctx, launch_csv_index(ctx->stream, text, len, nseg, offs, nl));
-  CsvArgs a{};
+  CsvArgs a = proto;
   a.text = text; a.len = len; a.nl = nl; a.newlines = newlines; a.lines = lines;
-  a.delim = sc->delimiter;
-  a.want[0] = sc->objid_field; a.want[1] = sc->time_field; a.want[2] = sc->x_field; a.want[3] = sc->y_field;
   a.x = x; a.y = y; a.objID = objID; a.ts = ts; a.cx = cx; a.cy = cy;
   if (g) { a.minX = g->minX; a.minY = g->minY; a.cl = g->cellLength; }
   a.err = err;
@@ -99,11 +97,13 @@ extern "C" int gf_csv_parse_dict(gf_ctx* ctx, gf_objid_dict* dict, const char* t
   if (he.line != ~0ull) {
     if (bad_line) *bad_line = (int64_t)he.line;
     if (bad_kind) *bad_kind = he.kind;
-    static const char* what[] = {"ok", "NumberFormatException", "unsupported numeric literal (hexadecimal, or > 19 "
-                                 "significant digits at a rounding boundary)", "missing field (IndexOutOfBounds)",
+    static const char* what[] = {"ok", "NumberFormatException", "unsupported literal (hexadecimal, > 19 significant "
+                                 "digits at a rounding boundary, a JSON escape, a non-integer objID, a pre-1583 date)",
+                                 "missing field (IndexOutOfBounds / no geometry coordinates / malformed JSON)",
                                  "empty line"};
     const int k = he.kind >= 0 && he.kind <= 4 ? he.kind : 1;
-    return set_err(ctx, GF_ERR_ARG, "gf_csv_parse: line " + std::to_string(he.line) + ": " + what[k]);
+    return set_err(ctx, GF_ERR_ARG, std::string(proto.format == 1 ? "gf_geojson_parse" : "gf_csv_parse") + ": line " +
+                                        std::to_string(he.line) + ": " + what[k]);
   }
   // objID Strings that are not canonical decimals: keys from the dictionary (ids in line order)
   const uint32_t nw = (uint32_t)dn[0];
@@ -112,4 +112,42 @@ extern "C" int gf_csv_parse_dict(gf_ctx* ctx, gf_objid_dict* dict, const char* t
     if ((st = dict_run(dict, text, 1, nw, (uint64_t)lines, objID))) return st;
   }
   return GF_OK;
+}
+
+extern "C" int gf_csv_parse_dict(gf_ctx* ctx, gf_objid_dict* dict, const char* text, int64_t len,
+                                 const gf_csv_schema* sc, const gf_grid* g, double* x, double* y, int64_t* objID,
+                                 int64_t* ts, int32_t* cx, int32_t* cy, int64_t cap, int64_t* n_out, int64_t* bad_line,
+                                 int32_t* bad_kind) {
+  if (!ctx) return GF_ERR_ARG;
+  if (!sc || sc->objid_field < 0 || sc->time_field < 0 || sc->x_field < 0 || sc->y_field < 0)
+    return set_err(ctx, GF_ERR_ARG, "gf_csv_parse: bad schema");
+  CsvArgs a{};
+  a.format = 0;
+  a.delim = sc->delimiter;
+  a.want[0] = sc->objid_field; a.want[1] = sc->time_field; a.want[2] = sc->x_field; a.want[3] = sc->y_field;
+  return parse_text_lines(ctx, dict, text, len, a, g, x, y, objID, ts, cx, cy, cap, n_out, bad_line, bad_kind);
+}
+
+// Deserialization.GeoJSONToTSpatial.map (Deserialization.java:149-211) -- k_csv.hip eval_geojson_line
+extern "C" int gf_geojson_parse(gf_ctx* ctx, gf_objid_dict* dict, const char* text, int64_t len,
+                                const gf_geojson_schema* sc, const gf_grid* g, double* x, double* y, int64_t* objID,
+                                int64_t* ts, int32_t* cx, int32_t* cy, int64_t cap, int64_t* n_out, int64_t* bad_line,
+                                int32_t* bad_kind) {
+  if (!ctx) return GF_ERR_ARG;
+  if (!sc || (sc->date_format != 0 && sc->date_format != 1))
+    return set_err(ctx, GF_ERR_ARG, "gf_geojson_parse: bad schema");
+  CsvArgs a{};
+  a.format = 1;
+  a.len_obj = a.len_ts = -1;
+  for (int k = 0; k < 2; ++k) {
+    const char* name = k ? sc->time_property : sc->objid_property;
+    if (!name) continue;
+    const size_t n = std::strlen(name);
+    if (n >= (size_t)kGeoPropMax) return set_err(ctx, GF_ERR_ARG, "gf_geojson_parse: property name longer than 63 bytes");
+    std::memcpy(k ? a.prop_ts : a.prop_obj, name, n);
+    (k ? a.len_ts : a.len_obj) = (int32_t)n;
+  }
+  a.date_fmt = sc->date_format;
+  a.tz_off_ms = (int64_t)sc->tz_offset_minutes * 60000;
+  return parse_text_lines(ctx, dict, text, len, a, g, x, y, objID, ts, cx, cy, cap, n_out, bad_line, bad_kind);
 }

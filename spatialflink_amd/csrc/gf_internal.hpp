@@ -357,6 +357,7 @@ struct CsvErr {
   int kind;
   int pad;
 };
+constexpr int kGeoPropMax = 64;  // longest GeoJSON property name taken
 struct CsvArgs {
   const char* text;
   int64_t len;
@@ -377,6 +378,14 @@ struct CsvArgs {
   DictWork* dict_work;           // [lines]
   uint32_t* dict_n;
   unsigned long long* dict_bytes;  // sum of their raw lengths (arena bound)
+  // GeoJSON lines (gf_geojson_parse): format 1; the property names (propertyObjID,
+  // propertyTimeStamp; length -1 = not requested) and the timestamp interpretation
+  int32_t format;
+  int32_t len_obj, len_ts;
+  int32_t date_fmt;              // 0: Long.parseLong of a JSON integer; 1: "yyyy-MM-dd HH:mm:ss" text
+  int64_t tz_off_ms;             // date_fmt 1: UTC offset of the JVM default time zone
+  char prop_obj[kGeoPropMax];
+  char prop_ts[kGeoPropMax];
 };
 hipError_t launch_csv_count(hipStream_t st, const char* text, int64_t len, int64_t nseg, uint32_t* counts);
 hipError_t launch_csv_index(hipStream_t st, const char* text, int64_t len, int64_t nseg, const uint32_t* seg_off,

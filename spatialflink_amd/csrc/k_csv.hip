@@ -169,7 +169,7 @@ struct LineOut {
   Field f_obj;
 };
 template <class Src>
-__device__ __forceinline__ int eval_line(const CsvArgs& a, const Src& s, int64_t j, LineOut* o) {
+__device__ __forceinline__ int eval_csv_line(const CsvArgs& a, const Src& s, int64_t j, LineOut* o) {
   const int64_t b = j == 0 ? 0 : a.nl[j - 1] + 1;
   int64_t e = j < a.newlines ? a.nl[j] : a.len;
   if (e > b && s(e - 1) == '\r') --e;  // TextInputFormat drops the '\r' of "\r\n"
@@ -188,6 +188,261 @@ __device__ __forceinline__ int eval_line(const CsvArgs& a, const Src& s, int64_t
   if (a.want[3] >= nf) return kCsvMissingField;
   if ((st = parse_java_double(s, f[3], kPow5Dev, &o->y))) return st == kNumUnsupported ? kCsvUnsupported : kCsvNumberFormat;
   return kCsvOk;
+}
+
+// ---------------------------------------------------------------------------------------
+// GeoJSON lines (Deserialization.GeoJSONToTSpatial.map, Deserialization.java:149-211): a small
+// JSON scanner over the line's bytes -- member lookup (last duplicate wins, as Jackson's
+// ObjectNode), value skipping, and the three values the map reads: the geometry's first
+// coordinate, the time property, the objID property.
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ bool jws(char c) { return c == ' ' || c == '\t' || c == '\n' || c == '\r'; }
+template <class Src>
+__device__ __forceinline__ int64_t jskip(const Src& s, int64_t p, int64_t e) {
+  while (p < e && jws(s(p))) ++p;
+  return p;
+}
+// the string at p (s(p) == '"'): index past its closing quote, -1 if unterminated
+template <class Src>
+__device__ int64_t jstr_end(const Src& s, int64_t p, int64_t e, bool* esc) {
+  for (++p; p < e; ++p) {
+    const char c = s(p);
+    if (c == '\\') {
+      *esc = true;
+      ++p;
+    } else if (c == '"') {
+      return p + 1;
+    }
+  }
+  return -1;
+}
+// end of the value at p (p at its first byte), -1 if malformed
+template <class Src>
+__device__ int64_t jval_end(const Src& s, int64_t p, int64_t e) {
+  char c = s(p);
+  if (c == '"') {
+    bool esc = false;
+    return jstr_end(s, p, e, &esc);
+  }
+  if (c == '{' || c == '[') {
+    int depth = 0;
+    while (p < e) {
+      c = s(p);
+      if (c == '"') {
+        bool esc = false;
+        p = jstr_end(s, p, e, &esc);
+        if (p < 0) return -1;
+        continue;
+      }
+      if (c == '{' || c == '[') ++depth;
+      else if ((c == '}' || c == ']') && --depth == 0) return p + 1;
+      ++p;
+    }
+    return -1;
+  }
+  int64_t q = p;
+  while (q < e && !(s(q) == ',' || s(q) == '}' || s(q) == ']' || jws(s(q)))) ++q;
+  return q > p ? q : -1;
+}
+// the value of the LAST member `key` of the object at p (s(p) == '{'): its first byte, -1 when
+// absent, -2 when the object is malformed
+template <class Src>
+__device__ int64_t jfind(const Src& s, int64_t p, int64_t e, const char* key, int klen) {
+  int64_t found = -1;
+  p = jskip(s, p + 1, e);
+  if (p < e && s(p) == '}') return -1;
+  while (p < e) {
+    if (s(p) != '"') return -2;
+    bool esc = false;
+    const int64_t ke = jstr_end(s, p, e, &esc);
+    if (ke < 0) return -2;
+    bool match = !esc && ke - p - 2 == klen;
+    for (int i = 0; match && i < klen; ++i) match = s(p + 1 + i) == key[i];
+    p = jskip(s, ke, e);
+    if (p >= e || s(p) != ':') return -2;
+    p = jskip(s, p + 1, e);
+    if (p >= e) return -2;
+    const int64_t ve = jval_end(s, p, e);
+    if (ve < 0) return -2;
+    if (match) found = p;
+    p = jskip(s, ve, e);
+    if (p >= e) return -2;
+    if (s(p) == ',') {
+      p = jskip(s, p + 1, e);
+      continue;
+    }
+    return s(p) == '}' ? found : -2;
+  }
+  return -2;
+}
+// JSON number token [p, q): -?(0|[1-9][0-9]*)(.[0-9]+)?([eE][+-]?[0-9]+)?; *integral = no frac/exp
+template <class Src>
+__device__ bool jnumber(const Src& s, int64_t p, int64_t q, bool* integral) {
+  int64_t i = p;
+  if (i < q && s(i) == '-') ++i;
+  if (i >= q) return false;
+  if (s(i) == '0') ++i;
+  else if (s(i) >= '1' && s(i) <= '9') while (i < q && s(i) >= '0' && s(i) <= '9') ++i;
+  else return false;
+  *integral = true;
+  if (i < q && s(i) == '.') {
+    *integral = false;
+    const int64_t d = ++i;
+    while (i < q && s(i) >= '0' && s(i) <= '9') ++i;
+    if (i == d) return false;
+  }
+  if (i < q && (s(i) == 'e' || s(i) == 'E')) {
+    *integral = false;
+    ++i;
+    if (i < q && (s(i) == '+' || s(i) == '-')) ++i;
+    const int64_t d = i;
+    while (i < q && s(i) >= '0' && s(i) <= '9') ++i;
+    if (i == d) return false;
+  }
+  return i == q;
+}
+// days since 1970-01-01 of the proleptic Gregorian date (y, m 1..12, day 1)
+__device__ __forceinline__ int64_t days_from_civil(int64_t y, int64_t m) {
+  y -= m <= 2;
+  const int64_t era = (y >= 0 ? y : y - 399) / 400;
+  const int64_t yoe = y - era * 400;
+  const int64_t doy = (153 * (m + (m > 2 ? -3 : 9)) + 2) / 5;
+  return era * 146097 + yoe * 365 + yoe / 4 - yoe / 100 + doy - 719468;
+}
+// SimpleDateFormat("yyyy-MM-dd HH:mm:ss").parse (lenient: fields roll over) of the string content
+// [p, q): 0 = parsed, 1 = ParseException (time stays 0), 2 = unsupported (before 1583)
+template <class Src>
+__device__ int jdate(const Src& s, int64_t p, int64_t q, int64_t tz_off_ms, int64_t* ms) {
+  const char sep[5] = {'-', '-', ' ', ':', ':'};
+  int64_t f[6];
+  for (int k = 0; k < 6; ++k) {
+    int nd = 0;
+    int64_t v = 0;
+    while (p < q && s(p) >= '0' && s(p) <= '9' && nd < 10) {
+      v = v * 10 + (s(p) - '0');
+      ++p;
+      ++nd;
+    }
+    if (nd == 0) return 1;
+    if (nd == 10) return 2;  // int overflow territory of the lenient calendar: not restated
+    f[k] = v;
+    if (k < 5) {
+      if (p >= q || s(p) != sep[k]) return 1;
+      ++p;
+    }
+  }
+  const int64_t m0 = f[1] - 1;
+  const int64_t y = f[0] + (m0 >= 0 ? m0 / 12 : (m0 - 11) / 12);
+  const int64_t m = m0 - 12 * (y - f[0]) + 1;
+  const int64_t days = days_from_civil(y, m) + f[2] - 1;
+  const int64_t secs = ((days * 24 + f[3]) * 60 + f[4]) * 60 + f[5];
+  if (secs < -12219292800ll) return 2;  // before 1582-10-15: Java's Julian calendar
+  *ms = secs * 1000 - tz_off_ms;
+  return 0;
+}
+
+template <class Src>
+__device__ int eval_geojson_line(const CsvArgs& a, const Src& s, int64_t j, LineOut* o) {
+  const int64_t b = j == 0 ? 0 : a.nl[j - 1] + 1;
+  int64_t e = j < a.newlines ? a.nl[j] : a.len;
+  if (e > b && s(e - 1) == '\r') --e;
+  if (e <= b) return kCsvEmptyLine;
+  int64_t p = jskip(s, b, e);
+  if (p >= e || s(p) != '{') return kCsvMissingField;
+  // the feature: the record's "value" object, or the line's object itself
+  int64_t feat = p;
+  const int64_t v = jfind(s, p, e, "value", 5);
+  if (v == -2) return kCsvMissingField;
+  if (v >= 0 && s(v) == '{') feat = v;
+  const int64_t g = jfind(s, feat, e, "geometry", 8);
+  if (g < 0 || s(g) != '{') return kCsvMissingField;
+  int64_t c = jfind(s, g, e, "coordinates", 11);
+  if (c < 0 || s(c) != '[') return kCsvMissingField;
+  while (c < e && s(c) == '[') c = jskip(s, c + 1, e);  // the first coordinate of any nesting
+  double xy[2];
+  for (int k = 0; k < 2; ++k) {
+    if (c >= e) return kCsvMissingField;
+    const int64_t ce = jval_end(s, c, e);
+    bool integral;
+    if (ce < 0 || !jnumber(s, c, ce, &integral)) return kCsvNumberFormat;
+    const int st = parse_java_double(s, Field{c, ce}, kPow5Dev, &xy[k]);
+    if (st) return st == kNumUnsupported ? kCsvUnsupported : kCsvNumberFormat;
+    c = jskip(s, ce, e);
+    if (k == 0) {
+      if (c >= e || s(c) != ',') return kCsvMissingField;
+      c = jskip(s, c + 1, e);
+    }
+  }
+  o->x = xy[0];
+  o->y = xy[1];
+  o->ts = 0;
+  o->obj = GF_OBJID_NULL;
+  o->dict = false;
+  const int64_t pr = jfind(s, feat, e, "properties", 10);
+  if (pr == -2) return kCsvMissingField;
+  if (pr < 0 || s(pr) != '{') return kCsvOk;
+  if (a.len_ts >= 0) {
+    const int64_t t = jfind(s, pr, e, a.prop_ts, a.len_ts);
+    if (t == -2) return kCsvMissingField;
+    if (t >= 0) {
+      const int64_t te = jval_end(s, t, e);
+      if (a.date_fmt == 0) {  // Long.parseLong(String.valueOf(node)): a JSON integer only
+        bool integral;
+        if (!jnumber(s, t, te, &integral) || !integral) return kCsvNumberFormat;
+        if (parse_java_long(s, Field{t, te}, &o->ts)) return kCsvNumberFormat;
+      } else {  // dateFormat.parse(node.textValue()); ParseException -> 0
+        if (s(t) != '"') return kCsvNumberFormat;  // textValue() null: the parse throws
+        bool esc = false;
+        jstr_end(s, t, e, &esc);
+        if (esc) return kCsvUnsupported;
+        int64_t ms = 0;
+        const int st = jdate(s, t + 1, te - 1, a.tz_off_ms, &ms);
+        if (st == 2) return kCsvUnsupported;
+        if (st == 0) o->ts = ms;
+      }
+    }
+  }
+  if (a.len_obj >= 0) {
+    const int64_t q = jfind(s, pr, e, a.prop_obj, a.len_obj);
+    if (q == -2) return kCsvMissingField;
+    if (q >= 0) {  // nodeOId.toString() with every '"' removed
+      const int64_t qe = jval_end(s, q, e);
+      Field f{q, qe};
+      const char c0 = s(q);
+      if (c0 == '"') {
+        bool esc = false;
+        jstr_end(s, q, e, &esc);
+        if (esc) return kCsvUnsupported;
+        f = Field{q + 1, qe - 1};
+      } else if (c0 == '{' || c0 == '[') {
+        return kCsvUnsupported;
+      } else if (c0 == '-' || (c0 >= '0' && c0 <= '9')) {
+        bool integral;
+        if (!jnumber(s, q, qe, &integral)) return kCsvMissingField;
+        if (!integral) return kCsvUnsupported;  // Double.toString rendering: not restated
+        if (qe - q == 2 && c0 == '-' && s(q + 1) == '0') {  // IntNode(0).toString() == "0"
+          o->obj = 0;
+          return kCsvOk;
+        }
+      } else {  // true / false / null print as themselves
+        bool lit = false;
+        const int64_t n = qe - q;
+        if (n == 4) lit = (s(q) == 't' && s(q + 1) == 'r' && s(q + 2) == 'u' && s(q + 3) == 'e') ||
+                          (s(q) == 'n' && s(q + 1) == 'u' && s(q + 2) == 'l' && s(q + 3) == 'l');
+        if (n == 5) lit = s(q) == 'f' && s(q + 1) == 'a' && s(q + 2) == 'l' && s(q + 3) == 's' && s(q + 4) == 'e';
+        if (!lit) return kCsvMissingField;
+      }
+      o->dict = !canonical_objid_key(s, f, &o->obj);
+      o->f_obj = f;
+      if (o->dict && f.e - f.b > (int64_t)kDictLenMask) return kCsvUnsupported;
+    }
+  }
+  return kCsvOk;
+}
+
+template <class Src>
+__device__ __forceinline__ int eval_line(const CsvArgs& a, const Src& s, int64_t j, LineOut* o) {
+  return a.format == 1 ? eval_geojson_line(a, s, j, o) : eval_csv_line(a, s, j, o);
 }
 
 // parse + store line j; returns true when its objID needs the dictionary (*w filled)

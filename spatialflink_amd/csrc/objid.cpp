@@ -280,6 +280,9 @@ extern "C" int gf_objid_decode(gf_objid_dict* d, const int64_t* keys, int64_t n,
       const unsigned long long m = d->h_idmap[id];
       p = d->h_arena.data() + (m >> kDictLenBits);
       len = (size_t)(m & kDictLenMask);
+    } else if (k == GF_OBJID_NULL) {  // a null objID decodes as the empty byte string
+      p = num;
+      len = 0;
     } else if (k >= GF_OBJID_NUMERIC_END) {
       return set_err(ctx, GF_ERR_ARG, "gf_objid_decode: not an objID key");
     } else {

@@ -81,8 +81,10 @@ class ObjIdDict:
         raise _lib.GeoFlinkError(_lib.GF_ERR_CAPACITY, "gf_objid_decode")
 
     def decode(self, keys):
-        """int64 keys -> list of str"""
-        return [b.decode("utf-8", "surrogateescape") for b in self.decode_bytes(keys)]
+        """int64 keys -> list of str (None for OBJID_NULL: a GeoJSON feature without the objID property)"""
+        k = np.asarray(keys, np.int64)
+        return [None if kk == _lib.OBJID_NULL else b.decode("utf-8", "surrogateescape")
+                for kk, b in zip(k.tolist(), self.decode_bytes(k))]
 
     def __del__(self):
         h = getattr(self, "handle", None)

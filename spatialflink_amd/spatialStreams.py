@@ -1,5 +1,6 @@
 """Ingest -- mirror of GeoFlink.spatialStreams.Deserialization for the CSV/TSV point stream
-(Deserialization.CSVTSVToTSpatial, Deserialization.java:291-325), run on the GPU.
+(Deserialization.CSVTSVToTSpatial, Deserialization.java:291-325) and the GeoJSON point stream
+(Deserialization.GeoJSONToTSpatial, Deserialization.java:149-211), run on the GPU.
 
 The reference maps each text line to a Point with String.split + Long.valueOf +
 Double.valueOf and assigns its grid cell in the Point constructor (Point.java:98).  Here a whole
@@ -43,7 +44,72 @@ def device_text(text, device=None):
     return torch.from_numpy(np.ascontiguousarray(arr)).to(dev)
 
 
+class GfGeojsonSchema(C.Structure):
+    _fields_ = [("objid_property", C.c_char_p), ("time_property", C.c_char_p), ("date_format", C.c_int32),
+                ("tz_offset_minutes", C.c_int32)]
+
+
+GEOJSON_DATE_FORMATS = {None: 0, "yyyy-MM-dd HH:mm:ss": 1}
+
+
+def _parse_lines(fn, schema, uGrid, text, device, capacity, objid_dict):
+    import torch
+
+    t = device_text(text, device)
+    dev = t.device
+    ctx = _lib.context(dev.index)
+    d = objid_dict or ObjIdDict.default(dev.index)
+    n = int(t.numel())
+    cap = capacity if capacity is not None else max(1, n // 8 + 1)
+    nout, bl, bk = C.c_int64(), C.c_int64(), C.c_int32()
+    while True:
+        x = torch.empty(cap, dtype=torch.float64, device=dev)
+        y = torch.empty(cap, dtype=torch.float64, device=dev)
+        o = torch.empty(cap, dtype=torch.int64, device=dev)
+        ts = torch.empty(cap, dtype=torch.int64, device=dev)
+        cx = torch.empty(cap, dtype=torch.int32, device=dev) if uGrid is not None else None
+        cy = torch.empty(cap, dtype=torch.int32, device=dev) if uGrid is not None else None
+        st = fn(ctx.handle, d.handle, C.c_void_p(t.data_ptr()), n, C.byref(schema),
+                C.byref(uGrid.c_grid) if uGrid is not None else None, x.data_ptr(), y.data_ptr(), o.data_ptr(),
+                ts.data_ptr(), cx.data_ptr() if cx is not None else None, cy.data_ptr() if cy is not None else None,
+                cap, C.byref(nout), C.byref(bl), C.byref(bk))
+        if st == _lib.GF_ERR_CAPACITY:
+            cap = nout.value
+            continue
+        if st == _lib.GF_ERR_ARG and bl.value >= 0:
+            raise ValueError(f"line {bl.value}: {CSV_KINDS.get(bk.value, bk.value)}")
+        _lib.check(st, ctx.handle, "parse")
+        break
+    m = nout.value
+    w = PointWindow(x[:m], y[:m], o[:m], ts[:m], objid_dict=d)
+    if cx is not None:
+        w.extra["cx"], w.extra["cy"] = cx[:m], cy[:m]
+    return w
+
+
 class Deserialization:
+    class GeoJSONToTSpatial:
+        """GeoJSONToTSpatial(uGrid, dateFormat, propertyTimeStamp, propertyObjID)
+        (Deserialization.java:149-211) over lines of GeoJSON: one Kafka key/value record
+        ({"key": .., "value": Feature}) or bare Feature per line, run on the GPU
+        (gf_geojson_parse).  dateFormat: None (the time property is integer milliseconds) or
+        "yyyy-MM-dd HH:mm:ss" in a fixed UTC offset `tz_offset_minutes` (the reference JVM's
+        default zone).  A feature without the objID property has objID None (key OBJID_NULL)."""
+
+        def __init__(self, uGrid=None, dateFormat=None, propertyTimeStamp=None, propertyObjID=None,
+                     tz_offset_minutes=0):
+            if dateFormat not in GEOJSON_DATE_FORMATS:
+                raise ValueError(f"dateFormat {dateFormat!r}: supported {list(GEOJSON_DATE_FORMATS)}")
+            self.uGrid = uGrid
+            self._names = (propertyObjID.encode() if propertyObjID else None,
+                           propertyTimeStamp.encode() if propertyTimeStamp else None)
+            self.schema = GfGeojsonSchema(self._names[0], self._names[1], GEOJSON_DATE_FORMATS[dateFormat],
+                                          int(tz_offset_minutes))
+
+        def parse(self, text, device=None, capacity=None, objid_dict: ObjIdDict = None) -> PointWindow:
+            return _parse_lines(_lib.lib().gf_geojson_parse, self.schema, self.uGrid, text, device, capacity,
+                                objid_dict)
+
     class CSVTSVToTSpatial:
         """CSVTSVToTSpatial(uGrid, dateFormat, delimiter, csvTsvSchemaAttr) -- csvTsvSchemaAttr
         lists the field indices of objID, timestamp, x, y (Deserialization.java:314-322).
@@ -60,38 +126,5 @@ class Deserialization:
         def parse(self, text, device=None, capacity=None, objid_dict: ObjIdDict = None) -> PointWindow:
             """All lines of `text` -> one PointWindow (extra: cx, cy when a grid is set).  objID
             Strings become keys of `objid_dict` (default: the device context's dictionary)."""
-            import torch
-
-            t = device_text(text, device)
-            dev = t.device
-            ctx = _lib.context(dev.index)
-            d = objid_dict or ObjIdDict.default(dev.index)
-            n = int(t.numel())
-            cap = capacity if capacity is not None else max(1, n // 8 + 1)
-            L = _lib.lib()
-            nout, bl, bk = C.c_int64(), C.c_int64(), C.c_int32()
-            while True:
-                x = torch.empty(cap, dtype=torch.float64, device=dev)
-                y = torch.empty(cap, dtype=torch.float64, device=dev)
-                o = torch.empty(cap, dtype=torch.int64, device=dev)
-                ts = torch.empty(cap, dtype=torch.int64, device=dev)
-                cx = torch.empty(cap, dtype=torch.int32, device=dev) if self.uGrid is not None else None
-                cy = torch.empty(cap, dtype=torch.int32, device=dev) if self.uGrid is not None else None
-                st = L.gf_csv_parse_dict(ctx.handle, d.handle, C.c_void_p(t.data_ptr()), n, C.byref(self.schema),
-                                    C.byref(self.uGrid.c_grid) if self.uGrid is not None else None,
-                                    x.data_ptr(), y.data_ptr(), o.data_ptr(), ts.data_ptr(),
-                                    cx.data_ptr() if cx is not None else None,
-                                    cy.data_ptr() if cy is not None else None, cap, C.byref(nout), C.byref(bl),
-                                    C.byref(bk))
-                if st == _lib.GF_ERR_CAPACITY:
-                    cap = nout.value
-                    continue
-                if st == _lib.GF_ERR_ARG and bl.value >= 0:
-                    raise ValueError(f"line {bl.value}: {CSV_KINDS.get(bk.value, bk.value)}")
-                _lib.check(st, ctx.handle, "gf_csv_parse")
-                break
-            m = nout.value
-            w = PointWindow(x[:m], y[:m], o[:m], ts[:m], objid_dict=d)
-            if cx is not None:
-                w.extra["cx"], w.extra["cy"] = cx[:m], cy[:m]
-            return w
+            return _parse_lines(_lib.lib().gf_csv_parse_dict, self.schema, self.uGrid, text, device, capacity,
+                                objid_dict)

@@ -760,21 +760,24 @@ def bench_sliding(args):
         dist.destroy_process_group()
 
 
-def bench_csv(args):
+def bench_csv(args, geojson=False):
     """C1 ingest: 1M-line CSV window (objID, ts, x, y; shortest round-trip doubles, the way Java's
     Double.toString prints them) device-resident as text -> gf_csv_parse (SoA + 100x100 cells),
     then the C1 point-point range query on the parsed window.  value = lines/s of the whole
-    text -> range-hits step; the parse kernel's roofline counts text bytes + 40 B/point out."""
+    text -> range-hits step; the parse kernel's roofline counts text bytes + 40 B/point out.
+    geojson: the same with 1M GeoJSON lines (tests/geojson_gen.py: Kafka records and bare
+    Features, date-string timestamps in UTC+8) -> gf_geojson_parse (Deserialization.java:149-211)."""
     import torch
 
     import spatialflink_amd as sf
     from spatialflink_amd import _lib
-    from spatialflink_amd.spatialStreams import GfCsvSchema, device_text
+    from spatialflink_amd.spatialStreams import GfCsvSchema, GfGeojsonSchema, device_text
 
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     from csv_gen import make_csv
+    from geojson_gen import lines as geojson_lines
 
     n = args.points or 1_000_000
     L = _lib.lib()
@@ -782,10 +785,15 @@ def bench_csv(args):
     grid = sf.UniformGrid(100, *BEIJING)
     texts = []
     for j in range(2):
-        text, px, py, po, pt = make_csv(n, seed=31 + j)
-        texts.append((text, px, py, po, device_text(text)))
+        if geojson:
+            text = geojson_lines(31 + j, n, 1)
+            texts.append((text, None, None, None, device_text(text)))
+        else:
+            text, px, py, po, pt = make_csv(n, seed=31 + j)
+            texts.append((text, px, py, po, device_text(text)))
     nbytes = len(texts[0][0])
-    sc = GfCsvSchema(b",", b"\0\0\0", 0, 1, 2, 3)
+    sc = GfGeojsonSchema(b"oID", b"timestamp", 1, 480) if geojson else GfCsvSchema(b",", b"\0\0\0", 0, 1, 2, 3)
+    dict_h = sf.ObjIdDict.default(0).handle
     x = torch.empty(n, dtype=torch.float64, device="cuda"); y = torch.empty_like(x)
     o = torch.empty(n, dtype=torch.int64, device="cuda"); ts = torch.empty_like(o)
     cx = torch.empty(n, dtype=torch.int32, device="cuda"); cy = torch.empty_like(cx)
@@ -801,9 +809,10 @@ def bench_csv(args):
 
     def parse(i):
         t = texts[i % 2][4]
-        _lib.check(L.gf_csv_parse(ctx.handle, C.c_void_p(t.data_ptr()), t.numel(), C.byref(sc), C.byref(grid.c_grid),
-                                  x.data_ptr(), y.data_ptr(), o.data_ptr(), ts.data_ptr(), cx.data_ptr(), cy.data_ptr(),
-                                  n, C.byref(nout), C.byref(bl), C.byref(bk)), ctx.handle, "gf_csv_parse")
+        fn = L.gf_geojson_parse if geojson else L.gf_csv_parse_dict
+        _lib.check(fn(ctx.handle, dict_h, C.c_void_p(t.data_ptr()), t.numel(), C.byref(sc), C.byref(grid.c_grid),
+                      x.data_ptr(), y.data_ptr(), o.data_ptr(), ts.data_ptr(), cx.data_ptr(), cy.data_ptr(),
+                      n, C.byref(nout), C.byref(bl), C.byref(bk)), ctx.handle, "parse")
 
     def step(i):
         parse(i)
@@ -832,11 +841,14 @@ def bench_csv(args):
     j = (args.steps - 1) % 2
     parse(j)
     text = texts[j][0]
-    ex, ey, eo, et, ebl, ebk = O.csv_parse(text, ",", [0, 1, 2, 3])
+    oracle_parse = (lambda t_: O.geojson_parse(t_, "oID", "timestamp", 1, 480)) if geojson else (
+        lambda t_: O.csv_parse(t_, ",", [0, 1, 2, 3]))
+    ex, ey, eo, et, ebl, ebk = oracle_parse(text)
     # objIDs: the keys decode to the oracle's Strings exactly (numeric Strings are their own key)
     verified = bool(ebl == -1 and np.array_equal(x.cpu().numpy().view(np.int64), ex.view(np.int64))
                     and np.array_equal(y.cpu().numpy().view(np.int64), ey.view(np.int64))
-                    and sf.ObjIdDict.default(0).decode_bytes(o.cpu().numpy()) == eo
+                    and [None if k_ == _lib.OBJID_NULL else b_ for k_, b_ in
+                         zip(o.cpu().numpy().tolist(), sf.ObjIdDict.default(0).decode_bytes(o.cpu().numpy()))] == eo
                     and np.array_equal(ts.cpu().numpy(), et))
     og = O.grid(100, *BEIJING)
     ecx, ecy = O.assign_cells(og, ex, ey)
@@ -849,18 +861,22 @@ def bench_csv(args):
     if not args.no_cpu_baseline:  # the oracle's restatement of the reference's per-line map, 1 thread
         reps, tc = 0, time.perf_counter()
         while True:
-            O.csv_parse(text, ",", [0, 1, 2, 3])
+            oracle_parse(text)
             reps += 1
             if time.perf_counter() - tc >= min(args.cpu_seconds, 10.0):
                 break
         ct = time.perf_counter() - tc
         cpu = {"value": round(reps * n / ct, 1), "unit": "lines/s", "cores": 1, "kind": "port",
-               "sample": f"the {n}-line window x {reps} ({ct:.1f}s): oracle orc_csv_parse (quote removal, Java split "
-                         "rule, Long.valueOf, strtod), 1 thread -- ingest only"}
+               "sample": (f"the {n}-line window x {reps} ({ct:.1f}s): oracle geojson_parse (Python json module per "
+                          "line + the map's property logic), 1 thread -- ingest only") if geojson else
+                         (f"the {n}-line window x {reps} ({ct:.1f}s): oracle orc_csv_parse (quote removal, Java split "
+                          "rule, Long.valueOf, strtod), 1 thread -- ingest only")}
     avg_parse = pms / 1000.0 / max(pcnt, 1)
-    _line("CSV ingest + point-point range", n * args.steps / elapsed, "lines/s", args.steps, args.warmup, elapsed,
-          "csv_parse_kernel", float(nbytes + 40 * n), avg_parse,
-          {"config": {"workload": f"csv_{n // 1_000_000}Mlines_range_r{args.radius}_grid100", "lines": n,
+    _line(("GeoJSON" if geojson else "CSV") + " ingest + point-point range", n * args.steps / elapsed, "lines/s",
+          args.steps, args.warmup, elapsed, "csv_parse_kernel" + (" (GeoJSON lines)" if geojson else ""),
+          float(nbytes + 40 * n), avg_parse,
+          {"config": {"workload": f"{'geojson' if geojson else 'csv'}_{n // 1_000_000}Mlines_range_r{args.radius}_grid100",
+                      "lines": n,
                       "text_bytes": nbytes, "radius": args.radius},
            "breakdown": {"parse_kernel_us": round(avg_parse * 1e6, 2),
                          "range_kernel_us": round(rms * 1000.0 / max(rcnt, 1), 2),
@@ -1009,6 +1025,8 @@ def run(args):
         bench_sliding(args)
     elif args.workload == "csv":
         bench_csv(args)
+    elif args.workload == "geojson":
+        bench_csv(args, geojson=True)
     elif args.workload == "polyknn":
         bench_polyknn(args)
     elif args.workload == "bucket":
