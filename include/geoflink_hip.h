@@ -200,7 +200,13 @@ int  gf_bitmap_to_indices_async(gf_ctx* ctx, const uint64_t* bitmap, int64_t n, 
 typedef struct gf_knn_plan gf_knn_plan;
 /* PointPointKNNQuery.run(stream, queryPoint, r, k) -- PointPointKNNQuery.java:33,132-150 */
 int    gf_knn_pp_plan_create(gf_ctx* ctx, const gf_grid* g, double qx, double qy, double r,
-                             int32_t k, int metric, gf_knn_plan** out);   /* 1 <= k <= 512 */
+                             int32_t k, int metric, gf_knn_plan** out);   /* 1 <= k <= 2^24 */
+/* k <= 512: sample -> scan -> one-block select (pipeline depths 1..3).  k > 512 (the
+ * reference's PriorityQueue takes any k, KNNQuery.java:216): every candidate within r is kept
+ * and the record comes from two stable device radix sorts of them ((objID, d, idx) -> first of
+ * each objID -> (d, objID, idx)); the enqueue reads two counts from the device (synchronizes),
+ * pipeline depth 1 only, no sliding engine and no gf_knn_merge_dev (records of k <= 512).  The
+ * exact re-evaluation of a flagged window (gf_knn_decode) takes the same sorted path. */
 /* PointPolygonKNNQuery.run(stream, queryPolygon, r, k) -- knn/PointPolygonKNNQuery.java:245-317:
  * kNN of the window's points to ONE query polygon (polys->npoly == 1): candidates have their cell
  * in C u G of the polygon's bbox cells and d <= r, d = JTS point-polygon distance (0 inside) or,

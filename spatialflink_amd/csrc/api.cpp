@@ -1143,8 +1143,8 @@ static int knn_alloc_candidates(gf_knn_plan* P, int64_t cap) {
 
 extern "C" int gf_knn_pp_plan_create(gf_ctx* ctx, const gf_grid* g, double qx, double qy, double r, int32_t k,
                                      int metric, gf_knn_plan** out) {
-  if (!ctx || !out || !grid_ok(g) || k < 1 || k > kMaxK || (metric != 0 && metric != 1))
-    return set_err(ctx, GF_ERR_ARG, "gf_knn_pp_plan_create: bad argument (k must be in [1, 512])");
+  if (!ctx || !out || !grid_ok(g) || k < 1 || k > kMaxKLarge || (metric != 0 && metric != 1))
+    return set_err(ctx, GF_ERR_ARG, "gf_knn_pp_plan_create: bad argument (k must be in [1, 2^24])");
   *out = nullptr;
   int st = bind(ctx);
   if (st) return st;
@@ -1162,6 +1162,7 @@ extern "C" int gf_knn_pp_plan_create(gf_ctx* ctx, const gf_grid* g, double qx, d
   if ((e = hipHostMalloc(&P->host_result, gf_knn_result_bytes(k), hipHostMallocDefault)) != hipSuccess)
     return fail(hip_err(ctx, e, "hipHostMalloc"));
   P->scan_blocks = 0;
+  P->large = k > kMaxK;
   *out = P;
   return GF_OK;
 }
@@ -1172,8 +1173,8 @@ extern "C" int gf_knn_pp_plan_create(gf_ctx* ctx, const gf_grid* g, double qx, d
 // validKey), the polygon on the device for the exact JTS distance.
 extern "C" int gf_knn_ppoly_plan_create(gf_ctx* ctx, const gf_grid* g, const gf_polygons* poly, double r,
                                         int32_t k, int approximate, int metric, gf_knn_plan** out) {
-  if (!ctx || !out || !grid_ok(g) || !poly || poly->npoly != 1 || k < 1 || k > kMaxK || (metric != 0 && metric != 1))
-    return set_err(ctx, GF_ERR_ARG, "gf_knn_ppoly_plan_create: bad argument (one polygon, 1 <= k <= 512)");
+  if (!ctx || !out || !grid_ok(g) || !poly || poly->npoly != 1 || k < 1 || k > kMaxKLarge || (metric != 0 && metric != 1))
+    return set_err(ctx, GF_ERR_ARG, "gf_knn_ppoly_plan_create: bad argument (one polygon, 1 <= k <= 2^24)");
   *out = nullptr;
   const int32_t nrings = poly->ring_off[1] - poly->ring_off[0];
   if (poly->ring_off[0] != 0 || nrings < 1) return set_err(ctx, GF_ERR_ARG, "polygon without a shell");
@@ -1336,6 +1337,84 @@ static int knn_scan_select(gf_knn_plan* P, int j, const gf_points* pts, int64_t 
   return GF_OK;
 }
 
+// k > kMaxK (KNNQuery.java:216 takes any k): every candidate within r (T = r; lane 0's buffers
+// hold the whole window, so nothing overflows), one host read of their count, then two stable
+// LSD radix sorts of the candidate permutation over 32-bit key fields (the K2 bucketing passes):
+// (objID, d, idx) -> the first entry of each objID -> those by (d, objID, idx) -> the first k.
+static int knn_large(gf_knn_plan* P, const gf_points* pts, void* result) {
+  gf_ctx* ctx = P->ctx;
+  int st;
+  const int64_t n = pts->n;
+  if (P->cap < n && (st = knn_alloc_candidates(P, n))) return st;
+  if (P->poly) {  // JTS point-polygon distances (prefilter + refine), T = r
+    if ((st = poly_buffers(P))) return st;
+    GF_HIP_CHECK(ctx, launch_knn_poly_scan(ctx, poly_args(P, 0, pts, 0, n, 0, 0), scan_blocks_for(P, (n + 1) / 2)));
+  } else {
+    const KnnScanArgs s = scan_args(P, 0, pts, 0, n, 0);  // T = r
+    GF_HIP_CHECK(ctx, launch_knn_scan(ctx, s, scan_blocks_for(P, n), P->scan_unroll, P->scan_nt));
+  }
+  unsigned long long m64 = 0;
+  if ((st = read_scalar_sync(ctx, &P->lane[0].st->count, &m64))) return st;
+  const int64_t m = (int64_t)m64;
+  // ready for the lane's next window (the select kernel does this on the other paths)
+  GF_HIP_CHECK(ctx, hipMemsetAsync(&P->lane[0].st->count, 0, sizeof(unsigned long long), ctx->stream));
+  GF_HIP_CHECK(ctx, hipMemsetAsync(&P->lane[0].st->maybe, 0, sizeof(unsigned long long), ctx->stream));
+  const gf_knn_plan::Lane& L = P->lane[0];
+  const int blocks = (int)std::min<int64_t>(std::max<int64_t>(m / (4 * 4096), 1), (int64_t)ctx->num_cus * 2);
+  const int64_t mat = (int64_t)kRadixDigits * blocks * (kBlock / 64);
+  const int64_t mm = std::max<int64_t>(m, 1);
+  Arena ar;
+  size_t o_k[2] = {ar.take<uint32_t>(mm), ar.take<uint32_t>(mm)};
+  size_t o_p[2] = {ar.take<uint32_t>(mm), ar.take<uint32_t>(mm)};
+  size_t o_flag = ar.take<uint32_t>(mm), o_off = ar.take<uint32_t>(mm + 1);
+  size_t o_m = ar.take<uint32_t>(mat), o_ms = ar.take<uint32_t>(mat + 1);
+  size_t o_tmp = ar.take<uint32_t>(std::max(scan_tmp_elems(mat), scan_tmp_elems(mm)));
+  char* base = (char*)ctx_scratch(ctx, ar.off, &st);
+  if (st) return st;
+  auto U32 = [&](size_t o) { return (uint32_t*)(base + o); };
+  KnnLargeArgs a{};
+  a.cd = L.cand_d; a.co = L.cand_o; a.ci = L.cand_i; a.k = P->k; a.T = P->r; a.idx_base = P->idx_base;
+  a.result = result;
+  int cur = 0;  // the permutation lives in o_p[cur]
+  // stable sort of the first `cnt` entries of the permutation by key fields (least significant first)
+  auto sort_by = [&](int64_t cnt, std::initializer_list<int> fields) -> int {
+    if (cnt <= 1) return GF_OK;
+    const int nb = (int)std::min<int64_t>(std::max<int64_t>(cnt / (4 * 4096), 1), (int64_t)ctx->num_cus * 2);
+    const int64_t nmat = (int64_t)kRadixDigits * nb * (kBlock / 64);
+    for (int f : fields) {
+      a.m = cnt; a.perm = U32(o_p[cur]); a.field = f; a.keys = U32(o_k[0]);
+      GF_HIP_CHECK(ctx, launch_knn_large(ctx, 1, a));
+      for (int p = 0; p < 3; ++p) {  // 32 bits = 3 passes of kRadixBits (11)
+        RadixArgs r{};
+        r.n = cnt;
+        r.kin = U32(o_k[p & 1]); r.vin = U32(o_p[cur]);
+        r.kout = U32(o_k[(p + 1) & 1]); r.vout = U32(o_p[cur ^ 1]);
+        r.shift = p * kRadixBits; r.M = U32(o_m); r.Ms = U32(o_ms);
+        GF_HIP_CHECK(ctx, launch_radix(ctx, 0, r, nb));
+        GF_HIP_CHECK(ctx, launch_exclusive_scan(ctx->stream, U32(o_m), nmat, U32(o_ms), U32(o_tmp)));
+        GF_HIP_CHECK(ctx, launch_radix(ctx, 1, r, nb));
+        cur ^= 1;
+      }
+    }
+    return GF_OK;
+  };
+  a.m = m; a.perm = U32(o_p[cur]);
+  GF_HIP_CHECK(ctx, launch_knn_large(ctx, 0, a));                 // identity permutation
+  if ((st = sort_by(m, {0, 1, 2, 3, 4}))) return st;               // (objID, d, idx)
+  a.m = m; a.perm = U32(o_p[cur]); a.flag = U32(o_flag);
+  GF_HIP_CHECK(ctx, launch_knn_large(ctx, 2, a));                 // first of each objID
+  GF_HIP_CHECK(ctx, launch_exclusive_scan(ctx->stream, U32(o_flag), m, U32(o_off), U32(o_tmp)));
+  a.off = U32(o_off); a.out = U32(o_p[cur ^ 1]);
+  GF_HIP_CHECK(ctx, launch_knn_large(ctx, 3, a));
+  cur ^= 1;
+  uint32_t nsurv = 0;  // survivors: their count sizes the second sort
+  if ((st = read_scalar_sync(ctx, U32(o_off) + m, &nsurv))) return st;
+  if ((st = sort_by(nsurv, {0, 3, 4, 1, 2}))) return st;          // (d, objID, idx)
+  a.perm = U32(o_p[cur]); a.nsurv = U32(o_off) + m; a.m = m;
+  GF_HIP_CHECK(ctx, launch_knn_large(ctx, 4, a));
+  return GF_OK;
+}
+
 static int knn_launch_sample(gf_knn_plan* P, int j, const gf_points* pts, int use_hint) {
   if (P->poly) {
     GF_HIP_CHECK(P->ctx, launch_knn_poly_sample(P->ctx, poly_args(P, j, pts, 0, pts->n, 1, use_hint)));
@@ -1416,6 +1495,7 @@ int gf::knn_enqueue_merge(gf_knn_plan* P, const gf_points* pts, void* result, co
     P->pend_idx_base = P->idx_base;  // the index base in force when this window was enqueued
     return GF_OK;
   }
+  if (P->large) return knn_large(P, pts, result);
   // threshold: the previous window's hint (continuous query) or the sample; tiny windows
   // scan to r
   const bool staged = pts->n >= kSampleMinN;
@@ -1521,8 +1601,9 @@ extern "C" int gf_knn_merge_host(int32_t k, int32_t nlists, const int32_t* count
   return GF_OK;
 }
 
-// Re-evaluation of a flagged window: first the sample path with the hint ignored; if that
-// is still inconclusive, exhaustive T = r over capacity-sized partitions merged on the host.
+// Re-evaluation of a flagged window: first the sample path with the hint ignored; if that is
+// still inconclusive, the exact sorted path over every candidate within r (knn_large) -- on the
+// device, like every other result.
 static int knn_fallback(gf_knn_plan* P, const gf_points* pts, int64_t* oo, double* od, int64_t* oi, int32_t* n_out) {
   gf_ctx* ctx = P->ctx;
   const size_t rb = gf_knn_result_bytes(P->k);
@@ -1534,25 +1615,15 @@ static int knn_fallback(gf_knn_plan* P, const gf_points* pts, int64_t* oo, doubl
   };
   int st = gf_knn_plan_flush(P);  // lane 0 is free afterwards
   if (st) return st;
-  if (pts->n >= kSampleMinN) {
+  if (!P->poly && pts->n >= kSampleMinN) {
     if ((st = knn_launch_sample(P, 0, pts, 0)) ||
         (st = knn_scan_select(P, 0, pts, 0, pts->n, 1, P->use_hint, P->tmp_result)) || (st = fetch()))
       return st;
     if (h->status == 0) return gf_knn_decode(P, pts, P->host_result, oo, od, oi, n_out);
   }
-  const int64_t part = std::max<int64_t>(2, P->cap & ~(int64_t)1);
-  std::vector<Ent> all;
-  for (int64_t lo = 0; lo < pts->n; lo += part) {
-    const int64_t hi = std::min(pts->n, lo + part);
-    if ((st = knn_scan_select(P, 0, pts, lo, hi, 0, 0, P->tmp_result)) || (st = fetch())) return st;
-    if (h->status != 0) return set_err(ctx, GF_ERR_HIP, "kNN partition did not converge");
-    const double* d = (const double*)(h + 1);
-    const int64_t* o = (const int64_t*)(d + P->k);
-    const int64_t* i = o + P->k;
-    for (int32_t j = 0; j < h->n; ++j) all.push_back({d[j], o[j], i[j]});
-  }
-  merge_lists(P->k, all, oo, od, oi, n_out);
-  return GF_OK;
+  if ((st = knn_large(P, pts, P->tmp_result)) || (st = fetch())) return st;
+  if (h->status != 0) return set_err(ctx, GF_ERR_HIP, "kNN exact path did not converge");
+  return gf_knn_decode(P, pts, P->host_result, oo, od, oi, n_out);
 }
 
 extern "C" int gf_knn_decode(gf_knn_plan* P, const gf_points* pts, const void* result_host, int64_t* oo,

@@ -398,6 +398,27 @@ hipError_t launch_pane_bounds(hipStream_t s, const int64_t* ts, int64_t n, int64
 hipError_t launch_knn_sample(gf_ctx* ctx, const KnnSampleArgs& a);
 hipError_t launch_knn_scan(gf_ctx* ctx, const KnnScanArgs& a, int blocks, int unroll, int nt);
 hipError_t launch_knn_select(gf_ctx* ctx, const KnnSelectArgs& a);
+// k > kMaxK: candidate sorts (k_knn.hip).  op 0 iota perm, 1 key field -> keys, 2 first-of-objID
+// flags, 3 compact flagged perm entries to out, 4 the record
+struct KnnLargeArgs {
+  const double* cd;
+  const int64_t* co;
+  const uint32_t* ci;
+  uint32_t* perm;
+  int64_t m;
+  int field;
+  uint32_t* keys;
+  uint32_t* flag;
+  const uint32_t* off;
+  uint32_t* out;
+  const uint32_t* nsurv;
+  int32_t k;
+  double T;
+  int64_t idx_base;
+  void* result;
+};
+hipError_t launch_knn_large(gf_ctx* ctx, int op, const KnnLargeArgs& a);
+constexpr int32_t kMaxKLarge = 1 << 24;  // largest k of the sorted (k > kMaxK) path
 
 hipError_t launch_knn_poly_sample(gf_ctx* ctx, const KnnPolyArgs& a);
 hipError_t launch_knn_poly_scan(gf_ctx* ctx, const KnnPolyArgs& a, int blocks);  // prefilter + refine
@@ -643,6 +664,7 @@ struct gf_knn_plan {
   int scan_blocks = 0;   // tuning: 0 = auto (4 blocks per CU)
   int scan_unroll = 1;   // point pairs per lane per iteration (tools/tune_knn.py sweep)
   int scan_nt = 1;       // nontemporal loads
+  int large = 0;         // k > kMaxK: every candidate within r, sorted (knn_large)
   // polygon query (gf_knn_ppoly_plan_create): device copy of the polygon, depth 1 only
   int poly = 0, approx = 0;
   int32_t* ring_off = nullptr;

@@ -717,6 +717,108 @@ __global__ __launch_bounds__(kSelT) void knn_select_kernel(KnnSelectArgs a) {
   knn_select_body<SelFull, true>(a, L);
 }
 
+// ---------------------------------------------------------------------------------------
+// k > kMaxK (the reference's PriorityQueue takes any k, KNNQuery.java:216): every candidate
+// within r is kept (T = r, capacity >= window), then two stable LSD radix sorts over 32-bit key
+// fields of the candidate permutation -- (objID, d, idx) to keep each objID's first occurrence,
+// then the survivors by (d, objID, idx) -- and the first k are the record.  Kernels below; the
+// driver (api.cpp knn_large) reuses the K2 radix passes (k_points.hip).
+// ---------------------------------------------------------------------------------------
+// field: 0 idx, 1 d low word, 2 d high word (d >= 0: IEEE bits order as values), 3 objID low
+// word, 4 objID high word with the sign bit flipped (signed order)
+__global__ __launch_bounds__(kBlock) void knn_large_key_kernel(const double* __restrict__ cd,
+                                                               const int64_t* __restrict__ co,
+                                                               const uint32_t* __restrict__ ci,
+                                                               const uint32_t* __restrict__ perm, int64_t m,
+                                                               int field, uint32_t* __restrict__ kout) {
+  for (int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x; j < m; j += (int64_t)gridDim.x * kBlock) {
+    const uint32_t p = perm[j];
+    uint32_t v;
+    switch (field) {
+      case 0: v = ci[p]; break;
+      case 1: v = lo32(cd[p]); break;
+      case 2: v = hi32(cd[p]); break;
+      case 3: v = (uint32_t)(uint64_t)co[p]; break;
+      default: v = (uint32_t)((uint64_t)co[p] >> 32) ^ 0x80000000u; break;
+    }
+    kout[j] = v;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void knn_large_iota_kernel(uint32_t* __restrict__ perm, int64_t m) {
+  for (int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x; j < m; j += (int64_t)gridDim.x * kBlock)
+    perm[j] = (uint32_t)j;
+}
+
+// in (objID, d, idx) order: the first entry of every objID is its minimum -- the one the
+// reference's merge keeps (KNNQuery.java:232-251)
+__global__ __launch_bounds__(kBlock) void knn_large_first_kernel(const int64_t* __restrict__ co,
+                                                                 const uint32_t* __restrict__ perm, int64_t m,
+                                                                 uint32_t* __restrict__ flag) {
+  for (int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x; j < m; j += (int64_t)gridDim.x * kBlock)
+    flag[j] = j == 0 || co[perm[j]] != co[perm[j - 1]];
+}
+
+__global__ __launch_bounds__(kBlock) void knn_large_compact_kernel(const uint32_t* __restrict__ perm,
+                                                                   const uint32_t* __restrict__ flag,
+                                                                   const uint32_t* __restrict__ off, int64_t m,
+                                                                   uint32_t* __restrict__ out) {
+  for (int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x; j < m; j += (int64_t)gridDim.x * kBlock)
+    if (flag[j]) out[off[j]] = perm[j];
+}
+
+// the record: header + the first min(k, survivors) entries in (d, objID, idx) order
+__global__ __launch_bounds__(kBlock) void knn_large_record_kernel(const double* __restrict__ cd,
+                                                                  const int64_t* __restrict__ co,
+                                                                  const uint32_t* __restrict__ ci,
+                                                                  const uint32_t* __restrict__ perm,
+                                                                  const uint32_t* __restrict__ nsurv, int32_t k,
+                                                                  int64_t m, double T, int64_t idx_base,
+                                                                  void* result) {
+  gf_knn_header* h = reinterpret_cast<gf_knn_header*>(result);
+  const int32_t n = (int64_t)*nsurv < (int64_t)k ? (int32_t)*nsurv : k;
+  double* rd = reinterpret_cast<double*>(h + 1);
+  int64_t* ro = reinterpret_cast<int64_t*>(rd + k);
+  int64_t* ri = ro + k;
+  for (int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x; j < n; j += (int64_t)gridDim.x * kBlock) {
+    const uint32_t p = perm[j];
+    rd[j] = cd[p];
+    ro[j] = co[p];
+    ri[j] = (int64_t)ci[p] + idx_base;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    h->status = 0;
+    h->n = n;
+    h->k = k;
+    h->flags = 0;
+    h->candidates = m;
+    h->threshold = T;
+  }
+}
+
+static unsigned large_blocks(int64_t items) {
+  const int64_t b = (items + kBlock - 1) / kBlock;
+  return (unsigned)(b < 1 ? 1 : (b > 2048 ? 2048 : b));
+}
+
+hipError_t launch_knn_large(gf_ctx* ctx, int op, const KnnLargeArgs& a) {
+  hipStream_t s = ctx->stream;
+  const dim3 g(large_blocks(a.m)), b(kBlock);
+  switch (op) {
+    case 0: hipLaunchKernelGGL(knn_large_iota_kernel, g, b, 0, s, a.perm, a.m); break;
+    case 1: hipLaunchKernelGGL(knn_large_key_kernel, g, b, 0, s, a.cd, a.co, a.ci, a.perm, a.m, a.field, a.keys); break;
+    case 2: hipLaunchKernelGGL(knn_large_first_kernel, g, b, 0, s, a.co, a.perm, a.m, a.flag); break;
+    case 3: hipLaunchKernelGGL(knn_large_compact_kernel, g, b, 0, s, a.perm, a.flag, a.off, a.m, a.out); break;
+    default: {
+      const dim3 gr(large_blocks(a.k));
+      hipLaunchKernelGGL(knn_large_record_kernel, gr, b, 0, s, a.cd, a.co, a.ci, a.perm, a.nsurv, a.k, a.m, a.T,
+                         a.idx_base, a.result);
+      break;
+    }
+  }
+  return hipGetLastError();
+}
+
 hipError_t launch_knn_select(gf_ctx* ctx, const KnnSelectArgs& a) {
   KTimer t(ctx, GF_K_KNN_SELECT);
   hipLaunchKernelGGL(knn_select_kernel, dim3(1), dim3(kSelT), 0, ctx->stream, a);

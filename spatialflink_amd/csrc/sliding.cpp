@@ -93,6 +93,7 @@ extern "C" int gf_knn_sliding_create(gf_knn_plan* plan, int64_t size_ms, int64_t
   if (!plan || !out || size_ms <= 0 || slide_ms <= 0) return GF_ERR_ARG;
   *out = nullptr;
   gf_ctx* ctx = plan->ctx;
+  if (plan->k > kMaxK) return set_err(ctx, GF_ERR_ARG, "gf_knn_sliding_create: k <= 512 (pane records are merged)");
   const int64_t pane = std::gcd(size_ms, slide_ms);
   const int64_t W = size_ms / pane, S = slide_ms / pane;
   if (W > kMaxMergeRecs)

@@ -1,0 +1,93 @@
+"""GPU: kNN with k > 512 (the reference's PriorityQueue takes any k, KNNQuery.java:216).  Such
+plans keep every candidate within r and derive the record from two stable device radix sorts
+((objID, d, idx) -> first of each objID -> (d, objID, idx)); the exact re-evaluation of a
+flagged window takes the same path.  Results == the oracle's contract (orc_knn_contract /
+orc_knn_ppoly_contract), bit-exact, for point and polygon queries, duplicate objIDs, fewer
+distinct objIDs than k, clustered input; depths 2 / 3 and the sliding engine refuse k > 512."""
+import numpy as np
+import pytest
+
+from conftest import BEIJING, QPOINT
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def sf(gpu):
+    import spatialflink_amd
+
+    return spatialflink_amd
+
+
+def conf(sf):
+    return sf.QueryConfiguration(sf.QueryType.WindowBased)
+
+
+def check(res, oo, od, oi):
+    np.testing.assert_array_equal(res.objID, oo)
+    np.testing.assert_array_equal(res.dist.view(np.int64), od.view(np.int64))
+    np.testing.assert_array_equal(res.idx, oi)
+
+
+@pytest.mark.parametrize("n,grid_n,r,k,dup", [
+    (2_000_001, 500, 0.05, 513, False),
+    (2_000_001, 500, 0.5, 5_000, True),
+    (1_000_000, 100, 0.3, 100_000, True),    # more than the distinct objIDs within r? checked below
+    (300_000, 1000, 0.004, 2_000, False),    # fewer candidates than k
+    (0, 500, 0.5, 1000, False),
+])
+def test_knn_large_k(sf, oracle_mod, n, grid_n, r, k, dup):
+    g = sf.UniformGrid(grid_n, *BEIJING)
+    og = oracle_mod.grid(grid_n, *BEIJING)
+    x, y = oracle_mod.java_random_points(grid_n + k, n, *BEIJING)
+    obj = np.random.default_rng(k).permutation(n).astype(np.int64)
+    if dup:
+        obj %= max(1, n // 7)
+    q = sf.Point("q", *QPOINT, 0, g)
+    res = sf.PointPointKNNQuery(conf(sf), g).run(sf.PointWindow.from_numpy(x, y, obj), q, r, k)
+    st, oo, od, oi = oracle_mod.knn(og, x, y, obj, QPOINT[0], QPOINT[1], r, k)
+    check(res, oo, od, oi)
+    if n == 300_000:
+        assert len(oo) < k
+
+
+def test_knn_large_k_clustered_and_continuous(sf, oracle_mod):
+    g = sf.UniformGrid(500, *BEIJING)
+    og = oracle_mod.grid(500, *BEIJING)
+    q = sf.Point("q", *QPOINT, 0, g)
+    op = sf.PointPointKNNQuery(conf(sf), g)  # one plan, several windows (buffers reused / grown)
+    for seed, n in ((3, 500_000), (4, 1_500_000), (5, 800_000)):
+        x, y = sf.synthetic_clustered(seed, n, *BEIJING, centers=[QPOINT])
+        obj = np.arange(n, dtype=np.int64) % (n // 2)
+        res = op.run(sf.PointWindow.from_numpy(x, y, obj), q, 0.1, 3_000)
+        st, oo, od, oi = oracle_mod.knn(og, x, y, obj, QPOINT[0], QPOINT[1], 0.1, 3_000)
+        check(res, oo, od, oi)
+
+
+def test_polygon_knn_large_k(sf, oracle_mod):
+    g = sf.UniformGrid(500, *BEIJING)
+    og = oracle_mod.grid(500, *BEIJING)
+    h = 0.01
+    ring = [(QPOINT[0] - h, QPOINT[1] - h), (QPOINT[0] + h, QPOINT[1] - h), (QPOINT[0] + h, QPOINT[1] + h),
+            (QPOINT[0] - h, QPOINT[1] + h), (QPOINT[0] - h, QPOINT[1] - h)]
+    P = sf.Polygon([ring], g)
+    x, y = oracle_mod.java_random_points(17, 1_200_000, *BEIJING)
+    obj = (np.arange(len(x)) % 400_000).astype(np.int64)
+    res = sf.PointPolygonKNNQuery(conf(sf), g).run(sf.PointWindow.from_numpy(x, y, obj), P, 0.2, 1_500)
+    m, eo, ed, ei = oracle_mod.knn_ppoly(og, x, y, obj, oracle_mod.Polygons([P.rings]), 0.2, 1_500)
+    check(res, eo, ed, ei)
+
+
+def test_large_k_refuses_pipelines_and_sliding(sf):
+    from spatialflink_amd import _lib
+
+    g = sf.UniformGrid(100, *BEIJING)
+    q = sf.Point("q", *QPOINT, 0, g)
+    op = sf.PointPointKNNQuery(conf(sf), g)
+    with pytest.raises(ValueError):
+        op.set_pipeline(0, q, 0.5, 600, 2)
+    ctx, plan = op.plan(0, q, 0.5, 600)
+    import ctypes as C
+
+    s = C.c_void_p()
+    assert _lib.lib().gf_knn_sliding_create(plan, 10_000, 5_000, C.byref(s)) == _lib.GF_ERR_ARG
