@@ -53,7 +53,7 @@ extern "C" {
 #define GF_K_RANGE_SCAN  3
 #define GF_K_ASSIGN      4
 #define GF_K_JOIN_PROBE  5
-#define GF_K_RANGE_TEST  6  /* deferred candidate tests of the many-object range plans */
+#define GF_K_RANGE_TEST  6  /* point-polygon join passes (the range plans' deferred tests run in the scan) */
 #define GF_K_JOIN_BUCKET 7  /* ordinary-side bucketing of the join */
 #define GF_K_KNN_MERGE   8  /* top-k record merges (shards, sliding-window panes) */
 #define GF_K_CSV_PARSE   9  /* CSV ingest: the per-line parse kernel */

@@ -877,9 +877,6 @@ extern "C" int gf_join_ppoly_plan_create(gf_ctx* ctx, const gf_grid* qgrid, cons
   return ppoly_plan_create(ctx, qgrid, polys, r, approximate, metric, 1, out);
 }
 
-#ifndef GF_TEST_BPC
-#define GF_TEST_BPC 4  // range_test_kernel blocks per CU (4: 28 us vs 31-32 us at 8 or 2, C3)
-#endif
 namespace {
 RangeArgs range_args(const gf_range_plan* P, const gf_points* pts, uint64_t* bitmap, uint64_t* multi) {
   RangeArgs a{};
@@ -941,7 +938,7 @@ int scan_blocks_range(const gf_range_plan* P, int64_t n) {
   // blocks per CU (the sweep in tools/bench_workloads.py: 1024 blocks best at 10M points)
   int blocks = (int)std::min<int64_t>(std::max<int64_t>(n / (4 * 128 * 2 * 2), 1), (int64_t)P->ctx->num_cus * 4);
   if (P->scan_blocks > 0) blocks = P->scan_blocks;
-  return std::min(blocks, 2048);  // range_test_kernel's segment prefix (kMaxSegs)
+  return std::min(blocks, 2048);  // queue segments / partial slots per window
 }
 }  // namespace
 
@@ -966,7 +963,6 @@ extern "C" int gf_range_run(gf_range_plan* P, const gf_points* pts, uint64_t* bi
   const bool defer = can_defer && (P->defer_mode == 2 || (P->defer_mode == 0 && P->cls_cells[1] * 20 > live));
   if (defer) {
     if ((st = ensure_queue(P, a, blocks, false))) return st;
-    a.test_blocks = ctx->num_cus * GF_TEST_BPC;
   }
   // the counts are summed by the last block of the window's last kernel (no finalize launch)
   a.counts = counts;
@@ -1836,6 +1832,13 @@ extern "C" int gf_join_pp(gf_ctx* ctx, const gf_grid* ugrid, const gf_grid* qgri
   GF_HIP_CHECK(ctx, launch_join_probe(ctx, a, 1, blocks));
   GF_HIP_CHECK(ctx, hipStreamSynchronize(s));
   return GF_OK;
+}
+
+// the exact record of one window (any k, status 0), stream-ordered on the context stream
+int gf::knn_exact_record(gf_knn_plan* P, const gf_points* pts, void* result) {
+  int st = gf_knn_plan_flush(P);  // lane 0 is free afterwards
+  if (st) return st;
+  return knn_large(P, pts, result);
 }
 
 // ---------------------------------------------------------------------------------------

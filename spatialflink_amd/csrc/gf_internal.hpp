@@ -259,7 +259,6 @@ struct RangeArgs {
   uint32_t* queue_count;     // [blocks] entries per segment
   double* queue_xy;          // [2 * blocks * seg_cap] the queued points' coordinates
   int64_t seg_cap;           // points one scan block visits at most
-  int test_blocks;
   const uint8_t* rect;       // [npoly] axis-aligned rectangle shells without holes (nullable)
   // point-polygon join: bbox cells per polygon (x0, x1, y0, y1) and the layer counts
   const int32_t* brect;
@@ -419,6 +418,8 @@ struct KnnLargeArgs {
 };
 hipError_t launch_knn_large(gf_ctx* ctx, int op, const KnnLargeArgs& a);
 constexpr int32_t kMaxKLarge = 1 << 24;  // largest k of the sorted (k > kMaxK) path
+// the exact record (status 0) of one window through the sorted path, any k (api.cpp)
+int knn_exact_record(gf_knn_plan* P, const gf_points* pts, void* result);
 
 hipError_t launch_knn_poly_sample(gf_ctx* ctx, const KnnPolyArgs& a);
 hipError_t launch_knn_poly_scan(gf_ctx* ctx, const KnnPolyArgs& a, int blocks);  // prefilter + refine

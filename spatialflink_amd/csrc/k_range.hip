@@ -161,7 +161,8 @@ __device__ __forceinline__ bool test_point(const RangeArgs& a, double px, double
 
 
 // DEFER: candidate-cell points are not tested inline (a wave would serialise on its slowest
-// lane's object list) but appended to a queue that range_test_kernel drains densely.
+// lane's object list) but appended to the block's queue segment, drained densely at the end of
+// the block (drain_own_queue).
 template <int TABLE, int POLY, int DEFER>
 __device__ __forceinline__ void eval_point(const RangeArgs& a, double px, double py, int cls, bool valid, bool& hit,
                                            bool& multi, bool& defer) {
@@ -350,6 +351,71 @@ __device__ __forceinline__ void finalize_counts(const RangeArgs& a, int nparts, 
   }
 }
 
+// One candidate object of a queued point: within r?  (envelope-pruned for exact polygons)
+template <int POLY>
+__device__ __forceinline__ bool test_object(const RangeArgs& a, double px, double py, int32_t o) {
+  if (!POLY) {
+    const double dx = a.qx[o] - px, dy = a.qy[o] - py;
+    return a.metric == 0 ? (dx * dx + dy * dy <= a.s_r) : (fdlibm_hypot(dx, dy) <= a.r);
+  }
+  if (a.approx) return point_bbox_distance(px, py, a.bbox + 4 * o) <= a.r;
+  if (px == px && py == py && env_far(a.bbox + 4 * o, px, py, a.r)) return false;
+  return point_polygon_distance(px, py, a, o) <= a.r;
+}
+
+constexpr int kTestGroup = 8;
+// DEFER 1: after its scan loop, a block drains its OWN queue segment (the candidate-cell points
+// it queued) -- no second launch, no grid-wide prefix of the segment counts.  A queued point is
+// a group of 8 lanes that test its candidate objects in parallel (8 at a time, stopping once one
+// hits), so the dependent chain per point is one object test, not the list length.  Hits are
+// OR-ed into the bitmap words this block stored during the scan: every wave drains its stores
+// (s_waitcnt vmcnt(0): acknowledged by L2) before the barrier, so the atomics land after them.
+// Returns this wave's added hits (wave-uniform).
+template <int POLY>
+__device__ uint64_t drain_own_queue(const RangeArgs& a, const uint32_t& lcount) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const uint32_t total = lcount;
+  const int lane = threadIdx.x & 63, g = lane & (kTestGroup - 1);
+  constexpr int kGroups = kBlock / kTestGroup;
+  const int grp = threadIdx.x / kTestGroup;
+  const uint64_t gmask = ((1ull << kTestGroup) - 1) << (lane & ~(kTestGroup - 1));
+  const size_t seg = (size_t)blockIdx.x * a.seg_cap;
+  uint64_t hits = 0;
+  for (uint32_t e0 = 0; e0 < total; e0 += kGroups) {  // block-uniform
+    const uint32_t e = e0 + grp;
+    const bool valid = e < total;
+    const size_t pos = seg + e;
+    double px = 0.0, py = 0.0;
+    int32_t b = 0, end = 0;
+    if (valid) {
+      px = a.queue_xy[2 * pos];
+      py = a.queue_xy[2 * pos + 1];
+      end = POLY ? a.npoly : a.nq;
+      if (a.cand_off) {
+        const int32_t cell = cell_index(py, a.minY, a.cl) * a.grid_n + cell_index(px, a.minX, a.cl);
+        b = a.cand_off[cell];
+        end = a.cand_off[cell + 1];
+      }
+    }
+    bool hit = false;
+    for (int32_t t = b + g;; t += kTestGroup) {
+      const uint64_t hb = __ballot(hit);  // all lanes: the loop is wave-uniform
+      const bool mine = t < end && !(hb & gmask);
+      if (!__ballot(mine)) break;  // every group of the wave is done
+      if (mine) hit = test_object<POLY>(a, px, py, a.cand_off ? a.cand_list[t] : t);
+    }
+    const bool ghit = (__ballot(hit) & gmask) != 0;
+    const uint64_t won = __ballot(valid && g == 0 && ghit);
+    if (valid && g == 0 && ghit) {
+      const uint32_t i = a.queue[pos];
+      atomicOr((unsigned long long*)&a.bitmap[i >> 6], 1ull << (i & 63));
+    }
+    hits += (uint64_t)__popcll(won);
+  }
+  return hits;
+}
+
 // dynamic-LDS header of range_kernel: lcount, pad, sh[kBlock/64], sm[kBlock/64] (16 B multiple)
 constexpr int kRangeHdrWords = 4 + 2 * 2 * (kBlock / 64);
 #ifndef GF_RANGE_WAVES
@@ -413,6 +479,7 @@ __global__ __launch_bounds__(kBlock, GF_RANGE_WAVES) void range_kernel(RangeArgs
     range_stage<TABLE, POLY, DEFER, U>(a, L, A, ta, B, ta + sstride, tstride, hits, mult, &lcount);
     range_stage<TABLE, POLY, DEFER, U>(a, L, B, ta + sstride, A, ta + 2 * sstride, tstride, hits, mult, &lcount);
   }
+  if (DEFER == 1) hits += drain_own_queue<POLY>(a, lcount);
   // per-block partial counts (plain stores; summed by range_finalize)
   const int wid = threadIdx.x >> 6;
   if ((threadIdx.x & 63) == 0) { sh[wid] = hits; sm[wid] = mult; }
@@ -422,120 +489,11 @@ __global__ __launch_bounds__(kBlock, GF_RANGE_WAVES) void range_kernel(RangeArgs
     for (int w = 0; w < kBlock / 64; ++w) { th += sh[w]; tm += sm[w]; }
     store_partial(&a.partials[2 * blockIdx.x], th);
     store_partial(&a.partials[2 * blockIdx.x + 1], th + tm * (uint64_t)(a.nq > 1 ? a.nq - 1 : 0));
-    if (DEFER) a.queue_count[blockIdx.x] = lcount;
+    if (DEFER == 2) a.queue_count[blockIdx.x] = lcount;
   }
-  // no deferred tests follow: this kernel's last block sums the window's counts (sh / sm are
-  // free again after the partials, lds_base[1] is header padding)
-  if (!DEFER && a.counts) finalize_counts(a, gridDim.x, &lds_base[1], sh);
-}
-
-// One candidate object of a queued point: within r?  (envelope-pruned for exact polygons)
-template <int POLY>
-__device__ __forceinline__ bool test_object(const RangeArgs& a, double px, double py, int32_t o) {
-  if (!POLY) {
-    const double dx = a.qx[o] - px, dy = a.qy[o] - py;
-    return a.metric == 0 ? (dx * dx + dy * dy <= a.s_r) : (fdlibm_hypot(dx, dy) <= a.r);
-  }
-  if (a.approx) return point_bbox_distance(px, py, a.bbox + 4 * o) <= a.r;
-  if (px == px && py == py && env_far(a.bbox + 4 * o, px, py, a.r)) return false;
-  return point_polygon_distance(px, py, a, o) <= a.r;
-}
-
-// Drains the candidate queue (the scan blocks' segments).  A queued point is a group of 8
-// lanes that test the point's candidate objects in parallel (8 at a time, stopping once one
-// hits), so the dependent chain per point is one object test, not the list length; and the
-// entries of all segments are dealt out over the whole grid (a block-local prefix of the
-// segment counts in LDS) so the queue is drained in one round of dependent loads.  Hits are
-// OR-ed into the bitmap the scan wrote (stream-ordered after it); partials go to slots
-// [part_base + block].
-constexpr int kTestGroup = 8;
-constexpr int kMaxSegs = 2048;  // scan blocks <= 8 per CU
-template <int POLY>
-__global__ __launch_bounds__(kBlock) void range_test_kernel(RangeArgs a, int part_base) {
-  __shared__ uint64_t wsum_fin[2 * (kBlock / 64)];
-  __shared__ uint32_t pre[kMaxSegs + 1];
-  __shared__ uint32_t wsum[kBlock / 64];
-  const int lane = threadIdx.x & 63, g = lane & (kTestGroup - 1);
-  constexpr int kGroups = kBlock / kTestGroup;
-  const int grp = threadIdx.x / kTestGroup;
-  const uint64_t gmask = ((1ull << kTestGroup) - 1) << (lane & ~(kTestGroup - 1));
-  // exclusive prefix of the segment counts (kMaxSegs / kBlock = 8 per thread)
-  constexpr int kPer = kMaxSegs / kBlock;
-  uint32_t v[kPer], sum = 0;
-#pragma unroll
-  for (int j = 0; j < kPer; ++j) {
-    const int sgi = threadIdx.x * kPer + j;
-    v[j] = sgi < part_base ? a.queue_count[sgi] : 0u;
-    sum += v[j];
-  }
-  uint32_t inc = sum;
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const uint32_t t = __shfl_up(inc, off, 64);
-    if (lane >= off) inc += t;
-  }
-  if (lane == 63) wsum[threadIdx.x >> 6] = inc;
-  __syncthreads();
-  uint32_t run = inc - sum;
-  for (int w = 0; w < (int)(threadIdx.x >> 6); ++w) run += wsum[w];
-#pragma unroll
-  for (int j = 0; j < kPer; ++j) {
-    pre[threadIdx.x * kPer + j] = run;
-    run += v[j];
-  }
-  if (threadIdx.x == kBlock - 1) pre[kMaxSegs] = run;
-  __syncthreads();
-  const uint32_t total = pre[kMaxSegs];
-  uint64_t hits = 0;
-  for (uint32_t e0 = blockIdx.x * kGroups; e0 < total; e0 += gridDim.x * kGroups) {  // block-uniform
-    const uint32_t e = e0 + grp;
-    const bool valid = e < total;
-    size_t pos = 0;
-    double px = 0.0, py = 0.0;
-    int32_t b = 0, end = 0;
-    if (valid) {
-      int lo = 0, hi = kMaxSegs;  // last segment with pre[seg] <= e
-      while (hi - lo > 1) {
-        const int mid = (lo + hi) >> 1;
-        if (pre[mid] <= e) lo = mid; else hi = mid;
-      }
-      pos = (size_t)lo * a.seg_cap + (e - pre[lo]);
-      px = a.queue_xy[2 * pos];
-      py = a.queue_xy[2 * pos + 1];
-      end = POLY ? a.npoly : a.nq;
-      if (a.cand_off) {
-        const int32_t cell = cell_index(py, a.minY, a.cl) * a.grid_n + cell_index(px, a.minX, a.cl);
-        b = a.cand_off[cell];
-        end = a.cand_off[cell + 1];
-      }
-    }
-    bool hit = false;
-    for (int32_t t = b + g;; t += kTestGroup) {
-      const uint64_t hb = __ballot(hit);  // all lanes: the loop is wave-uniform
-      const bool mine = t < end && !(hb & gmask);
-      if (!__ballot(mine)) break;  // every group of the wave is done
-      if (mine) hit = test_object<POLY>(a, px, py, a.cand_off ? a.cand_list[t] : t);
-    }
-    const bool ghit = (__ballot(hit) & gmask) != 0;
-    if (valid && g == 0 && ghit) {
-      const uint32_t i = a.queue[pos];
-      atomicOr((unsigned long long*)&a.bitmap[i >> 6], 1ull << (i & 63));
-      ++hits;
-    }
-  }
-  __shared__ uint64_t sh[kBlock];
-  sh[threadIdx.x] = hits;
-  __syncthreads();
-  for (int s = kBlock / 2; s > 0; s >>= 1) {
-    if (threadIdx.x < s) sh[threadIdx.x] += sh[threadIdx.x + s];
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) {
-    store_partial(&a.partials[2 * (part_base + blockIdx.x)], sh[0]);
-    store_partial(&a.partials[2 * (part_base + blockIdx.x) + 1], sh[0]);
-  }
-  __shared__ uint32_t s_flag;
-  if (a.counts) finalize_counts(a, part_base + gridDim.x, &s_flag, reinterpret_cast<uint64_t*>(wsum_fin));
+  // no kernel follows (the join's passes do for DEFER 2): this kernel's last block sums the
+  // window's counts (sh / sm are free again after the partials, lds_base[1] is header padding)
+  if (DEFER != 2 && a.counts) finalize_counts(a, gridDim.x, &lds_base[1], sh);
 }
 
 #ifndef GF_RANGE_U
@@ -819,11 +777,7 @@ hipError_t launch_range(gf_ctx* ctx, const RangeArgs& a, int table_mode, int pol
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
-  if (!defer) return hipSuccess;
-  KTimer t(ctx, GF_K_RANGE_TEST);
-  if (poly) hipLaunchKernelGGL(range_test_kernel<1>, dim3(a.test_blocks), b, 0, ctx->stream, a, blocks);
-  else hipLaunchKernelGGL(range_test_kernel<0>, dim3(a.test_blocks), b, 0, ctx->stream, a, blocks);
-  return hipGetLastError();
+  return hipSuccess;  // deferred tests: drained by each scan block at its end (drain_own_queue)
 }
 
 }  // namespace gf

@@ -212,37 +212,43 @@ extern "C" int gf_knn_sliding_decode(gf_knn_sliding* s, int64_t window_end, cons
   gf_knn_plan* P = s->plan;
   const gf_knn_header* h = (const gf_knn_header*)result_host;
   if (h->status == 0) return gf_knn_decode(P, nullptr, result_host, oo, od, oi, n_out);
-  // a pane overflowed its candidate buffer or its threshold guess failed: evaluate each pane of
-  // the window exactly (the plan's decode fallback) and merge on the host
+  // a pane overflowed its candidate buffer or its threshold guess failed: each pane of the
+  // window exactly (the plan's sorted exact path) into device records, merged on the device
   const int64_t p = floor_div(window_end, s->pane_ms) - 1;
   int st = gf_knn_sliding_flush(s);
   if (st) return st;
-  std::vector<int32_t> counts;
-  std::vector<int64_t> o, i;
-  std::vector<double> d;
+  gf_ctx* ctx = P->ctx;
   const int32_t k = P->k;
-  std::vector<int64_t> to(k), ti(k);
-  std::vector<double> td(k);
+  const size_t rb = gf_knn_result_bytes(k);
+  char* recs = nullptr;
+  GF_HIP_CHECK(ctx, hipMalloc(&recs, rb * (size_t)(s->W + 1)));
+  char* merged = recs + rb * (size_t)s->W;
   const int64_t saved_base = P->idx_base;
-  for (int64_t q = p - s->W + 1; q <= p; ++q) {
+  int32_t nrec = 0;
+  for (int64_t q = p - s->W + 1; q <= p && !st; ++q) {
     if (q < s->first) continue;  // before the stream: empty
     const gf_knn_sliding::Pane& pn = slot(s, q);
     if (pn.index != q) {
-      P->idx_base = saved_base;
-      return set_err(P->ctx, GF_ERR_ARG, "gf_knn_sliding_decode: the window's panes left the ring");
+      st = set_err(ctx, GF_ERR_ARG, "gf_knn_sliding_decode: the window's panes left the ring");
+      break;
     }
     if (pn.pts.n == 0) continue;
-    int32_t m = 0;
     P->idx_base = pn.base;
-    if ((st = gf_knn_run(P, &pn.pts, to.data(), td.data(), ti.data(), &m))) {
-      P->idx_base = saved_base;
-      return st;
-    }
-    counts.push_back(m);
-    o.insert(o.end(), to.begin(), to.begin() + m);
-    d.insert(d.end(), td.begin(), td.begin() + m);
-    i.insert(i.end(), ti.begin(), ti.begin() + m);
+    st = knn_exact_record(P, &pn.pts, recs + rb * (size_t)nrec);
+    ++nrec;
   }
   P->idx_base = saved_base;
-  return gf_knn_merge_host(k, (int32_t)counts.size(), counts.data(), o.data(), d.data(), i.data(), oo, od, oi, n_out);
+  if (!st && nrec > 0) st = gf_knn_merge_dev(ctx, k, recs, nrec, merged);
+  if (!st && nrec > 0) {
+    if (hipMemcpyAsync(P->host_result, merged, rb, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
+        hipStreamSynchronize(ctx->stream) != hipSuccess)
+      st = set_err(ctx, GF_ERR_HIP, "gf_knn_sliding_decode: copy");
+  }
+  hipFree(recs);
+  if (st) return st;
+  if (nrec == 0) {
+    *n_out = 0;
+    return GF_OK;
+  }
+  return gf_knn_decode(P, nullptr, P->host_result, oo, od, oi, n_out);
 }
