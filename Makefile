@@ -17,7 +17,7 @@ all: $(LIB) oracle
 
 $(OBJDIR)/%.o: $(SRC)/% $(HEADERS)
 	@mkdir -p $(OBJDIR)
-	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
+	$(HIPCC) $(HIPFLAGS) $(GF_DEFS) -x hip -c $< -o $@
 
 $(LIB): $(OBJECTS)
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(OBJECTS)

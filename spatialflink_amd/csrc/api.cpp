@@ -1062,7 +1062,7 @@ extern "C" int gf_bitmap_to_indices_async(gf_ctx* ctx, const uint64_t* bitmap, i
     return set_err(ctx, GF_ERR_ARG, "gf_bitmap_to_indices_async: bad argument");
   int st = bind(ctx);
   if (st) return st;
-  const int64_t words = (n + 63) / 64, blocks = (words + kBlock - 1) / kBlock;
+  const int64_t words = (n + 63) / 64, blocks = expand_blocks(words);
   if (!ctx->expand_ticket) {
     GF_HIP_CHECK(ctx, hipMalloc(&ctx->expand_ticket, sizeof(unsigned long long)));
     GF_HIP_CHECK(ctx, hipMemset(ctx->expand_ticket, 0, sizeof(unsigned long long)));

@@ -16,7 +16,7 @@ __device__ __forceinline__ void two_sum(double a, double b, double& s, double& e
   e = (a - av) + (b - bv);
 }
 // exact sign of x1*y2 - y1*x2 (what JTS RobustDeterminant.signOfDet2x2 returns)
-static __device__ __noinline__ int sign_det2x2(double x1, double y1, double x2, double y2) {
+static __device__ __forceinline__ int sign_det2x2(double x1, double y1, double x2, double y2) {
   const double p1 = x1 * y2, e1 = fma(x1, y2, -p1);
   const double p2 = y1 * x2, e2 = fma(y1, x2, -p2);
   const double terms[4] = {e1, -e2, p1, -p2};
@@ -43,7 +43,7 @@ static __device__ __noinline__ int sign_det2x2(double x1, double y1, double x2, 
 constexpr int kLocInterior = 0, kLocBoundary = 1, kLocExterior = 2;
 
 // RayCrossingCounter.locatePointInRing (JTS 1.16) behind PointLocator's envelope test
-static __device__ __noinline__ int locate_in_ring(double px, double py, const double* vx, const double* vy, int nv,
+static __device__ __forceinline__ int locate_in_ring(double px, double py, const double* vx, const double* vy, int nv,
                               const double* env) {
   if (px > env[1] || px < env[0] || py > env[3] || py < env[2]) return kLocExterior;
   int crossings = 0;
@@ -89,8 +89,10 @@ static __device__ inline double env_point_distance(const double* e, double px, d
   return sqrt(dx * dx + dy * dy);
 }
 
-// DistanceOp(point, polygon): containment (shell, holes), then min facet distance
-static __device__ __noinline__ double polygon_distance(double px, double py, const PolyView& a, int p) {
+// DistanceOp(point, polygon): containment (shell, holes), then min facet distance.  Inlined
+// like its helpers: as calls, the ABI's callee-saved registers and stack cost every kernel that
+// tests polygons (the range scan with its deferred drain: 101 -> 87 VGPRs, 5 waves/SIMD).
+static __device__ __forceinline__ double polygon_distance(double px, double py, const PolyView& a, int p) {
   const int r0 = a.ring_off[p], r1 = a.ring_off[p + 1];
   if (a.rect && a.rect[p]) {
     // one-ring axis-aligned rectangle: PointLocator's interior-or-boundary is exactly the

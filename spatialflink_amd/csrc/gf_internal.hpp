@@ -300,6 +300,8 @@ struct ExpandState {
   unsigned long long* status;  // [blocks] epoch-tagged aggregate / inclusive prefix
   uint32_t epoch;
 };
+constexpr int kExpandWords = 1024;  // bitmap words (= threads) per expand_async block
+int64_t expand_blocks(int64_t words);
 hipError_t launch_expand_bitmap_async(hipStream_t s, const uint64_t* bitmap, int64_t words, int64_t n, uint32_t* idx,
                                       int64_t cap, int64_t* count, const ExpandState& st);
 

@@ -17,6 +17,11 @@
 #include "gf_geom.hpp"
 #include "gf_internal.hpp"
 
+// range_kernel<1, 1, 0, U> (inline polygon tests, a tuning fallback to the deferred queue): the
+// inlined JTS code is too large for range_stage's tile unroll, which then stays a loop; that
+// variant is slower anyway, and calls (the alternative) cost it more registers than the loop.
+#pragma clang diagnostic ignored "-Wpass-failed"
+
 namespace gf {
 
 // DistanceOp(point, polygon) of polygon p of the plan's set (gf_geom.hpp)

@@ -42,10 +42,8 @@ def work_bands(n_cols: int, world: int, col_points, col_candidates=None, candida
     return column_bands(n_cols, world, w)
 
 
-def candidate_columns(grid, cx, cy, bboxes, r):
-    """Per-column count of the points that lie in a cell touched by some query object's bbox
-    expanded by r (the cells a range / join plan tests exactly) -- the candidate term of
-    work_bands.  bboxes: [m, 4] (x1, y1, x2, y2)."""
+def _hit_cells(grid, bboxes, r):
+    """[n, n] (row-major by cy): cells touched by some query object's bbox expanded by r."""
     n = grid.getNumGridPartitions()
     cl = grid.getCellLength()
     hit = np.zeros((n, n), dtype=bool)
@@ -56,6 +54,21 @@ def candidate_columns(grid, cx, cy, bboxes, r):
         b1 = min(int(np.floor((y2 + r - grid.getMinY()) / cl)), n - 1)
         if a0 <= a1 and b0 <= b1:
             hit[b0:b1 + 1, a0:a1 + 1] = True
+    return hit
+
+
+def candidate_cells_per_column(grid, bboxes, r):
+    """Per-column number of cells the plan tests exactly: with uniform points, the expected
+    candidate term of work_bands is this times the points per cell."""
+    return _hit_cells(grid, bboxes, r).sum(axis=0)
+
+
+def candidate_columns(grid, cx, cy, bboxes, r):
+    """Per-column count of the points that lie in a cell touched by some query object's bbox
+    expanded by r (the cells a range / join plan tests exactly) -- the candidate term of
+    work_bands.  bboxes: [m, 4] (x1, y1, x2, y2)."""
+    n = grid.getNumGridPartitions()
+    hit = _hit_cells(grid, bboxes, r)
     cx = np.asarray(cx, np.int64)
     cy = np.asarray(cy, np.int64)
     ok = (cx >= 0) & (cy >= 0) & (cx < n) & (cy < n)

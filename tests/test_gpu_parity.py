@@ -879,10 +879,11 @@ def test_range_windows_in_flight_on_two_contexts(sf, oracle_mod):
             L.gf_range_plan_destroy(h)
 
 
-@pytest.mark.parametrize("n", [1, 63, 64, 65, 1_000_000, 10_000_001])
+@pytest.mark.parametrize("n", [1, 63, 64, 65, 1_000_000, 10_000_001, 40_000_003])
 def test_bitmap_to_indices_async(sf, n):
     """One-launch async expansion == the synchronous one (ascending indices, count on the
-    device, indices past cap not written), on random bitmaps of every density."""
+    device, indices past cap not written, bits past n ignored), on random bitmaps of every
+    density; 40M points = 1221 blocks, so the look-back walks more than one 512-block round."""
     import ctypes as C
 
     import torch
@@ -894,9 +895,9 @@ def test_bitmap_to_indices_async(sf, n):
     words = (n + 63) // 64
     for dens in (0.0, 0.01, 0.5, 1.0):
         bits = rng.random(words * 64) < dens
-        bits[n:] = False
+        bits[n:] = dens == 1.0  # the last word's bits past n are ignored
         bm = torch.from_numpy(np.packbits(bits.reshape(-1, 8)[:, ::-1]).view(np.int64).copy()).cuda()
-        exp = np.flatnonzero(bits)
+        exp = np.flatnonzero(bits[:n])
         for cap in (len(exp), max(len(exp) // 2, 0)):
             idx = torch.full((max(cap, 1),), -1, dtype=torch.int32, device="cuda")
             cnt = torch.full((1,), -7, dtype=torch.int64, device="cuda")

@@ -143,7 +143,11 @@ def bench_range(args, polygons=False):
     """C1 / C3 range windows.  N > 1: weak scaling -- each rank holds the per-GPU window share
     (1M / 10M points) in its cell-column band and evaluates it with the full query set (query
     points / polygons replicated); hits need no exchange (each point is owned by one rank), so
-    there is no collective in the data path.  value = points of all ranks / max elapsed."""
+    there is no collective in the data path.  value = points of all ranks / max elapsed.
+    C3 at N > 1: the global window (N x 10M uniform points) is cut into bands balanced by WORK
+    (sharding.work_bands: a point scan + 8 scans per point in a cell the plan tests exactly) --
+    the 1000 polygons sit in the first ~37 of 500 columns, so even column bands would leave
+    that work on rank 0 and the other ranks idle; a rank holds its band's share of the points."""
     import torch
 
     import spatialflink_amd as sf
@@ -163,12 +167,27 @@ def bench_range(args, polygons=False):
         og = O.grid(grid_n, *BEIJING)
         # enough distinct windows that their x, y (16 B/point) exceed the 256 MB Infinity Cache:
         # every window is then read from HBM, not from the last window's residue
-        nwin = max(4, -(-384 * 2**20 // (16 * n)))
-        wins = _windows(sf, n, nwin, 7 + 1000 * rank, dev, _band(sf, grid, grid_n, world, rank))
-        ctx = _lib.context(dev)
         r = 0.001 if polygons else args.radius
+        band = _band(sf, grid, grid_n, world, rank)
+        n_total = n * world
         if polygons:
             raw = O.generate_query_polygons(1000, BEIJING[0], BEIJING[2], BEIJING[1], BEIJING[3])
+            if world > 1:
+                from spatialflink_amd import sharding
+
+                bb = [(min(p_[0] for p_ in rg[0]), min(p_[1] for p_ in rg[0]), max(p_[0] for p_ in rg[0]),
+                       max(p_[1] for p_ in rg[0])) for rg in raw]
+                per_cell = n_total / float(grid_n * grid_n)
+                bands = sharding.work_bands(grid_n, world, np.full(grid_n, n_total / grid_n),
+                                            sharding.candidate_cells_per_column(grid, bb, r) * per_cell,
+                                            candidate_cost=8.0)
+                lo, hi = bands[rank]
+                band = sharding.band_x_range(grid, lo, hi)
+                n = max(128, int(round(n_total * (hi - lo) / grid_n)))
+        nwin = max(4, -(-384 * 2**20 // (16 * n)))
+        wins = _windows(sf, n, nwin, 7 + 1000 * rank, dev, band)
+        ctx = _lib.context(dev)
+        if polygons:
             polys = [sf.Polygon(rings, grid) for rings in raw]
             ps = sf.PolygonSet(polys)
             cs = ps.c_struct()
@@ -285,16 +304,19 @@ def bench_range(args, polygons=False):
               else f"range_pp_r{r}_{n // 1_000_000}Mpts_grid{grid_n}")
         if world > 1:
             wl += f"_per_gpu_x{world}"
-        _line("point-polygon range" if polygons else "point-point range", world * n * args.steps / elapsed,
+        n_all = int(_reduce_sum(float(n), world, args, dev)) if world > 1 else n
+        _line("point-polygon range" if polygons else "point-point range", n_all * args.steps / elapsed,
               "points/s", args.steps, args.warmup, elapsed,
               "range_kernel + range_test_kernel" if tcnt else "range_kernel", 16.0 * n + n / 8.0 + 4.0 * hits, avg,
               {"n_gpus": world,
-               "config": {"workload": wl, "points_per_window": n * world, "points_per_gpu": n, "grid": grid_n,
+               "config": {"workload": wl, "points_per_window": n_all, "points_per_gpu": n, "grid": grid_n,
                           "radius": r, "hits_window0": hits, "scan_blocks": blocks, "defer_mode": dmode,
                           "windows_in_flight": nstreams, "distinct_windows": nwin,
                           "window_set_MB": round(16.0 * n * nwin / 2**20, 1),
                           "step": "gf_range_run (bitmap + counts) + gf_bitmap_to_indices_async (index list)",
-                          "parallelism": f"cell-column shards x{world} (no collective)",
+                          "parallelism": f"cell-column shards x{world} (no collective)" + (
+                              ", bands balanced by work (points + 8 x candidate-cell points)"
+                              if polygons and world > 1 else ""),
                           "cells_none_candidate_guaranteed_inside": [c.value for c in cells]},
                "breakdown": {"scan_us": round(avg_scan * 1e6, 2), "test_us": round(avg_test * 1e6, 2),
                              "achieved_basis": basis},
