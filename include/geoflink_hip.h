@@ -128,8 +128,10 @@ int         gf_ctx_join(gf_ctx* ctx);
 int         gf_ctx_fork(gf_ctx* ctx);
 const char* gf_ctx_last_error(gf_ctx* ctx);
 /* Context flags (testing / tuning).  GF_FLAG_JOIN_LEGACY: 1 = gf_join_pp probes the query
- * buckets from global memory in input order instead of the row-bucketed LDS path. */
+ * buckets from global memory in input order instead of the row-bucketed LDS path.
+ * GF_FLAG_JOIN_COARSE: 1 = the row-bucketed path never takes its sub-cell (fine) variant. */
 #define GF_FLAG_JOIN_LEGACY 1
+#define GF_FLAG_JOIN_COARSE 2
 int gf_ctx_set_flag(gf_ctx* ctx, int flag, int value);
 
 /* Record HIP events around launches of the kernels in `mask` (bit 1 << GF_K_*; 0 = off). */

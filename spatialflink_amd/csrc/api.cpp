@@ -255,6 +255,7 @@ extern "C" void gf_ctx_destroy(gf_ctx* ctx) {
   if (ctx->dict) gf_objid_dict_destroy(ctx->dict);
   if (ctx->expand_ticket) hipFree(ctx->expand_ticket);
   if (ctx->expand_status) hipFree(ctx->expand_status);
+  if (ctx->join_ticket) hipFree(ctx->join_ticket);
   for (auto& e : ctx->pending) { hipEventDestroy(e.a); hipEventDestroy(e.b); }
   for (auto e : ctx->pool) hipEventDestroy(e);
   if (ctx->scratch) hipFree(ctx->scratch);
@@ -310,6 +311,7 @@ extern "C" const char* gf_ctx_last_error(gf_ctx* ctx) { return ctx ? ctx->last_e
 extern "C" int gf_ctx_set_flag(gf_ctx* ctx, int flag, int value) {
   if (!ctx) return GF_ERR_ARG;
   if (flag == GF_FLAG_JOIN_LEGACY) { ctx->join_legacy = value != 0; return GF_OK; }
+  if (flag == GF_FLAG_JOIN_COARSE) { ctx->join_coarse = value != 0; return GF_OK; }
   return set_err(ctx, GF_ERR_ARG, "gf_ctx_set_flag: unknown flag");
 }
 
@@ -1056,13 +1058,9 @@ extern "C" int gf_bitmap_to_indices(gf_ctx* ctx, const uint64_t* bitmap, int64_t
   return GF_OK;
 }
 
-extern "C" int gf_bitmap_to_indices_async(gf_ctx* ctx, const uint64_t* bitmap, int64_t n, uint32_t* idx, int64_t cap,
-                                          int64_t* count) {
-  if (!ctx || !bitmap || n < 0 || n > (int64_t)UINT32_MAX || !count || cap < 0 || (cap > 0 && !idx))
-    return set_err(ctx, GF_ERR_ARG, "gf_bitmap_to_indices_async: bad argument");
-  int st = bind(ctx);
-  if (st) return st;
-  const int64_t words = (n + 63) / 64, blocks = expand_blocks(words);
+// Ticket + epoch-tagged status words of the decoupled look-back kernels (expand_async, scan1)
+// for a launch of `blocks` blocks; the caller adds `blocks` to ctx->expand_base after launching.
+static int lookback_state(gf_ctx* ctx, int64_t blocks, gf::ExpandState* es) {
   if (!ctx->expand_ticket) {
     GF_HIP_CHECK(ctx, hipMalloc(&ctx->expand_ticket, sizeof(unsigned long long)));
     GF_HIP_CHECK(ctx, hipMemset(ctx->expand_ticket, 0, sizeof(unsigned long long)));
@@ -1076,10 +1074,22 @@ extern "C" int gf_bitmap_to_indices_async(gf_ctx* ctx, const uint64_t* bitmap, i
     GF_HIP_CHECK(ctx, hipMemset(ctx->expand_status, 0, sizeof(unsigned long long) * (size_t)cap_b));
     ctx->expand_status_cap = cap_b;
   }
-  ExpandState es{ctx->expand_ticket, ctx->expand_base, ctx->expand_status, 0};
+  *es = gf::ExpandState{ctx->expand_ticket, ctx->expand_base, ctx->expand_status, 0};
   ctx->expand_epoch = (ctx->expand_epoch + 1) & 0x3FFFFFFu;
   if (ctx->expand_epoch == 0) ctx->expand_epoch = 1;
-  es.epoch = ctx->expand_epoch;
+  es->epoch = ctx->expand_epoch;
+  return GF_OK;
+}
+
+extern "C" int gf_bitmap_to_indices_async(gf_ctx* ctx, const uint64_t* bitmap, int64_t n, uint32_t* idx, int64_t cap,
+                                          int64_t* count) {
+  if (!ctx || !bitmap || n < 0 || n > (int64_t)UINT32_MAX || !count || cap < 0 || (cap > 0 && !idx))
+    return set_err(ctx, GF_ERR_ARG, "gf_bitmap_to_indices_async: bad argument");
+  int st = bind(ctx);
+  if (st) return st;
+  const int64_t words = (n + 63) / 64, blocks = expand_blocks(words);
+  ExpandState es;
+  if ((st = lookback_state(ctx, blocks, &es))) return st;
   GF_HIP_CHECK(ctx, launch_expand_bitmap_async(ctx->stream, bitmap, words, n, idx, cap, count, es));
   ctx->expand_base += (unsigned long long)(words > 0 ? blocks : 0);
   return GF_OK;
@@ -1709,30 +1719,38 @@ extern "C" int gf_join_pp(gf_ctx* ctx, const gf_grid* ugrid, const gf_grid* qgri
   const int64_t qn = qgrid->n, W = qn + 2, bins = W * W;
   if (bins >= (int64_t)INT32_MAX / 2) return set_err(ctx, GF_ERR_ARG, "query grid too large");
   const int blocks = (int)std::min<int64_t>(std::max<int64_t>((no + kBlock - 1) / kBlock, 1), (int64_t)ctx->num_cus * 8);
+  // row-bucketed path (k_join.hip): bucket the ordinary side by cell row, probe per task
+  // (pairs carry u32 sorted slots or query indices with the top bit as a flag: nq < 2^31)
+  const bool rowpath = c >= 0 && 2 * c + 1 <= kJoinMaxRows && qn + 8 <= 8192 && nq < ((int64_t)1 << 31) &&
+                       !ctx->join_legacy;
+  // fine path (k_join.hip): c == 1, exact distances, one grid for both sides
+  int32_t f = 1;
+  if (rowpath && c == 1 && !approximate && !ctx->join_coarse && ugrid->n == qgrid->n && ugrid->minX == qgrid->minX &&
+      ugrid->minY == qgrid->minY && ugrid->cellLength == qgrid->cellLength) {
+    const double ext = (double)qn * qgrid->cellLength;
+    const double maxabs = std::max({std::fabs(qgrid->minX), std::fabs(qgrid->minY), std::fabs(qgrid->minX + ext),
+                                    std::fabs(qgrid->minY + ext)});
+    f = join_fine_factor(qgrid->cellLength, r, (int32_t)qn, maxabs);
+  }
+  const int64_t fbins = (int64_t)f * W * f * W;  // q_off entries (sub-cells on the fine path)
   Arena ar;
   size_t o_keys = ar.take<uint32_t>(nq), o_qcx = ar.take<int32_t>(nq), o_qcy = ar.take<int32_t>(nq);
-  size_t o_hist = ar.take<uint32_t>(bins), o_off = ar.take<uint32_t>(bins + 1), o_cur = ar.take<uint32_t>(bins);
+  size_t o_hist = ar.take<uint32_t>(bins), o_off = ar.take<uint32_t>(std::max(bins, fbins) + 1), o_cur = ar.take<uint32_t>(std::max(bins, fbins));
   size_t o_tmp = ar.take<uint32_t>(std::max(scan_tmp_elems(bins), scan_tmp_elems(blocks)));
   size_t o_sqx = ar.take<double>(nq), o_sqy = ar.take<double>(nq);
   size_t o_sqcx = ar.take<int32_t>(nq), o_sqcy = ar.take<int32_t>(nq), o_sqi = ar.take<uint32_t>(nq);
   size_t o_cnt = ar.take<uint32_t>(blocks), o_boff = ar.take<uint32_t>(blocks + 1);
-  // row-bucketed path (k_join.hip): bucket the ordinary side by cell row, probe per task
-  const bool rowpath = c >= 0 && 2 * c + 1 <= kJoinMaxRows && qn + 8 <= 8192 && !ctx->join_legacy;
-  // query side of the row path: row bucketing + per-row column sort (no global atomics)
-  const int qblk = (int)std::min<int64_t>(std::min<int64_t>(std::max<int64_t>(nq / 4096, 1), (int64_t)ctx->num_cus * 2), W);
-  const int64_t qmat = rowpath ? W * qblk : 1;
-  size_t o_qmat = ar.take<uint32_t>(qmat), o_qmats = ar.take<uint32_t>(qmat + 1);
-  size_t o_txy = ar.take<double>(rowpath ? 2 * nq : 1), o_tc = ar.take<int32_t>(rowpath ? 2 * nq : 1);
-  size_t o_tidx = ar.take<uint32_t>(rowpath ? nq : 1);
+  // bucketing grids: one block per CU in the scatter (its tile buffers fill the LDS), split
+  // between the sides by their point counts
+  const int qblk = (int)std::max<int64_t>(1, std::min<int64_t>(nq / 8192 + 1, (int64_t)ctx->num_cus * nq / (no + nq)));
+  const int sblocks = (int)std::max<int64_t>(1, std::min<int64_t>(no / 8192 + 1, (int64_t)ctx->num_cus - qblk));
+  const int64_t nrows = qn;  // ordinary-side rows
   // probe grid / task slots: >= the tasks (sum of ceil(row / kJoinTask)) + 8, a multiple of 8
-  const int64_t max_tasks = (no / kJoinTask + qn + 1 + 8 + 7) / 8 * 8;
-#ifndef GF_JOIN_SBPC
-#define GF_JOIN_SBPC 1  // ordinary-side bucketing blocks per CU (1024 threads, one tile buffer each)
-#endif
-  const int sblocks = (int)std::min<int64_t>(std::max<int64_t>(no / 8192, 1), (int64_t)ctx->num_cus * GF_JOIN_SBPC);
-  const int64_t mat = rowpath ? qn * sblocks : 1;
-  size_t o_rmat = ar.take<uint32_t>(mat), o_rmats = ar.take<uint32_t>(mat + 1), o_roff = ar.take<uint32_t>(qn + 1);
-  size_t o_rtask = ar.take<uint32_t>(qn), o_toff = ar.take<uint32_t>(qn + 1);
+  const int64_t max_tasks = (no / kJoinTask + nrows + 1 + 8 + 7) / 8 * 8;
+  const int64_t qmat = rowpath ? W * 2 * qblk : 1, mat = rowpath ? nrows * 2 * sblocks : 1;  // kHistSplit = 2
+  size_t o_cat = ar.take<uint32_t>(qmat + mat), o_cats = ar.take<uint32_t>(qmat + mat + 1);
+  size_t o_txy = ar.take<double>(rowpath ? 2 * nq : 1), o_tidx = ar.take<uint32_t>(rowpath ? nq : 1);
+  size_t o_roff = ar.take<uint32_t>(nrows + 1), o_toff = ar.take<uint32_t>(nrows + 1);
   size_t o_gcnt = ar.take<unsigned long long>(2);  // overflow count, total
   // task output regions, sized from the last join's pairs per point (x1.25 + one round)
   const double ppp = ctx->join_ppp > 0 ? ctx->join_ppp : 1.0;
@@ -1743,7 +1761,6 @@ extern "C" int gf_join_pp(gf_ctx* ctx, const gf_grid* ugrid, const gf_grid* qgri
   tcap = std::min<int64_t>(tcap, std::max<int64_t>(kJoinTask, ((int64_t)1 << 33) / 8 / std::max<int64_t>(max_tasks, 1)));
   size_t o_tpairs = ar.take<uint64_t>(rowpath ? max_tasks * tcap : 1), o_tcnt = ar.take<uint32_t>(rowpath ? max_tasks : 1);
   size_t o_tkoff = ar.take<uint32_t>(rowpath ? max_tasks + 1 : 1);
-  size_t o_btmp = ar.take<uint32_t>(std::max({scan_tmp_elems(mat), scan_tmp_elems(qn), scan_tmp_elems(max_tasks)}));
   size_t o_soxy = ar.take<double>(rowpath ? 2 * no : 1), o_soidx = ar.take<uint32_t>(rowpath ? no : 1);
   char* base = (char*)ctx_scratch(ctx, ar.off, &st);
   if (st) return st;
@@ -1752,58 +1769,51 @@ extern "C" int gf_join_pp(gf_ctx* ctx, const gf_grid* ugrid, const gf_grid* qgri
   auto F64 = [&](size_t o) { return (double*)(base + o); };
   hipStream_t s = ctx->stream;
   if (rowpath) {
+    if (!ctx->join_ticket) {  // the probe's ticket (its last block resets it)
+      GF_HIP_CHECK(ctx, hipMalloc(&ctx->join_ticket, sizeof(uint32_t)));
+      GF_HIP_CHECK(ctx, hipMemset(ctx->join_ticket, 0, sizeof(uint32_t)));
+    }
     JoinQueryArgs q{};
     q.qx = qry->x; q.qy = qry->y; q.nq = nq;
-    q.minX = qgrid->minX; q.minY = qgrid->minY; q.cl = qgrid->cellLength; q.qn = (int32_t)qn; q.nblk = qblk;
-    q.qmat = U32(o_qmat); q.qmat_scan = U32(o_qmats);
-    q.txy = F64(o_txy); q.tc = I32(o_tc); q.tidx = U32(o_tidx);
-    q.q_off = U32(o_off); q.sqx = F64(o_sqx); q.sqy = F64(o_sqy); q.sqcx = I32(o_sqcx); q.sqcy = I32(o_sqcy);
-    q.sqidx = U32(o_sqi);
-    GF_HIP_CHECK(ctx, launch_join_qrows(ctx, q, 0));
-    GF_HIP_CHECK(ctx, launch_exclusive_scan(s, q.qmat, qmat, q.qmat_scan, U32(o_tmp)));
-    GF_HIP_CHECK(ctx, launch_join_qrows(ctx, q, 1));
-    GF_HIP_CHECK(ctx, launch_join_qrows(ctx, q, 2));
-  } else {
-    GF_HIP_CHECK(ctx, hipMemsetAsync(U32(o_hist), 0, bins * sizeof(uint32_t), s));
-    GF_HIP_CHECK(ctx, launch_join_qkeys(s, qry->x, qry->y, nq, qgrid->minX, qgrid->minY, qgrid->cellLength,
-                                        qgrid->n, U32(o_keys), I32(o_qcx), I32(o_qcy)));
-    GF_HIP_CHECK(ctx, launch_histogram(s, U32(o_keys), nq, U32(o_hist)));
-    GF_HIP_CHECK(ctx, launch_exclusive_scan(s, U32(o_hist), bins, U32(o_off), U32(o_tmp)));
-    GF_HIP_CHECK(ctx, hipMemcpyAsync(U32(o_cur), U32(o_off), bins * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
-    GF_HIP_CHECK(ctx, launch_join_qscatter(s, qry->x, qry->y, I32(o_qcx), I32(o_qcy), U32(o_keys), nq, U32(o_cur),
-                                           F64(o_sqx), F64(o_sqy), I32(o_sqcx), I32(o_sqcy), U32(o_sqi)));
-  }
-  if (rowpath) {
-    auto R32 = [&](size_t o) { return (uint32_t*)(base + o); };
+    q.minX = qgrid->minX; q.minY = qgrid->minY; q.cl = qgrid->cellLength; q.qn = (int32_t)qn;
+    q.nblk = qblk; q.qmat = U32(o_cat); q.qmat_scan = U32(o_cats);
+    q.txy = F64(o_txy); q.tidx = U32(o_tidx); q.q_off = U32(o_off);
+    q.sqx = F64(o_sqx); q.sqy = F64(o_sqy); q.sqcx = I32(o_sqcx); q.sqcy = I32(o_sqcy); q.sqidx = U32(o_sqi);
+    q.f = f; q.fs = (double)f / qgrid->cellLength;
     JoinRowArgs j{};
     j.ox = ord->x; j.oy = ord->y; j.no = no;
     j.u_minX = ugrid->minX; j.u_minY = ugrid->minY; j.u_cl = ugrid->cellLength;
     j.qn = (int32_t)qn; j.c = c; j.q_off = U32(o_off);
     j.sqx = F64(o_sqx); j.sqy = F64(o_sqy); j.sqcx = I32(o_sqcx); j.sqcy = I32(o_sqcy); j.sqidx = U32(o_sqi);
     j.approx = approximate != 0; j.metric = metric; j.r = r; j.s_r = s_prefilter(r, 0);
-    j.row_mat = R32(o_rmat); j.row_mat_scan = R32(o_rmats); j.row_off_w = R32(o_roff); j.row_off = R32(o_roff);
-    j.row_tasks = R32(o_rtask);
-    j.task_off = R32(o_toff); j.soxy = (double*)(base + o_soxy); j.soidx = R32(o_soidx);
+    j.nblk = sblocks; j.nrows = (int32_t)nrows;
+    j.row_mat = U32(o_cat) + qmat; j.row_mat_scan = U32(o_cats) + qmat; j.mat_base = (uint32_t)nq;
+    j.row_off_w = U32(o_roff); j.row_off = U32(o_roff); j.task_off_w = U32(o_toff); j.task_off = U32(o_toff);
+    j.soxy = (double*)(base + o_soxy); j.soidx = U32(o_soidx);
     unsigned long long* cnt2 = (unsigned long long*)(base + o_gcnt);
     j.tpairs = (uint2*)(base + o_tpairs);
     j.task_cap = (uint32_t)tcap;
-    j.task_cnt = R32(o_tcnt);
+    j.task_cnt = U32(o_tcnt);
+    j.nslots = (uint32_t)max_tasks; j.ticket = ctx->join_ticket; j.tkoff = U32(o_tkoff);
     j.ovf_count = cnt2;
     j.pairs = pairs;
     j.cap = pairs ? (uint64_t)std::max<int64_t>(cap, 0) : 0;
     j.pairs_aligned = ((uintptr_t)pairs & 7) == 0;
-    j.lds_budget = join_probe_budget(nq, qn, c);
-    GF_HIP_CHECK(ctx, hipMemsetAsync(cnt2, 0, sizeof(unsigned long long), s));
-    GF_HIP_CHECK(ctx, launch_join_rows(ctx, j, 0, sblocks));
-    GF_HIP_CHECK(ctx, launch_exclusive_scan(s, j.row_mat, mat, j.row_mat_scan, R32(o_btmp)));
-    GF_HIP_CHECK(ctx, launch_join_rows(ctx, j, 1, sblocks));
-    GF_HIP_CHECK(ctx, launch_join_rows(ctx, j, 2, sblocks));
-    GF_HIP_CHECK(ctx, launch_exclusive_scan(s, j.row_tasks, qn, R32(o_toff), R32(o_btmp)));
-    // one probe pass into the task regions (+ overflow), then one packing launch
-    GF_HIP_CHECK(ctx, launch_join_rows(ctx, j, 3, (int)max_tasks));
-    GF_HIP_CHECK(ctx, launch_exclusive_scan(s, j.task_cnt, max_tasks, R32(o_tkoff), R32(o_btmp)));
+    j.f = f; j.fs = (double)f / ugrid->cellLength;
+    j.lds_budget = join_probe_budget(nq, qn, c, f);
+    // (1) row histograms of both sides, (2) one scan of both matrices, (3) write-combined row
+    // scatter of both sides, (4) query rows sorted by (sub-)cell + ordinary row / task offsets,
+    // (5) probe (its last block scans the task counts), (6) packing
+    GF_HIP_CHECK(ctx, launch_join_rows(ctx, j, q, 0));
+    ExpandState es;
+    if ((st = lookback_state(ctx, scan1_blocks(qmat + mat), &es))) return st;
+    GF_HIP_CHECK(ctx, launch_scan1(s, U32(o_cat), qmat + mat, U32(o_cats), nullptr, 0, 0, es));
+    ctx->expand_base += (unsigned long long)scan1_blocks(qmat + mat);
+    GF_HIP_CHECK(ctx, launch_join_rows(ctx, j, q, 1));
+    GF_HIP_CHECK(ctx, launch_join_rows(ctx, j, q, 2));
+    GF_HIP_CHECK(ctx, launch_join_rows(ctx, j, q, 3));
     JoinCompactArgs k{};
-    k.tpairs = j.tpairs; k.task_cap = j.task_cap; k.task_cnt = j.task_cnt; k.task_off = R32(o_tkoff);
+    k.tpairs = j.tpairs; k.task_cap = j.task_cap; k.task_cnt = j.task_cnt; k.task_off = U32(o_tkoff);
     k.ntask = (uint32_t)max_tasks;
     k.ovf_count = cnt2; k.pairs = pairs; k.cap = j.cap; k.pairs_aligned = j.pairs_aligned; k.total = cnt2 + 1;
     GF_HIP_CHECK(ctx, launch_join_compact(ctx, k));
@@ -1814,6 +1824,14 @@ extern "C" int gf_join_pp(gf_ctx* ctx, const gf_grid* ugrid, const gf_grid* qgri
     if ((int64_t)total > cap || (total > 0 && !pairs)) return GF_ERR_CAPACITY;
     return GF_OK;
   }
+  GF_HIP_CHECK(ctx, hipMemsetAsync(U32(o_hist), 0, bins * sizeof(uint32_t), s));
+  GF_HIP_CHECK(ctx, launch_join_qkeys(s, qry->x, qry->y, nq, qgrid->minX, qgrid->minY, qgrid->cellLength,
+                                      qgrid->n, U32(o_keys), I32(o_qcx), I32(o_qcy)));
+  GF_HIP_CHECK(ctx, launch_histogram(s, U32(o_keys), nq, U32(o_hist)));
+  GF_HIP_CHECK(ctx, launch_exclusive_scan(s, U32(o_hist), bins, U32(o_off), U32(o_tmp)));
+  GF_HIP_CHECK(ctx, hipMemcpyAsync(U32(o_cur), U32(o_off), bins * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
+  GF_HIP_CHECK(ctx, launch_join_qscatter(s, qry->x, qry->y, I32(o_qcx), I32(o_qcy), U32(o_keys), nq, U32(o_cur),
+                                         F64(o_sqx), F64(o_sqy), I32(o_sqcx), I32(o_sqcy), U32(o_sqi)));
   JoinArgs a{};
   a.ox = ord->x; a.oy = ord->y; a.no = no;
   a.u_minX = ugrid->minX; a.u_minY = ugrid->minY; a.u_cl = ugrid->cellLength;

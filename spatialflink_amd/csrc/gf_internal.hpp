@@ -33,6 +33,7 @@ struct gf_ctx {
   size_t pinned_bytes = 0;
   int num_cus = 256;
   int join_legacy = 0;  // testing: force the original (unbucketed) join probe
+  int join_coarse = 0;  // testing: the row path without sub-cells
   double join_ppp = 0.0;  // pairs per ordinary point of the last join (sizes the task regions)
   hipStream_t aux = nullptr;  // kNN depth 3: odd windows' launches (created on first use)
   gf_objid_dict* dict = nullptr;  // the context's default objID dictionary (created on first use)
@@ -42,6 +43,7 @@ struct gf_ctx {
   unsigned long long* expand_status = nullptr;
   int64_t expand_status_cap = 0;
   uint32_t expand_epoch = 0;
+  uint32_t* join_ticket = nullptr;  // row-bucketed join: the probe's ticket (zero between calls)
 };
 
 // objID dictionary (objid.cpp): device hash table + arena, batch buffers, host mirror for decode
@@ -302,6 +304,12 @@ struct ExpandState {
 };
 constexpr int kExpandWords = 1024;  // bitmap words (= threads) per expand_async block
 int64_t expand_blocks(int64_t words);
+// single-pass exclusive scan (decoupled look-back on the same ticket / status words; see
+// k_points.hip): out[L] = total, out2[0..n2) = a copy of out, in[0..nz) zeroed after reading.
+// in / out / out2 16-byte aligned.
+int64_t scan1_blocks(int64_t L);
+hipError_t launch_scan1(hipStream_t s, uint32_t* in, int64_t L, uint32_t* out, uint32_t* out2, int64_t n2, int64_t nz,
+                        const ExpandState& st);
 hipError_t launch_expand_bitmap_async(hipStream_t s, const uint64_t* bitmap, int64_t words, int64_t n, uint32_t* idx,
                                       int64_t cap, int64_t* count, const ExpandState& st);
 
@@ -496,12 +504,15 @@ struct JoinRowArgs {
   const uint32_t* sqidx;
   int approx, metric;
   double r, s_r;            // s_r = smax(r): exact squared-distance bound for metric 0
-  uint32_t* row_mat;        // [qn * nblk] per-block row histograms (row-major)
-  uint32_t* row_mat_scan;   // [qn * nblk + 1] its exclusive scan: run start per (row, block)
-  uint32_t* row_off_w;      // [qn+1] row starts (written by the finish kernel)
+  int32_t nblk;             // ordinary-side bucketing blocks
+  int32_t nrows;            // ordinary-side rows: qn cell rows, or f*qn sub-rows on the fine path
+  uint32_t* row_mat;        // [nrows * nblk] per-block row histograms (row-major)
+  const uint32_t* row_mat_scan;  // its exclusive scan (+ mat_base): run start per (row, block)
+  uint32_t mat_base;        // the matrix scan's offset (it follows the query histogram's)
+  uint32_t* row_off_w;      // [nrows+1] row starts (written by the finish kernel)
   const uint32_t* row_off;  // same buffer, read by the probe
-  uint32_t* row_tasks;      // [qn]
-  const uint32_t* task_off; // [qn+1]
+  uint32_t* task_off_w;     // [nrows+1] first task of each row (finish kernel)
+  const uint32_t* task_off; // same buffer, read by the probe
   double* soxy;             // [2*no] row-bucketed ordinary xy
   uint32_t* soidx;          // [no]
   // output: task t writes its pairs to the private region tpairs[t * task_cap ...]; a round
@@ -510,11 +521,19 @@ struct JoinRowArgs {
   uint2* tpairs;
   uint32_t task_cap;
   uint32_t* task_cnt;       // [max_tasks] pairs in each task's region
+  uint32_t nslots;          // max_tasks (the probe grid)
+  uint32_t* ticket;         // probe blocks done (the last one scans task_cnt; reset to 0 by it)
+  uint32_t* tkoff;          // [max_tasks + 1] exclusive scan of task_cnt (by the last probe block)
   unsigned long long* ovf_count;
   uint32_t* pairs;          // caller's [2 * cap]
   uint64_t cap;
   int pairs_aligned;        // 8-byte aligned: one 8-byte store per pair
   int lds_budget;
+  // fine sub-cells (k_join.hip, "fine path"): f > 1 splits every cell into f x f sub-cells of
+  // side cl / f > r, the query side is sorted by sub-cell and q_off indexes sub-cells
+  // ((f*(qn+2))^2 + 1 entries); f == 1: q_off indexes cells as before
+  int32_t f;
+  double fs;                // f / cl
 };
 // Dense output [0, total): the task regions packed in task order (offsets = exclusive scan
 // of task_cnt, task_off[ntask] = their sum), then the overflow moved down from the buffer's
@@ -550,9 +569,10 @@ constexpr int kJoinReg = 3;  // pairs per ordinary point kept in registers by th
 __host__ __device__ inline size_t join_row_lds_bytes(int64_t W, uint32_t m) {
   return ((size_t)(W + 1) * 2 + 15) / 16 * 16 + (size_t)m * 16;
 }
-hipError_t launch_join_rows(gf_ctx* ctx, const JoinRowArgs& a, int stage, int blocks);
 // LDS budget of the probe's staged query rows for nq query points on a qn x qn grid, 2c+1 rows
-int join_probe_budget(int64_t nq, int32_t qn, int64_t c);
+int join_probe_budget(int64_t nq, int32_t qn, int64_t c, int32_t f);
+// sub-cells per cell and axis for the fine path (1: the cell path) -- see k_join.hip
+int32_t join_fine_factor(double cl, double r, int32_t qn, double maxabs);
 // row path, query side: cell-sorted query arrays + q_off without global atomics
 struct JoinQueryArgs {
   const double* qx;
@@ -560,20 +580,24 @@ struct JoinQueryArgs {
   int64_t nq;
   double minX, minY, cl;
   int32_t qn;
-  int32_t nblk;            // bucketing grid
-  uint32_t* qmat;          // [(qn+2) * nblk] per-block row histograms (row-major)
-  uint32_t* qmat_scan;     // [(qn+2) * nblk + 1]
+  int32_t nblk;            // query blocks at the front of the histogram / scatter launches
+  uint32_t* qmat;          // [(qn+2) * nblk] per-block clamped-row histograms (row-major)
+  const uint32_t* qmat_scan;  // its exclusive scan (the front of the joint scan)
   double* txy;             // [2*nq] row-bucketed xy
-  int32_t* tc;             // [2*nq] row-bucketed (cx, cy)
-  uint32_t* tidx;          // [nq]
-  uint32_t* q_off;         // [(qn+2)^2 + 1]
+  uint32_t* tidx;          // [nq] their input indices
+  uint32_t* q_off;         // [(f(qn+2))^2 + 1] first point of each sub-cell (cell when f == 1)
   double* sqx;
   double* sqy;
   int32_t* sqcx;
   int32_t* sqcy;
   uint32_t* sqidx;
+  int32_t f;               // sub-cells per cell and axis (1: cells)
+  double fs;               // f / cl
 };
-hipError_t launch_join_qrows(gf_ctx* ctx, const JoinQueryArgs& a, int stage);
+// launches of the row path (k_join.hip): 0 histograms, 1 scatter, 2 row / task offsets, 3 probe
+hipError_t launch_join_rows(gf_ctx* ctx, const JoinRowArgs& a, const JoinQueryArgs& q, int stage);
+size_t join_scatter_lds_bytes(int32_t qn);
+
 
 }  // namespace gf
 

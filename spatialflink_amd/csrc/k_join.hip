@@ -159,12 +159,14 @@ hipError_t launch_join_probe(gf_ctx* ctx, const JoinArgs& a, int write_pass, int
 
 // =======================================================================================
 // Row-bucketed join (the default path when c >= 0).  The ordinary points are bucketed by
-// their cell row (counting sort over qn rows, block-local LDS histograms, one global atomic
-// per block and row to reserve a run), then processed as tasks of <= kJoinTask points of one
-// row: a task stages the query buckets of rows cy-c .. cy+c (u16 bucket offsets + xy) in LDS
-// and tests each ordinary point against the (2c+1) bucket runs around its cell -- all LDS.
-// A task whose rows do not fit the LDS budget probes the same runs from global memory.
-// Counts pass -> scan over tasks -> write pass; pair order inside a task is unspecified.
+// their cell row (block-local LDS histograms -> one scan -> write-combined scatter), then
+// processed as tasks of <= kJoinTask points of one row: a task stages the query buckets of rows
+// cy-c .. cy+c (u16 bucket offsets + xy) in LDS and tests each ordinary point against the
+// (2c+1) bucket runs around its cell -- all LDS.  A task whose rows do not fit the LDS budget
+// probes the same runs from global memory.  The query side is sorted by (sub-)cell with a
+// global histogram.  One window = 6 launches: histograms (both sides) -> one scan of both ->
+// scatter (both sides) -> row / task offsets -> probe (its last block scans the task counts)
+// -> packing.
 // =======================================================================================
 constexpr int kRowMax = 8192;  // rows staged as LDS histograms by the bucketing kernels
 
@@ -172,9 +174,9 @@ constexpr int kRowMax = 8192;  // rows staged as LDS histograms by the bucketing
 // the row-major matrix M[row][block] (plain stores).  The exclusive scan of M (flattened) is
 // then, for every (row, block), the start of that block's run of the row -- no contended
 // atomics, and the order inside a row is the block order.
-__device__ __forceinline__ void chunk_of(int64_t no, int64_t& beg, int64_t& end) {
-  const int64_t chunk = (no + gridDim.x - 1) / gridDim.x;
-  beg = (int64_t)blockIdx.x * chunk;
+__device__ __forceinline__ void chunk_of(int64_t no, int64_t bid, int64_t nblk, int64_t& beg, int64_t& end) {
+  const int64_t chunk = (no + nblk - 1) / nblk;
+  beg = bid * chunk;
   end = beg + chunk < no ? beg + chunk : no;
   if (beg > no) beg = no;
 }
@@ -184,76 +186,129 @@ __device__ __forceinline__ void chunk_of(int64_t no, int64_t& beg, int64_t& end)
 constexpr int kBucketU = 8;
 
 constexpr int kScatThreads = 1024;
+constexpr int kHistSplit = 2;  // histogram chunks per scatter block
 constexpr int kScatTile = 4096;
 constexpr int kScatPer = kScatTile / kScatThreads;
 
-__global__ __launch_bounds__(kScatThreads) void join_orow_hist_kernel(JoinRowArgs a, uint32_t* __restrict__ M) {
+__device__ __forceinline__ int32_t clamp_key(int32_t c, int32_t qn) { return (c < -1 ? -1 : (c > qn ? qn : c)) + 1; }
+
+// Sub-cell of coordinate v inside its in-grid cell c (0 .. f-1): any function that is monotone
+// in v, identical for both sides and gives every sub-cell a width > r serves (see the fine path
+// below); this one is within a few ulps of the cell split into f equal parts.
+__device__ __forceinline__ int32_t join_sub(double v, double mn, double cl, int32_t c, double fs, int32_t f) {
+  const int32_t j = jint((v - (mn + (double)c * cl)) * fs);
+  return j < 0 ? 0 : (j > f - 1 ? f - 1 : j);
+}
+
+// q_off index of a query point: its sub-cell (f sub-rows x f sub-columns per clamped cell,
+// sub 0 in clamped cells) in row-major order over f(qn+2) sub-columns; f == 1: the clamped cell
+__device__ __forceinline__ uint32_t join_fine_key(const JoinQueryArgs& q, double x, double y, int32_t& cx,
+                                                  int32_t& cy) {
+  cx = cell_index(x, q.minX, q.cl);
+  cy = cell_index(y, q.minY, q.cl);
+  const int64_t fW = (int64_t)q.f * (q.qn + 2);
+  int32_t jx = 0, jy = 0;
+  if (q.f > 1) {
+    if (cx >= 0 && cx < q.qn) jx = join_sub(x, q.minX, q.cl, cx, q.fs, q.f);
+    if (cy >= 0 && cy < q.qn) jy = join_sub(y, q.minY, q.cl, cy, q.fs, q.f);
+  }
+  return (uint32_t)(((int64_t)q.f * clamp_key(cy, q.qn) + jy) * fW + (int64_t)q.f * clamp_key(cx, q.qn) + jx);
+}
+
+// Row of an ordinary point: its cell row, -1 outside the grid (no replicated key can match it).  Row of a query point: its clamped cell row (0 .. qn+1).
+__device__ __forceinline__ int32_t join_orow(const JoinRowArgs& a, double x, double y) {
+  const int32_t cx = cell_index(x, a.u_minX, a.u_cl), cy = cell_index(y, a.u_minY, a.u_cl);
+  return cx >= 0 && cy >= 0 && cx < a.qn && cy < a.qn ? cy : -1;
+}
+__device__ __forceinline__ int32_t join_qrow(const JoinQueryArgs& q, double, double y) {
+  return clamp_key(cell_index(y, q.minY, q.cl), q.qn);
+}
+
+// Block `bid` of `nblk` counts its chunk of (X, Y) per row in LDS and stores the counts as
+// column bid of the row-major matrix M[row][block] (plain stores, no global atomics).
+template <class RowF>
+__device__ __forceinline__ void lds_row_hist(const double* X, const double* Y, int64_t n, int64_t bid, int64_t nblk,
+                                             int32_t nrows, uint32_t* M, RowF rowf) {
   __shared__ uint32_t h[kRowMax];
   int64_t beg, end;
-  chunk_of(a.no, beg, end);
-  for (int j = threadIdx.x; j < a.qn; j += kScatThreads) h[j] = 0u;
+  chunk_of(n, bid, nblk, beg, end);
+  for (int j = threadIdx.x; j < nrows; j += kScatThreads) h[j] = 0u;
   __syncthreads();
   for (int64_t i0 = beg + threadIdx.x; i0 < end; i0 += kScatThreads * kBucketU) {
     double x[kBucketU], y[kBucketU];
 #pragma unroll
     for (int u = 0; u < kBucketU; ++u) {
       const int64_t i = i0 + u * kScatThreads;
-      x[u] = i < end ? __builtin_nontemporal_load(a.ox + i) : NAN;
-      y[u] = i < end ? __builtin_nontemporal_load(a.oy + i) : NAN;
+      x[u] = i < end ? __builtin_nontemporal_load(X + i) : 0.0;
+      y[u] = i < end ? __builtin_nontemporal_load(Y + i) : 0.0;
     }
 #pragma unroll
     for (int u = 0; u < kBucketU; ++u) {
-      if (!(x[u] == x[u])) {  // NaN (or past the end): cell 0 per Java, but i may be past the end
-        if (i0 + u * kScatThreads >= end) continue;
-      }
-      const int32_t cx = cell_index(x[u], a.u_minX, a.u_cl);
-      const int32_t cy = cell_index(y[u], a.u_minY, a.u_cl);
-      if (cx >= 0 && cy >= 0 && cx < a.qn && cy < a.qn) atomicAdd(&h[cy], 1u);
+      if (i0 + u * kScatThreads >= end) continue;
+      const int32_t row = rowf(x[u], y[u]);
+      if (row >= 0) atomicAdd(&h[row], 1u);
     }
   }
   __syncthreads();
-  for (int j = threadIdx.x; j < a.qn; j += kScatThreads) M[(size_t)j * gridDim.x + blockIdx.x] = h[j];
+  for (int j = threadIdx.x; j < nrows; j += kScatThreads) M[(size_t)j * nblk + bid] = h[j];
 }
 
-// Write-combining row scatter.  Stores straight from the registers put every lane of a wave
-// into a different row: 64 separate 16 B + 4 B writes per store instruction, each a partial
-// line that reaches HBM on its own (rocprofv3 r02: WRITE_SIZE 2.5x the bytes, 208 us).  Here a
-// block takes its chunk in tiles of kScatTile points: cells -> LDS row histogram -> scan ->
-// the tile's points placed row-contiguously in LDS (with their destination) -> written out in
-// that order, so consecutive lanes write consecutive slots of one row (runs of ~tile/qn
-// points) and successive tiles extend the same runs.  Destinations: the block's run start of
-// each row (scan of the histogram matrix, as before) advanced tile by tile.
-
-size_t join_scatter_lds_bytes(int32_t qn) {
-  return (size_t)kScatTile * (16 + 4 + 4) + 2 * 4 * (size_t)qn + 4 * (kScatThreads / 64);
+// Launch 1: blocks [0, kHistSplit * q.nblk) histogram the query side by clamped row (matrix
+// q.qmat), the rest the ordinary side by row (a.row_mat); one scan of [q.qmat | a.row_mat]
+// follows.  Each side is cut into kHistSplit chunks per scatter block (two histogram blocks per
+// CU keep more loads in flight; scatter block b takes chunks kHistSplit*b ..).
+__global__ __launch_bounds__(kScatThreads) void join_hist_kernel(JoinRowArgs a, JoinQueryArgs q) {
+  if ((int)blockIdx.x < kHistSplit * q.nblk)
+    lds_row_hist(q.qx, q.qy, q.nq, blockIdx.x, kHistSplit * q.nblk, q.qn + 2, q.qmat,
+                 [&](double x, double y) { return join_qrow(q, x, y); });
+  else
+    lds_row_hist(a.ox, a.oy, a.no, (int64_t)blockIdx.x - kHistSplit * q.nblk, kHistSplit * a.nblk, a.nrows,
+                 a.row_mat, [&](double x, double y) { return join_orow(a, x, y); });
 }
 
-__global__ __launch_bounds__(kScatThreads) void join_orow_scatter_kernel(JoinRowArgs a, const uint32_t* __restrict__ Ms) {
+// Launch 3: write-combining row scatter of both sides (query blocks first).  Stores straight
+// from the registers would put every lane of a wave into a different row: 64 separate 16 B +
+// 4 B writes per store instruction, each a partial line that reaches HBM on its own (rocprofv3
+// r02: WRITE_SIZE 2.5x the bytes, 208 us).  Here a block takes its chunk in tiles of kScatTile
+// points: rows -> LDS row histogram -> scan -> the tile's points placed row-contiguously in LDS
+// (with their destination) -> written out in that order, so consecutive lanes write
+// consecutive slots of one row (runs of ~tile/rows points) and successive tiles extend the
+// same runs.  Destinations: the block's run start of each row (the matrix scan, minus `base`)
+// advanced tile by tile.
+size_t join_scatter_lds_bytes(int32_t nrows) {
+  return (size_t)kScatTile * (16 + 4 + 4) + 2 * 4 * (size_t)nrows + 4 * (kScatThreads / 64);
+}
+
+template <class RowF>
+__device__ __forceinline__ void wc_row_scatter(const double* X, const double* Y, int64_t n, int64_t bid, int64_t nblk,
+                                               int32_t nrows, const uint32_t* Ms, uint32_t base, double2* oxy,
+                                               uint32_t* oidx, RowF rowf) {
   extern __shared__ __attribute__((aligned(16))) char sm[];
   double2* const sxy = reinterpret_cast<double2*>(sm);
   uint32_t* const sidx = reinterpret_cast<uint32_t*>(sxy + kScatTile);
   uint32_t* const sdst = sidx + kScatTile;
-  uint32_t* const th = sdst + kScatTile;  // [qn] tile counts -> starts -> ends
-  uint32_t* const gd = th + a.qn;         // [qn] next global slot of the row (tile-local: minus start)
-  uint32_t* const wsum = gd + a.qn;
-  const int qn = a.qn;
+  uint32_t* const th = sdst + kScatTile;  // [nrows] tile counts -> starts -> ends
+  uint32_t* const gd = th + nrows;        // [nrows] next global slot of the row (tile-local: minus start)
+  uint32_t* const wsum = gd + nrows;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  int64_t beg, end;
-  chunk_of(a.no, beg, end);
-  for (int r = threadIdx.x; r < qn; r += kScatThreads) {
-    gd[r] = Ms[(size_t)r * gridDim.x + blockIdx.x];
+  int64_t beg, end, b2, e2;
+  chunk_of(n, kHistSplit * bid, kHistSplit * nblk, beg, end);  // the block's histogram chunks
+  chunk_of(n, kHistSplit * bid + kHistSplit - 1, kHistSplit * nblk, b2, e2);
+  end = e2 > end ? e2 : end;
+  for (int r = threadIdx.x; r < nrows; r += kScatThreads) {
+    gd[r] = Ms[(size_t)r * kHistSplit * nblk + kHistSplit * bid] - base;
     th[r] = 0u;
   }
   __syncthreads();
-  const int per = (qn + kScatThreads - 1) / kScatThreads, r0 = threadIdx.x * per;
+  const int per = (nrows + kScatThreads - 1) / kScatThreads, r0 = threadIdx.x * per;
   // the next tile's coordinates are loaded while this tile goes through its LDS phases
   double xn[kScatPer], yn[kScatPer];
   auto load_tile = [&](int64_t t0) {
 #pragma unroll
     for (int u = 0; u < kScatPer; ++u) {
       const int64_t i = t0 + threadIdx.x + u * kScatThreads;
-      xn[u] = i < end ? __builtin_nontemporal_load(a.ox + i) : 0.0;
-      yn[u] = i < end ? __builtin_nontemporal_load(a.oy + i) : 0.0;
+      xn[u] = i < end ? __builtin_nontemporal_load(X + i) : 0.0;
+      yn[u] = i < end ? __builtin_nontemporal_load(Y + i) : 0.0;
     }
   };
   load_tile(beg);
@@ -269,16 +324,14 @@ __global__ __launch_bounds__(kScatThreads) void join_orow_scatter_kernel(JoinRow
 #pragma unroll
     for (int u = 0; u < kScatPer; ++u) {
       const int64_t i = t0 + threadIdx.x + u * kScatThreads;
-      const int32_t cx = cell_index(x[u], a.u_minX, a.u_cl);
-      const int32_t cy = cell_index(y[u], a.u_minY, a.u_cl);
-      row[u] = i < end && cx >= 0 && cy >= 0 && cx < qn && cy < qn ? cy : -1;
+      row[u] = i < end ? rowf(x[u], y[u]) : -1;
       if (row[u] >= 0) atomicAdd(&th[row[u]], 1u);
     }
     __syncthreads();
     // exclusive scan of the tile counts (a contiguous run of rows per thread); gd becomes
     // (next global slot - tile start) so that slot + gd is the destination
     uint32_t run = 0;
-    for (int r = r0; r < r0 + per && r < qn; ++r) run += th[r];
+    for (int r = r0; r < r0 + per && r < nrows; ++r) run += th[r];
     uint32_t inc = run;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -291,7 +344,7 @@ __global__ __launch_bounds__(kScatThreads) void join_orow_scatter_kernel(JoinRow
     for (int w = 0; w < wid; ++w) before += wsum[w];
     uint32_t kept = 0;
     for (int w = 0; w < kScatThreads / 64; ++w) kept += wsum[w];
-    for (int r = r0; r < r0 + per && r < qn; ++r) {
+    for (int r = r0; r < r0 + per && r < nrows; ++r) {
       const uint32_t v = th[r];
       th[r] = before;
       gd[r] -= before;
@@ -309,10 +362,10 @@ __global__ __launch_bounds__(kScatThreads) void join_orow_scatter_kernel(JoinRow
     __syncthreads();
     for (uint32_t k = threadIdx.x; k < kept; k += kScatThreads) {
       const uint32_t d = sdst[k];
-      reinterpret_cast<double2*>(a.soxy)[d] = sxy[k];
-      a.soidx[d] = sidx[k];
+      oxy[d] = sxy[k];
+      oidx[d] = sidx[k];
     }
-    for (int r = r0; r < r0 + per && r < qn; ++r) {  // th[r] = tile end of the row
+    for (int r = r0; r < r0 + per && r < nrows; ++r) {  // th[r] = tile end of the row
       gd[r] += th[r];
       th[r] = 0u;
     }
@@ -320,149 +373,137 @@ __global__ __launch_bounds__(kScatThreads) void join_orow_scatter_kernel(JoinRow
   }
 }
 
-// ---------------------------------------------------------------------------------------
-// Query side of the row path: the same cell order as the histogram + scan + atomic scatter
-// of the legacy path (q_off[(ky)*W + kx] = first point of clamped cell (kx, ky)), built
-// without global atomics: row histograms in LDS -> one scan -> row scatter -> one block per
-// row counting-sorts its points by clamped column in LDS and writes that row of q_off.
-// ---------------------------------------------------------------------------------------
-__device__ __forceinline__ int32_t clamp_key(int32_t c, int32_t qn) { return (c < -1 ? -1 : (c > qn ? qn : c)) + 1; }
-
-__global__ __launch_bounds__(kBlock) void join_qrow_hist_kernel(JoinQueryArgs a, uint32_t* __restrict__ M) {
-  __shared__ uint32_t h[kRowMax];
-  int64_t beg, end;
-  chunk_of(a.nq, beg, end);
-  const int32_t W = a.qn + 2;
-  for (int j = threadIdx.x; j < W; j += kBlock) h[j] = 0u;
-  __syncthreads();
-  for (int64_t i0 = beg + threadIdx.x; i0 < end; i0 += kBlock * kBucketU) {
-    double y[kBucketU];  // all loads in flight before the first use
-#pragma unroll
-    for (int u = 0; u < kBucketU; ++u) y[u] = i0 + u * kBlock < end ? a.qy[i0 + u * kBlock] : 0.0;
-#pragma unroll
-    for (int u = 0; u < kBucketU; ++u)
-      if (i0 + u * kBlock < end) atomicAdd(&h[clamp_key(cell_index(y[u], a.minY, a.cl), a.qn)], 1u);
-  }
-  __syncthreads();
-  for (int j = threadIdx.x; j < W; j += kBlock) M[(size_t)j * gridDim.x + blockIdx.x] = h[j];
+__global__ __launch_bounds__(kScatThreads) void join_scatter_kernel(JoinRowArgs a, JoinQueryArgs q) {
+  if ((int)blockIdx.x < q.nblk)
+    wc_row_scatter(q.qx, q.qy, q.nq, blockIdx.x, q.nblk, q.qn + 2, q.qmat_scan, 0u,
+                   reinterpret_cast<double2*>(q.txy), q.tidx, [&](double x, double y) { return join_qrow(q, x, y); });
+  else
+    wc_row_scatter(a.ox, a.oy, a.no, (int64_t)blockIdx.x - q.nblk, a.nblk, a.nrows, a.row_mat_scan, a.mat_base,
+                   reinterpret_cast<double2*>(a.soxy), a.soidx, [&](double x, double y) { return join_orow(a, x, y); });
 }
 
-__global__ __launch_bounds__(kBlock) void join_qrow_scatter_kernel(JoinQueryArgs a, const uint32_t* __restrict__ Ms) {
-  __shared__ uint32_t h[kRowMax];
-  int64_t beg, end;
-  chunk_of(a.nq, beg, end);
-  const int32_t W = a.qn + 2;
-  for (int j = threadIdx.x; j < W; j += kBlock) h[j] = Ms[(size_t)j * gridDim.x + blockIdx.x];
-  __syncthreads();
-  for (int64_t i0 = beg + threadIdx.x; i0 < end; i0 += kBlock * kBucketU) {
-    double x[kBucketU], y[kBucketU];
-#pragma unroll
-    for (int u = 0; u < kBucketU; ++u) {
-      const int64_t i = i0 + u * kBlock;
-      x[u] = i < end ? a.qx[i] : 0.0;
-      y[u] = i < end ? a.qy[i] : 0.0;
-    }
-#pragma unroll
-    for (int u = 0; u < kBucketU; ++u) {
-      const int64_t i = i0 + u * kBlock;
-      if (i >= end) continue;
-      const int32_t cx = cell_index(x[u], a.minX, a.cl), cy = cell_index(y[u], a.minY, a.cl);
-      const uint32_t pos = atomicAdd(&h[clamp_key(cy, a.qn)], 1u);
-      reinterpret_cast<double2*>(a.txy)[pos] = make_double2(x[u], y[u]);
-      reinterpret_cast<int2*>(a.tc)[pos] = make_int2(cx, cy);
-      a.tidx[pos] = (uint32_t)i;
-    }
-  }
-}
-
-// one block per clamped row ky: column histogram + scan in LDS, q_off row, scatter in the row
-__global__ __launch_bounds__(kBlock) void join_qrow_sort_kernel(JoinQueryArgs a, const uint32_t* __restrict__ Ms,
-                                                                uint32_t total_idx) {
-  __shared__ uint32_t h[kRowMax];
-  __shared__ uint32_t wsum[kBlock / 64];
-  const int32_t W = a.qn + 2, ky = blockIdx.x;
-  const uint32_t rb = Ms[(size_t)ky * a.nblk], re = ky + 1 < W ? Ms[(size_t)(ky + 1) * a.nblk] : Ms[total_idx];
-  for (int j = threadIdx.x; j < W; j += kBlock) h[j] = 0u;
-  __syncthreads();
-  for (uint32_t i0 = rb + threadIdx.x; i0 < re; i0 += kBlock * 4) {
-    int32_t cx[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) cx[u] = i0 + u * kBlock < re ? a.tc[2 * (i0 + u * kBlock)] : 0;
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-      if (i0 + u * kBlock < re) atomicAdd(&h[clamp_key(cx[u], a.qn)], 1u);
-  }
-  __syncthreads();
-  // exclusive scan of h[0..W) in place: each thread owns a contiguous span of columns
-  const int per = (W + kBlock - 1) / kBlock, j0 = threadIdx.x * per;
-  uint32_t run = 0;
-  for (int j = j0; j < j0 + per && j < W; ++j) run += h[j];
+// block-wide exclusive scan of one value per thread (NT threads); *total = the block's sum
+template <int NT>
+__device__ __forceinline__ uint32_t join_block_scan(uint32_t v, uint32_t* total, uint32_t* ws) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  uint32_t inc = run;
+  uint32_t inc = v;
+#pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
     const uint32_t t = __shfl_up(inc, o, 64);
     if (lane >= o) inc += t;
   }
-  if (lane == 63) wsum[wid] = inc;
+  if (lane == 63) ws[wid] = inc;
   __syncthreads();
-  uint32_t before = inc - run;
-  for (int w = 0; w < wid; ++w) before += wsum[w];
-  for (int j = j0; j < j0 + per && j < W; ++j) {
-    const uint32_t c = h[j];
-    h[j] = rb + before;  // now the cell's cursor (absolute position)
-    a.q_off[(size_t)ky * W + j] = rb + before;
-    before += c;
+  uint32_t before = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < NT / 64; ++w) {
+    before += w < wid ? ws[w] : 0u;
+    tot += ws[w];
   }
-  if (ky == W - 1 && threadIdx.x == 0) a.q_off[(size_t)W * W] = re;
+  *total = tot;
   __syncthreads();
-  for (uint32_t i0 = rb + threadIdx.x; i0 < re; i0 += kBlock * 4) {
-    int2 cc[4];
+  return before + inc - v;
+}
+
+// Launch 4.  Blocks [0, qn+2): query row ky sorted by sub-cell -- (sub-row, sub-column) keys
+// (join_fine_key; f == 1: the clamped column) counted in LDS, scanned, the row's q_off entries
+// written (coalesced), the points placed (with their true cells and input index).  Block qn+2:
+// the ordinary side's row starts (row_off[j] = M_scan[j][0], row_off[rows] = the total), tasks
+// per row (ceil(row / kJoinTask)) and their exclusive scan task_off[0..rows]; it also zeroes
+// the overflow count the probe accumulates.
+__global__ __launch_bounds__(kScatThreads) void join_sort_finish_kernel(JoinRowArgs a, JoinQueryArgs q) {
+  __shared__ uint32_t h[kRowMax];
+  __shared__ uint32_t ws[kScatThreads / 64];
+  const int32_t W = q.qn + 2;
+  if ((int)blockIdx.x == W) {
+    const int nr = a.nrows, per = (nr + kScatThreads - 1) / kScatThreads, j0 = threadIdx.x * per;
+    const uint32_t* Ms = a.row_mat_scan;
+    const size_t nc = (size_t)kHistSplit * a.nblk, tot_idx = (size_t)nr * nc;
+    auto rows_at = [&](int j, uint32_t& b, uint32_t& e) {
+      b = Ms[(size_t)j * nc] - a.mat_base;
+      e = Ms[j + 1 < nr ? (size_t)(j + 1) * nc : tot_idx] - a.mat_base;
+    };
+    uint32_t run = 0;
+    for (int j = j0; j < j0 + per && j < nr; ++j) {
+      uint32_t b, e;
+      rows_at(j, b, e);
+      a.row_off_w[j] = b;
+      run += (e - b + kJoinTask - 1) / kJoinTask;
+    }
+    uint32_t total;
+    uint32_t before = join_block_scan<kScatThreads>(run, &total, ws);
+    for (int j = j0; j < j0 + per && j < nr; ++j) {
+      uint32_t b, e;
+      rows_at(j, b, e);
+      a.task_off_w[j] = before;
+      before += (e - b + kJoinTask - 1) / kJoinTask;
+    }
+    if (threadIdx.x == 0) {
+      a.row_off_w[nr] = Ms[tot_idx] - a.mat_base;
+      a.task_off_w[nr] = total;
+      *a.ovf_count = 0ull;
+    }
+    return;
+  }
+  const int32_t ky = blockIdx.x, H = q.f * q.f * W;  // H <= kRowMax (host)
+  const uint32_t* Ms = q.qmat_scan;
+  const size_t nc = (size_t)kHistSplit * q.nblk;
+  const uint32_t rb = Ms[(size_t)ky * nc], re = Ms[ky + 1 < W ? (size_t)(ky + 1) * nc : (size_t)W * nc];
+  const double2* txy = reinterpret_cast<const double2*>(q.txy);
+  const uint32_t fH = (uint32_t)((int64_t)q.f * W);  // sub-columns per sub-row
+  auto key_of = [&](double2 v, int32_t& cx, int32_t& cy) {
+    const uint32_t k = join_fine_key(q, v.x, v.y, cx, cy);
+    return k - (uint32_t)ky * (uint32_t)q.f * fH;  // relative to the row's first sub-row
+  };
+  for (int j = threadIdx.x; j < H; j += kScatThreads) h[j] = 0u;
+  __syncthreads();
+  for (uint32_t i0 = rb + threadIdx.x; i0 < re; i0 += kScatThreads * 4) {
+    double2 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = txy[i0 + u * kScatThreads < re ? i0 + u * kScatThreads : rb];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (i0 + u * kScatThreads >= re) continue;
+      int32_t cx, cy;
+      atomicAdd(&h[key_of(v[u], cx, cy)], 1u);
+    }
+  }
+  __syncthreads();
+  {  // exclusive scan of h[0..H) in place (a contiguous span of keys per thread)
+    const int per = (H + kScatThreads - 1) / kScatThreads, j0 = threadIdx.x * per;
+    uint32_t run = 0;
+    for (int j = j0; j < j0 + per && j < H; ++j) run += h[j];
+    uint32_t total;
+    uint32_t before = join_block_scan<kScatThreads>(run, &total, ws);
+    for (int j = j0; j < j0 + per && j < H; ++j) {
+      const uint32_t c = h[j];
+      h[j] = rb + before;  // the key's cursor (absolute position)
+      before += c;
+    }
+  }
+  __syncthreads();
+  for (int j = threadIdx.x; j < H; j += kScatThreads) q.q_off[(size_t)ky * H + j] = h[j];
+  if (ky == W - 1 && threadIdx.x == 0) q.q_off[(size_t)W * H] = re;
+  __syncthreads();
+  for (uint32_t i0 = rb + threadIdx.x; i0 < re; i0 += kScatThreads * 4) {
     double2 v[4];
     uint32_t ix[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      const uint32_t i = i0 + u * kBlock < re ? i0 + u * kBlock : rb;
-      cc[u] = reinterpret_cast<const int2*>(a.tc)[i];
-      v[u] = reinterpret_cast<const double2*>(a.txy)[i];
-      ix[u] = a.tidx[i];
+      const uint32_t i = i0 + u * kScatThreads < re ? i0 + u * kScatThreads : rb;
+      v[u] = txy[i];
+      ix[u] = q.tidx[i];
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      if (i0 + u * kBlock >= re) continue;
-      const uint32_t pos = atomicAdd(&h[clamp_key(cc[u].x, a.qn)], 1u);
-      a.sqx[pos] = v[u].x;
-      a.sqy[pos] = v[u].y;
-      a.sqcx[pos] = cc[u].x;
-      a.sqcy[pos] = cc[u].y;
-      a.sqidx[pos] = ix[u];
-    }
-  }
-}
-
-hipError_t launch_join_qrows(gf_ctx* ctx, const JoinQueryArgs& a, int stage) {
-  hipStream_t s = ctx->stream;
-  KTimer t(ctx, GF_K_JOIN_BUCKET);
-  if (stage == 0)
-    hipLaunchKernelGGL(join_qrow_hist_kernel, dim3(a.nblk), dim3(kBlock), 0, s, a, a.qmat);
-  else if (stage == 1)
-    hipLaunchKernelGGL(join_qrow_scatter_kernel, dim3(a.nblk), dim3(kBlock), 0, s, a, a.qmat_scan);
-  else
-    hipLaunchKernelGGL(join_qrow_sort_kernel, dim3(a.qn + 2), dim3(kBlock), 0, s, a, a.qmat_scan,
-                       (uint32_t)((size_t)(a.qn + 2) * a.nblk));
-  return hipGetLastError();
-}
-
-// row_off[j] = Ms[j][0] (row starts), row_off[qn] = total; tasks per row
-__global__ __launch_bounds__(kBlock) void join_rows_finish_kernel(const uint32_t* __restrict__ Ms, int32_t qn,
-                                                                  int32_t nblk, uint32_t total_idx,
-                                                                  uint32_t* __restrict__ row_off,
-                                                                  uint32_t* __restrict__ row_tasks) {
-  for (int j = blockIdx.x * kBlock + threadIdx.x; j <= qn; j += gridDim.x * kBlock) {
-    const uint32_t b = Ms[j < qn ? (size_t)j * nblk : total_idx];
-    row_off[j] = b;
-    if (j < qn) {
-      const uint32_t e = Ms[j + 1 < qn ? (size_t)(j + 1) * nblk : total_idx];
-      row_tasks[j] = (e - b + kJoinTask - 1) / kJoinTask;
+      if (i0 + u * kScatThreads >= re) continue;
+      int32_t cx, cy;
+      const uint32_t pos = atomicAdd(&h[key_of(v[u], cx, cy)], 1u);
+      q.sqx[pos] = v[u].x;
+      q.sqy[pos] = v[u].y;
+      q.sqcx[pos] = cx;
+      q.sqcy[pos] = cy;
+      q.sqidx[pos] = ix[u];
     }
   }
 }
@@ -485,33 +526,56 @@ struct JoinProbeHdr {
   uint32_t fit_end;  // end of the last reservation that fit the region
   uint32_t wsum[kJoinThreads / 64];
   QRow rows[kJoinMaxRows];
+  uint32_t g0;       // fine path: sorted index of the first staged query point
+  uint32_t gm;       // fine path: staged query points (0: none; their indices are in LDS)
+  uint32_t lqidx;    // fine path: LDS byte offset of the staged query indices
 };
 constexpr int kJoinHdrBytes = (int)((sizeof(JoinProbeHdr) + 15) / 16 * 16);
 constexpr int kJoinWaveBuf = 128;  // pairs a wave collects in LDS before one coalesced flush
 static_assert(kJoinTask <= 8192, "local index packed in 13 bits");
-// u16 column keys, later (same bytes) the wave pair buffers
-constexpr size_t kJoinUnionBytes = 2 * kJoinTask > kJoinWaveBuf * 8 * (kJoinThreads / 64)
-                                       ? 2 * kJoinTask : kJoinWaveBuf * 8 * (kJoinThreads / 64);
-
 // Dynamic LDS of the probe: header | staged rows (budget) | sorted (column << 13 | local index)
-// u32 per point | column keys / wave pair buffers | column histogram [qn + 1]
-static size_t join_probe_lds_fixed(int32_t qn) {
-  return kJoinHdrBytes + 4 * (size_t)kJoinTask + kJoinUnionBytes + 4 * ((size_t)qn + 1);
+// u32 per point | union { task prologue: u16 column keys + column histogram [columns + 1]
+// (columns = qn, or f(qn+2) sub-columns on the fine path); walk: the wave pair buffers }
+static size_t join_probe_union_bytes(int32_t qn, int32_t f) {
+  const size_t cols = f > 1 ? (size_t)f * ((size_t)qn + 2) : (size_t)qn;
+  const size_t pro = 2 * (size_t)kJoinTask + 4 * (cols + 1), wb = (size_t)kJoinWaveBuf * 8 * (kJoinThreads / 64);
+  return ((pro > wb ? pro : wb) + 15) / 16 * 16;
 }
-static size_t join_probe_lds_bytes(int lds_budget, int32_t qn) { return join_probe_lds_fixed(qn) + (size_t)lds_budget; }
+static size_t join_probe_lds_fixed(int32_t qn, int32_t f) {
+  return kJoinHdrBytes + 4 * (size_t)kJoinTask + join_probe_union_bytes(qn, f);
+}
+static size_t join_probe_lds_bytes(int lds_budget, int32_t qn, int32_t f) {
+  return join_probe_lds_fixed(qn, f) + (size_t)lds_budget;
+}
 
-// Two blocks per CU (80 KB each of the 160 KB LDS) when the expected staged rows fit: 2c+1 rows
-// of 1.15 x the mean row + 64 points (C4: 3 x 1000-point rows = 59 KB); otherwise one block
-// with the rest of the 160 KB.  A task whose rows exceed the budget reads them from global
-// memory (same results, slower).
-int join_probe_budget(int64_t nq, int32_t qn, int64_t c) {
+// The staged query rows get what the fixed layout leaves of the 160 KB (one block per CU).  A
+// task whose rows exceed the budget reads them from global memory (same results, slower).
+int join_probe_budget(int64_t nq, int32_t qn, int64_t c, int32_t f) {
   const int64_t W = (int64_t)qn + 2;
   const double mean = (double)nq / (double)(qn > 0 ? qn : 1);
-  const size_t need = (size_t)(2 * c + 1) * join_row_lds_bytes(W, (uint32_t)(mean + 4.0 * std::sqrt(mean) + 16.0));
-  const size_t fixed = join_probe_lds_fixed(qn);
-  const size_t half = 80 * 1024, full = 160 * 1024;
-  if (fixed < half && need <= half - fixed) return (int)(half - fixed);
+  size_t need;
+  if (f > 1) {  // 3 sub-rows
+    const double m = mean * 3.0 / (double)f;
+    need = 3 * join_row_lds_bytes((int64_t)f * W, 0) + (size_t)(m + 4.0 * std::sqrt(m) + 16.0) * 20;
+  } else {
+    need = (size_t)(2 * c + 1) * join_row_lds_bytes(W, (uint32_t)(mean + 4.0 * std::sqrt(mean) + 16.0));
+  }
+  // one block per CU (the probe's registers: > 64 VGPRs), so the staged rows get the rest
+  (void)need;
+  const size_t fixed = join_probe_lds_fixed(qn, f), full = 160 * 1024;
   return fixed < full ? (int)(full - fixed) : 0;
+}
+
+// Fine path factor: the largest f <= 4 whose sub-cells are wider than r with a margin far
+// above the rounding of the sub-cell bounds (cl/f against r: relative 1e-9, plus 64 ulps of the
+// largest grid coordinate), and whose per-row sort keys fit the LDS histogram.
+int32_t join_fine_factor(double cl, double r, int32_t qn, double maxabs) {
+  const double slack = 1e-9 * cl + 64.0 * std::ldexp(1.0, std::ilogb(maxabs > 1.0 ? maxabs : 1.0) - 52);
+  for (int32_t f = 4; f >= 2; --f) {
+    if ((int64_t)f * f * ((int64_t)qn + 2) > kRowMax || (int64_t)f * ((int64_t)qn + 2) >= (1 << 13)) continue;
+    if (cl / f - slack > r * (1.0 + 1e-12)) return f;
+  }
+  return 1;
 }
 
 // Wave-uniform value (the compiler cannot prove it): one readfirstlane, so the loops that use
@@ -537,12 +601,23 @@ struct JoinWaveBuf {
     uint32_t wb = 0;
     if (lane == 0) wb = atomicAdd(&hd.used, cnt);
     wb = join_uni(wb);
-    // the query slot becomes the query index here (an L2 gather of the sorted query side)
+    // the query slot becomes the query index here: from LDS when the fine path staged it,
+    // else an L2 gather of the sorted query side
+    const uint32_t g0 = hd.g0, gm = join_uni(hd.gm);
+    const uint32_t* lq = reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(&hd) + hd.lqidx);
+    auto qidx = [&](uint32_t slot) { return slot - g0 < gm ? lq[slot - g0] : a.sqidx[slot]; };
     if (wb + cnt <= a.task_cap) {
       if (lane == 0) atomicMax(&hd.fit_end, wb + cnt);
-      for (uint32_t i = lane; i < cnt; i += 64) {
-        const uint2 v = buf[i];
-        region[wb + i] = make_uint2(v.x, a.sqidx[v.y]);
+      if (gm > 0) {  // staged: every slot was mapped at push time (top bit) or lies in the staged range
+        for (uint32_t i = lane; i < cnt; i += 64) {
+          const uint2 v = buf[i];
+          region[wb + i] = make_uint2(v.x, v.y & 0x80000000u ? v.y & 0x7fffffffu : lq[v.y - g0]);
+        }
+      } else {
+        for (uint32_t i = lane; i < cnt; i += 64) {
+          const uint2 v = buf[i];
+          region[wb + i] = make_uint2(v.x, v.y & 0x80000000u ? v.y & 0x7fffffffu : a.sqidx[v.y]);
+        }
       }
     } else {
       unsigned long long ob = 0;
@@ -550,7 +625,8 @@ struct JoinWaveBuf {
       ob = ((unsigned long long)join_uni((uint32_t)(ob >> 32)) << 32) | join_uni((uint32_t)ob);
       for (uint32_t i = lane; i < cnt; i += 64) {
         const uint2 v = buf[i];
-        if (ob + i < a.cap) join_store(a.pairs, a.pairs_aligned, a.cap - 1 - (ob + i), make_uint2(v.x, a.sqidx[v.y]));
+        const uint32_t qi = v.y & 0x80000000u ? v.y & 0x7fffffffu : qidx(v.y);
+        if (ob + i < a.cap) join_store(a.pairs, a.pairs_aligned, a.cap - 1 - (ob + i), make_uint2(v.x, qi));
       }
     }
     cnt = 0;
@@ -584,7 +660,9 @@ struct JoinWaveBuf {
 // exit is a ballot, so the loop and the pair count stay wave-uniform).  Column-sorted lanes
 // share columns, so most lanes of a round read the same few LDS addresses.  SLOW: the run
 // touches a clamped bucket or row, so each candidate's true cell is checked (Chebyshev <= c).
-template <int MODE, bool LDS, bool SLOW>
+// MAPQ: the pair carries the query index itself (top bit set) instead of the sorted slot -- the
+// fine path's cell-path waves, whose slots may lie outside the task's staged range.
+template <int MODE, bool LDS, bool SLOW, bool MAPQ = false>
 __device__ __forceinline__ void join_lane_run(const JoinRowArgs& a, const double2* lxy, uint32_t gb, uint32_t tb,
                                               uint32_t te, const JoinLane& ln, JoinWaveBuf& wbuf, JoinProbeHdr& hd,
                                               uint2* region) {
@@ -625,8 +703,58 @@ __device__ __forceinline__ void join_lane_run(const JoinRowArgs& a, const double
     }
 #pragma unroll
     for (int i = 0; i < R; ++i) hit[i] = test(act[i], t[i], v[i]);
+    if constexpr (MAPQ) {
+#pragma unroll
+      for (int i = 0; i < R; ++i) q[i] = hit[i] ? a.sqidx[q[i]] | 0x80000000u : 0u;
+    }
     wbuf.push<R>(hit, ln.pidx, q, a, hd, region);
   }
+}
+
+// Fine path: one lane's candidates are three runs [b_s, e_s) of the sorted query side (the
+// sub-columns SC-1 .. SC+1 of the sub-rows SR-1 .. SR+1 around its sub-cell), walked as ONE
+// concatenated sequence, R candidates per round until every lane is done (ballot exit).  Indices
+// are relative to the first staged point g0; LDS: the staged xy at those indices.
+template <int MODE, bool LDS, int R>
+__device__ __forceinline__ void join_fine_walk(const JoinRowArgs& a, const double2* lxy, uint32_t g0,
+                                               const uint32_t (&b)[3], const uint32_t (&e)[3], const JoinLane& ln,
+                                               JoinWaveBuf& wbuf, JoinProbeHdr& hd, uint2* region) {
+  const uint32_t L0 = e[0] - b[0], L1 = L0 + (e[1] - b[1]), L2 = L1 + (e[2] - b[2]);
+  const uint32_t d0 = b[0], d1 = b[1] - L0, d2 = b[2] - L1;  // run s: index = k + d_s (mod 2^32)
+  for (uint32_t k = 0; __ballot(k < L2) != 0; k += R) {
+    bool hit[R];
+    uint32_t t[R], q[R];
+    double2 v[R];
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      const uint32_t kk = k + i;
+      t[i] = kk < L2 ? kk + (kk < L0 ? d0 : (kk < L1 ? d1 : d2)) : 0u;
+      q[i] = g0 + t[i];
+    }
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      if constexpr (LDS) {  // a finished lane reads staged slot 0 (some lane has a candidate)
+        v[i] = lxy[t[i]];
+      } else {
+        v[i] = make_double2(0.0, 0.0);
+        if (k + i < L2) v[i] = make_double2(a.sqx[q[i]], a.sqy[q[i]]);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      const double dx = ln.px - v[i].x, dy = ln.py - v[i].y;
+      bool ok;
+      if constexpr (MODE == 0) ok = dx * dx + dy * dy <= a.s_r;
+      else ok = a.metric == 0 ? dx * dx + dy * dy <= a.s_r : fdlibm_hypot(dx, dy) <= a.r;
+      hit[i] = k + i < L2 && ok;
+    }
+    wbuf.push<R>(hit, ln.pidx, q, a, hd, region);
+  }
+}
+
+// write-through (agent-scope) store: read by the last block of the launch on another XCD
+__device__ __forceinline__ void store_u32_wt(uint32_t* p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // One block per task = <= kJoinTask ordinary points of one cell row.  The 2c+1 query rows
@@ -638,24 +766,23 @@ __device__ __forceinline__ void join_lane_run(const JoinRowArgs& a, const double
 // the rounds per row are the longest run among ~8 columns instead of the union of all of them.
 // Pairs go through the wave's LDS buffer into the task's private region in coalesced runs;
 // join_compact_kernel packs the regions.
-template <int MODE>  // 0: exact, metric 0 (squared-distance bound); 1: approximate or hypot
-__global__ __launch_bounds__(kJoinThreads) void join_row_probe_kernel(JoinRowArgs a) {
-  // every LDS variable lives in the dynamic region, header first (a static __shared__ block in
-  // front would shift the dynamic base off 16 B: misaligned ds_read_b128 of the staged xy)
-  extern __shared__ __attribute__((aligned(16))) char lds_base[];
+//
+// FINE (the fine path, f > 1: c == 1, exact distances, one grid for both sides, cl/f > r): a
+// pair needs d <= r, so its points lie in sub-cells at most one apart on each axis (sub-cells are
+// wider than r and the sub-cell index is monotone), and then their cells are at most one apart --
+// the key match is implied.  An interior lane (cell column and row in [1, qn-2], so every
+// candidate is an in-grid point) therefore tests only the 3 x 3 sub-cells around its own: runs
+// of the f + 2 sub-rows the task stages (cl^2 (3/f)^2 of candidates instead of 9 cl^2).  A wave
+// holding an edge lane, and every task of rows 0 and qn-1, takes the cell path over global
+// memory (the true-cell check on every candidate), sub-row by sub-row.
+template <int MODE, int FINE>  // MODE 0: exact, metric 0 (squared-distance bound); 1: approximate or hypot
+__device__ __forceinline__ void join_probe_task(const JoinRowArgs& a, uint32_t task, char* const lds_base) {
   JoinProbeHdr& hd = *reinterpret_cast<JoinProbeHdr*>(lds_base);
   char* const lds = lds_base + kJoinHdrBytes;
   QRow* const rows = hd.rows;
-  // XCD-aware task order: workgroups go round-robin to the 8 XCDs, so XCD x gets the
-  // consecutive tasks [x * per, (x + 1) * per) -- neighbouring row tasks stage the same query
-  // rows, and they now meet in the same L2.  The grid is >= ntask + 8 (host); slots past ntask
-  // are zeroed by the block of the same index.
-  const uint32_t ntask = a.task_off[a.qn];
-  if (blockIdx.x >= ntask && threadIdx.x == 0) a.task_cnt[blockIdx.x] = 0u;
-  const uint32_t per = (ntask + 7) / 8;
-  const uint32_t task = (blockIdx.x & 7u) * per + (blockIdx.x >> 3);
-  if ((blockIdx.x >> 3) >= per || task >= ntask) return;
   const int64_t W = (int64_t)a.qn + 2, c = a.c, qn = a.qn;
+  const int32_t f = FINE ? a.f : 1;
+  const int64_t fW = (int64_t)f * W;  // sub-columns (FINE) per sub-row
   // the task's row: the one j with task_off[j] <= task < task_off[j+1] (a parallel search --
   // one round of loads, where a serial binary search costs ~10 dependent ones)
   if (threadIdx.x == 0) {
@@ -663,80 +790,133 @@ __global__ __launch_bounds__(kJoinThreads) void join_row_probe_kernel(JoinRowArg
     hd.fit_end = 0u;
     hd.need = 0u;
     hd.fit = 1;
+    hd.gm = 0u;
+    hd.g0 = 0u;
+    hd.lqidx = 0u;
   }
-  for (int j = threadIdx.x; j < a.qn; j += kJoinThreads)
+  for (int j = threadIdx.x; j < a.nrows; j += kJoinThreads)
     if (a.task_off[j] <= task && task < a.task_off[j + 1]) hd.row = j;
   __syncthreads();
-  const int32_t cy = hd.row;
+  const int32_t orow = hd.row, cy = orow;  // the task's cell row
   const int64_t r0 = cy - c < -1 ? -1 : cy - c, r1 = cy + c > qn ? qn : cy + c;
   const int nrows = (int)(r1 - r0 + 1);
+  const bool task_edge = FINE && (cy < 1 || cy > qn - 2);  // every lane takes the cell path
+  const size_t fine_rb = join_row_lds_bytes(fW, 0);          // one staged sub-row's u16 offsets
   if (threadIdx.x == 0) {
     // the row's tasks split it evenly (10000 points: 2 x 5000, not 8192 + 1808)
-    const uint32_t k = task - a.task_off[cy], nt = a.task_off[cy + 1] - a.task_off[cy];
-    const uint32_t rb = a.row_off[cy], re = a.row_off[cy + 1], size = (re - rb + nt - 1) / nt;
+    const uint32_t k = task - a.task_off[orow], nt = a.task_off[orow + 1] - a.task_off[orow];
+    const uint32_t rb = a.row_off[orow], re = a.row_off[orow + 1], size = (re - rb + nt - 1) / nt;
     hd.beg = rb + k * size;
     hd.end = rb + (k + 1) * size < re ? rb + (k + 1) * size : re;
+    if (FINE) {  // sub-rows f(cy+1)-1 .. f(cy+1)+f: consecutive in the sorted query side
+      if (task_edge) {
+        hd.fit = 0;
+        hd.g0 = 0u;
+      } else {
+        const int64_t fy0 = (int64_t)f * (cy + 1) - 1;
+        const uint32_t g0 = a.q_off[fy0 * fW], g1 = a.q_off[(fy0 + f + 2) * fW], m = g1 - g0;
+        hd.g0 = g0;
+        hd.need = (uint32_t)((size_t)(f + 2) * fine_rb + (size_t)m * 20);
+        hd.fit = m < 65536u && hd.need <= (uint32_t)a.lds_budget;
+        if (hd.fit) {
+          hd.gm = m;
+          hd.lqidx = (uint32_t)(kJoinHdrBytes + (size_t)(f + 2) * fine_rb + (size_t)m * 16);
+        }
+      }
+    }
   }
-  if ((int)threadIdx.x < nrows && nrows <= kJoinMaxRows) {  // staged bytes of every query row
+  if (!FINE && (int)threadIdx.x < nrows && nrows <= kJoinMaxRows) {  // staged bytes of every query row
     const uint32_t* qo = a.q_off + (r0 + threadIdx.x + 1) * W;
     const uint32_t m = qo[W] - qo[0];
     if (m >= 65536u) hd.fit = 0;
     atomicAdd(&hd.need, (uint32_t)join_row_lds_bytes(W, m < 65536u ? m : 65536u));
   }
   __syncthreads();
-  const bool fit = hd.fit && nrows <= kJoinMaxRows && hd.need <= (uint32_t)a.lds_budget;
-  // stage (or describe) the query rows
-  size_t off = 0;
-  for (int j = 0; j < nrows; ++j) {
-    const int64_t ry = r0 + j;
-    const uint32_t* qo = a.q_off + (ry + 1) * W;
-    const uint32_t b = qo[0], e = qo[W];
-    if (fit) {
-      const uint32_t o16 = (uint32_t)off;
-      uint16_t* lo16 = reinterpret_cast<uint16_t*>(lds + off);
-      off += ((size_t)(W + 1) * 2 + 15) / 16 * 16;
-      const uint32_t oxy = (uint32_t)off;
-      double2* lxy = reinterpret_cast<double2*>(lds + off);
-      off += (size_t)(e - b) * 16;
-      for (int64_t t = threadIdx.x; t <= W; t += kJoinThreads) lo16[t] = (uint16_t)(qo[t] - b);
-      for (uint32_t t = threadIdx.x; t < e - b; t += kJoinThreads) lxy[t] = make_double2(a.sqx[b + t], a.sqy[b + t]);
-      if (threadIdx.x == 0) rows[j] = QRow{(int32_t)ry, b, o16, oxy};
-    } else if (threadIdx.x == 0) {
-      rows[j] = QRow{(int32_t)ry, b, 0xffffffffu, 0u};
+  const bool fit = FINE ? hd.fit != 0 : (hd.fit && nrows <= kJoinMaxRows && hd.need <= (uint32_t)a.lds_budget);
+  const uint32_t g0 = FINE ? hd.g0 : 0u;
+  if (FINE) {
+    if (fit) {  // u16 offsets (relative to g0) of every sub-column of the f + 2 sub-rows, then xy, indices
+      const int64_t fy0 = (int64_t)f * (cy + 1) - 1;
+      for (int sr = 0; sr < f + 2; ++sr) {
+        uint16_t* lo16 = reinterpret_cast<uint16_t*>(lds + sr * fine_rb);
+        const uint32_t* qo = a.q_off + (fy0 + sr) * fW;
+        for (int64_t t = threadIdx.x; t <= fW; t += kJoinThreads) lo16[t] = (uint16_t)(qo[t] - g0);
+      }
+      double2* lxy = reinterpret_cast<double2*>(lds + (f + 2) * fine_rb);
+      const uint32_t m = hd.gm;
+      uint32_t* lq = reinterpret_cast<uint32_t*>(lxy + m);
+      for (uint32_t t = threadIdx.x; t < m; t += kJoinThreads) {
+        lxy[t] = make_double2(a.sqx[g0 + t], a.sqy[g0 + t]);
+        lq[t] = a.sqidx[g0 + t];
+      }
+    }
+  } else {
+    // stage (or describe) the query rows
+    size_t off = 0;
+    for (int j = 0; j < nrows; ++j) {
+      const int64_t ry = r0 + j;
+      const uint32_t* qo = a.q_off + (ry + 1) * W;
+      const uint32_t b = qo[0], e = qo[W];
+      if (fit) {
+        const uint32_t o16 = (uint32_t)off;
+        uint16_t* lo16 = reinterpret_cast<uint16_t*>(lds + off);
+        off += ((size_t)(W + 1) * 2 + 15) / 16 * 16;
+        const uint32_t oxy = (uint32_t)off;
+        double2* lxy = reinterpret_cast<double2*>(lds + off);
+        off += (size_t)(e - b) * 16;
+        for (int64_t t = threadIdx.x; t <= W; t += kJoinThreads) lo16[t] = (uint16_t)(qo[t] - b);
+        for (uint32_t t = threadIdx.x; t < e - b; t += kJoinThreads) lxy[t] = make_double2(a.sqx[b + t], a.sqy[b + t]);
+        if (threadIdx.x == 0) rows[j] = QRow{(int32_t)ry, b, o16, oxy};
+      } else if (threadIdx.x == 0) {
+        rows[j] = QRow{(int32_t)ry, b, 0xffffffffu, 0u};
+      }
     }
   }
-  // the task's points, counting-sorted by column: column per point (u16), column histogram ->
-  // exclusive scan (cursors) -> sorted (column << 13 | local index)
+  // the task's points, counting-sorted by column: column per point (u16; FINE: sub-column |
+  // sub-row << 13), column histogram -> exclusive scan (cursors) -> sorted (column << 13 |
+  // local index; FINE: sub-column << 15 | sub-row << 13 | local index)
+  const int32_t ncol = FINE ? (int32_t)fW : a.qn;
   uint32_t* const lsort = reinterpret_cast<uint32_t*>(lds + a.lds_budget);
   uint16_t* const lcx = reinterpret_cast<uint16_t*>(lsort + kJoinTask);
-  uint32_t* const hist = reinterpret_cast<uint32_t*>(lcx + kJoinTask);  // [qn + 1]
+  uint32_t* const hist = reinterpret_cast<uint32_t*>(lcx + kJoinTask);  // [ncol + 1] (kJoinTask even: 4-B aligned)
   const uint32_t beg = hd.beg, cnt = hd.end - hd.beg;
-  for (int j = threadIdx.x; j <= a.qn; j += kJoinThreads) hist[j] = 0u;
+  for (int j = threadIdx.x; j <= ncol; j += kJoinThreads) hist[j] = 0u;
   __syncthreads();
   {
     constexpr int PER = kJoinTask / kJoinThreads;  // all loads in flight before the first use
-    double xs[PER];
+    double xs[PER], ys[PER];
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
       const uint32_t i = threadIdx.x + u * kJoinThreads;
-      xs[u] = i < cnt ? a.soxy[2 * (size_t)(beg + i)] : 0.0;
+      if (FINE) {
+        const double2 v = i < cnt ? reinterpret_cast<const double2*>(a.soxy)[beg + i] : make_double2(0.0, 0.0);
+        xs[u] = v.x;
+        ys[u] = v.y;
+      } else {
+        xs[u] = i < cnt ? a.soxy[2 * (size_t)(beg + i)] : 0.0;
+      }
     }
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
       const uint32_t i = threadIdx.x + u * kJoinThreads;
       if (i < cnt) {
         const int32_t cx = cell_index(xs[u], a.u_minX, a.u_cl);  // in [0, qn): bucketed points are in grid
-        lcx[i] = (uint16_t)cx;
-        atomicAdd(&hist[cx], 1u);
+        int32_t col = cx, key = cx;
+        if (FINE) {
+          col = f * (cx + 1) + join_sub(xs[u], a.u_minX, a.u_cl, cx, a.fs, f);
+          key = join_sub(ys[u], a.u_minY, a.u_cl, cy, a.fs, f) << 13 | col;
+        }
+        lcx[i] = (uint16_t)key;
+        atomicAdd(&hist[col], 1u);
       }
     }
   }
   __syncthreads();
-  {  // exclusive scan of hist[0 .. qn) in place (each thread a contiguous run of columns)
+  {  // exclusive scan of hist[0 .. ncol) in place (each thread a contiguous run of columns)
     uint32_t* const wsum = hd.wsum;
-    const int per = (a.qn + kJoinThreads - 1) / kJoinThreads, j0 = threadIdx.x * per;
+    const int per = (ncol + kJoinThreads - 1) / kJoinThreads, j0 = threadIdx.x * per;
     uint32_t run = 0;
-    for (int j = j0; j < j0 + per && j < a.qn; ++j) run += hist[j];
+    for (int j = j0; j < j0 + per && j < ncol; ++j) run += hist[j];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     uint32_t inc = run;
 #pragma unroll
@@ -748,7 +928,7 @@ __global__ __launch_bounds__(kJoinThreads) void join_row_probe_kernel(JoinRowArg
     __syncthreads();
     uint32_t before = inc - run;
     for (int w = 0; w < wid; ++w) before += wsum[w];
-    for (int j = j0; j < j0 + per && j < a.qn; ++j) {
+    for (int j = j0; j < j0 + per && j < ncol; ++j) {
       const uint32_t v = hist[j];
       hist[j] = before;
       before += v;
@@ -756,8 +936,9 @@ __global__ __launch_bounds__(kJoinThreads) void join_row_probe_kernel(JoinRowArg
   }
   __syncthreads();
   for (uint32_t i = threadIdx.x; i < cnt; i += kJoinThreads) {
-    const uint32_t cx = lcx[i];
-    lsort[atomicAdd(&hist[cx], 1u)] = cx << 13 | i;
+    const uint32_t key = lcx[i];
+    if (FINE) lsort[atomicAdd(&hist[key & 8191u], 1u)] = (key & 8191u) << 15 | (key >> 13) << 13 | i;
+    else lsort[atomicAdd(&hist[key], 1u)] = key << 13 | i;
   }
   __syncthreads();  // lcx is dead from here: its space holds the wave buffers
 
@@ -765,18 +946,18 @@ __global__ __launch_bounds__(kJoinThreads) void join_row_probe_kernel(JoinRowArg
   const int32_t qnn = a.qn, cc = (int32_t)c;
   uint2* const region = a.tpairs + (size_t)task * a.task_cap;
   JoinWaveBuf wbuf{reinterpret_cast<uint2*>(lcx) + (threadIdx.x >> 6) * kJoinWaveBuf, 0u};
-  // the next wave-step's points are fetched before this step's candidates are walked
+  // the next wave-step's points are fetched before this step's candidates are walked;
+  // branch-free (a lane past the end re-reads entry 0): a load under a branch is waited on at the
+  // branch's join
   struct Pt {
     double2 v;
     uint32_t idx, e;
   };
   auto fetch = [&](uint32_t s) {
-    Pt p{make_double2(0.0, 0.0), 0u, 0u};
-    if (s + lane < cnt) {
-      p.e = lsort[s + lane];
-      p.v = reinterpret_cast<const double2*>(a.soxy)[beg + (p.e & 8191u)];
-      p.idx = a.soidx[beg + (p.e & 8191u)];
-    }
+    Pt p;
+    p.e = lsort[s + lane < cnt ? s + lane : 0u];
+    p.v = reinterpret_cast<const double2*>(a.soxy)[beg + (p.e & 8191u)];
+    p.idx = a.soidx[beg + (p.e & 8191u)];
     return p;
   };
   Pt nxt = fetch((threadIdx.x >> 6) * 64);
@@ -784,6 +965,46 @@ __global__ __launch_bounds__(kJoinThreads) void join_row_probe_kernel(JoinRowArg
     const bool valid = s + lane < cnt;
     const Pt cur = nxt;
     nxt = fetch(s + kJoinThreads);
+    if (FINE) {
+      const int32_t col = (int32_t)(cur.e >> 15), sub = (int32_t)((cur.e >> 13) & 3u);
+      const int32_t cx = col / f - 1;
+      const bool edge = valid && (cx < 1 || cx > qnn - 2);
+      if (task_edge || __ballot(edge) != 0) {  // the cell path, sub-row by sub-row, global memory
+        const JoinLane ln{cur.v.x, cur.v.y, valid ? cx : 0, cy, cur.idx};
+        const int32_t kb = (ln.cx - cc < -1 ? -1 : ln.cx - cc) + 1, ke = (ln.cx + cc > qnn ? qnn : ln.cx + cc) + 2;
+        for (int64_t ry = r0; ry <= r1; ++ry) {
+          for (int32_t sr = 0; sr < f; ++sr) {
+            const uint32_t* qo = a.q_off + ((ry + 1) * f + sr) * fW;
+            const uint32_t tb = valid ? qo[f * kb] : 0u, te = valid ? qo[f * ke] : 0u;
+            join_lane_run<MODE, false, true, true>(a, nullptr, 0u, tb, te, ln, wbuf, hd, region);
+          }
+        }
+      } else {
+        const JoinLane ln{cur.v.x, cur.v.y, cx, cy, cur.idx};
+        uint32_t b[3], e[3];
+        if (fit) {
+          const uint16_t* lo = reinterpret_cast<const uint16_t*>(lds);
+          const uint32_t rs = (uint32_t)(fine_rb / 2);
+#pragma unroll
+          for (int k = 0; k < 3; ++k) {
+            b[k] = valid ? lo[(sub + k) * rs + col - 1] : 0u;
+            e[k] = valid ? lo[(sub + k) * rs + col + 2] : 0u;
+          }
+          const double2* lxy = reinterpret_cast<const double2*>(lds + (f + 2) * fine_rb);
+          join_fine_walk<MODE, true, 4>(a, lxy, g0, b, e, ln, wbuf, hd, region);
+        } else {
+          const int64_t fy0 = (int64_t)f * (cy + 1) - 1;
+#pragma unroll
+          for (int k = 0; k < 3; ++k) {
+            const uint32_t* qo = a.q_off + (fy0 + sub + k) * fW;
+            b[k] = valid ? qo[col - 1] - g0 : 0u;
+            e[k] = valid ? qo[col + 2] - g0 : 0u;
+          }
+          join_fine_walk<MODE, false, 4>(a, nullptr, g0, b, e, ln, wbuf, hd, region);
+        }
+      }
+      continue;
+    }
     const JoinLane ln{cur.v.x, cur.v.y, valid ? (int32_t)(cur.e >> 13) : 0, cy, cur.idx};
     const int32_t kb = (ln.cx - cc < -1 ? -1 : ln.cx - cc) + 1, ke = (ln.cx + cc > qnn ? qnn : ln.cx + cc) + 2;
     for (int j = 0; j < nrows; ++j) {
@@ -810,7 +1031,45 @@ __global__ __launch_bounds__(kJoinThreads) void join_row_probe_kernel(JoinRowArg
   }
   if (wbuf.cnt > 0) wbuf.flush(a, hd, region);
   __syncthreads();
-  if (threadIdx.x == 0) a.task_cnt[task] = hd.fit_end;
+  if (threadIdx.x == 0) store_u32_wt(&a.task_cnt[task], hd.fit_end);
+}
+
+template <int MODE, int FINE>
+__global__ __launch_bounds__(kJoinThreads) void join_row_probe_kernel(JoinRowArgs a) {
+  // every LDS variable lives in the dynamic region, header first (a static __shared__ block in
+  // front would shift the dynamic base off 16 B: misaligned ds_read_b128 of the staged xy)
+  extern __shared__ __attribute__((aligned(16))) char lds_base[];
+  JoinProbeHdr& hd = *reinterpret_cast<JoinProbeHdr*>(lds_base);
+  // XCD-aware task order: workgroups go round-robin to the 8 XCDs, so XCD x gets the
+  // consecutive tasks [x * per, (x + 1) * per) -- neighbouring row tasks stage the same query
+  // rows, and they now meet in the same L2.  The grid is >= ntask + 8 (host); slots past ntask
+  // are zeroed by the block of the same index.
+  const uint32_t ntask = a.task_off[a.nrows];
+  if (blockIdx.x >= ntask && threadIdx.x == 0) store_u32_wt(&a.task_cnt[blockIdx.x], 0u);
+  const uint32_t per = (ntask + 7) / 8;
+  const uint32_t task = (blockIdx.x & 7u) * per + (blockIdx.x >> 3);
+  if ((blockIdx.x >> 3) < per && task < ntask) join_probe_task<MODE, FINE>(a, task, lds_base);
+  // the last block to finish scans the task counts into the packing offsets (no scan launch);
+  // each block's count was stored write-through and drained before its ticket
+  if (threadIdx.x == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    hd.fit = atomicAdd(a.ticket, 1u) == gridDim.x - 1 ? 1 : 0;
+  }
+  __syncthreads();
+  if (!hd.fit) return;
+  uint32_t carry = 0;
+  for (uint32_t b = 0; b < a.nslots; b += kJoinThreads) {  // block-uniform
+    const uint32_t i = b + threadIdx.x;
+    const uint32_t v = i < a.nslots ? __hip_atomic_load(&a.task_cnt[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+    uint32_t total;
+    const uint32_t ex = join_block_scan<kJoinThreads>(v, &total, hd.wsum);
+    if (i < a.nslots) a.tkoff[i] = carry + ex;
+    carry += total;
+  }
+  if (threadIdx.x == 0) {
+    a.tkoff[a.nslots] = carry;
+    __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 // Block t < ntask: its output offset = sum of task_cnt[0..t) (a block reduction over <= a few
@@ -862,31 +1121,38 @@ hipError_t launch_join_compact(gf_ctx* ctx, const JoinCompactArgs& a) {
   return hipGetLastError();
 }
 
-hipError_t launch_join_rows(gf_ctx* ctx, const JoinRowArgs& a, int stage, int blocks) {
+hipError_t launch_join_rows(gf_ctx* ctx, const JoinRowArgs& a, const JoinQueryArgs& q, int stage) {
   hipStream_t s = ctx->stream;
+  const dim3 grid((unsigned)(q.nblk + a.nblk));
   switch (stage) {
     case 0: {
       KTimer t(ctx, GF_K_JOIN_BUCKET);
-      hipLaunchKernelGGL(join_orow_hist_kernel, dim3(blocks), dim3(kScatThreads), 0, s, a, a.row_mat);
+      hipLaunchKernelGGL(join_hist_kernel, dim3((unsigned)(kHistSplit * (q.nblk + a.nblk))), dim3(kScatThreads), 0, s,
+                         a, q);
       break;
     }
     case 1: {
       KTimer t(ctx, GF_K_JOIN_BUCKET);
-      hipLaunchKernelGGL(join_orow_scatter_kernel, dim3(blocks), dim3(kScatThreads), join_scatter_lds_bytes(a.qn), s,
-                         a, a.row_mat_scan);
+      hipLaunchKernelGGL(join_scatter_kernel, grid, dim3(kScatThreads),
+                         join_scatter_lds_bytes(a.nrows > q.qn + 2 ? a.nrows : q.qn + 2), s, a, q);
       break;
     }
-    case 2:  // blocks = the bucketing grid size
-      hipLaunchKernelGGL(join_rows_finish_kernel, dim3((a.qn + 1 + kBlock - 1) / kBlock), dim3(kBlock), 0, s,
-                         a.row_mat_scan, a.qn, blocks, (uint32_t)((size_t)a.qn * blocks), a.row_off_w, a.row_tasks);
+    case 2:
+      hipLaunchKernelGGL(join_sort_finish_kernel, dim3((unsigned)(q.qn + 3)), dim3(kScatThreads), 0, s, a, q);
       break;
     case 3: {
       KTimer t(ctx, GF_K_JOIN_PROBE);
-      const size_t lds = join_probe_lds_bytes(a.lds_budget, a.qn);
-      if (!a.approx && a.metric == 0)
-        hipLaunchKernelGGL(join_row_probe_kernel<0>, dim3(blocks), dim3(kJoinThreads), lds, s, a);
-      else
-        hipLaunchKernelGGL(join_row_probe_kernel<1>, dim3(blocks), dim3(kJoinThreads), lds, s, a);
+      const size_t lds = join_probe_lds_bytes(a.lds_budget, a.qn, a.f);
+      const dim3 pg(a.nslots);
+      const bool m0 = !a.approx && a.metric == 0;
+      if (a.f > 1) {  // host: the fine path is exact (never approximate)
+        if (m0) hipLaunchKernelGGL((join_row_probe_kernel<0, 1>), pg, dim3(kJoinThreads), lds, s, a);
+        else hipLaunchKernelGGL((join_row_probe_kernel<1, 1>), pg, dim3(kJoinThreads), lds, s, a);
+      } else if (m0) {
+        hipLaunchKernelGGL((join_row_probe_kernel<0, 0>), pg, dim3(kJoinThreads), lds, s, a);
+      } else {
+        hipLaunchKernelGGL((join_row_probe_kernel<1, 0>), pg, dim3(kJoinThreads), lds, s, a);
+      }
       break;
     }
   }

@@ -498,6 +498,116 @@ __global__ __launch_bounds__(kExpandWords) void expand_async_kernel(const uint64
   if (bid == (uint64_t)gridDim.x - 1 && threadIdx.x == 0) *count = (int64_t)(base + total);
 }
 
+// Single-pass exclusive scan (one launch): tiles of 1024 threads x 16 items, each tile's
+// prefix by the same decoupled look-back as expand_async (ticket-ordered tile ids, epoch-tagged
+// status words).  out[L] = total; out2[i] = out[i] for i < n2 (a cursor copy); in[i] = 0 for
+// i < nz after it is read (a histogram that must be zero for the next call).
+constexpr int kScan1Items = 16;
+constexpr int kScan1Tile = kScanThreads * kScan1Items;
+int64_t scan1_blocks(int64_t L) { return (L + kScan1Tile - 1) / kScan1Tile; }
+
+__global__ __launch_bounds__(kScanThreads) void scan1_kernel(uint32_t* __restrict__ in, int64_t L,
+                                                             uint32_t* __restrict__ out, uint32_t* __restrict__ out2,
+                                                             int64_t n2, int64_t nz, ExpandState st) {
+  __shared__ unsigned long long s_bid, s_prefix;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (threadIdx.x == 0) s_bid = atomicAdd(st.ticket, 1ull) - st.base;
+  __syncthreads();
+  const uint64_t bid = s_bid;
+  const int64_t base = (int64_t)bid * kScan1Tile + (int64_t)threadIdx.x * kScan1Items;
+  uint32_t v[kScan1Items];
+  uint32_t s = 0;
+  if (base + kScan1Items <= L) {  // 16-byte aligned (host): four uint4 loads
+#pragma unroll
+    for (int j = 0; j < kScan1Items / 4; ++j) {
+      const uint4 u = reinterpret_cast<const uint4*>(in + base)[j];
+      v[4 * j] = u.x; v[4 * j + 1] = u.y; v[4 * j + 2] = u.z; v[4 * j + 3] = u.w;
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < kScan1Items; ++j) v[j] = base + j < L ? in[base + j] : 0u;
+  }
+#pragma unroll
+  for (int j = 0; j < kScan1Items; ++j) s += v[j];
+  if (base < nz) {
+    if (base + kScan1Items <= nz) {
+#pragma unroll
+      for (int j = 0; j < kScan1Items / 4; ++j) reinterpret_cast<uint4*>(in + base)[j] = make_uint4(0u, 0u, 0u, 0u);
+    } else {
+      for (int j = 0; j < kScan1Items; ++j) if (base + j < nz) in[base + j] = 0u;
+    }
+  }
+  uint32_t total;
+  const uint32_t ex = block_excl_scan(s, &total);
+  if (wid == 0) {  // publish the aggregate, then look back (as expand_async_kernel)
+    unsigned long long* my = st.status + bid;
+    const uint64_t ep = st.epoch & 0x3FFFFFFu;
+    if (bid == 0) {
+      if (lane == 0) __hip_atomic_store(my, lb_pack(st.epoch, kLbInc, total), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (lane == 0) s_prefix = 0;
+    } else {
+      if (lane == 0) __hip_atomic_store(my, lb_pack(st.epoch, kLbAgg, total), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      uint64_t prefix = 0;
+      int64_t hi = (int64_t)bid - 1;
+      for (;;) {
+        const int64_t p = hi - lane;
+        const uint64_t w = p >= 0 ? __hip_atomic_load(st.status + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+        const bool ready = p < 0 || ((w >> 38) == ep && ((w >> 36) & 3ull) != 0ull);
+        if (__ballot(!ready)) {
+          __builtin_amdgcn_s_sleep(1);
+          continue;
+        }
+        const bool incl = p >= 0 && ((w >> 36) & 3ull) == kLbInc;
+        const uint64_t incm = __ballot(incl);
+        const int stop = incm ? __ffsll((unsigned long long)incm) - 1 : 64;
+        uint64_t add = lane <= stop ? (w & ((1ull << 36) - 1ull)) : 0ull;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) add += __shfl_xor(add, o, 64);
+        prefix += add;
+        if (incm || hi - 64 < 0) break;
+        hi -= 64;
+      }
+      if (lane == 0) {
+        __hip_atomic_store(my, lb_pack(st.epoch, kLbInc, prefix + total), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_prefix = prefix;
+      }
+    }
+  }
+  __syncthreads();
+  uint32_t run = (uint32_t)s_prefix + ex;
+  uint32_t o[kScan1Items];
+#pragma unroll
+  for (int j = 0; j < kScan1Items; ++j) {
+    o[j] = run;
+    run += v[j];
+    if (base + j == L - 1) out[L] = run;  // the total
+  }
+  if (base + kScan1Items <= L) {
+#pragma unroll
+    for (int j = 0; j < kScan1Items / 4; ++j)
+      reinterpret_cast<uint4*>(out + base)[j] = make_uint4(o[4 * j], o[4 * j + 1], o[4 * j + 2], o[4 * j + 3]);
+  } else {
+    for (int j = 0; j < kScan1Items; ++j) if (base + j < L) out[base + j] = o[j];
+  }
+  if (base < n2) {
+    if (base + kScan1Items <= n2) {
+#pragma unroll
+      for (int j = 0; j < kScan1Items / 4; ++j)
+        reinterpret_cast<uint4*>(out2 + base)[j] = make_uint4(o[4 * j], o[4 * j + 1], o[4 * j + 2], o[4 * j + 3]);
+    } else {
+      for (int j = 0; j < kScan1Items; ++j) if (base + j < n2) out2[base + j] = o[j];
+    }
+  }
+}
+
+hipError_t launch_scan1(hipStream_t s, uint32_t* in, int64_t L, uint32_t* out, uint32_t* out2, int64_t n2, int64_t nz,
+                        const ExpandState& st) {
+  if (L <= 0) return hipMemsetAsync(out, 0, sizeof(uint32_t), s);
+  hipLaunchKernelGGL(scan1_kernel, dim3((unsigned)scan1_blocks(L)), dim3(kScanThreads), 0, s, in, L, out, out2, n2, nz,
+                     st);
+  return hipGetLastError();
+}
+
 int64_t expand_blocks(int64_t words) { return (words + kExpandWords - 1) / kExpandWords; }
 
 hipError_t launch_expand_bitmap_async(hipStream_t s, const uint64_t* bitmap, int64_t words, int64_t n, uint32_t* idx,

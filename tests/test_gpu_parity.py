@@ -529,6 +529,48 @@ def test_join_row_path_edges(sf, oracle_mod, n, r, qn, qbox):
         np.testing.assert_array_equal(got, exp, err_msg=f"legacy={legacy}")
 
 
+@pytest.mark.parametrize("n,r,metric", [(1000, 0.001, 0), (100, 0.0069, 0), (100, 0.0052, 1), (300, 0.0034, 0),
+                                         (300, 0.0034, 1)])
+def test_join_fine_subcells(sf, oracle_mod, n, r, metric):
+    """The row path's sub-cell variant (c == 1, cl/f > r: f = 2, 3, 4) against the cell
+    variant (GF_FLAG_JOIN_COARSE) and the oracle: r just below cl/f, pairs straddling cell and
+    sub-cell bounds (points on the bounds, +-1 ulp, partners at r (1 - 1e-15) across them),
+    edge cells, NaN and outside-the-grid points on both sides."""
+    from spatialflink_amd import _lib
+
+    g = sf.UniformGrid(n, *BEIJING)
+    og = oracle_mod.grid(n, *BEIJING)
+    cl = (BEIJING[1] - BEIJING[0]) / n
+    f = 4 if cl / 4 > r else (3 if cl / 3 > r else 2)
+    ox, oy = oracle_mod.java_random_points(101, 150_000, 115.45, 117.65, 39.55, 41.15)
+    qx, qy = oracle_mod.java_random_points(102, 40_000, 115.45, 117.65, 39.55, 41.15)
+    rng = np.random.default_rng(7)
+    k = rng.integers(0, n * f, 4000)
+    bx = BEIJING[0] + k * (cl / f)  # sub-cell and cell bounds
+    by = BEIJING[2] + rng.integers(0, n * f, 4000) * (cl / f)
+    bx = np.where(rng.random(4000) < 0.5, np.nextafter(bx, np.inf), np.nextafter(bx, -np.inf))
+    ox[:4000], oy[:4000] = bx, by
+    ang = rng.random(4000) * 2 * np.pi
+    qx[:4000] = bx + r * (1 - 1e-15) * np.cos(ang)
+    qy[:4000] = by + r * (1 - 1e-15) * np.sin(ang)
+    qx[4000:4400], qy[4000:4400] = bx[:400] + r * (1 - 1e-15), by[:400]  # axis-aligned partners
+    ox[5000:5003] = np.nan
+    qy[5000:5003] = np.nan
+    qx[6000:6030] = BEIJING[0] - np.linspace(0, 0.02, 30)
+    ox[6000:6030] = BEIJING[0] + np.linspace(0, 0.0005, 30)
+    st, pairs = oracle_mod.join_pp(og, og, ox, oy, qx, qy, r, metric=metric)
+    assert st == 0 and len(pairs) > 4000
+    exp = np.array(sorted(map(tuple, pairs.tolist())), np.int64).reshape(-1, 2)
+    ctx = _lib.context(0)
+    for coarse in (0, 1):
+        _lib.check(_lib.lib().gf_ctx_set_flag(ctx.handle, _lib.FLAG_JOIN_COARSE, coarse), ctx.handle, "flag")
+        try:
+            got = sf.PointPointJoinQuery(conf(sf, False, metric), g, g).run(win(sf, ox, oy), win(sf, qx, qy), r)
+        finally:
+            _lib.lib().gf_ctx_set_flag(ctx.handle, _lib.FLAG_JOIN_COARSE, 0)
+        np.testing.assert_array_equal(got, exp, err_msg=f"coarse={coarse} f={f}")
+
+
 def test_join_dense_rows_fall_back_to_global(sf, oracle_mod):
     """A query row too dense to stage in LDS (every query point in one cell row) takes the
     task's global-memory probe; a single dense cell as well."""
