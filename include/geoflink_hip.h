@@ -187,7 +187,9 @@ int  gf_range_run(gf_range_plan* plan, const gf_points* pts, uint64_t* bitmap,
 int  gf_range_plan_stats(const gf_range_plan* plan, int64_t* none_cells, int64_t* candidate_cells,
                          int64_t* guaranteed_cells, int64_t* inside_cells);
 /* Tuning: scan blocks (0 = auto, <= 8 per CU); candidate tests: 0 auto, 1 inline in the scan,
- * 2 deferred to a second kernel over the queued points (table modes). */
+ * 2 deferred (each scan block tests the candidate-cell points it queued at its end), 3 deferred
+ * with the span prefilter (the scan only rules out points outside the class spans; every other
+ * point is classified by the table at the block's end) -- table modes. */
 int  gf_range_plan_set_tuning(gf_range_plan* plan, int32_t scan_blocks, int32_t defer_mode);
 /* Sync: selection bitmap -> ascending point indices (device uint32[cap]). */
 int  gf_bitmap_to_indices(gf_ctx* ctx, const uint64_t* bitmap, int64_t n, uint32_t* idx,

@@ -649,6 +649,15 @@ int build_table(gf_range_plan* P, const std::vector<Rect>& base, bool need_lists
       }
     P->sx_lo = chi < 0 ? xt[n] : xt[clo];  // empty: sx_lo == sx_hi, every x fails
     P->sx_hi = chi < 0 ? xt[n] : xt[chi + 1];
+    int64_t rlo = n, rhi = -1;  // rows holding any class
+    for (int64_t y = 0; y < n; ++y)
+      if ((rows[y] & 0xffffu) <= (rows[y] >> 16)) {
+        rlo = std::min<int64_t>(rlo, y);
+        rhi = std::max<int64_t>(rhi, y);
+      }
+    P->sy_lo = rhi < 0 ? yt[n] : yt[rlo];
+    P->sy_hi = rhi < 0 ? yt[n] : yt[rhi + 1];
+    P->span_frac = chi < 0 ? 0.0 : (double)(chi - clo + 1) * (double)(rhi - rlo + 1) / ((double)n * (double)n);
     if ((st = upload(ctx, &P->xt, xt)) || (st = upload(ctx, &P->yt, yt))) return st;
   }
 
@@ -892,6 +901,7 @@ RangeArgs range_args(const gf_range_plan* P, const gf_points* pts, uint64_t* bit
   a.span_lds = P->span_bytes <= kSpanLdsBytes;
   a.xt = P->xt; a.yt = P->yt; a.x_lo = P->x_lo; a.x_hi = P->x_hi; a.y_lo = P->y_lo; a.y_hi = P->y_hi;
   a.sx_lo = P->sx_lo; a.sx_hi = P->sx_hi;
+  a.sy_lo = P->sy_lo; a.sy_hi = P->sy_hi;
   a.inv_cl = 1.0 / P->grid.cellLength;
   a.cand_off = P->cand_off; a.cand_list = P->cand_list;
   a.approx = P->approx; a.metric = P->metric; a.r = P->r; a.s_r = s_prefilter(P->r, 0);
@@ -962,9 +972,12 @@ extern "C" int gf_range_run(gf_range_plan* P, const gf_points* pts, uint64_t* bi
   // Auto: defer while candidate cells are more than 5% of the non-none cells.
   const int64_t live = P->cls_cells[1] + P->cls_cells[2] + P->cls_cells[3];
   const bool can_defer = P->table_mode && (P->poly || !P->approx);
-  const bool defer = can_defer && (P->defer_mode == 2 || (P->defer_mode == 0 && P->cls_cells[1] * 20 > live));
+  const bool defer = can_defer && (P->defer_mode >= 2 || (P->defer_mode == 0 && P->cls_cells[1] * 20 > live));
   if (defer) {
     if ((st = ensure_queue(P, a, blocks, false))) return st;
+    // span prefilter when the class spans cover at most a quarter of the grid (defer_mode 3
+    // forces it): the stream skips the table, the block's queued points are classified after it
+    a.span_mode = P->xt && (P->defer_mode == 3 || (P->defer_mode != 2 && P->span_frac <= 0.25));
   }
   // the counts are summed by the last block of the window's last kernel (no finalize launch)
   a.counts = counts;
@@ -1022,7 +1035,7 @@ extern "C" int gf_range_plan_stats(const gf_range_plan* P, int64_t* none_cells, 
 }
 
 extern "C" int gf_range_plan_set_tuning(gf_range_plan* P, int32_t scan_blocks, int32_t defer_mode) {
-  if (!P || scan_blocks < 0 || scan_blocks > P->ctx->num_cus * 8 || defer_mode < 0 || defer_mode > 2)
+  if (!P || scan_blocks < 0 || scan_blocks > P->ctx->num_cus * 8 || defer_mode < 0 || defer_mode > 3)
     return GF_ERR_ARG;
   P->scan_blocks = scan_blocks;
   P->defer_mode = defer_mode;

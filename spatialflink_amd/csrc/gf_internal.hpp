@@ -237,6 +237,8 @@ struct RangeArgs {
   const double* yt;
   double x_lo, x_hi, y_lo, y_hi;  // xt[0], xt[n], yt[0], yt[n]
   double sx_lo, sx_hi;       // xt[first], xt[last + 1] over every row's span: x outside => no class
+  double sy_lo, sy_hi;       // yt[first], yt[last + 1] over the rows holding a class
+  int span_mode;             // deferred tests with the span prefilter (range_kernel DEFER 3)
   double inv_cl;
   const int32_t* extra;      // [n_extra*4]: x0, x1, y0, y1 (inclusive) accepted out-of-grid cells
   int32_t n_extra;
@@ -620,6 +622,8 @@ struct gf_range_plan {
   double* yt = nullptr;
   double x_lo = 0, x_hi = 0, y_lo = 0, y_hi = 0;
   double sx_lo = 0, sx_hi = 0;
+  double sy_lo = 0, sy_hi = 0;
+  double span_frac = 1.0;  // share of the grid's cells inside the x / y spans
   int32_t* extra = nullptr;
   int32_t n_extra = 0;
   int32_t* cand_off = nullptr;

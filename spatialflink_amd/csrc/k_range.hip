@@ -115,6 +115,15 @@ __device__ __forceinline__ int classify_finish(const RangeArgs& a, double px, do
 }
 
 
+// OR bit i into the bitmap word this block stored during its scan: workgroup scope -- the
+// atomic is performed in this XCD's L2, which holds the block's own (drained) store of the word;
+// other blocks only write other words, byte-masked (device scope went past L2 for each of the
+// ~5e5 accepted points of a C3 window).
+__device__ __forceinline__ void bitmap_or(uint64_t* bitmap, uint32_t i) {
+  __hip_atomic_fetch_or(reinterpret_cast<unsigned long long*>(bitmap) + (i >> 6), 1ull << (i & 63),
+                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
 // candidate-cell test: exists object within r (first hit wins, emitted once).  The answer is
 // an existential over the cell's object list, so visiting order is free: polygons whose
 // envelope holds the point go first, polygons whose envelope is farther than r are skipped.
@@ -175,8 +184,8 @@ __device__ __forceinline__ void eval_point(const RangeArgs& a, double px, double
   multi = false;
   defer = false;
   if (!valid) return;
-  if (DEFER == 2) {  // point-polygon join: every point whose key some polygon replicates to
-    defer = cls != kNone;
+  if (DEFER >= 2) {  // 2: point-polygon join (every point whose key some polygon replicates to);
+    defer = cls != kNone;  // 3: span prefilter (every point not ruled out by the class spans)
     return;
   }
   if (cls == kAccept) {
@@ -223,11 +232,58 @@ __device__ __forceinline__ void queue_append2(bool c0, uint32_t i0, double x0, d
   }
 }
 
+// Span prefilter (DEFER 3): the points not ruled out by span_maybe are collected in a per-wave
+// LDS buffer (ballot + mbcnt, the count in a scalar register) and classified with the table 64
+// at a time, one per lane, interleaved with the stream: accepted points set their bit (an atomic
+// OR into the word this wave stored), candidate-cell points go to the block's queue for
+// drain_own_queue at the block's end.  (Classifying them all at the end of each block cost
+// 21 us of a 74 us C3 window: no block's stream overlapped it.)
+constexpr int kWaveQ = 192;  // < 64 left after a round + one tile's 128
+struct WaveQ {
+  uint32_t* idx;
+  double2* xy;
+  uint32_t cnt;
+};
+template <int POLY>
+__device__ __forceinline__ void waveq_round(const RangeArgs& a, const RangeLds& L, WaveQ& q, uint32_t take,
+                                            uint64_t& hits, uint32_t* lcount) {
+  const uint32_t lane = threadIdx.x & 63;
+  const bool valid = lane < take;
+  const uint32_t i = q.idx[valid ? lane : 0u];
+  const double2 v = q.xy[valid ? lane : 0u];
+  const int32_t slot = cell_slot<1>(a, L, v.x, v.y);
+  const int cls = valid ? classify_finish<1>(a, v.x, v.y, slot, table_load(a, L, slot)) : kNone;
+  const bool acc = cls == kAccept;
+  if (acc) bitmap_or(a.bitmap, i);
+  hits += (uint64_t)__popcll(__ballot(acc));
+  queue_append2(cls == kTest, i, v.x, v.y, false, 0u, 0.0, 0.0, a, lcount);
+  // the rest [take, cnt) moves to the front (all reads before the writes)
+  const uint32_t rest = q.cnt - take;
+  uint32_t ri[2];
+  double2 rv[2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const uint32_t r = lane + 64 * k;
+    ri[k] = r < rest ? q.idx[take + r] : 0u;
+    rv[k] = r < rest ? q.xy[take + r] : make_double2(0.0, 0.0);
+  }
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const uint32_t r = lane + 64 * k;
+    if (r < rest) {
+      q.idx[r] = ri[k];
+      q.xy[r] = rv[k];
+    }
+  }
+  q.cnt = rest;
+}
+
 // One wave-tile = 128 consecutive points = bitmap words w, w+1: lane l evaluates points
 // t + l and t + 64 + l, so the two ballots ARE the two words (one 16-B store by lane 0).
 template <int TABLE, int POLY, int DEFER, bool FULL>
 __device__ __forceinline__ void range_tile(const RangeArgs& a, int64_t t, double x0, double y0, double x1, double y1,
-                                           int c0, int c1, uint64_t& hits, uint64_t& mult, uint32_t* lcount) {
+                                           int c0, int c1, uint64_t& hits, uint64_t& mult, uint32_t* lcount,
+                                           WaveQ& wq, const RangeLds& L) {
   const int lane = threadIdx.x & 63;
   const int64_t i0 = t + lane, i1 = t + 64 + lane;
   const bool v0 = FULL || i0 < a.n, v1 = FULL || i1 < a.n;
@@ -248,7 +304,25 @@ __device__ __forceinline__ void range_tile(const RangeArgs& a, int64_t t, double
     }
     mult += (uint64_t)(__popcll(e0) + __popcll(e1));
   }
-  if (DEFER) queue_append2(d0, (uint32_t)i0, x0, y0, d1, (uint32_t)i1, x1, y1, a, lcount);
+  if (DEFER == 3) {  // into the wave's buffer; classify whenever 64 are collected
+    const uint64_t q0 = __ballot(d0), q1 = __ballot(d1);
+    const uint32_t n0 = (uint32_t)__popcll(q0);
+    const uint64_t below = (1ull << lane) - 1ull;
+    if (d0) {
+      const uint32_t pos = wq.cnt + (uint32_t)__popcll(q0 & below);
+      wq.idx[pos] = (uint32_t)i0;
+      wq.xy[pos] = make_double2(x0, y0);
+    }
+    if (d1) {
+      const uint32_t pos = wq.cnt + n0 + (uint32_t)__popcll(q1 & below);
+      wq.idx[pos] = (uint32_t)i1;
+      wq.xy[pos] = make_double2(x1, y1);
+    }
+    wq.cnt += n0 + (uint32_t)__popcll(q1);
+    while (wq.cnt >= 64) waveq_round<POLY>(a, L, wq, 64u, hits, lcount);
+  } else if (DEFER) {
+    queue_append2(d0, (uint32_t)i0, x0, y0, d1, (uint32_t)i1, x1, y1, a, lcount);
+  }
   hits += (uint64_t)(__popcll(b0) + __popcll(b1));
 }
 
@@ -285,9 +359,28 @@ __device__ __forceinline__ void range_load(RangeBuf<U>& b, const RangeArgs& a, i
 template <int TABLE, int POLY, int DEFER, int U>
 __device__ __forceinline__ void range_stage(const RangeArgs& a, const RangeLds& L, const RangeBuf<U>& cur, int64_t t, RangeBuf<U>& nxt,
                                             int64_t tn, int64_t tstride, uint64_t& hits, uint64_t& mult,
-                                            uint32_t* lcount) {
+                                            uint32_t* lcount, WaveQ& wq) {
   int32_t s0[U], s1[U];
   int c0[U], c1[U];
+  if constexpr (DEFER == 3) {  // span prefilter: no table gathers in the stream (WaveQ)
+    range_load<U>(nxt, a, tn, tstride);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      c0[u] = span_maybe(a, cur.xa[u], cur.ya[u]) ? kTest : kNone;
+      c1[u] = span_maybe(a, cur.xb[u], cur.yb[u]) ? kTest : kNone;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t tu = t + u * tstride;
+      if (tu + 128 <= a.n)
+        range_tile<TABLE, POLY, DEFER, true>(a, tu, cur.xa[u], cur.ya[u], cur.xb[u], cur.yb[u], c0[u], c1[u], hits,
+                                             mult, lcount, wq, L);
+      else if (tu < a.n)
+        range_tile<TABLE, POLY, DEFER, false>(a, tu, cur.xa[u], cur.ya[u], cur.xb[u], cur.yb[u], c0[u], c1[u], hits,
+                                              mult, lcount, wq, L);
+    }
+    return;
+  }
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     s0[u] = cell_slot<TABLE>(a, L, cur.xa[u], cur.ya[u]);
@@ -309,10 +402,10 @@ __device__ __forceinline__ void range_stage(const RangeArgs& a, const RangeLds& 
     const int64_t tu = t + u * tstride;
     if (tu + 128 <= a.n)
       range_tile<TABLE, POLY, DEFER, true>(a, tu, cur.xa[u], cur.ya[u], cur.xb[u], cur.yb[u], c0[u], c1[u], hits,
-                                           mult, lcount);
+                                           mult, lcount, wq, L);
     else if (tu < a.n)
       range_tile<TABLE, POLY, DEFER, false>(a, tu, cur.xa[u], cur.ya[u], cur.xb[u], cur.yb[u], c0[u], c1[u], hits,
-                                            mult, lcount);
+                                            mult, lcount, wq, L);
   }
 }
 
@@ -414,11 +507,22 @@ __device__ uint64_t drain_own_queue(const RangeArgs& a, const uint32_t& lcount) 
     const uint64_t won = __ballot(valid && g == 0 && ghit);
     if (valid && g == 0 && ghit) {
       const uint32_t i = a.queue[pos];
-      atomicOr((unsigned long long*)&a.bitmap[i >> 6], 1ull << (i & 63));
+      bitmap_or(a.bitmap, i);
     }
     hits += (uint64_t)__popcll(won);
   }
   return hits;
+}
+
+// Span prefilter (DEFER 3): an in-grid point whose x lies outside the union of the rows' class
+// spans, or whose y lies outside the rows holding any class, is in a none cell (exact through
+// the cell thresholds); every other point -- NaN and out-of-grid ones included -- is queued and
+// classified with the table at the end of its block (drain_span_queue).  The stream then has
+// the interval kernel's shape (two compares per point, no table gathers, a small register
+// footprint), which pays when the classes cover a small part of the grid.
+__device__ __forceinline__ bool span_maybe(const RangeArgs& a, double px, double py) {
+  const bool in_grid = px >= a.x_lo && px < a.x_hi && py >= a.y_lo && py < a.y_hi;
+  return !in_grid || (px >= a.sx_lo && px < a.sx_hi && py >= a.sy_lo && py < a.sy_hi);
 }
 
 // dynamic-LDS header of range_kernel: lcount, pad, sh[kBlock/64], sm[kBlock/64] (16 B multiple)
@@ -440,6 +544,7 @@ __global__ __launch_bounds__(kBlock, GF_RANGE_WAVES) void range_kernel(RangeArgs
   uint64_t* const sm = sh + kBlock / 64;                           // [kBlock / 64] multiplicity
   uint32_t* const lds = lds_base + kRangeHdrWords;
   RangeLds L{nullptr, nullptr, nullptr, nullptr, nullptr};
+  WaveQ wq{nullptr, nullptr, 0u};
   if (DEFER || TABLE) {
     if (threadIdx.x == 0) lcount = 0u;
     if (TABLE) {
@@ -468,6 +573,13 @@ __global__ __launch_bounds__(kBlock, GF_RANGE_WAVES) void range_kernel(RangeArgs
         const uint32_t* gs = reinterpret_cast<const uint32_t*>(a.spans);
         for (int j = threadIdx.x; j < (a.span_bytes + 3) / 4; j += kBlock) ls[j] = gs[j];
         L.spans = reinterpret_cast<const uint8_t*>(ls);
+        tail += (a.span_bytes + 3) & ~3;
+      }
+      if (DEFER == 3) {  // the waves' buffers (16-B aligned)
+        char* wb = reinterpret_cast<char*>(((uintptr_t)tail + 15) & ~(uintptr_t)15);
+        const int w = threadIdx.x >> 6;
+        wq.xy = reinterpret_cast<double2*>(wb) + w * kWaveQ;
+        wq.idx = reinterpret_cast<uint32_t*>(reinterpret_cast<double2*>(wb) + (kBlock / 64) * kWaveQ) + w * kWaveQ;
       }
     }
     __syncthreads();
@@ -481,10 +593,14 @@ __global__ __launch_bounds__(kBlock, GF_RANGE_WAVES) void range_kernel(RangeArgs
   if (pairs > 0) range_load<U>(A, a, t0, tstride);
   for (int64_t p = 0; p < pairs; ++p) {
     const int64_t ta = t0 + 2 * p * sstride;
-    range_stage<TABLE, POLY, DEFER, U>(a, L, A, ta, B, ta + sstride, tstride, hits, mult, &lcount);
-    range_stage<TABLE, POLY, DEFER, U>(a, L, B, ta + sstride, A, ta + 2 * sstride, tstride, hits, mult, &lcount);
+    range_stage<TABLE, POLY, DEFER, U>(a, L, A, ta, B, ta + sstride, tstride, hits, mult, &lcount, wq);
+    range_stage<TABLE, POLY, DEFER, U>(a, L, B, ta + sstride, A, ta + 2 * sstride, tstride, hits, mult, &lcount, wq);
   }
   if (DEFER == 1) hits += drain_own_queue<POLY>(a, lcount);
+  if (DEFER == 3) {
+    if (wq.cnt > 0) waveq_round<POLY>(a, L, wq, wq.cnt, hits, &lcount);
+    hits += drain_own_queue<POLY>(a, lcount);
+  }
   // per-block partial counts (plain stores; summed by range_finalize)
   const int wid = threadIdx.x >> 6;
   if ((threadIdx.x & 63) == 0) { sh[wid] = hits; sm[wid] = mult; }
@@ -768,15 +884,18 @@ hipError_t launch_range(gf_ctx* ctx, const RangeArgs& a, int table_mode, int pol
   const size_t lds = 4 * kRangeHdrWords + (table_mode ? sizeof(uint32_t) * (size_t)((2 * a.grid_n + 1) & ~1) +
                                            (a.xt ? 2 * sizeof(double) * (size_t)(a.grid_n + 1) : 0) +
                                            (a.span_lds ? (size_t)((a.span_bytes + 3) & ~3) : 0)
-                                     : 0);
+                                     : 0) +
+                     (a.span_mode ? 16 + (size_t)(kBlock / 64) * kWaveQ * (16 + 4) : 0);
   {
     KTimer t(ctx, GF_K_RANGE_SCAN);
     if (!table_mode && !poly) hipLaunchKernelGGL((range_kernel<0, 0, 0, kRangeU>), g, b, lds, ctx->stream, a);
     else if (!poly) {
-      if (defer) hipLaunchKernelGGL((range_kernel<1, 0, 1, kRangeU>), g, b, lds, ctx->stream, a);
+      if (defer && a.span_mode) hipLaunchKernelGGL((range_kernel<1, 0, 3, kRangeU>), g, b, lds, ctx->stream, a);
+      else if (defer) hipLaunchKernelGGL((range_kernel<1, 0, 1, kRangeU>), g, b, lds, ctx->stream, a);
       else hipLaunchKernelGGL((range_kernel<1, 0, 0, kRangeU>), g, b, lds, ctx->stream, a);
     } else {
-      if (defer) hipLaunchKernelGGL((range_kernel<1, 1, 1, kRangeU>), g, b, lds, ctx->stream, a);
+      if (defer && a.span_mode) hipLaunchKernelGGL((range_kernel<1, 1, 3, kRangeU>), g, b, lds, ctx->stream, a);
+      else if (defer) hipLaunchKernelGGL((range_kernel<1, 1, 1, kRangeU>), g, b, lds, ctx->stream, a);
       else hipLaunchKernelGGL((range_kernel<1, 1, 0, kRangeU>), g, b, lds, ctx->stream, a);
     }
     hipError_t e = hipGetLastError();

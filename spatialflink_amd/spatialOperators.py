@@ -188,6 +188,10 @@ class _RangeBase(SpatialOperator):
         if plan is None:
             plan = create()
             self._plans.put(key, plan)
+            tuning = getattr(self, "tuning", None)  # (scan_blocks, defer_mode): gf_range_plan_set_tuning
+            if tuning is not None:
+                _lib.check(_lib.lib().gf_range_plan_set_tuning(plan, int(tuning[0]), int(tuning[1])), None,
+                           "gf_range_plan_set_tuning")
         return plan
 
     def __del__(self):

@@ -228,6 +228,37 @@ def test_range_ppoly_generated_1000(sf, oracle_mod, n, r):
         np.testing.assert_array_equal(res.indices().astype(np.int64), exp)
 
 
+@pytest.mark.parametrize("mode", [1, 2, 3])
+def test_range_table_defer_modes(sf, oracle_mod, mode):
+    """Table-mode candidate tests inline (1), deferred (2) and deferred behind the span
+    prefilter (3, the C3 default: the stream only rules out points outside the class spans, the
+    block classifies the rest with the table at its end): the 1000 generateQueryPolygons squares
+    with points across the whole grid, NaN and outside-the-grid points; a many-point query set."""
+    n = 500
+    g = sf.UniformGrid(n, *BEIJING)
+    og = oracle_mod.grid(n, *BEIJING)
+    raw = oracle_mod.generate_query_polygons(1000, 115.5, 39.6, 117.6, 41.1)
+    polys = [sf.Polygon(p, g) for p in raw]
+    x, y = oracle_mod.java_random_points(33, 400_000, 115.4, 117.7, 39.5, 41.2)
+    x[:5] = np.nan
+    y[5:10] = np.nan
+    x[10:20] = BEIJING[0] - 1e-3
+    w = win(sf, x, y)
+    for ap in (False, True):
+        op = sf.PointPolygonRangeQuery(conf(sf, ap), g)
+        op.tuning = (0, mode)
+        res = op.run(w, polys, 0.001)
+        exp = oracle_mod.range_ppoly(og, x, y, oracle_mod.Polygons(raw), 0.001, ap)
+        np.testing.assert_array_equal(res.indices().astype(np.int64), exp, err_msg=f"ap={ap}")
+        assert res.count() == len(exp)
+    qx, qy = oracle_mod.java_random_points(34, 300, 115.5, 115.6, 40.0, 40.4)
+    op = sf.PointPointRangeQuery(conf(sf), g)
+    op.tuning = (0, mode)
+    res = op.run(w, [sf.Point(str(i), qx[i], qy[i], 0, g) for i in range(len(qx))], 0.004)
+    exp = oracle_mod.range_pp(og, x, y, qx, qy, 0.004)
+    np.testing.assert_array_equal(res.indices().astype(np.int64), exp)
+
+
 def _ulps(v, k):
     for _ in range(abs(k)):
         v = np.nextafter(v, np.inf if k > 0 else -np.inf)
