@@ -200,8 +200,16 @@ __device__ __forceinline__ int32_t join_sub(double v, double mn, double cl, int3
   return j < 0 ? 0 : (j > f - 1 ? f - 1 : j);
 }
 
-// q_off index of a query point: its sub-cell (f sub-rows x f sub-columns per clamped cell,
-// sub 0 in clamped cells) in row-major order over f(qn+2) sub-columns; f == 1: the clamped cell
+// q_off index of a query point: its sub-cell (f sub-rows x f sub-columns per clamped cell) in
+// row-major order over f(qn+2) sub-columns; f == 1: the clamped cell.  A point outside the grid
+// goes to the sub-cell of its clamped cell ADJACENT to the grid (sub f-1 below the grid, 0
+// above): it can pair only with an ordinary point within r < cl/f of the grid's edge, i.e. in
+// the outermost sub-cell, whose 3 x 3 neighbourhood then holds it -- so edge lanes need no
+// true-cell check either (a clamped point farther than one cell out fails d <= r).
+__device__ __forceinline__ int32_t join_sub_clamped(double v, double mn, double cl, int32_t c, double fs, int32_t f,
+                                                    int32_t qn) {
+  return c < 0 ? f - 1 : (c >= qn ? 0 : join_sub(v, mn, cl, c, fs, f));
+}
 __device__ __forceinline__ uint32_t join_fine_key(const JoinQueryArgs& q, double x, double y, int32_t& cx,
                                                   int32_t& cy) {
   cx = cell_index(x, q.minX, q.cl);
@@ -209,8 +217,8 @@ __device__ __forceinline__ uint32_t join_fine_key(const JoinQueryArgs& q, double
   const int64_t fW = (int64_t)q.f * (q.qn + 2);
   int32_t jx = 0, jy = 0;
   if (q.f > 1) {
-    if (cx >= 0 && cx < q.qn) jx = join_sub(x, q.minX, q.cl, cx, q.fs, q.f);
-    if (cy >= 0 && cy < q.qn) jy = join_sub(y, q.minY, q.cl, cy, q.fs, q.f);
+    jx = join_sub_clamped(x, q.minX, q.cl, cx, q.fs, q.f, q.qn);
+    jy = join_sub_clamped(y, q.minY, q.cl, cy, q.fs, q.f, q.qn);
   }
   return (uint32_t)(((int64_t)q.f * clamp_key(cy, q.qn) + jy) * fW + (int64_t)q.f * clamp_key(cx, q.qn) + jx);
 }
@@ -660,9 +668,7 @@ struct JoinWaveBuf {
 // exit is a ballot, so the loop and the pair count stay wave-uniform).  Column-sorted lanes
 // share columns, so most lanes of a round read the same few LDS addresses.  SLOW: the run
 // touches a clamped bucket or row, so each candidate's true cell is checked (Chebyshev <= c).
-// MAPQ: the pair carries the query index itself (top bit set) instead of the sorted slot -- the
-// fine path's cell-path waves, whose slots may lie outside the task's staged range.
-template <int MODE, bool LDS, bool SLOW, bool MAPQ = false>
+template <int MODE, bool LDS, bool SLOW>
 __device__ __forceinline__ void join_lane_run(const JoinRowArgs& a, const double2* lxy, uint32_t gb, uint32_t tb,
                                               uint32_t te, const JoinLane& ln, JoinWaveBuf& wbuf, JoinProbeHdr& hd,
                                               uint2* region) {
@@ -703,10 +709,6 @@ __device__ __forceinline__ void join_lane_run(const JoinRowArgs& a, const double
     }
 #pragma unroll
     for (int i = 0; i < R; ++i) hit[i] = test(act[i], t[i], v[i]);
-    if constexpr (MAPQ) {
-#pragma unroll
-      for (int i = 0; i < R; ++i) q[i] = hit[i] ? a.sqidx[q[i]] | 0x80000000u : 0u;
-    }
     wbuf.push<R>(hit, ln.pidx, q, a, hd, region);
   }
 }
@@ -770,11 +772,12 @@ __device__ __forceinline__ void store_u32_wt(uint32_t* p, uint32_t v) {
 // FINE (the fine path, f > 1: c == 1, exact distances, one grid for both sides, cl/f > r): a
 // pair needs d <= r, so its points lie in sub-cells at most one apart on each axis (sub-cells are
 // wider than r and the sub-cell index is monotone), and then their cells are at most one apart --
-// the key match is implied.  An interior lane (cell column and row in [1, qn-2], so every
-// candidate is an in-grid point) therefore tests only the 3 x 3 sub-cells around its own: runs
-// of the f + 2 sub-rows the task stages (cl^2 (3/f)^2 of candidates instead of 9 cl^2).  A wave
-// holding an edge lane, and every task of rows 0 and qn-1, takes the cell path over global
-// memory (the true-cell check on every candidate), sub-row by sub-row.
+// the key match is implied.  Every lane therefore tests only the 3 x 3 sub-cells around its own:
+// runs of the f + 2 sub-rows the task stages (cl^2 (3/f)^2 of candidates instead of 9 cl^2).
+// Query points outside the grid sit in the sub-cell adjacent to it (join_fine_key), so lanes in
+// the grid's edge cells need no true-cell check.  (A first version sent every wave holding an
+// edge lane through the cell path over global memory: ~2 such waves per task, each a chain of
+// dependent global round trips the whole task waited for: probe 282 -> 225 us without it.)
 template <int MODE, int FINE>  // MODE 0: exact, metric 0 (squared-distance bound); 1: approximate or hypot
 __device__ __forceinline__ void join_probe_task(const JoinRowArgs& a, uint32_t task, char* const lds_base) {
   JoinProbeHdr& hd = *reinterpret_cast<JoinProbeHdr*>(lds_base);
@@ -800,7 +803,6 @@ __device__ __forceinline__ void join_probe_task(const JoinRowArgs& a, uint32_t t
   const int32_t orow = hd.row, cy = orow;  // the task's cell row
   const int64_t r0 = cy - c < -1 ? -1 : cy - c, r1 = cy + c > qn ? qn : cy + c;
   const int nrows = (int)(r1 - r0 + 1);
-  const bool task_edge = FINE && (cy < 1 || cy > qn - 2);  // every lane takes the cell path
   const size_t fine_rb = join_row_lds_bytes(fW, 0);          // one staged sub-row's u16 offsets
   if (threadIdx.x == 0) {
     // the row's tasks split it evenly (10000 points: 2 x 5000, not 8192 + 1808)
@@ -809,10 +811,7 @@ __device__ __forceinline__ void join_probe_task(const JoinRowArgs& a, uint32_t t
     hd.beg = rb + k * size;
     hd.end = rb + (k + 1) * size < re ? rb + (k + 1) * size : re;
     if (FINE) {  // sub-rows f(cy+1)-1 .. f(cy+1)+f: consecutive in the sorted query side
-      if (task_edge) {
-        hd.fit = 0;
-        hd.g0 = 0u;
-      } else {
+      {
         const int64_t fy0 = (int64_t)f * (cy + 1) - 1;
         const uint32_t g0 = a.q_off[fy0 * fW], g1 = a.q_off[(fy0 + f + 2) * fW], m = g1 - g0;
         hd.g0 = g0;
@@ -968,18 +967,7 @@ __device__ __forceinline__ void join_probe_task(const JoinRowArgs& a, uint32_t t
     if (FINE) {
       const int32_t col = (int32_t)(cur.e >> 15), sub = (int32_t)((cur.e >> 13) & 3u);
       const int32_t cx = col / f - 1;
-      const bool edge = valid && (cx < 1 || cx > qnn - 2);
-      if (task_edge || __ballot(edge) != 0) {  // the cell path, sub-row by sub-row, global memory
-        const JoinLane ln{cur.v.x, cur.v.y, valid ? cx : 0, cy, cur.idx};
-        const int32_t kb = (ln.cx - cc < -1 ? -1 : ln.cx - cc) + 1, ke = (ln.cx + cc > qnn ? qnn : ln.cx + cc) + 2;
-        for (int64_t ry = r0; ry <= r1; ++ry) {
-          for (int32_t sr = 0; sr < f; ++sr) {
-            const uint32_t* qo = a.q_off + ((ry + 1) * f + sr) * fW;
-            const uint32_t tb = valid ? qo[f * kb] : 0u, te = valid ? qo[f * ke] : 0u;
-            join_lane_run<MODE, false, true, true>(a, nullptr, 0u, tb, te, ln, wbuf, hd, region);
-          }
-        }
-      } else {
+      {
         const JoinLane ln{cur.v.x, cur.v.y, cx, cy, cur.idx};
         uint32_t b[3], e[3];
         if (fit) {
