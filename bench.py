@@ -121,6 +121,8 @@ def main():
                     help="CPU baseline budget, split over its three lines (rank 0, N=1)")
     ap.add_argument("--cpu-sample", type=int, default=1_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--join-sync", action="store_true",
+                    help="join workload: gf_join_pp per window (pair count read back) instead of gf_join_pp_async")
     ap.add_argument("--clustered", action="store_true",
                     help="BASELINE.md section 3 clustered variant: 80%% of the points in 8 Gaussian hot spots (sigma 0.01)")
     ap.add_argument("--no-verify", action="store_true")

@@ -401,6 +401,14 @@ int gf_geojson_parse(gf_ctx* ctx, gf_objid_dict* dict, const char* text, int64_t
 int gf_join_pp(gf_ctx* ctx, const gf_grid* ugrid, const gf_grid* qgrid, const gf_points* ordinary,
                const gf_points* query, double r, int approximate, int metric, uint32_t* pairs,
                int64_t cap, int64_t* npairs);
+/* The same window join without a host wait: every launch stream-ordered on the context stream,
+ * the pair count written by the last kernel to *total (device or mapped pinned memory), so the
+ * next window's launches queue behind this one.  Pairs past cap are not written: the caller
+ * re-runs the window with a larger buffer when *total > cap.  (r == 0 -- every cell a key --
+ * takes the synchronous path and then stores *total.) */
+int gf_join_pp_async(gf_ctx* ctx, const gf_grid* ugrid, const gf_grid* qgrid, const gf_points* ordinary,
+                     const gf_points* query, double r, int approximate, int metric, uint32_t* pairs,
+                     int64_t cap, unsigned long long* total);
 
 /* Point-polygon window join: JoinQuery.getReplicatedPolygonQueryStream + PointPolygonJoinQuery
  * .windowBased (JoinQuery.java:93-115, PointPolygonJoinQuery.java:154-213).  Polygon q is

@@ -46,7 +46,7 @@ EXPORTS = [
     "gf_knn_sliding_create", "gf_knn_sliding_destroy", "gf_knn_sliding_geometry", "gf_knn_sliding_push",
     "gf_knn_sliding_flush", "gf_knn_sliding_decode", "gf_pane_bounds", "gf_csv_parse", "gf_csv_parse_dict", "gf_geojson_parse",
     "gf_objid_dict_create", "gf_objid_dict_destroy", "gf_ctx_objid_dict", "gf_objid_dict_size", "gf_objid_intern",
-    "gf_objid_decode", "gf_join_pp",
+    "gf_objid_decode", "gf_join_pp", "gf_join_pp_async",
     "gf_join_ppoly_plan_create", "gf_join_ppoly_run", "gf_join_ppoly",
     "gf_window_create",
     "gf_window_destroy", "gf_window_upload", "gf_window_points", "gf_synth_uniform", "gf_pinned_alloc",
@@ -177,6 +177,8 @@ def lib():
             "gf_objid_decode": ([P, P, i64, P, i64, P], C.c_int),
             "gf_join_pp": ([P, C.POINTER(GfGrid), C.POINTER(GfGrid), C.POINTER(GfPoints), C.POINTER(GfPoints), d,
                             C.c_int, C.c_int, P, i64, pi64], C.c_int),
+            "gf_join_pp_async": ([P, C.POINTER(GfGrid), C.POINTER(GfGrid), C.POINTER(GfPoints), C.POINTER(GfPoints), d,
+                                  C.c_int, C.c_int, P, i64, P], C.c_int),
             "gf_join_ppoly_plan_create": ([P, C.POINTER(GfGrid), C.POINTER(GfPolygons), d, C.c_int, C.c_int,
                                            C.POINTER(P)], C.c_int),
             "gf_join_ppoly_run": ([P, C.POINTER(GfGrid), C.POINTER(GfPoints), P, i64, pi64], C.c_int),

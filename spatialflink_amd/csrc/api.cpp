@@ -1711,11 +1711,14 @@ extern "C" int gf_knn_merge_dev_batch(gf_ctx* ctx, int32_t k, const void* record
 // ---------------------------------------------------------------------------------------
 // join
 // ---------------------------------------------------------------------------------------
-extern "C" int gf_join_pp(gf_ctx* ctx, const gf_grid* ugrid, const gf_grid* qgrid, const gf_points* ord,
-                          const gf_points* qry, double r, int approximate, int metric, uint32_t* pairs, int64_t cap,
-                          int64_t* npairs) {
+// total_out == nullptr: synchronous (*npairs from a pinned readback); else asynchronous (the
+// packing kernel writes the count to total_out; *npairs untouched)
+static int join_pp_impl(gf_ctx* ctx, const gf_grid* ugrid, const gf_grid* qgrid, const gf_points* ord,
+                        const gf_points* qry, double r, int approximate, int metric, uint32_t* pairs, int64_t cap,
+                        int64_t* npairs, unsigned long long* total_out) {
   if (!ctx || !grid_ok(ugrid) || !grid_ok(qgrid) || !npairs || (metric != 0 && metric != 1))
     return set_err(ctx, GF_ERR_ARG, "gf_join_pp: bad argument");
+  ctx->join_async_done = 0;
   int st = bind(ctx);
   if (st) return st;
   if ((st = check_points(ctx, ord)) || (st = check_points(ctx, qry))) return st;
@@ -1828,8 +1831,13 @@ extern "C" int gf_join_pp(gf_ctx* ctx, const gf_grid* ugrid, const gf_grid* qgri
     JoinCompactArgs k{};
     k.tpairs = j.tpairs; k.task_cap = j.task_cap; k.task_cnt = j.task_cnt; k.task_off = U32(o_tkoff);
     k.ntask = (uint32_t)max_tasks;
-    k.ovf_count = cnt2; k.pairs = pairs; k.cap = j.cap; k.pairs_aligned = j.pairs_aligned; k.total = cnt2 + 1;
+    k.ovf_count = cnt2; k.pairs = pairs; k.cap = j.cap; k.pairs_aligned = j.pairs_aligned;
+    k.total = total_out ? total_out : cnt2 + 1;
     GF_HIP_CHECK(ctx, launch_join_compact(ctx, k));
+    if (total_out) {  // the caller reads *total_out stream-ordered
+      ctx->join_async_done = 1;
+      return GF_OK;
+    }
     unsigned long long total = 0;
     if (int e = read_scalar_sync(ctx, cnt2 + 1, &total)) return e;
     *npairs = (int64_t)total;
@@ -1862,6 +1870,28 @@ extern "C" int gf_join_pp(gf_ctx* ctx, const gf_grid* ugrid, const gf_grid* qgri
   if (!pairs) return set_err(ctx, GF_ERR_ARG, "null pairs");
   GF_HIP_CHECK(ctx, launch_join_probe(ctx, a, 1, blocks));
   GF_HIP_CHECK(ctx, hipStreamSynchronize(s));
+  return GF_OK;
+}
+
+extern "C" int gf_join_pp(gf_ctx* ctx, const gf_grid* ugrid, const gf_grid* qgrid, const gf_points* ord,
+                          const gf_points* qry, double r, int approximate, int metric, uint32_t* pairs, int64_t cap,
+                          int64_t* npairs) {
+  return join_pp_impl(ctx, ugrid, qgrid, ord, qry, r, approximate, metric, pairs, cap, npairs, nullptr);
+}
+
+extern "C" int gf_join_pp_async(gf_ctx* ctx, const gf_grid* ugrid, const gf_grid* qgrid, const gf_points* ord,
+                                const gf_points* qry, double r, int approximate, int metric, uint32_t* pairs,
+                                int64_t cap, unsigned long long* total) {
+  if (!total) return set_err(ctx, GF_ERR_ARG, "gf_join_pp_async: null total");
+  int64_t n = 0;
+  int st = join_pp_impl(ctx, ugrid, qgrid, ord, qry, r, approximate, metric, pairs, cap, &n, total);
+  if (st == GF_ERR_CAPACITY) st = GF_OK;  // the count is in *total
+  if (st) return st;
+  if (!ctx->join_async_done) {  // the synchronous paths (r == 0, empty sides): store the count
+    const unsigned long long v = (unsigned long long)n;
+    GF_HIP_CHECK(ctx, hipMemcpyAsync(total, &v, sizeof v, hipMemcpyHostToDevice, ctx->stream));
+    GF_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+  }
   return GF_OK;
 }
 

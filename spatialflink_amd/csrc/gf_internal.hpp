@@ -34,6 +34,7 @@ struct gf_ctx {
   int num_cus = 256;
   int join_legacy = 0;  // testing: force the original (unbucketed) join probe
   int join_coarse = 0;  // testing: the row path without sub-cells
+  int join_async_done = 0;  // gf_join_pp_async: the packing kernel wrote the count
   double join_ppp = 0.0;  // pairs per ordinary point of the last join (sizes the task regions)
   hipStream_t aux = nullptr;  // kNN depth 3: odd windows' launches (created on first use)
   gf_objid_dict* dict = nullptr;  // the context's default objID dictionary (created on first use)

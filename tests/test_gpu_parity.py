@@ -602,6 +602,60 @@ def test_join_fine_subcells(sf, oracle_mod, n, r, metric):
         np.testing.assert_array_equal(got, exp, err_msg=f"coarse={coarse} f={f}")
 
 
+def test_join_async_matches_sync(sf, oracle_mod):
+    """gf_join_pp_async: consecutive windows queued without a host wait, counts in device
+    memory -- the same pairs and counts as gf_join_pp; a window past the capacity reports its
+    count (> cap); r == 0 takes the synchronous path and still stores the count."""
+    import ctypes as C
+
+    import torch
+    from spatialflink_amd import _lib
+
+    L = _lib.lib()
+    g = sf.UniformGrid(500, *BEIJING)
+    ctx = _lib.context(0)
+    wins = []
+    for j in range(3):
+        ox, oy = oracle_mod.java_random_points(110 + j, 200_000, *BEIJING)
+        qx, qy = oracle_mod.java_random_points(120 + j, 40_000, *BEIJING)
+        wins.append((win(sf, ox, oy), win(sf, qx, qy)))
+    for r in (0.002, 0.01):
+        exp = []
+        for wo, wq in wins:
+            exp.append(sf.PointPointJoinQuery(conf(sf), g, g).run(wo, wq, r))
+        cap = max(len(e) for e in exp) + 16
+        bufs = [torch.zeros(2 * cap, dtype=torch.int32, device="cuda") for _ in wins]
+        totals = torch.zeros(len(wins), dtype=torch.int64, device="cuda")
+        torch.cuda.synchronize()
+        for j, (wo, wq) in enumerate(wins):
+            po, pq = wo.c_struct(), wq.c_struct()
+            _lib.check(L.gf_join_pp_async(ctx.handle, C.byref(g.c_grid), C.byref(g.c_grid), C.byref(po), C.byref(pq), r,
+                                          0, 0, bufs[j].data_ptr(), cap, totals[j].data_ptr()), ctx.handle, "async")
+        ctx.synchronize()
+        for j in range(len(wins)):
+            n = int(totals[j].item())
+            assert n == len(exp[j])
+            got = bufs[j][: 2 * n].cpu().numpy().view(np.uint32).astype(np.int64).reshape(-1, 2)
+            got = np.array(sorted(map(tuple, got.tolist())), np.int64).reshape(-1, 2)
+            np.testing.assert_array_equal(got, exp[j])
+        # capacity too small: the count still arrives
+        po, pq = wins[0][0].c_struct(), wins[0][1].c_struct()
+        _lib.check(L.gf_join_pp_async(ctx.handle, C.byref(g.c_grid), C.byref(g.c_grid), C.byref(po), C.byref(pq), r, 0,
+                                      0, bufs[0].data_ptr(), 8, totals[0].data_ptr()), ctx.handle, "async small")
+        ctx.synchronize()
+        assert int(totals[0].item()) == len(exp[0])
+    small = [(win(sf, wo_x, wo_y), win(sf, q_x, q_y)) for wo_x, wo_y, q_x, q_y in
+             [(*oracle_mod.java_random_points(130, 3000, *BEIJING), *oracle_mod.java_random_points(131, 300, *BEIJING))]]
+    exp0 = sf.PointPointJoinQuery(conf(sf), g, g).run(small[0][0], small[0][1], 0.0)
+    buf = torch.zeros(2 * (len(exp0) + 16), dtype=torch.int32, device="cuda")
+    po, pq = small[0][0].c_struct(), small[0][1].c_struct()
+    torch.cuda.synchronize()
+    _lib.check(L.gf_join_pp_async(ctx.handle, C.byref(g.c_grid), C.byref(g.c_grid), C.byref(po), C.byref(pq), 0.0, 0, 0,
+                                  buf.data_ptr(), len(exp0) + 16, totals[1].data_ptr()), ctx.handle, "async r=0")
+    ctx.synchronize()
+    assert int(totals[1].item()) == len(exp0)
+
+
 def test_join_dense_rows_fall_back_to_global(sf, oracle_mod):
     """A query row too dense to stage in LDS (every query point in one cell row) takes the
     task's global-memory probe; a single dense cell as well."""

@@ -380,6 +380,16 @@ def bench_join(args):
         del pairs
         pairs = torch.empty(2 * cap, dtype=torch.int32, device=dev)
 
+    # default: gf_join_pp_async -- each window's launches queue behind the previous window (no
+    # host wait for its pair count); the counts land in device memory, read after the final sync
+    use_async = not getattr(args, "join_sync", False)
+    totals = torch.zeros(max(args.steps, 1), dtype=torch.int64, device=dev)
+
+    def step_async(i):
+        _lib.check(L.gf_join_pp_async(ctx.handle, C.byref(grid.c_grid), C.byref(grid.c_grid), C.byref(po[i % 2]),
+                                      C.byref(pq[i % 2]), r, 0, 0, pairs.data_ptr(), cap, totals[i].data_ptr()),
+                   ctx.handle, "gf_join_pp_async")
+
     for i in range(args.warmup):
         step(i)
     _sync(world)
@@ -388,10 +398,18 @@ def bench_join(args):
     t0 = time.perf_counter()
     total_pairs = 0
     for i in range(args.steps):
-        step(i)
-        total_pairs += npairs.value
+        if use_async:
+            step_async(i)
+        else:
+            step(i)
+            total_pairs += npairs.value
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    if use_async:
+        counts = totals.cpu().numpy()
+        if (counts > cap).any():
+            raise RuntimeError("gf_join_pp_async: a window's pairs exceeded the buffer")
+        total_pairs = int(counts.sum())
     if world > 1:
         import torch.distributed as dist
 
@@ -412,6 +430,8 @@ def bench_join(args):
         import oracle as O
 
         step(0)
+        if use_async:  # the async windows' counts equal the synchronous call's
+            assert int(totals[0].item()) == npairs.value, "gf_join_pp_async count != gf_join_pp count"
         m = min(no, 1_000_000)
         got = pairs[: 2 * npairs.value].cpu().numpy().view(np.uint32).astype(np.int64).reshape(-1, 2)
         got = got[got[:, 0] < m]
@@ -438,6 +458,8 @@ def bench_join(args):
           {"n_gpus": world,
            "config": {"workload": wl, "ordinary": no * world, "query": nq * world, "radius": r,
                       "pairs_per_window": pp_all, "query_per_rank_with_halo": nq_rank,
+                      "window_api": "gf_join_pp_async (windows queued back to back, counts read after the final sync)"
+                      if use_async else "gf_join_pp (pair count read back per window)",
                       "parallelism": f"cell-column shards x{world}, query halo c columns (no collective)"},
            "breakdown": {"probe_us_per_launch": round(avg * 1e6, 2), "probe_launches_per_window": cnt / args.steps,
                          "probe_GBps_row_bucketed_in_pairs_out": round((20.0 * no + 8.0 * pp) / avg / 1e9, 1) if avg > 0 else None,
