@@ -205,6 +205,8 @@ static int stream_blocks(gf_ctx* ctx, int64_t items_per_thread_pairs) {
 
 using namespace gf;
 
+static int lookback_state(gf_ctx* ctx, int64_t blocks, gf::ExpandState* es);
+
 // ---------------------------------------------------------------------------------------
 // library / context
 // ---------------------------------------------------------------------------------------
@@ -430,10 +432,11 @@ extern "C" int gf_bucket_by_cell(gf_ctx* ctx, const gf_grid* g, const gf_points*
   }
   int bits = 1;
   while (((int64_t)1 << bits) < bins) ++bits;
-  const int passes = (bits + kRadixBits - 1) / kRadixBits;
-  // >= ~4K points per wave-chunk, <= 2 blocks per CU (the digit matrix is 2048 x wave-chunks)
-  const int blocks = (int)std::min<int64_t>(std::max<int64_t>(n / (4 * 4096), 1), (int64_t)ctx->num_cus * 2);
-  const int64_t mat = (int64_t)kRadixDigits * blocks * (kBlock / 64);
+  const int passes = (bits + kRadixMaxBits - 1) / kRadixMaxBits, pbits = (bits + passes - 1) / passes;
+  // one block per CU (the scatter's tile buffers), >= ~4 tiles per block
+  const int64_t tiles = (n + kRadixTile - 1) / kRadixTile;
+  const int blocks = (int)std::min<int64_t>(std::max<int64_t>(tiles / 4, 1), (int64_t)ctx->num_cus);
+  const int64_t mat = ((int64_t)1 << pbits) * blocks;
   Arena ar;
   size_t o_k[2] = {ar.take<uint32_t>(n), ar.take<uint32_t>(n)};
   size_t o_v[2] = {ar.take<uint32_t>(n), ar.take<uint32_t>(n)};
@@ -446,16 +449,20 @@ extern "C" int gf_bucket_by_cell(gf_ctx* ctx, const gf_grid* g, const gf_points*
   RadixArgs a{};
   a.x = pts->x; a.y = pts->y; a.n = n;
   a.minX = g->minX; a.minY = g->minY; a.cl = g->cellLength; a.gn = g->n;
+  a.bits = pbits; a.nblk = blocks;
   uint32_t* k0 = U32(o_k0);
   for (int p = 0; p < passes; ++p) {
     a.kin = p == 0 ? nullptr : U32(o_k[(p - 1) & 1]);
     a.vin = p == 0 ? nullptr : U32(o_v[(p - 1) & 1]);
     a.kout = p == 0 ? k0 : U32(o_k[p & 1]);
-    a.shift = p * kRadixBits;
+    a.shift = p * pbits;
     a.M = U32(o_m);
     a.Ms = U32(o_ms);
     GF_HIP_CHECK(ctx, launch_radix(ctx, 0, a, blocks));  // pass 0: keys -> k0
-    GF_HIP_CHECK(ctx, launch_exclusive_scan(ctx->stream, U32(o_m), mat, U32(o_ms), U32(o_tmp)));
+    ExpandState es;
+    if ((st = lookback_state(ctx, scan1_blocks(mat), &es))) return st;
+    GF_HIP_CHECK(ctx, launch_scan1(ctx->stream, U32(o_m), mat, U32(o_ms), nullptr, 0, 0, es));
+    ctx->expand_base += (unsigned long long)scan1_blocks(mat);
     if (p == 0) a.kin = k0;  // the scatter reads the stored keys, index = position
     a.kout = U32(o_k[p & 1]);
     a.vout = p == passes - 1 ? perm : U32(o_v[p & 1]);
@@ -1379,8 +1386,8 @@ static int knn_large(gf_knn_plan* P, const gf_points* pts, void* result) {
   GF_HIP_CHECK(ctx, hipMemsetAsync(&P->lane[0].st->count, 0, sizeof(unsigned long long), ctx->stream));
   GF_HIP_CHECK(ctx, hipMemsetAsync(&P->lane[0].st->maybe, 0, sizeof(unsigned long long), ctx->stream));
   const gf_knn_plan::Lane& L = P->lane[0];
-  const int blocks = (int)std::min<int64_t>(std::max<int64_t>(m / (4 * 4096), 1), (int64_t)ctx->num_cus * 2);
-  const int64_t mat = (int64_t)kRadixDigits * blocks * (kBlock / 64);
+  const int blocks = (int)std::min<int64_t>(std::max<int64_t>((m + kRadixTile - 1) / kRadixTile / 4, 1), (int64_t)ctx->num_cus);
+  const int64_t mat = (int64_t)256 * blocks;  // 8-bit digits
   const int64_t mm = std::max<int64_t>(m, 1);
   Arena ar;
   size_t o_k[2] = {ar.take<uint32_t>(mm), ar.take<uint32_t>(mm)};
@@ -1398,19 +1405,22 @@ static int knn_large(gf_knn_plan* P, const gf_points* pts, void* result) {
   // stable sort of the first `cnt` entries of the permutation by key fields (least significant first)
   auto sort_by = [&](int64_t cnt, std::initializer_list<int> fields) -> int {
     if (cnt <= 1) return GF_OK;
-    const int nb = (int)std::min<int64_t>(std::max<int64_t>(cnt / (4 * 4096), 1), (int64_t)ctx->num_cus * 2);
-    const int64_t nmat = (int64_t)kRadixDigits * nb * (kBlock / 64);
+    const int nb = (int)std::min<int64_t>(std::max<int64_t>((cnt + kRadixTile - 1) / kRadixTile / 4, 1), (int64_t)ctx->num_cus);
+    const int64_t nmat = (int64_t)256 * nb;
     for (int f : fields) {
       a.m = cnt; a.perm = U32(o_p[cur]); a.field = f; a.keys = U32(o_k[0]);
       GF_HIP_CHECK(ctx, launch_knn_large(ctx, 1, a));
-      for (int p = 0; p < 3; ++p) {  // 32 bits = 3 passes of kRadixBits (11)
+      for (int p = 0; p < 4; ++p) {  // 32 bits = 4 passes of 8
         RadixArgs r{};
         r.n = cnt;
         r.kin = U32(o_k[p & 1]); r.vin = U32(o_p[cur]);
         r.kout = U32(o_k[(p + 1) & 1]); r.vout = U32(o_p[cur ^ 1]);
-        r.shift = p * kRadixBits; r.M = U32(o_m); r.Ms = U32(o_ms);
+        r.shift = p * 8; r.bits = 8; r.nblk = nb; r.M = U32(o_m); r.Ms = U32(o_ms);
         GF_HIP_CHECK(ctx, launch_radix(ctx, 0, r, nb));
-        GF_HIP_CHECK(ctx, launch_exclusive_scan(ctx->stream, U32(o_m), nmat, U32(o_ms), U32(o_tmp)));
+        ExpandState es;
+        if (int e = lookback_state(ctx, scan1_blocks(nmat), &es)) return e;
+        GF_HIP_CHECK(ctx, launch_scan1(ctx->stream, U32(o_m), nmat, U32(o_ms), nullptr, 0, 0, es));
+        ctx->expand_base += (unsigned long long)scan1_blocks(nmat);
         GF_HIP_CHECK(ctx, launch_radix(ctx, 1, r, nb));
         cur ^= 1;
       }

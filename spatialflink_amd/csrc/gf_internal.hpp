@@ -274,8 +274,10 @@ struct RangeArgs {
 hipError_t launch_assign(gf_ctx* ctx, const gf_grid* g, const gf_points* p, int32_t* cx, int32_t* cy);
 hipError_t launch_histogram(hipStream_t s, const uint32_t* keys, int64_t n, uint32_t* hist);
 // K2: stable LSD radix bucketing (k_points.hip)
-constexpr int kRadixBits = 11;
-constexpr int kRadixDigits = 1 << kRadixBits;
+constexpr int kRadixMaxBits = 9;  // digit bits per pass (<=)
+constexpr int kRadixMaxDigits = 1 << kRadixMaxBits;
+constexpr int kRadixThreads = 1024;
+constexpr int kRadixTile = 8192;  // points per scatter tile (16 waves x 512)
 struct RadixArgs {
   const double* x;          // pass 0 input (kin == null): keys from the cells of x, y
   const double* y;
@@ -286,10 +288,12 @@ struct RadixArgs {
   const uint32_t* vin;
   uint32_t* kout;
   uint32_t* vout;
-  int shift;                // digit = (key >> shift) & (kRadixDigits - 1)
-  uint32_t* M;              // stage 0: [kRadixDigits][wave chunks]; stage 2: bucket sizes (zeroed)
+  int shift, bits;          // digit = (key >> shift) & ((1 << bits) - 1)
+  int nblk;                 // blocks (chunks of whole tiles)
+  uint32_t* M;              // stage 0: [digits][blocks]; stage 2: bucket sizes (zeroed)
   const uint32_t* Ms;       // stage 1: the exclusive scan of M
 };
+size_t radix_scatter_lds_bytes();
 // stage 0 histogram, 1 scatter, 2 bucket sizes of the sorted kout
 hipError_t launch_radix(gf_ctx* ctx, int stage, const RadixArgs& a, int blocks);
 // exclusive scan: out[0..L] (out[L] = total); tmp >= scan_tmp_elems(L) uint32

@@ -187,7 +187,10 @@ constexpr int kBucketU = 8;
 
 constexpr int kScatThreads = 1024;
 constexpr int kHistSplit = 2;  // histogram chunks per scatter block
-constexpr int kScatTile = 4096;
+#ifndef GF_SCAT_TILE
+#define GF_SCAT_TILE 4096
+#endif
+constexpr int kScatTile = GF_SCAT_TILE;  // points per write-combining tile
 constexpr int kScatPer = kScatTile / kScatThreads;
 
 __device__ __forceinline__ int32_t clamp_key(int32_t c, int32_t qn) { return (c < -1 ? -1 : (c > qn ? qn : c)) + 1; }

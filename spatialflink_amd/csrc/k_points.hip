@@ -81,15 +81,19 @@ hipError_t launch_pane_bounds(hipStream_t s, const int64_t* ts, int64_t n, int64
 // ---------------------------------------------------------------------------------------
 // K2: bucketing by cell -- the keyBy(gridID) shuffle (PointPointRangeQuery.java:144-148): a
 // stable LSD radix sort of the points' bucket keys (valid cell -> cy*n + cx, out-of-grid ->
-// n*n), kRadixBits per pass, so every bucket lists its points in input (arrival) order -- the
+// n*n), <= 9 bits per pass, so every bucket lists its points in input (arrival) order -- the
 // order Flink's per-key window buffer iterates -- and the result never depends on scheduling.
-//   radix_hist     per WAVE-chunk LDS histograms of the pass's digit (no global atomics)
-//   (scan)         of the digit-major matrix M[digit][wave-chunk] -> every wave-chunk's
-//                  first output slot per digit
-//   radix_scatter  each wave walks its chunk 64 points at a time: the lanes sharing a digit are
-//                  found with kRadixBits ballots, their rank = popcount below, and one LDS
-//                  atomic per (step, digit) on the wave's own cursors places the run -- no block
-//                  barrier, no global atomic, stable by construction.
+//   radix_hist     block b's digit histogram of its chunk in LDS -> column b of M[digit][block]
+//   (scan)         of M, digit-major (one look-back launch): every block's first output slot
+//                  per digit
+//   radix_scatter  block b walks its chunk in tiles of kRadixTile points.  A tile's element e
+//                  belongs to wave e / 512; a wave ranks its elements stably (lanes sharing a
+//                  digit found with `bits` ballots, rank = popcount below + the wave's running
+//                  count of that digit in LDS), a digit-major scan over (digit, wave) of the
+//                  waves' counts gives every element its slot in the tile, the tile is placed
+//                  in LDS in that order and written out in it -- consecutive lanes write
+//                  consecutive slots of one digit's run (r02's per-wave scatter wrote 4 B per
+//                  lane to up to 64 digits per store: 201 us per pass on 10M points).
 // Pass 0's histogram reads x, y (16 B/point) and stores the keys; every scatter reads (key,
 // index) -- pass 0's index is the position itself.
 // Afterwards: bucket sizes from the sorted keys' run boundaries -> exclusive scan = cell_start.
@@ -100,91 +104,142 @@ __device__ __forceinline__ uint32_t bucket_key(double x, double y, const RadixAr
   return valid ? (uint32_t)cy * (uint32_t)a.gn + (uint32_t)cx : (uint32_t)a.gn * (uint32_t)a.gn;
 }
 
-// wave-chunk w of the nw = gridDim.x * waves_per_block chunks: [beg, end)
-__device__ __forceinline__ void wave_chunk(int64_t n, int64_t& beg, int64_t& end, int& w) {
-  const int64_t nw = (int64_t)gridDim.x * (kBlock / 64);
-  w = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
-  const int64_t chunk = (n + nw - 1) / nw;
-  beg = (int64_t)w * chunk;
-  end = beg + chunk < n ? beg + chunk : n;
-  if (beg > n) beg = n;
+// block b's chunk [beg, end) of the a.nblk chunks (whole tiles except the last)
+__device__ __forceinline__ void radix_chunk(const RadixArgs& a, int64_t& beg, int64_t& end) {
+  const int64_t tiles = (a.n + kRadixTile - 1) / kRadixTile;
+  const int64_t per = (tiles + a.nblk - 1) / a.nblk;
+  beg = (int64_t)blockIdx.x * per * kRadixTile;
+  end = beg + per * kRadixTile < a.n ? beg + per * kRadixTile : a.n;
+  if (beg > a.n) beg = a.n;
 }
 
-constexpr int kRadixU = 8;  // 64-point steps whose loads are in flight together
-
-// FIRST: the key from x, y (histogram of pass 0, which also stores the keys); otherwise
-// (key, index) from the previous pass -- pass 0's scatter has vin == null: index = position
 template <bool FIRST>
-__device__ __forceinline__ void radix_load(const RadixArgs& a, int64_t i, int64_t end, uint32_t& k, uint32_t& v) {
-  if (i < end) {
-    if (FIRST) {
-      k = bucket_key(__builtin_nontemporal_load(a.x + i), __builtin_nontemporal_load(a.y + i), a);
-    } else {
-      k = a.kin[i];
+__global__ __launch_bounds__(kRadixThreads) void radix_hist_kernel(RadixArgs a) {
+  __shared__ uint32_t h[kRadixMaxDigits];
+  const uint32_t D = 1u << a.bits, mask = D - 1u;
+  for (uint32_t j = threadIdx.x; j < D; j += kRadixThreads) h[j] = 0u;
+  __syncthreads();
+  int64_t beg, end;
+  radix_chunk(a, beg, end);
+  constexpr int U = 8;  // loads in flight together
+  for (int64_t i0 = beg + threadIdx.x; i0 < end; i0 += (int64_t)kRadixThreads * U) {
+    uint32_t k[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = i0 + (int64_t)u * kRadixThreads;
+      if (FIRST) k[u] = i < end ? bucket_key(__builtin_nontemporal_load(a.x + i), __builtin_nontemporal_load(a.y + i), a) : 0u;
+      else k[u] = i < end ? a.kin[i] : 0u;
     }
-    v = a.vin ? a.vin[i] : (uint32_t)i;
-  } else {
-    k = 0u;
-    v = 0u;
-  }
-}
-
-template <bool FIRST>
-__global__ __launch_bounds__(kBlock) void radix_hist_kernel(RadixArgs a) {
-  __shared__ uint32_t h[kBlock / 64][kRadixDigits];
-  const int wl = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  for (int j = lane; j < kRadixDigits; j += 64) h[wl][j] = 0u;
-  int64_t beg, end;
-  int w;
-  wave_chunk(a.n, beg, end, w);
-  for (int64_t i0 = beg + lane; i0 < end; i0 += 64 * kRadixU) {
-    uint32_t k[kRadixU], v[kRadixU];
 #pragma unroll
-    for (int u = 0; u < kRadixU; ++u) radix_load<FIRST>(a, i0 + 64 * u, end, k[u], v[u]);
-#pragma unroll
-    for (int u = 0; u < kRadixU; ++u)
-      if (i0 + 64 * u < end) {
-        atomicAdd(&h[wl][(k[u] >> a.shift) & (kRadixDigits - 1)], 1u);
-        if (FIRST) a.kout[i0 + 64 * u] = k[u];  // pass 0's scatter reads the keys, not x, y
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = i0 + (int64_t)u * kRadixThreads;
+      if (i < end) {
+        atomicAdd(&h[(k[u] >> a.shift) & mask], 1u);
+        if (FIRST) a.kout[i] = k[u];  // pass 0's scatter reads the keys, not x, y
       }
+    }
   }
-  const int64_t nw = (int64_t)gridDim.x * (kBlock / 64);
-  for (int j = lane; j < kRadixDigits; j += 64) a.M[(size_t)j * nw + w] = h[wl][j];
+  __syncthreads();
+  for (uint32_t j = threadIdx.x; j < D; j += kRadixThreads) a.M[(size_t)j * a.nblk + blockIdx.x] = h[j];
 }
 
-__global__ __launch_bounds__(kBlock) void radix_scatter_kernel(RadixArgs a) {
-  __shared__ uint32_t cur[kBlock / 64][kRadixDigits];
-  const int wl = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  int64_t beg, end;
-  int w;
-  wave_chunk(a.n, beg, end, w);
-  const int64_t nw = (int64_t)gridDim.x * (kBlock / 64);
-  for (int j = lane; j < kRadixDigits; j += 64) cur[wl][j] = a.Ms[(size_t)j * nw + w];
+size_t radix_scatter_lds_bytes() {
+  return (size_t)kRadixTile * 8 + (size_t)(kRadixThreads / 64) * kRadixMaxDigits * 4 + 2 * (size_t)(kRadixMaxDigits + 1) * 4;
+}
+
+__global__ __launch_bounds__(kRadixThreads) void radix_scatter_kernel(RadixArgs a) {
+  extern __shared__ uint32_t rsm[];
+  constexpr int W = kRadixThreads / 64, EPW = kRadixTile / W, U = EPW / 64;  // elements per wave, steps
+  uint32_t* const lk = rsm;                           // [kRadixTile] the tile's keys in sorted order
+  uint32_t* const lv = lk + kRadixTile;               // [kRadixTile] their values
+  uint32_t* const wc = lv + kRadixTile;               // [W][kRadixMaxDigits] wave counts -> slots
+  uint32_t* const tb = wc + W * kRadixMaxDigits;      // [D + 1] tile start per digit
+  uint32_t* const gc = tb + kRadixMaxDigits + 1;      // [D] next global slot per digit
+  __shared__ uint32_t ws[kRadixThreads / 64];
+  const uint32_t D = 1u << a.bits, mask = D - 1u;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const uint64_t below = (1ull << lane) - 1ull;
-  for (int64_t s0 = beg; s0 < end; s0 += 64 * kRadixU) {  // wave-uniform
-    uint32_t k[kRadixU], v[kRadixU];
+  int64_t beg, end;
+  radix_chunk(a, beg, end);
+  for (uint32_t d = threadIdx.x; d < D; d += kRadixThreads) gc[d] = a.Ms[(size_t)d * a.nblk + blockIdx.x];
+  for (int64_t t0 = beg; t0 < end; t0 += kRadixTile) {  // block-uniform
+    const uint32_t cnt = (uint32_t)(end - t0 < kRadixTile ? end - t0 : kRadixTile);
+    uint32_t k[U], v[U], r[U];
 #pragma unroll
-    for (int u = 0; u < kRadixU; ++u) radix_load<false>(a, s0 + 64 * u + lane, end, k[u], v[u]);
+    for (int u = 0; u < U; ++u) {
+      const uint32_t e = w * EPW + u * 64 + lane;
+      k[u] = e < cnt ? a.kin[t0 + e] : 0u;
+      v[u] = e < cnt ? (a.vin ? a.vin[t0 + e] : (uint32_t)(t0 + e)) : 0u;
+    }
+    for (uint32_t d = lane; d < D; d += 64) wc[w * kRadixMaxDigits + d] = 0u;  // this wave's row
 #pragma unroll
-    for (int u = 0; u < kRadixU; ++u) {
-      const bool valid = s0 + 64 * u + lane < end;
-      const uint32_t d = (k[u] >> a.shift) & (kRadixDigits - 1);
+    for (int u = 0; u < U; ++u) {  // stable ranks within the wave
+      const uint32_t e = w * EPW + u * 64 + lane;
+      const bool valid = e < cnt;
+      const uint32_t d = (k[u] >> a.shift) & mask;
       uint64_t peers = __ballot(valid);
-#pragma unroll
-      for (int b = 0; b < kRadixBits; ++b) {
+      for (int b = 0; b < a.bits; ++b) {
         const uint64_t bal = __ballot((d >> b) & 1u);
         peers &= ((d >> b) & 1u) ? bal : ~bal;
       }
-      const uint32_t rank = (uint32_t)__popcll(peers & below);
       uint32_t base = 0;
-      if (valid && rank == 0) base = atomicAdd(&cur[wl][d], (uint32_t)__popcll(peers));
+      if (valid && (peers & below) == 0) base = atomicAdd(&wc[w * kRadixMaxDigits + d], (uint32_t)__popcll(peers));
       const int leader = valid ? __ffsll((unsigned long long)peers) - 1 : lane;
       base = __shfl(base, leader, 64);
-      if (valid) {
-        a.kout[base + rank] = k[u];
-        a.vout[base + rank] = v[u];
+      r[u] = base + (uint32_t)__popcll(peers & below);
+    }
+    __syncthreads();
+    {  // exclusive scan of the counts in (digit, wave) order: entry j = d * W + w
+      constexpr int PT = W * kRadixMaxDigits / kRadixThreads;  // entries per thread
+      const uint32_t j0 = threadIdx.x * PT;
+      uint32_t c[PT], run = 0;
+#pragma unroll
+      for (int q = 0; q < PT; ++q) {
+        const uint32_t j = j0 + q, d = j / W, ww = j % W;
+        c[q] = d < D ? wc[ww * kRadixMaxDigits + d] : 0u;
+        run += c[q];
+      }
+      uint32_t inc = run;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = __shfl_up(inc, o, 64);
+        if (lane >= o) inc += t;
+      }
+      if (lane == 63) ws[w] = inc;
+      __syncthreads();
+      uint32_t before = inc - run;
+      for (int q = 0; q < w; ++q) before += ws[q];
+#pragma unroll
+      for (int q = 0; q < PT; ++q) {
+        const uint32_t j = j0 + q, d = j / W, ww = j % W;
+        if (d < D) {
+          wc[ww * kRadixMaxDigits + d] = before;
+          if (ww == 0) tb[d] = before;
+        }
+        before += c[q];
+      }
+      if (threadIdx.x == 0) tb[D] = cnt;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < U; ++u) {  // the tile in (digit, input) order
+      const uint32_t e = w * EPW + u * 64 + lane;
+      if (e < cnt) {
+        const uint32_t p = wc[w * kRadixMaxDigits + ((k[u] >> a.shift) & mask)] + r[u];
+        lk[p] = k[u];
+        lv[p] = v[u];
       }
     }
+    __syncthreads();
+    for (uint32_t p = threadIdx.x; p < cnt; p += kRadixThreads) {  // runs of one digit: consecutive slots
+      const uint32_t kk = lk[p], d = (kk >> a.shift) & mask;
+      const uint32_t o = gc[d] + (p - tb[d]);
+      a.kout[o] = kk;
+      a.vout[o] = lv[p];
+    }
+    __syncthreads();
+    for (uint32_t d = threadIdx.x; d < D; d += kRadixThreads) gc[d] += tb[d + 1] - tb[d];
+    __syncthreads();
   }
 }
 
@@ -204,11 +259,11 @@ hipError_t launch_radix(gf_ctx* ctx, int stage, const RadixArgs& a, int blocks) 
   KTimer t(ctx, GF_K_BUCKET);
   switch (stage) {
     case 0:  // kin == null: pass 0, keys from x, y stored to kout
-      if (!a.kin) hipLaunchKernelGGL(radix_hist_kernel<true>, dim3(blocks), dim3(kBlock), 0, s, a);
-      else hipLaunchKernelGGL(radix_hist_kernel<false>, dim3(blocks), dim3(kBlock), 0, s, a);
+      if (!a.kin) hipLaunchKernelGGL(radix_hist_kernel<true>, dim3(blocks), dim3(kRadixThreads), 0, s, a);
+      else hipLaunchKernelGGL(radix_hist_kernel<false>, dim3(blocks), dim3(kRadixThreads), 0, s, a);
       break;
     case 1:
-      hipLaunchKernelGGL(radix_scatter_kernel, dim3(blocks), dim3(kBlock), 0, s, a);
+      hipLaunchKernelGGL(radix_scatter_kernel, dim3(blocks), dim3(kRadixThreads), radix_scatter_lds_bytes(), s, a);
       break;
     default:
       if (a.n > 0)
