@@ -603,7 +603,7 @@ struct JoinQueryArgs {
 };
 // launches of the row path (k_join.hip): 0 histograms, 1 scatter, 2 row / task offsets, 3 probe
 hipError_t launch_join_rows(gf_ctx* ctx, const JoinRowArgs& a, const JoinQueryArgs& q, int stage);
-size_t join_scatter_lds_bytes(int32_t qn);
+size_t join_scatter_lds_bytes(int32_t nrows, int tile);
 
 
 }  // namespace gf

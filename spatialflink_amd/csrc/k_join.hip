@@ -187,11 +187,9 @@ constexpr int kBucketU = 8;
 
 constexpr int kScatThreads = 1024;
 constexpr int kHistSplit = 2;  // histogram chunks per scatter block
-#ifndef GF_SCAT_TILE
-#define GF_SCAT_TILE 4096
-#endif
-constexpr int kScatTile = GF_SCAT_TILE;  // points per write-combining tile
-constexpr int kScatPer = kScatTile / kScatThreads;
+// points per write-combining tile: 6144 where the row arrays leave room in LDS (6-point row
+// runs at C4's 1000 rows: scatter 121 -> 110 us), else 4096
+constexpr int kScatTileBig = 6144, kScatTileSmall = 4096;
 
 __device__ __forceinline__ int32_t clamp_key(int32_t c, int32_t qn) { return (c < -1 ? -1 : (c > qn ? qn : c)) + 1; }
 
@@ -286,14 +284,18 @@ __global__ __launch_bounds__(kScatThreads) void join_hist_kernel(JoinRowArgs a, 
 // consecutive slots of one row (runs of ~tile/rows points) and successive tiles extend the
 // same runs.  Destinations: the block's run start of each row (the matrix scan, minus `base`)
 // advanced tile by tile.
-size_t join_scatter_lds_bytes(int32_t nrows) {
-  return (size_t)kScatTile * (16 + 4 + 4) + 2 * 4 * (size_t)nrows + 4 * (kScatThreads / 64);
+size_t join_scatter_lds_bytes(int32_t nrows, int tile) {
+  return (size_t)tile * (16 + 4 + 4) + 2 * 4 * (size_t)nrows + 4 * (kScatThreads / 64);
+}
+int join_scatter_tile(int32_t nrows) {
+  return join_scatter_lds_bytes(nrows, kScatTileBig) <= 160 * 1024 ? kScatTileBig : kScatTileSmall;
 }
 
-template <class RowF>
+template <int kScatTile, class RowF>
 __device__ __forceinline__ void wc_row_scatter(const double* X, const double* Y, int64_t n, int64_t bid, int64_t nblk,
                                                int32_t nrows, const uint32_t* Ms, uint32_t base, double2* oxy,
                                                uint32_t* oidx, RowF rowf) {
+  constexpr int kScatPer = kScatTile / kScatThreads;
   extern __shared__ __attribute__((aligned(16))) char sm[];
   double2* const sxy = reinterpret_cast<double2*>(sm);
   uint32_t* const sidx = reinterpret_cast<uint32_t*>(sxy + kScatTile);
@@ -384,13 +386,15 @@ __device__ __forceinline__ void wc_row_scatter(const double* X, const double* Y,
   }
 }
 
+template <int TILE>
 __global__ __launch_bounds__(kScatThreads) void join_scatter_kernel(JoinRowArgs a, JoinQueryArgs q) {
   if ((int)blockIdx.x < q.nblk)
-    wc_row_scatter(q.qx, q.qy, q.nq, blockIdx.x, q.nblk, q.qn + 2, q.qmat_scan, 0u,
-                   reinterpret_cast<double2*>(q.txy), q.tidx, [&](double x, double y) { return join_qrow(q, x, y); });
+    wc_row_scatter<TILE>(q.qx, q.qy, q.nq, blockIdx.x, q.nblk, q.qn + 2, q.qmat_scan, 0u,
+                         reinterpret_cast<double2*>(q.txy), q.tidx, [&](double x, double y) { return join_qrow(q, x, y); });
   else
-    wc_row_scatter(a.ox, a.oy, a.no, (int64_t)blockIdx.x - q.nblk, a.nblk, a.nrows, a.row_mat_scan, a.mat_base,
-                   reinterpret_cast<double2*>(a.soxy), a.soidx, [&](double x, double y) { return join_orow(a, x, y); });
+    wc_row_scatter<TILE>(a.ox, a.oy, a.no, (int64_t)blockIdx.x - q.nblk, a.nblk, a.nrows, a.row_mat_scan, a.mat_base,
+                         reinterpret_cast<double2*>(a.soxy), a.soidx,
+                         [&](double x, double y) { return join_orow(a, x, y); });
 }
 
 // block-wide exclusive scan of one value per thread (NT threads); *total = the block's sum
@@ -1124,8 +1128,13 @@ hipError_t launch_join_rows(gf_ctx* ctx, const JoinRowArgs& a, const JoinQueryAr
     }
     case 1: {
       KTimer t(ctx, GF_K_JOIN_BUCKET);
-      hipLaunchKernelGGL(join_scatter_kernel, grid, dim3(kScatThreads),
-                         join_scatter_lds_bytes(a.nrows > q.qn + 2 ? a.nrows : q.qn + 2), s, a, q);
+      const int32_t nr = a.nrows > q.qn + 2 ? a.nrows : q.qn + 2;
+      if (join_scatter_tile(nr) == kScatTileBig)
+        hipLaunchKernelGGL(join_scatter_kernel<kScatTileBig>, grid, dim3(kScatThreads),
+                           join_scatter_lds_bytes(nr, kScatTileBig), s, a, q);
+      else
+        hipLaunchKernelGGL(join_scatter_kernel<kScatTileSmall>, grid, dim3(kScatThreads),
+                           join_scatter_lds_bytes(nr, kScatTileSmall), s, a, q);
       break;
     }
     case 2:
