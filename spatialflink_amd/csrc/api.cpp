@@ -314,6 +314,7 @@ extern "C" int gf_ctx_set_flag(gf_ctx* ctx, int flag, int value) {
   if (!ctx) return GF_ERR_ARG;
   if (flag == GF_FLAG_JOIN_LEGACY) { ctx->join_legacy = value != 0; return GF_OK; }
   if (flag == GF_FLAG_JOIN_COARSE) { ctx->join_coarse = value != 0; return GF_OK; }
+  if (flag == GF_FLAG_GEOJSON_WALK) { ctx->geojson_walk = value != 0; return GF_OK; }
   return set_err(ctx, GF_ERR_ARG, "gf_ctx_set_flag: unknown flag");
 }
 

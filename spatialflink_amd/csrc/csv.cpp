@@ -148,6 +148,7 @@ extern "C" int gf_geojson_parse(gf_ctx* ctx, gf_objid_dict* dict, const char* te
     (k ? a.len_ts : a.len_obj) = (int32_t)n;
   }
   a.date_fmt = sc->date_format;
+  a.geo_fast = !ctx->geojson_walk;
   a.tz_off_ms = (int64_t)sc->tz_offset_minutes * 60000;
   return parse_text_lines(ctx, dict, text, len, a, g, x, y, objID, ts, cx, cy, cap, n_out, bad_line, bad_kind);
 }

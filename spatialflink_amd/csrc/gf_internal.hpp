@@ -34,6 +34,7 @@ struct gf_ctx {
   int num_cus = 256;
   int join_legacy = 0;  // testing: force the original (unbucketed) join probe
   int join_coarse = 0;  // testing: the row path without sub-cells
+  int geojson_walk = 0; // testing: every GeoJSON line takes the member-by-member walk
   int join_async_done = 0;  // gf_join_pp_async: the packing kernel wrote the count
   double join_ppp = 0.0;  // pairs per ordinary point of the last join (sizes the task regions)
   hipStream_t aux = nullptr;  // kNN depth 3: odd windows' launches (created on first use)
@@ -366,7 +367,8 @@ int ctx_dict(gf_ctx* ctx, gf_objid_dict** out);  // the context's default dictio
 
 // CSV ingest (k_csv.hip)
 constexpr int64_t kCsvSeg = 64 * 1024;  // text bytes per count / index block
-constexpr int kCsvLds = 24 * 1024;      // parse: a block's 256 lines staged in LDS when they fit
+constexpr int kCsvLds = 24 * 1024;      // parse: least LDS staging per block (256 lines staged when they fit)
+constexpr int kCsvLdsMax = 64 * 1024;   // parse: most (sized from the mean line length, launch_csv_parse)
 enum { kCsvOk = 0, kCsvNumberFormat = 1, kCsvUnsupported = 2, kCsvMissingField = 3, kCsvEmptyLine = 4 };
 struct CsvErr {
   unsigned long long line;  // first bad line (~0 = none)
@@ -402,6 +404,8 @@ struct CsvArgs {
   int64_t tz_off_ms;             // date_fmt 1: UTC offset of the JVM default time zone
   char prop_obj[kGeoPropMax];
   char prop_ts[kGeoPropMax];
+  int32_t lds_cap;               // set by launch_csv_parse: the block's dynamic LDS staging bytes
+  int32_t geo_fast;              // GeoJSON: 1 = one-pass member location first (k_csv.hip geo_locate)
 };
 hipError_t launch_csv_count(hipStream_t st, const char* text, int64_t len, int64_t nseg, uint32_t* counts);
 hipError_t launch_csv_index(hipStream_t st, const char* text, int64_t len, int64_t nseg, const uint32_t* seg_off,

@@ -341,23 +341,9 @@ __device__ int jdate(const Src& s, int64_t p, int64_t q, int64_t tz_off_ms, int6
   return 0;
 }
 
+// the geometry's first coordinate pair: c at the coordinates array's '['
 template <class Src>
-__device__ int eval_geojson_line(const CsvArgs& a, const Src& s, int64_t j, LineOut* o) {
-  const int64_t b = j == 0 ? 0 : a.nl[j - 1] + 1;
-  int64_t e = j < a.newlines ? a.nl[j] : a.len;
-  if (e > b && s(e - 1) == '\r') --e;
-  if (e <= b) return kCsvEmptyLine;
-  int64_t p = jskip(s, b, e);
-  if (p >= e || s(p) != '{') return kCsvMissingField;
-  // the feature: the record's "value" object, or the line's object itself
-  int64_t feat = p;
-  const int64_t v = jfind(s, p, e, "value", 5);
-  if (v == -2) return kCsvMissingField;
-  if (v >= 0 && s(v) == '{') feat = v;
-  const int64_t g = jfind(s, feat, e, "geometry", 8);
-  if (g < 0 || s(g) != '{') return kCsvMissingField;
-  int64_t c = jfind(s, g, e, "coordinates", 11);
-  if (c < 0 || s(c) != '[') return kCsvMissingField;
+__device__ __forceinline__ int geo_coords(const Src& s, int64_t c, int64_t e, LineOut* o) {
   while (c < e && s(c) == '[') c = jskip(s, c + 1, e);  // the first coordinate of any nesting
   double xy[2];
   for (int k = 0; k < 2; ++k) {
@@ -378,11 +364,22 @@ __device__ int eval_geojson_line(const CsvArgs& a, const Src& s, int64_t j, Line
   o->ts = 0;
   o->obj = GF_OBJID_NULL;
   o->dict = false;
-  const int64_t pr = jfind(s, feat, e, "properties", 10);
-  if (pr == -2) return kCsvMissingField;
-  if (pr < 0 || s(pr) != '{') return kCsvOk;
+  return kCsvOk;
+}
+
+// what the property lookups need of CsvArgs (passed by value: a reference to the kernel's
+// argument block in an outlined call would copy the whole block to scratch, per lane)
+struct GeoProps {
+  const char* kts;   // property names (the block's LDS copies)
+  const char* kobj;
+  int32_t len_ts, len_obj, date_fmt;
+  int64_t tz_off_ms;
+};
+
+// the time and objID properties: t, q = their values' first bytes (-1 absent, -2 malformed object)
+template <class Src>
+__device__ __forceinline__ int geo_props(const GeoProps& a, const Src& s, int64_t e, int64_t t, int64_t q, LineOut* o) {
   if (a.len_ts >= 0) {
-    const int64_t t = jfind(s, pr, e, a.prop_ts, a.len_ts);
     if (t == -2) return kCsvMissingField;
     if (t >= 0) {
       const int64_t te = jval_end(s, t, e);
@@ -403,7 +400,6 @@ __device__ int eval_geojson_line(const CsvArgs& a, const Src& s, int64_t j, Line
     }
   }
   if (a.len_obj >= 0) {
-    const int64_t q = jfind(s, pr, e, a.prop_obj, a.len_obj);
     if (q == -2) return kCsvMissingField;
     if (q >= 0) {  // nodeOId.toString() with every '"' removed
       const int64_t qe = jval_end(s, q, e);
@@ -440,16 +436,245 @@ __device__ int eval_geojson_line(const CsvArgs& a, const Src& s, int64_t j, Line
   return kCsvOk;
 }
 
+// Member-by-member walk (jfind per looked-up member): exact on any line, malformed ones included.
+// p: the line's first non-blank byte, a '{'.
 template <class Src>
-__device__ __forceinline__ int eval_line(const CsvArgs& a, const Src& s, int64_t j, LineOut* o) {
-  return a.format == 1 ? eval_geojson_line(a, s, j, o) : eval_csv_line(a, s, j, o);
+__device__ __noinline__ int eval_geojson_walk(GeoProps a, Src s, int64_t p, int64_t e, LineOut* o) {
+  // the feature: the record's "value" object, or the line's object itself
+  int64_t feat = p;
+  const int64_t v = jfind(s, p, e, "value", 5);
+  if (v == -2) return kCsvMissingField;
+  if (v >= 0 && s(v) == '{') feat = v;
+  const int64_t g = jfind(s, feat, e, "geometry", 8);
+  if (g < 0 || s(g) != '{') return kCsvMissingField;
+  const int64_t c = jfind(s, g, e, "coordinates", 11);
+  if (c < 0 || s(c) != '[') return kCsvMissingField;
+  int st = geo_coords(s, c, e, o);
+  if (st) return st;
+  const int64_t pr = jfind(s, feat, e, "properties", 10);
+  if (pr == -2) return kCsvMissingField;
+  if (pr < 0 || s(pr) != '{') return kCsvOk;
+  const int64_t t = a.len_ts >= 0 ? jfind(s, pr, e, a.kts, a.len_ts) : -1;
+  const int64_t q = a.len_obj >= 0 ? jfind(s, pr, e, a.kobj, a.len_obj) : -1;
+  return geo_props(a, s, e, t, q, o);
+}
+
+// ---------------------------------------------------------------------------------------
+// One-pass member location (the common case).  The walk above re-scans the feature once per
+// member it looks up, with nested data-dependent loops per lane: with 64 lines per wave in
+// different places of that loop nest the exec-mask bookkeeping dominated (~2.7 k scalar
+// instructions per line).  Here each lane runs one table-driven automaton over its line,
+// byte by byte (state x byte class -> next state + action, tables in LDS): a strict JSON
+// syntax check plus a small stack of container roles (top object, the record's "value" object,
+// the geometry and properties objects under either), recording the LAST value position of each
+// member the walk would look up.  On a line that passes the check -- strictly valid JSON, no
+// backslash, nesting <= 63 -- every jfind of the walk returns exactly that last member (the
+// walk's looser scanning agrees with JSON on valid input), so the results are the walk's.  Any
+// other line (malformed, escapes, deeper nesting) takes the walk itself.
+// ---------------------------------------------------------------------------------------
+enum : uint8_t { JS_VAL, JS_ARR0, JS_OBJ0, JS_KEY, JS_COLON, JS_AFT, JS_VSTR, JS_KSTR, JS_TOK, JS_END, JS_ERR, JS_N };
+enum : uint8_t { JC_WS, JC_LBRACE, JC_RBRACE, JC_LBRACK, JC_RBRACK, JC_QUOTE, JC_COMMA, JC_COLON, JC_BSL, JC_TOK, JC_OTHER,
+                 JC_N = 16 };
+enum : uint8_t { JA_NONE, JA_PUSH_OBJ, JA_PUSH_ARR, JA_POP_OBJ, JA_POP_ARR, JA_COMMA, JA_KEY_BEGIN, JA_KEY_END };
+enum : int { JR_NONE, JR_TOP, JR_VAL, JR_GEO_T, JR_PROP_T, JR_GEO_V, JR_PROP_V };        // container roles
+enum : int { JK_NONE, JK_VALUE, JK_GEO, JK_PROP, JK_COORD, JK_TS, JK_OBJ, JK_TSOBJ };     // member kinds
+constexpr int kGeoTabBytes = 256 + JS_N * JC_N;
+constexpr int kGeoKeys = 6;  // value, geometry, properties, coordinates, time property, objID property
+
+__device__ __forceinline__ uint8_t jclass(int c) {
+  switch (c) {
+    case ' ': case '\t': case '\n': case '\r': return JC_WS;
+    case '{': return JC_LBRACE;
+    case '}': return JC_RBRACE;
+    case '[': return JC_LBRACK;
+    case ']': return JC_RBRACK;
+    case '"': return JC_QUOTE;
+    case ',': return JC_COMMA;
+    case ':': return JC_COLON;
+    case '\\': return JC_BSL;
+    default: break;
+  }
+  if ((c >= '0' && c <= '9') || (c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z') || c == '+' || c == '-' || c == '.')
+    return JC_TOK;
+  return JC_OTHER;
+}
+// entry: next state | action << 4 | value-start << 7
+__device__ __forceinline__ uint8_t jtrans(int st, int cl) {
+  auto E = [](int n, int act, int vs) { return (uint8_t)(n | act << 4 | vs << 7); };
+  if (st == JS_VSTR) return cl == JC_QUOTE ? E(JS_AFT, JA_NONE, 0) : cl == JC_BSL ? E(JS_ERR, 0, 0) : E(JS_VSTR, 0, 0);
+  if (st == JS_KSTR) return cl == JC_QUOTE ? E(JS_COLON, JA_KEY_END, 0) : cl == JC_BSL ? E(JS_ERR, 0, 0) : E(JS_KSTR, 0, 0);
+  if (cl == JC_WS) return E(st == JS_TOK ? JS_AFT : st, 0, 0);
+  switch (st) {
+    case JS_VAL: case JS_ARR0:
+      if (cl == JC_LBRACE) return E(JS_OBJ0, JA_PUSH_OBJ, 1);
+      if (cl == JC_LBRACK) return E(JS_ARR0, JA_PUSH_ARR, 1);
+      if (cl == JC_QUOTE) return E(JS_VSTR, 0, 1);
+      if (cl == JC_TOK) return E(JS_TOK, 0, 1);
+      if (st == JS_ARR0 && cl == JC_RBRACK) return E(JS_AFT, JA_POP_ARR, 0);
+      return E(JS_ERR, 0, 0);
+    case JS_OBJ0:
+      if (cl == JC_QUOTE) return E(JS_KSTR, JA_KEY_BEGIN, 0);
+      if (cl == JC_RBRACE) return E(JS_AFT, JA_POP_OBJ, 0);
+      return E(JS_ERR, 0, 0);
+    case JS_KEY: return cl == JC_QUOTE ? E(JS_KSTR, JA_KEY_BEGIN, 0) : E(JS_ERR, 0, 0);
+    case JS_COLON: return cl == JC_COLON ? E(JS_VAL, 0, 0) : E(JS_ERR, 0, 0);
+    case JS_TOK: return cl == JC_TOK ? E(JS_TOK, 0, 0) : E(JS_ERR, 0, 0);  // other classes: looked up as JS_AFT
+    case JS_AFT:
+      if (cl == JC_COMMA) return E(JS_VAL, JA_COMMA, 0);
+      if (cl == JC_RBRACE) return E(JS_AFT, JA_POP_OBJ, 0);
+      if (cl == JC_RBRACK) return E(JS_AFT, JA_POP_ARR, 0);
+      return E(JS_ERR, 0, 0);
+    default: return E(JS_ERR, 0, 0);  // JS_END: only blanks; JS_ERR stays
+  }
+}
+
+// LDS tables of a block: byte classes, transitions, the looked-up member names
+struct GeoTabs {
+  const uint8_t* tab;  // [256 classes | JS_N x JC_N transitions]
+  const char* keys;    // kGeoKeys x kGeoPropMax
+  int32_t klen[kGeoKeys];
+};
+
+__device__ void geo_tabs_fill(const CsvArgs& a, uint8_t* tab, char* keys) {
+  for (int i = threadIdx.x; i < kGeoTabBytes; i += blockDim.x)
+    tab[i] = i < 256 ? jclass(i) : jtrans((i - 256) / JC_N, (i - 256) % JC_N);
+  for (int i = threadIdx.x; i < kGeoKeys * kGeoPropMax; i += blockDim.x) {
+    const int k = i / kGeoPropMax, c = i % kGeoPropMax;
+    const char* names[4] = {"value", "geometry", "properties", "coordinates"};
+    char ch = 0;
+    if (k < 4) {
+      const int n = k == 0 ? 5 : k == 1 ? 8 : k == 2 ? 10 : 11;
+      ch = c < n ? names[k][c] : 0;
+    } else {
+      ch = k == 4 ? a.prop_ts[c] : a.prop_obj[c];
+    }
+    keys[i] = ch;
+  }
+}
+
+template <class Src>
+__device__ __forceinline__ bool jkey_eq(const Src& s, int64_t ks, int len, const GeoTabs& gt, int k) {
+  if (gt.klen[k] != len) return false;
+  bool eq = true;
+  for (int i = 0; eq && i < len; ++i) eq = s(ks + i) == gt.keys[k * kGeoPropMax + i];
+  return eq;
+}
+
+// The automaton over [p, e) (s(p) == '{').  Returns false when the line must take the walk;
+// otherwise the member positions: g, c (coordinates), pr, t, q of the feature, -1 when absent.
+template <class Src>
+__device__ __forceinline__ bool geo_locate(const Src& s, int64_t p, int64_t e, const GeoTabs& gt, int64_t* loc) {
+  if (e - p >= INT32_MAX) return false;
+  int st = JS_VAL, depth = 0, pend = JK_NONE;
+  uint64_t kinds = 0;  // bit d: the container at depth d is an object
+  uint32_t roles = 0;  // 4 bits per depth 1..7
+  int32_t ks = 0;
+  // last value positions (offsets from p): the record's "value"; per feature (top / value object)
+  int32_t v = -1, gT = -1, prT = -1, cT = -1, tT = -1, qT = -1, gV = -1, prV = -1, cV = -1, tV = -1, qV = -1;
+  const int32_t n = (int32_t)(e - p);
+  for (int32_t i = 0; i < n; ++i) {
+    const int cl = gt.tab[(uint8_t)s(p + i)];
+    const int se = st == JS_TOK && cl != JC_TOK ? JS_AFT : st;
+    const int ent = gt.tab[256 + se * JC_N + cl];
+    int nst = ent & 15;
+    const int act = (ent >> 4) & 7;
+    if (ent & 0xF0) {
+      const int role = depth <= 7 ? (int)(roles >> (4 * depth)) & 15 : JR_NONE;
+      if ((ent & 0x80) && pend) {  // the value of a looked-up member starts here
+        if (role == JR_TOP) {
+          if (pend == JK_VALUE) { v = i; gV = prV = cV = tV = qV = -1; }
+          if (pend == JK_GEO) { gT = i; cT = -1; }
+          if (pend == JK_PROP) { prT = i; tT = qT = -1; }
+        } else if (role == JR_VAL) {
+          if (pend == JK_GEO) { gV = i; cV = -1; }
+          if (pend == JK_PROP) { prV = i; tV = qV = -1; }
+        } else if (role == JR_GEO_T) {
+          cT = i;
+        } else if (role == JR_GEO_V) {
+          cV = i;
+        } else if (role == JR_PROP_T) {
+          if (pend != JK_OBJ) tT = i;
+          if (pend != JK_TS) qT = i;
+        } else if (role == JR_PROP_V) {
+          if (pend != JK_OBJ) tV = i;
+          if (pend != JK_TS) qV = i;
+        }
+      }
+      if (act == JA_PUSH_OBJ || act == JA_PUSH_ARR) {
+        if (depth == 63) return false;
+        int child = JR_NONE;
+        if (act == JA_PUSH_OBJ) {
+          if (depth == 0) child = JR_TOP;
+          else if (role == JR_TOP) child = pend == JK_VALUE ? JR_VAL : pend == JK_GEO ? JR_GEO_T : pend == JK_PROP ? JR_PROP_T : JR_NONE;
+          else if (role == JR_VAL) child = pend == JK_GEO ? JR_GEO_V : pend == JK_PROP ? JR_PROP_V : JR_NONE;
+        }
+        ++depth;
+        kinds = (kinds & ~(1ull << depth)) | ((uint64_t)(act == JA_PUSH_OBJ) << depth);
+        if (depth <= 7) roles = (roles & ~(15u << (4 * depth))) | ((uint32_t)child << (4 * depth));
+      }
+      if (ent & 0x80) pend = JK_NONE;
+      if (act == JA_POP_OBJ || act == JA_POP_ARR) {
+        if ((int)((kinds >> depth) & 1) != (act == JA_POP_OBJ)) return false;
+        if (--depth == 0) nst = JS_END;
+      } else if (act == JA_COMMA) {
+        nst = (kinds >> depth) & 1 ? JS_KEY : JS_VAL;
+      } else if (act == JA_KEY_BEGIN) {
+        ks = i + 1;
+      } else if (act == JA_KEY_END) {
+        const int len = i - ks;
+        pend = JK_NONE;
+        if (role == JR_TOP || role == JR_VAL) {
+          if (role == JR_TOP && jkey_eq(s, p + ks, len, gt, 0)) pend = JK_VALUE;
+          else if (jkey_eq(s, p + ks, len, gt, 1)) pend = JK_GEO;
+          else if (jkey_eq(s, p + ks, len, gt, 2)) pend = JK_PROP;
+        } else if (role == JR_GEO_T || role == JR_GEO_V) {
+          if (jkey_eq(s, p + ks, len, gt, 3)) pend = JK_COORD;
+        } else if (role == JR_PROP_T || role == JR_PROP_V) {
+          const bool ts = jkey_eq(s, p + ks, len, gt, 4), ob = jkey_eq(s, p + ks, len, gt, 5);
+          pend = ts && ob ? JK_TSOBJ : ts ? JK_TS : ob ? JK_OBJ : JK_NONE;
+        }
+      }
+    }
+    if (nst == JS_ERR) return false;
+    st = nst;
+  }
+  if (st != JS_END) return false;
+  const bool val = v >= 0 && s(p + v) == '{';
+  const int32_t off[5] = {val ? gV : gT, val ? cV : cT, val ? prV : prT, val ? tV : tT, val ? qV : qT};
+#pragma unroll
+  for (int k = 0; k < 5; ++k) loc[k] = off[k] < 0 ? -1 : p + off[k];
+  return true;
+}
+
+// FAST: try the one-pass locator first (the LDS-staged path); otherwise the walk
+template <bool FAST, class Src>
+__device__ __forceinline__ int eval_geojson_line(const CsvArgs& a, const Src& s, int64_t j, LineOut* o, const GeoTabs& gt) {
+  const int64_t b = j == 0 ? 0 : a.nl[j - 1] + 1;
+  int64_t e = j < a.newlines ? a.nl[j] : a.len;
+  if (e > b && s(e - 1) == '\r') --e;
+  if (e <= b) return kCsvEmptyLine;
+  const int64_t p = jskip(s, b, e);
+  if (p >= e || s(p) != '{') return kCsvMissingField;
+  const GeoProps gp{gt.keys + 4 * kGeoPropMax, gt.keys + 5 * kGeoPropMax, a.len_ts, a.len_obj, a.date_fmt, a.tz_off_ms};
+  int64_t loc[5];
+  if (!FAST || !geo_locate(s, p, e, gt, loc)) return eval_geojson_walk(gp, s, p, e, o);
+  const int64_t g = loc[0], c = loc[1], pr = loc[2];
+  if (g < 0 || s(g) != '{') return kCsvMissingField;
+  if (c < 0 || s(c) != '[') return kCsvMissingField;
+  const int st = geo_coords(s, c, e, o);
+  if (st) return st;
+  if (pr < 0 || s(pr) != '{') return kCsvOk;
+  return geo_props(gp, s, e, a.len_ts >= 0 ? loc[3] : -1, a.len_obj >= 0 ? loc[4] : -1, o);
 }
 
 // parse + store line j; returns true when its objID needs the dictionary (*w filled)
-template <class Src>
-__device__ __forceinline__ bool parse_line(const CsvArgs& a, const Src& s, int64_t j, DictWork* w) {
+template <int FMT, bool FAST, class Src>
+__device__ __forceinline__ bool parse_line(const CsvArgs& a, const Src& s, int64_t j, DictWork* w, const GeoTabs& gt) {
   LineOut o{0, 0, 0.0, 0.0, false, {0, 0}};
-  if (eval_line(a, s, j, &o) != kCsvOk) {
+  int st;
+  if constexpr (FMT == 1) st = eval_geojson_line<FAST>(a, s, j, &o, gt);
+  else st = eval_csv_line(a, s, j, &o);
+  if (st != kCsvOk) {
     atomicMin(&a.err->line, (unsigned long long)j);
     return false;
   }
@@ -465,13 +690,16 @@ __device__ __forceinline__ bool parse_line(const CsvArgs& a, const Src& s, int64
   return o.dict;
 }
 
-// A block takes 256 consecutive lines.  Their bytes are contiguous: when they fit kCsvLds they
-// are staged in LDS with coalesced 16-B loads first, so the per-byte reads of the split/parse
-// state machines (a dependent chain per lane) hit LDS instead of waiting on L2 one byte at a time.
+// A block takes 256 consecutive lines.  Their bytes are contiguous: when they fit the block's
+// staging area (a.lds_cap bytes of dynamic LDS, sized from the mean line length) they are staged
+// in LDS with coalesced 16-B loads first, so the per-byte reads of the split/parse state machines
+// (a dependent chain per lane) hit LDS instead of waiting on L2 one byte at a time.  GeoJSON
+// blocks also fill the one-pass locator's tables (geo_locate) in LDS.
 // Dictionary objIDs are queued with one atomic per wave (the queue order is free: ids follow
 // line order, k_objid.hip).
+template <int FMT>  // 0: CSV / TSV, 1: GeoJSON (a.format)
 __global__ __launch_bounds__(kBlock) void csv_parse_kernel(CsvArgs a) {
-  __shared__ __attribute__((aligned(16))) char lds[kCsvLds];
+  extern __shared__ __attribute__((aligned(16))) char lds[];
   const int64_t L0 = (int64_t)blockIdx.x * kBlock;
   const int64_t L1 = L0 + kBlock < a.lines ? L0 + kBlock : a.lines;  // exclusive
   const int64_t b0 = L0 == 0 ? 0 : a.nl[L0 - 1] + 1;
@@ -480,7 +708,14 @@ __global__ __launch_bounds__(kBlock) void csv_parse_kernel(CsvArgs a) {
   const int64_t j = L0 + threadIdx.x;
   DictWork w{0, 0, 0};
   bool need = false;
-  if (b1 - a0 <= kCsvLds) {  // block-uniform
+  __shared__ uint8_t gtab[FMT == 1 ? kGeoTabBytes : 1];
+  __shared__ char gkeys[FMT == 1 ? kGeoKeys * kGeoPropMax : 1];
+  const GeoTabs gt{gtab, gkeys, {5, 8, 10, 11, a.len_ts, a.len_obj}};
+  if (FMT == 1) {
+    geo_tabs_fill(a, gtab, gkeys);
+    __syncthreads();
+  }
+  if (b1 - a0 <= a.lds_cap) {  // block-uniform
     for (int64_t off = a0 + 16 * threadIdx.x; off < b1; off += 16 * kBlock) {
       if (off + 16 <= a.len) {
         *reinterpret_cast<uint4*>(lds + (off - a0)) = *reinterpret_cast<const uint4*>(a.text + off);
@@ -489,9 +724,12 @@ __global__ __launch_bounds__(kBlock) void csv_parse_kernel(CsvArgs a) {
       }
     }
     __syncthreads();
-    if (j < L1) need = parse_line(a, LBytes{lds, a0}, j, &w);
+    if (j < L1) {
+      if (a.geo_fast) need = parse_line<FMT, true>(a, LBytes{lds, a0}, j, &w, gt);
+      else need = parse_line<FMT, false>(a, LBytes{lds, a0}, j, &w, gt);
+    }
   } else if (j < L1) {
-    need = parse_line(a, GBytes{a.text}, j, &w);
+    need = parse_line<FMT, false>(a, GBytes{a.text}, j, &w, gt);
   }
   const uint64_t m = __ballot(need);
   if (m) {
@@ -512,9 +750,16 @@ __global__ __launch_bounds__(kBlock) void csv_parse_kernel(CsvArgs a) {
 // error kind of the first bad line (re-derived by a one-lane pass over that line)
 __global__ void csv_error_kernel(CsvArgs a) {
   const unsigned long long j = a.err->line;
-  if (j == ~0ull || threadIdx.x != 0) return;
+  if (j == ~0ull) return;  // block-uniform
+  __shared__ uint8_t gtab[kGeoTabBytes];
+  __shared__ char gkeys[kGeoKeys * kGeoPropMax];
+  const GeoTabs gt{gtab, gkeys, {5, 8, 10, 11, a.len_ts, a.len_obj}};
+  if (a.format == 1) geo_tabs_fill(a, gtab, gkeys);
+  __syncthreads();
+  if (threadIdx.x != 0) return;
   LineOut o{0, 0, 0.0, 0.0, false, {0, 0}};
-  a.err->kind = eval_line(a, GBytes{a.text}, (int64_t)j, &o);
+  const GBytes s{a.text};
+  a.err->kind = a.format == 1 ? eval_geojson_line<false>(a, s, (int64_t)j, &o, gt) : eval_csv_line(a, s, (int64_t)j, &o);
 }
 
 hipError_t launch_csv_count(hipStream_t st, const char* text, int64_t len, int64_t nseg, uint32_t* counts) {
@@ -528,11 +773,22 @@ hipError_t launch_csv_index(hipStream_t st, const char* text, int64_t len, int64
   return hipGetLastError();
 }
 
-hipError_t launch_csv_parse(gf_ctx* ctx, const CsvArgs& a) {
+// Staging size: 256 mean-length lines plus a tenth for the spread of a block's sum, in 4-KB
+// steps between kCsvLds and kCsvLdsMax (CSV points ~55 B/line keep the 24 KB floor, so 6 blocks
+// share a CU; GeoJSON features ~183 B/line take 52 KB, 3 blocks per CU).  A block whose lines
+// exceed it parses from global memory (same result, one dependent L2 read per byte).
+hipError_t launch_csv_parse(gf_ctx* ctx, const CsvArgs& a0) {
   KTimer t(ctx, GF_K_CSV_PARSE);
+  CsvArgs a = a0;
+  const int64_t mean = a.lines > 0 ? (a.len + a.lines - 1) / a.lines : 0;
+  int64_t cap = (mean * kBlock * 11 / 10 + 4095) & ~(int64_t)4095;
+  a.lds_cap = (int32_t)(cap < kCsvLds ? kCsvLds : cap > kCsvLdsMax ? kCsvLdsMax : cap);
   if (a.lines > 0) {
     const unsigned blocks = (unsigned)((a.lines + kBlock - 1) / kBlock);
-    hipLaunchKernelGGL(csv_parse_kernel, dim3(blocks), dim3(kBlock), 0, ctx->stream, a);
+    if (a.format == 1)
+      hipLaunchKernelGGL(csv_parse_kernel<1>, dim3(blocks), dim3(kBlock), (size_t)a.lds_cap, ctx->stream, a);
+    else
+      hipLaunchKernelGGL(csv_parse_kernel<0>, dim3(blocks), dim3(kBlock), (size_t)a.lds_cap, ctx->stream, a);
   }
   hipLaunchKernelGGL(csv_error_kernel, dim3(1), dim3(64), 0, ctx->stream, a);
   return hipGetLastError();

@@ -81,3 +81,43 @@ def test_first_bad_line(sf, oracle_mod, bad, kind):
     assert (bl, bk) == (137, kind)
     with pytest.raises(ValueError, match=f"line 137: {sf.spatialStreams.CSV_KINDS[kind]}"):
         parse(sf, text)
+
+
+DEEP = b'{"geometry":{"coordinates":[1,2]},"x":' + b"[" * 70 + b"]" * 70 + b"}"
+TRICKY = [  # valid JSON the one-pass locator takes (or hands to the walk: depth > 63)
+    b'{"value":{"geometry":{"coordinates":[1,2]}},"value":{"geometry":{"coordinates":[3,4]},"properties":{"oID":"a"}}}',
+    b'{"value":{"geometry":{"coordinates":[1,2]}},"value":7,"geometry":{"coordinates":[5,6]}}',
+    b'{"geometry":{"coordinates":[1,2],"coordinates":[[8,9]]},"properties":{"timestamp":5,"oID":1,"oID":"x y"}}',
+    b'{"geometry":{"type":"Point","coordinates":[1,2]},"geometry":{"coordinates":[3,4]}}',
+    b'{"a":[{"geometry":{"coordinates":[9,9]}}],"geometry":{"coordinates":[1.5e1,-2]},"properties":{"p":{"oID":3},"oID":"7"}}',
+    b'{"value":{"value":{"geometry":{"coordinates":[0,0]}},"geometry":{"coordinates":[2,3]}}}',
+    b'{"properties":{"timestamp":1,"oID":2},"geometry":{"coordinates":[1,2]},"properties":[1,2]}',
+    ' { "geometry" : { "coordinates" : [ 1 , 2 ] } , "properties" : { "oID" : "é☃" } } '.encode(),
+    DEEP,
+    b'{"geometry":{"coordinates":[1,2]},"properties":{"coordinates":1,"timestamp":2,"oIDx":3,"oI":4}}',
+    b'{"geometry":{"coordinates":[[[1,2],[3,4]]]},"properties":{}}',
+    b'{"s":"}{][,:","geometry":{"coordinates":[1,2]},"properties":{"oID":"q"}}',
+    b'{"":1,"geometry":{"coordinates":[1,2]},"properties":{"oID":true,"timestamp":-0}}',
+    b'{"geometry":{"coordinates":[3,4]},"value":[{"properties":{"oID":5}}],"properties":{"oID":6}}',
+    b'{"value":{"geometry":{"coordinates":[3,4]}},"value":{"geometry":{"coordinates":[3,4]}},"properties":{"oID":6}}',
+    b'{"value":{"geometry":{"coordinates":[1,2]},"properties":{"oID":"v"}},"value":{"geometry":{"coordinates":[5,6]}}}',
+    b'{"geometry":{"coordinates":[1,2]},"properties":{"oID":null,"timestamp":-12}}',
+    b'{"key":1,"value":{"type":"Feature","geometry":{"coordinates":[1e-3,2E+1],"type":"Point"},"properties":{"oID":-5}}}',
+]
+
+
+@pytest.mark.parametrize("walk", [0, 1])
+def test_locator_matches_walk(sf, oracle_mod, walk):
+    """The one-pass member locator (k_csv.hip geo_locate) and the member-by-member walk it stands
+    in for give the oracle's results on generated lines plus valid JSON built to exercise last-wins
+    duplicates at each level, a non-object last "value", members inside arrays and deeper
+    objects, whitespace, UTF-8, structural bytes inside strings and nesting deeper than the
+    locator's stack.  (Escapes and malformed lines: test_first_bad_line, with the locator on.)"""
+    from spatialflink_amd import _lib
+    text = lines(21, 5_000, 0) + b"\n".join(TRICKY * 40) + b"\n"
+    ctx = _lib.context(0)
+    _lib.check(_lib.lib().gf_ctx_set_flag(ctx.handle, _lib.FLAG_GEOJSON_WALK, walk), ctx.handle, "flag")
+    try:
+        check(sf, oracle_mod, text, None, 0)
+    finally:
+        _lib.lib().gf_ctx_set_flag(ctx.handle, _lib.FLAG_GEOJSON_WALK, 0)
