@@ -463,22 +463,27 @@ __device__ __noinline__ int eval_geojson_walk(GeoProps a, Src s, int64_t p, int6
 // One-pass member location (the common case).  The walk above re-scans the feature once per
 // member it looks up, with nested data-dependent loops per lane: with 64 lines per wave in
 // different places of that loop nest the exec-mask bookkeeping dominated (~2.7 k scalar
-// instructions per line).  Here each lane runs one table-driven automaton over its line,
-// byte by byte (state x byte class -> next state + action, tables in LDS): a strict JSON
-// syntax check plus a small stack of container roles (top object, the record's "value" object,
-// the geometry and properties objects under either), recording the LAST value position of each
-// member the walk would look up.  On a line that passes the check -- strictly valid JSON, no
-// backslash, nesting <= 63 -- every jfind of the walk returns exactly that last member (the
-// walk's looser scanning agrees with JSON on valid input), so the results are the walk's.  Any
-// other line (malformed, escapes, deeper nesting) takes the walk itself.
+// instructions per line).  Here each lane runs one automaton over its line, byte by byte: a
+// strict JSON syntax check plus a small stack of container roles (the top object, the record's
+// "value" object, the geometry and properties objects under either), noting the position of
+// the LAST key of each member the walk would look up.  On a line that passes the check --
+// strictly valid JSON, no backslash, nesting <= 63 -- every jfind of the walk returns exactly
+// that last member's value (the walk's looser scanning agrees with JSON on valid input), so the
+// results are the walk's.  Any other line (malformed, escapes, deeper nesting) takes the walk.
+//
+// The per-byte step: one 8-B LDS entry per byte value holds the (next state, action) pair of
+// all 9 states (7 bits each), so the lookup does not wait on the state and the state update is
+// a shift; only the actions (brackets, commas, key quotes) do more, and the key comparison runs
+// only for keys of a looked-up length in a looked-up container.  (A select-only form of the
+// actions measured slower: 1.82 vs 1.67 ms for the locator over 1M lines.)  Stale
+// notes need no reset: a note is current when it lies after the note of its container's key
+// (e.g. the coordinates key after the last geometry key).
 // ---------------------------------------------------------------------------------------
-enum : uint8_t { JS_VAL, JS_ARR0, JS_OBJ0, JS_KEY, JS_COLON, JS_AFT, JS_VSTR, JS_KSTR, JS_TOK, JS_END, JS_ERR, JS_N };
-enum : uint8_t { JC_WS, JC_LBRACE, JC_RBRACE, JC_LBRACK, JC_RBRACK, JC_QUOTE, JC_COMMA, JC_COLON, JC_BSL, JC_TOK, JC_OTHER,
-                 JC_N = 16 };
+enum : uint8_t { JS_VAL, JS_ARR0, JS_OBJ0, JS_KEY, JS_COLON, JS_AFT, JS_VSTR, JS_KSTR, JS_TOK, JS_N, JS_ERR = 9 };
+enum : uint8_t { JC_WS, JC_LBRACE, JC_RBRACE, JC_LBRACK, JC_RBRACK, JC_QUOTE, JC_COMMA, JC_COLON, JC_BSL, JC_TOK, JC_OTHER };
 enum : uint8_t { JA_NONE, JA_PUSH_OBJ, JA_PUSH_ARR, JA_POP_OBJ, JA_POP_ARR, JA_COMMA, JA_KEY_BEGIN, JA_KEY_END };
-enum : int { JR_NONE, JR_TOP, JR_VAL, JR_GEO_T, JR_PROP_T, JR_GEO_V, JR_PROP_V };        // container roles
-enum : int { JK_NONE, JK_VALUE, JK_GEO, JK_PROP, JK_COORD, JK_TS, JK_OBJ, JK_TSOBJ };     // member kinds
-constexpr int kGeoTabBytes = 256 + JS_N * JC_N;
+enum : int { JR_NONE, JR_TOP, JR_VAL, JR_GEO_T, JR_PROP_T, JR_GEO_V, JR_PROP_V };  // container roles
+enum : int { JK_NONE, JK_VALUE, JK_GEO, JK_PROP };                                 // member kinds
 constexpr int kGeoKeys = 6;  // value, geometry, properties, coordinates, time property, objID property
 
 __device__ __forceinline__ uint8_t jclass(int c) {
@@ -498,46 +503,54 @@ __device__ __forceinline__ uint8_t jclass(int c) {
     return JC_TOK;
   return JC_OTHER;
 }
-// entry: next state | action << 4 | value-start << 7
+// next state | action << 4.  After the top object closes the state is JS_AFT at depth 0, where
+// a comma or a closer is an error (checked with the depth, geo_locate).
 __device__ __forceinline__ uint8_t jtrans(int st, int cl) {
-  auto E = [](int n, int act, int vs) { return (uint8_t)(n | act << 4 | vs << 7); };
-  if (st == JS_VSTR) return cl == JC_QUOTE ? E(JS_AFT, JA_NONE, 0) : cl == JC_BSL ? E(JS_ERR, 0, 0) : E(JS_VSTR, 0, 0);
-  if (st == JS_KSTR) return cl == JC_QUOTE ? E(JS_COLON, JA_KEY_END, 0) : cl == JC_BSL ? E(JS_ERR, 0, 0) : E(JS_KSTR, 0, 0);
-  if (cl == JC_WS) return E(st == JS_TOK ? JS_AFT : st, 0, 0);
+  auto E = [](int n, int act) { return (uint8_t)(n | act << 4); };
+  if (st == JS_VSTR) return cl == JC_QUOTE ? E(JS_AFT, 0) : cl == JC_BSL ? E(JS_ERR, 0) : E(JS_VSTR, 0);
+  if (st == JS_KSTR) return cl == JC_QUOTE ? E(JS_COLON, JA_KEY_END) : cl == JC_BSL ? E(JS_ERR, 0) : E(JS_KSTR, 0);
+  if (st == JS_TOK) {
+    if (cl == JC_TOK) return E(JS_TOK, 0);
+    st = JS_AFT;  // the token ends here: the byte is read as after a value
+  }
+  if (cl == JC_WS) return E(st, 0);
   switch (st) {
     case JS_VAL: case JS_ARR0:
-      if (cl == JC_LBRACE) return E(JS_OBJ0, JA_PUSH_OBJ, 1);
-      if (cl == JC_LBRACK) return E(JS_ARR0, JA_PUSH_ARR, 1);
-      if (cl == JC_QUOTE) return E(JS_VSTR, 0, 1);
-      if (cl == JC_TOK) return E(JS_TOK, 0, 1);
-      if (st == JS_ARR0 && cl == JC_RBRACK) return E(JS_AFT, JA_POP_ARR, 0);
-      return E(JS_ERR, 0, 0);
+      if (cl == JC_LBRACE) return E(JS_OBJ0, JA_PUSH_OBJ);
+      if (cl == JC_LBRACK) return E(JS_ARR0, JA_PUSH_ARR);
+      if (cl == JC_QUOTE) return E(JS_VSTR, 0);
+      if (cl == JC_TOK) return E(JS_TOK, 0);
+      if (st == JS_ARR0 && cl == JC_RBRACK) return E(JS_AFT, JA_POP_ARR);
+      return E(JS_ERR, 0);
     case JS_OBJ0:
-      if (cl == JC_QUOTE) return E(JS_KSTR, JA_KEY_BEGIN, 0);
-      if (cl == JC_RBRACE) return E(JS_AFT, JA_POP_OBJ, 0);
-      return E(JS_ERR, 0, 0);
-    case JS_KEY: return cl == JC_QUOTE ? E(JS_KSTR, JA_KEY_BEGIN, 0) : E(JS_ERR, 0, 0);
-    case JS_COLON: return cl == JC_COLON ? E(JS_VAL, 0, 0) : E(JS_ERR, 0, 0);
-    case JS_TOK: return cl == JC_TOK ? E(JS_TOK, 0, 0) : E(JS_ERR, 0, 0);  // other classes: looked up as JS_AFT
+      if (cl == JC_QUOTE) return E(JS_KSTR, JA_KEY_BEGIN);
+      if (cl == JC_RBRACE) return E(JS_AFT, JA_POP_OBJ);
+      return E(JS_ERR, 0);
+    case JS_KEY: return cl == JC_QUOTE ? E(JS_KSTR, JA_KEY_BEGIN) : E(JS_ERR, 0);
+    case JS_COLON: return cl == JC_COLON ? E(JS_VAL, 0) : E(JS_ERR, 0);
     case JS_AFT:
-      if (cl == JC_COMMA) return E(JS_VAL, JA_COMMA, 0);
-      if (cl == JC_RBRACE) return E(JS_AFT, JA_POP_OBJ, 0);
-      if (cl == JC_RBRACK) return E(JS_AFT, JA_POP_ARR, 0);
-      return E(JS_ERR, 0, 0);
-    default: return E(JS_ERR, 0, 0);  // JS_END: only blanks; JS_ERR stays
+      if (cl == JC_COMMA) return E(JS_VAL, JA_COMMA);
+      if (cl == JC_RBRACE) return E(JS_AFT, JA_POP_OBJ);
+      if (cl == JC_RBRACK) return E(JS_AFT, JA_POP_ARR);
+      return E(JS_ERR, 0);
+    default: return E(JS_ERR, 0);
   }
 }
 
-// LDS tables of a block: byte classes, transitions, the looked-up member names
+// LDS tables of a block: per byte value the 9 states' entries; the looked-up member names
 struct GeoTabs {
-  const uint8_t* tab;  // [256 classes | JS_N x JC_N transitions]
-  const char* keys;    // kGeoKeys x kGeoPropMax
+  const uint64_t* tab;  // [256]: entry of state s at bits 7s..7s+6
+  const char* keys;     // kGeoKeys x kGeoPropMax
   int32_t klen[kGeoKeys];
 };
 
-__device__ void geo_tabs_fill(const CsvArgs& a, uint8_t* tab, char* keys) {
-  for (int i = threadIdx.x; i < kGeoTabBytes; i += blockDim.x)
-    tab[i] = i < 256 ? jclass(i) : jtrans((i - 256) / JC_N, (i - 256) % JC_N);
+__device__ void geo_tabs_fill(const CsvArgs& a, uint64_t* tab, char* keys) {
+  for (int b = threadIdx.x; b < 256; b += blockDim.x) {
+    const int cl = jclass(b);
+    uint64_t t = 0;
+    for (int st = 0; st < JS_N; ++st) t |= (uint64_t)jtrans(st, cl) << (7 * st);
+    tab[b] = t;
+  }
   for (int i = threadIdx.x; i < kGeoKeys * kGeoPropMax; i += blockDim.x) {
     const int k = i / kGeoPropMax, c = i % kGeoPropMax;
     const char* names[4] = {"value", "geometry", "properties", "coordinates"};
@@ -560,89 +573,119 @@ __device__ __forceinline__ bool jkey_eq(const Src& s, int64_t ks, int len, const
   return eq;
 }
 
-// The automaton over [p, e) (s(p) == '{').  Returns false when the line must take the walk;
-// otherwise the member positions: g, c (coordinates), pr, t, q of the feature, -1 when absent.
+// the value of the member whose key's closing quote is at k (valid JSON: '"' ws ':' ws value)
 template <class Src>
-__device__ __forceinline__ bool geo_locate(const Src& s, int64_t p, int64_t e, const GeoTabs& gt, int64_t* loc) {
+__device__ __forceinline__ int64_t jmember_value(const Src& s, int64_t k, int64_t e) {
+  return jskip(s, jskip(s, k + 1, e) + 1, e);
+}
+
+// The automaton over the line [p, e) (s(p) == '{'), staged in LDS (lds + (pos - base)).  Returns
+// false when the line must take the walk; otherwise the feature's member values g, c
+// (coordinates), pr, t, q: first byte, -1 when absent.
+__device__ __forceinline__ bool geo_locate(const LBytes& s, int64_t p, int64_t e, const GeoTabs& gt, int64_t* loc) {
   if (e - p >= INT32_MAX) return false;
   int st = JS_VAL, depth = 0, pend = JK_NONE;
+  bool bad = false;
   uint64_t kinds = 0;  // bit d: the container at depth d is an object
   uint32_t roles = 0;  // 4 bits per depth 1..7
   int32_t ks = 0;
-  // last value positions (offsets from p): the record's "value"; per feature (top / value object)
+  // closing-quote positions (from p) of the last keys noted: the record's "value"; per feature
+  // (top object T / value object V) geometry, properties, coordinates, time, objID
   int32_t v = -1, gT = -1, prT = -1, cT = -1, tT = -1, qT = -1, gV = -1, prV = -1, cV = -1, tV = -1, qV = -1;
-  const int32_t n = (int32_t)(e - p);
-  for (int32_t i = 0; i < n; ++i) {
-    const int cl = gt.tab[(uint8_t)s(p + i)];
-    const int se = st == JS_TOK && cl != JC_TOK ? JS_AFT : st;
-    const int ent = gt.tab[256 + se * JC_N + cl];
-    int nst = ent & 15;
-    const int act = (ent >> 4) & 7;
-    if (ent & 0xF0) {
-      const int role = depth <= 7 ? (int)(roles >> (4 * depth)) & 15 : JR_NONE;
-      if ((ent & 0x80) && pend) {  // the value of a looked-up member starts here
-        if (role == JR_TOP) {
-          if (pend == JK_VALUE) { v = i; gV = prV = cV = tV = qV = -1; }
-          if (pend == JK_GEO) { gT = i; cT = -1; }
-          if (pend == JK_PROP) { prT = i; tT = qT = -1; }
-        } else if (role == JR_VAL) {
-          if (pend == JK_GEO) { gV = i; cV = -1; }
-          if (pend == JK_PROP) { prV = i; tV = qV = -1; }
-        } else if (role == JR_GEO_T) {
-          cT = i;
-        } else if (role == JR_GEO_V) {
-          cV = i;
-        } else if (role == JR_PROP_T) {
-          if (pend != JK_OBJ) tT = i;
-          if (pend != JK_TS) qT = i;
-        } else if (role == JR_PROP_V) {
-          if (pend != JK_OBJ) tV = i;
-          if (pend != JK_TS) qV = i;
-        }
-      }
-      if (act == JA_PUSH_OBJ || act == JA_PUSH_ARR) {
-        if (depth == 63) return false;
-        int child = JR_NONE;
-        if (act == JA_PUSH_OBJ) {
-          if (depth == 0) child = JR_TOP;
-          else if (role == JR_TOP) child = pend == JK_VALUE ? JR_VAL : pend == JK_GEO ? JR_GEO_T : pend == JK_PROP ? JR_PROP_T : JR_NONE;
-          else if (role == JR_VAL) child = pend == JK_GEO ? JR_GEO_V : pend == JK_PROP ? JR_PROP_V : JR_NONE;
-        }
-        ++depth;
-        kinds = (kinds & ~(1ull << depth)) | ((uint64_t)(act == JA_PUSH_OBJ) << depth);
-        if (depth <= 7) roles = (roles & ~(15u << (4 * depth))) | ((uint32_t)child << (4 * depth));
-      }
-      if (ent & 0x80) pend = JK_NONE;
-      if (act == JA_POP_OBJ || act == JA_POP_ARR) {
-        if ((int)((kinds >> depth) & 1) != (act == JA_POP_OBJ)) return false;
-        if (--depth == 0) nst = JS_END;
-      } else if (act == JA_COMMA) {
-        nst = (kinds >> depth) & 1 ? JS_KEY : JS_VAL;
-      } else if (act == JA_KEY_BEGIN) {
-        ks = i + 1;
-      } else if (act == JA_KEY_END) {
-        const int len = i - ks;
-        pend = JK_NONE;
-        if (role == JR_TOP || role == JR_VAL) {
-          if (role == JR_TOP && jkey_eq(s, p + ks, len, gt, 0)) pend = JK_VALUE;
-          else if (jkey_eq(s, p + ks, len, gt, 1)) pend = JK_GEO;
-          else if (jkey_eq(s, p + ks, len, gt, 2)) pend = JK_PROP;
-        } else if (role == JR_GEO_T || role == JR_GEO_V) {
-          if (jkey_eq(s, p + ks, len, gt, 3)) pend = JK_COORD;
-        } else if (role == JR_PROP_T || role == JR_PROP_V) {
-          const bool ts = jkey_eq(s, p + ks, len, gt, 4), ob = jkey_eq(s, p + ks, len, gt, 5);
-          pend = ts && ob ? JK_TSOBJ : ts ? JK_TS : ob ? JK_OBJ : JK_NONE;
-        }
-      }
-    }
-    if (nst == JS_ERR) return false;
-    st = nst;
-  }
-  if (st != JS_END) return false;
-  const bool val = v >= 0 && s(p + v) == '{';
-  const int32_t off[5] = {val ? gV : gT, val ? cV : cT, val ? prV : prT, val ? tV : tT, val ? qV : qT};
+  // length filters of the keys looked up per container group (lengths < 64)
+  const uint64_t lf_top = (1ull << 5) | (1ull << 8) | (1ull << 10), lf_geo = 1ull << 11;
+  const uint64_t lf_prop = (gt.klen[4] >= 0 ? 1ull << gt.klen[4] : 0) | (gt.klen[5] >= 0 ? 1ull << gt.klen[5] : 0);
+  const int64_t w0 = (p - s.base) & ~(int64_t)3, w1 = e - s.base;  // LDS word range
+  for (int64_t w = w0; w < w1 && !bad; w += 4) {
+    const uint32_t word = *reinterpret_cast<const uint32_t*>(s.p + w);
 #pragma unroll
-  for (int k = 0; k < 5; ++k) loc[k] = off[k] < 0 ? -1 : p + off[k];
+    for (int k = 0; k < 4; ++k) {
+      const int64_t at = w + k;  // LDS offset
+      const int32_t i = (int32_t)(at + s.base - p);
+      const uint32_t byte = i < 0 || at >= w1 ? (uint32_t)' ' : (word >> (8 * k)) & 0xFFu;
+      const uint32_t ent = (uint32_t)(gt.tab[byte] >> (7 * st)) & 0x7Fu;
+      int nst = (int)(ent & 15u);
+      const int act = (int)(ent >> 4);
+      if (act) {
+        const int role = (unsigned)depth <= 7u ? (int)(roles >> (4 * depth)) & 15 : JR_NONE;
+        if (act == JA_PUSH_OBJ || act == JA_PUSH_ARR) {
+          int child = depth == 0 ? JR_TOP
+                    : role == JR_TOP ? (int)(0x4320u >> (4 * pend)) & 15   // value, geometry, properties
+                    : role == JR_VAL ? (int)(0x6500u >> (4 * pend)) & 15   // geometry, properties
+                    : JR_NONE;
+          if (act == JA_PUSH_ARR) child = JR_NONE;
+          ++depth;
+          bad |= depth > 63;
+          kinds = (kinds & ~(1ull << (depth & 63))) | ((uint64_t)(act == JA_PUSH_OBJ) << (depth & 63));
+          if ((unsigned)depth <= 7u) roles = (roles & ~(15u << (4 * depth))) | ((uint32_t)child << (4 * depth));
+        } else if (act == JA_POP_OBJ || act == JA_POP_ARR) {
+          bad |= depth <= 0 || (int)((kinds >> (depth & 63)) & 1) != (act == JA_POP_OBJ);
+          --depth;
+        } else if (act == JA_COMMA) {
+          bad |= depth <= 0;
+          nst = (kinds >> (depth & 63)) & 1 ? JS_KEY : JS_VAL;
+        } else if (act == JA_KEY_BEGIN) {
+          ks = i + 1;
+        } else {  // JA_KEY_END: note a looked-up member of a looked-up container
+          const int len = i - ks;
+          const uint64_t lf = role == JR_TOP || role == JR_VAL ? lf_top
+                            : role == JR_GEO_T || role == JR_GEO_V ? lf_geo
+                            : role == JR_PROP_T || role == JR_PROP_V ? lf_prop : 0;
+          pend = JK_NONE;
+          if (len < 64 && ((lf >> len) & 1)) {
+            const int64_t kp = p + ks;
+            if (role == JR_TOP || role == JR_VAL) {
+              if (role == JR_TOP && jkey_eq(s, kp, len, gt, 0)) {
+                pend = JK_VALUE;
+                v = i;
+              } else if (jkey_eq(s, kp, len, gt, 1)) {
+                pend = JK_GEO;
+                if (role == JR_TOP) gT = i; else gV = i;
+              } else if (jkey_eq(s, kp, len, gt, 2)) {
+                pend = JK_PROP;
+                if (role == JR_TOP) prT = i; else prV = i;
+              }
+            } else if (role == JR_GEO_T || role == JR_GEO_V) {
+              if (jkey_eq(s, kp, len, gt, 3)) {
+                if (role == JR_GEO_T) cT = i; else cV = i;
+              }
+            } else {
+              if (jkey_eq(s, kp, len, gt, 4)) {
+                if (role == JR_PROP_T) tT = i; else tV = i;
+              }
+              if (jkey_eq(s, kp, len, gt, 5)) {
+                if (role == JR_PROP_T) qT = i; else qV = i;
+              }
+            }
+          }
+        }
+      }
+      bad |= nst == JS_ERR;
+      st = nst == JS_ERR ? JS_AFT : nst;
+    }
+  }
+  if (bad || st != JS_AFT || depth != 0) return false;
+  auto val = [&](int32_t k) { return k < 0 ? (int64_t)-1 : jmember_value(s, p + k, e); };
+  const int64_t vv = val(v);
+  int32_t g, c, pr, t, q;
+  if (vv >= 0 && s(vv) == '{') {  // notes inside an earlier "value" object or member are stale
+    g = gV > v ? gV : -1;
+    pr = prV > v ? prV : -1;
+    c = g >= 0 && cV > g ? cV : -1;
+    t = pr >= 0 && tV > pr ? tV : -1;
+    q = pr >= 0 && qV > pr ? qV : -1;
+  } else {
+    g = gT;
+    pr = prT;
+    c = g >= 0 && cT > g ? cT : -1;
+    t = pr >= 0 && tT > pr ? tT : -1;
+    q = pr >= 0 && qT > pr ? qT : -1;
+  }
+  loc[0] = val(g);
+  loc[1] = val(c);
+  loc[2] = val(pr);
+  loc[3] = val(t);
+  loc[4] = val(q);
   return true;
 }
 
@@ -657,13 +700,26 @@ __device__ __forceinline__ int eval_geojson_line(const CsvArgs& a, const Src& s,
   if (p >= e || s(p) != '{') return kCsvMissingField;
   const GeoProps gp{gt.keys + 4 * kGeoPropMax, gt.keys + 5 * kGeoPropMax, a.len_ts, a.len_obj, a.date_fmt, a.tz_off_ms};
   int64_t loc[5];
-  if (!FAST || !geo_locate(s, p, e, gt, loc)) return eval_geojson_walk(gp, s, p, e, o);
+  bool located = false;
+  if constexpr (FAST) located = geo_locate(s, p, e, gt, loc);
+#if GF_ABL_GEO == 3
+  if (!located) { o->x = -12345.0; o->y = 0; o->ts = 0; o->obj = GF_OBJID_NULL; o->dict = false; return kCsvOk; }
+#endif
+  if (!located) return eval_geojson_walk(gp, s, p, e, o);
+#if GF_ABL_GEO == 1
+  o->x = (double)(loc[0] + loc[1] + loc[2] + loc[3] + loc[4]); o->y = 0; o->ts = 0; o->obj = GF_OBJID_NULL; o->dict = false;
+  return kCsvOk;
+#endif
   const int64_t g = loc[0], c = loc[1], pr = loc[2];
   if (g < 0 || s(g) != '{') return kCsvMissingField;
   if (c < 0 || s(c) != '[') return kCsvMissingField;
   const int st = geo_coords(s, c, e, o);
   if (st) return st;
   if (pr < 0 || s(pr) != '{') return kCsvOk;
+#if GF_ABL_GEO == 2
+  o->ts = loc[3] + loc[4];
+  return kCsvOk;
+#endif
   return geo_props(gp, s, e, a.len_ts >= 0 ? loc[3] : -1, a.len_obj >= 0 ? loc[4] : -1, o);
 }
 
@@ -708,7 +764,7 @@ __global__ __launch_bounds__(kBlock) void csv_parse_kernel(CsvArgs a) {
   const int64_t j = L0 + threadIdx.x;
   DictWork w{0, 0, 0};
   bool need = false;
-  __shared__ uint8_t gtab[FMT == 1 ? kGeoTabBytes : 1];
+  __shared__ uint64_t gtab[FMT == 1 ? 256 : 1];
   __shared__ char gkeys[FMT == 1 ? kGeoKeys * kGeoPropMax : 1];
   const GeoTabs gt{gtab, gkeys, {5, 8, 10, 11, a.len_ts, a.len_obj}};
   if (FMT == 1) {
@@ -751,7 +807,7 @@ __global__ __launch_bounds__(kBlock) void csv_parse_kernel(CsvArgs a) {
 __global__ void csv_error_kernel(CsvArgs a) {
   const unsigned long long j = a.err->line;
   if (j == ~0ull) return;  // block-uniform
-  __shared__ uint8_t gtab[kGeoTabBytes];
+  __shared__ uint64_t gtab[256];
   __shared__ char gkeys[kGeoKeys * kGeoPropMax];
   const GeoTabs gt{gtab, gkeys, {5, 8, 10, 11, a.len_ts, a.len_obj}};
   if (a.format == 1) geo_tabs_fill(a, gtab, gkeys);
@@ -773,15 +829,20 @@ hipError_t launch_csv_index(hipStream_t st, const char* text, int64_t len, int64
   return hipGetLastError();
 }
 
-// Staging size: 256 mean-length lines plus a tenth for the spread of a block's sum, in 4-KB
+// Staging size: 256 mean-length lines plus a tenth for the spread of a block's sum, in 1-KB
 // steps between kCsvLds and kCsvLdsMax (CSV points ~55 B/line keep the 24 KB floor, so 6 blocks
-// share a CU; GeoJSON features ~183 B/line take 52 KB, 3 blocks per CU).  A block whose lines
-// exceed it parses from global memory (same result, one dependent L2 read per byte).
+// share a CU).  GeoJSON features (~183 B/line, ~47 KB a block) are held to 50 KB when a mean
+// block fits it with 5% to spare, so that 3 blocks (with the locator's 2.4 KB of tables) share
+// a CU.  A block whose lines exceed the staging area parses from global memory with the walk
+// (same results, one dependent L2 read per byte).
 hipError_t launch_csv_parse(gf_ctx* ctx, const CsvArgs& a0) {
   KTimer t(ctx, GF_K_CSV_PARSE);
   CsvArgs a = a0;
   const int64_t mean = a.lines > 0 ? (a.len + a.lines - 1) / a.lines : 0;
-  int64_t cap = (mean * kBlock * 11 / 10 + 4095) & ~(int64_t)4095;
+  const int64_t need = mean * kBlock;
+  int64_t cap = (need * 11 / 10 + 1023) & ~(int64_t)1023;
+  constexpr int64_t kGeoLds3 = 50 * 1024;
+  if (a.format == 1 && cap > kGeoLds3 && need * 20 <= kGeoLds3 * 19) cap = kGeoLds3;
   a.lds_cap = (int32_t)(cap < kCsvLds ? kCsvLds : cap > kCsvLdsMax ? kCsvLdsMax : cap);
   if (a.lines > 0) {
     const unsigned blocks = (unsigned)((a.lines + kBlock - 1) / kBlock);
