@@ -702,24 +702,13 @@ __device__ __forceinline__ int eval_geojson_line(const CsvArgs& a, const Src& s,
   int64_t loc[5];
   bool located = false;
   if constexpr (FAST) located = geo_locate(s, p, e, gt, loc);
-#if GF_ABL_GEO == 3
-  if (!located) { o->x = -12345.0; o->y = 0; o->ts = 0; o->obj = GF_OBJID_NULL; o->dict = false; return kCsvOk; }
-#endif
   if (!located) return eval_geojson_walk(gp, s, p, e, o);
-#if GF_ABL_GEO == 1
-  o->x = (double)(loc[0] + loc[1] + loc[2] + loc[3] + loc[4]); o->y = 0; o->ts = 0; o->obj = GF_OBJID_NULL; o->dict = false;
-  return kCsvOk;
-#endif
   const int64_t g = loc[0], c = loc[1], pr = loc[2];
   if (g < 0 || s(g) != '{') return kCsvMissingField;
   if (c < 0 || s(c) != '[') return kCsvMissingField;
   const int st = geo_coords(s, c, e, o);
   if (st) return st;
   if (pr < 0 || s(pr) != '{') return kCsvOk;
-#if GF_ABL_GEO == 2
-  o->ts = loc[3] + loc[4];
-  return kCsvOk;
-#endif
   return geo_props(gp, s, e, a.len_ts >= 0 ? loc[3] : -1, a.len_obj >= 0 ? loc[4] : -1, o);
 }
 
