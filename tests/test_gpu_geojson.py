@@ -84,7 +84,7 @@ def test_first_bad_line(sf, oracle_mod, bad, kind):
 
 
 DEEP = b'{"geometry":{"coordinates":[1,2]},"x":' + b"[" * 70 + b"]" * 70 + b"}"
-TRICKY = [  # valid JSON the one-pass locator takes (or hands to the walk: depth > 63)
+TRICKY = [  # valid JSON the one-pass locator takes (or hands to the walk: escapes, depth > 63)
     b'{"value":{"geometry":{"coordinates":[1,2]}},"value":{"geometry":{"coordinates":[3,4]},"properties":{"oID":"a"}}}',
     b'{"value":{"geometry":{"coordinates":[1,2]}},"value":7,"geometry":{"coordinates":[5,6]}}',
     b'{"geometry":{"coordinates":[1,2],"coordinates":[[8,9]]},"properties":{"timestamp":5,"oID":1,"oID":"x y"}}',
@@ -97,6 +97,7 @@ TRICKY = [  # valid JSON the one-pass locator takes (or hands to the walk: depth
     b'{"geometry":{"coordinates":[1,2]},"properties":{"coordinates":1,"timestamp":2,"oIDx":3,"oI":4}}',
     b'{"geometry":{"coordinates":[[[1,2],[3,4]]]},"properties":{}}',
     b'{"s":"}{][,:","geometry":{"coordinates":[1,2]},"properties":{"oID":"q"}}',
+    b'{"s":"a\\"b\\u0041","geometry":{"coordinates":[1,2]},"properties":{"oID":"q","timestamp":3}}',
     b'{"":1,"geometry":{"coordinates":[1,2]},"properties":{"oID":true,"timestamp":-0}}',
     b'{"geometry":{"coordinates":[3,4]},"value":[{"properties":{"oID":5}}],"properties":{"oID":6}}',
     b'{"value":{"geometry":{"coordinates":[3,4]}},"value":{"geometry":{"coordinates":[3,4]}},"properties":{"oID":6}}',
@@ -111,8 +112,8 @@ def test_locator_matches_walk(sf, oracle_mod, walk):
     """The one-pass member locator (k_csv.hip geo_locate) and the member-by-member walk it stands
     in for give the oracle's results on generated lines plus valid JSON built to exercise last-wins
     duplicates at each level, a non-object last "value", members inside arrays and deeper
-    objects, whitespace, UTF-8, structural bytes inside strings and nesting deeper than the
-    locator's stack.  (Escapes and malformed lines: test_first_bad_line, with the locator on.)"""
+    objects, whitespace, UTF-8, structural bytes inside strings, an escape in a member not taken and nesting deeper than
+    the locator's stack.  (Escapes and malformed lines: test_first_bad_line, with the locator on.)"""
     from spatialflink_amd import _lib
     text = lines(21, 5_000, 0) + b"\n".join(TRICKY * 40) + b"\n"
     ctx = _lib.context(0)
