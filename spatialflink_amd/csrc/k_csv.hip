@@ -595,14 +595,13 @@ __device__ __forceinline__ bool geo_locate(const LBytes& s, int64_t p, int64_t e
   // length filters of the keys looked up per container group (lengths < 64)
   const uint64_t lf_top = (1ull << 5) | (1ull << 8) | (1ull << 10), lf_geo = 1ull << 11;
   const uint64_t lf_prop = (gt.klen[4] >= 0 ? 1ull << gt.klen[4] : 0) | (gt.klen[5] >= 0 ? 1ull << gt.klen[5] : 0);
-  const int64_t w0 = (p - s.base) & ~(int64_t)3, w1 = e - s.base;  // LDS word range
-  for (int64_t w = w0; w < w1 && !bad; w += 4) {
+  const int32_t o0 = (int32_t)(p - s.base), o1 = (int32_t)(e - s.base);  // the line's LDS offsets
+  for (int32_t w = o0 & ~3; w < o1 && !bad; w += 4) {
     const uint32_t word = *reinterpret_cast<const uint32_t*>(s.p + w);
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      const int64_t at = w + k;  // LDS offset
-      const int32_t i = (int32_t)(at + s.base - p);
-      const uint32_t byte = i < 0 || at >= w1 ? (uint32_t)' ' : (word >> (8 * k)) & 0xFFu;
+      const int32_t i = w + k - o0;  // offset in the line
+      const uint32_t byte = i < 0 || w + k >= o1 ? (uint32_t)' ' : (word >> (8 * k)) & 0xFFu;
       const uint32_t ent = (uint32_t)(gt.tab[byte] >> (7 * st)) & 0x7Fu;
       int nst = (int)(ent & 15u);
       const int act = (int)(ent >> 4);
