@@ -11,7 +11,7 @@ LIB      := spatialflink_amd/libgeoflink_hip.so
 SOURCES  := $(SRC)/api.cpp $(SRC)/sliding.cpp $(SRC)/csv.cpp $(SRC)/objid.cpp $(SRC)/k_points.hip $(SRC)/k_knn.hip \
             $(SRC)/k_range.hip $(SRC)/k_join.hip $(SRC)/k_csv.hip $(SRC)/k_objid.hip
 OBJECTS  := $(patsubst $(SRC)/%,$(OBJDIR)/%.o,$(SOURCES))
-HEADERS  := include/geoflink_hip.h $(SRC)/gf_internal.hpp $(SRC)/gf_numerics.hpp $(SRC)/gf_decimal.hpp $(SRC)/gf_pow5.hpp $(SRC)/gf_geom.hpp
+HEADERS  := include/geoflink_hip.h $(SRC)/gf_internal.hpp $(SRC)/gf_text.hpp $(SRC)/gf_geojson.hpp $(SRC)/gf_numerics.hpp $(SRC)/gf_decimal.hpp $(SRC)/gf_pow5.hpp $(SRC)/gf_geom.hpp
 
 all: $(LIB) oracle
 

@@ -212,6 +212,10 @@ def main():
     def exchange(first, lo, hi):  # windows [lo, hi] of one group: one all-gather + one merge launch
         g = (lo - first) // B
         sharding.allgather_knn_records_batch(slots[g % 2, : hi - lo + 1], args.k, host.ptr(lo))
+        if args.pipeline == 3:
+            # depth 3 writes odd windows' records on the plan's second stream: it must not
+            # reuse slots[g % 2] (group g + 2) before this all-gather + merge have read them
+            _lib.check(L.gf_ctx_fork(ctx.handle), ctx.handle, "gf_ctx_fork")
 
     def step(i, first):
         if world == 1:  # the select writes the final record straight into pinned host memory
@@ -379,6 +383,30 @@ def main():
 
     verified = None
     cpu = None
+    if rank == 0 and world > 1 and not args.no_verify and world * n <= 100_000_000:
+        # the merged record of window 0 (every rank's band of it, all-gathered over the
+        # backend and merged on the device) == the oracle on the whole window: rank 0
+        # regenerates the other ranks' bands (same seeds) and concatenates them in rank order,
+        # so the global index of rank r's point i is r * n + i (its plan's index base)
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle as O
+
+        t = time.perf_counter()
+        xs, ys, objs = [], [], []
+        for r_ in range(world):
+            blo, bhi = sharding.column_bands(args.grid, world)[r_]
+            bx0, bx1 = sharding.band_x_range(grid, blo, bhi)
+            x_, y_ = W.gen_points(sf, 42 + 1000 * r_, n, bx0, bx1)
+            xs.append(x_); ys.append(y_); objs.append(np.arange(r_ * n, (r_ + 1) * n, dtype=np.int64))
+        og = O.grid(args.grid, *BEIJING)
+        st, oo, od, oi = O.knn(og, np.concatenate(xs), np.concatenate(ys), np.concatenate(objs), QPOINT[0],
+                               QPOINT[1], args.radius, args.k)
+        got = per_window[0]
+        verified = bool(st == 0 and np.array_equal(oo, got[0]) and np.array_equal(od, got[1])
+                        and np.array_equal(oi, got[2]))
+        log(f"oracle verification of window 0 over {world} ranks x {n} points: {verified} "
+            f"({time.perf_counter()-t:.1f}s)")
+        assert verified, "merged multi-rank kNN differs from the oracle"
     if rank == 0 and world == 1:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle as O

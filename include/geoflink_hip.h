@@ -248,7 +248,8 @@ int    gf_knn_plan_set_pipeline(gf_knn_plan* plan, int depth);
 int    gf_knn_plan_flush(gf_knn_plan* plan);
 /* Result record: gf_knn_header followed by double dist[k], int64 objID[k], int64 idx[k]. */
 typedef struct {
-  int32_t status;        /* 0 = final; 1 = needs the exact fallback (see gf_knn_decode) */
+  int32_t status;        /* 0 = final; 1 = needs the exact fallback (see gf_knn_decode);
+                            2 = a GF_MERGE_FOREIGN_KEYS merge met dictionary objID keys */
   int32_t n;             /* entries (<= k) */
   int32_t k;
   int32_t flags;
@@ -273,9 +274,17 @@ int    gf_knn_merge_dev(gf_ctx* ctx, int32_t k, const void* records, int32_t nre
 /* Batched: nwin windows in one launch (one block each), so one RCCL all-gather can carry the
  * records of several windows.  layout GF_MERGE_SHARD_MAJOR: record (shard s, window w) at
  * index s*nwin + w (an all-gather of each rank's nwin consecutive records);
- * GF_MERGE_WINDOW_MAJOR: at index w*nrec + s.  `results` receives nwin consecutive records. */
+ * GF_MERGE_WINDOW_MAJOR: at index w*nrec + s.  `results` receives nwin consecutive records.
+ * layout | GF_MERGE_FOREIGN_KEYS: the records come from other contexts (an all-gather across
+ * ranks).  Dictionary objID keys (below GF_OBJID_NUMERIC_MIN, GF_OBJID_NULL aside) are ids in
+ * their own context's gf_objid_dict, so keys of different ranks cannot be compared or deduped:
+ * a window holding one gets status 2 (GF_KNN_STATUS_FOREIGN_KEYS) and no entries -- merge such
+ * windows by their Strings instead (spatialflink_amd.sharding.allgather_knn_string_lists).
+ * Canonical decimal objIDs are their values and merge across ranks. */
 #define GF_MERGE_SHARD_MAJOR  0
 #define GF_MERGE_WINDOW_MAJOR 1
+#define GF_MERGE_FOREIGN_KEYS 0x100
+#define GF_KNN_STATUS_FOREIGN_KEYS 2
 int    gf_knn_merge_dev_batch(gf_ctx* ctx, int32_t k, const void* records, int32_t nrec, int32_t nwin,
                               int32_t layout, void* results);
 /* Host merge of per-shard sorted lists: top-k distinct objIDs by (dist, objID). */
@@ -372,25 +381,39 @@ int gf_csv_parse_dict(gf_ctx* ctx, gf_objid_dict* dict, const char* text, int64_
 
 /* ---- GeoJSON ingest ------------------------------------------------------------------
  * Deserialization.GeoJSONToTSpatial(uGrid, dateFormat, propertyTimeStamp, propertyObjID).map
- * (Deserialization.java:149-211) over a chunk of lines, one JSON object per line: the Kafka
- * key/value record {"key":..,"value":{Feature}} (the object under "value" is the feature) or a
- * bare Feature (Serialization.PointToGeoJSONOutputSchema's output).  Per line, in the reference's
- * order: x, y = the geometry's first coordinate (geometry.getCoordinate(): "coordinates" of
- * "geometry", first number pair, descending nested arrays); then from "properties" (absent or not
- * an object: objID null, ts 0): ts from `time_property` -- date_format 0: Long.parseLong of the
- * node's text (a JSON integer; anything else throws NumberFormatException: GF_CSV_NUMBER_FORMAT),
- * date_format 1: the string value parsed as SimpleDateFormat("yyyy-MM-dd HH:mm:ss") (lenient
- * field rollover) in a fixed UTC offset (tz_offset_minutes; DST not modelled), unparsable -> 0;
- * objID from `objid_property` -- node.toString() without '"': a string's content, an integer's
- * digits ("-0" -> "0"), true / false / null as text; absent -> GF_OBJID_NULL.  The last of
- * duplicate keys wins (Jackson ObjectNode).  GF_CSV_UNSUPPORTED: strings with escapes where a
- * value is taken, non-integer or structured objID values, years before 1583 (Julian calendar),
- * property names longer than 63 bytes. */
+ * (Deserialization.java:149-211) over a chunk of lines, one JSON object per line: the ObjectNode
+ * the map receives -- the Kafka record {"key":..,"value":..} (JSONKeyValueDeserializationSchema)
+ * -- or, with value_lines = 1, the record's value itself (a Feature as
+ * Serialization.PointToGeoJSONOutputSchema writes it).  Per line, in the map's order:
+ *  - the record must be strict JSON as Jackson reads it (no NaN / Infinity, leading zeros,
+ *    unescaped control bytes; UTF-8 checked structurally), else GF_CSV_MISSING_FIELD;
+ *  - V = "value" (last duplicate wins, Jackson ObjectNode); missing / not an object:
+ *    GF_CSV_MISSING_FIELD (the map's NullPointerException);
+ *  - geometry = readGeoJSON(V) (jts-io-common 1.18.0 GeoJsonReader): V's "type" "Point" ->
+ *    V's "coordinates"; on failure, and for "Feature" or a missing / non-string / unknown
+ *    "type", the reference's catch branch readGeoJSON(V.geometry): "type" "Point" and
+ *    "coordinates", else the line fails (GF_CSV_MISSING_FIELD; a non-number ordinate
+ *    GF_CSV_NUMBER_FORMAT).  x, y = ordinates 0 and 1 (an integer literal is (double) of its
+ *    long: "-0" -> 0.0);
+ *  - from V's "properties" (absent or not an object: objID null, ts 0): ts from time_property
+ *    -- date_format 0: Long.parseLong of the node's text (a JSON integer; anything else throws
+ *    NumberFormatException: GF_CSV_NUMBER_FORMAT), date_format 1: the string value parsed as
+ *    SimpleDateFormat("yyyy-MM-dd HH:mm:ss") (lenient field rollover) in a fixed UTC offset
+ *    (tz_offset_minutes; DST not modelled), unparsable -> 0; objID from objid_property --
+ *    node.toString() without '"': a string's content, an integer's digits ("-0" -> "0"),
+ *    true / false / null as text; absent -> GF_OBJID_NULL.
+ * GF_CSV_UNSUPPORTED (not restated, never guessed): geometry types other than Point (JTS builds
+ * and validates them) and FeatureCollection; Point coordinates with fewer than two ordinates or
+ * a non-number third; a number Jackson hands json-simple as text it cannot read back (a float
+ * literal overflowing to Infinity, an integer literal outside long) anywhere on the line;
+ * nesting deeper than 256; escapes in a taken string or in a member name of an object a value is
+ * looked up in; non-integer or structured objID values; years before 1583 (Julian calendar). */
 typedef struct {
-  const char* objid_property;   /* propertyObjID (host C string); NULL: objID always null */
+  const char* objid_property;   /* propertyObjID (host C string, < 64 bytes); NULL: objID always null */
   const char* time_property;    /* propertyTimeStamp; NULL: ts always 0 */
   int32_t date_format;          /* 0: integer milliseconds; 1: "yyyy-MM-dd HH:mm:ss" */
   int32_t tz_offset_minutes;    /* date_format 1: offset of the reference JVM's default zone */
+  int32_t value_lines;          /* 0: each line is the record {"key":..,"value":..}; 1: its value */
 } gf_geojson_schema;
 /* Same conventions as gf_csv_parse_dict (device text, outputs, capacity, first bad line). */
 int gf_geojson_parse(gf_ctx* ctx, gf_objid_dict* dict, const char* text, int64_t len, const gf_geojson_schema* schema,

@@ -11,6 +11,8 @@ import ctypes as C
 import os
 import subprocess
 
+import math
+
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -307,16 +309,33 @@ def csv_parse(text: bytes, delim: str, want):
 
 # ---------------------------------------------------------------------------------------------
 # GeoJSON point ingest -- Deserialization.GeoJSONToTSpatial.map (Deserialization.java:149-211),
-# restated over Python's json module (a JSON parser independent of the device scanner):
-#   geometry = readGeoJSON(value) -- the geometry's first coordinate (:170-178, :203/:207);
+# restated over Python's json module (a JSON parser independent of the device scanner).  A line is
+# the map's input ObjectNode: the Kafka record {"key": .., "value": ..} (JSONKeyValue-
+# DeserializationSchema); value_lines: the record's value itself.  Per line:
+#   Jackson reads the record: strict JSON (json.loads with NaN / Infinity refused, as Jackson's
+#     defaults do; UTF-8 checked structurally, as Jackson's UTF-8 reader does) -> else kind 3;
+#   V = record.get("value") (last duplicate); missing / not an object -> kind 3 (the map's NPE);
+#   geometry = readGeoJSON(V.toString()) -- jts-io-common 1.18.0 GeoJsonReader (pom.xml:100-104,
+#     absent from the reference tree; its published algorithm): V.type "Point" -> V.coordinates;
+#     on failure, and for "Feature" (createFeature reads the same V.geometry) or a missing /
+#     non-string / unknown type, the catch branch (:136-141, :172-178):
+#     readGeoJSON(V.get("geometry").toString()) must be a Point, else the line fails;
 #   time: dateFormat null -> Long.parseLong(String.valueOf(node)) (:190; a non-integer node throws
 #         NumberFormatException), else dateFormat.parse(node.textValue()).getTime() (:187; a
 #         ParseException leaves time 0, :193);
 #   objID: node.toString().replaceAll("\"", "") (:197) -- a string's content, an integer's digits,
 #          true / false / null as text; absent properties / objID -> null.
-# Kinds as gf_geojson_parse: 1 NumberFormatException, 2 outside the restated subset (escaped
-# strings, non-integer objIDs, dates before 1583), 3 malformed / no coordinates, 4 empty line.
+# Kinds as gf_geojson_parse: 1 NumberFormatException / ClassCastException of an ordinate, 2 outside
+# the restated subset (include/geoflink_hip.h: non-Point geometries, FeatureCollection, < 2 or a
+# non-number third ordinate, a number json-simple cannot read back anywhere on the line -- a float
+# overflowing to Infinity or an integer outside long --, nesting > 256, escapes in taken strings or
+# in member names of a looked-up object, non-integer objIDs, dates before 1583), 3 malformed /
+# missing value or geometry, 4 empty line.
 # ---------------------------------------------------------------------------------------------
+_GEO_OTHER = {"LineString", "Polygon", "MultiPoint", "MultiLineString", "MultiPolygon", "GeometryCollection"}
+_GEO_MAX_DEPTH = 256
+
+
 def _jdate(v: str, tz_off_min: int):
     import calendar
     import re
@@ -342,88 +361,232 @@ class _JStr(str):
     escaped = False
 
 
-def _json_decoder():
-    """json's pure-Python decoder with strings tagged by escape use: the device path reports a
-    taken string written with an escape as unsupported (k_csv.hip geo_props), and only that one --
-    an escape elsewhere in the line is parsed like any other string."""
+class _JObj(dict):
+    """A JSON object (last duplicate wins, Jackson ObjectNode) that remembers whether one of its
+    member names was written with an escape."""
+    esc_keys = False
+
+
+def _too_deep(line: bytes) -> bool:
+    """Nesting deeper than _GEO_MAX_DEPTH (brackets outside strings), on any input."""
+    if line.count(b"{") + line.count(b"[") <= _GEO_MAX_DEPTH:
+        return False
+    d, st, i = 0, False, 0
+    while i < len(line):
+        c = line[i]
+        if st:
+            if c == 0x5C:
+                i += 1
+            elif c == 0x22:
+                st = False
+        elif c == 0x22:
+            st = True
+        elif c in (0x7B, 0x5B):
+            d += 1
+            if d > _GEO_MAX_DEPTH:
+                return True
+        elif c in (0x7D, 0x5D):
+            d -= 1
+        i += 1
+    return False
+
+
+def _utf8_structural(line: bytes) -> bool:
+    """Jackson's UTF-8 reader: a lead byte 110xxxxx / 1110xxxx / 11110xxx takes 1 / 2 / 3 bytes
+    10xxxxxx; no overlong / surrogate / range checks."""
+    i, n = 0, len(line)
+    while i < n:
+        c = line[i]
+        if c < 0x80:
+            i += 1
+            continue
+        k = 1 if c & 0xE0 == 0xC0 else 2 if c & 0xF0 == 0xE0 else 3 if c & 0xF8 == 0xF0 else -1
+        if k < 0 or i + k >= n:
+            return False
+        for j in range(1, k + 1):
+            if line[i + j] & 0xC0 != 0x80:
+                return False
+        i += k + 1
+    return True
+
+
+def _json_decoder(escapes: bool, poison: list):
+    """json's decoder, strict, with NaN / Infinity refused (Jackson), numbers json-simple could not
+    read back flagged (poison[0]) and objects as _JObj; with escapes, the pure-Python scanner with
+    strings tagged by escape use (the device reports a taken string or a looked-up object's member
+    name written with an escape as unsupported)."""
     import json
     import json.scanner
 
-    def scan(s, end, strict=True):
-        v, e = json.decoder.py_scanstring(s, end, strict)
-        r = _JStr(v)
-        r.escaped = "\\" in s[end:e]
-        return r, e
+    def pint(t):
+        v = int(t)
+        if not -(1 << 63) <= v < (1 << 63):
+            poison[0] = True
+        return v
 
-    dec = json.JSONDecoder()
-    dec.parse_string = scan
-    dec.scan_once = json.scanner.py_make_scanner(dec)
+    def pfloat(t):
+        v = float(t)
+        if math.isinf(v):
+            poison[0] = True
+        return v
+
+    def pconst(t):
+        raise ValueError(f"{t}: not JSON (Jackson's defaults refuse it)")
+
+    def pairs(kv):
+        d = _JObj(kv)
+        d.esc_keys = any(getattr(k, "escaped", False) for k, _ in kv)
+        return d
+
+    dec = json.JSONDecoder(parse_int=pint, parse_float=pfloat, parse_constant=pconst, object_pairs_hook=pairs)
+    if escapes:
+        dec.parse_string = _tagged_scanstring
+        dec.scan_once = json.scanner.py_make_scanner(dec)
     return dec
 
 
-def _geojson_line(line: bytes, prop_obj, prop_ts, date_fmt, tz_off_min):
-    import json
+def _tagged_scanstring(s, end, strict=True):
+    import json.decoder
 
+    v, e = json.decoder.py_scanstring(s, end, strict)
+    r = _JStr(v)
+    r.escaped = "\\" in s[end:e]
+    return r, e
+
+
+class _Unsupported(Exception):
+    pass
+
+
+def _num(v):
+    return isinstance(v, (int, float)) and not isinstance(v, bool)
+
+
+def _point(c):
+    """GeoJsonReader.createPoint's coordinates -> ("ok", x, y) / ("fail", kind) / ("unsup",)."""
+    if not isinstance(c, list):
+        return ("fail", 3)
+    for i, v in enumerate(c[:3]):
+        if not _num(v):
+            return ("fail", 1) if i < 2 else ("unsup",)
+    if len(c) < 2:
+        return ("unsup",)
+    x, y = float(c[0]), float(c[1])  # an int is Jackson's IntNode / LongNode: (double) of the long
+    return ("ok", x, y)
+
+
+def _gtype(obj, get):
+    t = get(obj, "type")
+    if not isinstance(t, str):
+        return None
+    if getattr(t, "escaped", False):
+        raise _Unsupported()
+    return t
+
+
+def _geojson_line(line: bytes, prop_obj, prop_ts, date_fmt, tz_off_min, value_lines=False):
     if line.endswith(b"\r"):
         line = line[:-1]
     if not line:
         return None, 4
+    if _too_deep(line):
+        return None, 2
+    if not _utf8_structural(line):
+        return None, 3
+    poison = [False]
     try:
-        # escapes tagged per string only where there are any (the C scanner is much faster)
-        d = _json_decoder().decode(line.decode("utf-8")) if b"\\" in line else json.loads(line)
+        text = line.decode("utf-8", "surrogateescape")
+        if b"\\" in line:  # member names go through json.decoder's module-level scanstring: tag them too
+            import json.decoder as jd
+
+            saved = jd.scanstring
+            jd.scanstring = _tagged_scanstring
+            try:
+                d = _json_decoder(True, poison).decode(text)
+            finally:
+                jd.scanstring = saved
+        else:
+            d = _json_decoder(False, poison).decode(text)
     except ValueError:
         return None, 3
     if not isinstance(d, dict):
         return None, 3
-    feat = d["value"] if isinstance(d.get("value"), dict) else d
-    geom = feat.get("geometry")
-    if not isinstance(geom, dict) or not isinstance(geom.get("coordinates"), list):
-        return None, 3
-    c = geom["coordinates"]
-    while c and isinstance(c[0], list):
-        c = c[0]
-    if len(c) < 2:
-        return None, 3
-    num = lambda v: isinstance(v, (int, float)) and not isinstance(v, bool)  # noqa: E731
-    if not (num(c[0]) and num(c[1])):
-        return None, 1
-    x, y = float(c[0]), float(c[1])
-    ts, obj = 0, None
-    props = feat.get("properties")
-    if isinstance(props, dict):
-        if prop_ts is not None and prop_ts in props:
-            v = props[prop_ts]
-            if date_fmt == 0:
-                if not (isinstance(v, int) and not isinstance(v, bool)) or not -(1 << 63) <= v < (1 << 63):
-                    return None, 1
-                ts = v
-            else:
-                if not isinstance(v, str):
-                    return None, 1
-                if getattr(v, "escaped", False):  # the string is written with an escape
-                    return None, 2
-                t, k = _jdate(v, tz_off_min)
-                if k:
-                    return None, k
-                ts = t
-        if prop_obj is not None and prop_obj in props:
-            v = props[prop_obj]
-            if isinstance(v, bool):
-                obj = b"true" if v else b"false"
-            elif v is None:
-                obj = b"null"
-            elif isinstance(v, int):
-                obj = str(v).encode()
-            elif isinstance(v, str):
-                if getattr(v, "escaped", False):
-                    return None, 2
-                obj = v.encode("utf-8", "surrogateescape")
-            else:
+    if poison[0]:
+        return None, 2
+
+    def get(obj, name):  # ObjectNode.get on an object the map looks a member up in
+        if obj.esc_keys:
+            raise _Unsupported()
+        return obj.get(name)
+
+    try:
+        V = d if value_lines else get(d, "value")
+        if not isinstance(V, dict):
+            return None, 3
+        xy = None
+        tv = _gtype(V, get)
+        if tv in _GEO_OTHER or tv == "FeatureCollection":
+            return None, 2
+        if tv == "Point":                      # readGeoJSON(value.toString())
+            r = _point(get(V, "coordinates"))
+            if r[0] == "unsup":
                 return None, 2
+            if r[0] == "ok":
+                xy = r[1:]
+        if xy is None:                         # the catch branch: readGeoJSON(value.get("geometry"))
+            G = get(V, "geometry")
+            if not isinstance(G, dict):
+                return None, 3
+            tg = _gtype(G, get)
+            if tg is None or tg not in _GEO_OTHER | {"Point", "Feature", "FeatureCollection"}:
+                return None, 3
+            if tg != "Point":
+                return None, 2
+            r = _point(get(G, "coordinates"))
+            if r[0] != "ok":
+                return None, (2 if r[0] == "unsup" else r[1])
+            xy = r[1:]
+        x, y = xy
+        ts, obj = 0, None
+        props = get(V, "properties")
+        if isinstance(props, dict) and (prop_ts is not None or prop_obj is not None):
+            if props.esc_keys:
+                raise _Unsupported()
+            if prop_ts is not None and prop_ts in props:
+                v = props[prop_ts]
+                if date_fmt == 0:
+                    if not (isinstance(v, int) and not isinstance(v, bool)) or not -(1 << 63) <= v < (1 << 63):
+                        return None, 1
+                    ts = v
+                else:
+                    if not isinstance(v, str):
+                        return None, 1
+                    if getattr(v, "escaped", False):  # the string is written with an escape
+                        return None, 2
+                    t, k = _jdate(v, tz_off_min)
+                    if k:
+                        return None, k
+                    ts = t
+            if prop_obj is not None and prop_obj in props:
+                v = props[prop_obj]
+                if isinstance(v, bool):
+                    obj = b"true" if v else b"false"
+                elif v is None:
+                    obj = b"null"
+                elif isinstance(v, int):
+                    obj = str(v).encode()
+                elif isinstance(v, str):
+                    if getattr(v, "escaped", False):
+                        return None, 2
+                    obj = v.encode("utf-8", "surrogateescape")
+                else:
+                    return None, 2
+    except _Unsupported:
+        return None, 2
     return (x, y, ts, obj), 0
 
 
-def geojson_parse(text: bytes, prop_obj=None, prop_ts=None, date_fmt=0, tz_off_min=0):
+def geojson_parse(text: bytes, prop_obj=None, prop_ts=None, date_fmt=0, tz_off_min=0, value_lines=False):
     """GeoJSONToTSpatial.map per line -> (x, y, objID Strings as bytes or None, ts, bad_line,
     bad_kind); bad lines contribute zeros."""
     lines = text.split(b"\n")
@@ -433,7 +596,7 @@ def geojson_parse(text: bytes, prop_obj=None, prop_ts=None, date_fmt=0, tz_off_m
     x = np.zeros(n); y = np.zeros(n); t = np.zeros(n, np.int64); o = [None] * n
     bad_line, bad_kind = -1, 0
     for i, ln in enumerate(lines):
-        r, k = _geojson_line(ln, prop_obj, prop_ts, date_fmt, tz_off_min)
+        r, k = _geojson_line(ln, prop_obj, prop_ts, date_fmt, tz_off_min, value_lines)
         if k:
             if bad_line < 0:
                 bad_line, bad_kind = i, k

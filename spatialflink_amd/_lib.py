@@ -17,6 +17,8 @@ GF_OK = 0
 OBJID_NUMERIC_MIN, OBJID_NUMERIC_END = -(1 << 62), 1 << 62
 OBJID_NULL = (1 << 63) - 1  # GeoJSON feature without the objID property
 GF_MERGE_SHARD_MAJOR, GF_MERGE_WINDOW_MAJOR = 0, 1
+GF_MERGE_FOREIGN_KEYS = 0x100      # records from other ranks' contexts: dictionary objID keys refused
+KNN_STATUS_FOREIGN_KEYS = 2        # merged record status: a window held dictionary keys of another rank
 GF_ERR_ARG = -1
 GF_ERR_CAPACITY = -2
 GF_ERR_HIP = -3

@@ -1700,12 +1700,14 @@ extern "C" int gf_knn_merge_dev(gf_ctx* ctx, int32_t k, const void* records, int
   int st = bind(ctx);
   if (st) return st;
   const size_t rb = gf_knn_result_bytes(k);
-  GF_HIP_CHECK(ctx, launch_knn_merge(ctx, k, records, nrec, rb, 1, 0, result, 0));
+  GF_HIP_CHECK(ctx, launch_knn_merge(ctx, k, records, nrec, rb, 1, 0, result, 0, 0));
   return GF_OK;
 }
 
 extern "C" int gf_knn_merge_dev_batch(gf_ctx* ctx, int32_t k, const void* records, int32_t nrec, int32_t nwin,
                                       int32_t layout, void* results) {
+  const int foreign = (layout & GF_MERGE_FOREIGN_KEYS) != 0;
+  layout &= ~GF_MERGE_FOREIGN_KEYS;
   if (!ctx || k < 1 || k > kMaxK || nrec < 1 || nrec > 64 || nwin < 1 || nwin > 65535 || !records || !results ||
       (layout != GF_MERGE_SHARD_MAJOR && layout != GF_MERGE_WINDOW_MAJOR))
     return set_err(ctx, GF_ERR_ARG, "gf_knn_merge_dev_batch: bad argument");
@@ -1715,7 +1717,7 @@ extern "C" int gf_knn_merge_dev_batch(gf_ctx* ctx, int32_t k, const void* record
   // shard-major = all_gather of each rank's [nwin] records: record (shard s, window w) at (s*nwin + w)*rb
   const size_t rec_stride = layout == GF_MERGE_SHARD_MAJOR ? (size_t)nwin * rb : rb;
   const size_t win_stride = layout == GF_MERGE_SHARD_MAJOR ? rb : (size_t)nrec * rb;
-  GF_HIP_CHECK(ctx, launch_knn_merge(ctx, k, records, nrec, rec_stride, nwin, win_stride, results, rb));
+  GF_HIP_CHECK(ctx, launch_knn_merge(ctx, k, records, nrec, rec_stride, nwin, win_stride, results, rb, foreign));
   return GF_OK;
 }
 

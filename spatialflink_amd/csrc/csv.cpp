@@ -134,7 +134,7 @@ extern "C" int gf_geojson_parse(gf_ctx* ctx, gf_objid_dict* dict, const char* te
                                 int64_t* ts, int32_t* cx, int32_t* cy, int64_t cap, int64_t* n_out, int64_t* bad_line,
                                 int32_t* bad_kind) {
   if (!ctx) return GF_ERR_ARG;
-  if (!sc || (sc->date_format != 0 && sc->date_format != 1))
+  if (!sc || (sc->date_format != 0 && sc->date_format != 1) || (sc->value_lines != 0 && sc->value_lines != 1))
     return set_err(ctx, GF_ERR_ARG, "gf_geojson_parse: bad schema");
   CsvArgs a{};
   a.format = 1;
@@ -149,6 +149,7 @@ extern "C" int gf_geojson_parse(gf_ctx* ctx, gf_objid_dict* dict, const char* te
   }
   a.date_fmt = sc->date_format;
   a.geo_fast = !ctx->geojson_walk;
+  a.value_lines = sc->value_lines;
   a.tz_off_ms = (int64_t)sc->tz_offset_minutes * 60000;
   return parse_text_lines(ctx, dict, text, len, a, g, x, y, objID, ts, cx, cy, cap, n_out, bad_line, bad_kind);
 }

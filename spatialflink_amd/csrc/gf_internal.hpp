@@ -8,6 +8,7 @@
 #include <vector>
 
 #include "../../include/geoflink_hip.h"
+#include "gf_text.hpp"
 #include "gf_numerics.hpp"
 
 // ---------------------------------------------------------------------------------------
@@ -322,8 +323,6 @@ hipError_t launch_expand_bitmap_async(hipStream_t s, const uint64_t* bitmap, int
                                       int64_t cap, int64_t* count, const ExpandState& st);
 
 // objID dictionary (k_objid.hip, objid.cpp)
-constexpr int kDictLenBits = 20;  // slot meta = arena offset << 20 | String length
-constexpr uint64_t kDictLenMask = (1ull << kDictLenBits) - 1;
 struct DictSlot {                 // 32 B
   unsigned long long tag;         // 0 = empty, else hash | 1
   unsigned long long meta;        // arena offset << kDictLenBits | length
@@ -369,13 +368,11 @@ int ctx_dict(gf_ctx* ctx, gf_objid_dict** out);  // the context's default dictio
 constexpr int64_t kCsvSeg = 64 * 1024;  // text bytes per count / index block
 constexpr int kCsvLds = 24 * 1024;      // parse: least LDS staging per block (256 lines staged when they fit)
 constexpr int kCsvLdsMax = 64 * 1024;   // parse: most (sized from the mean line length, launch_csv_parse)
-enum { kCsvOk = 0, kCsvNumberFormat = 1, kCsvUnsupported = 2, kCsvMissingField = 3, kCsvEmptyLine = 4 };
 struct CsvErr {
   unsigned long long line;  // first bad line (~0 = none)
   int kind;
   int pad;
 };
-constexpr int kGeoPropMax = 64;  // longest GeoJSON property name taken
 struct CsvArgs {
   const char* text;
   int64_t len;
@@ -406,6 +403,7 @@ struct CsvArgs {
   char prop_ts[kGeoPropMax];
   int32_t lds_cap;               // set by launch_csv_parse: the block's dynamic LDS staging bytes
   int32_t geo_fast;              // GeoJSON: 1 = one-pass member location first (k_csv.hip geo_locate)
+  int32_t value_lines;           // GeoJSON: 1 = each line is the record's value (else the record)
 };
 hipError_t launch_csv_count(hipStream_t st, const char* text, int64_t len, int64_t nseg, uint32_t* counts);
 hipError_t launch_csv_index(hipStream_t st, const char* text, int64_t len, int64_t nseg, const uint32_t* seg_off,
@@ -445,7 +443,7 @@ int knn_exact_record(gf_knn_plan* P, const gf_points* pts, void* result);
 hipError_t launch_knn_poly_sample(gf_ctx* ctx, const KnnPolyArgs& a);
 hipError_t launch_knn_poly_scan(gf_ctx* ctx, const KnnPolyArgs& a, int blocks);  // prefilter + refine
 hipError_t launch_knn_merge(gf_ctx* ctx, int32_t k, const void* records, int32_t nrec, size_t rec_stride,
-                            int32_t nwin, size_t win_stride, void* result, size_t res_stride);
+                            int32_t nwin, size_t win_stride, void* result, size_t res_stride, int foreign);
 // records of one merge given as a pointer list (kernel argument; the panes of a sliding window)
 constexpr int kMaxMergeRecs = 64;
 struct KnnRecList {

@@ -9,7 +9,7 @@
 //               the objID String as its key (canonical decimals directly, the rest queued for
 //               the dictionary, k_objid.hip), Long.valueOf(time), Double.valueOf(x, y) correctly
 //               rounded on the device (gf_decimal.hpp), cell (cx, cy), SoA stores.
-#include "gf_decimal.hpp"
+#include "gf_geojson.hpp"
 #include "gf_internal.hpp"
 
 namespace gf {
@@ -92,21 +92,11 @@ __global__ __launch_bounds__(kBlock) void csv_index_kernel(const char* __restric
   }
 }
 
-struct GBytes {
-  const char* p;
-  __device__ char operator()(int64_t i) const { return p[i]; }
-};
 
 __device__ __forceinline__ bool java_s(char c) {  // regex \s: [ \t\n\x0B\f\r]
   return c == ' ' || c == '\t' || c == '\n' || c == '\x0B' || c == '\f' || c == '\r';
 }
 
-// the bytes of a block's lines staged in LDS: text position i lives at p[i - base]
-struct LBytes {
-  const char* p;
-  int64_t base;
-  __device__ char operator()(int64_t i) const { return p[i - base]; }
-};
 
 // Field ranges of the wanted columns of line [b, e).  Returns the number of fields.
 template <class Src>
@@ -162,12 +152,6 @@ __device__ int split_line(const Src& s, int64_t b, int64_t e, char d, const int3
 // their key here, the rest is queued for the dictionary), time = Long.valueOf(get(time)),
 // x = Double.valueOf(get(x)), y = Double.valueOf(get(y)); the first missing field
 // (IndexOutOfBounds) or malformed number (NumberFormatException) is the line's error.
-struct LineOut {
-  int64_t obj, ts;
-  double x, y;
-  bool dict;        // objID is not a canonical decimal: f_obj goes to the dictionary
-  Field f_obj;
-};
 template <class Src>
 __device__ __forceinline__ int eval_csv_line(const CsvArgs& a, const Src& s, int64_t j, LineOut* o) {
   const int64_t b = j == 0 ? 0 : a.nl[j - 1] + 1;
@@ -190,502 +174,18 @@ __device__ __forceinline__ int eval_csv_line(const CsvArgs& a, const Src& s, int
   return kCsvOk;
 }
 
-// ---------------------------------------------------------------------------------------
-// GeoJSON lines (Deserialization.GeoJSONToTSpatial.map, Deserialization.java:149-211): a small
-// JSON scanner over the line's bytes -- member lookup (last duplicate wins, as Jackson's
-// ObjectNode), value skipping, and the three values the map reads: the geometry's first
-// coordinate, the time property, the objID property.
-// ---------------------------------------------------------------------------------------
-__device__ __forceinline__ bool jws(char c) { return c == ' ' || c == '\t' || c == '\n' || c == '\r'; }
-template <class Src>
-__device__ __forceinline__ int64_t jskip(const Src& s, int64_t p, int64_t e) {
-  while (p < e && jws(s(p))) ++p;
-  return p;
-}
-// the string at p (s(p) == '"'): index past its closing quote, -1 if unterminated
-template <class Src>
-__device__ int64_t jstr_end(const Src& s, int64_t p, int64_t e, bool* esc) {
-  for (++p; p < e; ++p) {
-    const char c = s(p);
-    if (c == '\\') {
-      *esc = true;
-      ++p;
-    } else if (c == '"') {
-      return p + 1;
-    }
-  }
-  return -1;
-}
-// end of the value at p (p at its first byte), -1 if malformed
-template <class Src>
-__device__ int64_t jval_end(const Src& s, int64_t p, int64_t e) {
-  char c = s(p);
-  if (c == '"') {
-    bool esc = false;
-    return jstr_end(s, p, e, &esc);
-  }
-  if (c == '{' || c == '[') {
-    int depth = 0;
-    while (p < e) {
-      c = s(p);
-      if (c == '"') {
-        bool esc = false;
-        p = jstr_end(s, p, e, &esc);
-        if (p < 0) return -1;
-        continue;
-      }
-      if (c == '{' || c == '[') ++depth;
-      else if ((c == '}' || c == ']') && --depth == 0) return p + 1;
-      ++p;
-    }
-    return -1;
-  }
-  int64_t q = p;
-  while (q < e && !(s(q) == ',' || s(q) == '}' || s(q) == ']' || jws(s(q)))) ++q;
-  return q > p ? q : -1;
-}
-// the value of the LAST member `key` of the object at p (s(p) == '{'): its first byte, -1 when
-// absent, -2 when the object is malformed
-template <class Src>
-__device__ int64_t jfind(const Src& s, int64_t p, int64_t e, const char* key, int klen) {
-  int64_t found = -1;
-  p = jskip(s, p + 1, e);
-  if (p < e && s(p) == '}') return -1;
-  while (p < e) {
-    if (s(p) != '"') return -2;
-    bool esc = false;
-    const int64_t ke = jstr_end(s, p, e, &esc);
-    if (ke < 0) return -2;
-    bool match = !esc && ke - p - 2 == klen;
-    for (int i = 0; match && i < klen; ++i) match = s(p + 1 + i) == key[i];
-    p = jskip(s, ke, e);
-    if (p >= e || s(p) != ':') return -2;
-    p = jskip(s, p + 1, e);
-    if (p >= e) return -2;
-    const int64_t ve = jval_end(s, p, e);
-    if (ve < 0) return -2;
-    if (match) found = p;
-    p = jskip(s, ve, e);
-    if (p >= e) return -2;
-    if (s(p) == ',') {
-      p = jskip(s, p + 1, e);
-      continue;
-    }
-    return s(p) == '}' ? found : -2;
-  }
-  return -2;
-}
-// JSON number token [p, q): -?(0|[1-9][0-9]*)(.[0-9]+)?([eE][+-]?[0-9]+)?; *integral = no frac/exp
-template <class Src>
-__device__ bool jnumber(const Src& s, int64_t p, int64_t q, bool* integral) {
-  int64_t i = p;
-  if (i < q && s(i) == '-') ++i;
-  if (i >= q) return false;
-  if (s(i) == '0') ++i;
-  else if (s(i) >= '1' && s(i) <= '9') while (i < q && s(i) >= '0' && s(i) <= '9') ++i;
-  else return false;
-  *integral = true;
-  if (i < q && s(i) == '.') {
-    *integral = false;
-    const int64_t d = ++i;
-    while (i < q && s(i) >= '0' && s(i) <= '9') ++i;
-    if (i == d) return false;
-  }
-  if (i < q && (s(i) == 'e' || s(i) == 'E')) {
-    *integral = false;
-    ++i;
-    if (i < q && (s(i) == '+' || s(i) == '-')) ++i;
-    const int64_t d = i;
-    while (i < q && s(i) >= '0' && s(i) <= '9') ++i;
-    if (i == d) return false;
-  }
-  return i == q;
-}
-// days since 1970-01-01 of the proleptic Gregorian date (y, m 1..12, day 1)
-__device__ __forceinline__ int64_t days_from_civil(int64_t y, int64_t m) {
-  y -= m <= 2;
-  const int64_t era = (y >= 0 ? y : y - 399) / 400;
-  const int64_t yoe = y - era * 400;
-  const int64_t doy = (153 * (m + (m > 2 ? -3 : 9)) + 2) / 5;
-  return era * 146097 + yoe * 365 + yoe / 4 - yoe / 100 + doy - 719468;
-}
-// SimpleDateFormat("yyyy-MM-dd HH:mm:ss").parse (lenient: fields roll over) of the string content
-// [p, q): 0 = parsed, 1 = ParseException (time stays 0), 2 = unsupported (before 1583)
-template <class Src>
-__device__ int jdate(const Src& s, int64_t p, int64_t q, int64_t tz_off_ms, int64_t* ms) {
-  const char sep[5] = {'-', '-', ' ', ':', ':'};
-  int64_t f[6];
-  for (int k = 0; k < 6; ++k) {
-    int nd = 0;
-    int64_t v = 0;
-    while (p < q && s(p) >= '0' && s(p) <= '9' && nd < 10) {
-      v = v * 10 + (s(p) - '0');
-      ++p;
-      ++nd;
-    }
-    if (nd == 0) return 1;
-    if (nd == 10) return 2;  // int overflow territory of the lenient calendar: not restated
-    f[k] = v;
-    if (k < 5) {
-      if (p >= q || s(p) != sep[k]) return 1;
-      ++p;
-    }
-  }
-  const int64_t m0 = f[1] - 1;
-  const int64_t y = f[0] + (m0 >= 0 ? m0 / 12 : (m0 - 11) / 12);
-  const int64_t m = m0 - 12 * (y - f[0]) + 1;
-  const int64_t days = days_from_civil(y, m) + f[2] - 1;
-  const int64_t secs = ((days * 24 + f[3]) * 60 + f[4]) * 60 + f[5];
-  if (secs < -12219292800ll) return 2;  // before 1582-10-15: Java's Julian calendar
-  *ms = secs * 1000 - tz_off_ms;
-  return 0;
-}
-
-// the geometry's first coordinate pair: c at the coordinates array's '['
-template <class Src>
-__device__ __forceinline__ int geo_coords(const Src& s, int64_t c, int64_t e, LineOut* o) {
-  while (c < e && s(c) == '[') c = jskip(s, c + 1, e);  // the first coordinate of any nesting
-  double xy[2];
-  for (int k = 0; k < 2; ++k) {
-    if (c >= e) return kCsvMissingField;
-    const int64_t ce = jval_end(s, c, e);
-    bool integral;
-    if (ce < 0 || !jnumber(s, c, ce, &integral)) return kCsvNumberFormat;
-    const int st = parse_java_double(s, Field{c, ce}, kPow5Dev, &xy[k]);
-    if (st) return st == kNumUnsupported ? kCsvUnsupported : kCsvNumberFormat;
-    c = jskip(s, ce, e);
-    if (k == 0) {
-      if (c >= e || s(c) != ',') return kCsvMissingField;
-      c = jskip(s, c + 1, e);
-    }
-  }
-  o->x = xy[0];
-  o->y = xy[1];
-  o->ts = 0;
-  o->obj = GF_OBJID_NULL;
-  o->dict = false;
-  return kCsvOk;
-}
-
-// what the property lookups need of CsvArgs (passed by value: a reference to the kernel's
-// argument block in an outlined call would copy the whole block to scratch, per lane)
-struct GeoProps {
-  const char* kts;   // property names (the block's LDS copies)
-  const char* kobj;
-  int32_t len_ts, len_obj, date_fmt;
-  int64_t tz_off_ms;
-};
-
-// the time and objID properties: t, q = their values' first bytes (-1 absent, -2 malformed object)
-template <class Src>
-__device__ __forceinline__ int geo_props(const GeoProps& a, const Src& s, int64_t e, int64_t t, int64_t q, LineOut* o) {
-  if (a.len_ts >= 0) {
-    if (t == -2) return kCsvMissingField;
-    if (t >= 0) {
-      const int64_t te = jval_end(s, t, e);
-      if (a.date_fmt == 0) {  // Long.parseLong(String.valueOf(node)): a JSON integer only
-        bool integral;
-        if (!jnumber(s, t, te, &integral) || !integral) return kCsvNumberFormat;
-        if (parse_java_long(s, Field{t, te}, &o->ts)) return kCsvNumberFormat;
-      } else {  // dateFormat.parse(node.textValue()); ParseException -> 0
-        if (s(t) != '"') return kCsvNumberFormat;  // textValue() null: the parse throws
-        bool esc = false;
-        jstr_end(s, t, e, &esc);
-        if (esc) return kCsvUnsupported;
-        int64_t ms = 0;
-        const int st = jdate(s, t + 1, te - 1, a.tz_off_ms, &ms);
-        if (st == 2) return kCsvUnsupported;
-        if (st == 0) o->ts = ms;
-      }
-    }
-  }
-  if (a.len_obj >= 0) {
-    if (q == -2) return kCsvMissingField;
-    if (q >= 0) {  // nodeOId.toString() with every '"' removed
-      const int64_t qe = jval_end(s, q, e);
-      Field f{q, qe};
-      const char c0 = s(q);
-      if (c0 == '"') {
-        bool esc = false;
-        jstr_end(s, q, e, &esc);
-        if (esc) return kCsvUnsupported;
-        f = Field{q + 1, qe - 1};
-      } else if (c0 == '{' || c0 == '[') {
-        return kCsvUnsupported;
-      } else if (c0 == '-' || (c0 >= '0' && c0 <= '9')) {
-        bool integral;
-        if (!jnumber(s, q, qe, &integral)) return kCsvMissingField;
-        if (!integral) return kCsvUnsupported;  // Double.toString rendering: not restated
-        if (qe - q == 2 && c0 == '-' && s(q + 1) == '0') {  // IntNode(0).toString() == "0"
-          o->obj = 0;
-          return kCsvOk;
-        }
-      } else {  // true / false / null print as themselves
-        bool lit = false;
-        const int64_t n = qe - q;
-        if (n == 4) lit = (s(q) == 't' && s(q + 1) == 'r' && s(q + 2) == 'u' && s(q + 3) == 'e') ||
-                          (s(q) == 'n' && s(q + 1) == 'u' && s(q + 2) == 'l' && s(q + 3) == 'l');
-        if (n == 5) lit = s(q) == 'f' && s(q + 1) == 'a' && s(q + 2) == 'l' && s(q + 3) == 's' && s(q + 4) == 'e';
-        if (!lit) return kCsvMissingField;
-      }
-      o->dict = !canonical_objid_key(s, f, &o->obj);
-      o->f_obj = f;
-      if (o->dict && f.e - f.b > (int64_t)kDictLenMask) return kCsvUnsupported;
-    }
-  }
-  return kCsvOk;
-}
-
-// Member-by-member walk (jfind per looked-up member): exact on any line, malformed ones included.
-// p: the line's first non-blank byte, a '{'.
-template <class Src>
-__device__ __noinline__ int eval_geojson_walk(GeoProps a, Src s, int64_t p, int64_t e, LineOut* o) {
-  // the feature: the record's "value" object, or the line's object itself
-  int64_t feat = p;
-  const int64_t v = jfind(s, p, e, "value", 5);
-  if (v == -2) return kCsvMissingField;
-  if (v >= 0 && s(v) == '{') feat = v;
-  const int64_t g = jfind(s, feat, e, "geometry", 8);
-  if (g < 0 || s(g) != '{') return kCsvMissingField;
-  const int64_t c = jfind(s, g, e, "coordinates", 11);
-  if (c < 0 || s(c) != '[') return kCsvMissingField;
-  int st = geo_coords(s, c, e, o);
-  if (st) return st;
-  const int64_t pr = jfind(s, feat, e, "properties", 10);
-  if (pr == -2) return kCsvMissingField;
-  if (pr < 0 || s(pr) != '{') return kCsvOk;
-  const int64_t t = a.len_ts >= 0 ? jfind(s, pr, e, a.kts, a.len_ts) : -1;
-  const int64_t q = a.len_obj >= 0 ? jfind(s, pr, e, a.kobj, a.len_obj) : -1;
-  return geo_props(a, s, e, t, q, o);
-}
-
-// ---------------------------------------------------------------------------------------
-// One-pass member location (the common case).  The walk above re-scans the feature once per
-// member it looks up, with nested data-dependent loops per lane: with 64 lines per wave in
-// different places of that loop nest the exec-mask bookkeeping dominated (~2.7 k scalar
-// instructions per line).  Here each lane runs one automaton over its line, byte by byte: a
-// strict JSON syntax check plus a small stack of container roles (the top object, the record's
-// "value" object, the geometry and properties objects under either), noting the position of
-// the LAST key of each member the walk would look up.  On a line that passes the check --
-// strictly valid JSON, no backslash, nesting <= 63 -- every jfind of the walk returns exactly
-// that last member's value (the walk's looser scanning agrees with JSON on valid input), so the
-// results are the walk's.  Any other line (malformed, escapes, deeper nesting) takes the walk.
-//
-// The per-byte step: one 8-B LDS entry per byte value holds the (next state, action) pair of
-// all 9 states (7 bits each), so the lookup does not wait on the state and the state update is
-// a shift; only the actions (brackets, commas, key quotes) do more, and the key comparison runs
-// only for keys of a looked-up length in a looked-up container.  (A select-only form of the
-// actions measured slower: 1.82 vs 1.67 ms for the locator over 1M lines.)  Stale
-// notes need no reset: a note is current when it lies after the note of its container's key
-// (e.g. the coordinates key after the last geometry key).
-// ---------------------------------------------------------------------------------------
-enum : uint8_t { JS_VAL, JS_ARR0, JS_OBJ0, JS_KEY, JS_COLON, JS_AFT, JS_VSTR, JS_KSTR, JS_TOK, JS_N, JS_ERR = 9 };
-enum : uint8_t { JC_WS, JC_LBRACE, JC_RBRACE, JC_LBRACK, JC_RBRACK, JC_QUOTE, JC_COMMA, JC_COLON, JC_BSL, JC_TOK, JC_OTHER };
-enum : uint8_t { JA_NONE, JA_PUSH_OBJ, JA_PUSH_ARR, JA_POP_OBJ, JA_POP_ARR, JA_COMMA, JA_KEY_BEGIN, JA_KEY_END };
-enum : int { JR_NONE, JR_TOP, JR_VAL, JR_GEO_T, JR_PROP_T, JR_GEO_V, JR_PROP_V };  // container roles
-enum : int { JK_NONE, JK_VALUE, JK_GEO, JK_PROP };                                 // member kinds
-constexpr int kGeoKeys = 6;  // value, geometry, properties, coordinates, time property, objID property
-
-__device__ __forceinline__ uint8_t jclass(int c) {
-  switch (c) {
-    case ' ': case '\t': case '\n': case '\r': return JC_WS;
-    case '{': return JC_LBRACE;
-    case '}': return JC_RBRACE;
-    case '[': return JC_LBRACK;
-    case ']': return JC_RBRACK;
-    case '"': return JC_QUOTE;
-    case ',': return JC_COMMA;
-    case ':': return JC_COLON;
-    case '\\': return JC_BSL;
-    default: break;
-  }
-  if ((c >= '0' && c <= '9') || (c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z') || c == '+' || c == '-' || c == '.')
-    return JC_TOK;
-  return JC_OTHER;
-}
-// next state | action << 4.  After the top object closes the state is JS_AFT at depth 0, where
-// a comma or a closer is an error (checked with the depth, geo_locate).
-__device__ __forceinline__ uint8_t jtrans(int st, int cl) {
-  auto E = [](int n, int act) { return (uint8_t)(n | act << 4); };
-  if (st == JS_VSTR) return cl == JC_QUOTE ? E(JS_AFT, 0) : cl == JC_BSL ? E(JS_ERR, 0) : E(JS_VSTR, 0);
-  if (st == JS_KSTR) return cl == JC_QUOTE ? E(JS_COLON, JA_KEY_END) : cl == JC_BSL ? E(JS_ERR, 0) : E(JS_KSTR, 0);
-  if (st == JS_TOK) {
-    if (cl == JC_TOK) return E(JS_TOK, 0);
-    st = JS_AFT;  // the token ends here: the byte is read as after a value
-  }
-  if (cl == JC_WS) return E(st, 0);
-  switch (st) {
-    case JS_VAL: case JS_ARR0:
-      if (cl == JC_LBRACE) return E(JS_OBJ0, JA_PUSH_OBJ);
-      if (cl == JC_LBRACK) return E(JS_ARR0, JA_PUSH_ARR);
-      if (cl == JC_QUOTE) return E(JS_VSTR, 0);
-      if (cl == JC_TOK) return E(JS_TOK, 0);
-      if (st == JS_ARR0 && cl == JC_RBRACK) return E(JS_AFT, JA_POP_ARR);
-      return E(JS_ERR, 0);
-    case JS_OBJ0:
-      if (cl == JC_QUOTE) return E(JS_KSTR, JA_KEY_BEGIN);
-      if (cl == JC_RBRACE) return E(JS_AFT, JA_POP_OBJ);
-      return E(JS_ERR, 0);
-    case JS_KEY: return cl == JC_QUOTE ? E(JS_KSTR, JA_KEY_BEGIN) : E(JS_ERR, 0);
-    case JS_COLON: return cl == JC_COLON ? E(JS_VAL, 0) : E(JS_ERR, 0);
-    case JS_AFT:
-      if (cl == JC_COMMA) return E(JS_VAL, JA_COMMA);
-      if (cl == JC_RBRACE) return E(JS_AFT, JA_POP_OBJ);
-      if (cl == JC_RBRACK) return E(JS_AFT, JA_POP_ARR);
-      return E(JS_ERR, 0);
-    default: return E(JS_ERR, 0);
-  }
-}
-
-// LDS tables of a block: per byte value the 9 states' entries; the looked-up member names
-struct GeoTabs {
-  const uint64_t* tab;  // [256]: entry of state s at bits 7s..7s+6
-  const char* keys;     // kGeoKeys x kGeoPropMax
-  int32_t klen[kGeoKeys];
-};
-
-__device__ void geo_tabs_fill(const CsvArgs& a, uint64_t* tab, char* keys) {
-  for (int b = threadIdx.x; b < 256; b += blockDim.x) {
-    const int cl = jclass(b);
-    uint64_t t = 0;
-    for (int st = 0; st < JS_N; ++st) t |= (uint64_t)jtrans(st, cl) << (7 * st);
-    tab[b] = t;
-  }
+__device__ void geo_tabs_fill(const CsvArgs& a, uint64_t* tab, uint64_t* ttab, char* keys) {
+  for (int b = threadIdx.x; b < 256; b += blockDim.x) geo_tab_entry(b, tab + b, ttab + b);
   for (int i = threadIdx.x; i < kGeoKeys * kGeoPropMax; i += blockDim.x) {
     const int k = i / kGeoPropMax, c = i % kGeoPropMax;
-    const char* names[4] = {"value", "geometry", "properties", "coordinates"};
+    const char* names[5] = {"value", "geometry", "properties", "coordinates", "type"};
+    const int nl[5] = {5, 8, 10, 11, 4};
+    const int nk = k < 4 ? k : 4;
     char ch = 0;
-    if (k < 4) {
-      const int n = k == 0 ? 5 : k == 1 ? 8 : k == 2 ? 10 : 11;
-      ch = c < n ? names[k][c] : 0;
-    } else {
-      ch = k == 4 ? a.prop_ts[c] : a.prop_obj[c];
-    }
+    if (k == 4 || k == 5) ch = k == 4 ? a.prop_ts[c] : a.prop_obj[c];
+    else ch = c < nl[nk] ? names[nk][c] : 0;
     keys[i] = ch;
   }
-}
-
-template <class Src>
-__device__ __forceinline__ bool jkey_eq(const Src& s, int64_t ks, int len, const GeoTabs& gt, int k) {
-  if (gt.klen[k] != len) return false;
-  bool eq = true;
-  for (int i = 0; eq && i < len; ++i) eq = s(ks + i) == gt.keys[k * kGeoPropMax + i];
-  return eq;
-}
-
-// the value of the member whose key's closing quote is at k (valid JSON: '"' ws ':' ws value)
-template <class Src>
-__device__ __forceinline__ int64_t jmember_value(const Src& s, int64_t k, int64_t e) {
-  return jskip(s, jskip(s, k + 1, e) + 1, e);
-}
-
-// The automaton over the line [p, e) (s(p) == '{'), staged in LDS (lds + (pos - base)).  Returns
-// false when the line must take the walk; otherwise the feature's member values g, c
-// (coordinates), pr, t, q: first byte, -1 when absent.
-__device__ __forceinline__ bool geo_locate(const LBytes& s, int64_t p, int64_t e, const GeoTabs& gt, int64_t* loc) {
-  if (e - p >= INT32_MAX) return false;
-  int st = JS_VAL, depth = 0, pend = JK_NONE;
-  bool bad = false;
-  uint64_t kinds = 0;  // bit d: the container at depth d is an object
-  uint32_t roles = 0;  // 4 bits per depth 1..7
-  int32_t ks = 0;
-  // closing-quote positions (from p) of the last keys noted: the record's "value"; per feature
-  // (top object T / value object V) geometry, properties, coordinates, time, objID
-  int32_t v = -1, gT = -1, prT = -1, cT = -1, tT = -1, qT = -1, gV = -1, prV = -1, cV = -1, tV = -1, qV = -1;
-  // length filters of the keys looked up per container group (lengths < 64)
-  const uint64_t lf_top = (1ull << 5) | (1ull << 8) | (1ull << 10), lf_geo = 1ull << 11;
-  const uint64_t lf_prop = (gt.klen[4] >= 0 ? 1ull << gt.klen[4] : 0) | (gt.klen[5] >= 0 ? 1ull << gt.klen[5] : 0);
-  const int32_t o0 = (int32_t)(p - s.base), o1 = (int32_t)(e - s.base);  // the line's LDS offsets
-  for (int32_t w = o0 & ~3; w < o1 && !bad; w += 4) {
-    const uint32_t word = *reinterpret_cast<const uint32_t*>(s.p + w);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int32_t i = w + k - o0;  // offset in the line
-      const uint32_t byte = i < 0 || w + k >= o1 ? (uint32_t)' ' : (word >> (8 * k)) & 0xFFu;
-      const uint32_t ent = (uint32_t)(gt.tab[byte] >> (7 * st)) & 0x7Fu;
-      int nst = (int)(ent & 15u);
-      const int act = (int)(ent >> 4);
-      if (act) {
-        const int role = (unsigned)depth <= 7u ? (int)(roles >> (4 * depth)) & 15 : JR_NONE;
-        if (act == JA_PUSH_OBJ || act == JA_PUSH_ARR) {
-          int child = depth == 0 ? JR_TOP
-                    : role == JR_TOP ? (int)(0x4320u >> (4 * pend)) & 15   // value, geometry, properties
-                    : role == JR_VAL ? (int)(0x6500u >> (4 * pend)) & 15   // geometry, properties
-                    : JR_NONE;
-          if (act == JA_PUSH_ARR) child = JR_NONE;
-          ++depth;
-          bad |= depth > 63;
-          kinds = (kinds & ~(1ull << (depth & 63))) | ((uint64_t)(act == JA_PUSH_OBJ) << (depth & 63));
-          if ((unsigned)depth <= 7u) roles = (roles & ~(15u << (4 * depth))) | ((uint32_t)child << (4 * depth));
-        } else if (act == JA_POP_OBJ || act == JA_POP_ARR) {
-          bad |= depth <= 0 || (int)((kinds >> (depth & 63)) & 1) != (act == JA_POP_OBJ);
-          --depth;
-        } else if (act == JA_COMMA) {
-          bad |= depth <= 0;
-          nst = (kinds >> (depth & 63)) & 1 ? JS_KEY : JS_VAL;
-        } else if (act == JA_KEY_BEGIN) {
-          ks = i + 1;
-        } else {  // JA_KEY_END: note a looked-up member of a looked-up container
-          const int len = i - ks;
-          const uint64_t lf = role == JR_TOP || role == JR_VAL ? lf_top
-                            : role == JR_GEO_T || role == JR_GEO_V ? lf_geo
-                            : role == JR_PROP_T || role == JR_PROP_V ? lf_prop : 0;
-          pend = JK_NONE;
-          if (len < 64 && ((lf >> len) & 1)) {
-            const int64_t kp = p + ks;
-            if (role == JR_TOP || role == JR_VAL) {
-              if (role == JR_TOP && jkey_eq(s, kp, len, gt, 0)) {
-                pend = JK_VALUE;
-                v = i;
-              } else if (jkey_eq(s, kp, len, gt, 1)) {
-                pend = JK_GEO;
-                if (role == JR_TOP) gT = i; else gV = i;
-              } else if (jkey_eq(s, kp, len, gt, 2)) {
-                pend = JK_PROP;
-                if (role == JR_TOP) prT = i; else prV = i;
-              }
-            } else if (role == JR_GEO_T || role == JR_GEO_V) {
-              if (jkey_eq(s, kp, len, gt, 3)) {
-                if (role == JR_GEO_T) cT = i; else cV = i;
-              }
-            } else {
-              if (jkey_eq(s, kp, len, gt, 4)) {
-                if (role == JR_PROP_T) tT = i; else tV = i;
-              }
-              if (jkey_eq(s, kp, len, gt, 5)) {
-                if (role == JR_PROP_T) qT = i; else qV = i;
-              }
-            }
-          }
-        }
-      }
-      bad |= nst == JS_ERR;
-      st = nst == JS_ERR ? JS_AFT : nst;
-    }
-  }
-  if (bad || st != JS_AFT || depth != 0) return false;
-  auto val = [&](int32_t k) { return k < 0 ? (int64_t)-1 : jmember_value(s, p + k, e); };
-  const int64_t vv = val(v);
-  int32_t g, c, pr, t, q;
-  if (vv >= 0 && s(vv) == '{') {  // notes inside an earlier "value" object or member are stale
-    g = gV > v ? gV : -1;
-    pr = prV > v ? prV : -1;
-    c = g >= 0 && cV > g ? cV : -1;
-    t = pr >= 0 && tV > pr ? tV : -1;
-    q = pr >= 0 && qV > pr ? qV : -1;
-  } else {
-    g = gT;
-    pr = prT;
-    c = g >= 0 && cT > g ? cT : -1;
-    t = pr >= 0 && tT > pr ? tT : -1;
-    q = pr >= 0 && qT > pr ? qT : -1;
-  }
-  loc[0] = val(g);
-  loc[1] = val(c);
-  loc[2] = val(pr);
-  loc[3] = val(t);
-  loc[4] = val(q);
-  return true;
 }
 
 // FAST: try the one-pass locator first (the LDS-staged path); otherwise the walk
@@ -696,19 +196,11 @@ __device__ __forceinline__ int eval_geojson_line(const CsvArgs& a, const Src& s,
   if (e > b && s(e - 1) == '\r') --e;
   if (e <= b) return kCsvEmptyLine;
   const int64_t p = jskip(s, b, e);
-  if (p >= e || s(p) != '{') return kCsvMissingField;
-  const GeoProps gp{gt.keys + 4 * kGeoPropMax, gt.keys + 5 * kGeoPropMax, a.len_ts, a.len_obj, a.date_fmt, a.tz_off_ms};
-  int64_t loc[5];
-  bool located = false;
-  if constexpr (FAST) located = geo_locate(s, p, e, gt, loc);
-  if (!located) return eval_geojson_walk(gp, s, p, e, o);
-  const int64_t g = loc[0], c = loc[1], pr = loc[2];
-  if (g < 0 || s(g) != '{') return kCsvMissingField;
-  if (c < 0 || s(c) != '[') return kCsvMissingField;
-  const int st = geo_coords(s, c, e, o);
-  if (st) return st;
-  if (pr < 0 || s(pr) != '{') return kCsvOk;
-  return geo_props(gp, s, e, a.len_ts >= 0 ? loc[3] : -1, a.len_obj >= 0 ? loc[4] : -1, o);
+  if (p >= e || s(p) != '{') return kCsvMissingField;  // not an object: malformed record
+  const GeoProps gp{gt.keys + 4 * kGeoPropMax, gt.keys + 5 * kGeoPropMax, a.len_ts, a.len_obj, a.date_fmt, a.tz_off_ms,
+                    kPow5Dev};
+  if constexpr (FAST) return geojson_line(gt, gp, s, p, e, a.value_lines, true, o);
+  else return geojson_line(gt, gp, s, p, e, a.value_lines, o);
 }
 
 // parse + store line j; returns true when its objID needs the dictionary (*w filled)
@@ -752,11 +244,11 @@ __global__ __launch_bounds__(kBlock) void csv_parse_kernel(CsvArgs a) {
   const int64_t j = L0 + threadIdx.x;
   DictWork w{0, 0, 0};
   bool need = false;
-  __shared__ uint64_t gtab[FMT == 1 ? 256 : 1];
+  __shared__ uint64_t gtab[FMT == 1 ? 256 : 1], gttab[FMT == 1 ? 256 : 1];
   __shared__ char gkeys[FMT == 1 ? kGeoKeys * kGeoPropMax : 1];
-  const GeoTabs gt{gtab, gkeys, {5, 8, 10, 11, a.len_ts, a.len_obj}};
+  const GeoTabs gt{gtab, gttab, gkeys, {5, 8, 10, 11, a.len_ts, a.len_obj, 4}};
   if (FMT == 1) {
-    geo_tabs_fill(a, gtab, gkeys);
+    geo_tabs_fill(a, gtab, gttab, gkeys);
     __syncthreads();
   }
   if (b1 - a0 <= a.lds_cap) {  // block-uniform
@@ -795,10 +287,10 @@ __global__ __launch_bounds__(kBlock) void csv_parse_kernel(CsvArgs a) {
 __global__ void csv_error_kernel(CsvArgs a) {
   const unsigned long long j = a.err->line;
   if (j == ~0ull) return;  // block-uniform
-  __shared__ uint64_t gtab[256];
+  __shared__ uint64_t gtab[256], gttab[256];
   __shared__ char gkeys[kGeoKeys * kGeoPropMax];
-  const GeoTabs gt{gtab, gkeys, {5, 8, 10, 11, a.len_ts, a.len_obj}};
-  if (a.format == 1) geo_tabs_fill(a, gtab, gkeys);
+  const GeoTabs gt{gtab, gttab, gkeys, {5, 8, 10, 11, a.len_ts, a.len_obj, 4}};
+  if (a.format == 1) geo_tabs_fill(a, gtab, gttab, gkeys);
   __syncthreads();
   if (threadIdx.x != 0) return;
   LineOut o{0, 0, 0.0, 0.0, false, {0, 0}};

@@ -843,11 +843,14 @@ struct ListRecs {
 
 // LDS: SelFull (merge kernels, any k) or SelLite (block 0 of the fused kernel, k <= 128 so the
 // running list plus one whole record fit its 256-key sort area).
+// foreign: the records come from other contexts (an all-gather across ranks), whose dictionary
+// objID keys are ids in their own dictionaries -- a window holding one is refused (status 2).
 template <class LDS, class Src>
-__device__ void knn_merge_body(int32_t k, const Src& src, int32_t nrec, void* result, LDS& L) {
-  __shared__ int s_off[kMaxMergeRecs + 1], s_status;
+__device__ void knn_merge_body(int32_t k, const Src& src, int32_t nrec, void* result, LDS& L, int foreign = 0) {
+  __shared__ int s_off[kMaxMergeRecs + 1], s_status, s_foreign;
   const int tid = threadIdx.x;
   if (tid == 0) {
+    s_foreign = 0;
     int off = 0, st = 0;
     for (int r = 0; r < nrec; ++r) {
       const gf_knn_header* h = (const gf_knn_header*)src(r);
@@ -867,7 +870,9 @@ __device__ void knn_merge_body(int32_t k, const Src& src, int32_t nrec, void* re
       RecView in = rec_view((void*)src(r), k);
       const int n = s_off[r + 1] - s_off[r];
       for (int i = tid; i < n; i += kSelT) {
-        L.sd[cnt + i] = dbits(in.d[i]); L.so[cnt + i] = okey(in.o[i]); L.si[cnt + i] = in.i[i];
+        const int64_t o = in.o[i];
+        L.sd[cnt + i] = dbits(in.d[i]); L.so[cnt + i] = okey(o); L.si[cnt + i] = in.i[i];
+        if (foreign && o < GF_OBJID_NUMERIC_MIN && o != GF_OBJID_NULL) s_foreign = 1;
       }
       cnt += n;
       ++r;
@@ -877,12 +882,15 @@ __device__ void knn_merge_body(int32_t k, const Src& src, int32_t nrec, void* re
     nr = dedupe_topk(L, cnt, k);
   }
   RecView out = rec_view(result, k);
-  for (int i = tid; i < nr; i += kSelT) {
-    out.d[i] = from_bits(L.rd[i]); out.o[i] = from_okey(L.ro[i]); out.i[i] = L.ri[i];
-  }
+  __syncthreads();  // s_foreign complete
+  const int status = s_foreign ? GF_KNN_STATUS_FOREIGN_KEYS : s_status;
+  if (status == 0)
+    for (int i = tid; i < nr; i += kSelT) {
+      out.d[i] = from_bits(L.rd[i]); out.o[i] = from_okey(L.ro[i]); out.i[i] = L.ri[i];
+    }
   if (tid == 0) {
-    out.h->status = s_status;
-    out.h->n = s_status ? 0 : nr;
+    out.h->status = status;
+    out.h->n = status ? 0 : nr;
     out.h->k = k;
     out.h->flags = 0;
     out.h->candidates = s_off[nrec];
@@ -943,10 +951,10 @@ hipError_t launch_knn_fused(gf_ctx* ctx, const KnnScanArgs& a, const KnnSelectAr
 // the merged record goes to result + w*res_stride.
 __global__ __launch_bounds__(kSelT) void knn_merge_kernel(int32_t k, const char* records, int32_t nrec,
                                                           size_t rec_stride, size_t win_stride, void* result_base,
-                                                          size_t res_stride) {
+                                                          size_t res_stride, int foreign) {
   __shared__ SelFull L;
   const StridedRecs src{records + (size_t)blockIdx.x * win_stride, rec_stride};
-  knn_merge_body(k, src, nrec, (char*)result_base + (size_t)blockIdx.x * res_stride, L);
+  knn_merge_body(k, src, nrec, (char*)result_base + (size_t)blockIdx.x * res_stride, L, foreign);
 }
 
 __global__ __launch_bounds__(kSelT) void knn_merge_list_kernel(int32_t k, KnnRecList list, int32_t nrec,
@@ -957,10 +965,10 @@ __global__ __launch_bounds__(kSelT) void knn_merge_list_kernel(int32_t k, KnnRec
 }
 
 hipError_t launch_knn_merge(gf_ctx* ctx, int32_t k, const void* records, int32_t nrec, size_t rec_stride,
-                            int32_t nwin, size_t win_stride, void* result, size_t res_stride) {
+                            int32_t nwin, size_t win_stride, void* result, size_t res_stride, int foreign) {
   KTimer t(ctx, GF_K_KNN_MERGE);
   hipLaunchKernelGGL(knn_merge_kernel, dim3(nwin), dim3(kSelT), 0, ctx->stream, k, (const char*)records, nrec,
-                     rec_stride, win_stride, result, res_stride);
+                     rec_stride, win_stride, result, res_stride, foreign);
   return hipGetLastError();
 }
 

@@ -153,8 +153,10 @@ def allgather_knn_records(record, k: int, merged_out, group=None):
     _all_gather_bytes(gathered, record, group)
     ctx = _lib.context(record.device.index)
     out = merged_out if isinstance(merged_out, int) else merged_out.data_ptr()
-    _lib.check(_lib.lib().gf_knn_merge_dev(ctx.handle, int(k), gathered.data_ptr(), world, out),
-               ctx.handle, "gf_knn_merge_dev")
+    # the records come from every rank's context: dictionary objID keys are refused (status 2)
+    _lib.check(_lib.lib().gf_knn_merge_dev_batch(ctx.handle, int(k), gathered.data_ptr(), world, 1,
+                                                 _lib.GF_MERGE_SHARD_MAJOR | _lib.GF_MERGE_FOREIGN_KEYS, out),
+               ctx.handle, "gf_knn_merge_dev_batch")
     return merged_out
 
 
@@ -188,7 +190,19 @@ def allgather_knn_records_batch(records, k: int, results, group=None):
     (gf_knn_merge_dev_batch, shard-major) into `results` -- nwin consecutive records (device
     tensor or an int address from PinnedRecords.ptr()).  Stream-ordered, no host sync.
     Batching amortises the collective's latency over nwin windows (xGMI is point to point:
-    small messages are latency-, not bandwidth-bound)."""
+    small messages are latency-, not bandwidth-bound).
+
+    objID keys: canonical decimal objIDs are their values on every rank and merge as is.  A
+    dictionary key (a non-numeric String objID) is an id in its own rank's gf_objid_dict, so
+    keys of different ranks cannot be compared: the merge refuses such a window (record status
+    _lib.KNN_STATUS_FOREIGN_KEYS, no entries) -- merge those by their Strings with
+    allgather_knn_string_lists.
+
+    Ordering (pipeline depth 3): odd windows' records are written on the plan's second stream.
+    Before this call, gf_ctx_join (the context stream waits for the second stream) so the
+    records are complete; after it, gf_ctx_fork (the second stream waits for the context
+    stream) before `records` is handed to later enqueues, so no later window overwrites them
+    while the all-gather still reads them."""
     import torch.distributed as dist_
 
     world = dist_.get_world_size(group)
@@ -197,8 +211,46 @@ def allgather_knn_records_batch(records, k: int, results, group=None):
     ctx = _lib.context(records.device.index)
     out = results if isinstance(results, int) else results.data_ptr()
     _lib.check(_lib.lib().gf_knn_merge_dev_batch(ctx.handle, int(k), gathered.data_ptr(), world, int(nwin),
-                                                 _lib.GF_MERGE_SHARD_MAJOR, out), ctx.handle, "gf_knn_merge_dev_batch")
+                                                 _lib.GF_MERGE_SHARD_MAJOR | _lib.GF_MERGE_FOREIGN_KEYS, out),
+               ctx.handle, "gf_knn_merge_dev_batch")
     return results
+
+
+def merge_string_lists(k: int, lists):
+    """Top-k-distinct merge of per-shard lists whose objIDs are Strings (bytes): sorted by
+    (dist, objID String bytes), one entry per String (its minimum (dist, idx) occurrence), first
+    k.  The rank-independent order for objIDs that are dictionary Strings: a dictionary key is an
+    id in its own rank's dictionary, so only the Strings themselves compare across ranks (ties
+    at exactly equal distances are ordered by the String's bytes)."""
+    ent = []
+    for objs, dist, idx in lists:
+        ent += [(float(d), bytes(o), int(i)) for o, d, i in zip(objs, dist, idx)]
+    ent.sort(key=lambda e: (e[0], e[1], e[2]))
+    seen, out = set(), []
+    for d, o, i in ent:
+        if o in seen:
+            continue
+        seen.add(o)
+        out.append((o, d, i))
+        if len(out) == k:
+            break
+    return [e[0] for e in out], np.array([e[1] for e in out], np.float64), np.array([e[2] for e in out], np.int64)
+
+
+def allgather_knn_string_lists(objid_strings, dist, idx, k: int, group=None):
+    """kNN exchange for windows whose objIDs are dictionary Strings (keys of
+    different ranks' dictionaries cannot be merged as integers).  Each rank decodes its sorted
+    list's keys to Strings (PointWindow.objid_strings / ObjIdDict.decode_bytes), the lists are
+    all-gathered (any backend) and merged by merge_string_lists -- identical on every rank.
+    Intern the merged Strings into a rank's own dictionary to get its keys back."""
+    import torch.distributed as dist_
+
+    world = dist_.get_world_size(group)
+    mine = ([o.encode() if isinstance(o, str) else bytes(o) for o in objid_strings],
+            np.asarray(dist, np.float64), np.asarray(idx, np.int64))
+    gathered = [None] * world
+    dist_.all_gather_object(gathered, mine, group=group)
+    return merge_string_lists(k, gathered)
 
 
 def join_query_halo(qcx: np.ndarray, band, c: int) -> np.ndarray:

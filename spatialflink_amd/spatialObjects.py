@@ -243,7 +243,12 @@ class PointWindow:
         d = objid_dict or ObjIdDict.default(dev)
         x = np.array([p.x for p in points], np.float64)
         y = np.array([p.y for p in points], np.float64)
-        o = d.intern([str(p.objID) if p.objID is not None else "null" for p in points])
+        # a null objID (Java null: e.g. a GeoJSON feature without the objID property) stays the
+        # null key; the String "null" (a JSON null literal's text) is a different objID
+        o = np.full(len(points), _lib.OBJID_NULL, np.int64)
+        have = [i for i, p in enumerate(points) if p.objID is not None]
+        if have:
+            o[have] = d.intern([str(points[i].objID) for i in have])
         ts = np.array([p.timeStampMillisec for p in points], np.int64)
         w = cls.from_numpy(x, y, o, ts, device, start, end)
         w.objid_dict = d

@@ -46,7 +46,7 @@ def device_text(text, device=None):
 
 class GfGeojsonSchema(C.Structure):
     _fields_ = [("objid_property", C.c_char_p), ("time_property", C.c_char_p), ("date_format", C.c_int32),
-                ("tz_offset_minutes", C.c_int32)]
+                ("tz_offset_minutes", C.c_int32), ("value_lines", C.c_int32)]
 
 
 GEOJSON_DATE_FORMATS = {None: 0, "yyyy-MM-dd HH:mm:ss": 1}
@@ -90,21 +90,22 @@ def _parse_lines(fn, schema, uGrid, text, device, capacity, objid_dict):
 class Deserialization:
     class GeoJSONToTSpatial:
         """GeoJSONToTSpatial(uGrid, dateFormat, propertyTimeStamp, propertyObjID)
-        (Deserialization.java:149-211) over lines of GeoJSON: one Kafka key/value record
-        ({"key": .., "value": Feature}) or bare Feature per line, run on the GPU
-        (gf_geojson_parse).  dateFormat: None (the time property is integer milliseconds) or
-        "yyyy-MM-dd HH:mm:ss" in a fixed UTC offset `tz_offset_minutes` (the reference JVM's
+        (Deserialization.java:149-211) over lines of GeoJSON, run on the GPU (gf_geojson_parse):
+        one Kafka key/value record ({"key": .., "value": ..}, the ObjectNode the map receives) per
+        line, or with value_lines=True the record's value itself (a Feature as the reference's
+        Serialization writes it).  dateFormat: None (the time property is integer milliseconds)
+        or "yyyy-MM-dd HH:mm:ss" in a fixed UTC offset `tz_offset_minutes` (the reference JVM's
         default zone).  A feature without the objID property has objID None (key OBJID_NULL)."""
 
         def __init__(self, uGrid=None, dateFormat=None, propertyTimeStamp=None, propertyObjID=None,
-                     tz_offset_minutes=0):
+                     tz_offset_minutes=0, value_lines=False):
             if dateFormat not in GEOJSON_DATE_FORMATS:
                 raise ValueError(f"dateFormat {dateFormat!r}: supported {list(GEOJSON_DATE_FORMATS)}")
             self.uGrid = uGrid
             self._names = (propertyObjID.encode() if propertyObjID else None,
                            propertyTimeStamp.encode() if propertyTimeStamp else None)
             self.schema = GfGeojsonSchema(self._names[0], self._names[1], GEOJSON_DATE_FORMATS[dateFormat],
-                                          int(tz_offset_minutes))
+                                          int(tz_offset_minutes), int(bool(value_lines)))
 
         def parse(self, text, device=None, capacity=None, objid_dict: ObjIdDict = None) -> PointWindow:
             return _parse_lines(_lib.lib().gf_geojson_parse, self.schema, self.uGrid, text, device, capacity,

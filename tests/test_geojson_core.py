@@ -1,0 +1,91 @@
+"""CPU: the GeoJSON ingest's per-line evaluator (spatialflink_amd/csrc/gf_geojson.hpp -- the same
+code the GPU parse kernel runs per lane, built here for the host by tests/native/geojson_core.cpp)
+against the oracle (oracle.geojson_parse over Python's json module), through BOTH of its paths:
+the one-pass locator (LDS-staged bytes) and the walk.  x / y bit-exact, ts, objID (canonical key
+or the String bytes the dictionary receives) and the kind of every bad line
+(Deserialization.GeoJSONToTSpatial.map, Deserialization.java:149-211)."""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+from geojson_gen import BAD, TRICKY, lines
+
+OBJID_NULL = (1 << 63) - 1
+
+
+@pytest.fixture(scope="module")
+def core(tmp_path_factory):
+    out = str(tmp_path_factory.mktemp("gcore") / "geojson_core.so")
+    subprocess.run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off",
+                    os.path.join(ROOT, "tests", "native", "geojson_core.cpp"), "-o", out], check=True)
+    L = C.CDLL(out)
+    L.geojson_core_parse.argtypes = [C.c_char_p, C.c_void_p, C.c_int64, C.c_char_p, C.c_char_p, C.c_int, C.c_int,
+                                     C.c_int, C.c_int] + [C.c_void_p] * 8
+    return L
+
+
+def run(core, lns, prop_obj, prop_ts, date_fmt, tz, vl, walk):
+    off = np.zeros(len(lns) + 1, np.int64)
+    off[1:] = np.cumsum([len(b) for b in lns])
+    buf = b"".join(lns) + b"\0" * 16  # the locator reads whole words past a line's end
+    n = len(lns)
+    kind = np.zeros(n, np.int32); x = np.zeros(n); y = np.zeros(n); ts = np.zeros(n, np.int64)
+    obj = np.zeros(n, np.int64); dic = np.zeros(n, np.int32); ob = np.zeros(n, np.int64); oe = np.zeros(n, np.int64)
+    core.geojson_core_parse(buf, off.ctypes.data, n, prop_obj and prop_obj.encode(), prop_ts and prop_ts.encode(),
+                            date_fmt, tz, int(vl), int(walk), *(a.ctypes.data for a in (kind, x, y, ts, obj, dic, ob, oe)))
+    objs = []
+    for i in range(n):
+        if dic[i]:
+            objs.append(buf[ob[i]:oe[i]])
+        elif obj[i] == OBJID_NULL:
+            objs.append(None)
+        else:
+            objs.append(str(int(obj[i])).encode())
+    return kind, x, y, ts, objs
+
+
+def compare(core, oracle_mod, lns, date_fmt=0, tz=0, vl=False, props=("oID", "timestamp")):
+    for walk in (0, 1):
+        kind, x, y, ts, objs = run(core, lns, props[0], props[1], date_fmt, tz, vl, walk)
+        for i, ln in enumerate(lns):
+            ex, ey, eo, et, bl, bk = oracle_mod.geojson_parse(ln, props[0], props[1], date_fmt, tz, vl)
+            assert kind[i] == (bk if bl == 0 else 0), (walk, ln[:200], kind[i], bk)
+            if bl < 0:
+                assert x[i].tobytes() == ex[0].tobytes() and y[i].tobytes() == ey[0].tobytes(), (walk, ln[:200])
+                assert ts[i] == et[0] and objs[i] == eo[0], (walk, ln[:200], ts[i], et[0], objs[i], eo[0])
+
+
+@pytest.mark.parametrize("date_fmt,tz,vl", [(0, 0, False), (1, 480, False), (0, 0, True), (1, -300, True)])
+def test_generated(core, oracle_mod, date_fmt, tz, vl):
+    lns = lines(31 + date_fmt + 2 * vl, 3000, date_fmt, value_lines=vl).split(b"\n")[:-1]
+    compare(core, oracle_mod, lns, date_fmt, tz, vl)
+
+
+def test_tricky_and_bad(core, oracle_mod):
+    compare(core, oracle_mod, TRICKY + [b for b, _ in BAD])
+    kind, *_ = run(core, [b for b, _ in BAD], "oID", "timestamp", 0, 0, False, 0)
+    assert kind.tolist() == [k for _, k in BAD]
+
+
+def test_no_property_names(core, oracle_mod):
+    compare(core, oracle_mod, lines(7, 300, 0).split(b"\n")[:-1] + TRICKY, props=(None, None))
+
+
+def test_mutations(core, oracle_mod):
+    """Every line of a sample with one byte replaced, deleted or duplicated (mostly malformed, some
+    still valid): the locator, the walk and the oracle agree on each kind and value."""
+    rng = np.random.default_rng(3)
+    base = lines(41, 60, 0).split(b"\n")[:-1] + TRICKY[:12]
+    alphabet = b'{}[]",:\\ 0123456789.-+eEtfnulrsaI\t\x01\xc3\xa9\x80'
+    out = []
+    for ln in base:
+        for _ in range(12):
+            i = int(rng.integers(0, len(ln)))
+            op = rng.integers(0, 3)
+            c = bytes([alphabet[int(rng.integers(0, len(alphabet)))]])
+            out.append(ln[:i] + c + ln[i + 1:] if op == 0 else ln[:i] + ln[i + 1:] if op == 1 else ln[:i] + c + ln[i:])
+    compare(core, oracle_mod, out)

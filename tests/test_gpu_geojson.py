@@ -6,7 +6,7 @@ import numpy as np
 import pytest
 
 from conftest import BEIJING
-from geojson_gen import lines
+from geojson_gen import BAD, TRICKY, lines
 
 pytestmark = pytest.mark.gpu
 
@@ -21,14 +21,15 @@ def sf(gpu):
     return spatialflink_amd
 
 
-def parse(sf, text, date_fmt=None, tz=0, grid=None, props=("oID", "timestamp")):
-    d = sf.Deserialization.GeoJSONToTSpatial(grid, date_fmt, props[1], props[0], tz_offset_minutes=tz)
+def parse(sf, text, date_fmt=None, tz=0, grid=None, props=("oID", "timestamp"), value_lines=False):
+    d = sf.Deserialization.GeoJSONToTSpatial(grid, date_fmt, props[1], props[0], tz_offset_minutes=tz,
+                                             value_lines=value_lines)
     return d.parse(text)
 
 
-def check(sf, oracle_mod, text, date_fmt, tz, grid=None, og=None):
-    w = parse(sf, text, date_fmt, tz, grid)
-    ex, ey, eo, et, bl, bk = oracle_mod.geojson_parse(text, "oID", "timestamp", 1 if date_fmt else 0, tz)
+def check(sf, oracle_mod, text, date_fmt, tz, grid=None, og=None, value_lines=False):
+    w = parse(sf, text, date_fmt, tz, grid, value_lines=value_lines)
+    ex, ey, eo, et, bl, bk = oracle_mod.geojson_parse(text, "oID", "timestamp", 1 if date_fmt else 0, tz, value_lines)
     assert bl == -1
     np.testing.assert_array_equal(w.x.cpu().numpy().view(np.uint64), ex.view(np.uint64))
     np.testing.assert_array_equal(w.y.cpu().numpy().view(np.uint64), ey.view(np.uint64))
@@ -48,11 +49,14 @@ def test_reference_example(sf, oracle_mod):
     assert int(w.timeStampMillisec[0]) == 1201954352000
 
 
-@pytest.mark.parametrize("seed,n,date_fmt,tz", [(1, 50_000, None, 0), (2, 50_000, "yyyy-MM-dd HH:mm:ss", 480),
-                                                (3, 3_000, "yyyy-MM-dd HH:mm:ss", -300), (4, 1, None, 0)])
-def test_generated_lines(sf, oracle_mod, seed, n, date_fmt, tz):
+@pytest.mark.parametrize("seed,n,date_fmt,tz,vl", [(1, 50_000, None, 0, False),
+                                                   (2, 50_000, "yyyy-MM-dd HH:mm:ss", 480, False),
+                                                   (3, 3_000, "yyyy-MM-dd HH:mm:ss", -300, False), (4, 1, None, 0, False),
+                                                   (5, 40_000, None, 0, True), (6, 3_000, "yyyy-MM-dd HH:mm:ss", 60, True)])
+def test_generated_lines(sf, oracle_mod, seed, n, date_fmt, tz, vl):
     g = sf.UniformGrid(100, *BEIJING)
-    check(sf, oracle_mod, lines(seed, n, 1 if date_fmt else 0), date_fmt, tz, g, oracle_mod.grid(100, *BEIJING))
+    check(sf, oracle_mod, lines(seed, n, 1 if date_fmt else 0, value_lines=vl), date_fmt, tz, g,
+          oracle_mod.grid(100, *BEIJING), value_lines=vl)
 
 
 def test_crlf_and_missing_final_newline(sf, oracle_mod):
@@ -65,55 +69,34 @@ def test_no_property_names(sf):
     assert w.objid_strings() == [None] and int(w.timeStampMillisec[0]) == 0
 
 
-@pytest.mark.parametrize("bad,kind", [
-    (b"", 4),
-    (b'{"geometry":{"type":"Point"}}', 3),
-    (b'{"geometry":{"coordinates":["1",2]}}', 1),
-    (b'{"geometry":{"coordinates":[1,2]},"properties":{"timestamp":1.5}}', 1),
-    (b'{"geometry":{"coordinates":[1,2]},"properties":{"oID":2.5}}', 2),
-    (b'{"geometry":{"coordinates":[1,2]},"properties":{"oID":"a\\"b"}}', 2),
-    (b'{"geometry":{"coordinates":[1,2]', 3),
-])
-def test_first_bad_line(sf, oracle_mod, bad, kind):
+@pytest.mark.parametrize("walk", [0, 1])
+def test_first_bad_line(sf, oracle_mod, walk):
+    """Each bad line inside a chunk of good ones: the chunk fails at that line with the oracle's kind
+    (the locator's strict check sends every one of them to the walk, which decides)."""
+    from spatialflink_amd import _lib
     good = lines(11, 300, 0).split(b"\n")[:300]
-    text = b"\n".join(good[:137] + [bad] + good[137:]) + b"\n"
-    *_, bl, bk = oracle_mod.geojson_parse(text, "oID", "timestamp", 0, 0)
-    assert (bl, bk) == (137, kind)
-    with pytest.raises(ValueError, match=f"line 137: {sf.spatialStreams.CSV_KINDS[kind]}"):
-        parse(sf, text)
-
-
-DEEP = b'{"geometry":{"coordinates":[1,2]},"x":' + b"[" * 70 + b"]" * 70 + b"}"
-TRICKY = [  # valid JSON the one-pass locator takes (or hands to the walk: escapes, depth > 63)
-    b'{"value":{"geometry":{"coordinates":[1,2]}},"value":{"geometry":{"coordinates":[3,4]},"properties":{"oID":"a"}}}',
-    b'{"value":{"geometry":{"coordinates":[1,2]}},"value":7,"geometry":{"coordinates":[5,6]}}',
-    b'{"geometry":{"coordinates":[1,2],"coordinates":[[8,9]]},"properties":{"timestamp":5,"oID":1,"oID":"x y"}}',
-    b'{"geometry":{"type":"Point","coordinates":[1,2]},"geometry":{"coordinates":[3,4]}}',
-    b'{"a":[{"geometry":{"coordinates":[9,9]}}],"geometry":{"coordinates":[1.5e1,-2]},"properties":{"p":{"oID":3},"oID":"7"}}',
-    b'{"value":{"value":{"geometry":{"coordinates":[0,0]}},"geometry":{"coordinates":[2,3]}}}',
-    b'{"properties":{"timestamp":1,"oID":2},"geometry":{"coordinates":[1,2]},"properties":[1,2]}',
-    ' { "geometry" : { "coordinates" : [ 1 , 2 ] } , "properties" : { "oID" : "é☃" } } '.encode(),
-    DEEP,
-    b'{"geometry":{"coordinates":[1,2]},"properties":{"coordinates":1,"timestamp":2,"oIDx":3,"oI":4}}',
-    b'{"geometry":{"coordinates":[[[1,2],[3,4]]]},"properties":{}}',
-    b'{"s":"}{][,:","geometry":{"coordinates":[1,2]},"properties":{"oID":"q"}}',
-    b'{"s":"a\\"b\\u0041","geometry":{"coordinates":[1,2]},"properties":{"oID":"q","timestamp":3}}',
-    b'{"":1,"geometry":{"coordinates":[1,2]},"properties":{"oID":true,"timestamp":-0}}',
-    b'{"geometry":{"coordinates":[3,4]},"value":[{"properties":{"oID":5}}],"properties":{"oID":6}}',
-    b'{"value":{"geometry":{"coordinates":[3,4]}},"value":{"geometry":{"coordinates":[3,4]}},"properties":{"oID":6}}',
-    b'{"value":{"geometry":{"coordinates":[1,2]},"properties":{"oID":"v"}},"value":{"geometry":{"coordinates":[5,6]}}}',
-    b'{"geometry":{"coordinates":[1,2]},"properties":{"oID":null,"timestamp":-12}}',
-    b'{"key":1,"value":{"type":"Feature","geometry":{"coordinates":[1e-3,2E+1],"type":"Point"},"properties":{"oID":-5}}}',
-]
+    ctx = _lib.context(0)
+    _lib.check(_lib.lib().gf_ctx_set_flag(ctx.handle, _lib.FLAG_GEOJSON_WALK, walk), ctx.handle, "flag")
+    try:
+        for bad, kind in BAD:
+            text = b"\n".join(good[:137] + [bad] + good[137:]) + b"\n"
+            *_, bl, bk = oracle_mod.geojson_parse(text, "oID", "timestamp", 0, 0)
+            assert (bl, bk) == (137, kind), bad
+            with pytest.raises(ValueError, match=f"line 137: {sf.spatialStreams.CSV_KINDS[kind]}"):
+                parse(sf, text)
+    finally:
+        _lib.lib().gf_ctx_set_flag(ctx.handle, _lib.FLAG_GEOJSON_WALK, 0)
 
 
 @pytest.mark.parametrize("walk", [0, 1])
 def test_locator_matches_walk(sf, oracle_mod, walk):
     """The one-pass member locator (k_csv.hip geo_locate) and the member-by-member walk it stands
-    in for give the oracle's results on generated lines plus valid JSON built to exercise last-wins
-    duplicates at each level, a non-object last "value", members inside arrays and deeper
-    objects, whitespace, UTF-8, structural bytes inside strings, an escape in a member not taken and nesting deeper than
-    the locator's stack.  (Escapes and malformed lines: test_first_bad_line, with the locator on.)"""
+    in for give the oracle's results on generated lines plus valid records built to exercise
+    last-wins duplicates at each level, the value's own Point before its geometry, every catch-
+    branch trigger, members inside arrays and deeper objects, whitespace, UTF-8 (2-4 byte
+    sequences), structural bytes inside strings, escapes in members not taken, literals, long and
+    3-digit-exponent numbers json-simple reads back, -0 ordinates and nesting deeper than the
+    locator's stack.  (Malformed / unsupported lines: test_first_bad_line, both paths.)"""
     from spatialflink_amd import _lib
     text = lines(21, 5_000, 0) + b"\n".join(TRICKY * 40) + b"\n"
     ctx = _lib.context(0)

@@ -160,3 +160,50 @@ def test_join_shards_with_query_halo(sf, oracle_mod, r):
     assert st == 0 and len(exp) > 1000
     exp = exp[np.lexsort((exp[:, 1], exp[:, 0]))]
     np.testing.assert_array_equal(got, exp)
+
+
+def test_knn_merge_refuses_foreign_dictionary_keys(sf, oracle_mod):
+    """a dictionary objID key (a non-numeric String) is an id in its own context's
+    dictionary, so records all-gathered from other ranks cannot be merged by key.  With
+    GF_MERGE_FOREIGN_KEYS (what sharding.allgather_knn_records[_batch] pass) a window holding
+    one gets status 2 and no entries; canonical decimal objIDs (their values on every rank)
+    still merge; within one context (no flag) dictionary keys merge as before."""
+    import torch
+    from spatialflink_amd import _lib
+
+    L = _lib.lib()
+    g = sf.UniformGrid(500, *BEIJING)
+    q = sf.Point("q", *QPOINT, 0, g)
+    k = 30
+    rb = sf.spatialOperators.knn_record_bytes(k)
+    x, y = oracle_mod.java_random_points(77, 400_000, *BEIJING)
+    d = sf.ObjIdDict(0)
+    names = [f"bus-{i}" for i in range(len(x))]
+    for strings, nwin in ((True, 2), (False, 2)):
+        keys = d.intern(names) if strings else np.arange(len(x), dtype=np.int64)
+        recs = torch.zeros(2, nwin, rb, dtype=torch.uint8, device="cuda")
+        half = len(x) // 2
+        for s in range(2):
+            sl = slice(s * half, (s + 1) * half)
+            op = sf.PointPointKNNQuery(conf(sf), g)
+            pw = sf.PointWindow.from_numpy(x[sl], y[sl], keys[sl])
+            for w in range(nwin):
+                op.enqueue(pw, q, 0.5, k, recs[s, w])
+            op.flush(0, q, 0.5, k)
+        torch.cuda.synchronize()
+        ctx = _lib.context(0)
+        for flag in (_lib.GF_MERGE_FOREIGN_KEYS, 0):
+            out = torch.zeros(nwin, rb, dtype=torch.uint8, device="cuda")
+            _lib.check(L.gf_knn_merge_dev_batch(ctx.handle, k, recs.data_ptr(), 2, nwin,
+                                                _lib.GF_MERGE_SHARD_MAJOR | flag, out.data_ptr()), ctx.handle, "merge")
+            host = out.cpu().numpy()
+            for w in range(nwin):
+                st, o, dd, i = sf.spatialOperators.decode_knn_record(host[w].tobytes(), k)
+                if strings and flag:
+                    assert st == _lib.KNN_STATUS_FOREIGN_KEYS and len(o) == 0
+                else:
+                    og = oracle_mod.grid(500, *BEIJING)
+                    est, eo, ed, ei = oracle_mod.knn(og, x, y, np.arange(len(x), dtype=np.int64), *QPOINT, 0.5, k)
+                    assert st == 0 and np.array_equal(dd, ed)
+                    got = d.decode(o) if strings else o.tolist()
+                    assert got == ([names[j] for j in eo] if strings else eo.tolist())

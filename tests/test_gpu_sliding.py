@@ -51,16 +51,19 @@ def conf(sf):
     return sf.QueryConfiguration(sf.QueryType.WindowBased)
 
 
-@pytest.mark.parametrize("size,slide,k,depth,n,cap", [
-    (3000, 1000, 50, 2, 900_000, None),
-    (3000, 1000, 50, 1, 900_000, None),
-    (4000, 2000, 120, 1, 700_000, None),
-    (5000, 3000, 7, 2, 600_000, None),
-    (2000, 1000, 50, 2, 400_000, 64),      # every pane overflows: pane-by-pane exact decode
+@pytest.mark.parametrize("size,slide,k,depth,n,cap,gn", [
+    (3000, 1000, 50, 2, 900_000, None, 500),
+    (3000, 1000, 50, 1, 900_000, None, 500),
+    (4000, 2000, 120, 1, 700_000, None, 500),
+    (5000, 3000, 7, 2, 600_000, None, 500),
+    (2000, 1000, 50, 2, 400_000, 64, 500),     # every pane overflows: pane-by-pane exact decode
+    # C5's shape (BASELINE.json configs[4]): k = 100, 1000 x 1000 grid, size / slide = 2
+    (2000, 1000, 100, 2, 1_500_000, None, 1000),
+    (2000, 1000, 100, 1, 800_000, None, 1000),
 ])
-def test_sliding_knn_matches_oracle(sf, oracle_mod, size, slide, k, depth, n, cap):
-    g = sf.UniformGrid(500, *BEIJING)
-    og = oracle_mod.grid(500, *BEIJING)
+def test_sliding_knn_matches_oracle(sf, oracle_mod, size, slide, k, depth, n, cap, gn):
+    g = sf.UniformGrid(gn, *BEIJING)
+    og = oracle_mod.grid(gn, *BEIJING)
     q = sf.Point("q", *QPOINT, 0, g)
     x, y, obj, ts = make_stream(oracle_mod, size + slide + k, n, 10_000, 24_000, gap=(15_200, 17_900))
     op = sf.SlidingKNNQuery(conf(sf), g, q, 0.5, k, size_ms=size, slide_ms=slide, pipeline=depth)

@@ -79,6 +79,11 @@ def _worker(rank, world, port, ret):
                                                       idx[O.knn(og, x[idx], y[idx], obj[idx], QPOINT[0], QPOINT[1], r, k)[3]], k)
             st, fo, fd, fi = O.knn(og, x, y, obj, QPOINT[0], QPOINT[1], r, k)
             assert np.array_equal(mo, fo) and np.array_equal(md, fd) and np.array_equal(mi, fi), (r, k)
+            # String objIDs (dictionary keys are per-rank ids): the exchange carries the Strings
+            name = lambda v: f"bus-{v:05d}"  # noqa: E731  (non-numeric: dictionary Strings on a device)
+            st, so_, sd_, si_ = O.knn(og, x[idx], y[idx], obj[idx], QPOINT[0], QPOINT[1], r, k)
+            mo, md, mi = sharding.allgather_knn_string_lists([name(v) for v in so_], sd_, idx[si_], k)
+            assert mo == [name(v).encode() for v in fo] and np.array_equal(md, fd) and np.array_equal(mi, fi), (r, k)
 
         # range: per-shard hits, concatenated
         for r in (0.5, 0.05):

@@ -742,6 +742,29 @@ def bench_sliding(args):
             print(f"oracle check of one {len(X)}-point window: {verified} ({time.perf_counter() - t:.1f}s)",
                   file=sys.stderr, flush=True)
             assert verified, "pane-merged window differs from the oracle"
+    if world > 1 and rank == 0 and not args.no_verify and window_pts <= 100_000_000:
+        # the all-gathered, device-merged record of one window == the oracle on the union of
+        # every rank's two panes (rank 0 regenerates the other bands from their seeds).  objIDs
+        # are globally unique; idx is each rank's own stream position, so it is not compared.
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle as O
+
+        (a, b), (o, d, ix) = sorted(per.items())[0]
+        xs, ys, obs = [], [], []
+        for r_ in range(world):
+            blo, bhi = sharding.column_bands(grid_n, world)[r_]
+            bx0, bx1 = sharding.band_x_range(grid, blo, bhi)
+            for j in (a, b):
+                x_, y_ = sf.synthetic_uniform(4242 + 1000 * r_ + j, pane_pts, bx0, bx1, BEIJING[2], BEIJING[3])
+                xs.append(x_); ys.append(y_)
+                obs.append(np.arange(pane_pts, dtype=np.int64) + (r_ * npanes + j) * pane_pts)
+        t = time.perf_counter()
+        st, eo, ed, ei = O.knn(O.grid(grid_n, *BEIJING), np.concatenate(xs), np.concatenate(ys), np.concatenate(obs),
+                               QPOINT[0], QPOINT[1], args.radius, k)
+        verified = bool(st == 0 and np.array_equal(eo, o) and np.array_equal(ed, d))
+        print(f"oracle check of one window over {world} ranks: {verified} ({time.perf_counter() - t:.1f}s)",
+              file=sys.stderr, flush=True)
+        assert verified, "all-gathered sliding window differs from the oracle"
 
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
