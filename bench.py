@@ -121,6 +121,8 @@ def main():
                     help="CPU baseline budget, split over its three lines (rank 0, N=1)")
     ap.add_argument("--cpu-sample", type=int, default=1_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--join-stream", action="store_true",
+                    help="join workload: experiment -- bucket only the query side, stream the ordinary points")
     ap.add_argument("--join-sync", action="store_true",
                     help="join workload: gf_join_pp per window (pair count read back) instead of gf_join_pp_async")
     ap.add_argument("--clustered", action="store_true",
@@ -209,6 +211,8 @@ def main():
     pts_ref = [ctypes.byref(p_) for p_ in pts]
     enqueue = L.gf_knn_enqueue
 
+    pending = [0]  # first window whose record has not been exchanged yet
+
     def exchange(first, lo, hi):  # windows [lo, hi] of one group: one all-gather + one merge launch
         g = (lo - first) // B
         sharding.allgather_knn_records_batch(slots[g % 2, : hi - lo + 1], args.k, host.ptr(lo))
@@ -216,6 +220,7 @@ def main():
             # depth 3 writes odd windows' records on the plan's second stream: it must not
             # reuse slots[g % 2] (group g + 2) before this all-gather + merge have read them
             _lib.check(L.gf_ctx_fork(ctx.handle), ctx.handle, "gf_ctx_fork")
+        pending[0] = hi + 1
 
     def step(i, first):
         if world == 1:  # the select writes the final record straight into pinned host memory
@@ -223,6 +228,8 @@ def main():
             if st:
                 _lib.check(st, ctx.handle, "gf_knn_enqueue")
         else:
+            if i == first:
+                pending[0] = first
             g, w_ = divmod(i - first, B)
             _lib.check(enqueue(plan, pts_ref[i % args.windows], slots[g % 2, w_].data_ptr()), ctx.handle, "enqueue")
             c = i - lag  # this window's record is complete now
@@ -232,11 +239,10 @@ def main():
                 exchange(first, c - B + 1, c)
 
     def drain(first, last):
-        _lib.check(L.gf_knn_plan_flush(plan), ctx.handle, "flush")
-        if world > 1:
-            lo = first + ((last - first) // B) * B
-            if lag or (last - first) % B != B - 1:  # the last group is still pending
-                exchange(first, lo, last)
+        _lib.check(L.gf_knn_plan_flush(plan), ctx.handle, "flush")  # joins the second stream
+        while world > 1 and pending[0] <= last:  # the groups still pending (up to lag / B + 1 of them)
+            lo = pending[0]
+            exchange(first, lo, min(last, first + ((lo - first) // B + 1) * B - 1))
 
     for i in range(args.warmup):
         step(i, 0)

@@ -131,10 +131,13 @@ const char* gf_ctx_last_error(gf_ctx* ctx);
  * buckets from global memory in input order instead of the row-bucketed LDS path.
  * GF_FLAG_JOIN_COARSE: 1 = the row-bucketed path never takes its sub-cell (fine) variant.
  * GF_FLAG_GEOJSON_WALK: 1 = gf_geojson_parse takes the member-by-member walk on every line
- * (no one-pass locator); the results are the same. */
+ * (no one-pass locator); the results are the same.
+ * GF_FLAG_JOIN_STREAM: 1 = gf_join_pp's fine path buckets only the query side and streams the
+ * ordinary points in input order (an experiment the default path is measured against). */
 #define GF_FLAG_JOIN_LEGACY 1
 #define GF_FLAG_JOIN_COARSE 2
 #define GF_FLAG_GEOJSON_WALK 4
+#define GF_FLAG_JOIN_STREAM 8
 int gf_ctx_set_flag(gf_ctx* ctx, int flag, int value);
 
 /* Record HIP events around launches of the kernels in `mask` (bit 1 << GF_K_*; 0 = off). */

@@ -1432,3 +1432,286 @@ int64_t orc_csv_parse(const char* text, int64_t len, char delim, const int32_t* 
   free(fidx);
   return line;
 }
+
+/* ------------------------------------------------------------------------------------ */
+/* Multi-core CPU baselines (bench only; TEST / BASELINE INFRASTRUCTURE).  The reference  */
+/* operators as Flink runs them with parallelism T (conf/geoflink-conf.yml:55): source    */
+/* subtasks evaluate the per-point work up to the keyBy(gridID) (string cell ID, HashSet  */
+/* membership), survivors are shuffled to key subtask hash(gridID) % T, and the key        */
+/* subtasks run the window apply; results are concatenated.  Same outputs as the serial    */
+/* restatements above (ascending indices / the same pair set).                            */
+/* ------------------------------------------------------------------------------------ */
+#include <omp.h>
+
+typedef struct { int64_t* v; int64_t n, cap; } lvec;
+static void lvec_push(lvec* a, int64_t x) {
+  if (a->n == a->cap) { a->cap = a->cap ? 2 * a->cap : 256; a->v = (int64_t*)realloc(a->v, 8 * (size_t)a->cap); }
+  a->v[a->n++] = x;
+}
+static int cmp_i64(const void* a, const void* b) {
+  int64_t x = *(const int64_t*)a, y = *(const int64_t*)b;
+  return x < y ? -1 : (x > y);
+}
+static int cmp_pair(const void* a, const void* b) {
+  const int64_t* x = (const int64_t*)a; const int64_t* y = (const int64_t*)b;
+  if (x[0] != y[0]) return x[0] < y[0] ? -1 : 1;
+  return x[1] < y[1] ? -1 : (x[1] > y[1]);
+}
+/* concatenation of per-thread results (sorted ascending) into out[cap]; returns the count */
+static int64_t gather_sorted(lvec* res, int T, int64_t* out, int64_t cap, int width) {
+  int64_t tot = 0;
+  for (int t = 0; t < T; t++) tot += res[t].n;
+  int64_t* all = (int64_t*)malloc(8 * (size_t)(tot > 0 ? tot : 1));
+  int64_t w = 0;
+  for (int t = 0; t < T; t++) { memcpy(all + w, res[t].v, 8 * (size_t)res[t].n); w += res[t].n; free(res[t].v); }
+  qsort(all, (size_t)(tot / width), 8 * (size_t)width, width == 1 ? cmp_i64 : cmp_pair);
+  memcpy(out, all, 8 * (size_t)(tot < cap * width ? tot : cap * width));
+  free(all);
+  return tot / width;
+}
+
+/* shared shape of the range operators: G / C built by the driver, then T subtasks */
+static int64_t range_mt(const orc_grid* g, int64_t n, const double* x, const double* y, const strset* G,
+                        const strset* C, int nthreads, int64_t* out_idx, int64_t cap,
+                        int (*apply)(const void* ctx, int64_t i, int64_t* reps), const void* actx) {
+  const int T = nthreads < 1 ? 1 : nthreads;
+  lvec* box = (lvec*)calloc((size_t)T * (size_t)T, sizeof(lvec)); /* survivors: i << 1 | inG */
+  lvec* res = (lvec*)calloc((size_t)T, sizeof(lvec));
+#pragma omp parallel num_threads(T)
+  {
+    const int t = omp_get_thread_num();
+    char id[32];
+    for (int64_t i = n * t / T; i < n * (t + 1) / T; i++) { /* source subtask: filter, keyBy */
+      int32_t cx, cy;
+      orc_cell_of(g, x[i], y[i], &cx, &cy);
+      orc_cell_id(cx, cy, id);
+      const int inG = ss_contains(G, id);
+      if (!(inG || ss_contains(C, id))) continue;
+      lvec_push(&box[(int64_t)t * T + (int64_t)(str_hash(id) % (uint64_t)T)], i << 1 | inG);
+    }
+#pragma omp barrier
+    for (int s = 0; s < T; s++) { /* key subtask t: the window apply per point */
+      const lvec* b = &box[(int64_t)s * T + t];
+      for (int64_t j = 0; j < b->n; j++) {
+        const int64_t i = b->v[j] >> 1;
+        if (b->v[j] & 1) { lvec_push(&res[t], i); continue; }
+        int64_t reps = 0;
+        if (apply(actx, i, &reps))
+          for (int64_t k = 0; k < reps; k++) lvec_push(&res[t], i);
+      }
+    }
+  }
+  for (int64_t i = 0; i < (int64_t)T * T; i++) free(box[i].v);
+  free(box);
+  int64_t cnt = gather_sorted(res, T, out_idx, cap, 1);
+  free(res);
+  return cnt;
+}
+
+typedef struct { const double *x, *y, *qx, *qy; int32_t nq; double r; int approx, metric; } pp_ctx;
+static int pp_apply(const void* c_, int64_t i, int64_t* reps) { /* PointPointRangeQuery.java:158-183 */
+  const pp_ctx* c = (const pp_ctx*)c_;
+  if (c->approx) { *reps = c->nq; return c->nq > 0; }
+  for (int32_t q = 0; q < c->nq; q++)
+    if (orc_distance(c->qx[q], c->qy[q], c->x[i], c->y[i], c->metric) <= c->r) { *reps = 1; return 1; }
+  return 0;
+}
+int64_t orc_range_pp_mt(const orc_grid* g, int64_t n, const double* x, const double* y, int32_t nq,
+                        const double* qx, const double* qy, double r, int approximate, int metric, int nthreads,
+                        int64_t* out_idx, int64_t cap) {
+  strset G, C;
+  char id[32];
+  ss_init(&G, 64); ss_init(&C, 64);
+  for (int32_t q = 0; q < nq; q++) {
+    int32_t cx, cy;
+    strset Gq, Cq;
+    orc_cell_of(g, qx[q], qy[q], &cx, &cy);
+    orc_cell_id(cx, cy, id);
+    ss_init(&Gq, 64); g_cells_of(g, r, id, &Gq); ss_add_all(&G, &Gq); ss_free(&Gq);
+    ss_init(&Cq, 64); c_cells_of(g, r, id, &G, &Cq); ss_add_all(&C, &Cq); ss_free(&Cq);
+  }
+  pp_ctx c = {x, y, qx, qy, nq, r, approximate, metric};
+  int64_t cnt = range_mt(g, n, x, y, &G, &C, nthreads, out_idx, cap, pp_apply, &c);
+  ss_free(&G); ss_free(&C);
+  return cnt;
+}
+
+typedef struct { const double *x, *y, *bb; const orc_polygons* P; double r; int approx, metric; } ppoly_ctx;
+static int ppoly_apply(const void* c_, int64_t i, int64_t* reps) { /* PointPolygonRangeQuery.java:179-201 */
+  const ppoly_ctx* c = (const ppoly_ctx*)c_;
+  for (int32_t p = 0; p < c->P->npoly; p++) {
+    const double* b = c->bb + 4 * p;
+    double d = c->approx ? orc_point_bbox_distance(c->x[i], c->y[i], b[0], b[1], b[2], b[3])
+                         : orc_point_polygon_distance(c->x[i], c->y[i], c->P, p, c->metric);
+    if (d <= c->r) { *reps = 1; return 1; }
+  }
+  return 0;
+}
+int64_t orc_range_ppoly_mt(const orc_grid* g, int64_t n, const double* x, const double* y, const orc_polygons* P,
+                           double r, int approximate, int metric, int nthreads, int64_t* out_idx, int64_t cap) {
+  strset G, C;
+  char id[32];
+  ss_init(&G, 64); ss_init(&C, 64);
+  double* bb = (double*)malloc(sizeof(double) * 4 * (size_t)(P->npoly > 0 ? P->npoly : 1));
+  for (int32_t p = 0; p < P->npoly; p++) {
+    double x1, y1, x2, y2;
+    polygon_bbox(P, p, &x1, &y1, &x2, &y2);
+    bb[4 * p] = x1; bb[4 * p + 1] = y1; bb[4 * p + 2] = x2; bb[4 * p + 3] = y2;
+    int32_t xi1, yi1, xi2, yi2;
+    orc_cell_of(g, x1, y1, &xi1, &yi1);
+    orc_cell_of(g, x2, y2, &xi2, &yi2);
+    strset Gp, Cp;
+    ss_init(&Gp, 64);
+    for (int64_t a = xi1; a <= xi2; a++)
+      for (int64_t b = yi1; b <= yi2; b++) { orc_cell_id((int32_t)a, (int32_t)b, id); g_cells_of(g, r, id, &Gp); }
+    ss_add_all(&G, &Gp); ss_free(&Gp);
+    ss_init(&Cp, 64);
+    for (int64_t a = xi1; a <= xi2; a++)
+      for (int64_t b = yi1; b <= yi2; b++) { orc_cell_id((int32_t)a, (int32_t)b, id); c_cells_of(g, r, id, &G, &Cp); }
+    ss_add_all(&C, &Cp); ss_free(&Cp);
+  }
+  ppoly_ctx c = {x, y, bb, P, r, approximate, metric};
+  int64_t cnt = range_mt(g, n, x, y, &G, &C, nthreads, out_idx, cap, ppoly_apply, &c);
+  free(bb);
+  ss_free(&G); ss_free(&C);
+  return cnt;
+}
+
+/* PointPointJoinQuery with parallelism T: the query stream's replication (JoinQuery.java:73-90)
+ * by the driver-side restatement above (orc_join_pp's first half), the ordinary points keyed by
+ * gridID over T subtasks, each joining its keys' co-located pairs.  Pairs (sorted) out. */
+int64_t orc_join_pp_mt(const orc_grid* ugrid, const orc_grid* qgrid, int64_t no, const double* ox, const double* oy,
+                       int64_t nq, const double* qx, const double* qy, double r, int approximate, int metric,
+                       int nthreads, int64_t* out_pairs, int64_t cap) {
+  const int T = nthreads < 1 ? 1 : nthreads;
+  char id[32];
+  int32_t cl = 0;
+  if (!(r == 0)) {
+    cl = orc_candidate_layers(qgrid, r);
+    if (cl <= 0) return ORC_ERR_LAYERS;
+  }
+  strset cells;
+  ss_init(&cells, 1024);
+  lvec rq = {0, 0, 0}, rk = {0, 0, 0};  /* replica: query index, key hash */
+  for (int64_t q = 0; q < nq; q++) {
+    int64_t i0, i1, j0, j1;
+    if (r == 0) { i0 = 0; i1 = qgrid->n - 1; j0 = 0; j1 = qgrid->n - 1; }
+    else {
+      int32_t cx, cy, px, py;
+      orc_cell_of(qgrid, qx[q], qy[q], &cx, &cy);
+      orc_cell_id(cx, cy, id);
+      orc_parse_cell_id(id, &px, &py);
+      i0 = lmax((int64_t)px - cl, 0); i1 = lmin((int64_t)px + cl, qgrid->n - 1);
+      j0 = lmax((int64_t)py - cl, 0); j1 = lmin((int64_t)py + cl, qgrid->n - 1);
+    }
+    for (int64_t i = i0; i <= i1; i++)
+      for (int64_t j = j0; j <= j1; j++) {
+        if (!valid_key(qgrid, i, j)) continue;
+        orc_cell_id((int32_t)i, (int32_t)j, id);
+        ss_add(&cells, id);
+        lvec_push(&rq, q);
+        lvec_push(&rk, (int64_t)(((uint64_t)i << 32) | (uint64_t)j));
+      }
+  }
+  int64_t* off = (int64_t*)calloc((size_t)cells.cap + 1, 8);
+  int64_t* slot = (int64_t*)malloc(8 * (size_t)(rq.n > 0 ? rq.n : 1));
+  for (int64_t t = 0; t < rq.n; t++) {
+    orc_cell_id((int32_t)(rk.v[t] >> 32), (int32_t)(rk.v[t] & 0xffffffff), id);
+    slot[t] = ss_find(&cells, id);
+    off[slot[t] + 1]++;
+  }
+  for (int64_t s = 0; s < cells.cap; s++) off[s + 1] += off[s];
+  int64_t* lst = (int64_t*)malloc(8 * (size_t)(rq.n > 0 ? rq.n : 1));
+  {
+    int64_t* cur = (int64_t*)malloc(8 * (size_t)(cells.cap > 0 ? cells.cap : 1));
+    memcpy(cur, off, 8 * (size_t)cells.cap);
+    for (int64_t t = 0; t < rq.n; t++) lst[cur[slot[t]]++] = rq.v[t];
+    free(cur);
+  }
+  lvec* box = (lvec*)calloc((size_t)T * (size_t)T, sizeof(lvec));  /* (p, key slot) */
+  lvec* res = (lvec*)calloc((size_t)T, sizeof(lvec));
+#pragma omp parallel num_threads(T)
+  {
+    const int t = omp_get_thread_num();
+    char pid[32];
+    for (int64_t p = no * t / T; p < no * (t + 1) / T; p++) {  /* ordinary stream: keyBy(gridID) */
+      int32_t cx, cy;
+      orc_cell_of(ugrid, ox[p], oy[p], &cx, &cy);
+      orc_cell_id(cx, cy, pid);
+      const int64_t s = ss_find(&cells, pid);
+      if (s < 0) continue;  /* no replica carries this key: the coGroup emits nothing */
+      lvec* b = &box[(int64_t)t * T + (int64_t)(str_hash(pid) % (uint64_t)T)];
+      lvec_push(b, p);
+      lvec_push(b, s);
+    }
+#pragma omp barrier
+    for (int s_ = 0; s_ < T; s_++) {  /* key subtask: JoinFunction.join per co-located pair */
+      const lvec* b = &box[(int64_t)s_ * T + t];
+      for (int64_t j = 0; j < b->n; j += 2) {
+        const int64_t p = b->v[j], s = b->v[j + 1];
+        for (int64_t k = off[s]; k < off[s + 1]; k++) {
+          const int64_t q = lst[k];
+          if (approximate || orc_distance(ox[p], oy[p], qx[q], qy[q], metric) <= r) {
+            lvec_push(&res[t], p);
+            lvec_push(&res[t], q);
+          }
+        }
+      }
+    }
+  }
+  for (int64_t i = 0; i < (int64_t)T * T; i++) free(box[i].v);
+  free(box);
+  int64_t cnt = gather_sorted(res, T, out_pairs, cap, 2);
+  free(res); free(off); free(slot); free(lst); free(rq.v); free(rk.v);
+  ss_free(&cells);
+  return cnt;
+}
+
+/* CSVTSVToTSpatial.map on T threads: the chunk's lines split into T contiguous parts (the
+ * source parallelism of a Flink map), each parsed by orc_csv_parse into its own buffers.
+ * Fills x, y, ts in line order; returns the line count (bad lines: first one reported). */
+int64_t orc_csv_parse_mt(const char* text, int64_t len, char delim, const int32_t* want, double* x, double* y,
+                         int64_t* ts, int64_t cap, int nthreads, int64_t* bad_line, int32_t* bad_kind) {
+  const int T = nthreads < 1 ? 1 : nthreads;
+  int64_t* cut = (int64_t*)malloc(8 * (size_t)(T + 1));
+  cut[0] = 0;
+  for (int t = 1; t < T; t++) {  /* part boundaries after a '\n' */
+    int64_t p = len * t / T;
+    if (p < cut[t - 1]) p = cut[t - 1];
+    if (p > 0)
+      while (p < len && text[p - 1] != '\n') ++p;
+    cut[t] = p;
+  }
+  cut[T] = len;
+  int64_t* nl = (int64_t*)calloc((size_t)T + 1, 8);
+  int64_t* bl = (int64_t*)malloc(8 * (size_t)T);
+  int32_t* bk = (int32_t*)malloc(4 * (size_t)T);
+#pragma omp parallel num_threads(T)
+  {  /* count lines per part, then parse into the part's slice */
+    const int t = omp_get_thread_num();
+    int64_t c = 0;
+    for (int64_t i = cut[t]; i < cut[t + 1]; i++) c += text[i] == '\n';
+    if (cut[t + 1] > cut[t] && text[cut[t + 1] - 1] != '\n') c++;
+    nl[t + 1] = c;
+#pragma omp barrier
+#pragma omp single
+    for (int u = 0; u < T; u++) nl[u + 1] += nl[u];
+    const int64_t o = nl[t], m = nl[t + 1] - nl[t];
+    if (m > 0 && o + m <= cap) {
+      char* oid = (char*)malloc((size_t)(cut[t + 1] - cut[t]) + 16);
+      int64_t* off = (int64_t*)malloc(8 * (size_t)(m + 1));
+      int64_t ol = 0;
+      orc_csv_parse(text + cut[t], cut[t + 1] - cut[t], delim, want, x + o, y + o, oid, cut[t + 1] - cut[t] + 16, off,
+                    &ol, ts + o, m, &bl[t], &bk[t]);
+      free(oid); free(off);
+    } else {
+      bl[t] = -1; bk[t] = 0;
+    }
+  }
+  *bad_line = -1; *bad_kind = 0;
+  for (int t = 0; t < T; t++)
+    if (bl[t] >= 0) { *bad_line = nl[t] + bl[t]; *bad_kind = bk[t]; break; }
+  const int64_t lines = nl[T];
+  free(cut); free(nl); free(bl); free(bk);
+  return lines;
+}

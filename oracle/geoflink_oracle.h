@@ -178,4 +178,29 @@ int64_t orc_csv_parse(const char* text, int64_t len, char delim, const int32_t* 
 #ifdef __cplusplus
 }
 #endif
+
+/* Multi-core CPU baselines (bench.py / tools/bench_workloads.py cpu_baseline lines): the
+ * reference operators as Flink runs them with parallelism nthreads (source subtasks up to the
+ * keyBy(gridID), a hash shuffle of the survivors, key subtasks running the apply) -- the same
+ * results as orc_range_pp / orc_range_ppoly / orc_join_pp (indices ascending, pairs sorted). */
+int64_t orc_range_pp_mt(const orc_grid* g, int64_t n, const double* x, const double* y, int32_t nq,
+                        const double* qx, const double* qy, double r, int approximate, int metric, int nthreads,
+                        int64_t* out_idx, int64_t cap);
+int64_t orc_range_ppoly_mt(const orc_grid* g, int64_t n, const double* x, const double* y, const orc_polygons* P,
+                           double r, int approximate, int metric, int nthreads, int64_t* out_idx, int64_t cap);
+int64_t orc_join_pp_mt(const orc_grid* ugrid, const orc_grid* qgrid, int64_t no, const double* ox, const double* oy,
+                       int64_t nq, const double* qx, const double* qy, double r, int approximate, int metric,
+                       int nthreads, int64_t* out_pairs, int64_t cap);
+int64_t orc_csv_parse_mt(const char* text, int64_t len, char delim, const int32_t* want, double* x, double* y,
+                         int64_t* ts, int64_t cap, int nthreads, int64_t* bad_line, int32_t* bad_kind);
+/* Optimised OpenMP lines (oracle/cpu_scan.c): integer cell classes instead of String keys,
+ * per-thread outputs; the same results as the reference-shaped restatements. */
+int64_t orc_range_pp_omp(const orc_grid* g, int64_t n, const double* x, const double* y, int32_t nq,
+                         const double* qx, const double* qy, double r, int approximate, int metric, int nthreads,
+                         int64_t* out_idx, int64_t cap);
+int64_t orc_range_ppoly_omp(const orc_grid* g, int64_t n, const double* x, const double* y, const orc_polygons* P,
+                            double r, int approximate, int metric, int nthreads, int64_t* out_idx, int64_t cap);
+int64_t orc_join_pp_omp(const orc_grid* grid, int64_t no, const double* ox, const double* oy, int64_t nq,
+                        const double* qx, const double* qy, double r, int metric, int nthreads, int64_t* out_pairs,
+                        int64_t cap);
 #endif

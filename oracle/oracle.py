@@ -8,10 +8,9 @@ oracle/geoflink_oracle.h and DESIGN.md).
 from __future__ import annotations
 
 import ctypes as C
+import math
 import os
 import subprocess
-
-import math
 
 import numpy as np
 
@@ -86,6 +85,24 @@ def lib():
         L.orc_csv_parse.argtypes = [C.c_char_p, i64, C.c_char, P, P, P, C.c_char_p, i64, P, C.POINTER(i64), P, i64,
                                     C.POINTER(i64), C.POINTER(i32)]
         L.orc_csv_parse.restype = i64
+        # multi-core baselines (bench cpu_baseline lines)
+        L.orc_range_pp_mt.argtypes = [C.POINTER(OrcGrid), i64, P, P, i32, P, P, d, C.c_int, C.c_int, C.c_int, P, i64]
+        L.orc_range_pp_mt.restype = i64
+        L.orc_range_pp_omp.argtypes = L.orc_range_pp_mt.argtypes
+        L.orc_range_pp_omp.restype = i64
+        L.orc_range_ppoly_mt.argtypes = [C.POINTER(OrcGrid), i64, P, P, C.POINTER(OrcPolygons), d, C.c_int, C.c_int,
+                                         C.c_int, P, i64]
+        L.orc_range_ppoly_mt.restype = i64
+        L.orc_range_ppoly_omp.argtypes = L.orc_range_ppoly_mt.argtypes
+        L.orc_range_ppoly_omp.restype = i64
+        L.orc_join_pp_mt.argtypes = [C.POINTER(OrcGrid), C.POINTER(OrcGrid), i64, P, P, i64, P, P, d, C.c_int, C.c_int,
+                                     C.c_int, P, i64]
+        L.orc_join_pp_mt.restype = i64
+        L.orc_join_pp_omp.argtypes = [C.POINTER(OrcGrid), i64, P, P, i64, P, P, d, C.c_int, C.c_int, P, i64]
+        L.orc_join_pp_omp.restype = i64
+        L.orc_csv_parse_mt.argtypes = [C.c_char_p, i64, C.c_char, P, P, P, P, i64, C.c_int, C.POINTER(i64),
+                                       C.POINTER(i32)]
+        L.orc_csv_parse_mt.restype = i64
         _lib = L
     return _lib
 
@@ -261,6 +278,58 @@ def join_pp(ugrid, qgrid, ox, oy, qx, qy, r, approximate=False, metric=METRIC_SQ
         if cnt <= cap:
             return 0, out[: 2 * cnt].reshape(-1, 2)
         cap = int(cnt)
+
+
+def _grow(fn, cap, width):
+    while True:
+        out = np.empty(width * max(cap, 1), np.int64)
+        cnt = fn(out, max(cap, 1))
+        if cnt < 0:
+            raise ValueError(f"oracle baseline: status {cnt}")
+        if cnt <= max(cap, 1):
+            return out[: width * cnt].reshape(-1, width) if width > 1 else out[:cnt]
+        cap = int(cnt)
+
+
+def range_pp_mt(g, x, y, qx, qy, r, nthreads, approximate=False, metric=METRIC_SQRT, optimized=False):
+    """orc_range_pp_mt (reference-shaped, Flink parallelism nthreads) or orc_range_pp_omp
+    (optimised OpenMP): ascending indices, = range_pp."""
+    x, y, qx, qy = _f64(x), _f64(y), _f64(np.atleast_1d(qx)), _f64(np.atleast_1d(qy))
+    fn = lib().orc_range_pp_omp if optimized else lib().orc_range_pp_mt
+    return _grow(lambda out, cap: fn(C.byref(g), len(x), _p(x), _p(y), len(qx), _p(qx), _p(qy), float(r),
+                                     int(approximate), int(metric), int(nthreads), _p(out), cap), len(x), 1)
+
+
+def range_ppoly_mt(g, x, y, P: "Polygons", r, nthreads, approximate=False, metric=METRIC_SQRT, optimized=False):
+    x, y = _f64(x), _f64(y)
+    fn = lib().orc_range_ppoly_omp if optimized else lib().orc_range_ppoly_mt
+    return _grow(lambda out, cap: fn(C.byref(g), len(x), _p(x), _p(y), C.byref(P.c), float(r), int(approximate),
+                                     int(metric), int(nthreads), _p(out), cap), len(x), 1)
+
+
+def join_pp_mt(ugrid, qgrid, ox, oy, qx, qy, r, nthreads, metric=METRIC_SQRT, optimized=False):
+    """Sorted pairs[m, 2]: orc_join_pp_mt (reference-shaped) or orc_join_pp_omp (optimised; one
+    grid, exact, r > 0)."""
+    ox, oy, qx, qy = _f64(ox), _f64(oy), _f64(qx), _f64(qy)
+    if optimized:
+        return _grow(lambda out, cap: lib().orc_join_pp_omp(C.byref(ugrid), len(ox), _p(ox), _p(oy), len(qx), _p(qx),
+                                                            _p(qy), float(r), int(metric), int(nthreads), _p(out), cap),
+                     1 << 16, 2)
+    return _grow(lambda out, cap: lib().orc_join_pp_mt(C.byref(ugrid), C.byref(qgrid), len(ox), _p(ox), _p(oy), len(qx),
+                                                       _p(qx), _p(qy), float(r), 0, int(metric), int(nthreads), _p(out),
+                                                       cap), 1 << 16, 2)
+
+
+def csv_parse_mt(text: bytes, delim: str, want, nthreads):
+    """orc_csv_parse on nthreads parts of the chunk (a Flink map with that parallelism) ->
+    (x, y, ts, bad_line, bad_kind)."""
+    n = text.count(b"\n") + (0 if text.endswith(b"\n") or not text else 1)
+    w = np.asarray(want, np.int32)
+    x = np.zeros(n); y = np.zeros(n); t = np.zeros(n, np.int64)
+    bl, bk = C.c_int64(), C.c_int32()
+    lib().orc_csv_parse_mt(text, len(text), delim.encode(), _p(w), _p(x), _p(y), _p(t), n, int(nthreads),
+                           C.byref(bl), C.byref(bk))
+    return x, y, t, bl.value, bk.value
 
 
 def join_ppoly(ugrid, qgrid, ox, oy, P: Polygons, r, approximate=False, metric=METRIC_SQRT):

@@ -32,6 +32,7 @@ METRIC_HYPOT = 1
 FLAG_JOIN_LEGACY = 1
 FLAG_JOIN_COARSE = 2
 FLAG_GEOJSON_WALK = 4
+FLAG_JOIN_STREAM = 8
 (K_KNN_SCAN, K_KNN_SAMPLE, K_KNN_SELECT, K_RANGE_SCAN, K_ASSIGN, K_JOIN_PROBE, K_RANGE_TEST, K_JOIN_BUCKET,
  K_KNN_MERGE, K_CSV_PARSE, K_BUCKET, K_JOIN_COMPACT) = range(12)
 

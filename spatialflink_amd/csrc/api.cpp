@@ -257,7 +257,8 @@ extern "C" void gf_ctx_destroy(gf_ctx* ctx) {
   if (ctx->dict) gf_objid_dict_destroy(ctx->dict);
   if (ctx->expand_ticket) hipFree(ctx->expand_ticket);
   if (ctx->expand_status) hipFree(ctx->expand_status);
-  if (ctx->join_ticket) hipFree(ctx->join_ticket);
+  if (ctx->join_gctr) hipFree(ctx->join_gctr);
+  if (ctx->join_hint) hipHostFree(ctx->join_hint);
   for (auto& e : ctx->pending) { hipEventDestroy(e.a); hipEventDestroy(e.b); }
   for (auto e : ctx->pool) hipEventDestroy(e);
   if (ctx->scratch) hipFree(ctx->scratch);
@@ -315,6 +316,7 @@ extern "C" int gf_ctx_set_flag(gf_ctx* ctx, int flag, int value) {
   if (flag == GF_FLAG_JOIN_LEGACY) { ctx->join_legacy = value != 0; return GF_OK; }
   if (flag == GF_FLAG_JOIN_COARSE) { ctx->join_coarse = value != 0; return GF_OK; }
   if (flag == GF_FLAG_GEOJSON_WALK) { ctx->geojson_walk = value != 0; return GF_OK; }
+  if (flag == GF_FLAG_JOIN_STREAM) { ctx->join_stream = value != 0; return GF_OK; }
   return set_err(ctx, GF_ERR_ARG, "gf_ctx_set_flag: unknown flag");
 }
 
@@ -1774,22 +1776,29 @@ static int join_pp_impl(gf_ctx* ctx, const gf_grid* ugrid, const gf_grid* qgrid,
   const int qblk = (int)std::max<int64_t>(1, std::min<int64_t>(nq / 8192 + 1, (int64_t)ctx->num_cus * nq / (no + nq)));
   const int sblocks = (int)std::max<int64_t>(1, std::min<int64_t>(no / 8192 + 1, (int64_t)ctx->num_cus - qblk));
   const int64_t nrows = qn;  // ordinary-side rows
-  // probe grid / task slots: >= the tasks (sum of ceil(row / kJoinTask)) + 8, a multiple of 8
-  const int64_t max_tasks = (no / kJoinTask + nrows + 1 + 8 + 7) / 8 * 8;
-  const int64_t qmat = rowpath ? W * 2 * qblk : 1, mat = rowpath ? nrows * 2 * sblocks : 1;  // kHistSplit = 2
+  // experiment: only the query side bucketed, the ordinary points streamed (fine path)
+  const bool stream = rowpath && f > 1 && ctx->join_stream;
+  const int64_t qmat = rowpath ? W * 2 * qblk : 1, mat = rowpath && !stream ? nrows * 2 * sblocks : 1;  // kHistSplit = 2
   size_t o_cat = ar.take<uint32_t>(qmat + mat), o_cats = ar.take<uint32_t>(qmat + mat + 1);
   size_t o_txy = ar.take<double>(rowpath ? 2 * nq : 1), o_tidx = ar.take<uint32_t>(rowpath ? nq : 1);
   size_t o_roff = ar.take<uint32_t>(nrows + 1), o_toff = ar.take<uint32_t>(nrows + 1);
-  size_t o_gcnt = ar.take<unsigned long long>(2);  // overflow count, total
-  // task output regions, sized from the last join's pairs per point (x1.25 + one round)
-  const double ppp = ctx->join_ppp > 0 ? ctx->join_ppp : 1.0;
-  int64_t tcap = (int64_t)std::ceil(1.25 * ppp * kJoinTask) + 2 * kJoinThreads;
-  tcap = std::max<int64_t>(tcap, kJoinTask);
-  // regions of all tasks <= 8 GiB (1G pairs: their u32 offsets cannot wrap); denser windows spill
-  // to the overflow run
-  tcap = std::min<int64_t>(tcap, std::max<int64_t>(kJoinTask, ((int64_t)1 << 33) / 8 / std::max<int64_t>(max_tasks, 1)));
-  size_t o_tpairs = ar.take<uint64_t>(rowpath ? max_tasks * tcap : 1), o_tcnt = ar.take<uint32_t>(rowpath ? max_tasks : 1);
-  size_t o_tkoff = ar.take<uint32_t>(rowpath ? max_tasks + 1 : 1);
+  size_t o_gcnt = ar.take<unsigned long long>(2);  // -, total
+  // output (JoinOut): the persistent probe's waves, one chunk each at a time, sized from the last
+  // join's pairs per point so that a window takes ~8 chunks per wave: few atomics, small holes
+  const int64_t probe_blocks = std::max(8, ctx->num_cus / 8 * 8);
+  const int64_t nwaves = probe_blocks * (kJoinThreads / 64);
+  // pairs per point of the last join: its exact count (sync) or the fix-up's pinned copy (async)
+  double ppp = ctx->join_ppp > 0 ? ctx->join_ppp : 1.0;
+  if (ctx->join_hint && ctx->join_hint_no > 0) {
+    const unsigned long long h = *(volatile unsigned long long*)ctx->join_hint;
+    if (h > 0) ppp = (double)h / (double)ctx->join_hint_no;
+  }
+  int64_t chunk = 256;
+  while (chunk < 65536 && (double)chunk * nwaves * 8 < ppp * (double)no) chunk <<= 1;
+  size_t o_spill = ar.take<uint64_t>(rowpath ? nwaves * chunk : 1);
+  size_t o_tb = ar.take<uint64_t>(nwaves), o_tf = ar.take<uint32_t>(nwaves);
+  size_t o_hs = ar.take<uint64_t>(nwaves + 1), o_hp = ar.take<uint64_t>(nwaves + 2);
+  size_t o_ss = ar.take<uint64_t>(nwaves + 2), o_sp = ar.take<uint64_t>(nwaves + 3), o_fc = ar.take<uint32_t>(2);
   size_t o_soxy = ar.take<double>(rowpath ? 2 * no : 1), o_soidx = ar.take<uint32_t>(rowpath ? no : 1);
   char* base = (char*)ctx_scratch(ctx, ar.off, &st);
   if (st) return st;
@@ -1798,10 +1807,16 @@ static int join_pp_impl(gf_ctx* ctx, const gf_grid* ugrid, const gf_grid* qgrid,
   auto F64 = [&](size_t o) { return (double*)(base + o); };
   hipStream_t s = ctx->stream;
   if (rowpath) {
-    if (!ctx->join_ticket) {  // the probe's ticket (its last block resets it)
-      GF_HIP_CHECK(ctx, hipMalloc(&ctx->join_ticket, sizeof(uint32_t)));
-      GF_HIP_CHECK(ctx, hipMemset(ctx->join_ticket, 0, sizeof(uint32_t)));
+    if (!ctx->join_gctr) {  // the output counter (the fix-up resets it) and the size hint
+      GF_HIP_CHECK(ctx, hipMalloc(&ctx->join_gctr, sizeof(unsigned long long)));
+      GF_HIP_CHECK(ctx, hipMemset(ctx->join_gctr, 0, sizeof(unsigned long long)));
+      void* h = nullptr;
+      if (gf_pinned_alloc(sizeof(unsigned long long), &h) == GF_OK) {
+        ctx->join_hint = (unsigned long long*)h;
+        *ctx->join_hint = 0ull;
+      }
     }
+    ctx->join_hint_no = no;
     JoinQueryArgs q{};
     q.qx = qry->x; q.qy = qry->y; q.nq = nq;
     q.minX = qgrid->minX; q.minY = qgrid->minY; q.cl = qgrid->cellLength; q.qn = (int32_t)qn;
@@ -1815,19 +1830,22 @@ static int join_pp_impl(gf_ctx* ctx, const gf_grid* ugrid, const gf_grid* qgrid,
     j.qn = (int32_t)qn; j.c = c; j.q_off = U32(o_off);
     j.sqx = F64(o_sqx); j.sqy = F64(o_sqy); j.sqcx = I32(o_sqcx); j.sqcy = I32(o_sqcy); j.sqidx = U32(o_sqi);
     j.approx = approximate != 0; j.metric = metric; j.r = r; j.s_r = s_prefilter(r, 0);
-    j.nblk = sblocks; j.nrows = (int32_t)nrows;
+    j.nblk = stream ? 0 : sblocks; j.nrows = stream ? 0 : (int32_t)nrows;
     j.row_mat = U32(o_cat) + qmat; j.row_mat_scan = U32(o_cats) + qmat; j.mat_base = (uint32_t)nq;
     j.row_off_w = U32(o_roff); j.row_off = U32(o_roff); j.task_off_w = U32(o_toff); j.task_off = U32(o_toff);
     j.soxy = (double*)(base + o_soxy); j.soidx = U32(o_soidx);
     unsigned long long* cnt2 = (unsigned long long*)(base + o_gcnt);
-    j.tpairs = (uint2*)(base + o_tpairs);
-    j.task_cap = (uint32_t)tcap;
-    j.task_cnt = U32(o_tcnt);
-    j.nslots = (uint32_t)max_tasks; j.ticket = ctx->join_ticket; j.tkoff = U32(o_tkoff);
-    j.ovf_count = cnt2;
-    j.pairs = pairs;
-    j.cap = pairs ? (uint64_t)std::max<int64_t>(cap, 0) : 0;
-    j.pairs_aligned = ((uintptr_t)pairs & 7) == 0;
+    JoinOut& o = j.out;
+    o.pairs = pairs;
+    o.cap = pairs ? (uint64_t)std::max<int64_t>(cap, 0) : 0;
+    o.aligned = ((uintptr_t)pairs & 7) == 0;
+    o.chunk = (uint32_t)chunk;
+    o.spill = (uint2*)(base + o_spill);
+    o.spill_cap = (uint64_t)(nwaves * chunk);
+    o.gctr = ctx->join_gctr;
+    o.tail_base = (uint64_t*)(base + o_tb);
+    o.tail_fill = U32(o_tf);
+    o.nwaves = (uint32_t)nwaves;
     j.f = f; j.fs = (double)f / ugrid->cellLength;
     j.lds_budget = join_probe_budget(nq, qn, c, f);
     // (1) row histograms of both sides, (2) one scan of both matrices, (3) write-combined row
@@ -1840,13 +1858,20 @@ static int join_pp_impl(gf_ctx* ctx, const gf_grid* ugrid, const gf_grid* qgrid,
     ctx->expand_base += (unsigned long long)scan1_blocks(qmat + mat);
     GF_HIP_CHECK(ctx, launch_join_rows(ctx, j, q, 1));
     GF_HIP_CHECK(ctx, launch_join_rows(ctx, j, q, 2));
-    GF_HIP_CHECK(ctx, launch_join_rows(ctx, j, q, 3));
-    JoinCompactArgs k{};
-    k.tpairs = j.tpairs; k.task_cap = j.task_cap; k.task_cnt = j.task_cnt; k.task_off = U32(o_tkoff);
-    k.ntask = (uint32_t)max_tasks;
-    k.ovf_count = cnt2; k.pairs = pairs; k.cap = j.cap; k.pairs_aligned = j.pairs_aligned;
-    k.total = total_out ? total_out : cnt2 + 1;
-    GF_HIP_CHECK(ctx, launch_join_compact(ctx, k));
+    if (stream) {
+      j.out.nwaves = (uint32_t)nwaves;  // the stream grid: kBlock-thread blocks, same wave count
+      GF_HIP_CHECK(ctx, launch_join_stream(ctx, j));
+    } else {
+      GF_HIP_CHECK(ctx, launch_join_rows(ctx, j, q, 3));
+    }
+    JoinFixup fx{};
+    fx.o = j.out;
+    fx.total = total_out ? total_out : cnt2 + 1;
+    fx.hint = ctx->join_hint;
+    fx.hole_start = (uint64_t*)(base + o_hs); fx.hole_pref = (uint64_t*)(base + o_hp);
+    fx.seg_start = (uint64_t*)(base + o_ss); fx.seg_pref = (uint64_t*)(base + o_sp);
+    fx.counts = U32(o_fc);
+    GF_HIP_CHECK(ctx, launch_join_fixup(ctx, fx));
     if (total_out) {  // the caller reads *total_out stream-ordered
       ctx->join_async_done = 1;
       return GF_OK;

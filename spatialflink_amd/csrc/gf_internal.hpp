@@ -35,9 +35,10 @@ struct gf_ctx {
   int num_cus = 256;
   int join_legacy = 0;  // testing: force the original (unbucketed) join probe
   int join_coarse = 0;  // testing: the row path without sub-cells
+  int join_stream = 0;  // experiment: the fine path's streaming probe (query side bucketed only)
   int geojson_walk = 0; // testing: every GeoJSON line takes the member-by-member walk
   int join_async_done = 0;  // gf_join_pp_async: the packing kernel wrote the count
-  double join_ppp = 0.0;  // pairs per ordinary point of the last join (sizes the task regions)
+  double join_ppp = 0.0;  // pairs per ordinary point of the last join (sizes the output chunks)
   hipStream_t aux = nullptr;  // kNN depth 3: odd windows' launches (created on first use)
   gf_objid_dict* dict = nullptr;  // the context's default objID dictionary (created on first use)
   // gf_bitmap_to_indices_async: block tickets + look-back status (grown on demand)
@@ -46,7 +47,9 @@ struct gf_ctx {
   unsigned long long* expand_status = nullptr;
   int64_t expand_status_cap = 0;
   uint32_t expand_epoch = 0;
-  uint32_t* join_ticket = nullptr;  // row-bucketed join: the probe's ticket (zero between calls)
+  unsigned long long* join_gctr = nullptr;  // row-bucketed join: reserved output positions (zero between calls)
+  unsigned long long* join_hint = nullptr;  // mapped pinned: the pair count of the last join (async too)
+  int64_t join_hint_no = 0;                 // ordinary points of that join
 };
 
 // objID dictionary (objid.cpp): device hash table + arena, batch buffers, host mirror for decode
@@ -498,6 +501,24 @@ hipError_t launch_join_probe(gf_ctx* ctx, const JoinArgs& a, int write_pass, int
 constexpr int kJoinTask = 8192;      // ordinary points per probe task (part of one row)
 constexpr int kJoinThreads = 1024;   // two probe blocks per CU when the staged rows fit 80 KB
 constexpr int kJoinMaxRows = 16;     // staged query rows (2c+1) per task
+// Join output (k_join.hip).  Pairs go straight to the caller's buffer: every wave of the
+// (persistent) probe owns one chunk of `chunk` positions at a time, reserved with one atomic on
+// gctr; its last chunk stays partly filled, so the reserved space [0, G) holds one hole per wave
+// and T = G - (the holes) pairs.  The fix-up moves the pairs stored at positions >= T into the
+// holes below T: dense [0, T), in an unspecified order.  Positions >= cap live in `spill`
+// (sized for every wave's hole), so a window whose T fits cap is complete.
+struct JoinOut {
+  uint32_t* pairs;           // caller's [2 * cap]
+  uint64_t cap;
+  int aligned;               // 8-byte aligned: one 8-byte store per pair
+  uint32_t chunk;            // positions per chunk
+  uint2* spill;              // [spill_cap]: positions cap, cap + 1, ...
+  uint64_t spill_cap;
+  unsigned long long* gctr;  // reserved positions (0 between calls: the fix-up resets it)
+  uint64_t* tail_base;       // [nwaves] base of each wave's last chunk (~0: none)
+  uint32_t* tail_fill;       // [nwaves]
+  uint32_t nwaves;
+};
 struct JoinRowArgs {
   const double* ox;
   const double* oy;
@@ -524,41 +545,13 @@ struct JoinRowArgs {
   const uint32_t* task_off; // same buffer, read by the probe
   double* soxy;             // [2*no] row-bucketed ordinary xy
   uint32_t* soidx;          // [no]
-  // output: task t writes its pairs to the private region tpairs[t * task_cap ...]; a round
-  // that does not fit goes to the overflow: the caller's buffer filled from its END (pair i
-  // of the overflow at slot cap-1-i), one atomic on ovf_count per such round
-  uint2* tpairs;
-  uint32_t task_cap;
-  uint32_t* task_cnt;       // [max_tasks] pairs in each task's region
-  uint32_t nslots;          // max_tasks (the probe grid)
-  uint32_t* ticket;         // probe blocks done (the last one scans task_cnt; reset to 0 by it)
-  uint32_t* tkoff;          // [max_tasks + 1] exclusive scan of task_cnt (by the last probe block)
-  unsigned long long* ovf_count;
-  uint32_t* pairs;          // caller's [2 * cap]
-  uint64_t cap;
-  int pairs_aligned;        // 8-byte aligned: one 8-byte store per pair
+  JoinOut out;              // pairs straight to the caller's buffer in per-wave chunks
   int lds_budget;
   // fine sub-cells (k_join.hip, "fine path"): f > 1 splits every cell into f x f sub-cells of
   // side cl / f > r, the query side is sorted by sub-cell and q_off indexes sub-cells
   // ((f*(qn+2))^2 + 1 entries); f == 1: q_off indexes cells as before
   int32_t f;
   double fs;                // f / cl
-};
-// Dense output [0, total): the task regions packed in task order (offsets = exclusive scan
-// of task_cnt, task_off[ntask] = their sum), then the overflow moved down from the buffer's
-// end.  The probe already stores (ordinary idx, query idx).  *total = pairs found (also when
-// > cap: nothing is then valid).
-struct JoinCompactArgs {
-  const uint2* tpairs;
-  uint32_t task_cap;
-  const uint32_t* task_cnt;
-  const uint32_t* task_off;  // [ntask + 1]
-  uint32_t ntask;
-  const unsigned long long* ovf_count;
-  uint32_t* pairs;
-  uint64_t cap;
-  int pairs_aligned;
-  unsigned long long* total;
 };
 __device__ __forceinline__ void join_store(uint32_t* pairs, int aligned, uint64_t pos, uint2 v) {
   if (aligned) {
@@ -572,7 +565,19 @@ __device__ __forceinline__ uint2 join_load(const uint32_t* pairs, int aligned, u
   if (aligned) return reinterpret_cast<const uint2*>(pairs)[pos];
   return make_uint2(pairs[2 * pos], pairs[2 * pos + 1]);
 }
-hipError_t launch_join_compact(gf_ctx* ctx, const JoinCompactArgs& a);
+// The join's fix-up (k_join.hip): the pairs stored at positions >= T moved into the holes < T.
+struct JoinFixup {
+  JoinOut o;
+  unsigned long long* total;  // the pair count T (device or mapped pinned memory)
+  unsigned long long* hint;   // mapped pinned: T again, the next call's chunk-size hint
+  uint64_t* hole_start;       // [nwaves] holes below T, by position
+  uint64_t* hole_pref;        // [nwaves + 1] their exclusive prefix of lengths
+  uint64_t* seg_start;        // [nwaves + 1] stored runs in [T, G), by position
+  uint64_t* seg_pref;         // [nwaves + 2]
+  uint32_t* counts;           // [2] holes below T, runs above T
+};
+hipError_t launch_join_fixup(gf_ctx* ctx, const JoinFixup& f);
+hipError_t launch_join_stream(gf_ctx* ctx, const JoinRowArgs& a);
 constexpr int kJoinReg = 3;  // pairs per ordinary point kept in registers by the probe
 // LDS bytes of one staged query row with m points: u16 bucket offsets, xy
 __host__ __device__ inline size_t join_row_lds_bytes(int64_t W, uint32_t m) {

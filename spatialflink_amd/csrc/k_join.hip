@@ -456,7 +456,6 @@ __global__ __launch_bounds__(kScatThreads) void join_sort_finish_kernel(JoinRowA
     if (threadIdx.x == 0) {
       a.row_off_w[nr] = Ms[tot_idx] - a.mat_base;
       a.task_off_w[nr] = total;
-      *a.ovf_count = 0ull;
     }
     return;
   }
@@ -537,8 +536,6 @@ struct JoinProbeHdr {
   int32_t row, fit;
   uint32_t need;     // staged bytes of the task's query rows
   uint32_t beg, end;
-  uint32_t used;     // pairs placed in the task's region so far (wave reservations)
-  uint32_t fit_end;  // end of the last reservation that fit the region
   uint32_t wsum[kJoinThreads / 64];
   QRow rows[kJoinMaxRows];
   uint32_t g0;       // fine path: sorted index of the first staged query point
@@ -604,52 +601,70 @@ struct JoinLane {  // this lane's ordinary point
   uint32_t pidx;
 };
 
+__device__ __forceinline__ uint64_t join_uni64(uint64_t v) {
+  return (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v) |
+         ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32)) << 32);
+}
+
+// A wave's output chunk (wave-uniform): positions [base, base + chunk) of the reserved space,
+// `fill` of them used (fill == chunk: take a new one at the next store).
+struct JoinWaveOut {
+  uint64_t base;
+  uint32_t fill;
+};
+__device__ __forceinline__ void join_vstore(const JoinOut& o, uint64_t pos, uint2 v) {
+  if (pos < o.cap) join_store(o.pairs, o.aligned, pos, v);
+  else if (pos - o.cap < o.spill_cap) o.spill[pos - o.cap] = v;
+}
+// The wave stores entries get(0 .. cnt) (cnt wave-uniform) at its chunk's next positions,
+// taking new chunks (one device atomic each) as they fill: consecutive lanes, consecutive slots.
+template <class Get>
+__device__ __forceinline__ void join_emit(const JoinOut& o, JoinWaveOut& w, uint32_t cnt, Get get) {
+  const uint32_t lane = threadIdx.x & 63;
+  uint32_t done = 0;
+  while (done < cnt) {  // wave-uniform
+    if (w.fill >= o.chunk) {
+      unsigned long long b = 0;
+      if (lane == 0) b = atomicAdd(o.gctr, (unsigned long long)o.chunk);
+      w.base = join_uni64(b);
+      w.fill = 0;
+    }
+    const uint32_t take = cnt - done < o.chunk - w.fill ? cnt - done : o.chunk - w.fill;
+    for (uint32_t i = lane; i < take; i += 64) join_vstore(o, w.base + w.fill + i, get(done + i));
+    w.fill += take;
+    done += take;
+  }
+}
+// the wave's last chunk, for the fix-up (hole = [base + fill, base + chunk))
+__device__ __forceinline__ void join_emit_close(const JoinOut& o, const JoinWaveOut& w, uint32_t wslot) {
+  if ((threadIdx.x & 63) == 0) {
+    o.tail_base[wslot] = w.fill <= o.chunk && w.base != ~0ull ? w.base : ~0ull;
+    o.tail_fill[wslot] = w.fill;
+  }
+}
+
 // The wave's pair buffer in LDS: hits are appended in ballot order (one mbcnt per hit round,
-// the count stays in a scalar register); past kJoinWaveBuf - 64 the wave reserves a run in the
-// task's region (one LDS atomic) -- or, when the region is full, in the overflow at the end of
-// the caller's buffer (one device atomic) -- and copies the buffer out with coalesced stores.
+// the count stays in a scalar register); past kJoinWaveBuf - 64 the wave writes the buffer out
+// (join_emit: coalesced stores into its output chunk) with each query slot mapped to its query
+// index (from LDS when the fine path staged it, else an L2 gather of the sorted query side).
 struct JoinWaveBuf {
   uint2* buf;
   uint32_t cnt;
-  __device__ __forceinline__ void flush(const JoinRowArgs& a, JoinProbeHdr& hd, uint2* region) {
-    const uint32_t lane = threadIdx.x & 63;
-    uint32_t wb = 0;
-    if (lane == 0) wb = atomicAdd(&hd.used, cnt);
-    wb = join_uni(wb);
-    // the query slot becomes the query index here: from LDS when the fine path staged it,
-    // else an L2 gather of the sorted query side
+  __device__ __forceinline__ void flush(const JoinRowArgs& a, JoinProbeHdr& hd, JoinWaveOut& wo) {
     const uint32_t g0 = hd.g0, gm = join_uni(hd.gm);
     const uint32_t* lq = reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(&hd) + hd.lqidx);
-    auto qidx = [&](uint32_t slot) { return slot - g0 < gm ? lq[slot - g0] : a.sqidx[slot]; };
-    if (wb + cnt <= a.task_cap) {
-      if (lane == 0) atomicMax(&hd.fit_end, wb + cnt);
-      if (gm > 0) {  // staged: every slot was mapped at push time (top bit) or lies in the staged range
-        for (uint32_t i = lane; i < cnt; i += 64) {
-          const uint2 v = buf[i];
-          region[wb + i] = make_uint2(v.x, v.y & 0x80000000u ? v.y & 0x7fffffffu : lq[v.y - g0]);
-        }
-      } else {
-        for (uint32_t i = lane; i < cnt; i += 64) {
-          const uint2 v = buf[i];
-          region[wb + i] = make_uint2(v.x, v.y & 0x80000000u ? v.y & 0x7fffffffu : a.sqidx[v.y]);
-        }
-      }
-    } else {
-      unsigned long long ob = 0;
-      if (lane == 0) ob = atomicAdd(a.ovf_count, (unsigned long long)cnt);
-      ob = ((unsigned long long)join_uni((uint32_t)(ob >> 32)) << 32) | join_uni((uint32_t)ob);
-      for (uint32_t i = lane; i < cnt; i += 64) {
-        const uint2 v = buf[i];
-        const uint32_t qi = v.y & 0x80000000u ? v.y & 0x7fffffffu : qidx(v.y);
-        if (ob + i < a.cap) join_store(a.pairs, a.pairs_aligned, a.cap - 1 - (ob + i), make_uint2(v.x, qi));
-      }
-    }
+    const uint2* b = buf;
+    join_emit(a.out, wo, cnt, [&](uint32_t i) {
+      const uint2 v = b[i];
+      const uint32_t qi = v.y & 0x80000000u ? v.y & 0x7fffffffu : (v.y - g0 < gm ? lq[v.y - g0] : a.sqidx[v.y]);
+      return make_uint2(v.x, qi);
+    });
     cnt = 0;
   }
   // one round's hits: hit i of this lane (candidate q[i]) goes after all hits of rounds < i
   template <int R>
   __device__ __forceinline__ void push(const bool (&hit)[R], uint32_t p, const uint32_t (&q)[R], const JoinRowArgs& a,
-                                       JoinProbeHdr& hd, uint2* region) {
+                                       JoinProbeHdr& hd, JoinWaveOut& wo) {
     uint64_t m[R];
     uint64_t any = 0;
 #pragma unroll
@@ -665,7 +680,7 @@ struct JoinWaveBuf {
         buf[cnt + __builtin_amdgcn_mbcnt_hi((uint32_t)(m[i] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m[i], 0u))] =
             make_uint2(p, q[i]);
       cnt += (uint32_t)__popcll(m[i]);
-      if (cnt > kJoinWaveBuf - 64) flush(a, hd, region);
+      if (cnt > kJoinWaveBuf - 64) flush(a, hd, wo);
     }
   }
 };
@@ -678,7 +693,7 @@ struct JoinWaveBuf {
 template <int MODE, bool LDS, bool SLOW>
 __device__ __forceinline__ void join_lane_run(const JoinRowArgs& a, const double2* lxy, uint32_t gb, uint32_t tb,
                                               uint32_t te, const JoinLane& ln, JoinWaveBuf& wbuf, JoinProbeHdr& hd,
-                                              uint2* region) {
+                                              JoinWaveOut& wo) {
   const uint32_t len = te - tb;
   auto test = [&](bool act, uint32_t t, double2 q) {
     bool in = act;
@@ -716,7 +731,7 @@ __device__ __forceinline__ void join_lane_run(const JoinRowArgs& a, const double
     }
 #pragma unroll
     for (int i = 0; i < R; ++i) hit[i] = test(act[i], t[i], v[i]);
-    wbuf.push<R>(hit, ln.pidx, q, a, hd, region);
+    wbuf.push<R>(hit, ln.pidx, q, a, hd, wo);
   }
 }
 
@@ -727,7 +742,7 @@ __device__ __forceinline__ void join_lane_run(const JoinRowArgs& a, const double
 template <int MODE, bool LDS, int R>
 __device__ __forceinline__ void join_fine_walk(const JoinRowArgs& a, const double2* lxy, uint32_t g0,
                                                const uint32_t (&b)[3], const uint32_t (&e)[3], const JoinLane& ln,
-                                               JoinWaveBuf& wbuf, JoinProbeHdr& hd, uint2* region) {
+                                               JoinWaveBuf& wbuf, JoinProbeHdr& hd, JoinWaveOut& wo) {
   const uint32_t L0 = e[0] - b[0], L1 = L0 + (e[1] - b[1]), L2 = L1 + (e[2] - b[2]);
   const uint32_t d0 = b[0], d1 = b[1] - L0, d2 = b[2] - L1;  // run s: index = k + d_s (mod 2^32)
   for (uint32_t k = 0; __ballot(k < L2) != 0; k += R) {
@@ -757,14 +772,10 @@ __device__ __forceinline__ void join_fine_walk(const JoinRowArgs& a, const doubl
       else ok = a.metric == 0 ? dx * dx + dy * dy <= a.s_r : fdlibm_hypot(dx, dy) <= a.r;
       hit[i] = k + i < L2 && ok;
     }
-    wbuf.push<R>(hit, ln.pidx, q, a, hd, region);
+    wbuf.push<R>(hit, ln.pidx, q, a, hd, wo);
   }
 }
 
-// write-through (agent-scope) store: read by the last block of the launch on another XCD
-__device__ __forceinline__ void store_u32_wt(uint32_t* p, uint32_t v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 
 // One block per task = <= kJoinTask ordinary points of one cell row.  The 2c+1 query rows
 // around it are staged in LDS (u16 bucket offsets per column + xy), then the task's points are
@@ -773,8 +784,8 @@ __device__ __forceinline__ void store_u32_wt(uint32_t* p, uint32_t v) {
 // replicated-key match, true cell within Chebyshev c) with the exact distance test.  Sorting
 // makes the lanes' runs overlap, so the per-round LDS reads hit few distinct addresses, and
 // the rounds per row are the longest run among ~8 columns instead of the union of all of them.
-// Pairs go through the wave's LDS buffer into the task's private region in coalesced runs;
-// join_compact_kernel packs the regions.
+// Pairs go through the wave's LDS buffer into its output chunk in coalesced runs (join_emit);
+// join_fixup_* makes the output dense.
 //
 // FINE (the fine path, f > 1: c == 1, exact distances, one grid for both sides, cl/f > r): a
 // pair needs d <= r, so its points lie in sub-cells at most one apart on each axis (sub-cells are
@@ -786,7 +797,8 @@ __device__ __forceinline__ void store_u32_wt(uint32_t* p, uint32_t v) {
 // edge lane through the cell path over global memory: ~2 such waves per task, each a chain of
 // dependent global round trips the whole task waited for: probe 282 -> 225 us without it.)
 template <int MODE, int FINE>  // MODE 0: exact, metric 0 (squared-distance bound); 1: approximate or hypot
-__device__ __forceinline__ void join_probe_task(const JoinRowArgs& a, uint32_t task, char* const lds_base) {
+__device__ __forceinline__ void join_probe_task(const JoinRowArgs& a, uint32_t task, char* const lds_base,
+                                                JoinWaveOut& wo) {
   JoinProbeHdr& hd = *reinterpret_cast<JoinProbeHdr*>(lds_base);
   char* const lds = lds_base + kJoinHdrBytes;
   QRow* const rows = hd.rows;
@@ -796,8 +808,6 @@ __device__ __forceinline__ void join_probe_task(const JoinRowArgs& a, uint32_t t
   // the task's row: the one j with task_off[j] <= task < task_off[j+1] (a parallel search --
   // one round of loads, where a serial binary search costs ~10 dependent ones)
   if (threadIdx.x == 0) {
-    hd.used = 0u;
-    hd.fit_end = 0u;
     hd.need = 0u;
     hd.fit = 1;
     hd.gm = 0u;
@@ -950,7 +960,6 @@ __device__ __forceinline__ void join_probe_task(const JoinRowArgs& a, uint32_t t
 
   const uint32_t lane = threadIdx.x & 63;
   const int32_t qnn = a.qn, cc = (int32_t)c;
-  uint2* const region = a.tpairs + (size_t)task * a.task_cap;
   JoinWaveBuf wbuf{reinterpret_cast<uint2*>(lcx) + (threadIdx.x >> 6) * kJoinWaveBuf, 0u};
   // the next wave-step's points are fetched before this step's candidates are walked;
   // branch-free (a lane past the end re-reads entry 0): a load under a branch is waited on at the
@@ -986,7 +995,7 @@ __device__ __forceinline__ void join_probe_task(const JoinRowArgs& a, uint32_t t
             e[k] = valid ? lo[(sub + k) * rs + col + 2] : 0u;
           }
           const double2* lxy = reinterpret_cast<const double2*>(lds + (f + 2) * fine_rb);
-          join_fine_walk<MODE, true, 4>(a, lxy, g0, b, e, ln, wbuf, hd, region);
+          join_fine_walk<MODE, true, 4>(a, lxy, g0, b, e, ln, wbuf, hd, wo);
         } else {
           const int64_t fy0 = (int64_t)f * (cy + 1) - 1;
 #pragma unroll
@@ -995,7 +1004,7 @@ __device__ __forceinline__ void join_probe_task(const JoinRowArgs& a, uint32_t t
             b[k] = valid ? qo[col - 1] - g0 : 0u;
             e[k] = valid ? qo[col + 2] - g0 : 0u;
           }
-          join_fine_walk<MODE, false, 4>(a, nullptr, g0, b, e, ln, wbuf, hd, region);
+          join_fine_walk<MODE, false, 4>(a, nullptr, g0, b, e, ln, wbuf, hd, wo);
         }
       }
       continue;
@@ -1013,106 +1022,258 @@ __device__ __forceinline__ void join_probe_task(const JoinRowArgs& a, uint32_t t
         const uint32_t tb = valid ? lo16[kb] : 0u, te = valid ? lo16[ke] : 0u;
         // clamped buckets 0 (column -1) and W-1 (column qn): [0, lo16[1]) and [lo16[W-1], ...)
         const bool slow = te > tb && (brow || kb == 0 || ke == (int32_t)W);
-        if (__ballot(slow) != 0) join_lane_run<MODE, true, true>(a, lxy, gb, tb, te, ln, wbuf, hd, region);
-        else join_lane_run<MODE, true, false>(a, lxy, gb, tb, te, ln, wbuf, hd, region);
+        if (__ballot(slow) != 0) join_lane_run<MODE, true, true>(a, lxy, gb, tb, te, ln, wbuf, hd, wo);
+        else join_lane_run<MODE, true, false>(a, lxy, gb, tb, te, ln, wbuf, hd, wo);
       } else {
         const uint32_t* qo = a.q_off + (size_t)(ry + 1) * W;
         const uint32_t tb = valid ? qo[kb] - gb : 0u, te = valid ? qo[ke] - gb : 0u;
         const bool slow = te > tb && (brow || kb == 0 || ke == (int32_t)W);
-        if (__ballot(slow) != 0) join_lane_run<MODE, false, true>(a, nullptr, gb, tb, te, ln, wbuf, hd, region);
-        else join_lane_run<MODE, false, false>(a, nullptr, gb, tb, te, ln, wbuf, hd, region);
+        if (__ballot(slow) != 0) join_lane_run<MODE, false, true>(a, nullptr, gb, tb, te, ln, wbuf, hd, wo);
+        else join_lane_run<MODE, false, false>(a, nullptr, gb, tb, te, ln, wbuf, hd, wo);
       }
     }
   }
-  if (wbuf.cnt > 0) wbuf.flush(a, hd, region);
-  __syncthreads();
-  if (threadIdx.x == 0) store_u32_wt(&a.task_cnt[task], hd.fit_end);
+  if (wbuf.cnt > 0) wbuf.flush(a, hd, wo);
+  __syncthreads();  // the task's LDS is reused by the next one
 }
 
+// Persistent: gridDim blocks (one per CU, the staged rows fill its LDS) take the tasks in an
+// XCD-aware order -- workgroups go round-robin to the 8 XCDs, so XCD x gets the consecutive
+// tasks [x * per, (x + 1) * per): neighbouring row tasks stage the same query rows, and they meet
+// in the same L2.  Each wave keeps one output chunk across its tasks (join_emit), closed at exit.
 template <int MODE, int FINE>
 __global__ __launch_bounds__(kJoinThreads) void join_row_probe_kernel(JoinRowArgs a) {
   // every LDS variable lives in the dynamic region, header first (a static __shared__ block in
   // front would shift the dynamic base off 16 B: misaligned ds_read_b128 of the staged xy)
   extern __shared__ __attribute__((aligned(16))) char lds_base[];
-  JoinProbeHdr& hd = *reinterpret_cast<JoinProbeHdr*>(lds_base);
-  // XCD-aware task order: workgroups go round-robin to the 8 XCDs, so XCD x gets the
-  // consecutive tasks [x * per, (x + 1) * per) -- neighbouring row tasks stage the same query
-  // rows, and they now meet in the same L2.  The grid is >= ntask + 8 (host); slots past ntask
-  // are zeroed by the block of the same index.
   const uint32_t ntask = a.task_off[a.nrows];
-  if (blockIdx.x >= ntask && threadIdx.x == 0) store_u32_wt(&a.task_cnt[blockIdx.x], 0u);
-  const uint32_t per = (ntask + 7) / 8;
-  const uint32_t task = (blockIdx.x & 7u) * per + (blockIdx.x >> 3);
-  if ((blockIdx.x >> 3) < per && task < ntask) join_probe_task<MODE, FINE>(a, task, lds_base);
-  // the last block to finish scans the task counts into the packing offsets (no scan launch);
-  // each block's count was stored write-through and drained before its ticket
-  if (threadIdx.x == 0) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    hd.fit = atomicAdd(a.ticket, 1u) == gridDim.x - 1 ? 1 : 0;
+  const uint32_t per = (ntask + 7) / 8, xcd = blockIdx.x & 7u, nb = (gridDim.x + 7 - xcd) / 8;
+  JoinWaveOut wo{~0ull, a.out.chunk};
+  for (uint32_t k = blockIdx.x >> 3; k < per; k += nb) {  // block-uniform
+    const uint32_t task = xcd * per + k;
+    if (task < ntask) join_probe_task<MODE, FINE>(a, task, lds_base, wo);
   }
-  __syncthreads();
-  if (!hd.fit) return;
-  uint32_t carry = 0;
-  for (uint32_t b = 0; b < a.nslots; b += kJoinThreads) {  // block-uniform
-    const uint32_t i = b + threadIdx.x;
-    const uint32_t v = i < a.nslots ? __hip_atomic_load(&a.task_cnt[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
-    uint32_t total;
-    const uint32_t ex = join_block_scan<kJoinThreads>(v, &total, hd.wsum);
-    if (i < a.nslots) a.tkoff[i] = carry + ex;
-    carry += total;
-  }
-  if (threadIdx.x == 0) {
-    a.tkoff[a.nslots] = carry;
-    __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
+  join_emit_close(a.out, wo, blockIdx.x * (kJoinThreads / 64) + (threadIdx.x >> 6));
 }
 
-// Block t < ntask: its output offset = sum of task_cnt[0..t) (a block reduction over <= a few
-// thousand L2-resident counts -- no separate scan launches), then a coalesced copy of the
-// region to [off, off + n) with each pair's query slot mapped to the query index.  Blocks >=
-// ntask handle the overflow, which sits at [cap - n_ovf, cap): its pair i goes to T + i (T =
-// sum of all regions); where [T, T + n_ovf) overlaps the source the pairs are mapped in place,
-// the rest of the target takes the source's remainder (every position read and written by one
-// thread; disjoint from [0, T) whenever T + n_ovf <= cap -- otherwise the call fails anyway).
-__global__ __launch_bounds__(kBlock) void join_compact_kernel(JoinCompactArgs a) {
-  const uint64_t T = a.task_off[a.ntask];
-  if (blockIdx.x < a.ntask) {  // block b copies task b's region to its offset (capacity clipped)
-    const uint64_t off = a.task_off[blockIdx.x];
-    const uint32_t n0 = a.task_cnt[blockIdx.x];
-    const uint32_t n = off >= a.cap ? 0u : (uint32_t)(off + n0 > a.cap ? a.cap - off : n0);
-    const uint2* src = a.tpairs + (size_t)blockIdx.x * a.task_cap;
-    constexpr int kCompactU = 4;  // region loads in flight before the stores
-    for (uint32_t i0 = threadIdx.x; i0 < n; i0 += kBlock * kCompactU) {
-      uint2 v[kCompactU];
+// ---- streaming probe (experiment, GF_FLAG_JOIN_STREAM) --------------------------------------
+// Only the query side is bucketed (sorted by sub-cell, q_off); the ordinary points are read once
+// in input order, one lane each, and every lane walks its 3 x 3 sub-cell neighbourhood straight
+// from the sorted query arrays in global memory (L2 / Infinity Cache gathers: the lanes of a wave
+// hold unrelated points).  The alternative the row-bucketed path is measured against (VERDICT r02
+// "bucket only the query side; stream the ordinary points").  Fine path only (f > 1).
+template <int MODE>
+__global__ __launch_bounds__(kBlock) void join_stream_kernel(JoinRowArgs a) {
+  __shared__ uint2 wbuf[kBlock / 64][kJoinWaveBuf];
+  const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  uint2* const buf = wbuf[wid];
+  uint32_t cnt = 0;
+  JoinWaveOut wo{~0ull, a.out.chunk};
+  const int32_t f = a.f, qn = a.qn;
+  const int64_t fW = (int64_t)f * (qn + 2);
+  auto flush = [&]() {
+    join_emit(a.out, wo, cnt, [&](uint32_t i) {
+      const uint2 v = buf[i];
+      return make_uint2(v.x, a.sqidx[v.y]);
+    });
+    cnt = 0;
+  };
+  const int64_t nwave = (int64_t)gridDim.x * (kBlock / 64);
+  for (int64_t s0 = ((int64_t)blockIdx.x * (kBlock / 64) + wid) * 64; s0 < a.no; s0 += nwave * 64) {  // wave-uniform
+    const int64_t p = s0 + lane;
+    const bool valid = p < a.no;
+    const double px = valid ? a.ox[p] : 0.0, py = valid ? a.oy[p] : 0.0;
+    const int32_t cx = cell_index(px, a.u_minX, a.u_cl), cy = cell_index(py, a.u_minY, a.u_cl);
+    const bool in = valid && cx >= 0 && cy >= 0 && cx < qn && cy < qn;
+    uint32_t b[3] = {0u, 0u, 0u}, e[3] = {0u, 0u, 0u};
+    if (in) {
+      const int32_t col = f * (cx + 1) + join_sub(px, a.u_minX, a.u_cl, cx, a.fs, f);
+      const int32_t srow = f * (cy + 1) + join_sub(py, a.u_minY, a.u_cl, cy, a.fs, f);
 #pragma unroll
-      for (int u = 0; u < kCompactU; ++u) {
-        const uint32_t i = i0 + u * kBlock;
-        v[u] = src[i < n ? i : i0];
-      }
-#pragma unroll
-      for (int u = 0; u < kCompactU; ++u) {
-        const uint32_t i = i0 + u * kBlock;
-        if (i < n) join_store(a.pairs, a.pairs_aligned, off + i, v[u]);
+      for (int k = 0; k < 3; ++k) {
+        const uint32_t* qo = a.q_off + (int64_t)(srow - 1 + k) * fW;
+        b[k] = qo[col - 1];
+        e[k] = qo[col + 2];
       }
     }
-    return;
+    const uint32_t L0 = e[0] - b[0], L1 = L0 + (e[1] - b[1]), L2 = L1 + (e[2] - b[2]);
+    const uint32_t d0 = b[0], d1 = b[1] - L0, d2 = b[2] - L1;
+    constexpr int R = 4;
+    for (uint32_t k = 0; __ballot(k < L2) != 0; k += R) {
+      bool hit[R];
+      uint32_t q[R];
+      double2 v[R];
+#pragma unroll
+      for (int i = 0; i < R; ++i) {
+        const uint32_t kk = k + i;
+        q[i] = kk < L2 ? kk + (kk < L0 ? d0 : (kk < L1 ? d1 : d2)) : 0u;
+        v[i] = kk < L2 ? make_double2(a.sqx[q[i]], a.sqy[q[i]]) : make_double2(0.0, 0.0);
+      }
+#pragma unroll
+      for (int i = 0; i < R; ++i) {
+        const double dx = px - v[i].x, dy = py - v[i].y;
+        const bool ok = MODE == 0 ? dx * dx + dy * dy <= a.s_r : fdlibm_hypot(dx, dy) <= a.r;
+        hit[i] = k + i < L2 && ok;
+      }
+#pragma unroll
+      for (int i = 0; i < R; ++i) {
+        const uint64_t m = __ballot(hit[i]);
+        if (m == 0) continue;
+        if (hit[i])
+          buf[cnt + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] =
+              make_uint2((uint32_t)p, q[i]);
+        cnt += (uint32_t)__popcll(m);
+        if (cnt > kJoinWaveBuf - 64) flush();
+      }
+    }
   }
-  const unsigned long long nov = *a.ovf_count;
-  if (blockIdx.x == a.ntask && threadIdx.x == 0) *a.total = T + nov;
-  if (nov == 0 || T + nov > a.cap) return;
-  const uint64_t lo = a.cap - nov;  // overflow source [lo, cap), target [T, T + nov)
-  const bool apart = lo >= T + nov;
-  for (uint64_t i = (uint64_t)(blockIdx.x - a.ntask) * kBlock + threadIdx.x; i < nov;
-       i += (uint64_t)(gridDim.x - a.ntask) * kBlock) {
-    const uint64_t dst = T + i;
-    const uint64_t src = apart ? lo + i : (dst < lo ? T + nov + i : dst);
-    join_store(a.pairs, a.pairs_aligned, dst, join_load(a.pairs, a.pairs_aligned, src));
+  if (cnt > 0) flush();
+  join_emit_close(a.out, wo, blockIdx.x * (kBlock / 64) + wid);
+}
+
+hipError_t launch_join_stream(gf_ctx* ctx, const JoinRowArgs& a) {
+  KTimer t(ctx, GF_K_JOIN_PROBE);
+  const dim3 g(a.out.nwaves / (kBlock / 64));
+  if (!a.approx && a.metric == 0) hipLaunchKernelGGL(join_stream_kernel<0>, g, dim3(kBlock), 0, ctx->stream, a);
+  else hipLaunchKernelGGL(join_stream_kernel<1>, g, dim3(kBlock), 0, ctx->stream, a);
+  return hipGetLastError();
+}
+
+// ---- the output fix-up ------------------------------------------------------------------------
+// (1) one block: the waves' last chunks sorted by position; their holes; T = G - the holes = the
+// pair count (written to *total; gctr reset to 0 for the next call); the holes below T and the
+// stored runs in [T, G) with their exclusive prefixes.  (2) a grid: stored position k of the runs
+// goes to hole position k (both lists in position order; dst < T <= src, no overlap).
+constexpr int kFixupMax = 8192;  // waves of the probe grid
+__global__ __launch_bounds__(1024) void join_fixup_prep_kernel(JoinFixup f) {
+  __shared__ uint64_t key[kFixupMax];  // chunk index << 20 | hole length (~0: no chunk)
+  __shared__ uint64_t wsum[16];
+  __shared__ unsigned long long s_T;
+  const uint32_t n = f.o.nwaves, C = f.o.chunk, tid = threadIdx.x;
+  uint32_t np = 1;
+  while (np < n) np <<= 1;
+  for (uint32_t i = tid; i < np; i += 1024) {
+    uint64_t k = ~0ull;
+    if (i < n) {
+      const uint64_t b = f.o.tail_base[i];
+      const uint32_t fill = f.o.tail_fill[i];
+      if (b != ~0ull && fill < C) k = (b / C) << 20 | (uint64_t)(C - fill);
+    }
+    key[i] = k;
+  }
+  __syncthreads();
+  for (uint32_t kk = 2; kk <= np; kk <<= 1)  // bitonic sort, ascending
+    for (uint32_t j = kk >> 1; j > 0; j >>= 1) {
+      for (uint32_t i = tid; i < np; i += 1024) {
+        const uint32_t l = i ^ j;
+        if (l > i) {
+          const uint64_t x = key[i], y = key[l];
+          if ((x > y) == ((i & kk) == 0)) { key[i] = y; key[l] = x; }
+        }
+      }
+      __syncthreads();
+    }
+  // hole i: [start_i, start_i + len_i), start_i = (chunk + 1) * C - len_i; total H
+  auto hstart = [&](uint64_t k) { return ((k >> 20) + 1) * (uint64_t)C - (k & 0xFFFFF); };
+  uint64_t h = 0;
+  for (uint32_t i = tid; i < np; i += 1024) h += key[i] == ~0ull ? 0 : (key[i] & 0xFFFFF);
+  for (int o = 32; o > 0; o >>= 1) h += __shfl_xor(h, o, 64);
+  if ((tid & 63) == 0) wsum[tid >> 6] = h;
+  __syncthreads();
+  if (tid == 0) {
+    uint64_t H = 0;
+    for (int w = 0; w < 16; ++w) H += wsum[w];
+    const unsigned long long G = *f.o.gctr;
+    s_T = G - H;
+    *f.total = G - H;
+    if (f.hint) *f.hint = G - H;
+    *f.o.gctr = 0ull;
+  }
+  __syncthreads();
+  const uint64_t T = s_T, G = T + [&] { uint64_t H = 0; for (int w = 0; w < 16; ++w) H += wsum[w]; return H; }();
+  // the holes (sorted by position; those below T are a prefix: clipped to [0, T)) and the runs
+  // of [T, G) before each hole (empty ones kept: join_bsearch takes the last equal prefix), plus
+  // the run after the last hole; exclusive prefixes by a block scan over per-thread spans
+  const bool fits = T <= f.o.cap;
+  const uint32_t per = np / 1024 > 0 ? np / 1024 : 1, i0 = tid * per;
+  auto ent = [&](uint32_t i, uint64_t& st, uint64_t& en) {  // hole i, or [G, G) past the last
+    if (i < np && key[i] != ~0ull) { st = hstart(key[i]); en = st + (key[i] & 0xFFFFF); }
+    else { st = G; en = G; }
+  };
+  uint64_t hl = 0, rl = 0;  // this thread's hole / run lengths
+  for (uint32_t i = i0; i < i0 + per && i < np; ++i) {
+    uint64_t st, en, ps, pe;
+    ent(i, st, en);
+    if (i == 0) pe = T; else { ent(i - 1, ps, pe); pe = pe > T ? pe : T; }
+    hl += st < T ? (en < T ? en : T) - st : 0;
+    rl += st > pe ? st - pe : 0;
+  }
+  // block exclusive scans of (hl, rl)
+  __shared__ uint64_t sh[1024], sr[1024];
+  sh[tid] = hl; sr[tid] = rl;
+  __syncthreads();
+  for (uint32_t o = 1; o < 1024; o <<= 1) {
+    const uint64_t a1 = tid >= o ? sh[tid - o] : 0, b1 = tid >= o ? sr[tid - o] : 0;
+    __syncthreads();
+    sh[tid] += a1; sr[tid] += b1;
+    __syncthreads();
+  }
+  uint64_t hp = sh[tid] - hl, rp = sr[tid] - rl;
+  // holes with a chunk (nk) and those of them starting below T (nh: a prefix of the sorted list)
+  uint64_t cnt2 = 0;  // nk << 32 | nh
+  for (uint32_t i = tid; i < np; i += 1024)
+    if (key[i] != ~0ull) cnt2 += (1ull << 32) | (hstart(key[i]) < T ? 1ull : 0ull);
+  for (int o = 32; o > 0; o >>= 1) cnt2 += __shfl_xor(cnt2, o, 64);
+  __syncthreads();
+  if ((tid & 63) == 0) wsum[tid >> 6] = cnt2;
+  __syncthreads();
+  uint64_t c2 = 0;
+  for (int w = 0; w < 16; ++w) c2 += wsum[w];
+  const uint32_t nk = (uint32_t)(c2 >> 32), nh = (uint32_t)c2;
+  for (uint32_t i = i0; i < i0 + per && i < np; ++i) {
+    uint64_t st, en, ps, pe;
+    ent(i, st, en);
+    if (i == 0) pe = T; else { ent(i - 1, ps, pe); pe = pe > T ? pe : T; }
+    if (i < nk && st < T) { f.hole_start[i] = st; f.hole_pref[i] = hp; hp += (en < T ? en : T) - st; }
+    if (i <= nk) { f.seg_start[i] = pe; f.seg_pref[i] = rp; rp += st > pe ? st - pe : 0; }
+  }
+  if (tid == 1023) {
+    f.hole_pref[nh] = sh[1023];
+    f.seg_pref[nk + 1] = sr[1023];
+    f.counts[0] = fits ? nh : 0;
+    f.counts[1] = fits ? nk + 1 : 0;
   }
 }
 
-hipError_t launch_join_compact(gf_ctx* ctx, const JoinCompactArgs& a) {
+__device__ __forceinline__ uint2 join_vload(const JoinOut& o, uint64_t pos) {
+  return pos < o.cap ? join_load(o.pairs, o.aligned, pos) : o.spill[pos - o.cap];
+}
+// the last index i < n with pref[i] <= k
+__device__ __forceinline__ uint32_t join_bsearch(const uint64_t* pref, uint32_t n, uint64_t k) {
+  uint32_t lo = 0, hi = n;  // pref[lo] <= k < pref[hi]
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (pref[mid] <= k) lo = mid;
+    else hi = mid;
+  }
+  return lo;
+}
+__global__ __launch_bounds__(kBlock) void join_fixup_copy_kernel(JoinFixup f) {
+  const uint32_t nh = f.counts[0], ns = f.counts[1];
+  if (nh == 0 || ns == 0) return;
+  const uint64_t M = f.hole_pref[nh];
+  for (uint64_t k = (uint64_t)blockIdx.x * kBlock + threadIdx.x; k < M; k += (uint64_t)gridDim.x * kBlock) {
+    const uint32_t h = join_bsearch(f.hole_pref, nh, k), sg = join_bsearch(f.seg_pref, ns, k);
+    const uint64_t dst = f.hole_start[h] + (k - f.hole_pref[h]);
+    const uint64_t src = f.seg_start[sg] + (k - f.seg_pref[sg]);
+    join_store(f.o.pairs, f.o.aligned, dst, join_vload(f.o, src));
+  }
+}
+
+hipError_t launch_join_fixup(gf_ctx* ctx, const JoinFixup& f) {
   KTimer t(ctx, GF_K_JOIN_COMPACT);
-  hipLaunchKernelGGL(join_compact_kernel, dim3(a.ntask + 64), dim3(kBlock), 0, ctx->stream, a);
+  hipLaunchKernelGGL(join_fixup_prep_kernel, dim3(1), dim3(1024), 0, ctx->stream, f);
+  hipLaunchKernelGGL(join_fixup_copy_kernel, dim3(1024), dim3(kBlock), 0, ctx->stream, f);
   return hipGetLastError();
 }
 
@@ -1143,7 +1304,7 @@ hipError_t launch_join_rows(gf_ctx* ctx, const JoinRowArgs& a, const JoinQueryAr
     case 3: {
       KTimer t(ctx, GF_K_JOIN_PROBE);
       const size_t lds = join_probe_lds_bytes(a.lds_budget, a.qn, a.f);
-      const dim3 pg(a.nslots);
+      const dim3 pg(a.out.nwaves / (kJoinThreads / 64));
       const bool m0 = !a.approx && a.metric == 0;
       if (a.f > 1) {  // host: the fine path is exact (never approximate)
         if (m0) hipLaunchKernelGGL((join_row_probe_kernel<0, 1>), pg, dim3(kJoinThreads), lds, s, a);

@@ -593,13 +593,17 @@ def test_join_fine_subcells(sf, oracle_mod, n, r, metric):
     assert st == 0 and len(pairs) > 4000
     exp = np.array(sorted(map(tuple, pairs.tolist())), np.int64).reshape(-1, 2)
     ctx = _lib.context(0)
-    for coarse in (0, 1):
+    # the fine path, the cell path, and the streaming experiment (GF_FLAG_JOIN_STREAM: only the
+    # query side bucketed, the ordinary points probed in input order)
+    for coarse, stream in ((0, 0), (1, 0), (0, 1)):
         _lib.check(_lib.lib().gf_ctx_set_flag(ctx.handle, _lib.FLAG_JOIN_COARSE, coarse), ctx.handle, "flag")
+        _lib.check(_lib.lib().gf_ctx_set_flag(ctx.handle, _lib.FLAG_JOIN_STREAM, stream), ctx.handle, "flag")
         try:
             got = sf.PointPointJoinQuery(conf(sf, False, metric), g, g).run(win(sf, ox, oy), win(sf, qx, qy), r)
         finally:
             _lib.lib().gf_ctx_set_flag(ctx.handle, _lib.FLAG_JOIN_COARSE, 0)
-        np.testing.assert_array_equal(got, exp, err_msg=f"coarse={coarse} f={f}")
+            _lib.lib().gf_ctx_set_flag(ctx.handle, _lib.FLAG_JOIN_STREAM, 0)
+        np.testing.assert_array_equal(got, exp, err_msg=f"coarse={coarse} stream={stream} f={f}")
 
 
 def test_join_async_matches_sync(sf, oracle_mod):

@@ -251,3 +251,39 @@ def test_synthetic_clustered_deterministic_and_in_bounds():
     # 80% in 8 spots of sigma 0.01: the spot on the query point holds ~10% within 3 sigma
     near = np.hypot(x - QPOINT[0], y - QPOINT[1]) < 0.03
     assert 0.08 < near.mean() < 0.12
+
+
+@pytest.mark.parametrize("threads", [1, 3, 8])
+def test_multicore_baselines_equal_serial(oracle_mod, threads):
+    """The bench's multi-core CPU baseline lines (reference-shaped with Flink parallelism, and
+    the optimised OpenMP scans) return exactly the serial restatements' results."""
+    O = oracle_mod
+    B = (115.5, 117.6, 39.6, 41.1)
+    x, y = O.java_random_points(3, 60_000, 115.4, 117.7, 39.5, 41.2)
+    x[:5] = np.nan
+    for n, qs, r in ((100, [(116.414899, 39.920374)], 0.5), (100, [(116.4, 40.0), (117.0, 40.5), (115.3, 39.5)], 0.05),
+                     (500, [(116.414899, 39.920374)], 0.002)):
+        g = O.grid(n, *B)
+        qx, qy = [q[0] for q in qs], [q[1] for q in qs]
+        for ap in (False, True):
+            exp = O.range_pp(g, x, y, qx, qy, r, ap)
+            assert np.array_equal(O.range_pp_mt(g, x, y, qx, qy, r, threads, ap), exp)
+            assert np.array_equal(O.range_pp_mt(g, x, y, qx, qy, r, threads, ap, optimized=True), exp)
+    g = O.grid(500, *B)
+    polys = O.Polygons(O.generate_query_polygons(1000, 115.5, 39.6, 117.6, 41.1))
+    xs, ys = O.java_random_points(4, 40_000, 115.45, 115.75, *B[2:])
+    for r, ap in ((0.001, False), (0.001, True), (0.05, False)):
+        exp = O.range_ppoly(g, xs, ys, polys, r, ap)
+        assert np.array_equal(O.range_ppoly_mt(g, xs, ys, polys, r, threads, ap), exp)
+        assert np.array_equal(O.range_ppoly_mt(g, xs, ys, polys, r, threads, ap, optimized=True), exp)
+    g = O.grid(1000, *B)
+    qx, qy = O.java_random_points(5, 8_000, 115.4, 117.7, 39.5, 41.2)
+    for r in (0.001, 0.004):
+        st, exp = O.join_pp(g, g, x, y, qx, qy, r)
+        exp = exp[np.lexsort((exp[:, 1], exp[:, 0]))]
+        assert np.array_equal(O.join_pp_mt(g, g, x, y, qx, qy, r, threads), exp)
+        assert np.array_equal(O.join_pp_mt(g, g, x, y, qx, qy, r, threads, optimized=True), exp)
+    text = b"".join(b"%d,%d,%.9f,%.9f\n" % (i, 1000 + i, 116 + i * 1e-6, 40 - i * 1e-6) for i in range(5000))
+    ex, ey, eo, et, bl, bk = O.csv_parse(text, ",", (0, 1, 2, 3))
+    mx, my, mt, mbl, mbk = O.csv_parse_mt(text, ",", (0, 1, 2, 3), threads)
+    assert bl == mbl == -1 and np.array_equal(ex, mx) and np.array_equal(ey, my) and np.array_equal(et, mt)

@@ -80,6 +80,57 @@ def _cpu_line(value, unit, sample):
     return {"value": round(value, 1), "unit": unit, "cores": 1, "kind": "port", "sample": sample}
 
 
+def _host_threads():
+    """This process's CPU share (OMP_NUM_THREADS on the GPU box, else every core), the machine's
+    core count and CPU model."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+
+    nproc, model = O.host_cpu()
+    return min(nproc, int(os.environ.get("OMP_NUM_THREADS") or nproc)), nproc, model
+
+
+def _timed(fn, budget):
+    reps, t = 0, time.perf_counter()
+    while True:
+        out = fn()
+        reps += 1
+        el = time.perf_counter() - t
+        if el >= budget:
+            return reps, el, out
+
+
+def _cpu_lines(args, unit, lines, check):
+    """SURVEY.md 8(d) CPU baselines of a workload line, in the same run (rank 0, N = 1):
+      value           the reference-shaped operator on every thread of this process's CPU share,
+                      shaped as Flink runs it with that parallelism (conf/geoflink-conf.yml:55)
+      single_thread   the same operator restated serially (1 thread)
+      optimized_scan  an optimised OpenMP C line on the same threads (when there is one)
+    lines: {"mt": (units per rep, fn(T), sample), "single": (...), "omp": (...) or None};
+    check(results by name) -> every line's result equals the others' and the GPU's."""
+    T, nproc, model = _host_threads()
+    budget = max(1.0, args.cpu_seconds / 3.0)
+    res, rate, samp = {}, {}, {}
+    for name, spec in lines.items():
+        if spec is None:
+            continue
+        units, fn, sample = spec
+        reps, el, out = _timed(lambda: fn(1 if name == "single" else T), budget)
+        res[name], rate[name] = out, reps * units / el
+        samp[name] = f"{sample} x {reps} ({el:.1f}s)"
+    ok = bool(check(res))
+    d = {"value": round(rate["mt"], 1), "unit": unit, "cores": T, "kind": "port", "nproc": nproc, "cpu_model": model,
+         "threads_note": "threads = this process's CPU share on the GPU box (OMP_NUM_THREADS), of nproc",
+         "sample": samp["mt"] + ": the reference-shaped operator (C restatement) with Flink parallelism = threads",
+         "results_equal_gpu": ok,
+         "single_thread": {"value": round(rate["single"], 1), "unit": unit, "cores": 1, "kind": "port",
+                           "sample": samp["single"] + ": the same operator, 1 thread"}}
+    if "omp" in rate:
+        d["optimized_scan"] = {"value": round(rate["omp"], 1), "unit": unit, "cores": T, "kind": "port",
+                               "sample": samp["omp"] + ": optimised OpenMP C (integer cells, per-thread outputs)"}
+    return d
+
+
 def _band(sf, grid, grid_n, world, rank):
     """x range of this rank's cell-column band (the whole grid at N = 1)."""
     from spatialflink_amd import sharding
@@ -279,16 +330,27 @@ def bench_range(args, polygons=False):
         x, y, _ = wins[0]
         verified, cpu = None, None
         if not args.no_verify:
-            tc = time.perf_counter()
             exp = (O.range_ppoly(og, x[:m], y[:m], O.Polygons(raw), r) if polygons
                    else O.range_pp(og, x[:m], y[:m], [QPOINT[0]], [QPOINT[1]], r))
-            tc = time.perf_counter() - tc
-            if world == 1 and not args.no_cpu_baseline:
-                cpu = _cpu_line(m / tc, "points/s", f"first {m} points of window 0, 1 pass ({tc:.2f}s): oracle's "
-                                "reference-shaped evaluator (string cell IDs, HashSet G/C filter, per-point JTS "
-                                "distance loop), C restatement of the Java operator, 1 thread")
             got = sf.spatialOperators.bitmap_indices(ctx, bitmaps[0], n).astype(np.int64)
             verified = bool(_reduce(float(np.array_equal(got[got < m], exp)), world, args, dev, op="min"))
+            if world == 1 and not args.no_cpu_baseline:
+                Pg = O.Polygons(raw) if polygons else None
+                S = min(n, 200_000) if polygons else m  # the serial C3 operator tests 1000 polygons per point
+                if polygons:
+                    f1 = lambda T, k=S: O.range_ppoly(og, x[:k], y[:k], Pg, r)  # noqa: E731
+                    fm = lambda T: O.range_ppoly_mt(og, x, y, Pg, r, T)  # noqa: E731
+                    fo = lambda T: O.range_ppoly_mt(og, x, y, Pg, r, T, optimized=True)  # noqa: E731
+                else:
+                    f1 = lambda T, k=S: O.range_pp(og, x[:k], y[:k], [QPOINT[0]], [QPOINT[1]], r)  # noqa: E731
+                    fm = lambda T: O.range_pp_mt(og, x, y, [QPOINT[0]], [QPOINT[1]], r, T)  # noqa: E731
+                    fo = lambda T: O.range_pp_mt(og, x, y, [QPOINT[0]], [QPOINT[1]], r, T, optimized=True)  # noqa: E731
+                cpu = _cpu_lines(args, "points/s", {
+                    "mt": (n, fm, f"the whole {n}-point window 0"),
+                    "single": (S, f1, f"first {S} points of window 0"),
+                    "omp": (n, fo, f"the whole {n}-point window 0")},
+                    lambda R: np.array_equal(R["mt"], got) and np.array_equal(R["omp"], got)
+                    and np.array_equal(R["single"], got[got < S]))
         for hp in plans:
             L.gf_range_plan_destroy(hp)
         avg_scan = ms / 1000.0 / max(cnt, 1)
@@ -342,6 +404,8 @@ def bench_join(args):
     grid_n = 1000
     grid = sf.UniformGrid(grid_n, *BEIJING)
     ctx = _lib.context(dev)
+    if getattr(args, "join_stream", False):  # experiment: query side bucketed only, ordinary points streamed
+        _lib.check(L.gf_ctx_set_flag(ctx.handle, _lib.FLAG_JOIN_STREAM, 1), ctx.handle, "flag")
     ow = _windows(sf, no, 2, 11 + 1000 * rank, dev, _band(sf, grid, grid_n, world, rank))
     r = 0.001
     if world == 1:
@@ -437,17 +501,22 @@ def bench_join(args):
         got = got[got[:, 0] < m]
         og = O.grid(grid_n, *BEIJING)
         (x, y, _), (qx, qy, _) = ow[0], qw[0]
-        tc = time.perf_counter()
         st, exp = O.join_pp(og, og, x[:m], y[:m], qx, qy, r)
-        tc = time.perf_counter() - tc
         order = np.lexsort((got[:, 1], got[:, 0]))
         eo = np.lexsort((exp[:, 1], exp[:, 0]))
-        verified = bool(st == 0 and np.array_equal(got[order], exp[eo]))
-        if not args.no_cpu_baseline:
-            cpu = _cpu_line((m + len(qx)) / tc, "points/s", f"first {m} ordinary points of window 0 x the {len(qx)} "
-                            f"query points, 1 pass ({tc:.2f}s): oracle's reference-shaped join (query points "
-                            "replicated to string keys, hash join on gridID, distance per co-located pair), "
-                            "C restatement, 1 thread")
+        got_s = got[order]
+        verified = bool(st == 0 and np.array_equal(got_s, exp[eo]))
+        if not args.no_cpu_baseline:  # the first m ordinary points x the whole query window (pairs are per point)
+            def sorted_pairs(a):
+                return a[np.lexsort((a[:, 1], a[:, 0]))]
+            cpu = _cpu_lines(args, "points/s", {
+                "mt": (m + len(qx), lambda T: O.join_pp_mt(og, og, x[:m], y[:m], qx, qy, r, T),
+                       f"first {m} ordinary points of window 0 x the {len(qx)} query points"),
+                "single": (m + len(qx), lambda T: sorted_pairs(O.join_pp(og, og, x[:m], y[:m], qx, qy, r)[1]),
+                           f"first {m} ordinary points of window 0 x the {len(qx)} query points"),
+                "omp": (m + len(qx), lambda T: O.join_pp_mt(og, og, x[:m], y[:m], qx, qy, r, T, optimized=True),
+                        f"first {m} ordinary points of window 0 x the {len(qx)} query points")},
+                lambda R: all(np.array_equal(R[k_], got_s) for k_ in ("mt", "single", "omp")))
     wl = f"join_pp_{no // 1_000_000}Mx{nq / 1e6:g}M_r{r}_grid1000" + (f"_per_gpu_x{world}" if world > 1 else "") + (
         "_clustered" if CLUSTERED else "")
     # roofline over the WHOLE window (every join kernel: both bucketings, probe, packing): the
@@ -768,6 +837,8 @@ def bench_sliding(args):
 
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
+        # the reference evaluates every window from scratch (PointPointKNNQuery.java:158-200):
+        # its rate in window points / s on a sample of one window's points, the three lines
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle as O
 
@@ -775,17 +846,20 @@ def bench_sliding(args):
         x, y, obj = host[0]
         xs, ys, os_ = (np.ascontiguousarray(a[:S]) for a in (x, y, obj))
         og = O.grid(grid_n, *BEIJING)
-        reps, t = 0, time.perf_counter()
-        while True:
-            O.knn(og, xs, ys, os_, QPOINT[0], QPOINT[1], args.radius, k, reference_shaped=True)
-            reps += 1
-            if time.perf_counter() - t >= args.cpu_seconds:
-                break
-        ct = time.perf_counter() - t
-        cpu = {"value": round(reps * S / ct, 1), "unit": "window points/s", "cores": 1, "kind": "port",
-               "sample": (f"first {S} points of a window x {reps} reps ({ct:.1f}s): oracle's reference-shaped "
-                          "evaluator (string cell IDs, HashSet C/G filter, per-cell PriorityQueue, windowAll merge), "
-                          "1 thread; the reference evaluates every window from scratch")}
+        q5 = (QPOINT[0], QPOINT[1], args.radius, k)
+
+        def final(res):  # (objID, dist) sorted by (dist, objID): the reference's heap in rank order
+            st, o, d = res[0], res[1], res[2]
+            i = np.lexsort((o, d))
+            return st, o[i], d[i]
+        cpu = _cpu_lines(args, "window points/s", {
+            "mt": (S, lambda T: final(O.knn_mt(og, xs, ys, os_, *q5, T)), f"first {S} points of a window"),
+            "single": (S, lambda T: final(O.knn(og, xs, ys, os_, *q5, reference_shaped=True)),
+                       f"first {S} points of a window"),
+            "omp": (S, lambda T: final(O.knn_mt(og, xs, ys, os_, *q5, T, optimized=True)),
+                    f"first {S} points of a window")},
+            lambda R: all(R[k_][0] == 0 for k_ in R) and all(
+                np.array_equal(R[k_][1], R["mt"][1]) and np.array_equal(R[k_][2], R["mt"][2]) for k_ in R))
     traffic, traffic_src = None, None
     if rank == 0:  # HBM bytes per pane launch from the committed rocprofv3 PMC passes
         import glob
@@ -827,6 +901,47 @@ def bench_sliding(args):
         dist.destroy_process_group()
 
 
+def _geojson_chunk(args_):
+    """Process-pool worker of the GeoJSON multi-core CPU line: the oracle's per-line map."""
+    text, = args_
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+
+    x, y, o, t, bl, bk = O.geojson_parse(text, "oID", "timestamp", 1, 480)
+    return x, y, bl
+
+
+def _geojson_pool_baseline(args, text):
+    """The GeoJSON map on T processes (Flink map parallelism T): the chunk's lines split into T
+    contiguous parts, each parsed by the oracle (Python json per line) in its own process.
+    Returns (T, lines/s, sample, results equal the serial oracle)."""
+    import multiprocessing as mp
+
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+
+    T, nproc, model = _host_threads()
+    lines_ = text.split(b"\n")[:-1]
+    n = len(lines_)
+    parts = [b"\n".join(lines_[n * t // T: n * (t + 1) // T]) + b"\n" for t in range(T)]
+    with mp.get_context("spawn").Pool(T) as pool:
+        pool.map(_geojson_chunk, [(b'{"value":{"type":"Point","coordinates":[1,2]}}\n',)] * T)  # warm workers
+        budget = min(args.cpu_seconds / 3.0, 10.0)
+        reps, t0 = 0, time.perf_counter()
+        while True:
+            out = pool.map(_geojson_chunk, [(p_,) for p_ in parts])
+            reps += 1
+            if time.perf_counter() - t0 >= budget:
+                break
+        el = time.perf_counter() - t0
+    ex, ey, *_ = O.geojson_parse(text, "oID", "timestamp", 1, 480)
+    agree = all(o_[2] == -1 for o_ in out) and np.array_equal(np.concatenate([o_[0] for o_ in out]), ex) and \
+        np.array_equal(np.concatenate([o_[1] for o_ in out]), ey)
+    sample = (f"the {n}-line window x {reps} ({el:.1f}s): oracle geojson_parse (Python json per line) on {T} "
+              f"processes, contiguous parts (Flink map parallelism {T}; {nproc} cores, {model})")
+    return T, reps * n / el, sample, agree
+
+
 def bench_csv(args, geojson=False):
     """C1 ingest: 1M-line CSV window (objID, ts, x, y; shortest round-trip doubles, the way Java's
     Double.toString prints them) device-resident as text -> gf_csv_parse (SoA + 100x100 cells),
@@ -848,16 +963,19 @@ def bench_csv(args, geojson=False):
 
     n = args.points or 1_000_000
     L = _lib.lib()
-    ctx = _lib.context(0)
-    grid = sf.UniformGrid(100, *BEIJING)
-    texts = []
+    host_texts = []
     for j in range(2):
         if geojson:
-            text = geojson_lines(31 + j, n, 1)
-            texts.append((text, None, None, None, device_text(text)))
+            host_texts.append((geojson_lines(31 + j, n, 1), None, None, None))
         else:
-            text, px, py, po, pt = make_csv(n, seed=31 + j)
-            texts.append((text, px, py, po, device_text(text)))
+            host_texts.append(make_csv(n, seed=31 + j)[:4])
+    # the GeoJSON oracle is Python (json module per line): its multi-core line runs on a process
+    # pool, started before this process touches the GPU (no fork of a GPU-initialised process)
+    geo_pool_lines = _geojson_pool_baseline(args, host_texts[(args.steps - 1) % 2][0]) if (
+        geojson and not args.no_cpu_baseline) else None
+    ctx = _lib.context(0)
+    grid = sf.UniformGrid(100, *BEIJING)
+    texts = [(t_[0], t_[1], t_[2], t_[3], device_text(t_[0])) for t_ in host_texts]
     nbytes = len(texts[0][0])
     sc = GfGeojsonSchema(b"oID", b"timestamp", 1, 480) if geojson else GfCsvSchema(b",", b"\0\0\0", 0, 1, 2, 3)
     dict_h = sf.ObjIdDict.default(0).handle
@@ -925,19 +1043,29 @@ def bench_csv(args, geojson=False):
     verified &= bool(np.array_equal(got, O.range_pp(og, ex, ey, [QPOINT[0]], [QPOINT[1]], args.radius)))
     L.gf_range_plan_destroy(h)
     cpu = None
-    if not args.no_cpu_baseline:  # the oracle's restatement of the reference's per-line map, 1 thread
+    if not args.no_cpu_baseline and geojson:  # the oracle's restatement of the map, Python json per line
         reps, tc = 0, time.perf_counter()
         while True:
             oracle_parse(text)
             reps += 1
-            if time.perf_counter() - tc >= min(args.cpu_seconds, 10.0):
+            if time.perf_counter() - tc >= min(args.cpu_seconds / 3.0, 10.0):
                 break
         ct = time.perf_counter() - tc
-        cpu = {"value": round(reps * n / ct, 1), "unit": "lines/s", "cores": 1, "kind": "port",
-               "sample": (f"the {n}-line window x {reps} ({ct:.1f}s): oracle geojson_parse (Python json module per "
-                          "line + the map's property logic), 1 thread -- ingest only") if geojson else
-                         (f"the {n}-line window x {reps} ({ct:.1f}s): oracle orc_csv_parse (quote removal, Java split "
-                          "rule, Long.valueOf, strtod), 1 thread -- ingest only")}
+        T, rate_mt, samp_mt, agree_mt = geo_pool_lines
+        cpu = {"value": round(rate_mt, 1), "unit": "lines/s", "cores": T, "kind": "port",
+               "sample": samp_mt, "results_equal_gpu": bool(agree_mt and verified),
+               "single_thread": {"value": round(reps * n / ct, 1), "unit": "lines/s", "cores": 1, "kind": "port",
+                                 "sample": f"the {n}-line window x {reps} ({ct:.1f}s): oracle geojson_parse (Python "
+                                           "json module per line + the map's geometry / property logic), 1 thread"}}
+    elif not args.no_cpu_baseline:  # CSV: orc_csv_parse per line (the reference's map restated in C)
+        def xy(res):
+            return res[0], res[1]
+        cpu = _cpu_lines(args, "lines/s", {
+            "mt": (n, lambda T: xy(O.csv_parse_mt(text, ",", [0, 1, 2, 3], T)),
+                   f"the {n}-line window: orc_csv_parse on contiguous parts (Flink map parallelism)"),
+            "single": (n, lambda T: xy(O.csv_parse(text, ",", [0, 1, 2, 3])),
+                       f"the {n}-line window: orc_csv_parse (quote removal, Java split rule, Long.valueOf, strtod)")},
+            lambda R: all(np.array_equal(R[k_][0], ex) and np.array_equal(R[k_][1], ey) for k_ in R))
     avg_parse = pms / 1000.0 / max(pcnt, 1)
     _line(("GeoJSON" if geojson else "CSV") + " ingest + point-point range", n * args.steps / elapsed, "lines/s",
           args.steps, args.warmup, elapsed, "csv_parse_kernel" + (" (GeoJSON lines)" if geojson else ""),
