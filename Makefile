@@ -13,7 +13,16 @@ SOURCES  := $(SRC)/api.cpp $(SRC)/sliding.cpp $(SRC)/csv.cpp $(SRC)/objid.cpp $(
 OBJECTS  := $(patsubst $(SRC)/%,$(OBJDIR)/%.o,$(SOURCES))
 HEADERS  := include/geoflink_hip.h $(SRC)/gf_internal.hpp $(SRC)/gf_text.hpp $(SRC)/gf_geojson.hpp $(SRC)/gf_numerics.hpp $(SRC)/gf_decimal.hpp $(SRC)/gf_pow5.hpp $(SRC)/gf_geom.hpp
 
-all: $(LIB) oracle
+all: $(LIB) oracle shim
+
+# the plain-C core of the JNI shim (integration/jni/geoflink_shim.c) as a library the tests drive
+# through ctypes exactly as geoflink_jni.c's natives call it (no JDK in the image)
+SHIM     := integration/jni/libgeoflink_shim.so
+$(SHIM): integration/jni/geoflink_shim.c integration/jni/geoflink_shim.h include/geoflink_hip.h $(LIB)
+	gcc -O2 -std=c11 -Wall -Wextra -Werror -fPIC -shared -Iinclude -I/opt/rocm/include -D__HIP_PLATFORM_AMD__ \
+	    $< -o $@ -Lspatialflink_amd -lgeoflink_hip -L/opt/rocm/lib -lamdhip64 \
+	    -Wl,-rpath,'$$ORIGIN/../../spatialflink_amd' -Wl,-rpath,/opt/rocm/lib
+shim: $(SHIM)
 
 $(OBJDIR)/%.o: $(SRC)/% $(HEADERS)
 	@mkdir -p $(OBJDIR)
@@ -41,7 +50,7 @@ isa: $(LIB)
 	/opt/rocm/lib/llvm/bin/clang-offload-bundler --list --type=o --input=$(OBJDIR)/k_knn.hip.o
 
 clean:
-	rm -rf build $(LIB)
+	rm -rf build $(LIB) $(SHIM)
 	$(MAKE) -s -C oracle clean
 
-.PHONY: all oracle clean isa trace
+.PHONY: all oracle shim clean isa trace

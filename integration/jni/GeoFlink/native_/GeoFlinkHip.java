@@ -3,58 +3,122 @@
  * window operators (see INTEGRATION.md).  NOT COMPILED in this repository: the build image has
  * no JDK (no javac, no jni.h).  It is kept as a real source file so a maintainer can drop it
  * next to the reference's operators (package GeoFlink.native_) and build it with the JDK.
+ * tests/test_shim_native.py checks that every native here has its C function in geoflink_jni.c
+ * with the JNI types of these parameters, and drives the C core each of them calls on the GPU.
  *
  * Every handle is a native pointer held in a long.  Window buffers are direct ByteBuffers in
- * native byte order (x, y: double; objID, ts: long).  Each plan caches its device window(s), so
- * a continuous query uploads into the same device buffers window after window.
+ * native byte order (x, y: double; objID keys, ts: long).  A context (ctxCreate) is one Flink
+ * subtask's device context plus the device buffers its windows reuse; plans cache their own
+ * device windows, so a continuous query uploads into the same device buffers window after
+ * window.  Nothing is shared between contexts.
  *
  * Anchors (what each native call replaces):
+ *   objidIntern / objidDecode  Point.objID Strings (Point.java:41-47) <-> the int64 keys the
+ *                device evaluates (include/geoflink_hip.h, "objID keys")
  *   knnWindow    PointPointKNNQuery.windowBased (PointPointKNNQuery.java:132-201) +
  *                KNNQuery.kNNWinAllEvaluationPointStream (KNNQuery.java:213-272)
+ *   knnPolygonPlan  PointPolygonKNNQuery (PointPolygonKNNQuery.java:245-317)
+ *   knnSliding*  SlidingProcessingTimeWindows.of(size, slide) around the kNN apply
+ *                (PointPointKNNQuery.java:158,198-200): panes evaluated once, windows merged
  *   rangeWindow  PointPointRangeQuery.windowBased apply (PointPointRangeQuery.java:150-186),
  *                PointPolygonRangeQuery apply (PointPolygonRangeQuery.java:170-204)
  *   joinWindow   JoinQuery.getReplicatedPointQueryStream (JoinQuery.java:73-90) +
  *                PointPointJoinQuery.windowBased (PointPointJoinQuery.java:148-182)
  *   polygonJoinWindow  JoinQuery.java:93-115 + PointPolygonJoinQuery.java:154-213
  *   csvParse     Deserialization.CSVTSVToTSpatial.map (Deserialization.java:291-325)
- *   geoJsonParse Deserialization.GeoJSONToSpatial (Deserialization.java:149-211), Point features
+ *   geoJsonParse Deserialization.GeoJSONToTSpatial(uGrid, dateFormat, propertyTimeStamp,
+ *                propertyObjID).map (Deserialization.java:64-70,149-211), Point geometries
  */
 package GeoFlink.native_;
 
 import java.nio.ByteBuffer;
+import java.nio.charset.StandardCharsets;
 
 public final class GeoFlinkHip {
   static { System.loadLibrary("geoflink_jni"); }   // libgeoflink_jni.so -> libgeoflink_hip.so
 
   private GeoFlinkHip() {}
 
+  /** objID key of a null String (a GeoJSON feature without the objID property). */
+  public static final long OBJID_NULL = Long.MAX_VALUE;
+
   // one context per Flink subtask (RichAllWindowFunction.open / close)
   public static native long ctxCreate(int device);
   public static native void ctxDestroy(long ctx);
 
-  // ---- kNN (point query) ----------------------------------------------------------------
-  // UniformGrid(n, minX, maxX, minY, maxY) is passed by value
-  public static native long knnPlan(long ctx, int n, double minX, double maxX, double minY, double maxY,
-                                    double qx, double qy, double r, int k);
+  // ---- objID Strings <-> keys (the context's dictionary) ------------------------------------
+  // String i = UTF-8 bytes[offs[i], offs[i+1]) (offs: n + 1 entries) -> keys[i]
+  public static native void objidIntern(long ctx, byte[] bytes, long[] offs, int n, long[] keys);
+  // keys -> the Strings' UTF-8 bytes; offs (n + 1 entries) filled
+  public static native byte[] objidDecode(long ctx, long[] keys, int n, long[] offs);
+
+  /** Point.objID Strings of a window -> keys (null -> OBJID_NULL) */
+  public static long[] intern(long ctx, String[] objIDs, int n) {
+    byte[][] enc = new byte[n][];
+    long[] offs = new long[n + 1];
+    for (int i = 0; i < n; i++) {
+      enc[i] = objIDs[i] == null ? new byte[0] : objIDs[i].getBytes(StandardCharsets.UTF_8);
+      offs[i + 1] = offs[i] + enc[i].length;
+    }
+    byte[] bytes = new byte[(int) offs[n]];
+    for (int i = 0; i < n; i++) System.arraycopy(enc[i], 0, bytes, (int) offs[i], enc[i].length);
+    long[] keys = new long[n];
+    objidIntern(ctx, bytes, offs, n, keys);
+    for (int i = 0; i < n; i++) if (objIDs[i] == null) keys[i] = OBJID_NULL;
+    return keys;
+  }
+
+  /** result keys -> Point.objID Strings (UTF-8, not JNI's modified UTF-8) */
+  public static String[] decode(long ctx, long[] keys, int n) {
+    long[] offs = new long[n + 1];
+    byte[] bytes = objidDecode(ctx, keys, n, offs);
+    String[] out = new String[n];
+    for (int i = 0; i < n; i++)
+      out[i] = keys[i] == OBJID_NULL ? null
+             : new String(bytes, (int) offs[i], (int) (offs[i + 1] - offs[i]), StandardCharsets.UTF_8);
+    return out;
+  }
+
+  // ---- kNN ----------------------------------------------------------------------------------
+  // grids as double[] {n, minX, maxX, minY, maxY} (UniformGrid(n, minX, maxX, minY, maxY))
+  public static native long knnPlan(long ctx, double[] grid, double qx, double qy, double r, int k);
+  // polygons as CSR: ringOff[npoly+1] into vertOff, vertOff[nrings+1] into vx / vy (closed rings)
+  public static native long knnPolygonPlan(long ctx, double[] grid, int[] ringOff, int[] vertOff, double[] vx,
+                                           double[] vy, double r, int k, boolean approximate);
   public static native void knnPlanDestroy(long plan);
-  // x, y, objID of one window (ts is not read by window evaluation); returns the number of
-  // neighbours written to out* (ascending (dist, objID)), outIdx = the window-local indices
-  public static native int knnWindow(long plan, ByteBuffer x, ByteBuffer y, ByteBuffer objID, int n,
-                                     long[] outObjID, double[] outDist, long[] outIdx);
+  // x, y, objID keys of one window (ts is not read by window evaluation); returns the number of
+  // neighbours written to out* (ascending (dist, objID)), outIdx = the window-local indices;
+  // out* hold at least k entries
+  public static native int knnWindow(long ctx, long plan, ByteBuffer x, ByteBuffer y, ByteBuffer objID, int n,
+                                     long[] outObjID, double[] outDist, long[] outIdx, int k);
+
+  // ---- sliding kNN (pane engine) ---------------------------------------------------------
+  // size / gcd(size, slide) <= 64; the plan must outlive the sliding handle
+  public static native long knnSlidingCreate(long ctx, long plan, long sizeMs, long slideMs);
+  public static native void knnSlidingDestroy(long sliding);
+  // pane p holds timestamps [p * paneMs, (p + 1) * paneMs)
+  public static native long knnSlidingPaneMs(long sliding);
+  // push pane `pane` (consecutive indices; an empty pane with n = 0); returns the end (ms) of
+  // the window it closed, or -1.  Decode a closed window within the next 8 windows.
+  public static native long knnSlidingPush(long ctx, long sliding, long pane, ByteBuffer x, ByteBuffer y,
+                                           ByteBuffer objID, int n);
+  // a closed window's neighbours; outIdx = the point's position in the pushed stream
+  public static native int knnSlidingDecode(long ctx, long sliding, long windowEnd, long[] outObjID,
+                                            double[] outDist, long[] outIdx, int k);
 
   // ---- range ---------------------------------------------------------------------------
-  public static native long rangePlan(long ctx, int n, double minX, double maxX, double minY, double maxY,
-                                      double[] qx, double[] qy, double r, boolean approximate);
-  // polygons as CSR: ringOff[npoly+1] into vertOff, vertOff[nrings+1] into vx / vy (closed rings)
-  public static native long rangePolygonPlan(long ctx, int n, double minX, double maxX, double minY, double maxY,
-                                             int[] ringOff, int[] vertOff, double[] vx, double[] vy, double r,
-                                             boolean approximate);
+  public static native long rangePlan(long ctx, double[] grid, double[] qx, double[] qy, double r,
+                                      boolean approximate);
+  public static native long rangePolygonPlan(long ctx, double[] grid, int[] ringOff, int[] vertOff, double[] vx,
+                                             double[] vy, double r, boolean approximate);
   public static native void rangePlanDestroy(long plan);
-  // emitted point indices, ascending
-  public static native int[] rangeWindow(long plan, ByteBuffer x, ByteBuffer y, int n);
+  // emitted point indices, ascending, into out (a direct int buffer of outCap entries); returns
+  // their count -- larger than outCap: call again with a larger buffer
+  public static native long rangeWindow(long ctx, long plan, ByteBuffer x, ByteBuffer y, int n, ByteBuffer out,
+                                        int outCap);
 
   // ---- joins ---------------------------------------------------------------------------
-  // grids as {n, minX, maxX, minY, maxY}; pairs (ordinary index, query index) flattened
+  // pairs (ordinary / point index, query / polygon index) flattened
   public static native long[] joinWindow(long ctx, double[] uGrid, double[] qGrid, ByteBuffer ox, ByteBuffer oy,
                                          int no, ByteBuffer qx, ByteBuffer qy, int nq, double r,
                                          boolean approximate);
@@ -64,10 +128,15 @@ public final class GeoFlinkHip {
 
   // ---- ingest --------------------------------------------------------------------------
   // a chunk of complete lines -> x, y, objID keys, ts (direct buffers of capacity >= lines);
-  // returns the number of points; objID Strings are interned in the context's dictionary
+  // returns the number of points; objID Strings are interned in the context's dictionary.
+  // A bad line throws (NumberFormatException / IllegalArgumentException naming the line).
   public static native int csvParse(long ctx, ByteBuffer text, int len, char delimiter, int[] schema /* objID, ts, x, y */,
                                     ByteBuffer x, ByteBuffer y, ByteBuffer objID, ByteBuffer ts, int capacity);
-  // GeoJSON Point features (one per line) -> the same columns
-  public static native int geoJsonParse(long ctx, ByteBuffer text, int len, ByteBuffer x, ByteBuffer y,
-                                        ByteBuffer objID, ByteBuffer ts, int capacity);
+  // GeoJSONToTSpatial(uGrid, dateFormat, propertyTimeStamp, propertyObjID): dateFormat null
+  // (integer ms) or "yyyy-MM-dd HH:mm:ss"; tzOffsetMinutes = TimeZone.getDefault().getRawOffset()
+  // / 60000; valueLines: each line is the record's value instead of {"key":..,"value":..}
+  public static native int geoJsonParse(long ctx, ByteBuffer text, int len, String propertyTimeStamp,
+                                        String propertyObjID, String dateFormat, int tzOffsetMinutes,
+                                        boolean valueLines, ByteBuffer x, ByteBuffer y, ByteBuffer objID,
+                                        ByteBuffer ts, int capacity);
 }

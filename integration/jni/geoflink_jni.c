@@ -1,393 +1,440 @@
 /*
- * geoflink_jni.c -- the C side of the JNI shim behind GeoFlink.native_.GeoFlinkHip (see
- * INTEGRATION.md).  NOT COMPILED in this repository: the build image has no JDK, so jni.h is
- * absent.  It is kept as a real source file; on a machine with a JDK:
+ * geoflink_jni.c -- the JNI side of the shim behind GeoFlink.native_.GeoFlinkHip (see
+ * INTEGRATION.md).  Every native is a thin wrapper: it checks the Java arguments (direct-buffer
+ * capacities, array lengths), pins them, and calls ONE function of the plain-C core
+ * (geoflink_shim.h), which makes the whole gf_* call sequence.  The core is compiled and run
+ * without a JDK by tests/native/shim_check.c (tests/test_shim_native.py); this file needs jni.h,
+ * which the build image lacks, so it is built on a machine with a JDK:
  *
  *   gcc -O2 -fPIC -shared -I$JAVA_HOME/include -I$JAVA_HOME/include/linux -Iinclude \
  *       -I/opt/rocm/include -D__HIP_PLATFORM_AMD__ integration/jni/geoflink_jni.c \
- *       -Lspatialflink_amd -lgeoflink_hip -L/opt/rocm/lib -lamdhip64 -o libgeoflink_jni.so
+ *       integration/jni/geoflink_shim.c -Lspatialflink_amd -lgeoflink_hip \
+ *       -L/opt/rocm/lib -lamdhip64 -o libgeoflink_jni.so
  *
- * Ownership: a plan handle is a shim struct holding the library plan, its context and the
- * device window(s) it uploads into -- created once per continuous query and reused window
- * after window (gf_window_upload into the same device buffers; only the columns the query
- * reads are copied: x, y for range / join, + objID for kNN).  Errors become Java exceptions
- * (IllegalArgumentException for GF_ERR_ARG, RuntimeException otherwise: the reference's
- * System.exit(1) on non-positive candidate layers is GF_ERR_LAYERS).
+ * Handles are native pointers in a long: a context (shim_ctx: one Flink subtask's gf_ctx plus
+ * the device buffers its windows reuse), and plans (kNN, range, sliding kNN) that hold their
+ * own device windows.  Nothing is shared between contexts.  Errors become Java exceptions:
+ * IllegalArgumentException for GF_ERR_ARG (the reference's map / apply would have thrown), an
+ * IndexOutOfBoundsException for a buffer smaller than the call needs, RuntimeException otherwise
+ * (the reference's System.exit(1) on non-positive candidate layers is GF_ERR_LAYERS).
  */
 #include <jni.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
-#include <hip/hip_runtime_api.h>
+#include "geoflink_shim.h"
 
-#include "geoflink_hip.h"
+#define CTX(h) ((shim_ctx*)(intptr_t)(h))
 
-static void throw_status(JNIEnv* env, int st, gf_ctx* ctx) {
-  const char* cls = st == GF_ERR_ARG ? "java/lang/IllegalArgumentException" : "java/lang/RuntimeException";
-  (*env)->ThrowNew(env, (*env)->FindClass(env, cls), ctx ? gf_ctx_last_error(ctx) : gf_status_string(st));
+static void throw_msg(JNIEnv* env, const char* cls, const char* msg) {
+  if ((*env)->ExceptionCheck(env)) return;
+  (*env)->ThrowNew(env, (*env)->FindClass(env, cls), msg);
 }
-
-static void* buf(JNIEnv* env, jobject b) { return b ? (*env)->GetDirectBufferAddress(env, b) : NULL; }
-
-/* a device window of at least n points, grown (recreated) only when a window is larger */
-typedef struct {
-  gf_window* w;
-  int64_t cap;
-} cached_window;
-
-static int window_for(gf_ctx* ctx, cached_window* c, int64_t n) {
-  if (c->w && c->cap >= n) return GF_OK;
-  if (c->w) gf_window_destroy(c->w);
-  c->w = NULL;
-  c->cap = n > 1024 ? n + n / 4 : 1024;
-  return gf_window_create(ctx, c->cap, &c->w);
-}
-
-/* upload the given columns and return the device points (ordered after the copy) */
-static int upload(gf_ctx* ctx, cached_window* c, const double* x, const double* y, const int64_t* objID, int64_t n,
-                  gf_points* pts) {
-  int st = window_for(ctx, c, n);
-  if (!st) st = gf_window_upload(c->w, x, y, objID, NULL, n);
-  if (!st) st = gf_window_points(c->w, pts);
+static int throw_status(JNIEnv* env, int st, shim_ctx* c) {
+  if (st)
+    throw_msg(env, st == GF_ERR_ARG ? "java/lang/IllegalArgumentException" : "java/lang/RuntimeException",
+              c ? shim_last_error(c) : gf_status_string(st));
   return st;
 }
 
-JNIEXPORT jlong JNICALL Java_GeoFlink_native_1_GeoFlinkHip_ctxCreate(JNIEnv* env, jclass cls, jint dev) {
-  gf_ctx* ctx = NULL;
-  int st = gf_ctx_create(dev, &ctx);
-  if (st) throw_status(env, st, NULL);
-  return (jlong)(intptr_t)ctx;
+/* a direct ByteBuffer holding at least `bytes` -> its address; NULL + IndexOutOfBounds otherwise */
+static void* direct(JNIEnv* env, jobject b, int64_t bytes, const char* what) {
+  if ((*env)->ExceptionCheck(env)) return NULL;  /* an earlier argument already threw */
+  if (bytes <= 0) return b ? (*env)->GetDirectBufferAddress(env, b) : NULL;
+  void* p = b ? (*env)->GetDirectBufferAddress(env, b) : NULL;
+  if (!p) {
+    throw_msg(env, "java/lang/IllegalArgumentException", what);
+    return NULL;
+  }
+  if ((*env)->GetDirectBufferCapacity(env, b) < bytes) {
+    throw_msg(env, "java/lang/IndexOutOfBoundsException", what);
+    return NULL;
+  }
+  return p;
 }
-
-JNIEXPORT void JNICALL Java_GeoFlink_native_1_GeoFlinkHip_ctxDestroy(JNIEnv* env, jclass cls, jlong ctx) {
-  gf_ctx_destroy((gf_ctx*)(intptr_t)ctx);
-}
-
-/* ---- kNN ------------------------------------------------------------------------------ */
-typedef struct {
-  gf_ctx* ctx;
-  gf_knn_plan* plan;
-  cached_window win;
-} knn_handle;
-
-JNIEXPORT jlong JNICALL Java_GeoFlink_native_1_GeoFlinkHip_knnPlan(JNIEnv* env, jclass cls, jlong ctxh, jint n,
-    jdouble minX, jdouble maxX, jdouble minY, jdouble maxY, jdouble qx, jdouble qy, jdouble r, jint k) {
-  gf_ctx* ctx = (gf_ctx*)(intptr_t)ctxh;
-  knn_handle* h = (knn_handle*)calloc(1, sizeof(knn_handle));
-  gf_grid g;
-  int st = h ? gf_grid_make(n, minX, maxX, minY, maxY, &g) : GF_ERR_NOMEM;
-  if (!st) st = gf_knn_pp_plan_create(ctx, &g, qx, qy, r, k, GF_METRIC_SQRT, &h->plan);
-  if (st) {
-    free(h);
-    throw_status(env, st, ctx);
+static int need_len(JNIEnv* env, jarray a, jsize n, const char* what) {
+  if (!a || (*env)->GetArrayLength(env, a) < n) {
+    throw_msg(env, "java/lang/IndexOutOfBoundsException", what);
     return 0;
   }
-  h->ctx = ctx;
+  return 1;
+}
+
+/* UniformGrid(n, minX, maxX, minY, maxY) as double[5] */
+static int grid_of(JNIEnv* env, jdoubleArray jg, gf_grid* g) {
+  if (!need_len(env, jg, 5, "grid: {n, minX, maxX, minY, maxY}")) return GF_ERR_ARG;
+  jdouble d[5];
+  (*env)->GetDoubleArrayRegion(env, jg, 0, 5, d);
+  int st = gf_grid_make((int32_t)d[0], d[1], d[2], d[3], d[4], g);
+  if (st) throw_msg(env, "java/lang/IllegalArgumentException", "grid");
+  return st;
+}
+
+/* polygons as CSR int[] ringOff (npoly+1), int[] vertOff (nrings+1), double[] vx, vy */
+typedef struct {
+  jintArray ro, vo;
+  jdoubleArray vx, vy;
+  gf_polygons P;
+} jpolys;
+static int polys_get(JNIEnv* env, jpolys* j) {
+  memset(&j->P, 0, sizeof j->P);
+  if (!j->ro || !j->vo || !j->vx || !j->vy) {
+    throw_msg(env, "java/lang/IllegalArgumentException", "polygons");
+    return GF_ERR_ARG;
+  }
+  const jsize npoly = (*env)->GetArrayLength(env, j->ro) - 1;
+  const jsize nv = (*env)->GetArrayLength(env, j->vx);
+  if (npoly < 0 || (*env)->GetArrayLength(env, j->vy) != nv) {
+    throw_msg(env, "java/lang/IllegalArgumentException", "polygons: ringOff / vx / vy");
+    return GF_ERR_ARG;
+  }
+  j->P.npoly = npoly;
+  j->P.ring_off = (*env)->GetIntArrayElements(env, j->ro, NULL);
+  j->P.vert_off = (*env)->GetIntArrayElements(env, j->vo, NULL);
+  j->P.vx = (*env)->GetDoubleArrayElements(env, j->vx, NULL);
+  j->P.vy = (*env)->GetDoubleArrayElements(env, j->vy, NULL);
+  return GF_OK;  /* offsets are validated by the library (GF_ERR_ARG) */
+}
+static void polys_release(JNIEnv* env, jpolys* j) {
+  if (j->P.vy) (*env)->ReleaseDoubleArrayElements(env, j->vy, (jdouble*)j->P.vy, JNI_ABORT);
+  if (j->P.vx) (*env)->ReleaseDoubleArrayElements(env, j->vx, (jdouble*)j->P.vx, JNI_ABORT);
+  if (j->P.vert_off) (*env)->ReleaseIntArrayElements(env, j->vo, (jint*)j->P.vert_off, JNI_ABORT);
+  if (j->P.ring_off) (*env)->ReleaseIntArrayElements(env, j->ro, (jint*)j->P.ring_off, JNI_ABORT);
+}
+
+/* ---- context ---------------------------------------------------------------------------- */
+JNIEXPORT jlong JNICALL Java_GeoFlink_native_1_GeoFlinkHip_ctxCreate(JNIEnv* env, jclass cls, jint dev) {
+  shim_ctx* c = NULL;
+  throw_status(env, shim_ctx_create(dev, &c), NULL);
+  return (jlong)(intptr_t)c;
+}
+JNIEXPORT void JNICALL Java_GeoFlink_native_1_GeoFlinkHip_ctxDestroy(JNIEnv* env, jclass cls, jlong ctx) {
+  shim_ctx_destroy(CTX(ctx));
+}
+
+/* ---- objID Strings <-> keys --------------------------------------------------------------
+ * Java encodes the window's objID Strings as UTF-8 into one byte[] with long[] offsets (n + 1);
+ * decode returns the bytes and fills offsets, Java builds new String(bytes, off, len, UTF_8)
+ * (not NewStringUTF: modified UTF-8 differs for NUL and supplementary characters). */
+JNIEXPORT void JNICALL Java_GeoFlink_native_1_GeoFlinkHip_objidIntern(JNIEnv* env, jclass cls, jlong ctx,
+    jbyteArray jbytes, jlongArray joffs, jint n, jlongArray jkeys) {
+  if (n < 0 || !need_len(env, joffs, n + 1, "objidIntern: offs") || !need_len(env, jkeys, n, "objidIntern: keys"))
+    return;
+  jlong* offs = (*env)->GetLongArrayElements(env, joffs, NULL);
+  const jlong total = offs[n];
+  if (offs[0] != 0 || total < 0 || !need_len(env, jbytes, (jsize)total, "objidIntern: bytes")) {
+    (*env)->ReleaseLongArrayElements(env, joffs, offs, JNI_ABORT);
+    throw_msg(env, "java/lang/IllegalArgumentException", "objidIntern: offs");
+    return;
+  }
+  jbyte* bytes = (*env)->GetByteArrayElements(env, jbytes, NULL);
+  jlong* keys = (*env)->GetLongArrayElements(env, jkeys, NULL);
+  int st = shim_objid_intern(CTX(ctx), (const char*)bytes, (const int64_t*)offs, n, (int64_t*)keys);
+  (*env)->ReleaseLongArrayElements(env, jkeys, keys, st ? JNI_ABORT : 0);
+  (*env)->ReleaseByteArrayElements(env, jbytes, bytes, JNI_ABORT);
+  (*env)->ReleaseLongArrayElements(env, joffs, offs, JNI_ABORT);
+  throw_status(env, st, CTX(ctx));
+}
+
+JNIEXPORT jbyteArray JNICALL Java_GeoFlink_native_1_GeoFlinkHip_objidDecode(JNIEnv* env, jclass cls, jlong ctx,
+    jlongArray jkeys, jint n, jlongArray joffs) {
+  if (n < 0 || !need_len(env, jkeys, n, "objidDecode: keys") || !need_len(env, joffs, n + 1, "objidDecode: offs"))
+    return NULL;
+  jlong* keys = (*env)->GetLongArrayElements(env, jkeys, NULL);
+  jlong* offs = (*env)->GetLongArrayElements(env, joffs, NULL);
+  int64_t cap = 32 * (int64_t)n + 64;
+  char* b = (char*)malloc((size_t)cap);
+  int st = b ? shim_objid_decode(CTX(ctx), (const int64_t*)keys, n, b, cap, (int64_t*)offs) : GF_ERR_NOMEM;
+  if (st == GF_ERR_CAPACITY) {  /* offs[n] = the bytes needed */
+    cap = offs[n];
+    free(b);
+    b = (char*)malloc((size_t)(cap > 0 ? cap : 1));
+    st = b ? shim_objid_decode(CTX(ctx), (const int64_t*)keys, n, b, cap, (int64_t*)offs) : GF_ERR_NOMEM;
+  }
+  jbyteArray out = NULL;
+  if (!st) {
+    out = (*env)->NewByteArray(env, (jsize)offs[n]);
+    if (out) (*env)->SetByteArrayRegion(env, out, 0, (jsize)offs[n], (const jbyte*)b);
+  }
+  free(b);
+  (*env)->ReleaseLongArrayElements(env, joffs, offs, st ? JNI_ABORT : 0);
+  (*env)->ReleaseLongArrayElements(env, jkeys, keys, JNI_ABORT);
+  throw_status(env, st, CTX(ctx));
+  return out;
+}
+
+/* ---- kNN (PointPointKNNQuery.java:132-201 + KNNQuery.java:213-272; PointPolygonKNNQuery
+ * .java:245-317) ----------------------------------------------------------------------------- */
+JNIEXPORT jlong JNICALL Java_GeoFlink_native_1_GeoFlinkHip_knnPlan(JNIEnv* env, jclass cls, jlong ctx,
+    jdoubleArray jg, jdouble qx, jdouble qy, jdouble r, jint k) {
+  gf_grid g;
+  shim_knn* h = NULL;
+  if (grid_of(env, jg, &g)) return 0;
+  throw_status(env, shim_knn_plan(CTX(ctx), &g, qx, qy, r, k, &h), CTX(ctx));
   return (jlong)(intptr_t)h;
 }
 
-JNIEXPORT void JNICALL Java_GeoFlink_native_1_GeoFlinkHip_knnPlanDestroy(JNIEnv* env, jclass cls, jlong p) {
-  knn_handle* h = (knn_handle*)(intptr_t)p;
-  if (!h) return;
-  if (h->win.w) gf_window_destroy(h->win.w);
-  gf_knn_plan_destroy(h->plan);
-  free(h);
+JNIEXPORT jlong JNICALL Java_GeoFlink_native_1_GeoFlinkHip_knnPolygonPlan(JNIEnv* env, jclass cls, jlong ctx,
+    jdoubleArray jg, jintArray jro, jintArray jvo, jdoubleArray jvx, jdoubleArray jvy, jdouble r, jint k,
+    jboolean approximate) {
+  gf_grid g;
+  shim_knn* h = NULL;
+  jpolys p = {jro, jvo, jvx, jvy};
+  if (grid_of(env, jg, &g) || polys_get(env, &p)) {
+    polys_release(env, &p);
+    return 0;
+  }
+  int st = shim_knn_polygon_plan(CTX(ctx), &g, &p.P, r, k, approximate, &h);
+  polys_release(env, &p);
+  throw_status(env, st, CTX(ctx));
+  return (jlong)(intptr_t)h;
 }
 
-/* PointPointKNNQuery.windowBased apply + windowAll merge for one window */
-JNIEXPORT jint JNICALL Java_GeoFlink_native_1_GeoFlinkHip_knnWindow(JNIEnv* env, jclass cls, jlong p, jobject bx,
-    jobject by, jobject bo, jint n, jlongArray oo, jdoubleArray od, jlongArray oi) {
-  knn_handle* h = (knn_handle*)(intptr_t)p;
-  gf_points pts;
+JNIEXPORT void JNICALL Java_GeoFlink_native_1_GeoFlinkHip_knnPlanDestroy(JNIEnv* env, jclass cls, jlong plan) {
+  shim_knn_destroy((shim_knn*)(intptr_t)plan);
+}
+
+/* x, y (double), objID keys (long) of one window in direct buffers; out* hold >= k entries */
+JNIEXPORT jint JNICALL Java_GeoFlink_native_1_GeoFlinkHip_knnWindow(JNIEnv* env, jclass cls, jlong ctx, jlong plan,
+    jobject bx, jobject by, jobject bo, jint n, jlongArray oo, jdoubleArray od, jlongArray oi, jint k) {
+  const double* x = direct(env, bx, 8 * (int64_t)n, "knnWindow: x");
+  const double* y = direct(env, by, 8 * (int64_t)n, "knnWindow: y");
+  const int64_t* o = direct(env, bo, 8 * (int64_t)n, "knnWindow: objID");
+  if ((*env)->ExceptionCheck(env) || !need_len(env, oo, k, "knnWindow: out") || !need_len(env, od, k, "knnWindow: out") ||
+      !need_len(env, oi, k, "knnWindow: out"))
+    return 0;
   int32_t m = 0;
-  int st = upload(h->ctx, &h->win, buf(env, bx), buf(env, by), buf(env, bo), n, &pts);
   jlong* po = (*env)->GetPrimitiveArrayCritical(env, oo, NULL);
   jdouble* pd = (*env)->GetPrimitiveArrayCritical(env, od, NULL);
   jlong* pi = (*env)->GetPrimitiveArrayCritical(env, oi, NULL);
-  if (!st) st = gf_knn_run(h->plan, &pts, (int64_t*)po, pd, (int64_t*)pi, &m);
+  int st = shim_knn_window((shim_knn*)(intptr_t)plan, x, y, o, n, (int64_t*)po, pd, (int64_t*)pi, &m);
   (*env)->ReleasePrimitiveArrayCritical(env, oi, pi, 0);
   (*env)->ReleasePrimitiveArrayCritical(env, od, pd, 0);
   (*env)->ReleasePrimitiveArrayCritical(env, oo, po, 0);
-  if (st) {
-    throw_status(env, st, h->ctx);
-    return 0;
-  }
+  throw_status(env, st, CTX(ctx));
   return m;
 }
 
-/* ---- range ---------------------------------------------------------------------------- */
-typedef struct {
-  gf_ctx* ctx;
-  gf_range_plan* plan;
-  cached_window win;
-  uint64_t* bitmap;   /* device */
-  uint32_t* idx;      /* device */
-  int64_t cap;
-} range_handle;
-
-static jlong range_handle_new(JNIEnv* env, gf_ctx* ctx, gf_range_plan* plan, int st) {
-  range_handle* h = st ? NULL : (range_handle*)calloc(1, sizeof(range_handle));
-  if (st || !h) {
-    if (plan) gf_range_plan_destroy(plan);
-    throw_status(env, st ? st : GF_ERR_NOMEM, ctx);
+/* ---- sliding kNN: the pane engine (PointPointKNNQuery.java:158,198-200) ------------------- */
+JNIEXPORT jlong JNICALL Java_GeoFlink_native_1_GeoFlinkHip_knnSlidingCreate(JNIEnv* env, jclass cls, jlong ctx,
+    jlong plan, jlong size_ms, jlong slide_ms) {
+  shim_sliding* s = NULL;
+  throw_status(env, shim_sliding_create((shim_knn*)(intptr_t)plan, size_ms, slide_ms, &s), CTX(ctx));
+  return (jlong)(intptr_t)s;
+}
+JNIEXPORT void JNICALL Java_GeoFlink_native_1_GeoFlinkHip_knnSlidingDestroy(JNIEnv* env, jclass cls, jlong s) {
+  shim_sliding_destroy((shim_sliding*)(intptr_t)s);
+}
+JNIEXPORT jlong JNICALL Java_GeoFlink_native_1_GeoFlinkHip_knnSlidingPaneMs(JNIEnv* env, jclass cls, jlong s) {
+  int64_t p = 0;
+  shim_sliding_pane_ms((shim_sliding*)(intptr_t)s, &p);
+  return p;
+}
+/* returns the end (ms) of the window the pane closed, or -1 */
+JNIEXPORT jlong JNICALL Java_GeoFlink_native_1_GeoFlinkHip_knnSlidingPush(JNIEnv* env, jclass cls, jlong ctx,
+    jlong s, jlong pane, jobject bx, jobject by, jobject bo, jint n) {
+  const double* x = direct(env, bx, 8 * (int64_t)n, "knnSlidingPush: x");
+  const double* y = direct(env, by, 8 * (int64_t)n, "knnSlidingPush: y");
+  const int64_t* o = direct(env, bo, 8 * (int64_t)n, "knnSlidingPush: objID");
+  if ((*env)->ExceptionCheck(env)) return -1;
+  int32_t closed = 0;
+  int64_t end = -1;
+  int st = shim_sliding_push((shim_sliding*)(intptr_t)s, pane, x, y, o, n, &closed, &end);
+  throw_status(env, st, CTX(ctx));
+  return !st && closed ? end : -1;
+}
+JNIEXPORT jint JNICALL Java_GeoFlink_native_1_GeoFlinkHip_knnSlidingDecode(JNIEnv* env, jclass cls, jlong ctx,
+    jlong s, jlong window_end, jlongArray oo, jdoubleArray od, jlongArray oi, jint k) {
+  if (!need_len(env, oo, k, "knnSlidingDecode: out") || !need_len(env, od, k, "knnSlidingDecode: out") ||
+      !need_len(env, oi, k, "knnSlidingDecode: out"))
     return 0;
-  }
-  h->ctx = ctx;
-  h->plan = plan;
+  int32_t m = 0;
+  jlong* po = (*env)->GetPrimitiveArrayCritical(env, oo, NULL);
+  jdouble* pd = (*env)->GetPrimitiveArrayCritical(env, od, NULL);
+  jlong* pi = (*env)->GetPrimitiveArrayCritical(env, oi, NULL);
+  int st = shim_sliding_decode((shim_sliding*)(intptr_t)s, window_end, (int64_t*)po, pd, (int64_t*)pi, &m);
+  (*env)->ReleasePrimitiveArrayCritical(env, oi, pi, 0);
+  (*env)->ReleasePrimitiveArrayCritical(env, od, pd, 0);
+  (*env)->ReleasePrimitiveArrayCritical(env, oo, po, 0);
+  throw_status(env, st, CTX(ctx));
+  return m;
+}
+
+/* ---- range (PointPointRangeQuery.java:150-186, PointPolygonRangeQuery.java:170-204) -------- */
+JNIEXPORT jlong JNICALL Java_GeoFlink_native_1_GeoFlinkHip_rangePlan(JNIEnv* env, jclass cls, jlong ctx,
+    jdoubleArray jg, jdoubleArray jqx, jdoubleArray jqy, jdouble r, jboolean approximate) {
+  gf_grid g;
+  shim_range* h = NULL;
+  if (grid_of(env, jg, &g)) return 0;
+  const jsize nq = jqx ? (*env)->GetArrayLength(env, jqx) : -1;
+  if (nq < 0 || !need_len(env, jqy, nq, "rangePlan: qy")) return 0;
+  jdouble* qx = (*env)->GetDoubleArrayElements(env, jqx, NULL);
+  jdouble* qy = (*env)->GetDoubleArrayElements(env, jqy, NULL);
+  int st = shim_range_plan(CTX(ctx), &g, qx, qy, nq, r, approximate, &h);
+  (*env)->ReleaseDoubleArrayElements(env, jqy, qy, JNI_ABORT);
+  (*env)->ReleaseDoubleArrayElements(env, jqx, qx, JNI_ABORT);
+  throw_status(env, st, CTX(ctx));
   return (jlong)(intptr_t)h;
 }
 
-JNIEXPORT jlong JNICALL Java_GeoFlink_native_1_GeoFlinkHip_rangePlan(JNIEnv* env, jclass cls, jlong ctxh, jint n,
-    jdouble minX, jdouble maxX, jdouble minY, jdouble maxY, jdoubleArray jqx, jdoubleArray jqy, jdouble r,
+JNIEXPORT jlong JNICALL Java_GeoFlink_native_1_GeoFlinkHip_rangePolygonPlan(JNIEnv* env, jclass cls, jlong ctx,
+    jdoubleArray jg, jintArray jro, jintArray jvo, jdoubleArray jvx, jdoubleArray jvy, jdouble r,
     jboolean approximate) {
-  gf_ctx* ctx = (gf_ctx*)(intptr_t)ctxh;
   gf_grid g;
-  gf_range_plan* plan = NULL;
-  int st = gf_grid_make(n, minX, maxX, minY, maxY, &g);
-  jdouble* qx = (*env)->GetDoubleArrayElements(env, jqx, NULL);
-  jdouble* qy = (*env)->GetDoubleArrayElements(env, jqy, NULL);
-  if (!st) st = gf_range_pp_plan_create(ctx, &g, qx, qy, (*env)->GetArrayLength(env, jqx), r, approximate,
-                                        GF_METRIC_SQRT, &plan);
-  (*env)->ReleaseDoubleArrayElements(env, jqy, qy, JNI_ABORT);
-  (*env)->ReleaseDoubleArrayElements(env, jqx, qx, JNI_ABORT);
-  return range_handle_new(env, ctx, plan, st);
-}
-
-static void polygons_get(JNIEnv* env, jintArray jro, jintArray jvo, jdoubleArray jvx, jdoubleArray jvy, gf_polygons* P) {
-  P->npoly = (*env)->GetArrayLength(env, jro) - 1;
-  P->ring_off = (*env)->GetIntArrayElements(env, jro, NULL);
-  P->vert_off = (*env)->GetIntArrayElements(env, jvo, NULL);
-  P->vx = (*env)->GetDoubleArrayElements(env, jvx, NULL);
-  P->vy = (*env)->GetDoubleArrayElements(env, jvy, NULL);
-}
-
-static void polygons_release(JNIEnv* env, jintArray jro, jintArray jvo, jdoubleArray jvx, jdoubleArray jvy,
-                             gf_polygons* P) {
-  (*env)->ReleaseDoubleArrayElements(env, jvy, (jdouble*)P->vy, JNI_ABORT);
-  (*env)->ReleaseDoubleArrayElements(env, jvx, (jdouble*)P->vx, JNI_ABORT);
-  (*env)->ReleaseIntArrayElements(env, jvo, (jint*)P->vert_off, JNI_ABORT);
-  (*env)->ReleaseIntArrayElements(env, jro, (jint*)P->ring_off, JNI_ABORT);
-}
-
-JNIEXPORT jlong JNICALL Java_GeoFlink_native_1_GeoFlinkHip_rangePolygonPlan(JNIEnv* env, jclass cls, jlong ctxh,
-    jint n, jdouble minX, jdouble maxX, jdouble minY, jdouble maxY, jintArray jro, jintArray jvo, jdoubleArray jvx,
-    jdoubleArray jvy, jdouble r, jboolean approximate) {
-  gf_ctx* ctx = (gf_ctx*)(intptr_t)ctxh;
-  gf_grid g;
-  gf_polygons P;
-  gf_range_plan* plan = NULL;
-  int st = gf_grid_make(n, minX, maxX, minY, maxY, &g);
-  polygons_get(env, jro, jvo, jvx, jvy, &P);
-  if (!st) st = gf_range_ppoly_plan_create(ctx, &g, &P, r, approximate, GF_METRIC_SQRT, &plan);
-  polygons_release(env, jro, jvo, jvx, jvy, &P);
-  return range_handle_new(env, ctx, plan, st);
-}
-
-JNIEXPORT void JNICALL Java_GeoFlink_native_1_GeoFlinkHip_rangePlanDestroy(JNIEnv* env, jclass cls, jlong p) {
-  range_handle* h = (range_handle*)(intptr_t)p;
-  if (!h) return;
-  if (h->win.w) gf_window_destroy(h->win.w);
-  hipFree(h->bitmap);
-  hipFree(h->idx);
-  gf_range_plan_destroy(h->plan);
-  free(h);
-}
-
-/* PointPointRangeQuery / PointPolygonRangeQuery window apply: emitted indices, ascending */
-JNIEXPORT jintArray JNICALL Java_GeoFlink_native_1_GeoFlinkHip_rangeWindow(JNIEnv* env, jclass cls, jlong p,
-    jobject bx, jobject by, jint n) {
-  range_handle* h = (range_handle*)(intptr_t)p;
-  gf_points pts;
-  int64_t count = 0;
-  int st = upload(h->ctx, &h->win, buf(env, bx), buf(env, by), NULL, n, &pts);
-  if (!st && h->cap < n) {  /* per-plan result buffers, grown with the window */
-    hipFree(h->bitmap);
-    hipFree(h->idx);
-    h->bitmap = NULL;
-    h->idx = NULL;
-    h->cap = h->win.cap;
-    if (hipMalloc((void**)&h->bitmap, 8 * (size_t)((h->cap + 63) / 64)) != hipSuccess ||
-        hipMalloc((void**)&h->idx, 4 * (size_t)h->cap) != hipSuccess) {
-      h->cap = 0;
-      st = GF_ERR_NOMEM;
-    }
-  }
-  if (!st) st = gf_range_run(h->plan, &pts, h->bitmap, NULL, NULL);
-  if (!st) st = gf_bitmap_to_indices(h->ctx, h->bitmap, n, h->idx, h->cap, &count);
-  jintArray out = NULL;
-  if (!st) {
-    out = (*env)->NewIntArray(env, (jsize)count);
-    jint* po = (*env)->GetPrimitiveArrayCritical(env, out, NULL);
-    if (hipMemcpy(po, h->idx, 4 * (size_t)count, hipMemcpyDeviceToHost) != hipSuccess) st = GF_ERR_HIP;
-    (*env)->ReleasePrimitiveArrayCritical(env, out, po, 0);
-  }
-  if (st) throw_status(env, st, h->ctx);
-  return out;
-}
-
-/* ---- joins ---------------------------------------------------------------------------- */
-static int grid_of(JNIEnv* env, jdoubleArray jg, gf_grid* g) {
-  jdouble* d = (*env)->GetDoubleArrayElements(env, jg, NULL);  /* n, minX, maxX, minY, maxY */
-  int st = gf_grid_make((int32_t)d[0], d[1], d[2], d[3], d[4], g);
-  (*env)->ReleaseDoubleArrayElements(env, jg, d, JNI_ABORT);
-  return st;
-}
-
-/* device pairs -> a Java long[2m] of (ordinary / point index, query / polygon index) */
-static jlongArray pairs_out(JNIEnv* env, const uint32_t* dev_pairs, int64_t m, int* st) {
-  uint32_t* host = (uint32_t*)malloc(8 * (size_t)(m > 0 ? m : 1));
-  jlongArray out = NULL;
-  if (!host || hipMemcpy(host, dev_pairs, 8 * (size_t)m, hipMemcpyDeviceToHost) != hipSuccess) {
-    *st = GF_ERR_HIP;
-  } else {
-    out = (*env)->NewLongArray(env, (jsize)(2 * m));
-    jlong* po = (*env)->GetPrimitiveArrayCritical(env, out, NULL);
-    for (int64_t i = 0; i < 2 * m; ++i) po[i] = host[i];
-    (*env)->ReleasePrimitiveArrayCritical(env, out, po, 0);
-  }
-  free(host);
-  return out;
-}
-
-/* JoinQuery.getReplicatedPointQueryStream + PointPointJoinQuery.windowBased for one window pair.
- * Two-phase capacity: count with pairs = NULL, then allocate and run. */
-JNIEXPORT jlongArray JNICALL Java_GeoFlink_native_1_GeoFlinkHip_joinWindow(JNIEnv* env, jclass cls, jlong ctxh,
-    jdoubleArray jug, jdoubleArray jqg, jobject box, jobject boy, jint no, jobject bqx, jobject bqy, jint nq,
-    jdouble r, jboolean approximate) {
-  gf_ctx* ctx = (gf_ctx*)(intptr_t)ctxh;
-  static __thread cached_window wo, wq;  /* one context per subtask thread */
-  gf_grid ug, qg;
-  gf_points po, pq;
-  int64_t m = 0;
-  uint32_t* dev_pairs = NULL;
-  int st = grid_of(env, jug, &ug);
-  if (!st) st = grid_of(env, jqg, &qg);
-  if (!st) st = upload(ctx, &wo, buf(env, box), buf(env, boy), NULL, no, &po);
-  if (!st) st = upload(ctx, &wq, buf(env, bqx), buf(env, bqy), NULL, nq, &pq);
-  if (!st) st = gf_join_pp(ctx, &ug, &qg, &po, &pq, r, approximate, GF_METRIC_SQRT, NULL, 0, &m);
-  if (st == GF_ERR_CAPACITY) {
-    st = hipMalloc((void**)&dev_pairs, 8 * (size_t)(m > 0 ? m : 1)) == hipSuccess ? GF_OK : GF_ERR_NOMEM;
-    if (!st) st = gf_join_pp(ctx, &ug, &qg, &po, &pq, r, approximate, GF_METRIC_SQRT, dev_pairs, m, &m);
-  }
-  jlongArray out = NULL;
-  if (!st) out = pairs_out(env, dev_pairs, m, &st);
-  hipFree(dev_pairs);
-  if (st) throw_status(env, st, ctx);
-  return out;
-}
-
-/* JoinQuery.getReplicatedPolygonQueryStream + PointPolygonJoinQuery.windowBased */
-JNIEXPORT jlongArray JNICALL Java_GeoFlink_native_1_GeoFlinkHip_polygonJoinWindow(JNIEnv* env, jclass cls,
-    jlong ctxh, jdoubleArray jg, jobject bx, jobject by, jint n, jintArray jro, jintArray jvo, jdoubleArray jvx,
-    jdoubleArray jvy, jdouble r, jboolean approximate) {
-  gf_ctx* ctx = (gf_ctx*)(intptr_t)ctxh;
-  static __thread cached_window wp;
-  gf_grid g;
-  gf_polygons P;
-  gf_points pts;
-  gf_range_plan* plan = NULL;
-  int64_t m = 0;
-  uint32_t* dev_pairs = NULL;
-  int st = grid_of(env, jg, &g);
-  polygons_get(env, jro, jvo, jvx, jvy, &P);
-  if (!st) st = gf_join_ppoly_plan_create(ctx, &g, &P, r, approximate, GF_METRIC_SQRT, &plan);
-  polygons_release(env, jro, jvo, jvx, jvy, &P);
-  if (!st) st = upload(ctx, &wp, buf(env, bx), buf(env, by), NULL, n, &pts);
-  if (!st) st = gf_join_ppoly_run(plan, &g, &pts, NULL, 0, &m);
-  if (st == GF_ERR_CAPACITY) {
-    st = hipMalloc((void**)&dev_pairs, 8 * (size_t)(m > 0 ? m : 1)) == hipSuccess ? GF_OK : GF_ERR_NOMEM;
-    if (!st) st = gf_join_ppoly_run(plan, &g, &pts, dev_pairs, m, &m);
-  }
-  jlongArray out = NULL;
-  if (!st) out = pairs_out(env, dev_pairs, m, &st);
-  hipFree(dev_pairs);
-  if (plan) gf_range_plan_destroy(plan);
-  if (st) throw_status(env, st, ctx);
-  return out;
-}
-
-/* ---- ingest --------------------------------------------------------------------------- */
-/* device text buffer, per subtask thread, grown on demand */
-static int device_text(JNIEnv* env, jobject btext, jint len, char** dev) {
-  static __thread char* d = NULL;
-  static __thread size_t cap = 0;
-  if ((size_t)len > cap) {
-    hipFree(d);
-    d = NULL;
-    cap = (size_t)len + (size_t)len / 4 + 4096;
-    if (hipMalloc((void**)&d, cap) != hipSuccess) {
-      cap = 0;
-      return GF_ERR_NOMEM;
-    }
-  }
-  if (len && hipMemcpy(d, buf(env, btext), (size_t)len, hipMemcpyHostToDevice) != hipSuccess) return GF_ERR_HIP;
-  *dev = d;
-  return GF_OK;
-}
-
-/* parsed device columns -> the caller's direct buffers */
-static int columns_out(JNIEnv* env, int64_t n, double* x, double* y, int64_t* o, int64_t* t, jobject bx, jobject by,
-                       jobject bo, jobject bt) {
-  const size_t b = 8 * (size_t)n;
-  if (hipMemcpy(buf(env, bx), x, b, hipMemcpyDeviceToHost) != hipSuccess ||
-      hipMemcpy(buf(env, by), y, b, hipMemcpyDeviceToHost) != hipSuccess ||
-      hipMemcpy(buf(env, bo), o, b, hipMemcpyDeviceToHost) != hipSuccess ||
-      hipMemcpy(buf(env, bt), t, b, hipMemcpyDeviceToHost) != hipSuccess)
-    return GF_ERR_HIP;
-  return GF_OK;
-}
-
-static jint parse_common(JNIEnv* env, gf_ctx* ctx, jobject btext, jint len, jobject bx, jobject by, jobject bo,
-                         jobject bt, jint capacity, int geojson, const void* schema) {
-  char* text = NULL;
-  double *x = NULL, *y = NULL;
-  int64_t *o = NULL, *t = NULL, n = 0, bad_line = -1;
-  int32_t bad_kind = 0;
-  const size_t b = 8 * (size_t)(capacity > 0 ? capacity : 1);
-  int st = device_text(env, btext, len, &text);
-  if (!st && (hipMalloc((void**)&x, b) != hipSuccess || hipMalloc((void**)&y, b) != hipSuccess ||
-              hipMalloc((void**)&o, b) != hipSuccess || hipMalloc((void**)&t, b) != hipSuccess))
-    st = GF_ERR_NOMEM;
-  if (!st)
-    st = geojson ? gf_geojson_parse(ctx, NULL, text, len, (const gf_geojson_schema*)schema, NULL, x, y, o, t, NULL,
-                                    NULL, capacity, &n, &bad_line, &bad_kind)
-                 : gf_csv_parse(ctx, text, len, (const gf_csv_schema*)schema, NULL, x, y, o, t, NULL, NULL, capacity,
-                                &n, &bad_line, &bad_kind);
-  if (!st) st = columns_out(env, n, x, y, o, t, bx, by, bo, bt);
-  hipFree(x);
-  hipFree(y);
-  hipFree(o);
-  hipFree(t);
-  if (st) {
-    throw_status(env, st, ctx);  /* GF_ERR_ARG: the reference's map would have thrown on bad_line */
+  shim_range* h = NULL;
+  jpolys p = {jro, jvo, jvx, jvy};
+  if (grid_of(env, jg, &g) || polys_get(env, &p)) {
+    polys_release(env, &p);
     return 0;
   }
-  return (jint)n;
+  int st = shim_range_polygon_plan(CTX(ctx), &g, &p.P, r, approximate, &h);
+  polys_release(env, &p);
+  throw_status(env, st, CTX(ctx));
+  return (jlong)(intptr_t)h;
 }
 
-/* Deserialization.CSVTSVToTSpatial.map over a chunk of complete lines */
-JNIEXPORT jint JNICALL Java_GeoFlink_native_1_GeoFlinkHip_csvParse(JNIEnv* env, jclass cls, jlong ctxh, jobject btext,
-    jint len, jchar delimiter, jintArray jschema, jobject bx, jobject by, jobject bo, jobject bt, jint capacity) {
+JNIEXPORT void JNICALL Java_GeoFlink_native_1_GeoFlinkHip_rangePlanDestroy(JNIEnv* env, jclass cls, jlong plan) {
+  shim_range_destroy((shim_range*)(intptr_t)plan);
+}
+
+/* emitted point indices, ascending, into the direct int buffer out (capacity outCap ints);
+ * returns their count -- larger than outCap: the buffer was too small, call again with more */
+JNIEXPORT jlong JNICALL Java_GeoFlink_native_1_GeoFlinkHip_rangeWindow(JNIEnv* env, jclass cls, jlong ctx,
+    jlong plan, jobject bx, jobject by, jint n, jobject bout, jint out_cap) {
+  const double* x = direct(env, bx, 8 * (int64_t)n, "rangeWindow: x");
+  const double* y = direct(env, by, 8 * (int64_t)n, "rangeWindow: y");
+  int32_t* out = direct(env, bout, 4 * (int64_t)out_cap, "rangeWindow: out");
+  if ((*env)->ExceptionCheck(env)) return 0;
+  int64_t count = 0;
+  int st = shim_range_window((shim_range*)(intptr_t)plan, x, y, n, out, out_cap, &count);
+  if (st != GF_ERR_CAPACITY) throw_status(env, st, CTX(ctx));
+  return count;
+}
+
+/* ---- joins (JoinQuery.java:73-115, PointPointJoinQuery.java:148-182,
+ * PointPolygonJoinQuery.java:154-213) -> long[2m] of (ordinary / point, query / polygon) ------ */
+static jlongArray pairs_array(JNIEnv* env, const uint32_t* pairs, int64_t m) {
+  jlongArray out = (*env)->NewLongArray(env, (jsize)(2 * m));
+  if (!out) return NULL;
+  jlong* po = (*env)->GetPrimitiveArrayCritical(env, out, NULL);
+  for (int64_t i = 0; i < 2 * m; ++i) po[i] = pairs[i];
+  (*env)->ReleasePrimitiveArrayCritical(env, out, po, 0);
+  return out;
+}
+
+JNIEXPORT jlongArray JNICALL Java_GeoFlink_native_1_GeoFlinkHip_joinWindow(JNIEnv* env, jclass cls, jlong ctx,
+    jdoubleArray jug, jdoubleArray jqg, jobject box, jobject boy, jint no, jobject bqx, jobject bqy, jint nq,
+    jdouble r, jboolean approximate) {
+  gf_grid ug, qg;
+  if (grid_of(env, jug, &ug) || grid_of(env, jqg, &qg)) return NULL;
+  const double* ox = direct(env, box, 8 * (int64_t)no, "joinWindow: ox");
+  const double* oy = direct(env, boy, 8 * (int64_t)no, "joinWindow: oy");
+  const double* qx = direct(env, bqx, 8 * (int64_t)nq, "joinWindow: qx");
+  const double* qy = direct(env, bqy, 8 * (int64_t)nq, "joinWindow: qy");
+  if ((*env)->ExceptionCheck(env)) return NULL;
+  const uint32_t* pairs = NULL;
+  int64_t m = 0;
+  int st = shim_join_window(CTX(ctx), &ug, &qg, ox, oy, no, qx, qy, nq, r, approximate, &pairs, &m);
+  if (throw_status(env, st, CTX(ctx))) return NULL;
+  return pairs_array(env, pairs, m);
+}
+
+JNIEXPORT jlongArray JNICALL Java_GeoFlink_native_1_GeoFlinkHip_polygonJoinWindow(JNIEnv* env, jclass cls,
+    jlong ctx, jdoubleArray jg, jobject bx, jobject by, jint n, jintArray jro, jintArray jvo, jdoubleArray jvx,
+    jdoubleArray jvy, jdouble r, jboolean approximate) {
+  gf_grid g;
+  if (grid_of(env, jg, &g)) return NULL;
+  const double* x = direct(env, bx, 8 * (int64_t)n, "polygonJoinWindow: x");
+  const double* y = direct(env, by, 8 * (int64_t)n, "polygonJoinWindow: y");
+  if ((*env)->ExceptionCheck(env)) return NULL;
+  jpolys p = {jro, jvo, jvx, jvy};
+  const uint32_t* pairs = NULL;
+  int64_t m = 0;
+  int st = polys_get(env, &p);
+  if (!st) st = shim_polygon_join_window(CTX(ctx), &g, x, y, n, &p.P, r, approximate, &pairs, &m);
+  polys_release(env, &p);
+  if (throw_status(env, st, CTX(ctx))) return NULL;
+  return pairs_array(env, pairs, m);
+}
+
+/* ---- ingest (Deserialization.java:149-211, 291-325) ----------------------------------------
+ * a chunk of complete lines in a direct buffer -> x, y, objID keys, ts (direct buffers of
+ * `capacity` entries); returns the points parsed.  A bad line throws IllegalArgumentException
+ * naming its index and kind -- the reference's map would have thrown on it. */
+static jint parse_out(JNIEnv* env, shim_ctx* c, int st, int64_t n, int64_t bad_line, int32_t bad_kind) {
+  if (st == GF_ERR_ARG && bad_line >= 0) {
+    char msg[160];
+    snprintf(msg, sizeof msg, "line %lld: %s (kind %d)", (long long)bad_line,
+             bad_kind == GF_CSV_NUMBER_FORMAT ? "NumberFormatException" : "malformed record", (int)bad_kind);
+    throw_msg(env, bad_kind == GF_CSV_NUMBER_FORMAT ? "java/lang/NumberFormatException"
+                                                   : "java/lang/IllegalArgumentException", msg);
+    return 0;
+  }
+  if (st == GF_ERR_CAPACITY) {
+    throw_msg(env, "java/lang/IndexOutOfBoundsException", "parse: more lines than capacity");
+    return 0;
+  }
+  throw_status(env, st, c);
+  return st ? 0 : (jint)n;
+}
+
+JNIEXPORT jint JNICALL Java_GeoFlink_native_1_GeoFlinkHip_csvParse(JNIEnv* env, jclass cls, jlong ctx,
+    jobject btext, jint len, jchar delimiter, jintArray jschema, jobject bx, jobject by, jobject bo, jobject bt,
+    jint capacity) {
+  const char* text = direct(env, btext, len, "csvParse: text");
+  double* x = direct(env, bx, 8 * (int64_t)capacity, "csvParse: x");
+  double* y = direct(env, by, 8 * (int64_t)capacity, "csvParse: y");
+  int64_t* o = direct(env, bo, 8 * (int64_t)capacity, "csvParse: objID");
+  int64_t* t = direct(env, bt, 8 * (int64_t)capacity, "csvParse: ts");
+  if ((*env)->ExceptionCheck(env) || !need_len(env, jschema, 4, "csvParse: schema {objID, ts, x, y}")) return 0;
   gf_csv_schema sc;
   memset(&sc, 0, sizeof sc);
-  jint* s = (*env)->GetIntArrayElements(env, jschema, NULL);
+  jint s[4];
+  (*env)->GetIntArrayRegion(env, jschema, 0, 4, s);
   sc.delimiter = (char)delimiter;
   sc.objid_field = s[0];
   sc.time_field = s[1];
   sc.x_field = s[2];
   sc.y_field = s[3];
-  (*env)->ReleaseIntArrayElements(env, jschema, s, JNI_ABORT);
-  return parse_common(env, (gf_ctx*)(intptr_t)ctxh, btext, len, bx, by, bo, bt, capacity, 0, &sc);
+  int64_t n = 0, bad_line = -1;
+  int32_t bad_kind = 0;
+  int st = shim_csv_parse(CTX(ctx), text, len, &sc, x, y, o, t, capacity, &n, &bad_line, &bad_kind);
+  return parse_out(env, CTX(ctx), st, n, bad_line, bad_kind);
 }
 
-/* Deserialization.GeoJSONToTSpatial.map over a chunk of lines (oID / timestamp properties, the
- * reference's Serialization names; date strings "yyyy-MM-dd HH:mm:ss" in the JVM's zone) */
-JNIEXPORT jint JNICALL Java_GeoFlink_native_1_GeoFlinkHip_geoJsonParse(JNIEnv* env, jclass cls, jlong ctxh,
-    jobject btext, jint len, jobject bx, jobject by, jobject bo, jobject bt, jint capacity) {
+/* GeoJSONToTSpatial(uGrid, dateFormat, propertyTimeStamp, propertyObjID) (Deserialization.java:
+ * 64-70,158-165): dateFormat null -> 0 (integer ms), else 1 ("yyyy-MM-dd HH:mm:ss", the only
+ * pattern restated; another throws IllegalArgumentException); tzOffsetMinutes =
+ * TimeZone.getDefault().getRawOffset() / 60000 on the Java side; valueLines = each line is the
+ * record's value (Serialization.PointToGeoJSONOutputSchema output) instead of the Kafka record */
+JNIEXPORT jint JNICALL Java_GeoFlink_native_1_GeoFlinkHip_geoJsonParse(JNIEnv* env, jclass cls, jlong ctx,
+    jobject btext, jint len, jstring jts_prop, jstring jobj_prop, jstring jdate_format, jint tz_offset_minutes,
+    jboolean value_lines, jobject bx, jobject by, jobject bo, jobject bt, jint capacity) {
+  const char* text = direct(env, btext, len, "geoJsonParse: text");
+  double* x = direct(env, bx, 8 * (int64_t)capacity, "geoJsonParse: x");
+  double* y = direct(env, by, 8 * (int64_t)capacity, "geoJsonParse: y");
+  int64_t* o = direct(env, bo, 8 * (int64_t)capacity, "geoJsonParse: objID");
+  int64_t* t = direct(env, bt, 8 * (int64_t)capacity, "geoJsonParse: ts");
+  if ((*env)->ExceptionCheck(env)) return 0;
   gf_geojson_schema sc;
-  sc.objid_property = "oID";
-  sc.time_property = "timestamp";
-  sc.date_format = 1;
-  sc.tz_offset_minutes = 0;  /* the shim sets TimeZone.getDefault().getRawOffset() / 60000 here */
-  return parse_common(env, (gf_ctx*)(intptr_t)ctxh, btext, len, bx, by, bo, bt, capacity, 1, &sc);
+  memset(&sc, 0, sizeof sc);
+  const char* fmt = jdate_format ? (*env)->GetStringUTFChars(env, jdate_format, NULL) : NULL;
+  if (fmt && strcmp(fmt, "yyyy-MM-dd HH:mm:ss") != 0) {
+    (*env)->ReleaseStringUTFChars(env, jdate_format, fmt);
+    throw_msg(env, "java/lang/IllegalArgumentException", "geoJsonParse: dateFormat other than yyyy-MM-dd HH:mm:ss");
+    return 0;
+  }
+  sc.date_format = fmt ? 1 : 0;
+  sc.tz_offset_minutes = tz_offset_minutes;
+  sc.value_lines = value_lines ? 1 : 0;
+  sc.time_property = jts_prop ? (*env)->GetStringUTFChars(env, jts_prop, NULL) : NULL;
+  sc.objid_property = jobj_prop ? (*env)->GetStringUTFChars(env, jobj_prop, NULL) : NULL;
+  int64_t n = 0, bad_line = -1;
+  int32_t bad_kind = 0;
+  int st = shim_geojson_parse(CTX(ctx), text, len, &sc, x, y, o, t, capacity, &n, &bad_line, &bad_kind);
+  if (sc.objid_property) (*env)->ReleaseStringUTFChars(env, jobj_prop, sc.objid_property);
+  if (sc.time_property) (*env)->ReleaseStringUTFChars(env, jts_prop, sc.time_property);
+  if (fmt) (*env)->ReleaseStringUTFChars(env, jdate_format, fmt);
+  return parse_out(env, CTX(ctx), st, n, bad_line, bad_kind);
 }

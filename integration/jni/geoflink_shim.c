@@ -1,0 +1,474 @@
+/*
+ * geoflink_shim.c -- the plain-C core of the JNI shim (see geoflink_shim.h).
+ * Built with any C compiler against include/geoflink_hip.h and the HIP runtime:
+ *
+ *   gcc -O2 -fPIC -c -Iinclude -I/opt/rocm/include -D__HIP_PLATFORM_AMD__ integration/jni/geoflink_shim.c
+ *
+ * and linked into libgeoflink_jni.so together with geoflink_jni.c (which needs a JDK), or into
+ * tests/native/shim_check.c (which does not).
+ */
+#include "geoflink_shim.h"
+
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <hip/hip_runtime_api.h>
+
+/* a device buffer grown on demand (never shrunk) */
+typedef struct {
+  void* p;
+  size_t cap;
+} dbuf;
+static int dbuf_need(dbuf* b, size_t bytes) {
+  if (b->p && b->cap >= bytes) return GF_OK;
+  if (b->p) hipFree(b->p);
+  b->p = NULL;
+  b->cap = bytes > 4096 ? bytes + bytes / 4 : 4096;
+  if (hipMalloc(&b->p, b->cap) != hipSuccess) {
+    b->cap = 0;
+    return GF_ERR_NOMEM;
+  }
+  return GF_OK;
+}
+static void dbuf_free(dbuf* b) {
+  if (b->p) hipFree(b->p);
+  b->p = NULL;
+  b->cap = 0;
+}
+/* pinned (mapped) host memory grown on demand: kernels write it, the host reads it after a sync */
+typedef struct {
+  void* p;
+  size_t cap;
+} pbuf;
+static int pbuf_need(pbuf* b, size_t bytes) {
+  if (b->p && b->cap >= bytes) return GF_OK;
+  if (b->p) gf_pinned_free(b->p);
+  b->p = NULL;
+  b->cap = bytes > 4096 ? bytes + bytes / 4 : 4096;
+  int st = gf_pinned_alloc(b->cap, &b->p);
+  if (st) b->cap = 0;
+  return st;
+}
+static void pbuf_free(pbuf* b) {
+  if (b->p) gf_pinned_free(b->p);
+  b->p = NULL;
+  b->cap = 0;
+}
+
+/* a device window of at least n points, grown (recreated) only when a window is larger */
+typedef struct {
+  gf_window* w;
+  int64_t cap;
+} cached_window;
+static int window_for(gf_ctx* ctx, cached_window* c, int64_t n) {
+  if (c->w && c->cap >= n) return GF_OK;
+  if (c->w) gf_window_destroy(c->w);
+  c->w = NULL;
+  c->cap = n > 1024 ? n + n / 4 : 1024;
+  return gf_window_create(ctx, c->cap, &c->w);
+}
+/* upload the given columns (ts never: window evaluation does not read it) -> device points,
+ * ordered after the copy on the context's streams */
+static int upload(gf_ctx* ctx, cached_window* c, const double* x, const double* y, const int64_t* objID, int64_t n,
+                  gf_points* pts) {
+  int st = window_for(ctx, c, n);
+  if (!st) st = gf_window_upload(c->w, x, y, objID, NULL, n);
+  if (!st) st = gf_window_points(c->w, pts);
+  return st;
+}
+static void window_free(cached_window* c) {
+  if (c->w) gf_window_destroy(c->w);
+  c->w = NULL;
+  c->cap = 0;
+}
+
+struct shim_ctx {
+  gf_ctx* ctx;
+  char err[256];
+  cached_window wo, wq;   /* join windows (ordinary / query or point side) */
+  dbuf pairs;             /* device join pairs */
+  pbuf hpairs;            /* their pinned host copy (shim_join_window's *pairs) */
+  int64_t pair_hint;      /* capacity of the last join's pairs */
+  dbuf text, cols;        /* ingest: device text, 4 device columns */
+};
+
+/* a copy ordered on the context's stream (after the work enqueued there, before what follows) */
+static int copy(shim_ctx* c, void* dst, const void* src, size_t bytes, hipMemcpyKind kind) {
+  return hipMemcpyAsync(dst, src, bytes, kind, (hipStream_t)gf_ctx_stream(c->ctx)) != hipSuccess;
+}
+
+static int fail(shim_ctx* c, int st, const char* what) {
+  if (st && c) {
+    const char* e = c->ctx ? gf_ctx_last_error(c->ctx) : "";
+    snprintf(c->err, sizeof c->err, "%s: %s%s%s", what, gf_status_string(st), e && *e ? ": " : "", e ? e : "");
+  }
+  return st;
+}
+
+int shim_ctx_create(int device, shim_ctx** out) {
+  *out = NULL;
+  shim_ctx* c = (shim_ctx*)calloc(1, sizeof(shim_ctx));
+  if (!c) return GF_ERR_NOMEM;
+  int st = gf_ctx_create(device, &c->ctx);
+  if (st) {
+    free(c);
+    return st;
+  }
+  *out = c;
+  return GF_OK;
+}
+
+void shim_ctx_destroy(shim_ctx* c) {
+  if (!c) return;
+  gf_ctx_synchronize(c->ctx);
+  window_free(&c->wo);
+  window_free(&c->wq);
+  dbuf_free(&c->pairs);
+  pbuf_free(&c->hpairs);
+  dbuf_free(&c->text);
+  dbuf_free(&c->cols);
+  gf_ctx_destroy(c->ctx);
+  free(c);
+}
+
+const char* shim_last_error(shim_ctx* c) { return c ? c->err : "null context"; }
+gf_ctx* shim_gf_ctx(shim_ctx* c) { return c ? c->ctx : NULL; }
+
+/* ---- objID ------------------------------------------------------------------------------ */
+int shim_objid_intern(shim_ctx* c, const char* bytes, const int64_t* offs, int64_t n, int64_t* keys) {
+  gf_objid_dict* d = NULL;
+  int st = gf_ctx_objid_dict(c->ctx, &d);
+  if (!st) st = gf_objid_intern(d, bytes, offs, n, keys);
+  return fail(c, st, "objidIntern");
+}
+int shim_objid_decode(shim_ctx* c, const int64_t* keys, int64_t n, char* buf, int64_t cap, int64_t* offs) {
+  gf_objid_dict* d = NULL;
+  int st = gf_ctx_objid_dict(c->ctx, &d);
+  if (!st) st = gf_objid_decode(d, keys, n, buf, cap, offs);
+  return st == GF_ERR_CAPACITY ? st : fail(c, st, "objidDecode");
+}
+
+/* ---- kNN -------------------------------------------------------------------------------- */
+struct shim_knn {
+  shim_ctx* c;
+  gf_knn_plan* plan;
+  int32_t k;
+  cached_window win;
+};
+
+int shim_knn_plan(shim_ctx* c, const gf_grid* g, double qx, double qy, double r, int32_t k, shim_knn** out) {
+  *out = NULL;
+  shim_knn* h = (shim_knn*)calloc(1, sizeof(shim_knn));
+  if (!h) return GF_ERR_NOMEM;
+  int st = gf_knn_pp_plan_create(c->ctx, g, qx, qy, r, k, GF_METRIC_SQRT, &h->plan);
+  if (st) {
+    free(h);
+    return fail(c, st, "knnPlan");
+  }
+  h->c = c;
+  h->k = k;
+  *out = h;
+  return GF_OK;
+}
+
+int shim_knn_polygon_plan(shim_ctx* c, const gf_grid* g, const gf_polygons* poly, double r, int32_t k,
+                          int approximate, shim_knn** out) {
+  *out = NULL;
+  shim_knn* h = (shim_knn*)calloc(1, sizeof(shim_knn));
+  if (!h) return GF_ERR_NOMEM;
+  int st = gf_knn_ppoly_plan_create(c->ctx, g, poly, r, k, approximate, GF_METRIC_SQRT, &h->plan);
+  if (st) {
+    free(h);
+    return fail(c, st, "knnPolygonPlan");
+  }
+  h->c = c;
+  h->k = k;
+  *out = h;
+  return GF_OK;
+}
+
+void shim_knn_destroy(shim_knn* h) {
+  if (!h) return;
+  gf_ctx_synchronize(h->c->ctx);
+  window_free(&h->win);
+  gf_knn_plan_destroy(h->plan);
+  free(h);
+}
+
+int shim_knn_window(shim_knn* h, const double* x, const double* y, const int64_t* objID, int64_t n, int64_t* out_objID,
+                    double* out_dist, int64_t* out_idx, int32_t* m) {
+  gf_points pts;
+  *m = 0;
+  int st = upload(h->c->ctx, &h->win, x, y, objID, n, &pts);
+  if (!st) st = gf_knn_run(h->plan, &pts, out_objID, out_dist, out_idx, m);
+  return fail(h->c, st, "knnWindow");
+}
+
+/* ---- sliding kNN -------------------------------------------------------------------------- */
+#define SHIM_SLIDE_RECS 8
+struct shim_sliding {
+  shim_knn* plan;
+  gf_knn_sliding* s;
+  int64_t pane_ms;
+  int32_t nwin;           /* device pane windows kept (the engine's ring borrows them) */
+  cached_window* wins;
+  void* rec[SHIM_SLIDE_RECS];      /* pinned window records */
+  int64_t rec_end[SHIM_SLIDE_RECS];
+  int32_t next;
+  int64_t pending_end;    /* depth 2: the window whose record the next push / flush completes */
+};
+
+int shim_sliding_create(shim_knn* plan, int64_t size_ms, int64_t slide_ms, shim_sliding** out) {
+  *out = NULL;
+  shim_sliding* s = (shim_sliding*)calloc(1, sizeof(shim_sliding));
+  if (!s) return GF_ERR_NOMEM;
+  s->plan = plan;
+  s->pending_end = -1;
+  int32_t ppw = 0, pps = 0, ring = 0;
+  int st = gf_knn_plan_set_pipeline(plan->plan, 2);  /* one fused launch per pane */
+  if (!st) st = gf_knn_sliding_create(plan->plan, size_ms, slide_ms, &s->s);
+  if (!st) st = gf_knn_sliding_geometry(s->s, &s->pane_ms, &ppw, &pps, &ring);
+  if (!st) {
+    s->nwin = ring + 1;
+    s->wins = (cached_window*)calloc((size_t)s->nwin, sizeof(cached_window));
+    if (!s->wins) st = GF_ERR_NOMEM;
+  }
+  for (int i = 0; i < SHIM_SLIDE_RECS; ++i) s->rec_end[i] = -1;
+  for (int i = 0; !st && i < SHIM_SLIDE_RECS; ++i) st = gf_pinned_alloc(gf_knn_result_bytes(plan->k), &s->rec[i]);
+  if (st) {
+    shim_sliding_destroy(s);
+    return fail(plan->c, st, "knnSlidingCreate");
+  }
+  *out = s;
+  return GF_OK;
+}
+
+void shim_sliding_destroy(shim_sliding* s) {
+  if (!s) return;
+  gf_ctx_synchronize(s->plan->c->ctx);
+  if (s->s) gf_knn_sliding_destroy(s->s);
+  for (int32_t i = 0; s->wins && i < s->nwin; ++i) window_free(&s->wins[i]);
+  free(s->wins);
+  for (int i = 0; i < SHIM_SLIDE_RECS; ++i)
+    if (s->rec[i]) gf_pinned_free(s->rec[i]);
+  free(s);
+}
+
+int shim_sliding_pane_ms(const shim_sliding* s, int64_t* pane_ms) {
+  *pane_ms = s->pane_ms;
+  return GF_OK;
+}
+
+int shim_sliding_push(shim_sliding* s, int64_t pane_index, const double* x, const double* y, const int64_t* objID,
+                      int64_t n, int32_t* closed, int64_t* window_end) {
+  gf_ctx* ctx = s->plan->c->ctx;
+  gf_points pts;
+  memset(&pts, 0, sizeof pts);
+  *closed = 0;
+  int st = GF_OK;
+  if (n > 0) st = upload(ctx, &s->wins[pane_index % s->nwin], x, y, objID, n, &pts);
+  const int32_t k = s->next % SHIM_SLIDE_RECS;
+  if (!st) st = gf_knn_sliding_push(s->s, pane_index, &pts, s->rec[k], closed, window_end);
+  if (st) return fail(s->plan->c, st, "knnSlidingPush");
+  s->pending_end = -1;  /* this push completed the previous window's record */
+  if (*closed) {
+    s->rec_end[k] = *window_end;
+    s->pending_end = *window_end;
+    s->next++;
+  }
+  return GF_OK;
+}
+
+int shim_sliding_flush(shim_sliding* s) {
+  int st = gf_knn_sliding_flush(s->s);
+  if (!st) s->pending_end = -1;
+  return fail(s->plan->c, st, "knnSlidingFlush");
+}
+
+int shim_sliding_decode(shim_sliding* s, int64_t window_end, int64_t* out_objID, double* out_dist, int64_t* out_idx,
+                        int32_t* m) {
+  *m = 0;
+  int k = -1;
+  for (int i = 0; i < SHIM_SLIDE_RECS; ++i)
+    if (s->rec_end[i] == window_end) k = i;
+  if (k < 0) return fail(s->plan->c, GF_ERR_ARG, "knnSlidingDecode: no such closed window (decode within 8 windows)");
+  int st = GF_OK;
+  if (s->pending_end == window_end) st = shim_sliding_flush(s);  /* its record is written by the flush */
+  if (!st) st = gf_ctx_synchronize(s->plan->c->ctx);
+  if (!st) st = gf_knn_sliding_decode(s->s, window_end, s->rec[k], out_objID, out_dist, out_idx, m);
+  return fail(s->plan->c, st, "knnSlidingDecode");
+}
+
+/* ---- range ------------------------------------------------------------------------------ */
+struct shim_range {
+  shim_ctx* c;
+  gf_range_plan* plan;
+  cached_window win;
+  dbuf bitmap;
+  pbuf idx;      /* pinned: the index list written by the device, then the count */
+};
+
+static int range_new(shim_ctx* c, gf_range_plan* plan, int st, shim_range** out, const char* what) {
+  *out = NULL;
+  shim_range* h = st ? NULL : (shim_range*)calloc(1, sizeof(shim_range));
+  if (st || !h) {
+    if (plan) gf_range_plan_destroy(plan);
+    return fail(c, st ? st : GF_ERR_NOMEM, what);
+  }
+  h->c = c;
+  h->plan = plan;
+  *out = h;
+  return GF_OK;
+}
+
+int shim_range_plan(shim_ctx* c, const gf_grid* g, const double* qx, const double* qy, int32_t nq, double r,
+                    int approximate, shim_range** out) {
+  gf_range_plan* plan = NULL;
+  int st = gf_range_pp_plan_create(c->ctx, g, qx, qy, nq, r, approximate, GF_METRIC_SQRT, &plan);
+  return range_new(c, plan, st, out, "rangePlan");
+}
+
+int shim_range_polygon_plan(shim_ctx* c, const gf_grid* g, const gf_polygons* polys, double r, int approximate,
+                            shim_range** out) {
+  gf_range_plan* plan = NULL;
+  int st = gf_range_ppoly_plan_create(c->ctx, g, polys, r, approximate, GF_METRIC_SQRT, &plan);
+  return range_new(c, plan, st, out, "rangePolygonPlan");
+}
+
+void shim_range_destroy(shim_range* h) {
+  if (!h) return;
+  gf_ctx_synchronize(h->c->ctx);
+  window_free(&h->win);
+  dbuf_free(&h->bitmap);
+  pbuf_free(&h->idx);
+  gf_range_plan_destroy(h->plan);
+  free(h);
+}
+
+int shim_range_window(shim_range* h, const double* x, const double* y, int64_t n, int32_t* out_idx, int64_t cap,
+                      int64_t* count) {
+  gf_points pts;
+  *count = 0;
+  int st = upload(h->c->ctx, &h->win, x, y, NULL, n, &pts);
+  if (!st) st = dbuf_need(&h->bitmap, 8 * (size_t)((n + 63) / 64 + 1));
+  if (!st) st = pbuf_need(&h->idx, 4 * (size_t)(n > 0 ? n : 1) + 16);
+  if (!st) st = gf_range_run(h->plan, &pts, (uint64_t*)h->bitmap.p, NULL, NULL);
+  /* the index list straight into pinned host memory, its count after it: one sync */
+  int64_t* dcount = (int64_t*)((char*)h->idx.p + ((4 * (size_t)(n > 0 ? n : 1) + 7) / 8) * 8);
+  if (!st) st = gf_bitmap_to_indices_async(h->c->ctx, (const uint64_t*)h->bitmap.p, n, (uint32_t*)h->idx.p, n, dcount);
+  if (!st) st = gf_ctx_synchronize(h->c->ctx);
+  if (st) return fail(h->c, st, "rangeWindow");
+  *count = *dcount;
+  memcpy(out_idx, h->idx.p, 4 * (size_t)(*count < cap ? *count : cap));
+  return *count > cap ? GF_ERR_CAPACITY : GF_OK;
+}
+
+/* ---- joins ------------------------------------------------------------------------------ */
+/* pairs of a join run into the context's device buffer, sized from the last join (grown and
+ * re-run once on GF_ERR_CAPACITY), then copied to the pinned staging *pairs */
+typedef int (*join_fn)(shim_ctx* c, const void* a, uint32_t* pairs, int64_t cap, int64_t* m);
+static int join_common(shim_ctx* c, join_fn fn, const void* a, const uint32_t** pairs, int64_t* m, const char* what) {
+  *pairs = NULL;
+  *m = 0;
+  int64_t cap = c->pair_hint > 1024 ? c->pair_hint + c->pair_hint / 8 : 1 << 16;
+  int st = dbuf_need(&c->pairs, 8 * (size_t)cap);
+  if (!st) st = fn(c, a, (uint32_t*)c->pairs.p, cap, m);
+  if (st == GF_ERR_CAPACITY) {
+    cap = *m + *m / 8 + 1024;
+    st = dbuf_need(&c->pairs, 8 * (size_t)cap);
+    if (!st) st = fn(c, a, (uint32_t*)c->pairs.p, cap, m);
+  }
+  if (!st) st = pbuf_need(&c->hpairs, 8 * (size_t)(*m > 0 ? *m : 1));
+  if (!st && *m > 0 && copy(c, c->hpairs.p, c->pairs.p, 8 * (size_t)*m, hipMemcpyDeviceToHost)) st = GF_ERR_HIP;
+  if (!st) st = gf_ctx_synchronize(c->ctx);
+  if (st) return fail(c, st, what);
+  c->pair_hint = *m;
+  *pairs = (const uint32_t*)c->hpairs.p;
+  return GF_OK;
+}
+
+typedef struct {
+  const gf_grid *ug, *qg;
+  gf_points po, pq;
+  double r;
+  int approximate;
+} pp_args;
+static int run_pp(shim_ctx* c, const void* a_, uint32_t* pairs, int64_t cap, int64_t* m) {
+  const pp_args* a = (const pp_args*)a_;
+  return gf_join_pp(c->ctx, a->ug, a->qg, &a->po, &a->pq, a->r, a->approximate, GF_METRIC_SQRT, pairs, cap, m);
+}
+
+int shim_join_window(shim_ctx* c, const gf_grid* ug, const gf_grid* qg, const double* ox, const double* oy, int64_t no,
+                     const double* qx, const double* qy, int64_t nq, double r, int approximate, const uint32_t** pairs,
+                     int64_t* m) {
+  pp_args a;
+  a.ug = ug; a.qg = qg; a.r = r; a.approximate = approximate;
+  int st = upload(c->ctx, &c->wo, ox, oy, NULL, no, &a.po);
+  if (!st) st = upload(c->ctx, &c->wq, qx, qy, NULL, nq, &a.pq);
+  if (st) return fail(c, st, "joinWindow");
+  return join_common(c, run_pp, &a, pairs, m, "joinWindow");
+}
+
+typedef struct {
+  gf_range_plan* plan;
+  const gf_grid* g;
+  gf_points pts;
+} ppoly_args;
+static int run_ppoly(shim_ctx* c, const void* a_, uint32_t* pairs, int64_t cap, int64_t* m) {
+  const ppoly_args* a = (const ppoly_args*)a_;
+  (void)c;
+  return gf_join_ppoly_run(a->plan, a->g, &a->pts, pairs, cap, m);
+}
+
+int shim_polygon_join_window(shim_ctx* c, const gf_grid* g, const double* x, const double* y, int64_t n,
+                             const gf_polygons* polys, double r, int approximate, const uint32_t** pairs, int64_t* m) {
+  ppoly_args a;
+  a.g = g;
+  a.plan = NULL;
+  int st = gf_join_ppoly_plan_create(c->ctx, g, polys, r, approximate, GF_METRIC_SQRT, &a.plan);
+  if (!st) st = upload(c->ctx, &c->wo, x, y, NULL, n, &a.pts);
+  if (!st) st = join_common(c, run_ppoly, &a, pairs, m, "polygonJoinWindow");
+  else fail(c, st, "polygonJoinWindow");
+  if (a.plan) gf_range_plan_destroy(a.plan);
+  return st;
+}
+
+/* ---- ingest ----------------------------------------------------------------------------- */
+static int parse_common(shim_ctx* c, const char* text, int64_t len, int geojson, const void* schema, double* x,
+                        double* y, int64_t* objID, int64_t* ts, int64_t cap, int64_t* n, int64_t* bad_line,
+                        int32_t* bad_kind) {
+  *n = 0;
+  *bad_line = -1;
+  *bad_kind = 0;
+  const size_t col = 8 * (size_t)(cap > 0 ? cap : 1);
+  int st = dbuf_need(&c->text, (size_t)len + 16);
+  if (!st) st = dbuf_need(&c->cols, 4 * col);
+  if (!st && len > 0 && copy(c, c->text.p, text, (size_t)len, hipMemcpyHostToDevice)) st = GF_ERR_HIP;
+  double* dx = (double*)c->cols.p;
+  double* dy = (double*)((char*)c->cols.p + col);
+  int64_t* dob = (int64_t*)((char*)c->cols.p + 2 * col);
+  int64_t* dts = (int64_t*)((char*)c->cols.p + 3 * col);
+  if (!st)
+    st = geojson ? gf_geojson_parse(c->ctx, NULL, (const char*)c->text.p, len, (const gf_geojson_schema*)schema, NULL,
+                                    dx, dy, dob, dts, NULL, NULL, cap, n, bad_line, bad_kind)
+                 : gf_csv_parse(c->ctx, (const char*)c->text.p, len, (const gf_csv_schema*)schema, NULL, dx, dy, dob,
+                                dts, NULL, NULL, cap, n, bad_line, bad_kind);
+  const size_t b = 8 * (size_t)(*n < cap ? *n : cap);
+  if (!st && b && (copy(c, x, dx, b, hipMemcpyDeviceToHost) || copy(c, y, dy, b, hipMemcpyDeviceToHost) ||
+                   copy(c, objID, dob, b, hipMemcpyDeviceToHost) || copy(c, ts, dts, b, hipMemcpyDeviceToHost)))
+    st = GF_ERR_HIP;
+  if (!st) st = gf_ctx_synchronize(c->ctx);
+  return st == GF_ERR_CAPACITY ? st : fail(c, st, geojson ? "geoJsonParse" : "csvParse");
+}
+
+int shim_csv_parse(shim_ctx* c, const char* text, int64_t len, const gf_csv_schema* schema, double* x, double* y,
+                   int64_t* objID, int64_t* ts, int64_t cap, int64_t* n, int64_t* bad_line, int32_t* bad_kind) {
+  return parse_common(c, text, len, 0, schema, x, y, objID, ts, cap, n, bad_line, bad_kind);
+}
+
+int shim_geojson_parse(shim_ctx* c, const char* text, int64_t len, const gf_geojson_schema* schema, double* x,
+                       double* y, int64_t* objID, int64_t* ts, int64_t cap, int64_t* n, int64_t* bad_line,
+                       int32_t* bad_kind) {
+  return parse_common(c, text, len, 1, schema, x, y, objID, ts, cap, n, bad_line, bad_kind);
+}

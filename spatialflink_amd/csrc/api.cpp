@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <array>
 #include <cmath>
 #include <cstdio>
@@ -1795,6 +1796,10 @@ static int join_pp_impl(gf_ctx* ctx, const gf_grid* ugrid, const gf_grid* qgrid,
   }
   int64_t chunk = 256;
   while (chunk < 65536 && (double)chunk * nwaves * 8 < ppp * (double)no) chunk <<= 1;
+  if (const char* e = std::getenv("GF_JOIN_CHUNK")) {  // testing / tuning: a fixed chunk (power of 2)
+    const int64_t v = std::atoll(e);
+    if (v >= 64 && v <= (1 << 20) && (v & (v - 1)) == 0) chunk = v;
+  }
   size_t o_spill = ar.take<uint64_t>(rowpath ? nwaves * chunk : 1);
   size_t o_tb = ar.take<uint64_t>(nwaves), o_tf = ar.take<uint32_t>(nwaves);
   size_t o_hs = ar.take<uint64_t>(nwaves + 1), o_hp = ar.take<uint64_t>(nwaves + 2);
