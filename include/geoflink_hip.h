@@ -325,6 +325,29 @@ int  gf_knn_sliding_flush(gf_knn_sliding* s);
 int  gf_knn_sliding_decode(gf_knn_sliding* s, int64_t window_end, const void* result_host, int64_t* objID,
                            double* dist, int64_t* idx, int32_t* n_out);
 
+/* ---- sliding range: the pane engine for PointPointRangeQuery / PointPolygonRangeQuery under
+ * SlidingProcessingTimeWindows.of(size, slide) (PointPointRangeQuery.java:149-186,
+ * PointPolygonRangeQuery.java:170-204).  Each pane (gcd(size, slide) ms, as gf_knn_sliding) is
+ * evaluated ONCE on `plan` -- gf_range_run into a device pane bitmap, compacted on the device into
+ * the pane's index list -- and a closed window's emitted points are its panes' lists
+ * concatenated: identical to evaluating the window whole (each point's test is independent).
+ * Window indices are window-local: positions in the window's panes concatenated in push order,
+ * ascending, each emitted point once (approximate multi-query multiplicity: gf_range_run). */
+typedef struct gf_range_sliding gf_range_sliding;
+/* size / gcd(size, slide) <= 64; plan: gf_range_pp_plan_create / gf_range_ppoly_plan_create */
+int  gf_range_sliding_create(gf_range_plan* plan, int64_t size_ms, int64_t slide_ms, gf_range_sliding** out);
+void gf_range_sliding_destroy(gf_range_sliding* s);
+int  gf_range_sliding_geometry(const gf_range_sliding* s, int64_t* pane_ms, int32_t* panes_per_window,
+                               int32_t* panes_per_slide);
+/* Async.  Push pane `pane_index` (consecutive indices; an empty pane with n = 0; the pane's
+ * device points must stay valid until the context stream has passed this call).  If a window
+ * closes with it and holds a point: *closed = 1, *window_end = its end (ms), *window_n = its
+ * points, and the stream writes the window's index list to idx (device or pinned uint32[cap])
+ * and its length to *count (device or pinned int64).  cap < *window_n: GF_ERR_CAPACITY with
+ * nothing enqueued (push the same pane again with a larger idx). */
+int  gf_range_sliding_push(gf_range_sliding* s, int64_t pane_index, const gf_points* pane, uint32_t* idx,
+                           int64_t cap, int64_t* count, int32_t* closed, int64_t* window_end, int64_t* window_n);
+
 /* Async window assembler for a batch in timestamp order (processing-time ingestion):
  * bounds (device int64[npanes + 1]) [j] = first i with ts[i] >= (first_pane + j) * pane_ms, so
  * pane first_pane + j is the slice [bounds[j], bounds[j+1]).  ts must be non-decreasing. */

@@ -20,6 +20,7 @@
  *   knnPolygonPlan  PointPolygonKNNQuery (PointPolygonKNNQuery.java:245-317)
  *   knnSliding*  SlidingProcessingTimeWindows.of(size, slide) around the kNN apply
  *                (PointPointKNNQuery.java:158,198-200): panes evaluated once, windows merged
+ *   rangeSliding*  the same apply under SlidingProcessingTimeWindows (PointPointRangeQuery.java:149)
  *   rangeWindow  PointPointRangeQuery.windowBased apply (PointPointRangeQuery.java:150-186),
  *                PointPolygonRangeQuery apply (PointPolygonRangeQuery.java:170-204)
  *   joinWindow   JoinQuery.getReplicatedPointQueryStream (JoinQuery.java:73-90) +
@@ -116,6 +117,18 @@ public final class GeoFlinkHip {
   // their count -- larger than outCap: call again with a larger buffer
   public static native long rangeWindow(long ctx, long plan, ByteBuffer x, ByteBuffer y, int n, ByteBuffer out,
                                         int outCap);
+
+  // ---- sliding range (pane engine) ---------------------------------------------------------
+  // SlidingProcessingTimeWindows.of(size, slide) around the range apply (PointPointRangeQuery.java:
+  // 149-186): each pane evaluated once; plan from rangePlan / rangePolygonPlan (outlives this)
+  public static native long rangeSlidingCreate(long ctx, long plan, long sizeMs, long slideMs);
+  public static native void rangeSlidingDestroy(long sliding);
+  public static native long rangeSlidingPaneMs(long sliding);
+  // push pane `pane` (consecutive; empty with n = 0): the emitted points of the window it closed
+  // (positions in the window's panes concatenated, ascending), windowEnd[0] = its end; null when
+  // no window holding a point closed
+  public static native int[] rangeSlidingPush(long ctx, long sliding, long pane, ByteBuffer x, ByteBuffer y, int n,
+                                              long[] windowEnd);
 
   // ---- joins ---------------------------------------------------------------------------
   // pairs (ordinary / point index, query / polygon index) flattened

@@ -312,6 +312,39 @@ JNIEXPORT jlong JNICALL Java_GeoFlink_native_1_GeoFlinkHip_rangeWindow(JNIEnv* e
   return count;
 }
 
+/* ---- sliding range: the pane engine (PointPointRangeQuery.java:149-186) -------------------- */
+JNIEXPORT jlong JNICALL Java_GeoFlink_native_1_GeoFlinkHip_rangeSlidingCreate(JNIEnv* env, jclass cls, jlong ctx,
+    jlong plan, jlong size_ms, jlong slide_ms) {
+  shim_range_sliding* s = NULL;
+  throw_status(env, shim_range_sliding_create((shim_range*)(intptr_t)plan, size_ms, slide_ms, &s), CTX(ctx));
+  return (jlong)(intptr_t)s;
+}
+JNIEXPORT void JNICALL Java_GeoFlink_native_1_GeoFlinkHip_rangeSlidingDestroy(JNIEnv* env, jclass cls, jlong s) {
+  shim_range_sliding_destroy((shim_range_sliding*)(intptr_t)s);
+}
+JNIEXPORT jlong JNICALL Java_GeoFlink_native_1_GeoFlinkHip_rangeSlidingPaneMs(JNIEnv* env, jclass cls, jlong s) {
+  int64_t p = 0;
+  shim_range_sliding_pane_ms((shim_range_sliding*)(intptr_t)s, &p);
+  return p;
+}
+/* the closed window's emitted points (window-local, ascending) with windowEnd[0] = its end, or
+ * null when the pane closed no window holding a point */
+JNIEXPORT jintArray JNICALL Java_GeoFlink_native_1_GeoFlinkHip_rangeSlidingPush(JNIEnv* env, jclass cls, jlong ctx,
+    jlong s, jlong pane, jobject bx, jobject by, jint n, jlongArray jend) {
+  const double* x = direct(env, bx, 8 * (int64_t)n, "rangeSlidingPush: x");
+  const double* y = direct(env, by, 8 * (int64_t)n, "rangeSlidingPush: y");
+  if ((*env)->ExceptionCheck(env) || !need_len(env, jend, 1, "rangeSlidingPush: windowEnd")) return NULL;
+  int64_t end = -1, count = 0;
+  const uint32_t* idx = NULL;
+  int st = shim_range_sliding_push((shim_range_sliding*)(intptr_t)s, pane, x, y, n, &end, &idx, &count);
+  if (throw_status(env, st, CTX(ctx)) || end < 0) return NULL;
+  jlong e = end;
+  (*env)->SetLongArrayRegion(env, jend, 0, 1, &e);
+  jintArray out = (*env)->NewIntArray(env, (jsize)count);
+  if (out && count) (*env)->SetIntArrayRegion(env, out, 0, (jsize)count, (const jint*)idx);
+  return out;
+}
+
 /* ---- joins (JoinQuery.java:73-115, PointPointJoinQuery.java:148-182,
  * PointPolygonJoinQuery.java:154-213) -> long[2m] of (ordinary / point, query / polygon) ------ */
 static jlongArray pairs_array(JNIEnv* env, const uint32_t* pairs, int64_t m) {

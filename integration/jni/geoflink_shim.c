@@ -364,6 +364,82 @@ int shim_range_window(shim_range* h, const double* x, const double* y, int64_t n
   return *count > cap ? GF_ERR_CAPACITY : GF_OK;
 }
 
+/* ---- sliding range ---------------------------------------------------------------------- */
+struct shim_range_sliding {
+  shim_range* plan;
+  gf_range_sliding* s;
+  int64_t pane_ms;
+  cached_window win[2];   /* pane uploads alternate (each is ordered after the work before it) */
+  int32_t next;
+  pbuf idx;               /* pinned: the closed window's index list, then its count */
+};
+
+/* pinned staging of a window: cap uint32 indices, then the int64 count (8-byte aligned) */
+static int64_t slide_cap(const pbuf* b) { return (int64_t)((b->cap - 16) / 4); }
+static int64_t* slide_count(const pbuf* b) {
+  return (int64_t*)((char*)b->p + ((4 * (size_t)slide_cap(b) + 7) & ~(size_t)7));
+}
+
+int shim_range_sliding_create(shim_range* plan, int64_t size_ms, int64_t slide_ms, shim_range_sliding** out) {
+  *out = NULL;
+  shim_range_sliding* s = (shim_range_sliding*)calloc(1, sizeof(shim_range_sliding));
+  if (!s) return GF_ERR_NOMEM;
+  s->plan = plan;
+  int st = gf_range_sliding_create(plan->plan, size_ms, slide_ms, &s->s);
+  if (!st) st = gf_range_sliding_geometry(s->s, &s->pane_ms, NULL, NULL);
+  if (!st) st = pbuf_need(&s->idx, 4096);
+  if (st) {
+    shim_range_sliding_destroy(s);
+    return fail(plan->c, st, "rangeSlidingCreate");
+  }
+  *out = s;
+  return GF_OK;
+}
+
+void shim_range_sliding_destroy(shim_range_sliding* s) {
+  if (!s) return;
+  gf_ctx_synchronize(s->plan->c->ctx);
+  if (s->s) gf_range_sliding_destroy(s->s);
+  window_free(&s->win[0]);
+  window_free(&s->win[1]);
+  pbuf_free(&s->idx);
+  free(s);
+}
+
+int shim_range_sliding_pane_ms(const shim_range_sliding* s, int64_t* pane_ms) {
+  *pane_ms = s->pane_ms;
+  return GF_OK;
+}
+
+int shim_range_sliding_push(shim_range_sliding* s, int64_t pane_index, const double* x, const double* y, int64_t n,
+                            int64_t* window_end, const uint32_t** idx, int64_t* count) {
+  gf_ctx* ctx = s->plan->c->ctx;
+  gf_points pts;
+  memset(&pts, 0, sizeof pts);
+  *window_end = -1;
+  *idx = NULL;
+  *count = 0;
+  int st = GF_OK;
+  if (n > 0) st = upload(ctx, &s->win[s->next++ & 1], x, y, NULL, n, &pts);
+  int32_t closed = 0;
+  int64_t end = -1, wn = 0;
+  for (;;) {  /* the staging holds the window's index list, then its count */
+    st = st ? st
+            : gf_range_sliding_push(s->s, pane_index, &pts, (uint32_t*)s->idx.p, slide_cap(&s->idx),
+                                    slide_count(&s->idx), &closed, &end, &wn);
+    if (st != GF_ERR_CAPACITY) break;
+    st = pbuf_need(&s->idx, 4 * (size_t)wn + 32);  /* nothing was enqueued: push the pane again */
+  }
+  if (!st && closed) st = gf_ctx_synchronize(ctx);
+  if (st) return fail(s->plan->c, st, "rangeSlidingPush");
+  if (closed) {
+    *window_end = end;
+    *idx = (const uint32_t*)s->idx.p;
+    *count = *slide_count(&s->idx);
+  }
+  return GF_OK;
+}
+
 /* ---- joins ------------------------------------------------------------------------------ */
 /* pairs of a join run into the context's device buffer, sized from the last join (grown and
  * re-run once on GF_ERR_CAPACITY), then copied to the pinned staging *pairs */

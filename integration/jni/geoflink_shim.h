@@ -76,6 +76,19 @@ void shim_range_destroy(shim_range* h);
 int shim_range_window(shim_range* h, const double* x, const double* y, int64_t n, int32_t* out_idx, int64_t cap,
                       int64_t* count);
 
+/* ---- sliding range: SlidingProcessingTimeWindows.of(size, slide) around the range apply
+ * (PointPointRangeQuery.java:149-186) -- the pane engine (gf_range_sliding_*) ------------------ */
+typedef struct shim_range_sliding shim_range_sliding;
+int shim_range_sliding_create(shim_range* plan, int64_t size_ms, int64_t slide_ms, shim_range_sliding** out);
+void shim_range_sliding_destroy(shim_range_sliding* s);
+int shim_range_sliding_pane_ms(const shim_range_sliding* s, int64_t* pane_ms);
+/* push pane `pane_index` (host x, y; n may be 0).  When it closes a window holding a point:
+ * *window_end = its end, *idx = the window's emitted points (positions in the window's panes
+ * concatenated, ascending; in the shim's pinned staging until the next push), *count; else
+ * *window_end = -1. */
+int shim_range_sliding_push(shim_range_sliding* s, int64_t pane_index, const double* x, const double* y, int64_t n,
+                            int64_t* window_end, const uint32_t** idx, int64_t* count);
+
 /* ---- joins (JoinQuery.java:73-115, PointPointJoinQuery.java:148-182,
  * PointPolygonJoinQuery.java:154-213): pairs (ordinary / point index, query / polygon index) ---
  * The pairs stay in the context's pinned staging until the next join on it: *pairs points there

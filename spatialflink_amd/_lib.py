@@ -48,7 +48,8 @@ EXPORTS = [
     "gf_knn_result_bytes", "gf_knn_enqueue",
     "gf_knn_decode", "gf_knn_run", "gf_knn_merge_dev", "gf_knn_merge_dev_batch", "gf_knn_merge_host",
     "gf_knn_sliding_create", "gf_knn_sliding_destroy", "gf_knn_sliding_geometry", "gf_knn_sliding_push",
-    "gf_knn_sliding_flush", "gf_knn_sliding_decode", "gf_pane_bounds", "gf_csv_parse", "gf_csv_parse_dict", "gf_geojson_parse",
+    "gf_knn_sliding_flush", "gf_knn_sliding_decode", "gf_range_sliding_create", "gf_range_sliding_destroy",
+    "gf_range_sliding_geometry", "gf_range_sliding_push", "gf_pane_bounds", "gf_csv_parse", "gf_csv_parse_dict", "gf_geojson_parse",
     "gf_objid_dict_create", "gf_objid_dict_destroy", "gf_ctx_objid_dict", "gf_objid_dict_size", "gf_objid_intern",
     "gf_objid_decode", "gf_join_pp", "gf_join_pp_async",
     "gf_join_ppoly_plan_create", "gf_join_ppoly_run", "gf_join_ppoly",
@@ -167,6 +168,10 @@ def lib():
             "gf_knn_sliding_push": ([P, i64, C.POINTER(GfPoints), P, pi32, pi64], C.c_int),
             "gf_knn_sliding_flush": ([P], C.c_int),
             "gf_knn_sliding_decode": ([P, i64, P, P, P, P, pi32], C.c_int),
+            "gf_range_sliding_create": ([P, i64, i64, C.POINTER(P)], C.c_int),
+            "gf_range_sliding_destroy": ([P], None),
+            "gf_range_sliding_geometry": ([P, pi64, pi32, pi32], C.c_int),
+            "gf_range_sliding_push": ([P, i64, C.POINTER(GfPoints), P, i64, P, pi32, pi64, pi64], C.c_int),
             "gf_pane_bounds": ([P, P, i64, i64, i64, i32, P], C.c_int),
             "gf_csv_parse": ([P, P, i64, P, C.POINTER(GfGrid), P, P, P, P, P, P, i64, pi64, pi64, pi32], C.c_int),
             "gf_geojson_parse": ([P, P, P, i64, P, C.POINTER(GfGrid), P, P, P, P, P, P, i64, pi64, pi64, pi32],

@@ -467,6 +467,18 @@ hipError_t launch_knn_fused(gf_ctx* ctx, const KnnScanArgs& a, const KnnSelectAr
 int knn_enqueue_merge(gf_knn_plan* P, const gf_points* pts, void* result, const KnnMergeArgs* merge, int* merged);
 
 hipError_t launch_range(gf_ctx* ctx, const RangeArgs& a, int table_mode, int poly, int blocks);
+// sliding range (sliding.cpp): a closed window's emitted indices = its non-empty panes' index
+// lists concatenated, each shifted by the pane's first position in the window (k_points.hip)
+struct RangeGatherArgs {
+  const uint32_t* list[kMaxMergeRecs];  // pane-local ascending indices (gf_bitmap_to_indices_async)
+  const int64_t* cnt[kMaxMergeRecs];    // their device counts
+  int64_t base[kMaxMergeRecs];          // the pane's first position in the window
+  int32_t npanes;
+  int64_t total;                        // points in the window (an upper bound of the hits)
+  uint32_t* out;
+  int64_t* count;
+};
+hipError_t launch_range_window_gather(hipStream_t s, const RangeGatherArgs& a);
 hipError_t launch_join_ppoly(gf_ctx* ctx, const RangeArgs& a, int blocks, int jblocks, uint32_t* ecnt, uint32_t* ecand,
                              uint32_t* btot, unsigned long long* total, uint32_t* pairs, int64_t cap, int aligned);
 

@@ -71,6 +71,56 @@ __global__ __launch_bounds__(64) void pane_bounds_kernel(const int64_t* __restri
   bounds[j] = lo;
 }
 
+// ---------------------------------------------------------------------------------------
+// Sliding range: a closed window's index list.  The window's virtual position space is its
+// panes concatenated (pane j at base[j], n_j points); block b owns positions [b*span, (b+1)*span)
+// and copies the ones that are list entries (position - base[j] < cnt[j]) to their place in the
+// window's list (the prefix of the earlier panes' counts + the entry's rank).  Every block
+// prefix-sums the <= 64 counts itself (one wave), so there is no inter-block step; block 0
+// writes the window's count.  O(window points / span) blocks, O(hits) bytes moved.
+// ---------------------------------------------------------------------------------------
+constexpr int kGatherThreads = 256;
+constexpr int64_t kGatherSpan = 8192;
+
+__global__ __launch_bounds__(kGatherThreads) void range_window_gather_kernel(RangeGatherArgs a) {
+  __shared__ int64_t s_pre[kMaxMergeRecs + 1];
+  __shared__ int64_t s_base[kMaxMergeRecs + 1];
+  const int t = threadIdx.x;
+  if (t < 64) {
+    int64_t c = t < a.npanes ? *a.cnt[t] : 0;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int64_t v = __shfl_up(c, o, 64);
+      if (t >= o) c += v;
+    }
+    s_pre[t + 1] = c;
+    s_base[t] = t < a.npanes ? a.base[t] : INT64_MAX;
+    if (t == 0) {
+      s_pre[0] = 0;
+      s_base[64] = INT64_MAX;
+    }
+  }
+  __syncthreads();
+  if (blockIdx.x == 0 && t == 0) *a.count = s_pre[a.npanes];
+  const int64_t v0 = (int64_t)blockIdx.x * kGatherSpan;
+  const int64_t v1 = v0 + kGatherSpan < a.total ? v0 + kGatherSpan : a.total;
+  // the pane holding v0 (largest j with base[j] <= v0), then walk forward with v
+  int j = 0;
+  while (j + 1 < a.npanes && s_base[j + 1] <= v0) ++j;
+  for (int64_t v = v0 + t; v < v1; v += kGatherThreads) {
+    int p = j;
+    while (p + 1 < a.npanes && s_base[p + 1] <= v) ++p;
+    const int64_t e = v - s_base[p];
+    if (e < s_pre[p + 1] - s_pre[p]) a.out[s_pre[p] + e] = (uint32_t)(s_base[p] + a.list[p][e]);
+  }
+}
+
+hipError_t launch_range_window_gather(hipStream_t s, const RangeGatherArgs& a) {
+  const int64_t blocks = a.total > 0 ? (a.total + kGatherSpan - 1) / kGatherSpan : 1;
+  hipLaunchKernelGGL(range_window_gather_kernel, dim3((unsigned)blocks), dim3(kGatherThreads), 0, s, a);
+  return hipGetLastError();
+}
+
 hipError_t launch_pane_bounds(hipStream_t s, const int64_t* ts, int64_t n, int64_t pane_ms, int64_t first_pane,
                               int32_t nb, int64_t* bounds) {
   hipLaunchKernelGGL(pane_bounds_kernel, dim3((nb + 63) / 64), dim3(64), 0, s, ts, n, pane_ms, first_pane, nb,

@@ -252,3 +252,150 @@ extern "C" int gf_knn_sliding_decode(gf_knn_sliding* s, int64_t window_end, cons
   }
   return gf_knn_decode(P, nullptr, P->host_result, oo, od, oi, n_out);
 }
+
+// ---------------------------------------------------------------------------------------
+// Sliding range (PointPointRangeQuery / PointPolygonRangeQuery under
+// SlidingProcessingTimeWindows.of(size, slide), PointPointRangeQuery.java:149): the reference
+// applies the window function to every window, so each point is tested size/slide times.  Here
+// each pane is tested ONCE (gf_range_run into the pane's bitmap, compacted on the device into
+// the pane's ascending index list + count), and a closed window's list is its panes' lists
+// concatenated with the panes' window offsets (launch_range_window_gather): identical to
+// evaluating the window whole, since the per-point test does not depend on the other points.
+// ---------------------------------------------------------------------------------------
+struct gf_range_sliding {
+  gf_range_plan* plan = nullptr;
+  int64_t size_ms = 0, slide_ms = 0, pane_ms = 0;
+  int32_t W = 0, S = 0;
+  struct Pane {
+    int64_t index = LLONG_MIN;
+    int64_t n = 0;
+    uint64_t* bitmap = nullptr;
+    uint32_t* list = nullptr;
+    int64_t cap = 0;        // points the buffers hold
+  };
+  std::vector<Pane> ring;   // W slots: pane p in slot p mod W
+  int64_t* counts = nullptr;  // device int64[W]: the slots' list lengths
+  bool started = false;
+  int64_t last = 0;
+};
+
+namespace {
+gf_range_sliding::Pane& rslot(gf_range_sliding* s, int64_t p) { return s->ring[(size_t)floor_mod(p, s->W)]; }
+bool rcloses(const gf_range_sliding* s, int64_t p) { return floor_mod(p + 1 - s->W, s->S) == 0; }
+}  // namespace
+
+extern "C" int gf_range_sliding_create(gf_range_plan* plan, int64_t size_ms, int64_t slide_ms, gf_range_sliding** out) {
+  if (!plan || !out || size_ms <= 0 || slide_ms <= 0) return GF_ERR_ARG;
+  *out = nullptr;
+  gf_ctx* ctx = plan->ctx;
+  if (plan->join) return set_err(ctx, GF_ERR_ARG, "gf_range_sliding_create: a join plan");
+  const int64_t pane = std::gcd(size_ms, slide_ms);
+  const int64_t W = size_ms / pane, S = slide_ms / pane;
+  if (W > kMaxMergeRecs)
+    return set_err(ctx, GF_ERR_ARG, "gf_range_sliding_create: size / gcd(size, slide) must be <= 64 panes");
+  int st = bind(ctx);
+  if (st) return st;
+  gf_range_sliding* s = new gf_range_sliding();
+  s->plan = plan;
+  s->size_ms = size_ms; s->slide_ms = slide_ms; s->pane_ms = pane;
+  s->W = (int32_t)W; s->S = (int32_t)S;
+  s->ring.resize((size_t)W);
+  hipError_t e = hipMalloc(&s->counts, sizeof(int64_t) * (size_t)W);
+  if (e != hipSuccess) {
+    delete s;
+    return hip_err(ctx, e, "hipMalloc");
+  }
+  *out = s;
+  return GF_OK;
+}
+
+extern "C" void gf_range_sliding_destroy(gf_range_sliding* s) {
+  if (!s) return;
+  hipSetDevice(s->plan->ctx->device);
+  hipStreamSynchronize(s->plan->ctx->stream);
+  for (auto& p : s->ring) {
+    if (p.bitmap) hipFree(p.bitmap);
+    if (p.list) hipFree(p.list);
+  }
+  if (s->counts) hipFree(s->counts);
+  delete s;
+}
+
+extern "C" int gf_range_sliding_geometry(const gf_range_sliding* s, int64_t* pane_ms, int32_t* panes_per_window,
+                                         int32_t* panes_per_slide) {
+  if (!s) return GF_ERR_ARG;
+  if (pane_ms) *pane_ms = s->pane_ms;
+  if (panes_per_window) *panes_per_window = s->W;
+  if (panes_per_slide) *panes_per_slide = s->S;
+  return GF_OK;
+}
+
+extern "C" int gf_range_sliding_push(gf_range_sliding* s, int64_t pane_index, const gf_points* pane, uint32_t* idx,
+                                     int64_t cap, int64_t* count, int32_t* closed, int64_t* window_end,
+                                     int64_t* window_n) {
+  if (!s || !pane || !closed || cap < 0) return GF_ERR_ARG;
+  gf_ctx* ctx = s->plan->ctx;
+  *closed = 0;
+  if (s->started && pane_index != s->last + 1)
+    return set_err(ctx, GF_ERR_ARG, "gf_range_sliding_push: panes must be pushed consecutively (empty panes with n = 0)");
+  if (pane->n < 0 || pane->n > (int64_t)UINT32_MAX) return set_err(ctx, GF_ERR_ARG, "gf_range_sliding_push: bad n");
+  int st = bind(ctx);
+  if (st) return st;
+  // the window this pane closes (if any) and its points, before anything changes: a too-small
+  // idx is refused with nothing enqueued, so the caller can push the same pane again
+  const bool closes = rcloses(s, pane_index);
+  int64_t wn = 0;
+  if (closes)
+    for (int64_t q = pane_index - s->W + 1; q <= pane_index; ++q) {
+      if (q == pane_index) wn += pane->n;
+      else if (rslot(s, q).index == q) wn += rslot(s, q).n;
+    }
+  if (window_n) *window_n = closes ? wn : 0;
+  if (closes && wn > 0) {
+    if (wn > (int64_t)UINT32_MAX) return set_err(ctx, GF_ERR_ARG, "gf_range_sliding_push: window too large");
+    if (cap < wn) return GF_ERR_CAPACITY;
+    if (!idx || !count) return set_err(ctx, GF_ERR_ARG, "gf_range_sliding_push: a window closes, idx / count null");
+  }
+  gf_range_sliding::Pane& pn = rslot(s, pane_index);
+  pn.index = pane_index;
+  pn.n = pane->n;
+  if (pane->n > 0) {
+    if (pn.cap < pane->n) {  // grow: the stream may still read the old buffers (an earlier window)
+      GF_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+      if (pn.bitmap) GF_HIP_CHECK(ctx, hipFree(pn.bitmap));
+      if (pn.list) GF_HIP_CHECK(ctx, hipFree(pn.list));
+      pn.bitmap = nullptr;
+      pn.list = nullptr;
+      pn.cap = 0;
+      const int64_t c = std::max<int64_t>(pane->n + pane->n / 4, 4096);
+      GF_HIP_CHECK(ctx, hipMalloc(&pn.bitmap, sizeof(uint64_t) * (size_t)((c + 63) / 64)));
+      GF_HIP_CHECK(ctx, hipMalloc(&pn.list, sizeof(uint32_t) * (size_t)c));
+      pn.cap = c;
+    }
+    int64_t* cnt = s->counts + floor_mod(pane_index, s->W);
+    if ((st = gf_range_run(s->plan, pane, pn.bitmap, nullptr, nullptr))) return st;
+    if ((st = gf_bitmap_to_indices_async(ctx, pn.bitmap, pane->n, pn.list, pane->n, cnt))) return st;
+  }
+  s->started = true;
+  s->last = pane_index;
+  if (closes && wn > 0) {  // a window with no point never fires
+    RangeGatherArgs a{};
+    int64_t base = 0;
+    for (int64_t q = pane_index - s->W + 1; q <= pane_index; ++q) {
+      const gf_range_sliding::Pane& w = rslot(s, q);
+      if (w.index != q || w.n == 0) continue;
+      a.list[a.npanes] = w.list;
+      a.cnt[a.npanes] = s->counts + floor_mod(q, s->W);
+      a.base[a.npanes] = base;
+      ++a.npanes;
+      base += w.n;
+    }
+    a.total = base;
+    a.out = idx;
+    a.count = count;
+    GF_HIP_CHECK(ctx, launch_range_window_gather(ctx->stream, a));
+    *closed = 1;
+    if (window_end) *window_end = (pane_index + 1) * s->pane_ms;
+  }
+  return GF_OK;
+}

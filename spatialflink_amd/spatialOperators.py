@@ -77,6 +77,12 @@ class _PlanCache:
         self._destroy_name = destroy_name
         self.limit = int(limit)
         self._d = OrderedDict()
+        self._pinned = set()  # plans with state beyond their key (pipeline, capacity, a pane engine)
+
+    def pin(self, plan):
+        """Never evict `plan`: a plan with settings or pending pipelined work, or one a pane
+        engine (gf_*_sliding) holds, lives until the operator closes."""
+        self._pinned.add(plan.value if hasattr(plan, "value") else plan)
 
     def get(self, key):
         plan = self._d.get(key)
@@ -86,9 +92,13 @@ class _PlanCache:
 
     def put(self, key, plan):
         self._d[key] = plan
-        while len(self._d) > self.limit:
-            _, old = self._d.popitem(last=False)
-            self._destroy(old)
+        over = len(self._d) - self.limit
+        for k in [k for k, p in self._d.items() if self._pv(p) not in self._pinned][:max(over, 0)]:
+            self._destroy(self._d.pop(k))
+
+    @staticmethod
+    def _pv(plan):
+        return plan.value if hasattr(plan, "value") else plan
 
     def _destroy(self, plan):
         if _lib._lib is not None:
@@ -204,11 +214,18 @@ class PointPointRangeQuery(_RangeBase):
     """range/PointPointRangeQuery.java -- window-based point-point range query."""
 
     def run(self, window: PointWindow, queryPointSet, queryRadius: float) -> RangeResult:
+        qs = list(queryPointSet)
+        ctx, plan = self.plan(window.x.device.index, qs, queryRadius)
+        nq = len(qs) if self.conf.approximateQuery else 1
+        return self._evaluate(plan, window, nq)
+
+    def plan(self, device: int, queryPointSet, queryRadius: float):
+        """(context, gf_range_plan) of this query on `device` (cached by query contents)."""
         _require_supported(self.conf)
         qs = list(queryPointSet)
         qx = np.array([q.x for q in qs], np.float64)
         qy = np.array([q.y for q in qs], np.float64)
-        ctx = _lib.context(window.x.device.index)
+        ctx = _lib.context(device)
         key = (ctx.device, tuple(qx.tolist()), tuple(qy.tolist()), float(queryRadius),
                bool(self.conf.approximateQuery), int(self.conf.distanceMetric))
 
@@ -221,18 +238,21 @@ class PointPointRangeQuery(_RangeBase):
             _lib.check(st, ctx.handle, "gf_range_pp_plan_create")
             return h
 
-        plan = self._plan(key, create)
-        nq = len(qs) if self.conf.approximateQuery else 1
-        return self._evaluate(plan, window, nq)
+        return ctx, self._plan(key, create)
 
 
 class PointPolygonRangeQuery(_RangeBase):
     """range/PointPolygonRangeQuery.java -- window-based point-polygon range query."""
 
     def run(self, window: PointWindow, queryPolygonSet, queryRadius: float) -> RangeResult:
+        ctx, plan = self.plan(window.x.device.index, queryPolygonSet, queryRadius)
+        return self._evaluate(plan, window, 1)
+
+    def plan(self, device: int, queryPolygonSet, queryRadius: float):
+        """(context, gf_range_plan) of this query on `device` (cached by query contents)."""
         _require_supported(self.conf)
         ps = PolygonSet(queryPolygonSet)
-        ctx = _lib.context(window.x.device.index)
+        ctx = _lib.context(device)
         key = (ctx.device, ps.digest(), float(queryRadius), bool(self.conf.approximateQuery),
                int(self.conf.distanceMetric))
 
@@ -245,8 +265,7 @@ class PointPolygonRangeQuery(_RangeBase):
             _lib.check(st, ctx.handle, "gf_range_ppoly_plan_create")
             return h
 
-        plan = self._plan(key, create)
-        return self._evaluate(plan, window, 1)
+        return ctx, self._plan(key, create)
 
 
 # ----------------------------------------------------------------------------------------
@@ -377,6 +396,7 @@ class PointPointKNNQuery(SpatialOperator):
         enqueue (its select runs in block 0 of window i+1's scan) or by flush()."""
         ctx, plan = self.plan(window_device, queryPoint, queryRadius, k)
         _lib.check(_lib.lib().gf_knn_plan_set_pipeline(plan, int(depth)), ctx.handle, "set_pipeline")
+        self._plans.pin(plan)  # its depth and pending records must survive the LRU
 
     def flush(self, window_device, queryPoint, queryRadius, k):
         ctx, plan = self.plan(window_device, queryPoint, queryRadius, k)
@@ -385,6 +405,7 @@ class PointPointKNNQuery(SpatialOperator):
     def set_capacity(self, window_device, queryPoint, queryRadius, k, cap):
         ctx, plan = self.plan(window_device, queryPoint, queryRadius, k)
         _lib.check(_lib.lib().gf_knn_plan_set_capacity(plan, int(cap)), ctx.handle, "set_capacity")
+        self._plans.pin(plan)
 
     def __del__(self):
         plans = getattr(self, "_plans", None)

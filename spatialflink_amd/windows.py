@@ -159,6 +159,7 @@ class SlidingKNNQuery:
         self.k = int(k)
         self.op = PointPointKNNQuery(conf, grid)
         self.ctx, self.plan = self.op.plan(device, queryPoint, queryRadius, k)
+        self.op._plans.pin(self.plan)  # the pane engine holds it
         self.depth = int(pipeline) if self.k <= 256 else 1
         _lib.check(_lib.lib().gf_knn_plan_set_pipeline(self.plan, self.depth), self.ctx.handle, "set_pipeline")
         h = C.c_void_p()
@@ -265,8 +266,10 @@ class SlidingKNNQuery:
 
 class SlidingRangeQuery:
     """Sliding-window range query (PointPointRangeQuery / PointPolygonRangeQuery with
-    SlidingProcessingTimeWindows): each pane is evaluated once (gf_range_run); a window's
-    hits = its panes' hits concatenated (positions within the window)."""
+    SlidingProcessingTimeWindows, PointPointRangeQuery.java:149-186) on the device pane engine
+    (gf_range_sliding_*): each pane is evaluated once, a closed window's hits (positions within
+    the window, ascending) are assembled on the device from its panes' index lists, and
+    results() reads every fired window after one stream sync."""
 
     def __init__(self, op, queries, queryRadius: float, size_ms: int, slide_ms: int):
         self.op = op
@@ -274,9 +277,23 @@ class SlidingRangeQuery:
         self.r = queryRadius
         self.geo = SlidingWindows(size_ms, slide_ms)
         self.stream = _PaneStream(self.geo)
-        self.panes = OrderedDict()   # pane index -> (n, hits as pane positions)
+        self.handle = None
+        self.ctx = None
         self.last_pane = None
-        self.fired = []
+        self.fired = []              # (start, end, device idx, device count)
+
+    def _engine(self, device):
+        import torch
+
+        if self.handle is None:
+            self.ctx, plan = self.op.plan(device, self.queries, self.r)
+            self.op._plans.pin(plan)
+            h = C.c_void_p()
+            _lib.check(_lib.lib().gf_range_sliding_create(plan, self.geo.size, self.geo.slide, C.byref(h)),
+                       self.ctx.handle, "gf_range_sliding_create")
+            self.handle = h
+            self._spare = torch.empty(1, dtype=torch.int32, device=f"cuda:{self.ctx.device}")
+        return self.handle
 
     def _pane(self, p, pane):
         if self.last_pane is not None:
@@ -285,25 +302,28 @@ class SlidingRangeQuery:
         self._one(p, pane)
 
     def _one(self, p, pane):
-        if pane is None or pane.n == 0:
-            self.panes[p] = (0, np.zeros(0, np.int64))
-        else:
-            res = self.op.run(pane, self.queries, self.r)
-            self.panes[p] = (pane.n, bitmap_indices(res.ctx, res.bitmap, pane.n).astype(np.int64))
-        while len(self.panes) > self.geo.panes_per_window:
-            self.panes.popitem(last=False)
+        import torch
+
+        if self.handle is None:
+            if pane is None:
+                return  # nothing before the first pane with points
+            self._engine(pane.x.device.index)
+        empty = pane is None or pane.n == 0
+        cs = _lib.GfPoints(None, None, None, None, 0) if empty else pane.c_struct()
+        closed, end, wn = C.c_int32(), C.c_int64(), C.c_int64()
+        dev = f"cuda:{self.ctx.device}"
+        idx, cnt = self._spare, torch.zeros(1, dtype=torch.int64, device=dev)
+        while True:  # the window's index buffer: sized from the window's points on a capacity miss
+            st = _lib.lib().gf_range_sliding_push(self.handle, int(p), C.byref(cs), idx.data_ptr(), idx.numel(),
+                                                  cnt.data_ptr(), C.byref(closed), C.byref(end), C.byref(wn))
+            if st != _lib.GF_ERR_CAPACITY:
+                break
+            idx = torch.empty(int(wn.value), dtype=torch.int32, device=dev)
+        _lib.check(st, self.ctx.handle, "gf_range_sliding_push")
+        self._spare = torch.empty(1, dtype=torch.int32, device=dev) if closed.value else idx
         self.last_pane = p
-        if self.geo.closes(p):
-            first = p - self.geo.panes_per_window + 1
-            off, hits, total = 0, [], 0
-            for q in range(first, p + 1):
-                n, h = self.panes.get(q, (0, np.zeros(0, np.int64)))
-                hits.append(h + off)
-                off += n
-                total += n
-            if total:
-                s, e = self.geo.window_of_last_pane(p)
-                self.fired.append((s, e, np.concatenate(hits)))
+        if closed.value:
+            self.fired.append((end.value - self.geo.size, end.value, idx, cnt))
 
     def push(self, batch: PointWindow):
         for p, pane in self.stream.feed(batch):
@@ -322,5 +342,22 @@ class SlidingRangeQuery:
                 self._one(p, None)
 
     def results(self):
-        out, self.fired = self.fired, []
+        """(windowStart, windowEnd, hits) of every window fired so far; hits = ascending
+        positions within the window (its panes concatenated in time order)."""
+        if not self.fired:
+            return []
+        fired, self.fired = self.fired, []
+        self.ctx.synchronize()
+        out = []
+        for s0, e, idx, cnt in fired:
+            m = int(cnt.item())
+            out.append((s0, e, idx[:m].cpu().numpy().view(np.uint32).astype(np.int64)))
         return out
+
+    def close(self):
+        if self.handle is not None and _lib._lib is not None:
+            _lib.lib().gf_range_sliding_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        self.close()

@@ -99,12 +99,24 @@ def test_pane_bounds_kernel(sf, oracle_mod):
         np.testing.assert_array_equal(b, exp)
 
 
-def test_sliding_range_matches_oracle(sf, oracle_mod):
+@pytest.mark.parametrize("size,slide,poly", [(3000, 1000, False), (5000, 2000, False), (3000, 1000, True),
+                                             (2000, 2000, True)])
+def test_sliding_range_matches_oracle(sf, oracle_mod, size, slide, poly):
+    """The device pane engine (gf_range_sliding_*): every window holding a point fires with its
+    hits = the oracle over that window's points (positions within the window)."""
     g = sf.UniformGrid(100, *BEIJING)
     og = oracle_mod.grid(100, *BEIJING)
     q = sf.Point("q", *QPOINT, 0, g)
-    x, y, obj, ts = make_stream(oracle_mod, 77, 500_000, 0, 9_000, gap=(3_000, 4_500))
-    op = sf.SlidingRangeQuery(sf.PointPointRangeQuery(conf(sf), g), [q], 0.05, 3000, 1000)
+    x, y, obj, ts = make_stream(oracle_mod, 77 + size, 500_000, 0, 9_000, gap=(3_000, 4_500))
+    if poly:
+        rings = oracle_mod.generate_query_polygons(12, BEIJING[0], BEIJING[2], BEIJING[1], BEIJING[3])
+        OP = oracle_mod.Polygons(rings)
+        polys = [sf.Polygon(r, g) for r in rings]
+        op = sf.SlidingRangeQuery(sf.PointPolygonRangeQuery(conf(sf), g), polys, 0.01, size, slide)
+        expect = lambda m: oracle_mod.range_ppoly(og, x[m], y[m], OP, 0.01)  # noqa: E731
+    else:
+        op = sf.SlidingRangeQuery(sf.PointPointRangeQuery(conf(sf), g), [q], 0.05, size, slide)
+        expect = lambda m: oracle_mod.range_pp(og, x[m], y[m], [QPOINT[0]], [QPOINT[1]], 0.05)  # noqa: E731
     got = []
     for b in batches(sf, x, y, obj, ts, 3):
         op.push(b)
@@ -113,7 +125,7 @@ def test_sliding_range_matches_oracle(sf, oracle_mod):
     got += op.results()
     windows = [(s, e) for s, e, _ in got]
     # every window holding a point fires, the trailing ones included (Flink's final watermark)
-    assert windows == expected_windows(ts, 3000, 1000)
+    assert windows == expected_windows(ts, size, slide)
     for s, e, hits in got:
         m = (ts >= s) & (ts < e)
-        np.testing.assert_array_equal(hits, oracle_mod.range_pp(og, x[m], y[m], [QPOINT[0]], [QPOINT[1]], 0.05))
+        np.testing.assert_array_equal(hits, expect(m))

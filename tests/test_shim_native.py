@@ -121,6 +121,10 @@ def shim(gpu):
     S.shim_range_polygon_plan.argtypes = [P, P, P, d, C.c_int, pp]
     S.shim_range_destroy.argtypes = [P]
     S.shim_range_window.argtypes = [P, P, P, i64, P, i64, P]
+    S.shim_range_sliding_create.argtypes = [P, i64, i64, pp]
+    S.shim_range_sliding_destroy.argtypes = [P]
+    S.shim_range_sliding_pane_ms.argtypes = [P, P]
+    S.shim_range_sliding_push.argtypes = [P, i64, P, P, i64, P, pp, P]
     S.shim_join_window.argtypes = [P, P, P, P, P, i64, P, P, i64, d, C.c_int, pp, P]
     S.shim_polygon_join_window.argtypes = [P, P, P, P, i64, P, d, C.c_int, pp, P]
     S.shim_csv_parse.argtypes = [P, C.c_char_p, i64, P, P, P, P, P, i64, P, P, P]
@@ -323,6 +327,47 @@ def test_range_polygon(shim, ctx, oracle_mod):
         _ok(shim, ctx, st, "rangeWindow(polygon)")
         np.testing.assert_array_equal(out[:cnt].astype(np.int64), exp)
     finally:
+        shim.shim_range_destroy(plan)
+
+
+@pytest.mark.gpu
+def test_sliding_range(shim, ctx, oracle_mod):
+    """rangeSlidingPush's C sequence: panes pushed consecutively (an empty one included), every
+    window holding a point compared with the oracle over that window's points."""
+    size, slide = 3000, 1000
+    g, og = grid(100), oracle_mod.grid(100, *BEIJING)
+    qx, qy = np.array([QPOINT[0]]), np.array([QPOINT[1]])
+    n = 400_000
+    x, y = oracle_mod.java_random_points(12, n, *BEIJING)
+    ts = np.sort(np.random.default_rng(12).integers(0, 8000, n)).astype(np.int64)
+    keep = (ts < 3000) | (ts >= 4000)
+    x, y, ts = x[keep], y[keep], ts[keep]
+    plan, s = P(), P()
+    _ok(shim, ctx, shim.shim_range_plan(ctx, C.byref(g), _a(qx), _a(qy), 1, 0.05, 0, C.byref(plan)), "plan")
+    try:
+        _ok(shim, ctx, shim.shim_range_sliding_create(plan, size, slide, C.byref(s)), "create")
+        pane = i64()
+        shim.shim_range_sliding_pane_ms(s, C.byref(pane))
+        assert pane.value == 1000
+        fired = 0
+        for p in range(int(ts.max()) // 1000 + 3):  # + the empty panes that close the last windows
+            lo, hi = np.searchsorted(ts, [p * 1000, (p + 1) * 1000])
+            px, py = np.ascontiguousarray(x[lo:hi]), np.ascontiguousarray(y[lo:hi])
+            end, idx, cnt = i64(), P(), i64()
+            _ok(shim, ctx, shim.shim_range_sliding_push(s, p, _a(px), _a(py), hi - lo, C.byref(end), C.byref(idx),
+                                                        C.byref(cnt)), "push")
+            if end.value < 0:
+                continue
+            fired += 1
+            wlo, whi = np.searchsorted(ts, [end.value - size, end.value])
+            exp = oracle_mod.range_pp(og, x[wlo:whi], y[wlo:whi], qx, qy, 0.05)
+            got = (np.ctypeslib.as_array(C.cast(idx, C.POINTER(C.c_uint32)), shape=(cnt.value,)).astype(np.int64)
+                   if cnt.value else np.zeros(0, np.int64))
+            np.testing.assert_array_equal(got, exp)
+        assert fired == 10  # windows ending 1000 .. 10000 all hold a point
+    finally:
+        if s:
+            shim.shim_range_sliding_destroy(s)
         shim.shim_range_destroy(plan)
 
 

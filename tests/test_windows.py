@@ -56,3 +56,19 @@ def test_pane_merge_equals_window(oracle_mod):
             np.testing.assert_array_equal(mo, eo)
             np.testing.assert_array_equal(md, ed)
             np.testing.assert_array_equal(mi, ei)
+
+
+def test_plan_cache_keeps_pinned_plans(monkeypatch):
+    """The operator plan LRU (spatialOperators._PlanCache) evicts only unpinned plans: a plan with
+    a pipeline depth / capacity or held by a pane engine survives any number of other keys."""
+    from spatialflink_amd import spatialOperators as so
+
+    destroyed = []
+    monkeypatch.setattr(so._PlanCache, "_destroy", lambda self, p: destroyed.append(p))
+    c = so._PlanCache("unused", limit=2)
+    c.put("a", 101)
+    c.pin(101)
+    for i, k in enumerate("bcdef"):
+        c.put(k, 200 + i)
+    assert c.get("a") == 101 and 101 not in destroyed
+    assert len(c) == 2 and destroyed == [200, 201, 202, 203]  # the LRU unpinned ones go
