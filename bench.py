@@ -112,6 +112,9 @@ def main():
     ap.add_argument("--range-defer", default="0", help="range/ppoly candidate tests: 0 auto, 1 inline, 2 deferred (list = sweep)")
     ap.add_argument("--range-streams", type=int, default=2,
                     help="range/ppoly: consecutive windows alternate over this many contexts (HIP streams)")
+    ap.add_argument("--range-batch", type=int, default=0,
+                    help="range/ppoly: windows per gf_range_run_batch launch (0 = auto: 8 for windows of <= 2M "
+                         "points, else 1 = one gf_range_run per window)")
     ap.add_argument("--no-indices", action="store_true",
                     help="range/ppoly: leave the index list out of the step (bitmap + counts only; ablation)")
     ap.add_argument("--k", type=int, default=50)

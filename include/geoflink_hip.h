@@ -188,6 +188,14 @@ void gf_range_plan_destroy(gf_range_plan* plan);
  * window's last kernel (no extra launch). */
 int  gf_range_run(gf_range_plan* plan, const gf_points* pts, uint64_t* bitmap,
                   uint64_t* multi_bitmap, int64_t* counts);
+/* Up to 16 windows of one plan in ONE launch (window w = pts[w], its bitmap bitmaps[w] and
+ * counts[w] as gf_range_run; no multiplicity bitmap), plus -- idx non-null -- every window's
+ * ascending index list in one more launch (idx[w] of capacity idx_cap[w], its length to
+ * idx_count[w], as gf_bitmap_to_indices_async).  Async.  For windows that are available together
+ * (a catch-up, several keys): small windows stop paying a launch each (PointPointRangeQuery.java:
+ * 150-186 per window). */
+int  gf_range_run_batch(gf_range_plan* plan, int32_t nwin, const gf_points* pts, uint64_t* const* bitmaps,
+                        int64_t* const* counts, uint32_t* const* idx, const int64_t* idx_cap, int64_t* const* idx_count);
 /* Plan diagnostics: in-grid cells by class (none / candidate / guaranteed / candidate cells
  * accepted untested because closed rectangles cover them); any pointer may be null. */
 int  gf_range_plan_stats(const gf_range_plan* plan, int64_t* none_cells, int64_t* candidate_cells,

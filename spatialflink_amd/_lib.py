@@ -42,7 +42,7 @@ EXPORTS = [
     "gf_ctx_set_stream", "gf_ctx_stream", "gf_ctx_synchronize", "gf_ctx_join", "gf_ctx_fork", "gf_ctx_last_error", "gf_ctx_set_timing", "gf_ctx_set_timing_period", "gf_ctx_set_flag",
     "gf_ctx_timing", "gf_grid_make", "gf_grid_layers", "gf_cell_of", "gf_format_cell_id", "gf_parse_cell_id",
     "gf_assign_cells", "gf_bucket_by_cell", "gf_range_pp_plan_create", "gf_range_ppoly_plan_create",
-    "gf_range_plan_destroy", "gf_range_run", "gf_range_plan_stats", "gf_range_plan_set_tuning", "gf_bitmap_to_indices", "gf_bitmap_to_indices_async", "gf_knn_pp_plan_create",
+    "gf_range_plan_destroy", "gf_range_run", "gf_range_run_batch", "gf_range_plan_stats", "gf_range_plan_set_tuning", "gf_bitmap_to_indices", "gf_bitmap_to_indices_async", "gf_knn_pp_plan_create",
     "gf_knn_ppoly_plan_create",
     "gf_knn_plan_destroy", "gf_knn_plan_set_capacity", "gf_knn_plan_set_index_base", "gf_knn_plan_set_tuning", "gf_knn_plan_set_hint", "gf_knn_plan_set_pipeline", "gf_knn_plan_flush",
     "gf_knn_result_bytes", "gf_knn_enqueue",
@@ -141,6 +141,8 @@ def lib():
                                             C.POINTER(P)], C.c_int),
             "gf_range_plan_destroy": ([P], None),
             "gf_range_run": ([P, C.POINTER(GfPoints), P, P, P], C.c_int),
+            "gf_range_run_batch": ([P, i32, C.POINTER(GfPoints), C.POINTER(P), C.POINTER(P), C.POINTER(P), pi64,
+                                    C.POINTER(P)], C.c_int),
             "gf_range_plan_stats": ([P, pi64, pi64, pi64, pi64], C.c_int),
             "gf_range_plan_set_tuning": ([P, C.c_int32, C.c_int32], C.c_int),
             "gf_bitmap_to_indices": ([P, P, i64, P, i64, pi64], C.c_int),

@@ -738,7 +738,8 @@ extern "C" void gf_range_plan_destroy(gf_range_plan* P) {
   hipStreamSynchronize(P->ctx->stream);
   void* bufs[] = {P->table, P->extra, P->cand_off, P->cand_list, P->qx, P->qy, P->ring_off, P->vert_off,
                   P->vx, P->vy, P->bbox, P->ring_env, P->partials, P->queue, P->queue_count, P->queue_xy, P->rows, P->xt, P->yt,
-                  P->rowoff, P->spans, P->brect, P->rect, P->jecnt, P->jecand, P->jbtot, P->jtotal};
+                  P->rowoff, P->spans, P->brect, P->rect, P->jecnt, P->jecand, P->jbtot, P->jtotal,
+                  P->batch_partials};
   for (void* b : bufs)
     if (b) hipFree(b);
   delete P;
@@ -993,6 +994,58 @@ extern "C" int gf_range_run(gf_range_plan* P, const gf_points* pts, uint64_t* bi
   // the counts are summed by the last block of the window's last kernel (no finalize launch)
   a.counts = counts;
   GF_HIP_CHECK(ctx, launch_range(ctx, a, P->table_mode, P->poly, blocks));
+  return GF_OK;
+}
+
+extern "C" int gf_range_run_batch(gf_range_plan* P, int32_t nwin, const gf_points* pts, uint64_t* const* bitmaps,
+                                  int64_t* const* counts, uint32_t* const* idx, const int64_t* idx_cap,
+                                  int64_t* const* idx_count) {
+  if (!P || nwin < 1 || nwin > kRangeBatchMax || !pts || !bitmaps || !counts)
+    return set_err(P ? P->ctx : nullptr, GF_ERR_ARG, "gf_range_run_batch: 1 <= nwin <= 16, pts / bitmaps / counts");
+  if (P->join) return set_err(P->ctx, GF_ERR_ARG, "gf_range_run_batch: a join plan");
+  gf_ctx* ctx = P->ctx;
+  int st = bind(ctx);
+  if (st) return st;
+  int64_t nmax = 0;
+  for (int32_t w = 0; w < nwin; ++w) {
+    if ((st = check_points(ctx, &pts[w]))) return st;
+    if (!bitmaps[w] || !counts[w]) return set_err(ctx, GF_ERR_ARG, "gf_range_run_batch: null bitmap / counts");
+    if (idx && (pts[w].n > (int64_t)UINT32_MAX || !idx_cap || !idx_count || !idx_count[w] || idx_cap[w] < 0 ||
+                (idx_cap[w] > 0 && !idx[w])))
+      return set_err(ctx, GF_ERR_ARG, "gf_range_run_batch: index lists need idx, idx_cap, idx_count per window");
+    nmax = std::max(nmax, pts[w].n);
+  }
+  if (!P->batch_partials) {  // tickets start at 0 and every finalising block resets its own
+    GF_HIP_CHECK(ctx, hipMalloc(&P->batch_partials, sizeof(uint64_t) * (size_t)kRangeBatchMax * (kRangeTicketSlot + 1)));
+    GF_HIP_CHECK(ctx, hipMemsetAsync(P->batch_partials, 0,
+                                     sizeof(uint64_t) * (size_t)kRangeBatchMax * (kRangeTicketSlot + 1), ctx->stream));
+  }
+  RangeArgs a = range_args(P, &pts[0], bitmaps[0], nullptr);
+  RangeBatch b{};
+  for (int32_t w = 0; w < nwin; ++w)
+    b.w[w] = RangeWin{pts[w].x, pts[w].y, pts[w].n, bitmaps[w], nullptr,
+                      P->batch_partials + (size_t)w * (kRangeTicketSlot + 1), counts[w]};
+  // blocks per window from the largest window (an empty window's blocks exit after the partials)
+  const int blocks = scan_blocks_range(P, nmax);
+  GF_HIP_CHECK(ctx, launch_range_batch(ctx, a, b, nwin, P->table_mode, P->poly, blocks));
+  if (!idx) return GF_OK;
+  ExpandBatch e{};
+  e.nwin = nwin;
+  int64_t tiles = 0;
+  for (int32_t w = 0; w < nwin; ++w) {
+    e.bm[w] = bitmaps[w];
+    e.n[w] = pts[w].n;
+    e.idx[w] = idx[w];
+    e.cap[w] = idx_cap[w];
+    e.count[w] = idx_count[w];
+    e.tile0[w] = (int32_t)tiles;
+    tiles += std::max<int64_t>(expand_blocks((pts[w].n + 63) / 64), 1);  // >= 1: its block writes the count
+  }
+  e.tile0[nwin] = (int32_t)tiles;
+  ExpandState es;
+  if ((st = lookback_state(ctx, tiles, &es))) return st;
+  GF_HIP_CHECK(ctx, launch_expand_batch(ctx->stream, e, es));
+  ctx->expand_base += (unsigned long long)tiles;
   return GF_OK;
 }
 

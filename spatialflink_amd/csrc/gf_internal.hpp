@@ -324,6 +324,18 @@ hipError_t launch_scan1(hipStream_t s, uint32_t* in, int64_t L, uint32_t* out, u
                         const ExpandState& st);
 hipError_t launch_expand_bitmap_async(hipStream_t s, const uint64_t* bitmap, int64_t words, int64_t n, uint32_t* idx,
                                       int64_t cap, int64_t* count, const ExpandState& st);
+// a batch of windows (gf_range_run_batch): window w's expansion owns tickets [tile0[w], tile0[w+1])
+constexpr int kRangeBatchMax = 16;
+struct ExpandBatch {
+  const uint64_t* bm[kRangeBatchMax];
+  int64_t n[kRangeBatchMax];
+  uint32_t* idx[kRangeBatchMax];
+  int64_t cap[kRangeBatchMax];
+  int64_t* count[kRangeBatchMax];
+  int32_t tile0[kRangeBatchMax + 1];
+  int32_t nwin;
+};
+hipError_t launch_expand_batch(hipStream_t s, const ExpandBatch& b, const ExpandState& st);
 
 // objID dictionary (k_objid.hip, objid.cpp)
 struct DictSlot {                 // 32 B
@@ -467,6 +479,21 @@ hipError_t launch_knn_fused(gf_ctx* ctx, const KnnScanArgs& a, const KnnSelectAr
 int knn_enqueue_merge(gf_knn_plan* P, const gf_points* pts, void* result, const KnnMergeArgs* merge, int* merged);
 
 hipError_t launch_range(gf_ctx* ctx, const RangeArgs& a, int table_mode, int poly, int blocks);
+// a batch of windows of one plan in one launch (blockIdx.y = window; inline tests, DEFER 0)
+struct RangeWin {
+  const double* x;
+  const double* y;
+  int64_t n;
+  uint64_t* bitmap;
+  uint64_t* multi;
+  uint64_t* partials;  // the window's own partials + ticket
+  int64_t* counts;
+};
+struct RangeBatch {
+  RangeWin w[kRangeBatchMax];
+};
+hipError_t launch_range_batch(gf_ctx* ctx, const RangeArgs& a, const RangeBatch& b, int nwin, int table_mode, int poly,
+                              int blocks);
 // sliding range (sliding.cpp): a closed window's emitted indices = its non-empty panes' index
 // lists concatenated, each shifted by the pane's first position in the window (k_points.hip)
 struct RangeGatherArgs {
@@ -662,6 +689,7 @@ struct gf_range_plan {
   double* bbox = nullptr;
   double* ring_env = nullptr;
   uint64_t* partials = nullptr;
+  uint64_t* batch_partials = nullptr;  // gf_range_run_batch: kRangeBatchMax x (partials + ticket)
   int blocks = 0;
   uint32_t* queue = nullptr;       // deferred candidate tests (grown to blocks x seg_cap)
   double* queue_xy = nullptr;

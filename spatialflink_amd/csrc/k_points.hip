@@ -512,17 +512,16 @@ __device__ __forceinline__ uint64_t lb_pack(uint32_t epoch, uint64_t flag, uint6
   return ((uint64_t)(epoch & 0x3FFFFFFu) << 38) | (flag << 36) | v;  // v < 2^36
 }
 
-__global__ __launch_bounds__(kExpandWords) void expand_async_kernel(const uint64_t* __restrict__ bm, int64_t words, int64_t n,
-                                                              uint32_t* __restrict__ idx, int64_t cap,
-                                                              int64_t* __restrict__ count, ExpandState st) {
-  extern __shared__ uint16_t lidx[];  // [kExpandWords * 64] this block's indices - its first point
-  __shared__ uint32_t wsum[kExpandWords / 64];
-  __shared__ unsigned long long s_bid, s_prefix;
+// One window's expansion by the block with global ticket `bid`: its tiles are the global ids
+// [lo, last]; the look-back stops at lo (a batch of windows shares one ticket sequence, each
+// window a contiguous range of it, so every logical predecessor within the window has started).
+__device__ __forceinline__ void expand_window(const uint64_t* __restrict__ bm, int64_t words, int64_t n,
+                                              uint32_t* __restrict__ idx, int64_t cap, int64_t* __restrict__ count,
+                                              const ExpandState& st, uint64_t bid, uint64_t lo, uint64_t last,
+                                              uint16_t* lidx, uint32_t* wsum, unsigned long long& s_prefix) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  if (threadIdx.x == 0) s_bid = atomicAdd(st.ticket, 1ull) - st.base;
-  __syncthreads();
-  const uint64_t bid = s_bid;
-  const int64_t w = (int64_t)bid * kExpandWords + threadIdx.x;
+  const uint64_t tile = bid - lo;
+  const int64_t w = (int64_t)tile * kExpandWords + threadIdx.x;
   uint64_t m = w < words ? bm[w] : 0ull;
   if (w == words - 1 && (n & 63)) m &= (1ull << (n & 63)) - 1ull;
   const uint32_t c = (uint32_t)__popcll(m);
@@ -543,21 +542,22 @@ __global__ __launch_bounds__(kExpandWords) void expand_async_kernel(const uint64
   if (wid == 0) {  // publish the aggregate; wave 0 looks back 64 x kLbPerLane predecessors a round
     unsigned long long* my = st.status + bid;
     const uint64_t ep = st.epoch & 0x3FFFFFFu;
-    if (bid == 0) {
+    if (tile == 0) {
       if (lane == 0) __hip_atomic_store(my, lb_pack(st.epoch, kLbInc, total), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (lane == 0) s_prefix = 0;
     } else {
       if (lane == 0) __hip_atomic_store(my, lb_pack(st.epoch, kLbAgg, total), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       uint64_t prefix = 0;
       int64_t hi = (int64_t)bid - 1;  // lane l reads predecessors hi - l*kLbPerLane - j (nearest first)
+      const int64_t l0 = (int64_t)lo;
       for (;;) {
         uint64_t v[kLbPerLane];
         bool ready = true;
 #pragma unroll
         for (int j = 0; j < kLbPerLane; ++j) {
           const int64_t p = hi - lane * kLbPerLane - j;
-          v[j] = p >= 0 ? __hip_atomic_load(st.status + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
-          ready = ready && (p < 0 || ((v[j] >> 38) == ep && ((v[j] >> 36) & 3ull) != 0ull));
+          v[j] = p >= l0 ? __hip_atomic_load(st.status + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+          ready = ready && (p < l0 || ((v[j] >> 38) == ep && ((v[j] >> 36) & 3ull) != 0ull));
         }
         if (__ballot(!ready)) {  // some predecessor has not published: poll the window again
           __builtin_amdgcn_s_sleep(1);
@@ -578,7 +578,7 @@ __global__ __launch_bounds__(kExpandWords) void expand_async_kernel(const uint64
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) add += __shfl_xor(add, o, 64);
         prefix += add;
-        if (incm || hi - 64 * kLbPerLane < 0) break;
+        if (incm || hi - 64 * kLbPerLane < l0) break;
         hi -= 64 * kLbPerLane;
       }
       if (lane == 0) {
@@ -597,10 +597,35 @@ __global__ __launch_bounds__(kExpandWords) void expand_async_kernel(const uint64
   }
   __syncthreads();
   const uint64_t base = s_prefix;
-  const uint32_t first = (uint32_t)((int64_t)bid * kExpandWords * 64);
+  const uint32_t first = (uint32_t)((int64_t)tile * kExpandWords * 64);
   for (uint32_t j = threadIdx.x; j < total; j += kExpandWords)  // coalesced copy out
     if ((int64_t)(base + j) < cap) idx[base + j] = first + lidx[j];
-  if (bid == (uint64_t)gridDim.x - 1 && threadIdx.x == 0) *count = (int64_t)(base + total);
+  if (bid == last && threadIdx.x == 0) *count = (int64_t)(base + total);
+}
+
+__global__ __launch_bounds__(kExpandWords) void expand_async_kernel(const uint64_t* __restrict__ bm, int64_t words, int64_t n,
+                                                              uint32_t* __restrict__ idx, int64_t cap,
+                                                              int64_t* __restrict__ count, ExpandState st) {
+  extern __shared__ uint16_t lidx[];  // [kExpandWords * 64] this block's indices - its first point
+  __shared__ uint32_t wsum[kExpandWords / 64];
+  __shared__ unsigned long long s_bid, s_prefix;
+  if (threadIdx.x == 0) s_bid = atomicAdd(st.ticket, 1ull) - st.base;
+  __syncthreads();
+  expand_window(bm, words, n, idx, cap, count, st, s_bid, 0, gridDim.x - 1, lidx, wsum, s_prefix);
+}
+
+// A batch of windows' expansions in one launch: window w owns the tickets [tile0[w], tile0[w+1]).
+__global__ __launch_bounds__(kExpandWords) void expand_batch_kernel(ExpandBatch b, ExpandState st) {
+  extern __shared__ uint16_t lidx[];
+  __shared__ uint32_t wsum[kExpandWords / 64];
+  __shared__ unsigned long long s_bid, s_prefix;
+  if (threadIdx.x == 0) s_bid = atomicAdd(st.ticket, 1ull) - st.base;
+  __syncthreads();
+  const uint64_t bid = s_bid;
+  int w = 0;
+  while (w + 1 < b.nwin && (uint64_t)b.tile0[w + 1] <= bid) ++w;
+  expand_window(b.bm[w], (b.n[w] + 63) / 64, b.n[w], b.idx[w], b.cap[w], b.count[w], st, bid, (uint64_t)b.tile0[w],
+                (uint64_t)b.tile0[w + 1] - 1, lidx, wsum, s_prefix);
 }
 
 // Single-pass exclusive scan (one launch): tiles of 1024 threads x 16 items, each tile's
@@ -720,6 +745,14 @@ hipError_t launch_expand_bitmap_async(hipStream_t s, const uint64_t* bitmap, int
   if (words <= 0) return hipMemsetAsync(count, 0, sizeof(int64_t), s);
   hipLaunchKernelGGL(expand_async_kernel, dim3((unsigned)expand_blocks(words)), dim3(kExpandWords),
                      sizeof(uint16_t) * 64 * kExpandWords, s, bitmap, words, n, idx, cap, count, st);
+  return hipGetLastError();
+}
+
+hipError_t launch_expand_batch(hipStream_t s, const ExpandBatch& b, const ExpandState& st) {
+  const int32_t blocks = b.tile0[b.nwin];
+  if (blocks <= 0) return hipSuccess;
+  hipLaunchKernelGGL(expand_batch_kernel, dim3((unsigned)blocks), dim3(kExpandWords),
+                     sizeof(uint16_t) * 64 * kExpandWords, s, b, st);
   return hipGetLastError();
 }
 

@@ -531,7 +531,7 @@ constexpr int kRangeHdrWords = 4 + 2 * 2 * (kBlock / 64);
 #define GF_RANGE_WAVES 1
 #endif
 template <int TABLE, int POLY, int DEFER, int U>
-__global__ __launch_bounds__(kBlock, GF_RANGE_WAVES) void range_kernel(RangeArgs a) {
+__device__ __forceinline__ void range_body(const RangeArgs& a) {
   const int64_t tstride = (int64_t)gridDim.x * (kBlock / 64) * 128;       // points per grid sweep
   const int64_t t0 = ((int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * 128;
   uint64_t hits = 0, mult = 0;
@@ -615,6 +615,28 @@ __global__ __launch_bounds__(kBlock, GF_RANGE_WAVES) void range_kernel(RangeArgs
   // no kernel follows (the join's passes do for DEFER 2): this kernel's last block sums the
   // window's counts (sh / sm are free again after the partials, lds_base[1] is header padding)
   if (DEFER != 2 && a.counts) finalize_counts(a, gridDim.x, &lds_base[1], sh);
+}
+
+template <int TABLE, int POLY, int DEFER, int U>
+__global__ __launch_bounds__(kBlock, GF_RANGE_WAVES) void range_kernel(RangeArgs a) {
+  range_body<TABLE, POLY, DEFER, U>(a);
+}
+
+// A batch of windows of one plan (gf_range_run_batch): window blockIdx.y, gridDim.x blocks
+// each; the window's columns, bitmaps and partials replace the single window's (wave-uniform
+// scalars), everything else is the plan's.  Inline tests only (DEFER 0: no queues to share).
+template <int TABLE, int POLY, int U>
+__global__ __launch_bounds__(kBlock, GF_RANGE_WAVES) void range_batch_kernel(RangeArgs a, RangeBatch b) {
+  const RangeWin& w = b.w[blockIdx.y];
+  RangeArgs c = a;
+  c.x = w.x;
+  c.y = w.y;
+  c.n = w.n;
+  c.bitmap = w.bitmap;
+  c.multi = w.multi;
+  c.partials = w.partials;
+  c.counts = w.counts;
+  range_body<TABLE, POLY, 0, U>(c);
 }
 
 #ifndef GF_RANGE_U
@@ -902,6 +924,20 @@ hipError_t launch_range(gf_ctx* ctx, const RangeArgs& a, int table_mode, int pol
     if (e != hipSuccess) return e;
   }
   return hipSuccess;  // deferred tests: drained by each scan block at its end (drain_own_queue)
+}
+
+hipError_t launch_range_batch(gf_ctx* ctx, const RangeArgs& a, const RangeBatch& b, int nwin, int table_mode, int poly,
+                              int blocks) {
+  const dim3 g(blocks, nwin), t(kBlock);
+  const size_t lds = 4 * kRangeHdrWords + (table_mode ? sizeof(uint32_t) * (size_t)((2 * a.grid_n + 1) & ~1) +
+                                           (a.xt ? 2 * sizeof(double) * (size_t)(a.grid_n + 1) : 0) +
+                                           (a.span_lds ? (size_t)((a.span_bytes + 3) & ~3) : 0)
+                                     : 0);
+  KTimer k(ctx, GF_K_RANGE_SCAN);
+  if (!table_mode && !poly) hipLaunchKernelGGL((range_batch_kernel<0, 0, kRangeU>), g, t, lds, ctx->stream, a, b);
+  else if (!poly) hipLaunchKernelGGL((range_batch_kernel<1, 0, kRangeU>), g, t, lds, ctx->stream, a, b);
+  else hipLaunchKernelGGL((range_batch_kernel<1, 1, kRangeU>), g, t, lds, ctx->stream, a, b);
+  return hipGetLastError();
 }
 
 }  // namespace gf

@@ -1056,3 +1056,62 @@ def test_range_counts_folded_in_kernel(sf, oracle_mod):
         assert res.count() == len(oracle_mod.range_ppoly(og, x, y, oracle_mod.Polygons(raw), 0.002))
         res = qop.run(w, [q], 0.3)
         assert res.count() == len(oracle_mod.range_pp(og, x, y, [QPOINT[0]], [QPOINT[1]], 0.3))
+
+
+@pytest.mark.parametrize("kind", ["arith", "table", "poly"])
+def test_range_run_batch(sf, oracle_mod, kind):
+    """gf_range_run_batch: up to 16 windows of one plan in one launch (+ one index-list launch),
+    windows of every size (0, 1, ragged, 1M) -- each window's counts, bitmap and index list equal
+    the oracle's over that window alone."""
+    import ctypes as C
+
+    import torch
+    from spatialflink_amd import _lib
+
+    L = _lib.lib()
+    g = sf.UniformGrid(100, *BEIJING)
+    og = oracle_mod.grid(100, *BEIJING)
+    ctx = _lib.context(0)
+    h = C.c_void_p()
+    if kind == "poly":
+        raw = oracle_mod.generate_query_polygons(50, 115.5, 39.6, 117.6, 41.1)
+        ps = sf.PolygonSet([sf.Polygon(p, g) for p in raw])
+        cs = ps.c_struct()
+        _lib.check(L.gf_range_ppoly_plan_create(ctx.handle, C.byref(g.c_grid), C.byref(cs), 0.01, 0, 0, C.byref(h)),
+                   ctx.handle, "plan")
+        expect = lambda x, y: oracle_mod.range_ppoly(og, x, y, oracle_mod.Polygons(raw), 0.01)  # noqa: E731
+    else:
+        qx = np.array([QPOINT[0]] + ([116.9, 117.2] if kind == "table" else []))
+        qy = np.array([QPOINT[1]] + ([40.3, 40.8] if kind == "table" else []))
+        r = 0.5 if kind == "arith" else 0.03
+        _lib.check(L.gf_range_pp_plan_create(ctx.handle, C.byref(g.c_grid), qx.ctypes.data, qy.ctypes.data, len(qx),
+                                             r, 0, 0, C.byref(h)), ctx.handle, "plan")
+        expect = lambda x, y: oracle_mod.range_pp(og, x, y, qx, qy, r)  # noqa: E731
+    try:
+        sizes = [1_000_000, 0, 1, 63, 64, 65, 70_001, 1_000_000, 333_333, 5, 2]
+        wins = []
+        for j, n in enumerate(sizes):
+            x, y = oracle_mod.java_random_points(500 + j, n, 115.4, 117.7, 39.5, 41.2)
+            wins.append((x, y, win(sf, x, y)))
+        B = len(sizes)
+        pts = (_lib.GfPoints * B)(*[w[2].c_struct() for w in wins])
+        bms = [torch.zeros(max(1, (n + 63) // 64), dtype=torch.int64, device="cuda") for n in sizes]
+        cnts = [torch.full((2,), -1, dtype=torch.int64, device="cuda") for _ in sizes]
+        idxs = [torch.full((max(n, 1),), -1, dtype=torch.int32, device="cuda") for n in sizes]
+        icnt = [torch.full((1,), -1, dtype=torch.int64, device="cuda") for _ in sizes]
+        P_ = C.c_void_p
+        for rep in range(2):  # the second call reuses the tickets / partials the first reset
+            st = L.gf_range_run_batch(h, B, pts, (P_ * B)(*[b.data_ptr() for b in bms]),
+                                      (P_ * B)(*[c.data_ptr() for c in cnts]),
+                                      (P_ * B)(*[i.data_ptr() for i in idxs]), (C.c_int64 * B)(*sizes),
+                                      (P_ * B)(*[c.data_ptr() for c in icnt]))
+            _lib.check(st, ctx.handle, "gf_range_run_batch")
+            torch.cuda.synchronize()
+            for j, (x, y, w) in enumerate(wins):
+                exp = expect(x, y)
+                assert int(cnts[j][0]) == len(exp) == int(icnt[j][0]), (kind, j)
+                np.testing.assert_array_equal(idxs[j][:len(exp)].cpu().numpy().astype(np.int64), exp)
+                got = sf.spatialOperators.bitmap_indices(ctx, bms[j], sizes[j]).astype(np.int64)
+                np.testing.assert_array_equal(got, exp)
+    finally:
+        L.gf_range_plan_destroy(h)

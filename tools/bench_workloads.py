@@ -279,8 +279,33 @@ def bench_range(args, polygons=False):
         pts = [w[2].c_struct() for w in wins]
 
         nstreams = len(plans)
+        batch = args.range_batch if args.range_batch > 0 else (8 if n <= 2_000_000 else 1)
+        batch = max(1, min(batch, 16, nwin))
+        if batch > 1:  # windows i .. i+B-1 in one gf_range_run_batch (+ one index-list launch)
+            P_ = C.c_void_p
+            bms = [bitmaps[j].data_ptr() for j in range(nwin)]
+            cnts = [counts[j].data_ptr() for j in range(nwin)]
+            icnts = [icount[j].data_ptr() for j in range(nwin)]
+            caps = (C.c_int64 * batch)(*([n] * batch))
+            batch_args = []
+            for g in range(nwin):  # group starting at window g (windows wrap around)
+                js = [(g + u) % nwin for u in range(batch)]
+                batch_args.append(((_lib.GfPoints * batch)(*[pts[j] for j in js]),
+                                   (P_ * batch)(*[bms[j] for j in js]), (P_ * batch)(*[cnts[j] for j in js]),
+                                   (P_ * batch)(*[idx[(g + u) % 4].data_ptr() for u in range(batch)]),
+                                   (P_ * batch)(*[icnts[j] for j in js])))
 
         def step(i):
+            if batch > 1:
+                if i % batch:
+                    return
+                pa, bm, ct, ix, ic = batch_args[i % nwin]
+                c = ctxs[(i // batch) % nstreams].handle
+                st = L.gf_range_run_batch(plans[(i // batch) % nstreams], batch, pa, bm, ct,
+                                          None if args.no_indices else ix, caps, ic)
+                if st:
+                    _lib.check(st, c, "gf_range_run_batch")
+                return
             j = i % nwin
             c = ctxs[i % nstreams].handle
             st = L.gf_range_run(plans[i % nstreams], C.byref(pts[j]), bitmaps[j].data_ptr(), None,
@@ -296,7 +321,8 @@ def bench_range(args, polygons=False):
                 c.synchronize()
             torch.cuda.synchronize()
 
-        for i in range(args.warmup):
+        steps = -(-args.steps // batch) * batch  # whole batches
+        for i in range(-(-args.warmup // batch) * batch):
             step(i)
         sync_all()
         _sync(world)
@@ -305,7 +331,7 @@ def bench_range(args, polygons=False):
             c.set_timing((1 << _lib.K_RANGE_SCAN) | (1 << _lib.K_RANGE_TEST))
         _sync(world)
         t0 = time.perf_counter()
-        for i in range(args.steps):
+        for i in range(steps):
             step(i)
         sync_all()
         elapsed = time.perf_counter() - t0
@@ -353,29 +379,32 @@ def bench_range(args, polygons=False):
                     and np.array_equal(R["single"], got[got < S]))
         for hp in plans:
             L.gf_range_plan_destroy(hp)
-        avg_scan = ms / 1000.0 / max(cnt, 1)
+        avg_scan = ms / 1000.0 / max(cnt, 1) / batch  # a batched launch evaluates `batch` windows
         avg_test = tms / 1000.0 / tcnt if tcnt else 0.0
         avg = avg_scan + avg_test
         # with windows in flight on several streams a launch's own duration counts shared time
         # more than once: the roofline then uses the sustained interval between windows
-        basis = "bytes per window / average launch duration (one stream)"
+        basis = "bytes per window / average launch duration per window (one stream)"
         if nstreams > 1:
-            avg = elapsed / args.steps
+            avg = elapsed / steps
             basis = f"bytes per window / window interval ({nstreams} streams; includes host work)"
         wl = (f"ppoly_{len(polys)}polys_r{r}_{n // 1_000_000}Mpts_grid{grid_n}" if polygons
               else f"range_pp_r{r}_{n // 1_000_000}Mpts_grid{grid_n}")
         if world > 1:
             wl += f"_per_gpu_x{world}"
         n_all = int(_reduce_sum(float(n), world, args, dev)) if world > 1 else n
-        _line("point-polygon range" if polygons else "point-point range", n_all * args.steps / elapsed,
-              "points/s", args.steps, args.warmup, elapsed,
+        _line("point-polygon range" if polygons else "point-point range", n_all * steps / elapsed,
+              "points/s", steps, args.warmup, elapsed,
               "range_kernel + range_test_kernel" if tcnt else "range_kernel", 16.0 * n + n / 8.0 + 4.0 * hits, avg,
               {"n_gpus": world,
                "config": {"workload": wl, "points_per_window": n_all, "points_per_gpu": n, "grid": grid_n,
                           "radius": r, "hits_window0": hits, "scan_blocks": blocks, "defer_mode": dmode,
                           "windows_in_flight": nstreams, "distinct_windows": nwin,
                           "window_set_MB": round(16.0 * n * nwin / 2**20, 1),
-                          "step": "gf_range_run (bitmap + counts) + gf_bitmap_to_indices_async (index list)",
+                          "step": ("gf_range_run (bitmap + counts) + gf_bitmap_to_indices_async (index list)"
+                                   if batch == 1 else f"gf_range_run_batch of {batch} windows (bitmaps + counts "
+                                   "in one launch, index lists in one more); value counts every window"),
+                          "windows_per_launch": batch,
                           "parallelism": f"cell-column shards x{world} (no collective)" + (
                               ", bands balanced by work (points + 8 x candidate-cell points)"
                               if polygons and world > 1 else ""),
