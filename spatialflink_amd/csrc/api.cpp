@@ -1560,6 +1560,27 @@ int gf::knn_enqueue_merge(gf_knn_plan* P, const gf_points* pts, void* result, co
     ctx->stream = main;
     return rc;
   }
+  if (P->pipeline == 2 && P->poly) {
+    // polygon query: the prefilter scan of this window on lane j with the previous window's
+    // select (other lane) in block 0, then this window's refine; its select rides the next launch
+    const int j = (int)(P->seq++ & 1);
+    if ((st = poly_buffers(P))) return st;
+    const bool sample = pts->n >= kSampleMinN && (!P->use_hint || !P->lane_warm[j]);
+    if (sample && (st = knn_launch_sample(P, j, pts, 0))) return st;
+    P->lane_warm[j] = 1;
+    const KnnPolyArgs a = poly_args(P, j, pts, 0, pts->n, sample ? 2 : 1, 0);
+    KnnSelectArgs q{};
+    const int has_prev = P->pend_lane >= 0;
+    if (has_prev) q = select_args(P, P->pend_lane, 1, P->use_hint, P->pend_result, P->pend_idx_base);
+    const bool fold = merge && merge->nrec > 0 && has_prev && P->k <= kFusedMergeMaxK;
+    GF_HIP_CHECK(ctx, launch_knn_poly_fused(ctx, a, q, has_prev, scan_blocks_for(P, (pts->n + 1) / 2),
+                                           fold ? merge : nullptr));
+    *merged = fold ? 1 : 0;
+    P->pend_lane = j;
+    P->pend_result = result;
+    P->pend_idx_base = P->idx_base;
+    return GF_OK;
+  }
   if (P->pipeline == 2) {
     // one fused launch: scan this window on lane j (threshold = the lane's hint), select the
     // pending previous window on the other lane in block 0
@@ -1624,8 +1645,8 @@ extern "C" int gf_knn_plan_set_pipeline(gf_knn_plan* P, int depth) {
   gf_ctx* ctx = P->ctx;
   if (depth >= 2 && P->k > 256)
     return set_err(ctx, GF_ERR_ARG, "gf_knn_plan_set_pipeline: depth 2 / 3 needs k <= 256");
-  if (depth >= 2 && P->poly)
-    return set_err(ctx, GF_ERR_ARG, "gf_knn_plan_set_pipeline: polygon queries run at depth 1");
+  if (depth == 3 && P->poly)
+    return set_err(ctx, GF_ERR_ARG, "gf_knn_plan_set_pipeline: polygon queries run at depth <= 2");
   int st = bind(ctx);
   if (st || (st = gf_knn_plan_flush(P))) return st;
   GF_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));

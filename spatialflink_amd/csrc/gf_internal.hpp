@@ -457,6 +457,11 @@ int knn_exact_record(gf_knn_plan* P, const gf_points* pts, void* result);
 
 hipError_t launch_knn_poly_sample(gf_ctx* ctx, const KnnPolyArgs& a);
 hipError_t launch_knn_poly_scan(gf_ctx* ctx, const KnnPolyArgs& a, int blocks);  // prefilter + refine
+struct KnnSelectArgs;
+struct KnnMergeArgs;
+// depth 2: prefilter of this window + (block 0) the previous window's select / window merge, then refine
+hipError_t launch_knn_poly_fused(gf_ctx* ctx, const KnnPolyArgs& a, const KnnSelectArgs& prev, int has_prev,
+                                 int blocks, const KnnMergeArgs* merge);
 hipError_t launch_knn_merge(gf_ctx* ctx, int32_t k, const void* records, int32_t nrec, size_t rec_stride,
                             int32_t nwin, size_t win_stride, void* result, size_t res_stride, int foreign);
 // records of one merge given as a pointer list (kernel argument; the panes of a sliding window)

@@ -1041,12 +1041,11 @@ __device__ __forceinline__ void maybe_append(const KnnPolyArgs& a, bool c, int64
 
 // Two points per lane per iteration from 16-B loads of x and y (begin is even, x / y 16-B
 // aligned), like the point scan; the odd last point in a checked tail.
-__global__ __launch_bounds__(kBlock) void knn_poly_scan_kernel(KnnPolyArgs a) {
-  const double T = a.use_state ? a.st->T : a.r;
+__device__ __forceinline__ void knn_poly_scan_body(const KnnPolyArgs& a, double T, int64_t bid, int64_t nblk) {
   const int lane = threadIdx.x & 63;
-  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  const int64_t stride = nblk * kBlock;
   const int64_t pb = a.begin >> 1, pe = a.end >> 1;  // complete pairs [pb, pe)
-  for (int64_t p = pb + (int64_t)blockIdx.x * kBlock + threadIdx.x; p - lane < pe; p += stride) {
+  for (int64_t p = pb + bid * kBlock + threadIdx.x; p - lane < pe; p += stride) {
     const bool in = p < pe;
     dbl2 xv = {0.0, 0.0}, yv = {0.0, 0.0};
     if (in) {
@@ -1059,10 +1058,43 @@ __global__ __launch_bounds__(kBlock) void knn_poly_scan_kernel(KnnPolyArgs a) {
     maybe_append(a, c0, 2 * p);
     maybe_append(a, c1, 2 * p + 1);
   }
-  if ((a.end & 1) && blockIdx.x == 0 && threadIdx.x < 64) {  // the odd last point, one wave
+  if ((a.end & 1) && bid == 0 && threadIdx.x < 64) {  // the odd last point, one wave
     const int64_t i = a.end - 1;
     maybe_append(a, lane == 0 && poly_maybe(a, a.x[i], a.y[i], T), i);
   }
+}
+
+__global__ __launch_bounds__(kBlock) void knn_poly_scan_kernel(KnnPolyArgs a) {
+  knn_poly_scan_body(a, a.use_state ? a.st->T : a.r, blockIdx.x, gridDim.x);
+}
+
+// Polygon query at pipeline depth 2: blocks 1.. run window i's prefilter scan with the lane's
+// hint threshold (use_state 2: the sample just taken), block 0 the select of window i-1 (whose
+// refine ran before this launch) on the other lane -- and, for a sliding window closing with it,
+// the window merge.  Window i's refine follows in its own launch; its select rides in window
+// i+1's launch (or gf_knn_plan_flush).  Two launches per window instead of three.
+__global__ __launch_bounds__(kBlock) void knn_poly_fused_kernel(KnnPolyArgs a, KnnSelectArgs prev, int has_prev,
+                                                                KnnMergeArgs m) {
+  __shared__ SelLite L;
+  if (blockIdx.x == 0) {
+    if (has_prev) knn_select_body<SelLite, false>(prev, L);
+    if (m.nrec > 0) {
+      __threadfence();
+      __syncthreads();
+      const ListRecs src{&m.list};
+      knn_merge_body(prev.k, src, m.nrec, m.result, L);
+    }
+    return;
+  }
+  double T;
+  if (a.use_state == 2) {
+    T = a.st->T;
+  } else {
+    const double h = a.st->hint_T;
+    T = (h > 0.0 && h < a.r) ? h : a.r;
+    if (blockIdx.x == 1 && threadIdx.x == 0) a.st->T = T;  // the refine and the select read it
+  }
+  knn_poly_scan_body(a, T, blockIdx.x - 1, gridDim.x - 1);
 }
 
 // Refine: exact distance of each prefilter survivor; d <= T -> (d, idx, objID) candidates.  A
@@ -1106,6 +1138,20 @@ __global__ __launch_bounds__(kBlock) void knn_poly_refine_kernel(KnnPolyArgs a) 
 hipError_t launch_knn_poly_sample(gf_ctx* ctx, const KnnPolyArgs& a) {
   KTimer t(ctx, GF_K_KNN_SAMPLE);
   hipLaunchKernelGGL(knn_poly_sample_kernel, dim3(kSampleBlocks), dim3(kBlock), 0, ctx->stream, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_knn_poly_fused(gf_ctx* ctx, const KnnPolyArgs& a, const KnnSelectArgs& prev, int has_prev,
+                                 int blocks, const KnnMergeArgs* merge) {
+  KnnMergeArgs m{};
+  if (merge && has_prev) m = *merge;
+  {
+    KTimer t(ctx, GF_K_KNN_SCAN);
+    hipLaunchKernelGGL(knn_poly_fused_kernel, dim3(blocks + 1), dim3(kBlock), 0, ctx->stream, a, prev, has_prev, m);
+  }
+  KnnPolyArgs r = a;
+  r.use_state = 1;  // the refine reads the threshold the scan blocks stored
+  hipLaunchKernelGGL(knn_poly_refine_kernel, dim3(256), dim3(kBlock), 0, ctx->stream, r);
   return hipGetLastError();
 }
 

@@ -85,9 +85,44 @@ def test_polyknn_continuous_and_fallback(sf, oracle_mod):
     run_case(sf, oracle_mod, POLYS["square"], 400_000, 0.5, 50, cap=64)  # every scan overflows
 
 
-def test_polyknn_rejects_pipeline_depth_2(sf, oracle_mod):
-    g = sf.UniformGrid(100, *BEIJING)
-    P = sf.Polygon(POLYS["square"], g)
-    op = sf.PointPolygonKNNQuery(conf(sf), g)
+@pytest.mark.parametrize("name,approx,k", [("holed", False, 60), ("square", True, 20), ("generated", False, 128)])
+def test_polyknn_pipeline_depth_2(sf, oracle_mod, name, approx, k):
+    """Depth 2 (PointPolygonKNNQuery.java:245-317 per window): one launch per window carries the
+    previous window's select; windows of mixed sizes (sampled and small), a window far from the
+    polygon (empty result), flush, then the synchronous API on the same plan.  Depth 3 is refused."""
+    import torch
+
+    g = sf.UniformGrid(500, *BEIJING)
+    og = oracle_mod.grid(500, *BEIJING)
+    P = sf.Polygon(POLYS[name], g)
+    OP = oracle_mod.Polygons([P.rings])
+    op = sf.PointPolygonKNNQuery(conf(sf, approx), g)
+    data = []
+    for seed, n, bounds in ((31, 1_100_000, BEIJING), (32, 300_000, BEIJING), (33, 1_300_000, BEIJING),
+                            (34, 50_000, (117.5, 117.6, 41.0, 41.1)), (35, 1_050_000, BEIJING)):
+        x, y = oracle_mod.java_random_points(seed, n, *bounds)
+        obj = (np.random.default_rng(seed).permutation(n) % max(1, n // 2)).astype(np.int64)
+        data.append((x, y, obj, sf.PointWindow.from_numpy(x, y, obj)))
+    op.set_pipeline(0, P, 0.2, k, 2)
+    order = [0, 1, 2, 3, 4, 0, 0, 2, 3, 1]
+    rec = sf.PinnedRecords(len(order), k)
+    for i, j in enumerate(order):
+        op.enqueue(data[j][3], P, 0.2, k, rec.ptr(i))
+    op.flush(0, P, 0.2, k)
+    torch.cuda.synchronize()
+    for i, j in enumerate(order):
+        x, y, obj, w = data[j]
+        res = op.finish(w, P, 0.2, k, rec.raw(i))
+        m, eo, ed, ei = oracle_mod.knn_ppoly(og, x, y, obj, OP, 0.2, k, approx)
+        np.testing.assert_array_equal(res.objID, eo)
+        np.testing.assert_array_equal(res.dist, ed)
+        np.testing.assert_array_equal(res.idx, ei)
+    for j in (2, 3):  # synchronous API on the pipelined plan
+        x, y, obj, w = data[j]
+        res = op.run(w, P, 0.2, k)
+        m, eo, ed, ei = oracle_mod.knn_ppoly(og, x, y, obj, OP, 0.2, k, approx)
+        np.testing.assert_array_equal(res.objID, eo)
+        np.testing.assert_array_equal(res.dist, ed)
     with pytest.raises(ValueError):
-        op.set_pipeline(0, P, 0.5, 10, 2)
+        op.set_pipeline(0, P, 0.2, k, 3)
+    op.set_pipeline(0, P, 0.2, k, 1)
