@@ -1868,13 +1868,20 @@ static int join_pp_impl(gf_ctx* ctx, const gf_grid* ugrid, const gf_grid* qgrid,
     const unsigned long long h = *(volatile unsigned long long*)ctx->join_hint;
     if (h > 0) ppp = (double)h / (double)ctx->join_hint_no;
   }
-  int64_t chunk = 256;
-  while (chunk < 65536 && (double)chunk * nwaves * 8 < ppp * (double)no) chunk <<= 1;
+  // block chunks (default): a probe block's waves share its chunks -- LDS offsets, one device
+  // atomic per chunk of ~1/4 of the block's expected pairs, tails (holes) per block.  Wave chunks
+  // (GF_JOIN_WAVE_CHUNKS=1, and the streaming experiment): one device atomic per wave chunk.
+  const char* wenv = std::getenv("GF_JOIN_WAVE_CHUNKS");
+  const bool block_chunks = !(wenv && *wenv == '1') && !stream;
+  const int64_t ntails = block_chunks ? probe_blocks : nwaves;
+  int64_t chunk = block_chunks ? 4096 : 256;
+  while (chunk < (block_chunks ? (1 << 20) : 65536) && (double)chunk * ntails * (block_chunks ? 4 : 8) < ppp * (double)no)
+    chunk <<= 1;
   if (const char* e = std::getenv("GF_JOIN_CHUNK")) {  // testing / tuning: a fixed chunk (power of 2)
     const int64_t v = std::atoll(e);
-    if (v >= 64 && v <= (1 << 20) && (v & (v - 1)) == 0) chunk = v;
+    if (v >= (block_chunks ? 4096 : 64) && v <= (1 << 20) && (v & (v - 1)) == 0) chunk = v;
   }
-  size_t o_spill = ar.take<uint64_t>(rowpath ? nwaves * chunk : 1);
+  size_t o_spill = ar.take<uint64_t>(rowpath ? ntails * chunk : 1);
   size_t o_tb = ar.take<uint64_t>(nwaves), o_tf = ar.take<uint32_t>(nwaves);
   size_t o_hs = ar.take<uint64_t>(nwaves + 1), o_hp = ar.take<uint64_t>(nwaves + 2);
   size_t o_ss = ar.take<uint64_t>(nwaves + 2), o_sp = ar.take<uint64_t>(nwaves + 3), o_fc = ar.take<uint32_t>(2);
@@ -1920,11 +1927,12 @@ static int join_pp_impl(gf_ctx* ctx, const gf_grid* ugrid, const gf_grid* qgrid,
     o.aligned = ((uintptr_t)pairs & 7) == 0;
     o.chunk = (uint32_t)chunk;
     o.spill = (uint2*)(base + o_spill);
-    o.spill_cap = (uint64_t)(nwaves * chunk);
+    o.spill_cap = (uint64_t)(ntails * chunk);
     o.gctr = ctx->join_gctr;
     o.tail_base = (uint64_t*)(base + o_tb);
     o.tail_fill = U32(o_tf);
-    o.nwaves = (uint32_t)nwaves;
+    o.nwaves = (uint32_t)ntails;
+    o.block_chunks = block_chunks;
     j.f = f; j.fs = (double)f / ugrid->cellLength;
     j.lds_budget = join_probe_budget(nq, qn, c, f);
     // (1) row histograms of both sides, (2) one scan of both matrices, (3) write-combined row
@@ -1939,6 +1947,7 @@ static int join_pp_impl(gf_ctx* ctx, const gf_grid* ugrid, const gf_grid* qgrid,
     GF_HIP_CHECK(ctx, launch_join_rows(ctx, j, q, 2));
     if (stream) {
       j.out.nwaves = (uint32_t)nwaves;  // the stream grid: kBlock-thread blocks, same wave count
+      j.out.block_chunks = 0;
       GF_HIP_CHECK(ctx, launch_join_stream(ctx, j));
     } else {
       GF_HIP_CHECK(ctx, launch_join_rows(ctx, j, q, 3));

@@ -561,7 +561,9 @@ struct JoinOut {
   unsigned long long* gctr;  // reserved positions (0 between calls: the fix-up resets it)
   uint64_t* tail_base;       // [nwaves] base of each wave's last chunk (~0: none)
   uint32_t* tail_fill;       // [nwaves]
-  uint32_t nwaves;
+  uint32_t nwaves;           // tail entries: the probe's waves, or its blocks (block_chunks)
+  int block_chunks;          // row probe: a block's waves share its chunks (LDS offsets, one
+                             // global atomic per chunk); tails per block
 };
 struct JoinRowArgs {
   const double* ox;

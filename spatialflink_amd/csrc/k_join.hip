@@ -541,7 +541,13 @@ struct JoinProbeHdr {
   uint32_t g0;       // fine path: sorted index of the first staged query point
   uint32_t gm;       // fine path: staged query points (0: none; their indices are in LDS)
   uint32_t lqidx;    // fine path: LDS byte offset of the staged query indices
+  // block chunks (JoinOut.block_chunks): the block's pairs so far, and the bases of its chunks
+  // (chunk c in slot c % kJoinRing, tagged c + 1 once published)
+  uint32_t bfill;
+  uint32_t ctag[64];
+  unsigned long long cbase[64];
 };
+constexpr uint32_t kJoinRing = 64;
 constexpr int kJoinHdrBytes = (int)((sizeof(JoinProbeHdr) + 15) / 16 * 16);
 constexpr int kJoinWaveBuf = 128;  // pairs a wave collects in LDS before one coalesced flush
 static_assert(kJoinTask <= 8192, "local index packed in 13 bits");
@@ -643,6 +649,55 @@ __device__ __forceinline__ void join_emit_close(const JoinOut& o, const JoinWave
   }
 }
 
+// Block chunks: the wave takes `cnt` consecutive block positions with one LDS atomic; a block
+// position p lives in the block's chunk p / C at offset p % C.  The wave whose range holds the
+// first position of a chunk allocates it (one device atomic) and publishes its base in the LDS
+// ring; the others spin on the ring tag (the allocating wave has its offset already and never
+// waits before publishing, so the spin ends).  A flush (<= kJoinWaveBuf pairs) spans at most two
+// chunks (C >= 4096).  The ring holds the latest kJoinRing chunks: a wave reads its bases right
+// after its own LDS atomic, long before the block can have issued kJoinRing * C more positions.
+template <class Get>
+__device__ __forceinline__ void join_emit_block(const JoinOut& o, JoinProbeHdr& hd, uint32_t cnt, Get get) {
+  const uint32_t lane = threadIdx.x & 63, C = o.chunk;
+  uint32_t off = 0;
+  if (lane == 0) off = atomicAdd(&hd.bfill, cnt);
+  off = join_uni(off);
+  const uint32_t c0 = off / C, c1 = (off + cnt - 1) / C;
+  for (uint32_t c = c0; c <= c1; ++c) {  // chunks that start inside [off, off + cnt): allocate
+    if (c * C >= off && lane == 0) {
+      const unsigned long long b = atomicAdd(o.gctr, (unsigned long long)C);
+      hd.cbase[c % kJoinRing] = b;  // the release store below orders it before the tag
+      __hip_atomic_store(&hd.ctag[c % kJoinRing], c + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+  }
+  unsigned long long base[2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const uint32_t c = c0 + k <= c1 ? c0 + k : c1;
+    while (__hip_atomic_load(&hd.ctag[c % kJoinRing], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != c + 1)
+      __builtin_amdgcn_s_sleep(1);
+    base[k] = join_uni64(hd.cbase[c % kJoinRing]);
+  }
+  for (uint32_t i = lane; i < cnt; i += 64) {
+    const uint32_t p = off + i, c = p / C;
+    join_vstore(o, (c == c0 ? base[0] : base[1]) + (p - c * C), get(i));
+  }
+}
+// the block's last chunk, for the fix-up (after the block's final barrier)
+__device__ __forceinline__ void join_block_close(const JoinOut& o, const JoinProbeHdr& hd) {
+  if (threadIdx.x == 0) {
+    const uint32_t n = hd.bfill, C = o.chunk;
+    if (n == 0) {
+      o.tail_base[blockIdx.x] = ~0ull;
+      o.tail_fill[blockIdx.x] = 0u;
+    } else {
+      const uint32_t c = (n - 1) / C;
+      o.tail_base[blockIdx.x] = hd.cbase[c % kJoinRing];
+      o.tail_fill[blockIdx.x] = n - c * C;
+    }
+  }
+}
+
 // The wave's pair buffer in LDS: hits are appended in ballot order (one mbcnt per hit round,
 // the count stays in a scalar register); past kJoinWaveBuf - 64 the wave writes the buffer out
 // (join_emit: coalesced stores into its output chunk) with each query slot mapped to its query
@@ -654,11 +709,13 @@ struct JoinWaveBuf {
     const uint32_t g0 = hd.g0, gm = join_uni(hd.gm);
     const uint32_t* lq = reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(&hd) + hd.lqidx);
     const uint2* b = buf;
-    join_emit(a.out, wo, cnt, [&](uint32_t i) {
+    auto get = [&](uint32_t i) {
       const uint2 v = b[i];
       const uint32_t qi = v.y & 0x80000000u ? v.y & 0x7fffffffu : (v.y - g0 < gm ? lq[v.y - g0] : a.sqidx[v.y]);
       return make_uint2(v.x, qi);
-    });
+    };
+    if (a.out.block_chunks) join_emit_block(a.out, hd, cnt, get);
+    else join_emit(a.out, wo, cnt, get);
     cnt = 0;
   }
   // one round's hits: hit i of this lane (candidate q[i]) goes after all hits of rounds < i
@@ -1049,11 +1106,22 @@ __global__ __launch_bounds__(kJoinThreads) void join_row_probe_kernel(JoinRowArg
   const uint32_t ntask = a.task_off[a.nrows];
   const uint32_t per = (ntask + 7) / 8, xcd = blockIdx.x & 7u, nb = (gridDim.x + 7 - xcd) / 8;
   JoinWaveOut wo{~0ull, a.out.chunk};
+  JoinProbeHdr& hd = *reinterpret_cast<JoinProbeHdr*>(lds_base);
+  if (a.out.block_chunks) {
+    for (uint32_t j = threadIdx.x; j < kJoinRing; j += kJoinThreads) hd.ctag[j] = 0u;
+    if (threadIdx.x == 0) hd.bfill = 0u;
+    __syncthreads();
+  }
   for (uint32_t k = blockIdx.x >> 3; k < per; k += nb) {  // block-uniform
     const uint32_t task = xcd * per + k;
     if (task < ntask) join_probe_task<MODE, FINE>(a, task, lds_base, wo);
   }
-  join_emit_close(a.out, wo, blockIdx.x * (kJoinThreads / 64) + (threadIdx.x >> 6));
+  if (a.out.block_chunks) {
+    __syncthreads();  // every wave's last flush is in
+    join_block_close(a.out, hd);
+  } else {
+    join_emit_close(a.out, wo, blockIdx.x * (kJoinThreads / 64) + (threadIdx.x >> 6));
+  }
 }
 
 // ---- streaming probe (experiment, GF_FLAG_JOIN_STREAM) --------------------------------------
@@ -1304,7 +1372,7 @@ hipError_t launch_join_rows(gf_ctx* ctx, const JoinRowArgs& a, const JoinQueryAr
     case 3: {
       KTimer t(ctx, GF_K_JOIN_PROBE);
       const size_t lds = join_probe_lds_bytes(a.lds_budget, a.qn, a.f);
-      const dim3 pg(a.out.nwaves / (kJoinThreads / 64));
+      const dim3 pg(a.out.block_chunks ? a.out.nwaves : a.out.nwaves / (kJoinThreads / 64));
       const bool m0 = !a.approx && a.metric == 0;
       if (a.f > 1) {  // host: the fine path is exact (never approximate)
         if (m0) hipLaunchKernelGGL((join_row_probe_kernel<0, 1>), pg, dim3(kJoinThreads), lds, s, a);
