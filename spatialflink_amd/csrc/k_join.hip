@@ -224,10 +224,13 @@ __device__ __forceinline__ uint32_t join_fine_key(const JoinQueryArgs& q, double
   return (uint32_t)(((int64_t)q.f * clamp_key(cy, q.qn) + jy) * fW + (int64_t)q.f * clamp_key(cx, q.qn) + jx);
 }
 
-// Row of an ordinary point: its cell row, -1 outside the grid (no replicated key can match it).  Row of a query point: its clamped cell row (0 .. qn+1).
-__device__ __forceinline__ int32_t join_orow(const JoinRowArgs& a, double x, double y) {
-  const int32_t cx = cell_index(x, a.u_minX, a.u_cl), cy = cell_index(y, a.u_minY, a.u_cl);
-  return cx >= 0 && cy >= 0 && cx < a.qn && cy < a.qn ? cy : -1;
+// Row of an ordinary point: its cell row, -1 when the row is outside the grid; a point whose
+// COLUMN is outside the grid is bucketed too and dropped by the probe's sort (no replicated key
+// can match it), so the histogram pass reads y alone.  Row of a query point: its clamped cell
+// row (0 .. qn+1).
+__device__ __forceinline__ int32_t join_orow(const JoinRowArgs& a, double, double y) {
+  const int32_t cy = cell_index(y, a.u_minY, a.u_cl);
+  return cy >= 0 && cy < a.qn ? cy : -1;
 }
 __device__ __forceinline__ int32_t join_qrow(const JoinQueryArgs& q, double, double y) {
   return clamp_key(cell_index(y, q.minY, q.cl), q.qn);
@@ -543,6 +546,7 @@ struct JoinProbeHdr {
   uint32_t lqidx;    // fine path: LDS byte offset of the staged query indices
   // block chunks (JoinOut.block_chunks): the block's pairs so far, and the bases of its chunks
   // (chunk c in slot c % kJoinRing, tagged c + 1 once published)
+  uint32_t kept;     // the task's points inside the grid (sorted; the rest dropped)
   uint32_t bfill;
   uint32_t ctag[64];
   unsigned long long cbase[64];
@@ -973,7 +977,11 @@ __device__ __forceinline__ void join_probe_task(const JoinRowArgs& a, uint32_t t
     for (int u = 0; u < PER; ++u) {
       const uint32_t i = threadIdx.x + u * kJoinThreads;
       if (i < cnt) {
-        const int32_t cx = cell_index(xs[u], a.u_minX, a.u_cl);  // in [0, qn): bucketed points are in grid
+        const int32_t cx = cell_index(xs[u], a.u_minX, a.u_cl);  // the row is in the grid, the column maybe not
+        if (cx < 0 || cx >= qn) {
+          lcx[i] = 0xFFFFu;  // outside the grid: no key matches (never a valid key: < 4 << 13)
+          continue;
+        }
         int32_t col = cx, key = cx;
         if (FINE) {
           col = f * (cx + 1) + join_sub(xs[u], a.u_minX, a.u_cl, cx, a.fs, f);
@@ -1006,10 +1014,16 @@ __device__ __forceinline__ void join_probe_task(const JoinRowArgs& a, uint32_t t
       hist[j] = before;
       before += v;
     }
+    if (threadIdx.x == 0) {
+      uint32_t t = 0;
+      for (int w = 0; w < kJoinThreads / 64; ++w) t += wsum[w];
+      hd.kept = t;
+    }
   }
   __syncthreads();
   for (uint32_t i = threadIdx.x; i < cnt; i += kJoinThreads) {
     const uint32_t key = lcx[i];
+    if (key == 0xFFFFu) continue;
     if (FINE) lsort[atomicAdd(&hist[key & 8191u], 1u)] = (key & 8191u) << 15 | (key >> 13) << 13 | i;
     else lsort[atomicAdd(&hist[key], 1u)] = key << 13 | i;
   }
@@ -1025,16 +1039,17 @@ __device__ __forceinline__ void join_probe_task(const JoinRowArgs& a, uint32_t t
     double2 v;
     uint32_t idx, e;
   };
-  auto fetch = [&](uint32_t s) {
+  const uint32_t kept = hd.kept;
+  auto fetch = [&](uint32_t s) {  // past the end: entry 0 of the task's points (always present)
     Pt p;
-    p.e = lsort[s + lane < cnt ? s + lane : 0u];
+    p.e = s + lane < kept ? lsort[s + lane] : 0u;
     p.v = reinterpret_cast<const double2*>(a.soxy)[beg + (p.e & 8191u)];
     p.idx = a.soidx[beg + (p.e & 8191u)];
     return p;
   };
   Pt nxt = fetch((threadIdx.x >> 6) * 64);
-  for (uint32_t s = (threadIdx.x >> 6) * 64; s < cnt; s += kJoinThreads) {  // wave-uniform
-    const bool valid = s + lane < cnt;
+  for (uint32_t s = (threadIdx.x >> 6) * 64; s < kept; s += kJoinThreads) {  // wave-uniform
+    const bool valid = s + lane < kept;
     const Pt cur = nxt;
     nxt = fetch(s + kJoinThreads);
     if (FINE) {
