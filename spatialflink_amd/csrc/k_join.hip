@@ -553,7 +553,11 @@ struct JoinProbeHdr {
 };
 constexpr uint32_t kJoinRing = 64;
 constexpr int kJoinHdrBytes = (int)((sizeof(JoinProbeHdr) + 15) / 16 * 16);
-constexpr int kJoinWaveBuf = 128;  // pairs a wave collects in LDS before one coalesced flush
+// pairs a wave collects in LDS: a wave-step's pairs (64 points) normally fit, so the walk's
+// inner loop has no global memory operation (the buffer is written out after the step, or when a
+// round could overflow it -- outside the round loop, join_*_walk)
+constexpr int kJoinWaveBuf = 384;
+constexpr int kJoinRound = 4;  // candidates per lane per walk round (their loads in flight together)
 static_assert(kJoinTask <= 8192, "local index packed in 13 bits");
 // Dynamic LDS of the probe: header | staged rows (budget) | sorted (column << 13 | local index)
 // u32 per point | union { task prologue: u16 column keys + column histogram [columns + 1]
@@ -722,28 +726,20 @@ struct JoinWaveBuf {
     else join_emit(a.out, wo, cnt, get);
     cnt = 0;
   }
-  // one round's hits: hit i of this lane (candidate q[i]) goes after all hits of rounds < i
+  // one round's hits: hit i of this lane (candidate q[i]) goes after all hits of rounds < i.
+  // The caller guarantees room for a full round (room()).
   template <int R>
-  __device__ __forceinline__ void push(const bool (&hit)[R], uint32_t p, const uint32_t (&q)[R], const JoinRowArgs& a,
-                                       JoinProbeHdr& hd, JoinWaveOut& wo) {
-    uint64_t m[R];
-    uint64_t any = 0;
+  __device__ __forceinline__ void push(const bool (&hit)[R], uint32_t p, const uint32_t (&q)[R]) {
 #pragma unroll
     for (int i = 0; i < R; ++i) {
-      m[i] = __ballot(hit[i]);
-      any |= m[i];
-    }
-    if (any == 0) return;
-#pragma unroll
-    for (int i = 0; i < R; ++i) {
-      if (m[i] == 0) continue;
+      const uint64_t m = __ballot(hit[i]);
       if (hit[i])
-        buf[cnt + __builtin_amdgcn_mbcnt_hi((uint32_t)(m[i] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m[i], 0u))] =
+        buf[cnt + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] =
             make_uint2(p, q[i]);
-      cnt += (uint32_t)__popcll(m[i]);
-      if (cnt > kJoinWaveBuf - 64) flush(a, hd, wo);
+      cnt += (uint32_t)__popcll(m);
     }
   }
+  __device__ __forceinline__ bool room() const { return cnt <= (uint32_t)(kJoinWaveBuf - 64 * kJoinRound); }
 };
 
 // One lane's candidates [tb, te) of one query row (relative to the row's first point gb): the
@@ -770,29 +766,39 @@ __device__ __forceinline__ void join_lane_run(const JoinRowArgs& a, const double
     else ok = a.approx || (a.metric == 0 ? dx * dx + dy * dy <= a.s_r : fdlibm_hypot(dx, dy) <= a.r);
     return in && ok;
   };
-  constexpr int R = 4;  // candidates per round: their loads are in flight together
-  for (uint32_t k = 0; __ballot(k < len) != 0; k += R) {
-    bool act[R], hit[R];
-    uint32_t t[R], q[R];
-    double2 v[R];
-#pragma unroll
-    for (int i = 0; i < R; ++i) {
-      act[i] = k + i < len;
-      t[i] = tb + (act[i] ? k + i : 0u);
-      q[i] = gb + t[i];
-    }
-#pragma unroll
-    for (int i = 0; i < R; ++i) {
-      if constexpr (LDS) {  // a stale slot for a finished lane reads in-bounds LDS, masked below
-        v[i] = lxy[t[i]];
-      } else {
-        v[i] = make_double2(0.0, 0.0);
-        if (act[i]) v[i] = make_double2(a.sqx[q[i]], a.sqy[q[i]]);
+  constexpr int R = kJoinRound;
+  uint32_t k = 0;
+  for (;;) {  // the round loop stops only to write a full buffer out (outside it: no VMEM inside)
+    bool full = false;
+    for (; __ballot(k < len) != 0; k += R) {
+      if (!wbuf.room()) {
+        full = true;
+        break;
       }
-    }
+      bool act[R], hit[R];
+      uint32_t t[R], q[R];
+      double2 v[R];
 #pragma unroll
-    for (int i = 0; i < R; ++i) hit[i] = test(act[i], t[i], v[i]);
-    wbuf.push<R>(hit, ln.pidx, q, a, hd, wo);
+      for (int i = 0; i < R; ++i) {
+        act[i] = k + i < len;
+        t[i] = tb + (act[i] ? k + i : 0u);
+        q[i] = gb + t[i];
+      }
+#pragma unroll
+      for (int i = 0; i < R; ++i) {
+        if constexpr (LDS) {  // a stale slot for a finished lane reads in-bounds LDS, masked below
+          v[i] = lxy[t[i]];
+        } else {
+          v[i] = make_double2(0.0, 0.0);
+          if (act[i]) v[i] = make_double2(a.sqx[q[i]], a.sqy[q[i]]);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < R; ++i) hit[i] = test(act[i], t[i], v[i]);
+      wbuf.push<R>(hit, ln.pidx, q);
+    }
+    if (!full) break;
+    wbuf.flush(a, hd, wo);
   }
 }
 
@@ -806,34 +812,44 @@ __device__ __forceinline__ void join_fine_walk(const JoinRowArgs& a, const doubl
                                                JoinWaveBuf& wbuf, JoinProbeHdr& hd, JoinWaveOut& wo) {
   const uint32_t L0 = e[0] - b[0], L1 = L0 + (e[1] - b[1]), L2 = L1 + (e[2] - b[2]);
   const uint32_t d0 = b[0], d1 = b[1] - L0, d2 = b[2] - L1;  // run s: index = k + d_s (mod 2^32)
-  for (uint32_t k = 0; __ballot(k < L2) != 0; k += R) {
-    bool hit[R];
-    uint32_t t[R], q[R];
-    double2 v[R];
-#pragma unroll
-    for (int i = 0; i < R; ++i) {
-      const uint32_t kk = k + i;
-      t[i] = kk < L2 ? kk + (kk < L0 ? d0 : (kk < L1 ? d1 : d2)) : 0u;
-      q[i] = g0 + t[i];
-    }
-#pragma unroll
-    for (int i = 0; i < R; ++i) {
-      if constexpr (LDS) {  // a finished lane reads staged slot 0 (some lane has a candidate)
-        v[i] = lxy[t[i]];
-      } else {
-        v[i] = make_double2(0.0, 0.0);
-        if (k + i < L2) v[i] = make_double2(a.sqx[q[i]], a.sqy[q[i]]);
+  uint32_t k = 0;
+  for (;;) {  // as join_lane_run: the buffer is written out only outside the round loop
+    bool full = false;
+    for (; __ballot(k < L2) != 0; k += R) {
+      if (!wbuf.room()) {
+        full = true;
+        break;
       }
-    }
+      bool hit[R];
+      uint32_t t[R], q[R];
+      double2 v[R];
 #pragma unroll
-    for (int i = 0; i < R; ++i) {
-      const double dx = ln.px - v[i].x, dy = ln.py - v[i].y;
-      bool ok;
-      if constexpr (MODE == 0) ok = dx * dx + dy * dy <= a.s_r;
-      else ok = a.metric == 0 ? dx * dx + dy * dy <= a.s_r : fdlibm_hypot(dx, dy) <= a.r;
-      hit[i] = k + i < L2 && ok;
+      for (int i = 0; i < R; ++i) {
+        const uint32_t kk = k + i;
+        t[i] = kk < L2 ? kk + (kk < L0 ? d0 : (kk < L1 ? d1 : d2)) : 0u;
+        q[i] = g0 + t[i];
+      }
+#pragma unroll
+      for (int i = 0; i < R; ++i) {
+        if constexpr (LDS) {  // a finished lane reads staged slot 0 (some lane has a candidate)
+          v[i] = lxy[t[i]];
+        } else {
+          v[i] = make_double2(0.0, 0.0);
+          if (k + i < L2) v[i] = make_double2(a.sqx[q[i]], a.sqy[q[i]]);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < R; ++i) {
+        const double dx = ln.px - v[i].x, dy = ln.py - v[i].y;
+        bool ok;
+        if constexpr (MODE == 0) ok = dx * dx + dy * dy <= a.s_r;
+        else ok = a.metric == 0 ? dx * dx + dy * dy <= a.s_r : fdlibm_hypot(dx, dy) <= a.r;
+        hit[i] = k + i < L2 && ok;
+      }
+      wbuf.push<R>(hit, ln.pidx, q);
     }
-    wbuf.push<R>(hit, ln.pidx, q, a, hd, wo);
+    if (!full) break;
+    wbuf.flush(a, hd, wo);
   }
 }
 
@@ -1047,11 +1063,19 @@ __device__ __forceinline__ void join_probe_task(const JoinRowArgs& a, uint32_t t
     p.idx = a.soidx[beg + (p.e & 8191u)];
     return p;
   };
-  Pt nxt = fetch((threadIdx.x >> 6) * 64);
+  // per wave-step: the next step's points are fetched, this step's candidates walked (LDS only,
+  // pairs into the wave buffer), then -- the fetch has landed during the walk -- the wait is
+  // taken BEFORE the step's stores go out: a wait after them would be vmcnt(0) (the compiler
+  // cannot count a data-dependent number of stores) and every step would pay the store latency
+  Pt cur = fetch((threadIdx.x >> 6) * 64);
   for (uint32_t s = (threadIdx.x >> 6) * 64; s < kept; s += kJoinThreads) {  // wave-uniform
     const bool valid = s + lane < kept;
-    const Pt cur = nxt;
-    nxt = fetch(s + kJoinThreads);
+    const Pt nxt = fetch(s + kJoinThreads);
+    auto step_end = [&]() {
+      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): nxt is in registers
+      if (!wbuf.room()) wbuf.flush(a, hd, wo);  // the next step starts with room for a round
+      cur = nxt;
+    };
     if (FINE) {
       const int32_t col = (int32_t)(cur.e >> 15), sub = (int32_t)((cur.e >> 13) & 3u);
       const int32_t cx = col / f - 1;
@@ -1067,7 +1091,7 @@ __device__ __forceinline__ void join_probe_task(const JoinRowArgs& a, uint32_t t
             e[k] = valid ? lo[(sub + k) * rs + col + 2] : 0u;
           }
           const double2* lxy = reinterpret_cast<const double2*>(lds + (f + 2) * fine_rb);
-          join_fine_walk<MODE, true, 4>(a, lxy, g0, b, e, ln, wbuf, hd, wo);
+          join_fine_walk<MODE, true, kJoinRound>(a, lxy, g0, b, e, ln, wbuf, hd, wo);
         } else {
           const int64_t fy0 = (int64_t)f * (cy + 1) - 1;
 #pragma unroll
@@ -1076,9 +1100,10 @@ __device__ __forceinline__ void join_probe_task(const JoinRowArgs& a, uint32_t t
             b[k] = valid ? qo[col - 1] - g0 : 0u;
             e[k] = valid ? qo[col + 2] - g0 : 0u;
           }
-          join_fine_walk<MODE, false, 4>(a, nullptr, g0, b, e, ln, wbuf, hd, wo);
+          join_fine_walk<MODE, false, kJoinRound>(a, nullptr, g0, b, e, ln, wbuf, hd, wo);
         }
       }
+      step_end();
       continue;
     }
     const JoinLane ln{cur.v.x, cur.v.y, valid ? (int32_t)(cur.e >> 13) : 0, cy, cur.idx};
@@ -1104,6 +1129,7 @@ __device__ __forceinline__ void join_probe_task(const JoinRowArgs& a, uint32_t t
         else join_lane_run<MODE, false, false>(a, nullptr, gb, tb, te, ln, wbuf, hd, wo);
       }
     }
+    step_end();
   }
   if (wbuf.cnt > 0) wbuf.flush(a, hd, wo);
   __syncthreads();  // the task's LDS is reused by the next one

@@ -214,6 +214,7 @@ class PointPointRangeQuery(_RangeBase):
     """range/PointPointRangeQuery.java -- window-based point-point range query."""
 
     def run(self, window: PointWindow, queryPointSet, queryRadius: float) -> RangeResult:
+        _require_supported(self.conf)
         qs = list(queryPointSet)
         ctx, plan = self.plan(window.x.device.index, qs, queryRadius)
         nq = len(qs) if self.conf.approximateQuery else 1
@@ -245,6 +246,7 @@ class PointPolygonRangeQuery(_RangeBase):
     """range/PointPolygonRangeQuery.java -- window-based point-polygon range query."""
 
     def run(self, window: PointWindow, queryPolygonSet, queryRadius: float) -> RangeResult:
+        _require_supported(self.conf)
         ctx, plan = self.plan(window.x.device.index, queryPolygonSet, queryRadius)
         return self._evaluate(plan, window, 1)
 
