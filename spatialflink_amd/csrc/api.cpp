@@ -260,6 +260,8 @@ extern "C" void gf_ctx_destroy(gf_ctx* ctx) {
   if (ctx->expand_status) hipFree(ctx->expand_status);
   if (ctx->join_gctr) hipFree(ctx->join_gctr);
   if (ctx->join_hint) hipHostFree(ctx->join_hint);
+  if (ctx->join_hist) hipFree(ctx->join_hist);
+  if (ctx->join_ovf) hipFree(ctx->join_ovf);
   for (auto& e : ctx->pending) { hipEventDestroy(e.a); hipEventDestroy(e.b); }
   for (auto e : ctx->pool) hipEventDestroy(e);
   if (ctx->scratch) hipFree(ctx->scratch);
@@ -1871,8 +1873,11 @@ static int join_pp_impl(gf_ctx* ctx, const gf_grid* ugrid, const gf_grid* qgrid,
   // block chunks (default): a probe block's waves share its chunks -- LDS offsets, one device
   // atomic per chunk of ~1/4 of the block's expected pairs, tails (holes) per block.  Wave chunks
   // (GF_JOIN_WAVE_CHUNKS=1, and the streaming experiment): one device atomic per wave chunk.
-  const char* wenv = std::getenv("GF_JOIN_WAVE_CHUNKS");
-  const bool block_chunks = !(wenv && *wenv == '1') && !stream;
+  // fine path: the band probe (k_join.hip) unless the row probe is asked for (A/B testing)
+  const char* renv = std::getenv("GF_JOIN_ROWPROBE");
+  const bool band = rowpath && f > 1 && !stream && !(renv && *renv == '1') && ctx->num_cus <= 1016;
+  const char* benv = std::getenv("GF_JOIN_BLOCK_CHUNKS");  // experiment (row probe only)
+  const bool block_chunks = benv && *benv == '1' && !stream && !band;
   const int64_t ntails = block_chunks ? probe_blocks : nwaves;
   int64_t chunk = block_chunks ? 4096 : 256;
   while (chunk < (block_chunks ? (1 << 20) : 65536) && (double)chunk * ntails * (block_chunks ? 4 : 8) < ppp * (double)no)
@@ -1881,7 +1886,16 @@ static int join_pp_impl(gf_ctx* ctx, const gf_grid* ugrid, const gf_grid* qgrid,
     const int64_t v = std::atoll(e);
     if (v >= (block_chunks ? 4096 : 64) && v <= (1 << 20) && (v & (v - 1)) == 0) chunk = v;
   }
-  size_t o_spill = ar.take<uint64_t>(rowpath ? ntails * chunk : 1);
+  // band probe regions: e_lim bounds the regions' total (hint x 1.125 + 1024 per block, at least
+  // cap), the spill holds the regions past cap plus an overflow area of 1/16 of the hint
+  const double t_hint = ppp * (double)no;
+  const uint64_t ucap = pairs ? (uint64_t)std::max<int64_t>(cap, 0) : 0;
+  const uint64_t e_lim = std::max<uint64_t>(ucap, (uint64_t)(1.125 * t_hint) + (uint64_t)probe_blocks * 1024);
+  const uint64_t spill_cap = band ? (ucap == 0 ? 0 : (e_lim - ucap) + std::max<uint64_t>(65536, (uint64_t)(t_hint / 16)))
+                                  : (uint64_t)(ntails * chunk);
+  size_t o_spill = ar.take<uint64_t>(rowpath ? std::max<uint64_t>(spill_cap, 1) : 1);
+  size_t o_reg = ar.take<uint64_t>(probe_blocks + 1), o_rlen = ar.take<uint64_t>(probe_blocks);
+  size_t o_bcnt = ar.take<uint64_t>(probe_blocks), o_bsl = ar.take<uint64_t>(probe_blocks);
   size_t o_tb = ar.take<uint64_t>(nwaves), o_tf = ar.take<uint32_t>(nwaves);
   size_t o_hs = ar.take<uint64_t>(nwaves + 1), o_hp = ar.take<uint64_t>(nwaves + 2);
   size_t o_ss = ar.take<uint64_t>(nwaves + 2), o_sp = ar.take<uint64_t>(nwaves + 3), o_fc = ar.take<uint32_t>(2);
@@ -1927,11 +1941,28 @@ static int join_pp_impl(gf_ctx* ctx, const gf_grid* ugrid, const gf_grid* qgrid,
     o.aligned = ((uintptr_t)pairs & 7) == 0;
     o.chunk = (uint32_t)chunk;
     o.spill = (uint2*)(base + o_spill);
-    o.spill_cap = (uint64_t)(ntails * chunk);
+    o.spill_cap = spill_cap;
+    if (band) {
+      if (!ctx->join_hist) {  // zero: no history (the first call's regions come from ppp)
+        GF_HIP_CHECK(ctx, hipMalloc(&ctx->join_hist, 2 * sizeof(uint64_t) * (size_t)probe_blocks));
+        GF_HIP_CHECK(ctx, hipMemsetAsync(ctx->join_hist, 0, 2 * sizeof(uint64_t) * (size_t)probe_blocks, s));
+        GF_HIP_CHECK(ctx, hipMalloc(&ctx->join_ovf, sizeof(unsigned long long)));
+        GF_HIP_CHECK(ctx, hipMemsetAsync(ctx->join_ovf, 0, sizeof(unsigned long long), s));
+      }
+      o.regions = 1;
+      o.reg_off = (uint64_t*)(base + o_reg);
+      o.reg_len = (uint64_t*)(base + o_rlen);
+      o.bcount = (uint64_t*)(base + o_bcnt);
+      o.bslice = (uint64_t*)(base + o_bsl);
+      o.hist = ctx->join_hist;
+      o.ovf = ctx->join_ovf;
+      o.e_lim = e_lim;
+      o.ppp = ppp;
+    }
     o.gctr = ctx->join_gctr;
     o.tail_base = (uint64_t*)(base + o_tb);
     o.tail_fill = U32(o_tf);
-    o.nwaves = (uint32_t)ntails;
+    o.nwaves = (uint32_t)(band ? probe_blocks : ntails);  // tails: the probe's waves, or its blocks / regions
     o.block_chunks = block_chunks;
     j.f = f; j.fs = (double)f / ugrid->cellLength;
     j.lds_budget = join_probe_budget(nq, qn, c, f);
@@ -1945,7 +1976,9 @@ static int join_pp_impl(gf_ctx* ctx, const gf_grid* ugrid, const gf_grid* qgrid,
     ctx->expand_base += (unsigned long long)scan1_blocks(qmat + mat);
     GF_HIP_CHECK(ctx, launch_join_rows(ctx, j, q, 1));
     GF_HIP_CHECK(ctx, launch_join_rows(ctx, j, q, 2));
-    if (stream) {
+    if (band) {
+      GF_HIP_CHECK(ctx, launch_join_band(ctx, j, (int)probe_blocks));  // nwaves: 16 per block, as the row probe
+    } else if (stream) {
       j.out.nwaves = (uint32_t)nwaves;  // the stream grid: kBlock-thread blocks, same wave count
       j.out.block_chunks = 0;
       GF_HIP_CHECK(ctx, launch_join_stream(ctx, j));

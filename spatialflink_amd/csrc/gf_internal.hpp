@@ -49,6 +49,8 @@ struct gf_ctx {
   uint32_t expand_epoch = 0;
   unsigned long long* join_gctr = nullptr;  // row-bucketed join: reserved output positions (zero between calls)
   unsigned long long* join_hint = nullptr;  // mapped pinned: the pair count of the last join (async too)
+  uint64_t* join_hist = nullptr;            // band probe: the last join's pairs | points per block ([2 * blocks], zero: none)
+  unsigned long long* join_ovf = nullptr;   // band probe: overflow counter (zero between calls)
   int64_t join_hint_no = 0;                 // ordinary points of that join
 };
 
@@ -564,6 +566,20 @@ struct JoinOut {
   uint32_t nwaves;           // tail entries: the probe's waves, or its blocks (block_chunks)
   int block_chunks;          // row probe: a block's waves share its chunks (LDS offsets, one
                              // global atomic per chunk); tails per block
+  // Band probe REGIONS (k_join.hip): block b owns positions [reg_off[b], reg_off[b] + reg_len[b])
+  // and fills them through an LDS cursor (no global atomic); pairs beyond its region go to the
+  // dense overflow area [E, E + *ovf) (E = reg_off[G]; one atomic per overflowing flush).  The
+  // regions come from the last call's pairs per point of every block (hist), scaled down to e_lim
+  // when they would exceed it; the fix-up moves the pairs above T into the regions' unused tails.
+  int regions;
+  uint64_t* reg_off;         // [G + 1] written by the probe's blocks
+  uint64_t* reg_len;         // [G]
+  uint64_t* bcount;          // [G] this call's pairs per block
+  uint64_t* bslice;          // [G] this call's ordinary points per block
+  uint64_t* hist;            // [2G] persistent: the last call's pairs | points per block (zero: none)
+  unsigned long long* ovf;   // persistent overflow counter (the fix-up resets it)
+  uint64_t e_lim;            // the regions' total never exceeds it (cap + spill covers it)
+  double ppp;                // pairs per point when there is no history
 };
 struct JoinRowArgs {
   const double* ox;
@@ -624,6 +640,7 @@ struct JoinFixup {
 };
 hipError_t launch_join_fixup(gf_ctx* ctx, const JoinFixup& f);
 hipError_t launch_join_stream(gf_ctx* ctx, const JoinRowArgs& a);
+hipError_t launch_join_band(gf_ctx* ctx, const JoinRowArgs& a, int blocks);  // fine path
 constexpr int kJoinReg = 3;  // pairs per ordinary point kept in registers by the probe
 // LDS bytes of one staged query row with m points: u16 bucket offsets, xy
 __host__ __device__ inline size_t join_row_lds_bytes(int64_t W, uint32_t m) {

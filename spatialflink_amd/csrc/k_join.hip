@@ -429,12 +429,16 @@ __device__ __forceinline__ uint32_t join_block_scan(uint32_t v, uint32_t* total,
 // the ordinary side's row starts (row_off[j] = M_scan[j][0], row_off[rows] = the total), tasks
 // per row (ceil(row / kJoinTask)) and their exclusive scan task_off[0..rows]; it also zeroes
 // the overflow count the probe accumulates.
-__global__ __launch_bounds__(kScatThreads) void join_sort_finish_kernel(JoinRowArgs a, JoinQueryArgs q) {
+// 256-thread blocks: ~1000 query points per row, and all qn + 3 blocks resident at once
+// (five per CU by the LDS histogram) -- with 1024-thread blocks two rounds of latency-bound
+// blocks took 34 us for 1M points
+constexpr int kSortThreads = 256;
+__global__ __launch_bounds__(kSortThreads) void join_sort_finish_kernel(JoinRowArgs a, JoinQueryArgs q) {
   __shared__ uint32_t h[kRowMax];
-  __shared__ uint32_t ws[kScatThreads / 64];
+  __shared__ uint32_t ws[kSortThreads / 64];
   const int32_t W = q.qn + 2;
   if ((int)blockIdx.x == W) {
-    const int nr = a.nrows, per = (nr + kScatThreads - 1) / kScatThreads, j0 = threadIdx.x * per;
+    const int nr = a.nrows, per = (nr + kSortThreads - 1) / kSortThreads, j0 = threadIdx.x * per;
     const uint32_t* Ms = a.row_mat_scan;
     const size_t nc = (size_t)kHistSplit * a.nblk, tot_idx = (size_t)nr * nc;
     auto rows_at = [&](int j, uint32_t& b, uint32_t& e) {
@@ -449,7 +453,7 @@ __global__ __launch_bounds__(kScatThreads) void join_sort_finish_kernel(JoinRowA
       run += (e - b + kJoinTask - 1) / kJoinTask;
     }
     uint32_t total;
-    uint32_t before = join_block_scan<kScatThreads>(run, &total, ws);
+    uint32_t before = join_block_scan<kSortThreads>(run, &total, ws);
     for (int j = j0; j < j0 + per && j < nr; ++j) {
       uint32_t b, e;
       rows_at(j, b, e);
@@ -472,26 +476,26 @@ __global__ __launch_bounds__(kScatThreads) void join_sort_finish_kernel(JoinRowA
     const uint32_t k = join_fine_key(q, v.x, v.y, cx, cy);
     return k - (uint32_t)ky * (uint32_t)q.f * fH;  // relative to the row's first sub-row
   };
-  for (int j = threadIdx.x; j < H; j += kScatThreads) h[j] = 0u;
+  for (int j = threadIdx.x; j < H; j += kSortThreads) h[j] = 0u;
   __syncthreads();
-  for (uint32_t i0 = rb + threadIdx.x; i0 < re; i0 += kScatThreads * 4) {
+  for (uint32_t i0 = rb + threadIdx.x; i0 < re; i0 += kSortThreads * 4) {
     double2 v[4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) v[u] = txy[i0 + u * kScatThreads < re ? i0 + u * kScatThreads : rb];
+    for (int u = 0; u < 4; ++u) v[u] = txy[i0 + u * kSortThreads < re ? i0 + u * kSortThreads : rb];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      if (i0 + u * kScatThreads >= re) continue;
+      if (i0 + u * kSortThreads >= re) continue;
       int32_t cx, cy;
       atomicAdd(&h[key_of(v[u], cx, cy)], 1u);
     }
   }
   __syncthreads();
   {  // exclusive scan of h[0..H) in place (a contiguous span of keys per thread)
-    const int per = (H + kScatThreads - 1) / kScatThreads, j0 = threadIdx.x * per;
+    const int per = (H + kSortThreads - 1) / kSortThreads, j0 = threadIdx.x * per;
     uint32_t run = 0;
     for (int j = j0; j < j0 + per && j < H; ++j) run += h[j];
     uint32_t total;
-    uint32_t before = join_block_scan<kScatThreads>(run, &total, ws);
+    uint32_t before = join_block_scan<kSortThreads>(run, &total, ws);
     for (int j = j0; j < j0 + per && j < H; ++j) {
       const uint32_t c = h[j];
       h[j] = rb + before;  // the key's cursor (absolute position)
@@ -499,27 +503,29 @@ __global__ __launch_bounds__(kScatThreads) void join_sort_finish_kernel(JoinRowA
     }
   }
   __syncthreads();
-  for (int j = threadIdx.x; j < H; j += kScatThreads) q.q_off[(size_t)ky * H + j] = h[j];
+  for (int j = threadIdx.x; j < H; j += kSortThreads) q.q_off[(size_t)ky * H + j] = h[j];
   if (ky == W - 1 && threadIdx.x == 0) q.q_off[(size_t)W * H] = re;
   __syncthreads();
-  for (uint32_t i0 = rb + threadIdx.x; i0 < re; i0 += kScatThreads * 4) {
+  for (uint32_t i0 = rb + threadIdx.x; i0 < re; i0 += kSortThreads * 4) {
     double2 v[4];
     uint32_t ix[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      const uint32_t i = i0 + u * kScatThreads < re ? i0 + u * kScatThreads : rb;
+      const uint32_t i = i0 + u * kSortThreads < re ? i0 + u * kSortThreads : rb;
       v[u] = txy[i];
       ix[u] = q.tidx[i];
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      if (i0 + u * kScatThreads >= re) continue;
+      if (i0 + u * kSortThreads >= re) continue;
       int32_t cx, cy;
       const uint32_t pos = atomicAdd(&h[key_of(v[u], cx, cy)], 1u);
       q.sqx[pos] = v[u].x;
       q.sqy[pos] = v[u].y;
-      q.sqcx[pos] = cx;
-      q.sqcy[pos] = cy;
+      if (q.f == 1) {  // true cells: only the cell path's clamped-bucket check reads them
+        q.sqcx[pos] = cx;
+        q.sqcy[pos] = cy;
+      }
       q.sqidx[pos] = ix[u];
     }
   }
@@ -1248,6 +1254,451 @@ hipError_t launch_join_stream(gf_ctx* ctx, const JoinRowArgs& a) {
   return hipGetLastError();
 }
 
+// ---- band probe (the fine path's default) ---------------------------------------------------
+// Block b takes an equal slice of the row-bucketed ordinary points (slices of one XCD are
+// consecutive: neighbouring rows share query sub-rows in its L2).  A slice crosses ~2-3 rows;
+// per row segment the block stages the row's query BAND -- the f + 2 sub-rows around the row:
+// u16 sub-column offsets (absolute staged slots), xy and query indices -- in LDS, then streams
+// the segment's points in bucket order: coalesced 16-B + 4-B loads, two points per lane per
+// wave-step with the next step in flight, no per-task sort (the row probe's sorted lanes gathered
+// their points from global memory one wave-step at a time and paid a histogram / scan / scatter
+// per 8192-point task).  Each lane tests the 3 x 3 sub-cells around its own (see the fine path
+// above) out of LDS.  A band larger than the staging budget (clustered input) is staged in
+// sub-column WINDOWS [c0, c1) -- the query points of sub-columns [c0 - 1, c1 + 1) of every band
+// sub-row -- and the segment is streamed once per window, each lane working only in the window of
+// its sub-column; a window that cannot hold even one sub-column reads that sub-column's
+// candidates from global memory.
+// Pairs: the wave's LDS buffer (ordinary index, staged slot | global index), written out between
+// wave-steps into the block's REGION of the output (JoinOut.regions): one LDS atomic per flush,
+// no device atomic unless the region is full (then the dense overflow area).  Per-wave output
+// chunks cost one device atomic each on ONE counter: ~20K of them serialised at the memory side
+// (the row probe: 240 us with block chunks, 361 us with wave chunks).
+constexpr int kBandThreads = 1024, kBandWaves = kBandThreads / 64;
+constexpr int kBandBuf = 384;        // pairs per wave buffer (a wave-step's pairs normally fit)
+constexpr int kBandRound = 4;        // candidates per lane per walk round
+constexpr int kBandMaxSub = 6;       // staged sub-rows f + 2 (f <= 4)
+constexpr uint32_t kBandGlobal = 0x80000000u;  // buffer entry: a global sorted query index
+struct BandHdr {
+  int32_t row;
+  uint32_t c1;           // the window's end (wave 0)
+  uint32_t m;            // staged query points
+  uint32_t gstart[kBandMaxSub], lstart[kBandMaxSub + 1];  // per band sub-row: first global / staged point
+  unsigned long long fill;  // the block's pairs so far: its region cursor
+  uint64_t roff, rlen, E;   // the block's region, the regions' end (overflow area start)
+  uint64_t wsum[kBandWaves];
+};
+constexpr int kBandHdrBytes = (int)((sizeof(BandHdr) + 15) / 16 * 16);
+constexpr size_t kBandLds = 160 * 1024;
+constexpr size_t kBandStage = kBandLds - kBandHdrBytes - (size_t)kBandWaves * kBandBuf * 8;
+// staged offset entries per band sub-row for window [c0, c1): sub-columns c0 - 1 .. c1 + 1
+__device__ __forceinline__ uint32_t band_ncol(uint32_t c0, uint32_t c1) { return (c1 - c0 + 3 + 7) & ~7u; }
+__device__ __forceinline__ uint32_t band_off_bytes(int32_t f, uint32_t c0, uint32_t c1) {
+  return (uint32_t)(f + 2) * band_ncol(c0, c1) * 2u;
+}
+// the slice of the bucketed points block `blk` of G takes (G % 8 == 0, host): XCD x = blk % 8
+// holds the consecutive slices [x G/8, (x + 1) G/8)
+__device__ __forceinline__ void band_slice(uint32_t N, uint32_t G, uint32_t blk, uint32_t& p0, uint32_t& p1) {
+  const uint32_t s = (blk & 7u) * (G >> 3) + (blk >> 3);
+  p0 = (uint32_t)((uint64_t)N * s / G);
+  p1 = (uint32_t)((uint64_t)N * (s + 1) / G);
+}
+// block-wide exclusive scan of one u64 per thread (kBandThreads), *total = the sum
+__device__ __forceinline__ uint64_t band_scan(uint64_t v, uint64_t* total, uint64_t* ws) {
+  const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  uint64_t inc = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint64_t t = __shfl_up(inc, o, 64);
+    if (lane >= (uint32_t)o) inc += t;
+  }
+  if (lane == 63) ws[wid] = inc;
+  __syncthreads();
+  uint64_t before = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < kBandWaves; ++w) {
+    before += w < (int)wid ? ws[w] : 0ull;
+    tot += ws[w];
+  }
+  *total = tot;
+  __syncthreads();
+  return before + inc - v;
+}
+// Every block derives all G regions the same way (so no launch is needed for them): block t's
+// pairs per point from the last call (hist; none: the host's estimate) x its slice now, + 1/16
+// + 512; scaled down so that the total stays <= e_lim.  Block 0 records them for the fix-up.
+__device__ __forceinline__ void band_regions(const JoinOut& o, uint32_t N, BandHdr& hd) {
+  const uint32_t G = gridDim.x, t = threadIdx.x;
+  uint64_t hp = 0, hn = 0, slice = 0;
+  if (t < G) {
+    uint32_t p0, p1;
+    band_slice(N, G, t, p0, p1);
+    slice = p1 - p0;
+    hp = o.hist[t];
+    hn = o.hist[G + t];
+  }
+  uint64_t HP, HN;
+  band_scan(hp, &HP, hd.wsum);
+  band_scan(hn, &HN, hd.wsum);
+  const double gppp = HN > 0 ? (double)HP / (double)HN : o.ppp;
+  uint64_t est = 0;
+  if (t < G) est = (uint64_t)ceil((hn > 0 ? (double)hp / (double)hn : gppp) * (double)slice * 1.0625) + 512;
+  uint64_t E;
+  uint64_t off = band_scan(est, &E, hd.wsum);
+  if (E > o.e_lim) {  // floor(est * s) with s < e_lim / E: the sum stays <= e_lim
+    const double sc = (double)(o.e_lim > (uint64_t)G + 1 ? o.e_lim - G - 1 : 0) / (double)E;
+    est = t < G ? (uint64_t)((double)est * sc) : 0;
+    off = band_scan(est, &E, hd.wsum);
+  }
+  if (t == blockIdx.x) {
+    hd.roff = off;
+    hd.rlen = est;
+  }
+  if (t == 0) {
+    hd.E = E;
+    hd.fill = 0ull;
+  }
+  if (blockIdx.x == 0 && t < G) {
+    o.reg_off[t] = off;
+    o.reg_len[t] = est;
+    if (t == G - 1) o.reg_off[G] = E;
+  }
+  __syncthreads();
+}
+// The wave's cnt pairs get(0 .. cnt) at the block's next region positions; those past the region
+// go to the overflow area (one device atomic for the wave's excess).
+template <class Get>
+__device__ __forceinline__ void band_emit(const JoinOut& o, BandHdr& hd, uint32_t cnt, Get get) {
+  const uint32_t lane = threadIdx.x & 63;
+  unsigned long long off = 0;
+  if (lane == 0) off = atomicAdd(&hd.fill, (unsigned long long)cnt);
+  off = join_uni64(off);
+  const uint64_t R = hd.rlen, O = hd.roff, split = off > R ? off : R;
+  uint64_t ob = 0;
+  if (off + cnt > R) {  // wave-uniform
+    unsigned long long b = 0;
+    if (lane == 0) b = atomicAdd(o.ovf, (unsigned long long)(off + cnt - split));
+    ob = hd.E + join_uni64(b);
+  }
+  for (uint32_t i = lane; i < cnt; i += 64) {
+    const uint64_t p = off + i;
+    join_vstore(o, p < R ? O + p : ob + (p - split), get(i));
+  }
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kBandThreads) void join_band_probe_kernel(JoinRowArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char lds_base[];
+  BandHdr& hd = *reinterpret_cast<BandHdr*>(lds_base);
+  char* const stg = lds_base + kBandHdrBytes + (size_t)kBandWaves * kBandBuf * 8;
+  const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  uint2* const buf = reinterpret_cast<uint2*>(lds_base + kBandHdrBytes) + wid * kBandBuf;
+  uint32_t cnt = 0;  // wave-uniform
+  const int32_t f = a.f, qn = a.qn;
+  const int64_t fW = (int64_t)f * (qn + 2);
+  const uint32_t cbeg = (uint32_t)f, cend = (uint32_t)f * (uint32_t)(qn + 1);  // in-grid sub-columns
+  const uint32_t N = a.row_off[qn];
+  band_regions(a.out, N, hd);
+  uint32_t pos, P1;
+  band_slice(N, gridDim.x, blockIdx.x, pos, P1);
+  const uint32_t P0 = pos;
+  while (pos < P1) {  // block-uniform: one row segment
+    for (int j = threadIdx.x; j < qn; j += kBandThreads)
+      if (a.row_off[j] <= pos && pos < a.row_off[j + 1]) hd.row = j;
+    __syncthreads();
+    const int32_t cy = hd.row;
+    const uint32_t sb = pos, se = a.row_off[cy + 1] < P1 ? a.row_off[cy + 1] : P1;
+    const int64_t fy0 = (int64_t)f * (cy + 1) - 1;  // the band's first sub-row
+    for (uint32_t c0 = cbeg; c0 < cend;) {          // block-uniform: one window
+      if (wid == 0) {
+        // the window's end: the largest c1 <= cend whose staged bytes fit (64-way search)
+        auto cost = [&](uint32_t c1) {
+          uint32_t m = 0;
+          for (int s = 0; s < f + 2; ++s) {
+            const uint32_t* qo = a.q_off + (fy0 + s) * fW;
+            m += qo[c1 + 1] - qo[c0 - 1];
+          }
+          return (uint64_t)band_off_bytes(f, c0, c1) + 20ull * m;
+        };
+        uint32_t lo = c0, hi = cend;
+        if (cost(cend) <= kBandStage) {
+          lo = cend;
+        } else {
+          while (hi - lo > 1) {  // cost(lo) fits (lo == c0: nothing), cost(hi) does not
+            const uint32_t step = (hi - lo + 63) / 64, c = lo + (lane + 1) * step;
+            const uint64_t ok = __ballot(c < hi && cost(c) <= kBandStage);
+            if (ok == 0) {
+              hi = lo + step < hi ? lo + step : hi;
+            } else {
+              const uint32_t L = 63u - (uint32_t)__builtin_clzll(ok), lo2 = lo + (L + 1) * step;
+              hi = lo + (L + 2) * step < hi ? lo + (L + 2) * step : hi;
+              lo = lo2;
+            }
+          }
+        }
+        if (lane == 0) {
+          hd.c1 = lo;  // == c0: not even one sub-column fits -- [c0, c0 + 1) from global memory
+          uint32_t m = 0;
+          if (lo > c0) {
+            for (int s = 0; s < f + 2; ++s) {
+              const uint32_t* qo = a.q_off + (fy0 + s) * fW;
+              hd.gstart[s] = qo[c0 - 1];
+              hd.lstart[s] = m;
+              m += qo[lo + 1] - qo[c0 - 1];
+            }
+          }
+          hd.lstart[f + 2] = m;
+          hd.m = m;
+        }
+      }
+      __syncthreads();
+      const bool lds = hd.c1 > c0;
+      const uint32_t c1 = lds ? hd.c1 : c0 + 1, m = hd.m, ncol = band_ncol(c0, c1);
+      uint16_t* const lo16 = reinterpret_cast<uint16_t*>(stg);
+      double2* const lxy = reinterpret_cast<double2*>(stg + ((band_off_bytes(f, c0, c1) + 15u) & ~15u));
+      uint32_t* const lq = reinterpret_cast<uint32_t*>(lxy + m);
+      if (lds) {  // stage: offsets (absolute staged slots), xy, query indices -- loads batched
+        const uint32_t nent = (uint32_t)(f + 2) * ncol, span = c1 - c0 + 3;
+        for (uint32_t t0 = threadIdx.x; t0 < nent; t0 += 8 * kBandThreads) {
+          uint32_t v[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            const uint32_t t = t0 + u * kBandThreads, s = t / ncol, j = t - s * ncol;
+            v[u] = t < nent && j < span ? a.q_off[(fy0 + s) * fW + c0 - 1 + j] - hd.gstart[s] + hd.lstart[s] : 0u;
+          }
+#pragma unroll
+          for (int u = 0; u < 8; ++u)
+            if (t0 + u * kBandThreads < nent) lo16[t0 + u * kBandThreads] = (uint16_t)v[u];
+        }
+        for (uint32_t t0 = threadIdx.x; t0 < m; t0 += 4 * kBandThreads) {
+          double x[4], y[4];
+          uint32_t qi[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const uint32_t t = t0 + u * kBandThreads < m ? t0 + u * kBandThreads : t0;
+            int s = 0;
+            while (t >= hd.lstart[s + 1]) ++s;
+            const uint32_t g = hd.gstart[s] + (t - hd.lstart[s]);
+            x[u] = a.sqx[g];
+            y[u] = a.sqy[g];
+            qi[u] = a.sqidx[g];
+          }
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const uint32_t t = t0 + u * kBandThreads;
+            if (t < m) {
+              lxy[t] = make_double2(x[u], y[u]);
+              lq[t] = qi[u];
+            }
+          }
+        }
+      }
+      __syncthreads();
+      auto flush = [&]() {
+        band_emit(a.out, hd, cnt, [&](uint32_t i) {
+          const uint2 v = buf[i];
+          return make_uint2(v.x, v.y & kBandGlobal ? a.sqidx[v.y & ~kBandGlobal] : lq[v.y]);
+        });
+        cnt = 0;
+      };
+      // DENSE window (clustered input: ~> 12 candidates per point): each wave-step's 64 points are
+      // sorted by (sub-column, sub-row) across the wave first (bitonic over 64 lanes in
+      // registers), so neighbouring lanes share most candidates -- LDS broadcast reads, and
+      // similar run lengths (the rounds are the longest run of the wave).  Not worth its ~300
+      // instructions at ~3 candidates per point.
+      const bool dense = lds && (uint64_t)m * 9u > 12ull * (uint64_t)(f + 2) * (c1 - c0 + 2);
+      // one point: its 3 x 3 sub-cell neighbourhood, kBandRound candidates per round
+      auto probe = [&](double px, double py, uint32_t pidx, bool valid) {
+        int32_t cx = cell_index(px, a.u_minX, a.u_cl);
+        bool in = valid && cx >= 0 && cx < qn;  // outside the grid's columns: no key matches
+        int32_t col = in ? f * (cx + 1) + join_sub(px, a.u_minX, a.u_cl, cx, a.fs, f) : 0;
+        int32_t sub = join_sub(py, a.u_minY, a.u_cl, cy, a.fs, f);
+        in = in && (uint32_t)col >= c0 && (uint32_t)col < c1;
+        if (dense) {  // wave-uniform
+          uint32_t key = in ? (uint32_t)(col - (int32_t)c0) << 3 | (uint32_t)sub : 0xFFFFFFFFu, src = lane;
+#pragma unroll
+          for (int size = 2; size <= 64; size <<= 1)
+#pragma unroll
+            for (int stride = size >> 1; stride > 0; stride >>= 1) {
+              const uint32_t ko = __shfl_xor(key, stride, 64), so = __shfl_xor(src, stride, 64);
+              const bool asc = (lane & (uint32_t)size) == 0 || size == 64, lower = (lane & (uint32_t)stride) == 0;
+              const bool less = ko < key || (ko == key && so < src);
+              if (lower == asc ? less : !less && !(ko == key && so == src)) {
+                key = ko;
+                src = so;
+              }
+            }
+          px = __shfl(px, (int)src, 64);
+          py = __shfl(py, (int)src, 64);
+          pidx = __shfl(pidx, (int)src, 64);
+          col = __shfl(col, (int)src, 64);
+          sub = __shfl(sub, (int)src, 64);
+          in = key != 0xFFFFFFFFu;
+        }
+        uint32_t b[3], e[3];
+        if (lds) {  // (a lane outside the window reads in-bounds entries, masked)
+          const uint16_t* lo = lo16 + (in ? sub * ncol + (col - (int32_t)c0) : 0);
+#pragma unroll
+          for (int k = 0; k < 3; ++k) {
+            b[k] = in ? lo[k * ncol] : 0u;
+            e[k] = in ? lo[k * ncol + 3] : 0u;
+          }
+        } else {
+          const uint32_t* qo = a.q_off + (in ? (fy0 + sub) * fW + col : fy0 * fW + c0);
+#pragma unroll
+          for (int k = 0; k < 3; ++k) {
+            b[k] = in ? qo[k * fW - 1] : 0u;
+            e[k] = in ? qo[k * fW + 2] : 0u;
+          }
+        }
+        // the three runs walked as one sequence (ballot exit); a full buffer is written out
+        // between rounds
+        const uint32_t L0 = e[0] - b[0], L1 = L0 + (e[1] - b[1]), L2 = L1 + (e[2] - b[2]);
+        const uint32_t d0 = b[0], d1 = b[1] - L0, d2 = b[2] - L1;
+        uint32_t k = 0;
+        for (;;) {
+          bool full = false;
+          for (; __ballot(k < L2) != 0; k += kBandRound) {
+            if (cnt > (uint32_t)(kBandBuf - 64 * kBandRound)) {
+              full = true;
+              break;
+            }
+            uint32_t t[kBandRound];
+            double2 v[kBandRound];
+#pragma unroll
+            for (int i = 0; i < kBandRound; ++i) {
+              const uint32_t kk = k + i;
+              t[i] = kk < L2 ? kk + (kk < L0 ? d0 : (kk < L1 ? d1 : d2)) : (lds ? 0u : b[0]);
+            }
+#pragma unroll
+            for (int i = 0; i < kBandRound; ++i) {
+              if (lds) {
+                v[i] = lxy[t[i]];  // a finished lane reads slot 0 (staged: m > 0 when any lane runs)
+              } else {
+                v[i] = make_double2(0.0, 0.0);
+                if (k + i < L2) v[i] = make_double2(a.sqx[t[i]], a.sqy[t[i]]);
+              }
+            }
+#pragma unroll
+            for (int i = 0; i < kBandRound; ++i) {
+              const double dx = px - v[i].x, dy = py - v[i].y;
+              bool ok;
+              if constexpr (MODE == 0) ok = dx * dx + dy * dy <= a.s_r;
+              else ok = a.metric == 0 ? dx * dx + dy * dy <= a.s_r : fdlibm_hypot(dx, dy) <= a.r;
+              const bool hit = k + i < L2 && ok;
+              const uint64_t hm = __ballot(hit);
+              if (hit)
+                buf[cnt + __builtin_amdgcn_mbcnt_hi((uint32_t)(hm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)hm, 0u))] =
+                    make_uint2(pidx, lds ? t[i] : (t[i] | kBandGlobal));
+              cnt += (uint32_t)__popcll(hm);
+            }
+          }
+          if (!full) break;
+          flush();
+        }
+      };
+      // the segment, 128 consecutive points per wave-step (two per lane); past the end a lane
+      // re-reads the segment's first point (always present) and is masked
+      struct Pt {
+        double2 v[2];
+        uint32_t idx[2];
+      };
+      auto fetch = [&](uint32_t s0) {
+        Pt p;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const uint32_t i = s0 + u * 64 + lane, k = i < se ? i : sb;
+          p.v[u] = reinterpret_cast<const double2*>(a.soxy)[k];
+          p.idx[u] = a.soidx[k];
+        }
+        return p;
+      };
+      Pt cur = fetch(sb + wid * 128);
+      for (uint32_t s0 = sb + wid * 128; s0 < se; s0 += kBandWaves * 128) {  // wave-uniform
+        const Pt nxt = fetch(s0 + kBandWaves * 128);
+        probe(cur.v[0].x, cur.v[0].y, cur.idx[0], s0 + lane < se);
+        probe(cur.v[1].x, cur.v[1].y, cur.idx[1], s0 + 64 + lane < se);
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): nxt is in registers (before any store)
+        if (cnt > (uint32_t)(kBandBuf - 64 * kBandRound)) flush();
+        cur = nxt;
+      }
+      if (cnt > 0) flush();  // staged slots change with the next window
+      __syncthreads();
+      c0 = c1;
+    }
+    pos = se;
+  }
+  __syncthreads();  // every wave's pairs are counted
+  if (threadIdx.x == 0) {
+    a.out.bcount[blockIdx.x] = hd.fill;
+    a.out.bslice[blockIdx.x] = P1 - P0;
+  }
+}
+
+hipError_t launch_join_band(gf_ctx* ctx, const JoinRowArgs& a, int blocks) {
+  KTimer t(ctx, GF_K_JOIN_PROBE);
+  if (!a.approx && a.metric == 0)
+    hipLaunchKernelGGL(join_band_probe_kernel<0>, dim3(blocks), dim3(kBandThreads), kBandLds, ctx->stream, a);
+  else
+    hipLaunchKernelGGL(join_band_probe_kernel<1>, dim3(blocks), dim3(kBandThreads), kBandLds, ctx->stream, a);
+  return hipGetLastError();
+}
+
+// The regions' fix-up (one block, G <= 1023 regions): T = the pairs; region t keeps
+// [off_t, off_t + min(n_t, len_t)), its unused tail is a hole, and the overflow area
+// [E, E + ovf) is the last run; holes below T and stored runs at or above T (both already in
+// position order -- no sort) with their exclusive prefixes for join_fixup_copy_kernel.  Also:
+// the history (pairs, points per block) for the next call's regions, and the overflow reset.
+// A pair stored past cap + spill_cap was dropped: when T <= cap that is reported as T = cap + 1
+// (GF_ERR_CAPACITY; the caller's retry gets regions sized from this call's exact counts).
+__global__ __launch_bounds__(kBandThreads) void join_region_prep_kernel(JoinFixup f) {
+  __shared__ uint64_t ws[kBandWaves];
+  const JoinOut& o = f.o;
+  const uint32_t G = o.nwaves, t = threadIdx.x;
+  uint64_t O = 0, R = 0, n = 0;
+  if (t < G) {
+    O = o.reg_off[t];
+    R = o.reg_len[t];
+    n = o.bcount[t];
+  }
+  const uint64_t u = n < R ? n : R;
+  uint64_t T;
+  band_scan(n, &T, ws);
+  const uint64_t E = o.reg_off[G], ov = *o.ovf;
+  const bool lost = E + ov > o.cap + o.spill_cap;
+  const bool fits = T <= o.cap && !lost;
+  uint64_t hl = 0, hs = 0, sl = 0, ss = 0;
+  if (t < G) {
+    hs = O + u;
+    hl = hs < T ? (O + R < T ? O + R : T) - hs : 0;
+    ss = O > T ? O : T;
+    sl = O + u > ss ? O + u - ss : 0;
+  } else if (t == G) {
+    ss = E > T ? E : T;
+    sl = E + ov > ss ? E + ov - ss : 0;
+  }
+  uint64_t H, S;
+  const uint64_t hp = band_scan(hl, &H, ws), sp = band_scan(sl, &S, ws);
+  if (t < G) {
+    f.hole_start[t] = hs;
+    f.hole_pref[t] = hp;
+    o.hist[t] = n;
+    o.hist[G + t] = o.bslice[t];
+  }
+  if (t <= G) {
+    f.seg_start[t] = ss;
+    f.seg_pref[t] = sp;
+  }
+  if (t == 0) {
+    f.hole_pref[G] = H;
+    f.seg_pref[G + 1] = S;
+    f.counts[0] = fits ? G : 0u;
+    f.counts[1] = fits ? G + 1 : 0u;
+    *f.total = T <= o.cap && lost ? o.cap + 1 : T;
+    if (f.hint) *f.hint = T;
+    *o.ovf = 0ull;
+  }
+}
+
 // ---- the output fix-up ------------------------------------------------------------------------
 // (1) one block: the waves' last chunks sorted by position; their holes; T = G - the holes = the
 // pair count (written to *total; gctr reset to 0 for the next call); the holes below T and the
@@ -1367,22 +1818,37 @@ __device__ __forceinline__ uint32_t join_bsearch(const uint64_t* pref, uint32_t 
   }
   return lo;
 }
+// One block per hole (blocks >= the hole count exit): the hole's first source run by one
+// binary search, then each thread walks forward from it (a hole's range crosses few runs).  A
+// grid-stride loop with two binary searches per pair was latency-bound (17 us for ~1M pairs).
 __global__ __launch_bounds__(kBlock) void join_fixup_copy_kernel(JoinFixup f) {
   const uint32_t nh = f.counts[0], ns = f.counts[1];
   if (nh == 0 || ns == 0) return;
-  const uint64_t M = f.hole_pref[nh];
-  for (uint64_t k = (uint64_t)blockIdx.x * kBlock + threadIdx.x; k < M; k += (uint64_t)gridDim.x * kBlock) {
-    const uint32_t h = join_bsearch(f.hole_pref, nh, k), sg = join_bsearch(f.seg_pref, ns, k);
-    const uint64_t dst = f.hole_start[h] + (k - f.hole_pref[h]);
-    const uint64_t src = f.seg_start[sg] + (k - f.seg_pref[sg]);
-    join_store(f.o.pairs, f.o.aligned, dst, join_vload(f.o, src));
+  __shared__ uint32_t s_sg;
+  for (uint32_t h = blockIdx.x; h < nh; h += gridDim.x) {  // block-uniform
+    const uint64_t k0 = f.hole_pref[h], k1 = f.hole_pref[h + 1], d0 = f.hole_start[h];
+    if (threadIdx.x == 0) s_sg = join_bsearch(f.seg_pref, ns, k0);
+    __syncthreads();
+    const uint32_t sg0 = s_sg;
+    for (uint64_t k = k0 + threadIdx.x; k < k1; k += kBlock) {
+      uint32_t sg = sg0;
+      int steps = 0;
+      while (sg + 1 < ns && f.seg_pref[sg + 1] <= k && steps < 8) { ++sg; ++steps; }
+      if (steps == 8) sg = join_bsearch(f.seg_pref, ns, k);
+      const uint64_t src = f.seg_start[sg] + (k - f.seg_pref[sg]);
+      join_store(f.o.pairs, f.o.aligned, d0 + (k - k0), join_vload(f.o, src));
+    }
+    __syncthreads();
   }
 }
 
 hipError_t launch_join_fixup(gf_ctx* ctx, const JoinFixup& f) {
   KTimer t(ctx, GF_K_JOIN_COMPACT);
-  hipLaunchKernelGGL(join_fixup_prep_kernel, dim3(1), dim3(1024), 0, ctx->stream, f);
-  hipLaunchKernelGGL(join_fixup_copy_kernel, dim3(1024), dim3(kBlock), 0, ctx->stream, f);
+  if (f.o.regions)
+    hipLaunchKernelGGL(join_region_prep_kernel, dim3(1), dim3(kBandThreads), 0, ctx->stream, f);
+  else
+    hipLaunchKernelGGL(join_fixup_prep_kernel, dim3(1), dim3(1024), 0, ctx->stream, f);
+  hipLaunchKernelGGL(join_fixup_copy_kernel, dim3(f.o.nwaves), dim3(kBlock), 0, ctx->stream, f);
   return hipGetLastError();
 }
 
@@ -1408,7 +1874,7 @@ hipError_t launch_join_rows(gf_ctx* ctx, const JoinRowArgs& a, const JoinQueryAr
       break;
     }
     case 2:
-      hipLaunchKernelGGL(join_sort_finish_kernel, dim3((unsigned)(q.qn + 3)), dim3(kScatThreads), 0, s, a, q);
+      hipLaunchKernelGGL(join_sort_finish_kernel, dim3((unsigned)(q.qn + 3)), dim3(kSortThreads), 0, s, a, q);
       break;
     case 3: {
       KTimer t(ctx, GF_K_JOIN_PROBE);

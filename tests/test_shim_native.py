@@ -442,7 +442,10 @@ def test_csv_parse(shim, ctx, oracle_mod):
     np.testing.assert_array_equal(y.view(np.int64), ey.view(np.int64))
     np.testing.assert_array_equal(t, et)
     assert _decode(shim, ctx, o) == eo
+    # two more lines than the window (the cut line and the inserted one): room for them, so the
+    # bad line is reported, not GF_ERR_CAPACITY (the header: capacity is checked first)
     bad = text[:1000] + b"\n1,2,x,4\n" + text[1000:]
+    x, y, o, t = _cols(200_008)
     st = shim.shim_csv_parse(ctx, bad, len(bad), C.byref(sc), _a(x), _a(y), _a(o), _a(t), len(x), C.byref(n),
                              C.byref(bl), C.byref(bk))
     *_, ebl, ebk = oracle_mod.csv_parse(bad, ",", [2, 0, 3, 1])
