@@ -1870,21 +1870,18 @@ static int join_pp_impl(gf_ctx* ctx, const gf_grid* ugrid, const gf_grid* qgrid,
     const unsigned long long h = *(volatile unsigned long long*)ctx->join_hint;
     if (h > 0) ppp = (double)h / (double)ctx->join_hint_no;
   }
-  // block chunks (default): a probe block's waves share its chunks -- LDS offsets, one device
-  // atomic per chunk of ~1/4 of the block's expected pairs, tails (holes) per block.  Wave chunks
-  // (GF_JOIN_WAVE_CHUNKS=1, and the streaming experiment): one device atomic per wave chunk.
+  // output: the band probe fills per-block regions (JoinOut.regions); the row probe and the
+  // streaming experiment take per-wave chunks (one device atomic each, one hole per wave).
   // fine path: the band probe (k_join.hip) unless the row probe is asked for (A/B testing)
   const char* renv = std::getenv("GF_JOIN_ROWPROBE");
   const bool band = rowpath && f > 1 && !stream && !(renv && *renv == '1') && ctx->num_cus <= 1016;
-  const char* benv = std::getenv("GF_JOIN_BLOCK_CHUNKS");  // experiment (row probe only)
-  const bool block_chunks = benv && *benv == '1' && !stream && !band;
-  const int64_t ntails = block_chunks ? probe_blocks : nwaves;
-  int64_t chunk = block_chunks ? 4096 : 256;
-  while (chunk < (block_chunks ? (1 << 20) : 65536) && (double)chunk * ntails * (block_chunks ? 4 : 8) < ppp * (double)no)
+  const int64_t ntails = nwaves;
+  int64_t chunk = 256;
+  while (chunk < 65536 && (double)chunk * ntails * 8 < ppp * (double)no)
     chunk <<= 1;
   if (const char* e = std::getenv("GF_JOIN_CHUNK")) {  // testing / tuning: a fixed chunk (power of 2)
     const int64_t v = std::atoll(e);
-    if (v >= (block_chunks ? 4096 : 64) && v <= (1 << 20) && (v & (v - 1)) == 0) chunk = v;
+    if (v >= 64 && v <= 65536 && (v & (v - 1)) == 0) chunk = v;
   }
   // band probe regions: e_lim bounds the regions' total (hint x 1.125 + 1024 per block, at least
   // cap), the spill holds the regions past cap plus an overflow area of 1/16 of the hint
@@ -1946,8 +1943,8 @@ static int join_pp_impl(gf_ctx* ctx, const gf_grid* ugrid, const gf_grid* qgrid,
       if (!ctx->join_hist) {  // zero: no history (the first call's regions come from ppp)
         GF_HIP_CHECK(ctx, hipMalloc(&ctx->join_hist, 2 * sizeof(uint64_t) * (size_t)probe_blocks));
         GF_HIP_CHECK(ctx, hipMemsetAsync(ctx->join_hist, 0, 2 * sizeof(uint64_t) * (size_t)probe_blocks, s));
-        GF_HIP_CHECK(ctx, hipMalloc(&ctx->join_ovf, sizeof(unsigned long long)));
-        GF_HIP_CHECK(ctx, hipMemsetAsync(ctx->join_ovf, 0, sizeof(unsigned long long), s));
+        GF_HIP_CHECK(ctx, hipMalloc(&ctx->join_ovf, 2 * sizeof(unsigned long long)));  // overflow, ticket
+        GF_HIP_CHECK(ctx, hipMemsetAsync(ctx->join_ovf, 0, 2 * sizeof(unsigned long long), s));
       }
       o.regions = 1;
       o.reg_off = (uint64_t*)(base + o_reg);
@@ -1963,7 +1960,6 @@ static int join_pp_impl(gf_ctx* ctx, const gf_grid* ugrid, const gf_grid* qgrid,
     o.tail_base = (uint64_t*)(base + o_tb);
     o.tail_fill = U32(o_tf);
     o.nwaves = (uint32_t)(band ? probe_blocks : ntails);  // tails: the probe's waves, or its blocks / regions
-    o.block_chunks = block_chunks;
     j.f = f; j.fs = (double)f / ugrid->cellLength;
     j.lds_budget = join_probe_budget(nq, qn, c, f);
     // (1) row histograms of both sides, (2) one scan of both matrices, (3) write-combined row
@@ -1976,15 +1972,6 @@ static int join_pp_impl(gf_ctx* ctx, const gf_grid* ugrid, const gf_grid* qgrid,
     ctx->expand_base += (unsigned long long)scan1_blocks(qmat + mat);
     GF_HIP_CHECK(ctx, launch_join_rows(ctx, j, q, 1));
     GF_HIP_CHECK(ctx, launch_join_rows(ctx, j, q, 2));
-    if (band) {
-      GF_HIP_CHECK(ctx, launch_join_band(ctx, j, (int)probe_blocks));  // nwaves: 16 per block, as the row probe
-    } else if (stream) {
-      j.out.nwaves = (uint32_t)nwaves;  // the stream grid: kBlock-thread blocks, same wave count
-      j.out.block_chunks = 0;
-      GF_HIP_CHECK(ctx, launch_join_stream(ctx, j));
-    } else {
-      GF_HIP_CHECK(ctx, launch_join_rows(ctx, j, q, 3));
-    }
     JoinFixup fx{};
     fx.o = j.out;
     fx.total = total_out ? total_out : cnt2 + 1;
@@ -1992,6 +1979,17 @@ static int join_pp_impl(gf_ctx* ctx, const gf_grid* ugrid, const gf_grid* qgrid,
     fx.hole_start = (uint64_t*)(base + o_hs); fx.hole_pref = (uint64_t*)(base + o_hp);
     fx.seg_start = (uint64_t*)(base + o_ss); fx.seg_pref = (uint64_t*)(base + o_sp);
     fx.counts = U32(o_fc);
+    if (band) {  // its last block prepares the fix-up (fx)
+      j.fx = fx;
+      j.ticket = ctx->join_ovf + 1;
+      GF_HIP_CHECK(ctx, launch_join_band(ctx, j, (int)probe_blocks));
+    } else if (stream) {
+      j.out.nwaves = (uint32_t)nwaves;  // the stream grid: kBlock-thread blocks, same wave count
+      GF_HIP_CHECK(ctx, launch_join_stream(ctx, j));
+    } else {
+      GF_HIP_CHECK(ctx, launch_join_rows(ctx, j, q, 3));
+    }
+    fx.o = j.out;  // (the streaming experiment changed its wave count)
     GF_HIP_CHECK(ctx, launch_join_fixup(ctx, fx));
     if (total_out) {  // the caller reads *total_out stream-ordered
       ctx->join_async_done = 1;

@@ -563,9 +563,7 @@ struct JoinOut {
   unsigned long long* gctr;  // reserved positions (0 between calls: the fix-up resets it)
   uint64_t* tail_base;       // [nwaves] base of each wave's last chunk (~0: none)
   uint32_t* tail_fill;       // [nwaves]
-  uint32_t nwaves;           // tail entries: the probe's waves, or its blocks (block_chunks)
-  int block_chunks;          // row probe: a block's waves share its chunks (LDS offsets, one
-                             // global atomic per chunk); tails per block
+  uint32_t nwaves;           // tail entries: the probe's waves (regions: its blocks)
   // Band probe REGIONS (k_join.hip): block b owns positions [reg_off[b], reg_off[b] + reg_len[b])
   // and fills them through an LDS cursor (no global atomic); pairs beyond its region go to the
   // dense overflow area [E, E + *ovf) (E = reg_off[G]; one atomic per overflowing flush).  The
@@ -580,6 +578,17 @@ struct JoinOut {
   unsigned long long* ovf;   // persistent overflow counter (the fix-up resets it)
   uint64_t e_lim;            // the regions' total never exceeds it (cap + spill covers it)
   double ppp;                // pairs per point when there is no history
+};
+// The join's fix-up (k_join.hip): the pairs stored at positions >= T moved into the holes < T.
+struct JoinFixup {
+  JoinOut o;
+  unsigned long long* total;  // the pair count T (device or mapped pinned memory)
+  unsigned long long* hint;   // mapped pinned: T again, the next call's chunk-size hint
+  uint64_t* hole_start;       // [nwaves] holes below T, by position
+  uint64_t* hole_pref;        // [nwaves + 1] their exclusive prefix of lengths
+  uint64_t* seg_start;        // [nwaves + 1] stored runs in [T, G), by position
+  uint64_t* seg_pref;         // [nwaves + 2]
+  uint32_t* counts;           // [2] holes below T, runs above T
 };
 struct JoinRowArgs {
   const double* ox;
@@ -614,6 +623,10 @@ struct JoinRowArgs {
   // ((f*(qn+2))^2 + 1 entries); f == 1: q_off indexes cells as before
   int32_t f;
   double fs;                // f / cl
+  // band probe: its last block (ticket) computes the regions' fix-up (join_region_prep) --
+  // no separate launch; the copy kernel follows
+  JoinFixup fx;
+  unsigned long long* ticket;  // zero between calls (the last block resets it)
 };
 __device__ __forceinline__ void join_store(uint32_t* pairs, int aligned, uint64_t pos, uint2 v) {
   if (aligned) {
@@ -627,17 +640,6 @@ __device__ __forceinline__ uint2 join_load(const uint32_t* pairs, int aligned, u
   if (aligned) return reinterpret_cast<const uint2*>(pairs)[pos];
   return make_uint2(pairs[2 * pos], pairs[2 * pos + 1]);
 }
-// The join's fix-up (k_join.hip): the pairs stored at positions >= T moved into the holes < T.
-struct JoinFixup {
-  JoinOut o;
-  unsigned long long* total;  // the pair count T (device or mapped pinned memory)
-  unsigned long long* hint;   // mapped pinned: T again, the next call's chunk-size hint
-  uint64_t* hole_start;       // [nwaves] holes below T, by position
-  uint64_t* hole_pref;        // [nwaves + 1] their exclusive prefix of lengths
-  uint64_t* seg_start;        // [nwaves + 1] stored runs in [T, G), by position
-  uint64_t* seg_pref;         // [nwaves + 2]
-  uint32_t* counts;           // [2] holes below T, runs above T
-};
 hipError_t launch_join_fixup(gf_ctx* ctx, const JoinFixup& f);
 hipError_t launch_join_stream(gf_ctx* ctx, const JoinRowArgs& a);
 hipError_t launch_join_band(gf_ctx* ctx, const JoinRowArgs& a, int blocks);  // fine path

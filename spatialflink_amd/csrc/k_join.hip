@@ -490,16 +490,31 @@ __global__ __launch_bounds__(kSortThreads) void join_sort_finish_kernel(JoinRowA
     }
   }
   __syncthreads();
-  {  // exclusive scan of h[0..H) in place (a contiguous span of keys per thread)
-    const int per = (H + kSortThreads - 1) / kSortThreads, j0 = threadIdx.x * per;
-    uint32_t run = 0;
-    for (int j = j0; j < j0 + per && j < H; ++j) run += h[j];
-    uint32_t total;
-    uint32_t before = join_block_scan<kSortThreads>(run, &total, ws);
-    for (int j = j0; j < j0 + per && j < H; ++j) {
-      const uint32_t c = h[j];
-      h[j] = rb + before;  // the key's cursor (absolute position)
-      before += c;
+  {  // exclusive scan of h[0..H) in place, as cursors (absolute positions): wave w owns the
+     // quarter [w Q, (w + 1) Q), walked in 64-key chunks (lane = key: no bank conflicts -- a
+     // contiguous span per thread put 16 lanes on one bank), its total first, then the chunks
+     // scanned with the running offset
+    constexpr int NW = kSortThreads / 64;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, Q = (H + NW - 1) / NW;
+    const int q0 = wid * Q, q1 = q0 + Q < H ? q0 + Q : H;
+    uint32_t sum = 0;
+    for (int j = q0 + lane; j < q1; j += 64) sum += h[j];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
+    if (lane == 0) ws[wid] = sum;
+    __syncthreads();
+    uint32_t run = rb;
+    for (int w = 0; w < wid; ++w) run += ws[w];
+    for (int j0 = q0; j0 < q1; j0 += 64) {  // wave-uniform
+      const uint32_t v = j0 + lane < q1 ? h[j0 + lane] : 0u;
+      uint32_t inc = v;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = __shfl_up(inc, o, 64);
+        if (lane >= o) inc += t;
+      }
+      if (j0 + lane < q1) h[j0 + lane] = run + inc - v;
+      run += (uint32_t)__shfl(inc, 63, 64);
     }
   }
   __syncthreads();
@@ -550,14 +565,8 @@ struct JoinProbeHdr {
   uint32_t g0;       // fine path: sorted index of the first staged query point
   uint32_t gm;       // fine path: staged query points (0: none; their indices are in LDS)
   uint32_t lqidx;    // fine path: LDS byte offset of the staged query indices
-  // block chunks (JoinOut.block_chunks): the block's pairs so far, and the bases of its chunks
-  // (chunk c in slot c % kJoinRing, tagged c + 1 once published)
   uint32_t kept;     // the task's points inside the grid (sorted; the rest dropped)
-  uint32_t bfill;
-  uint32_t ctag[64];
-  unsigned long long cbase[64];
 };
-constexpr uint32_t kJoinRing = 64;
 constexpr int kJoinHdrBytes = (int)((sizeof(JoinProbeHdr) + 15) / 16 * 16);
 // pairs a wave collects in LDS: a wave-step's pairs (64 points) normally fit, so the walk's
 // inner loop has no global memory operation (the buffer is written out after the step, or when a
@@ -663,55 +672,6 @@ __device__ __forceinline__ void join_emit_close(const JoinOut& o, const JoinWave
   }
 }
 
-// Block chunks: the wave takes `cnt` consecutive block positions with one LDS atomic; a block
-// position p lives in the block's chunk p / C at offset p % C.  The wave whose range holds the
-// first position of a chunk allocates it (one device atomic) and publishes its base in the LDS
-// ring; the others spin on the ring tag (the allocating wave has its offset already and never
-// waits before publishing, so the spin ends).  A flush (<= kJoinWaveBuf pairs) spans at most two
-// chunks (C >= 4096).  The ring holds the latest kJoinRing chunks: a wave reads its bases right
-// after its own LDS atomic, long before the block can have issued kJoinRing * C more positions.
-template <class Get>
-__device__ __forceinline__ void join_emit_block(const JoinOut& o, JoinProbeHdr& hd, uint32_t cnt, Get get) {
-  const uint32_t lane = threadIdx.x & 63, C = o.chunk;
-  uint32_t off = 0;
-  if (lane == 0) off = atomicAdd(&hd.bfill, cnt);
-  off = join_uni(off);
-  const uint32_t c0 = off / C, c1 = (off + cnt - 1) / C;
-  for (uint32_t c = c0; c <= c1; ++c) {  // chunks that start inside [off, off + cnt): allocate
-    if (c * C >= off && lane == 0) {
-      const unsigned long long b = atomicAdd(o.gctr, (unsigned long long)C);
-      hd.cbase[c % kJoinRing] = b;  // the release store below orders it before the tag
-      __hip_atomic_store(&hd.ctag[c % kJoinRing], c + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
-  }
-  unsigned long long base[2];
-#pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    const uint32_t c = c0 + k <= c1 ? c0 + k : c1;
-    while (__hip_atomic_load(&hd.ctag[c % kJoinRing], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != c + 1)
-      __builtin_amdgcn_s_sleep(1);
-    base[k] = join_uni64(hd.cbase[c % kJoinRing]);
-  }
-  for (uint32_t i = lane; i < cnt; i += 64) {
-    const uint32_t p = off + i, c = p / C;
-    join_vstore(o, (c == c0 ? base[0] : base[1]) + (p - c * C), get(i));
-  }
-}
-// the block's last chunk, for the fix-up (after the block's final barrier)
-__device__ __forceinline__ void join_block_close(const JoinOut& o, const JoinProbeHdr& hd) {
-  if (threadIdx.x == 0) {
-    const uint32_t n = hd.bfill, C = o.chunk;
-    if (n == 0) {
-      o.tail_base[blockIdx.x] = ~0ull;
-      o.tail_fill[blockIdx.x] = 0u;
-    } else {
-      const uint32_t c = (n - 1) / C;
-      o.tail_base[blockIdx.x] = hd.cbase[c % kJoinRing];
-      o.tail_fill[blockIdx.x] = n - c * C;
-    }
-  }
-}
-
 // The wave's pair buffer in LDS: hits are appended in ballot order (one mbcnt per hit round,
 // the count stays in a scalar register); past kJoinWaveBuf - 64 the wave writes the buffer out
 // (join_emit: coalesced stores into its output chunk) with each query slot mapped to its query
@@ -728,8 +688,7 @@ struct JoinWaveBuf {
       const uint32_t qi = v.y & 0x80000000u ? v.y & 0x7fffffffu : (v.y - g0 < gm ? lq[v.y - g0] : a.sqidx[v.y]);
       return make_uint2(v.x, qi);
     };
-    if (a.out.block_chunks) join_emit_block(a.out, hd, cnt, get);
-    else join_emit(a.out, wo, cnt, get);
+    join_emit(a.out, wo, cnt, get);
     cnt = 0;
   }
   // one round's hits: hit i of this lane (candidate q[i]) goes after all hits of rounds < i.
@@ -1153,22 +1112,11 @@ __global__ __launch_bounds__(kJoinThreads) void join_row_probe_kernel(JoinRowArg
   const uint32_t ntask = a.task_off[a.nrows];
   const uint32_t per = (ntask + 7) / 8, xcd = blockIdx.x & 7u, nb = (gridDim.x + 7 - xcd) / 8;
   JoinWaveOut wo{~0ull, a.out.chunk};
-  JoinProbeHdr& hd = *reinterpret_cast<JoinProbeHdr*>(lds_base);
-  if (a.out.block_chunks) {
-    for (uint32_t j = threadIdx.x; j < kJoinRing; j += kJoinThreads) hd.ctag[j] = 0u;
-    if (threadIdx.x == 0) hd.bfill = 0u;
-    __syncthreads();
-  }
   for (uint32_t k = blockIdx.x >> 3; k < per; k += nb) {  // block-uniform
     const uint32_t task = xcd * per + k;
     if (task < ntask) join_probe_task<MODE, FINE>(a, task, lds_base, wo);
   }
-  if (a.out.block_chunks) {
-    __syncthreads();  // every wave's last flush is in
-    join_block_close(a.out, hd);
-  } else {
-    join_emit_close(a.out, wo, blockIdx.x * (kJoinThreads / 64) + (threadIdx.x >> 6));
-  }
+  join_emit_close(a.out, wo, blockIdx.x * (kJoinThreads / 64) + (threadIdx.x >> 6));
 }
 
 // ---- streaming probe (experiment, GF_FLAG_JOIN_STREAM) --------------------------------------
@@ -1274,8 +1222,14 @@ hipError_t launch_join_stream(gf_ctx* ctx, const JoinRowArgs& a) {
 // chunks cost one device atomic each on ONE counter: ~20K of them serialised at the memory side
 // (the row probe: 240 us with block chunks, 361 us with wave chunks).
 constexpr int kBandThreads = 1024, kBandWaves = kBandThreads / 64;
-constexpr int kBandBuf = 384;        // pairs per wave buffer (a wave-step's pairs normally fit)
-constexpr int kBandRound = 4;        // candidates per lane per walk round
+#ifndef GF_BAND_BUF
+#define GF_BAND_BUF 512
+#endif
+constexpr int kBandBuf = GF_BAND_BUF;        // pairs per wave buffer (written out before a round could overflow it)
+#ifndef GF_BAND_R
+#define GF_BAND_R 4
+#endif
+constexpr int kBandRound = GF_BAND_R;  // candidates per lane per walk round
 constexpr int kBandMaxSub = 6;       // staged sub-rows f + 2 (f <= 4)
 constexpr uint32_t kBandGlobal = 0x80000000u;  // buffer entry: a global sorted query index
 struct BandHdr {
@@ -1286,10 +1240,13 @@ struct BandHdr {
   unsigned long long fill;  // the block's pairs so far: its region cursor
   uint64_t roff, rlen, E;   // the block's region, the regions' end (overflow area start)
   uint64_t wsum[kBandWaves];
+  int32_t last;             // this block took the last ticket
 };
 constexpr int kBandHdrBytes = (int)((sizeof(BandHdr) + 15) / 16 * 16);
 constexpr size_t kBandLds = 160 * 1024;
-constexpr size_t kBandStage = kBandLds - kBandHdrBytes - (size_t)kBandWaves * kBandBuf * 8;
+constexpr int kBandQueue = 128;      // windowed bands: queued point positions per wave
+constexpr size_t kBandPerWave = (size_t)kBandBuf * 8 + kBandQueue * 4;
+constexpr size_t kBandStage = kBandLds - kBandHdrBytes - (size_t)kBandWaves * kBandPerWave;
 // staged offset entries per band sub-row for window [c0, c1): sub-columns c0 - 1 .. c1 + 1
 __device__ __forceinline__ uint32_t band_ncol(uint32_t c0, uint32_t c1) { return (c1 - c0 + 3 + 7) & ~7u; }
 __device__ __forceinline__ uint32_t band_off_bytes(int32_t f, uint32_t c0, uint32_t c1) {
@@ -1324,8 +1281,8 @@ __device__ __forceinline__ uint64_t band_scan(uint64_t v, uint64_t* total, uint6
   return before + inc - v;
 }
 // Every block derives all G regions the same way (so no launch is needed for them): block t's
-// pairs per point from the last call (hist; none: the host's estimate) x its slice now, + 1/16
-// + 512; scaled down so that the total stays <= e_lim.  Block 0 records them for the fix-up.
+// pairs per point from the last call (hist; none: the host's estimate) x its slice now, + 1/32
+// + 256; scaled down so that the total stays <= e_lim.  Block 0 records them for the fix-up.
 __device__ __forceinline__ void band_regions(const JoinOut& o, uint32_t N, BandHdr& hd) {
   const uint32_t G = gridDim.x, t = threadIdx.x;
   uint64_t hp = 0, hn = 0, slice = 0;
@@ -1341,7 +1298,7 @@ __device__ __forceinline__ void band_regions(const JoinOut& o, uint32_t N, BandH
   band_scan(hn, &HN, hd.wsum);
   const double gppp = HN > 0 ? (double)HP / (double)HN : o.ppp;
   uint64_t est = 0;
-  if (t < G) est = (uint64_t)ceil((hn > 0 ? (double)hp / (double)hn : gppp) * (double)slice * 1.0625) + 512;
+  if (t < G) est = (uint64_t)ceil((hn > 0 ? (double)hp / (double)hn : gppp) * (double)slice * 1.03125) + 256;
   uint64_t E;
   uint64_t off = band_scan(est, &E, hd.wsum);
   if (E > o.e_lim) {  // floor(est * s) with s < e_lim / E: the sum stays <= e_lim
@@ -1385,14 +1342,72 @@ __device__ __forceinline__ void band_emit(const JoinOut& o, BandHdr& hd, uint32_
   }
 }
 
+// The regions' fix-up (one block, G <= 1023 regions): T = the pairs; region t keeps
+// [off_t, off_t + min(n_t, len_t)), its unused tail is a hole, and the overflow area
+// [E, E + ovf) is the last run; holes below T and stored runs at or above T (both already in
+// position order -- no sort) with their exclusive prefixes for join_fixup_copy_kernel.  Also:
+// the history (pairs, points per block) for the next call's regions, and the overflow reset.
+// A pair stored past cap + spill_cap was dropped: when T <= cap that is reported as T = cap + 1
+// (GF_ERR_CAPACITY; the caller's retry gets regions sized from this call's exact counts).
+__device__ __forceinline__ void join_region_prep(const JoinFixup& f, uint64_t* ws) {
+  const JoinOut& o = f.o;
+  const uint32_t G = o.nwaves, t = threadIdx.x;
+  uint64_t O = 0, R = 0, n = 0;
+  if (t < G) {
+    O = o.reg_off[t];
+    R = o.reg_len[t];
+    n = o.bcount[t];
+  }
+  const uint64_t u = n < R ? n : R;
+  uint64_t T;
+  band_scan(n, &T, ws);
+  const uint64_t E = o.reg_off[G], ov = *o.ovf;
+  const bool lost = E + ov > o.cap + o.spill_cap;
+  const bool fits = T <= o.cap && !lost;
+  uint64_t hl = 0, hs = 0, sl = 0, ss = 0;
+  if (t < G) {
+    hs = O + u;
+    hl = hs < T ? (O + R < T ? O + R : T) - hs : 0;
+    ss = O > T ? O : T;
+    sl = O + u > ss ? O + u - ss : 0;
+  } else if (t == G) {
+    ss = E > T ? E : T;
+    sl = E + ov > ss ? E + ov - ss : 0;
+  }
+  uint64_t H, S;
+  const uint64_t hp = band_scan(hl, &H, ws), sp = band_scan(sl, &S, ws);
+  if (t < G) {
+    f.hole_start[t] = hs;
+    f.hole_pref[t] = hp;
+    o.hist[t] = n;
+    o.hist[G + t] = o.bslice[t];
+  }
+  if (t <= G) {
+    f.seg_start[t] = ss;
+    f.seg_pref[t] = sp;
+  }
+  if (t == 0) {
+    f.hole_pref[G] = H;
+    f.seg_pref[G + 1] = S;
+    f.counts[0] = fits ? G : 0u;
+    f.counts[1] = fits ? G + 1 : 0u;
+    *f.total = T <= o.cap && lost ? o.cap + 1 : T;
+    if (f.hint) *f.hint = T;
+    *o.ovf = 0ull;
+  }
+}
+
 template <int MODE>
 __global__ __launch_bounds__(kBandThreads) void join_band_probe_kernel(JoinRowArgs a) {
   extern __shared__ __attribute__((aligned(16))) char lds_base[];
   BandHdr& hd = *reinterpret_cast<BandHdr*>(lds_base);
-  char* const stg = lds_base + kBandHdrBytes + (size_t)kBandWaves * kBandBuf * 8;
+  char* const stg = lds_base + kBandHdrBytes + (size_t)kBandWaves * kBandPerWave;
   const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  uint2* const buf = reinterpret_cast<uint2*>(lds_base + kBandHdrBytes) + wid * kBandBuf;
+  char* const wbase = lds_base + kBandHdrBytes + (size_t)wid * kBandPerWave;
+  uint2* const buf = reinterpret_cast<uint2*>(wbase);
+  uint32_t* const wq = reinterpret_cast<uint32_t*>(wbase + kBandBuf * 8);
   uint32_t cnt = 0;  // wave-uniform
+  uint32_t sink = 0;  // experiment builds (GF_BAND_EXP_*) only
   const int32_t f = a.f, qn = a.qn;
   const int64_t fW = (int64_t)f * (qn + 2);
   const uint32_t cbeg = (uint32_t)f, cend = (uint32_t)f * (uint32_t)(qn + 1);  // in-grid sub-columns
@@ -1550,18 +1565,20 @@ __global__ __launch_bounds__(kBandThreads) void join_band_probe_kernel(JoinRowAr
             e[k] = in ? qo[k * fW + 2] : 0u;
           }
         }
-        // the three runs walked as one sequence (ballot exit); a full buffer is written out
-        // between rounds
+#ifdef GF_BAND_EXP_NOWALK  // experiment build: setup and streaming only (no pairs)
+        sink += e[0] ^ e[1] ^ e[2] ^ b[0] ^ b[1] ^ b[2];
+        return;
+#endif
         const uint32_t L0 = e[0] - b[0], L1 = L0 + (e[1] - b[1]), L2 = L1 + (e[2] - b[2]);
         const uint32_t d0 = b[0], d1 = b[1] - L0, d2 = b[2] - L1;
-        uint32_t k = 0;
-        for (;;) {
-          bool full = false;
-          for (; __ballot(k < L2) != 0; k += kBandRound) {
-            if (cnt > (uint32_t)(kBandBuf - 64 * kBandRound)) {
-              full = true;
-              break;
-            }
+        // the three runs walked as one sequence by each lane, kBandRound candidates per round
+        // (ballot exit); the buffer is written out before a round whose hits might not fit.
+        // (Measured, r03: a PACKED walk -- the wave's candidates laid out densely in LDS and tested
+        // 64 per round through lane permutes -- ran no faster, 184.8 vs 183.0 us: the walk is not
+        // bound by its idle lanes; R = 2 rounds: 182.6 us.)
+        for (uint32_t k = 0; __ballot(k < L2) != 0; k += kBandRound) {
+          if (cnt > (uint32_t)(kBandBuf - 64 * kBandRound)) flush();
+          {
             uint32_t t[kBandRound];
             double2 v[kBandRound];
 #pragma unroll
@@ -1586,14 +1603,16 @@ __global__ __launch_bounds__(kBandThreads) void join_band_probe_kernel(JoinRowAr
               else ok = a.metric == 0 ? dx * dx + dy * dy <= a.s_r : fdlibm_hypot(dx, dy) <= a.r;
               const bool hit = k + i < L2 && ok;
               const uint64_t hm = __ballot(hit);
+#ifdef GF_BAND_EXP_NOPUSH  // experiment build: hits ballotted, never stored
+              sink ^= (uint32_t)hm;
+              continue;
+#endif
               if (hit)
                 buf[cnt + __builtin_amdgcn_mbcnt_hi((uint32_t)(hm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)hm, 0u))] =
                     make_uint2(pidx, lds ? t[i] : (t[i] | kBandGlobal));
               cnt += (uint32_t)__popcll(hm);
             }
           }
-          if (!full) break;
-          flush();
         }
       };
       // the segment, 128 consecutive points per wave-step (two per lane); past the end a lane
@@ -1612,14 +1631,49 @@ __global__ __launch_bounds__(kBandThreads) void join_band_probe_kernel(JoinRowAr
         }
         return p;
       };
-      Pt cur = fetch(sb + wid * 128);
-      for (uint32_t s0 = sb + wid * 128; s0 < se; s0 += kBandWaves * 128) {  // wave-uniform
-        const Pt nxt = fetch(s0 + kBandWaves * 128);
-        probe(cur.v[0].x, cur.v[0].y, cur.idx[0], s0 + lane < se);
-        probe(cur.v[1].x, cur.v[1].y, cur.idx[1], s0 + 64 + lane < se);
-        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): nxt is in registers (before any store)
-        if (cnt > (uint32_t)(kBandBuf - 64 * kBandRound)) flush();
-        cur = nxt;
+      if (c0 == cbeg && c1 == cend) {  // the whole band in one window: every point streams through
+        Pt cur = fetch(sb + wid * 128);
+        for (uint32_t s0 = sb + wid * 128; s0 < se; s0 += kBandWaves * 128) {  // wave-uniform
+          const Pt nxt = fetch(s0 + kBandWaves * 128);
+          // the buffer is written out right after the next step's loads are issued, so the
+          // stores complete under this step's walk: vmcnt counts stores too, and a flush after
+          // the step's wait made every following step wait for its stores
+          if (cnt > (uint32_t)(kBandBuf / 2)) flush();
+          probe(cur.v[0].x, cur.v[0].y, cur.idx[0], s0 + lane < se);
+          probe(cur.v[1].x, cur.v[1].y, cur.idx[1], s0 + 64 + lane < se);
+          __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): nxt is in registers
+          cur = nxt;
+        }
+      } else {
+        // windowed band: the wave queues the positions of its points inside the window (LDS) and
+        // probes them 64 at a time, so the lanes of other windows do not ride along
+        uint32_t qc = 0;  // wave-uniform
+        for (uint32_t s0 = sb + wid * 64; s0 < se; s0 += kBandWaves * 64) {
+          const uint32_t i = s0 + lane;
+          const bool valid = i < se;
+          const double px = a.soxy[2 * (size_t)(valid ? i : sb)];
+          const int32_t cx = cell_index(px, a.u_minX, a.u_cl);
+          bool act = valid && cx >= 0 && cx < qn;
+          const int32_t col = act ? f * (cx + 1) + join_sub(px, a.u_minX, a.u_cl, cx, a.fs, f) : 0;
+          act = act && (uint32_t)col >= c0 && (uint32_t)col < c1;
+          const uint64_t am = __ballot(act);
+          if (act) wq[qc + __builtin_amdgcn_mbcnt_hi((uint32_t)(am >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)am, 0u))] = i;
+          qc += (uint32_t)__popcll(am);
+          if (qc >= 64) {
+            const uint32_t k = wq[lane], rest = qc - 64;
+            const uint32_t mv = lane < rest ? wq[64 + lane] : 0u;
+            if (lane < rest) wq[lane] = mv;
+            qc = rest;
+            const double2 v = reinterpret_cast<const double2*>(a.soxy)[k];
+            probe(v.x, v.y, a.soidx[k], true);
+            if (cnt > (uint32_t)(kBandBuf - 64 * kBandRound)) flush();
+          }
+        }
+        if (qc > 0) {
+          const uint32_t k = wq[lane < qc ? lane : 0];
+          const double2 v = reinterpret_cast<const double2*>(a.soxy)[k];
+          probe(v.x, v.y, a.soidx[k], lane < qc);
+        }
       }
       if (cnt > 0) flush();  // staged slots change with the next window
       __syncthreads();
@@ -1628,9 +1682,18 @@ __global__ __launch_bounds__(kBandThreads) void join_band_probe_kernel(JoinRowAr
     pos = se;
   }
   __syncthreads();  // every wave's pairs are counted
+  if (sink == 0xdeadbeefu) a.out.bslice[blockIdx.x] = sink;  // keeps experiment builds' work alive
   if (threadIdx.x == 0) {
     a.out.bcount[blockIdx.x] = hd.fill;
     a.out.bslice[blockIdx.x] = P1 - P0;
+    __threadfence();
+    hd.last = atomicAdd(a.ticket, 1ull) == (unsigned long long)gridDim.x - 1;
+  }
+  __syncthreads();
+  if (hd.last) {  // block-uniform: every other block's counts are in
+    __threadfence();
+    join_region_prep(a.fx, hd.wsum);
+    if (threadIdx.x == 0) *a.ticket = 0ull;
   }
 }
 
@@ -1643,61 +1706,6 @@ hipError_t launch_join_band(gf_ctx* ctx, const JoinRowArgs& a, int blocks) {
   return hipGetLastError();
 }
 
-// The regions' fix-up (one block, G <= 1023 regions): T = the pairs; region t keeps
-// [off_t, off_t + min(n_t, len_t)), its unused tail is a hole, and the overflow area
-// [E, E + ovf) is the last run; holes below T and stored runs at or above T (both already in
-// position order -- no sort) with their exclusive prefixes for join_fixup_copy_kernel.  Also:
-// the history (pairs, points per block) for the next call's regions, and the overflow reset.
-// A pair stored past cap + spill_cap was dropped: when T <= cap that is reported as T = cap + 1
-// (GF_ERR_CAPACITY; the caller's retry gets regions sized from this call's exact counts).
-__global__ __launch_bounds__(kBandThreads) void join_region_prep_kernel(JoinFixup f) {
-  __shared__ uint64_t ws[kBandWaves];
-  const JoinOut& o = f.o;
-  const uint32_t G = o.nwaves, t = threadIdx.x;
-  uint64_t O = 0, R = 0, n = 0;
-  if (t < G) {
-    O = o.reg_off[t];
-    R = o.reg_len[t];
-    n = o.bcount[t];
-  }
-  const uint64_t u = n < R ? n : R;
-  uint64_t T;
-  band_scan(n, &T, ws);
-  const uint64_t E = o.reg_off[G], ov = *o.ovf;
-  const bool lost = E + ov > o.cap + o.spill_cap;
-  const bool fits = T <= o.cap && !lost;
-  uint64_t hl = 0, hs = 0, sl = 0, ss = 0;
-  if (t < G) {
-    hs = O + u;
-    hl = hs < T ? (O + R < T ? O + R : T) - hs : 0;
-    ss = O > T ? O : T;
-    sl = O + u > ss ? O + u - ss : 0;
-  } else if (t == G) {
-    ss = E > T ? E : T;
-    sl = E + ov > ss ? E + ov - ss : 0;
-  }
-  uint64_t H, S;
-  const uint64_t hp = band_scan(hl, &H, ws), sp = band_scan(sl, &S, ws);
-  if (t < G) {
-    f.hole_start[t] = hs;
-    f.hole_pref[t] = hp;
-    o.hist[t] = n;
-    o.hist[G + t] = o.bslice[t];
-  }
-  if (t <= G) {
-    f.seg_start[t] = ss;
-    f.seg_pref[t] = sp;
-  }
-  if (t == 0) {
-    f.hole_pref[G] = H;
-    f.seg_pref[G + 1] = S;
-    f.counts[0] = fits ? G : 0u;
-    f.counts[1] = fits ? G + 1 : 0u;
-    *f.total = T <= o.cap && lost ? o.cap + 1 : T;
-    if (f.hint) *f.hint = T;
-    *o.ovf = 0ull;
-  }
-}
 
 // ---- the output fix-up ------------------------------------------------------------------------
 // (1) one block: the waves' last chunks sorted by position; their holes; T = G - the holes = the
@@ -1818,37 +1826,43 @@ __device__ __forceinline__ uint32_t join_bsearch(const uint64_t* pref, uint32_t 
   }
   return lo;
 }
-// One block per hole (blocks >= the hole count exit): the hole's first source run by one
-// binary search, then each thread walks forward from it (a hole's range crosses few runs).  A
-// grid-stride loop with two binary searches per pair was latency-bound (17 us for ~1M pairs).
+// kFixupParts blocks per hole (blocks past the holes exit), block p of a hole taking its pieces
+// p, p + kFixupParts, .. of kBlock pairs: each piece's first source run by one binary search,
+// then each thread walks forward from it (a piece crosses few runs).  A grid-stride loop with two
+// binary searches per pair was latency-bound (17 us for ~1M pairs).
+constexpr int kFixupParts = 8;
 __global__ __launch_bounds__(kBlock) void join_fixup_copy_kernel(JoinFixup f) {
   const uint32_t nh = f.counts[0], ns = f.counts[1];
   if (nh == 0 || ns == 0) return;
   __shared__ uint32_t s_sg;
-  for (uint32_t h = blockIdx.x; h < nh; h += gridDim.x) {  // block-uniform
-    const uint64_t k0 = f.hole_pref[h], k1 = f.hole_pref[h + 1], d0 = f.hole_start[h];
-    if (threadIdx.x == 0) s_sg = join_bsearch(f.seg_pref, ns, k0);
-    __syncthreads();
-    const uint32_t sg0 = s_sg;
-    for (uint64_t k = k0 + threadIdx.x; k < k1; k += kBlock) {
-      uint32_t sg = sg0;
-      int steps = 0;
-      while (sg + 1 < ns && f.seg_pref[sg + 1] <= k && steps < 8) { ++sg; ++steps; }
-      if (steps == 8) sg = join_bsearch(f.seg_pref, ns, k);
-      const uint64_t src = f.seg_start[sg] + (k - f.seg_pref[sg]);
-      join_store(f.o.pairs, f.o.aligned, d0 + (k - k0), join_vload(f.o, src));
+  const uint32_t part = blockIdx.x % kFixupParts;
+  for (uint32_t h = blockIdx.x / kFixupParts; h < nh; h += gridDim.x / kFixupParts) {  // block-uniform
+    const uint64_t hk0 = f.hole_pref[h], k1 = f.hole_pref[h + 1], d0 = f.hole_start[h];
+    for (uint64_t k0 = hk0 + (uint64_t)part * kBlock; k0 < k1; k0 += (uint64_t)kFixupParts * kBlock) {
+      if (threadIdx.x == 0) s_sg = join_bsearch(f.seg_pref, ns, k0);
+      __syncthreads();
+      const uint64_t k = k0 + threadIdx.x;
+      if (k < k1) {
+        uint32_t sg = s_sg;
+        int steps = 0;
+        while (sg + 1 < ns && f.seg_pref[sg + 1] <= k && steps < 8) {
+          ++sg;
+          ++steps;
+        }
+        if (steps == 8) sg = join_bsearch(f.seg_pref, ns, k);
+        const uint64_t src = f.seg_start[sg] + (k - f.seg_pref[sg]);
+        join_store(f.o.pairs, f.o.aligned, d0 + (k - hk0), join_vload(f.o, src));
+      }
+      __syncthreads();
     }
-    __syncthreads();
   }
 }
 
 hipError_t launch_join_fixup(gf_ctx* ctx, const JoinFixup& f) {
   KTimer t(ctx, GF_K_JOIN_COMPACT);
-  if (f.o.regions)
-    hipLaunchKernelGGL(join_region_prep_kernel, dim3(1), dim3(kBandThreads), 0, ctx->stream, f);
-  else
+  if (!f.o.regions)  // regions: the band probe's last block prepared the fix-up
     hipLaunchKernelGGL(join_fixup_prep_kernel, dim3(1), dim3(1024), 0, ctx->stream, f);
-  hipLaunchKernelGGL(join_fixup_copy_kernel, dim3(f.o.nwaves), dim3(kBlock), 0, ctx->stream, f);
+  hipLaunchKernelGGL(join_fixup_copy_kernel, dim3(f.o.nwaves * kFixupParts), dim3(kBlock), 0, ctx->stream, f);
   return hipGetLastError();
 }
 
@@ -1879,7 +1893,7 @@ hipError_t launch_join_rows(gf_ctx* ctx, const JoinRowArgs& a, const JoinQueryAr
     case 3: {
       KTimer t(ctx, GF_K_JOIN_PROBE);
       const size_t lds = join_probe_lds_bytes(a.lds_budget, a.qn, a.f);
-      const dim3 pg(a.out.block_chunks ? a.out.nwaves : a.out.nwaves / (kJoinThreads / 64));
+      const dim3 pg(a.out.nwaves / (kJoinThreads / 64));
       const bool m0 = !a.approx && a.metric == 0;
       if (a.f > 1) {  // host: the fine path is exact (never approximate)
         if (m0) hipLaunchKernelGGL((join_row_probe_kernel<0, 1>), pg, dim3(kJoinThreads), lds, s, a);
