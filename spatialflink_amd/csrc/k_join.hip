@@ -1573,9 +1573,10 @@ __global__ __launch_bounds__(kBandThreads) void join_band_probe_kernel(JoinRowAr
         const uint32_t d0 = b[0], d1 = b[1] - L0, d2 = b[2] - L1;
         // the three runs walked as one sequence by each lane, kBandRound candidates per round
         // (ballot exit); the buffer is written out before a round whose hits might not fit.
-        // (Measured, r03: a PACKED walk -- the wave's candidates laid out densely in LDS and tested
-        // 64 per round through lane permutes -- ran no faster, 184.8 vs 183.0 us: the walk is not
-        // bound by its idle lanes; R = 2 rounds: 182.6 us.)
+        // (Measured, r03, probe us: a PACKED walk -- the wave's candidates laid out densely in LDS
+        // and tested 64 per round through lane permutes -- 184.8 vs 183.0: the walk is not bound
+        // by its idle lanes; R = 2: 182.6, R = 8: 211; buffers of 384 / 768 pairs: +4 / +81 (the
+        // band then needs windows); flushing at the step's start instead of its end: no change.)
         for (uint32_t k = 0; __ballot(k < L2) != 0; k += kBandRound) {
           if (cnt > (uint32_t)(kBandBuf - 64 * kBandRound)) flush();
           {
@@ -1635,13 +1636,10 @@ __global__ __launch_bounds__(kBandThreads) void join_band_probe_kernel(JoinRowAr
         Pt cur = fetch(sb + wid * 128);
         for (uint32_t s0 = sb + wid * 128; s0 < se; s0 += kBandWaves * 128) {  // wave-uniform
           const Pt nxt = fetch(s0 + kBandWaves * 128);
-          // the buffer is written out right after the next step's loads are issued, so the
-          // stores complete under this step's walk: vmcnt counts stores too, and a flush after
-          // the step's wait made every following step wait for its stores
-          if (cnt > (uint32_t)(kBandBuf / 2)) flush();
           probe(cur.v[0].x, cur.v[0].y, cur.idx[0], s0 + lane < se);
           probe(cur.v[1].x, cur.v[1].y, cur.idx[1], s0 + 64 + lane < se);
-          __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): nxt is in registers
+          __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): nxt is in registers (before any store)
+          if (cnt > (uint32_t)(kBandBuf - 64 * kBandRound)) flush();
           cur = nxt;
         }
       } else {
