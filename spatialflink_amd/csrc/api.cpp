@@ -1891,7 +1891,6 @@ static int join_pp_impl(gf_ctx* ctx, const gf_grid* ugrid, const gf_grid* qgrid,
   const uint64_t spill_cap = band ? (ucap == 0 ? 0 : (e_lim - ucap) + std::max<uint64_t>(65536, (uint64_t)(t_hint / 16)))
                                   : (uint64_t)(ntails * chunk);
   size_t o_spill = ar.take<uint64_t>(rowpath ? std::max<uint64_t>(spill_cap, 1) : 1);
-  size_t o_reg = ar.take<uint64_t>(probe_blocks + 1), o_rlen = ar.take<uint64_t>(probe_blocks);
   size_t o_bcnt = ar.take<uint64_t>(probe_blocks), o_bsl = ar.take<uint64_t>(probe_blocks);
   size_t o_tb = ar.take<uint64_t>(nwaves), o_tf = ar.take<uint32_t>(nwaves);
   size_t o_hs = ar.take<uint64_t>(nwaves + 1), o_hp = ar.take<uint64_t>(nwaves + 2);
@@ -1947,8 +1946,6 @@ static int join_pp_impl(gf_ctx* ctx, const gf_grid* ugrid, const gf_grid* qgrid,
         GF_HIP_CHECK(ctx, hipMemsetAsync(ctx->join_ovf, 0, 2 * sizeof(unsigned long long), s));
       }
       o.regions = 1;
-      o.reg_off = (uint64_t*)(base + o_reg);
-      o.reg_len = (uint64_t*)(base + o_rlen);
       o.bcount = (uint64_t*)(base + o_bcnt);
       o.bslice = (uint64_t*)(base + o_bsl);
       o.hist = ctx->join_hist;

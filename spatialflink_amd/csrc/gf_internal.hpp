@@ -564,14 +564,12 @@ struct JoinOut {
   uint64_t* tail_base;       // [nwaves] base of each wave's last chunk (~0: none)
   uint32_t* tail_fill;       // [nwaves]
   uint32_t nwaves;           // tail entries: the probe's waves (regions: its blocks)
-  // Band probe REGIONS (k_join.hip): block b owns positions [reg_off[b], reg_off[b] + reg_len[b])
-  // and fills them through an LDS cursor (no global atomic); pairs beyond its region go to the
-  // dense overflow area [E, E + *ovf) (E = reg_off[G]; one atomic per overflowing flush).  The
-  // regions come from the last call's pairs per point of every block (hist), scaled down to e_lim
+  // Band probe REGIONS (k_join.hip): block b owns a region of positions (derived by every block
+  // alike from hist) and fills it through an LDS cursor (no global atomic); pairs beyond its
+  // region go to the dense overflow area after the regions (one atomic per overflowing flush).
+  // Regions come from the last call's pairs per point of every block (hist), scaled down to e_lim
   // when they would exceed it; the fix-up moves the pairs above T into the regions' unused tails.
   int regions;
-  uint64_t* reg_off;         // [G + 1] written by the probe's blocks
-  uint64_t* reg_len;         // [G]
   uint64_t* bcount;          // [G] this call's pairs per block
   uint64_t* bslice;          // [G] this call's ordinary points per block
   uint64_t* hist;            // [2G] persistent: the last call's pairs | points per block (zero: none)

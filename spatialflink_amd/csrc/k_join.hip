@@ -1283,7 +1283,8 @@ __device__ __forceinline__ uint64_t band_scan(uint64_t v, uint64_t* total, uint6
 // Every block derives all G regions the same way (so no launch is needed for them): block t's
 // pairs per point from the last call (hist; none: the host's estimate) x its slice now, + 1/32
 // + 256; scaled down so that the total stays <= e_lim.  Block 0 records them for the fix-up.
-__device__ __forceinline__ void band_regions(const JoinOut& o, uint32_t N, BandHdr& hd) {
+__device__ __forceinline__ void band_regions(const JoinOut& o, uint32_t N, BandHdr& hd, uint64_t& my_off,
+                                             uint64_t& my_len) {
   const uint32_t G = gridDim.x, t = threadIdx.x;
   uint64_t hp = 0, hn = 0, slice = 0;
   if (t < G) {
@@ -1314,11 +1315,8 @@ __device__ __forceinline__ void band_regions(const JoinOut& o, uint32_t N, BandH
     hd.E = E;
     hd.fill = 0ull;
   }
-  if (blockIdx.x == 0 && t < G) {
-    o.reg_off[t] = off;
-    o.reg_len[t] = est;
-    if (t == G - 1) o.reg_off[G] = E;
-  }
+  my_off = off;  // thread t keeps region t (the last block's fix-up reads them from registers)
+  my_len = est;
   __syncthreads();
 }
 // The wave's cnt pairs get(0 .. cnt) at the block's next region positions; those past the region
@@ -1349,19 +1347,21 @@ __device__ __forceinline__ void band_emit(const JoinOut& o, BandHdr& hd, uint32_
 // the history (pairs, points per block) for the next call's regions, and the overflow reset.
 // A pair stored past cap + spill_cap was dropped: when T <= cap that is reported as T = cap + 1
 // (GF_ERR_CAPACITY; the caller's retry gets regions sized from this call's exact counts).
-__device__ __forceinline__ void join_region_prep(const JoinFixup& f, uint64_t* ws) {
+// O, R: region t of thread t (every block derived all of them, band_regions), E their end.  The
+// other blocks' counts were stored write-through and drained before their tickets, so they are
+// read with agent-scope loads -- no __threadfence (an L2 write-back per block).
+__device__ __forceinline__ void join_region_prep(const JoinFixup& f, uint64_t* ws, uint64_t O, uint64_t R, uint64_t E) {
   const JoinOut& o = f.o;
   const uint32_t G = o.nwaves, t = threadIdx.x;
-  uint64_t O = 0, R = 0, n = 0;
+  uint64_t n = 0, sl0 = 0;
   if (t < G) {
-    O = o.reg_off[t];
-    R = o.reg_len[t];
-    n = o.bcount[t];
+    n = __hip_atomic_load(o.bcount + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    sl0 = __hip_atomic_load(o.bslice + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   const uint64_t u = n < R ? n : R;
   uint64_t T;
   band_scan(n, &T, ws);
-  const uint64_t E = o.reg_off[G], ov = *o.ovf;
+  const uint64_t ov = __hip_atomic_load(o.ovf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const bool lost = E + ov > o.cap + o.spill_cap;
   const bool fits = T <= o.cap && !lost;
   uint64_t hl = 0, hs = 0, sl = 0, ss = 0;
@@ -1380,7 +1380,7 @@ __device__ __forceinline__ void join_region_prep(const JoinFixup& f, uint64_t* w
     f.hole_start[t] = hs;
     f.hole_pref[t] = hp;
     o.hist[t] = n;
-    o.hist[G + t] = o.bslice[t];
+    o.hist[G + t] = sl0;
   }
   if (t <= G) {
     f.seg_start[t] = ss;
@@ -1412,7 +1412,8 @@ __global__ __launch_bounds__(kBandThreads) void join_band_probe_kernel(JoinRowAr
   const int64_t fW = (int64_t)f * (qn + 2);
   const uint32_t cbeg = (uint32_t)f, cend = (uint32_t)f * (uint32_t)(qn + 1);  // in-grid sub-columns
   const uint32_t N = a.row_off[qn];
-  band_regions(a.out, N, hd);
+  uint64_t my_off, my_len;
+  band_regions(a.out, N, hd, my_off, my_len);
   uint32_t pos, P1;
   band_slice(N, gridDim.x, blockIdx.x, pos, P1);
   const uint32_t P0 = pos;
@@ -1681,17 +1682,16 @@ __global__ __launch_bounds__(kBandThreads) void join_band_probe_kernel(JoinRowAr
   }
   __syncthreads();  // every wave's pairs are counted
   if (sink == 0xdeadbeefu) a.out.bslice[blockIdx.x] = sink;  // keeps experiment builds' work alive
-  if (threadIdx.x == 0) {
-    a.out.bcount[blockIdx.x] = hd.fill;
-    a.out.bslice[blockIdx.x] = P1 - P0;
-    __threadfence();
+  if (threadIdx.x == 0) {  // write-through, drained before the ticket (see join_region_prep)
+    __hip_atomic_store(a.out.bcount + blockIdx.x, (uint64_t)hd.fill, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(a.out.bslice + blockIdx.x, (uint64_t)(P1 - P0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     hd.last = atomicAdd(a.ticket, 1ull) == (unsigned long long)gridDim.x - 1;
   }
   __syncthreads();
   if (hd.last) {  // block-uniform: every other block's counts are in
-    __threadfence();
-    join_region_prep(a.fx, hd.wsum);
-    if (threadIdx.x == 0) *a.ticket = 0ull;
+    join_region_prep(a.fx, hd.wsum, my_off, my_len, hd.E);
+    if (threadIdx.x == 0) __hip_atomic_store(a.ticket, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
