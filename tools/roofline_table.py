@@ -6,10 +6,12 @@ Inputs (all committed under profiles/):
                           commands (tools/gpu_pmc_r03.sh): per kernel the median FETCH_SIZE /
                           WRITE_SIZE per dispatch and the dispatch counts
 
-Per line:  frac      = roofline.bytes_per_launch / roofline.avg_launch_us / peak  (the line's
-                       own basis: bytes of one window over the timed interval per window)
+Per line:  frac      = roofline.bytes_per_launch / time / peak, time = the line's own basis:
+                       the window interval (ms_per_step) when it keeps windows in flight
+                       ("interval" in achieved_basis), else the kernel's average launch
            traffic   = sum over the workload's kernels of (2 x FETCH_SIZE + WRITE_SIZE) per
-                       dispatch x dispatches per window (relative to the line's main kernel);
+                       dispatch x dispatches per main-kernel launch, / windows per launch
+                       (config.windows_per_launch: batched range windows);
                        FETCH_SIZE doubled per MI355X_MICROARCH.md (gfx950 reports half of wide
                        streaming reads; other access widths are uncalibrated -- an upper bound)
            ratio     = traffic / algorithmic bytes
@@ -78,7 +80,11 @@ def main():
         w = d["config"]["workload"]
         r = d["roofline"]
         bpl, us = r.get("bytes_per_launch"), r.get("avg_launch_us")
+        basis = (r.get("achieved_basis") or (d.get("breakdown") or {}).get("achieved_basis") or "")
+        if "interval" in basis:  # windows in flight: bytes of a window over the window interval
+            us = 1000.0 * d["ms_per_step"]
         frac = bpl / (us * 1e-6) / 1e9 / PEAK if bpl and us else None
+        wpl = d["config"].get("windows_per_launch", 1) or 1  # batched launches carry several windows
         row = {"workload": w, "ms_per_step": d["ms_per_step"], "algorithmic_MB": round(bpl / 1e6, 1) if bpl else None,
                "frac_line": r.get("frac"), "frac_recomputed": round(frac, 4) if frac else None,
                "traffic_MB": None, "traffic_ratio": None, "pmc": None, "kernels": None}
@@ -89,6 +95,7 @@ def main():
                 pm = json.load(fh)["pmc"]
             t, rows = traffic_of(pm, main, allk)
             if t:
+                t /= wpl
                 row.update(traffic_MB=round(t / 1e6, 1), traffic_ratio=round(t / bpl, 3) if bpl else None,
                            pmc=os.path.relpath(p, ROOT), kernels=rows)
         res.append(row)
