@@ -433,8 +433,16 @@ __device__ __forceinline__ uint32_t join_block_scan(uint32_t v, uint32_t* total,
 // (five per CU by the LDS histogram) -- with 1024-thread blocks two rounds of latency-bound
 // blocks took 34 us for 1M points
 constexpr int kSortThreads = 256;
+// A row of <= kSortStage points is placed in LDS in its sorted order and written out coalesced
+// (its scattered 8-B / 4-B stores cost ~9 of the kernel's 30 us at C4); larger rows scatter
+// straight to global memory.
+constexpr int kSortStage = 1536;
+size_t join_sort_lds_bytes(int32_t f, int32_t qn) {
+  return ((size_t)f * f * (qn + 2) * 4 + 15) / 16 * 16 + (size_t)kSortStage * 20;
+}
 __global__ __launch_bounds__(kSortThreads) void join_sort_finish_kernel(JoinRowArgs a, JoinQueryArgs q) {
-  __shared__ uint32_t h[kRowMax];
+  extern __shared__ __attribute__((aligned(16))) char sort_lds[];
+  uint32_t* const h = reinterpret_cast<uint32_t*>(sort_lds);  // [H] key histogram -> cursors
   __shared__ uint32_t ws[kSortThreads / 64];
   const int32_t W = q.qn + 2;
   if ((int)blockIdx.x == W) {
@@ -521,6 +529,9 @@ __global__ __launch_bounds__(kSortThreads) void join_sort_finish_kernel(JoinRowA
   for (int j = threadIdx.x; j < H; j += kSortThreads) q.q_off[(size_t)ky * H + j] = h[j];
   if (ky == W - 1 && threadIdx.x == 0) q.q_off[(size_t)W * H] = re;
   __syncthreads();
+  const bool staged = re - rb <= (uint32_t)kSortStage;  // block-uniform
+  double2* const sxy = reinterpret_cast<double2*>(sort_lds + ((size_t)H * 4 + 15) / 16 * 16);
+  uint32_t* const sidx = reinterpret_cast<uint32_t*>(sxy + kSortStage);
   for (uint32_t i0 = rb + threadIdx.x; i0 < re; i0 += kSortThreads * 4) {
     double2 v[4];
     uint32_t ix[4];
@@ -535,6 +546,11 @@ __global__ __launch_bounds__(kSortThreads) void join_sort_finish_kernel(JoinRowA
       if (i0 + u * kSortThreads >= re) continue;
       int32_t cx, cy;
       const uint32_t pos = atomicAdd(&h[key_of(v[u], cx, cy)], 1u);
+      if (staged && q.f > 1) {
+        sxy[pos - rb] = v[u];
+        sidx[pos - rb] = ix[u];
+        continue;
+      }
       q.sqx[pos] = v[u].x;
       q.sqy[pos] = v[u].y;
       if (q.f == 1) {  // true cells: only the cell path's clamped-bucket check reads them
@@ -542,6 +558,15 @@ __global__ __launch_bounds__(kSortThreads) void join_sort_finish_kernel(JoinRowA
         q.sqcy[pos] = cy;
       }
       q.sqidx[pos] = ix[u];
+    }
+  }
+  if (staged && q.f > 1) {  // the sorted row, coalesced
+    __syncthreads();
+    for (uint32_t t = threadIdx.x; t < re - rb; t += kSortThreads) {
+      const double2 v = sxy[t];
+      q.sqx[rb + t] = v.x;
+      q.sqy[rb + t] = v.y;
+      q.sqidx[rb + t] = sidx[t];
     }
   }
 }
@@ -1886,7 +1911,8 @@ hipError_t launch_join_rows(gf_ctx* ctx, const JoinRowArgs& a, const JoinQueryAr
       break;
     }
     case 2:
-      hipLaunchKernelGGL(join_sort_finish_kernel, dim3((unsigned)(q.qn + 3)), dim3(kSortThreads), 0, s, a, q);
+      hipLaunchKernelGGL(join_sort_finish_kernel, dim3((unsigned)(q.qn + 3)), dim3(kSortThreads),
+                         join_sort_lds_bytes(q.f, q.qn), s, a, q);
       break;
     case 3: {
       KTimer t(ctx, GF_K_JOIN_PROBE);
