@@ -239,11 +239,28 @@ __device__ __forceinline__ void queue_append2(bool c0, uint32_t i0, double x0, d
 // drain_own_queue at the block's end.  (Classifying them all at the end of each block cost
 // 21 us of a 74 us C3 window: no block's stream overlapped it.)
 constexpr int kWaveQ = 192;  // < 64 left after a round + one tile's 128
+// The bitmap words of the wave's last kWaveRing tiles stay in LDS (a ring, two words per tile),
+// so the bits of points the classification accepts later are OR-ed there (ds_or) and every word
+// reaches global memory once, when its tile leaves the ring or at the end of the stream.  (Each
+// accepted point of the span prefilter used to take a workgroup-scope atomic OR on the word the
+// wave had already stored: ~5e5 L2 atomics and 21 MB of partial-line writes per C3 window.)
+// Points whose tile already left the ring (sparse stretches) still take the atomic.
+constexpr int kWaveRing = 32;
 struct WaveQ {
   uint32_t* idx;
   double2* xy;
   uint32_t cnt;
+  unsigned long long* ring;  // [2 * kWaveRing]: tile k's words at 2 (k % kWaveRing) + {0, 1}
+  uint32_t ntile;            // tiles pushed so far (wave-uniform)
+  uint32_t t0, tstride;      // the wave's first tile and the tile stride (points)
 };
+// tile k of the wave leaves the ring: its words to global memory (the tail word only in range)
+__device__ __forceinline__ void ring_store(const RangeArgs& a, const WaveQ& q, uint32_t k) {
+  const int64_t t = (int64_t)q.t0 + (int64_t)k * q.tstride;
+  const uint32_t j = k % kWaveRing;
+  a.bitmap[t >> 6] = q.ring[2 * j];
+  if (t + 64 < a.n) a.bitmap[(t >> 6) + 1] = q.ring[2 * j + 1];
+}
 template <int POLY>
 __device__ __forceinline__ void waveq_round(const RangeArgs& a, const RangeLds& L, WaveQ& q, uint32_t take,
                                             uint64_t& hits, uint32_t* lcount) {
@@ -254,7 +271,13 @@ __device__ __forceinline__ void waveq_round(const RangeArgs& a, const RangeLds& 
   const int32_t slot = cell_slot<1>(a, L, v.x, v.y);
   const int cls = valid ? classify_finish<1>(a, v.x, v.y, slot, table_load(a, L, slot)) : kNone;
   const bool acc = cls == kAccept;
-  if (acc) bitmap_or(a.bitmap, i);
+  if (acc) {
+    const uint32_t k = (i - q.t0) / q.tstride;  // the point's tile of this wave
+    if (k + kWaveRing >= q.ntile)               // still in the ring
+      atomicOr(&q.ring[2 * (k % kWaveRing) + ((i >> 6) & 1u)], 1ull << (i & 63));
+    else
+      bitmap_or(a.bitmap, i);
+  }
   hits += (uint64_t)__popcll(__ballot(acc));
   queue_append2(cls == kTest, i, v.x, v.y, false, 0u, 0.0, 0.0, a, lcount);
   // the rest [take, cnt) moves to the front (all reads before the writes)
@@ -292,7 +315,14 @@ __device__ __forceinline__ void range_tile(const RangeArgs& a, int64_t t, double
   eval_point<TABLE, POLY, DEFER>(a, x1, y1, c1, v1, h1, m1, d1);
   const uint64_t b0 = __ballot(h0), b1 = __ballot(h1);
   const int64_t w = t >> 6;
-  if (DEFER != 2 && lane == 0) {  // the caller's bitmap is only 8-B aligned
+  if (DEFER == 3) {  // into the ring (the tile that leaves it goes to global memory)
+    const uint32_t k = wq.ntile++;
+    if (lane == 0) {
+      if (k >= (uint32_t)kWaveRing) ring_store(a, wq, k - kWaveRing);
+      wq.ring[2 * (k % kWaveRing)] = b0;
+      wq.ring[2 * (k % kWaveRing) + 1] = b1;
+    }
+  } else if (DEFER != 2 && lane == 0) {  // the caller's bitmap is only 8-B aligned
     a.bitmap[w] = b0;
     if (FULL || t + 64 < a.n) a.bitmap[w + 1] = b1;
   }
@@ -544,7 +574,7 @@ __device__ __forceinline__ void range_body(const RangeArgs& a) {
   uint64_t* const sm = sh + kBlock / 64;                           // [kBlock / 64] multiplicity
   uint32_t* const lds = lds_base + kRangeHdrWords;
   RangeLds L{nullptr, nullptr, nullptr, nullptr, nullptr};
-  WaveQ wq{nullptr, nullptr, 0u};
+  WaveQ wq{nullptr, nullptr, 0u, nullptr, 0u, (uint32_t)t0, (uint32_t)tstride};
   if (DEFER || TABLE) {
     if (threadIdx.x == 0) lcount = 0u;
     if (TABLE) {
@@ -580,6 +610,8 @@ __device__ __forceinline__ void range_body(const RangeArgs& a) {
         const int w = threadIdx.x >> 6;
         wq.xy = reinterpret_cast<double2*>(wb) + w * kWaveQ;
         wq.idx = reinterpret_cast<uint32_t*>(reinterpret_cast<double2*>(wb) + (kBlock / 64) * kWaveQ) + w * kWaveQ;
+        wq.ring = reinterpret_cast<unsigned long long*>(reinterpret_cast<double2*>(wb) + (kBlock / 64) * kWaveQ) +
+                  ((size_t)(kBlock / 64) * kWaveQ * 4 + 7) / 8 + (size_t)w * 2 * kWaveRing;
       }
     }
     __syncthreads();
@@ -599,6 +631,9 @@ __device__ __forceinline__ void range_body(const RangeArgs& a) {
   if (DEFER == 1) hits += drain_own_queue<POLY>(a, lcount);
   if (DEFER == 3) {
     if (wq.cnt > 0) waveq_round<POLY>(a, L, wq, wq.cnt, hits, &lcount);
+    // the ring's tiles to global memory (before the block's candidate tests OR into them)
+    const uint32_t lane = threadIdx.x & 63, held = wq.ntile < (uint32_t)kWaveRing ? wq.ntile : kWaveRing;
+    if (lane < held) ring_store(a, wq, wq.ntile - held + lane);
     hits += drain_own_queue<POLY>(a, lcount);
   }
   // per-block partial counts (plain stores; summed by range_finalize)
@@ -907,7 +942,7 @@ hipError_t launch_range(gf_ctx* ctx, const RangeArgs& a, int table_mode, int pol
                                            (a.xt ? 2 * sizeof(double) * (size_t)(a.grid_n + 1) : 0) +
                                            (a.span_lds ? (size_t)((a.span_bytes + 3) & ~3) : 0)
                                      : 0) +
-                     (a.span_mode ? 16 + (size_t)(kBlock / 64) * kWaveQ * (16 + 4) : 0);
+                     (a.span_mode ? 16 + (size_t)(kBlock / 64) * (kWaveQ * (16 + 4) + 8 + 16 * kWaveRing) : 0);
   {
     KTimer t(ctx, GF_K_RANGE_SCAN);
     if (!table_mode && !poly) hipLaunchKernelGGL((range_kernel<0, 0, 0, kRangeU>), g, b, lds, ctx->stream, a);
