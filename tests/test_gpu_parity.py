@@ -859,6 +859,34 @@ def test_join_dense_spot_and_capacity(sf, oracle_mod):
     assert big[0].item() == 0 and big[-1].item() == 0  # nothing written outside the buffer
 
 
+def test_join_band_global_window(sf, oracle_mod):
+    """Band probe (the fine path) when even a one-sub-column window of a band cannot be staged:
+    6000 query points inside one sub-cell (120 KB of staging against the ~86 KB budget) -- that
+    sub-column's candidates are read from global memory, the rest of the band from windows in LDS
+    -- plus a second dense spot that needs several windows; == the oracle, then the same window
+    again (regions sized from the first call's per-block counts)."""
+    g = sf.UniformGrid(1000, *BEIJING)
+    og = oracle_mod.grid(1000, *BEIJING)
+    x, y = oracle_mod.java_random_points(91, 300_000, *BEIJING)
+    qx, qy = oracle_mod.java_random_points(92, 50_000, *BEIJING)
+    rng = np.random.default_rng(93)
+    qx[:6000] = 116.4 + rng.uniform(0.0, 2e-4, 6000)      # one sub-cell (side 0.00105)
+    qy[:6000] = 40.0 + rng.uniform(0.0, 2e-4, 6000)
+    qx[6000:12000] = 116.1 + rng.uniform(0.0, 0.02, 6000)  # a dense stretch of one row band
+    qy[6000:12000] = 40.3 + rng.uniform(0.0, 2e-3, 6000)
+    x[:1500] = 116.4 + rng.uniform(-1e-3, 1.2e-3, 1500)
+    y[:1500] = 40.0 + rng.uniform(-1e-3, 1.2e-3, 1500)
+    x[1500:4000] = 116.1 + rng.uniform(0.0, 0.02, 2500)
+    y[1500:4000] = 40.3 + rng.uniform(0.0, 2e-3, 2500)
+    st, exp = oracle_mod.join_pp(og, og, x, y, qx, qy, 0.001)
+    assert st == 0 and len(exp) > 1_000_000
+    exp = exp[np.lexsort((exp[:, 1], exp[:, 0]))]
+    op = sf.PointPointJoinQuery(conf(sf), g)
+    wo, wq = win(sf, x, y), win(sf, qx, qy)
+    for _ in range(2):
+        np.testing.assert_array_equal(op.run(wo, wq, 0.001), exp)
+
+
 # ------------------------------------------------------------------ point-polygon join
 def test_join_ppoly_golden(sf):
     f = load("join_ppoly.npz")

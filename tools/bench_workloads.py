@@ -452,6 +452,15 @@ def bench_join(args):
     cap = 4 * (no + nq_rank)
     pairs = torch.empty(2 * cap, dtype=torch.int32, device=dev)
     npairs = C.c_int64()
+    # windows in flight (--join-streams, default 2): consecutive windows alternate over contexts --
+    # each its own stream, scratch, output buffer and region history -- so one window's kernels
+    # fill the other's launch gaps and latency-bound phases (the kNN plan's depth 3, the range
+    # bench's --range-streams); every window still runs its whole join
+    nstreams = max(1, getattr(args, "join_streams", 2))
+    ctxs = [ctx] + [_lib.Context(dev) for _ in range(nstreams - 1)]
+    if getattr(args, "join_stream", False):
+        for c_ in ctxs[1:]:
+            _lib.check(L.gf_ctx_set_flag(c_.handle, _lib.FLAG_JOIN_STREAM, 1), c_.handle, "flag")
     po = [w[2].c_struct() for w in ow]
     pq = [w[2].c_struct() for w in qw]
 
@@ -472,6 +481,11 @@ def bench_join(args):
     if 2 * cap > pairs.numel():
         del pairs
         pairs = torch.empty(2 * cap, dtype=torch.int32, device=dev)
+    outs = [pairs] + [torch.empty(2 * cap, dtype=torch.int32, device=dev) for _ in range(nstreams - 1)]
+    for c_ in ctxs[1:]:  # each context's region history from a call on the same windows
+        for i in range(2):
+            L.gf_join_pp(c_.handle, C.byref(grid.c_grid), C.byref(grid.c_grid), C.byref(po[i]), C.byref(pq[i]), r,
+                         0, 0, None, 0, C.byref(npairs))
 
     # default: gf_join_pp_async -- each window's launches queue behind the previous window (no
     # host wait for its pair count); the counts land in device memory, read after the final sync
@@ -479,14 +493,18 @@ def bench_join(args):
     totals = torch.zeros(max(args.steps, 1), dtype=torch.int64, device=dev)
 
     def step_async(i):
-        _lib.check(L.gf_join_pp_async(ctx.handle, C.byref(grid.c_grid), C.byref(grid.c_grid), C.byref(po[i % 2]),
-                                      C.byref(pq[i % 2]), r, 0, 0, pairs.data_ptr(), cap, totals[i].data_ptr()),
-                   ctx.handle, "gf_join_pp_async")
+        c_ = ctxs[i % nstreams]
+        _lib.check(L.gf_join_pp_async(c_.handle, C.byref(grid.c_grid), C.byref(grid.c_grid), C.byref(po[i % 2]),
+                                      C.byref(pq[i % 2]), r, 0, 0, outs[i % nstreams].data_ptr(), cap,
+                                      totals[i].data_ptr()), c_.handle, "gf_join_pp_async")
 
     for i in range(args.warmup):
         step(i)
     _sync(world)
-    ctx.set_timing((1 << _lib.K_JOIN_PROBE) | (1 << _lib.K_JOIN_BUCKET))
+    if use_async and nstreams > 1:  # the windows' inputs were produced before: no cross-stream waits
+        torch.cuda.synchronize()
+    for c_ in ctxs:
+        c_.set_timing((1 << _lib.K_JOIN_PROBE) | (1 << _lib.K_JOIN_BUCKET))
     _sync(world)
     t0 = time.perf_counter()
     total_pairs = 0
@@ -508,9 +526,12 @@ def bench_join(args):
 
         dist.barrier()
     elapsed = _reduce(elapsed, world, args, dev)
-    ms, cnt = ctx.timing(_lib.K_JOIN_PROBE)
-    bms, bcnt = ctx.timing(_lib.K_JOIN_BUCKET)
-    ctx.set_timing(0)
+    ms = cnt = bms = bcnt = 0
+    for c_ in ctxs:  # each context times its own windows' launches (HIP events on its stream)
+        m_, c1 = c_.timing(_lib.K_JOIN_PROBE)
+        b_, c2 = c_.timing(_lib.K_JOIN_BUCKET)
+        ms, cnt, bms, bcnt = ms + m_, cnt + c1, bms + b_, bcnt + c2
+        c_.set_timing(0)
     avg = ms / 1000.0 / max(cnt, 1)
     pp = total_pairs / args.steps
     pp_all = pp if world == 1 else _reduce_sum(pp, world, args, dev)
@@ -556,8 +577,10 @@ def bench_join(args):
           {"n_gpus": world,
            "config": {"workload": wl, "ordinary": no * world, "query": nq * world, "radius": r,
                       "pairs_per_window": pp_all, "query_per_rank_with_halo": nq_rank,
-                      "window_api": "gf_join_pp_async (windows queued back to back, counts read after the final sync)"
+                      "window_api": (f"gf_join_pp_async, {nstreams} windows in flight (consecutive windows alternate over "
+                                     f"{nstreams} contexts / streams; counts read after the final sync)")
                       if use_async else "gf_join_pp (pair count read back per window)",
+                      "windows_in_flight": nstreams if use_async else 1,
                       "parallelism": f"cell-column shards x{world}, query halo c columns (no collective)"},
            "breakdown": {"probe_us_per_launch": round(avg * 1e6, 2), "probe_launches_per_window": cnt / args.steps,
                          "probe_GBps_row_bucketed_in_pairs_out": round((20.0 * no + 8.0 * pp) / avg / 1e9, 1) if avg > 0 else None,
