@@ -1132,9 +1132,11 @@ int64_t orc_join_pp(const orc_grid* ugrid, const orc_grid* qgrid,
  * equals it; JoinFunction.join keeps (p, q) if approximate or getDistance(p, q) <= r
  * (DistanceFunctions.java:33-36).  A polygon's keys form a set, so a pair appears at most once.
  * Pairs come out grouped by point, polygons in replication order. */
-int64_t orc_join_ppoly(const orc_grid* ugrid, const orc_grid* qgrid, int64_t no, const double* ox,
-                       const double* oy, const orc_polygons* P, double r, int approximate, int metric,
-                       int64_t* out_pairs, int64_t cap) {
+/* The polygon side's replication (JoinQuery.getReplicatedPolygonQueryStream) as a key -> polygon
+ * CSR: cells holds every replicated key; the replicas of key slot s are lst[off[s] .. off[s+1]),
+ * in replication order. */
+static void ppoly_replicate(const orc_grid* qgrid, const orc_polygons* P, double r, strset* cells_out,
+                            int64_t** off_out, int64_t** lst_out) {
   char id[32];
   strset cells; /* every replicated key */
   ss_init(&cells, 1024);
@@ -1189,6 +1191,19 @@ int64_t orc_join_ppoly(const orc_grid* ugrid, const orc_grid* qgrid, int64_t no,
     for (int64_t t = 0; t < nrep; t++) lst[cur[slot[t]]++] = rep_q[t];
     free(cur);
   }
+  free(slot); free(rep_key); free(rep_q);
+  *cells_out = cells;
+  *off_out = off;
+  *lst_out = lst;
+}
+
+int64_t orc_join_ppoly(const orc_grid* ugrid, const orc_grid* qgrid, int64_t no, const double* ox,
+                       const double* oy, const orc_polygons* P, double r, int approximate, int metric,
+                       int64_t* out_pairs, int64_t cap) {
+  char id[32];
+  strset cells;
+  int64_t *off, *lst;
+  ppoly_replicate(qgrid, P, r, &cells, &off, &lst);
   int64_t cnt = 0;
   for (int64_t p = 0; p < no; p++) {
     int32_t cx, cy;
@@ -1204,7 +1219,7 @@ int64_t orc_join_ppoly(const orc_grid* ugrid, const orc_grid* qgrid, int64_t no,
       }
     }
   }
-  free(off); free(slot); free(lst); free(rep_key); free(rep_q);
+  free(off); free(lst);
   ss_free(&cells);
   return cnt;
 }
@@ -1665,6 +1680,105 @@ int64_t orc_join_pp_mt(const orc_grid* ugrid, const orc_grid* qgrid, int64_t no,
   free(res); free(off); free(slot); free(lst); free(rq.v); free(rk.v);
   ss_free(&cells);
   return cnt;
+}
+
+/* PointPolygonJoinQuery with parallelism T: the polygon stream's replication (serial, as the
+ * driver-side restatement in orc_join_ppoly), the points split into T contiguous parts -- each
+ * part's points keyed by gridID and joined with their key's replicas (JoinFunction.join: JTS
+ * distance per co-located pair).  Pairs (sorted by point, then polygon) out. */
+int64_t orc_join_ppoly_mt(const orc_grid* ugrid, const orc_grid* qgrid, int64_t no, const double* ox,
+                          const double* oy, const orc_polygons* P, double r, int approximate, int metric,
+                          int nthreads, int64_t* out_pairs, int64_t cap) {
+  const int T = nthreads < 1 ? 1 : nthreads;
+  strset cells;
+  int64_t *off, *lst;
+  ppoly_replicate(qgrid, P, r, &cells, &off, &lst);
+  lvec* res = (lvec*)calloc((size_t)T, sizeof(lvec));
+#pragma omp parallel num_threads(T)
+  {
+    const int t = omp_get_thread_num();
+    char id[32];
+    for (int64_t p = no * t / T; p < no * (t + 1) / T; p++) {
+      int32_t cx, cy;
+      orc_cell_of(ugrid, ox[p], oy[p], &cx, &cy);
+      orc_cell_id(cx, cy, id);
+      const int64_t s2 = ss_find(&cells, id);
+      if (s2 < 0) continue;
+      for (int64_t k = off[s2]; k < off[s2 + 1]; k++) {
+        const int64_t q = lst[k];
+        if (approximate || orc_point_polygon_distance(ox[p], oy[p], P, (int32_t)q, metric) <= r) {
+          lvec_push(&res[t], p);
+          lvec_push(&res[t], q);
+        }
+      }
+    }
+  }
+  int64_t cnt = gather_sorted(res, T, out_pairs, cap, 2);
+  free(res); free(off); free(lst);
+  ss_free(&cells);
+  return cnt;
+}
+
+/* PointPolygonKNNQuery with parallelism T: the polygon's G / C key sets built once, the window's
+ * points split into T contiguous parts (cell filter + JTS distance per point, as
+ * orc_knn_ppoly_contract), the parts' candidates concatenated and merged by the same contract
+ * (one entry per objID, (d, objID) order, first k): identical output. */
+int32_t orc_knn_ppoly_mt(const orc_grid* g, int64_t n, const double* x, const double* y, const int64_t* objID,
+                         const orc_polygons* P, double r, int32_t k, int approximate, int metric, int nthreads,
+                         int64_t* out_objID, double* out_d, int64_t* out_idx) {
+  const int T = nthreads < 1 ? 1 : nthreads;
+  strset G, C;
+  char id[32];
+  double x1, y1, x2, y2;
+  int32_t xi1, yi1, xi2, yi2;
+  if (k <= 0 || P->npoly != 1) return ORC_ERR_ARG;
+  ss_init(&G, 64); ss_init(&C, 64);
+  polygon_bbox(P, 0, &x1, &y1, &x2, &y2);
+  orc_cell_of(g, x1, y1, &xi1, &yi1);
+  orc_cell_of(g, x2, y2, &xi2, &yi2);
+  for (int64_t a = xi1; a <= xi2; a++)
+    for (int64_t b = yi1; b <= yi2; b++) { orc_cell_id((int32_t)a, (int32_t)b, id); g_cells_of(g, r, id, &G); }
+  for (int64_t a = xi1; a <= xi2; a++)
+    for (int64_t b = yi1; b <= yi2; b++) { orc_cell_id((int32_t)a, (int32_t)b, id); c_cells_of(g, r, id, &G, &C); }
+  tup* c = (tup*)malloc(sizeof(tup) * (size_t)(n > 0 ? n : 1));
+  int64_t* cnt = (int64_t*)calloc((size_t)T + 1, 8);
+#pragma omp parallel num_threads(T)
+  {
+    const int t = omp_get_thread_num();
+    char cid[32];
+    const int64_t b = n * t / T, e = n * (t + 1) / T;
+    int64_t m = b;  /* this part's candidates at c[b ..) */
+    for (int64_t i = b; i < e; i++) {
+      int32_t cx, cy;
+      orc_cell_of(g, x[i], y[i], &cx, &cy);
+      orc_cell_id(cx, cy, cid);
+      if (!(ss_contains(&C, cid) || ss_contains(&G, cid))) continue;
+      const double d = approximate ? orc_point_bbox_distance(x[i], y[i], x1, y1, x2, y2)
+                                   : orc_point_polygon_distance(x[i], y[i], P, 0, metric);
+      if (!(d <= r)) continue;
+      c[m].d = d; c[m].obj = objID[i]; c[m].idx = i; m++;
+    }
+    cnt[t] = m - b;
+  }
+  int64_t m = 0;
+  for (int t = 0; t < T; t++) {  /* compact the parts */
+    const int64_t b = n * t / T;
+    memmove(c + m, c + b, sizeof(tup) * (size_t)cnt[t]);
+    m += cnt[t];
+  }
+  free(cnt);
+  ss_free(&G); ss_free(&C);
+  qsort(c, (size_t)m, sizeof(tup), cmp_obj_d_idx);
+  int64_t u = 0;
+  for (int64_t i = 0; i < m; i++)
+    if (u == 0 || c[u - 1].obj != c[i].obj) c[u++] = c[i];
+  qsort(c, (size_t)u, sizeof(tup), cmp_d_obj);
+  const int32_t nout = (int32_t)(u < k ? u : k);
+  for (int32_t i = 0; i < nout; i++) {
+    out_objID[i] = c[i].obj; out_d[i] = c[i].d; out_idx[i] = c[i].idx;
+  }
+  free(c);
+  return nout;
 }
 
 /* CSVTSVToTSpatial.map on T threads: the chunk's lines split into T contiguous parts (the

@@ -143,6 +143,9 @@ int32_t orc_knn_scan_omp(const orc_grid* g, int64_t n, const double* x, const do
 int64_t orc_join_ppoly(const orc_grid* ugrid, const orc_grid* qgrid, int64_t no, const double* ox,
                        const double* oy, const orc_polygons* P, double r, int approximate, int metric,
                        int64_t* out_pairs, int64_t cap);
+int64_t orc_join_ppoly_mt(const orc_grid* ugrid, const orc_grid* qgrid, int64_t no, const double* ox,
+                          const double* oy, const orc_polygons* P, double r, int approximate, int metric,
+                          int nthreads, int64_t* out_pairs, int64_t cap);
 int64_t orc_join_pp(const orc_grid* ugrid, const orc_grid* qgrid,
                     int64_t no, const double* ox, const double* oy,
                     int64_t nq, const double* qx, const double* qy,
@@ -164,6 +167,9 @@ int32_t orc_knn_ppoly_contract(const orc_grid* g, int64_t n, const double* x, co
                                const int64_t* objID, const orc_polygons* P, double r, int32_t k,
                                int approximate, int metric, int64_t* out_objID, double* out_d,
                                int64_t* out_idx);
+int32_t orc_knn_ppoly_mt(const orc_grid* g, int64_t n, const double* x, const double* y, const int64_t* objID,
+                         const orc_polygons* P, double r, int32_t k, int approximate, int metric, int nthreads,
+                         int64_t* out_objID, double* out_d, int64_t* out_idx);
 
 /* Deserialization.CSVTSVToTSpatial.map over the lines of text (Deserialization.java:314-322):
  * want = csvTsvSchemaAttr (objID, time, x, y field indices).  Returns the line count (rows past

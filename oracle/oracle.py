@@ -76,12 +76,18 @@ def lib():
         L.orc_join_ppoly.argtypes = [C.POINTER(OrcGrid), C.POINTER(OrcGrid), i64, P, P, C.POINTER(OrcPolygons), d,
                                      C.c_int, C.c_int, P, i64]
         L.orc_join_ppoly.restype = i64
+        L.orc_join_ppoly_mt.argtypes = [C.POINTER(OrcGrid), C.POINTER(OrcGrid), i64, P, P, C.POINTER(OrcPolygons), d,
+                                        C.c_int, C.c_int, C.c_int, P, i64]
+        L.orc_join_ppoly_mt.restype = i64
         L.orc_generate_query_polygons.argtypes = [i32, d, d, d, d, P, P, i32]
         L.orc_generate_query_polygons.restype = i32
         L.orc_java_random_points.argtypes = [i64, i64, d, d, d, d, P, P]
         L.orc_knn_ppoly_contract.argtypes = [C.POINTER(OrcGrid), i64, P, P, P, C.POINTER(OrcPolygons), d, i32,
                                              C.c_int, C.c_int, P, P, P]
         L.orc_knn_ppoly_contract.restype = i32
+        L.orc_knn_ppoly_mt.argtypes = [C.POINTER(OrcGrid), i64, P, P, P, C.POINTER(OrcPolygons), d, i32,
+                                       C.c_int, C.c_int, C.c_int, P, P, P]
+        L.orc_knn_ppoly_mt.restype = i32
         L.orc_csv_parse.argtypes = [C.c_char_p, i64, C.c_char, P, P, P, C.c_char_p, i64, P, C.POINTER(i64), P, i64,
                                     C.POINTER(i64), C.POINTER(i32)]
         L.orc_csv_parse.restype = i64
@@ -343,6 +349,15 @@ def join_ppoly(ugrid, qgrid, ox, oy, P: Polygons, r, approximate=False, metric=M
         if cnt <= cap:
             return out[: 2 * cnt].reshape(-1, 2)
         cap = int(cnt)
+
+
+def join_ppoly_mt(ugrid, qgrid, ox, oy, P: "Polygons", r, nthreads, approximate=False, metric=METRIC_SQRT):
+    """orc_join_ppoly_mt: the point-polygon join with Flink parallelism nthreads (the polygon side
+    replicated once, the points in nthreads parts); sorted pairs[m, 2]."""
+    ox, oy = _f64(ox), _f64(oy)
+    return _grow(lambda out, cap: lib().orc_join_ppoly_mt(C.byref(ugrid), C.byref(qgrid), len(ox), _p(ox), _p(oy),
+                                                          C.byref(P.c), float(r), int(approximate), int(metric),
+                                                          int(nthreads), _p(out), cap), 1 << 16, 2)
 
 
 def generate_query_polygons(num, minX, minY, maxX, maxY):
@@ -672,6 +687,17 @@ def geojson_parse(text: bytes, prop_obj=None, prop_ts=None, date_fmt=0, tz_off_m
             continue
         x[i], y[i], t[i], o[i] = r
     return x, y, o, t, bad_line, bad_kind
+
+
+def knn_ppoly_mt(g, x, y, objID, P: "Polygons", r, k, nthreads, approximate=False, metric=METRIC_SQRT):
+    """orc_knn_ppoly_mt: knn_ppoly with Flink parallelism nthreads (identical output)."""
+    x, y, objID = _f64(x), _f64(y), np.ascontiguousarray(objID, np.int64)
+    oo = np.zeros(k, np.int64); od = np.zeros(k); oi = np.zeros(k, np.int64)
+    m = lib().orc_knn_ppoly_mt(C.byref(g), len(x), _p(x), _p(y), _p(objID), C.byref(P.c), float(r), int(k),
+                               int(approximate), int(metric), int(nthreads), _p(oo), _p(od), _p(oi))
+    if m < 0:
+        raise ValueError(f"orc_knn_ppoly_mt: {m}")
+    return m, oo[:m], od[:m], oi[:m]
 
 
 def knn_ppoly(g, x, y, objID, P: "Polygons", r, k, approximate=False, metric=METRIC_SQRT):

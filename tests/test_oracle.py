@@ -287,3 +287,32 @@ def test_multicore_baselines_equal_serial(oracle_mod, threads):
     ex, ey, eo, et, bl, bk = O.csv_parse(text, ",", (0, 1, 2, 3))
     mx, my, mt, mbl, mbk = O.csv_parse_mt(text, ",", (0, 1, 2, 3), threads)
     assert bl == mbl == -1 and np.array_equal(ex, mx) and np.array_equal(ey, my) and np.array_equal(et, mt)
+
+
+def test_join_ppoly_mt_matches_serial(oracle_mod):
+    """The point-polygon join's CPU baseline with Flink parallelism T (orc_join_ppoly_mt) returns
+    the serial restatement's pair set."""
+    import numpy as np
+
+    g = oracle_mod.grid(500, 115.5, 117.6, 39.6, 41.1)
+    x, y = oracle_mod.java_random_points(5, 100_000, 115.5, 117.6, 39.6, 41.1)
+    P = oracle_mod.Polygons(oracle_mod.generate_query_polygons(1000, 115.5, 39.6, 117.6, 41.1))
+    a = oracle_mod.join_ppoly(g, g, x, y, P, 0.001)
+    a = a[np.lexsort((a[:, 1], a[:, 0]))]
+    for T in (1, 3, 8):
+        assert np.array_equal(oracle_mod.join_ppoly_mt(g, g, x, y, P, 0.001, T), a)
+
+
+def test_knn_ppoly_mt_matches_serial(oracle_mod):
+    """Polygon kNN's CPU baseline with Flink parallelism T (orc_knn_ppoly_mt) == the serial contract."""
+    import numpy as np
+
+    g = oracle_mod.grid(500, 115.5, 117.6, 39.6, 41.1)
+    x, y = oracle_mod.java_random_points(6, 200_000, 115.5, 117.6, 39.6, 41.1)
+    obj = np.arange(len(x), dtype=np.int64) % 150_000  # duplicated objIDs: the dedupe matters
+    sq = [[(116.40, 39.91), (116.42, 39.91), (116.42, 39.93), (116.40, 39.93), (116.40, 39.91)]]
+    P = oracle_mod.Polygons([sq])
+    ref = oracle_mod.knn_ppoly(g, x, y, obj, P, 0.5, 50)
+    for T in (1, 4, 7):
+        got = oracle_mod.knn_ppoly_mt(g, x, y, obj, P, 0.5, 50, T)
+        assert got[0] == ref[0] and all(np.array_equal(a, b) for a, b in zip(got[1:], ref[1:]))

@@ -76,10 +76,6 @@ def _reduce_sum(v, world, args, dev):
     return float(t.item())
 
 
-def _cpu_line(value, unit, sample):
-    return {"value": round(value, 1), "unit": unit, "cores": 1, "kind": "port", "sample": sample}
-
-
 def _host_threads():
     """This process's CPU share (OMP_NUM_THREADS on the GPU box, else every core), the machine's
     core count and CPU model."""
@@ -664,9 +660,18 @@ def bench_pjoin(args):
         tc = time.perf_counter() - tc
         exp = sorted(map(tuple, exp.tolist()))
         if world == 1 and not args.no_cpu_baseline:
-            cpu = _cpu_line(m / tc, "points/s", f"first {m} points of window 0 x the 1000 polygons, 1 pass ({tc:.2f}s): "
-                            "oracle's reference-shaped join (polygons replicated to string keys, hash join on "
-                            "gridID, JTS distance per co-located pair), C restatement, 1 thread")
+            Pg = O.Polygons(raw)
+
+            def sorted_pairs(a_):
+                return a_[np.lexsort((a_[:, 1], a_[:, 0]))]
+            exp_arr = np.array(exp, dtype=np.int64).reshape(-1, 2)
+            cpu = _cpu_lines(args, "points/s", {
+                "mt": (m, lambda T: O.join_ppoly_mt(og, og, x[:m], y[:m], Pg, r, T),
+                       f"first {m} points of window 0 x the 1000 polygons (polygons replicated to string keys, hash "
+                       "join on gridID, JTS distance per co-located pair)"),
+                "single": (m, lambda T: sorted_pairs(O.join_ppoly(og, og, x[:m], y[:m], Pg, r)),
+                           f"first {m} points of window 0 x the 1000 polygons")},
+                lambda R: all(np.array_equal(R[k_], exp_arr) for k_ in ("mt", "single")))
         verified = bool(_reduce(float(got == exp), world, args, dev, op="min"))
     L.gf_range_plan_destroy(h)
     avg_scan = ms / 1000.0 / max(cnt, 1)
@@ -1179,15 +1184,20 @@ def bench_polyknn(args):
     if not args.no_verify:  # the first window against the oracle
         x, y, w = wins[args.warmup % 4]
         st, o, d, ix = recs.decode(args.warmup)
-        tc = time.perf_counter()
-        m, eo, ed, ei = O.knn_ppoly(O.grid(500, *BEIJING), x, y, np.arange(n, dtype=np.int64),
-                                    O.Polygons([P.rings]), args.radius, args.k)
-        tc = time.perf_counter() - tc
+        og, oP, oid = O.grid(500, *BEIJING), O.Polygons([P.rings]), np.arange(n, dtype=np.int64)
+        m, eo, ed, ei = O.knn_ppoly_mt(og, x, y, oid, oP, args.radius, args.k, _host_threads()[0])
         verified = bool(st == 0 and np.array_equal(o, eo) and np.array_equal(d, ed) and np.array_equal(ix, ei))
         if not args.no_cpu_baseline:
-            cpu = _cpu_line(n / tc, "points/s", f"the whole {n}-point window, 1 pass ({tc:.2f}s): oracle's C "
-                            "restatement of PointPolygonKNNQuery (polygon G/C cell filter, JTS point-polygon "
-                            "distance, bounded k-heap), 1 thread")
+            def same(res):
+                return all(r[0] == m and all(np.array_equal(a, b) for a, b in zip(r[1:], (eo, ed, ei)))
+                           for r in res.values())
+            cpu = _cpu_lines(args, "points/s", {
+                "mt": (n, lambda T: O.knn_ppoly_mt(og, x, y, oid, oP, args.radius, args.k, T),
+                       f"the whole {n}-point window: PointPolygonKNNQuery restated (polygon G/C cell filter, "
+                       "JTS point-polygon distance, objID dedupe, first k) over point parts"),
+                "single": (n, lambda T: O.knn_ppoly(og, x, y, oid, oP, args.radius, args.k),
+                           f"the whole {n}-point window"),
+            }, same)
     avg = sms / 1000.0 / max(scnt, 1)
     _line("polygon-query kNN k=%d" % args.k, n * args.steps / elapsed, "points/s", args.steps, args.warmup, elapsed,
           "knn_poly_scan", 16.0 * n, avg,
