@@ -110,10 +110,10 @@ def main():
                          "bucket: tools/bench_workloads.py")
     ap.add_argument("--range-blocks", default="0", help="range/ppoly scan blocks, comma list = sweep (0 = auto)")
     ap.add_argument("--range-defer", default="0", help="range/ppoly candidate tests: 0 auto, 1 inline, 2 deferred (list = sweep)")
-    ap.add_argument("--range-streams", type=int, default=2,
+    ap.add_argument("--range-streams", type=int, default=3,
                     help="range/ppoly: consecutive windows alternate over this many contexts (HIP streams)")
     ap.add_argument("--range-batch", type=int, default=0,
-                    help="range/ppoly: windows per gf_range_run_batch launch (0 = auto: 8 for windows of <= 2M "
+                    help="range/ppoly: windows per gf_range_run_batch launch (0 = auto: 16 for windows of <= 2M "
                          "points, else 1 = one gf_range_run per window)")
     ap.add_argument("--no-indices", action="store_true",
                     help="range/ppoly: leave the index list out of the step (bitmap + counts only; ablation)")

@@ -1220,6 +1220,9 @@ static int knn_alloc_lane(gf_knn_plan* P, int j, int64_t cap) {
 
 static int knn_alloc_candidates(gf_knn_plan* P, int64_t cap) {
   int st;
+  // queued windows may still read the old buffers (the k > kMaxK path queues without host reads)
+  GF_HIP_CHECK(P->ctx, hipStreamSynchronize(P->ctx->stream));
+  if (P->ctx->aux) GF_HIP_CHECK(P->ctx, hipStreamSynchronize(P->ctx->aux));
   for (int j = 0; j < 4; ++j)  // lanes 1.. only once pipelining allocated them
     if ((j == 0 || P->lane[j].st) && (st = knn_alloc_lane(P, j, cap))) return st;
   P->cap = cap;
@@ -1423,9 +1426,11 @@ static int knn_scan_select(gf_knn_plan* P, int j, const gf_points* pts, int64_t 
 }
 
 // k > kMaxK (KNNQuery.java:216 takes any k): every candidate within r (T = r; lane 0's buffers
-// hold the whole window, so nothing overflows), one host read of their count, then two stable
-// LSD radix sorts of the candidate permutation over 32-bit key fields (the K2 bucketing passes):
-// (objID, d, idx) -> the first entry of each objID -> those by (d, objID, idx) -> the first k.
+// hold the whole window, so nothing overflows), then two stable LSD radix sorts of the candidate
+// permutation over 32-bit key fields (the K2 bucketing passes): (objID, d, idx) -> the first
+// entry of each objID -> those by (d, objID, idx) -> the first k.  Grids and scratch are sized
+// by the window (an upper bound of the candidate count) and every kernel reads the counts on
+// the device: no host read, so windows queue back to back like the pipelined paths'.
 static int knn_large(gf_knn_plan* P, const gf_points* pts, void* result) {
   gf_ctx* ctx = P->ctx;
   int st;
@@ -1438,67 +1443,54 @@ static int knn_large(gf_knn_plan* P, const gf_points* pts, void* result) {
     const KnnScanArgs s = scan_args(P, 0, pts, 0, n, 0);  // T = r
     GF_HIP_CHECK(ctx, launch_knn_scan(ctx, s, scan_blocks_for(P, n), P->scan_unroll, P->scan_nt));
   }
-  unsigned long long m64 = 0;
-  if ((st = read_scalar_sync(ctx, &P->lane[0].st->count, &m64))) return st;
-  const int64_t m = (int64_t)m64;
-  // ready for the lane's next window (the select kernel does this on the other paths)
-  GF_HIP_CHECK(ctx, hipMemsetAsync(&P->lane[0].st->count, 0, sizeof(unsigned long long), ctx->stream));
-  GF_HIP_CHECK(ctx, hipMemsetAsync(&P->lane[0].st->maybe, 0, sizeof(unsigned long long), ctx->stream));
   const gf_knn_plan::Lane& L = P->lane[0];
-  const int blocks = (int)std::min<int64_t>(std::max<int64_t>((m + kRadixTile - 1) / kRadixTile / 4, 1), (int64_t)ctx->num_cus);
-  const int64_t mat = (int64_t)256 * blocks;  // 8-bit digits
-  const int64_t mm = std::max<int64_t>(m, 1);
+  const int64_t mm = std::max<int64_t>(n, 1);
+  const int nb = (int)std::min<int64_t>(std::max<int64_t>((mm + kRadixTile - 1) / kRadixTile / 4, 1), (int64_t)ctx->num_cus);
+  const int64_t mat = (int64_t)256 * nb;  // 8-bit digits
   Arena ar;
   size_t o_k[2] = {ar.take<uint32_t>(mm), ar.take<uint32_t>(mm)};
   size_t o_p[2] = {ar.take<uint32_t>(mm), ar.take<uint32_t>(mm)};
-  size_t o_flag = ar.take<uint32_t>(mm), o_off = ar.take<uint32_t>(mm + 1);
-  size_t o_m = ar.take<uint32_t>(mat), o_ms = ar.take<uint32_t>(mat + 1);
-  size_t o_tmp = ar.take<uint32_t>(std::max(scan_tmp_elems(mat), scan_tmp_elems(mm)));
+  size_t o_c = ar.take<uint32_t>(2), o_m = ar.take<uint32_t>(mat), o_ms = ar.take<uint32_t>(mat + 1);
   char* base = (char*)ctx_scratch(ctx, ar.off, &st);
   if (st) return st;
   auto U32 = [&](size_t o) { return (uint32_t*)(base + o); };
   KnnLargeArgs a{};
   a.cd = L.cand_d; a.co = L.cand_o; a.ci = L.cand_i; a.k = P->k; a.T = P->r; a.idx_base = P->idx_base;
-  a.result = result;
+  a.result = result; a.m = mm; a.cnt = U32(o_c);
+  a.lane_count = &L.st->count; a.lane_maybe = &L.st->maybe;
+  GF_HIP_CHECK(ctx, launch_knn_large(ctx, 5, a));                 // counts
   int cur = 0;  // the permutation lives in o_p[cur]
-  // stable sort of the first `cnt` entries of the permutation by key fields (least significant first)
-  auto sort_by = [&](int64_t cnt, std::initializer_list<int> fields) -> int {
-    if (cnt <= 1) return GF_OK;
-    const int nb = (int)std::min<int64_t>(std::max<int64_t>((cnt + kRadixTile - 1) / kRadixTile / 4, 1), (int64_t)ctx->num_cus);
-    const int64_t nmat = (int64_t)256 * nb;
+  // stable sort of the first cnt[pass] entries of the permutation by key fields (least
+  // significant first)
+  auto sort_by = [&](int pass, std::initializer_list<int> fields) -> int {
     for (int f : fields) {
-      a.m = cnt; a.perm = U32(o_p[cur]); a.field = f; a.keys = U32(o_k[0]);
+      a.perm = U32(o_p[cur]); a.field = f; a.keys = U32(o_k[0]); a.pass = pass;
       GF_HIP_CHECK(ctx, launch_knn_large(ctx, 1, a));
       for (int p = 0; p < 4; ++p) {  // 32 bits = 4 passes of 8
         RadixArgs r{};
-        r.n = cnt;
+        r.n = mm; r.n_dev = a.cnt + pass;
         r.kin = U32(o_k[p & 1]); r.vin = U32(o_p[cur]);
         r.kout = U32(o_k[(p + 1) & 1]); r.vout = U32(o_p[cur ^ 1]);
         r.shift = p * 8; r.bits = 8; r.nblk = nb; r.M = U32(o_m); r.Ms = U32(o_ms);
         GF_HIP_CHECK(ctx, launch_radix(ctx, 0, r, nb));
         ExpandState es;
-        if (int e = lookback_state(ctx, scan1_blocks(nmat), &es)) return e;
-        GF_HIP_CHECK(ctx, launch_scan1(ctx->stream, U32(o_m), nmat, U32(o_ms), nullptr, 0, 0, es));
-        ctx->expand_base += (unsigned long long)scan1_blocks(nmat);
+        if (int e = lookback_state(ctx, scan1_blocks(mat), &es)) return e;
+        GF_HIP_CHECK(ctx, launch_scan1(ctx->stream, U32(o_m), mat, U32(o_ms), nullptr, 0, 0, es));
+        ctx->expand_base += (unsigned long long)scan1_blocks(mat);
         GF_HIP_CHECK(ctx, launch_radix(ctx, 1, r, nb));
         cur ^= 1;
       }
     }
     return GF_OK;
   };
-  a.m = m; a.perm = U32(o_p[cur]);
+  a.perm = U32(o_p[cur]);
   GF_HIP_CHECK(ctx, launch_knn_large(ctx, 0, a));                 // identity permutation
-  if ((st = sort_by(m, {0, 1, 2, 3, 4}))) return st;               // (objID, d, idx)
-  a.m = m; a.perm = U32(o_p[cur]); a.flag = U32(o_flag);
-  GF_HIP_CHECK(ctx, launch_knn_large(ctx, 2, a));                 // first of each objID
-  GF_HIP_CHECK(ctx, launch_exclusive_scan(ctx->stream, U32(o_flag), m, U32(o_off), U32(o_tmp)));
-  a.off = U32(o_off); a.out = U32(o_p[cur ^ 1]);
-  GF_HIP_CHECK(ctx, launch_knn_large(ctx, 3, a));
+  if ((st = sort_by(0, {0, 1, 2, 3, 4}))) return st;               // (objID, d, idx)
+  a.perm = U32(o_p[cur]); a.out = U32(o_p[cur ^ 1]);
+  GF_HIP_CHECK(ctx, launch_knn_large(ctx, 2, a));                 // first of each objID -> cnt[1]
   cur ^= 1;
-  uint32_t nsurv = 0;  // survivors: their count sizes the second sort
-  if ((st = read_scalar_sync(ctx, U32(o_off) + m, &nsurv))) return st;
-  if ((st = sort_by(nsurv, {0, 3, 4, 1, 2}))) return st;          // (d, objID, idx)
-  a.perm = U32(o_p[cur]); a.nsurv = U32(o_off) + m; a.m = m;
+  if ((st = sort_by(1, {0, 3, 4, 1, 2}))) return st;               // (d, objID, idx)
+  a.perm = U32(o_p[cur]);
   GF_HIP_CHECK(ctx, launch_knn_large(ctx, 4, a));
   return GF_OK;
 }
@@ -1530,6 +1522,9 @@ int gf::knn_enqueue_merge(gf_knn_plan* P, const gf_points* pts, void* result, co
   if (st) return st;
   if ((st = check_points(ctx, pts))) return st;
   if (pts->n > 0 && !pts->objID) return set_err(ctx, GF_ERR_ARG, "kNN needs objID");
+  // k > kMaxK: the sorted path queues without host reads at every depth (its record is complete
+  // in stream order, earlier than a pipelined plan promises)
+  if (P->large) return knn_large(P, pts, result);
   if (P->pipeline == 3) {
     // window k scans on lane k % 4 and selects window k-2 in block 0; odd windows launch on the
     // aux stream, so consecutive windows' kernels overlap (ramp-up of one under the tail of the
@@ -1604,7 +1599,6 @@ int gf::knn_enqueue_merge(gf_knn_plan* P, const gf_points* pts, void* result, co
     P->pend_idx_base = P->idx_base;  // the index base in force when this window was enqueued
     return GF_OK;
   }
-  if (P->large) return knn_large(P, pts, result);
   // threshold: the previous window's hint (continuous query) or the sample; tiny windows
   // scan to r
   const bool staged = pts->n >= kSampleMinN;
@@ -1645,8 +1639,8 @@ extern "C" int gf_knn_plan_flush(gf_knn_plan* P) {
 extern "C" int gf_knn_plan_set_pipeline(gf_knn_plan* P, int depth) {
   if (!P || depth < 1 || depth > 3) return GF_ERR_ARG;
   gf_ctx* ctx = P->ctx;
-  if (depth >= 2 && P->k > 256)
-    return set_err(ctx, GF_ERR_ARG, "gf_knn_plan_set_pipeline: depth 2 / 3 needs k <= 256");
+  if (depth >= 2 && P->k > 256 && !P->large)
+    return set_err(ctx, GF_ERR_ARG, "gf_knn_plan_set_pipeline: depth 2 / 3 needs k <= 256 or k > 512");
   if (depth == 3 && P->poly)
     return set_err(ctx, GF_ERR_ARG, "gf_knn_plan_set_pipeline: polygon queries run at depth <= 2");
   int st = bind(ctx);

@@ -299,6 +299,7 @@ struct RadixArgs {
   int nblk;                 // blocks (chunks of whole tiles)
   uint32_t* M;              // stage 0: [digits][blocks]; stage 2: bucket sizes (zeroed)
   const uint32_t* Ms;       // stage 1: the exclusive scan of M
+  const uint32_t* n_dev;    // non-null: the item count is min(n, *n_dev), read on the device
 };
 size_t radix_scatter_lds_bytes();
 // stage 0 histogram, 1 scatter, 2 bucket sizes of the sorted kout
@@ -433,8 +434,10 @@ hipError_t launch_pane_bounds(hipStream_t s, const int64_t* ts, int64_t n, int64
 hipError_t launch_knn_sample(gf_ctx* ctx, const KnnSampleArgs& a);
 hipError_t launch_knn_scan(gf_ctx* ctx, const KnnScanArgs& a, int blocks, int unroll, int nt);
 hipError_t launch_knn_select(gf_ctx* ctx, const KnnSelectArgs& a);
-// k > kMaxK: candidate sorts (k_knn.hip).  op 0 iota perm, 1 key field -> keys, 2 first-of-objID
-// flags, 3 compact flagged perm entries to out, 4 the record
+// k > kMaxK: candidate sorts (k_knn.hip), sized on the host by the window (m >= the candidate
+// count) and bounded on the device by *cnt, so a window needs no host read.  op 0 iota perm,
+// 1 key field -> keys, 2 the first entry of each objID appended to out (count cnt[1]), 4 the
+// record, 5 start: cnt[0] = the lane's candidate count, cnt[1] = 0, lane counters reset
 struct KnnLargeArgs {
   const double* cd;
   const int64_t* co;
@@ -443,10 +446,11 @@ struct KnnLargeArgs {
   int64_t m;
   int field;
   uint32_t* keys;
-  uint32_t* flag;
-  const uint32_t* off;
   uint32_t* out;
-  const uint32_t* nsurv;
+  uint32_t* cnt;                 // [2] candidates, survivors
+  int pass;                      // ops 0 / 1: bounded by cnt[pass]
+  unsigned long long* lane_count;
+  unsigned long long* lane_maybe;
   int32_t k;
   double T;
   int64_t idx_base;

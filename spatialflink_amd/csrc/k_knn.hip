@@ -330,7 +330,8 @@ struct SelFull {
   };
   uint32_t wsum[kSelT / 64];
   int s_cnt, s_bin, s_maxpos;
-  uint32_t s_S;
+  uint32_t s_S, s_below;
+  unsigned long long s_rng[4];  // the k-th bin's key range (tie refinement): d min / max, objID min / max
 };
 struct SelLite {
   static constexpr int kCap = 256, kHBits = 9, kK = 256;
@@ -349,7 +350,8 @@ struct SelLite {
   };
   uint32_t wsum[kSelT / 64];
   int s_cnt, s_bin, s_maxpos;
-  uint32_t s_S;
+  uint32_t s_S, s_below;
+  unsigned long long s_rng[4];  // the k-th bin's key range (tie refinement): d min / max, objID min / max
 };
 static_assert(SelFull::kCap > kMaxK, "the general path needs room for the running list plus a chunk");
 static_assert(sizeof(SelLite) <= 29 * 1024, "fused kernel: 5 blocks per CU must fit the LDS");
@@ -520,6 +522,40 @@ __device__ __forceinline__ void lds_push(LDS& L, bool c, uint64_t d, uint64_t o,
   }
 }
 
+// The bin of L.hist holding the target-th entry (1-based): L.s_bin, L.s_S = base + entries in
+// bins <= it, L.s_below = base + entries below it (bin kDistBins - 1 with everything when the
+// histogram holds fewer).  16 bins per thread, block scan over 4 waves.
+template <class LDS>
+__device__ void kth_bin(LDS& L, uint32_t target, uint32_t base) {
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  constexpr int kB = kDistBins / kSelT;
+  uint32_t v[kB], s = 0;
+#pragma unroll
+  for (int j = 0; j < kB; ++j) { v[j] = L.hist[kB * tid + j]; s += v[j]; }
+  uint32_t inc = s;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t t = __shfl_up(inc, off, 64);
+    if (lane >= off) inc += t;
+  }
+  if (lane == 63) L.wsum[wid] = inc;
+  __syncthreads();
+  const uint32_t total = L.wsum[0] + L.wsum[1] + L.wsum[2] + L.wsum[3];
+  uint32_t before = 0;
+  for (int w = 0; w < wid; ++w) before += L.wsum[w];
+  const uint32_t excl = before + inc - s;
+  if (target > total) {
+    if (tid == kSelT - 1) { L.s_bin = kDistBins - 1; L.s_S = base + total; L.s_below = base + total - v[kB - 1]; }
+  } else if (excl < target && target <= excl + s) {
+    uint32_t run = excl;
+    for (int j = 0; j < kB; ++j) {
+      run += v[j];
+      if (run >= target) { L.s_bin = kB * tid + j; L.s_S = base + run; L.s_below = base + run - v[j]; break; }
+    }
+  }
+  __syncthreads();
+}
+
 #ifdef GF_TRACE  // phase timestamps (100 MHz wall clock) after the record, tools/trace_select.py
 #define GF_TR(j) do { if (threadIdx.x == 0) tr[j] = wall_clock64(); } while (0)
 #else
@@ -540,7 +576,7 @@ __device__ __forceinline__ void lds_push(LDS& L, bool c, uint64_t d, uint64_t o,
 template <class LDS, bool GENERAL>
 __device__ void knn_select_body(const KnnSelectArgs& a, LDS& L) {
   const int tid = threadIdx.x;
-  const int lane = tid & 63, wid = tid >> 6;
+  const int lane = tid & 63;
   const int k = a.k;
   constexpr int kPer = LDS::kCap / kSelT;
 #ifdef GF_TRACE
@@ -575,60 +611,93 @@ __device__ void knn_select_body(const KnnSelectArgs& a, LDS& L) {
     GF_TR(5);
   } else if (!overflow) {
     for (int i = tid; i < kDistBins; i += kSelT) L.hist[i] = 0u;
-    if (tid == 0) { L.s_bin = kDistBins - 1; L.s_S = (uint32_t)M; L.s_cnt = 0; }
+    if (tid == 0) { L.s_cnt = 0; }
     __syncthreads();
-    const bool staged = M <= LDS::kCap;
     const int64_t bbase = dist_bin_base(T);
-    if (staged) {
+    // every candidate once, f(valid, d, objID, idx): the first LDS::kCap from the registers
+    // loaded above, the rest from memory kU x 256 at a time with the loads issued together
+    // (these passes are latency-bound: a few thousand candidates at most)
+    constexpr int kU = GENERAL ? 4 : 2;
+    auto each = [&](auto&& f) {
 #pragma unroll
-      for (int j = 0; j < kPer; ++j)
-        if (tid + (int64_t)j * kSelT < M) atomicAdd(&L.hist[dist_bin(dv[j], bbase)], 1u);
-    } else {
-      for (int64_t i = tid; i < M; i += kSelT) atomicAdd(&L.hist[dist_bin(a.cand_d[i], bbase)], 1u);
-    }
+      for (int j = 0; j < kPer; ++j) f(tid + (int64_t)j * kSelT < M, dv[j], ov[j], iv[j]);
+      for (int64_t i0 = LDS::kCap; i0 < M; i0 += (int64_t)kU * kSelT) {  // block-uniform
+        double d[kU];
+        int64_t o[kU];
+        uint32_t x[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+          const int64_t i = i0 + (int64_t)u * kSelT + tid;
+          const bool in = i < M;
+          d[u] = in ? a.cand_d[i] : 0.0;
+          o[u] = in ? a.cand_o[i] : 0;
+          x[u] = in ? a.cand_i[i] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < kU; ++u) f(i0 + (int64_t)u * kSelT + tid < M, d[u], o[u], x[u]);
+      }
+    };
+    each([&](bool v, double d, int64_t, uint32_t) {
+      if (v) atomicAdd(&L.hist[dist_bin(d, bbase)], 1u);
+    });
     __syncthreads();
     GF_TR(2);
-    // bin holding the k-th candidate: 16 bins per thread, block scan over 4 waves
-    constexpr int kB = kDistBins / kSelT;
-    uint32_t v[kB], s = 0;
-#pragma unroll
-    for (int j = 0; j < kB; ++j) { v[j] = L.hist[kB * tid + j]; s += v[j]; }
-    uint32_t inc = s;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      const uint32_t t = __shfl_up(inc, off, 64);
-      if (lane >= off) inc += t;
-    }
-    if (lane == 63) L.wsum[wid] = inc;
-    __syncthreads();
-    uint32_t before = 0;
-    for (int w = 0; w < wid; ++w) before += L.wsum[w];
-    const uint32_t excl = before + inc - s;
-    if (excl < (uint32_t)k && (uint32_t)k <= excl + s) {
-      uint32_t run = excl;
-      for (int j = 0; j < kB; ++j) {
-        run += v[j];
-        if (run >= (uint32_t)k) { L.s_bin = kB * tid + j; L.s_S = run; break; }
-      }
-    }
-    __syncthreads();
+    // bin holding the k-th candidate
+    kth_bin(L, (uint32_t)k, 0u);
     GF_TR(3);
     const int bstar = L.s_bin;
-    if (L.s_S <= (uint32_t)LDS::kCap) {  // survivors (bins <= bstar) fit the sort area
-      if (staged) {
+    // Tie refinement: when the k-th bin alone overflows the sort area (points inside a query
+    // polygon all have d = 0; a dense ring of equal distances), split that bin by a second
+    // histogram over its own key range -- the distance bits, or the objID key when every
+    // distance in it is equal -- and keep the prefix (in (d, objID) order) up to the bucket
+    // of the k-th.  A prefix of the key order holds each of its objIDs' first entry, so its
+    // top k distinct are the window's whenever it has k distinct.
+    uint64_t cut_d = ~0ull, cut_o = ~0ull;
+    if (L.s_S > (uint32_t)LDS::kCap) {  // block-uniform
+      uint64_t r0 = ~0ull, r1 = 0ull, r2 = ~0ull, r3 = 0ull;
+      each([&](bool v, double d, int64_t o, uint32_t) {
+        if (v && dist_bin(d, bbase) == bstar) {
+          const uint64_t db = dbits(d), ok = okey(o);
+          r0 = db < r0 ? db : r0; r1 = db > r1 ? db : r1;
+          r2 = ok < r2 ? ok : r2; r3 = ok > r3 ? ok : r3;
+        }
+      });
 #pragma unroll
-        for (int j = 0; j < kPer; ++j) {
-          const bool c = tid + (int64_t)j * kSelT < M && dist_bin(dv[j], bbase) <= bstar;
-          lds_push(L, c, dbits(dv[j]), okey(ov[j]), (int64_t)iv[j]);
-        }
-      } else {
-        for (int64_t i0 = 0; i0 < M; i0 += kSelT) {  // block-uniform trip count
-          const int64_t i = i0 + tid;
-          const double d = i < M ? a.cand_d[i] : 0.0;
-          const bool c = i < M && dist_bin(d, bbase) <= bstar;
-          lds_push(L, c, dbits(d), c ? okey(a.cand_o[i]) : 0ull, c ? (int64_t)a.cand_i[i] : 0);
-        }
+      for (int off = 1; off < 64; off <<= 1) {
+        const uint64_t t0 = __shfl_xor(r0, off, 64), t1 = __shfl_xor(r1, off, 64);
+        const uint64_t t2 = __shfl_xor(r2, off, 64), t3 = __shfl_xor(r3, off, 64);
+        r0 = t0 < r0 ? t0 : r0; r1 = t1 > r1 ? t1 : r1; r2 = t2 < r2 ? t2 : r2; r3 = t3 > r3 ? t3 : r3;
       }
+      if (tid == 0) { L.s_rng[0] = ~0ull; L.s_rng[1] = 0ull; L.s_rng[2] = ~0ull; L.s_rng[3] = 0ull; }
+      for (int i = tid; i < kDistBins; i += kSelT) L.hist[i] = 0u;
+      __syncthreads();
+      if (lane == 0) {
+        atomicMin(&L.s_rng[0], r0); atomicMax(&L.s_rng[1], r1);
+        atomicMin(&L.s_rng[2], r2); atomicMax(&L.s_rng[3], r3);
+      }
+      __syncthreads();
+      const bool tie = L.s_rng[0] == L.s_rng[1];
+      const uint64_t kmin = tie ? L.s_rng[2] : L.s_rng[0], span = (tie ? L.s_rng[3] : L.s_rng[1]) - kmin;
+      const int bits = span ? 64 - __clzll((long long)span) : 0;
+      const int shift = bits > 12 ? bits - 12 : 0;  // kDistBins = 4096 buckets
+      each([&](bool v, double d, int64_t o, uint32_t) {
+        if (v && dist_bin(d, bbase) == bstar) atomicAdd(&L.hist[((tie ? okey(o) : dbits(d)) - kmin) >> shift], 1u);
+      });
+      __syncthreads();
+      const uint32_t below = L.s_below;
+      kth_bin(L, (uint32_t)k - below, below);
+      const int b2 = L.s_bin;
+      const uint64_t cut = b2 >= kDistBins - 1 ? ~0ull : kmin + ((((uint64_t)b2 + 1ull) << shift) - 1ull);
+      cut_d = tie ? L.s_rng[0] : cut;  // tie: every distance of the bin is equal
+      cut_o = tie ? cut : ~0ull;
+    }
+    if (L.s_S <= (uint32_t)LDS::kCap) {  // survivors (bins < bstar, bin bstar up to the cut) fit
+      each([&](bool v, double d, int64_t o, uint32_t x) {
+        const int b = dist_bin(d, bbase);
+        const uint64_t ok = okey(o);
+        const bool c = v && (b < bstar || (b == bstar && dbits(d) <= cut_d && ok <= cut_o));
+        lds_push(L, c, dbits(d), ok, (int64_t)x);
+      });
       __syncthreads();
       GF_TR(4);
       const int cnt = L.s_cnt;
@@ -724,75 +793,90 @@ __global__ __launch_bounds__(kSelT) void knn_select_kernel(KnnSelectArgs a) {
 // then the survivors by (d, objID, idx) -- and the first k are the record.  Kernels below; the
 // driver (api.cpp knn_large) reuses the K2 radix passes (k_points.hip).
 // ---------------------------------------------------------------------------------------
+__device__ __forceinline__ int64_t large_count(const KnnLargeArgs& a, int which) {
+  const int64_t c = (int64_t)a.cnt[which];
+  return c < a.m ? c : a.m;
+}
+
 // field: 0 idx, 1 d low word, 2 d high word (d >= 0: IEEE bits order as values), 3 objID low
 // word, 4 objID high word with the sign bit flipped (signed order)
-__global__ __launch_bounds__(kBlock) void knn_large_key_kernel(const double* __restrict__ cd,
-                                                               const int64_t* __restrict__ co,
-                                                               const uint32_t* __restrict__ ci,
-                                                               const uint32_t* __restrict__ perm, int64_t m,
-                                                               int field, uint32_t* __restrict__ kout) {
+__global__ __launch_bounds__(kBlock) void knn_large_key_kernel(KnnLargeArgs a) {
+  const int64_t m = large_count(a, a.pass);
   for (int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x; j < m; j += (int64_t)gridDim.x * kBlock) {
-    const uint32_t p = perm[j];
+    const uint32_t p = a.perm[j];
     uint32_t v;
-    switch (field) {
-      case 0: v = ci[p]; break;
-      case 1: v = lo32(cd[p]); break;
-      case 2: v = hi32(cd[p]); break;
-      case 3: v = (uint32_t)(uint64_t)co[p]; break;
-      default: v = (uint32_t)((uint64_t)co[p] >> 32) ^ 0x80000000u; break;
+    switch (a.field) {
+      case 0: v = a.ci[p]; break;
+      case 1: v = lo32(a.cd[p]); break;
+      case 2: v = hi32(a.cd[p]); break;
+      case 3: v = (uint32_t)(uint64_t)a.co[p]; break;
+      default: v = (uint32_t)((uint64_t)a.co[p] >> 32) ^ 0x80000000u; break;
     }
-    kout[j] = v;
+    a.keys[j] = v;
   }
 }
 
-__global__ __launch_bounds__(kBlock) void knn_large_iota_kernel(uint32_t* __restrict__ perm, int64_t m) {
+__global__ __launch_bounds__(kBlock) void knn_large_iota_kernel(KnnLargeArgs a) {
+  const int64_t m = large_count(a, 0);
   for (int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x; j < m; j += (int64_t)gridDim.x * kBlock)
-    perm[j] = (uint32_t)j;
+    a.perm[j] = (uint32_t)j;
 }
 
-// in (objID, d, idx) order: the first entry of every objID is its minimum -- the one the
-// reference's merge keeps (KNNQuery.java:232-251)
-__global__ __launch_bounds__(kBlock) void knn_large_first_kernel(const int64_t* __restrict__ co,
-                                                                 const uint32_t* __restrict__ perm, int64_t m,
-                                                                 uint32_t* __restrict__ flag) {
-  for (int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x; j < m; j += (int64_t)gridDim.x * kBlock)
-    flag[j] = j == 0 || co[perm[j]] != co[perm[j - 1]];
+// the window's candidate count into cnt[0] (the bound of the first sort), the survivor counter
+// zeroed, the lane ready for its next window (the select kernel does this on the other paths)
+__global__ void knn_large_start_kernel(KnnLargeArgs a) {
+  a.cnt[0] = (uint32_t)*a.lane_count;
+  a.cnt[1] = 0u;
+  *a.lane_count = 0ull;
+  *a.lane_maybe = 0ull;
 }
 
-__global__ __launch_bounds__(kBlock) void knn_large_compact_kernel(const uint32_t* __restrict__ perm,
-                                                                   const uint32_t* __restrict__ flag,
-                                                                   const uint32_t* __restrict__ off, int64_t m,
-                                                                   uint32_t* __restrict__ out) {
-  for (int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x; j < m; j += (int64_t)gridDim.x * kBlock)
-    if (flag[j]) out[off[j]] = perm[j];
+// in (objID, d, idx) order the first entry of every objID is its minimum -- the one the
+// reference's merge keeps (KNNQuery.java:232-251); the survivors are appended in any order
+// (one wave-aggregated atomic per wave step): the second sort's key (d, objID, idx) is total
+__global__ __launch_bounds__(kBlock) void knn_large_first_kernel(KnnLargeArgs a) {
+  const int64_t m = large_count(a, 0);
+  const int lane = threadIdx.x & 63;
+  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  for (int64_t j0 = (int64_t)blockIdx.x * kBlock + (threadIdx.x & ~63); j0 < m; j0 += stride) {  // wave-uniform
+    const int64_t j = j0 + lane;
+    uint32_t p = 0u;
+    bool first = false;
+    if (j < m) {
+      p = a.perm[j];
+      first = j == 0 || a.co[p] != a.co[a.perm[j - 1]];
+    }
+    const uint64_t bal = __ballot(first);
+    if (bal == 0ull) continue;
+    const int leader = __ffsll((unsigned long long)bal) - 1;
+    uint32_t base = 0u;
+    if (lane == leader) base = atomicAdd(&a.cnt[1], (uint32_t)__popcll(bal));
+    base = __shfl(base, leader, 64);
+    if (first) a.out[base + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull))] = p;
+  }
 }
 
 // the record: header + the first min(k, survivors) entries in (d, objID, idx) order
-__global__ __launch_bounds__(kBlock) void knn_large_record_kernel(const double* __restrict__ cd,
-                                                                  const int64_t* __restrict__ co,
-                                                                  const uint32_t* __restrict__ ci,
-                                                                  const uint32_t* __restrict__ perm,
-                                                                  const uint32_t* __restrict__ nsurv, int32_t k,
-                                                                  int64_t m, double T, int64_t idx_base,
-                                                                  void* result) {
-  gf_knn_header* h = reinterpret_cast<gf_knn_header*>(result);
-  const int32_t n = (int64_t)*nsurv < (int64_t)k ? (int32_t)*nsurv : k;
+__global__ __launch_bounds__(kBlock) void knn_large_record_kernel(KnnLargeArgs a) {
+  gf_knn_header* h = reinterpret_cast<gf_knn_header*>(a.result);
+  const int32_t k = a.k;
+  const int32_t n = (int64_t)a.cnt[1] < (int64_t)k ? (int32_t)a.cnt[1] : k;
   double* rd = reinterpret_cast<double*>(h + 1);
   int64_t* ro = reinterpret_cast<int64_t*>(rd + k);
   int64_t* ri = ro + k;
   for (int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x; j < n; j += (int64_t)gridDim.x * kBlock) {
-    const uint32_t p = perm[j];
-    rd[j] = cd[p];
-    ro[j] = co[p];
-    ri[j] = (int64_t)ci[p] + idx_base;
+    const uint32_t p = a.perm[j];
+    rd[j] = a.cd[p];
+    ro[j] = a.co[p];
+    ri[j] = (int64_t)a.ci[p] + a.idx_base;
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     h->status = 0;
     h->n = n;
     h->k = k;
     h->flags = 0;
-    h->candidates = m;
-    h->threshold = T;
+    h->candidates = a.cnt[0];
+    h->threshold = a.T;
   }
 }
 
@@ -805,16 +889,11 @@ hipError_t launch_knn_large(gf_ctx* ctx, int op, const KnnLargeArgs& a) {
   hipStream_t s = ctx->stream;
   const dim3 g(large_blocks(a.m)), b(kBlock);
   switch (op) {
-    case 0: hipLaunchKernelGGL(knn_large_iota_kernel, g, b, 0, s, a.perm, a.m); break;
-    case 1: hipLaunchKernelGGL(knn_large_key_kernel, g, b, 0, s, a.cd, a.co, a.ci, a.perm, a.m, a.field, a.keys); break;
-    case 2: hipLaunchKernelGGL(knn_large_first_kernel, g, b, 0, s, a.co, a.perm, a.m, a.flag); break;
-    case 3: hipLaunchKernelGGL(knn_large_compact_kernel, g, b, 0, s, a.perm, a.flag, a.off, a.m, a.out); break;
-    default: {
-      const dim3 gr(large_blocks(a.k));
-      hipLaunchKernelGGL(knn_large_record_kernel, gr, b, 0, s, a.cd, a.co, a.ci, a.perm, a.nsurv, a.k, a.m, a.T,
-                         a.idx_base, a.result);
-      break;
-    }
+    case 0: hipLaunchKernelGGL(knn_large_iota_kernel, g, b, 0, s, a); break;
+    case 1: hipLaunchKernelGGL(knn_large_key_kernel, g, b, 0, s, a); break;
+    case 2: hipLaunchKernelGGL(knn_large_first_kernel, g, b, 0, s, a); break;
+    case 5: hipLaunchKernelGGL(knn_large_start_kernel, dim3(1), dim3(1), 0, s, a); break;
+    default: hipLaunchKernelGGL(knn_large_record_kernel, dim3(large_blocks(a.k)), b, 0, s, a); break;
   }
   return hipGetLastError();
 }

@@ -156,11 +156,13 @@ __device__ __forceinline__ uint32_t bucket_key(double x, double y, const RadixAr
 
 // block b's chunk [beg, end) of the a.nblk chunks (whole tiles except the last)
 __device__ __forceinline__ void radix_chunk(const RadixArgs& a, int64_t& beg, int64_t& end) {
-  const int64_t tiles = (a.n + kRadixTile - 1) / kRadixTile;
+  int64_t n = a.n;
+  if (a.n_dev && (int64_t)*a.n_dev < n) n = (int64_t)*a.n_dev;
+  const int64_t tiles = (n + kRadixTile - 1) / kRadixTile;
   const int64_t per = (tiles + a.nblk - 1) / a.nblk;
   beg = (int64_t)blockIdx.x * per * kRadixTile;
-  end = beg + per * kRadixTile < a.n ? beg + per * kRadixTile : a.n;
-  if (beg > a.n) beg = a.n;
+  end = beg + per * kRadixTile < n ? beg + per * kRadixTile : n;
+  if (beg > n) beg = n;
 }
 
 template <bool FIRST>

@@ -3,7 +3,8 @@ plans keep every candidate within r and derive the record from two stable device
 ((objID, d, idx) -> first of each objID -> (d, objID, idx)); the exact re-evaluation of a
 flagged window takes the same path.  Results == the oracle's contract (orc_knn_contract /
 orc_knn_ppoly_contract), bit-exact, for point and polygon queries, duplicate objIDs, fewer
-distinct objIDs than k, clustered input; depths 2 / 3 and the sliding engine refuse k > 512."""
+distinct objIDs than k, clustered input.  The sorted path reads its counts on the device, so
+windows queue back to back (depths 2 / 3 accept k > 512); the sliding engine refuses k > 512."""
 import numpy as np
 import pytest
 
@@ -78,14 +79,50 @@ def test_polygon_knn_large_k(sf, oracle_mod):
     check(res, eo, ed, ei)
 
 
-def test_large_k_refuses_pipelines_and_sliding(sf):
+@pytest.mark.parametrize("depth", [1, 2, 3])
+def test_knn_large_k_queued_windows(sf, oracle_mod, depth):
+    """Several k > 512 windows enqueued back to back with no host read in between (records
+    written by the kernels straight into pinned host memory), then one flush: each record ==
+    the oracle's.  Window sizes shrink and grow (candidate buffers regrown in stream order)."""
+    import torch
+
+    g = sf.UniformGrid(500, *BEIJING)
+    og = oracle_mod.grid(500, *BEIJING)
+    q = sf.Point("q", *QPOINT, 0, g)
+    op = sf.PointPointKNNQuery(conf(sf), g)
+    k, r = 700, 0.2
+    data = []
+    for seed, n in ((31, 900_000), (32, 200_000), (33, 1_300_000), (34, 0), (35, 600_000)):
+        x, y = oracle_mod.java_random_points(seed, n, *BEIJING)
+        obj = (np.arange(n) % max(1, n // 3)).astype(np.int64)
+        data.append((x, y, obj, sf.PointWindow.from_numpy(x, y, obj)))
+    op.set_pipeline(0, q, r, k, depth)
+    order = [0, 1, 2, 3, 4, 2, 0]
+    rec = sf.PinnedRecords(len(order), k)
+    for i, j in enumerate(order):
+        op.enqueue(data[j][3], q, r, k, rec.ptr(i))
+    op.flush(0, q, r, k)
+    torch.cuda.synchronize()
+    for i, j in enumerate(order):
+        x, y, obj, w = data[j]
+        res = op.finish(w, q, r, k, rec.raw(i))
+        st, oo, od, oi = oracle_mod.knn(og, x, y, obj, QPOINT[0], QPOINT[1], r, k)
+        check(res, oo, od, oi)
+    op.set_pipeline(0, q, r, k, 1)
+
+
+def test_large_k_pipelines_and_sliding(sf):
+    """k in (256, 512] keeps depth 1 (the fused select in block 0 holds k <= 256); k > 512 takes
+    any depth; the sliding engine merges pane records of k <= 512 only."""
     from spatialflink_amd import _lib
 
     g = sf.UniformGrid(100, *BEIJING)
     q = sf.Point("q", *QPOINT, 0, g)
     op = sf.PointPointKNNQuery(conf(sf), g)
     with pytest.raises(ValueError):
-        op.set_pipeline(0, q, 0.5, 600, 2)
+        op.set_pipeline(0, q, 0.5, 300, 2)
+    op.set_pipeline(0, q, 0.5, 600, 2)
+    op.set_pipeline(0, q, 0.5, 600, 1)
     ctx, plan = op.plan(0, q, 0.5, 600)
     import ctypes as C
 

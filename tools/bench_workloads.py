@@ -232,6 +232,12 @@ def bench_range(args, polygons=False):
                 band = sharding.band_x_range(grid, lo, hi)
                 n = max(128, int(round(n_total * (hi - lo) / grid_n)))
         nwin = max(4, -(-384 * 2**20 // (16 * n)))
+        ns_ = max(1, args.range_streams)
+        batch = args.range_batch if args.range_batch > 0 else (16 if n <= 2_000_000 else 1)
+        batch = max(1, min(batch, 16))
+        # launch q (windows q*batch ..) runs on stream q % ns_; window j's buffers (points, bitmap,
+        # index list) are reused by window j + nwin, which then runs on the same stream
+        nwin = -(-nwin // (ns_ * batch)) * (ns_ * batch)
         wins = _windows(sf, n, nwin, 7 + 1000 * rank, dev, band)
         ctx = _lib.context(dev)
         if polygons:
@@ -270,13 +276,11 @@ def bench_range(args, polygons=False):
         counts = torch.zeros(nwin, 2, dtype=torch.int64, device=dev)
         # the step ends with the window's ascending index list on the device (what the Java
         # collector emits), produced by one async expansion launch after the scan
-        idx = torch.empty(4, n, dtype=torch.int32, device=dev)
+        idx = torch.empty(nwin, n, dtype=torch.int32, device=dev)  # window j's index list: idx[j]
         icount = torch.zeros(nwin, dtype=torch.int64, device=dev)
         pts = [w[2].c_struct() for w in wins]
 
         nstreams = len(plans)
-        batch = args.range_batch if args.range_batch > 0 else (8 if n <= 2_000_000 else 1)
-        batch = max(1, min(batch, 16, nwin))
         if batch > 1:  # windows i .. i+B-1 in one gf_range_run_batch (+ one index-list launch)
             P_ = C.c_void_p
             bms = [bitmaps[j].data_ptr() for j in range(nwin)]
@@ -288,7 +292,7 @@ def bench_range(args, polygons=False):
                 js = [(g + u) % nwin for u in range(batch)]
                 batch_args.append(((_lib.GfPoints * batch)(*[pts[j] for j in js]),
                                    (P_ * batch)(*[bms[j] for j in js]), (P_ * batch)(*[cnts[j] for j in js]),
-                                   (P_ * batch)(*[idx[(g + u) % 4].data_ptr() for u in range(batch)]),
+                                   (P_ * batch)(*[idx[j].data_ptr() for j in js]),
                                    (P_ * batch)(*[icnts[j] for j in js])))
 
         def step(i):
@@ -307,7 +311,7 @@ def bench_range(args, polygons=False):
             st = L.gf_range_run(plans[i % nstreams], C.byref(pts[j]), bitmaps[j].data_ptr(), None,
                                 counts[j].data_ptr())
             if not st and not args.no_indices:
-                st = L.gf_bitmap_to_indices_async(c, bitmaps[j].data_ptr(), n, idx[i % 4].data_ptr(), n,
+                st = L.gf_bitmap_to_indices_async(c, bitmaps[j].data_ptr(), n, idx[j].data_ptr(), n,
                                                   icount[j].data_ptr())
             if st:
                 _lib.check(st, c, "gf_range_run")
@@ -1160,6 +1164,9 @@ def bench_polyknn(args):
     wins = _windows(sf, n, 4, 61)
     op = sf.PointPolygonKNNQuery(sf.QueryConfiguration(sf.QueryType.WindowBased), grid)
     ctx, plan = op.plan(0, P, args.radius, args.k)
+    # polygon plans run at depth <= 2: window i's select rides in block 0 of window i+1's scan
+    depth = min(args.pipeline, 2)
+    _lib.check(L.gf_knn_plan_set_pipeline(plan, depth), ctx.handle, "pipeline")
     recs = sf.PinnedRecords(args.warmup + args.steps, args.k)
     pts = [w[2].c_struct() for w in wins]
 
@@ -1168,11 +1175,13 @@ def bench_polyknn(args):
 
     for i in range(args.warmup):
         step(i)
+    _lib.check(L.gf_knn_plan_flush(plan), ctx.handle, "flush")
     torch.cuda.synchronize()
     ctx.set_timing((1 << _lib.K_KNN_SCAN) | (1 << _lib.K_KNN_SAMPLE) | (1 << _lib.K_KNN_SELECT))
     t0 = time.perf_counter()
     for i in range(args.warmup, args.warmup + args.steps):
         step(i)
+    _lib.check(L.gf_knn_plan_flush(plan), ctx.handle, "flush")
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     sms, scnt = ctx.timing(_lib.K_KNN_SCAN)
@@ -1200,9 +1209,10 @@ def bench_polyknn(args):
             }, same)
     avg = sms / 1000.0 / max(scnt, 1)
     _line("polygon-query kNN k=%d" % args.k, n * args.steps / elapsed, "points/s", args.steps, args.warmup, elapsed,
-          "knn_poly_scan", 16.0 * n, avg,
+          "knn_poly_fused (prefilter scan + the previous window's select in block 0)" if depth == 2 else "knn_poly_scan",
+          16.0 * n, avg,
           {"config": {"workload": f"knn_ppoly_k{args.k}_r{args.radius}_{n // 1_000_000}Mpts_grid500_square0.02",
-                      "points_per_window": n, "k": args.k, "radius": args.radius},
+                      "points_per_window": n, "k": args.k, "radius": args.radius, "pipeline_depth": depth},
            "breakdown": {"scan_us": round(avg * 1e6, 2), "sample_us": round(1000 * pms / max(pcnt, 1), 2),
                          "select_us": round(1000 * lms / max(lcnt, 1), 2)},
            "fallback_windows": fallbacks, "verified_vs_oracle": verified,

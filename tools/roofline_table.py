@@ -30,7 +30,7 @@ PEAK = 8000.0  # GB/s (MI355X_MICROARCH.md)
 TAGS = [
     ("knn_k50_r0.5_10Mpts_per_gpu_grid500x500_clustered", None, None, None),
     ("knn_k50", "knn", r"knn_fused", r"knn_"),
-    ("knn_ppoly", "polyknn", r"knn_poly_scan", r"knn_"),
+    ("knn_ppoly", "polyknn", r"knn_poly_scan|knn_poly_fused", r"knn_"),
     ("range_pp_r0.5_1Mpts", "range1m", r"range_batch|range_kernel", r"range_|expand"),
     ("range_pp_r0.5_10Mpts", "range10m", r"range_kernel", r"range_|expand"),
     ("ppoly_", "ppoly", r"range_kernel", r"range_|expand"),

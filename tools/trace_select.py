@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
 """Phase timestamps of the kNN pipeline (trace build: `make trace`, GF_TRACE).  Prints the
 median per-phase durations over a run of continuous-query windows, hint on and off.
-Timestamps: 100 MHz wall clock (10 ns ticks) written by thread 0 of the select kernel."""
+Timestamps: 100 MHz wall clock (10 ns ticks) written by thread 0 of the select kernel.
+POLY=1: the polygon-query plan of `bench.py --workload polyknn` (0.02-degree square around the
+query point; the sample / scan timestamps then do not apply)."""
 import ctypes as C
 import os
 import sys
@@ -28,15 +30,24 @@ def main():
     for j in range(W):
         x, y = sf.synthetic_uniform(42 + j, n, *BEIJING[:4])
         wins.append(sf.PointWindow.from_numpy(x, y, np.arange(n, dtype=np.int64), device=0))
-    op = sf.PointPointKNNQuery(sf.QueryConfiguration(sf.QueryType.WindowBased), grid)
-    q = sf.Point("q", Q[0], Q[1], 0, grid)
-    ctx, plan = op.plan(0, q, 0.5, k)
+    if os.environ.get("POLY") == "1":
+        h = 0.01
+        ring = [(Q[0] - h, Q[1] - h), (Q[0] + h, Q[1] - h), (Q[0] + h, Q[1] + h), (Q[0] - h, Q[1] + h),
+                (Q[0] - h, Q[1] - h)]
+        op = sf.PointPolygonKNNQuery(sf.QueryConfiguration(sf.QueryType.WindowBased), grid)
+        ctx, plan = op.plan(0, sf.Polygon([ring], grid), 0.5, k)
+    else:
+        op = sf.PointPointKNNQuery(sf.QueryConfiguration(sf.QueryType.WindowBased), grid)
+        q = sf.Point("q", Q[0], Q[1], 0, grid)
+        ctx, plan = op.plan(0, q, 0.5, k)
     L = _lib.lib()
     rb = L.gf_knn_result_bytes(k)
     stride = rb + 128
-    base = C.c_void_p()
-    _lib.check(L.gf_pinned_alloc(stride * reps, C.byref(base)), None, "pinned")
-    buf = np.ctypeslib.as_array((C.c_uint8 * (stride * reps)).from_address(base.value))
+    # records (and the timestamps after them) in device memory: a store to mapped host memory
+    # holds every later barrier for a PCIe round trip (s_waitcnt vmcnt(0) counts stores)
+    dbuf = torch.zeros(stride * reps, dtype=torch.uint8, device="cuda")
+    base = C.c_void_p(dbuf.data_ptr())
+    buf = np.zeros(stride * reps, np.uint8)
     pts = [w.c_struct() for w in wins]
     names = ["load+zero", "hist", "binsearch", "compact", "sort+dedupe", "tail"]
     for hint in (1, 0):
@@ -44,10 +55,13 @@ def main():
         for i in range(8):
             L.gf_knn_enqueue(plan, C.byref(pts[i % W]), C.c_void_p(base.value + (i % reps) * stride))
         torch.cuda.synchronize()
-        buf[:] = 0
+        dbuf.zero_()
+        torch.cuda.synchronize()
         for i in range(reps):
             L.gf_knn_enqueue(plan, C.byref(pts[i % W]), C.c_void_p(base.value + i * stride))
+        L.gf_knn_plan_flush(plan)
         torch.cuda.synchronize()
+        buf[:] = dbuf.cpu().numpy()
         rows = []
         for i in range(1, reps):
             tr = np.frombuffer(buf[i * stride + rb: i * stride + rb + 96].tobytes(), np.uint64).astype(np.int64)
@@ -68,7 +82,6 @@ def main():
             for nm, v in zip(names + ["sample->scan start", "scan span", "scan end->select start", "select body",
                                       "prev select->sample", "survivors cnt"], m):
                 print(f"  {nm:24s} {v:8.2f}")
-    _lib.lib().gf_pinned_free(base)
 
 
 if __name__ == "__main__":
