@@ -222,14 +222,16 @@ int    gf_knn_pp_plan_create(gf_ctx* ctx, const gf_grid* g, double qx, double qy
 /* k <= 512: sample -> scan -> one-block select (pipeline depths 1..3).  k > 512 (the
  * reference's PriorityQueue takes any k, KNNQuery.java:216): every candidate within r is kept
  * and the record comes from two stable device radix sorts of them ((objID, d, idx) -> first of
- * each objID -> (d, objID, idx)); the enqueue reads two counts from the device (synchronizes),
- * pipeline depth 1 only, no sliding engine and no gf_knn_merge_dev (records of k <= 512).  The
- * exact re-evaluation of a flagged window (gf_knn_decode) takes the same sorted path. */
+ * each objID -> (d, objID, idx)); the passes are sized by the window and bounded by the counts
+ * on the device, so the enqueue never synchronizes and windows queue back to back at any
+ * pipeline depth (each record complete in stream order); no sliding engine and no
+ * gf_knn_merge_dev (records of k <= 512).  The exact re-evaluation of a flagged window
+ * (gf_knn_decode) takes the same sorted path. */
 /* PointPolygonKNNQuery.run(stream, queryPolygon, r, k) -- knn/PointPolygonKNNQuery.java:245-317:
  * kNN of the window's points to ONE query polygon (polys->npoly == 1): candidates have their cell
  * in C u G of the polygon's bbox cells and d <= r, d = JTS point-polygon distance (0 inside) or,
  * approximate, DistanceFunctions.getPointPolygonBBoxMinEuclideanDistance.  Same records, decode
- * and contract as point queries ((d, objID) order, one entry per objID); pipeline depth 1. */
+ * and contract as point queries ((d, objID) order, one entry per objID); pipeline depth <= 2. */
 int    gf_knn_ppoly_plan_create(gf_ctx* ctx, const gf_grid* g, const gf_polygons* polys, double r, int32_t k,
                                 int approximate, int metric, gf_knn_plan** out);
 void   gf_knn_plan_destroy(gf_knn_plan* plan);
@@ -244,7 +246,7 @@ int    gf_knn_plan_set_hint(gf_knn_plan* plan, int enable);
 /* Offset added to the window-local point index in results (a shard's first global index). */
 int    gf_knn_plan_set_index_base(gf_knn_plan* plan, int64_t base);
 /* Continuous-query pipeline.  depth 1 (default): each enqueue runs sample -> scan -> select,
- * stream-ordered.  depth 2 (k <= 256): ONE fused launch per window -- blocks 1.. scan window i
+ * stream-ordered.  depth 2 (k <= 256, or k > 512: see above): ONE fused launch per window -- blocks 1.. scan window i
  * with the threshold hint left by window i-2 (two device lanes), block 0 runs window i-1's
  * select meanwhile.  Window i's record is therefore written by the NEXT enqueue on the plan,
  * or by gf_knn_plan_flush (stream-ordered on the context stream).  No sample kernel: a cold
