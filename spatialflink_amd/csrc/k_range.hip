@@ -238,7 +238,15 @@ __device__ __forceinline__ void queue_append2(bool c0, uint32_t i0, double x0, d
 // OR into the word this wave stored), candidate-cell points go to the block's queue for
 // drain_own_queue at the block's end.  (Classifying them all at the end of each block cost
 // 21 us of a 74 us C3 window: no block's stream overlapped it.)
-constexpr int kWaveQ = 192;  // < 64 left after a round + one tile's 128
+// The tile's two halves are appended separately with a round in between, so the buffer holds
+// < 64 left after a round + one half's 64: 128 entries (192 before r03: the whole tile at once --
+// 5 KB more LDS per block, which held C3's blocks to 3 per CU).
+#ifndef GF_RANGE_WAVEQ
+#define GF_RANGE_WAVEQ 128
+#endif
+constexpr int kWaveQ = GF_RANGE_WAVEQ;
+static_assert(kWaveQ >= 127, "a round leaves < 64, a half-tile adds <= 64");
+constexpr int kRestIters = (kWaveQ - 64 + 63) / 64;  // entries left after a round, 64 per step
 // The bitmap words of the wave's last kWaveRing tiles stay in LDS (a ring, two words per tile),
 // so the bits of points the classification accepts later are OR-ed there (ds_or) and every word
 // reaches global memory once, when its tile leaves the ring or at the end of the stream.  (Each
@@ -282,16 +290,16 @@ __device__ __forceinline__ void waveq_round(const RangeArgs& a, const RangeLds& 
   queue_append2(cls == kTest, i, v.x, v.y, false, 0u, 0.0, 0.0, a, lcount);
   // the rest [take, cnt) moves to the front (all reads before the writes)
   const uint32_t rest = q.cnt - take;
-  uint32_t ri[2];
-  double2 rv[2];
+  uint32_t ri[kRestIters];
+  double2 rv[kRestIters];
 #pragma unroll
-  for (int k = 0; k < 2; ++k) {
+  for (int k = 0; k < kRestIters; ++k) {
     const uint32_t r = lane + 64 * k;
     ri[k] = r < rest ? q.idx[take + r] : 0u;
     rv[k] = r < rest ? q.xy[take + r] : make_double2(0.0, 0.0);
   }
 #pragma unroll
-  for (int k = 0; k < 2; ++k) {
+  for (int k = 0; k < kRestIters; ++k) {
     const uint32_t r = lane + 64 * k;
     if (r < rest) {
       q.idx[r] = ri[k];
@@ -338,18 +346,19 @@ __device__ __forceinline__ void range_tile(const RangeArgs& a, int64_t t, double
     const uint64_t q0 = __ballot(d0), q1 = __ballot(d1);
     const uint32_t n0 = (uint32_t)__popcll(q0);
     const uint64_t below = (1ull << lane) - 1ull;
-    if (d0) {
-      const uint32_t pos = wq.cnt + (uint32_t)__popcll(q0 & below);
-      wq.idx[pos] = (uint32_t)i0;
-      wq.xy[pos] = make_double2(x0, y0);
+    (void)n0;
+#pragma unroll 1
+    for (int h = 0; h < 2; ++h) {  // one round call site (inlined twice it spilled)
+      const bool d = h ? d1 : d0;
+      const uint64_t qm = h ? q1 : q0;
+      if (d) {
+        const uint32_t pos = wq.cnt + (uint32_t)__popcll(qm & below);
+        wq.idx[pos] = (uint32_t)(h ? i1 : i0);
+        wq.xy[pos] = h ? make_double2(x1, y1) : make_double2(x0, y0);
+      }
+      wq.cnt += (uint32_t)__popcll(qm);
+      if (wq.cnt >= 64) waveq_round<POLY>(a, L, wq, 64u, hits, lcount);  // leaves < 64
     }
-    if (d1) {
-      const uint32_t pos = wq.cnt + n0 + (uint32_t)__popcll(q1 & below);
-      wq.idx[pos] = (uint32_t)i1;
-      wq.xy[pos] = make_double2(x1, y1);
-    }
-    wq.cnt += n0 + (uint32_t)__popcll(q1);
-    while (wq.cnt >= 64) waveq_round<POLY>(a, L, wq, 64u, hits, lcount);
   } else if (DEFER) {
     queue_append2(d0, (uint32_t)i0, x0, y0, d1, (uint32_t)i1, x1, y1, a, lcount);
   }
