@@ -959,10 +959,13 @@ int ensure_queue(gf_range_plan* P, RangeArgs& a, int blocks, bool with_counts) {
   return GF_OK;
 }
 
-int scan_blocks_range(const gf_range_plan* P, int64_t n) {
+int scan_blocks_range(const gf_range_plan* P, int64_t n, bool span = false) {
   // every wave should run >= 2 pipeline stages of kRangeU tiles (range_kernel); at most 4
-  // blocks per CU (the sweep in tools/bench_workloads.py: 1024 blocks best at 10M points)
-  int blocks = (int)std::min<int64_t>(std::max<int64_t>(n / (4 * 128 * 2 * 2), 1), (int64_t)P->ctx->num_cus * 4);
+  // blocks per CU (the sweep in tools/bench_workloads.py: 1024 blocks best at 10M points), 2
+  // for the span prefilter (C3, three windows in flight: 48.9 us per window at 512 blocks,
+  // 51.5 at 1024; tools/gpu_r03_c3blocks.sh)
+  int blocks = (int)std::min<int64_t>(std::max<int64_t>(n / (4 * 128 * 2 * 2), 1),
+                                      (int64_t)P->ctx->num_cus * (span ? 2 : 4));
   if (P->scan_blocks > 0) blocks = P->scan_blocks;
   return std::min(blocks, 2048);  // queue segments / partial slots per window
 }
@@ -981,17 +984,18 @@ extern "C" int gf_range_run(gf_range_plan* P, const gf_points* pts, uint64_t* bi
     return GF_OK;
   }
   RangeArgs a = range_args(P, pts, bitmap, multi);
-  const int blocks = scan_blocks_range(P, pts->n);
   // Deferred tests pay a second launch; inline tests stall the waves holding candidate lanes.
   // Auto: defer while candidate cells are more than 5% of the non-none cells.
   const int64_t live = P->cls_cells[1] + P->cls_cells[2] + P->cls_cells[3];
   const bool can_defer = P->table_mode && (P->poly || !P->approx);
   const bool defer = can_defer && (P->defer_mode >= 2 || (P->defer_mode == 0 && P->cls_cells[1] * 20 > live));
+  // span prefilter when the class spans cover at most a quarter of the grid (defer_mode 3
+  // forces it): the stream skips the table, the block's queued points are classified after it
+  const bool span = defer && P->xt && (P->defer_mode == 3 || (P->defer_mode != 2 && P->span_frac <= 0.25));
+  const int blocks = scan_blocks_range(P, pts->n, span);
   if (defer) {
     if ((st = ensure_queue(P, a, blocks, false))) return st;
-    // span prefilter when the class spans cover at most a quarter of the grid (defer_mode 3
-    // forces it): the stream skips the table, the block's queued points are classified after it
-    a.span_mode = P->xt && (P->defer_mode == 3 || (P->defer_mode != 2 && P->span_frac <= 0.25));
+    a.span_mode = span;
   }
   // the counts are summed by the last block of the window's last kernel (no finalize launch)
   a.counts = counts;

@@ -11,8 +11,8 @@ mkdir -p $O
 S=tools/gpu_step.sh
 $S wl_knn 300 python -u bench.py --steps 50 --warmup 10 --cpu-seconds 5
 $S wl_range1m 300 python -u bench.py --workload range --points 1000000 --steps 800 --warmup 48 --cpu-seconds 5
-$S wl_range10m 300 python -u bench.py --workload range --points 10000000 --steps 50 --warmup 10 --cpu-seconds 5
-$S wl_ppoly 300 python -u bench.py --workload ppoly --steps 30 --warmup 5 --cpu-seconds 5
+$S wl_range10m 300 python -u bench.py --workload range --points 10000000 --steps 300 --warmup 30 --cpu-seconds 5
+$S wl_ppoly 300 python -u bench.py --workload ppoly --steps 300 --warmup 30 --cpu-seconds 5
 $S wl_join 300 python -u bench.py --workload join --steps 20 --warmup 5 --cpu-seconds 5
 $S wl_sliding 400 python -u bench.py --workload sliding --steps 20 --warmup 4 --cpu-seconds 5
 $S wl_csv 300 python -u bench.py --workload csv --steps 20 --warmup 3 --cpu-seconds 5
