@@ -438,7 +438,7 @@ extern "C" int gf_bucket_by_cell(gf_ctx* ctx, const gf_grid* g, const gf_points*
   }
   int bits = 1;
   while (((int64_t)1 << bits) < bins) ++bits;
-  const int passes = (bits + kRadixMaxBits - 1) / kRadixMaxBits, pbits = (bits + passes - 1) / passes;
+  const int passes = (bits + kBucketBits - 1) / kBucketBits, pbits = (bits + passes - 1) / passes;
   // one block per CU (the scatter's tile buffers), >= ~4 tiles per block
   const int64_t tiles = (n + kRadixTile - 1) / kRadixTile;
   const int blocks = (int)std::min<int64_t>(std::max<int64_t>(tiles / 4, 1), (int64_t)ctx->num_cus);

@@ -285,6 +285,11 @@ constexpr int kRadixMaxBits = 9;  // digit bits per pass (<=)
 constexpr int kRadixMaxDigits = 1 << kRadixMaxBits;
 constexpr int kRadixThreads = 1024;
 constexpr int kRadixTile = 8192;  // points per scatter tile (16 waves x 512)
+#ifndef GF_BUCKET_BITS
+#define GF_BUCKET_BITS 9
+#endif
+constexpr int kBucketBits = GF_BUCKET_BITS;  // K2 (gf_bucket_by_cell): digit bits per pass, <= kRadixMaxBits
+static_assert(kBucketBits >= 1 && kBucketBits <= kRadixMaxBits, "K2 digit bits");
 struct RadixArgs {
   const double* x;          // pass 0 input (kin == null): keys from the cells of x, y
   const double* y;
