@@ -18,6 +18,8 @@
 // below T (or T == r); otherwise it is flagged and gf_knn_decode re-evaluates the window
 // (sample path, then exhaustive T = r partitions).  Output: (d, objID) ascending, the
 // minimum-(d, idx) occurrence per objID.
+#include <type_traits>
+
 #include "gf_geom.hpp"
 #include "gf_internal.hpp"
 
@@ -618,7 +620,7 @@ __device__ void knn_select_body(const KnnSelectArgs& a, LDS& L) {
     // loaded above, the rest from memory kU x 256 at a time with the loads issued together
     // (these passes are latency-bound: a few thousand candidates at most)
     constexpr int kU = GENERAL ? 4 : 2;
-    auto each = [&](auto&& f) {
+    auto each_of = [&](auto&& f, auto with_oi) {
 #pragma unroll
       for (int j = 0; j < kPer; ++j) f(tid + (int64_t)j * kSelT < M, dv[j], ov[j], iv[j]);
       for (int64_t i0 = LDS::kCap; i0 < M; i0 += (int64_t)kU * kSelT) {  // block-uniform
@@ -630,16 +632,18 @@ __device__ void knn_select_body(const KnnSelectArgs& a, LDS& L) {
           const int64_t i = i0 + (int64_t)u * kSelT + tid;
           const bool in = i < M;
           d[u] = in ? a.cand_d[i] : 0.0;
-          o[u] = in ? a.cand_o[i] : 0;
-          x[u] = in ? a.cand_i[i] : 0u;
+          o[u] = in && decltype(with_oi)::value ? a.cand_o[i] : 0;
+          x[u] = in && decltype(with_oi)::value ? a.cand_i[i] : 0u;
         }
 #pragma unroll
         for (int u = 0; u < kU; ++u) f(i0 + (int64_t)u * kSelT + tid < M, d[u], o[u], x[u]);
       }
     };
-    each([&](bool v, double d, int64_t, uint32_t) {
+    auto each = [&](auto&& f) { each_of(f, std::true_type{}); };
+    // the distance histogram reads the distances alone (a cold window can hold ~10^6 candidates)
+    each_of([&](bool v, double d, int64_t, uint32_t) {
       if (v) atomicAdd(&L.hist[dist_bin(d, bbase)], 1u);
-    });
+    }, std::false_type{});
     __syncthreads();
     GF_TR(2);
     // bin holding the k-th candidate
