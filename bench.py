@@ -126,6 +126,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--join-stream", action="store_true",
                     help="join workload: experiment -- bucket only the query side, stream the ordinary points")
+    ap.add_argument("--poly-streams", type=int, default=3,
+                    help="polyknn: consecutive windows alternate over this many plans / contexts (HIP streams)")
     ap.add_argument("--join-streams", type=int, default=2,
                     help="join workload: windows in flight (consecutive windows alternate over this many contexts)")
     ap.add_argument("--join-sync", action="store_true",

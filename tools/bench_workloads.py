@@ -1145,7 +1145,10 @@ def bench_csv(args, geojson=False):
 def bench_polyknn(args):
     """Polygon-query kNN (PointPolygonKNNQuery.java:245-317, §8f row 4): k = 50, r = 0.5, a
     0.02-degree square around the README query point, 500 x 500 grid, 10M points per window,
-    continuous query over a ring of distinct windows (threshold hint carried), depth 1."""
+    continuous query over a ring of distinct windows (threshold hint carried), depth 2;
+    --poly-streams S: consecutive windows alternate over S plans on their own contexts (HIP
+    streams), so one window's launches ramp up under the other's tail (each plan carries the
+    hint of every S-th window)."""
     import torch
 
     import spatialflink_amd as sf
@@ -1167,27 +1170,50 @@ def bench_polyknn(args):
     # polygon plans run at depth <= 2: window i's select rides in block 0 of window i+1's scan
     depth = min(args.pipeline, 2)
     _lib.check(L.gf_knn_plan_set_pipeline(plan, depth), ctx.handle, "pipeline")
+    ctxs, plans = [ctx], [plan]
+    cs = sf.PolygonSet([P]).c_struct()
+    for _ in range(max(1, args.poly_streams) - 1):
+        c2 = _lib.Context(0)
+        h2 = C.c_void_p()
+        _lib.check(L.gf_knn_ppoly_plan_create(c2.handle, C.byref(grid.c_grid), C.byref(cs), float(args.radius),
+                                              int(args.k), 0, 0, C.byref(h2)), c2.handle, "plan")
+        _lib.check(L.gf_knn_plan_set_pipeline(h2, depth), c2.handle, "pipeline")
+        ctxs.append(c2)
+        plans.append(h2)
+    nst = len(plans)
     recs = sf.PinnedRecords(args.warmup + args.steps, args.k)
     pts = [w[2].c_struct() for w in wins]
 
     def step(i):
-        _lib.check(L.gf_knn_enqueue(plan, C.byref(pts[i % 4]), C.c_void_p(recs.ptr(i))), ctx.handle, "enqueue")
+        _lib.check(L.gf_knn_enqueue(plans[i % nst], C.byref(pts[i % 4]), C.c_void_p(recs.ptr(i))),
+                   ctxs[i % nst].handle, "enqueue")
+
+    def flush_all():
+        for c, pl in zip(ctxs, plans):
+            _lib.check(L.gf_knn_plan_flush(pl), c.handle, "flush")
+        for c in ctxs:
+            c.synchronize()
+        torch.cuda.synchronize()
 
     for i in range(args.warmup):
         step(i)
-    _lib.check(L.gf_knn_plan_flush(plan), ctx.handle, "flush")
-    torch.cuda.synchronize()
-    ctx.set_timing((1 << _lib.K_KNN_SCAN) | (1 << _lib.K_KNN_SAMPLE) | (1 << _lib.K_KNN_SELECT))
+    flush_all()
+    for c in ctxs:
+        c.set_timing((1 << _lib.K_KNN_SCAN) | (1 << _lib.K_KNN_SAMPLE) | (1 << _lib.K_KNN_SELECT))
     t0 = time.perf_counter()
     for i in range(args.warmup, args.warmup + args.steps):
         step(i)
-    _lib.check(L.gf_knn_plan_flush(plan), ctx.handle, "flush")
-    torch.cuda.synchronize()
+    flush_all()
     elapsed = time.perf_counter() - t0
-    sms, scnt = ctx.timing(_lib.K_KNN_SCAN)
-    pms, pcnt = ctx.timing(_lib.K_KNN_SAMPLE)
-    lms, lcnt = ctx.timing(_lib.K_KNN_SELECT)
-    ctx.set_timing(0)
+    sms = scnt = pms = pcnt = lms = lcnt = 0
+    for c in ctxs:
+        a_ms, a_n = c.timing(_lib.K_KNN_SCAN)
+        b_ms, b_n = c.timing(_lib.K_KNN_SAMPLE)
+        c_ms, c_n = c.timing(_lib.K_KNN_SELECT)
+        sms, scnt, pms, pcnt, lms, lcnt = sms + a_ms, scnt + a_n, pms + b_ms, pcnt + b_n, lms + c_ms, lcnt + c_n
+        c.set_timing(0)
+    for pl in plans[1:]:
+        L.gf_knn_plan_destroy(pl)
     fallbacks = sum(1 for i in range(args.warmup, args.warmup + args.steps) if recs.decode(i)[0] != 0)
     verified, cpu = None, None
     if not args.no_verify:  # the first window against the oracle
@@ -1208,13 +1234,18 @@ def bench_polyknn(args):
                            f"the whole {n}-point window"),
             }, same)
     avg = sms / 1000.0 / max(scnt, 1)
+    # windows in flight: a launch's own duration counts shared time several times, so the rate
+    # is bytes per window over the window interval (as the range lines)
+    basis = (f"bytes per window / window interval ({nst} streams; includes host work)" if nst > 1
+             else "bytes per window / average prefilter-scan launch")
     _line("polygon-query kNN k=%d" % args.k, n * args.steps / elapsed, "points/s", args.steps, args.warmup, elapsed,
           "knn_poly_fused (prefilter scan + the previous window's select in block 0)" if depth == 2 else "knn_poly_scan",
-          16.0 * n, avg,
+          16.0 * n, elapsed / args.steps if nst > 1 else avg,
           {"config": {"workload": f"knn_ppoly_k{args.k}_r{args.radius}_{n // 1_000_000}Mpts_grid500_square0.02",
-                      "points_per_window": n, "k": args.k, "radius": args.radius, "pipeline_depth": depth},
+                      "points_per_window": n, "k": args.k, "radius": args.radius, "pipeline_depth": depth,
+                      "windows_in_flight": nst},
            "breakdown": {"scan_us": round(avg * 1e6, 2), "sample_us": round(1000 * pms / max(pcnt, 1), 2),
-                         "select_us": round(1000 * lms / max(lcnt, 1), 2)},
+                         "select_us": round(1000 * lms / max(lcnt, 1), 2), "achieved_basis": basis},
            "fallback_windows": fallbacks, "verified_vs_oracle": verified,
            **({"cpu_baseline": cpu} if cpu else {})})
 

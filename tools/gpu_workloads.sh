@@ -16,7 +16,7 @@ $S wl_ppoly 300 python -u bench.py --workload ppoly --steps 300 --warmup 30 --cp
 $S wl_join 300 python -u bench.py --workload join --steps 20 --warmup 5 --cpu-seconds 5
 $S wl_sliding 400 python -u bench.py --workload sliding --steps 20 --warmup 4 --cpu-seconds 5
 $S wl_csv 300 python -u bench.py --workload csv --steps 20 --warmup 3 --cpu-seconds 5
-$S wl_polyknn 300 python -u bench.py --workload polyknn --steps 30 --warmup 5 --cpu-seconds 5
+$S wl_polyknn 300 python -u bench.py --workload polyknn --steps 200 --warmup 10 --cpu-seconds 5
 $S wl_pjoin 300 python -u bench.py --workload pjoin --steps 20 --warmup 3 --cpu-seconds 5
 $S wl_geojson 300 python -u bench.py --workload geojson --steps 20 --warmup 3 --cpu-seconds 5
 $S wl_bucket 300 python -u bench.py --workload bucket --steps 20 --warmup 3
