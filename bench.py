@@ -99,6 +99,50 @@ def cpu_baselines(args, O, og, window, gpu_result, n):
                                           "top-k-distinct heap, one merge)")}}
 
 
+def intern_fixed(sdict, prefix: bytes, values, digits: int):
+    """Intern the Strings prefix + "%0{digits}d" % v of int64 values into `sdict` (gf_objid_intern on
+    one fixed-width blob) -> int64 keys."""
+    v = np.asarray(values, np.int64)
+    w = len(prefix) + digits
+    a = np.empty((len(v), w), np.uint8)
+    a[:, :len(prefix)] = np.frombuffer(prefix, np.uint8)
+    for j in range(digits):
+        a[:, len(prefix) + j] = 48 + (v // 10 ** (digits - 1 - j)) % 10
+    offs = np.arange(len(v) + 1, dtype=np.int64) * w
+    keys = np.empty(len(v), np.int64)
+    from spatialflink_amd import _lib
+
+    _lib.check(_lib.lib().gf_objid_intern(sdict.handle, a.tobytes(), offs.ctypes.data, len(v), keys.ctypes.data),
+               sdict.ctx.handle, "gf_objid_intern")
+    return keys
+
+
+class PinnedStringRecords:
+    """A ring of string records (sharding.string_record_bytes) in mapped pinned host memory."""
+
+    def __init__(self, count: int, k: int, cap: int):
+        from spatialflink_amd import _lib, sharding
+
+        self.k, self.cap, self.count = int(k), int(cap), int(count)
+        self.bytes = sharding.string_record_bytes(k, cap)
+        p = ctypes.c_void_p()
+        _lib.check(_lib.lib().gf_pinned_alloc(self.bytes * self.count, ctypes.byref(p)), None, "gf_pinned_alloc")
+        self._base = p.value
+        self.view = np.ctypeslib.as_array((ctypes.c_uint8 * (self.bytes * self.count)).from_address(self._base))
+
+    def ptr(self, i: int) -> int:
+        return self._base + (i % self.count) * self.bytes
+
+    def decode(self, i: int):
+        """-> (status, objID ints parsed from "veh%09d", dist, idx)"""
+        from spatialflink_amd import sharding
+
+        j = i % self.count
+        st, strs, d, ix = sharding.decode_string_record(self.view[j * self.bytes:(j + 1) * self.bytes].tobytes(),
+                                                         self.k, self.cap)
+        return st, np.array([int(s_[3:]) for s_ in strs], np.int64), d, ix
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -143,6 +187,9 @@ def main():
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                     help="gloo: rehearse the N > 1 path with several ranks on one GPU (not a benchmark)")
     ap.add_argument("--scan-blocks", type=int, default=0, help="kNN scan grid (0 = auto: 4 blocks per CU)")
+    ap.add_argument("--string-objids", action="store_true",
+                    help="objIDs are dictionary Strings (\"veh%%09d\", MN_Q1.java:52's deviceId): N > 1 exchanges "
+                         "string records (gf_knn_attach_strings + gf_knn_merge_dev_strings)")
     ap.add_argument("--pipeline", type=int, default=3, choices=(1, 2, 3),
                     help="windows in flight: 2 overlaps window i's select with window i+1's scan; 3 also "
                          "overlaps consecutive windows' launches on two streams")
@@ -197,6 +244,19 @@ def main():
     torch.cuda.synchronize()
     log(f"[rank {rank}] {args.windows} window shards x {n} points, x in [{xlo}, {xhi}): "
         f"generated+uploaded in {time.perf_counter()-t:.2f}s")
+    sdict, scap = None, 0
+    if args.string_objids:
+        # every window of this rank carries the objIDs rank*n .. as the Strings "veh%09d", interned
+        # into this rank's own dictionary (ids assigned in this rank's first-occurrence order, so
+        # another rank's keys for the same String differ); "veh%09d" orders like its number, so the
+        # oracle on the integers is the String contract
+        t = time.perf_counter()
+        sdict = sf.ObjIdDict(dev.index)
+        keys = intern_fixed(sdict, b"veh", np.arange(rank * n, (rank + 1) * n, dtype=np.int64), 9)
+        kt = torch.from_numpy(keys).to(dev)
+        wins = [sf.PointWindow(w_.x, w_.y, kt, w_.timeStampMillisec) for w_ in wins]
+        scap = 16 * args.k + 64
+        log(f"[rank {rank}] {n} String objIDs interned in {time.perf_counter()-t:.2f}s")
     w = wins[0]
 
     conf = sf.QueryConfiguration(sf.QueryType.WindowBased)
@@ -213,6 +273,7 @@ def main():
     slots = torch.zeros(2, B, rb, dtype=torch.uint8, device=dev)  # two groups of B device records
     total_steps = args.warmup + args.steps
     host = sf.PinnedRecords(total_steps, args.k)
+    hstr = PinnedStringRecords(total_steps, args.k, scap) if (sdict is not None and world > 1) else None
     L = _lib.lib()
     pts = [w_.c_struct() for w_ in wins]
     pts_ref = [ctypes.byref(p_) for p_ in pts]
@@ -222,7 +283,10 @@ def main():
 
     def exchange(first, lo, hi):  # windows [lo, hi] of one group: one all-gather + one merge launch
         g = (lo - first) // B
-        sharding.allgather_knn_records_batch(slots[g % 2, : hi - lo + 1], args.k, host.ptr(lo))
+        if hstr is not None:  # String objIDs: the records travel with their Strings, merged by String
+            sharding.allgather_knn_records_strings(slots[g % 2, : hi - lo + 1], args.k, scap, sdict, hstr.ptr(lo))
+        else:
+            sharding.allgather_knn_records_batch(slots[g % 2, : hi - lo + 1], args.k, host.ptr(lo))
         if args.pipeline == 3:
             # depth 3 writes odd windows' records on the plan's second stream: it must not
             # reuse slots[g % 2] (group g + 2) before this all-gather + merge have read them
@@ -284,7 +348,12 @@ def main():
     per_window = {}
     fallbacks = 0
     for i in range(args.warmup, total_steps):
-        st, o, d, ix = host.decode(i)
+        if hstr is not None:
+            st, o, d, ix = hstr.decode(i)
+        else:
+            st, o, d, ix = host.decode(i)
+            if sdict is not None and st == 0:  # one rank: the keys of its own dictionary
+                o = np.array([int(s_[3:]) for s_ in sdict.decode_bytes(o)], np.int64)
         if st != 0:
             fallbacks += 1
             continue
@@ -443,10 +512,21 @@ def main():
         import glob
 
         kname = "knn_fused" if args.pipeline >= 2 else "knn_scan"
-        for f in sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{kname}_pmc.json")), reverse=True):
+        # newest round first: r<NN>_knn_pmc.json (tools/pmc_table.py: per-kernel medians) or the
+        # older r<NN>_<kernel>_pmc.json (one kernel, FETCH_SIZE / WRITE_SIZE summaries)
+        files = glob.glob(os.path.join(ROOT, "profiles", "r*_knn_pmc.json")) + \
+            glob.glob(os.path.join(ROOT, "profiles", f"r*_{kname}_pmc.json"))
+        for f in sorted(files, key=lambda f: os.path.basename(f).split("_")[0], reverse=True):
             with open(f) as fh:
                 pm = json.load(fh)
-            if pm.get("points_per_launch", n) == n and "FETCH_SIZE" in pm:
+            if "pmc" in pm:  # tools/pmc_table.py layout: the dominant kernel's entry
+                ent = [v for k_, v in pm["pmc"].items() if f"{kname}_kernel" in k_]
+                if ent and "hbm_read_bytes_corrected" in ent[0]:
+                    traffic = ent[0]["hbm_read_bytes_corrected"] + ent[0].get("hbm_write_bytes", 0.0)
+                    traffic_src = (os.path.relpath(f, ROOT) + f": rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE passes, "
+                                   f"median per {kname}_kernel launch, FETCH_SIZE x2 (gfx950)")
+                    break
+            elif pm.get("points_per_launch", n) == n and "FETCH_SIZE" in pm:
                 traffic = pm["FETCH_SIZE"]["corrected_bytes_per_launch"] + 1024.0 * pm["WRITE_SIZE"]["median_KB"]
                 traffic_src = (os.path.relpath(f, ROOT) + ": rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE passes, "
                                "median per launch, FETCH_SIZE x2 (gfx950)")
@@ -489,6 +569,8 @@ def main():
                 "parallelism": f"cell-column shards x{world}" + (" + RCCL all-gather top-k" if world > 1 else ""),
                 "windows_in_flight": args.pipeline,
                 "exchange_batch": B if world > 1 else None,
+                "objid": ("dictionary Strings" + (" (string records merged by String)" if world > 1 else ""))
+                         if args.string_objids else "canonical decimal (int64 keys)",
             },
             "roofline": {
                 "bound": "hbm",

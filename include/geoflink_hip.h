@@ -224,8 +224,8 @@ int    gf_knn_pp_plan_create(gf_ctx* ctx, const gf_grid* g, double qx, double qy
  * and the record comes from two stable device radix sorts of them ((objID, d, idx) -> first of
  * each objID -> (d, objID, idx)); the passes are sized by the window and bounded by the counts
  * on the device, so the enqueue never synchronizes and windows queue back to back at any
- * pipeline depth (each record complete in stream order); no sliding engine and no
- * gf_knn_merge_dev (records of k <= 512).  The exact re-evaluation of a flagged window
+ * pipeline depth (each record complete in stream order); the sliding engine and
+ * gf_knn_merge_dev(_batch) take records of any k.  The exact re-evaluation of a flagged window
  * (gf_knn_decode) takes the same sorted path. */
 /* PointPolygonKNNQuery.run(stream, queryPolygon, r, k) -- knn/PointPolygonKNNQuery.java:245-317:
  * kNN of the window's points to ONE query polygon (polys->npoly == 1): candidates have their cell
@@ -246,12 +246,16 @@ int    gf_knn_plan_set_hint(gf_knn_plan* plan, int enable);
 /* Offset added to the window-local point index in results (a shard's first global index). */
 int    gf_knn_plan_set_index_base(gf_knn_plan* plan, int64_t base);
 /* Continuous-query pipeline.  depth 1 (default): each enqueue runs sample -> scan -> select,
- * stream-ordered.  depth 2 (k <= 256, or k > 512: see above): ONE fused launch per window -- blocks 1.. scan window i
+ * stream-ordered.  depth 2 (k <= 256; larger k below): ONE fused launch per window -- blocks 1.. scan window i
  * with the threshold hint left by window i-2 (two device lanes), block 0 runs window i-1's
  * select meanwhile.  Window i's record is therefore written by the NEXT enqueue on the plan,
  * or by gf_knn_plan_flush (stream-ordered on the context stream).  No sample kernel: a cold
  * or failed hint flags the window (status 1, re-evaluated exactly by gf_knn_decode) and the
  * threshold adapts (shrinks after an overflow, doubles when fewer than k lie below it).
+ * k in (256, 512] at depth 2 / 3: the select needs the standalone kernel's sort area, so it is
+ * not fused: each window runs [sample] + scan + select on its lane, its record complete in stream
+ * order; depth 3 alternates two lanes between the context stream and the second stream (each
+ * lane's hint chain on one stream), so consecutive windows overlap.  k > 512: see above.
  * depth 3 (k <= 256): window i's fused launch selects window i-2; odd windows launch on a
  * second (non-blocking) stream, so consecutive launches overlap.  Window buffers must be
  * complete before their enqueue: no cross-stream wait is inserted for them (gf_ctx_fork after
@@ -282,7 +286,10 @@ int    gf_knn_run(gf_knn_plan* plan, const gf_points* pts, int64_t* objID, doubl
                   int64_t* idx, int32_t* n_out);
 /* Merge per-shard top-k records (device, `nrec` <= 64 contiguous records of
  * gf_knn_result_bytes(k)) into one record (async) -- the windowAll funnel across GPUs after
- * an RCCL all-gather.  `result` may be device memory or gf_pinned_alloc memory. */
+ * an RCCL all-gather.  `result` may be device memory or gf_pinned_alloc memory.  Any k
+ * (1 <= k <= 2^24): k <= 512 in one 256-thread block's LDS; larger k ranks every entry by binary
+ * searches in the other records (each is sorted by (d, objID, idx)) and dedupes objIDs through
+ * a hash table in the context's scratch, one 1024-thread block per window. */
 int    gf_knn_merge_dev(gf_ctx* ctx, int32_t k, const void* records, int32_t nrec, void* result);
 /* Batched: nwin windows in one launch (one block each), so one RCCL all-gather can carry the
  * records of several windows.  layout GF_MERGE_SHARD_MAJOR: record (shard s, window w) at
@@ -292,7 +299,7 @@ int    gf_knn_merge_dev(gf_ctx* ctx, int32_t k, const void* records, int32_t nre
  * ranks).  Dictionary objID keys (below GF_OBJID_NUMERIC_MIN, GF_OBJID_NULL aside) are ids in
  * their own context's gf_objid_dict, so keys of different ranks cannot be compared or deduped:
  * a window holding one gets status 2 (GF_KNN_STATUS_FOREIGN_KEYS) and no entries -- merge such
- * windows by their Strings instead (spatialflink_amd.sharding.allgather_knn_string_lists).
+ * windows by their Strings instead (gf_knn_attach_strings + gf_knn_merge_dev_strings below).
  * Canonical decimal objIDs are their values and merge across ranks. */
 #define GF_MERGE_SHARD_MAJOR  0
 #define GF_MERGE_WINDOW_MAJOR 1
@@ -300,6 +307,37 @@ int    gf_knn_merge_dev(gf_ctx* ctx, int32_t k, const void* records, int32_t nre
 #define GF_KNN_STATUS_FOREIGN_KEYS 2
 int    gf_knn_merge_dev_batch(gf_ctx* ctx, int32_t k, const void* records, int32_t nrec, int32_t nwin,
                               int32_t layout, void* results);
+/* ---- String objIDs across ranks (KNNQuery.java:232-251 dedupes by String.equals; MN_Q1.java:52
+ * feeds gps.deviceId Strings).  A dictionary key is an id in its own rank's dictionary, so the
+ * records travel with their Strings: a STRING RECORD is a kNN record followed by a sidecar
+ * {int32 status, int32 n, int64 nbytes, uint32 off[k+1] (8-aligned), bytes[cap_bytes]} holding
+ * the String of every dictionary objID of the record (entry i = bytes[off[i], off[i+1]), empty for
+ * canonical decimal / null keys); sidecar status 1 = the Strings needed more than cap_bytes.
+ *   rank r: gf_knn_attach_strings(its dictionary, its records) -> all-gather the string records
+ *   -> gf_knn_merge_dev_strings on every rank -> the same merged string record everywhere.
+ * The merge orders by (d, String, idx) -- dictionary Strings by their bytes (unsigned, a prefix
+ * first) and before canonical decimals, decimals by value (null last) -- and keeps the first
+ * entry of every String: rank independent.  (One rank's own select orders tied distances by
+ * dictionary id; the cross-rank order differs from it only between different Strings at exactly
+ * equal distances.)  The merged record's dictionary keys are the source ranks' and mean nothing
+ * elsewhere: read its Strings with gf_knn_string_record_decode.  An input record with status != 0
+ * or whose Strings did not fit gives status 2 (GF_KNN_STATUS_FOREIGN_KEYS) and no entries. */
+size_t gf_knn_string_record_bytes(int32_t k, int64_t cap_bytes);
+/* Async: nrec consecutive records (gf_knn_result_bytes(k) apart, device or pinned memory) ->
+ * nrec consecutive string records (gf_knn_string_record_bytes(k, cap_bytes) apart) with the
+ * Strings of their dictionary keys read from `dict` on the device. */
+int gf_knn_attach_strings(gf_objid_dict* dict, int32_t k, const void* records, int32_t nrec, int64_t cap_bytes,
+                          void* out);
+/* Async: as gf_knn_merge_dev_batch (layouts, nrec <= 64, one block per window, any k) over string
+ * records; results = nwin consecutive merged string records. */
+int gf_knn_merge_dev_strings(gf_ctx* ctx, int32_t k, int64_t cap_bytes, const void* records, int32_t nrec,
+                             int32_t nwin, int32_t layout, void* results);
+/* Host: decode a host copy of a string record: *status (0 ok, else the record's / 2), entries
+ * (objID keys, dist, idx; any may be null) and their Strings, String j = buf[offs[j], offs[j+1])
+ * (Long.toString for canonical decimal keys, empty for null); GF_ERR_CAPACITY when buf_cap is too
+ * small (offs[n] = the bytes needed). */
+int gf_knn_string_record_decode(const void* record, int32_t k, int64_t cap_bytes, int32_t* status, int64_t* objID,
+                                double* dist, int64_t* idx, char* buf, int64_t buf_cap, int64_t* offs, int32_t* n_out);
 /* Host merge of per-shard sorted lists: top-k distinct objIDs by (dist, objID). */
 int    gf_knn_merge_host(int32_t k, int32_t nlists, const int32_t* counts, const int64_t* objID,
                          const double* dist, const int64_t* idx, int64_t* out_objID,
@@ -316,8 +354,8 @@ int    gf_knn_merge_host(int32_t k, int32_t nlists, const int32_t* counts, const
  * pane ending at s + size, and fires only if it holds a point.  Result idx = the point's position
  * in the pushed stream (panes concatenated in push order). */
 typedef struct gf_knn_sliding gf_knn_sliding;
-/* size / gcd(size, slide) <= 64.  The plan's pipeline depth applies (depth 2: one fused launch
- * per pane). */
+/* size / gcd(size, slide) <= 64; any k (k > 512: pane records from the sorted path, merged by
+ * rank).  The plan's pipeline depth applies (depth 2: one fused launch per pane for k <= 256). */
 int  gf_knn_sliding_create(gf_knn_plan* plan, int64_t size_ms, int64_t slide_ms, gf_knn_sliding** out);
 void gf_knn_sliding_destroy(gf_knn_sliding* s);
 /* pane length, panes per window / per slide, and how many of the latest panes the engine keeps

@@ -3,7 +3,7 @@
  * INTEGRATION.md).  Every native is a thin wrapper: it checks the Java arguments (direct-buffer
  * capacities, array lengths), pins them, and calls ONE function of the plain-C core
  * (geoflink_shim.h), which makes the whole gf_* call sequence.  The core is compiled and run
- * without a JDK by tests/native/shim_check.c (tests/test_shim_native.py); this file needs jni.h,
+ * without a JDK as libgeoflink_shim.so, driven by tests/test_shim_native.py; this file needs jni.h,
  * which the build image lacks, so it is built on a machine with a JDK:
  *
  *   gcc -O2 -fPIC -shared -I$JAVA_HOME/include -I$JAVA_HOME/include/linux -Iinclude \

@@ -4,8 +4,9 @@
  *
  *   gcc -O2 -fPIC -c -Iinclude -I/opt/rocm/include -D__HIP_PLATFORM_AMD__ integration/jni/geoflink_shim.c
  *
- * and linked into libgeoflink_jni.so together with geoflink_jni.c (which needs a JDK), or into
- * tests/native/shim_check.c (which does not).
+ * and linked into libgeoflink_jni.so together with geoflink_jni.c (which needs a JDK), or built
+ * alone as integration/jni/libgeoflink_shim.so (Makefile target `shim`, no JDK), which
+ * tests/test_shim_native.py drives through ctypes.
  */
 #include "geoflink_shim.h"
 
@@ -267,7 +268,9 @@ int shim_sliding_push(shim_sliding* s, int64_t pane_index, const double* x, cons
   memset(&pts, 0, sizeof pts);
   *closed = 0;
   int st = GF_OK;
-  if (n > 0) st = upload(ctx, &s->wins[pane_index % s->nwin], x, y, objID, n, &pts);
+  /* floor mod: panes before the epoch (negative timestamps) have negative indices */
+  const int64_t slot = ((pane_index % s->nwin) + s->nwin) % s->nwin;
+  if (n > 0) st = upload(ctx, &s->wins[slot], x, y, objID, n, &pts);
   const int32_t k = s->next % SHIM_SLIDE_RECS;
   if (!st) st = gf_knn_sliding_push(s->s, pane_index, &pts, s->rec[k], closed, window_end);
   if (st) return fail(s->plan->c, st, "knnSlidingPush");

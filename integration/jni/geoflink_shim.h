@@ -3,8 +3,8 @@
  * GeoFlinkHip native is a thin JNI wrapper (direct-buffer addresses and capacities, Java arrays,
  * exceptions) around one function here, which makes the whole gf_* call sequence of that entry
  * on host pointers.  No JNI types, so the core is compiled and exercised without a JDK:
- * tests/native/shim_check.c calls each function the way its JNI wrapper does and compares the
- * results with the oracle (tests/test_shim_native.py: built on the CPU suite, run on the GPU).
+ * tests/test_shim_native.py calls each function of libgeoflink_shim.so (ctypes) the way its JNI
+ * wrapper does and compares the results with the oracle (built on the CPU suite, run on the GPU).
  *
  * Ownership: a shim_ctx is one Flink subtask's context (gf_ctx) plus the device buffers its
  * per-window calls reuse -- join windows, the ingest text buffer and columns, pinned result

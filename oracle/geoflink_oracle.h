@@ -209,4 +209,8 @@ int64_t orc_range_ppoly_omp(const orc_grid* g, int64_t n, const double* x, const
 int64_t orc_join_pp_omp(const orc_grid* grid, int64_t no, const double* ox, const double* oy, int64_t nq,
                         const double* qx, const double* qy, double r, int metric, int nthreads, int64_t* out_pairs,
                         int64_t cap);
+/* the same join's pair count, and *digest = sum mod 2^64 of fmix64(p << 32 | q) over its pairs */
+int64_t orc_join_pp_omp_digest(const orc_grid* grid, int64_t no, const double* ox, const double* oy, int64_t nq,
+                               const double* qx, const double* qy, double r, int metric, int nthreads,
+                               uint64_t* digest);
 #endif

@@ -106,6 +106,8 @@ def lib():
         L.orc_join_pp_mt.restype = i64
         L.orc_join_pp_omp.argtypes = [C.POINTER(OrcGrid), i64, P, P, i64, P, P, d, C.c_int, C.c_int, P, i64]
         L.orc_join_pp_omp.restype = i64
+        L.orc_join_pp_omp_digest.argtypes = [C.POINTER(OrcGrid), i64, P, P, i64, P, P, d, C.c_int, C.c_int, P]
+        L.orc_join_pp_omp_digest.restype = i64
         L.orc_csv_parse_mt.argtypes = [C.c_char_p, i64, C.c_char, P, P, P, P, i64, C.c_int, C.POINTER(i64),
                                        C.POINTER(i32)]
         L.orc_csv_parse_mt.restype = i64
@@ -324,6 +326,28 @@ def join_pp_mt(ugrid, qgrid, ox, oy, qx, qy, r, nthreads, metric=METRIC_SQRT, op
     return _grow(lambda out, cap: lib().orc_join_pp_mt(C.byref(ugrid), C.byref(qgrid), len(ox), _p(ox), _p(oy), len(qx),
                                                        _p(qx), _p(qy), float(r), 0, int(metric), int(nthreads), _p(out),
                                                        cap), 1 << 16, 2)
+
+
+def pair_digest(pairs) -> int:
+    """Order-independent digest of (p, q) pairs: sum mod 2^64 of fmix64(p << 32 | q) (numpy, the
+    oracle's orc_join_pp_omp_digest on the host side of a comparison)."""
+    k = (np.asarray(pairs, np.int64).reshape(-1, 2).astype(np.uint64) * np.array([1 << 32, 1], np.uint64)).sum(axis=1)
+    with np.errstate(over="ignore"):
+        k ^= k >> np.uint64(33); k *= np.uint64(0xff51afd7ed558ccd); k ^= k >> np.uint64(33)
+        k *= np.uint64(0xc4ceb9fe1a85ec53); k ^= k >> np.uint64(33)
+        return int(k.sum(dtype=np.uint64))
+
+
+def join_pp_digest(ugrid, ox, oy, qx, qy, r, nthreads, metric=METRIC_SQRT):
+    """(pair count, pair_digest) of the optimised OpenMP join, no pair stored (windows with
+    billions of pairs)."""
+    ox, oy, qx, qy = _f64(ox), _f64(oy), _f64(qx), _f64(qy)
+    dg = np.zeros(1, np.uint64)
+    cnt = lib().orc_join_pp_omp_digest(C.byref(ugrid), len(ox), _p(ox), _p(oy), len(qx), _p(qx), _p(qy), float(r),
+                                       int(metric), int(nthreads), _p(dg))
+    if cnt < 0:
+        raise ValueError(f"oracle join digest: status {cnt}")
+    return int(cnt), int(dg[0])
 
 
 def csv_parse_mt(text: bytes, delim: str, want, nthreads):

@@ -55,7 +55,8 @@ EXPORTS = [
     "gf_join_ppoly_plan_create", "gf_join_ppoly_run", "gf_join_ppoly",
     "gf_window_create",
     "gf_window_destroy", "gf_window_upload", "gf_window_points", "gf_synth_uniform", "gf_pinned_alloc",
-    "gf_pinned_free",
+    "gf_pinned_free", "gf_knn_string_record_bytes", "gf_knn_attach_strings", "gf_knn_merge_dev_strings",
+    "gf_knn_string_record_decode",
 ]
 
 
@@ -202,6 +203,10 @@ def lib():
             "gf_synth_uniform": ([i64, i64, d, d, d, d, P, P], C.c_int),
             "gf_pinned_alloc": ([sz, C.POINTER(P)], C.c_int),
             "gf_pinned_free": ([P], None),
+            "gf_knn_string_record_bytes": ([i32, i64], sz),
+            "gf_knn_attach_strings": ([P, i32, P, i32, i64, P], C.c_int),
+            "gf_knn_merge_dev_strings": ([P, i32, i64, P, i32, i32, i32, P], C.c_int),
+            "gf_knn_string_record_decode": ([P, i32, i64, pi32, P, P, P, P, i64, P, pi32], C.c_int),
         }
         for name, (argt, rest) in sig.items():
             fn = getattr(L, name)

@@ -1529,6 +1529,22 @@ int gf::knn_enqueue_merge(gf_knn_plan* P, const gf_points* pts, void* result, co
   // k > kMaxK: the sorted path queues without host reads at every depth (its record is complete
   // in stream order, earlier than a pipelined plan promises)
   if (P->large) return knn_large(P, pts, result);
+  if (P->pipeline >= 2 && P->k > kFusedSelectMaxK) {
+    // k in (256, 512]: the select needs the standalone kernel's sort area, so it is not fused;
+    // each window runs [sample] + scan + select on its lane, complete in stream order (earlier
+    // than the depth promises).  Depth 3 alternates lanes 0 / 1 between the context stream and
+    // the second stream: each lane's hint chain stays on one stream and consecutive windows'
+    // kernels overlap.
+    const uint64_t kseq = P->seq++;
+    const int j = P->pipeline == 3 ? (int)(kseq & 1) : 0;
+    hipStream_t main = ctx->stream;
+    if (j) ctx->stream = ctx->aux;
+    const bool staged = pts->n >= kSampleMinN;  // the sample kernel takes the lane's hint when it has one
+    int rc = staged ? knn_launch_sample(P, j, pts, P->use_hint) : GF_OK;
+    if (rc == GF_OK) rc = knn_scan_select(P, j, pts, 0, pts->n, staged ? 1 : 0, staged && P->use_hint, result);
+    ctx->stream = main;
+    return rc;
+  }
   if (P->pipeline == 3) {
     // window k scans on lane k % 4 and selects window k-2 in block 0; odd windows launch on the
     // aux stream, so consecutive windows' kernels overlap (ramp-up of one under the tail of the
@@ -1613,7 +1629,7 @@ int gf::knn_enqueue_merge(gf_knn_plan* P, const gf_points* pts, void* result, co
 extern "C" int gf_knn_plan_flush(gf_knn_plan* P) {
   if (!P) return GF_ERR_ARG;
   if (P->pipeline == 3) {
-    if (P->npq == 0) return GF_OK;
+    if (P->npq == 0) return P->k > kFusedSelectMaxK ? gf_ctx_join(P->ctx) : GF_OK;  // mid k: lane 1's stream
     gf_ctx* ctx = P->ctx;
     int st = bind(ctx);
     if (st) return st;
@@ -1643,17 +1659,18 @@ extern "C" int gf_knn_plan_flush(gf_knn_plan* P) {
 extern "C" int gf_knn_plan_set_pipeline(gf_knn_plan* P, int depth) {
   if (!P || depth < 1 || depth > 3) return GF_ERR_ARG;
   gf_ctx* ctx = P->ctx;
-  if (depth >= 2 && P->k > 256 && !P->large)
-    return set_err(ctx, GF_ERR_ARG, "gf_knn_plan_set_pipeline: depth 2 / 3 needs k <= 256 or k > 512");
   if (depth == 3 && P->poly)
     return set_err(ctx, GF_ERR_ARG, "gf_knn_plan_set_pipeline: polygon queries run at depth <= 2");
   int st = bind(ctx);
   if (st || (st = gf_knn_plan_flush(P))) return st;
   GF_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
   if (ctx->aux) GF_HIP_CHECK(ctx, hipStreamSynchronize(ctx->aux));
-  for (int j = 1; j < (depth == 3 ? 4 : depth); ++j)
+  // k > 512 plans return through knn_large (lane 0, stream-ordered) before any pipelined path:
+  // no extra lanes, no second stream
+  for (int j = 1; !P->large && j < (depth == 3 ? 4 : depth); ++j)
     if (!P->lane[j].st && (st = knn_alloc_lane(P, j, P->cap))) return st;
-  if (depth == 3 && !ctx->aux) GF_HIP_CHECK(ctx, hipStreamCreateWithFlags(&ctx->aux, hipStreamNonBlocking));
+  if (depth == 3 && !P->large && !ctx->aux)
+    GF_HIP_CHECK(ctx, hipStreamCreateWithFlags(&ctx->aux, hipStreamNonBlocking));
   P->pipeline = depth;
   P->seq = 0;
   for (int& w : P->lane_warm) w = 0;
@@ -1771,13 +1788,24 @@ extern "C" int gf_knn_run(gf_knn_plan* P, const gf_points* pts, int64_t* oo, dou
   return gf_knn_decode(P, pts, P->host_result, oo, od, oi, n_out);
 }
 
+// k > kMaxK merges rank entries in global scratch (the context's, stream-ordered)
+static int merge_scratch(gf_ctx* ctx, int32_t k, int32_t nrec, int32_t nwin, void** out) {
+  *out = nullptr;
+  if (k <= kMaxK) return GF_OK;
+  int st = GF_OK;
+  *out = ctx_scratch(ctx, merge_any_bytes(nrec, k) * (size_t)nwin, &st);
+  return st;
+}
+
 extern "C" int gf_knn_merge_dev(gf_ctx* ctx, int32_t k, const void* records, int32_t nrec, void* result) {
-  if (!ctx || k < 1 || k > kMaxK || nrec < 1 || nrec > 64 || !records || !result)
-    return set_err(ctx, GF_ERR_ARG, "gf_knn_merge_dev: need 1 <= nrec <= 64 and 1 <= k <= 512");
+  if (!ctx || k < 1 || k > kMaxKLarge || nrec < 1 || nrec > 64 || !records || !result)
+    return set_err(ctx, GF_ERR_ARG, "gf_knn_merge_dev: need 1 <= nrec <= 64 and 1 <= k <= 2^24");
   int st = bind(ctx);
   if (st) return st;
   const size_t rb = gf_knn_result_bytes(k);
-  GF_HIP_CHECK(ctx, launch_knn_merge(ctx, k, records, nrec, rb, 1, 0, result, 0, 0));
+  void* scratch;
+  if ((st = merge_scratch(ctx, k, nrec, 1, &scratch))) return st;
+  GF_HIP_CHECK(ctx, launch_knn_merge(ctx, k, records, nrec, rb, 1, 0, result, 0, 0, scratch));
   return GF_OK;
 }
 
@@ -1785,7 +1813,7 @@ extern "C" int gf_knn_merge_dev_batch(gf_ctx* ctx, int32_t k, const void* record
                                       int32_t layout, void* results) {
   const int foreign = (layout & GF_MERGE_FOREIGN_KEYS) != 0;
   layout &= ~GF_MERGE_FOREIGN_KEYS;
-  if (!ctx || k < 1 || k > kMaxK || nrec < 1 || nrec > 64 || nwin < 1 || nwin > 65535 || !records || !results ||
+  if (!ctx || k < 1 || k > kMaxKLarge || nrec < 1 || nrec > 64 || nwin < 1 || nwin > 65535 || !records || !results ||
       (layout != GF_MERGE_SHARD_MAJOR && layout != GF_MERGE_WINDOW_MAJOR))
     return set_err(ctx, GF_ERR_ARG, "gf_knn_merge_dev_batch: bad argument");
   int st = bind(ctx);
@@ -1794,7 +1822,10 @@ extern "C" int gf_knn_merge_dev_batch(gf_ctx* ctx, int32_t k, const void* record
   // shard-major = all_gather of each rank's [nwin] records: record (shard s, window w) at (s*nwin + w)*rb
   const size_t rec_stride = layout == GF_MERGE_SHARD_MAJOR ? (size_t)nwin * rb : rb;
   const size_t win_stride = layout == GF_MERGE_SHARD_MAJOR ? rb : (size_t)nrec * rb;
-  GF_HIP_CHECK(ctx, launch_knn_merge(ctx, k, records, nrec, rec_stride, nwin, win_stride, results, rb, foreign));
+  void* scratch;
+  if ((st = merge_scratch(ctx, k, nrec, nwin, &scratch))) return st;
+  GF_HIP_CHECK(ctx, launch_knn_merge(ctx, k, records, nrec, rec_stride, nwin, win_stride, results, rb, foreign,
+                                     scratch));
   return GF_OK;
 }
 

@@ -107,7 +107,8 @@ struct KTimer {
 // kernel argument blocks
 // ---------------------------------------------------------------------------------------
 constexpr int kBlock = 256;         // streaming kernels: 4 waves
-constexpr int kMaxK = 512;          // largest k on the device path
+constexpr int kMaxK = 512;          // largest k of the one-block select (larger k: the sorted path)
+constexpr int kFusedSelectMaxK = 256;  // largest k of the select fused into block 0 of a scan launch
 constexpr int kSampleBlocks = 128;  // kNN sample: 128 blocks x 2048 points = 256K points
 constexpr int kSamplePerBlock = 2048;
 constexpr int64_t kSampleMinN = 1 << 20;
@@ -473,14 +474,48 @@ struct KnnMergeArgs;
 // depth 2: prefilter of this window + (block 0) the previous window's select / window merge, then refine
 hipError_t launch_knn_poly_fused(gf_ctx* ctx, const KnnPolyArgs& a, const KnnSelectArgs& prev, int has_prev,
                                  int blocks, const KnnMergeArgs* merge);
+// k > kMaxK: the merge ranks every entry by binary searches in the other (sorted) records and
+// dedupes through a hash table, both in global scratch of merge_any_bytes(nrec, k) per window
+// (`scratch` may be null for k <= kMaxK)
+__host__ __device__ inline size_t merge_any_hash(int64_t e) {
+  size_t h = 1024;
+  while (h < 2 * (size_t)e) h <<= 1;
+  return h;
+}
+__host__ __device__ inline size_t merge_any_bytes(int32_t nrec, int32_t k) {
+  const int64_t e = (int64_t)nrec * k;
+  return ((size_t)e * 24 + merge_any_hash(e) * 12 + 255) & ~(size_t)255;
+}
 hipError_t launch_knn_merge(gf_ctx* ctx, int32_t k, const void* records, int32_t nrec, size_t rec_stride,
-                            int32_t nwin, size_t win_stride, void* result, size_t res_stride, int foreign);
+                            int32_t nwin, size_t win_stride, void* result, size_t res_stride, int foreign,
+                            void* scratch);
+// String records (gf_knn_attach_strings / gf_knn_merge_dev_strings): a kNN record followed by
+// the Strings of its dictionary objIDs -- {int32 status, int32 n, int64 nbytes, uint32 off[k+1],
+// bytes[cap]}; entry i's String = bytes[off[i], off[i+1]) (empty for canonical decimal keys)
+__host__ __device__ inline size_t str_side_off(int32_t k) { return ((size_t)4 * (k + 1) + 7) & ~(size_t)7; }
+__host__ __device__ inline size_t str_record_bytes(int32_t k, int64_t cap) {
+  return 32 + (size_t)24 * k + 16 + str_side_off(k) + (((size_t)cap + 7) & ~(size_t)7);
+}
+__host__ __device__ inline size_t strmerge_pow2(int64_t e) {
+  size_t p = 2;
+  while (p < (size_t)e) p <<= 1;
+  return p;
+}
+__host__ __device__ inline size_t strmerge_bytes(int32_t nrec, int32_t k) {
+  const int64_t e = (int64_t)nrec * k;
+  return ((size_t)e * 40 + strmerge_pow2(e) * 4 + strmerge_pow2(2 * e) * 8 + (size_t)k * 16 + 1024) & ~(size_t)255;
+}
+hipError_t launch_knn_attach_strings(gf_ctx* ctx, int32_t k, const unsigned long long* idmap, const char* arena,
+                                     int64_t dict_size, const void* records, int32_t nrec, int64_t cap, void* out);
+hipError_t launch_knn_merge_strings(gf_ctx* ctx, int32_t k, int64_t cap, const void* records, int32_t nrec,
+                                    size_t rec_stride, int32_t nwin, size_t win_stride, void* results, void* scratch);
 // records of one merge given as a pointer list (kernel argument; the panes of a sliding window)
 constexpr int kMaxMergeRecs = 64;
 struct KnnRecList {
   const char* rec[kMaxMergeRecs];
 };
-hipError_t launch_knn_merge_list(gf_ctx* ctx, int32_t k, const KnnRecList& list, int32_t nrec, void* result);
+hipError_t launch_knn_merge_list(gf_ctx* ctx, int32_t k, const KnnRecList& list, int32_t nrec, void* result,
+                                 void* scratch);
 // a window merge folded into block 0 of the next fused launch (after the select it waits for)
 constexpr int kFusedMergeMaxK = 128;
 struct KnnMergeArgs {

@@ -1387,7 +1387,16 @@ __device__ __forceinline__ void join_region_prep(const JoinFixup& f, uint64_t* w
   uint64_t T;
   band_scan(n, &T, ws);
   const uint64_t ov = __hip_atomic_load(o.ovf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const bool lost = E + ov > o.cap + o.spill_cap;
+  // lost = some pair was STORED past cap + spill_cap: region t holds [O, O + u), the overflow
+  // area [E, E + ov) (a region's unused tail past the limit loses nothing, so a count-only call,
+  // cap = spill_cap = 0, with no pairs reports 0, not cap + 1)
+  const uint64_t lim = o.cap + o.spill_cap;
+  uint64_t past = 0;
+  if (t < G) past = O + u > lim ? O + u - (O > lim ? O : lim) : 0;
+  else if (t == G) past = E + ov > lim ? E + ov - (E > lim ? E : lim) : 0;
+  uint64_t PAST;
+  band_scan(past, &PAST, ws);
+  const bool lost = PAST > 0;
   const bool fits = T <= o.cap && !lost;
   uint64_t hl = 0, hs = 0, sl = 0, ss = 0;
   if (t < G) {

@@ -981,6 +981,147 @@ __device__ void knn_merge_body(int32_t k, const Src& src, int32_t nrec, void* re
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Merge for k > kMaxK (KNNQuery.java:216 takes any k): the records no longer fit the LDS sort
+// area, but each is already sorted by (d, objID, idx) -- distinct keys within a record -- so
+// an entry's rank in the union is its position in its own record plus, for every other record,
+// the number of its entries below it (a binary search; ties between records go to the lower
+// record index, so ranks are a permutation).  Entries are placed by rank in global scratch,
+// the first occurrence of every objID is found through a hash table (objID -> lowest rank,
+// CAS insert + atomicMin), and a block scan over the keep flags emits the first k.  One
+// 1024-thread block per window.
+// ---------------------------------------------------------------------------------------
+constexpr int kMergeAnyT = 1024;
+
+template <class Src>
+__device__ void knn_merge_any_body(int32_t k, const Src& src, int32_t nrec, void* result, char* scratch, int foreign) {
+  __shared__ int s_off[kMaxMergeRecs + 1], s_status, s_foreign;
+  __shared__ uint32_t s_null, s_wsum[kMergeAnyT / 64];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  if (tid == 0) {
+    s_foreign = 0;
+    s_null = 0xFFFFFFFFu;
+    int off = 0, st = 0;
+    for (int r = 0; r < nrec; ++r) {
+      const gf_knn_header* h = (const gf_knn_header*)src(r);
+      s_off[r] = off;
+      off += h->status == 0 ? h->n : 0;
+      st = h->status > st ? h->status : st;
+    }
+    s_off[nrec] = off;
+    s_status = st;
+  }
+  const int64_t E = (int64_t)nrec * k;
+  const size_t H = merge_any_hash(E);
+  uint64_t* ed = reinterpret_cast<uint64_t*>(scratch);
+  uint64_t* eo = ed + E;
+  int64_t* ei = reinterpret_cast<int64_t*>(eo + E);
+  uint64_t* hkey = reinterpret_cast<uint64_t*>(ei + E);
+  uint32_t* hpos = reinterpret_cast<uint32_t*>(hkey + H);
+  for (size_t s = tid; s < H; s += kMergeAnyT) { hkey[s] = ~0ull; hpos[s] = 0xFFFFFFFFu; }
+  __syncthreads();
+  const int total = s_off[nrec];
+  // (1) ranks
+  for (int e = tid; e < total; e += kMergeAnyT) {
+    int r = 0;
+    while (s_off[r + 1] <= e) ++r;  // nrec <= 64
+    const int p = e - s_off[r];
+    const RecView in = rec_view((void*)src(r), k);
+    const int64_t o = in.o[p];
+    const uint64_t kd = dbits(in.d[p]), ko = okey(o);
+    const int64_t ki = in.i[p];
+    if (foreign && o < GF_OBJID_NUMERIC_MIN && o != GF_OBJID_NULL) s_foreign = 1;
+    int rank = p;
+    for (int q = 0; q < nrec; ++q) {
+      if (q == r) continue;
+      const RecView v = rec_view((void*)src(q), k);
+      int lo = 0, hi = s_off[q + 1] - s_off[q];  // first entry of q not below the key
+      while (lo < hi) {
+        const int m = (lo + hi) >> 1;
+        const uint64_t md = dbits(v.d[m]), mo = okey(v.o[m]);
+        const int64_t mi = v.i[m];
+        const bool below = q < r ? !kless(kd, ko, ki, md, mo, mi) : kless(md, mo, mi, kd, ko, ki);
+        if (below) lo = m + 1;
+        else hi = m;
+      }
+      rank += lo;
+    }
+    ed[rank] = kd; eo[rank] = ko; ei[rank] = ki;
+  }
+  __syncthreads();
+  // (2) the lowest rank of every objID (~0 = INT64_MAX, the table's empty marker: its own minimum)
+  for (int p = tid; p < total; p += kMergeAnyT) {
+    const uint64_t o = eo[p];
+    if (o == ~0ull) {
+      atomicMin(&s_null, (uint32_t)p);
+      continue;
+    }
+    size_t h = (size_t)((o * 0x9E3779B97F4A7C15ull) >> 20) & (H - 1);
+    for (;;) {
+      const unsigned long long prev = atomicCAS((unsigned long long*)&hkey[h], ~0ull, o);
+      if (prev == ~0ull || prev == o) break;
+      h = (h + 1) & (H - 1);
+    }
+    atomicMin(&hpos[h], (uint32_t)p);
+  }
+  __syncthreads();
+  // (3) the first k kept entries, in rank order
+  RecView out = rec_view(result, k);
+  const int status = s_foreign ? GF_KNN_STATUS_FOREIGN_KEYS : s_status;
+  int base = 0;
+  for (int p0 = 0; p0 < total && base < k; p0 += kMergeAnyT) {  // block-uniform
+    const int p = p0 + tid;
+    bool keep = false;
+    if (p < total) {
+      const uint64_t o = eo[p];
+      if (o == ~0ull) {
+        keep = s_null == (uint32_t)p;
+      } else {
+        size_t h = (size_t)((o * 0x9E3779B97F4A7C15ull) >> 20) & (H - 1);
+        while (hkey[h] != o) h = (h + 1) & (H - 1);
+        keep = hpos[h] == (uint32_t)p;
+      }
+    }
+    const uint64_t m = __ballot(keep);
+    if (lane == 0) s_wsum[w] = (uint32_t)__popcll(m);
+    __syncthreads();
+    int before = base, all = 0;
+    for (int v = 0; v < kMergeAnyT / 64; ++v) {
+      before += v < w ? (int)s_wsum[v] : 0;
+      all += (int)s_wsum[v];
+    }
+    const int pos = before + __popcll(m & ((1ull << lane) - 1ull));
+    if (keep && pos < k && status == 0) {
+      out.d[pos] = from_bits(ed[p]); out.o[pos] = from_okey(eo[p]); out.i[pos] = ei[p];
+    }
+    base += all;
+    __syncthreads();
+  }
+  if (tid == 0) {
+    out.h->status = status;
+    out.h->n = status ? 0 : (base < k ? base : k);
+    out.h->k = k;
+    out.h->flags = 0;
+    out.h->candidates = total;
+    out.h->threshold = 0.0;
+  }
+}
+
+__global__ __launch_bounds__(kMergeAnyT) void knn_merge_any_kernel(int32_t k, const char* records, int32_t nrec,
+                                                                   size_t rec_stride, size_t win_stride,
+                                                                   void* result_base, size_t res_stride, int foreign,
+                                                                   char* scratch, size_t scratch_stride) {
+  const StridedRecs src{records + (size_t)blockIdx.x * win_stride, rec_stride};
+  knn_merge_any_body(k, src, nrec, (char*)result_base + (size_t)blockIdx.x * res_stride,
+                     scratch + (size_t)blockIdx.x * scratch_stride, foreign);
+}
+
+__global__ __launch_bounds__(kMergeAnyT) void knn_merge_any_list_kernel(int32_t k, KnnRecList list, int32_t nrec,
+                                                                        void* result, char* scratch) {
+  const ListRecs src{&list};
+  knn_merge_any_body(k, src, nrec, result, scratch, 0);
+}
+
 // Fused continuous-query kernel (pipeline depth 2): blocks 1.. scan window i with the
 // threshold taken from the lane's hint (set by window i-2's select) -- or, for a lane's first
 // window (use_state 2), from the sample kernel launched just before; block 0, dispatched
@@ -1048,16 +1189,27 @@ __global__ __launch_bounds__(kSelT) void knn_merge_list_kernel(int32_t k, KnnRec
 }
 
 hipError_t launch_knn_merge(gf_ctx* ctx, int32_t k, const void* records, int32_t nrec, size_t rec_stride,
-                            int32_t nwin, size_t win_stride, void* result, size_t res_stride, int foreign) {
+                            int32_t nwin, size_t win_stride, void* result, size_t res_stride, int foreign,
+                            void* scratch) {
   KTimer t(ctx, GF_K_KNN_MERGE);
-  hipLaunchKernelGGL(knn_merge_kernel, dim3(nwin), dim3(kSelT), 0, ctx->stream, k, (const char*)records, nrec,
-                     rec_stride, win_stride, result, res_stride, foreign);
+  if (k > kMaxK)
+    hipLaunchKernelGGL(knn_merge_any_kernel, dim3(nwin), dim3(kMergeAnyT), 0, ctx->stream, k, (const char*)records,
+                       nrec, rec_stride, win_stride, result, res_stride, foreign, (char*)scratch,
+                       merge_any_bytes(nrec, k));
+  else
+    hipLaunchKernelGGL(knn_merge_kernel, dim3(nwin), dim3(kSelT), 0, ctx->stream, k, (const char*)records, nrec,
+                       rec_stride, win_stride, result, res_stride, foreign);
   return hipGetLastError();
 }
 
-hipError_t launch_knn_merge_list(gf_ctx* ctx, int32_t k, const KnnRecList& list, int32_t nrec, void* result) {
+hipError_t launch_knn_merge_list(gf_ctx* ctx, int32_t k, const KnnRecList& list, int32_t nrec, void* result,
+                                 void* scratch) {
   KTimer t(ctx, GF_K_KNN_MERGE);
-  hipLaunchKernelGGL(knn_merge_list_kernel, dim3(1), dim3(kSelT), 0, ctx->stream, k, list, nrec, result);
+  if (k > kMaxK)
+    hipLaunchKernelGGL(knn_merge_any_list_kernel, dim3(1), dim3(kMergeAnyT), 0, ctx->stream, k, list, nrec, result,
+                       (char*)scratch);
+  else
+    hipLaunchKernelGGL(knn_merge_list_kernel, dim3(1), dim3(kSelT), 0, ctx->stream, k, list, nrec, result);
   return hipGetLastError();
 }
 
@@ -1244,6 +1396,282 @@ hipError_t launch_knn_poly_scan(gf_ctx* ctx, const KnnPolyArgs& a, int blocks) {
     hipLaunchKernelGGL(knn_poly_scan_kernel, dim3(blocks), dim3(kBlock), 0, ctx->stream, a);
   }
   hipLaunchKernelGGL(knn_poly_refine_kernel, dim3(256), dim3(kBlock), 0, ctx->stream, a);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------
+// kNN across ranks with String objIDs (KNNQuery.java:232-251 dedupes by String.equals; the
+// in-repo caller MN_Q1.java:52 feeds gps.deviceId Strings).  A dictionary objID key is an id in
+// its own rank's gf_objid_dict, so before the all-gather every rank attaches the Strings of its
+// record's dictionary keys (a sidecar read from its dictionary's device arena); the merge then
+// orders and dedupes by the Strings themselves: (d, String, idx) with dictionary Strings by
+// their bytes (unsigned, a prefix first), dictionary Strings before canonical decimals, decimals
+// by value -- the same on every rank, so every rank gets the same merged record.
+// ---------------------------------------------------------------------------------------
+struct StrSide {
+  int32_t status;  // 0 ok; 1 the Strings did not fit cap (nbytes = what they need)
+  int32_t n;
+  int64_t nbytes;
+};
+__device__ __forceinline__ StrSide* side_of(void* rec, int32_t k) {
+  return reinterpret_cast<StrSide*>((char*)rec + 32 + (size_t)24 * k);
+}
+__device__ __forceinline__ uint32_t* side_off(void* rec, int32_t k) { return reinterpret_cast<uint32_t*>(side_of(rec, k) + 1); }
+__device__ __forceinline__ char* side_bytes(void* rec, int32_t k) { return (char*)side_off(rec, k) + str_side_off(k); }
+__device__ __forceinline__ bool dict_key(int64_t o) { return o < GF_OBJID_NUMERIC_MIN; }
+
+// block-wide exclusive scan of one u32 per thread (any block size <= 1024), returns the total
+template <int NT>
+__device__ __forceinline__ uint32_t block_excl(uint32_t v, uint32_t* excl, uint32_t* ws) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t inc = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t t = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += t;
+  }
+  if (lane == 63) ws[w] = inc;
+  __syncthreads();
+  uint32_t before = 0, tot = 0;
+#pragma unroll
+  for (int i = 0; i < NT / 64; ++i) {
+    before += i < w ? ws[i] : 0u;
+    tot += ws[i];
+  }
+  *excl = before + inc - v;
+  __syncthreads();
+  return tot;
+}
+
+// Strings of n entries (lengths len_of(i), sources src_of(i)) packed into a sidecar: offsets by a
+// chunked block scan, bytes copied one entry per thread; status 1 when they exceed cap
+template <int NT, class Len, class Src>
+__device__ void side_pack(void* rec, int32_t k, int n, int64_t cap, const Len& len_of, const Src& src_of, uint32_t* ws) {
+  StrSide* sd = side_of(rec, k);
+  uint32_t* off = side_off(rec, k);
+  char* bytes = side_bytes(rec, k);
+  uint32_t carry = 0;
+  for (int i0 = 0; i0 < n; i0 += NT) {  // block-uniform
+    const int i = i0 + (int)threadIdx.x;
+    const uint32_t l = i < n ? len_of(i) : 0u;
+    uint32_t ex;
+    const uint32_t tot = block_excl<NT>(l, &ex, ws);
+    if (i < n) off[i] = carry + ex;
+    carry += tot;
+  }
+  const bool fits = (int64_t)carry <= cap;
+  if (fits)
+    for (int i = threadIdx.x; i < n; i += NT) {
+      const uint32_t l = len_of(i);
+      const char* src = src_of(i);
+      char* dst = bytes + off[i];
+      for (uint32_t b = 0; b < l; ++b) dst[b] = src[b];
+    }
+  if (threadIdx.x == 0) {
+    off[n] = carry;
+    sd->status = fits ? 0 : 1;
+    sd->n = n;
+    sd->nbytes = (int64_t)carry;
+  }
+}
+
+// block r: record r copied into string record r, its dictionary keys' Strings attached
+__global__ __launch_bounds__(kBlock) void knn_attach_strings_kernel(int32_t k, const unsigned long long* idmap,
+                                                                    const char* arena, int64_t dict_size,
+                                                                    const char* records, int64_t cap, char* out) {
+  __shared__ uint32_t ws[kBlock / 64];
+  const size_t rb = 32 + (size_t)24 * k;
+  const char* in = records + (size_t)blockIdx.x * rb;
+  char* o = out + (size_t)blockIdx.x * str_record_bytes(k, cap);
+  for (size_t b = (size_t)threadIdx.x * 8; b < rb; b += (size_t)kBlock * 8)
+    *reinterpret_cast<uint64_t*>(o + b) = *reinterpret_cast<const uint64_t*>(in + b);
+  const gf_knn_header* h = reinterpret_cast<const gf_knn_header*>(in);
+  const int n = h->status == 0 ? h->n : 0;
+  const RecView v = rec_view((void*)in, k);
+  auto meta = [&](int i) -> unsigned long long {
+    const int64_t key = v.o[i];
+    if (!dict_key(key)) return 0ull;
+    const uint64_t id = (uint64_t)key - (uint64_t)INT64_MIN;
+    return id < (uint64_t)dict_size ? idmap[id] : 0ull;
+  };
+  side_pack<kBlock>(o, k, n, cap, [&](int i) { return (uint32_t)(meta(i) & kDictLenMask); },
+                    [&](int i) { return arena + (meta(i) >> kDictLenBits); }, ws);
+}
+
+hipError_t launch_knn_attach_strings(gf_ctx* ctx, int32_t k, const unsigned long long* idmap, const char* arena,
+                                     int64_t dict_size, const void* records, int32_t nrec, int64_t cap, void* out) {
+  hipLaunchKernelGGL(knn_attach_strings_kernel, dim3(nrec), dim3(kBlock), 0, ctx->stream, k, idmap, arena, dict_size,
+                     (const char*)records, cap, (char*)out);
+  return hipGetLastError();
+}
+
+struct StrEnt {  // one entry of a string merge, in global scratch (structure of arrays)
+  uint64_t* d;
+  int64_t* o;
+  int64_t* i;
+  const char** s;
+  uint32_t* len;
+  uint32_t* slot;
+};
+__device__ __forceinline__ int str_cmp(const char* a, uint32_t la, const char* b, uint32_t lb) {
+  const uint32_t m = la < lb ? la : lb;
+  for (uint32_t j = 0; j < m; ++j) {
+    const uint8_t x = (uint8_t)a[j], y = (uint8_t)b[j];
+    if (x != y) return x < y ? -1 : 1;
+  }
+  return la == lb ? 0 : (la < lb ? -1 : 1);
+}
+// (d, String, idx): dictionary Strings by bytes and before decimals, decimals by value
+__device__ __forceinline__ bool str_less(const StrEnt& E, uint32_t a, uint32_t b) {
+  if (E.d[a] != E.d[b]) return E.d[a] < E.d[b];
+  const int64_t oa = E.o[a], ob = E.o[b];
+  const bool da = dict_key(oa), db = dict_key(ob);
+  if (da != db) return da;
+  if (da) {
+    const int c = str_cmp(E.s[a], E.len[a], E.s[b], E.len[b]);
+    if (c) return c < 0;
+  } else if (oa != ob) {
+    return oa < ob;
+  }
+  if (E.i[a] != E.i[b]) return E.i[a] < E.i[b];
+  return a < b;  // identical entries: a total order still
+}
+__device__ __forceinline__ bool str_same(const StrEnt& E, uint32_t a, uint32_t b) {
+  const int64_t oa = E.o[a], ob = E.o[b];
+  const bool da = dict_key(oa), db = dict_key(ob);
+  if (da != db) return false;
+  return da ? str_cmp(E.s[a], E.len[a], E.s[b], E.len[b]) == 0 : oa == ob;
+}
+__device__ __forceinline__ uint64_t str_hash(const StrEnt& E, uint32_t a) {
+  const int64_t o = E.o[a];
+  uint64_t h;
+  if (dict_key(o)) {
+    h = 1469598103934665603ull;
+    for (uint32_t j = 0; j < E.len[a]; ++j) h = (h ^ (uint8_t)E.s[a][j]) * 1099511628211ull;
+    h ^= (uint64_t)E.len[a] << 40;
+  } else {
+    h = (uint64_t)o * 0x9E3779B97F4A7C15ull + 0x632BE59BD9B4E019ull;
+  }
+  h ^= h >> 33; h *= 0xff51afd7ed558ccdull; h ^= h >> 33;
+  return h;
+}
+
+constexpr int kStrMergeT = 1024;
+__global__ __launch_bounds__(kStrMergeT) void knn_merge_strings_kernel(int32_t k, int64_t cap, const char* records,
+                                                                       int32_t nrec, size_t rec_stride,
+                                                                       size_t win_stride, char* results,
+                                                                       char* scratch_base) {
+  __shared__ int s_off[kMaxMergeRecs + 1], s_status;
+  __shared__ uint32_t ws[kStrMergeT / 64];
+  const int tid = threadIdx.x;
+  const char* recs = records + (size_t)blockIdx.x * win_stride;
+  char* result = results + (size_t)blockIdx.x * str_record_bytes(k, cap);
+  char* scratch = scratch_base + (size_t)blockIdx.x * strmerge_bytes(nrec, k);
+  auto rec = [&](int r) { return (void*)(recs + (size_t)r * rec_stride); };
+  if (tid == 0) {
+    int off = 0, st = 0;
+    for (int r = 0; r < nrec; ++r) {
+      const gf_knn_header* h = (const gf_knn_header*)rec(r);
+      s_off[r] = off;
+      off += h->status == 0 ? h->n : 0;
+      st = h->status > st ? h->status : st;
+      if (h->status == 0 && side_of(rec(r), k)->status != 0) st = GF_KNN_STATUS_FOREIGN_KEYS;  // Strings missing
+    }
+    s_off[nrec] = off;
+    s_status = st;
+  }
+  __syncthreads();
+  const int total = s_off[nrec];
+  const int64_t Emax = (int64_t)nrec * k;
+  const size_t P = strmerge_pow2(total > 2 ? total : 2), H = strmerge_pow2(2 * (total > 1 ? total : 1));
+  StrEnt E;
+  E.d = reinterpret_cast<uint64_t*>(scratch);
+  E.o = reinterpret_cast<int64_t*>(E.d + Emax);
+  E.i = E.o + Emax;
+  E.s = reinterpret_cast<const char**>(E.i + Emax);
+  E.len = reinterpret_cast<uint32_t*>(E.s + Emax);
+  E.slot = E.len + Emax;
+  uint32_t* si = E.slot + Emax;                                  // [P] sorted entry order
+  uint32_t* hent = si + strmerge_pow2(Emax > 2 ? Emax : 2);      // [H] representative entry
+  uint32_t* hrank = hent + strmerge_pow2(2 * Emax);              // [H] its lowest sorted position
+  uint32_t* olen = hrank + strmerge_pow2(2 * Emax);              // [k]
+  const char** osrc = reinterpret_cast<const char**>(((uintptr_t)(olen + k) + 7) & ~(uintptr_t)7);  // [k]
+  // entries, the sort order, the table
+  for (int e = tid; e < total; e += kStrMergeT) {
+    int r = 0;
+    while (s_off[r + 1] <= e) ++r;
+    const int p = e - s_off[r];
+    void* rr = rec(r);
+    const RecView v = rec_view(rr, k);
+    E.d[e] = dbits(v.d[p]); E.o[e] = v.o[p]; E.i[e] = v.i[p];
+    const uint32_t* off = side_off(rr, k);
+    E.s[e] = side_bytes(rr, k) + off[p];
+    E.len[e] = off[p + 1] - off[p];
+  }
+  for (size_t t = tid; t < P; t += kStrMergeT) si[t] = t < (size_t)total ? (uint32_t)t : 0xFFFFFFFFu;
+  for (size_t t = tid; t < H; t += kStrMergeT) { hent[t] = 0xFFFFFFFFu; hrank[t] = 0xFFFFFFFFu; }
+  __syncthreads();
+  // bitonic sort of the entry order (padding ~0 sorts last)
+  for (size_t size = 2; size <= P; size <<= 1)
+    for (size_t stride = size >> 1; stride > 0; stride >>= 1) {
+      for (size_t t = tid; t < P / 2; t += kStrMergeT) {
+        const size_t i = 2 * stride * (t / stride) + (t & (stride - 1)), j = i + stride;
+        const uint32_t a = si[i], b = si[j];
+        const bool up = (i & size) == 0;
+        const bool j_less = b != 0xFFFFFFFFu && (a == 0xFFFFFFFFu || str_less(E, b, a));
+        if (j_less == up) { si[i] = b; si[j] = a; }
+      }
+      __syncthreads();
+    }
+  // the lowest sorted position of every String (equal Strings share a slot)
+  for (int p = tid; p < total; p += kStrMergeT) {
+    const uint32_t e = si[p];
+    size_t h = (size_t)str_hash(E, e) & (H - 1);
+    for (;;) {
+      const uint32_t cur = atomicCAS(&hent[h], 0xFFFFFFFFu, e);
+      if (cur == 0xFFFFFFFFu || str_same(E, cur, e)) break;
+      h = (h + 1) & (H - 1);
+    }
+    atomicMin(&hrank[h], (uint32_t)p);
+    E.slot[p] = (uint32_t)h;
+  }
+  __syncthreads();
+  // the first k kept entries in sorted order
+  RecView out = rec_view(result, k);
+  const int status = s_status;
+  int base = 0;
+  for (int p0 = 0; p0 < total && base < k; p0 += kStrMergeT) {  // block-uniform
+    const int p = p0 + tid;
+    const bool keep = p < total && hrank[E.slot[p]] == (uint32_t)p;
+    uint32_t ex;
+    const int all = (int)block_excl<kStrMergeT>(keep ? 1u : 0u, &ex, ws);
+    const int pos = base + (int)ex;
+    if (keep && pos < k) {
+      const uint32_t e = si[p];
+      out.d[pos] = from_bits(E.d[e]); out.o[pos] = E.o[e]; out.i[pos] = E.i[e];
+      olen[pos] = E.len[e];
+      osrc[pos] = E.s[e];
+    }
+    base += all;
+  }
+  const int n = status == 0 ? (base < k ? base : k) : 0;
+  __syncthreads();
+  side_pack<kStrMergeT>(result, k, n, cap, [&](int i) { return olen[i]; }, [&](int i) { return osrc[i]; }, ws);
+  if (tid == 0) {
+    out.h->status = status;
+    out.h->n = n;
+    out.h->k = k;
+    out.h->flags = 0;
+    out.h->candidates = total;
+    out.h->threshold = 0.0;
+  }
+}
+
+hipError_t launch_knn_merge_strings(gf_ctx* ctx, int32_t k, int64_t cap, const void* records, int32_t nrec,
+                                    size_t rec_stride, int32_t nwin, size_t win_stride, void* results, void* scratch) {
+  KTimer t(ctx, GF_K_KNN_MERGE);
+  hipLaunchKernelGGL(knn_merge_strings_kernel, dim3(nwin), dim3(kStrMergeT), 0, ctx->stream, k, cap,
+                     (const char*)records, nrec, rec_stride, win_stride, (char*)results, (char*)scratch);
   return hipGetLastError();
 }
 

@@ -295,3 +295,75 @@ extern "C" int gf_objid_decode(gf_objid_dict* d, const int64_t* keys, int64_t n,
   offs[n] = at;
   return at > cap || (at > 0 && !buf) ? GF_ERR_CAPACITY : GF_OK;
 }
+
+// ---- kNN records with Strings (the cross-rank merge of dictionary objIDs) ----------------------
+extern "C" size_t gf_knn_string_record_bytes(int32_t k, int64_t cap_bytes) {
+  return k < 1 || cap_bytes < 0 ? 0 : str_record_bytes(k, cap_bytes);
+}
+
+extern "C" int gf_knn_attach_strings(gf_objid_dict* d, int32_t k, const void* records, int32_t nrec, int64_t cap_bytes,
+                                     void* out) {
+  if (!d || k < 1 || k > kMaxKLarge || nrec < 0 || cap_bytes < 0 || cap_bytes > (int64_t)UINT32_MAX ||
+      (nrec > 0 && (!records || !out)))
+    return d ? set_err(d->ctx, GF_ERR_ARG, "gf_knn_attach_strings: bad argument") : GF_ERR_ARG;
+  gf_ctx* ctx = d->ctx;
+  int st = bind(ctx);
+  if (st || nrec == 0) return st;
+  GF_HIP_CHECK(ctx, launch_knn_attach_strings(ctx, k, d->idmap, d->arena, d->size, records, nrec, cap_bytes, out));
+  return GF_OK;
+}
+
+extern "C" int gf_knn_merge_dev_strings(gf_ctx* ctx, int32_t k, int64_t cap_bytes, const void* records, int32_t nrec,
+                                        int32_t nwin, int32_t layout, void* results) {
+  if (!ctx || k < 1 || k > kMaxKLarge || cap_bytes < 0 || cap_bytes > (int64_t)UINT32_MAX || nrec < 1 ||
+      nrec > kMaxMergeRecs || nwin < 1 || nwin > 65535 || !records || !results ||
+      (layout != GF_MERGE_SHARD_MAJOR && layout != GF_MERGE_WINDOW_MAJOR))
+    return set_err(ctx, GF_ERR_ARG, "gf_knn_merge_dev_strings: bad argument");
+  int st = bind(ctx);
+  if (st) return st;
+  const size_t sb = str_record_bytes(k, cap_bytes);
+  const size_t rec_stride = layout == GF_MERGE_SHARD_MAJOR ? (size_t)nwin * sb : sb;
+  const size_t win_stride = layout == GF_MERGE_SHARD_MAJOR ? sb : (size_t)nrec * sb;
+  void* scratch = ctx_scratch(ctx, strmerge_bytes(nrec, k) * (size_t)nwin, &st);
+  if (st) return st;
+  GF_HIP_CHECK(ctx, launch_knn_merge_strings(ctx, k, cap_bytes, records, nrec, rec_stride, nwin, win_stride, results,
+                                             scratch));
+  return GF_OK;
+}
+
+extern "C" int gf_knn_string_record_decode(const void* rec, int32_t k, int64_t cap_bytes, int32_t* status,
+                                           int64_t* objID, double* dist, int64_t* idx, char* buf, int64_t buf_cap,
+                                           int64_t* offs, int32_t* n_out) {
+  if (!rec || k < 1 || cap_bytes < 0 || !status || !n_out || !offs) return GF_ERR_ARG;
+  const gf_knn_header* h = (const gf_knn_header*)rec;
+  const double* d = (const double*)(h + 1);
+  const int64_t* o = (const int64_t*)(d + k);
+  const int64_t* i = o + k;
+  const char* side = (const char*)rec + gf_knn_result_bytes(k);
+  const int32_t side_status = *(const int32_t*)side;
+  const uint32_t* off = (const uint32_t*)(side + 16);
+  const char* bytes = (const char*)off + str_side_off(k);
+  *status = h->status != 0 ? h->status : (side_status != 0 ? GF_KNN_STATUS_FOREIGN_KEYS : 0);
+  *n_out = *status == 0 ? h->n : 0;
+  int64_t at = 0;
+  char num[32];
+  for (int32_t j = 0; j < *n_out; ++j) {
+    offs[j] = at;
+    const int64_t key = o[j];
+    const char* p = num;
+    size_t len = 0;
+    if (key < GF_OBJID_NUMERIC_MIN) {  // a dictionary String: from the record's own sidecar
+      p = bytes + off[j];
+      len = off[j + 1] - off[j];
+    } else if (key != GF_OBJID_NULL) {
+      len = (size_t)snprintf(num, sizeof num, "%lld", (long long)key);  // Long.toString
+    }
+    if (buf && at + (int64_t)len <= buf_cap) std::memcpy(buf + at, p, len);
+    at += (int64_t)len;
+    if (objID) objID[j] = key;
+    if (dist) dist[j] = d[j];
+    if (idx) idx[j] = i[j];
+  }
+  offs[*n_out] = at;
+  return at > buf_cap || (at > 0 && !buf) ? GF_ERR_CAPACITY : GF_OK;
+}

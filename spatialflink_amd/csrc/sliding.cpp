@@ -30,6 +30,7 @@ struct gf_knn_sliding {
   int32_t R = 0;   // ring slots (panes kept: borrowed buffers must stay alive that long)
   size_t rb = 0;
   char* recs = nullptr;  // device ring of R pane records
+  void* scratch = nullptr;  // k > kMaxK: the window merge's rank / dedupe scratch (W records)
   struct Pane {
     int64_t index = LLONG_MIN;
     gf_points pts{};
@@ -79,7 +80,7 @@ KnnMergeArgs window_merge(gf_knn_sliding* s, int64_t p, void* result) {
 int merge_window(gf_knn_sliding* s, int64_t p, void* result) {
   const KnnMergeArgs m = window_merge(s, p, result);
   gf_ctx* ctx = s->plan->ctx;
-  GF_HIP_CHECK(ctx, launch_knn_merge_list(ctx, s->plan->k, m.list, m.nrec, result));
+  GF_HIP_CHECK(ctx, launch_knn_merge_list(ctx, s->plan->k, m.list, m.nrec, result, s->scratch));
   return GF_OK;
 }
 
@@ -93,7 +94,6 @@ extern "C" int gf_knn_sliding_create(gf_knn_plan* plan, int64_t size_ms, int64_t
   if (!plan || !out || size_ms <= 0 || slide_ms <= 0) return GF_ERR_ARG;
   *out = nullptr;
   gf_ctx* ctx = plan->ctx;
-  if (plan->k > kMaxK) return set_err(ctx, GF_ERR_ARG, "gf_knn_sliding_create: k <= 512 (pane records are merged)");
   const int64_t pane = std::gcd(size_ms, slide_ms);
   const int64_t W = size_ms / pane, S = slide_ms / pane;
   if (W > kMaxMergeRecs)
@@ -108,7 +108,9 @@ extern "C" int gf_knn_sliding_create(gf_knn_plan* plan, int64_t size_ms, int64_t
   s->rb = gf_knn_result_bytes(plan->k);
   s->ring.resize((size_t)s->R);
   hipError_t e = hipMalloc(&s->recs, s->rb * (size_t)s->R);
+  if (e == hipSuccess && plan->k > kMaxK) e = hipMalloc(&s->scratch, merge_any_bytes((int32_t)W, plan->k));
   if (e != hipSuccess) {
+    if (s->recs) hipFree(s->recs);
     delete s;
     return hip_err(ctx, e, "hipMalloc");
   }
@@ -121,6 +123,7 @@ extern "C" void gf_knn_sliding_destroy(gf_knn_sliding* s) {
   hipSetDevice(s->plan->ctx->device);
   hipStreamSynchronize(s->plan->ctx->stream);
   if (s->recs) hipFree(s->recs);
+  if (s->scratch) hipFree(s->scratch);
   delete s;
 }
 

@@ -139,6 +139,13 @@ def _all_gather_bytes(out, inp, group):
         dist_.all_gather_into_tensor(out, inp, group=group)
 
 
+def _merge_layout(world: int) -> int:
+    """Shard-major; with more than one rank the records come from other ranks' contexts, whose
+    dictionary objID keys cannot be compared (GF_MERGE_FOREIGN_KEYS).  A one-rank group's records
+    all come from this context's own dictionary and merge as is."""
+    return _lib.GF_MERGE_SHARD_MAJOR | (_lib.GF_MERGE_FOREIGN_KEYS if world > 1 else 0)
+
+
 def allgather_knn_records(record, k: int, merged_out, group=None):
     """RCCL path: all-gather this rank's device kNN record (uint8 tensor of
     knn_record_bytes(k)) over xGMI, then merge the world's records on the device
@@ -153,9 +160,8 @@ def allgather_knn_records(record, k: int, merged_out, group=None):
     _all_gather_bytes(gathered, record, group)
     ctx = _lib.context(record.device.index)
     out = merged_out if isinstance(merged_out, int) else merged_out.data_ptr()
-    # the records come from every rank's context: dictionary objID keys are refused (status 2)
     _lib.check(_lib.lib().gf_knn_merge_dev_batch(ctx.handle, int(k), gathered.data_ptr(), world, 1,
-                                                 _lib.GF_MERGE_SHARD_MAJOR | _lib.GF_MERGE_FOREIGN_KEYS, out),
+                                                 _merge_layout(world), out),
                ctx.handle, "gf_knn_merge_dev_batch")
     return merged_out
 
@@ -195,8 +201,8 @@ def allgather_knn_records_batch(records, k: int, results, group=None):
     objID keys: canonical decimal objIDs are their values on every rank and merge as is.  A
     dictionary key (a non-numeric String objID) is an id in its own rank's gf_objid_dict, so
     keys of different ranks cannot be compared: the merge refuses such a window (record status
-    _lib.KNN_STATUS_FOREIGN_KEYS, no entries) -- merge those by their Strings with
-    allgather_knn_string_lists.
+    _lib.KNN_STATUS_FOREIGN_KEYS, no entries) -- merge those on the device by their Strings with
+    allgather_knn_records_strings.
 
     Ordering (pipeline depth 3): odd windows' records are written on the plan's second stream.
     Before this call, gf_ctx_join (the context stream waits for the second stream) so the
@@ -211,9 +217,75 @@ def allgather_knn_records_batch(records, k: int, results, group=None):
     ctx = _lib.context(records.device.index)
     out = results if isinstance(results, int) else results.data_ptr()
     _lib.check(_lib.lib().gf_knn_merge_dev_batch(ctx.handle, int(k), gathered.data_ptr(), world, int(nwin),
-                                                 _lib.GF_MERGE_SHARD_MAJOR | _lib.GF_MERGE_FOREIGN_KEYS, out),
+                                                 _merge_layout(world), out),
                ctx.handle, "gf_knn_merge_dev_batch")
     return results
+
+
+def string_record_bytes(k: int, cap_bytes: int) -> int:
+    """Bytes of a string record (a kNN record + the Strings of its dictionary objIDs)."""
+    return int(_lib.lib().gf_knn_string_record_bytes(int(k), int(cap_bytes)))
+
+
+def attach_strings(records, k: int, cap_bytes: int, dictionary, out=None):
+    """gf_knn_attach_strings: this rank's [nwin, rb] device records -> [nwin, sb] string records
+    carrying the Strings of their dictionary objIDs from `dictionary` (an ObjIdDict; async)."""
+    import torch
+
+    nwin = records.shape[0]
+    sb = string_record_bytes(k, cap_bytes)
+    if out is None:
+        out = torch.empty((nwin, sb), dtype=torch.uint8, device=records.device)
+    _lib.check(_lib.lib().gf_knn_attach_strings(dictionary.handle, int(k), records.data_ptr(), int(nwin),
+                                                int(cap_bytes), out.data_ptr()), dictionary.ctx.handle,
+               "gf_knn_attach_strings")
+    return out
+
+
+def allgather_knn_records_strings(records, k: int, cap_bytes: int, dictionary, results, group=None):
+    """The device path of a String-objID kNN across ranks (KNNQuery.java:232-251 dedupes by
+    String.equals): this rank's [nwin, rb] device records get their dictionary Strings attached
+    (gf_knn_attach_strings), ONE all-gather carries the string records of every rank, and every
+    rank merges all windows in one launch (gf_knn_merge_dev_strings, shard-major) into `results`
+    -- nwin consecutive string records (device tensor, or an int address of pinned memory).
+    Stream-ordered, no host sync; decode with decode_string_record.  The merge orders by
+    (d, String bytes, idx) and dedupes by String, so every rank gets the same records."""
+    import torch.distributed as dist_
+
+    world = dist_.get_world_size(group)
+    nwin = records.shape[0]
+    ext = attach_strings(records, k, cap_bytes, dictionary)
+    gathered = gather_records_batch(ext, group)
+    ctx = _lib.context(records.device.index)
+    out = results if isinstance(results, int) else results.data_ptr()
+    _lib.check(_lib.lib().gf_knn_merge_dev_strings(ctx.handle, int(k), int(cap_bytes), gathered.data_ptr(), world,
+                                                   int(nwin), _lib.GF_MERGE_SHARD_MAJOR, out),
+               ctx.handle, "gf_knn_merge_dev_strings")
+    return results
+
+
+def decode_string_record(raw: bytes, k: int, cap_bytes: int):
+    """Host bytes of a string record -> (status, [String bytes], dist, idx)
+    (gf_knn_string_record_decode: dictionary Strings from the sidecar, Long.toString for decimals)."""
+    import ctypes as C
+
+    raw = bytes(raw)
+    rec = C.create_string_buffer(raw, len(raw))
+    st, n = C.c_int32(), C.c_int32()
+    d = np.zeros(k, np.float64); i = np.zeros(k, np.int64); offs = np.zeros(k + 1, np.int64)
+    cap = max(64, len(raw))
+    for _ in range(2):
+        buf = C.create_string_buffer(cap)
+        rc = _lib.lib().gf_knn_string_record_decode(rec, int(k), int(cap_bytes), C.byref(st), None, d.ctypes.data,
+                                                    i.ctypes.data, buf, cap, offs.ctypes.data, C.byref(n))
+        if rc == _lib.GF_ERR_CAPACITY:
+            cap = int(offs[n.value]) + 1
+            continue
+        _lib.check(rc, None, "gf_knn_string_record_decode")
+        b = buf.raw
+        m = n.value
+        return st.value, [b[offs[j]:offs[j + 1]] for j in range(m)], d[:m].copy(), i[:m].copy()
+    raise _lib.GeoFlinkError(_lib.GF_ERR_CAPACITY, "gf_knn_string_record_decode")
 
 
 def merge_string_lists(k: int, lists):

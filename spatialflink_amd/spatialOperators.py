@@ -81,8 +81,14 @@ class _PlanCache:
 
     def pin(self, plan):
         """Never evict `plan`: a plan with settings or pending pipelined work, or one a pane
-        engine (gf_*_sliding) holds, lives until the operator closes."""
-        self._pinned.add(plan.value if hasattr(plan, "value") else plan)
+        engine (gf_*_sliding) holds, lives until it is unpinned or the operator closes."""
+        self._pinned.add(self._pv(plan))
+
+    def unpin(self, plan):
+        """The holder of a pin is done with it (a pane engine closed): the plan is an ordinary
+        LRU entry again and is evicted if the cache is over its limit."""
+        self._pinned.discard(self._pv(plan))
+        self._evict(None)
 
     def get(self, key):
         plan = self._d.get(key)
@@ -92,8 +98,17 @@ class _PlanCache:
 
     def put(self, key, plan):
         self._d[key] = plan
+        self._evict(key)
+
+    def _evict(self, keep):
+        """Destroy least recently used unpinned plans beyond `limit`, never `keep` (the plan being
+        inserted, which the caller is about to use): with `limit` pinned plans the cache simply
+        grows past its limit until pins are released."""
         over = len(self._d) - self.limit
-        for k in [k for k, p in self._d.items() if self._pv(p) not in self._pinned][:max(over, 0)]:
+        if over <= 0:
+            return
+        victims = [k for k, p in self._d.items() if k != keep and self._pv(p) not in self._pinned][:over]
+        for k in victims:
             self._destroy(self._d.pop(k))
 
     @staticmethod
@@ -111,6 +126,7 @@ class _PlanCache:
         while self._d:
             _, p = self._d.popitem(last=False)
             self._destroy(p)
+        self._pinned.clear()
 
 
 class SpatialOperator:

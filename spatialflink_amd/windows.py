@@ -160,7 +160,7 @@ class SlidingKNNQuery:
         self.op = PointPointKNNQuery(conf, grid)
         self.ctx, self.plan = self.op.plan(device, queryPoint, queryRadius, k)
         self.op._plans.pin(self.plan)  # the pane engine holds it
-        self.depth = int(pipeline) if self.k <= 256 else 1
+        self.depth = int(pipeline)  # k > 256: the select is not fused, records complete in stream order
         _lib.check(_lib.lib().gf_knn_plan_set_pipeline(self.plan, self.depth), self.ctx.handle, "set_pipeline")
         h = C.c_void_p()
         _lib.check(_lib.lib().gf_knn_sliding_create(self.plan, self.geo.size, self.geo.slide, C.byref(h)),
@@ -257,11 +257,16 @@ class SlidingKNNQuery:
                 return pos
         return self.pos
 
-    def __del__(self):
+    def close(self):
+        """Destroy the pane engine and release its pin on the plan."""
         h = getattr(self, "handle", None)
         if h and _lib._lib is not None:
             _lib._lib.gf_knn_sliding_destroy(h)
             self.handle = None
+            self.op._plans.unpin(self.plan)
+
+    def __del__(self):
+        self.close()
 
 
 class SlidingRangeQuery:
@@ -288,6 +293,7 @@ class SlidingRangeQuery:
         if self.handle is None:
             self.ctx, plan = self.op.plan(device, self.queries, self.r)
             self.op._plans.pin(plan)
+            self.plan = plan
             h = C.c_void_p()
             _lib.check(_lib.lib().gf_range_sliding_create(plan, self.geo.size, self.geo.slide, C.byref(h)),
                        self.ctx.handle, "gf_range_sliding_create")
@@ -355,9 +361,11 @@ class SlidingRangeQuery:
         return out
 
     def close(self):
-        if self.handle is not None and _lib._lib is not None:
+        """Destroy the pane engine and release its pin on the operator's plan."""
+        if getattr(self, "handle", None) is not None and _lib._lib is not None:
             _lib.lib().gf_range_sliding_destroy(self.handle)
             self.handle = None
+            self.op._plans.unpin(self.plan)
 
     def __del__(self):
         self.close()

@@ -57,6 +57,17 @@ def test_knn_two_ranks_verified(pipeline):
 
 
 @pytest.mark.timeout(900)
+def test_knn_two_ranks_string_objids_verified():
+    """String objIDs (each rank interns "veh%09d" into its own dictionary): the exchange attaches
+    the Strings (gf_knn_attach_strings), all-gathers the string records and merges them by String
+    on the device (gf_knn_merge_dev_strings) -- verified against the oracle on the whole window."""
+    line = _run_two_ranks(["--points", "400000", "--steps", "9", "--warmup", "3", "--windows", "4",
+                           "--exchange-batch", "2", "--pipeline", "3", "--string-objids"])
+    assert line["n_gpus"] == 2 and line["verified_vs_oracle"] is True
+    assert line["config"]["objid"] == "dictionary Strings"
+
+
+@pytest.mark.timeout(900)
 def test_sliding_two_ranks_verified():
     line = _run_two_ranks(["--workload", "sliding", "--points", "2000000", "--steps", "7", "--warmup", "3",
                            "--windows", "3", "--exchange-batch", "2"])

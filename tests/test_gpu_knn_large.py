@@ -4,7 +4,9 @@ plans keep every candidate within r and derive the record from two stable device
 flagged window takes the same path.  Results == the oracle's contract (orc_knn_contract /
 orc_knn_ppoly_contract), bit-exact, for point and polygon queries, duplicate objIDs, fewer
 distinct objIDs than k, clustered input.  The sorted path reads its counts on the device, so
-windows queue back to back (depths 2 / 3 accept k > 512); the sliding engine refuses k > 512."""
+windows queue back to back (depths 2 / 3 accept k > 512); k in (256, 512] pipelines unfused (the
+standalone select, lanes alternating over two streams at depth 3); records of any k merge on the
+device (gf_knn_merge_dev(_batch): ranks by binary search + objID dedupe for k > 512)."""
 import numpy as np
 import pytest
 
@@ -79,25 +81,26 @@ def test_polygon_knn_large_k(sf, oracle_mod):
     check(res, eo, ed, ei)
 
 
-@pytest.mark.parametrize("depth", [1, 2, 3])
-def test_knn_large_k_queued_windows(sf, oracle_mod, depth):
-    """Several k > 512 windows enqueued back to back with no host read in between (records
-    written by the kernels straight into pinned host memory), then one flush: each record ==
-    the oracle's.  Window sizes shrink and grow (candidate buffers regrown in stream order)."""
+@pytest.mark.parametrize("k,depth", [(700, 1), (700, 2), (700, 3), (300, 2), (300, 3), (512, 3)])
+def test_knn_large_k_queued_windows(sf, oracle_mod, k, depth):
+    """Several windows enqueued back to back with no host read in between (records written by the
+    kernels straight into pinned host memory), then one flush: each record == the oracle's.
+    Window sizes shrink and grow (candidate buffers regrown in stream order).  k > 512: the sorted
+    path; k in (256, 512]: the unfused pipeline (depth 3: two lanes on two streams)."""
     import torch
 
     g = sf.UniformGrid(500, *BEIJING)
     og = oracle_mod.grid(500, *BEIJING)
     q = sf.Point("q", *QPOINT, 0, g)
     op = sf.PointPointKNNQuery(conf(sf), g)
-    k, r = 700, 0.2
+    r = 0.2
     data = []
-    for seed, n in ((31, 900_000), (32, 200_000), (33, 1_300_000), (34, 0), (35, 600_000)):
+    for seed, n in ((31, 900_000), (32, 200_000), (33, 1_300_000), (34, 0), (35, 600_000), (36, 1_100_000)):
         x, y = oracle_mod.java_random_points(seed, n, *BEIJING)
         obj = (np.arange(n) % max(1, n // 3)).astype(np.int64)
         data.append((x, y, obj, sf.PointWindow.from_numpy(x, y, obj)))
     op.set_pipeline(0, q, r, k, depth)
-    order = [0, 1, 2, 3, 4, 2, 0]
+    order = [0, 1, 2, 3, 4, 2, 0, 5, 5, 2]
     rec = sf.PinnedRecords(len(order), k)
     for i, j in enumerate(order):
         op.enqueue(data[j][3], q, r, k, rec.ptr(i))
@@ -111,20 +114,53 @@ def test_knn_large_k_queued_windows(sf, oracle_mod, depth):
     op.set_pipeline(0, q, r, k, 1)
 
 
-def test_large_k_pipelines_and_sliding(sf):
-    """k in (256, 512] keeps depth 1 (the fused select in block 0 holds k <= 256); k > 512 takes
-    any depth; the sliding engine merges pane records of k <= 512 only."""
+@pytest.mark.parametrize("k,layout", [(600, 0), (600, 1), (2_000, 0)])
+def test_knn_merge_any_k(sf, oracle_mod, k, layout):
+    """Sharded windows at k > 512: each shard's record (the sorted path, index bases so idx is
+    global), merged by ONE gf_knn_merge_dev_batch launch (both layouts) == each window evaluated
+    whole.  objIDs repeat within and across shards, and exact distance ties across shards (points
+    duplicated into two shards with different objIDs / the same objID) must merge by (d, objID, idx)."""
+    import torch
+
     from spatialflink_amd import _lib
 
-    g = sf.UniformGrid(100, *BEIJING)
+    g = sf.UniformGrid(500, *BEIJING)
+    og = oracle_mod.grid(500, *BEIJING)
     q = sf.Point("q", *QPOINT, 0, g)
-    op = sf.PointPointKNNQuery(conf(sf), g)
-    with pytest.raises(ValueError):
-        op.set_pipeline(0, q, 0.5, 300, 2)
-    op.set_pipeline(0, q, 0.5, 600, 2)
-    op.set_pipeline(0, q, 0.5, 600, 1)
-    ctx, plan = op.plan(0, q, 0.5, 600)
-    import ctypes as C
-
-    s = C.c_void_p()
-    assert _lib.lib().gf_knn_sliding_create(plan, 10_000, 5_000, C.byref(s)) == _lib.GF_ERR_ARG
+    S, W = 4, 3
+    rb = sf.spatialOperators.knn_record_bytes(k)
+    recs = torch.zeros(S * W * rb, dtype=torch.uint8, device="cuda")
+    expect = []
+    ops = [sf.PointPointKNNQuery(conf(sf), g) for _ in range(S)]
+    for wi in range(W):
+        x, y = oracle_mod.java_random_points(500 + wi, 400_000, *BEIJING)
+        obj = (np.random.default_rng(wi).permutation(len(x)) % 150_000).astype(np.int64)
+        # exact ties: a block of points copied to the other half of the window (other shards)
+        x[200_000:201_000], y[200_000:201_000] = x[:1000], y[:1000]
+        obj[200_500:201_000] = obj[500:1000]
+        expect.append(oracle_mod.knn(og, x, y, obj, QPOINT[0], QPOINT[1], 0.3, k))
+        for s, ix in enumerate(np.array_split(np.arange(len(x)), S)):
+            ctx, plan = ops[s].plan(0, q, 0.3, k)
+            _lib.check(_lib.lib().gf_knn_plan_set_index_base(plan, int(ix[0])), ctx.handle, "base")
+            slot = s * W + wi if layout == 0 else wi * S + s
+            ops[s].enqueue(sf.PointWindow.from_numpy(x[ix], y[ix], obj[ix]), q, 0.3, k, recs[slot * rb:(slot + 1) * rb])
+    out = torch.zeros(W * rb, dtype=torch.uint8, device="cuda")
+    ctx = _lib.context(0)
+    _lib.check(_lib.lib().gf_knn_merge_dev_batch(ctx.handle, k, recs.data_ptr(), S, W, layout, out.data_ptr()),
+               ctx.handle, "merge batch")
+    raw = out.cpu().numpy().tobytes()
+    for wi in range(W):
+        st, o, d, i = sf.spatialOperators.decode_knn_record(raw[wi * rb:(wi + 1) * rb], k)
+        est, eo, ed, ei = expect[wi]
+        assert st == 0 and len(eo) == min(k, len(eo))
+        np.testing.assert_array_equal(o, eo)
+        np.testing.assert_array_equal(d.view(np.int64), ed.view(np.int64))
+        np.testing.assert_array_equal(i, ei)
+    # one window through gf_knn_merge_dev (shard-major records of window 0 are contiguous at layout 0)
+    if layout == 0:
+        one = torch.zeros(rb, dtype=torch.uint8, device="cuda")
+        win0 = torch.cat([recs[(s * W) * rb:(s * W + 1) * rb] for s in range(S)])
+        _lib.check(_lib.lib().gf_knn_merge_dev(ctx.handle, k, win0.data_ptr(), S, one.data_ptr()), ctx.handle, "merge")
+        st, o, d, i = sf.spatialOperators.decode_knn_record(one.cpu().numpy().tobytes(), k)
+        np.testing.assert_array_equal(o, expect[0][1])
+        np.testing.assert_array_equal(i, expect[0][3])

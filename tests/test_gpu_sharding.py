@@ -207,3 +207,71 @@ def test_knn_merge_refuses_foreign_dictionary_keys(sf, oracle_mod):
                     assert st == 0 and np.array_equal(dd, ed)
                     got = d.decode(o) if strings else o.tolist()
                     assert got == ([names[j] for j in eo] if strings else eo.tolist())
+
+
+@pytest.mark.parametrize("k", [40, 600])
+def test_knn_merge_strings_across_dictionaries(sf, oracle_mod, k):
+    """The device path of a String-objID kNN across ranks: S shards, each with its OWN dictionary
+    (what each rank holds), intern overlapping String objIDs in different orders (so one String has
+    a different key in every shard); each shard's records get their Strings attached
+    (gf_knn_attach_strings), the string records of all shards are merged in one launch
+    (gf_knn_merge_dev_strings, both layouts' shard-major case) and decoded: == the oracle on the
+    whole window, where "v%07d" Strings order like their numbers and come before the canonical
+    decimal objIDs ("123": numeric keys).  Exact distance ties across shards (points copied into
+    another shard under the same and under other Strings) merge by (d, String, idx)."""
+    import torch
+
+    from spatialflink_amd import _lib, sharding
+
+    L = _lib.lib()
+    g = sf.UniformGrid(500, *BEIJING)
+    og = oracle_mod.grid(500, *BEIJING)
+    q = sf.Point("q", *QPOINT, 0, g)
+    S, W = 3, 3
+    cap = 16 * k + 64
+    rb = sf.spatialOperators.knn_record_bytes(k)
+    sb = sharding.string_record_bytes(k, cap)
+    dicts = [sf.ObjIdDict(0) for _ in range(S)]
+    ops = [sf.PointPointKNNQuery(conf(sf), g) for _ in range(S)]
+    recs = torch.zeros(S, W, rb, dtype=torch.uint8, device="cuda")
+    expect = []
+    for wi in range(W):
+        n = 360_000
+        x, y = oracle_mod.java_random_points(900 + wi, n, *BEIJING)
+        rng = np.random.default_rng(wi)
+        ids = (rng.permutation(n) % 120_000).astype(np.int64)   # every objID about three times, across shards
+        numeric = ids % 10 == 3                                   # a tenth are canonical decimals
+        x[250_000:250_800], y[250_000:250_800] = x[:800], y[:800]   # exact ties in another shard
+        ids[250_400:250_800] = ids[400:800]                        # ... half of them under the same objID
+        names = [str(j).encode() if nm else b"v%07d" % j for j, nm in zip(ids.tolist(), numeric.tolist())]
+        oids = np.where(numeric, ids, ids - 10**9)                 # the oracle's integers in the same order
+        expect.append(oracle_mod.knn(og, x, y, oids, QPOINT[0], QPOINT[1], 0.5, k))
+        for s, ix in enumerate(np.array_split(np.arange(n), S)):
+            order = ix if s % 2 == 0 else ix[::-1]  # intern in different orders: different keys per shard
+            kk = dicts[s].intern([names[j] for j in order])
+            keys = np.ascontiguousarray(kk if s % 2 == 0 else kk[::-1])
+            ctx, plan = ops[s].plan(0, q, 0.5, k)
+            _lib.check(L.gf_knn_plan_set_index_base(plan, int(ix[0])), ctx.handle, "base")
+            ops[s].enqueue(sf.PointWindow.from_numpy(x[ix], y[ix], keys), q, 0.5, k, recs[s, wi])
+    torch.cuda.synchronize()
+    ext = torch.cat([sharding.attach_strings(recs[s], k, cap, dicts[s]) for s in range(S)])  # shard-major
+    out = torch.zeros(W, sb, dtype=torch.uint8, device="cuda")
+    ctx = _lib.context(0)
+    _lib.check(L.gf_knn_merge_dev_strings(ctx.handle, k, cap, ext.data_ptr(), S, W, _lib.GF_MERGE_SHARD_MAJOR,
+                                          out.data_ptr()), ctx.handle, "merge strings")
+    host = out.cpu().numpy()
+    for wi in range(W):
+        st, strs, d, i = sharding.decode_string_record(host[wi].tobytes(), k, cap)
+        est, eo, ed, ei = expect[wi]
+        assert st == 0 and est == 0 and len(strs) == len(eo)
+        got = np.array([int(s_[1:]) - 10**9 if s_.startswith(b"v") else int(s_) for s_ in strs], np.int64)
+        np.testing.assert_array_equal(got, eo)
+        np.testing.assert_array_equal(d.view(np.int64), ed.view(np.int64))
+        np.testing.assert_array_equal(i, ei)
+    # a sidecar too small for the Strings: the merge refuses those windows (status 2), not a guess
+    small = torch.cat([sharding.attach_strings(recs[s], k, 8, dicts[s]) for s in range(S)])
+    out2 = torch.zeros(W, sharding.string_record_bytes(k, 8), dtype=torch.uint8, device="cuda")
+    _lib.check(L.gf_knn_merge_dev_strings(ctx.handle, k, 8, small.data_ptr(), S, W, _lib.GF_MERGE_SHARD_MAJOR,
+                                          out2.data_ptr()), ctx.handle, "merge strings small")
+    st, strs, _, _ = sharding.decode_string_record(out2[0].cpu().numpy().tobytes(), k, 8)
+    assert st == _lib.KNN_STATUS_FOREIGN_KEYS and strs == []

@@ -60,6 +60,11 @@ def conf(sf):
     # C5's shape (BASELINE.json configs[4]): k = 100, 1000 x 1000 grid, size / slide = 2
     (2000, 1000, 100, 2, 1_500_000, None, 1000),
     (2000, 1000, 100, 1, 800_000, None, 1000),
+    # any k (KNNQuery.java:216): k in (256, 512] unfused at depth 2, k > 512 on the sorted path with
+    # the rank merge of pane records (k = 1000 at C5's grid)
+    (3000, 1000, 300, 2, 700_000, None, 500),
+    (3000, 1000, 600, 2, 700_000, None, 500),
+    (2000, 1000, 1000, 1, 600_000, None, 1000),
 ])
 def test_sliding_knn_matches_oracle(sf, oracle_mod, size, slide, k, depth, n, cap, gn):
     g = sf.UniformGrid(gn, *BEIJING)

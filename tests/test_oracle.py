@@ -316,3 +316,20 @@ def test_knn_ppoly_mt_matches_serial(oracle_mod):
     for T in (1, 4, 7):
         got = oracle_mod.knn_ppoly_mt(g, x, y, obj, P, 0.5, 50, T)
         assert got[0] == ref[0] and all(np.array_equal(a, b) for a, b in zip(got[1:], ref[1:]))
+
+
+def test_join_digest_matches_pairs(oracle_mod):
+    """orc_join_pp_omp_digest (the whole-window check of joins too large to materialise) ==
+    the count and pair_digest of the pairs the same join stores, and == the reference-shaped join."""
+    B = (115.5, 117.6, 39.6, 41.1)
+    og = oracle_mod.grid(1000, *B)
+    ox, oy = oracle_mod.java_random_points(5, 60_000, 116.0, 116.2, 39.8, 39.95)
+    qx, qy = oracle_mod.java_random_points(6, 6_000, 116.0, 116.2, 39.8, 39.95)
+    st, ref = oracle_mod.join_pp(og, og, ox, oy, qx, qy, 0.001)
+    assert st == 0 and len(ref) > 1000
+    cnt, dg = oracle_mod.join_pp_digest(og, ox, oy, qx, qy, 0.001, 4)
+    assert cnt == len(ref) and dg == oracle_mod.pair_digest(ref)
+    assert dg != oracle_mod.pair_digest(ref[1:])  # one pair missing changes it
+    swapped = ref.copy()
+    swapped[0] = swapped[0][::-1]
+    assert dg != oracle_mod.pair_digest(swapped)

@@ -72,3 +72,23 @@ def test_plan_cache_keeps_pinned_plans(monkeypatch):
         c.put(k, 200 + i)
     assert c.get("a") == 101 and 101 not in destroyed
     assert len(c) == 2 and destroyed == [200, 201, 202, 203]  # the LRU unpinned ones go
+
+
+def test_plan_cache_never_evicts_the_inserted_plan(monkeypatch):
+    """With `limit` pinned plans, a new plan is the only unpinned entry: put() must keep it (the
+    caller uses it next) and let the cache exceed its limit; unpinning restores the bound."""
+    from spatialflink_amd import spatialOperators as so
+
+    destroyed = []
+    monkeypatch.setattr(so._PlanCache, "_destroy", lambda self, p: destroyed.append(p))
+    c = so._PlanCache("unused", limit=3)
+    for i, k in enumerate("abc"):
+        c.put(k, 100 + i)
+        c.pin(100 + i)
+    c.put("d", 200)
+    assert destroyed == [] and c.get("d") == 200 and len(c) == 4
+    c.put("e", 201)  # "d" is now an ordinary LRU entry beyond the limit
+    assert destroyed == [200] and c.get("e") == 201 and len(c) == 4
+    c.unpin(100)  # released pin: the oldest unpinned entries go until the limit holds
+    assert destroyed == [200, 100] and len(c) == 3
+    assert c.get("e") == 201 and c.get("b") == 101 and c.get("c") == 102

@@ -127,6 +127,28 @@ def _cpu_lines(args, unit, lines, check):
     return d
 
 
+def _pair_digest_dev(pairs, m: int) -> int:
+    """oracle.pair_digest of the first m device pairs (uint32 pairs viewed as int32) computed on the
+    device in chunks: sum mod 2^64 of fmix64(p << 32 | q) (torch int64 arithmetic wraps; logical
+    right shifts by masking)."""
+    import torch
+
+    c1, c2 = 0xff51afd7ed558ccd - (1 << 64), 0xc4ceb9fe1a85ec53 - (1 << 64)
+    mask33 = (1 << 31) - 1
+    total = torch.zeros((), dtype=torch.int64, device=pairs.device)
+    v = pairs[: 2 * m].view(-1, 2)
+    for a in range(0, m, 1 << 27):
+        blk = v[a:a + (1 << 27)].to(torch.int64) & 0xffffffff
+        k = (blk[:, 0] << 32) | blk[:, 1]
+        k = k ^ ((k >> 33) & mask33)
+        k = k * c1
+        k = k ^ ((k >> 33) & mask33)
+        k = k * c2
+        k = k ^ ((k >> 33) & mask33)
+        total += k.sum()
+    return int(total.item()) & ((1 << 64) - 1)
+
+
 def _band(sf, grid, grid_n, world, rank):
     """x range of this rank's cell-column band (the whole grid at N = 1)."""
     from spatialflink_amd import sharding
@@ -535,30 +557,47 @@ def bench_join(args):
     avg = ms / 1000.0 / max(cnt, 1)
     pp = total_pairs / args.steps
     pp_all = pp if world == 1 else _reduce_sum(pp, world, args, dev)
-    # parity + CPU baseline (N = 1): pairs of the first 1M ordinary points of window 0 against
-    # the whole query window == the oracle's reference-shaped join of those points (pairs are
-    # per ordinary point), timed
+    # parity (N = 1): EVERY pair of both windows (the whole 10M x 1M window, not a sample) against
+    # the oracle's optimised OpenMP join, which the reference-shaped join pins on the first 1M
+    # ordinary points of window 0; every timed async window's count == its window's synchronous
+    # count.  CPU baseline on that 1M-point sample (pairs are per ordinary point), timed.
     verified, cpu = None, None
     if world == 1 and not args.no_verify:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle as O
 
-        step(0)
-        if use_async:  # the async windows' counts equal the synchronous call's
-            assert int(totals[0].item()) == npairs.value, "gf_join_pp_async count != gf_join_pp count"
-        m = min(no, 1_000_000)
-        got = pairs[: 2 * npairs.value].cpu().numpy().view(np.uint32).astype(np.int64).reshape(-1, 2)
-        got = got[got[:, 0] < m]
+        def sorted_pairs(a):
+            return a[np.lexsort((a[:, 1], a[:, 0]))]
+
         og = O.grid(grid_n, *BEIJING)
+        nthr = _host_threads()[0]
+        verified = True
+        digest_mode = False
+        for wi in range(2):
+            step(wi)
+            if use_async:
+                tc = totals[: args.steps].cpu().numpy()[wi::2]
+                if not (tc == npairs.value).all():
+                    raise RuntimeError(f"gf_join_pp_async counts {set(tc.tolist())} != gf_join_pp {npairs.value}")
+            (x, y, _), (qx, qy, _) = ow[wi], qw[wi]
+            if npairs.value > 200_000_000:  # (clustered: 2e9 pairs) count + order-free digest of every pair
+                digest_mode = True
+                ecnt, edg = O.join_pp_digest(og, x, y, qx, qy, r, nthr)
+                verified = verified and ecnt == npairs.value and edg == _pair_digest_dev(pairs, npairs.value)
+            else:
+                got_w = sorted_pairs(pairs[: 2 * npairs.value].cpu().numpy().view(np.uint32).astype(np.int64)
+                                     .reshape(-1, 2))
+                exp_w = O.join_pp_mt(og, og, x, y, qx, qy, r, nthr, optimized=True)
+                verified = verified and bool(np.array_equal(got_w, exp_w))
+            if wi == 0:
+                m = min(no, 1_000_000)
+                g0 = pairs[: 2 * npairs.value].view(-1, 2)
+                g0 = g0[g0[:, 0].to(torch.int64) < m].cpu().numpy().view(np.uint32).astype(np.int64).reshape(-1, 2)
+                got_s = sorted_pairs(g0)
         (x, y, _), (qx, qy, _) = ow[0], qw[0]
         st, exp = O.join_pp(og, og, x[:m], y[:m], qx, qy, r)
-        order = np.lexsort((got[:, 1], got[:, 0]))
-        eo = np.lexsort((exp[:, 1], exp[:, 0]))
-        got_s = got[order]
-        verified = bool(st == 0 and np.array_equal(got_s, exp[eo]))
+        verified = verified and bool(st == 0 and np.array_equal(got_s, sorted_pairs(exp)))
         if not args.no_cpu_baseline:  # the first m ordinary points x the whole query window (pairs are per point)
-            def sorted_pairs(a):
-                return a[np.lexsort((a[:, 1], a[:, 0]))]
             cpu = _cpu_lines(args, "points/s", {
                 "mt": (m + len(qx), lambda T: O.join_pp_mt(og, og, x[:m], y[:m], qx, qy, r, T),
                        f"first {m} ordinary points of window 0 x the {len(qx)} query points"),
@@ -587,7 +626,11 @@ def bench_join(args):
                          "bucket_us_per_launch": round(bms * 1000.0 / max(bcnt, 1), 2),
                          "bucket_launches_per_window": bcnt / args.steps},
            "pairs_per_s": round(pp_all * args.steps / elapsed, 1), "verified_vs_oracle": verified,
-           **({"verified_sample": f"pairs of the first {min(no, 1_000_000)} ordinary points of window 0"}
+           **({"verified_sample": ("whole window: " + ("the pair count and an order-free digest of every pair "
+                                  "(sum of fmix64(p << 32 | q))" if digest_mode else "every pair") +
+                                  " of both windows vs the oracle's OpenMP join; the pairs of the first 1M "
+                                  "ordinary points of window 0 vs the reference-shaped join; every timed "
+                                  "window's count == its window's")}
               if verified is not None else {}),
            **({"cpu_baseline": cpu} if cpu else {})}, rank=rank)
 
