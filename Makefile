@@ -49,8 +49,27 @@ trace: $(TRACE_LIB)
 isa: $(LIB)
 	/opt/rocm/lib/llvm/bin/clang-offload-bundler --list --type=o --input=$(OBJDIR)/k_knn.hip.o
 
+# Host sanitizer builds: the oracle and the host builds of the product's untrusted-text
+# parsers (gf_geojson.hpp / gf_decimal.hpp via tests/native/*.cpp) with AddressSanitizer +
+# UndefinedBehaviorSanitizer, and the CPU test suite run against them (the runtimes preloaded
+# into python).  Host code only: GPU sanitizers are not available on this pool.
+SANFLAGS := -fsanitize=address,undefined -fno-sanitize-recover=undefined -fno-omit-frame-pointer -g
+ASAN_ORACLE := build/asan/liboracle.so
+$(ASAN_ORACLE): oracle/geoflink_oracle.c oracle/cpu_scan.c oracle/geoflink_oracle.h
+	@mkdir -p build/asan
+	gcc -O1 -fPIC -std=c11 -ffp-contract=off -fno-fast-math -Wall -Wno-unused-function $(SANFLAGS) -pthread -fopenmp \
+	    -shared -o $@ oracle/geoflink_oracle.c oracle/cpu_scan.c -lm
+asan: $(ASAN_ORACLE)
+ASAN_RT := $(shell gcc -print-file-name=libasan.so):$(shell gcc -print-file-name=libubsan.so)
+asan-test: asan
+	LD_PRELOAD=$(ASAN_RT) ASAN_OPTIONS=detect_leaks=0:abort_on_error=1:allocator_may_return_null=1 \
+	UBSAN_OPTIONS=print_stacktrace=1:halt_on_error=1 GF_ORACLE_LIB=$(abspath $(ASAN_ORACLE)) \
+	GF_NATIVE_SANITIZE="$(SANFLAGS)" python -m pytest -x -q -s -m "not gpu" -p no:cacheprovider \
+	    tests/test_oracle.py tests/test_csv_core.py tests/test_geojson_core.py tests/test_csv_oracle.py \
+	    tests/test_geojson_oracle.py tests/test_windows.py
+
 clean:
 	rm -rf build $(LIB) $(SHIM)
 	$(MAKE) -s -C oracle clean
 
-.PHONY: all oracle shim clean isa trace
+.PHONY: all oracle shim clean isa trace asan asan-test

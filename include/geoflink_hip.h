@@ -554,6 +554,13 @@ void gf_window_destroy(gf_window* w);
 int  gf_window_upload(gf_window* w, const double* x, const double* y, const int64_t* objID,
                       const int64_t* ts, int64_t n);
 int  gf_window_points(gf_window* w, gf_points* out);
+/* kNN windows at 16 B per point over PCIe (HipKnnWindowFunction.java:96-106 hands x, y, objID):
+ * x and y are copied as gf_window_upload does, but the objID column stays in host memory --
+ * objID_pinned must be gf_pinned_alloc memory -- and the kernels read it in place through the
+ * mapping: only the few hundred candidates' objIDs ever cross the bus (the scan appends
+ * (d, idx, objID) for points below the threshold; nothing else reads objID).  The column must
+ * stay unchanged until the work that reads this window has completed. */
+int  gf_window_upload_mapped(gf_window* w, const double* x, const double* y, const int64_t* objID_pinned, int64_t n);
 
 /* ---- synthetic input (host) ----------------------------------------------------------
  * java.util.Random(seed): x = minX + nextDouble()*(maxX-minX), then y likewise, per point

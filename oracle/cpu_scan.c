@@ -437,9 +437,14 @@ static int64_t join_pp_omp_core(const orc_grid* grid, int64_t no, const double* 
   for (int t = 0; t < T; t++) tot += res[t].n;
   int64_t* all = (int64_t*)malloc(8 * (size_t)(tot > 0 ? tot : 1));
   int64_t w = 0;
-  for (int t = 0; t < T; t++) { memcpy(all + w, res[t].v, 8 * (size_t)res[t].n); w += res[t].n; free(res[t].v); }
+  for (int t = 0; t < T; t++) {
+    if (res[t].n) memcpy(all + w, res[t].v, 8 * (size_t)res[t].n);
+    w += res[t].n;
+    free(res[t].v);
+  }
   qsort(all, (size_t)(tot / 2), 16, cmp_pair64);
-  memcpy(out_pairs, all, 8 * (size_t)(tot < 2 * cap ? tot : 2 * cap));
+  const int64_t keep = tot < 2 * cap ? tot : 2 * cap;
+  if (keep > 0) memcpy(out_pairs, all, 8 * (size_t)keep);
   free(all); free(res); free(off); free(qc); free(lst);
   return tot / 2;
 }

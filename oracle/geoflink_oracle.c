@@ -777,7 +777,7 @@ static int32_t knn_cell_apply(const tup* c, int64_t m, int32_t k, tup* out) {
     }
   }
   int32_t n = pq.size;
-  memcpy(out, pq.q, sizeof(tup) * (size_t)n);
+  if (n > 0) memcpy(out, pq.q, sizeof(tup) * (size_t)n);
   jpq_free(&pq);
   return n;
 }
@@ -1012,7 +1012,7 @@ int32_t orc_knn_reference_mt(const orc_grid* g, int64_t n, const double* x, cons
   hoff[0] = 0;
   for (int64_t ci = 0; ci < ncell; ci++) {
     const cellrun* R = order[ci];
-    memcpy(heaps + hoff[ci], R->h, sizeof(tup) * (size_t)R->cnt);
+    if (R->cnt) memcpy(heaps + hoff[ci], R->h, sizeof(tup) * (size_t)R->cnt);
     hoff[ci + 1] = hoff[ci] + R->cnt;
   }
   int32_t st = knn_winall_merge(heaps, hoff, ncell, k, out_objID, out_d, out_idx);
@@ -1478,9 +1478,14 @@ static int64_t gather_sorted(lvec* res, int T, int64_t* out, int64_t cap, int wi
   for (int t = 0; t < T; t++) tot += res[t].n;
   int64_t* all = (int64_t*)malloc(8 * (size_t)(tot > 0 ? tot : 1));
   int64_t w = 0;
-  for (int t = 0; t < T; t++) { memcpy(all + w, res[t].v, 8 * (size_t)res[t].n); w += res[t].n; free(res[t].v); }
+  for (int t = 0; t < T; t++) {
+    if (res[t].n) memcpy(all + w, res[t].v, 8 * (size_t)res[t].n);
+    w += res[t].n;
+    free(res[t].v);
+  }
   qsort(all, (size_t)(tot / width), 8 * (size_t)width, width == 1 ? cmp_i64 : cmp_pair);
-  memcpy(out, all, 8 * (size_t)(tot < cap * width ? tot : cap * width));
+  const int64_t keep = tot < cap * width ? tot : cap * width;
+  if (keep > 0) memcpy(out, all, 8 * (size_t)keep);
   free(all);
   return tot / width;
 }

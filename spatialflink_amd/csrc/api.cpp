@@ -447,8 +447,7 @@ extern "C" int gf_bucket_by_cell(gf_ctx* ctx, const gf_grid* g, const gf_points*
   size_t o_k[2] = {ar.take<uint32_t>(n), ar.take<uint32_t>(n)};
   size_t o_v[2] = {ar.take<uint32_t>(n), ar.take<uint32_t>(n)};
   size_t o_k0 = ar.take<uint32_t>(n);  // pass 0's keys (stored by its histogram)
-  size_t o_m = ar.take<uint32_t>(mat), o_ms = ar.take<uint32_t>(mat + 1), o_h = ar.take<uint32_t>(bins);
-  size_t o_tmp = ar.take<uint32_t>(std::max(scan_tmp_elems(mat), scan_tmp_elems(bins)));
+  size_t o_m = ar.take<uint32_t>(mat), o_ms = ar.take<uint32_t>(mat + 1);
   char* base = (char*)ctx_scratch(ctx, ar.off, &st);
   if (st) return st;
   auto U32 = [&](size_t o) { return (uint32_t*)(base + o); };
@@ -474,11 +473,9 @@ extern "C" int gf_bucket_by_cell(gf_ctx* ctx, const gf_grid* g, const gf_points*
     a.vout = p == passes - 1 ? perm : U32(o_v[p & 1]);
     GF_HIP_CHECK(ctx, launch_radix(ctx, 1, a, blocks));
   }
-  // bucket sizes from the sorted keys' runs, then their exclusive scan = cell_start[0 .. bins]
-  GF_HIP_CHECK(ctx, hipMemsetAsync(U32(o_h), 0, sizeof(uint32_t) * (size_t)bins, ctx->stream));
-  a.M = U32(o_h);
+  // cell_start[0 .. bins] from the sorted keys' run boundaries (one kernel, every entry written once)
+  a.M = cell_start;
   GF_HIP_CHECK(ctx, launch_radix(ctx, 2, a, blocks));
-  GF_HIP_CHECK(ctx, launch_exclusive_scan(ctx->stream, U32(o_h), bins, cell_start, U32(o_tmp)));
   return GF_OK;
 }
 
@@ -1394,7 +1391,7 @@ static KnnPolyArgs poly_args(gf_knn_plan* P, int j, const gf_points* pts, int64_
   for (int i = 0; i < 4; ++i) a.bbox[i] = P->bbox[i];
   a.approx = P->approx; a.r = P->r; a.k = P->k; a.use_state = use_state; a.use_hint = use_hint;
   a.st = L.st; a.cand_d = L.cand_d; a.cand_i = L.cand_i; a.cand_o = L.cand_o; a.cap = (unsigned long long)P->cap;
-  a.maybe_i = P->maybe_i[j];
+  a.maybe_i = P->maybe_i[j & 1];  // one survivor buffer per stream (depth 3: lanes 0, 2 / 1, 3)
   return a;
 }
 
@@ -1402,6 +1399,7 @@ static KnnPolyArgs poly_args(gf_knn_plan* P, int j, const gf_points* pts, int64_
 static int poly_buffers(gf_knn_plan* P) {
   if (P->maybe_cap >= P->cap) return GF_OK;
   GF_HIP_CHECK(P->ctx, hipStreamSynchronize(P->ctx->stream));
+  if (P->ctx->aux) GF_HIP_CHECK(P->ctx, hipStreamSynchronize(P->ctx->aux));
   for (auto& m : P->maybe_i) {
     if (m) hipFree(m);
     m = nullptr;
@@ -1545,6 +1543,37 @@ int gf::knn_enqueue_merge(gf_knn_plan* P, const gf_points* pts, void* result, co
     ctx->stream = main;
     return rc;
   }
+  if (P->pipeline == 3 && P->poly) {
+    // polygon query at depth 3: as the point plans below -- window k's prefilter scan on lane
+    // k % 4 with window k-2's select in block 0, then its refine, both on stream k % 2 -- so one
+    // plan keeps two windows' launches in flight (PointPolygonKNNQuery.java:245-317 per window)
+    if ((st = poly_buffers(P))) return st;
+    const uint64_t kseq = P->seq++;
+    const int j = (int)(kseq & 3);
+    hipStream_t main = ctx->stream;
+    ctx->stream = (kseq & 1) ? ctx->aux : main;
+    int rc = GF_OK;
+    do {
+      const bool sample = pts->n >= kSampleMinN && (!P->use_hint || !P->lane_warm[j]);
+      if (sample && (rc = knn_launch_sample(P, j, pts, 0))) break;
+      P->lane_warm[j] = 1;
+      const KnnPolyArgs a = poly_args(P, j, pts, 0, pts->n, sample ? 2 : 1, 0);
+      KnnSelectArgs q{};
+      int has_prev = 0;
+      if (P->npq > 0 && P->pq[0].seq + 2 == kseq) {
+        const gf_knn_plan::Pend e = P->pq[0];
+        q = select_args(P, e.lane, 1, P->use_hint, e.result, e.idx_base);
+        has_prev = 1;
+        P->pq[0] = P->pq[1];
+        --P->npq;
+      }
+      hipError_t he = launch_knn_poly_fused(ctx, a, q, has_prev, scan_blocks_for(P, (pts->n + 1) / 2), nullptr);
+      if (he != hipSuccess) { rc = hip_err(ctx, he, "launch_knn_poly_fused"); break; }
+      P->pq[P->npq++] = gf_knn_plan::Pend{j, result, P->idx_base, kseq};
+    } while (0);
+    ctx->stream = main;
+    return rc;
+  }
   if (P->pipeline == 3) {
     // window k scans on lane k % 4 and selects window k-2 in block 0; odd windows launch on the
     // aux stream, so consecutive windows' kernels overlap (ramp-up of one under the tail of the
@@ -1659,8 +1688,6 @@ extern "C" int gf_knn_plan_flush(gf_knn_plan* P) {
 extern "C" int gf_knn_plan_set_pipeline(gf_knn_plan* P, int depth) {
   if (!P || depth < 1 || depth > 3) return GF_ERR_ARG;
   gf_ctx* ctx = P->ctx;
-  if (depth == 3 && P->poly)
-    return set_err(ctx, GF_ERR_ARG, "gf_knn_plan_set_pipeline: polygon queries run at depth <= 2");
   int st = bind(ctx);
   if (st || (st = gf_knn_plan_flush(P))) return st;
   GF_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
@@ -2168,9 +2195,26 @@ extern "C" int gf_window_upload(gf_window* w, const double* x, const double* y, 
   }
   GF_HIP_CHECK(ctx, hipEventRecord(w->ready, w->copy));
   w->has_objid = objID != nullptr;
+  w->objid_mapped = nullptr;
   w->has_ts = ts != nullptr;
   w->pending = true;
   w->n = n;
+  return GF_OK;
+}
+
+extern "C" int gf_window_upload_mapped(gf_window* w, const double* x, const double* y, const int64_t* objID_pinned,
+                                       int64_t n) {
+  if (!w || (n > 0 && !objID_pinned)) return GF_ERR_ARG;
+  void* dp = nullptr;
+  if (n > 0) {  // the objID column is read in place through the host mapping (candidates only)
+    int st = bind(w->ctx);
+    if (st) return st;
+    if (hipHostGetDevicePointer(&dp, (void*)objID_pinned, 0) != hipSuccess || !dp)
+      return set_err(w->ctx, GF_ERR_ARG, "gf_window_upload_mapped: objID is not pinned host memory (gf_pinned_alloc)");
+  }
+  int st = gf_window_upload(w, x, y, nullptr, nullptr, n);
+  if (st) return st;
+  w->objid_mapped = (const int64_t*)dp;
   return GF_OK;
 }
 
@@ -2185,7 +2229,7 @@ extern "C" int gf_window_points(gf_window* w, gf_points* out) {
     w->pending = false;
   }
   out->x = w->x; out->y = w->y; out->n = w->n;
-  out->objID = w->has_objid ? w->objID : nullptr;
+  out->objID = w->objid_mapped ? w->objid_mapped : (w->has_objid ? w->objID : nullptr);
   out->ts = w->has_ts ? w->ts : nullptr;
   return GF_OK;
 }

@@ -303,12 +303,12 @@ struct RadixArgs {
   uint32_t* vout;
   int shift, bits;          // digit = (key >> shift) & ((1 << bits) - 1)
   int nblk;                 // blocks (chunks of whole tiles)
-  uint32_t* M;              // stage 0: [digits][blocks]; stage 2: bucket sizes (zeroed)
+  uint32_t* M;              // stage 0: [digits][blocks]; stage 2: cell_start[0 .. gn*gn + 1] (output)
   const uint32_t* Ms;       // stage 1: the exclusive scan of M
   const uint32_t* n_dev;    // non-null: the item count is min(n, *n_dev), read on the device
 };
 size_t radix_scatter_lds_bytes();
-// stage 0 histogram, 1 scatter, 2 bucket sizes of the sorted kout
+// stage 0 histogram, 1 scatter, 2 cell_start from the sorted kout (every bucket's first position)
 hipError_t launch_radix(gf_ctx* ctx, int stage, const RadixArgs& a, int blocks);
 // exclusive scan: out[0..L] (out[L] = total); tmp >= scan_tmp_elems(L) uint32
 size_t scan_tmp_elems(int64_t L);
@@ -836,6 +836,7 @@ struct gf_window {
   int64_t* objID = nullptr;
   int64_t* ts = nullptr;
   bool has_objid = false, has_ts = false;  // columns of the last upload
+  const int64_t* objid_mapped = nullptr;   // gf_window_upload_mapped: the caller's pinned objID column
   // uploads run on the window's own copy stream: they wait for the work already enqueued on
   // the context's streams (which may still read the previous contents), and gf_window_points
   // makes the context's streams wait for the copy -- so upload(i+1) overlaps evaluate(i)

@@ -173,22 +173,51 @@ __global__ __launch_bounds__(kRadixThreads) void radix_hist_kernel(RadixArgs a) 
   __syncthreads();
   int64_t beg, end;
   radix_chunk(a, beg, end);
-  constexpr int U = 8;  // loads in flight together
-  for (int64_t i0 = beg + threadIdx.x; i0 < end; i0 += (int64_t)kRadixThreads * U) {
-    uint32_t k[U];
+  if (FIRST) {
+    // pass 0: two points per lane (16-B loads of x and y; chunks start at whole tiles, so pairs
+    // are 16-B aligned), keys stored as uint2
+    constexpr int U = 4;  // pairs in flight together
+    for (int64_t i0 = beg + 2 * (int64_t)threadIdx.x; i0 < end; i0 += (int64_t)kRadixThreads * 2 * U) {
+      uint32_t k0[U], k1[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int64_t i = i0 + (int64_t)u * kRadixThreads;
-      if (FIRST) k[u] = i < end ? bucket_key(__builtin_nontemporal_load(a.x + i), __builtin_nontemporal_load(a.y + i), a) : 0u;
-      else k[u] = i < end ? a.kin[i] : 0u;
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int64_t i = i0 + (int64_t)u * kRadixThreads;
-      if (i < end) {
-        atomicAdd(&h[(k[u] >> a.shift) & mask], 1u);
-        if (FIRST) a.kout[i] = k[u];  // pass 0's scatter reads the keys, not x, y
+      for (int u = 0; u < U; ++u) {
+        const int64_t i = i0 + (int64_t)u * kRadixThreads * 2;
+        if (i + 1 < end) {
+          typedef double v2d __attribute__((ext_vector_type(2)));
+          const v2d xv = __builtin_nontemporal_load(reinterpret_cast<const v2d*>(a.x + i));
+          const v2d yv = __builtin_nontemporal_load(reinterpret_cast<const v2d*>(a.y + i));
+          k0[u] = bucket_key(xv.x, yv.x, a);
+          k1[u] = bucket_key(xv.y, yv.y, a);
+        } else {
+          k0[u] = i < end ? bucket_key(a.x[i], a.y[i], a) : 0u;
+          k1[u] = 0u;
+        }
       }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t i = i0 + (int64_t)u * kRadixThreads * 2;
+        if (i + 1 < end) {
+          atomicAdd(&h[(k0[u] >> a.shift) & mask], 1u);
+          atomicAdd(&h[(k1[u] >> a.shift) & mask], 1u);
+          *reinterpret_cast<uint2*>(a.kout + i) = make_uint2(k0[u], k1[u]);  // pass 0's scatter reads the keys
+        } else if (i < end) {
+          atomicAdd(&h[(k0[u] >> a.shift) & mask], 1u);
+          a.kout[i] = k0[u];
+        }
+      }
+    }
+  } else {
+    constexpr int U = 8;  // loads in flight together
+    for (int64_t i0 = beg + threadIdx.x; i0 < end; i0 += (int64_t)kRadixThreads * U) {
+      uint32_t k[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t i = i0 + (int64_t)u * kRadixThreads;
+        k[u] = i < end ? a.kin[i] : 0u;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (i0 + (int64_t)u * kRadixThreads < end) atomicAdd(&h[(k[u] >> a.shift) & mask], 1u);
     }
   }
   __syncthreads();
@@ -214,15 +243,24 @@ __global__ __launch_bounds__(kRadixThreads) void radix_scatter_kernel(RadixArgs 
   int64_t beg, end;
   radix_chunk(a, beg, end);
   for (uint32_t d = threadIdx.x; d < D; d += kRadixThreads) gc[d] = a.Ms[(size_t)d * a.nblk + blockIdx.x];
-  for (int64_t t0 = beg; t0 < end; t0 += kRadixTile) {  // block-uniform
-    const uint32_t cnt = (uint32_t)(end - t0 < kRadixTile ? end - t0 : kRadixTile);
-    uint32_t k[U], v[U], r[U];
+  // a tile's (key, value) per lane; the next tile's loads are issued before this tile is ranked,
+  // placed and written, so their latency hides under that work (one block per CU: nothing else
+  // would cover it)
+  auto load_tile = [&](int64_t t, uint32_t* k, uint32_t* v) {
+    const uint32_t c = (uint32_t)(end - t < kRadixTile ? end - t : kRadixTile);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const uint32_t e = w * EPW + u * 64 + lane;
-      k[u] = e < cnt ? a.kin[t0 + e] : 0u;
-      v[u] = e < cnt ? (a.vin ? a.vin[t0 + e] : (uint32_t)(t0 + e)) : 0u;
+      k[u] = e < c ? a.kin[t + e] : 0u;
+      v[u] = e < c ? (a.vin ? a.vin[t + e] : (uint32_t)(t + e)) : 0u;
     }
+  };
+  uint32_t k[U], v[U];
+  if (beg < end) load_tile(beg, k, v);
+  for (int64_t t0 = beg; t0 < end; t0 += kRadixTile) {  // block-uniform
+    const uint32_t cnt = (uint32_t)(end - t0 < kRadixTile ? end - t0 : kRadixTile);
+    uint32_t kn[U], vn[U], r[U];
+    if (t0 + kRadixTile < end) load_tile(t0 + kRadixTile, kn, vn);
     for (uint32_t d = lane; d < D; d += 64) wc[w * kRadixMaxDigits + d] = 0u;  // this wave's row
 #pragma unroll
     for (int u = 0; u < U; ++u) {  // stable ranks within the wave
@@ -292,17 +330,34 @@ __global__ __launch_bounds__(kRadixThreads) void radix_scatter_kernel(RadixArgs 
     __syncthreads();
     for (uint32_t d = threadIdx.x; d < D; d += kRadixThreads) gc[d] += tb[d + 1] - tb[d];
     __syncthreads();
+#pragma unroll
+    for (int u = 0; u < U; ++u) { k[u] = kn[u]; v[u] = vn[u]; }
   }
 }
 
-// bucket sizes from the sorted keys: +(run end) at the last point of a run, -(run start) at
-// its first (two atomics per non-empty bucket; hist zeroed before)
-__global__ __launch_bounds__(kBlock) void radix_runs_kernel(const uint32_t* __restrict__ keys, int64_t n,
-                                                            uint32_t* __restrict__ hist) {
-  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
-    const uint32_t k = keys[i];
-    if (i == 0 || keys[i - 1] != k) atomicSub(&hist[k], (uint32_t)i);
-    if (i == n - 1 || keys[i + 1] != k) atomicAdd(&hist[k], (uint32_t)(i + 1));
+// cell_start straight from the sorted keys (no histogram, no scan): cell_start[b] = the first
+// position whose key is >= b, so position i (key[-1] = -1, key[n] = bins as sentinels) starts
+// every bucket b in (key[i-1], key[i]].  A wave takes 64 consecutive positions; its boundaries
+// are visited one at a time (ballot) and the wave writes each one's range together -- one
+// entry per lane, so a long run of empty buckets (clustered input, the out-of-grid bucket)
+// costs range / 64 wave stores.  Every entry of cell_start[0 .. bins] is written exactly once.
+__global__ __launch_bounds__(kBlock) void radix_bounds_kernel(const uint32_t* __restrict__ keys, int64_t n,
+                                                              uint32_t bins, uint32_t* __restrict__ cell_start) {
+  const int lane = threadIdx.x & 63;
+  const int64_t waves = (int64_t)gridDim.x * (kBlock / 64);
+  for (int64_t w0 = ((int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * 64; w0 <= n; w0 += waves * 64) {
+    const int64_t i = w0 + lane;
+    const int64_t cur = i < n ? (int64_t)keys[i] : (i == n ? (int64_t)bins : -1);
+    int64_t prev = __shfl_up(cur, 1, 64);
+    if (lane == 0) prev = w0 == 0 ? -1 : (int64_t)keys[w0 - 1];
+    uint64_t m = __ballot(i <= n && cur != prev);
+    while (m) {  // wave-uniform
+      const int src = __ffsll((unsigned long long)m) - 1;
+      m &= m - 1;
+      const int64_t lo = __shfl(prev, src, 64) + 1, hi = __shfl(cur, src, 64);
+      const uint32_t val = (uint32_t)(w0 + src);
+      for (int64_t b = lo + lane; b <= hi; b += 64) cell_start[b] = val;
+    }
   }
 }
 
@@ -317,11 +372,13 @@ hipError_t launch_radix(gf_ctx* ctx, int stage, const RadixArgs& a, int blocks) 
     case 1:
       hipLaunchKernelGGL(radix_scatter_kernel, dim3(blocks), dim3(kRadixThreads), radix_scatter_lds_bytes(), s, a);
       break;
-    default:
-      if (a.n > 0)
-        hipLaunchKernelGGL(radix_runs_kernel, dim3(stream_blocks(a.n, kBlock)), dim3(kBlock), 0, s, a.kout, a.n,
-                           a.M);
+    default: {  // cell_start[0 .. gn*gn + 1] of the sorted kout into a.M
+      const int64_t waves = (a.n + 1 + 63) / 64;
+      const int64_t nb = std::min<int64_t>(std::max<int64_t>((waves + kBlock / 64 - 1) / (kBlock / 64), 1), 4096);
+      hipLaunchKernelGGL(radix_bounds_kernel, dim3((unsigned)nb), dim3(kBlock), 0, s, a.kout, a.n,
+                         (uint32_t)a.gn * (uint32_t)a.gn + 1u, a.M);
       break;
+    }
   }
   return hipGetLastError();
 }

@@ -9,6 +9,9 @@ for p in (ROOT, os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests", "golde
         sys.path.insert(0, p)
 
 GOLDEN = os.path.join(ROOT, "tests", "golden")
+# extra flags for the host builds of native code the tests compile (tests/native/*.cpp):
+# `make asan-test` sets -fsanitize=address,undefined (the process preloads the runtimes)
+NATIVE_FLAGS = os.environ.get("GF_NATIVE_SANITIZE", "").split()
 BEIJING = (115.5, 117.6, 39.6, 41.1)
 QPOINT = (116.414899, 39.920374)
 

@@ -13,7 +13,7 @@ from fractions import Fraction
 import numpy as np
 import pytest
 
-from conftest import ROOT
+from conftest import NATIVE_FLAGS, ROOT
 
 OK, BAD, UNSUP = 0, 1, 2
 
@@ -21,7 +21,7 @@ OK, BAD, UNSUP = 0, 1, 2
 @pytest.fixture(scope="module")
 def core(tmp_path_factory):
     out = str(tmp_path_factory.mktemp("core") / "decimal_core.so")
-    subprocess.run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off",
+    subprocess.run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", *NATIVE_FLAGS,
                     os.path.join(ROOT, "tests", "native", "decimal_core.cpp"), "-o", out], check=True)
     L = C.CDLL(out)
     L.core_parse_double.argtypes = [C.c_char_p, C.c_int64, C.POINTER(C.c_double)]

@@ -11,7 +11,7 @@ import subprocess
 import numpy as np
 import pytest
 
-from conftest import ROOT
+from conftest import NATIVE_FLAGS, ROOT
 from geojson_gen import BAD, TRICKY, lines
 
 OBJID_NULL = (1 << 63) - 1
@@ -20,7 +20,7 @@ OBJID_NULL = (1 << 63) - 1
 @pytest.fixture(scope="module")
 def core(tmp_path_factory):
     out = str(tmp_path_factory.mktemp("gcore") / "geojson_core.so")
-    subprocess.run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off",
+    subprocess.run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", *NATIVE_FLAGS,
                     os.path.join(ROOT, "tests", "native", "geojson_core.cpp"), "-o", out], check=True)
     L = C.CDLL(out)
     L.geojson_core_parse.argtypes = [C.c_char_p, C.c_void_p, C.c_int64, C.c_char_p, C.c_char_p, C.c_int, C.c_int,

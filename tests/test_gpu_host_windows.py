@@ -107,3 +107,63 @@ def test_knn_needs_objid_column(sf, oracle_mod):
     np.testing.assert_array_equal(oi[: m.value], ei)
     L.gf_knn_plan_destroy(plan)
     L.gf_window_destroy(w)
+
+
+@pytest.mark.parametrize("depth", [1, 3])
+def test_knn_mapped_objid_stream(sf, oracle_mod, depth):
+    """Host windows at 16 B per point over PCIe (gf_window_upload_mapped): x, y copied, the objID
+    column read in place from pinned host memory -- only the candidates' objIDs cross the bus.
+    5 host windows double-buffered through 2 device windows (upload(i+1) before evaluate(i)), the
+    records written into pinned memory, a plan at depth 1 and at depth 3; every record == the
+    oracle's; pageable objID memory is refused (GF_ERR_ARG)."""
+    import torch
+
+    from spatialflink_amd import _lib
+
+    L = _lib.lib()
+    ctx = _lib.context(0)
+    g = sf.UniformGrid(500, *BEIJING)
+    og = oracle_mod.grid(500, *BEIJING)
+    n, k, r, nw = 1_100_000, 50, 0.5, 5
+    hosts = []
+    for i in range(nw):
+        x, y = oracle_mod.java_random_points(700 + i, n, *BEIJING)
+        obj = (np.random.default_rng(i).permutation(n) % (n // 2)).astype(np.int64)
+        hosts.append((x, y, obj))
+    pins = [pinned_columns(L, list(h)) for h in hosts]
+    wins = []
+    for _ in range(2):
+        w = C.c_void_p()
+        _lib.check(L.gf_window_create(ctx.handle, n, C.byref(w)), ctx.handle, "window")
+        wins.append(w)
+    q = sf.Point("q", *QPOINT, 0, g)
+    op = sf.PointPointKNNQuery(sf.QueryConfiguration(sf.QueryType.WindowBased), g)
+    _, plan = op.plan(0, q, r, k)
+    op.set_pipeline(0, q, r, k, depth)
+    rec = sf.PinnedRecords(nw, k)
+    cols = lambda i: pins[i][1]  # noqa: E731
+    _lib.check(L.gf_window_upload_mapped(wins[0], cols(0)[0], cols(0)[1], cols(0)[2], n), ctx.handle, "upload")
+    for i in range(nw):
+        if i + 1 < nw:
+            _lib.check(L.gf_window_upload_mapped(wins[(i + 1) % 2], cols(i + 1)[0], cols(i + 1)[1], cols(i + 1)[2], n),
+                       ctx.handle, "upload")
+        pts = _lib.GfPoints()
+        _lib.check(L.gf_window_points(wins[i % 2], C.byref(pts)), ctx.handle, "points")
+        assert pts.objID == cols(i)[2] or pts.objID  # the mapped host column
+        _lib.check(L.gf_knn_enqueue(plan, C.byref(pts), C.c_void_p(rec.ptr(i))), ctx.handle, "enqueue")
+    op.flush(0, q, r, k)
+    torch.cuda.synchronize()
+    for i, (x, y, obj) in enumerate(hosts):
+        st, o, d, ix = rec.decode(i)
+        est, eo, ed, ei = oracle_mod.knn(og, x, y, obj, QPOINT[0], QPOINT[1], r, k)
+        assert st == 0, f"window {i} flagged"
+        np.testing.assert_array_equal(o, eo)
+        np.testing.assert_array_equal(d, ed)
+        np.testing.assert_array_equal(ix, ei)
+    x, y, obj = hosts[0]
+    assert L.gf_window_upload_mapped(wins[0], x.ctypes.data, y.ctypes.data, obj.ctypes.data, n) == _lib.GF_ERR_ARG
+    op.set_pipeline(0, q, r, k, 1)
+    for w in wins:
+        L.gf_window_destroy(w)
+    for p, _ in pins:
+        L.gf_pinned_free(p)

@@ -85,11 +85,16 @@ def test_polyknn_continuous_and_fallback(sf, oracle_mod):
     run_case(sf, oracle_mod, POLYS["square"], 400_000, 0.5, 50, cap=64)  # every scan overflows
 
 
-@pytest.mark.parametrize("name,approx,k", [("holed", False, 60), ("square", True, 20), ("generated", False, 128)])
-def test_polyknn_pipeline_depth_2(sf, oracle_mod, name, approx, k):
-    """Depth 2 (PointPolygonKNNQuery.java:245-317 per window): one launch per window carries the
-    previous window's select; windows of mixed sizes (sampled and small), a window far from the
-    polygon (empty result), flush, then the synchronous API on the same plan.  Depth 3 is refused."""
+@pytest.mark.parametrize("name,approx,k,depth", [("holed", False, 60, 2), ("square", True, 20, 2),
+                                                ("generated", False, 128, 2), ("holed", False, 60, 3),
+                                                ("square", True, 20, 3), ("generated", False, 128, 3),
+                                                ("square", False, 300, 3)])
+def test_polyknn_pipeline_depth_2(sf, oracle_mod, name, approx, k, depth):
+    """Depths 2 / 3 (PointPolygonKNNQuery.java:245-317 per window): one prefilter launch per window
+    carries the select of the window before (depth 2) or of the window two back, the windows
+    alternating over two streams (depth 3, one plan); k = 300 takes the unfused pipeline.  Windows
+    of mixed sizes (sampled and small), a window far from the polygon (empty result), flush, then
+    the synchronous API on the same plan."""
     import torch
 
     g = sf.UniformGrid(500, *BEIJING)
@@ -103,7 +108,7 @@ def test_polyknn_pipeline_depth_2(sf, oracle_mod, name, approx, k):
         x, y = oracle_mod.java_random_points(seed, n, *bounds)
         obj = (np.random.default_rng(seed).permutation(n) % max(1, n // 2)).astype(np.int64)
         data.append((x, y, obj, sf.PointWindow.from_numpy(x, y, obj)))
-    op.set_pipeline(0, P, 0.2, k, 2)
+    op.set_pipeline(0, P, 0.2, k, depth)
     order = [0, 1, 2, 3, 4, 0, 0, 2, 3, 1]
     rec = sf.PinnedRecords(len(order), k)
     for i, j in enumerate(order):
@@ -123,6 +128,4 @@ def test_polyknn_pipeline_depth_2(sf, oracle_mod, name, approx, k):
         m, eo, ed, ei = oracle_mod.knn_ppoly(og, x, y, obj, OP, 0.2, k, approx)
         np.testing.assert_array_equal(res.objID, eo)
         np.testing.assert_array_equal(res.dist, ed)
-    with pytest.raises(ValueError):
-        op.set_pipeline(0, P, 0.2, k, 3)
     op.set_pipeline(0, P, 0.2, k, 1)

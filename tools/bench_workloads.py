@@ -1210,8 +1210,10 @@ def bench_polyknn(args):
     wins = _windows(sf, n, 4, 61)
     op = sf.PointPolygonKNNQuery(sf.QueryConfiguration(sf.QueryType.WindowBased), grid)
     ctx, plan = op.plan(0, P, args.radius, args.k)
-    # polygon plans run at depth <= 2: window i's select rides in block 0 of window i+1's scan
-    depth = min(args.pipeline, 2)
+    # depth 2: window i's select rides in block 0 of window i+1's prefilter scan; depth 3 (the
+    # default): in window i+2's, consecutive windows on the plan's two streams -- ONE plan, the
+    # product path a Flink shim holding one PointPolygonKNNQuery plan gets
+    depth = args.pipeline
     _lib.check(L.gf_knn_plan_set_pipeline(plan, depth), ctx.handle, "pipeline")
     ctxs, plans = [ctx], [plan]
     cs = sf.PolygonSet([P]).c_struct()
@@ -1279,14 +1281,17 @@ def bench_polyknn(args):
     avg = sms / 1000.0 / max(scnt, 1)
     # windows in flight: a launch's own duration counts shared time several times, so the rate
     # is bytes per window over the window interval (as the range lines)
-    basis = (f"bytes per window / window interval ({nst} streams; includes host work)" if nst > 1
-             else "bytes per window / average prefilter-scan launch")
+    interval = nst > 1 or depth == 3
+    basis = (f"bytes per window / window interval ({nst} plan(s), depth {depth}: launches of consecutive windows "
+             "overlap; includes host work)" if interval else "bytes per window / average prefilter-scan launch")
+    kern = {1: "knn_poly_scan", 2: "knn_poly_fused (prefilter scan + the previous window's select in block 0)",
+            3: "knn_poly_fused (prefilter scan + the select of the window two back in block 0; consecutive "
+               "windows on the plan's two streams)"}[depth]
     _line("polygon-query kNN k=%d" % args.k, n * args.steps / elapsed, "points/s", args.steps, args.warmup, elapsed,
-          "knn_poly_fused (prefilter scan + the previous window's select in block 0)" if depth == 2 else "knn_poly_scan",
-          16.0 * n, elapsed / args.steps if nst > 1 else avg,
+          kern, 16.0 * n, elapsed / args.steps if interval else avg,
           {"config": {"workload": f"knn_ppoly_k{args.k}_r{args.radius}_{n // 1_000_000}Mpts_grid500_square0.02",
                       "points_per_window": n, "k": args.k, "radius": args.radius, "pipeline_depth": depth,
-                      "windows_in_flight": nst},
+                      "plans": nst, "windows_in_flight": nst * (2 if depth == 3 else 1)},
            "breakdown": {"scan_us": round(avg * 1e6, 2), "sample_us": round(1000 * pms / max(pcnt, 1), 2),
                          "select_us": round(1000 * lms / max(lcnt, 1), 2), "achieved_basis": basis},
            "fallback_windows": fallbacks, "verified_vs_oracle": verified,
