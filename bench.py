@@ -191,7 +191,7 @@ def main():
     ap.add_argument("--string-objids", action="store_true",
                     help="objIDs are dictionary Strings (\"veh%%09d\", MN_Q1.java:52's deviceId): N > 1 exchanges "
                          "string records (gf_knn_attach_strings + gf_knn_merge_dev_strings)")
-    ap.add_argument("--pipeline", type=int, default=3, choices=(1, 2, 3),
+    ap.add_argument("--pipeline", type=int, default=3, choices=(1, 2, 3, 4),
                     help="windows in flight: 2 overlaps window i's select with window i+1's scan; 3 also "
                          "overlaps consecutive windows' launches on two streams")
     args = ap.parse_args()
@@ -288,8 +288,8 @@ def main():
             sharding.allgather_knn_records_strings(slots[g % 2, : hi - lo + 1], args.k, scap, sdict, hstr.ptr(lo))
         else:
             sharding.allgather_knn_records_batch(slots[g % 2, : hi - lo + 1], args.k, host.ptr(lo))
-        if args.pipeline == 3:
-            # depth 3 writes odd windows' records on the plan's second stream: it must not
+        if args.pipeline >= 3:
+            # depth >= 3 writes windows' records on the plan's other streams: they must not
             # reuse slots[g % 2] (group g + 2) before this all-gather + merge have read them
             _lib.check(L.gf_ctx_fork(ctx.handle), ctx.handle, "gf_ctx_fork")
         pending[0] = hi + 1
@@ -306,7 +306,7 @@ def main():
             _lib.check(enqueue(plan, pts_ref[i % args.windows], slots[g % 2, w_].data_ptr()), ctx.handle, "enqueue")
             c = i - lag  # this window's record is complete now
             if c >= first and (c - first) % B == B - 1:
-                if args.pipeline == 3:  # odd windows' records are written on the plan's second stream
+                if args.pipeline >= 3:  # windows' records are written on the plan's other streams too
                     L.gf_ctx_join(ctx.handle)
                 exchange(first, c - B + 1, c)
 
@@ -568,7 +568,7 @@ def main():
         # depth 3 keeps two launches in flight (one per stream), so a launch's own duration
         # overlaps its neighbour's: the kernel's sustained rate is then bytes per launch over the
         # launch interval (= ms_per_step, host included), not over one launch's duration
-        in_flight = 2 if args.pipeline == 3 else 1
+        in_flight = args.pipeline - 1 if args.pipeline >= 3 else 1
         interval_s = elapsed / args.steps if in_flight > 1 else avg_scan_s
         achieved = bytes_per_launch / interval_s / 1e9
         line = {
@@ -605,8 +605,10 @@ def main():
                 "kernel": {1: "knn_scan",
                            2: "knn_fused (scan of window i + select of window i-1 in block 0)",
                            3: "knn_fused (scan of window i + select of window i-2 in block 0; "
-                              "consecutive windows on two streams)"}[args.pipeline],
-                "achieved_basis": ("bytes per launch / launch interval (2 launches in flight)" if in_flight > 1
+                              "consecutive windows on two streams)",
+                           4: "knn_fused (scan of window i + select of window i-3 in block 0; "
+                              "consecutive windows on three streams)"}[args.pipeline],
+                "achieved_basis": (f"bytes per launch / launch interval ({in_flight} launches in flight)" if in_flight > 1
                                    else "bytes per launch / avg launch duration (HIP events)"),
                 "launches_in_flight": in_flight,
                 "achieved": round(achieved, 1),

@@ -119,12 +119,12 @@ void        gf_ctx_destroy(gf_ctx* ctx);
 int         gf_ctx_set_stream(gf_ctx* ctx, void* hip_stream);
 void*       gf_ctx_stream(gf_ctx* ctx);
 int         gf_ctx_synchronize(gf_ctx* ctx);
-/* Make the context stream wait for everything enqueued so far on the context's second stream
- * (kNN pipeline depth 3 launches odd windows there); no-op when it has none.  Host does not block. */
+/* Make the context stream wait for everything enqueued so far on the context's other streams
+ * (kNN pipeline depth >= 3 launches windows there); no-op when it has none.  Host does not block. */
 int         gf_ctx_join(gf_ctx* ctx);
-/* The converse: make the second stream wait for everything enqueued so far on the context
- * stream.  Call it after producing a window on the context stream and before a depth-3
- * gf_knn_enqueue of it (gf_window_upload and gf_knn_run do it themselves). */
+/* The converse: make the other streams wait for everything enqueued so far on the context
+ * stream.  Call it after producing a window on the context stream and before a depth >= 3
+ * gf_knn_enqueue of it (gf_window_points and gf_knn_run do it themselves). */
 int         gf_ctx_fork(gf_ctx* ctx);
 const char* gf_ctx_last_error(gf_ctx* ctx);
 /* Context flags (testing / tuning).  GF_FLAG_JOIN_LEGACY: 1 = gf_join_pp probes the query
@@ -252,15 +252,16 @@ int    gf_knn_plan_set_index_base(gf_knn_plan* plan, int64_t base);
  * or by gf_knn_plan_flush (stream-ordered on the context stream).  No sample kernel: a cold
  * or failed hint flags the window (status 1, re-evaluated exactly by gf_knn_decode) and the
  * threshold adapts (shrinks after an overflow, doubles when fewer than k lie below it).
- * k in (256, 512] at depth 2 / 3: the select needs the standalone kernel's sort area, so it is
- * not fused: each window runs [sample] + scan + select on its lane, its record complete in stream
- * order; depth 3 alternates two lanes between the context stream and the second stream (each
- * lane's hint chain on one stream), so consecutive windows overlap.  k > 512: see above.
- * depth 3 (k <= 256): window i's fused launch selects window i-2; odd windows launch on a
- * second (non-blocking) stream, so consecutive launches overlap.  Window buffers must be
- * complete before their enqueue: no cross-stream wait is inserted for them (gf_ctx_fork after
- * producing one on the context stream); gf_knn_plan_flush joins the second stream back.  The sliding engine rejects depth 3.
- * Results are identical at every depth. */
+ * depth d = 3 or 4 (k <= 256): S = d - 1 streams (the context stream + S - 1 non-blocking ones);
+ * window i launches on stream i % S, scans lane i % 2S and selects window i - S -- the previous
+ * launch on the same stream -- in block 0, so S launches are in flight and every dependency stays
+ * stream-ordered.  Polygon plans: the same, with each window's refine after its prefilter launch.
+ * Window buffers must be complete before their enqueue: no cross-stream wait is inserted for them
+ * (gf_ctx_fork after producing one on the context stream); gf_knn_plan_flush joins the other
+ * streams back.  k in (256, 512] at depth >= 2: the select needs the standalone kernel's sort
+ * area, so it is not fused: each window runs [sample] + scan + select on its lane, its record
+ * complete in stream order; depth d >= 3 spreads windows over S streams, one lane each.  k > 512:
+ * see above.  The sliding engine rejects depth > 2.  Results are identical at every depth. */
 int    gf_knn_plan_set_pipeline(gf_knn_plan* plan, int depth);
 int    gf_knn_plan_flush(gf_knn_plan* plan);
 /* Result record: gf_knn_header followed by double dist[k], int64 objID[k], int64 idx[k]. */

@@ -267,10 +267,11 @@ extern "C" void gf_ctx_destroy(gf_ctx* ctx) {
   if (ctx->scratch) hipFree(ctx->scratch);
   if (ctx->pinned) hipHostFree(ctx->pinned);
   if (ctx->own_stream) hipStreamDestroy(ctx->own_stream);
-  if (ctx->aux) {
-    hipStreamSynchronize(ctx->aux);
-    hipStreamDestroy(ctx->aux);
-  }
+  for (hipStream_t a : {ctx->aux, ctx->aux2})
+    if (a) {
+      hipStreamSynchronize(a);
+      hipStreamDestroy(a);
+    }
   delete ctx;
 }
 
@@ -286,10 +287,13 @@ extern "C" int gf_ctx_join(gf_ctx* ctx) {
   if (!ctx->aux) return GF_OK;
   int st = bind(ctx);
   if (st) return st;
-  hipEvent_t ev = take_event(ctx);
-  GF_HIP_CHECK(ctx, hipEventRecord(ev, ctx->aux));
-  GF_HIP_CHECK(ctx, hipStreamWaitEvent(ctx->stream, ev, 0));
-  ctx->pool.push_back(ev);
+  for (hipStream_t a : {ctx->aux, ctx->aux2}) {
+    if (!a) continue;
+    hipEvent_t ev = take_event(ctx);
+    GF_HIP_CHECK(ctx, hipEventRecord(ev, a));
+    GF_HIP_CHECK(ctx, hipStreamWaitEvent(ctx->stream, ev, 0));
+    ctx->pool.push_back(ev);
+  }
   return GF_OK;
 }
 
@@ -300,16 +304,24 @@ extern "C" int gf_ctx_fork(gf_ctx* ctx) {
   if (st) return st;
   hipEvent_t ev = take_event(ctx);
   GF_HIP_CHECK(ctx, hipEventRecord(ev, ctx->stream));
-  GF_HIP_CHECK(ctx, hipStreamWaitEvent(ctx->aux, ev, 0));
+  for (hipStream_t a : {ctx->aux, ctx->aux2})
+    if (a) GF_HIP_CHECK(ctx, hipStreamWaitEvent(a, ev, 0));
   ctx->pool.push_back(ev);
   return GF_OK;
 }
 
+namespace gf {
+int sync_aux(gf_ctx* ctx) {
+  for (hipStream_t a : {ctx->aux, ctx->aux2})
+    if (a) GF_HIP_CHECK(ctx, hipStreamSynchronize(a));
+  return GF_OK;
+}
+}  // namespace gf
+
 extern "C" int gf_ctx_synchronize(gf_ctx* ctx) {
   if (!ctx) return GF_ERR_ARG;
   GF_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
-  if (ctx->aux) GF_HIP_CHECK(ctx, hipStreamSynchronize(ctx->aux));
-  return GF_OK;
+  return sync_aux(ctx);
 }
 
 extern "C" const char* gf_ctx_last_error(gf_ctx* ctx) { return ctx ? ctx->last_error.c_str() : "null context"; }
@@ -341,7 +353,7 @@ extern "C" int gf_ctx_timing(gf_ctx* ctx, int kid, double* total_ms, int64_t* la
   int st = bind(ctx);
   if (st) return st;
   GF_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
-  if (ctx->aux) GF_HIP_CHECK(ctx, hipStreamSynchronize(ctx->aux));
+  if (int e = sync_aux(ctx)) return e;
   for (auto& e : ctx->pending) {
     float ms = 0.f;
     if (hipEventElapsedTime(&ms, e.a, e.b) == hipSuccess) {
@@ -1223,7 +1235,7 @@ static int knn_alloc_candidates(gf_knn_plan* P, int64_t cap) {
   int st;
   // queued windows may still read the old buffers (the k > kMaxK path queues without host reads)
   GF_HIP_CHECK(P->ctx, hipStreamSynchronize(P->ctx->stream));
-  if (P->ctx->aux) GF_HIP_CHECK(P->ctx, hipStreamSynchronize(P->ctx->aux));
+  if (int e = sync_aux(P->ctx)) return e;
   for (int j = 0; j < 4; ++j)  // lanes 1.. only once pipelining allocated them
     if ((j == 0 || P->lane[j].st) && (st = knn_alloc_lane(P, j, cap))) return st;
   P->cap = cap;
@@ -1391,7 +1403,8 @@ static KnnPolyArgs poly_args(gf_knn_plan* P, int j, const gf_points* pts, int64_
   for (int i = 0; i < 4; ++i) a.bbox[i] = P->bbox[i];
   a.approx = P->approx; a.r = P->r; a.k = P->k; a.use_state = use_state; a.use_hint = use_hint;
   a.st = L.st; a.cand_d = L.cand_d; a.cand_i = L.cand_i; a.cand_o = L.cand_o; a.cap = (unsigned long long)P->cap;
-  a.maybe_i = P->maybe_i[j & 1];  // one survivor buffer per stream (depth 3: lanes 0, 2 / 1, 3)
+  // one survivor buffer per stream (depth d >= 3: lane j runs on stream j % (d - 1); depth 2: lane j)
+  a.maybe_i = P->maybe_i[P->pipeline >= 3 ? j % (P->pipeline - 1) : j];
   return a;
 }
 
@@ -1399,7 +1412,7 @@ static KnnPolyArgs poly_args(gf_knn_plan* P, int j, const gf_points* pts, int64_
 static int poly_buffers(gf_knn_plan* P) {
   if (P->maybe_cap >= P->cap) return GF_OK;
   GF_HIP_CHECK(P->ctx, hipStreamSynchronize(P->ctx->stream));
-  if (P->ctx->aux) GF_HIP_CHECK(P->ctx, hipStreamSynchronize(P->ctx->aux));
+  if (int e = sync_aux(P->ctx)) return e;
   for (auto& m : P->maybe_i) {
     if (m) hipFree(m);
     m = nullptr;
@@ -1497,6 +1510,11 @@ static int knn_large(gf_knn_plan* P, const gf_points* pts, void* result) {
   return GF_OK;
 }
 
+// stream s of a pipelined plan's windows in flight: 0 = the context stream, then the extra ones
+static hipStream_t knn_stream(gf_ctx* ctx, hipStream_t main, int s) {
+  return s == 0 ? main : (s == 1 ? ctx->aux : ctx->aux2);
+}
+
 static int knn_launch_sample(gf_knn_plan* P, int j, const gf_points* pts, int use_hint) {
   if (P->poly) {
     GF_HIP_CHECK(P->ctx, launch_knn_poly_sample(P->ctx, poly_args(P, j, pts, 0, pts->n, 1, use_hint)));
@@ -1530,76 +1548,52 @@ int gf::knn_enqueue_merge(gf_knn_plan* P, const gf_points* pts, void* result, co
   if (P->pipeline >= 2 && P->k > kFusedSelectMaxK) {
     // k in (256, 512]: the select needs the standalone kernel's sort area, so it is not fused;
     // each window runs [sample] + scan + select on its lane, complete in stream order (earlier
-    // than the depth promises).  Depth 3 alternates lanes 0 / 1 between the context stream and
-    // the second stream: each lane's hint chain stays on one stream and consecutive windows'
-    // kernels overlap.
+    // than the depth promises).  Depth d >= 3 spreads windows over d - 1 streams with one lane
+    // each: a lane's hint chain stays on one stream and consecutive windows' kernels overlap.
     const uint64_t kseq = P->seq++;
-    const int j = P->pipeline == 3 ? (int)(kseq & 1) : 0;
+    const int S = P->pipeline >= 3 ? P->pipeline - 1 : 1, j = (int)(kseq % (uint64_t)S);
     hipStream_t main = ctx->stream;
-    if (j) ctx->stream = ctx->aux;
+    ctx->stream = knn_stream(ctx, main, j);
     const bool staged = pts->n >= kSampleMinN;  // the sample kernel takes the lane's hint when it has one
     int rc = staged ? knn_launch_sample(P, j, pts, P->use_hint) : GF_OK;
     if (rc == GF_OK) rc = knn_scan_select(P, j, pts, 0, pts->n, staged ? 1 : 0, staged && P->use_hint, result);
     ctx->stream = main;
     return rc;
   }
-  if (P->pipeline == 3 && P->poly) {
-    // polygon query at depth 3: as the point plans below -- window k's prefilter scan on lane
-    // k % 4 with window k-2's select in block 0, then its refine, both on stream k % 2 -- so one
-    // plan keeps two windows' launches in flight (PointPolygonKNNQuery.java:245-317 per window)
-    if ((st = poly_buffers(P))) return st;
-    const uint64_t kseq = P->seq++;
-    const int j = (int)(kseq & 3);
+  if (P->pipeline >= 3) {
+    // depth d >= 3, S = d - 1 streams: window k launches on stream k % S, scans lane k % 2S and
+    // selects window k - S -- the previous launch on the SAME stream -- in block 0.  Every
+    // dependency (window k - S's candidates, lane k % 2S's last select in launch k - 2S, its hint)
+    // stays stream-ordered; consecutive windows' launches overlap (one's ramp-up under the
+    // other's tail), S of them in flight.  Polygon queries: the fused launch is the prefilter
+    // scan, the window's refine follows on the same stream (PointPolygonKNNQuery.java:245-317 per
+    // window).  Window buffers must be complete when enqueued (no cross-stream wait is inserted).
+    if (P->poly && (st = poly_buffers(P))) return st;
+    const uint64_t S = (uint64_t)(P->pipeline - 1), kseq = P->seq++;
+    const int j = (int)(kseq % (2 * S));
     hipStream_t main = ctx->stream;
-    ctx->stream = (kseq & 1) ? ctx->aux : main;
+    ctx->stream = knn_stream(ctx, main, (int)(kseq % S));
     int rc = GF_OK;
     do {
       const bool sample = pts->n >= kSampleMinN && (!P->use_hint || !P->lane_warm[j]);
       if (sample && (rc = knn_launch_sample(P, j, pts, 0))) break;
       P->lane_warm[j] = 1;
-      const KnnPolyArgs a = poly_args(P, j, pts, 0, pts->n, sample ? 2 : 1, 0);
       KnnSelectArgs q{};
       int has_prev = 0;
-      if (P->npq > 0 && P->pq[0].seq + 2 == kseq) {
+      if (P->npq > 0 && P->pq[0].seq + S == kseq) {
         const gf_knn_plan::Pend e = P->pq[0];
         q = select_args(P, e.lane, 1, P->use_hint, e.result, e.idx_base);
         has_prev = 1;
-        P->pq[0] = P->pq[1];
+        for (int t = 1; t < P->npq; ++t) P->pq[t - 1] = P->pq[t];
         --P->npq;
       }
-      hipError_t he = launch_knn_poly_fused(ctx, a, q, has_prev, scan_blocks_for(P, (pts->n + 1) / 2), nullptr);
-      if (he != hipSuccess) { rc = hip_err(ctx, he, "launch_knn_poly_fused"); break; }
-      P->pq[P->npq++] = gf_knn_plan::Pend{j, result, P->idx_base, kseq};
-    } while (0);
-    ctx->stream = main;
-    return rc;
-  }
-  if (P->pipeline == 3) {
-    // window k scans on lane k % 4 and selects window k-2 in block 0; odd windows launch on the
-    // aux stream, so consecutive windows' kernels overlap (ramp-up of one under the tail of the
-    // other) while every dependency -- window k-2's candidates, lane k % 4's last select (in
-    // kernel k-2) and its hint -- stays on the same stream.  Window buffers must be complete
-    // when enqueued (no cross-stream wait is inserted for them).
-    const uint64_t kseq = P->seq++;
-    const int j = (int)(kseq & 3);
-    hipStream_t main = ctx->stream;
-    ctx->stream = (kseq & 1) ? ctx->aux : main;
-    int rc = GF_OK;
-    do {
-      const bool sample = pts->n >= kSampleMinN && (!P->use_hint || !P->lane_warm[j]);
-      if (sample && (rc = knn_launch_sample(P, j, pts, 0))) break;
-      P->lane_warm[j] = 1;
-      const KnnScanArgs s = scan_args(P, j, pts, 0, pts->n, sample ? 2 : 1);
-      KnnSelectArgs q{};
-      int has_prev = 0;
-      if (P->npq > 0 && P->pq[0].seq + 2 == kseq) {
-        const gf_knn_plan::Pend e = P->pq[0];
-        q = select_args(P, e.lane, 1, P->use_hint, e.result, e.idx_base);
-        has_prev = 1;
-        P->pq[0] = P->pq[1];
-        --P->npq;
-      }
-      hipError_t he = launch_knn_fused(ctx, s, q, has_prev, scan_blocks_for(P, pts->n), P->scan_nt, merge);
+      hipError_t he;
+      if (P->poly)
+        he = launch_knn_poly_fused(ctx, poly_args(P, j, pts, 0, pts->n, sample ? 2 : 1, 0), q, has_prev,
+                                   scan_blocks_for(P, (pts->n + 1) / 2), nullptr);
+      else
+        he = launch_knn_fused(ctx, scan_args(P, j, pts, 0, pts->n, sample ? 2 : 1), q, has_prev,
+                              scan_blocks_for(P, pts->n), P->scan_nt, merge);
       if (he != hipSuccess) { rc = hip_err(ctx, he, "launch_knn_fused"); break; }
       P->pq[P->npq++] = gf_knn_plan::Pend{j, result, P->idx_base, kseq};
     } while (0);
@@ -1657,15 +1651,15 @@ int gf::knn_enqueue_merge(gf_knn_plan* P, const gf_points* pts, void* result, co
 
 extern "C" int gf_knn_plan_flush(gf_knn_plan* P) {
   if (!P) return GF_ERR_ARG;
-  if (P->pipeline == 3) {
-    if (P->npq == 0) return P->k > kFusedSelectMaxK ? gf_ctx_join(P->ctx) : GF_OK;  // mid k: lane 1's stream
+  if (P->pipeline >= 3) {
+    if (P->npq == 0) return P->k > kFusedSelectMaxK ? gf_ctx_join(P->ctx) : GF_OK;  // mid k: the other streams
     gf_ctx* ctx = P->ctx;
     int st = bind(ctx);
     if (st) return st;
     hipStream_t main = ctx->stream;
     for (int e = 0; e < P->npq; ++e) {
       const gf_knn_plan::Pend& w = P->pq[e];
-      ctx->stream = (w.seq & 1) ? ctx->aux : main;
+      ctx->stream = knn_stream(ctx, main, (int)(w.seq % (uint64_t)(P->pipeline - 1)));
       hipError_t he = launch_knn_select(ctx, select_args(P, w.lane, 1, P->use_hint, w.result, w.idx_base));
       ctx->stream = main;
       if (he != hipSuccess) return hip_err(ctx, he, "launch_knn_select");
@@ -1686,18 +1680,21 @@ extern "C" int gf_knn_plan_flush(gf_knn_plan* P) {
 }
 
 extern "C" int gf_knn_plan_set_pipeline(gf_knn_plan* P, int depth) {
-  if (!P || depth < 1 || depth > 3) return GF_ERR_ARG;
+  if (!P || depth < 1 || depth > 4) return GF_ERR_ARG;
   gf_ctx* ctx = P->ctx;
   int st = bind(ctx);
   if (st || (st = gf_knn_plan_flush(P))) return st;
   GF_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
-  if (ctx->aux) GF_HIP_CHECK(ctx, hipStreamSynchronize(ctx->aux));
+  if (int e = sync_aux(ctx)) return e;
   // k > 512 plans return through knn_large (lane 0, stream-ordered) before any pipelined path:
   // no extra lanes, no second stream
-  for (int j = 1; !P->large && j < (depth == 3 ? 4 : depth); ++j)
+  const int lanes = depth >= 3 ? 2 * (depth - 1) : depth;
+  for (int j = 1; !P->large && j < lanes; ++j)
     if (!P->lane[j].st && (st = knn_alloc_lane(P, j, P->cap))) return st;
-  if (depth == 3 && !P->large && !ctx->aux)
+  if (depth >= 3 && !P->large && !ctx->aux)
     GF_HIP_CHECK(ctx, hipStreamCreateWithFlags(&ctx->aux, hipStreamNonBlocking));
+  if (depth >= 4 && !P->large && !ctx->aux2)
+    GF_HIP_CHECK(ctx, hipStreamCreateWithFlags(&ctx->aux2, hipStreamNonBlocking));
   P->pipeline = depth;
   P->seq = 0;
   for (int& w : P->lane_warm) w = 0;
@@ -1805,7 +1802,7 @@ extern "C" int gf_knn_run(gf_knn_plan* P, const gf_points* pts, int64_t* oo, dou
   gf_ctx* ctx = P->ctx;
   // the synchronous call may get a window the caller produced on the context stream just now:
   // order the second stream after it (nothing to overlap with in a synchronous call)
-  int st = P->pipeline == 3 ? gf_ctx_fork(ctx) : GF_OK;
+  int st = P->pipeline >= 3 ? gf_ctx_fork(ctx) : GF_OK;
   if (st) return st;
   st = gf_knn_enqueue(P, pts, P->tmp_result);
   if (st || (st = gf_knn_plan_flush(P))) return st;
@@ -2147,7 +2144,8 @@ extern "C" int gf_window_create(gf_ctx* ctx, int64_t capacity, gf_window** out) 
       hipStreamCreateWithFlags(&w->copy, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&w->ready, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&w->fence_main, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&w->fence_aux, hipEventDisableTiming) != hipSuccess) {
+      hipEventCreateWithFlags(&w->fence_aux, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&w->fence_aux2, hipEventDisableTiming) != hipSuccess) {
     gf_window_destroy(w);
     return set_err(ctx, GF_ERR_NOMEM, "gf_window_create: device allocation failed");
   }
@@ -2160,7 +2158,7 @@ extern "C" void gf_window_destroy(gf_window* w) {
   hipSetDevice(w->ctx->device);
   if (w->copy) hipStreamSynchronize(w->copy);
   hipStreamSynchronize(w->ctx->stream);
-  if (w->ctx->aux) hipStreamSynchronize(w->ctx->aux);
+  sync_aux(w->ctx);
   if (w->x) hipFree(w->x);
   if (w->y) hipFree(w->y);
   if (w->objID) hipFree(w->objID);
@@ -2168,6 +2166,7 @@ extern "C" void gf_window_destroy(gf_window* w) {
   if (w->ready) hipEventDestroy(w->ready);
   if (w->fence_main) hipEventDestroy(w->fence_main);
   if (w->fence_aux) hipEventDestroy(w->fence_aux);
+  if (w->fence_aux2) hipEventDestroy(w->fence_aux2);
   if (w->copy) hipStreamDestroy(w->copy);
   delete w;
 }
@@ -2185,6 +2184,10 @@ extern "C" int gf_window_upload(gf_window* w, const double* x, const double* y, 
   if (ctx->aux) {
     GF_HIP_CHECK(ctx, hipEventRecord(w->fence_aux, ctx->aux));
     GF_HIP_CHECK(ctx, hipStreamWaitEvent(w->copy, w->fence_aux, 0));
+  }
+  if (ctx->aux2) {
+    GF_HIP_CHECK(ctx, hipEventRecord(w->fence_aux2, ctx->aux2));
+    GF_HIP_CHECK(ctx, hipStreamWaitEvent(w->copy, w->fence_aux2, 0));
   }
   const size_t b = 8 * (size_t)n;
   if (n) {  // only the columns given: range / join read x, y (16 B per point), kNN adds objID

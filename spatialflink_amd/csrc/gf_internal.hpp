@@ -39,7 +39,8 @@ struct gf_ctx {
   int geojson_walk = 0; // testing: every GeoJSON line takes the member-by-member walk
   int join_async_done = 0;  // gf_join_pp_async: the packing kernel wrote the count
   double join_ppp = 0.0;  // pairs per ordinary point of the last join (sizes the output chunks)
-  hipStream_t aux = nullptr;  // kNN depth 3: odd windows' launches (created on first use)
+  hipStream_t aux = nullptr;   // kNN depth >= 3: the second stream of windows in flight (created on first use)
+  hipStream_t aux2 = nullptr;  // kNN depth 4: the third
   gf_objid_dict* dict = nullptr;  // the context's default objID dictionary (created on first use)
   // gf_bitmap_to_indices_async: block tickets + look-back status (grown on demand)
   unsigned long long* expand_ticket = nullptr;
@@ -85,6 +86,7 @@ namespace gf {
 int set_err(gf_ctx* ctx, int code, const std::string& msg);
 int hip_err(gf_ctx* ctx, hipError_t e, const char* what);
 void* ctx_scratch(gf_ctx* ctx, size_t bytes, int* status);
+int sync_aux(gf_ctx* ctx);  // synchronize the kNN pipeline's extra streams (depth >= 3)
 void* ctx_pinned(gf_ctx* ctx, size_t bytes, int* status);
 int bind(gf_ctx* ctx);
 
@@ -112,6 +114,17 @@ constexpr int kFusedSelectMaxK = 256;  // largest k of the select fused into blo
 constexpr int kSampleBlocks = 128;  // kNN sample: 128 blocks x 2048 points = 256K points
 constexpr int kSamplePerBlock = 2048;
 constexpr int64_t kSampleMinN = 1 << 20;
+
+// A block barrier for LDS hand-offs only: waits for this wave's LDS operations (lgkmcnt(0)), not
+// for its outstanding global loads -- __syncthreads() also drains vmcnt, which lands a tile loop's
+// prefetched next-tile loads at the current tile's first barrier.  Global stores are not ordered
+// by it either: use it only where the threads exchange data through LDS.
+__device__ __forceinline__ void lds_barrier() {
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // vmcnt(63) expcnt(7) lgkmcnt(0)
+  __builtin_amdgcn_s_barrier();
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+}
 
 // single-query classification (exact, from host-side cell thresholds)
 struct QueryRect {
@@ -791,12 +804,12 @@ struct gf_knn_plan {
     double* cand_d = nullptr;
     uint32_t* cand_i = nullptr;
     int64_t* cand_o = nullptr;
-  } lane[4];  // depth 3 uses four
+  } lane[6];  // depth d >= 3 uses 2 (d - 1): two per stream
   int64_t cap = 0;
   int pipeline = 1;               // 1: sample -> scan -> select per window; 2: fused
   uint64_t seq = 0;
   int pend_lane = -1;             // depth 2: the window whose select has not run yet
-  int lane_warm[4] = {0, 0, 0, 0};  // depth 2 / 3: the lane has a hint from an earlier window
+  int lane_warm[6] = {0, 0, 0, 0, 0, 0};  // depth >= 2: the lane has a hint from an earlier window
   void* pend_result = nullptr;
   int64_t pend_idx_base = 0;      // depth 2: idx_base of the pending window (set at its enqueue)
   // depth 3: windows whose select has not run yet (seq k-1, k-2), oldest first
@@ -806,7 +819,7 @@ struct gf_knn_plan {
     int64_t idx_base;
     uint64_t seq;
   };
-  Pend pq[2];
+  Pend pq[3];
   int npq = 0;
   int use_hint = 1;             // reuse the previous window's k-th distance as the threshold guess
   int64_t idx_base = 0;
@@ -824,7 +837,7 @@ struct gf_knn_plan {
   double* vy = nullptr;
   double* ring_env = nullptr;
   double bbox[4] = {0, 0, 0, 0};
-  uint32_t* maybe_i[2] = {nullptr, nullptr};  // per lane, cap entries
+  uint32_t* maybe_i[3] = {nullptr, nullptr, nullptr};  // per stream, cap entries
   int64_t maybe_cap = 0;
 };
 
@@ -841,6 +854,6 @@ struct gf_window {
   // the context's streams (which may still read the previous contents), and gf_window_points
   // makes the context's streams wait for the copy -- so upload(i+1) overlaps evaluate(i)
   hipStream_t copy = nullptr;
-  hipEvent_t ready = nullptr, fence_main = nullptr, fence_aux = nullptr;
+  hipEvent_t ready = nullptr, fence_main = nullptr, fence_aux = nullptr, fence_aux2 = nullptr;
   bool pending = false;
 };

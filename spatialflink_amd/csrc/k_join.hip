@@ -315,7 +315,7 @@ __device__ __forceinline__ void wc_row_scatter(const double* X, const double* Y,
     gd[r] = Ms[(size_t)r * kHistSplit * nblk + kHistSplit * bid] - base;
     th[r] = 0u;
   }
-  __syncthreads();
+  lds_barrier();
   const int per = (nrows + kScatThreads - 1) / kScatThreads, r0 = threadIdx.x * per;
   // the next tile's coordinates are loaded while this tile goes through its LDS phases
   double xn[kScatPer], yn[kScatPer];
@@ -343,7 +343,7 @@ __device__ __forceinline__ void wc_row_scatter(const double* X, const double* Y,
       row[u] = i < end ? rowf(x[u], y[u]) : -1;
       if (row[u] >= 0) atomicAdd(&th[row[u]], 1u);
     }
-    __syncthreads();
+    lds_barrier();
     // exclusive scan of the tile counts (a contiguous run of rows per thread); gd becomes
     // (next global slot - tile start) so that slot + gd is the destination
     uint32_t run = 0;
@@ -355,7 +355,7 @@ __device__ __forceinline__ void wc_row_scatter(const double* X, const double* Y,
       if (lane >= o) inc += t;
     }
     if (lane == 63) wsum[wid] = inc;
-    __syncthreads();
+    lds_barrier();
     uint32_t before = inc - run;
     for (int w = 0; w < wid; ++w) before += wsum[w];
     uint32_t kept = 0;
@@ -366,7 +366,7 @@ __device__ __forceinline__ void wc_row_scatter(const double* X, const double* Y,
       gd[r] -= before;
       before += v;
     }
-    __syncthreads();
+    lds_barrier();
 #pragma unroll
     for (int u = 0; u < kScatPer; ++u) {
       if (row[u] < 0) continue;
@@ -375,7 +375,7 @@ __device__ __forceinline__ void wc_row_scatter(const double* X, const double* Y,
       sidx[slot] = (uint32_t)(t0 + threadIdx.x + u * kScatThreads);
       sdst[slot] = gd[row[u]] + slot;
     }
-    __syncthreads();
+    lds_barrier();
     for (uint32_t k = threadIdx.x; k < kept; k += kScatThreads) {
       const uint32_t d = sdst[k];
       oxy[d] = sxy[k];
@@ -385,7 +385,7 @@ __device__ __forceinline__ void wc_row_scatter(const double* X, const double* Y,
       gd[r] += th[r];
       th[r] = 0u;
     }
-    __syncthreads();
+    lds_barrier();
   }
 }
 

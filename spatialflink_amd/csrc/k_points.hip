@@ -243,24 +243,17 @@ __global__ __launch_bounds__(kRadixThreads) void radix_scatter_kernel(RadixArgs 
   int64_t beg, end;
   radix_chunk(a, beg, end);
   for (uint32_t d = threadIdx.x; d < D; d += kRadixThreads) gc[d] = a.Ms[(size_t)d * a.nblk + blockIdx.x];
-  // a tile's (key, value) per lane; the next tile's loads are issued before this tile is ranked,
-  // placed and written, so their latency hides under that work (one block per CU: nothing else
-  // would cover it)
-  auto load_tile = [&](int64_t t, uint32_t* k, uint32_t* v) {
-    const uint32_t c = (uint32_t)(end - t < kRadixTile ? end - t : kRadixTile);
+  // (r04: prefetching the next tile into registers pushed the kernel to 128 VGPRs + 80 B of
+  // scratch per lane and cost 76 -> 88 us per pass; the tile is loaded at the top of its step)
+  for (int64_t t0 = beg; t0 < end; t0 += kRadixTile) {  // block-uniform
+    const uint32_t cnt = (uint32_t)(end - t0 < kRadixTile ? end - t0 : kRadixTile);
+    uint32_t k[U], v[U], r[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const uint32_t e = w * EPW + u * 64 + lane;
-      k[u] = e < c ? a.kin[t + e] : 0u;
-      v[u] = e < c ? (a.vin ? a.vin[t + e] : (uint32_t)(t + e)) : 0u;
+      k[u] = e < cnt ? a.kin[t0 + e] : 0u;
+      v[u] = e < cnt ? (a.vin ? a.vin[t0 + e] : (uint32_t)(t0 + e)) : 0u;
     }
-  };
-  uint32_t k[U], v[U];
-  if (beg < end) load_tile(beg, k, v);
-  for (int64_t t0 = beg; t0 < end; t0 += kRadixTile) {  // block-uniform
-    const uint32_t cnt = (uint32_t)(end - t0 < kRadixTile ? end - t0 : kRadixTile);
-    uint32_t kn[U], vn[U], r[U];
-    if (t0 + kRadixTile < end) load_tile(t0 + kRadixTile, kn, vn);
     for (uint32_t d = lane; d < D; d += 64) wc[w * kRadixMaxDigits + d] = 0u;  // this wave's row
 #pragma unroll
     for (int u = 0; u < U; ++u) {  // stable ranks within the wave
@@ -278,7 +271,7 @@ __global__ __launch_bounds__(kRadixThreads) void radix_scatter_kernel(RadixArgs 
       base = __shfl(base, leader, 64);
       r[u] = base + (uint32_t)__popcll(peers & below);
     }
-    __syncthreads();
+    lds_barrier();
     {  // exclusive scan of the counts in (digit, wave) order: entry j = d * W + w
       constexpr int PT = W * kRadixMaxDigits / kRadixThreads;  // entries per thread
       const uint32_t j0 = threadIdx.x * PT;
@@ -296,7 +289,7 @@ __global__ __launch_bounds__(kRadixThreads) void radix_scatter_kernel(RadixArgs 
         if (lane >= o) inc += t;
       }
       if (lane == 63) ws[w] = inc;
-      __syncthreads();
+      lds_barrier();
       uint32_t before = inc - run;
       for (int q = 0; q < w; ++q) before += ws[q];
 #pragma unroll
@@ -310,7 +303,7 @@ __global__ __launch_bounds__(kRadixThreads) void radix_scatter_kernel(RadixArgs 
       }
       if (threadIdx.x == 0) tb[D] = cnt;
     }
-    __syncthreads();
+    lds_barrier();
 #pragma unroll
     for (int u = 0; u < U; ++u) {  // the tile in (digit, input) order
       const uint32_t e = w * EPW + u * 64 + lane;
@@ -320,42 +313,62 @@ __global__ __launch_bounds__(kRadixThreads) void radix_scatter_kernel(RadixArgs 
         lv[p] = v[u];
       }
     }
-    __syncthreads();
+    lds_barrier();
     for (uint32_t p = threadIdx.x; p < cnt; p += kRadixThreads) {  // runs of one digit: consecutive slots
       const uint32_t kk = lk[p], d = (kk >> a.shift) & mask;
       const uint32_t o = gc[d] + (p - tb[d]);
       a.kout[o] = kk;
       a.vout[o] = lv[p];
     }
-    __syncthreads();
+    lds_barrier();
     for (uint32_t d = threadIdx.x; d < D; d += kRadixThreads) gc[d] += tb[d + 1] - tb[d];
-    __syncthreads();
-#pragma unroll
-    for (int u = 0; u < U; ++u) { k[u] = kn[u]; v[u] = vn[u]; }
+    lds_barrier();
   }
 }
 
 // cell_start straight from the sorted keys (no histogram, no scan): cell_start[b] = the first
 // position whose key is >= b, so position i (key[-1] = -1, key[n] = bins as sentinels) starts
-// every bucket b in (key[i-1], key[i]].  A wave takes 64 consecutive positions; its boundaries
-// are visited one at a time (ballot) and the wave writes each one's range together -- one
-// entry per lane, so a long run of empty buckets (clustered input, the out-of-grid bucket)
-// costs range / 64 wave stores.  Every entry of cell_start[0 .. bins] is written exactly once.
+// every bucket b in (key[i-1], key[i]].  One wave per 256 consecutive positions (four per lane,
+// one 16-B load); its boundaries are visited one at a time (ballot) and the wave writes each
+// one's range together -- one entry per lane, so a long run of empty buckets (clustered input,
+// the out-of-grid bucket) costs range / 64 wave stores.  Every entry of cell_start[0 .. bins] is
+// written exactly once.
+constexpr int kBoundsPer = 16;  // keys per lane: four 16-B loads in flight (one per lane was latency-bound)
 __global__ __launch_bounds__(kBlock) void radix_bounds_kernel(const uint32_t* __restrict__ keys, int64_t n,
                                                               uint32_t bins, uint32_t* __restrict__ cell_start) {
   const int lane = threadIdx.x & 63;
-  const int64_t waves = (int64_t)gridDim.x * (kBlock / 64);
-  for (int64_t w0 = ((int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * 64; w0 <= n; w0 += waves * 64) {
-    const int64_t i = w0 + lane;
-    const int64_t cur = i < n ? (int64_t)keys[i] : (i == n ? (int64_t)bins : -1);
-    int64_t prev = __shfl_up(cur, 1, 64);
-    if (lane == 0) prev = w0 == 0 ? -1 : (int64_t)keys[w0 - 1];
-    uint64_t m = __ballot(i <= n && cur != prev);
+  const int64_t w0 = ((int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * (64 * kBoundsPer);
+  if (w0 > n) return;  // wave-uniform
+  const int64_t p0 = w0 + (int64_t)lane * kBoundsPer;
+  uint32_t k[kBoundsPer];
+  if (w0 + 64 * kBoundsPer <= n) {  // keys (scratch) are 16-B aligned and w0 % 1024 == 0
+#pragma unroll
+    for (int q = 0; q < kBoundsPer / 4; ++q) {
+      const uint4 v = *reinterpret_cast<const uint4*>(keys + p0 + 4 * q);
+      k[4 * q] = v.x; k[4 * q + 1] = v.y; k[4 * q + 2] = v.z; k[4 * q + 3] = v.w;
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < kBoundsPer; ++j) {
+      const int64_t p = p0 + j;
+      k[j] = p < n ? keys[p] : bins;  // the sentinel key[n] = bins (positions past n are masked)
+    }
+  }
+  uint32_t prev = __shfl_up(k[kBoundsPer - 1], 1, 64);
+  if (lane == 0) prev = w0 == 0 ? 0u : keys[w0 - 1];
+  const bool first = lane == 0 && w0 == 0;  // key[-1] = -1: position 0 starts buckets [0, key[0]]
+#pragma unroll
+  for (int j = 0; j < kBoundsPer; ++j) {
+    const int64_t p = p0 + j;
+    const uint32_t cur = k[j], pv = j == 0 ? prev : k[j - 1];
+    const bool start = j == 0 && first;
+    uint64_t m = __ballot(p <= n && (cur != pv || start));
     while (m) {  // wave-uniform
       const int src = __ffsll((unsigned long long)m) - 1;
       m &= m - 1;
-      const int64_t lo = __shfl(prev, src, 64) + 1, hi = __shfl(cur, src, 64);
-      const uint32_t val = (uint32_t)(w0 + src);
+      const bool s0 = __shfl(start ? 1 : 0, src, 64) != 0;
+      const int64_t lo = s0 ? 0 : (int64_t)__shfl(pv, src, 64) + 1, hi = __shfl(cur, src, 64);
+      const uint32_t val = (uint32_t)(w0 + (int64_t)src * kBoundsPer + j);
       for (int64_t b = lo + lane; b <= hi; b += 64) cell_start[b] = val;
     }
   }
@@ -372,9 +385,9 @@ hipError_t launch_radix(gf_ctx* ctx, int stage, const RadixArgs& a, int blocks) 
     case 1:
       hipLaunchKernelGGL(radix_scatter_kernel, dim3(blocks), dim3(kRadixThreads), radix_scatter_lds_bytes(), s, a);
       break;
-    default: {  // cell_start[0 .. gn*gn + 1] of the sorted kout into a.M
-      const int64_t waves = (a.n + 1 + 63) / 64;
-      const int64_t nb = std::min<int64_t>(std::max<int64_t>((waves + kBlock / 64 - 1) / (kBlock / 64), 1), 4096);
+    default: {  // cell_start[0 .. gn*gn + 1] of the sorted kout into a.M: one wave per 256 positions
+      const int64_t waves = (a.n + 1 + 64 * kBoundsPer - 1) / (64 * kBoundsPer);
+      const int64_t nb = (waves + kBlock / 64 - 1) / (kBlock / 64);
       hipLaunchKernelGGL(radix_bounds_kernel, dim3((unsigned)nb), dim3(kBlock), 0, s, a.kout, a.n,
                          (uint32_t)a.gn * (uint32_t)a.gn + 1u, a.M);
       break;

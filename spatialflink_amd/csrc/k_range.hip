@@ -309,19 +309,48 @@ __device__ __forceinline__ void waveq_round(const RangeArgs& a, const RangeLds& 
   q.cnt = rest;
 }
 
-// One wave-tile = 128 consecutive points = bitmap words w, w+1: lane l evaluates points
-// t + l and t + 64 + l, so the two ballots ARE the two words (one 16-B store by lane 0).
+// Tile layout.  kRangeVec (default): lane l holds points t + 2l and t + 2l + 1, read with one
+// 16-B load per coordinate (half the load instructions of 8-B loads, twice the bytes in flight
+// per outstanding load -- the scan was latency-bound with 8-B loads: SQ_WAIT_ANY 0.62, VALU 0.25
+// on C3); a tile's bitmap words are the two ballots bit-interleaved (lanes 0-31 -> word w, lanes
+// 32-63 -> word w + 1).  Otherwise lane l holds t + l and t + 64 + l and the ballots ARE the words.
+#ifndef GF_RANGE_VEC
+#define GF_RANGE_VEC 1
+#endif
+constexpr bool kRangeVec = GF_RANGE_VEC != 0;
+__device__ __forceinline__ uint64_t spread32(uint32_t v) {  // bit i -> bit 2i
+  uint64_t x = v;
+  x = (x | (x << 16)) & 0x0000FFFF0000FFFFull;
+  x = (x | (x << 8)) & 0x00FF00FF00FF00FFull;
+  x = (x | (x << 4)) & 0x0F0F0F0F0F0F0F0Full;
+  x = (x | (x << 2)) & 0x3333333333333333ull;
+  x = (x | (x << 1)) & 0x5555555555555555ull;
+  return x;
+}
+// the tile's two bitmap words from the ballots of its first / second point per lane
+__device__ __forceinline__ void tile_words(uint64_t b0, uint64_t b1, uint64_t& w0, uint64_t& w1) {
+  if (kRangeVec) {
+    w0 = spread32((uint32_t)b0) | (spread32((uint32_t)b1) << 1);
+    w1 = spread32((uint32_t)(b0 >> 32)) | (spread32((uint32_t)(b1 >> 32)) << 1);
+  } else {
+    w0 = b0;
+    w1 = b1;
+  }
+}
+
+// One wave-tile = 128 consecutive points = bitmap words w, w+1 (one 16-B store by lane 0).
 template <int TABLE, int POLY, int DEFER, bool FULL>
 __device__ __forceinline__ void range_tile(const RangeArgs& a, int64_t t, double x0, double y0, double x1, double y1,
                                            int c0, int c1, uint64_t& hits, uint64_t& mult, uint32_t* lcount,
                                            WaveQ& wq, const RangeLds& L) {
   const int lane = threadIdx.x & 63;
-  const int64_t i0 = t + lane, i1 = t + 64 + lane;
+  const int64_t i0 = kRangeVec ? t + 2 * lane : t + lane, i1 = kRangeVec ? i0 + 1 : t + 64 + lane;
   const bool v0 = FULL || i0 < a.n, v1 = FULL || i1 < a.n;
   bool h0, h1, m0, m1, d0, d1;
   eval_point<TABLE, POLY, DEFER>(a, x0, y0, c0, v0, h0, m0, d0);
   eval_point<TABLE, POLY, DEFER>(a, x1, y1, c1, v1, h1, m1, d1);
-  const uint64_t b0 = __ballot(h0), b1 = __ballot(h1);
+  uint64_t b0, b1;
+  tile_words(__ballot(h0), __ballot(h1), b0, b1);
   const int64_t w = t >> 6;
   if (DEFER == 3) {  // into the ring (the tile that leaves it goes to global memory)
     const uint32_t k = wq.ntile++;
@@ -335,7 +364,8 @@ __device__ __forceinline__ void range_tile(const RangeArgs& a, int64_t t, double
     if (FULL || t + 64 < a.n) a.bitmap[w + 1] = b1;
   }
   if (a.multi) {
-    const uint64_t e0 = __ballot(m0), e1 = __ballot(m1);
+    uint64_t e0, e1;
+    tile_words(__ballot(m0), __ballot(m1), e0, e1);
     if (lane == 0) {
       a.multi[w] = e0;
       if (FULL || t + 64 < a.n) a.multi[w + 1] = e1;
@@ -369,22 +399,38 @@ __device__ __forceinline__ void range_tile(const RangeArgs& a, int64_t t, double
 // nontemporal 16-B loads (x, y are read once); the remainder goes through the checked tail.
 // All U tiles are classified (the table-mode cell-class gathers are independent loads that
 // overlap) before any tile stores, so U tiles' latencies overlap instead of adding up.
-// U tiles of one wave: coordinates of points t_u + lane and t_u + 64 + lane.  Loads clamp
-// the index to n - 1, so tiles past the end (the pipeline's last prefetch, a partial last
-// tile) read valid memory and are masked afterwards.
+// U tiles of one wave: coordinates of the lane's two points (kRangeVec: t_u + 2 lane and the
+// next, one 16-B load per coordinate for a whole tile).  A partial or past-the-end tile (the
+// pipeline's last prefetch, the last tile) loads per point with the index clamped to n - 1, so
+// it reads valid memory and is masked afterwards.
 template <int U>
 struct RangeBuf {
   double xa[U], ya[U], xb[U], yb[U];
 };
-template <int U>
+template <int U, bool VEC>
 __device__ __forceinline__ void range_load(RangeBuf<U>& b, const RangeArgs& a, int64_t t, int64_t tstride) {
   const int lane = threadIdx.x & 63;
+  if (VEC) {  // whole tiles only: the tile start is clamped to the last whole tile (a prefetch past
+              // the wave's last tile reads valid memory; those tiles are never evaluated)
+    typedef double v2d __attribute__((ext_vector_type(2)));
+    const int64_t tmax = (a.n & ~(int64_t)127) - 128;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t tu = t + u * tstride < tmax ? t + u * tstride : tmax;
+      const v2d xv = __builtin_nontemporal_load(reinterpret_cast<const v2d*>(a.x + tu) + lane);
+      const v2d yv = __builtin_nontemporal_load(reinterpret_cast<const v2d*>(a.y + tu) + lane);
+      b.xa[u] = xv.x; b.xb[u] = xv.y;
+      b.ya[u] = yv.x; b.yb[u] = yv.y;
+    }
+    return;
+  }
   const uint32_t last = (uint32_t)(a.n - 1);
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     const int64_t tu = t + u * tstride;
-    const uint32_t i0 = tu + lane < a.n ? (uint32_t)(tu + lane) : last;
-    const uint32_t i1 = tu + 64 + lane < a.n ? (uint32_t)(tu + 64 + lane) : last;
+    const int64_t p0 = kRangeVec ? tu + 2 * lane : tu + lane, p1 = kRangeVec ? p0 + 1 : tu + 64 + lane;
+    const uint32_t i0 = p0 < a.n ? (uint32_t)p0 : last;
+    const uint32_t i1 = p1 < a.n ? (uint32_t)p1 : last;
     b.xa[u] = __builtin_nontemporal_load(a.x + i0);
     b.xb[u] = __builtin_nontemporal_load(a.x + i1);
     b.ya[u] = __builtin_nontemporal_load(a.y + i0);
@@ -395,14 +441,14 @@ __device__ __forceinline__ void range_load(RangeBuf<U>& b, const RangeArgs& a, i
 // One pipeline stage: classify the U tiles of `cur` (issuing the class-table gathers first),
 // then issue the loads of `nxt`, then finish -- so the gathers are waited on (vmcnt is in
 // order) while the next stage's tiles stay in flight.
-template <int TABLE, int POLY, int DEFER, int U>
+template <int TABLE, int POLY, int DEFER, int U, bool VEC>
 __device__ __forceinline__ void range_stage(const RangeArgs& a, const RangeLds& L, const RangeBuf<U>& cur, int64_t t, RangeBuf<U>& nxt,
                                             int64_t tn, int64_t tstride, uint64_t& hits, uint64_t& mult,
                                             uint32_t* lcount, WaveQ& wq) {
   int32_t s0[U], s1[U];
   int c0[U], c1[U];
   if constexpr (DEFER == 3) {  // span prefilter: no table gathers in the stream (WaveQ)
-    range_load<U>(nxt, a, tn, tstride);
+    range_load<U, VEC>(nxt, a, tn, tstride);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       c0[u] = span_maybe(a, cur.xa[u], cur.ya[u]) ? kTest : kNone;
@@ -414,7 +460,7 @@ __device__ __forceinline__ void range_stage(const RangeArgs& a, const RangeLds& 
       if (tu + 128 <= a.n)
         range_tile<TABLE, POLY, DEFER, true>(a, tu, cur.xa[u], cur.ya[u], cur.xb[u], cur.yb[u], c0[u], c1[u], hits,
                                              mult, lcount, wq, L);
-      else if (tu < a.n)
+      else if (!VEC && tu < a.n)
         range_tile<TABLE, POLY, DEFER, false>(a, tu, cur.xa[u], cur.ya[u], cur.xb[u], cur.yb[u], c0[u], c1[u], hits,
                                               mult, lcount, wq, L);
     }
@@ -430,7 +476,7 @@ __device__ __forceinline__ void range_stage(const RangeArgs& a, const RangeLds& 
     c0[u] = TABLE ? table_load(a, L, s0[u]) : 0;
     c1[u] = TABLE ? table_load(a, L, s1[u]) : 0;
   }
-  range_load<U>(nxt, a, tn, tstride);
+  range_load<U, VEC>(nxt, a, tn, tstride);
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     c0[u] = classify_finish<TABLE>(a, cur.xa[u], cur.ya[u], s0[u], c0[u]);
@@ -442,7 +488,7 @@ __device__ __forceinline__ void range_stage(const RangeArgs& a, const RangeLds& 
     if (tu + 128 <= a.n)
       range_tile<TABLE, POLY, DEFER, true>(a, tu, cur.xa[u], cur.ya[u], cur.xb[u], cur.yb[u], c0[u], c1[u], hits,
                                            mult, lcount, wq, L);
-    else if (tu < a.n)
+    else if (!VEC && tu < a.n)
       range_tile<TABLE, POLY, DEFER, false>(a, tu, cur.xa[u], cur.ya[u], cur.xb[u], cur.yb[u], c0[u], c1[u], hits,
                                             mult, lcount, wq, L);
   }
@@ -627,15 +673,25 @@ __device__ __forceinline__ void range_body(const RangeArgs& a) {
   }
   // this wave's tiles t0 + k * tstride, k < K; stages of U tiles, run in pairs (buffers A, B
   // alternate, so no register copies -- and no wait -- sit on the loop's back edge)
-  const int64_t K = t0 < a.n ? (a.n - t0 + tstride - 1) / tstride : 0;
+  // kRangeVec: the stages run over the wave's WHOLE tiles with 16-B loads and no load branch
+  // (a branch between the loads made the waitcnt pass drain them: the prefetch was lost); the
+  // window's one partial tile, if this wave owns it, follows with checked 8-B loads
+  const int64_t nfull = kRangeVec ? (a.n & ~(int64_t)127) : a.n;
+  const int64_t K = t0 < nfull ? (nfull - t0 + tstride - 1) / tstride : 0;
   const int64_t pairs = (K + 2 * U - 1) / (2 * U);
   const int64_t sstride = U * tstride;
   RangeBuf<U> A, B;
-  if (pairs > 0) range_load<U>(A, a, t0, tstride);
+  if (pairs > 0) range_load<U, kRangeVec>(A, a, t0, tstride);
   for (int64_t p = 0; p < pairs; ++p) {
     const int64_t ta = t0 + 2 * p * sstride;
-    range_stage<TABLE, POLY, DEFER, U>(a, L, A, ta, B, ta + sstride, tstride, hits, mult, &lcount, wq);
-    range_stage<TABLE, POLY, DEFER, U>(a, L, B, ta + sstride, A, ta + 2 * sstride, tstride, hits, mult, &lcount, wq);
+    range_stage<TABLE, POLY, DEFER, U, kRangeVec>(a, L, A, ta, B, ta + sstride, tstride, hits, mult, &lcount, wq);
+    range_stage<TABLE, POLY, DEFER, U, kRangeVec>(a, L, B, ta + sstride, A, ta + 2 * sstride, tstride, hits, mult,
+                                                  &lcount, wq);
+  }
+  if (kRangeVec && nfull < a.n && t0 <= nfull && (nfull - t0) % tstride == 0) {  // this wave's partial tile
+    RangeBuf<1> T, Tn;
+    range_load<1, false>(T, a, nfull, tstride);
+    range_stage<TABLE, POLY, DEFER, 1, false>(a, L, T, nfull, Tn, nfull, tstride, hits, mult, &lcount, wq);
   }
   if (DEFER == 1) hits += drain_own_queue<POLY>(a, lcount);
   if (DEFER == 3) {

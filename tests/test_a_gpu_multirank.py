@@ -64,7 +64,7 @@ def test_knn_two_ranks_string_objids_verified():
     line = _run_two_ranks(["--points", "400000", "--steps", "9", "--warmup", "3", "--windows", "4",
                            "--exchange-batch", "2", "--pipeline", "3", "--string-objids"])
     assert line["n_gpus"] == 2 and line["verified_vs_oracle"] is True
-    assert line["config"]["objid"] == "dictionary Strings"
+    assert line["config"]["objid"].startswith("dictionary Strings")
 
 
 @pytest.mark.timeout(900)

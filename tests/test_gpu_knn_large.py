@@ -81,7 +81,7 @@ def test_polygon_knn_large_k(sf, oracle_mod):
     check(res, eo, ed, ei)
 
 
-@pytest.mark.parametrize("k,depth", [(700, 1), (700, 2), (700, 3), (300, 2), (300, 3), (512, 3)])
+@pytest.mark.parametrize("k,depth", [(700, 1), (700, 2), (700, 3), (700, 4), (300, 2), (300, 3), (512, 3), (400, 4)])
 def test_knn_large_k_queued_windows(sf, oracle_mod, k, depth):
     """Several windows enqueued back to back with no host read in between (records written by the
     kernels straight into pinned host memory), then one flush: each record == the oracle's.

@@ -726,7 +726,7 @@ def test_knn_pinned_records_async(sf, oracle_mod):
         check_knn(res, oo, od, oi)
 
 
-@pytest.mark.parametrize("k,depth", [(50, 2), (120, 2), (50, 3), (120, 3)])
+@pytest.mark.parametrize("k,depth", [(50, 2), (120, 2), (50, 3), (120, 3), (50, 4), (120, 4), (300, 4)])
 def test_knn_pipelined(sf, oracle_mod, k, depth):
     """Depth-2 pipeline: window i's select runs inside window i+1's fused scan kernel (depth 3:
     inside window i+2's, odd windows on a second stream); cold

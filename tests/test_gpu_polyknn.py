@@ -88,7 +88,8 @@ def test_polyknn_continuous_and_fallback(sf, oracle_mod):
 @pytest.mark.parametrize("name,approx,k,depth", [("holed", False, 60, 2), ("square", True, 20, 2),
                                                 ("generated", False, 128, 2), ("holed", False, 60, 3),
                                                 ("square", True, 20, 3), ("generated", False, 128, 3),
-                                                ("square", False, 300, 3)])
+                                                ("square", False, 300, 3), ("holed", False, 60, 4),
+                                                ("square", False, 300, 4)])
 def test_polyknn_pipeline_depth_2(sf, oracle_mod, name, approx, k, depth):
     """Depths 2 / 3 (PointPolygonKNNQuery.java:245-317 per window): one prefilter launch per window
     carries the select of the window before (depth 2) or of the window two back, the windows

@@ -1281,17 +1281,19 @@ def bench_polyknn(args):
     avg = sms / 1000.0 / max(scnt, 1)
     # windows in flight: a launch's own duration counts shared time several times, so the rate
     # is bytes per window over the window interval (as the range lines)
-    interval = nst > 1 or depth == 3
+    interval = nst > 1 or depth >= 3
     basis = (f"bytes per window / window interval ({nst} plan(s), depth {depth}: launches of consecutive windows "
              "overlap; includes host work)" if interval else "bytes per window / average prefilter-scan launch")
     kern = {1: "knn_poly_scan", 2: "knn_poly_fused (prefilter scan + the previous window's select in block 0)",
             3: "knn_poly_fused (prefilter scan + the select of the window two back in block 0; consecutive "
-               "windows on the plan's two streams)"}[depth]
+               "windows on the plan's two streams)",
+            4: "knn_poly_fused (prefilter scan + the select of the window three back in block 0; consecutive "
+               "windows on the plan's three streams)"}[depth]
     _line("polygon-query kNN k=%d" % args.k, n * args.steps / elapsed, "points/s", args.steps, args.warmup, elapsed,
           kern, 16.0 * n, elapsed / args.steps if interval else avg,
           {"config": {"workload": f"knn_ppoly_k{args.k}_r{args.radius}_{n // 1_000_000}Mpts_grid500_square0.02",
                       "points_per_window": n, "k": args.k, "radius": args.radius, "pipeline_depth": depth,
-                      "plans": nst, "windows_in_flight": nst * (2 if depth == 3 else 1)},
+                      "plans": nst, "windows_in_flight": nst * (depth - 1 if depth >= 3 else 1)},
            "breakdown": {"scan_us": round(avg * 1e6, 2), "sample_us": round(1000 * pms / max(pcnt, 1), 2),
                          "select_us": round(1000 * lms / max(lcnt, 1), 2), "achieved_basis": basis},
            "fallback_windows": fallbacks, "verified_vs_oracle": verified,
