@@ -171,6 +171,20 @@ int gf_assign_cells(gf_ctx* ctx, const gf_grid* g, const gf_points* pts, int32_t
 int gf_bucket_by_cell(gf_ctx* ctx, const gf_grid* g, const gf_points* pts, uint32_t* perm,
                       uint32_t* cell_start);
 
+/* ---- multi-GPU routing of an arriving window (async) ---------------------------------
+ * The window's points partitioned by owning GPU: band b owns cell columns [band_lo[b],
+ * band_lo[b+1]) (columns left of band_lo[1] -- out-of-grid ones too -- belong to band 0, those
+ * right of the last start to the last band; NaN x counts as column 0).  perm: device
+ * uint32[n], every band's points in arrival order; offsets: device uint32[nbands + 1], band b =
+ * perm[offsets[b] .. offsets[b+1]).  One stable radix pass over the band keys (K1 + K2), the
+ * keyBy(gridID) shuffle across ranks (PointPointRangeQuery.java:144-148).  nbands <= 64. */
+int gf_shard_by_columns(gf_ctx* ctx, const gf_grid* g, const gf_points* pts, int32_t nbands, const int32_t* band_lo,
+                        uint32_t* perm, uint32_t* offsets);
+/* A band's SoA slice: out[i] = in[perm[begin + i]], i < end - begin, for the columns given
+ * (device buffers; x, y, objID, ts may each be null). */
+int gf_gather_points(gf_ctx* ctx, const gf_points* pts, const uint32_t* perm, int64_t begin, int64_t end, double* x,
+                     double* y, int64_t* objID, int64_t* ts);
+
 /* ---- range queries ----------------------------------------------------------------- */
 typedef struct gf_range_plan gf_range_plan;
 /* PointPointRangeQuery.run(stream, Set<Point> queryPoints, r) -- guaranteed / candidate cell

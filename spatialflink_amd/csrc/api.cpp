@@ -491,6 +491,65 @@ extern "C" int gf_bucket_by_cell(gf_ctx* ctx, const gf_grid* g, const gf_points*
   return GF_OK;
 }
 
+// A window's points partitioned by owning GPU (multi-GPU sharding by cell-column bands, the
+// keyBy(gridID) shuffle of PointPointRangeQuery.java:144-148 across ranks): one stable radix pass
+// over the band keys (K1's column + the band search, fused into the histogram), so every shard
+// lists its points in arrival order -- identical to sharding.shard_order.
+extern "C" int gf_shard_by_columns(gf_ctx* ctx, const gf_grid* g, const gf_points* pts, int32_t nbands,
+                                   const int32_t* band_lo, uint32_t* perm, uint32_t* offsets) {
+  if (!ctx || !grid_ok(g) || !perm || !offsets || !band_lo || nbands < 1 || nbands > kMaxShardBands)
+    return set_err(ctx, GF_ERR_ARG, "gf_shard_by_columns: bad argument");
+  for (int j = 1; j < nbands; ++j)
+    if (band_lo[j] < band_lo[j - 1]) return set_err(ctx, GF_ERR_ARG, "gf_shard_by_columns: band starts must ascend");
+  int st = bind(ctx);
+  if (st) return st;
+  if ((st = check_points(ctx, pts))) return st;
+  const int64_t n = pts->n;
+  if (n == 0) {
+    GF_HIP_CHECK(ctx, hipMemsetAsync(offsets, 0, sizeof(uint32_t) * (size_t)(nbands + 1), ctx->stream));
+    return GF_OK;
+  }
+  if (n > (int64_t)UINT32_MAX) return set_err(ctx, GF_ERR_ARG, "gf_shard_by_columns: window too large");
+  int bits = 1;
+  while ((1 << bits) < nbands) ++bits;
+  const int64_t tiles = (n + kRadixTile - 1) / kRadixTile;
+  const int blocks = (int)std::min<int64_t>(std::max<int64_t>(tiles / 4, 1), (int64_t)ctx->num_cus);
+  const int64_t mat = ((int64_t)1 << bits) * blocks;
+  Arena ar;
+  size_t o_k0 = ar.take<uint32_t>(n), o_k = ar.take<uint32_t>(n);
+  size_t o_m = ar.take<uint32_t>(mat), o_ms = ar.take<uint32_t>(mat + 1);
+  char* base = (char*)ctx_scratch(ctx, ar.off, &st);
+  if (st) return st;
+  auto U32 = [&](size_t o) { return (uint32_t*)(base + o); };
+  RadixArgs a{};
+  a.x = pts->x; a.y = pts->y; a.n = n;
+  a.minX = g->minX; a.minY = g->minY; a.cl = g->cellLength; a.gn = g->n;
+  a.bits = bits; a.nblk = blocks; a.shift = 0;
+  a.nbands = nbands;
+  for (int j = 0; j < nbands; ++j) a.band_lo[j] = band_lo[j];
+  a.kin = nullptr; a.vin = nullptr; a.kout = U32(o_k0); a.M = U32(o_m); a.Ms = U32(o_ms);
+  GF_HIP_CHECK(ctx, launch_radix(ctx, 0, a, blocks));  // band keys -> k0, histograms
+  ExpandState es;
+  if ((st = lookback_state(ctx, scan1_blocks(mat), &es))) return st;
+  GF_HIP_CHECK(ctx, launch_scan1(ctx->stream, U32(o_m), mat, U32(o_ms), nullptr, 0, 0, es));
+  ctx->expand_base += (unsigned long long)scan1_blocks(mat);
+  a.kin = U32(o_k0); a.kout = U32(o_k); a.vout = perm;
+  GF_HIP_CHECK(ctx, launch_radix(ctx, 1, a, blocks));  // stable scatter: perm
+  a.M = offsets; a.bins = (uint32_t)nbands;
+  GF_HIP_CHECK(ctx, launch_radix(ctx, 2, a, blocks));  // offsets[0 .. nbands]
+  return GF_OK;
+}
+
+extern "C" int gf_gather_points(gf_ctx* ctx, const gf_points* pts, const uint32_t* perm, int64_t begin, int64_t end,
+                                double* x, double* y, int64_t* objID, int64_t* ts) {
+  if (!ctx || !pts || !perm || begin < 0 || end < begin || (objID && !pts->objID) || (ts && !pts->ts))
+    return set_err(ctx, GF_ERR_ARG, "gf_gather_points: bad argument");
+  int st = bind(ctx);
+  if (st) return st;
+  GF_HIP_CHECK(ctx, launch_gather_points(ctx->stream, *pts, perm, begin, end - begin, x, y, objID, ts));
+  return GF_OK;
+}
+
 // ---------------------------------------------------------------------------------------
 // range plans
 // ---------------------------------------------------------------------------------------

@@ -319,8 +319,14 @@ struct RadixArgs {
   uint32_t* M;              // stage 0: [digits][blocks]; stage 2: cell_start[0 .. gn*gn + 1] (output)
   const uint32_t* Ms;       // stage 1: the exclusive scan of M
   const uint32_t* n_dev;    // non-null: the item count is min(n, *n_dev), read on the device
+  int32_t nbands;           // > 0: pass 0's key is the point's column band (gf_shard_by_columns), not its cell
+  int32_t band_lo[64];      // the bands' first columns, ascending (band_lo[0] is taken as -inf)
+  uint32_t bins;            // stage 2: cell_start entries - 1 (0: gn * gn + 1)
 };
+constexpr int kMaxShardBands = 64;
 size_t radix_scatter_lds_bytes();
+hipError_t launch_gather_points(hipStream_t s, const gf_points& in, const uint32_t* perm, int64_t begin, int64_t m,
+                                double* ox, double* oy, int64_t* oo, int64_t* ot);
 // stage 0 histogram, 1 scatter, 2 cell_start from the sorted kout (every bucket's first position)
 hipError_t launch_radix(gf_ctx* ctx, int stage, const RadixArgs& a, int blocks);
 // exclusive scan: out[0..L] (out[L] = total); tmp >= scan_tmp_elems(L) uint32

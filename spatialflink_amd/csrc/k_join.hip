@@ -1374,7 +1374,10 @@ __device__ __forceinline__ void band_emit(const JoinOut& o, BandHdr& hd, uint32_
 // (GF_ERR_CAPACITY; the caller's retry gets regions sized from this call's exact counts).
 // O, R: region t of thread t (every block derived all of them, band_regions), E their end.  The
 // other blocks' counts were stored write-through and drained before their tickets, so they are
-// read with agent-scope loads -- no __threadfence (an L2 write-back per block).
+// read with agent-scope loads -- no __threadfence (an L2 write-back per block).  This is the
+// write-through hand-off of cdna_hip_programming.md Guideline 16 (R1): sc1 stores of the payload,
+// s_waitcnt vmcnt(0) by the storing lane, an atomic counter, sc1 loads in the last arriver (which
+// bypass its CU's L1, so no acquire is needed); tests/test_isa_handoff.py checks it in the ISA.
 __device__ __forceinline__ void join_region_prep(const JoinFixup& f, uint64_t* ws, uint64_t O, uint64_t R, uint64_t E) {
   const JoinOut& o = f.o;
   const uint32_t G = o.nwaves, t = threadIdx.x;

@@ -154,6 +154,19 @@ __device__ __forceinline__ uint32_t bucket_key(double x, double y, const RadixAr
   return valid ? (uint32_t)cy * (uint32_t)a.gn + (uint32_t)cx : (uint32_t)a.gn * (uint32_t)a.gn;
 }
 
+// gf_shard_by_columns: the band of a point's cell column (Java (int) of the floored x, NaN -> 0);
+// columns left of band 1 -- out-of-grid ones included -- belong to band 0, right of the last
+// band's start to the last band (sharding.shard_of_columns)
+__device__ __forceinline__ uint32_t band_key(double x, const RadixArgs& a) {
+  const int32_t cx = cell_index(x, a.minX, a.cl);
+  uint32_t b = 0;
+  for (int j = 1; j < a.nbands; ++j) b += cx >= a.band_lo[j] ? 1u : 0u;
+  return b;
+}
+__device__ __forceinline__ uint32_t pass0_key(double x, double y, const RadixArgs& a) {
+  return a.nbands > 0 ? band_key(x, a) : bucket_key(x, y, a);
+}
+
 // block b's chunk [beg, end) of the a.nblk chunks (whole tiles except the last)
 __device__ __forceinline__ void radix_chunk(const RadixArgs& a, int64_t& beg, int64_t& end) {
   int64_t n = a.n;
@@ -186,10 +199,10 @@ __global__ __launch_bounds__(kRadixThreads) void radix_hist_kernel(RadixArgs a) 
           typedef double v2d __attribute__((ext_vector_type(2)));
           const v2d xv = __builtin_nontemporal_load(reinterpret_cast<const v2d*>(a.x + i));
           const v2d yv = __builtin_nontemporal_load(reinterpret_cast<const v2d*>(a.y + i));
-          k0[u] = bucket_key(xv.x, yv.x, a);
-          k1[u] = bucket_key(xv.y, yv.y, a);
+          k0[u] = pass0_key(xv.x, yv.x, a);
+          k1[u] = pass0_key(xv.y, yv.y, a);
         } else {
-          k0[u] = i < end ? bucket_key(a.x[i], a.y[i], a) : 0u;
+          k0[u] = i < end ? pass0_key(a.x[i], a.y[i], a) : 0u;
           k1[u] = 0u;
         }
       }
@@ -389,10 +402,30 @@ hipError_t launch_radix(gf_ctx* ctx, int stage, const RadixArgs& a, int blocks) 
       const int64_t waves = (a.n + 1 + 64 * kBoundsPer - 1) / (64 * kBoundsPer);
       const int64_t nb = (waves + kBlock / 64 - 1) / (kBlock / 64);
       hipLaunchKernelGGL(radix_bounds_kernel, dim3((unsigned)nb), dim3(kBlock), 0, s, a.kout, a.n,
-                         (uint32_t)a.gn * (uint32_t)a.gn + 1u, a.M);
+                         a.bins ? a.bins : (uint32_t)a.gn * (uint32_t)a.gn + 1u, a.M);
       break;
     }
   }
+  return hipGetLastError();
+}
+
+// gf_gather_points: out[i] = in[perm[begin + i]] for the columns given (a shard's SoA slice)
+__global__ __launch_bounds__(kBlock) void gather_points_kernel(gf_points in, const uint32_t* __restrict__ perm,
+                                                               int64_t begin, int64_t m, double* ox, double* oy,
+                                                               int64_t* oo, int64_t* ot) {
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < m; i += (int64_t)gridDim.x * kBlock) {
+    const uint32_t p = perm[begin + i];
+    if (ox) ox[i] = in.x[p];
+    if (oy) oy[i] = in.y[p];
+    if (oo) oo[i] = in.objID[p];
+    if (ot) ot[i] = in.ts[p];
+  }
+}
+hipError_t launch_gather_points(hipStream_t s, const gf_points& in, const uint32_t* perm, int64_t begin, int64_t m,
+                                double* ox, double* oy, int64_t* oo, int64_t* ot) {
+  if (m <= 0) return hipSuccess;
+  hipLaunchKernelGGL(gather_points_kernel, dim3(stream_blocks(m, kBlock)), dim3(kBlock), 0, s, in, perm, begin, m, ox,
+                     oy, oo, ot);
   return hipGetLastError();
 }
 

@@ -9,6 +9,8 @@ records followed by the same deterministic top-k-distinct merge on every rank.
 """
 from __future__ import annotations
 
+import ctypes as C
+
 import numpy as np
 
 from . import _lib
@@ -85,6 +87,42 @@ def shard_order(cx, bands):
     perm = np.argsort(owner, kind="stable")
     offsets = np.searchsorted(owner[perm], np.arange(len(bands) + 1), side="left")
     return perm, offsets
+
+
+def shard_window(window, grid, bands):
+    """The device form of shard_order for an arriving window (gf_shard_by_columns): the window's
+    points grouped by owning band, arrival order kept inside a band -> (perm: torch uint32 as
+    int32 [n], offsets: numpy int64 [len(bands) + 1]); band s = perm[offsets[s]:offsets[s+1]]."""
+    import torch
+
+    ctx = _lib.context(window.x.device.index)
+    n = window.n
+    lo = np.ascontiguousarray([b[0] for b in bands], np.int32)
+    perm = torch.empty(max(n, 1), dtype=torch.int32, device=window.x.device)
+    off = torch.empty(len(bands) + 1, dtype=torch.int32, device=window.x.device)
+    pts = window.c_struct()
+    _lib.check(_lib.lib().gf_shard_by_columns(ctx.handle, C.byref(grid.c_grid), C.byref(pts), len(bands),
+                                              lo.ctypes.data, perm.data_ptr(), off.data_ptr()),
+               ctx.handle, "gf_shard_by_columns")
+    return perm[:n], off.cpu().numpy().view(np.uint32).astype(np.int64)
+
+
+def gather_shard(window, perm, offsets, s):
+    """Band s of a window routed by shard_window as its own PointWindow (gf_gather_points): the
+    SoA slice a rank receives."""
+    import torch
+
+    from .spatialObjects import PointWindow
+
+    ctx = _lib.context(window.x.device.index)
+    b, e = int(offsets[s]), int(offsets[s + 1])
+    dev = window.x.device
+    out = [torch.empty(max(e - b, 1), dtype=dt, device=dev) for dt in (torch.float64, torch.float64, torch.int64,
+                                                                        torch.int64)]
+    pts = window.c_struct()
+    _lib.check(_lib.lib().gf_gather_points(ctx.handle, C.byref(pts), perm.data_ptr(), b, e, *(t.data_ptr() for t in out)),
+               ctx.handle, "gf_gather_points")
+    return PointWindow(*(t[: e - b] for t in out))
 
 
 def band_x_range(grid, lo: int, hi: int):

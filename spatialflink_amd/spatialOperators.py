@@ -359,6 +359,14 @@ class PointPointKNNQuery(SpatialOperator):
 
     _destroy_name = "gf_knn_plan_destroy"
 
+    def __init__(self, conf: QueryConfiguration, index: UniformGrid):
+        super().__init__(conf, index)
+        self._depth = {}  # plan handle -> pipeline depth (set_pipeline)
+
+    @staticmethod
+    def _pv(plan):
+        return plan.value if hasattr(plan, "value") else plan
+
     def plan(self, window_device: int, queryPoint: Point, queryRadius: float, k: int):
         ctx = _lib.context(window_device)
         key = (ctx.device, queryPoint.x, queryPoint.y, float(queryRadius), int(k), int(self.conf.distanceMetric))
@@ -390,10 +398,19 @@ class PointPointKNNQuery(SpatialOperator):
     def enqueue(self, window: PointWindow, queryPoint: Point, queryRadius: float, k: int, record):
         """Async: evaluate the window into a record -- a torch uint8 device tensor of
         knn_record_bytes(k), or an int address from PinnedRecords.ptr() (kernel writes the
-        host record directly); pair with finish() once the record is on the host."""
+        host record directly); pair with finish() once the record is on the host.  The window's
+        tensors must stay alive until the record is complete (at depth >= 3 kernels on the plan's
+        other streams read them, which torch's caching allocator does not track)."""
         ctx, plan = self.plan(window.x.device.index, queryPoint, queryRadius, k)
         pts = window.c_struct()
         addr = record if isinstance(record, int) else record.data_ptr()
+        # depth >= 3 launches windows on the plan's other streams, which do not wait for the
+        # context stream (torch's current stream, where this window's tensors were produced):
+        # the first enqueue of a window orders those streams after it (gf_ctx_fork); a window
+        # seen before is complete (later enqueues of it pay nothing)
+        if self._depth.get(self._pv(plan), 1) >= 3 and not window.extra.get("gf_fenced"):
+            _lib.check(_lib.lib().gf_ctx_fork(ctx.handle), ctx.handle, "gf_ctx_fork")
+            window.extra["gf_fenced"] = True
         _lib.check(_lib.lib().gf_knn_enqueue(plan, C.byref(pts), C.c_void_p(addr)), ctx.handle, "gf_knn_enqueue")
 
     def finish(self, window: PointWindow, queryPoint: Point, queryRadius: float, k: int, raw: bytes) -> KNNResult:
@@ -415,6 +432,7 @@ class PointPointKNNQuery(SpatialOperator):
         ctx, plan = self.plan(window_device, queryPoint, queryRadius, k)
         _lib.check(_lib.lib().gf_knn_plan_set_pipeline(plan, int(depth)), ctx.handle, "set_pipeline")
         self._plans.pin(plan)  # its depth and pending records must survive the LRU
+        self._depth[self._pv(plan)] = int(depth)
 
     def flush(self, window_device, queryPoint, queryRadius, k):
         ctx, plan = self.plan(window_device, queryPoint, queryRadius, k)

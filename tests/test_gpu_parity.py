@@ -1143,3 +1143,47 @@ def test_range_run_batch(sf, oracle_mod, kind):
                 np.testing.assert_array_equal(got, exp)
     finally:
         L.gf_range_plan_destroy(h)
+
+
+@pytest.mark.parametrize("depth", [3, 4])
+def test_knn_enqueue_fresh_torch_windows(sf, oracle_mod, depth):
+    """Windows produced by torch on the context stream right before an ASYNC depth >= 3 enqueue
+    (windows launch on the plan's other streams, which do not wait for the context
+    stream): PointPointKNNQuery.enqueue orders them after the window's first use, so every
+    record == the oracle's."""
+    import torch
+
+    g = sf.UniformGrid(500, *BEIJING)
+    og = oracle_mod.grid(500, *BEIJING)
+    q = sf.Point("q", *QPOINT, 0, g)
+    op = sf.PointPointKNNQuery(conf(sf), g)
+    k, N = 50, 1_100_000
+    base = []
+    for seed in (61, 62, 63):
+        x, y = oracle_mod.java_random_points(seed, N, *BEIJING)
+        base.append((x, y, np.arange(N, dtype=np.int64) + seed * 10_000_000))
+    dev = [sf.PointWindow.from_numpy(*b) for b in base]
+    op.set_pipeline(0, q, 0.5, k, depth)
+    order = [(0, 1), (1, 2), (2, 0), (0, 2), (1, 0), (2, 1)]
+    rec = sf.PinnedRecords(len(order), k)
+    expect = []
+    keep = []  # a window's memory must stay valid until its record is complete (the C ABI's rule)
+    for i, (a, b) in enumerate(order):
+        # a fresh window: torch kernels on the current stream write it just before the enqueue
+        w = sf.PointWindow(torch.cat([dev[a].x, dev[b].x]) * 1.0, torch.cat([dev[a].y, dev[b].y]) * 1.0,
+                           torch.cat([dev[a].objID, dev[b].objID]), torch.cat([dev[a].timeStampMillisec,
+                                                                                dev[b].timeStampMillisec]))
+        op.enqueue(w, q, 0.5, k, rec.ptr(i))
+        expect.append(oracle_mod.knn(og, np.concatenate([base[a][0], base[b][0]]), np.concatenate([base[a][1], base[b][1]]),
+                                     np.concatenate([base[a][2], base[b][2]]), QPOINT[0], QPOINT[1], 0.5, k))
+        keep.append(w)
+    op.flush(0, q, 0.5, k)
+    torch.cuda.synchronize()
+    for i in range(len(order)):
+        st, o, d, ix = rec.decode(i)
+        est, eo, ed, ei = expect[i]
+        assert st == 0
+        np.testing.assert_array_equal(o, eo)
+        np.testing.assert_array_equal(d, ed)
+        np.testing.assert_array_equal(ix, ei)
+    op.set_pipeline(0, q, 0.5, k, 1)

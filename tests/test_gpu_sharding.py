@@ -275,3 +275,34 @@ def test_knn_merge_strings_across_dictionaries(sf, oracle_mod, k):
                                           out2.data_ptr()), ctx.handle, "merge strings small")
     st, strs, _, _ = sharding.decode_string_record(out2[0].cpu().numpy().tobytes(), k, 8)
     assert st == _lib.KNN_STATUS_FOREIGN_KEYS and strs == []
+
+
+@pytest.mark.parametrize("nb", [1, 3, 8])
+def test_shard_window_device_routing(sf, oracle_mod, nb):
+    """gf_shard_by_columns (the C-ABI router of an arriving window): every point to the rank of
+    its cell-column band, arrival order kept -- == sharding.shard_order on the K1 columns -- and
+    each band's gathered SoA slice (gf_gather_points) == the numpy take; NaN x (column 0), points
+    left / right of the grid (edge bands), bands balanced by a column histogram."""
+    from spatialflink_amd import sharding
+
+    g = sf.UniformGrid(500, *BEIJING)
+    x, y = oracle_mod.java_random_points(123, 700_001, 115.3, 117.9, 39.5, 41.2)
+    x[:50] = np.nan
+    x[50:60] = 200.0
+    x[60:70] = -200.0
+    obj = np.arange(len(x), dtype=np.int64) * 7
+    ts = np.arange(len(x), dtype=np.int64) + 5
+    w = sf.PointWindow.from_numpy(x, y, obj, ts)
+    cx = sf.assign_cells(w, g)[0].cpu().numpy()
+    bands = sharding.column_bands(500, nb, np.bincount(np.clip(cx, 0, 499), minlength=500))
+    perm, off = sharding.shard_window(w, g, bands)
+    eperm, eoff = sharding.shard_order(cx, bands)
+    np.testing.assert_array_equal(off, eoff)
+    np.testing.assert_array_equal(perm.cpu().numpy().view(np.uint32).astype(np.int64), eperm)
+    for s in range(nb):
+        part = sharding.gather_shard(w, perm, off, s)
+        ix = eperm[eoff[s]:eoff[s + 1]]
+        np.testing.assert_array_equal(part.x.cpu().numpy(), x[ix])
+        np.testing.assert_array_equal(part.y.cpu().numpy(), y[ix])
+        np.testing.assert_array_equal(part.objID.cpu().numpy(), obj[ix])
+        np.testing.assert_array_equal(part.timeStampMillisec.cpu().numpy(), ts[ix])

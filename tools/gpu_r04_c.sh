@@ -2,7 +2,7 @@
 # r04: range scan whole-tile 16-B loads, K2 bounds, join scatter LDS barriers, depth 4; tests + lines
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-tools/gpu_step.sh t_c1 800 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_parity.py tests/test_gpu_host_windows.py tests/test_gpu_polyknn.py tests/test_gpu_callers.py tests/test_gpu_clustered.py tests/test_gpu_join_density.py tests/test_gpu_knn_large.py || exit 1
+tools/gpu_step.sh t_c1 800 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_parity.py tests/test_gpu_host_windows.py tests/test_gpu_polyknn.py tests/test_gpu_callers.py tests/test_gpu_clustered.py tests/test_gpu_join_density.py tests/test_gpu_knn_large.py tests/test_gpu_sharding.py || exit 1
 tools/gpu_step.sh b_bucket 200 python -u bench.py --workload bucket --steps 20 --warmup 3 || exit 1
 tools/gpu_step.sh p_bucket 200 rocprofv3 --kernel-trace --stats -d gpurun_out/p_bucket -o stats --output-format csv -- python -u bench.py --workload bucket --steps 5 --warmup 2 --no-cpu-baseline --no-verify || exit 1
 tools/gpu_step.sh b_range10m 300 python -u bench.py --workload range --points 10000000 --steps 40 --warmup 5 --no-cpu-baseline || exit 1
