@@ -576,6 +576,9 @@ int  gf_window_points(gf_window* w, gf_points* out);
  * (d, idx, objID) for points below the threshold; nothing else reads objID).  The column must
  * stay unchanged until the work that reads this window has completed. */
 int  gf_window_upload_mapped(gf_window* w, const double* x, const double* y, const int64_t* objID_pinned, int64_t n);
+/* *pinned = 1 when p lies in pinned host memory (gf_pinned_alloc / registered), so a shim can
+ * take gf_window_upload_mapped for an objID column it was handed. */
+int  gf_host_pinned(const void* p, int* pinned);
 
 /* ---- synthetic input (host) ----------------------------------------------------------
  * java.util.Random(seed): x = minX + nextDouble()*(maxX-minX), then y likewise, per point

@@ -82,6 +82,11 @@ public final class GeoFlinkHip {
 
   // ---- kNN ----------------------------------------------------------------------------------
   // grids as double[] {n, minX, maxX, minY, maxY} (UniformGrid(n, minX, maxX, minY, maxY))
+  // pinned host memory as a direct ByteBuffer (native order is the caller's): a kNN window's
+  // objID column placed here is read in place by the kernels (16 B per point over PCIe, not 24);
+  // free it with pinnedFree, never let the GC drop it while a window may still read it
+  public static native ByteBuffer pinnedBuffer(long bytes);
+  public static native void pinnedFree(ByteBuffer buf);
   public static native long knnPlan(long ctx, double[] grid, double qx, double qy, double r, int k);
   // polygons as CSR: ringOff[npoly+1] into vertOff, vertOff[nrings+1] into vx / vy (closed rings)
   public static native long knnPolygonPlan(long ctx, double[] grid, int[] ringOff, int[] vertOff, double[] vx,

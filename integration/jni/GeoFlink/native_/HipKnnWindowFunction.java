@@ -74,6 +74,8 @@ public class HipKnnWindowFunction
 
   @Override
   public void close() {
+    if (bo != null) GeoFlinkHip.pinnedFree(bo);
+    bo = null;
     if (plan != 0) GeoFlinkHip.knnPlanDestroy(plan);
     if (ctx != 0) GeoFlinkHip.ctxDestroy(ctx);
     plan = ctx = 0;
@@ -82,7 +84,10 @@ public class HipKnnWindowFunction
   private void grow(int n) {
     bx = ByteBuffer.allocateDirect(8 * n).order(ByteOrder.nativeOrder());
     by = ByteBuffer.allocateDirect(8 * n).order(ByteOrder.nativeOrder());
-    bo = ByteBuffer.allocateDirect(8 * n).order(ByteOrder.nativeOrder());
+    // the objID keys in pinned memory: the kernels read only the candidates' keys through the
+    // mapping, so a window crosses PCIe at 16 B per point (x, y) instead of 24
+    if (bo != null) GeoFlinkHip.pinnedFree(bo);
+    bo = GeoFlinkHip.pinnedBuffer(8L * n).order(ByteOrder.nativeOrder());
     objIDs = new String[n];
   }
 

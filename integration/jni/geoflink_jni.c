@@ -164,6 +164,22 @@ JNIEXPORT jbyteArray JNICALL Java_GeoFlink_native_1_GeoFlinkHip_objidDecode(JNIE
   return out;
 }
 
+/* ---- pinned direct buffers: a window's objID column read in place by the kernels --------- */
+JNIEXPORT jobject JNICALL Java_GeoFlink_native_1_GeoFlinkHip_pinnedBuffer(JNIEnv* env, jclass cls, jlong bytes) {
+  void* p = NULL;
+  const int st = shim_pinned_alloc(bytes, &p);
+  if (st) {
+    throw_status(env, st, NULL);
+    return NULL;
+  }
+  return (*env)->NewDirectByteBuffer(env, p, bytes);
+}
+
+JNIEXPORT void JNICALL Java_GeoFlink_native_1_GeoFlinkHip_pinnedFree(JNIEnv* env, jclass cls, jobject buf) {
+  void* p = buf ? (*env)->GetDirectBufferAddress(env, buf) : NULL;
+  if (p) shim_pinned_free(p);
+}
+
 /* ---- kNN (PointPointKNNQuery.java:132-201 + KNNQuery.java:213-272; PointPolygonKNNQuery
  * .java:245-317) ----------------------------------------------------------------------------- */
 JNIEXPORT jlong JNICALL Java_GeoFlink_native_1_GeoFlinkHip_knnPlan(JNIEnv* env, jclass cls, jlong ctx,

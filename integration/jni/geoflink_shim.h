@@ -47,6 +47,10 @@ int shim_knn_polygon_plan(shim_ctx* c, const gf_grid* g, const gf_polygons* poly
                           int approximate, shim_knn** out);
 void shim_knn_destroy(shim_knn* h);
 /* one window (host x, y, objID keys) -> *m neighbours ascending (dist, objID); idx window-local */
+/* pinned host memory for a window column the kernels read in place (objID: only the candidates'
+ * keys cross PCIe -- gf_window_upload_mapped); upload() detects it with gf_host_pinned */
+int shim_pinned_alloc(int64_t bytes, void** out);
+void shim_pinned_free(void* p);
 int shim_knn_window(shim_knn* h, const double* x, const double* y, const int64_t* objID, int64_t n, int64_t* out_objID,
                     double* out_dist, int64_t* out_idx, int32_t* m);
 

@@ -57,6 +57,7 @@ EXPORTS = [
     "gf_window_destroy", "gf_window_upload", "gf_window_points", "gf_synth_uniform", "gf_pinned_alloc",
     "gf_pinned_free", "gf_knn_string_record_bytes", "gf_knn_attach_strings", "gf_knn_merge_dev_strings",
     "gf_knn_string_record_decode", "gf_window_upload_mapped", "gf_shard_by_columns", "gf_gather_points",
+    "gf_host_pinned",
 ]
 
 
@@ -203,6 +204,7 @@ def lib():
             "gf_window_upload_mapped": ([P, P, P, P, i64], C.c_int),
             "gf_shard_by_columns": ([P, C.POINTER(GfGrid), C.POINTER(GfPoints), i32, P, P, P], C.c_int),
             "gf_gather_points": ([P, C.POINTER(GfPoints), P, i64, i64, P, P, P, P], C.c_int),
+            "gf_host_pinned": ([P, C.POINTER(C.c_int)], C.c_int),
             "gf_synth_uniform": ([i64, i64, d, d, d, d, P, P], C.c_int),
             "gf_pinned_alloc": ([sz, C.POINTER(P)], C.c_int),
             "gf_pinned_free": ([P], None),

@@ -451,9 +451,9 @@ extern "C" int gf_bucket_by_cell(gf_ctx* ctx, const gf_grid* g, const gf_points*
   int bits = 1;
   while (((int64_t)1 << bits) < bins) ++bits;
   const int passes = (bits + kBucketBits - 1) / kBucketBits, pbits = (bits + passes - 1) / passes;
-  // one block per CU (the scatter's tile buffers), >= ~4 tiles per block
-  const int64_t tiles = (n + kRadixTile - 1) / kRadixTile;
-  const int blocks = (int)std::min<int64_t>(std::max<int64_t>(tiles / 4, 1), (int64_t)ctx->num_cus);
+  // the scatter's tile buffers bound the blocks per CU (radix_threads), >= ~4 tiles per block
+  const int64_t tiles = (n + radix_tile() - 1) / radix_tile();
+  const int blocks = (int)std::min<int64_t>(std::max<int64_t>(tiles / 4, 1), (int64_t)radix_max_blocks(ctx->num_cus));
   const int64_t mat = ((int64_t)1 << pbits) * blocks;
   Arena ar;
   size_t o_k[2] = {ar.take<uint32_t>(n), ar.take<uint32_t>(n)};
@@ -464,6 +464,7 @@ extern "C" int gf_bucket_by_cell(gf_ctx* ctx, const gf_grid* g, const gf_points*
   if (st) return st;
   auto U32 = [&](size_t o) { return (uint32_t*)(base + o); };
   RadixArgs a{};
+  a.tile = radix_tile();
   a.x = pts->x; a.y = pts->y; a.n = n;
   a.minX = g->minX; a.minY = g->minY; a.cl = g->cellLength; a.gn = g->n;
   a.bits = pbits; a.nblk = blocks;
@@ -512,8 +513,8 @@ extern "C" int gf_shard_by_columns(gf_ctx* ctx, const gf_grid* g, const gf_point
   if (n > (int64_t)UINT32_MAX) return set_err(ctx, GF_ERR_ARG, "gf_shard_by_columns: window too large");
   int bits = 1;
   while ((1 << bits) < nbands) ++bits;
-  const int64_t tiles = (n + kRadixTile - 1) / kRadixTile;
-  const int blocks = (int)std::min<int64_t>(std::max<int64_t>(tiles / 4, 1), (int64_t)ctx->num_cus);
+  const int64_t tiles = (n + radix_tile() - 1) / radix_tile();
+  const int blocks = (int)std::min<int64_t>(std::max<int64_t>(tiles / 4, 1), (int64_t)radix_max_blocks(ctx->num_cus));
   const int64_t mat = ((int64_t)1 << bits) * blocks;
   Arena ar;
   size_t o_k0 = ar.take<uint32_t>(n), o_k = ar.take<uint32_t>(n);
@@ -522,6 +523,7 @@ extern "C" int gf_shard_by_columns(gf_ctx* ctx, const gf_grid* g, const gf_point
   if (st) return st;
   auto U32 = [&](size_t o) { return (uint32_t*)(base + o); };
   RadixArgs a{};
+  a.tile = radix_tile();
   a.x = pts->x; a.y = pts->y; a.n = n;
   a.minX = g->minX; a.minY = g->minY; a.cl = g->cellLength; a.gn = g->n;
   a.bits = bits; a.nblk = blocks; a.shift = 0;
@@ -1519,7 +1521,8 @@ static int knn_large(gf_knn_plan* P, const gf_points* pts, void* result) {
   }
   const gf_knn_plan::Lane& L = P->lane[0];
   const int64_t mm = std::max<int64_t>(n, 1);
-  const int nb = (int)std::min<int64_t>(std::max<int64_t>((mm + kRadixTile - 1) / kRadixTile / 4, 1), (int64_t)ctx->num_cus);
+  const int nb = (int)std::min<int64_t>(std::max<int64_t>((mm + radix_tile() - 1) / radix_tile() / 4, 1),
+                                        (int64_t)radix_max_blocks(ctx->num_cus));
   const int64_t mat = (int64_t)256 * nb;  // 8-bit digits
   Arena ar;
   size_t o_k[2] = {ar.take<uint32_t>(mm), ar.take<uint32_t>(mm)};
@@ -1542,6 +1545,7 @@ static int knn_large(gf_knn_plan* P, const gf_points* pts, void* result) {
       GF_HIP_CHECK(ctx, launch_knn_large(ctx, 1, a));
       for (int p = 0; p < 4; ++p) {  // 32 bits = 4 passes of 8
         RadixArgs r{};
+        r.tile = radix_tile();
         r.n = mm; r.n_dev = a.cnt + pass;
         r.kin = U32(o_k[p & 1]); r.vin = U32(o_p[cur]);
         r.kout = U32(o_k[(p + 1) & 1]); r.vout = U32(o_p[cur ^ 1]);
@@ -2261,6 +2265,19 @@ extern "C" int gf_window_upload(gf_window* w, const double* x, const double* y, 
   w->has_ts = ts != nullptr;
   w->pending = true;
   w->n = n;
+  return GF_OK;
+}
+
+extern "C" int gf_host_pinned(const void* p, int* pinned) {
+  if (!pinned) return GF_ERR_ARG;
+  *pinned = 0;
+  if (!p) return GF_OK;
+  hipPointerAttribute_t at{};
+  if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+    (void)hipGetLastError();  // pageable memory is not a HIP allocation: clear the sticky error
+    return GF_OK;
+  }
+  *pinned = at.type == hipMemoryTypeHost ? 1 : 0;
   return GF_OK;
 }
 

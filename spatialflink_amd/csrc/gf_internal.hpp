@@ -322,7 +322,14 @@ struct RadixArgs {
   int32_t nbands;           // > 0: pass 0's key is the point's column band (gf_shard_by_columns), not its cell
   int32_t band_lo[64];      // the bands' first columns, ascending (band_lo[0] is taken as -inf)
   uint32_t bins;            // stage 2: cell_start entries - 1 (0: gn * gn + 1)
+  int32_t tile;             // points per scatter tile (radix_tile()); chunks are whole tiles
 };
+// scatter block size: 1024 threads (one 8192-point tile per block, one block per CU) or 512
+// (4096-point tiles, two blocks per CU: one block's LDS phases overlap the other's memory);
+// GF_RADIX_NT selects it (A/B), default below
+int radix_threads();
+inline int radix_tile() { return radix_threads() / 64 * 512; }
+inline int radix_max_blocks(int num_cus) { return num_cus * (1024 / radix_threads()); }
 constexpr int kMaxShardBands = 64;
 size_t radix_scatter_lds_bytes();
 hipError_t launch_gather_points(hipStream_t s, const gf_points& in, const uint32_t* perm, int64_t begin, int64_t m,

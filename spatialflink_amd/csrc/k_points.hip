@@ -1,6 +1,8 @@
 // k_points.hip -- per-point kernels: K1 cell assignment, K2 bucketing by cell (stable LSD
 // radix sort: per-wave LDS histograms, wave-ballot ranking), exclusive scan, and selection-
 // bitmap -> index expansion.  gfx950, wave64.
+#include <cstdlib>
+
 #include "gf_internal.hpp"
 
 namespace gf {
@@ -171,10 +173,10 @@ __device__ __forceinline__ uint32_t pass0_key(double x, double y, const RadixArg
 __device__ __forceinline__ void radix_chunk(const RadixArgs& a, int64_t& beg, int64_t& end) {
   int64_t n = a.n;
   if (a.n_dev && (int64_t)*a.n_dev < n) n = (int64_t)*a.n_dev;
-  const int64_t tiles = (n + kRadixTile - 1) / kRadixTile;
+  const int64_t T = a.tile, tiles = (n + T - 1) / T;
   const int64_t per = (tiles + a.nblk - 1) / a.nblk;
-  beg = (int64_t)blockIdx.x * per * kRadixTile;
-  end = beg + per * kRadixTile < n ? beg + per * kRadixTile : n;
+  beg = (int64_t)blockIdx.x * per * T;
+  end = beg + per * T < n ? beg + per * T : n;
   if (beg > n) beg = n;
 }
 
@@ -237,29 +239,39 @@ __global__ __launch_bounds__(kRadixThreads) void radix_hist_kernel(RadixArgs a) 
   for (uint32_t j = threadIdx.x; j < D; j += kRadixThreads) a.M[(size_t)j * a.nblk + blockIdx.x] = h[j];
 }
 
+int radix_threads() {
+  static const int nt = [] {
+    const char* e = std::getenv("GF_RADIX_NT");
+    return e && std::atoi(e) == 512 ? 512 : 1024;
+  }();
+  return nt;
+}
 size_t radix_scatter_lds_bytes() {
-  return (size_t)kRadixTile * 8 + (size_t)(kRadixThreads / 64) * kRadixMaxDigits * 4 + 2 * (size_t)(kRadixMaxDigits + 1) * 4;
+  return (size_t)radix_tile() * 8 + (size_t)(radix_threads() / 64) * kRadixMaxDigits * 4 +
+         2 * (size_t)(kRadixMaxDigits + 1) * 4;
 }
 
-__global__ __launch_bounds__(kRadixThreads) void radix_scatter_kernel(RadixArgs a) {
+template <int NT>
+__global__ __launch_bounds__(NT) void radix_scatter_kernel(RadixArgs a) {
   extern __shared__ uint32_t rsm[];
-  constexpr int W = kRadixThreads / 64, EPW = kRadixTile / W, U = EPW / 64;  // elements per wave, steps
-  uint32_t* const lk = rsm;                           // [kRadixTile] the tile's keys in sorted order
-  uint32_t* const lv = lk + kRadixTile;               // [kRadixTile] their values
-  uint32_t* const wc = lv + kRadixTile;               // [W][kRadixMaxDigits] wave counts -> slots
+  constexpr int kTile = NT / 64 * 512;
+  constexpr int W = NT / 64, EPW = kTile / W, U = EPW / 64;  // elements per wave, steps
+  uint32_t* const lk = rsm;                           // [kTile] the tile's keys in sorted order
+  uint32_t* const lv = lk + kTile;               // [kTile] their values
+  uint32_t* const wc = lv + kTile;               // [W][kRadixMaxDigits] wave counts -> slots
   uint32_t* const tb = wc + W * kRadixMaxDigits;      // [D + 1] tile start per digit
   uint32_t* const gc = tb + kRadixMaxDigits + 1;      // [D] next global slot per digit
-  __shared__ uint32_t ws[kRadixThreads / 64];
+  __shared__ uint32_t ws[NT / 64];
   const uint32_t D = 1u << a.bits, mask = D - 1u;
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const uint64_t below = (1ull << lane) - 1ull;
   int64_t beg, end;
   radix_chunk(a, beg, end);
-  for (uint32_t d = threadIdx.x; d < D; d += kRadixThreads) gc[d] = a.Ms[(size_t)d * a.nblk + blockIdx.x];
+  for (uint32_t d = threadIdx.x; d < D; d += NT) gc[d] = a.Ms[(size_t)d * a.nblk + blockIdx.x];
   // (r04: prefetching the next tile into registers pushed the kernel to 128 VGPRs + 80 B of
   // scratch per lane and cost 76 -> 88 us per pass; the tile is loaded at the top of its step)
-  for (int64_t t0 = beg; t0 < end; t0 += kRadixTile) {  // block-uniform
-    const uint32_t cnt = (uint32_t)(end - t0 < kRadixTile ? end - t0 : kRadixTile);
+  for (int64_t t0 = beg; t0 < end; t0 += kTile) {  // block-uniform
+    const uint32_t cnt = (uint32_t)(end - t0 < kTile ? end - t0 : kTile);
     uint32_t k[U], v[U], r[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -286,7 +298,7 @@ __global__ __launch_bounds__(kRadixThreads) void radix_scatter_kernel(RadixArgs 
     }
     lds_barrier();
     {  // exclusive scan of the counts in (digit, wave) order: entry j = d * W + w
-      constexpr int PT = W * kRadixMaxDigits / kRadixThreads;  // entries per thread
+      constexpr int PT = W * kRadixMaxDigits / NT;  // entries per thread
       const uint32_t j0 = threadIdx.x * PT;
       uint32_t c[PT], run = 0;
 #pragma unroll
@@ -327,14 +339,14 @@ __global__ __launch_bounds__(kRadixThreads) void radix_scatter_kernel(RadixArgs 
       }
     }
     lds_barrier();
-    for (uint32_t p = threadIdx.x; p < cnt; p += kRadixThreads) {  // runs of one digit: consecutive slots
+    for (uint32_t p = threadIdx.x; p < cnt; p += NT) {  // runs of one digit: consecutive slots
       const uint32_t kk = lk[p], d = (kk >> a.shift) & mask;
       const uint32_t o = gc[d] + (p - tb[d]);
       a.kout[o] = kk;
       a.vout[o] = lv[p];
     }
     lds_barrier();
-    for (uint32_t d = threadIdx.x; d < D; d += kRadixThreads) gc[d] += tb[d + 1] - tb[d];
+    for (uint32_t d = threadIdx.x; d < D; d += NT) gc[d] += tb[d + 1] - tb[d];
     lds_barrier();
   }
 }
@@ -396,7 +408,10 @@ hipError_t launch_radix(gf_ctx* ctx, int stage, const RadixArgs& a, int blocks) 
       else hipLaunchKernelGGL(radix_hist_kernel<false>, dim3(blocks), dim3(kRadixThreads), 0, s, a);
       break;
     case 1:
-      hipLaunchKernelGGL(radix_scatter_kernel, dim3(blocks), dim3(kRadixThreads), radix_scatter_lds_bytes(), s, a);
+      if (radix_threads() == 512)
+        hipLaunchKernelGGL(radix_scatter_kernel<512>, dim3(blocks), dim3(512), radix_scatter_lds_bytes(), s, a);
+      else
+        hipLaunchKernelGGL(radix_scatter_kernel<1024>, dim3(blocks), dim3(1024), radix_scatter_lds_bytes(), s, a);
       break;
     default: {  // cell_start[0 .. gn*gn + 1] of the sorted kout into a.M: one wave per 256 positions
       const int64_t waves = (a.n + 1 + 64 * kBoundsPer - 1) / (64 * kBoundsPer);

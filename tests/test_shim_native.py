@@ -129,6 +129,8 @@ def shim(gpu):
     S.shim_polygon_join_window.argtypes = [P, P, P, P, i64, P, d, C.c_int, pp, P]
     S.shim_csv_parse.argtypes = [P, C.c_char_p, i64, P, P, P, P, P, i64, P, P, P]
     S.shim_geojson_parse.argtypes = [P, C.c_char_p, i64, P, P, P, P, P, i64, P, P, P]
+    S.shim_pinned_alloc.argtypes = [i64, pp]
+    S.shim_pinned_free.argtypes = [P]
     return S
 
 
@@ -208,6 +210,35 @@ def test_knn_window(shim, ctx, oracle_mod, k, gn):
             np.testing.assert_array_equal(oi, ei)
     finally:
         shim.shim_knn_destroy(plan)
+
+
+@pytest.mark.gpu
+def test_knn_window_pinned_objid(shim, ctx, oracle_mod):
+    """knnWindow with the objID column in pinned memory (pinnedBuffer on the Java side): the shim
+    detects it (gf_host_pinned) and uploads x, y only (gf_window_upload_mapped) -- the kernels read
+    the candidates' keys in place.  Same records as the copied path; windows grow and shrink."""
+    g, og = grid(500), oracle_mod.grid(500, *BEIJING)
+    plan = P()
+    _ok(shim, ctx, shim.shim_knn_plan(ctx, C.byref(g), QPOINT[0], QPOINT[1], 0.5, 50, C.byref(plan)), "plan")
+    cap = 1_300_000
+    buf = P()
+    _ok(shim, ctx, shim.shim_pinned_alloc(8 * cap, C.byref(buf)), "pinned")
+    pinned = np.ctypeslib.as_array((C.c_int64 * cap).from_address(buf.value))
+    try:
+        for seed, n in ((5, 1_200_000), (6, 300_000), (7, 1_300_000)):
+            x, y = oracle_mod.java_random_points(seed, n, *BEIJING)
+            o = (np.random.default_rng(seed).permutation(n) % (n // 2)).astype(np.int64)
+            pinned[:n] = o
+            oo = np.zeros(50, np.int64); od = np.zeros(50); oi = np.zeros(50, np.int64); m = i32()
+            st = shim.shim_knn_window(plan, _a(x), _a(y), buf, n, _a(oo), _a(od), _a(oi), C.byref(m))
+            _ok(shim, ctx, st, "knnWindow pinned")
+            est, eo, ed, ei = oracle_mod.knn(og, x, y, o, *QPOINT, 0.5, 50)
+            np.testing.assert_array_equal(oo[:m.value], eo)
+            np.testing.assert_array_equal(od[:m.value].view(np.int64), ed.view(np.int64))
+            np.testing.assert_array_equal(oi[:m.value], ei)
+    finally:
+        shim.shim_knn_destroy(plan)
+        shim.shim_pinned_free(buf)
 
 
 @pytest.mark.gpu
