@@ -2288,8 +2288,10 @@ extern "C" int gf_window_upload_mapped(gf_window* w, const double* x, const doub
   if (n > 0) {  // the objID column is read in place through the host mapping (candidates only)
     int st = bind(w->ctx);
     if (st) return st;
-    if (hipHostGetDevicePointer(&dp, (void*)objID_pinned, 0) != hipSuccess || !dp)
+    if (hipHostGetDevicePointer(&dp, (void*)objID_pinned, 0) != hipSuccess || !dp) {
+      (void)hipGetLastError();  // clear the thread's sticky error: the next launch check must not see it
       return set_err(w->ctx, GF_ERR_ARG, "gf_window_upload_mapped: objID is not pinned host memory (gf_pinned_alloc)");
+    }
   }
   int st = gf_window_upload(w, x, y, nullptr, nullptr, n);
   if (st) return st;

@@ -142,6 +142,22 @@ def test_knn_mapped_objid_stream(sf, oracle_mod, depth):
     op.set_pipeline(0, q, r, k, depth)
     rec = sf.PinnedRecords(nw, k)
     cols = lambda i: pins[i][1]  # noqa: E731
+    try:
+        _stream_mapped(sf, oracle_mod, L, ctx, op, q, plan, wins, cols, hosts, rec, og, n, k, r, nw)
+    finally:
+        ctx.synchronize()
+        op.set_pipeline(0, q, r, k, 1)
+        for w in wins:
+            L.gf_window_destroy(w)
+        for p, _ in pins:
+            L.gf_pinned_free(p)
+
+
+def _stream_mapped(sf, oracle_mod, L, ctx, op, q, plan, wins, cols, hosts, rec, og, n, k, r, nw):
+    import torch
+
+    from spatialflink_amd import _lib
+
     _lib.check(L.gf_window_upload_mapped(wins[0], cols(0)[0], cols(0)[1], cols(0)[2], n), ctx.handle, "upload")
     for i in range(nw):
         if i + 1 < nw:
@@ -162,8 +178,7 @@ def test_knn_mapped_objid_stream(sf, oracle_mod, depth):
         np.testing.assert_array_equal(ix, ei)
     x, y, obj = hosts[0]
     assert L.gf_window_upload_mapped(wins[0], x.ctypes.data, y.ctypes.data, obj.ctypes.data, n) == _lib.GF_ERR_ARG
-    op.set_pipeline(0, q, r, k, 1)
-    for w in wins:
-        L.gf_window_destroy(w)
-    for p, _ in pins:
-        L.gf_pinned_free(p)
+    # the refused call leaves no sticky HIP error behind: the next launch works
+    res = op.run(sf.PointWindow.from_numpy(x, y, obj), q, r, k)
+    est, eo, ed, ei = oracle_mod.knn(og, x, y, obj, QPOINT[0], QPOINT[1], r, k)
+    np.testing.assert_array_equal(res.objID, eo)

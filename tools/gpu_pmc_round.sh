@@ -1,22 +1,23 @@
 #!/bin/bash
-# r03 PMC + kernel-stats campaign over the final kernels of every workload line (VERDICT r02
+# Per-round PMC + kernel-stats campaign over the final kernels of every workload line (VERDICT r02
 # item 2).  Per workload: one `rocprofv3 --kernel-trace --stats` run, then one --pmc run per
 # counter group (tools/gpu_pmc.sh: FETCH_SIZE and WRITE_SIZE never share a pass), summarised by
-# tools/pmc_table.py into gpurun_out/pmc_r03/<tag>.json -> copied to profiles/r03_<tag>_pmc.json.
-# usage: tools/gpu_pmc_r03.sh TAG... (default: all)   tags: knn range1m range10m ppoly join
+# tools/pmc_table.py into gpurun_out/pmc_${ROUND}/<tag>.json -> copied to profiles/${ROUND}_<tag>_pmc.json.
+# usage: ROUND=r04 tools/gpu_pmc_round.sh TAG... (default: all)   tags: knn range1m range10m ppoly join
 #        sliding bucket csv geojson polyknn
 set -e
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
+ROUND=${ROUND:-r04}
 COMMON="--steps 5 --warmup 2 --no-cpu-baseline --no-verify"
-OUT=gpurun_out/pmc_r03
+OUT=gpurun_out/pmc_${ROUND}
 mkdir -p $OUT
 one() {  # tag kernel-regex passes bench-args...
   local tag=$1 re=$2 passes=$3; shift 3
   timeout -s KILL 150 rocprofv3 --kernel-trace --stats -d $OUT/$tag/stats -o stats --output-format csv \
     -- python -u bench.py "$@" $COMMON > $OUT/$tag.stats.log 2>&1 || { echo "[stats $tag] failed"; tail -5 $OUT/$tag.stats.log; exit 1; }
-  PASSES="$passes" tools/gpu_pmc.sh "r03_$tag" "$re" "$@" $COMMON
-  python tools/pmc_table.py $OUT/$tag.json gpurun_out/pmc/r03_$tag --note "r03 $tag: $* $COMMON"
+  PASSES="$passes" tools/gpu_pmc.sh "${ROUND}_$tag" "$re" "$@" $COMMON
+  python tools/pmc_table.py $OUT/$tag.json gpurun_out/pmc/${ROUND}_$tag --note "${ROUND} $tag: $* $COMMON"
   cp $OUT/$tag/stats/*kernel_stats.csv $OUT/${tag}_kernel_stats.csv 2>/dev/null || true
   echo "[campaign $tag] ok"
 }

@@ -12,6 +12,6 @@ tools/gpu_step.sh b_polyknn4 300 python -u bench.py --workload polyknn --pipelin
 tools/gpu_step.sh b_knn4 300 python -u bench.py --pipeline 4 --steps 30 --warmup 8 --no-cpu-baseline || exit 1
 tools/gpu_step.sh b_join 400 python -u bench.py --workload join --steps 20 --warmup 3 --no-cpu-baseline || exit 1
 tools/gpu_step.sh p_join 200 rocprofv3 --kernel-trace --stats -d gpurun_out/p_join -o stats --output-format csv -- python -u bench.py --workload join --steps 5 --warmup 2 --no-cpu-baseline --no-verify || exit 1
-GF_RADIX_NT=512 tools/gpu_step.sh t_bucket512 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_parity.py -k "bucket" tests/test_gpu_knn_large.py -k "not merge" || exit 1
+GF_RADIX_NT=512 tools/gpu_step.sh t_bucket512 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_parity.py tests/test_gpu_knn_large.py -k "bucket or knn_large" || exit 1
 GF_RADIX_NT=512 tools/gpu_step.sh b_bucket512 200 python -u bench.py --workload bucket --steps 20 --warmup 3 || exit 1
 GF_RADIX_NT=512 tools/gpu_step.sh p_bucket512 200 rocprofv3 --kernel-trace --stats -d gpurun_out/p_bucket512 -o stats --output-format csv -- python -u bench.py --workload bucket --steps 5 --warmup 2 --no-cpu-baseline --no-verify || exit 1

@@ -2,7 +2,7 @@
 # every SURVEY §8 configuration's single-GPU line (bench.py / tools/bench_workloads.py), each
 # verified against the oracle (or the whole-window evaluation), with its CPU baselines; the
 # lines are collected into gpurun_out/wl/lines.jsonl (-> profiles/rNN_workloads.jsonl).  Kernel
-# statistics and PMC of the same commands: tools/gpu_pmc_r03.sh.
+# statistics and PMC of the same commands: tools/gpu_pmc_round.sh.
 set -e
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp

@@ -3,7 +3,7 @@
 Inputs (all committed under profiles/):
   rNN_workloads.jsonl     the bench lines (tools/gpu_workloads.sh: bench.py --workload ...)
   rNN_<tag>_pmc.json      tools/pmc_table.py summaries of the rocprofv3 --pmc passes of the same
-                          commands (tools/gpu_pmc_r03.sh): per kernel the median FETCH_SIZE /
+                          commands (tools/gpu_pmc_round.sh): per kernel the median FETCH_SIZE /
                           WRITE_SIZE per dispatch and the dispatch counts
 
 Per line:  frac      = roofline.bytes_per_launch / time / peak, time = the line's own basis:
