@@ -435,6 +435,67 @@ extern "C" int gf_assign_cells(gf_ctx* ctx, const gf_grid* g, const gf_points* p
   return GF_OK;
 }
 
+// K2 in row mode (grids up to 511 x 511, where the LSD sort takes two 9-bit passes): pass A
+// sorts stably by row (the keys' high digit, as the LSD's last pass would), pass B sorts every
+// row stably by column -- over row SEGMENTS, so each block's output lies inside its row's range
+// (row-local writes instead of 512 runs spread over the whole output), only the permutation is
+// written, and the cells' starts come from pass B's own scan (no key read-back, no bounds pass).
+constexpr int kRowSeg = 32768;  // points per row segment (a uniform 10M-point window on 500 x 500: one per row)
+static int bucket_rows(gf_ctx* ctx, const gf_grid* g, const gf_points* pts, uint32_t* perm, uint32_t* cell_start,
+                       int blocks) {
+  const int64_t n = pts->n;
+  const int64_t D = kRadixMaxDigits, matA = D * blocks;
+  const int64_t ub = n / kRowSeg + g->n + 2;  // segments <= sum over rows of (size / seg + 1)
+  const int64_t matB = D * ub;
+  Arena ar;
+  size_t o_k0 = ar.take<uint32_t>(n), o_k1 = ar.take<uint32_t>(n), o_v1 = ar.take<uint32_t>(n);
+  size_t o_ma = ar.take<uint32_t>(matA), o_msa = ar.take<uint32_t>(matA + 1);
+  size_t o_mb = ar.take<uint32_t>(matB), o_msb = ar.take<uint32_t>(matB + 1);
+  int st = 0;
+  char* base = (char*)ctx_scratch(ctx, ar.off, &st);
+  if (st) return st;
+  auto U32 = [&](size_t o) { return (uint32_t*)(base + o); };
+  RadixArgs a{};
+  a.tile = radix_tile();
+  a.x = pts->x; a.y = pts->y; a.n = n;
+  a.minX = g->minX; a.minY = g->minY; a.cl = g->cellLength; a.gn = g->n;
+  a.bits = kRadixMaxBits; a.nblk = blocks; a.rowmode = 1;
+  // pass A: row keys -> k0 with the histogram of rows, scan, stable scatter by row
+  a.kout = U32(o_k0);
+  a.shift = kRadixMaxBits;
+  a.M = U32(o_ma);
+  a.Ms = U32(o_msa);
+  GF_HIP_CHECK(ctx, launch_radix(ctx, 0, a, blocks));
+  ExpandState es;
+  if ((st = lookback_state(ctx, scan1_blocks(matA), &es))) return st;
+  GF_HIP_CHECK(ctx, launch_scan1(ctx->stream, U32(o_ma), matA, U32(o_msa), nullptr, 0, 0, es));
+  ctx->expand_base += (unsigned long long)scan1_blocks(matA);
+  a.kin = U32(o_k0);
+  a.vin = nullptr;
+  a.kout = U32(o_k1);
+  a.vout = U32(o_v1);
+  GF_HIP_CHECK(ctx, launch_radix(ctx, 1, a, blocks));
+  // pass B: per row segment column histograms, one scan, stable scatter by column (perm only)
+  RadixArgs b = a;
+  b.kin = U32(o_k1);
+  b.vin = U32(o_v1);
+  b.kout = nullptr;
+  b.vout = perm;
+  b.shift = 0;
+  b.seg = kRowSeg;
+  b.MsA = U32(o_msa);
+  b.nblkA = blocks;
+  b.M = U32(o_mb);
+  b.Ms = U32(o_msb);
+  b.cstart = cell_start;
+  GF_HIP_CHECK(ctx, launch_radix(ctx, 3, b, (int)ub));
+  if ((st = lookback_state(ctx, scan1_blocks(matB), &es))) return st;
+  GF_HIP_CHECK(ctx, launch_scan1(ctx->stream, U32(o_mb), matB, U32(o_msb), nullptr, 0, 0, es));
+  ctx->expand_base += (unsigned long long)scan1_blocks(matB);
+  GF_HIP_CHECK(ctx, launch_radix(ctx, 1, b, (int)ub));
+  return GF_OK;
+}
+
 extern "C" int gf_bucket_by_cell(gf_ctx* ctx, const gf_grid* g, const gf_points* pts, uint32_t* perm,
                                  uint32_t* cell_start) {
   if (!ctx || !grid_ok(g) || !perm || !cell_start) return set_err(ctx, GF_ERR_ARG, "gf_bucket_by_cell: bad argument");
@@ -454,6 +515,8 @@ extern "C" int gf_bucket_by_cell(gf_ctx* ctx, const gf_grid* g, const gf_points*
   // the scatter's tile buffers bound the blocks per CU (radix_threads), >= ~4 tiles per block
   const int64_t tiles = (n + radix_tile() - 1) / radix_tile();
   const int blocks = (int)std::min<int64_t>(std::max<int64_t>(tiles / 4, 1), (int64_t)radix_max_blocks(ctx->num_cus));
+  if (passes >= 2 && g->n + 1 <= kRadixMaxDigits && !std::getenv("GF_K2_LSD"))
+    return bucket_rows(ctx, g, pts, perm, cell_start, blocks);
   const int64_t mat = ((int64_t)1 << pbits) * blocks;
   Arena ar;
   size_t o_k[2] = {ar.take<uint32_t>(n), ar.take<uint32_t>(n)};

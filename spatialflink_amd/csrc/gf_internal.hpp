@@ -323,6 +323,13 @@ struct RadixArgs {
   int32_t band_lo[64];      // the bands' first columns, ascending (band_lo[0] is taken as -inf)
   uint32_t bins;            // stage 2: cell_start entries - 1 (0: gn * gn + 1)
   int32_t tile;             // points per scatter tile (radix_tile()); chunks are whole tiles
+  // row mode (gf_bucket_by_cell, gn + 1 <= 512 rows): pass A's key is row << 9 | column (row = cy,
+  // gn for the out-of-grid bucket) sorted by row; pass B sorts every row's SEGMENTS by column
+  int32_t rowmode;          // pass 0 keys are row keys
+  int32_t seg;              // > 0: pass B -- blocks are row segments of <= seg points
+  const uint32_t* MsA;      // pass B: pass A's scanned matrix (row r = [MsA[r nblkA], MsA[(r+1) nblkA]))
+  int32_t nblkA;
+  uint32_t* cstart;         // pass B: cell_start[0 .. gn*gn + 1], written by each row's first segment
 };
 // scatter block size: 1024 threads (one 8192-point tile per block, one block per CU) or 512
 // (4096-point tiles, two blocks per CU: one block's LDS phases overlap the other's memory);
@@ -334,7 +341,8 @@ constexpr int kMaxShardBands = 64;
 size_t radix_scatter_lds_bytes();
 hipError_t launch_gather_points(hipStream_t s, const gf_points& in, const uint32_t* perm, int64_t begin, int64_t m,
                                 double* ox, double* oy, int64_t* oo, int64_t* ot);
-// stage 0 histogram, 1 scatter, 2 cell_start from the sorted kout (every bucket's first position)
+// stage 0 histogram, 1 scatter, 2 cell_start from the sorted kout (every bucket's first position),
+// 3 row-segment histogram (pass B of row mode; `blocks` = the segment bound)
 hipError_t launch_radix(gf_ctx* ctx, int stage, const RadixArgs& a, int blocks);
 // exclusive scan: out[0..L] (out[L] = total); tmp >= scan_tmp_elems(L) uint32
 size_t scan_tmp_elems(int64_t L);

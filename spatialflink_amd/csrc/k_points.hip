@@ -165,8 +165,93 @@ __device__ __forceinline__ uint32_t band_key(double x, const RadixArgs& a) {
   for (int j = 1; j < a.nbands; ++j) b += cx >= a.band_lo[j] ? 1u : 0u;
   return b;
 }
+// row mode: row << 9 | column; the out-of-grid bucket is row gn, column 0 (so the row-major
+// order of (row, column) is the order of the cell keys cy * gn + cx, gn * gn last)
+__device__ __forceinline__ uint32_t row_key(double x, double y, const RadixArgs& a) {
+  const int32_t cx = cell_index(x, a.minX, a.cl), cy = cell_index(y, a.minY, a.cl);
+  const bool valid = cx >= 0 && cy >= 0 && cx < a.gn && cy < a.gn;
+  return valid ? (uint32_t)cy << kRadixMaxBits | (uint32_t)cx : (uint32_t)a.gn << kRadixMaxBits;
+}
 __device__ __forceinline__ uint32_t pass0_key(double x, double y, const RadixArgs& a) {
-  return a.nbands > 0 ? band_key(x, a) : bucket_key(x, y, a);
+  return a.nbands > 0 ? band_key(x, a) : (a.rowmode ? row_key(x, y, a) : bucket_key(x, y, a));
+}
+
+// Row mode, pass B: block b is segment j of row r -- rows have max(1, ceil(size / seg)) segments
+// (an empty row keeps one, which writes its cells' starts), numbered row by row.  Every block
+// derives the numbering from pass A's row totals (one scan over <= 512 rows, blockDim >= 512).
+struct RowSeg {
+  uint32_t r, j, nseg, base;  // row, segment in it, the row's segments, segments before the row
+  int64_t beg, end;           // positions [beg, end) of the sorted-by-row arrays
+  uint32_t total;             // segments of all rows (blocks >= total: none)
+  uint32_t wsum[16];
+};
+__device__ __forceinline__ void row_segment(const RadixArgs& a, RowSeg& rs) {
+  const uint32_t t = threadIdx.x, lane = t & 63, wid = t >> 6, R = (uint32_t)a.gn + 1u;
+  int64_t lo = 0, hi = 0;
+  uint32_t ns = 0;
+  if (t < R) {
+    lo = a.MsA[(size_t)t * a.nblkA];
+    hi = a.MsA[(size_t)(t + 1) * a.nblkA];  // t + 1 <= 512 digits: entry mat is the total
+    ns = hi > lo ? (uint32_t)((hi - lo + a.seg - 1) / a.seg) : 1u;
+  }
+  if (t >= R) ns = 0;
+  uint32_t inc = ns;  // block exclusive scan of ns (t < 512: waves 0..7)
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t v = __shfl_up(inc, o, 64);
+    if (lane >= (uint32_t)o) inc += v;
+  }
+  if (lane == 63 && wid < 16) rs.wsum[wid] = inc;
+  if (t == 0) rs.r = 0xFFFFFFFFu;
+  __syncthreads();
+  uint32_t before = inc - ns, tot = 0;
+  for (uint32_t w = 0; w < 8; ++w) {
+    before += w < wid ? rs.wsum[w] : 0u;
+    tot += rs.wsum[w];
+  }
+  const uint32_t b = blockIdx.x;
+  if (t < R && b >= before && b < before + ns) {
+    rs.r = t;
+    rs.j = b - before;
+    rs.nseg = ns;
+    rs.base = before;
+    rs.beg = lo + (int64_t)(b - before) * a.seg;
+    rs.end = rs.beg + a.seg < hi ? rs.beg + a.seg : hi;
+    if (rs.beg > hi) rs.beg = hi;
+  }
+  if (t == 0) rs.total = tot;
+  __syncthreads();
+}
+
+// pass B histogram: column counts of segment j of row r into M[(base * D) + d * nseg + j] -- for
+// every row the (column, segment) entries are consecutive and column-major, rows in order, so
+// ONE exclusive scan of M gives every (row, column, segment) its first output position.  Blocks
+// past the segments zero their D entries (the scan covers the launch's bound).
+__global__ __launch_bounds__(kRadixThreads) void radix_seg_hist_kernel(RadixArgs a) {
+  __shared__ uint32_t h[kRadixMaxDigits];
+  __shared__ RowSeg rs;
+  const uint32_t D = 1u << a.bits, mask = D - 1u;
+  for (uint32_t j = threadIdx.x; j < D; j += kRadixThreads) h[j] = 0u;
+  row_segment(a, rs);
+  if (rs.r == 0xFFFFFFFFu) {  // block-uniform
+    for (uint32_t d = threadIdx.x; d < D; d += kRadixThreads) a.M[(size_t)blockIdx.x * D + d] = 0u;
+    return;
+  }
+  constexpr int U = 8;
+  for (int64_t i0 = rs.beg + threadIdx.x; i0 < rs.end; i0 += (int64_t)kRadixThreads * U) {
+    uint32_t k[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = i0 + (int64_t)u * kRadixThreads;
+      k[u] = i < rs.end ? a.kin[i] : 0u;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (i0 + (int64_t)u * kRadixThreads < rs.end) atomicAdd(&h[k[u] & mask], 1u);
+  }
+  __syncthreads();
+  for (uint32_t d = threadIdx.x; d < D; d += kRadixThreads)
+    a.M[(size_t)rs.base * D + (size_t)d * rs.nseg + rs.j] = h[d];
 }
 
 // block b's chunk [beg, end) of the a.nblk chunks (whole tiles except the last)
@@ -242,17 +327,24 @@ __global__ __launch_bounds__(kRadixThreads) void radix_hist_kernel(RadixArgs a) 
 int radix_threads() {
   static const int nt = [] {
     const char* e = std::getenv("GF_RADIX_NT");
-    return e && std::atoi(e) == 512 ? 512 : 1024;
+    return e && std::atoi(e) == 1024 ? 1024 : 512;  // r04 A/B on K2: 512 (3 blocks per CU) 68 vs 77 us per pass
   }();
   return nt;
+}
+static bool radix_occ6() {
+  static const bool on = [] {
+    const char* e = std::getenv("GF_RADIX_OCC6");
+    return e && std::atoi(e) != 0;
+  }();
+  return on;
 }
 size_t radix_scatter_lds_bytes() {
   return (size_t)radix_tile() * 8 + (size_t)(radix_threads() / 64) * kRadixMaxDigits * 4 +
          2 * (size_t)(kRadixMaxDigits + 1) * 4;
 }
 
-template <int NT>
-__global__ __launch_bounds__(NT) void radix_scatter_kernel(RadixArgs a) {
+template <int NT, int MINW>
+__global__ __launch_bounds__(NT, MINW) void radix_scatter_kernel(RadixArgs a) {
   extern __shared__ uint32_t rsm[];
   constexpr int kTile = NT / 64 * 512;
   constexpr int W = NT / 64, EPW = kTile / W, U = EPW / 64;  // elements per wave, steps
@@ -266,8 +358,27 @@ __global__ __launch_bounds__(NT) void radix_scatter_kernel(RadixArgs a) {
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const uint64_t below = (1ull << lane) - 1ull;
   int64_t beg, end;
-  radix_chunk(a, beg, end);
-  for (uint32_t d = threadIdx.x; d < D; d += NT) gc[d] = a.Ms[(size_t)d * a.nblk + blockIdx.x];
+  if (a.seg > 0) {  // row mode pass B: a row segment; its columns' first slots; cells' starts
+    __shared__ RowSeg rs;
+    row_segment(a, rs);
+    if (rs.r == 0xFFFFFFFFu) return;  // block-uniform
+    beg = rs.beg;
+    end = rs.end;
+    const size_t m0 = (size_t)rs.base * D;
+    for (uint32_t d = threadIdx.x; d < D; d += NT) gc[d] = a.Ms[m0 + (size_t)d * rs.nseg + rs.j];
+    if (rs.j == 0) {  // the row's cells start at their columns' first slots
+      if (rs.r < (uint32_t)a.gn) {
+        for (int32_t c = threadIdx.x; c < a.gn; c += NT)
+          a.cstart[(size_t)rs.r * a.gn + c] = a.Ms[m0 + (size_t)c * rs.nseg];
+      } else if (threadIdx.x == 0) {
+        a.cstart[(size_t)a.gn * a.gn] = a.Ms[m0];
+        a.cstart[(size_t)a.gn * a.gn + 1] = (uint32_t)a.n;
+      }
+    }
+  } else {
+    radix_chunk(a, beg, end);
+    for (uint32_t d = threadIdx.x; d < D; d += NT) gc[d] = a.Ms[(size_t)d * a.nblk + blockIdx.x];
+  }
   // (r04: prefetching the next tile into registers pushed the kernel to 128 VGPRs + 80 B of
   // scratch per lane and cost 76 -> 88 us per pass; the tile is loaded at the top of its step)
   for (int64_t t0 = beg; t0 < end; t0 += kTile) {  // block-uniform
@@ -300,12 +411,11 @@ __global__ __launch_bounds__(NT) void radix_scatter_kernel(RadixArgs a) {
     {  // exclusive scan of the counts in (digit, wave) order: entry j = d * W + w
       constexpr int PT = W * kRadixMaxDigits / NT;  // entries per thread
       const uint32_t j0 = threadIdx.x * PT;
-      uint32_t c[PT], run = 0;
+      uint32_t run = 0;  // (the counts are read twice: keeping them costs PT registers)
 #pragma unroll
       for (int q = 0; q < PT; ++q) {
         const uint32_t j = j0 + q, d = j / W, ww = j % W;
-        c[q] = d < D ? wc[ww * kRadixMaxDigits + d] : 0u;
-        run += c[q];
+        run += d < D ? wc[ww * kRadixMaxDigits + d] : 0u;
       }
       uint32_t inc = run;
 #pragma unroll
@@ -321,10 +431,11 @@ __global__ __launch_bounds__(NT) void radix_scatter_kernel(RadixArgs a) {
       for (int q = 0; q < PT; ++q) {
         const uint32_t j = j0 + q, d = j / W, ww = j % W;
         if (d < D) {
+          const uint32_t c = wc[ww * kRadixMaxDigits + d];
           wc[ww * kRadixMaxDigits + d] = before;
           if (ww == 0) tb[d] = before;
+          before += c;
         }
-        before += c[q];
       }
       if (threadIdx.x == 0) tb[D] = cnt;
     }
@@ -342,7 +453,7 @@ __global__ __launch_bounds__(NT) void radix_scatter_kernel(RadixArgs a) {
     for (uint32_t p = threadIdx.x; p < cnt; p += NT) {  // runs of one digit: consecutive slots
       const uint32_t kk = lk[p], d = (kk >> a.shift) & mask;
       const uint32_t o = gc[d] + (p - tb[d]);
-      a.kout[o] = kk;
+      if (a.kout) a.kout[o] = kk;  // (pass B of row mode keeps only the permutation)
       a.vout[o] = lv[p];
     }
     lds_barrier();
@@ -353,12 +464,14 @@ __global__ __launch_bounds__(NT) void radix_scatter_kernel(RadixArgs a) {
 
 // cell_start straight from the sorted keys (no histogram, no scan): cell_start[b] = the first
 // position whose key is >= b, so position i (key[-1] = -1, key[n] = bins as sentinels) starts
-// every bucket b in (key[i-1], key[i]].  One wave per 256 consecutive positions (four per lane,
-// one 16-B load); its boundaries are visited one at a time (ballot) and the wave writes each
-// one's range together -- one entry per lane, so a long run of empty buckets (clustered input,
-// the out-of-grid bucket) costs range / 64 wave stores.  Every entry of cell_start[0 .. bins] is
-// written exactly once.
-constexpr int kBoundsPer = 16;  // keys per lane: four 16-B loads in flight (one per lane was latency-bound)
+// every bucket b in (key[i-1], key[i]].  One wave per 1024 consecutive positions (16 per lane,
+// four 16-B loads in flight).  A lane writes the range of each of its boundaries itself when it is
+// short (< kBoundsShort buckets: uniform input, one store per boundary, all lanes' stores in one
+// instruction); long ranges (clustered input, the out-of-grid bucket) are written by the whole
+// wave, one range at a time.  Every entry of cell_start[0 .. bins] is written exactly once.
+// (r04: the wave-at-a-time walk over EVERY boundary -- three lane shuffles and a store loop per
+// boundary, ~25 per wave on uniform input -- took 42-53 us for 10M points.)
+constexpr int kBoundsPer = 16, kBoundsShort = 8;
 __global__ __launch_bounds__(kBlock) void radix_bounds_kernel(const uint32_t* __restrict__ keys, int64_t n,
                                                               uint32_t bins, uint32_t* __restrict__ cell_start) {
   const int lane = threadIdx.x & 63;
@@ -387,14 +500,18 @@ __global__ __launch_bounds__(kBlock) void radix_bounds_kernel(const uint32_t* __
     const int64_t p = p0 + j;
     const uint32_t cur = k[j], pv = j == 0 ? prev : k[j - 1];
     const bool start = j == 0 && first;
-    uint64_t m = __ballot(p <= n && (cur != pv || start));
-    while (m) {  // wave-uniform
+    const bool bd = p <= n && (cur != pv || start);
+    const int64_t lo = start ? 0 : (int64_t)pv + 1, hi = cur;
+    const bool lng = bd && hi - lo >= kBoundsShort;
+    if (bd && !lng)
+      for (int64_t b = lo; b <= hi; ++b) cell_start[b] = (uint32_t)p;
+    uint64_t m = __ballot(lng);
+    while (m) {  // wave-uniform: the long ranges, one at a time
       const int src = __ffsll((unsigned long long)m) - 1;
       m &= m - 1;
-      const bool s0 = __shfl(start ? 1 : 0, src, 64) != 0;
-      const int64_t lo = s0 ? 0 : (int64_t)__shfl(pv, src, 64) + 1, hi = __shfl(cur, src, 64);
+      const int64_t l0 = __shfl(lo, src, 64), h0 = __shfl(hi, src, 64);
       const uint32_t val = (uint32_t)(w0 + (int64_t)src * kBoundsPer + j);
-      for (int64_t b = lo + lane; b <= hi; b += 64) cell_start[b] = val;
+      for (int64_t b = l0 + lane; b <= h0; b += 64) cell_start[b] = val;
     }
   }
 }
@@ -408,10 +525,15 @@ hipError_t launch_radix(gf_ctx* ctx, int stage, const RadixArgs& a, int blocks) 
       else hipLaunchKernelGGL(radix_hist_kernel<false>, dim3(blocks), dim3(kRadixThreads), 0, s, a);
       break;
     case 1:
-      if (radix_threads() == 512)
-        hipLaunchKernelGGL(radix_scatter_kernel<512>, dim3(blocks), dim3(512), radix_scatter_lds_bytes(), s, a);
+      if (radix_threads() == 1024)
+        hipLaunchKernelGGL((radix_scatter_kernel<1024, 1>), dim3(blocks), dim3(1024), radix_scatter_lds_bytes(), s, a);
+      else if (radix_occ6())  // A/B: 80 VGPRs (6 waves per SIMD, 3 blocks per CU) with a small spill
+        hipLaunchKernelGGL((radix_scatter_kernel<512, 6>), dim3(blocks), dim3(512), radix_scatter_lds_bytes(), s, a);
       else
-        hipLaunchKernelGGL(radix_scatter_kernel<1024>, dim3(blocks), dim3(1024), radix_scatter_lds_bytes(), s, a);
+        hipLaunchKernelGGL((radix_scatter_kernel<512, 1>), dim3(blocks), dim3(512), radix_scatter_lds_bytes(), s, a);
+      break;
+    case 3:
+      hipLaunchKernelGGL(radix_seg_hist_kernel, dim3(blocks), dim3(kRadixThreads), 0, s, a);
       break;
     default: {  // cell_start[0 .. gn*gn + 1] of the sorted kout into a.M: one wave per 256 positions
       const int64_t waves = (a.n + 1 + 64 * kBoundsPer - 1) / (64 * kBoundsPer);

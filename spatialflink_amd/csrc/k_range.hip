@@ -315,7 +315,7 @@ __device__ __forceinline__ void waveq_round(const RangeArgs& a, const RangeLds& 
 // on C3); a tile's bitmap words are the two ballots bit-interleaved (lanes 0-31 -> word w, lanes
 // 32-63 -> word w + 1).  Otherwise lane l holds t + l and t + 64 + l and the ballots ARE the words.
 #ifndef GF_RANGE_VEC
-#define GF_RANGE_VEC 1
+#define GF_RANGE_VEC 0
 #endif
 constexpr bool kRangeVec = GF_RANGE_VEC != 0;
 __device__ __forceinline__ uint64_t spread32(uint32_t v) {  // bit i -> bit 2i

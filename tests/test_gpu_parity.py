@@ -89,6 +89,8 @@ def bucket_expected(oracle_mod, og, gn, x, y):
     (2048, 700_000, BEIJING, True),                         # 23-bit keys: 3 passes, hot spots
     (7, 5_000, BEIJING, True),                              # 1 pass
     (500, 1, BEIJING, False), (500, 63, BEIJING, False), (500, 4097, BEIJING, True),
+    # row mode (gn <= 511): the most rows, out-of-grid points; mostly empty rows
+    (511, 800_000, (115.3, 117.8, 39.5, 41.2), True), (300, 100, BEIJING, False),
 ])
 def test_bucket_by_cell_exact(sf, oracle_mod, gn, n, box, clustered):
     g = sf.UniformGrid(gn, *BEIJING)
@@ -101,6 +103,27 @@ def test_bucket_by_cell_exact(sf, oracle_mod, gn, n, box, clustered):
         h = rng.random(n) < 0.8
         x = np.where(h, cxs[c] + 0.01 * rng.standard_normal(n), x)
         y = np.where(h, cys[c] + 0.01 * rng.standard_normal(n), y)
+    perm, start = sf.bucket_by_cell(win(sf, x, y), g)
+    perm = perm.cpu().numpy().view(np.uint32).astype(np.int64)
+    start = start.cpu().numpy().view(np.uint32).astype(np.int64)
+    ep, es = bucket_expected(oracle_mod, og, gn, x, y)
+    np.testing.assert_array_equal(perm, ep)
+    np.testing.assert_array_equal(start, es)
+
+
+@pytest.mark.parametrize("gn", [500, 2048])
+def test_bucket_by_cell_one_row_nan(sf, oracle_mod, gn):
+    """One row holding most points (row mode: ~10 segments chained in one row's scan; the LSD
+    path at gn = 2048), NaN / inf coordinates (out-of-grid bucket), points on cell bounds."""
+    g = sf.UniformGrid(gn, *BEIJING)
+    og = oracle_mod.grid(gn, *BEIJING)
+    n = 350_000
+    x, y = oracle_mod.java_random_points(77, n, *BEIJING)
+    y = np.where(np.arange(n) % 7 != 0, 40.31, y)  # 6/7 of the points in one row
+    x[::1001] = np.nan
+    y[5::997] = np.inf
+    cl = (BEIJING[1] - BEIJING[0]) / gn
+    x[3::501] = BEIJING[0] + cl * (np.arange(3, n, 501) % gn)  # exactly on column bounds
     perm, start = sf.bucket_by_cell(win(sf, x, y), g)
     perm = perm.cpu().numpy().view(np.uint32).astype(np.int64)
     start = start.cpu().numpy().view(np.uint32).astype(np.int64)
