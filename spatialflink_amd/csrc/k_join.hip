@@ -1255,6 +1255,10 @@ constexpr int kBandBuf = GF_BAND_BUF;        // pairs per wave buffer (written o
 #define GF_BAND_R 4
 #endif
 constexpr int kBandRound = GF_BAND_R;  // candidates per lane per walk round
+#ifndef GF_BAND_PAIR
+#define GF_BAND_PAIR 1
+#endif
+constexpr bool kBandPair = GF_BAND_PAIR != 0;  // sparse whole-band windows: a lane's two points in one walk
 constexpr int kBandMaxSub = 6;       // staged sub-rows f + 2 (f <= 4)
 constexpr uint32_t kBandGlobal = 0x80000000u;  // buffer entry: a global sorted query index
 struct BandHdr {
@@ -1654,6 +1658,72 @@ __global__ __launch_bounds__(kBandThreads) void join_band_probe_kernel(JoinRowAr
           }
         }
       };
+      // TWO points per lane walked as one sequence of six runs (sparse whole-band windows): the
+      // rounds of a wave are set by its longest lane, and the sum of two points' candidate counts
+      // varies less than one point's, so fewer slots idle (~3.2 candidates per point at C4)
+      auto probe2 = [&](double pxa, double pya, uint32_t ia, bool va, double pxb, double pyb, uint32_t ib,
+                        bool vb) {
+        uint32_t b[6], e[6];
+        auto runs = [&](double px, double py, bool valid, uint32_t (&bb)[3], uint32_t (&ee)[3]) {
+          const int32_t cx = cell_index(px, a.u_minX, a.u_cl);
+          bool in = valid && cx >= 0 && cx < qn;
+          const int32_t col = in ? f * (cx + 1) + join_sub(px, a.u_minX, a.u_cl, cx, a.fs, f) : 0;
+          const int32_t sub = join_sub(py, a.u_minY, a.u_cl, cy, a.fs, f);
+          in = in && (uint32_t)col >= c0 && (uint32_t)col < c1;
+          const uint16_t* lo = lo16 + (in ? sub * ncol + (col - (int32_t)c0) : 0);
+#pragma unroll
+          for (int k = 0; k < 3; ++k) {
+            bb[k] = in ? lo[k * ncol] : 0u;
+            ee[k] = in ? lo[k * ncol + 3] : 0u;
+          }
+        };
+        {
+          uint32_t b0[3], e0[3], b1[3], e1[3];
+          runs(pxa, pya, va, b0, e0);
+          runs(pxb, pyb, vb, b1, e1);
+#pragma unroll
+          for (int k = 0; k < 3; ++k) {
+            b[k] = b0[k]; e[k] = e0[k];
+            b[k + 3] = b1[k]; e[k + 3] = e1[k];
+          }
+        }
+        uint32_t L[6], dd[6], acc = 0;
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+          dd[k] = b[k] - acc;  // slot kk of run k is kk + dd[k] (mod 2^32)
+          acc += e[k] - b[k];
+          L[k] = acc;
+        }
+        const uint32_t LA = L[2], LT = L[5];
+        for (uint32_t k = 0; __ballot(k < LT) != 0; k += kBandRound) {
+          if (cnt > (uint32_t)(kBandBuf - 64 * kBandRound)) flush();
+          uint32_t t[kBandRound];
+          double2 v[kBandRound];
+#pragma unroll
+          for (int i = 0; i < kBandRound; ++i) {
+            const uint32_t kk = k + i;
+            const uint32_t d = kk < L[0] ? dd[0] : kk < L[1] ? dd[1] : kk < L[2] ? dd[2]
+                             : kk < L[3] ? dd[3] : kk < L[4] ? dd[4] : dd[5];
+            t[i] = kk < LT ? kk + d : 0u;
+          }
+#pragma unroll
+          for (int i = 0; i < kBandRound; ++i) v[i] = lxy[t[i]];  // a finished lane reads slot 0
+#pragma unroll
+          for (int i = 0; i < kBandRound; ++i) {
+            const bool second = k + i >= LA;
+            const double dx = (second ? pxb : pxa) - v[i].x, dy = (second ? pyb : pya) - v[i].y;
+            bool ok;
+            if constexpr (MODE == 0) ok = dx * dx + dy * dy <= a.s_r;
+            else ok = a.metric == 0 ? dx * dx + dy * dy <= a.s_r : fdlibm_hypot(dx, dy) <= a.r;
+            const bool hit = k + i < LT && ok;
+            const uint64_t hm = __ballot(hit);
+            if (hit)
+              buf[cnt + __builtin_amdgcn_mbcnt_hi((uint32_t)(hm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)hm, 0u))] =
+                  make_uint2(second ? ib : ia, t[i]);
+            cnt += (uint32_t)__popcll(hm);
+          }
+        }
+      };
       // the segment, 128 consecutive points per wave-step (two per lane); past the end a lane
       // re-reads the segment's first point (always present) and is masked
       struct Pt {
@@ -1674,8 +1744,13 @@ __global__ __launch_bounds__(kBandThreads) void join_band_probe_kernel(JoinRowAr
         Pt cur = fetch(sb + wid * 128);
         for (uint32_t s0 = sb + wid * 128; s0 < se; s0 += kBandWaves * 128) {  // wave-uniform
           const Pt nxt = fetch(s0 + kBandWaves * 128);
-          probe(cur.v[0].x, cur.v[0].y, cur.idx[0], s0 + lane < se);
-          probe(cur.v[1].x, cur.v[1].y, cur.idx[1], s0 + 64 + lane < se);
+          if (kBandPair && !dense) {  // wave-uniform
+            probe2(cur.v[0].x, cur.v[0].y, cur.idx[0], s0 + lane < se, cur.v[1].x, cur.v[1].y, cur.idx[1],
+                   s0 + 64 + lane < se);
+          } else {
+            probe(cur.v[0].x, cur.v[0].y, cur.idx[0], s0 + lane < se);
+            probe(cur.v[1].x, cur.v[1].y, cur.idx[1], s0 + 64 + lane < se);
+          }
           __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): nxt is in registers (before any store)
           if (cnt > (uint32_t)(kBandBuf - 64 * kBandRound)) flush();
           cur = nxt;

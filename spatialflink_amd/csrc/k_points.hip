@@ -150,6 +150,9 @@ hipError_t launch_pane_bounds(hipStream_t s, const int64_t* ts, int64_t n, int64
 // index) -- pass 0's index is the position itself.
 // Afterwards: bucket sizes from the sorted keys' run boundaries -> exclusive scan = cell_start.
 // ---------------------------------------------------------------------------------------
+#ifndef GF_RADIX_EXP
+#define GF_RADIX_EXP 0  // experiment builds only (tools/build_exp.sh): 1 no stores, 2 fake ranks, 3 no LDS permutation (scatter); 4 no histogram atomics, 5 no key stores (pass-0 histogram)
+#endif
 __device__ __forceinline__ uint32_t bucket_key(double x, double y, const RadixArgs& a) {
   const int32_t cx = cell_index(x, a.minX, a.cl), cy = cell_index(y, a.minY, a.cl);
   const bool valid = cx >= 0 && cy >= 0 && cx < a.gn && cy < a.gn;
@@ -296,6 +299,22 @@ __global__ __launch_bounds__(kRadixThreads) void radix_hist_kernel(RadixArgs a) 
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int64_t i = i0 + (int64_t)u * kRadixThreads * 2;
+#if GF_RADIX_EXP == 4  // experiment build: no LDS histogram atomics (keys still stored)
+        if (i + 1 < end) {
+          *reinterpret_cast<uint2*>(a.kout + i) = make_uint2(k0[u], k1[u]);
+        } else if (i < end) {
+          a.kout[i] = k0[u];
+        }
+        continue;
+#elif GF_RADIX_EXP == 5  // experiment build: no key stores (histogram only)
+        if (i + 1 < end) {
+          atomicAdd(&h[(k0[u] >> a.shift) & mask], 1u);
+          atomicAdd(&h[(k1[u] >> a.shift) & mask], 1u);
+        } else if (i < end) {
+          atomicAdd(&h[(k0[u] >> a.shift) & mask], 1u);
+        }
+        continue;
+#endif
         if (i + 1 < end) {
           atomicAdd(&h[(k0[u] >> a.shift) & mask], 1u);
           atomicAdd(&h[(k1[u] >> a.shift) & mask], 1u);
@@ -330,13 +349,6 @@ int radix_threads() {
     return e && std::atoi(e) == 1024 ? 1024 : 512;  // r04 A/B on K2: 512 (3 blocks per CU) 68 vs 77 us per pass
   }();
   return nt;
-}
-static bool radix_occ6() {
-  static const bool on = [] {
-    const char* e = std::getenv("GF_RADIX_OCC6");
-    return e && std::atoi(e) != 0;
-  }();
-  return on;
 }
 size_t radix_scatter_lds_bytes() {
   return (size_t)radix_tile() * 8 + (size_t)(radix_threads() / 64) * kRadixMaxDigits * 4 +
@@ -379,17 +391,23 @@ __global__ __launch_bounds__(NT, MINW) void radix_scatter_kernel(RadixArgs a) {
     radix_chunk(a, beg, end);
     for (uint32_t d = threadIdx.x; d < D; d += NT) gc[d] = a.Ms[(size_t)d * a.nblk + blockIdx.x];
   }
-  // (r04: prefetching the next tile into registers pushed the kernel to 128 VGPRs + 80 B of
-  // scratch per lane and cost 76 -> 88 us per pass; the tile is loaded at the top of its step)
-  for (int64_t t0 = beg; t0 < end; t0 += kTile) {  // block-uniform
-    const uint32_t cnt = (uint32_t)(end - t0 < kTile ? end - t0 : kTile);
-    uint32_t k[U], v[U], r[U];
+  // The next tile's keys / values are loaded into the same registers as soon as this tile sits in
+  // LDS (after its placement), so their latency overlaps the write-out and the barriers.  (r04: a
+  // prefetch into SEPARATE registers at the top pushed the 1024-thread kernel to 128 VGPRs + 80 B
+  // of scratch per lane and cost 76 -> 88 us per pass.)
+  uint32_t k[U], v[U], r[U];
+  auto load_tile = [&](int64_t t) {
+    const uint32_t c = (uint32_t)(end - t < kTile ? end - t : kTile);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const uint32_t e = w * EPW + u * 64 + lane;
-      k[u] = e < cnt ? a.kin[t0 + e] : 0u;
-      v[u] = e < cnt ? (a.vin ? a.vin[t0 + e] : (uint32_t)(t0 + e)) : 0u;
+      k[u] = e < c ? a.kin[t + e] : 0u;
+      v[u] = e < c ? (a.vin ? a.vin[t + e] : (uint32_t)(t + e)) : 0u;
     }
+  };
+  if (beg < end) load_tile(beg);
+  for (int64_t t0 = beg; t0 < end; t0 += kTile) {  // block-uniform
+    const uint32_t cnt = (uint32_t)(end - t0 < kTile ? end - t0 : kTile);
     for (uint32_t d = lane; d < D; d += 64) wc[w * kRadixMaxDigits + d] = 0u;  // this wave's row
 #pragma unroll
     for (int u = 0; u < U; ++u) {  // stable ranks within the wave
@@ -401,6 +419,11 @@ __global__ __launch_bounds__(NT, MINW) void radix_scatter_kernel(RadixArgs a) {
         const uint64_t bal = __ballot((d >> b) & 1u);
         peers &= ((d >> b) & 1u) ? bal : ~bal;
       }
+#if GF_RADIX_EXP == 2  // experiment build: counts only, fake ranks (output wrong, accesses in bounds)
+      if (valid) atomicAdd(&wc[w * kRadixMaxDigits + d], 1u);
+      r[u] = (uint32_t)(u * 64 + lane) + (uint32_t)(peers & 1u);
+      continue;
+#endif
       uint32_t base = 0;
       if (valid && (peers & below) == 0) base = atomicAdd(&wc[w * kRadixMaxDigits + d], (uint32_t)__popcll(peers));
       const int leader = valid ? __ffsll((unsigned long long)peers) - 1 : lane;
@@ -444,15 +467,31 @@ __global__ __launch_bounds__(NT, MINW) void radix_scatter_kernel(RadixArgs a) {
     for (int u = 0; u < U; ++u) {  // the tile in (digit, input) order
       const uint32_t e = w * EPW + u * 64 + lane;
       if (e < cnt) {
+#if GF_RADIX_EXP == 3  // experiment build: no permutation in LDS
+        const uint32_t p = e + (wc[w * kRadixMaxDigits + ((k[u] >> a.shift) & mask)] + r[u] == 0xFFFFFFFFu ? 1u : 0u);
+#elif GF_RADIX_EXP == 2
+        const uint32_t p = (wc[w * kRadixMaxDigits + ((k[u] >> a.shift) & mask)] + r[u]) & (uint32_t)(kTile - 1);
+#else
         const uint32_t p = wc[w * kRadixMaxDigits + ((k[u] >> a.shift) & mask)] + r[u];
+#endif
         lk[p] = k[u];
         lv[p] = v[u];
       }
     }
     lds_barrier();
-    for (uint32_t p = threadIdx.x; p < cnt; p += NT) {  // runs of one digit: consecutive slots
+    if (t0 + kTile < end) load_tile(t0 + kTile);  // block-uniform: in flight during the write-out
+#pragma unroll
+    for (int q = 0; q < kTile / NT; ++q) {  // runs of one digit: consecutive slots
+      const uint32_t p = threadIdx.x + q * NT;
+      if (p >= cnt) break;
       const uint32_t kk = lk[p], d = (kk >> a.shift) & mask;
       const uint32_t o = gc[d] + (p - tb[d]);
+#if GF_RADIX_EXP == 1  // experiment build: no global stores
+      if (o == 0xFFFFFFFFu) a.vout[0] = kk ^ lv[p];
+      continue;
+#elif GF_RADIX_EXP >= 2
+      if (o >= (uint32_t)a.n) continue;
+#endif
       if (a.kout) a.kout[o] = kk;  // (pass B of row mode keeps only the permutation)
       a.vout[o] = lv[p];
     }
@@ -527,8 +566,6 @@ hipError_t launch_radix(gf_ctx* ctx, int stage, const RadixArgs& a, int blocks) 
     case 1:
       if (radix_threads() == 1024)
         hipLaunchKernelGGL((radix_scatter_kernel<1024, 1>), dim3(blocks), dim3(1024), radix_scatter_lds_bytes(), s, a);
-      else if (radix_occ6())  // A/B: 80 VGPRs (6 waves per SIMD, 3 blocks per CU) with a small spill
-        hipLaunchKernelGGL((radix_scatter_kernel<512, 6>), dim3(blocks), dim3(512), radix_scatter_lds_bytes(), s, a);
       else
         hipLaunchKernelGGL((radix_scatter_kernel<512, 1>), dim3(blocks), dim3(512), radix_scatter_lds_bytes(), s, a);
       break;
