@@ -244,9 +244,9 @@ __global__ __launch_bounds__(kRadixThreads) void radix_seg_hist_kernel(RadixArgs
   for (int64_t i0 = rs.beg + threadIdx.x; i0 < rs.end; i0 += (int64_t)kRadixThreads * U) {
     uint32_t k[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
+    for (int u = 0; u < U; ++u) {  // clamped addresses (i0 < end): the U loads fly together
       const int64_t i = i0 + (int64_t)u * kRadixThreads;
-      k[u] = i < rs.end ? a.kin[i] : 0u;
+      k[u] = a.kin[i < rs.end ? i : rs.end - 1];
     }
 #pragma unroll
     for (int u = 0; u < U; ++u)
@@ -280,59 +280,48 @@ __global__ __launch_bounds__(kRadixThreads) void radix_hist_kernel(RadixArgs a) 
     // pass 0: two points per lane (16-B loads of x and y; chunks start at whole tiles, so pairs
     // are 16-B aligned), keys stored as uint2
     constexpr int U = 4;  // pairs in flight together
-    for (int64_t i0 = beg + 2 * (int64_t)threadIdx.x; i0 < end; i0 += (int64_t)kRadixThreads * 2 * U) {
-      uint32_t k0[U], k1[U];
+    // Full steps first: every lane's U pairs exist, so the loads are unconditional and all in
+    // flight together (a load under a per-pair branch was waited on inside its branch: the U
+    // round trips ran one after another); the chunk's remainder goes point by point.
+    constexpr int64_t kStep = (int64_t)kRadixThreads * 2 * U;
+    const int64_t full = beg + (end - beg) / kStep * kStep;  // block-uniform
+    typedef double v2d __attribute__((ext_vector_type(2)));
+    for (int64_t i0 = beg + 2 * (int64_t)threadIdx.x; i0 < full; i0 += kStep) {
+      v2d xv[U], yv[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int64_t i = i0 + (int64_t)u * kRadixThreads * 2;
-        if (i + 1 < end) {
-          typedef double v2d __attribute__((ext_vector_type(2)));
-          const v2d xv = __builtin_nontemporal_load(reinterpret_cast<const v2d*>(a.x + i));
-          const v2d yv = __builtin_nontemporal_load(reinterpret_cast<const v2d*>(a.y + i));
-          k0[u] = pass0_key(xv.x, yv.x, a);
-          k1[u] = pass0_key(xv.y, yv.y, a);
-        } else {
-          k0[u] = i < end ? pass0_key(a.x[i], a.y[i], a) : 0u;
-          k1[u] = 0u;
-        }
+        xv[u] = __builtin_nontemporal_load(reinterpret_cast<const v2d*>(a.x + i));
+        yv[u] = __builtin_nontemporal_load(reinterpret_cast<const v2d*>(a.y + i));
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int64_t i = i0 + (int64_t)u * kRadixThreads * 2;
-#if GF_RADIX_EXP == 4  // experiment build: no LDS histogram atomics (keys still stored)
-        if (i + 1 < end) {
-          *reinterpret_cast<uint2*>(a.kout + i) = make_uint2(k0[u], k1[u]);
-        } else if (i < end) {
-          a.kout[i] = k0[u];
-        }
-        continue;
-#elif GF_RADIX_EXP == 5  // experiment build: no key stores (histogram only)
-        if (i + 1 < end) {
-          atomicAdd(&h[(k0[u] >> a.shift) & mask], 1u);
-          atomicAdd(&h[(k1[u] >> a.shift) & mask], 1u);
-        } else if (i < end) {
-          atomicAdd(&h[(k0[u] >> a.shift) & mask], 1u);
-        }
-        continue;
+        const uint32_t k0 = pass0_key(xv[u].x, yv[u].x, a), k1 = pass0_key(xv[u].y, yv[u].y, a);
+#if GF_RADIX_EXP != 4  // experiment build 4: no LDS histogram atomics
+        atomicAdd(&h[(k0 >> a.shift) & mask], 1u);
+        atomicAdd(&h[(k1 >> a.shift) & mask], 1u);
 #endif
-        if (i + 1 < end) {
-          atomicAdd(&h[(k0[u] >> a.shift) & mask], 1u);
-          atomicAdd(&h[(k1[u] >> a.shift) & mask], 1u);
-          *reinterpret_cast<uint2*>(a.kout + i) = make_uint2(k0[u], k1[u]);  // pass 0's scatter reads the keys
-        } else if (i < end) {
-          atomicAdd(&h[(k0[u] >> a.shift) & mask], 1u);
-          a.kout[i] = k0[u];
-        }
+#if GF_RADIX_EXP != 5  // experiment build 5: no key stores
+        *reinterpret_cast<uint2*>(a.kout + i) = make_uint2(k0, k1);  // pass 0's scatter reads the keys
+#endif
       }
+    }
+    // (r04: software-pipelining the steps -- the next step's loads before this step's keys, two
+    // pairs per step to keep two blocks per CU -- measured 41.9 vs 40.9 us: no gain)
+    for (int64_t i = full + threadIdx.x; i < end; i += kRadixThreads) {
+      const uint32_t k0 = pass0_key(a.x[i], a.y[i], a);
+      atomicAdd(&h[(k0 >> a.shift) & mask], 1u);
+      a.kout[i] = k0;
     }
   } else {
     constexpr int U = 8;  // loads in flight together
     for (int64_t i0 = beg + threadIdx.x; i0 < end; i0 += (int64_t)kRadixThreads * U) {
       uint32_t k[U];
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
+      for (int u = 0; u < U; ++u) {  // clamped (always valid) addresses: the U loads fly together
         const int64_t i = i0 + (int64_t)u * kRadixThreads;
-        k[u] = i < end ? a.kin[i] : 0u;
+        k[u] = a.kin[i < end ? i : end - 1];
       }
 #pragma unroll
       for (int u = 0; u < U; ++u)
@@ -396,13 +385,23 @@ __global__ __launch_bounds__(NT, MINW) void radix_scatter_kernel(RadixArgs a) {
   // prefetch into SEPARATE registers at the top pushed the 1024-thread kernel to 128 VGPRs + 80 B
   // of scratch per lane and cost 76 -> 88 us per pass.)
   uint32_t k[U], v[U], r[U];
+  // (clamped addresses, masked after: a load under a per-element branch is waited on inside it,
+  // which ran the U loads one round trip after another)
   auto load_tile = [&](int64_t t) {
     const uint32_t c = (uint32_t)(end - t < kTile ? end - t : kTile);
+    int64_t idx[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const uint32_t e = w * EPW + u * 64 + lane;
-      k[u] = e < c ? a.kin[t + e] : 0u;
-      v[u] = e < c ? (a.vin ? a.vin[t + e] : (uint32_t)(t + e)) : 0u;
+      idx[u] = t + (e < c ? e : c - 1);
+      k[u] = a.kin[idx[u]];
+    }
+    if (a.vin) {  // kernel-uniform
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u] = a.vin[idx[u]];
+    } else {
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u] = (uint32_t)(t + w * EPW + u * 64 + lane);
     }
   };
   if (beg < end) load_tile(beg);
