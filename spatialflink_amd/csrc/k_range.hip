@@ -314,6 +314,9 @@ __device__ __forceinline__ void waveq_round(const RangeArgs& a, const RangeLds& 
 // per outstanding load -- the scan was latency-bound with 8-B loads: SQ_WAIT_ANY 0.62, VALU 0.25
 // on C3); a tile's bitmap words are the two ballots bit-interleaved (lanes 0-31 -> word w, lanes
 // 32-63 -> word w + 1).  Otherwise lane l holds t + l and t + 64 + l and the ballots ARE the words.
+#ifndef GF_RANGE_EXP
+#define GF_RANGE_EXP 0  // experiment builds only (tools/build_exp.sh): 1 no span-queue rounds, 2 nothing queued
+#endif
 #ifndef GF_RANGE_VEC
 #define GF_RANGE_VEC 0
 #endif
@@ -373,6 +376,9 @@ __device__ __forceinline__ void range_tile(const RangeArgs& a, int64_t t, double
     mult += (uint64_t)(__popcll(e0) + __popcll(e1));
   }
   if (DEFER == 3) {  // into the wave's buffer; classify whenever 64 are collected
+#if GF_RANGE_EXP == 2  // experiment build: nothing queued (the stream and the ring only)
+    d0 = d1 = false;
+#endif
     const uint64_t q0 = __ballot(d0), q1 = __ballot(d1);
     const uint32_t n0 = (uint32_t)__popcll(q0);
     const uint64_t below = (1ull << lane) - 1ull;
@@ -387,6 +393,10 @@ __device__ __forceinline__ void range_tile(const RangeArgs& a, int64_t t, double
         wq.xy[pos] = h ? make_double2(x1, y1) : make_double2(x0, y0);
       }
       wq.cnt += (uint32_t)__popcll(qm);
+#if GF_RANGE_EXP == 1  // experiment build: queued points dropped (no classification rounds)
+      if (wq.cnt >= 64) wq.cnt -= 64;
+      continue;
+#endif
       if (wq.cnt >= 64) waveq_round<POLY>(a, L, wq, 64u, hits, lcount);  // leaves < 64
     }
   } else if (DEFER) {
