@@ -1247,6 +1247,7 @@ hipError_t launch_join_stream(gf_ctx* ctx, const JoinRowArgs& a) {
 // chunks cost one device atomic each on ONE counter: ~20K of them serialised at the memory side
 // (the row probe: 240 us with block chunks, 361 us with wave chunks).
 constexpr int kBandThreads = 1024, kBandWaves = kBandThreads / 64;
+typedef const uint32_t __attribute__((address_space(3)))* lds_u32;
 #ifndef GF_BAND_BUF
 #define GF_BAND_BUF 512
 #endif
@@ -1553,7 +1554,10 @@ __global__ __launch_bounds__(kBandThreads) void join_band_probe_kernel(JoinRowAr
       auto flush = [&]() {
         band_emit(a.out, hd, cnt, [&](uint32_t i) {
           const uint2 v = buf[i];
-          return make_uint2(v.x, v.y & kBandGlobal ? a.sqidx[v.y & ~kBandGlobal] : lq[v.y]);
+          // (the staged read through an address_space(3) pointer: one generic pointer for both
+          // sources compiled to a FLAT load, whose wait drained the prefetched points at every flush)
+          const uint32_t q = v.y & kBandGlobal ? a.sqidx[v.y & ~kBandGlobal] : ((lds_u32)lq)[v.y];
+          return make_uint2(v.x, q);
         });
         cnt = 0;
       };

@@ -83,9 +83,14 @@ __device__ __forceinline__ int32_t cell_slot(const RangeArgs& a, const RangeLds&
   if (cx < lo || cx > (int32_t)(span >> 16)) return -2;
   return L.spans ? (int32_t)L.rowoff[cy] + (cx - lo) : cy * n + cx;
 }
+// (the LDS read goes through an address_space(3) pointer: with one generic pointer for both
+// sources the compiler merged the two loads into a FLAT load, whose wait also drains every
+// outstanding global load -- the stream's prefetched tiles)
+typedef const uint8_t __attribute__((address_space(3)))* lds_u8;
 __device__ __forceinline__ int table_load(const RangeArgs& a, const RangeLds& L, int32_t slot) {
-  if (L.spans) return L.spans[slot < 0 ? 0 : slot];
-  return a.table[slot < 0 ? 0 : slot];
+  const int32_t s = slot < 0 ? 0 : slot;
+  if (L.spans) return ((lds_u8)L.spans)[s];
+  return a.table[s];
 }
 template <int TABLE>
 __device__ __forceinline__ int classify_finish(const RangeArgs& a, double px, double py, int32_t slot, int tv) {
@@ -671,7 +676,12 @@ __device__ __forceinline__ void range_body(const RangeArgs& a) {
         tail += (a.span_bytes + 3) & ~3;
       }
       if (DEFER == 3) {  // the waves' buffers (16-B aligned)
-        char* wb = reinterpret_cast<char*>(((uintptr_t)tail + 15) & ~(uintptr_t)15);
+        // aligned by OFFSET from the LDS base: an integer round trip ((uintptr_t)tail + 15 & ~15)
+        // loses the address space, and the queue / ring accesses then compile to FLAT
+        // instructions, whose s_waitcnt vmcnt(0) lgkmcnt(0) drained the stream's prefetched tiles
+        // at every ring store
+        char* const lb = reinterpret_cast<char*>(lds_base);
+        char* wb = lb + (((size_t)(tail - lb) + 15) & ~(size_t)15);
         const int w = threadIdx.x >> 6;
         wq.xy = reinterpret_cast<double2*>(wb) + w * kWaveQ;
         wq.idx = reinterpret_cast<uint32_t*>(reinterpret_cast<double2*>(wb) + (kBlock / 64) * kWaveQ) + w * kWaveQ;
