@@ -1,7 +1,7 @@
-"""The committed round-3 evidence is self-consistent: tools/roofline_table.py recomputes every
-workload line's roofline fraction from profiles/r03_workloads.jsonl (bytes per launch over the
+"""The committed per-round evidence (rounds 3 and 4) is self-consistent: tools/roofline_table.py recomputes every
+workload line's roofline fraction from profiles/rNN_workloads.jsonl (bytes per launch over the
 line's own time basis) and its HBM traffic ratio from the committed rocprofv3 PMC summaries
-(profiles/r03_<tag>_pmc.json).  CPU only: reads committed files."""
+(profiles/rNN_<tag>_pmc.json).  CPU only: reads committed files."""
 import json
 import os
 import subprocess
@@ -12,11 +12,12 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-@pytest.mark.skipif(not os.path.exists(os.path.join(ROOT, "profiles", "r03_workloads.jsonl")),
-                    reason="no r03 workload lines")
-def test_r03_roofline_table_reproduces_lines(tmp_path):
+@pytest.mark.parametrize("rnd", ["r03", "r04"])
+def test_roofline_table_reproduces_lines(tmp_path, rnd):
+    if not os.path.exists(os.path.join(ROOT, "profiles", f"{rnd}_workloads.jsonl")):
+        pytest.skip(f"no {rnd} workload lines")
     out = tmp_path / "roof"
-    subprocess.run([sys.executable, os.path.join(ROOT, "tools", "roofline_table.py"), "r03", "--out", str(out)],
+    subprocess.run([sys.executable, os.path.join(ROOT, "tools", "roofline_table.py"), rnd, "--out", str(out)],
                    check=True, capture_output=True, timeout=120)
     rows = json.load(open(str(out) + ".json"))
     assert len(rows) >= 13
