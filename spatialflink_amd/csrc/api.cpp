@@ -1124,7 +1124,9 @@ extern "C" int gf_range_run(gf_range_plan* P, const gf_points* pts, uint64_t* bi
   const bool defer = can_defer && (P->defer_mode >= 2 || (P->defer_mode == 0 && P->cls_cells[1] * 20 > live));
   // span prefilter when the class spans cover at most a quarter of the grid (defer_mode 3
   // forces it): the stream skips the table, the block's queued points are classified after it
-  const bool span = defer && P->xt && (P->defer_mode == 3 || (P->defer_mode != 2 && P->span_frac <= 0.25));
+  // (the span prefilter's classification rounds read the span table from LDS only: it must fit)
+  const bool span = defer && P->xt && P->span_bytes <= kSpanLdsBytes &&
+                    (P->defer_mode == 3 || (P->defer_mode != 2 && P->span_frac <= 0.25));
   const int blocks = scan_blocks_range(P, pts->n, span);
   if (defer) {
     if ((st = ensure_queue(P, a, blocks, false))) return st;

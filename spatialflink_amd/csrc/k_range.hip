@@ -282,7 +282,11 @@ __device__ __forceinline__ void waveq_round(const RangeArgs& a, const RangeLds& 
   const uint32_t i = q.idx[valid ? lane : 0u];
   const double2 v = q.xy[valid ? lane : 0u];
   const int32_t slot = cell_slot<1>(a, L, v.x, v.y);
-  const int cls = valid ? classify_finish<1>(a, v.x, v.y, slot, table_load(a, L, slot)) : kNone;
+  // the span table is in LDS whenever the span prefilter runs (host: span_lds): with a global
+  // fallback here the two reads merge into one wait on vmcnt too, draining the stream's
+  // prefetched tiles at every round
+  const int tv = ((lds_u8)L.spans)[slot < 0 ? 0 : slot];
+  const int cls = valid ? classify_finish<1>(a, v.x, v.y, slot, tv) : kNone;
   const bool acc = cls == kAccept;
   if (acc) {
     const uint32_t k = (i - q.t0) / q.tstride;  // the point's tile of this wave
