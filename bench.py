@@ -285,17 +285,32 @@ def main():
     enqueue = L.gf_knn_enqueue
 
     pending = [0]  # first window whose record has not been exchanged yet
+    # Numeric objIDs: a group's exchange (RCCL all-gather + merge) runs on a SIDE stream with a
+    # context of its own, so the next group's windows keep streaming while it is in flight (the
+    # slots are double-buffered); the first window of group g + 2 waits for group g's exchange
+    # (done long before: a group is B windows of work).  String records stay on the plan's stream.
+    side = torch.cuda.Stream(dev) if (world > 1 and hstr is None) else None
+    xctx = None
+    if side is not None:
+        xctx = _lib.Context(dev.index)
+        xctx.set_stream(side.cuda_stream)
+    slot_free = [None, None]  # per slot parity: event after the exchange that last read it
 
     def exchange(first, lo, hi):  # windows [lo, hi] of one group: one all-gather + one merge launch
         g = (lo - first) // B
         if hstr is not None:  # String objIDs: the records travel with their Strings, merged by String
             sharding.allgather_knn_records_strings(slots[g % 2, : hi - lo + 1], args.k, scap, sdict, hstr.ptr(lo))
+            if args.pipeline >= 3:
+                # depth >= 3 writes windows' records on the plan's other streams: they must not
+                # reuse slots[g % 2] (group g + 2) before this all-gather + merge have read them
+                _lib.check(L.gf_ctx_fork(ctx.handle), ctx.handle, "gf_ctx_fork")
         else:
-            sharding.allgather_knn_records_batch(slots[g % 2, : hi - lo + 1], args.k, host.ptr(lo))
-        if args.pipeline >= 3:
-            # depth >= 3 writes windows' records on the plan's other streams: they must not
-            # reuse slots[g % 2] (group g + 2) before this all-gather + merge have read them
-            _lib.check(L.gf_ctx_fork(ctx.handle), ctx.handle, "gf_ctx_fork")
+            side.wait_stream(torch.cuda.current_stream(dev))  # the group's records are complete
+            with torch.cuda.stream(side):
+                sharding.allgather_knn_records_batch(slots[g % 2, : hi - lo + 1], args.k, host.ptr(lo), ctx=xctx)
+                ev = torch.cuda.Event()
+                ev.record(side)
+            slot_free[g % 2] = ev
         pending[0] = hi + 1
 
     def step(i, first):
@@ -307,6 +322,11 @@ def main():
             if i == first:
                 pending[0] = first
             g, w_ = divmod(i - first, B)
+            if w_ == 0 and slot_free[g % 2] is not None:  # group g - 2's exchange has read these slots
+                torch.cuda.current_stream(dev).wait_event(slot_free[g % 2])
+                slot_free[g % 2] = None
+                if args.pipeline >= 3:  # the plan's other streams write records too
+                    _lib.check(L.gf_ctx_fork(ctx.handle), ctx.handle, "gf_ctx_fork")
             _lib.check(enqueue(plan, pts_ref[i % args.windows], slots[g % 2, w_].data_ptr()), ctx.handle, "enqueue")
             c = i - lag  # this window's record is complete now
             if c >= first and (c - first) % B == B - 1:

@@ -228,7 +228,7 @@ def encode_knn_record(k: int, objID, dist, idx, status: int = 0, candidates: int
     return bytes(h) + d.tobytes() + o.tobytes() + i.tobytes()
 
 
-def allgather_knn_records_batch(records, k: int, results, group=None):
+def allgather_knn_records_batch(records, k: int, results, group=None, ctx=None):
     """One RCCL all-gather for several windows: `records` is this rank's [nwin, rb] uint8
     device tensor (consecutive windows); every rank merges all windows in one launch
     (gf_knn_merge_dev_batch, shard-major) into `results` -- nwin consecutive records (device
@@ -246,13 +246,19 @@ def allgather_knn_records_batch(records, k: int, results, group=None):
     Before this call, gf_ctx_join (the context stream waits for the second stream) so the
     records are complete; after it, gf_ctx_fork (the second stream waits for the context
     stream) before `records` is handed to later enqueues, so no later window overwrites them
-    while the all-gather still reads them."""
+    while the all-gather still reads them.
+
+    ctx: the context whose stream runs the merge (default: the thread's context, bound to
+    torch's current stream).  An exchange overlapped with the next windows runs under
+    `torch.cuda.stream(side)` with a context of its own bound to that side stream -- the thread's
+    cached context (the plan's) must not be rebound to it."""
     import torch.distributed as dist_
 
     world = dist_.get_world_size(group)
     nwin = records.shape[0]
     gathered = gather_records_batch(records, group)
-    ctx = _lib.context(records.device.index)
+    if ctx is None:
+        ctx = _lib.context(records.device.index)
     out = results if isinstance(results, int) else results.data_ptr()
     _lib.check(_lib.lib().gf_knn_merge_dev_batch(ctx.handle, int(k), gathered.data_ptr(), world, int(nwin),
                                                  _merge_layout(world), out),

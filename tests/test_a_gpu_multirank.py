@@ -48,7 +48,7 @@ def _run_two_ranks(extra):
 
 
 @pytest.mark.timeout(900)
-@pytest.mark.parametrize("pipeline", [3, 2])
+@pytest.mark.parametrize("pipeline", [3, 2, 4])
 def test_knn_two_ranks_verified(pipeline):
     line = _run_two_ranks(["--points", "400000", "--steps", "9", "--warmup", "3", "--windows", "4",
                            "--exchange-batch", "2", "--pipeline", str(pipeline)])
