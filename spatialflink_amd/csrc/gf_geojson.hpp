@@ -646,10 +646,10 @@ GF_DHD inline uint8_t jtok_trans(int t, int b) {
 
 // LDS tables of a block: per byte value the 9 syntax states' entries and the 16 token states'
 // next states; the looked-up member names
-struct GeoTabs {
-  const uint64_t* tab;   // [256]: entry of state s at bits 7s..7s+6
-  const uint64_t* ttab;  // [256]: next token state of state t at bits 4t..4t+3
-  const char* keys;      // kGeoKeys x kGeoPropMax
+struct GeoTabs {  // (in LDS on the device)
+  GF_LDS_PTR(uint64_t) tab;   // [256]: entry of state s at bits 7s..7s+6
+  GF_LDS_PTR(uint64_t) ttab;  // [256]: next token state of state t at bits 4t..4t+3
+  GF_LDS_PTR(char) keys;      // kGeoKeys x kGeoPropMax
   int32_t klen[kGeoKeys];
 };
 

@@ -14,6 +14,15 @@
 #define GF_NOINLINE __attribute__((noinline))
 #endif
 
+// A pointer into LDS.  In the device pass it carries address space 3, so the parsers' byte and
+// table reads compile to ds_read (a generic pointer makes them FLAT instructions, whose waits
+// cover every memory counter); the host test builds (tests/native/) see a plain pointer.
+#if defined(__HIP_DEVICE_COMPILE__)
+#define GF_LDS_PTR(T) const __attribute__((address_space(3))) T*
+#else
+#define GF_LDS_PTR(T) const T*
+#endif
+
 namespace gf {
 
 enum { kCsvOk = 0, kCsvNumberFormat = 1, kCsvUnsupported = 2, kCsvMissingField = 3, kCsvEmptyLine = 4 };
@@ -37,7 +46,7 @@ struct GBytes {
 };
 // the bytes of a block's lines staged in LDS: text position i lives at p[i - base]
 struct LBytes {
-  const char* p;
+  GF_LDS_PTR(char) p;
   int64_t base;
   GF_DHD char operator()(int64_t i) const { return p[i - base]; }
 };

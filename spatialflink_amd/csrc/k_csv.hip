@@ -246,7 +246,8 @@ __global__ __launch_bounds__(kBlock) void csv_parse_kernel(CsvArgs a) {
   bool need = false;
   __shared__ uint64_t gtab[FMT == 1 ? 256 : 1], gttab[FMT == 1 ? 256 : 1];
   __shared__ char gkeys[FMT == 1 ? kGeoKeys * kGeoPropMax : 1];
-  const GeoTabs gt{gtab, gttab, gkeys, {5, 8, 10, 11, a.len_ts, a.len_obj, 4}};
+  const GeoTabs gt{(GF_LDS_PTR(uint64_t))gtab, (GF_LDS_PTR(uint64_t))gttab, (GF_LDS_PTR(char))gkeys,
+                   {5, 8, 10, 11, a.len_ts, a.len_obj, 4}};
   if (FMT == 1) {
     geo_tabs_fill(a, gtab, gttab, gkeys);
     __syncthreads();
@@ -261,8 +262,8 @@ __global__ __launch_bounds__(kBlock) void csv_parse_kernel(CsvArgs a) {
     }
     __syncthreads();
     if (j < L1) {
-      if (a.geo_fast) need = parse_line<FMT, true>(a, LBytes{lds, a0}, j, &w, gt);
-      else need = parse_line<FMT, false>(a, LBytes{lds, a0}, j, &w, gt);
+      if (a.geo_fast) need = parse_line<FMT, true>(a, LBytes{(GF_LDS_PTR(char))lds, a0}, j, &w, gt);
+      else need = parse_line<FMT, false>(a, LBytes{(GF_LDS_PTR(char))lds, a0}, j, &w, gt);
     }
   } else if (j < L1) {
     need = parse_line<FMT, false>(a, GBytes{a.text}, j, &w, gt);
@@ -289,7 +290,8 @@ __global__ void csv_error_kernel(CsvArgs a) {
   if (j == ~0ull) return;  // block-uniform
   __shared__ uint64_t gtab[256], gttab[256];
   __shared__ char gkeys[kGeoKeys * kGeoPropMax];
-  const GeoTabs gt{gtab, gttab, gkeys, {5, 8, 10, 11, a.len_ts, a.len_obj, 4}};
+  const GeoTabs gt{(GF_LDS_PTR(uint64_t))gtab, (GF_LDS_PTR(uint64_t))gttab, (GF_LDS_PTR(char))gkeys,
+                   {5, 8, 10, 11, a.len_ts, a.len_obj, 4}};
   if (a.format == 1) geo_tabs_fill(a, gtab, gttab, gkeys);
   __syncthreads();
   if (threadIdx.x != 0) return;
