@@ -1551,14 +1551,23 @@ __global__ __launch_bounds__(kBandThreads) void join_band_probe_kernel(JoinRowAr
         }
       }
       __syncthreads();
+      // Pairs out.  With the band staged (lds: block-uniform) every buffered entry is a staged slot
+      // and the flush reads LDS only; the global form (a sub-column read from global memory) is a
+      // separate path -- sharing one, its global load and the LDS read wrote the same register,
+      // and the compiler's wait for that write-after-write (vmcnt(0)) drained the prefetched
+      // points at every flush iteration.
       auto flush = [&]() {
-        band_emit(a.out, hd, cnt, [&](uint32_t i) {
-          const uint2 v = buf[i];
-          // (the staged read through an address_space(3) pointer: one generic pointer for both
-          // sources compiled to a FLAT load, whose wait drained the prefetched points at every flush)
-          const uint32_t q = v.y & kBandGlobal ? a.sqidx[v.y & ~kBandGlobal] : ((lds_u32)lq)[v.y];
-          return make_uint2(v.x, q);
-        });
+        if (lds) {
+          band_emit(a.out, hd, cnt, [&](uint32_t i) {
+            const uint2 v = buf[i];
+            return make_uint2(v.x, ((lds_u32)lq)[v.y]);
+          });
+        } else {
+          band_emit(a.out, hd, cnt, [&](uint32_t i) {
+            const uint2 v = buf[i];
+            return make_uint2(v.x, a.sqidx[v.y & ~kBandGlobal]);
+          });
+        }
         cnt = 0;
       };
       // DENSE window (clustered input: ~> 12 candidates per point): each wave-step's 64 points are
@@ -1699,6 +1708,10 @@ __global__ __launch_bounds__(kBandThreads) void join_band_probe_kernel(JoinRowAr
           L[k] = acc;
         }
         const uint32_t LA = L[2], LT = L[5];
+#ifdef GF_BAND_EXP_NOWALK  // experiment build: setup and streaming only (no pairs)
+        sink += LT ^ dd[0] ^ dd[3];
+        return;
+#endif
         for (uint32_t k = 0; __ballot(k < LT) != 0; k += kBandRound) {
           if (cnt > (uint32_t)(kBandBuf - 64 * kBandRound)) flush();
           uint32_t t[kBandRound];
@@ -1721,6 +1734,10 @@ __global__ __launch_bounds__(kBandThreads) void join_band_probe_kernel(JoinRowAr
             else ok = a.metric == 0 ? dx * dx + dy * dy <= a.s_r : fdlibm_hypot(dx, dy) <= a.r;
             const bool hit = k + i < LT && ok;
             const uint64_t hm = __ballot(hit);
+#ifdef GF_BAND_EXP_NOPUSH  // experiment build: hits ballotted, never stored
+            sink ^= (uint32_t)hm;
+            continue;
+#endif
             if (hit)
               buf[cnt + __builtin_amdgcn_mbcnt_hi((uint32_t)(hm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)hm, 0u))] =
                   make_uint2(second ? ib : ia, t[i]);
