@@ -1514,7 +1514,11 @@ __global__ __launch_bounds__(kBandThreads) void join_band_probe_kernel(JoinRowAr
       uint16_t* const lo16 = reinterpret_cast<uint16_t*>(stg);
       double2* const lxy = reinterpret_cast<double2*>(stg + ((band_off_bytes(f, c0, c1) + 15u) & ~15u));
       uint32_t* const lq = reinterpret_cast<uint32_t*>(lxy + m);
+#ifdef GF_BAND_EXP_NOSTAGE  // experiment build (with NOWALK only): the band is not staged
+      if (false) {
+#else
       if (lds) {  // stage: offsets (absolute staged slots), xy, query indices -- loads batched
+#endif
         const uint32_t nent = (uint32_t)(f + 2) * ncol, span = c1 - c0 + 3;
         for (uint32_t t0 = threadIdx.x; t0 < nent; t0 += 8 * kBandThreads) {
           uint32_t v[8];
@@ -1708,6 +1712,9 @@ __global__ __launch_bounds__(kBandThreads) void join_band_probe_kernel(JoinRowAr
           L[k] = acc;
         }
         const uint32_t LA = L[2], LT = L[5];
+#if defined(GF_BAND_EXP_NOSTAGE) && !defined(GF_BAND_EXP_NOWALK)
+#error "GF_BAND_EXP_NOSTAGE needs GF_BAND_EXP_NOWALK (unstaged offsets must not be walked)"
+#endif
 #ifdef GF_BAND_EXP_NOWALK  // experiment build: setup and streaming only (no pairs)
         sink += LT ^ dd[0] ^ dd[3];
         return;
