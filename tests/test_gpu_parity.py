@@ -91,6 +91,8 @@ def bucket_expected(oracle_mod, og, gn, x, y):
     (500, 1, BEIJING, False), (500, 63, BEIJING, False), (500, 4097, BEIJING, True),
     # row mode (gn <= 511): the most rows, out-of-grid points; mostly empty rows
     (511, 800_000, (115.3, 117.8, 39.5, 41.2), True), (300, 100, BEIJING, False),
+    (23, 50, (115.3, 117.8, 39.5, 41.2), False),            # the smallest two-pass grid: fewer points than rows
+    (64, 70_000, (116.39, 116.41, 39.5, 41.2), False),      # one column: every row one cell
 ])
 def test_bucket_by_cell_exact(sf, oracle_mod, gn, n, box, clustered):
     g = sf.UniformGrid(gn, *BEIJING)
