@@ -1561,6 +1561,11 @@ __global__ __launch_bounds__(kBandThreads) void join_band_probe_kernel(JoinRowAr
       // and the compiler's wait for that write-after-write (vmcnt(0)) drained the prefetched
       // points at every flush iteration.
       auto flush = [&]() {
+#ifdef GF_BAND_EXP_NOEMIT  // experiment build: the buffered pairs are dropped (no band_emit)
+        sink ^= cnt;
+        cnt = 0;
+        return;
+#endif
         if (lds) {
           band_emit(a.out, hd, cnt, [&](uint32_t i) {
             const uint2 v = buf[i];
