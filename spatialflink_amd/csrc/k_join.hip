@@ -183,7 +183,10 @@ __device__ __forceinline__ void chunk_of(int64_t no, int64_t bid, int64_t nblk, 
 
 // kBucketU points per thread are loaded before any is used (the loop is latency-bound
 // otherwise: one HBM round trip per point per wave)
-constexpr int kBucketU = 8;
+#ifndef GF_JOIN_BUCKET_U
+#define GF_JOIN_BUCKET_U 8
+#endif
+constexpr int kBucketU = GF_JOIN_BUCKET_U;
 
 constexpr int kScatThreads = 1024;
 constexpr int kHistSplit = 2;  // histogram chunks per scatter block
@@ -376,11 +379,13 @@ __device__ __forceinline__ void wc_row_scatter(const double* X, const double* Y,
       sdst[slot] = gd[row[u]] + slot;
     }
     lds_barrier();
+#ifndef GF_SCAT_EXP_NOSTORE  // experiment build: the tile is placed in LDS but not written out
     for (uint32_t k = threadIdx.x; k < kept; k += kScatThreads) {
       const uint32_t d = sdst[k];
       oxy[d] = sxy[k];
       oidx[d] = sidx[k];
     }
+#endif
     for (int r = r0; r < r0 + per && r < nrows; ++r) {  // th[r] = tile end of the row
       gd[r] += th[r];
       th[r] = 0u;
