@@ -2121,8 +2121,8 @@ static int join_pp_impl(gf_ctx* ctx, const gf_grid* ugrid, const gf_grid* qgrid,
     o.spill_cap = spill_cap;
     if (band) {
       if (!ctx->join_hist) {  // zero: no history (the first call's regions come from ppp)
-        GF_HIP_CHECK(ctx, hipMalloc(&ctx->join_hist, 2 * sizeof(uint64_t) * (size_t)probe_blocks));
-        GF_HIP_CHECK(ctx, hipMemsetAsync(ctx->join_hist, 0, 2 * sizeof(uint64_t) * (size_t)probe_blocks, s));
+        GF_HIP_CHECK(ctx, hipMalloc(&ctx->join_hist, sizeof(uint64_t) * (3 * (size_t)probe_blocks + 1)));
+        GF_HIP_CHECK(ctx, hipMemsetAsync(ctx->join_hist, 0, sizeof(uint64_t) * (3 * (size_t)probe_blocks + 1), s));
         GF_HIP_CHECK(ctx, hipMalloc(&ctx->join_ovf, 2 * sizeof(unsigned long long)));  // overflow, ticket
         GF_HIP_CHECK(ctx, hipMemsetAsync(ctx->join_ovf, 0, 2 * sizeof(unsigned long long), s));
       }

@@ -50,7 +50,7 @@ struct gf_ctx {
   uint32_t expand_epoch = 0;
   unsigned long long* join_gctr = nullptr;  // row-bucketed join: reserved output positions (zero between calls)
   unsigned long long* join_hint = nullptr;  // mapped pinned: the pair count of the last join (async too)
-  uint64_t* join_hist = nullptr;            // band probe: the last join's pairs | points per block ([2 * blocks], zero: none)
+  uint64_t* join_hist = nullptr;            // band probe: the last join's pairs, points, slice start per block, did-not-fit ([3 * blocks + 1], zero: none)
   unsigned long long* join_ovf = nullptr;   // band probe: overflow counter (zero between calls)
   int64_t join_hint_no = 0;                 // ordinary points of that join
 };
@@ -650,7 +650,7 @@ struct JoinOut {
   int regions;
   uint64_t* bcount;          // [G] this call's pairs per block
   uint64_t* bslice;          // [G] this call's ordinary points per block
-  uint64_t* hist;            // [2G] persistent: the last call's pairs | points per block (zero: none)
+  uint64_t* hist;            // [3G + 1] persistent: the last call's pairs | points | slice start per block, did-not-fit (zero: none)
   unsigned long long* ovf;   // persistent overflow counter (the fix-up resets it)
   uint64_t e_lim;            // the regions' total never exceeds it (cap + spill covers it)
   double ppp;                // pairs per point when there is no history

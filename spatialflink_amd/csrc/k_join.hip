@@ -1275,6 +1275,8 @@ struct BandHdr {
   unsigned long long fill;  // the block's pairs so far: its region cursor
   uint64_t roff, rlen, E;   // the block's region, the regions' end (overflow area start)
   uint64_t wsum[kBandWaves];
+  uint32_t p0, p1;          // the block's slice of the bucketed points (band_regions)
+  int32_t nopart, unbal;    // band_regions: the history's slices not a partition / not balanced
   int32_t last;             // this block took the last ticket
 };
 constexpr int kBandHdrBytes = (int)((sizeof(BandHdr) + 15) / 16 * 16);
@@ -1282,6 +1284,7 @@ constexpr size_t kBandLds = 160 * 1024;
 constexpr int kBandQueue = 128;      // windowed bands: queued point positions per wave
 constexpr size_t kBandPerWave = (size_t)kBandBuf * 8 + kBandQueue * 4;
 constexpr size_t kBandStage = kBandLds - kBandHdrBytes - (size_t)kBandWaves * kBandPerWave;
+static_assert(kBandStage >= 5 * 8 * 1024, "band_regions' scratch (5 G u64, G <= 1024) in the staging area");
 // staged offset entries per band sub-row for window [c0, c1): sub-columns c0 - 1 .. c1 + 1
 __device__ __forceinline__ uint32_t band_ncol(uint32_t c0, uint32_t c1) { return (c1 - c0 + 3 + 7) & ~7u; }
 __device__ __forceinline__ uint32_t band_off_bytes(int32_t f, uint32_t c0, uint32_t c1) {
@@ -1315,26 +1318,100 @@ __device__ __forceinline__ uint64_t band_scan(uint64_t v, uint64_t* total, uint6
   __syncthreads();
   return before + inc - v;
 }
-// Every block derives all G regions the same way (so no launch is needed for them): block t's
-// pairs per point from the last call (hist; none: the host's estimate) x its slice now, + 1/32
-// + 256; scaled down so that the total stays <= e_lim.  Block 0 records them for the fix-up.
-__device__ __forceinline__ void band_regions(const JoinOut& o, uint32_t N, BandHdr& hd, uint64_t& my_off,
-                                             uint64_t& my_len) {
+// the block that took slice s (the inverse of band_slice's mapping)
+__device__ __forceinline__ uint32_t band_block_of(uint32_t G, uint32_t s) {
+  return (s % (G >> 3)) * 8u + s / (G >> 3);
+}
+// Every block derives all G slices and regions the same way (so no launch is needed for them).
+// History (hist, per block of the last call): its pairs, its slice's length and start, and
+// whether the call fit its output.  Slices: without a history, equal point slices.  With one,
+// the last call's slices (scaled to this call's N) when their WORK (pairs + points) was within
+// 1/8 of balanced or when the last call did not fit (a capacity retry: the same slices, so the
+// regions come from exact counts); else the bucketed points are cut at equal quantiles of the
+// last call's work, spread evenly over each of its slices (clustered input: equal point slices
+// left the busiest block ~1.8x the mean work).  Regions: the slice's pairs (by the same
+// interpolation; no history: the host's pairs per point x the slice), + 1/32 + 256; scaled
+// down so that the total stays <= e_lim.  scr: LDS scratch for 5 G u64 (the band staging area,
+// not yet in use); my_p0: block t's slice start for thread t (the history, join_region_prep).
+__device__ __forceinline__ void band_regions(const JoinOut& o, uint32_t N, BandHdr& hd, uint64_t* scr,
+                                             uint64_t& my_off, uint64_t& my_len, uint32_t& my_p0) {
   const uint32_t G = gridDim.x, t = threadIdx.x;
-  uint64_t hp = 0, hn = 0, slice = 0;
-  if (t < G) {
-    uint32_t p0, p1;
-    band_slice(N, G, t, p0, p1);
-    slice = p1 - p0;
-    hp = o.hist[t];
-    hn = o.hist[G + t];
+  uint64_t hp = 0, hn = 0, hs = 0;
+  if (t < G) {  // thread t: slice t's history
+    const uint32_t b = band_block_of(G, t);
+    hp = o.hist[b];
+    hn = o.hist[G + b];
+    hs = o.hist[2 * G + b];
+  }
+  if (t == 0) {  // (seen by all after band_scan's barriers; __syncthreads_or would add static LDS
+    hd.nopart = 0;  // to the kernel's full 160 KB: an invalid dispatch)
+    hd.unbal = 0;
   }
   uint64_t HP, HN;
-  band_scan(hp, &HP, hd.wsum);
-  band_scan(hn, &HN, hd.wsum);
-  const double gppp = HN > 0 ? (double)HP / (double)HN : o.ppp;
+  const uint64_t pc = band_scan(hp, &HP, hd.wsum), op = band_scan(hn, &HN, hd.wsum);
+  uint64_t* const sW = scr;            // work before slice s
+  uint64_t* const sOP = scr + G;       // points before slice s (last call)
+  uint64_t* const sPC = scr + 2 * G;   // pairs before slice s
+  uint64_t* const sHN = scr + 3 * G;
+  uint64_t* const sHP = scr + 4 * G;
+  if (t < G) {
+    sW[t] = pc + op;
+    sOP[t] = op;
+    sPC[t] = pc;
+    sHN[t] = hn;
+    sHP[t] = hp;
+  }
+  const uint64_t Wtot = HP + HN;
+  // the last call's slices a partition of [0, HN) in slice order (as a history from this probe
+  // always is), and every slice's work within 1/8 of the mean
+  if (t < G && hs != op) hd.nopart = 1;
+  if (t < G && (double)(hp + hn) * G > 1.125 * (double)Wtot) hd.unbal = 1;
+  __syncthreads();
+  const bool reuse = HN > 0 && !hd.nopart && (!hd.unbal || o.hist[3 * G] != 0);
+  const double scale = HN > 0 ? (double)N / (double)HN : 0.0;
+  // position (this call) and pairs before (last call) of the k-th of G work quantiles.  Integer
+  // positions, so the slices partition [0, N) exactly: within a slice floor(fr * HN) < HN for
+  // q before the next slice's work (fr < 1 in double at these magnitudes), and the next slice
+  // starts at sOP + HN -- monotone in k, and every block computes the same boundaries.
+  auto quantile = [&](uint32_t k, uint32_t& pos, double& pairs) {
+    if (k == 0) { pos = 0; pairs = 0.0; return; }
+    if (k >= G) { pos = N; pairs = (double)HP; return; }
+    const uint64_t q = (uint64_t)k * Wtot / G;  // (k < G <= 1024, Wtot < 2^53)
+    uint32_t lo = 0, hi = G;  // the last slice whose work starts at or before q
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (sW[mid] <= q) lo = mid;
+      else hi = mid;
+    }
+    const uint64_t w = sHN[lo] + sHP[lo];
+    const double fr = w > 0 ? (double)(q - sW[lo]) / (double)w : 0.0;
+    const uint64_t old = sOP[lo] + (uint64_t)(fr * (double)sHN[lo]);  // <= HN
+    pos = (uint32_t)(old * (uint64_t)N / HN);
+    pairs = (double)sPC[lo] + fr * (double)sHP[lo];
+  };
   uint64_t est = 0;
-  if (t < G) est = (uint64_t)ceil((hn > 0 ? (double)hp / (double)hn : gppp) * (double)slice * 1.03125) + 256;
+  if (t < G) {  // block t's slice and region
+    const uint32_t s = (t & 7u) * (G >> 3) + (t >> 3);
+    uint32_t p0, p1;
+    if (reuse) {  // (floor(x * N / HN) of a partition of [0, HN): a partition of [0, N))
+      p0 = (uint32_t)(sOP[s] * (uint64_t)N / HN);
+      p1 = (uint32_t)((sOP[s] + sHN[s]) * (uint64_t)N / HN);
+      est = (uint64_t)ceil((double)sHP[s] * scale * 1.03125) + 256;
+    } else if (HN > 0) {
+      double a0, a1;
+      quantile(s, p0, a0);
+      quantile(s + 1, p1, a1);
+      est = (uint64_t)ceil((a1 - a0) * scale * 1.03125) + 256;
+    } else {
+      band_slice(N, G, t, p0, p1);
+      est = (uint64_t)ceil(o.ppp * (double)(p1 - p0) * 1.03125) + 256;
+    }
+    if (t == blockIdx.x) {
+      hd.p0 = p0;
+      hd.p1 = p1;
+    }
+    my_p0 = p0;
+  }
   uint64_t E;
   uint64_t off = band_scan(est, &E, hd.wsum);
   if (E > o.e_lim) {  // floor(est * s) with s < e_lim / E: the sum stays <= e_lim
@@ -1388,7 +1465,8 @@ __device__ __forceinline__ void band_emit(const JoinOut& o, BandHdr& hd, uint32_
 // write-through hand-off of cdna_hip_programming.md Guideline 16 (R1): sc1 stores of the payload,
 // s_waitcnt vmcnt(0) by the storing lane, an atomic counter, sc1 loads in the last arriver (which
 // bypass its CU's L1, so no acquire is needed); tests/test_isa_handoff.py checks it in the ISA.
-__device__ __forceinline__ void join_region_prep(const JoinFixup& f, uint64_t* ws, uint64_t O, uint64_t R, uint64_t E) {
+__device__ __forceinline__ void join_region_prep(const JoinFixup& f, uint64_t* ws, uint64_t O, uint64_t R, uint64_t E,
+                                                 uint32_t P0) {
   const JoinOut& o = f.o;
   const uint32_t G = o.nwaves, t = threadIdx.x;
   uint64_t n = 0, sl0 = 0;
@@ -1428,6 +1506,7 @@ __device__ __forceinline__ void join_region_prep(const JoinFixup& f, uint64_t* w
     f.hole_pref[t] = hp;
     o.hist[t] = n;
     o.hist[G + t] = sl0;
+    o.hist[2 * G + t] = P0;
   }
   if (t <= G) {
     f.seg_start[t] = ss;
@@ -1439,6 +1518,7 @@ __device__ __forceinline__ void join_region_prep(const JoinFixup& f, uint64_t* w
     f.counts[0] = fits ? G : 0u;
     f.counts[1] = fits ? G + 1 : 0u;
     *f.total = T <= o.cap && lost ? o.cap + 1 : T;
+    o.hist[3 * G] = fits ? 0ull : 1ull;  // did not fit: the retry keeps these slices
     if (f.hint) *f.hint = T;
     *o.ovf = 0ull;
   }
@@ -1460,10 +1540,10 @@ __global__ __launch_bounds__(kBandThreads) void join_band_probe_kernel(JoinRowAr
   const uint32_t cbeg = (uint32_t)f, cend = (uint32_t)f * (uint32_t)(qn + 1);  // in-grid sub-columns
   const uint32_t N = a.row_off[qn];
   uint64_t my_off, my_len;
-  band_regions(a.out, N, hd, my_off, my_len);
-  uint32_t pos, P1;
-  band_slice(N, gridDim.x, blockIdx.x, pos, P1);
-  const uint32_t P0 = pos;
+  uint32_t my_p0 = 0;
+  band_regions(a.out, N, hd, reinterpret_cast<uint64_t*>(stg), my_off, my_len, my_p0);
+  uint32_t pos = hd.p0;
+  const uint32_t P0 = pos, P1 = hd.p1;
   while (pos < P1) {  // block-uniform: one row segment
     for (int j = threadIdx.x; j < qn; j += kBandThreads)
       if (a.row_off[j] <= pos && pos < a.row_off[j + 1]) hd.row = j;
@@ -1840,7 +1920,7 @@ __global__ __launch_bounds__(kBandThreads) void join_band_probe_kernel(JoinRowAr
   }
   __syncthreads();
   if (hd.last) {  // block-uniform: every other block's counts are in
-    join_region_prep(a.fx, hd.wsum, my_off, my_len, hd.E);
+    join_region_prep(a.fx, hd.wsum, my_off, my_len, hd.E, my_p0);
     if (threadIdx.x == 0) __hip_atomic_store(a.ticket, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }

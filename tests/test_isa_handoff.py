@@ -61,12 +61,22 @@ def check_handoff(body, n_payload):
     return ticket
 
 
+def static_lds(asm, mangled_prefix):
+    m = re.search(r"^\s*\.amdhsa_kernel (" + re.escape(mangled_prefix) + r"\S*)$", asm, re.M)
+    assert m, mangled_prefix
+    f = re.search(r"\.amdhsa_group_segment_fixed_size (\d+)", asm[m.end():])
+    return int(f.group(1))
+
+
 @pytest.mark.timeout(600)
 def test_join_band_probe_handoff_is_write_through(tmp_path):
     asm = device_asm("k_join.hip", tmp_path)
     for mode in (0, 1):
         body = function_body(asm, f"_ZN2gf22join_band_probe_kernelILi{mode}E")
         check_handoff(body, 2)  # bcount, bslice
+        # the probe takes the whole 160 KB as dynamic LDS: any static LDS (e.g. the scratch word
+        # of a __syncthreads_or) makes every dispatch invalid (HSA_STATUS_ERROR_INVALID_ALLOCATION)
+        assert static_lds(asm, f"_ZN2gf22join_band_probe_kernelILi{mode}E") == 0
 
 
 @pytest.mark.timeout(600)
