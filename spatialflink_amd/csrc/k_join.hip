@@ -1318,6 +1318,10 @@ __device__ __forceinline__ uint64_t band_scan(uint64_t v, uint64_t* total, uint6
   __syncthreads();
   return before + inc - v;
 }
+#ifndef GF_BAND_BALANCED
+#define GF_BAND_BALANCED 1.125
+#endif
+constexpr double kBandBalanced = GF_BAND_BALANCED;  // the last call's slices are kept below this max / mean work
 // the block that took slice s (the inverse of band_slice's mapping)
 __device__ __forceinline__ uint32_t band_block_of(uint32_t G, uint32_t s) {
   return (s % (G >> 3)) * 8u + s / (G >> 3);
@@ -1365,7 +1369,7 @@ __device__ __forceinline__ void band_regions(const JoinOut& o, uint32_t N, BandH
   // the last call's slices a partition of [0, HN) in slice order (as a history from this probe
   // always is), and every slice's work within 1/8 of the mean
   if (t < G && hs != op) hd.nopart = 1;
-  if (t < G && (double)(hp + hn) * G > 1.125 * (double)Wtot) hd.unbal = 1;
+  if (t < G && (double)(hp + hn) * G > kBandBalanced * (double)Wtot) hd.unbal = 1;
   __syncthreads();
   const bool reuse = HN > 0 && !hd.nopart && (!hd.unbal || o.hist[3 * G] != 0);
   const double scale = HN > 0 ? (double)N / (double)HN : 0.0;
