@@ -8,7 +8,7 @@ HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -ffp-contract=off -fno-f
 SRC      := spatialflink_amd/csrc
 OBJDIR   := build/obj
 LIB      := spatialflink_amd/libgeoflink_hip.so
-SOURCES  := $(SRC)/api.cpp $(SRC)/sliding.cpp $(SRC)/csv.cpp $(SRC)/objid.cpp $(SRC)/k_points.hip $(SRC)/k_knn.hip \
+SOURCES  := $(SRC)/api.cpp $(SRC)/comm.cpp $(SRC)/sliding.cpp $(SRC)/csv.cpp $(SRC)/objid.cpp $(SRC)/k_points.hip $(SRC)/k_knn.hip \
             $(SRC)/k_range.hip $(SRC)/k_join.hip $(SRC)/k_csv.hip $(SRC)/k_objid.hip
 OBJECTS  := $(patsubst $(SRC)/%,$(OBJDIR)/%.o,$(SOURCES))
 HEADERS  := include/geoflink_hip.h $(SRC)/gf_internal.hpp $(SRC)/gf_text.hpp $(SRC)/gf_geojson.hpp $(SRC)/gf_numerics.hpp $(SRC)/gf_decimal.hpp $(SRC)/gf_pow5.hpp $(SRC)/gf_geom.hpp
@@ -29,7 +29,7 @@ $(OBJDIR)/%.o: $(SRC)/% $(HEADERS)
 	$(HIPCC) $(HIPFLAGS) $(GF_DEFS) -x hip -c $< -o $@
 
 $(LIB): $(OBJECTS)
-	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(OBJECTS)
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(OBJECTS) -ldl
 
 oracle:
 	$(MAKE) -s -C oracle
@@ -42,7 +42,7 @@ $(TRACE_OBJDIR)/%.o: $(SRC)/% $(HEADERS)
 	@mkdir -p $(TRACE_OBJDIR)
 	$(HIPCC) $(HIPFLAGS) -DGF_TRACE -x hip -c $< -o $@
 $(TRACE_LIB): $(TRACE_OBJECTS)
-	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(TRACE_OBJECTS)
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(TRACE_OBJECTS) -ldl
 trace: $(TRACE_LIB)
 
 # gfx950 ISA listing for inspection (v_fma_f64 must not appear in the distance paths)

@@ -143,6 +143,44 @@ class PinnedStringRecords:
         return st, np.array([int(s_[3:]) for s_ in strs], np.int64), d, ix
 
 
+def _free_port() -> int:
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _launch_ranks(args):
+    """`--gpus N` is the job's parallelism (env.setParallelism, StreamingJob.java:177): one process
+    per GPU.  Launched by hand (no WORLD_SIZE in the environment) with N > 1, this process starts
+    `python -m torch.distributed.run --nproc-per-node N bench.py <same args>` as a CHILD -- before
+    anything here has touched the GPU (no torch import yet) -- relays its output (rank 0 prints the
+    one JSON line) and returns its exit code.  Under a launcher, WORLD_SIZE must equal N.
+    -> None when this process is a rank (or N == 1), else the launcher's exit code."""
+    import subprocess
+
+    world = os.environ.get("WORLD_SIZE")
+    if world is not None:
+        if int(world) != args.gpus:
+            log(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world} (the launcher started a different "
+                "number of ranks)")
+            return 2
+        return None
+    if args.gpus < 1:
+        log("bench.py: --gpus must be >= 1")
+        return 2
+    if args.gpus == 1:
+        return None
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    log(f"bench.py: launching {args.gpus} ranks: {' '.join(cmd)}")
+    sys.stdout.flush()
+    return subprocess.run(cmd, env=dict(os.environ, MASTER_ADDR="127.0.0.1")).returncode
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -187,6 +225,9 @@ def main():
                     help="N > 1: windows whose top-k records share one RCCL all-gather + one merge launch")
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                     help="gloo: rehearse the N > 1 path with several ranks on one GPU (not a benchmark)")
+    ap.add_argument("--exchange", default="auto", choices=("auto", "rccl", "torch"),
+                    help="N > 1 kNN record exchange: rccl = the C ABI's communicator (gf_knn_exchange_batch, "
+                         "the Java drop-in's path); torch = torch.distributed all-gather; auto = rccl on nccl")
     ap.add_argument("--scan-blocks", type=int, default=0, help="kNN scan grid (0 = auto: 4 blocks per CU)")
     ap.add_argument("--string-objids", action="store_true",
                     help="objIDs are dictionary Strings (\"veh%%09d\", MN_Q1.java:52's deviceId): N > 1 exchanges "
@@ -197,6 +238,9 @@ def main():
                          "for point kNN -- depth 4 measured 28.5 vs 24.6 us -- and 4 for polygon kNN, "
                          "30.3 vs 33.8 us)")
     args = ap.parse_args()
+    launched = _launch_ranks(args)
+    if launched is not None:
+        sys.exit(launched)
     if args.pipeline is None:
         args.pipeline = 4 if args.workload == "polyknn" else 3
     sys.path.insert(0, os.path.join(ROOT, "tools"))
@@ -289,6 +333,9 @@ def main():
     # context of its own, so the next group's windows keep streaming while it is in flight (the
     # slots are double-buffered); the first window of group g + 2 waits for group g's exchange
     # (done long before: a group is B windows of work).  String records stay on the plan's stream.
+    comm, xdesc = sharding.open_comm(dev.index, args.dist_backend, args.exchange) if world > 1 else (None, None)
+    if world > 1:
+        log(f"[rank {rank}] record exchange: {xdesc}")
     side = torch.cuda.Stream(dev) if (world > 1 and hstr is None) else None
     xctx = None
     if side is not None:
@@ -299,7 +346,10 @@ def main():
     def exchange(first, lo, hi):  # windows [lo, hi] of one group: one all-gather + one merge launch
         g = (lo - first) // B
         if hstr is not None:  # String objIDs: the records travel with their Strings, merged by String
-            sharding.allgather_knn_records_strings(slots[g % 2, : hi - lo + 1], args.k, scap, sdict, hstr.ptr(lo))
+            if comm is not None:
+                comm.exchange_strings_batch(slots[g % 2, : hi - lo + 1], args.k, scap, sdict, hstr.ptr(lo))
+            else:
+                sharding.allgather_knn_records_strings(slots[g % 2, : hi - lo + 1], args.k, scap, sdict, hstr.ptr(lo))
             if args.pipeline >= 3:
                 # depth >= 3 writes windows' records on the plan's other streams: they must not
                 # reuse slots[g % 2] (group g + 2) before this all-gather + merge have read them
@@ -307,7 +357,10 @@ def main():
         else:
             side.wait_stream(torch.cuda.current_stream(dev))  # the group's records are complete
             with torch.cuda.stream(side):
-                sharding.allgather_knn_records_batch(slots[g % 2, : hi - lo + 1], args.k, host.ptr(lo), ctx=xctx)
+                if comm is not None:
+                    comm.exchange_batch(slots[g % 2, : hi - lo + 1], args.k, host.ptr(lo), ctx=xctx)
+                else:
+                    sharding.allgather_knn_records_batch(slots[g % 2, : hi - lo + 1], args.k, host.ptr(lo), ctx=xctx)
                 ev = torch.cuda.Event()
                 ev.record(side)
             slot_free[g % 2] = ev
@@ -621,6 +674,7 @@ def main():
                 "parallelism": f"cell-column shards x{world}" + (" + RCCL all-gather top-k" if world > 1 else ""),
                 "windows_in_flight": args.pipeline,
                 "exchange_batch": B if world > 1 else None,
+                "exchange": xdesc,
                 "objid": ("dictionary Strings" + (" (string records merged by String)" if world > 1 else ""))
                          if args.string_objids else "canonical decimal (int64 keys)",
             },
@@ -651,6 +705,8 @@ def main():
             "verified_vs_oracle": verified,
         }
         print(json.dumps(line), flush=True)
+    if comm is not None:
+        comm.destroy()
     if world > 1:
         dist.destroy_process_group()
 

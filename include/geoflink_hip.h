@@ -41,6 +41,7 @@ extern "C" {
 #define GF_ERR_LAYERS    -5  /* candidate layers <= 0 where the reference calls System.exit(1)
                                 (UniformGrid.java:272-276, JoinQuery.java:80) */
 #define GF_ERR_ALIGN     -7  /* x / y not 16-byte aligned */
+#define GF_ERR_COMM      -8  /* RCCL unavailable or a collective failed (see gf_comm_last_error) */
 
 /* distance metric of JTS Coordinate.distance */
 #define GF_METRIC_SQRT  0    /* Math.sqrt(dx*dx + dy*dy) -- default */
@@ -357,6 +358,47 @@ int gf_knn_string_record_decode(const void* record, int32_t k, int64_t cap_bytes
 int    gf_knn_merge_host(int32_t k, int32_t nlists, const int32_t* counts, const int64_t* objID,
                          const double* dist, const int64_t* idx, int64_t* out_objID,
                          double* out_dist, int64_t* out_idx, int32_t* n_out);
+
+/* ---- multi-GPU: RCCL communicators and the kNN record exchange --------------------------------
+ * The windowAll funnel across GPUs (PointPointKNNQuery.java:198-200 -> KNNQuery.java:213-272):
+ * each GPU evaluates its cell-column band of the window (gf_shard_by_columns routes an arriving
+ * window) into a top-k record; the exchange all-gathers every rank's records over xGMI (RCCL
+ * ncclAllGather on the context's stream) and merges them on the device into the SAME record on
+ * every rank (gf_knn_merge_dev_batch, shard-major; with > 1 rank GF_MERGE_FOREIGN_KEYS).  RCCL is
+ * opened on first use (dlopen librccl.so.1; a process already holding it shares that copy).
+ *   one process per GPU:  rank 0 gf_comm_unique_id -> broadcast the 128 bytes over the job's own
+ *                         control plane -> every rank gf_comm_create(id, nranks, rank, device)
+ *                         (ncclCommInitRank; blocks until all ranks joined);
+ *   one process, N GPUs:  gf_comm_create_all(N, devices, comms) (ncclCommInitAll) -- then one
+ *                         thread per GPU calls gf_knn_exchange_batch on its own comm, or one
+ *                         thread drives all of them with gf_knn_exchange_group.
+ * A communicator's exchanges must be enqueued on one stream (its gather buffer is reused in
+ * stream order).  Every rank must call the exchange with the same k and nwin, in the same order.
+ * Input records must be final (status 0): a flagged record (status 1) makes the merged record
+ * flagged on every rank -- re-evaluate the shard exactly (gf_knn_decode) and exchange again. */
+#define GF_COMM_ID_BYTES 128
+typedef struct gf_comm gf_comm;
+int  gf_comm_available(void);               /* 1 when librccl.so.1 loads and has every entry used */
+int  gf_comm_unique_id(uint8_t* id);        /* id[GF_COMM_ID_BYTES] (ncclGetUniqueId), on one rank */
+int  gf_comm_create(const uint8_t* id, int32_t nranks, int32_t rank, int device, gf_comm** out);
+int  gf_comm_create_all(int32_t ndev, const int* devices, gf_comm** out /* [ndev] */);
+void gf_comm_destroy(gf_comm* comm);        /* drains the device first */
+int  gf_comm_info(const gf_comm* comm, int32_t* nranks, int32_t* rank, int* device);
+const char* gf_comm_last_error(const gf_comm* comm);  /* comm == NULL: why RCCL did not load */
+int  gf_comm_check(gf_comm* comm);          /* GF_ERR_COMM on an asynchronous RCCL error */
+/* Async: this rank's nwin consecutive device records (gf_knn_result_bytes(k) apart; ctx's device
+ * == the comm's) -> `merged` = nwin consecutive merged records (device or mapped pinned memory),
+ * identical on every rank.  One all-gather + one merge launch for all nwin windows. */
+int gf_knn_exchange_batch(gf_comm* comm, gf_ctx* ctx, int32_t k, const void* records, int32_t nwin, void* merged);
+/* Async, String objIDs: the records' dictionary Strings attached from `dict` (on dict's context,
+ * gf_knn_attach_strings), the string records all-gathered, merged by String
+ * (gf_knn_merge_dev_strings) -> nwin merged string records (gf_knn_string_record_bytes apart). */
+int gf_knn_exchange_strings_batch(gf_comm* comm, gf_objid_dict* dict, int32_t k, int64_t cap_bytes,
+                                  const void* records, int32_t nwin, void* merged);
+/* Async, one thread driving n communicators of one clique (gf_comm_create_all): the n
+ * all-gathers as one RCCL group, then the n merges (comms[i] with ctxs[i], records[i], merged[i]). */
+int gf_knn_exchange_group(int32_t n, gf_comm* const* comms, gf_ctx* const* ctxs, int32_t k,
+                          const void* const* records, int32_t nwin, void* const* merged);
 
 /* ---- sliding-window kNN: pane engine ------------------------------------------------
  * PointPointKNNQuery.windowBased with SlidingProcessingTimeWindows.of(size, slide)

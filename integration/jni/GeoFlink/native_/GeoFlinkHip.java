@@ -98,6 +98,22 @@ public final class GeoFlinkHip {
   public static native int knnWindow(long ctx, long plan, ByteBuffer x, ByteBuffer y, ByteBuffer objID, int n,
                                      long[] outObjID, double[] outDist, long[] outIdx, int k);
 
+  // ---- multi-GPU kNN: one subtask per GPU holds its cell-column band of every window; the
+  // windowAll merge (PointPointKNNQuery.java:198-200) is an RCCL exchange of the bands' top-k
+  // records.  One TaskManager per GPU: rank 0's commUniqueId() is broadcast to every subtask
+  // (a broadcast stream / the job configuration), each calls commCreate on its context (blocks
+  // until all ranks joined); one TaskManager holding every GPU: commCreateAll(devices).
+  public static native byte[] commUniqueId();
+  public static native long commCreate(long ctx, byte[] id, int nranks, int rank);
+  public static native long[] commCreateAll(int[] devices);
+  public static native void commDestroy(long comm);
+  // this subtask's band (its points are the window's global indices indexBase ..
+  // indexBase + n - 1) -> the WHOLE window's neighbours, identical on every rank; every rank calls
+  // it once per window, in the same order
+  public static native int knnWindowSharded(long ctx, long plan, long comm, ByteBuffer x, ByteBuffer y,
+                                            ByteBuffer objID, int n, long indexBase, long[] outObjID,
+                                            double[] outDist, long[] outIdx, int k);
+
   // ---- sliding kNN (pane engine) ---------------------------------------------------------
   // size / gcd(size, slide) <= 64; the plan must outlive the sliding handle
   public static native long knnSlidingCreate(long ctx, long plan, long sizeMs, long slideMs);

@@ -232,6 +232,72 @@ JNIEXPORT jint JNICALL Java_GeoFlink_native_1_GeoFlinkHip_knnWindow(JNIEnv* env,
   return m;
 }
 
+/* ---- multi-GPU kNN: RCCL exchange of the bands' records (PointPointKNNQuery.java:198-200,
+ * KNNQuery.java:213-272) ------------------------------------------------------------------------ */
+JNIEXPORT jbyteArray JNICALL Java_GeoFlink_native_1_GeoFlinkHip_commUniqueId(JNIEnv* env, jclass cls) {
+  uint8_t id[GF_COMM_ID_BYTES];
+  if (throw_status(env, shim_comm_unique_id(id), NULL)) return NULL;
+  jbyteArray out = (*env)->NewByteArray(env, GF_COMM_ID_BYTES);
+  if (out) (*env)->SetByteArrayRegion(env, out, 0, GF_COMM_ID_BYTES, (const jbyte*)id);
+  return out;
+}
+
+JNIEXPORT jlong JNICALL Java_GeoFlink_native_1_GeoFlinkHip_commCreate(JNIEnv* env, jclass cls, jlong ctx,
+    jbyteArray jid, jint nranks, jint rank) {
+  if (!need_len(env, jid, GF_COMM_ID_BYTES, "commCreate: id")) return 0;
+  uint8_t id[GF_COMM_ID_BYTES];
+  (*env)->GetByteArrayRegion(env, jid, 0, GF_COMM_ID_BYTES, (jbyte*)id);
+  shim_comm* h = NULL;
+  throw_status(env, shim_comm_create(CTX(ctx), id, nranks, rank, &h), CTX(ctx));
+  return (jlong)(intptr_t)h;
+}
+
+JNIEXPORT jlongArray JNICALL Java_GeoFlink_native_1_GeoFlinkHip_commCreateAll(JNIEnv* env, jclass cls,
+    jintArray jdev) {
+  const jsize n = jdev ? (*env)->GetArrayLength(env, jdev) : 0;
+  if (n < 1 || n > 64) {
+    throw_msg(env, "java/lang/IllegalArgumentException", "commCreateAll: 1..64 devices");
+    return NULL;
+  }
+  jint dev[64];
+  shim_comm* cs[64];
+  (*env)->GetIntArrayRegion(env, jdev, 0, n, dev);
+  if (throw_status(env, shim_comm_create_all(n, (const int*)dev, cs), NULL)) return NULL;
+  jlong hs[64];
+  for (jsize i = 0; i < n; ++i) hs[i] = (jlong)(intptr_t)cs[i];
+  jlongArray out = (*env)->NewLongArray(env, n);
+  if (out) (*env)->SetLongArrayRegion(env, out, 0, n, hs);
+  return out;
+}
+
+JNIEXPORT void JNICALL Java_GeoFlink_native_1_GeoFlinkHip_commDestroy(JNIEnv* env, jclass cls, jlong comm) {
+  shim_comm_destroy((shim_comm*)(intptr_t)comm);
+}
+
+/* this subtask's band of the window; out* hold >= k entries: the WHOLE window's neighbours */
+JNIEXPORT jint JNICALL Java_GeoFlink_native_1_GeoFlinkHip_knnWindowSharded(JNIEnv* env, jclass cls, jlong ctx,
+    jlong plan, jlong comm, jobject bx, jobject by, jobject bo, jint n, jlong indexBase, jlongArray oo,
+    jdoubleArray od, jlongArray oi, jint k) {
+  const double* x = direct(env, bx, 8 * (int64_t)n, "knnWindowSharded: x");
+  const double* y = direct(env, by, 8 * (int64_t)n, "knnWindowSharded: y");
+  const int64_t* o = direct(env, bo, 8 * (int64_t)n, "knnWindowSharded: objID");
+  if ((*env)->ExceptionCheck(env) || !need_len(env, oo, k, "knnWindowSharded: out") ||
+      !need_len(env, od, k, "knnWindowSharded: out") || !need_len(env, oi, k, "knnWindowSharded: out"))
+    return 0;
+  /* not GetPrimitiveArrayCritical: the call blocks on a collective with the other ranks */
+  int32_t m = 0;
+  jlong* po = (*env)->GetLongArrayElements(env, oo, NULL);
+  jdouble* pd = (*env)->GetDoubleArrayElements(env, od, NULL);
+  jlong* pi = (*env)->GetLongArrayElements(env, oi, NULL);
+  int st = shim_knn_window_sharded((shim_knn*)(intptr_t)plan, (shim_comm*)(intptr_t)comm, x, y, o, n, indexBase,
+                                   (int64_t*)po, pd, (int64_t*)pi, &m);
+  (*env)->ReleaseLongArrayElements(env, oi, pi, st ? JNI_ABORT : 0);
+  (*env)->ReleaseDoubleArrayElements(env, od, pd, st ? JNI_ABORT : 0);
+  (*env)->ReleaseLongArrayElements(env, oo, po, st ? JNI_ABORT : 0);
+  throw_status(env, st, CTX(ctx));
+  return m;
+}
+
 /* ---- sliding kNN: the pane engine (PointPointKNNQuery.java:158,198-200) ------------------- */
 JNIEXPORT jlong JNICALL Java_GeoFlink_native_1_GeoFlinkHip_knnSlidingCreate(JNIEnv* env, jclass cls, jlong ctx,
     jlong plan, jlong size_ms, jlong slide_ms) {

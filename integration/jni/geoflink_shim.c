@@ -90,6 +90,7 @@ static void window_free(cached_window* c) {
 
 struct shim_ctx {
   gf_ctx* ctx;
+  int device;
   char err[256];
   cached_window wo, wq;   /* join windows (ordinary / query or point side) */
   dbuf pairs;             /* device join pairs */
@@ -120,6 +121,7 @@ int shim_ctx_create(int device, shim_ctx** out) {
     free(c);
     return st;
   }
+  c->device = device;
   *out = c;
   return GF_OK;
 }
@@ -160,6 +162,8 @@ struct shim_knn {
   gf_knn_plan* plan;
   int32_t k;
   cached_window win;
+  dbuf rec;     /* sharded windows: this rank's device record */
+  pbuf merged;  /* ... and the merged record of all ranks (mapped pinned) */
 };
 
 int shim_knn_plan(shim_ctx* c, const gf_grid* g, double qx, double qy, double r, int32_t k, shim_knn** out) {
@@ -197,6 +201,8 @@ void shim_knn_destroy(shim_knn* h) {
   if (!h) return;
   gf_ctx_synchronize(h->c->ctx);
   window_free(&h->win);
+  dbuf_free(&h->rec);
+  pbuf_free(&h->merged);
   gf_knn_plan_destroy(h->plan);
   free(h);
 }
@@ -208,6 +214,110 @@ int shim_knn_window(shim_knn* h, const double* x, const double* y, const int64_t
   int st = upload(h->c->ctx, &h->win, x, y, objID, n, &pts);
   if (!st) st = gf_knn_run(h->plan, &pts, out_objID, out_dist, out_idx, m);
   return fail(h->c, st, "knnWindow");
+}
+
+/* ---- multi-GPU kNN: one Flink subtask per GPU, the window sharded by cell-column bands; the
+ * windowAll merge (PointPointKNNQuery.java:198-200, KNNQuery.java:213-272) is the RCCL record
+ * exchange behind the C ABI (gf_knn_exchange_batch) -------------------------------------------- */
+struct shim_comm {
+  gf_comm* comm;
+};
+
+int shim_comm_unique_id(uint8_t* id) { return gf_comm_unique_id(id); }
+
+int shim_comm_create(shim_ctx* c, const uint8_t* id, int32_t nranks, int32_t rank, shim_comm** out) {
+  *out = NULL;
+  shim_comm* h = (shim_comm*)calloc(1, sizeof(shim_comm));
+  if (!h) return GF_ERR_NOMEM;
+  int st = gf_comm_create(id, nranks, rank, c->device, &h->comm);
+  if (st) {
+    free(h);
+    snprintf(c->err, sizeof c->err, "commCreate: %s: %s", gf_status_string(st), gf_comm_last_error(NULL));
+    return st;
+  }
+  *out = h;
+  return GF_OK;
+}
+
+int shim_comm_create_all(int32_t ndev, const int* devices, shim_comm** out) {
+  gf_comm* cs[64];
+  if (ndev < 1 || ndev > 64) return GF_ERR_ARG;
+  for (int32_t i = 0; i < ndev; ++i) out[i] = NULL;
+  int st = gf_comm_create_all(ndev, devices, cs);
+  for (int32_t i = 0; !st && i < ndev; ++i) {
+    out[i] = (shim_comm*)calloc(1, sizeof(shim_comm));
+    if (!out[i]) st = GF_ERR_NOMEM;
+    else out[i]->comm = cs[i];
+  }
+  if (st) {
+    for (int32_t i = 0; i < ndev; ++i) {
+      if (out[i]) free(out[i]);
+      out[i] = NULL;
+    }
+  }
+  return st;
+}
+
+void shim_comm_destroy(shim_comm* h) {
+  if (!h) return;
+  gf_comm_destroy(h->comm);
+  free(h);
+}
+
+/* host lists -> a final record (status 0) in the rank's device record, for the second exchange */
+static int put_exact_record(shim_knn* h, const int64_t* o, const double* d, const int64_t* ix, int32_t m) {
+  const int32_t k = h->k;
+  const size_t rb = gf_knn_result_bytes(k);
+  char* rec = (char*)calloc(1, rb);
+  if (!rec) return GF_ERR_NOMEM;
+  gf_knn_header* hd = (gf_knn_header*)rec;
+  hd->status = 0;
+  hd->n = m;
+  hd->k = k;
+  double* rd = (double*)(hd + 1);
+  int64_t* ro = (int64_t*)(rd + k);
+  int64_t* ri = ro + k;
+  memcpy(rd, d, sizeof(double) * (size_t)m);
+  memcpy(ro, o, sizeof(int64_t) * (size_t)m);
+  memcpy(ri, ix, sizeof(int64_t) * (size_t)m);
+  int st = copy(h->c, h->rec.p, rec, rb, hipMemcpyHostToDevice) ? GF_ERR_HIP : GF_OK;
+  if (!st) st = gf_ctx_synchronize(h->c->ctx);  /* rec (host) is freed below */
+  free(rec);
+  return st;
+}
+
+int shim_knn_window_sharded(shim_knn* h, shim_comm* comm, const double* x, const double* y, const int64_t* objID,
+                            int64_t n, int64_t index_base, int64_t* out_objID, double* out_dist, int64_t* out_idx,
+                            int32_t* m) {
+  gf_ctx* ctx = h->c->ctx;
+  const int32_t k = h->k;
+  const size_t rb = gf_knn_result_bytes(k);
+  gf_points pts;
+  *m = 0;
+  int st = upload(ctx, &h->win, x, y, objID, n, &pts);
+  if (!st) st = dbuf_need(&h->rec, rb);
+  if (!st) st = pbuf_need(&h->merged, rb);
+  if (!st) st = gf_knn_plan_set_index_base(h->plan, index_base);
+  if (!st) st = gf_knn_enqueue(h->plan, &pts, h->rec.p);
+  if (!st) st = gf_knn_plan_flush(h->plan);
+  if (!st) st = gf_knn_exchange_batch(comm->comm, ctx, k, h->rec.p, 1, h->merged.p);
+  if (!st) st = gf_ctx_synchronize(ctx);
+  if (!st && ((const gf_knn_header*)h->merged.p)->status == 1) {
+    /* some rank's record needed the exact re-evaluation: the merged record is the same on every
+     * rank, so every rank takes this branch -- each re-evaluates its shard exactly (the local
+     * record, fetched into the merged buffer) and the ranks exchange again */
+    if (copy(h->c, h->merged.p, h->rec.p, rb, hipMemcpyDeviceToHost)) st = GF_ERR_HIP;
+    if (!st) st = gf_ctx_synchronize(ctx);
+    if (!st) st = gf_knn_decode(h->plan, &pts, h->merged.p, out_objID, out_dist, out_idx, m);
+    if (!st) st = put_exact_record(h, out_objID, out_dist, out_idx, *m);
+    if (!st) st = gf_knn_exchange_batch(comm->comm, ctx, k, h->rec.p, 1, h->merged.p);
+    if (!st) st = gf_ctx_synchronize(ctx);
+    *m = 0;
+  }
+  if (!st && ((const gf_knn_header*)h->merged.p)->status != 0) st = GF_ERR_ARG;  /* 2: dictionary keys */
+  if (!st) st = gf_knn_decode(h->plan, &pts, h->merged.p, out_objID, out_dist, out_idx, m);
+  if (!st) st = gf_knn_plan_set_index_base(h->plan, 0);
+  return fail(h->c, st, "knnWindowSharded");
 }
 
 /* ---- sliding kNN -------------------------------------------------------------------------- */

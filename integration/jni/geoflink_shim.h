@@ -54,6 +54,24 @@ void shim_pinned_free(void* p);
 int shim_knn_window(shim_knn* h, const double* x, const double* y, const int64_t* objID, int64_t n, int64_t* out_objID,
                     double* out_dist, int64_t* out_idx, int32_t* m);
 
+/* ---- multi-GPU kNN: one subtask per GPU holds its cell-column band of every window; the
+ * windowAll merge (PointPointKNNQuery.java:198-200, KNNQuery.java:213-272) becomes the RCCL
+ * exchange of the C ABI (gf_knn_exchange_batch).  One process per GPU: rank 0's
+ * shim_comm_unique_id (128 bytes) reaches every rank over the job's own channel (a Flink
+ * broadcast), then shim_comm_create on each rank's context; one process: shim_comm_create_all. */
+typedef struct shim_comm shim_comm;
+int shim_comm_unique_id(uint8_t* id /* [GF_COMM_ID_BYTES] */);
+int shim_comm_create(shim_ctx* c, const uint8_t* id, int32_t nranks, int32_t rank, shim_comm** out);
+int shim_comm_create_all(int32_t ndev, const int* devices, shim_comm** out /* [ndev] */);
+void shim_comm_destroy(shim_comm* comm);
+/* this rank's band of one window (host x, y, objID keys; its points are global indices
+ * index_base .. index_base + n - 1) -> the WHOLE window's *m neighbours, ascending (dist, objID),
+ * identical on every rank.  Every rank calls it once per window, in the same order.  A rank whose
+ * record needs the exact re-evaluation makes all ranks re-evaluate and exchange again. */
+int shim_knn_window_sharded(shim_knn* h, shim_comm* comm, const double* x, const double* y, const int64_t* objID,
+                            int64_t n, int64_t index_base, int64_t* out_objID, double* out_dist, int64_t* out_idx,
+                            int32_t* m);
+
 /* ---- sliding kNN: SlidingProcessingTimeWindows.of(size, slide) around the kNN apply
  * (PointPointKNNQuery.java:158,198-200) -- the pane engine (gf_knn_sliding_*) ---------------- */
 int shim_sliding_create(shim_knn* plan, int64_t size_ms, int64_t slide_ms, shim_sliding** out);

@@ -6,7 +6,7 @@ mirror of the reference operator API (UniformGrid, Point, Polygon, QueryConfigur
 PointPointRangeQuery, PointPolygonRangeQuery, PointPointKNNQuery, PointPointJoinQuery,
 PointPolygonKNNQuery, PointPolygonJoinQuery).
 """
-from . import _lib
+from . import _lib, sharding
 from .spatialIndices import UniformGrid, generateCellIDStr, getIntCellIndices, padLeadingZeroesToInt
 from .spatialObjects import ObjIdDict, Point, PointWindow, Polygon, PolygonSet
 from .spatialOperators import (KNNResult, PinnedRecords, PointPointJoinQuery, PointPointKNNQuery, PointPointRangeQuery,

@@ -25,6 +25,8 @@ GF_ERR_HIP = -3
 GF_ERR_NOMEM = -4
 GF_ERR_LAYERS = -5
 GF_ERR_ALIGN = -7
+GF_ERR_COMM = -8
+GF_COMM_ID_BYTES = 128
 
 METRIC_SQRT = 0
 METRIC_HYPOT = 1
@@ -57,7 +59,9 @@ EXPORTS = [
     "gf_window_destroy", "gf_window_upload", "gf_window_points", "gf_synth_uniform", "gf_pinned_alloc",
     "gf_pinned_free", "gf_knn_string_record_bytes", "gf_knn_attach_strings", "gf_knn_merge_dev_strings",
     "gf_knn_string_record_decode", "gf_window_upload_mapped", "gf_shard_by_columns", "gf_gather_points",
-    "gf_host_pinned",
+    "gf_host_pinned", "gf_comm_available", "gf_comm_unique_id", "gf_comm_create", "gf_comm_create_all",
+    "gf_comm_destroy", "gf_comm_info", "gf_comm_last_error", "gf_comm_check", "gf_knn_exchange_batch",
+    "gf_knn_exchange_strings_batch", "gf_knn_exchange_group",
 ]
 
 
@@ -212,6 +216,17 @@ def lib():
             "gf_knn_attach_strings": ([P, i32, P, i32, i64, P], C.c_int),
             "gf_knn_merge_dev_strings": ([P, i32, i64, P, i32, i32, i32, P], C.c_int),
             "gf_knn_string_record_decode": ([P, i32, i64, pi32, P, P, P, P, i64, P, pi32], C.c_int),
+            "gf_comm_available": ([], C.c_int),
+            "gf_comm_unique_id": ([P], C.c_int),
+            "gf_comm_create": ([P, i32, i32, C.c_int, C.POINTER(P)], C.c_int),
+            "gf_comm_create_all": ([i32, P, P], C.c_int),
+            "gf_comm_destroy": ([P], None),
+            "gf_comm_info": ([P, pi32, pi32, C.POINTER(C.c_int)], C.c_int),
+            "gf_comm_last_error": ([P], C.c_char_p),
+            "gf_comm_check": ([P], C.c_int),
+            "gf_knn_exchange_batch": ([P, P, i32, P, i32, P], C.c_int),
+            "gf_knn_exchange_strings_batch": ([P, P, i32, i64, P, i32, P], C.c_int),
+            "gf_knn_exchange_group": ([i32, P, P, i32, P, i32, P], C.c_int),
         }
         for name, (argt, rest) in sig.items():
             fn = getattr(L, name)

@@ -222,6 +222,7 @@ extern "C" const char* gf_status_string(int s) {
     case GF_ERR_NOMEM: return "out of device memory";
     case GF_ERR_LAYERS: return "candidate layers <= 0 (reference: System.exit(1))";
     case GF_ERR_ALIGN: return "x/y not 16-byte aligned";
+    case GF_ERR_COMM: return "RCCL error (see gf_comm_last_error)";
     default: return "unknown status";
   }
 }
@@ -607,10 +608,12 @@ extern "C" int gf_shard_by_columns(gf_ctx* ctx, const gf_grid* g, const gf_point
 
 extern "C" int gf_gather_points(gf_ctx* ctx, const gf_points* pts, const uint32_t* perm, int64_t begin, int64_t end,
                                 double* x, double* y, int64_t* objID, int64_t* ts) {
-  if (!ctx || !pts || !perm || begin < 0 || end < begin || (objID && !pts->objID) || (ts && !pts->ts))
-    return set_err(ctx, GF_ERR_ARG, "gf_gather_points: bad argument");
-  int st = bind(ctx);
+  if (!ctx || !pts || !perm || begin < 0 || end < begin || end > pts->n || (objID && !pts->objID) ||
+      (ts && !pts->ts))
+    return set_err(ctx, GF_ERR_ARG, "gf_gather_points: bad argument (need 0 <= begin <= end <= n)");
+  int st = check_points(ctx, pts);
   if (st) return st;
+  if ((st = bind(ctx))) return st;
   GF_HIP_CHECK(ctx, launch_gather_points(ctx->stream, *pts, perm, begin, end - begin, x, y, objID, ts));
   return GF_OK;
 }
@@ -1332,9 +1335,10 @@ extern "C" void gf_knn_plan_destroy(gf_knn_plan* P) {
   }
   if (P->tmp_result) hipFree(P->tmp_result);
   if (P->host_result) hipHostFree(P->host_result);
-  for (void* q : {(void*)P->ring_off, (void*)P->vert_off, (void*)P->vx, (void*)P->vy, (void*)P->ring_env,
-                  (void*)P->maybe_i[0], (void*)P->maybe_i[1]})
+  for (void* q : {(void*)P->ring_off, (void*)P->vert_off, (void*)P->vx, (void*)P->vy, (void*)P->ring_env})
     if (q) hipFree(q);
+  for (uint32_t* m : P->maybe_i)  // one survivor buffer per stream (depth 4: three)
+    if (m) hipFree(m);
   delete P;
 }
 
@@ -1362,7 +1366,7 @@ static int knn_alloc_candidates(gf_knn_plan* P, int64_t cap) {
   // queued windows may still read the old buffers (the k > kMaxK path queues without host reads)
   GF_HIP_CHECK(P->ctx, hipStreamSynchronize(P->ctx->stream));
   if (int e = sync_aux(P->ctx)) return e;
-  for (int j = 0; j < 4; ++j)  // lanes 1.. only once pipelining allocated them
+  for (int j = 0; j < (int)std::size(P->lane); ++j)  // lanes 1.. only once pipelining allocated them
     if ((j == 0 || P->lane[j].st) && (st = knn_alloc_lane(P, j, cap))) return st;
   P->cap = cap;
   return GF_OK;

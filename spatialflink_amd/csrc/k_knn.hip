@@ -1574,8 +1574,9 @@ __global__ __launch_bounds__(kStrMergeT) void knn_merge_strings_kernel(int32_t k
       const gf_knn_header* h = (const gf_knn_header*)rec(r);
       s_off[r] = off;
       off += h->status == 0 ? h->n : 0;
-      st = h->status > st ? h->status : st;
-      if (h->status == 0 && side_of(rec(r), k)->status != 0) st = GF_KNN_STATUS_FOREIGN_KEYS;  // Strings missing
+      // a flagged input (its rank's window needs the exact re-evaluation) or Strings that did not
+      // fit: the merged record holds other ranks' keys, so no caller could re-evaluate it -- 2
+      if (h->status != 0 || side_of(rec(r), k)->status != 0) st = GF_KNN_STATUS_FOREIGN_KEYS;
     }
     s_off[nrec] = off;
     s_status = st;

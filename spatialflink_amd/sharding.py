@@ -266,6 +266,123 @@ def allgather_knn_records_batch(records, k: int, results, group=None, ctx=None):
     return results
 
 
+class Comm:
+    """An RCCL communicator behind the C ABI (gf_comm_*): the transport of the kNN record exchange
+    the Java drop-in uses, so the exchange measured by bench.py is the same code.
+
+    Comm.from_group(device): one process per GPU -- rank 0's gf_comm_unique_id goes to every rank
+    over the job's control plane (torch.distributed broadcast_object_list: gloo or nccl), then
+    gf_comm_create (ncclCommInitRank).  Comm.single(device): a one-rank communicator.
+    Comm.create_all(devices): one process driving several GPUs (ncclCommInitAll)."""
+
+    def __init__(self, handle, device: int):
+        self.handle = handle
+        self.device = int(device)
+        n, r, d = C.c_int32(), C.c_int32(), C.c_int()
+        _lib.check(_lib.lib().gf_comm_info(handle, C.byref(n), C.byref(r), C.byref(d)), None, "gf_comm_info")
+        self.nranks, self.rank = n.value, r.value
+
+    @staticmethod
+    def available() -> bool:
+        return bool(_lib.lib().gf_comm_available())
+
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = (C.c_uint8 * _lib.GF_COMM_ID_BYTES)()
+        st = _lib.lib().gf_comm_unique_id(buf)
+        if st:
+            raise _lib.GeoFlinkError(st, "gf_comm_unique_id: " + (_lib.lib().gf_comm_last_error(None) or b"").decode())
+        return bytes(buf)
+
+    @classmethod
+    def create(cls, uid: bytes, nranks: int, rank: int, device: int) -> "Comm":
+        h = C.c_void_p()
+        idb = (C.c_uint8 * _lib.GF_COMM_ID_BYTES).from_buffer_copy(uid)
+        st = _lib.lib().gf_comm_create(idb, int(nranks), int(rank), int(device), C.byref(h))
+        if st:
+            raise _lib.GeoFlinkError(st, "gf_comm_create: " + (_lib.lib().gf_comm_last_error(None) or b"").decode())
+        return cls(h, device)
+
+    @classmethod
+    def single(cls, device: int) -> "Comm":
+        return cls.create(cls.unique_id(), 1, 0, device)
+
+    @classmethod
+    def from_group(cls, device: int, group=None) -> "Comm":
+        import torch.distributed as dist_
+
+        obj = [cls.unique_id() if dist_.get_rank(group) == 0 else None]
+        dist_.broadcast_object_list(obj, src=0, group=group)
+        return cls.create(obj[0], dist_.get_world_size(group), dist_.get_rank(group), device)
+
+    @classmethod
+    def create_all(cls, devices):
+        devs = (C.c_int * len(devices))(*devices)
+        hs = (C.c_void_p * len(devices))()
+        st = _lib.lib().gf_comm_create_all(len(devices), devs, hs)
+        if st:
+            raise _lib.GeoFlinkError(st, "gf_comm_create_all: " + (_lib.lib().gf_comm_last_error(None) or b"").decode())
+        return [cls(C.c_void_p(h), d) for h, d in zip(hs, devices)]
+
+    def check(self, st, ctx, what):
+        if st:
+            detail = (_lib.lib().gf_comm_last_error(self.handle) or b"").decode()
+            _lib.check(st, ctx, f"{what}: {detail}" if detail else what)
+
+    def exchange_batch(self, records, k: int, results, ctx=None):
+        """gf_knn_exchange_batch: this rank's [nwin, rb] uint8 device records -> nwin merged records
+        (`results`: device tensor or an int address of mapped pinned memory), identical on every
+        rank.  Async on ctx's stream (default: the thread's context)."""
+        if ctx is None:
+            ctx = _lib.context(records.device.index)
+        out = results if isinstance(results, int) else results.data_ptr()
+        self.check(_lib.lib().gf_knn_exchange_batch(self.handle, ctx.handle, int(k), records.data_ptr(),
+                                                    int(records.shape[0]), out), ctx.handle, "gf_knn_exchange_batch")
+        return results
+
+    def exchange_strings_batch(self, records, k: int, cap_bytes: int, dictionary, results):
+        """gf_knn_exchange_strings_batch: the String-objID form (records carry their Strings)."""
+        out = results if isinstance(results, int) else results.data_ptr()
+        self.check(_lib.lib().gf_knn_exchange_strings_batch(self.handle, dictionary.handle, int(k), int(cap_bytes),
+                                                            records.data_ptr(), int(records.shape[0]), out),
+                   dictionary.ctx.handle, "gf_knn_exchange_strings_batch")
+        return results
+
+    def destroy(self):
+        if self.handle:
+            _lib.lib().gf_comm_destroy(self.handle)
+            self.handle = None
+
+
+def open_comm(device: int, backend: str, mode: str = "auto", group=None):
+    """The N > 1 kNN exchange's transport -> (Comm or None, description).  mode "rccl": the C ABI's
+    communicator (gf_comm_create over the group's ranks) -- what the Java drop-in uses; "torch":
+    torch.distributed's all_gather_into_tensor + gf_knn_merge_dev_batch; "auto": rccl on the nccl
+    backend, torch on gloo (several ranks on one GPU, where RCCL refuses a duplicate device), and
+    torch -- reported in the description -- if the communicator cannot be built."""
+    if mode == "torch" or (mode == "auto" and backend != "nccl"):
+        return None, "torch.distributed all_gather_into_tensor + gf_knn_merge_dev_batch"
+    try:
+        c = Comm.from_group(device, group)
+        return c, "gf_knn_exchange_batch (RCCL ncclAllGather through the C ABI + gf_knn_merge_dev_batch)"
+    except Exception as e:  # noqa: BLE001
+        if mode == "rccl":
+            raise
+        return None, f"torch.distributed all_gather_into_tensor (gf_comm_create failed: {e})"
+
+
+def exchange_group(comms, ctxs, records, k: int, results):
+    """gf_knn_exchange_group: one thread drives every communicator of a create_all clique."""
+    n = len(comms)
+    hc = (C.c_void_p * n)(*[c.handle.value if isinstance(c.handle, C.c_void_p) else c.handle for c in comms])
+    hx = (C.c_void_p * n)(*[x.handle.value if isinstance(x.handle, C.c_void_p) else x.handle for x in ctxs])
+    rp = (C.c_void_p * n)(*[r.data_ptr() for r in records])
+    op = (C.c_void_p * n)(*[o if isinstance(o, int) else o.data_ptr() for o in results])
+    st = _lib.lib().gf_knn_exchange_group(n, hc, hx, int(k), rp, int(records[0].shape[0]), op)
+    comms[0].check(st, ctxs[0].handle, "gf_knn_exchange_group")
+    return results
+
+
 def string_record_bytes(k: int, cap_bytes: int) -> int:
     """Bytes of a string record (a kNN record + the Strings of its dictionary objIDs)."""
     return int(_lib.lib().gf_knn_string_record_bytes(int(k), int(cap_bytes)))

@@ -406,11 +406,10 @@ class PointPointKNNQuery(SpatialOperator):
         addr = record if isinstance(record, int) else record.data_ptr()
         # depth >= 3 launches windows on the plan's other streams, which do not wait for the
         # context stream (torch's current stream, where this window's tensors were produced):
-        # the first enqueue of a window orders those streams after it (gf_ctx_fork); a window
-        # seen before is complete (later enqueues of it pay nothing)
-        if self._depth.get(self._pv(plan), 1) >= 3 and not window.extra.get("gf_fenced"):
+        # every enqueue orders those streams after it (gf_ctx_fork records one event), so a
+        # window refilled in place on torch's stream is complete before any kernel reads it
+        if self._depth.get(self._pv(plan), 1) >= 3:
             _lib.check(_lib.lib().gf_ctx_fork(ctx.handle), ctx.handle, "gf_ctx_fork")
-            window.extra["gf_fenced"] = True
         _lib.check(_lib.lib().gf_knn_enqueue(plan, C.byref(pts), C.c_void_p(addr)), ctx.handle, "gf_knn_enqueue")
 
     def finish(self, window: PointWindow, queryPoint: Point, queryRadius: float, k: int, raw: bytes) -> KNNResult:

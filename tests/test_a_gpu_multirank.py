@@ -32,13 +32,17 @@ def _free_port():
     return p
 
 
-def _run_two_ranks(extra):
+def _run_two_ranks(extra, launcher=False):
+    """bench.py --gpus 2 as the user runs it: bench.py itself starts the two ranks
+    (torch.distributed.run as its child).  launcher=True: the driver's form, torchrun in front."""
     import torch
 
     assert not torch.cuda.is_initialized(), "start the ranks before this process touches the GPU"
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
-           "--gpus", "2", "--dist-backend", "gloo", "--no-cpu-baseline"] + extra
+    pre = [sys.executable]
+    if launcher:
+        pre += ["-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                "--master-addr", "127.0.0.1", "--master-port", str(_free_port())]
+    cmd = pre + [os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dist-backend", "gloo", "--no-cpu-baseline"] + extra
     env = dict(os.environ, OMP_NUM_THREADS="4")
     p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=400)
     assert p.returncode == 0, p.stdout[-3000:] + p.stderr[-6000:]
@@ -48,10 +52,10 @@ def _run_two_ranks(extra):
 
 
 @pytest.mark.timeout(900)
-@pytest.mark.parametrize("pipeline", [3, 2, 4])
-def test_knn_two_ranks_verified(pipeline):
+@pytest.mark.parametrize("pipeline,launcher", [(3, False), (2, False), (4, False), (3, True)])
+def test_knn_two_ranks_verified(pipeline, launcher):
     line = _run_two_ranks(["--points", "400000", "--steps", "9", "--warmup", "3", "--windows", "4",
-                           "--exchange-batch", "2", "--pipeline", str(pipeline)])
+                           "--exchange-batch", "2", "--pipeline", str(pipeline)], launcher=launcher)
     assert line["n_gpus"] == 2 and line["verified_vs_oracle"] is True
     assert line["config"]["points_per_window"] == 800_000
 

@@ -149,3 +149,25 @@ def test_gpu_calls_fail_loudly_without_device():
         pytest.skip("a device is visible")
     with pytest.raises(Exception):
         _lib.Context(0)
+
+
+def test_comm_entry_points_without_gpu():
+    """The RCCL entry points load lazily (librccl.so.1 dlopen on first use) and refuse bad
+    arguments before touching RCCL or a device."""
+    import ctypes as C
+
+    from spatialflink_amd import _lib
+
+    L = _lib.lib()
+    assert L.gf_comm_available() in (0, 1)
+    if not L.gf_comm_available():
+        assert L.gf_comm_last_error(None)
+    h = C.c_void_p()
+    uid = (C.c_uint8 * _lib.GF_COMM_ID_BYTES)()
+    assert L.gf_comm_create(uid, 0, 0, 0, C.byref(h)) == _lib.GF_ERR_ARG
+    assert L.gf_comm_create(uid, 2, 2, 0, C.byref(h)) == _lib.GF_ERR_ARG
+    assert L.gf_comm_create(None, 1, 0, 0, C.byref(h)) == _lib.GF_ERR_ARG
+    assert L.gf_comm_unique_id(None) == _lib.GF_ERR_ARG
+    assert L.gf_knn_exchange_batch(None, None, 50, None, 1, None) == _lib.GF_ERR_ARG
+    assert L.gf_knn_exchange_group(0, None, None, 50, None, 1, None) == _lib.GF_ERR_ARG
+    assert L.gf_status_string(_lib.GF_ERR_COMM).decode().startswith("RCCL")

@@ -131,6 +131,11 @@ def shim(gpu):
     S.shim_geojson_parse.argtypes = [P, C.c_char_p, i64, P, P, P, P, P, i64, P, P, P]
     S.shim_pinned_alloc.argtypes = [i64, pp]
     S.shim_pinned_free.argtypes = [P]
+    S.shim_comm_unique_id.argtypes = [P]
+    S.shim_comm_create.argtypes = [P, P, i32, i32, pp]
+    S.shim_comm_create_all.argtypes = [i32, P, P]
+    S.shim_comm_destroy.argtypes = [P]
+    S.shim_knn_window_sharded.argtypes = [P, P, P, P, P, i64, i64, P, P, P, P]
     return S
 
 
@@ -209,6 +214,47 @@ def test_knn_window(shim, ctx, oracle_mod, k, gn):
             np.testing.assert_array_equal(od.view(np.int64), ed.view(np.int64))
             np.testing.assert_array_equal(oi, ei)
     finally:
+        shim.shim_knn_destroy(plan)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("form", ["rank", "all"])
+def test_knn_window_sharded_one_rank(shim, ctx, oracle_mod, form):
+    """knnWindowSharded (the multi-GPU drop-in: the windowAll merge as the RCCL record exchange of
+    the C ABI) on a one-rank communicator -- ncclCommInitRank from a unique id, or ncclCommInitAll
+    -- vs the oracle, with a nonzero index base and a window that overflows the candidate buffer
+    (1.1M points stacked on the query point: the record is flagged, every rank re-evaluates
+    exactly and the ranks exchange again)."""
+    g, og = grid(500), oracle_mod.grid(500, *BEIJING)
+    plan, comm = P(), P()
+    _ok(shim, ctx, shim.shim_knn_plan(ctx, C.byref(g), QPOINT[0], QPOINT[1], 0.5, 50, C.byref(plan)), "plan")
+    if form == "rank":
+        uid = (C.c_uint8 * 128)()
+        assert shim.shim_comm_unique_id(uid) == 0
+        _ok(shim, ctx, shim.shim_comm_create(ctx, uid, 1, 0, C.byref(comm)), "commCreate")
+    else:
+        devs, hs = (C.c_int * 1)(0), (P * 1)()
+        assert shim.shim_comm_create_all(1, devs, hs) == 0
+        comm = P(hs[0])
+    try:
+        rng = np.random.default_rng(9)
+        for seed, n, base, stacked in ((11, 400_000, 0, 0), (12, 300_000, 1_000, 0), (13, 100_000, 7, 1_100_000)):
+            x, y = oracle_mod.java_random_points(seed, n, *BEIJING)
+            if stacked:
+                x = np.concatenate([x, np.full(stacked, QPOINT[0])])
+                y = np.concatenate([y, np.full(stacked, QPOINT[1])])
+            o = (rng.permutation(len(x)) % max(1, len(x) * 2 // 3)).astype(np.int64)
+            oo = np.zeros(50, np.int64); od = np.zeros(50); oi = np.zeros(50, np.int64); m = i32()
+            st = shim.shim_knn_window_sharded(plan, comm, _a(x), _a(y), _a(o), len(x), base, _a(oo), _a(od), _a(oi),
+                                              C.byref(m))
+            _ok(shim, ctx, st, "knnWindowSharded")
+            est, eo, ed, ei = oracle_mod.knn(og, x, y, o, *QPOINT, 0.5, 50)
+            assert est == 0
+            np.testing.assert_array_equal(oo[:m.value], eo)
+            np.testing.assert_array_equal(od[:m.value].view(np.int64), ed.view(np.int64))
+            np.testing.assert_array_equal(oi[:m.value], ei + base)
+    finally:
+        shim.shim_comm_destroy(comm)
         shim.shim_knn_destroy(plan)
 
 

@@ -809,8 +809,13 @@ def bench_sliding(args):
     lag = 1 if depth == 2 else 0
     push = L.gf_knn_sliding_push
 
+    comm, xdesc = sharding.open_comm(dev, args.dist_backend, args.exchange) if world > 1 else (None, None)
+
     def exchange(lo, hi):  # windows [lo, hi]: one all-gather + one merge launch
-        sharding.allgather_knn_records_batch(recs[lo:hi + 1], k, out.ptr(lo))
+        if comm is not None:  # the C ABI's RCCL communicator (gf_knn_exchange_batch)
+            comm.exchange_batch(recs[lo:hi + 1], k, out.ptr(lo), ctx=ctx)
+        else:
+            sharding.allgather_knn_records_batch(recs[lo:hi + 1], k, out.ptr(lo))
 
     def step(i, first):
         dst = recs[i].data_ptr() if world > 1 else out.ptr(i)
@@ -988,7 +993,7 @@ def bench_sliding(args):
                         "window_points": window_pts, "size_over_slide": W, "pane_points_per_gpu": pane_pts,
                         "k": k, "radius": args.radius, "grid": grid_n, "windows_in_flight": depth,
                         "parallelism": f"cell-column shards x{world}" + (" + RCCL all-gather top-k" if world > 1 else ""),
-                        "exchange_batch": B if world > 1 else None},
+                        "exchange_batch": B if world > 1 else None, "exchange": xdesc},
              "roofline": {"bound": "hbm", "kernel": "knn_fused (scan of pane i + select of pane i-1)",
                           "achieved": round(16.0 * pane_pts / avg / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                           "frac": round(16.0 * pane_pts / avg / 1e9 / HBM_PEAK_GBS, 4), "traffic": traffic,
@@ -1001,6 +1006,8 @@ def bench_sliding(args):
              "cpu_baseline": cpu, "verified_vs_whole_window_and_oracle": verified}
         print(json.dumps(d), flush=True)
     L.gf_knn_sliding_destroy(eng)
+    if comm is not None:
+        comm.destroy()
     if world > 1:
         dist.destroy_process_group()
 
