@@ -554,18 +554,18 @@ int gf_geojson_parse(gf_ctx* ctx, gf_objid_dict* dict, const char* text, int64_t
 /* ---- join (sync) --------------------------------------------------------------------
  * JoinQuery.getReplicatedPointQueryStream + PointPointJoinQuery.windowBased
  * (JoinQuery.java:73-90, PointPointJoinQuery.java:124-183).  pairs: device uint32[2*cap]
- * (ordinary idx, query idx), unordered.  *npairs = pairs found; GF_ERR_CAPACITY if > cap.
- * (Rare: when the window's output regions -- sized from the context's previous join -- and the
- * spill could not hold it, GF_ERR_CAPACITY comes with *npairs = cap + 1 even if the pairs fit; the
- * retry with a larger buffer sizes its regions from this call's exact per-block counts.) */
+ * (ordinary idx, query idx), unordered.  *npairs = pairs found; GF_ERR_CAPACITY (with *npairs =
+ * the exact count) if and only if that count > cap: the window's output regions are sized from
+ * the context's previous join, and the pairs of a block that outgrows its region go to a device
+ * spill sized so that every window whose pairs fit cap completes in one call. */
 int gf_join_pp(gf_ctx* ctx, const gf_grid* ugrid, const gf_grid* qgrid, const gf_points* ordinary,
                const gf_points* query, double r, int approximate, int metric, uint32_t* pairs,
                int64_t cap, int64_t* npairs);
 /* The same window join without a host wait: every launch stream-ordered on the context stream,
  * the pair count written by the last kernel to *total (device or mapped pinned memory), so the
  * next window's launches queue behind this one.  Pairs past cap are not written: the caller
- * re-runs the window with a larger buffer when *total > cap (*total = cap + 1 in gf_join_pp's
- * rare region case above).  (r == 0 -- every cell a key --
+ * re-runs the window with a larger buffer when *total > cap (*total = the exact count).  (r == 0
+ * -- every cell a key --
  * takes the synchronous path and then stores *total.) */
 int gf_join_pp_async(gf_ctx* ctx, const gf_grid* ugrid, const gf_grid* qgrid, const gf_points* ordinary,
                      const gf_points* query, double r, int approximate, int metric, uint32_t* pairs,

@@ -5,10 +5,10 @@ points on the 1000 x 1000 Beijing grid, r = 0.001 -> ~14 ordinary and ~1.4 query
 
 The C4 bench window spreads 10M points over the whole grid; here 400K x 40K points are confined to
 a 0.42 x 0.30 degree box (200 x 143 cells), which is the same density per cell, so the band probe's
-staged-band sizes, per-block regions, spill, the GF_ERR_CAPACITY retry and the fix-up copy run at
+staged-band sizes, per-block regions, spill and the fix-up copy run at
 the bench's occupancy.  Consecutive windows of DIFFERENT densities run on one context: each call
 sizes its output regions from the previous call's pairs per point of every block, so a denser
-window after a sparse one overflows its regions (overflow area / capacity retry), a sparser one
+window after a sparse one overflows its regions (the overflow area in the spill), a sparser one
 leaves long region tails (holes filled by the fix-up copy)."""
 import ctypes as C
 
@@ -76,8 +76,8 @@ def test_join_c4_density_reference_shaped(sf, oracle_mod):
 def test_join_c4_density_window_sequence(sf, oracle_mod):
     """Windows of density 1, 2, 0.25, clustered, 1 on ONE context through the raw C ABI with the
     capacity set to exactly the window's pair count: regions sized from the previous window's
-    per-block history overflow (denser) or leave holes (sparser); a GF_ERR_CAPACITY answer must
-    carry a count >= the pairs (the region case: cap + 1), and the retry returns every pair."""
+    per-block history overflow (denser) or leave holes (sparser), and every window must still
+    complete in ONE call (GF_OK, every pair): GF_ERR_CAPACITY only when the pairs exceed cap."""
     import torch
 
     from spatialflink_amd import _lib
@@ -99,8 +99,7 @@ def test_join_c4_density_window_sequence(sf, oracle_mod):
             n = C.c_int64()
             st = L.gf_join_pp(ctx.handle, C.byref(g.c_grid), C.byref(g.c_grid), C.byref(po), C.byref(pq), R, 0, 0,
                               buf.data_ptr(), cap, C.byref(n))
-            if st == _lib.GF_ERR_CAPACITY:
-                assert n.value == cap + 1, f"window {j}: capacity answer {n.value} for {len(exp)} pairs"
+            if st == _lib.GF_ERR_CAPACITY:  # (a failure: counted and reported below)
                 retries += 1
                 continue
             _lib.check(st, ctx.handle, "gf_join_pp")
@@ -109,14 +108,25 @@ def test_join_c4_density_window_sequence(sf, oracle_mod):
         got = buf[: 2 * len(exp)].cpu().numpy().view(np.uint32).astype(np.int64).reshape(-1, 2)
         np.testing.assert_array_equal(sorted_pairs(got), exp, err_msg=f"window {j} ({kind})")
         assert buf[-2:].cpu().tolist() == [-1, -1]  # nothing written past cap
-    # every window must finish within one retry (the retry sizes regions from exact counts)
-    assert retries <= 6
+    # cap == the exact count: no window may be answered GF_ERR_CAPACITY
+    assert retries == 0, f"{retries} GF_ERR_CAPACITY answers for windows whose pairs fit"
+    # a buffer one pair short: GF_ERR_CAPACITY with the exact count
+    ox, oy, qx, qy = window(oracle_mod, sf, 1.0, 499)
+    exp = expected(oracle_mod, og, ox, oy, qx, qy)
+    wo, wq = win(sf, ox, oy), win(sf, qx, qy)
+    po, pq = wo.c_struct(), wq.c_struct()
+    buf = torch.full((2 * len(exp),), -1, dtype=torch.int32, device="cuda")
+    n = C.c_int64()
+    st = L.gf_join_pp(ctx.handle, C.byref(g.c_grid), C.byref(g.c_grid), C.byref(po), C.byref(pq), R, 0, 0,
+                      buf.data_ptr(), len(exp) - 1, C.byref(n))
+    assert st == _lib.GF_ERR_CAPACITY and n.value == len(exp)
+    assert buf[-2:].cpu().tolist() == [-1, -1]  # nothing written past cap
 
 
 def test_join_c4_density_async_queue(sf, oracle_mod):
     """The same densities queued back to back with gf_join_pp_async on one context (no host wait
     between windows, counts in device memory), each with capacity = its exact pair count; a
-    window whose regions could not hold it reports cap + 1 and is re-run -- then == the oracle."""
+    window completes in its one call (no re-run) and == the oracle."""
     import torch
 
     from spatialflink_amd import _lib
@@ -140,13 +150,7 @@ def test_join_c4_density_async_queue(sf, oracle_mod):
                                       0, bufs[j].data_ptr(), len(e), totals[j].data_ptr()), ctx.handle, "async")
     ctx.synchronize()
     for j, (wo, wq, e) in enumerate(data):
-        n = int(totals[j].item())
-        if n == len(e) + 1:  # the region case: re-run (the count is a capacity answer)
-            po, pq = structs[j]
-            _lib.check(L.gf_join_pp_async(ctx.handle, C.byref(g.c_grid), C.byref(g.c_grid), C.byref(po), C.byref(pq), R,
-                                          0, 0, bufs[j].data_ptr(), len(e), totals[j].data_ptr()), ctx.handle, "retry")
-            ctx.synchronize()
-            n = int(totals[j].item())
+        n = int(totals[j].item())  # one call per window: capacity == the pairs always completes
         assert n == len(e), f"window {j} ({kinds[j]}): {n} pairs, expected {len(e)}"
         got = bufs[j][: 2 * n].cpu().numpy().view(np.uint32).astype(np.int64).reshape(-1, 2)
         np.testing.assert_array_equal(sorted_pairs(got), e, err_msg=f"window {j} ({kinds[j]})")

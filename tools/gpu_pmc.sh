@@ -21,7 +21,9 @@ for p in ${PASSES:-fetch write lds occ}; do
     fetch) run fetch FETCH_SIZE ;;
     write) run write WRITE_SIZE ;;
     lds) run lds SQ_WAVES SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES ;;
-    occ) run occ SQ_LEVEL_WAVES SQ_ACCUM_PREV_HIRES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE GRBM_COUNT ;;
+    # occupancy: mean resident waves = SQ_WAVE_CYCLES over the kernel's busy cycles (tools/pmc_table.py);
+    # SQ_LEVEL_WAVES / SQ_ACCUM_PREV_HIRES read 0 on gfx950 under rocprofv3 (r02-r04 files), so not used
+    occ) run occ SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE GRBM_COUNT ;;
     mem) run mem SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SMEM SQ_INST_CYCLES_VMEM SQ_WAIT_INST_LDS SQ_INSTS_BRANCH SQ_INSTS_FLAT SQ_WAVES ;;
   esac
 done

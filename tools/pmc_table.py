@@ -39,6 +39,13 @@ def pmc(dirpath):
                 d["valu_issue_share"] = 4.0 * m["SQ_INSTS_VALU"] / (1024.0 * cyc)
         if m.get("SQ_WAVE_CYCLES") and "SQ_WAIT_ANY" in m:
             d["wait_any_per_wave_cycle"] = m["SQ_WAIT_ANY"] / m["SQ_WAVE_CYCLES"]
+        if m.get("SQ_WAVE_CYCLES") and m.get("GRBM_GUI_ACTIVE"):
+            # measured occupancy: SQ_WAVE_CYCLES (quad-cycles, summed over every wave of the
+            # dispatch) x 4 = wave-cycles; over the dispatch's busy cycles per XCD (GRBM_GUI_ACTIVE / 8)
+            # and the 256 CUs x 4 SIMDs -> mean resident waves per SIMD over the kernel's lifetime
+            # (ramp-up and tail included, so below the launch's steady-state residency)
+            d["mean_waves_per_simd"] = 4.0 * m["SQ_WAVE_CYCLES"] / (m["GRBM_GUI_ACTIVE"] / 8.0 * 1024.0)
+            d["occupancy_basis"] = "4 * SQ_WAVE_CYCLES / (GRBM_GUI_ACTIVE / 8 * 256 CUs * 4 SIMDs)"
         out[k] = d
     return out
 

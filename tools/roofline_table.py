@@ -70,6 +70,29 @@ def traffic_of(pmc, main, allk):
     return tot, rows
 
 
+def _short(k):
+    """'void gf::knn_fused_kernel<0, 1>(gf::KnnScanArgs, ...) [clone .kd]' -> 'knn_fused_kernel<0, 1>'"""
+    k = re.sub(r"^void ", "", k.split("(")[0])
+    return k.replace("gf::", "")
+
+
+def occupancy_of(pmc, main, rnd):
+    """The main kernel's measured mean resident waves per SIMD (tools/pmc_table.py: SQ_WAVE_CYCLES over
+    the busy cycles) and the compiler's register bound (profiles/<rnd>_resource_usage.json)."""
+    meas = [(k, v["mean_waves_per_simd"]) for k, v in pmc.items() if re.search(main, k) and "mean_waves_per_simd" in v]
+    ru = os.path.join(ROOT, "profiles", f"{rnd}_resource_usage.json")
+    regs = {}
+    if os.path.exists(ru):
+        with open(ru) as fh:
+            regs = {_short(k): v for k, v in json.load(fh)["kernels"].items()}
+    out = []
+    for k, w in meas:
+        r = regs.get(_short(k), {})
+        out.append({"kernel": _short(k), "mean_waves_per_simd": round(w, 2),
+                    "vgpr": r.get("vgpr"), "reg_bound_waves_per_simd": r.get("waves_per_simd_regs")})
+    return out or None
+
+
 def main():
     rnd = sys.argv[1]
     out = sys.argv[sys.argv.index("--out") + 1] if "--out" in sys.argv else os.path.join(ROOT, "profiles", f"{rnd}_roofline")
@@ -87,12 +110,13 @@ def main():
         wpl = d["config"].get("windows_per_launch", 1) or 1  # batched launches carry several windows
         row = {"workload": w, "ms_per_step": d["ms_per_step"], "algorithmic_MB": round(bpl / 1e6, 1) if bpl else None,
                "frac_line": r.get("frac"), "frac_recomputed": round(frac, 4) if frac else None,
-               "traffic_MB": None, "traffic_ratio": None, "pmc": None, "kernels": None}
+               "traffic_MB": None, "traffic_ratio": None, "pmc": None, "kernels": None, "occupancy": None}
         tag, main, allk = tag_of(w)
         p = os.path.join(ROOT, "profiles", f"{rnd}_{tag}_pmc.json") if tag else None
         if p and os.path.exists(p):
             with open(p) as fh:
                 pm = json.load(fh)["pmc"]
+            row["occupancy"] = occupancy_of(pm, main, rnd)
             t, rows = traffic_of(pm, main, allk)
             if t:
                 t /= wpl
@@ -103,12 +127,19 @@ def main():
         json.dump(res, f, indent=1)
     with open(out + ".md", "w") as f:
         f.write(f"# {rnd} roofline table (tools/roofline_table.py {rnd})\n\n")
-        f.write("| workload | ms / window | algorithmic MB | frac (line) | frac (recomputed) | PMC traffic MB | traffic / algorithmic |\n")
-        f.write("|---|---|---|---|---|---|---|\n")
+        f.write("| workload | ms / window | algorithmic MB | frac (line) | frac (recomputed) | PMC traffic MB | "
+                "traffic / algorithmic | main kernel: measured mean waves/SIMD (register bound) |\n")
+        f.write("|---|---|---|---|---|---|---|---|\n")
         for r in res:
+            occ = "; ".join(f"{o['kernel']}: {o['mean_waves_per_simd']} ({o['reg_bound_waves_per_simd']})"
+                            for o in (r["occupancy"] or [])) or "n/a"
             f.write(f"| {r['workload']} | {r['ms_per_step']} | {r['algorithmic_MB']} | {r['frac_line']} | "
                     f"{r['frac_recomputed']} | {r['traffic_MB'] if r['traffic_MB'] is not None else 'n/a'} | "
-                    f"{r['traffic_ratio'] if r['traffic_ratio'] is not None else 'n/a'} |\n")
+                    f"{r['traffic_ratio'] if r['traffic_ratio'] is not None else 'n/a'} | {occ} |\n")
+        f.write("\nOccupancy: mean resident waves per SIMD over the kernel's lifetime = 4 x SQ_WAVE_CYCLES / "
+                "(GRBM_GUI_ACTIVE / 8 x 1024 SIMDs) from the occ PMC pass (ramp-up and tail included); in "
+                "parentheses the compiler's register bound (-Rpass-analysis=kernel-resource-usage, "
+                f"profiles/{rnd}_resource_usage.json) -- LDS and block size can bound a launch lower.\n")
     print(open(out + ".md").read())
 
 
