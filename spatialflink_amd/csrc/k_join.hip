@@ -1270,6 +1270,9 @@ constexpr int kBandMaxSub = 6;       // staged sub-rows f + 2 (f <= 4)
 // sub-column) -- both meaningful only inside the current window -- or, with this bit, the pair's
 // final query index (entries settled at a window's end stay buffered across windows)
 constexpr uint32_t kBandFinal = 0x80000000u;
+#ifndef GF_BAND_SETTLE
+#define GF_BAND_SETTLE 1
+#endif
 struct BandHdr {
   int32_t row;
   uint32_t c1;           // the window's end (wave 0)
@@ -1921,7 +1924,11 @@ __global__ __launch_bounds__(kBandThreads) void join_band_probe_kernel(JoinRowAr
           probe(v.x, v.y, a.soidx[k], lane < qc);
         }
       }
+#if GF_BAND_SETTLE
       settle();  // staged slots change with the next window
+#else
+      if (cnt > 0) flush();  // (A/B: the r04 flush at every window end)
+#endif
       __syncthreads();
       c0 = c1;
     }
