@@ -68,8 +68,33 @@ asan-test: asan
 	    tests/test_oracle.py tests/test_csv_core.py tests/test_geojson_core.py tests/test_csv_oracle.py \
 	    tests/test_geojson_oracle.py tests/test_windows.py
 
+# Host sanitizers over the PRODUCT's host code: every library source built with
+# ASan + UBSan on the host side only (-Xarch_host: the gfx950 device code is the ordinary code --
+# GPU sanitizers are not available on this pool), the shim core and the C oracle instrumented the
+# same way, and tests/native/asan_driver.c driving the dictionary, the pane ring, the ingest host
+# side and the shim's host paths against the oracle.  Built here, run on the GPU box
+# (tools/gpu_asan.sh).  clang's ASan runtime throughout (hipcc instruments with it).
+CLANG      := /opt/rocm/lib/llvm/bin/clang
+HOSTSAN    := -Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined -Xarch_host -fno-sanitize-recover=undefined \
+              -Xarch_host -fno-omit-frame-pointer -Xarch_host -g
+CSAN       := -fsanitize=address,undefined -fno-sanitize-recover=undefined -fno-omit-frame-pointer -g
+ASAN_GPU   := explibs/asan_gpu
+ASAN_OBJS  := $(patsubst $(SRC)/%,$(ASAN_GPU)/obj/%.o,$(SOURCES))
+$(ASAN_GPU)/obj/%.o: $(SRC)/% $(HEADERS)
+	@mkdir -p $(ASAN_GPU)/obj
+	$(HIPCC) $(HIPFLAGS) $(HOSTSAN) -x hip -c $< -o $@
+$(ASAN_GPU)/libgeoflink_hip.so: $(ASAN_OBJS)
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(ASAN_OBJS) -ldl
+$(ASAN_GPU)/asan_driver: tests/native/asan_driver.c integration/jni/geoflink_shim.c integration/jni/geoflink_shim.h \
+                         oracle/geoflink_oracle.c oracle/cpu_scan.c $(ASAN_GPU)/libgeoflink_hip.so
+	$(CLANG) -O1 -std=c11 $(CSAN) -ffp-contract=off -fopenmp -Iinclude -I/opt/rocm/include -D__HIP_PLATFORM_AMD__ \
+	    tests/native/asan_driver.c integration/jni/geoflink_shim.c oracle/geoflink_oracle.c oracle/cpu_scan.c \
+	    -o $@ -L$(ASAN_GPU) -lgeoflink_hip -L/opt/rocm/lib -lamdhip64 -lm -lpthread \
+	    -Wl,-rpath,'$$ORIGIN' -Wl,-rpath,/opt/rocm/lib -Wl,-rpath,/opt/rocm/lib/llvm/lib
+asan-gpu: $(ASAN_GPU)/asan_driver
+
 clean:
 	rm -rf build $(LIB) $(SHIM)
 	$(MAKE) -s -C oracle clean
 
-.PHONY: all oracle shim clean isa trace asan asan-test
+.PHONY: all oracle shim clean isa trace asan asan-test asan-gpu

@@ -1266,13 +1266,7 @@ constexpr int kBandRound = GF_BAND_R;  // candidates per lane per walk round
 #endif
 constexpr bool kBandPair = GF_BAND_PAIR != 0;  // sparse whole-band windows: a lane's two points in one walk
 constexpr int kBandMaxSub = 6;       // staged sub-rows f + 2 (f <= 4)
-// buffer entry .y: a staged slot (band in LDS) or a global sorted query index (unstaged
-// sub-column) -- both meaningful only inside the current window -- or, with this bit, the pair's
-// final query index (entries settled at a window's end stay buffered across windows)
-constexpr uint32_t kBandFinal = 0x80000000u;
-#ifndef GF_BAND_SETTLE
-#define GF_BAND_SETTLE 1
-#endif
+constexpr uint32_t kBandGlobal = 0x80000000u;  // buffer entry: a global sorted query index
 struct BandHdr {
   int32_t row;
   uint32_t c1;           // the window's end (wave 0)
@@ -1664,25 +1658,15 @@ __global__ __launch_bounds__(kBandThreads) void join_band_probe_kernel(JoinRowAr
         if (lds) {
           band_emit(a.out, hd, cnt, [&](uint32_t i) {
             const uint2 v = buf[i];
-            return make_uint2(v.x, (v.y & kBandFinal) ? v.y & ~kBandFinal : ((lds_u32)lq)[v.y]);
+            return make_uint2(v.x, ((lds_u32)lq)[v.y]);
           });
         } else {
           band_emit(a.out, hd, cnt, [&](uint32_t i) {
             const uint2 v = buf[i];
-            return make_uint2(v.x, (v.y & kBandFinal) ? v.y & ~kBandFinal : a.sqidx[v.y]);
+            return make_uint2(v.x, a.sqidx[v.y & ~kBandGlobal]);
           });
         }
         cnt = 0;
-      };
-      // the window ends: its buffered entries get their final query indices in place, and the
-      // buffer carries over to the next window / row segment -- written out only when full (a
-      // flush at every window end wrote ~28 pairs per store instruction on clustered input,
-      // r04 PMC: 72 M stores for 2.05e9 pairs); the lookup stays off the walk's critical path
-      auto settle = [&]() {
-        for (uint32_t i = lane; i < cnt; i += 64) {
-          const uint32_t y = buf[i].y;
-          if (!(y & kBandFinal)) buf[i].y = kBandFinal | (lds ? ((lds_u32)lq)[y] : a.sqidx[y]);
-        }
       };
       // DENSE window (clustered input: ~> 12 candidates per point): each wave-step's 64 points are
       // sorted by (sub-column, sub-row) across the wave first (bitonic over 64 lanes in
@@ -1779,7 +1763,7 @@ __global__ __launch_bounds__(kBandThreads) void join_band_probe_kernel(JoinRowAr
 #endif
               if (hit)
                 buf[cnt + __builtin_amdgcn_mbcnt_hi((uint32_t)(hm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)hm, 0u))] =
-                    make_uint2(pidx, t[i]);
+                    make_uint2(pidx, lds ? t[i] : (t[i] | kBandGlobal));
               cnt += (uint32_t)__popcll(hm);
             }
           }
@@ -1924,21 +1908,12 @@ __global__ __launch_bounds__(kBandThreads) void join_band_probe_kernel(JoinRowAr
           probe(v.x, v.y, a.soidx[k], lane < qc);
         }
       }
-#if GF_BAND_SETTLE
-      settle();  // staged slots change with the next window
-#else
-      if (cnt > 0) flush();  // (A/B: the r04 flush at every window end)
-#endif
+      if (cnt > 0) flush();  // staged slots change with the next window
       __syncthreads();
       c0 = c1;
     }
     pos = se;
   }
-  if (cnt > 0)  // the last settled entries
-    band_emit(a.out, hd, cnt, [&](uint32_t i) {
-      const uint2 v = buf[i];
-      return make_uint2(v.x, v.y & ~kBandFinal);
-    });
   __syncthreads();  // every wave's pairs are counted
   if (sink == 0xdeadbeefu) a.out.bslice[blockIdx.x] = sink;  // keeps experiment builds' work alive
   if (threadIdx.x == 0) {  // write-through, drained before the ticket (see join_region_prep)
