@@ -4,11 +4,11 @@
 # counter group (tools/gpu_pmc.sh: FETCH_SIZE and WRITE_SIZE never share a pass), summarised by
 # tools/pmc_table.py into gpurun_out/pmc_${ROUND}/<tag>.json -> copied to profiles/${ROUND}_<tag>_pmc.json.
 # usage: ROUND=r04 tools/gpu_pmc_round.sh TAG... (default: all)   tags: knn range1m range10m ppoly join
-#        sliding bucket csv geojson polyknn
+#        joinc pjoin sliding bucket csv geojson polyknn
 set -e
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-ROUND=${ROUND:-r04}
+ROUND=${ROUND:-r05}
 COMMON="--steps 5 --warmup 2 --no-cpu-baseline --no-verify"
 OUT=gpurun_out/pmc_${ROUND}
 mkdir -p $OUT
@@ -21,18 +21,20 @@ one() {  # tag kernel-regex passes bench-args...
   cp $OUT/$tag/stats/*kernel_stats.csv $OUT/${tag}_kernel_stats.csv 2>/dev/null || true
   echo "[campaign $tag] ok"
 }
-TAGS=${*:-knn range1m range10m ppoly join sliding bucket csv geojson polyknn}
+TAGS=${*:-knn range1m range10m ppoly join joinc pjoin sliding bucket csv geojson polyknn}
 for t in $TAGS; do
   case $t in
-    knn)      one knn "knn_fused|knn_sample" "fetch write" ;;
-    range1m)  one range1m "range_batch|range_kernel|expand" "fetch write" --workload range --points 1000000 ;;
-    range10m) one range10m "range_kernel|expand" "fetch write" --workload range --points 10000000 ;;
+    knn)      one knn "knn_fused|knn_sample" "fetch write occ" ;;
+    range1m)  one range1m "range_batch|range_kernel|expand" "fetch write occ" --workload range --points 1000000 ;;
+    range10m) one range10m "range_kernel|expand" "fetch write occ" --workload range --points 10000000 ;;
     ppoly)    one ppoly "range_kernel|range_test|expand" "fetch write lds occ" --workload ppoly ;;
     join)     one join "join_|scan1" "fetch write lds occ mem" --workload join ;;
-    sliding)  one sliding "knn_fused|knn_merge|pane_bounds" "fetch write" --workload sliding ;;
-    bucket)   one bucket "radix|scan1|assign" "fetch write lds" --workload bucket ;;
-    csv)      one csv "csv_" "fetch write" --workload csv ;;
-    geojson)  one geojson "csv_|geo" "fetch write" --workload geojson ;;
-    polyknn)  one polyknn "knn_poly|knn_select" "fetch write" --workload polyknn ;;
+    joinc)    one joinc "join_band" "write lds occ mem" --workload join --clustered ;;
+    pjoin)    one pjoin "range_kernel|join_ppoly" "fetch write occ" --workload pjoin ;;
+    sliding)  one sliding "knn_fused|knn_merge|pane_bounds" "fetch write occ" --workload sliding ;;
+    bucket)   one bucket "radix|scan1|assign" "fetch write lds occ" --workload bucket ;;
+    csv)      one csv "csv_" "fetch write occ" --workload csv ;;
+    geojson)  one geojson "csv_|geo" "fetch write lds occ" --workload geojson ;;
+    polyknn)  one polyknn "knn_poly|knn_select" "fetch write occ" --workload polyknn ;;
   esac
 done
