@@ -34,9 +34,9 @@ TAGS = [
     ("range_pp_r0.5_1Mpts", "range1m", r"range_batch|range_kernel", r"range_|expand"),
     ("range_pp_r0.5_10Mpts", "range10m", r"range_kernel", r"range_|expand"),
     ("ppoly_", "ppoly", r"range_kernel", r"range_|expand"),
-    ("join_pp_10Mx1M_r0.001_grid1000_clustered", None, None, None),
+    ("join_pp_10Mx1M_r0.001_grid1000_clustered", "joinc", r"join_band_probe", r"join_band"),
     ("join_pp_", "join", r"join_band_probe|join_row_probe", r"join_|scan1"),
-    ("join_ppoly", None, None, None),
+    ("join_ppoly", "pjoin", r"join_ppoly_count", r"range_|join_ppoly"),
     ("sliding_", "sliding", r"knn_fused", r"knn_|pane"),
     ("bucket_", "bucket", r"radix_scatter", r"radix|scan1|assign"),
     ("csv_", "csv", r"csv_parse", r"csv_|range_|expand|objid"),
