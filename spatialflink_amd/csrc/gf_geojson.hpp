@@ -460,11 +460,13 @@ GF_DHD inline int geo_props(const GeoProps& a, const Src& s, int64_t e, int64_t 
   return kCsvOk;
 }
 
-// steps 2-3 of the map over located members (both paths), in the map's order.  Outlined: once
-// per line, and inlined into the walk it trips an AMDGPU backend bug (an illegal
-// v_cmp_ne_u32_e32 against src_shared_base).
+// steps 2-3 of the map over located members (both paths), in the map's order.  The walk calls it
+// outlined (geo_eval: inlined into the walk it trips an AMDGPU backend bug -- an illegal
+// v_cmp_ne_u32_e32 against src_shared_base); the locator's path inlines the body (geo_eval_body):
+// an outlined call there cost every line a stack frame in scratch -- GeoPos, LineOut and the
+// saved registers, ~270 B of scratch writes per line (r04 PMC: 276 MB written per 1M lines).
 template <class Src>
-GF_DHD GF_NOINLINE int geo_eval(const GeoProps& a, const Src& s, int64_t e, const GeoPos& g, LineOut* o) {
+GF_DHD inline int geo_eval_body(const GeoProps& a, const Src& s, int64_t e, const GeoPos& g, LineOut* o) {
   if (g.V < 0 || s(g.V) != '{') return kCsvMissingField;  // value.toString() / .get("geometry"): NPE
   if (g.escV) return kCsvUnsupported;
   o->ts = 0;
@@ -490,6 +492,10 @@ GF_DHD GF_NOINLINE int geo_eval(const GeoProps& a, const Src& s, int64_t e, cons
   if (g.prV < 0 || s(g.prV) != '{') return kCsvOk;
   if (g.escP && (a.len_ts >= 0 || a.len_obj >= 0)) return kCsvUnsupported;
   return geo_props(a, s, e, g.tsP, g.qP, o);
+}
+template <class Src>
+GF_DHD GF_NOINLINE int geo_eval(const GeoProps& a, const Src& s, int64_t e, const GeoPos& g, LineOut* o) {
+  return geo_eval_body(a, s, e, g, o);
 }
 
 // The slow path: Jackson's strict parse, then member-by-member lookup (jfind) -- exact on any
@@ -789,15 +795,23 @@ GF_DHD inline bool geo_locate(const LBytes& s, int64_t p, int64_t e, const GeoTa
 template <class Src>
 GF_DHD inline int geojson_line(const GeoTabs& gt, const GeoProps& gp, const Src& s, int64_t p, int64_t e, int vlines,
                                LineOut* o) {
-  return eval_geojson_walk(gp, s, p, e, vlines, o);
+  LineOut w{0, 0, 0.0, 0.0, false, {0, 0}};  // (the outlined walk's own: see below)
+  const int st = eval_geojson_walk(gp, s, p, e, vlines, &w);
+  *o = w;
+  return st;
 }
 GF_DHD inline int geojson_line(const GeoTabs& gt, const GeoProps& gp, const LBytes& s, int64_t p, int64_t e,
                                int vlines, bool fast, LineOut* o) {
   if (fast) {
     GeoPos g;
-    if (geo_locate(s, p, e, gt, vlines, &g)) return geo_eval(gp, s, e, g, o);
+    if (geo_locate(s, p, e, gt, vlines, &g)) return geo_eval_body(gp, s, e, g, o);
   }
-  return eval_geojson_walk(gp, s, p, e, vlines, o);
+  // the walk is outlined: it gets its own LineOut, so that the caller's (whose address would
+  // otherwise escape into the call) stays in registers on the locator's path
+  LineOut w{0, 0, 0.0, 0.0, false, {0, 0}};
+  const int st = eval_geojson_walk(gp, s, p, e, vlines, &w);
+  *o = w;
+  return st;
 }
 
 // one entry of the locator's two per-byte tables (geo_tabs_fill)

@@ -174,7 +174,7 @@ __device__ __forceinline__ int eval_csv_line(const CsvArgs& a, const Src& s, int
   return kCsvOk;
 }
 
-__device__ void geo_tabs_fill(const CsvArgs& a, uint64_t* tab, uint64_t* ttab, char* keys) {
+__device__ __forceinline__ void geo_tabs_fill(const CsvArgs& a, uint64_t* tab, uint64_t* ttab, char* keys) {
   for (int b = threadIdx.x; b < 256; b += blockDim.x) geo_tab_entry(b, tab + b, ttab + b);
   for (int i = threadIdx.x; i < kGeoKeys * kGeoPropMax; i += blockDim.x) {
     const int k = i / kGeoPropMax, c = i % kGeoPropMax;
