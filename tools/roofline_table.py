@@ -38,7 +38,9 @@ TAGS = [
     ("join_pp_", "join", r"join_band_probe|join_row_probe", r"join_|scan1"),
     ("join_ppoly", "pjoin", r"join_ppoly_count", r"range_|join_ppoly"),
     ("sliding_", "sliding", r"knn_fused", r"knn_|pane"),
-    ("bucket_", "bucket", r"radix_scatter", r"radix|scan1|assign"),
+    # (the main-kernel regex sets the per-window normalisation: a kernel launched ONCE per window --
+    # K2 runs two scatter passes per window, so the scatter would halve the traffic)
+    ("bucket_", "bucket", r"radix_hist", r"radix|scan1|assign"),
     ("csv_", "csv", r"csv_parse", r"csv_|range_|expand|objid"),
     ("geojson_", "geojson", r"csv_parse", r"csv_|geo|range_|expand|objid"),
 ]
