@@ -17,9 +17,9 @@
  * distance)) with the same PQ order (Comparators.inTuplePointDistanceComparator: largest
  * distance at the head) and the same Point instances the window held.
  *
- * gridArgs are UniformGrid's constructor arguments {n, minX, maxX, minY, maxY} -- the library
- * applies the constructor's own bounds adjustment (UniformGrid.java:74-131), so pass them, not
- * the adjusted getMinX() ... values.
+ * gridArgs are the UniformGrid(int n, minX, maxX, minY, maxY) constructor's arguments
+ * {n, minX, maxX, minY, maxY} (UniformGrid.java:74-85): that constructor keeps the bounds as
+ * given and sets cellLength = (maxX - minX) / n, which gf_grid_make restates.
  */
 package GeoFlink.native_;
 
