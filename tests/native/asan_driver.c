@@ -182,15 +182,15 @@ static void test_sliding(shim_ctx* c) {
       if (pend[i] < 0) continue;
       const int64_t e = pend[i];
       pend[i] = -1;
-      /* window [e - 2000, e): panes e/1000 - 2 and e/1000 - 1 (pane 4 holds nothing) */
+      /* window [e - 2000, e): panes e/1000 - 2 and e/1000 - 1 (pane 4 holds nothing; the first
+       * window, [-1000, 1000), holds pane 0 only) */
       const int64_t p0 = e / 1000 - 2;
-      int64_t lo = p0 * per, hi = (p0 + 2) * per;
-      double* wx = malloc((hi - lo) * 8);
-      double* wy = malloc((hi - lo) * 8);
-      int64_t* wo = malloc((hi - lo) * 8);
+      double* wx = malloc(2 * per * 8);
+      double* wy = malloc(2 * per * 8);
+      int64_t* wo = malloc(2 * per * 8);
       int64_t m2 = 0;
       for (int64_t q = p0; q < p0 + 2; ++q)
-        if (q != 4)
+        if (q >= 0 && q < npane && q != 4)
           for (int64_t t = q * per; t < (q + 1) * per; ++t) { wx[m2] = x[t]; wy[m2] = y[t]; wo[m2] = o[t]; ++m2; }
       int64_t oo[100], oi[100], eo[100], ei[100];
       double od[100], ed[100];
