@@ -251,7 +251,7 @@ __device__ __forceinline__ void queue_append2(bool c0, uint32_t i0, double x0, d
 #endif
 constexpr int kWaveQ = GF_RANGE_WAVEQ;
 static_assert(kWaveQ >= 127, "a round leaves < 64, a half-tile adds <= 64");
-constexpr int kRestIters = (kWaveQ - 64 + 63) / 64;  // entries left after a round, 64 per step
+static_assert((kWaveQ & (kWaveQ - 1)) == 0, "the queue is a ring indexed mod kWaveQ");
 // The bitmap words of the wave's last kWaveRing tiles stay in LDS (a ring, two words per tile),
 // so the bits of points the classification accepts later are OR-ed there (ds_or) and every word
 // reaches global memory once, when its tile leaves the ring or at the end of the stream.  (Each
@@ -259,10 +259,11 @@ constexpr int kRestIters = (kWaveQ - 64 + 63) / 64;  // entries left after a rou
 // wave had already stored: ~5e5 L2 atomics and 21 MB of partial-line writes per C3 window.)
 // Points whose tile already left the ring (sparse stretches) still take the atomic.
 constexpr int kWaveRing = 32;
-struct WaveQ {
+struct WaveQ {  // a ring: entries head .. head + cnt - 1 (mod kWaveQ)
   uint32_t* idx;
   double2* xy;
   uint32_t cnt;
+  uint32_t head;
   unsigned long long* ring;  // [2 * kWaveRing]: tile k's words at 2 (k % kWaveRing) + {0, 1}
   uint32_t ntile;            // tiles pushed so far (wave-uniform)
   uint32_t t0, tstride;      // the wave's first tile and the tile stride (points)
@@ -279,8 +280,9 @@ __device__ __forceinline__ void waveq_round(const RangeArgs& a, const RangeLds& 
                                             uint64_t& hits, uint32_t* lcount) {
   const uint32_t lane = threadIdx.x & 63;
   const bool valid = lane < take;
-  const uint32_t i = q.idx[valid ? lane : 0u];
-  const double2 v = q.xy[valid ? lane : 0u];
+  const uint32_t slot_q = (q.head + (valid ? lane : 0u)) & (uint32_t)(kWaveQ - 1);
+  const uint32_t i = q.idx[slot_q];
+  const double2 v = q.xy[slot_q];
   const int32_t slot = cell_slot<1>(a, L, v.x, v.y);
   // the span table is in LDS whenever the span prefilter runs (host: span_lds): with a global
   // fallback here the two reads merge into one wait on vmcnt too, draining the stream's
@@ -297,25 +299,10 @@ __device__ __forceinline__ void waveq_round(const RangeArgs& a, const RangeLds& 
   }
   hits += (uint64_t)__popcll(__ballot(acc));
   queue_append2(cls == kTest, i, v.x, v.y, false, 0u, 0.0, 0.0, a, lcount);
-  // the rest [take, cnt) moves to the front (all reads before the writes)
-  const uint32_t rest = q.cnt - take;
-  uint32_t ri[kRestIters];
-  double2 rv[kRestIters];
-#pragma unroll
-  for (int k = 0; k < kRestIters; ++k) {
-    const uint32_t r = lane + 64 * k;
-    ri[k] = r < rest ? q.idx[take + r] : 0u;
-    rv[k] = r < rest ? q.xy[take + r] : make_double2(0.0, 0.0);
-  }
-#pragma unroll
-  for (int k = 0; k < kRestIters; ++k) {
-    const uint32_t r = lane + 64 * k;
-    if (r < rest) {
-      q.idx[r] = ri[k];
-      q.xy[r] = rv[k];
-    }
-  }
-  q.cnt = rest;
+  // the ring's head moves past the round (r04 moved the rest [take, cnt) to the front instead: two
+  // LDS reads and two writes per lane per round)
+  q.head = (q.head + take) & (uint32_t)(kWaveQ - 1);
+  q.cnt -= take;
 }
 
 // Tile layout.  kRangeVec (default): lane l holds points t + 2l and t + 2l + 1, read with one
@@ -397,13 +384,13 @@ __device__ __forceinline__ void range_tile(const RangeArgs& a, int64_t t, double
       const bool d = h ? d1 : d0;
       const uint64_t qm = h ? q1 : q0;
       if (d) {
-        const uint32_t pos = wq.cnt + (uint32_t)__popcll(qm & below);
+        const uint32_t pos = (wq.head + wq.cnt + (uint32_t)__popcll(qm & below)) & (uint32_t)(kWaveQ - 1);
         wq.idx[pos] = (uint32_t)(h ? i1 : i0);
         wq.xy[pos] = h ? make_double2(x1, y1) : make_double2(x0, y0);
       }
       wq.cnt += (uint32_t)__popcll(qm);
 #if GF_RANGE_EXP == 1  // experiment build: queued points dropped (no classification rounds)
-      if (wq.cnt >= 64) wq.cnt -= 64;
+      if (wq.cnt >= 64) { wq.head = (wq.head + 64) & (uint32_t)(kWaveQ - 1); wq.cnt -= 64; }
       continue;
 #endif
       if (wq.cnt >= 64) waveq_round<POLY>(a, L, wq, 64u, hits, lcount);  // leaves < 64
@@ -648,7 +635,7 @@ __device__ __forceinline__ void range_body(const RangeArgs& a) {
   uint64_t* const sm = sh + kBlock / 64;                           // [kBlock / 64] multiplicity
   uint32_t* const lds = lds_base + kRangeHdrWords;
   RangeLds L{nullptr, nullptr, nullptr, nullptr, nullptr};
-  WaveQ wq{nullptr, nullptr, 0u, nullptr, 0u, (uint32_t)t0, (uint32_t)tstride};
+  WaveQ wq{nullptr, nullptr, 0u, 0u, nullptr, 0u, (uint32_t)t0, (uint32_t)tstride};
   if (DEFER || TABLE) {
     if (threadIdx.x == 0) lcount = 0u;
     if (TABLE) {
