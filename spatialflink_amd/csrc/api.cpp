@@ -206,7 +206,6 @@ static int stream_blocks(gf_ctx* ctx, int64_t items_per_thread_pairs) {
 
 using namespace gf;
 
-static int lookback_state(gf_ctx* ctx, int64_t blocks, gf::ExpandState* es);
 
 // ---------------------------------------------------------------------------------------
 // library / context
@@ -1281,7 +1280,7 @@ extern "C" int gf_bitmap_to_indices(gf_ctx* ctx, const uint64_t* bitmap, int64_t
 
 // Ticket + epoch-tagged status words of the decoupled look-back kernels (expand_async, scan1)
 // for a launch of `blocks` blocks; the caller adds `blocks` to ctx->expand_base after launching.
-static int lookback_state(gf_ctx* ctx, int64_t blocks, gf::ExpandState* es) {
+int gf::lookback_state(gf_ctx* ctx, int64_t blocks, gf::ExpandState* es) {
   if (!ctx->expand_ticket) {
     GF_HIP_CHECK(ctx, hipMalloc(&ctx->expand_ticket, sizeof(unsigned long long)));
     GF_HIP_CHECK(ctx, hipMemset(ctx->expand_ticket, 0, sizeof(unsigned long long)));

@@ -1,8 +1,8 @@
 // csv.cpp -- host side of the GPU CSV/TSV ingest (k_csv.hip): Deserialization.CSVTSVToTSpatial
 // (Deserialization.java:291-325) over a chunk of HBM-resident text.
 //
-//   count newlines per 64 KB segment -> exclusive scan -> (sync: line count, capacity check)
-//   -> newline positions -> one lane per line parse + cell -> (sync: first bad line, if any)
+//   newline positions and count in one pass (64 KB segments, decoupled look-back) -> (sync: line
+//   count, capacity check) -> one lane per line parse + cell -> (sync: first bad line, if any)
 //   -> objID Strings that are not canonical decimals -> dictionary keys (objid.cpp)
 #include <cstring>
 #include <string>
@@ -36,48 +36,45 @@ static int parse_text_lines(gf_ctx* ctx, gf_objid_dict* dict, const char* text, 
   if (len == 0) return GF_OK;
   const int64_t nseg = (len + kCsvSeg - 1) / kCsvSeg;
   if (nseg >= (int64_t)INT32_MAX) return set_err(ctx, GF_ERR_ARG, "gf_csv_parse: text too large");
-  // scratch: counts | offsets | scan tmp | error | tail bytes
-  size_t o_cnt = 0, o_off = o_cnt + sizeof(uint32_t) * (size_t)(nseg + 1);
-  size_t o_tmp = o_off + sizeof(uint32_t) * (size_t)(nseg + 1);
-  size_t o_err = (o_tmp + sizeof(uint32_t) * scan_tmp_elems(nseg) + 15) & ~(size_t)15;
-  size_t o_nl = o_err + 64;
-  // the newline array is sized after the count; reserve a first guess (one line per 32 B)
-  char* base = (char*)ctx_scratch(ctx, o_nl + sizeof(int64_t) * (size_t)(len / 32 + 2), &st);
+  // scratch: total | error | newline positions (sized for one line per 32 B; regrown and the index
+  // re-run when the chunk holds more)
+  const size_t o_tot = 0, o_err = 64, o_nl = 128;
+  int64_t nl_cap = len / 32 + 2;
+  char* base = (char*)ctx_scratch(ctx, o_nl + sizeof(int64_t) * (size_t)nl_cap, &st);
   if (st) return st;
   uint32_t* pinned = (uint32_t*)ctx_pinned(ctx, 64, &st);
   if (st) return st;
-  auto count = [&]() -> int {
-    GF_HIP_CHECK(ctx, launch_csv_count(ctx->stream, text, len, nseg, (uint32_t*)(base + o_cnt)));
-    GF_HIP_CHECK(ctx, launch_exclusive_scan(ctx->stream, (uint32_t*)(base + o_cnt), nseg, (uint32_t*)(base + o_off),
-                                            (uint32_t*)(base + o_tmp)));
+  // one pass over the text: the newline positions and their count (k_csv.hip csv_nlindex_kernel)
+  auto index = [&]() -> int {
+    ExpandState es;
+    int e = lookback_state(ctx, nseg, &es);
+    if (e) return e;
+    GF_HIP_CHECK(ctx, launch_csv_nlindex(ctx->stream, text, len, nseg, (int64_t*)(base + o_nl), nl_cap,
+                                         (uint32_t*)(base + o_tot), es));
+    ctx->expand_base += (unsigned long long)nseg;
+    GF_HIP_CHECK(ctx, hipMemcpyAsync(pinned, base + o_tot, sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
+    GF_HIP_CHECK(ctx, hipMemcpyAsync((char*)pinned + 4, text + len - 1, 1, hipMemcpyDeviceToHost, ctx->stream));
+    GF_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
     return GF_OK;
   };
-  if ((st = count())) return st;
-  GF_HIP_CHECK(ctx, hipMemcpyAsync(pinned, (uint32_t*)(base + o_off) + nseg, sizeof(uint32_t), hipMemcpyDeviceToHost,
-                                   ctx->stream));
-  GF_HIP_CHECK(ctx, hipMemcpyAsync((char*)pinned + 4, text + len - 1, 1, hipMemcpyDeviceToHost, ctx->stream));
-  GF_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+  if ((st = index())) return st;
   const int64_t newlines = pinned[0];
   const int64_t lines = newlines + (((char*)pinned)[4] != '\n' ? 1 : 0);
   *n_out = lines;
   if (lines > cap) return set_err(ctx, GF_ERR_CAPACITY, "gf_csv_parse: more lines than capacity");
-  if ((size_t)newlines > (size_t)(len / 32 + 2)) {  // short lines: a larger scratch (it may move: recount)
-    char* nb = (char*)ctx_scratch(ctx, o_nl + sizeof(int64_t) * (size_t)(newlines + 1), &st);
+  if (newlines > nl_cap) {  // short lines: a larger array, the index again
+    nl_cap = newlines + 1;
+    base = (char*)ctx_scratch(ctx, o_nl + sizeof(int64_t) * (size_t)nl_cap, &st);
     if (st) return st;
-    if (nb != base) {
-      base = nb;
-      if ((st = count())) return st;
-    }
+    if ((st = index())) return st;
   }
   if (lines > (int64_t)UINT32_MAX) return set_err(ctx, GF_ERR_ARG, "gf_csv_parse: more than 2^32-1 lines");
   // the dictionary worklist: at most one String per line
   if ((st = dict_reserve_batch(dict, (uint64_t)lines, (uint64_t)lines))) return st;
   GF_HIP_CHECK(ctx, hipMemsetAsync(dict->counters + 2, 0, 2 * sizeof(unsigned long long), ctx->stream));
-  const uint32_t* offs = (const uint32_t*)(base + o_off);
   int64_t* nl = (int64_t*)(base + o_nl);
   CsvErr* err = (CsvErr*)(base + o_err);
   GF_HIP_CHECK(ctx, hipMemsetAsync(err, 0xFF, sizeof(CsvErr), ctx->stream));
-  GF_HIP_CHECK(ctx, launch_csv_index(ctx->stream, text, len, nseg, offs, nl));
   CsvArgs a = proto;
   a.text = text; a.len = len; a.nl = nl; a.newlines = newlines; a.lines = lines;
   a.x = x; a.y = y; a.objID = objID; a.ts = ts; a.cx = cx; a.cy = cy;

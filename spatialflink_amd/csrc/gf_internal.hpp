@@ -351,6 +351,11 @@ hipError_t launch_word_popcounts(hipStream_t s, const uint64_t* bitmap, int64_t 
 hipError_t launch_expand_bitmap(hipStream_t s, const uint64_t* bitmap, int64_t words, int64_t n,
                                 const uint32_t* off, uint32_t* idx, int64_t cap);
 // single-pass compaction state (per context): block tickets and look-back status words
+// decoupled look-back status words: epoch (26 bits) | flag (2) | value (36)
+constexpr uint64_t kLbAgg = 1ull, kLbInc = 2ull;  // status flags: aggregate / inclusive prefix
+__device__ __forceinline__ uint64_t lb_pack(uint32_t epoch, uint64_t flag, uint64_t v) {
+  return ((uint64_t)(epoch & 0x3FFFFFFu) << 38) | (flag << 36) | v;  // v < 2^36
+}
 struct ExpandState {
   unsigned long long* ticket;  // grows across launches; this launch's blocks take [base, base + blocks)
   unsigned long long base;
@@ -463,9 +468,9 @@ struct CsvArgs {
   int32_t geo_fast;              // GeoJSON: 1 = one-pass member location first (k_csv.hip geo_locate)
   int32_t value_lines;           // GeoJSON: 1 = each line is the record's value (else the record)
 };
-hipError_t launch_csv_count(hipStream_t st, const char* text, int64_t len, int64_t nseg, uint32_t* counts);
-hipError_t launch_csv_index(hipStream_t st, const char* text, int64_t len, int64_t nseg, const uint32_t* seg_off,
-                            int64_t* nl);
+hipError_t launch_csv_nlindex(hipStream_t st, const char* text, int64_t len, int64_t nseg, int64_t* nl, int64_t nl_cap,
+                              uint32_t* total, const ExpandState& es);
+int lookback_state(gf_ctx* ctx, int64_t blocks, ExpandState* es);  // api.cpp
 hipError_t launch_csv_parse(gf_ctx* ctx, const CsvArgs& a);
 
 hipError_t launch_pane_bounds(hipStream_t s, const int64_t* ts, int64_t n, int64_t pane_ms, int64_t first_pane,

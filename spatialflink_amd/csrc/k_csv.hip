@@ -1,9 +1,9 @@
 // k_csv.hip -- GPU CSV/TSV ingest: Deserialization.CSVTSVToTSpatial.map
 // (Deserialization.java:291-325) for a whole chunk of text lines at once, fused with
-// HelperClass.assignGridCellID (Point.java:98).  Three kernels over HBM-resident text:
+// HelperClass.assignGridCellID (Point.java:98).  Two kernels over HBM-resident text:
 //
-//   csv_count   newline bytes per 64 KB segment (16-B loads, SWAR byte compare)
-//   csv_index   the newline positions, in order (block-wide prefix of per-thread counts)
+//   csv_nlindex the newline positions, in order, and their count: one read of the text (16-B
+//               loads, SWAR byte compare, a decoupled look-back across 64 KB segments)
 //   csv_parse   one lane per line: quotes dropped, fields split on the delimiter with the
 //               surrounding whitespace (the reference's split("\\s*" + delim + "\\s*")),
 //               the objID String as its key (canonical decimals directly, the rest queued for
@@ -44,54 +44,6 @@ __device__ __forceinline__ uint32_t chunk_mask(const char* text, int64_t len, in
   for (int k = 0; k < 16 && off + k < len; ++k) m |= (uint32_t)(text[off + k] == '\n') << k;
   return m;
 }
-
-__global__ __launch_bounds__(kBlock) void csv_count_kernel(const char* __restrict__ text, int64_t len,
-                                                           uint32_t* __restrict__ counts) {
-  const int64_t s0 = (int64_t)blockIdx.x * kCsvSeg;
-  const int64_t s1 = s0 + kCsvSeg < len ? s0 + kCsvSeg : len;
-  uint32_t c = 0;
-  for (int64_t off = s0 + 16 * threadIdx.x; off < s1; off += 16 * kBlock) c += __popc(chunk_mask(text, len, off));
-  __shared__ uint32_t ws[kBlock / 64];
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
-  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = c;
-  __syncthreads();
-  if (threadIdx.x == 0) counts[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
-}
-
-__global__ __launch_bounds__(kBlock) void csv_index_kernel(const char* __restrict__ text, int64_t len,
-                                                           const uint32_t* __restrict__ seg_off,
-                                                           int64_t* __restrict__ nl) {
-  const int64_t s0 = (int64_t)blockIdx.x * kCsvSeg;
-  const int64_t s1 = s0 + kCsvSeg < len ? s0 + kCsvSeg : len;
-  __shared__ uint32_t ws[kBlock / 64];
-  uint32_t base = seg_off[blockIdx.x];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  for (int64_t it = s0; it < s1; it += 16 * kBlock) {  // block-uniform trip count
-    const int64_t off = it + 16 * threadIdx.x;
-    const uint32_t m = off < s1 ? chunk_mask(text, len, off) : 0u;
-    const uint32_t c = __popc(m);
-    uint32_t inc = c;  // inclusive wave prefix
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t t = __shfl_up(inc, o, 64);
-      if (lane >= o) inc += t;
-    }
-    if (lane == 63) ws[w] = inc;
-    __syncthreads();
-    uint32_t wbase = 0, tot = 0;
-#pragma unroll
-    for (int v = 0; v < kBlock / 64; ++v) {
-      wbase += v < w ? ws[v] : 0u;
-      tot += ws[v];
-    }
-    uint32_t pos = base + wbase + inc - c;
-    for (uint32_t mm = m; mm; mm &= mm - 1) nl[pos++] = off + __ffs(mm) - 1;
-    base += tot;
-    __syncthreads();
-  }
-}
-
 
 __device__ __forceinline__ bool java_s(char c) {  // regex \s: [ \t\n\x0B\f\r]
   return c == ' ' || c == '\t' || c == '\n' || c == '\x0B' || c == '\f' || c == '\r';
@@ -300,14 +252,107 @@ __global__ void csv_error_kernel(CsvArgs a) {
   a.err->kind = a.format == 1 ? eval_geojson_line<false>(a, s, (int64_t)j, &o, gt) : eval_csv_line(a, s, (int64_t)j, &o);
 }
 
-hipError_t launch_csv_count(hipStream_t st, const char* text, int64_t len, int64_t nseg, uint32_t* counts) {
-  hipLaunchKernelGGL(csv_count_kernel, dim3((unsigned)nseg), dim3(kBlock), 0, st, text, len, counts);
-  return hipGetLastError();
+// The newline index in ONE pass over the text (r05; the count + scan + index passes read the text
+// twice: 2 x 190 MB per 1M GeoJSON lines, r04 PMC).  A block takes one 64 KB segment (logical id
+// from a ticket taken at its start, so the look-back only waits on started blocks), keeps its 16
+// chunk masks in registers, counts, publishes its count and looks back for its prefix (the
+// decoupled look-back of expand_async_kernel, k_points.hip), then writes its newline positions in
+// order from the masks.  nl holds nl_cap positions (the ones past it are counted, not stored:
+// the host regrows and re-runs); the last logical block writes the total to *total.
+constexpr int kNlIters = (int)(kCsvSeg / (16 * kBlock));
+__global__ __launch_bounds__(kBlock) void csv_nlindex_kernel(const char* __restrict__ text, int64_t len,
+                                                             int64_t* __restrict__ nl, int64_t nl_cap,
+                                                             uint32_t* __restrict__ total, ExpandState st) {
+  __shared__ unsigned long long s_bid, s_prefix;
+  __shared__ uint32_t ws[kBlock / 64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (threadIdx.x == 0) s_bid = atomicAdd(st.ticket, 1ull) - st.base;
+  __syncthreads();
+  const uint64_t bid = s_bid;
+  const int64_t s0 = (int64_t)bid * kCsvSeg;
+  const int64_t s1 = s0 + kCsvSeg < len ? s0 + kCsvSeg : len;
+  uint32_t m[kNlIters], c = 0;
+#pragma unroll
+  for (int it = 0; it < kNlIters; ++it) {
+    const int64_t off = s0 + (int64_t)it * 16 * kBlock + 16 * threadIdx.x;
+    m[it] = off < s1 ? chunk_mask(text, len, off) : 0u;
+    c += (uint32_t)__popc(m[it]);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+  if (lane == 0) ws[w] = c;
+  __syncthreads();
+  uint32_t agg = 0;
+#pragma unroll
+  for (int v = 0; v < kBlock / 64; ++v) agg += ws[v];
+  if (w == 0) {  // publish the aggregate, look back for the prefix (as scan1_kernel)
+    unsigned long long* my = st.status + bid;
+    const uint64_t ep = st.epoch & 0x3FFFFFFu;
+    if (bid == 0) {
+      if (lane == 0) {
+        __hip_atomic_store(my, lb_pack(st.epoch, kLbInc, agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_prefix = 0;
+      }
+    } else {
+      if (lane == 0) __hip_atomic_store(my, lb_pack(st.epoch, kLbAgg, agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      uint64_t prefix = 0;
+      int64_t hi = (int64_t)bid - 1;
+      for (;;) {
+        const int64_t p = hi - lane;
+        const uint64_t v = p >= 0 ? __hip_atomic_load(st.status + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+        const bool ready = p < 0 || ((v >> 38) == ep && ((v >> 36) & 3ull) != 0ull);
+        if (__ballot(!ready)) {
+          __builtin_amdgcn_s_sleep(1);
+          continue;
+        }
+        const bool incl = p >= 0 && ((v >> 36) & 3ull) == kLbInc;
+        const uint64_t incm = __ballot(incl);
+        const int stop = incm ? __ffsll((unsigned long long)incm) - 1 : 64;
+        uint64_t add = lane <= stop ? (v & ((1ull << 36) - 1ull)) : 0ull;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) add += __shfl_xor(add, o, 64);
+        prefix += add;
+        if (incm || hi - 64 < 0) break;
+        hi -= 64;
+      }
+      if (lane == 0) {
+        __hip_atomic_store(my, lb_pack(st.epoch, kLbInc, prefix + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_prefix = prefix;
+      }
+    }
+  }
+  __syncthreads();
+  uint64_t base = s_prefix;
+  if (bid == gridDim.x - 1 && threadIdx.x == 0) *total = (uint32_t)(base + agg);
+#pragma unroll
+  for (int it = 0; it < kNlIters; ++it) {  // positions in order: chunk by chunk, threads in order
+    const int64_t off = s0 + (int64_t)it * 16 * kBlock + 16 * threadIdx.x;
+    const uint32_t cc = (uint32_t)__popc(m[it]);
+    uint32_t inc = cc;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t t = __shfl_up(inc, o, 64);
+      if (lane >= o) inc += t;
+    }
+    __syncthreads();  // (the previous iteration's reads of ws are done)
+    if (lane == 63) ws[w] = inc;
+    __syncthreads();
+    uint32_t wbase = 0, tot = 0;
+#pragma unroll
+    for (int v = 0; v < kBlock / 64; ++v) {
+      wbase += v < w ? ws[v] : 0u;
+      tot += ws[v];
+    }
+    uint64_t pos = base + wbase + inc - cc;
+    for (uint32_t mm = m[it]; mm; mm &= mm - 1, ++pos)
+      if ((int64_t)pos < nl_cap) nl[pos] = off + __ffs(mm) - 1;
+    base += tot;
+  }
 }
 
-hipError_t launch_csv_index(hipStream_t st, const char* text, int64_t len, int64_t nseg, const uint32_t* seg_off,
-                            int64_t* nl) {
-  hipLaunchKernelGGL(csv_index_kernel, dim3((unsigned)nseg), dim3(kBlock), 0, st, text, len, seg_off, nl);
+hipError_t launch_csv_nlindex(hipStream_t st, const char* text, int64_t len, int64_t nseg, int64_t* nl, int64_t nl_cap,
+                              uint32_t* total, const ExpandState& es) {
+  hipLaunchKernelGGL(csv_nlindex_kernel, dim3((unsigned)nseg), dim3(kBlock), 0, st, text, len, nl, nl_cap, total, es);
   return hipGetLastError();
 }
 

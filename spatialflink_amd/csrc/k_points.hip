@@ -797,11 +797,7 @@ __global__ __launch_bounds__(kBlock) void expand_kernel(const uint64_t* __restri
 // 6.4 / 9.4 us.  The ticket atomics serialise on one address and every poll is a round of
 // uncached status loads, so fewer, larger blocks win; reading 4 or 8 predecessors per lane a
 // round (fewer rounds, more polling traffic) measured slower (7.9 / 9.7 us).
-constexpr uint64_t kLbAgg = 1ull, kLbInc = 2ull;  // status flags
-constexpr int kLbPerLane = 1;
-__device__ __forceinline__ uint64_t lb_pack(uint32_t epoch, uint64_t flag, uint64_t v) {
-  return ((uint64_t)(epoch & 0x3FFFFFFu) << 38) | (flag << 36) | v;  // v < 2^36
-}
+constexpr int kLbPerLane = 1;  // (kLbAgg / kLbInc / lb_pack: gf_internal.hpp)
 
 // One window's expansion by the block with global ticket `bid`: its tiles are the global ids
 // [lo, last]; the look-back stops at lo (a batch of windows shares one ticket sequence, each
