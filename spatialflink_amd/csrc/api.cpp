@@ -1054,6 +1054,7 @@ RangeArgs range_args(const gf_range_plan* P, const gf_points* pts, uint64_t* bit
   a.inv_cl = 1.0 / P->grid.cellLength;
   a.cand_off = P->cand_off; a.cand_list = P->cand_list;
   a.approx = P->approx; a.metric = P->metric; a.r = P->r; a.s_r = s_prefilter(P->r, 0);
+  a.thr = P->metric == 0 ? a.s_r : a.r;
   a.qx0 = P->qx0; a.qy0 = P->qy0;
   a.qx = P->qx; a.qy = P->qy;
   a.npoly = P->npoly; a.ring_off = P->ring_off; a.vert_off = P->vert_off; a.vx = P->vx; a.vy = P->vy;

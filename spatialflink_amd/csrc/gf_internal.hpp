@@ -270,6 +270,7 @@ struct RangeArgs {
   int approx;
   int metric;
   double r, s_r;
+  double thr;                // the point-point test's one bound: s_r (metric 0, on dx^2 + dy^2) or r (hypot)
   double qx0, qy0;           // the query point (ARITH mode)
   const double* qx;          // point-point queries (device)
   const double* qy;

@@ -129,15 +129,22 @@ __device__ __forceinline__ void bitmap_or(uint64_t* bitmap, uint32_t i) {
                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
+// d <= r for a point pair: ONE bound field (RangeArgs.thr).  Written with the two fields (s_r on
+// the squared distance, r on hypot) the compiler folded the two compares into one load from a
+// select of the two members' ADDRESSES, which put the whole argument block in scratch (528 B per
+// lane in the 16-B-load build, plus an s_waitcnt vmcnt(0) on the scratch load that drained the
+// stream's prefetched tiles).
+__device__ __forceinline__ bool pp_within(const RangeArgs& a, double dx, double dy) {
+  return (a.metric == 0 ? dx * dx + dy * dy : fdlibm_hypot(dx, dy)) <= a.thr;
+}
+
 // candidate-cell test: exists object within r (first hit wins, emitted once).  The answer is
 // an existential over the cell's object list, so visiting order is free: polygons whose
 // envelope holds the point go first, polygons whose envelope is farther than r are skipped.
 template <int TABLE, int POLY>
 __device__ __forceinline__ bool test_point(const RangeArgs& a, double px, double py) {
   if (!POLY && !TABLE) {  // single query point: exact s <= smax(r) for the sqrt metric
-    const double dx = a.qx0 - px, dy = a.qy0 - py;
-    if (a.metric == 0) return dx * dx + dy * dy <= a.s_r;
-    return fdlibm_hypot(dx, dy) <= a.r;
+    return pp_within(a, a.qx0 - px, a.qy0 - py);
   }
   int32_t b = 0, e = POLY ? a.npoly : a.nq;
   const int32_t* lst = nullptr;
@@ -150,8 +157,7 @@ __device__ __forceinline__ bool test_point(const RangeArgs& a, double px, double
   if (!POLY) {
     for (int32_t t = b; t < e; ++t) {
       const int32_t o = lst ? lst[t] : t;
-      const double dx = a.qx[o] - px, dy = a.qy[o] - py;
-      if (a.metric == 0 ? (dx * dx + dy * dy <= a.s_r) : (fdlibm_hypot(dx, dy) <= a.r)) return true;
+      if (pp_within(a, a.qx[o] - px, a.qy[o] - py)) return true;
     }
     return false;
   }
@@ -544,8 +550,7 @@ __device__ __forceinline__ void finalize_counts(const RangeArgs& a, int nparts, 
 template <int POLY>
 __device__ __forceinline__ bool test_object(const RangeArgs& a, double px, double py, int32_t o) {
   if (!POLY) {
-    const double dx = a.qx[o] - px, dy = a.qy[o] - py;
-    return a.metric == 0 ? (dx * dx + dy * dy <= a.s_r) : (fdlibm_hypot(dx, dy) <= a.r);
+    return pp_within(a, a.qx[o] - px, a.qy[o] - py);
   }
   if (a.approx) return point_bbox_distance(px, py, a.bbox + 4 * o) <= a.r;
   if (px == px && py == py && env_far(a.bbox + 4 * o, px, py, a.r)) return false;
