@@ -8,6 +8,8 @@
 // query-grid cell within Chebyshev distance c of q's cell, exactly the replicated-key match.
 // Output: two passes over the ordinary side (count, then write at per-block scanned
 // offsets), so no global atomics and pairs come out grouped by ordinary point.
+#include <type_traits>
+
 #include "gf_internal.hpp"
 
 namespace gf {
@@ -1261,8 +1263,15 @@ constexpr int kBandBuf = GF_BAND_BUF;        // pairs per wave buffer (written o
 #define GF_BAND_R 4
 #endif
 constexpr int kBandRound = GF_BAND_R;  // candidates per lane per walk round
+#ifndef GF_BAND_R1
+#define GF_BAND_R1 2
+#endif
+constexpr int kBandRound1 = GF_BAND_R1;  // the same for MODE 1 (hypot: at 4 its walk spills to scratch in the loops)
 #ifndef GF_BAND_PAIR
 #define GF_BAND_PAIR 1
+#endif
+#ifndef GF_BAND_FLATSEL
+#define GF_BAND_FLATSEL 1
 #endif
 constexpr bool kBandPair = GF_BAND_PAIR != 0;  // sparse whole-band windows: a lane's two points in one walk
 constexpr int kBandMaxSub = 6;       // staged sub-rows f + 2 (f <= 4)
@@ -1532,6 +1541,7 @@ template <int MODE>
 __global__ __launch_bounds__(kBandThreads) void join_band_probe_kernel(JoinRowArgs a) {
   extern __shared__ __attribute__((aligned(16))) char lds_base[];
   BandHdr& hd = *reinterpret_cast<BandHdr*>(lds_base);
+  constexpr int kR = MODE == 0 ? kBandRound : kBandRound1;  // candidates per lane per walk round
   char* const stg = lds_base + kBandHdrBytes + (size_t)kBandWaves * kBandPerWave;
   const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   char* const wbase = lds_base + kBandHdrBytes + (size_t)wid * kBandPerWave;
@@ -1646,16 +1656,21 @@ __global__ __launch_bounds__(kBandThreads) void join_band_probe_kernel(JoinRowAr
       __syncthreads();
       // Pairs out.  With the band staged (lds: block-uniform) every buffered entry is a staged slot
       // and the flush reads LDS only; the global form (a sub-column read from global memory) is a
-      // separate path -- sharing one, its global load and the LDS read wrote the same register,
-      // and the compiler's wait for that write-after-write (vmcnt(0)) drained the prefetched
-      // points at every flush iteration.
-      auto flush = [&]() {
+      // separate COMPILE-TIME path (st: std::true_type = staged): the staged streaming loops
+      // contain no global load but the prefetch.  r05: with both forms behind one runtime branch
+      // in the same loop, the global form's load and the walk's hit-mask register were the same
+      // VGPR, and the compiler's wait for that write-after-write (vmcnt(0), in the FIRST walk
+      // round of every wave-step) drained the prefetched next points: their latency was exposed
+      // once per 128 points.  (r04 fixed the same hazard between the two flush forms.)
+      // st: std::true_type / std::false_type -- staged or not, fixed at compile time
+      auto staged = [](auto st) constexpr -> bool { return decltype(st)::value; };
+      auto flush_as = [&](auto st) {
 #ifdef GF_BAND_EXP_NOEMIT  // experiment build: the buffered pairs are dropped (no band_emit)
         sink ^= cnt;
         cnt = 0;
         return;
 #endif
-        if (lds) {
+        if (staged(st)) {
           band_emit(a.out, hd, cnt, [&](uint32_t i) {
             const uint2 v = buf[i];
             return make_uint2(v.x, ((lds_u32)lq)[v.y]);
@@ -1675,13 +1690,14 @@ __global__ __launch_bounds__(kBandThreads) void join_band_probe_kernel(JoinRowAr
       // instructions at ~3 candidates per point.
       const bool dense = lds && (uint64_t)m * 9u > 12ull * (uint64_t)(f + 2) * (c1 - c0 + 2);
       // one point: its 3 x 3 sub-cell neighbourhood, kBandRound candidates per round
-      auto probe = [&](double px, double py, uint32_t pidx, bool valid) {
+      auto probe = [&](auto st, double px, double py, uint32_t pidx, bool valid) {
+        const bool S = staged(st);  // staged band (lds)
         int32_t cx = cell_index(px, a.u_minX, a.u_cl);
         bool in = valid && cx >= 0 && cx < qn;  // outside the grid's columns: no key matches
         int32_t col = in ? f * (cx + 1) + join_sub(px, a.u_minX, a.u_cl, cx, a.fs, f) : 0;
         int32_t sub = join_sub(py, a.u_minY, a.u_cl, cy, a.fs, f);
         in = in && (uint32_t)col >= c0 && (uint32_t)col < c1;
-        if (dense) {  // wave-uniform
+        if (S && dense) {  // wave-uniform (dense implies staged)
           uint32_t key = in ? (uint32_t)(col - (int32_t)c0) << 3 | (uint32_t)sub : 0xFFFFFFFFu, src = lane;
 #pragma unroll
           for (int size = 2; size <= 64; size <<= 1)
@@ -1703,7 +1719,7 @@ __global__ __launch_bounds__(kBandThreads) void join_band_probe_kernel(JoinRowAr
           in = key != 0xFFFFFFFFu;
         }
         uint32_t b[3], e[3];
-        if (lds) {  // (a lane outside the window reads in-bounds entries, masked)
+        if (S) {  // (a lane outside the window reads in-bounds entries, masked)
           const uint16_t* lo = lo16 + (in ? sub * ncol + (col - (int32_t)c0) : 0);
 #pragma unroll
           for (int k = 0; k < 3; ++k) {
@@ -1730,19 +1746,25 @@ __global__ __launch_bounds__(kBandThreads) void join_band_probe_kernel(JoinRowAr
         // and tested 64 per round through lane permutes -- 184.8 vs 183.0: the walk is not bound
         // by its idle lanes; R = 2: 182.6, R = 8: 211; buffers of 384 / 768 pairs: +4 / +81 (the
         // band then needs windows); flushing at the step's start instead of its end: no change.)
-        for (uint32_t k = 0; __ballot(k < L2) != 0; k += kBandRound) {
-          if (cnt > (uint32_t)(kBandBuf - 64 * kBandRound)) flush();
+        for (uint32_t k = 0; __ballot(k < L2) != 0; k += kR) {
+          if (cnt > (uint32_t)(kBandBuf - 64 * kR)) flush_as(st);
           {
-            uint32_t t[kBandRound];
-            double2 v[kBandRound];
+            uint32_t t[kR];
+            double2 v[kR];
 #pragma unroll
-            for (int i = 0; i < kBandRound; ++i) {
+            for (int i = 0; i < kR; ++i) {
               const uint32_t kk = k + i;
-              t[i] = kk < L2 ? kk + (kk < L0 ? d0 : (kk < L1 ? d1 : d2)) : (lds ? 0u : b[0]);
+#if GF_BAND_FLATSEL
+              uint32_t d = kk < L1 ? d1 : d2;
+              d = kk < L0 ? d0 : d;
+              t[i] = kk < L2 ? kk + d : (S ? 0u : b[0]);
+#else
+              t[i] = kk < L2 ? kk + (kk < L0 ? d0 : (kk < L1 ? d1 : d2)) : (S ? 0u : b[0]);
+#endif
             }
 #pragma unroll
-            for (int i = 0; i < kBandRound; ++i) {
-              if (lds) {
+            for (int i = 0; i < kR; ++i) {
+              if (S) {
                 v[i] = lxy[t[i]];  // a finished lane reads slot 0 (staged: m > 0 when any lane runs)
               } else {
                 v[i] = make_double2(0.0, 0.0);
@@ -1750,7 +1772,7 @@ __global__ __launch_bounds__(kBandThreads) void join_band_probe_kernel(JoinRowAr
               }
             }
 #pragma unroll
-            for (int i = 0; i < kBandRound; ++i) {
+            for (int i = 0; i < kR; ++i) {
               const double dx = px - v[i].x, dy = py - v[i].y;
               bool ok;
               if constexpr (MODE == 0) ok = dx * dx + dy * dy <= a.s_r;
@@ -1763,7 +1785,7 @@ __global__ __launch_bounds__(kBandThreads) void join_band_probe_kernel(JoinRowAr
 #endif
               if (hit)
                 buf[cnt + __builtin_amdgcn_mbcnt_hi((uint32_t)(hm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)hm, 0u))] =
-                    make_uint2(pidx, lds ? t[i] : (t[i] | kBandGlobal));
+                    make_uint2(pidx, S ? t[i] : (t[i] | kBandGlobal));
               cnt += (uint32_t)__popcll(hm);
             }
           }
@@ -1813,21 +1835,27 @@ __global__ __launch_bounds__(kBandThreads) void join_band_probe_kernel(JoinRowAr
         sink += LT ^ dd[0] ^ dd[3];
         return;
 #endif
-        for (uint32_t k = 0; __ballot(k < LT) != 0; k += kBandRound) {
-          if (cnt > (uint32_t)(kBandBuf - 64 * kBandRound)) flush();
-          uint32_t t[kBandRound];
-          double2 v[kBandRound];
+        for (uint32_t k = 0; __ballot(k < LT) != 0; k += kR) {
+          if (cnt > (uint32_t)(kBandBuf - 64 * kR)) flush_as(std::true_type{});
+          uint32_t t[kR];
+          double2 v[kR];
 #pragma unroll
-          for (int i = 0; i < kBandRound; ++i) {
+          for (int i = 0; i < kR; ++i) {
             const uint32_t kk = k + i;
+#if GF_BAND_FLATSEL  // a flat select chain (the nested ?: compiles to exec-masked branches per level)
+            uint32_t d = dd[5];
+#pragma unroll
+            for (int j = 4; j >= 0; --j) d = kk < L[j] ? dd[j] : d;
+#else
             const uint32_t d = kk < L[0] ? dd[0] : kk < L[1] ? dd[1] : kk < L[2] ? dd[2]
                              : kk < L[3] ? dd[3] : kk < L[4] ? dd[4] : dd[5];
+#endif
             t[i] = kk < LT ? kk + d : 0u;
           }
 #pragma unroll
-          for (int i = 0; i < kBandRound; ++i) v[i] = lxy[t[i]];  // a finished lane reads slot 0
+          for (int i = 0; i < kR; ++i) v[i] = lxy[t[i]];  // a finished lane reads slot 0
 #pragma unroll
-          for (int i = 0; i < kBandRound; ++i) {
+          for (int i = 0; i < kR; ++i) {
             const bool second = k + i >= LA;
             const double dx = (second ? pxb : pxa) - v[i].x, dy = (second ? pyb : pya) - v[i].y;
             bool ok;
@@ -1862,24 +1890,34 @@ __global__ __launch_bounds__(kBandThreads) void join_band_probe_kernel(JoinRowAr
         }
         return p;
       };
-      if (c0 == cbeg && c1 == cend) {  // the whole band in one window: every point streams through
+      // the whole band in one window: every point streams through
+      auto stream_band = [&](auto st) {
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): nothing of another path pending in the loop
         Pt cur = fetch(sb + wid * 128);
         for (uint32_t s0 = sb + wid * 128; s0 < se; s0 += kBandWaves * 128) {  // wave-uniform
           const Pt nxt = fetch(s0 + kBandWaves * 128);
-          if (kBandPair && !dense) {  // wave-uniform
-            probe2(cur.v[0].x, cur.v[0].y, cur.idx[0], s0 + lane < se, cur.v[1].x, cur.v[1].y, cur.idx[1],
-                   s0 + 64 + lane < se);
-          } else {
-            probe(cur.v[0].x, cur.v[0].y, cur.idx[0], s0 + lane < se);
-            probe(cur.v[1].x, cur.v[1].y, cur.idx[1], s0 + 64 + lane < se);
+          bool two = false;
+          if (staged(st)) {
+            if (kBandPair && !dense) {  // wave-uniform
+              probe2(cur.v[0].x, cur.v[0].y, cur.idx[0], s0 + lane < se, cur.v[1].x, cur.v[1].y, cur.idx[1],
+                     s0 + 64 + lane < se);
+              two = true;
+            }
+          }
+          if (!two) {
+            probe(st, cur.v[0].x, cur.v[0].y, cur.idx[0], s0 + lane < se);
+            probe(st, cur.v[1].x, cur.v[1].y, cur.idx[1], s0 + 64 + lane < se);
           }
           __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): nxt is in registers (before any store)
-          if (cnt > (uint32_t)(kBandBuf - 64 * kBandRound)) flush();
+          if (cnt > (uint32_t)(kBandBuf - 64 * kR)) flush_as(st);
           cur = nxt;
         }
-      } else {
-        // windowed band: the wave queues the positions of its points inside the window (LDS) and
-        // probes them 64 at a time, so the lanes of other windows do not ride along
+        if (cnt > 0) flush_as(st);  // staged slots change with the next window
+      };
+      // windowed band: the wave queues the positions of its points inside the window (LDS) and
+      // probes them 64 at a time, so the lanes of other windows do not ride along
+      auto window_band = [&](auto st) {
+        __builtin_amdgcn_s_waitcnt(0x0F70);
         uint32_t qc = 0;  // wave-uniform
         for (uint32_t s0 = sb + wid * 64; s0 < se; s0 += kBandWaves * 64) {
           const uint32_t i = s0 + lane;
@@ -1898,17 +1936,24 @@ __global__ __launch_bounds__(kBandThreads) void join_band_probe_kernel(JoinRowAr
             if (lane < rest) wq[lane] = mv;
             qc = rest;
             const double2 v = reinterpret_cast<const double2*>(a.soxy)[k];
-            probe(v.x, v.y, a.soidx[k], true);
-            if (cnt > (uint32_t)(kBandBuf - 64 * kBandRound)) flush();
+            probe(st, v.x, v.y, a.soidx[k], true);
+            if (cnt > (uint32_t)(kBandBuf - 64 * kR)) flush_as(st);
           }
         }
         if (qc > 0) {
           const uint32_t k = wq[lane < qc ? lane : 0];
           const double2 v = reinterpret_cast<const double2*>(a.soxy)[k];
-          probe(v.x, v.y, a.soidx[k], lane < qc);
+          probe(st, v.x, v.y, a.soidx[k], lane < qc);
         }
+        if (cnt > 0) flush_as(st);  // staged slots change with the next window
+      };
+      if (c0 == cbeg && c1 == cend) {
+        if (lds) stream_band(std::true_type{});
+        else stream_band(std::false_type{});
+      } else {
+        if (lds) window_band(std::true_type{});
+        else window_band(std::false_type{});
       }
-      if (cnt > 0) flush();  // staged slots change with the next window
       __syncthreads();
       c0 = c1;
     }
