@@ -2047,7 +2047,11 @@ static int join_pp_impl(gf_ctx* ctx, const gf_grid* ugrid, const gf_grid* qgrid,
   size_t o_gcnt = ar.take<unsigned long long>(2);  // -, total
   // output (JoinOut): the persistent probe's waves, one chunk each at a time, sized from the last
   // join's pairs per point so that a window takes ~8 chunks per wave: few atomics, small holes
-  const int64_t probe_blocks = std::max(8, ctx->num_cus / 8 * 8);
+  // (GF_JOIN_BAND_PER_CU, A/B testing only: band probe blocks per CU -- the product's 160 KB
+  // block fills a CU's LDS; an experiment build with an 80 KB block can hold two)
+  const char* pcu = std::getenv("GF_JOIN_BAND_PER_CU");
+  const int64_t per_cu = pcu && *pcu >= '1' && *pcu <= '4' ? *pcu - '0' : 1;
+  const int64_t probe_blocks = std::max(8, ctx->num_cus / 8 * 8) * per_cu;
   const int64_t nwaves = probe_blocks * (kJoinThreads / 64);
   // pairs per point of the last join: its exact count (sync) or the fix-up's pinned copy (async)
   double ppp = ctx->join_ppp > 0 ? ctx->join_ppp : 1.0;
@@ -2059,7 +2063,7 @@ static int join_pp_impl(gf_ctx* ctx, const gf_grid* ugrid, const gf_grid* qgrid,
   // streaming experiment take per-wave chunks (one device atomic each, one hole per wave).
   // fine path: the band probe (k_join.hip) unless the row probe is asked for (A/B testing)
   const char* renv = std::getenv("GF_JOIN_ROWPROBE");
-  const bool band = rowpath && f > 1 && !stream && !(renv && *renv == '1') && ctx->num_cus <= 1016;
+  const bool band = rowpath && f > 1 && !stream && !(renv && *renv == '1') && probe_blocks <= 1016;
   const int64_t ntails = nwaves;
   int64_t chunk = 256;
   while (chunk < 65536 && (double)chunk * ntails * 8 < ppp * (double)no)

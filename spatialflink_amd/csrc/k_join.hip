@@ -1289,11 +1289,20 @@ struct BandHdr {
   int32_t last;             // this block took the last ticket
 };
 constexpr int kBandHdrBytes = (int)((sizeof(BandHdr) + 15) / 16 * 16);
-constexpr size_t kBandLds = 160 * 1024;
-constexpr int kBandQueue = 128;      // windowed bands: queued point positions per wave
+#ifndef GF_BAND_LDS_KB  // experiment builds: a smaller block (GF_BAND_MINBLK blocks per CU)
+#define GF_BAND_LDS_KB 160
+#endif
+#ifndef GF_BAND_MINBLK
+#define GF_BAND_MINBLK 1
+#endif
+#ifndef GF_BAND_QUEUE
+#define GF_BAND_QUEUE 128
+#endif
+constexpr size_t kBandLds = GF_BAND_LDS_KB * 1024;
+constexpr int kBandQueue = GF_BAND_QUEUE;  // windowed bands: queued point positions per wave
 constexpr size_t kBandPerWave = (size_t)kBandBuf * 8 + kBandQueue * 4;
 constexpr size_t kBandStage = kBandLds - kBandHdrBytes - (size_t)kBandWaves * kBandPerWave;
-static_assert(kBandStage >= 5 * 8 * 1024, "band_regions' scratch (5 G u64, G <= 1024) in the staging area");
+static_assert(kBandStage >= 5 * 8 * 1024 / GF_BAND_MINBLK, "band_regions' scratch (5 G u64, G <= 1024 / MINBLK) in the staging area");
 // staged offset entries per band sub-row for window [c0, c1): sub-columns c0 - 1 .. c1 + 1
 __device__ __forceinline__ uint32_t band_ncol(uint32_t c0, uint32_t c1) { return (c1 - c0 + 3 + 7) & ~7u; }
 __device__ __forceinline__ uint32_t band_off_bytes(int32_t f, uint32_t c0, uint32_t c1) {
@@ -1538,7 +1547,7 @@ __device__ __forceinline__ void join_region_prep(const JoinFixup& f, uint64_t* w
 }
 
 template <int MODE>
-__global__ __launch_bounds__(kBandThreads) void join_band_probe_kernel(JoinRowArgs a) {
+__global__ __launch_bounds__(kBandThreads, 4 * GF_BAND_MINBLK) void join_band_probe_kernel(JoinRowArgs a) {
   extern __shared__ __attribute__((aligned(16))) char lds_base[];
   BandHdr& hd = *reinterpret_cast<BandHdr*>(lds_base);
   constexpr int kR = MODE == 0 ? kBandRound : kBandRound1;  // candidates per lane per walk round
