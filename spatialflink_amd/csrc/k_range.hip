@@ -311,11 +311,12 @@ __device__ __forceinline__ void waveq_round(const RangeArgs& a, const RangeLds& 
   q.cnt -= take;
 }
 
-// Tile layout.  kRangeVec (default): lane l holds points t + 2l and t + 2l + 1, read with one
-// 16-B load per coordinate (half the load instructions of 8-B loads, twice the bytes in flight
-// per outstanding load -- the scan was latency-bound with 8-B loads: SQ_WAIT_ANY 0.62, VALU 0.25
-// on C3); a tile's bitmap words are the two ballots bit-interleaved (lanes 0-31 -> word w, lanes
-// 32-63 -> word w + 1).  Otherwise lane l holds t + l and t + 64 + l and the ballots ARE the words.
+// Tile layout.  Default: lane l holds t + l and t + 64 + l and the ballots ARE the bitmap words.
+// kRangeVec (GF_RANGE_VEC=1, an A/B variant): lane l holds points t + 2l and t + 2l + 1, read
+// with one 16-B load per coordinate (half the load instructions, twice the bytes in flight per
+// outstanding load); a tile's words are the two ballots bit-interleaved (lanes 0-31 -> word w,
+// lanes 32-63 -> word w + 1).  r05 A/B on one box: C1 1M 3.7 vs 4.5 us, C1 10M 32.7 vs 36.0 us,
+// C3 45.5 vs 45.0 us per window -- the 8-B layout stays.
 #ifndef GF_RANGE_EXP
 #define GF_RANGE_EXP 0  // experiment builds only (tools/build_exp.sh): 1 no span-queue rounds, 2 nothing queued
 #endif

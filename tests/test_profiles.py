@@ -1,4 +1,4 @@
-"""The committed per-round evidence (rounds 3 and 4) is self-consistent: tools/roofline_table.py recomputes every
+"""The committed per-round evidence (rounds 3 to 5) is self-consistent: tools/roofline_table.py recomputes every
 workload line's roofline fraction from profiles/rNN_workloads.jsonl (bytes per launch over the
 line's own time basis) and its HBM traffic ratio from the committed rocprofv3 PMC summaries
 (profiles/rNN_<tag>_pmc.json).  CPU only: reads committed files."""
@@ -12,7 +12,7 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-@pytest.mark.parametrize("rnd", ["r03", "r04"])
+@pytest.mark.parametrize("rnd", ["r03", "r04", "r05"])
 def test_roofline_table_reproduces_lines(tmp_path, rnd):
     if not os.path.exists(os.path.join(ROOT, "profiles", f"{rnd}_workloads.jsonl")):
         pytest.skip(f"no {rnd} workload lines")
@@ -33,3 +33,25 @@ def test_roofline_table_reproduces_lines(tmp_path, rnd):
     for w in ("knn_k50_r0.5_10Mpts_per_gpu_grid500x500", "range_pp_r0.5_10Mpts_grid100",
               "sliding_knn_k100_r0.5_100Mpts_grid1000"):
         assert covered[w] <= 1.05, (w, covered[w])
+
+
+def test_r05_occupancy_measured(tmp_path):
+    """from r05 on, every committed PMC summary carries a measured occupancy
+    (mean resident waves per SIMD from SQ_WAVE_CYCLES, never the all-zero SQ_LEVEL_WAVES), and the
+    roofline table reports it for every line with PMC next to the compiler's register bound."""
+    pm = [f for f in os.listdir(os.path.join(ROOT, "profiles")) if f.startswith("r05_") and f.endswith("_pmc.json")]
+    assert pm
+    for f in pm:
+        d = json.load(open(os.path.join(ROOT, "profiles", f)))["pmc"]
+        for k, v in d.items():
+            assert v.get("mean_waves_per_simd", 0) > 0, (f, k)
+            assert v["median"].get("SQ_WAVE_CYCLES", 0) > 0, (f, k)
+    if not os.path.exists(os.path.join(ROOT, "profiles", "r05_workloads.jsonl")):
+        pytest.skip("no r05 workload lines")
+    out = tmp_path / "roof"
+    subprocess.run([sys.executable, os.path.join(ROOT, "tools", "roofline_table.py"), "r05", "--out", str(out)],
+                   check=True, capture_output=True, timeout=120)
+    for r in json.load(open(str(out) + ".json")):
+        if r["pmc"]:
+            assert r["occupancy"] and all(o["mean_waves_per_simd"] > 0 and o["reg_bound_waves_per_simd"]
+                                          for o in r["occupancy"]), r["workload"]
