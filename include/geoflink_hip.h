@@ -384,7 +384,8 @@ int  gf_comm_create(const uint8_t* id, int32_t nranks, int32_t rank, int device,
 int  gf_comm_create_all(int32_t ndev, const int* devices, gf_comm** out /* [ndev] */);
 void gf_comm_destroy(gf_comm* comm);        /* drains the device first */
 int  gf_comm_info(const gf_comm* comm, int32_t* nranks, int32_t* rank, int* device);
-const char* gf_comm_last_error(const gf_comm* comm);  /* comm == NULL: why RCCL did not load */
+const char* gf_comm_last_error(const gf_comm* comm);  /* comm == NULL: why this thread's last unique-id /
+                                                      create call failed, else why RCCL did not load */
 int  gf_comm_check(gf_comm* comm);          /* GF_ERR_COMM on an asynchronous RCCL error */
 /* Async: this rank's nwin consecutive device records (gf_knn_result_bytes(k) apart; ctx's device
  * == the comm's) -> `merged` = nwin consecutive merged records (device or mapped pinned memory),

@@ -80,6 +80,14 @@ Rccl* rccl() {
   return R.so ? &R : nullptr;
 }
 
+// why this thread's last communicator-less call (unique id, create, create_all) failed
+thread_local std::string t_comm_err;
+
+int fail(const std::string& msg, int st = GF_ERR_COMM) {
+  t_comm_err = msg;
+  return st;
+}
+
 }  // namespace
 
 struct gf_comm {
@@ -129,12 +137,13 @@ static int comm_buffer(gf_comm* c, gf_ctx* ctx, void** buf, size_t* have, size_t
 extern "C" int gf_comm_available(void) { return rccl() != nullptr; }
 
 extern "C" int gf_comm_unique_id(uint8_t* id) {
-  if (!id) return GF_ERR_ARG;
+  if (!id) return fail("gf_comm_unique_id: null id", GF_ERR_ARG);
   Rccl* R = rccl();
-  if (!R) return GF_ERR_COMM;
+  if (!R) return fail(rccl_state().err);
   static_assert(sizeof(ncclUniqueId) == GF_COMM_ID_BYTES, "ncclUniqueId size");
   ncclUniqueId u;
-  if (R->GetUniqueId(&u) != ncclSuccess) return GF_ERR_COMM;
+  const ncclResult_t r = R->GetUniqueId(&u);
+  if (r != ncclSuccess) return fail(std::string("ncclGetUniqueId: ") + R->GetErrorString(r));
   std::memcpy(id, &u, sizeof u);
   return GF_OK;
 }
@@ -142,31 +151,38 @@ extern "C" int gf_comm_unique_id(uint8_t* id) {
 extern "C" int gf_comm_create(const uint8_t* id, int32_t nranks, int32_t rank, int device, gf_comm** out) {
   if (!out) return GF_ERR_ARG;
   *out = nullptr;
-  if (!id || nranks < 1 || nranks > kMaxMergeRecs || rank < 0 || rank >= nranks || device < 0) return GF_ERR_ARG;
+  if (!id || nranks < 1 || nranks > kMaxMergeRecs || rank < 0 || rank >= nranks || device < 0)
+    return fail("gf_comm_create: bad argument", GF_ERR_ARG);
   Rccl* R = rccl();
-  if (!R) return GF_ERR_COMM;
-  if (hipSetDevice(device) != hipSuccess) return GF_ERR_HIP;
+  if (!R) return fail(rccl_state().err);
+  // ncclCommInitRank binds the communicator to the CURRENT device; the caller's is restored
+  int prev = -1;
+  if (hipGetDevice(&prev) != hipSuccess || hipSetDevice(device) != hipSuccess)
+    return fail("gf_comm_create: hipSetDevice failed", GF_ERR_HIP);
   gf_comm* c = new gf_comm();
   c->nranks = nranks;
   c->rank = rank;
   c->device = device;
   ncclUniqueId u;
   std::memcpy(&u, id, sizeof u);
-  if (R->CommInitRank(&c->comm, nranks, u, rank) != ncclSuccess) {
+  const ncclResult_t r = R->CommInitRank(&c->comm, nranks, u, rank);
+  hipSetDevice(prev);
+  if (r != ncclSuccess) {
     delete c;
-    return GF_ERR_COMM;
+    return fail(std::string("ncclCommInitRank: ") + R->GetErrorString(r));
   }
   *out = c;
   return GF_OK;
 }
 
 extern "C" int gf_comm_create_all(int32_t ndev, const int* devices, gf_comm** out) {
-  if (!out || ndev < 1 || ndev > kMaxMergeRecs || !devices) return GF_ERR_ARG;
+  if (!out || ndev < 1 || ndev > kMaxMergeRecs || !devices) return fail("gf_comm_create_all: bad argument", GF_ERR_ARG);
   for (int32_t i = 0; i < ndev; ++i) out[i] = nullptr;
   Rccl* R = rccl();
-  if (!R) return GF_ERR_COMM;
+  if (!R) return fail(rccl_state().err);
   std::vector<ncclComm_t> comms(ndev, nullptr);
-  if (R->CommInitAll(comms.data(), ndev, devices) != ncclSuccess) return GF_ERR_COMM;
+  const ncclResult_t r = R->CommInitAll(comms.data(), ndev, devices);
+  if (r != ncclSuccess) return fail(std::string("ncclCommInitAll: ") + R->GetErrorString(r));
   for (int32_t i = 0; i < ndev; ++i) {
     gf_comm* c = new gf_comm();
     c->comm = comms[i];
@@ -198,7 +214,9 @@ extern "C" int gf_comm_info(const gf_comm* c, int32_t* nranks, int32_t* rank, in
 }
 
 extern "C" const char* gf_comm_last_error(const gf_comm* c) {
-  return c ? c->last_error.c_str() : rccl_state().err.c_str();  // null: why RCCL did not load
+  if (c) return c->last_error.c_str();
+  // null: why this thread's last unique-id / create call failed, else why RCCL did not load
+  return !t_comm_err.empty() ? t_comm_err.c_str() : rccl_state().err.c_str();
 }
 
 extern "C" int gf_comm_check(gf_comm* c) {

@@ -167,7 +167,11 @@ def test_comm_entry_points_without_gpu():
     assert L.gf_comm_create(uid, 0, 0, 0, C.byref(h)) == _lib.GF_ERR_ARG
     assert L.gf_comm_create(uid, 2, 2, 0, C.byref(h)) == _lib.GF_ERR_ARG
     assert L.gf_comm_create(None, 1, 0, 0, C.byref(h)) == _lib.GF_ERR_ARG
+    assert b"bad argument" in L.gf_comm_last_error(None)  # this thread's last failed create
     assert L.gf_comm_unique_id(None) == _lib.GF_ERR_ARG
+    assert b"null id" in L.gf_comm_last_error(None)
+    hs = (C.c_void_p * 2)()
+    assert L.gf_comm_create_all(0, None, hs) == _lib.GF_ERR_ARG
     assert L.gf_knn_exchange_batch(None, None, 50, None, 1, None) == _lib.GF_ERR_ARG
     assert L.gf_knn_exchange_group(0, None, None, 50, None, 1, None) == _lib.GF_ERR_ARG
     assert L.gf_status_string(_lib.GF_ERR_COMM).decode().startswith("RCCL")

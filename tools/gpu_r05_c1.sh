@@ -8,7 +8,9 @@ for rep in 1 2; do
   for b in 0 64 128 256; do
     $S c1b_${b}_$rep 200 python -u bench.py --workload range --points 1000000 --steps 800 --warmup 48 --range-blocks $b --no-cpu-baseline --no-verify || exit 1
   done
+  $S c1b_ni_$rep 200 python -u bench.py --workload range --points 1000000 --steps 800 --warmup 48 --no-indices --no-cpu-baseline --no-verify || exit 1
 done
+$S c1b_prof 200 rocprofv3 --kernel-trace --stats -d gpurun_out/c1b_prof -o stats --output-format csv -- python -u bench.py --workload range --points 1000000 --steps 800 --warmup 48 --range-streams 1 --no-cpu-baseline --no-verify || exit 1
 for f in gpurun_out/c1b_*.log; do
   echo "$f $(grep -h '^{' $f | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["ms_per_step"], d["config"].get("scan_blocks"))')"
 done
