@@ -1,9 +1,10 @@
 // csv.cpp -- host side of the GPU CSV/TSV ingest (k_csv.hip): Deserialization.CSVTSVToTSpatial
 // (Deserialization.java:291-325) over a chunk of HBM-resident text.
 //
-//   newline positions and count in one pass (64 KB segments, decoupled look-back) -> (sync: line
-//   count, capacity check) -> one lane per line parse + cell -> (sync: first bad line, if any)
-//   -> objID Strings that are not canonical decimals -> dictionary keys (objid.cpp)
+//   newline positions and count in one pass (64 KB segments, decoupled look-back) -> one lane per
+//   line parse + cell (the line count read on the device) -> the head (counts, first bad line,
+//   dictionary work) written into mapped pinned memory -> the call's one sync -> objID Strings
+//   that are not canonical decimals -> dictionary keys (objid.cpp)
 #include <cstring>
 #include <string>
 
@@ -36,61 +37,68 @@ static int parse_text_lines(gf_ctx* ctx, gf_objid_dict* dict, const char* text, 
   if (len == 0) return GF_OK;
   const int64_t nseg = (len + kCsvSeg - 1) / kCsvSeg;
   if (nseg >= (int64_t)INT32_MAX) return set_err(ctx, GF_ERR_ARG, "gf_csv_parse: text too large");
-  // scratch: total | error | newline positions (sized for one line per 32 B; regrown and the index
-  // re-run when the chunk holds more)
+  // scratch: newline total | error | newline positions (sized for one line per 32 B; regrown and
+  // the whole call re-run when the chunk holds more)
   const size_t o_tot = 0, o_err = 64, o_nl = 128;
   int64_t nl_cap = len / 32 + 2;
-  char* base = (char*)ctx_scratch(ctx, o_nl + sizeof(int64_t) * (size_t)nl_cap, &st);
-  if (st) return st;
-  uint32_t* pinned = (uint32_t*)ctx_pinned(ctx, 64, &st);
-  if (st) return st;
-  // one pass over the text: the newline positions and their count (k_csv.hip csv_nlindex_kernel)
-  auto index = [&]() -> int {
+  // the head lands in mapped pinned memory, written by the call's last kernel: the sync is the
+  // only host round trip (a 64-B device -> host copy was a ~20 us blit of its own)
+  if (!ctx->csv_head && (st = gf_pinned_alloc(sizeof(CsvHead), &ctx->csv_head))) return set_err(ctx, st, "gf_csv_parse: pinned head");
+  volatile CsvHead* const head = (volatile CsvHead*)ctx->csv_head;
+  CsvHead h{};
+  // One pass: index -> parse -> error/head kernels, then ONE sync.  The line count
+  // stays on the device (CsvArgs.nl_total): the parse grid covers min(nl_cap + 1, cap) lines and
+  // blocks past the chunk's lines return; when the count exceeds the index or the capacity the
+  // parse writes nothing and the host re-runs (bigger index) or reports (GF_ERR_CAPACITY).  (r04:
+  // a sync after the index for the count and another after the parse -- two host round trips and
+  // four small copies per chunk.)
+  for (int pass = 0; pass < 2; ++pass) {
+    char* base = (char*)ctx_scratch(ctx, o_nl + sizeof(int64_t) * (size_t)nl_cap, &st);
+    if (st) return st;
+    const int64_t grid_lines = std::min<int64_t>(nl_cap + 1, cap);
+    // the dictionary worklist: at most one String per line
+    if (grid_lines > 0 && (st = dict_reserve_batch(dict, (uint64_t)grid_lines, (uint64_t)grid_lines))) return st;
+    GF_HIP_CHECK(ctx, hipMemsetAsync(dict->counters + 2, 0, 2 * sizeof(unsigned long long), ctx->stream));
+    CsvErr* err = (CsvErr*)(base + o_err);
+    GF_HIP_CHECK(ctx, hipMemsetAsync(err, 0xFF, sizeof(CsvErr), ctx->stream));
     ExpandState es;
-    int e = lookback_state(ctx, nseg, &es);
-    if (e) return e;
+    if ((st = lookback_state(ctx, nseg, &es))) return st;
     GF_HIP_CHECK(ctx, launch_csv_nlindex(ctx->stream, text, len, nseg, (int64_t*)(base + o_nl), nl_cap,
                                          (uint32_t*)(base + o_tot), es));
     ctx->expand_base += (unsigned long long)nseg;
-    GF_HIP_CHECK(ctx, hipMemcpyAsync(pinned, base + o_tot, sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
-    GF_HIP_CHECK(ctx, hipMemcpyAsync((char*)pinned + 4, text + len - 1, 1, hipMemcpyDeviceToHost, ctx->stream));
+    CsvArgs a = proto;
+    a.text = text; a.len = len; a.nl = (int64_t*)(base + o_nl);
+    a.nl_total = (const uint32_t*)(base + o_tot);
+    a.nl_cap = nl_cap;
+    a.cap = cap;
+    a.grid_lines = grid_lines;
+    const int64_t last_mean = ctx->csv_mean_line[proto.format == 1];
+    a.mean_line = last_mean > 0 ? last_mean : (grid_lines > 0 ? (len + grid_lines - 1) / grid_lines : len);
+    a.head = (CsvHead*)ctx->csv_head;
+    a.x = x; a.y = y; a.objID = objID; a.ts = ts; a.cx = cx; a.cy = cy;
+    if (g) { a.minX = g->minX; a.minY = g->minY; a.cl = g->cellLength; }
+    a.err = err;
+    a.dict_work = (DictWork*)dict->work[0];
+    a.dict_n = (uint32_t*)(dict->counters + 2);
+    a.dict_bytes = dict->counters + 3;
+    GF_HIP_CHECK(ctx, launch_csv_parse(ctx, a));
     GF_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
-    return GF_OK;
-  };
-  if ((st = index())) return st;
-  const int64_t newlines = pinned[0];
-  const int64_t lines = newlines + (((char*)pinned)[4] != '\n' ? 1 : 0);
+    h.newlines = head->newlines;
+    h.lines = head->lines;
+    h.dict_n = head->dict_n;
+    h.dict_bytes = head->dict_bytes;
+    h.err.line = head->err.line;
+    h.err.kind = head->err.kind;
+    if ((int64_t)h.newlines <= nl_cap) break;
+    nl_cap = (int64_t)h.newlines + 1;  // short lines: a larger index, the call again (nothing was written)
+  }
+  const int64_t lines = (int64_t)h.lines;
   *n_out = lines;
   if (lines > cap) return set_err(ctx, GF_ERR_CAPACITY, "gf_csv_parse: more lines than capacity");
-  if (newlines > nl_cap) {  // short lines: a larger array, the index again
-    nl_cap = newlines + 1;
-    base = (char*)ctx_scratch(ctx, o_nl + sizeof(int64_t) * (size_t)nl_cap, &st);
-    if (st) return st;
-    if ((st = index())) return st;
-  }
   if (lines > (int64_t)UINT32_MAX) return set_err(ctx, GF_ERR_ARG, "gf_csv_parse: more than 2^32-1 lines");
-  // the dictionary worklist: at most one String per line
-  if ((st = dict_reserve_batch(dict, (uint64_t)lines, (uint64_t)lines))) return st;
-  GF_HIP_CHECK(ctx, hipMemsetAsync(dict->counters + 2, 0, 2 * sizeof(unsigned long long), ctx->stream));
-  int64_t* nl = (int64_t*)(base + o_nl);
-  CsvErr* err = (CsvErr*)(base + o_err);
-  GF_HIP_CHECK(ctx, hipMemsetAsync(err, 0xFF, sizeof(CsvErr), ctx->stream));
-  CsvArgs a = proto;
-  a.text = text; a.len = len; a.nl = nl; a.newlines = newlines; a.lines = lines;
-  a.x = x; a.y = y; a.objID = objID; a.ts = ts; a.cx = cx; a.cy = cy;
-  if (g) { a.minX = g->minX; a.minY = g->minY; a.cl = g->cellLength; }
-  a.err = err;
-  a.dict_work = (DictWork*)dict->work[0];
-  a.dict_n = (uint32_t*)(dict->counters + 2);
-  a.dict_bytes = dict->counters + 3;
-  GF_HIP_CHECK(ctx, launch_csv_parse(ctx, a));
-  CsvErr he{};
-  unsigned long long dn[2] = {0, 0};
-  GF_HIP_CHECK(ctx, hipMemcpyAsync(pinned, err, sizeof(CsvErr), hipMemcpyDeviceToHost, ctx->stream));
-  GF_HIP_CHECK(ctx, hipMemcpyAsync((char*)pinned + 32, dict->counters + 2, sizeof dn, hipMemcpyDeviceToHost, ctx->stream));
-  GF_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
-  std::memcpy(&he, pinned, sizeof(CsvErr));
-  std::memcpy(dn, (char*)pinned + 32, sizeof dn);
+  if (lines > 0) ctx->csv_mean_line[proto.format == 1] = (len + lines - 1) / lines;
+  const CsvErr he = h.err;
+  const unsigned long long dn[2] = {h.dict_n, h.dict_bytes};
   if (he.line != ~0ull) {
     if (bad_line) *bad_line = (int64_t)he.line;
     if (bad_kind) *bad_kind = he.kind;

@@ -651,12 +651,24 @@ GF_DHD inline uint8_t jtok_trans(int t, int b) {
 }
 
 // LDS tables of a block: per byte value the 9 syntax states' entries and the 16 token states'
-// next states; the looked-up member names
+// next states; the looked-up member names; the time / objID property names packed (geo_pack16)
+struct K16 {  // up to 16 bytes, first byte most significant: (hi, lo) after shifting each byte in
+  uint64_t hi, lo;
+};
+GF_DHD constexpr K16 geo_pack16(const char* s, int n) {
+  uint64_t hi = 0, lo = 0;
+  for (int i = 0; i < n; ++i) {
+    hi = (hi << 8) | (lo >> 56);
+    lo = (lo << 8) | (uint8_t)s[i];
+  }
+  return K16{hi, lo};
+}
 struct GeoTabs {  // (in LDS on the device)
   GF_LDS_PTR(uint64_t) tab;   // [256]: entry of state s at bits 7s..7s+6
   GF_LDS_PTR(uint64_t) ttab;  // [256]: next token state of state t at bits 4t..4t+3
   GF_LDS_PTR(char) keys;      // kGeoKeys x kGeoPropMax
   int32_t klen[kGeoKeys];
+  K16 pts, pobj;              // the time / objID property names when <= 16 bytes (klen[4], klen[5])
 };
 
 template <class Src>
@@ -675,23 +687,33 @@ GF_DHD inline int64_t jmember_value(const Src& s, int64_t k, int64_t e) {
 
 // The automaton over the line [p, e) (s(p) == '{'), staged in LDS (lds + (pos - base)).  Returns
 // false when the line must take the walk; otherwise *g = the members the map reads.
+// r05: the byte step is BRANCH-FREE.  64 lanes walk 64 different lines, so some lane meets an
+// action (a bracket, a comma, a key's quotes, a token's end) at nearly every step: as branches,
+// every step paid every case's exec-mask juggling (r04 PMC: ~210 vector + ~300 scalar
+// instructions per lane-byte).  Now each step computes every case with selects -- pushes and pops
+// update depth / kinds / roles arithmetically, the key's bytes are shifted into a 16-byte
+// accumulator while it is read, and its closing quote compares (length, accumulator) with the
+// looked-up names' packed constants.  Only literals (true / false / null) at a token's end and
+// property names longer than 16 bytes branch (rare).
 GF_DHD inline bool geo_locate(const LBytes& s, int64_t p, int64_t e, const GeoTabs& gt, int vlines,
                                            GeoPos* g) {
   if (e - p >= INT32_MAX) return false;
+  constexpr K16 kValue = geo_pack16("value", 5), kGeom = geo_pack16("geometry", 8);
+  constexpr K16 kProps = geo_pack16("properties", 10), kCoord = geo_pack16("coordinates", 11);
+  constexpr K16 kType = geo_pack16("type", 4);
   int st = JS_VAL, depth = 0, pend = JK_NONE;
   uint32_t ts = TS_IDLE;
   bool bad = false;
   uint64_t kinds = 0;  // bit d: the container at depth d is an object
   uint32_t roles = 0;  // 4 bits per depth 1..7
   int32_t ks = 0, tb = 0;
+  uint64_t khi = 0, klo = 0;  // the current key's last 16 bytes
   // closing-quote positions (from p) of the last keys noted: the record's "value"; in V: type,
   // coordinates, geometry, properties; in V.geometry: type, coordinates; in V.properties: the
   // time and objID properties
   int32_t v = -1, tV = -1, cV = -1, gV = -1, prV = -1, tG = -1, cG = -1, tP = -1, qP = -1;
-  // length filters of the keys looked up per container role (lengths < 64)
-  const uint64_t lf_top = 1ull << 5, lf_val = (1ull << 4) | (1ull << 8) | (1ull << 10) | (1ull << 11);
-  const uint64_t lf_geo = (1ull << 4) | (1ull << 11);
-  const uint64_t lf_prop = (gt.klen[4] >= 0 ? 1ull << gt.klen[4] : 0) | (gt.klen[5] >= 0 ? 1ull << gt.klen[5] : 0);
+  const int32_t lts = gt.klen[4], lobj = gt.klen[5];
+  const bool long_props = lts > 16 || lobj > 16;  // (then their names are compared byte by byte)
   const int top_role = vlines ? JR_VAL : JR_TOP;
   const int32_t o0 = (int32_t)(p - s.base), o1 = (int32_t)(e - s.base);  // the line's LDS offsets
   for (int32_t w = o0 & ~3; w < o1 && !bad; w += 4) {
@@ -705,68 +727,77 @@ GF_DHD inline bool geo_locate(const LBytes& s, int64_t p, int64_t e, const GeoTa
       int nst = (int)(ent & 15u);
       const int act = (int)(ent >> 4);
       const bool in_tok = nst == JS_TOK, in_str = nst == JS_VSTR || nst == JS_KSTR;
-      if (st == JS_TOK && !in_tok) {  // a token ended before this byte: its state decides
-        bool ok = ((kTsAccept >> ts) & 1u) && i - tb < 19;
-        if (ts == TS_LIT) {  // true / false / null
-          const int n = i - tb;
-          const char c0 = s(p + tb);
-          ok = n == (c0 == 'f' ? 5 : 4);
-          const char* wd = c0 == 't' ? "true" : c0 == 'f' ? "false" : "null";
-          for (int q = 1; ok && q < n; ++q) ok = s(p + tb + q) == wd[q];
-        }
+      // a token ended before this byte: its state decides (a literal's letters: the rare branch)
+      const bool tok_end = st == JS_TOK && !in_tok;
+      const bool lit = tok_end && ts == TS_LIT;
+      bad |= tok_end && !lit && !(((kTsAccept >> ts) & 1u) && i - tb < 19);
+      if (lit) {  // true / false / null
+        const int n = i - tb;
+        const char c0 = s(p + tb);
+        bool ok = n == (c0 == 'f' ? 5 : 4);
+        const char* wd = c0 == 't' ? "true" : c0 == 'f' ? "false" : "null";
+        for (int q = 1; ok && q < n; ++q) ok = s(p + tb + q) == wd[q];
         bad |= !ok;
       }
-      if (in_tok && st != JS_TOK) tb = i;
+      tb = in_tok && st != JS_TOK ? i : tb;
       // a string's bytes (its closing quote included) must leave the UTF-8 automaton accepting
       bad |= (in_str || st == JS_VSTR || st == JS_KSTR) && nts == TS_ERR;
       ts = in_tok || in_str ? nts : TS_IDLE;
-      if (act) {
-        const int role = (unsigned)depth <= 7u ? (int)(roles >> (4 * depth)) & 15 : JR_NONE;
-        if (act == JA_PUSH_OBJ || act == JA_PUSH_ARR) {
-          int child = depth == 0 ? top_role
-                    : role == JR_TOP ? (int)(0x0020u >> (4 * pend)) & 15   // value -> V
-                    : role == JR_VAL ? (int)(0x4300u >> (4 * pend)) & 15   // geometry, properties
-                    : JR_NONE;
-          if (act == JA_PUSH_ARR) child = JR_NONE;
-          ++depth;
-          bad |= depth > 63;
-          kinds = (kinds & ~(1ull << (depth & 63))) | ((uint64_t)(act == JA_PUSH_OBJ) << (depth & 63));
-          if ((unsigned)depth <= 7u) roles = (roles & ~(15u << (4 * depth))) | ((uint32_t)child << (4 * depth));
-        } else if (act == JA_POP_OBJ || act == JA_POP_ARR) {
-          bad |= depth <= 0 || (int)((kinds >> (depth & 63)) & 1) != (act == JA_POP_OBJ);
-          --depth;
-        } else if (act == JA_COMMA) {
-          bad |= depth <= 0;
-          nst = (kinds >> (depth & 63)) & 1 ? JS_KEY : JS_VAL;
-        } else if (act == JA_KEY_BEGIN) {
-          ks = i + 1;
-        } else {  // JA_KEY_END: note a looked-up member of a looked-up container
-          const int len = i - ks;
-          const uint64_t lf = role == JR_TOP ? lf_top : role == JR_VAL ? lf_val : role == JR_GEO ? lf_geo
-                            : role == JR_PROP ? lf_prop : 0;
-          pend = JK_NONE;
-          if (len < 64 && ((lf >> len) & 1)) {
-            const int64_t kp = p + ks;
-            if (role == JR_TOP) {
-              if (jkey_eq(s, kp, len, gt, 0)) {
-                pend = JK_VALUE;
-                v = i;
-              }
-            } else if (role == JR_VAL) {
-              if (jkey_eq(s, kp, len, gt, 6)) tV = i;
-              else if (jkey_eq(s, kp, len, gt, 3)) cV = i;
-              else if (jkey_eq(s, kp, len, gt, 1)) { pend = JK_GEO; gV = i; }
-              else if (jkey_eq(s, kp, len, gt, 2)) { pend = JK_PROP; prV = i; }
-            } else if (role == JR_GEO) {
-              if (jkey_eq(s, kp, len, gt, 6)) tG = i;
-              else if (jkey_eq(s, kp, len, gt, 3)) cG = i;
-            } else {
-              if (jkey_eq(s, kp, len, gt, 4)) tP = i;
-              if (jkey_eq(s, kp, len, gt, 5)) qP = i;
-            }
-          }
-        }
+      // the key's bytes (between its quotes) into the accumulator; its opening quote resets it
+      const bool in_key = st == JS_KSTR && nst == JS_KSTR;
+      const uint64_t nhi = (khi << 8) | (klo >> 56), nlo = (klo << 8) | byte;
+      const bool kb = act == JA_KEY_BEGIN;
+      khi = kb ? 0ull : in_key ? nhi : khi;
+      klo = kb ? 0ull : in_key ? nlo : klo;
+      ks = kb ? i + 1 : ks;
+      // containers: the role of the one we are in, a push's child role, the kind bits
+      const int role = (unsigned)depth <= 7u ? (int)(roles >> (4 * depth)) & 15 : JR_NONE;
+      const bool push = act == JA_PUSH_OBJ || act == JA_PUSH_ARR, pop = act == JA_POP_OBJ || act == JA_POP_ARR;
+      int child = depth == 0 ? top_role
+                : role == JR_TOP ? (int)(0x0020u >> (4 * pend)) & 15   // value -> V
+                : role == JR_VAL ? (int)(0x4300u >> (4 * pend)) & 15   // geometry, properties
+                : JR_NONE;
+      child = act == JA_PUSH_ARR ? JR_NONE : child;
+      const int nd = depth + 1;
+      const uint64_t nbit = 1ull << (nd & 63);
+      kinds = push ? (act == JA_PUSH_OBJ ? kinds | nbit : kinds & ~nbit) : kinds;
+      const uint32_t rsh = 4u * (uint32_t)(nd & 7);
+      roles = push && nd <= 7 ? (roles & ~(15u << rsh)) | ((uint32_t)child << rsh) : roles;
+      const bool kobj = (kinds >> (depth & 63)) & 1;  // (a pop or comma does not change kinds)
+      bad |= push && nd > 63;
+      bad |= pop && (depth <= 0 || kobj != (act == JA_POP_OBJ));
+      bad |= act == JA_COMMA && depth <= 0;
+      nst = act == JA_COMMA ? (kobj ? JS_KEY : JS_VAL) : nst;
+      depth += (int)push - (int)pop;
+      // a key's closing quote: note a looked-up member of a looked-up container
+      const bool kend = act == JA_KEY_END;
+      const int len = i - ks;
+      // (a key of <= 8 bytes leaves khi 0: the short names compare klo only)
+      const bool e_type = len == 4 && klo == kType.lo, e_value = len == 5 && klo == kValue.lo;
+      const bool e_geom = len == 8 && klo == kGeom.lo;
+      const bool e_props = len == 10 && klo == kProps.lo && khi == kProps.hi;
+      const bool e_coord = len == 11 && klo == kCoord.lo && khi == kCoord.hi;
+      const bool top = kend && role == JR_TOP, val = kend && role == JR_VAL;
+      const bool geo = kend && role == JR_GEO, prop = kend && role == JR_PROP;
+      const bool m_value = top && e_value;
+      const bool v_type = val && e_type, v_coord = val && e_coord;
+      const bool v_geom = val && e_geom, v_props = val && e_props;
+      bool p_ts = prop && len == lts && lts <= 16 && klo == gt.pts.lo && khi == gt.pts.hi;
+      bool p_obj = prop && len == lobj && lobj <= 16 && klo == gt.pobj.lo && khi == gt.pobj.hi;
+      if (long_props && prop && len > 16) {  // (rare: a property name longer than 16 bytes)
+        p_ts = jkey_eq(s, p + ks, len, gt, 4);
+        p_obj = jkey_eq(s, p + ks, len, gt, 5);
       }
+      pend = kend ? (m_value ? JK_VALUE : v_geom ? JK_GEO : v_props ? JK_PROP : JK_NONE) : pend;
+      v = m_value ? i : v;
+      tV = v_type ? i : tV;
+      cV = v_coord ? i : cV;
+      gV = v_geom ? i : gV;
+      prV = v_props ? i : prV;
+      tG = geo && e_type ? i : tG;
+      cG = geo && e_coord ? i : cG;
+      tP = p_ts ? i : tP;
+      qP = p_obj ? i : qP;
       bad |= nst == JS_ERR;
       st = nst == JS_ERR ? JS_AFT : nst;
     }

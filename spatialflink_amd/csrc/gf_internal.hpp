@@ -37,6 +37,7 @@ struct gf_ctx {
   int join_coarse = 0;  // testing: the row path without sub-cells
   int join_stream = 0;  // experiment: the fine path's streaming probe (query side bucketed only)
   int geojson_walk = 0; // testing: every GeoJSON line takes the member-by-member walk
+  int64_t csv_mean_line[2] = {0, 0};  // per format (CSV, GeoJSON): the last call's mean line length (sizes the next one's LDS staging)
   int join_async_done = 0;  // gf_join_pp_async: the packing kernel wrote the count
   double join_ppp = 0.0;  // pairs per ordinary point of the last join (sizes the output chunks)
   hipStream_t aux = nullptr;   // kNN depth >= 3: the second stream of windows in flight (created on first use)
@@ -50,6 +51,7 @@ struct gf_ctx {
   uint32_t expand_epoch = 0;
   unsigned long long* join_gctr = nullptr;  // row-bucketed join: reserved output positions (zero between calls)
   unsigned long long* join_hint = nullptr;  // mapped pinned: the pair count of the last join (async too)
+  void* csv_head = nullptr;                 // mapped pinned: the ingest head (CsvHead), written by csv_error_kernel
   uint64_t* join_hist = nullptr;            // band probe: the last join's pairs, points, slice start per block, did-not-fit ([3 * blocks + 1], zero: none)
   unsigned long long* join_ovf = nullptr;   // band probe: overflow counter (zero between calls)
   int64_t join_hint_no = 0;                 // ordinary points of that join
@@ -437,12 +439,28 @@ struct CsvErr {
   int kind;
   int pad;
 };
+// What the host reads after an ingest call's one sync: written by csv_error_kernel, the call's
+// last kernel, from the device-side counts into mapped pinned memory (gf_ctx.csv_head)
+struct CsvHead {
+  unsigned long long newlines;    // found by csv_nlindex (more than nl_cap: the index was cut)
+  unsigned long long lines;       // newlines + (unterminated last line)
+  unsigned long long dict_n;      // objIDs queued for the dictionary, and their bytes
+  unsigned long long dict_bytes;
+  CsvErr err;
+};
 struct CsvArgs {
   const char* text;
   int64_t len;
   const int64_t* nl;    // newline positions
-  int64_t newlines;
-  int64_t lines;        // newlines + (unterminated last line)
+  // the line count stays on the device between the index and the parse (no host round trip):
+  // nl_total = csv_nlindex's count; the parse writes nothing unless newlines <= nl_cap,
+  // lines <= cap and lines <= grid_lines (the host re-runs or reports after its one sync)
+  const uint32_t* nl_total;
+  int64_t nl_cap;
+  int64_t cap;          // the caller's output capacity in lines
+  int64_t grid_lines;   // lines the parse grid covers: min(nl_cap + 1, cap)
+  int64_t mean_line;    // staging hint: the mean line length (the last call's, or len / grid_lines)
+  CsvHead* head;
   char delim;
   int32_t want[4];      // field index of objID, time, x, y (csvTsvSchemaAttr)
   double* x;

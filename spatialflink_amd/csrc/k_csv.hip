@@ -105,9 +105,9 @@ __device__ int split_line(const Src& s, int64_t b, int64_t e, char d, const int3
 // x = Double.valueOf(get(x)), y = Double.valueOf(get(y)); the first missing field
 // (IndexOutOfBounds) or malformed number (NumberFormatException) is the line's error.
 template <class Src>
-__device__ __forceinline__ int eval_csv_line(const CsvArgs& a, const Src& s, int64_t j, LineOut* o) {
+__device__ __forceinline__ int eval_csv_line(const CsvArgs& a, const Src& s, int64_t j, int64_t newlines, LineOut* o) {
   const int64_t b = j == 0 ? 0 : a.nl[j - 1] + 1;
-  int64_t e = j < a.newlines ? a.nl[j] : a.len;
+  int64_t e = j < newlines ? a.nl[j] : a.len;
   if (e > b && s(e - 1) == '\r') --e;  // TextInputFormat drops the '\r' of "\r\n"
   if (e <= b) return kCsvEmptyLine;
   Field f[4] = {{0, 0}, {0, 0}, {0, 0}, {0, 0}};
@@ -142,9 +142,10 @@ __device__ __forceinline__ void geo_tabs_fill(const CsvArgs& a, uint64_t* tab, u
 
 // FAST: try the one-pass locator first (the LDS-staged path); otherwise the walk
 template <bool FAST, class Src>
-__device__ __forceinline__ int eval_geojson_line(const CsvArgs& a, const Src& s, int64_t j, LineOut* o, const GeoTabs& gt) {
+__device__ __forceinline__ int eval_geojson_line(const CsvArgs& a, const Src& s, int64_t j, int64_t newlines, LineOut* o,
+                                                 const GeoTabs& gt) {
   const int64_t b = j == 0 ? 0 : a.nl[j - 1] + 1;
-  int64_t e = j < a.newlines ? a.nl[j] : a.len;
+  int64_t e = j < newlines ? a.nl[j] : a.len;
   if (e > b && s(e - 1) == '\r') --e;
   if (e <= b) return kCsvEmptyLine;
   const int64_t p = jskip(s, b, e);
@@ -157,11 +158,12 @@ __device__ __forceinline__ int eval_geojson_line(const CsvArgs& a, const Src& s,
 
 // parse + store line j; returns true when its objID needs the dictionary (*w filled)
 template <int FMT, bool FAST, class Src>
-__device__ __forceinline__ bool parse_line(const CsvArgs& a, const Src& s, int64_t j, DictWork* w, const GeoTabs& gt) {
+__device__ __forceinline__ bool parse_line(const CsvArgs& a, const Src& s, int64_t j, int64_t newlines, DictWork* w,
+                                           const GeoTabs& gt) {
   LineOut o{0, 0, 0.0, 0.0, false, {0, 0}};
   int st;
-  if constexpr (FMT == 1) st = eval_geojson_line<FAST>(a, s, j, &o, gt);
-  else st = eval_csv_line(a, s, j, &o);
+  if constexpr (FMT == 1) st = eval_geojson_line<FAST>(a, s, j, newlines, &o, gt);
+  else st = eval_csv_line(a, s, j, newlines, &o);
   if (st != kCsvOk) {
     atomicMin(&a.err->line, (unsigned long long)j);
     return false;
@@ -185,13 +187,24 @@ __device__ __forceinline__ bool parse_line(const CsvArgs& a, const Src& s, int64
 // blocks also fill the one-pass locator's tables (geo_locate) in LDS.
 // Dictionary objIDs are queued with one atomic per wave (the queue order is free: ids follow
 // line order, k_objid.hip).
+// The chunk's line counts from the device (csv_nlindex's total): false when the parse must not
+// write -- the index was cut (more newlines than nl_cap: the host regrows and re-runs), more lines
+// than the caller's capacity (GF_ERR_CAPACITY), or than the grid covers / 2^32 - 1
+__device__ __forceinline__ bool csv_counts(const CsvArgs& a, int64_t& newlines, int64_t& lines) {
+  newlines = (int64_t)*a.nl_total;
+  lines = newlines + (a.text[a.len - 1] != '\n' ? 1 : 0);
+  return newlines <= a.nl_cap && lines <= a.cap && lines <= a.grid_lines && lines <= (int64_t)UINT32_MAX;
+}
 template <int FMT>  // 0: CSV / TSV, 1: GeoJSON (a.format)
 __global__ __launch_bounds__(kBlock) void csv_parse_kernel(CsvArgs a) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
+  int64_t newlines, lines;
+  const bool ok = csv_counts(a, newlines, lines);
   const int64_t L0 = (int64_t)blockIdx.x * kBlock;
-  const int64_t L1 = L0 + kBlock < a.lines ? L0 + kBlock : a.lines;  // exclusive
+  if (!ok || L0 >= lines) return;  // block-uniform
+  const int64_t L1 = L0 + kBlock < lines ? L0 + kBlock : lines;  // exclusive
   const int64_t b0 = L0 == 0 ? 0 : a.nl[L0 - 1] + 1;
-  const int64_t b1 = L1 - 1 < a.newlines ? a.nl[L1 - 1] : a.len;     // the last line's '\n' (or end)
+  const int64_t b1 = L1 - 1 < newlines ? a.nl[L1 - 1] : a.len;     // the last line's '\n' (or end)
   const int64_t a0 = b0 & ~(int64_t)15;
   const int64_t j = L0 + threadIdx.x;
   DictWork w{0, 0, 0};
@@ -199,7 +212,9 @@ __global__ __launch_bounds__(kBlock) void csv_parse_kernel(CsvArgs a) {
   __shared__ uint64_t gtab[FMT == 1 ? 256 : 1], gttab[FMT == 1 ? 256 : 1];
   __shared__ char gkeys[FMT == 1 ? kGeoKeys * kGeoPropMax : 1];
   const GeoTabs gt{(GF_LDS_PTR(uint64_t))gtab, (GF_LDS_PTR(uint64_t))gttab, (GF_LDS_PTR(char))gkeys,
-                   {5, 8, 10, 11, a.len_ts, a.len_obj, 4}};
+                   {5, 8, 10, 11, a.len_ts, a.len_obj, 4},
+                   geo_pack16(a.prop_ts, a.len_ts <= 16 ? a.len_ts : 0),
+                   geo_pack16(a.prop_obj, a.len_obj <= 16 ? a.len_obj : 0)};
   if (FMT == 1) {
     geo_tabs_fill(a, gtab, gttab, gkeys);
     __syncthreads();
@@ -214,11 +229,11 @@ __global__ __launch_bounds__(kBlock) void csv_parse_kernel(CsvArgs a) {
     }
     __syncthreads();
     if (j < L1) {
-      if (a.geo_fast) need = parse_line<FMT, true>(a, LBytes{(GF_LDS_PTR(char))lds, a0}, j, &w, gt);
-      else need = parse_line<FMT, false>(a, LBytes{(GF_LDS_PTR(char))lds, a0}, j, &w, gt);
+      if (a.geo_fast) need = parse_line<FMT, true>(a, LBytes{(GF_LDS_PTR(char))lds, a0}, j, newlines, &w, gt);
+      else need = parse_line<FMT, false>(a, LBytes{(GF_LDS_PTR(char))lds, a0}, j, newlines, &w, gt);
     }
   } else if (j < L1) {
-    need = parse_line<FMT, false>(a, GBytes{a.text}, j, &w, gt);
+    need = parse_line<FMT, false>(a, GBytes{a.text}, j, newlines, &w, gt);
   }
   const uint64_t m = __ballot(need);
   if (m) {
@@ -236,20 +251,35 @@ __global__ __launch_bounds__(kBlock) void csv_parse_kernel(CsvArgs a) {
   }
 }
 
-// error kind of the first bad line (re-derived by a one-lane pass over that line)
+// The call's last kernel: the error kind of the first bad line (re-derived by a one-lane pass over
+// that line), then the head the host reads back in one copy (counts, error, dictionary work)
 __global__ void csv_error_kernel(CsvArgs a) {
+  int64_t newlines, lines;
+  csv_counts(a, newlines, lines);
   const unsigned long long j = a.err->line;
-  if (j == ~0ull) return;  // block-uniform
-  __shared__ uint64_t gtab[256], gttab[256];
-  __shared__ char gkeys[kGeoKeys * kGeoPropMax];
-  const GeoTabs gt{(GF_LDS_PTR(uint64_t))gtab, (GF_LDS_PTR(uint64_t))gttab, (GF_LDS_PTR(char))gkeys,
-                   {5, 8, 10, 11, a.len_ts, a.len_obj, 4}};
-  if (a.format == 1) geo_tabs_fill(a, gtab, gttab, gkeys);
-  __syncthreads();
-  if (threadIdx.x != 0) return;
-  LineOut o{0, 0, 0.0, 0.0, false, {0, 0}};
-  const GBytes s{a.text};
-  a.err->kind = a.format == 1 ? eval_geojson_line<false>(a, s, (int64_t)j, &o, gt) : eval_csv_line(a, s, (int64_t)j, &o);
+  if (j != ~0ull) {  // block-uniform
+    __shared__ uint64_t gtab[256], gttab[256];
+    __shared__ char gkeys[kGeoKeys * kGeoPropMax];
+    const GeoTabs gt{(GF_LDS_PTR(uint64_t))gtab, (GF_LDS_PTR(uint64_t))gttab, (GF_LDS_PTR(char))gkeys,
+                     {5, 8, 10, 11, a.len_ts, a.len_obj, 4},
+                     geo_pack16(a.prop_ts, a.len_ts <= 16 ? a.len_ts : 0),
+                     geo_pack16(a.prop_obj, a.len_obj <= 16 ? a.len_obj : 0)};
+    if (a.format == 1) geo_tabs_fill(a, gtab, gttab, gkeys);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      LineOut o{0, 0, 0.0, 0.0, false, {0, 0}};
+      const GBytes s{a.text};
+      a.err->kind = a.format == 1 ? eval_geojson_line<false>(a, s, (int64_t)j, newlines, &o, gt)
+                                  : eval_csv_line(a, s, (int64_t)j, newlines, &o);
+    }
+  }
+  if (threadIdx.x == 0) {
+    a.head->newlines = (unsigned long long)newlines;
+    a.head->lines = (unsigned long long)lines;
+    a.head->dict_n = *a.dict_n;
+    a.head->dict_bytes = *a.dict_bytes;
+    a.head->err = *a.err;
+  }
 }
 
 // The newline index in ONE pass over the text (r05; the count + scan + index passes read the text
@@ -365,14 +395,14 @@ hipError_t launch_csv_nlindex(hipStream_t st, const char* text, int64_t len, int
 hipError_t launch_csv_parse(gf_ctx* ctx, const CsvArgs& a0) {
   KTimer t(ctx, GF_K_CSV_PARSE);
   CsvArgs a = a0;
-  const int64_t mean = a.lines > 0 ? (a.len + a.lines - 1) / a.lines : 0;
+  const int64_t mean = a.mean_line;
   const int64_t need = mean * kBlock;
   int64_t cap = (need * 11 / 10 + 1023) & ~(int64_t)1023;
   constexpr int64_t kGeoLds3 = 50 * 1024;
   if (a.format == 1 && cap > kGeoLds3 && need * 20 <= kGeoLds3 * 19) cap = kGeoLds3;
   a.lds_cap = (int32_t)(cap < kCsvLds ? kCsvLds : cap > kCsvLdsMax ? kCsvLdsMax : cap);
-  if (a.lines > 0) {
-    const unsigned blocks = (unsigned)((a.lines + kBlock - 1) / kBlock);
+  if (a.grid_lines > 0) {  // (blocks past the chunk's lines return at once)
+    const unsigned blocks = (unsigned)((a.grid_lines + kBlock - 1) / kBlock);
     if (a.format == 1)
       hipLaunchKernelGGL(csv_parse_kernel<1>, dim3(blocks), dim3(kBlock), (size_t)a.lds_cap, ctx->stream, a);
     else

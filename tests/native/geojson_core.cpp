@@ -26,7 +26,9 @@ extern "C" void geojson_core_parse(const char* buf, const int64_t* off, int64_t 
   const int len_obj = prop_obj ? (int)std::strlen(prop_obj) : -1, len_ts = prop_ts ? (int)std::strlen(prop_ts) : -1;
   if (prop_ts) std::memcpy(keys + 4 * gf::kGeoPropMax, prop_ts, len_ts);
   if (prop_obj) std::memcpy(keys + 5 * gf::kGeoPropMax, prop_obj, len_obj);
-  const gf::GeoTabs gt{tab, ttab, keys, {5, 8, 10, 11, len_ts, len_obj, 4}};
+  const gf::GeoTabs gt{tab, ttab, keys, {5, 8, 10, 11, len_ts, len_obj, 4},
+                       gf::geo_pack16(keys + 4 * gf::kGeoPropMax, len_ts <= 16 ? len_ts : 0),
+                       gf::geo_pack16(keys + 5 * gf::kGeoPropMax, len_obj <= 16 ? len_obj : 0)};
   const gf::GeoProps gp{keys + 4 * gf::kGeoPropMax, keys + 5 * gf::kGeoPropMax, len_ts, len_obj, date_fmt,
                         (int64_t)tz_off_min * 60000, kPow5Host};
   for (int64_t j = 0; j < n; ++j) {

@@ -89,3 +89,24 @@ def test_mutations(core, oracle_mod):
             c = bytes([alphabet[int(rng.integers(0, len(alphabet)))]])
             out.append(ln[:i] + c + ln[i + 1:] if op == 0 else ln[:i] + ln[i + 1:] if op == 1 else ln[:i] + c + ln[i:])
     compare(core, oracle_mod, out)
+
+
+@pytest.mark.parametrize("obj_name,ts_name", [("objid_17_chars_xy", "timestamp_abcdef"),   # 17 and 16 bytes
+                                              ("a_very_long_object_identifier", "t"),       # 29 and 1
+                                              ("oID", "the_time_property_name_longer")])    # 3 and 29
+def test_property_name_lengths(core, oracle_mod, obj_name, ts_name):
+    """The locator matches member names by (length, 16-byte packed accumulator) and compares names
+    longer than 16 bytes byte by byte: property names of 1, 3, 16, 17 and 29 bytes, with decoy
+    members whose names share the length (and the last 16 bytes) but not the bytes."""
+    lns = lines(53, 400, 0).split(b"\n")[:-1]
+    o, t = obj_name.encode(), ts_name.encode()
+    decoy_o = (b"X" + o[1:]) if len(o) > 1 else b"Y"
+    decoy_t = (b"Z" + t[1:]) if len(t) > 1 else b"W"
+    out = []
+    for k, ln in enumerate(lns):
+        ln = ln.replace(b'"oID"', b'"' + o + b'"').replace(b'"timestamp"', b'"' + t + b'"')
+        if k % 3 == 0:  # decoys (same lengths, different first byte) before the real members
+            ln = ln.replace(b'"properties": {', b'"properties": {"' + decoy_o + b'": "decoy", "' + decoy_t + b'": 7, ', 1)
+            ln = ln.replace(b'"properties":{', b'"properties":{"' + decoy_o + b'":"decoy","' + decoy_t + b'":7,', 1)
+        out.append(ln)
+    compare(core, oracle_mod, out, props=(obj_name, ts_name))
