@@ -51,31 +51,60 @@ __device__ __forceinline__ bool java_s(char c) {  // regex \s: [ \t\n\x0B\f\r]
 
 
 // Field ranges of the wanted columns of line [b, e).  Returns the number of fields.
+// A delimiter that is not whitespace (r05): the scan is branch-free -- every delimiter byte
+// selects the wanted fields' raw ranges and advances the field count -- and only the (at most 4)
+// wanted fields are trimmed afterwards, as close() below trims every field as it goes (64 lanes
+// on 64 lines meet delimiters at different bytes: as a branch, close() ran at most steps).
 template <class Src>
 __device__ int split_line(const Src& s, int64_t b, int64_t e, char d, const int32_t* want, Field* got) {
   const bool wsd = java_s(d);
-  int field = 0;
-  int64_t fs = b;
-  auto close = [&](int64_t fe, bool last) {
-    int64_t x0 = fs, x1 = fe;
-    if (!wsd) {  // whitespace next to a delimiter belongs to the delimiter
-      if (field > 0)
-        while (x0 < x1 && (java_s(s(x0)) || s(x0) == '"')) ++x0;
-      if (!last)
-        while (x1 > x0 && (java_s(s(x1 - 1)) || s(x1 - 1) == '"')) --x1;
+  if (!wsd) {
+    int32_t wk[4];
+    int64_t gb[4], ge[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      wk[k] = want[k];
+      gb[k] = ge[k] = -1;
+    }
+    int32_t field = 0;
+    int64_t fs = b;
+    for (int64_t i = b; i < e; ++i) {
+      const bool isd = s(i) == d;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const bool c = isd && wk[k] == field;
+        gb[k] = c ? fs : gb[k];
+        ge[k] = c ? i : ge[k];
+      }
+      field += (int32_t)isd;
+      fs = isd ? i + 1 : fs;
     }
 #pragma unroll
+    for (int k = 0; k < 4; ++k) {  // the last field [fs, e); then the wanted fields trimmed
+      if (wk[k] == field) {
+        gb[k] = fs;
+        ge[k] = e;
+      }
+      if (gb[k] < 0) continue;
+      int64_t x0 = gb[k], x1 = ge[k];
+      if (wk[k] > 0)  // whitespace (and quotes) next to a delimiter belong to the delimiter
+        while (x0 < x1 && (java_s(s(x0)) || s(x0) == '"')) ++x0;
+      if (wk[k] != field)
+        while (x1 > x0 && (java_s(s(x1 - 1)) || s(x1 - 1) == '"')) --x1;
+      got[k] = Field{x0, x1};
+    }
+    return field + 1;
+  }
+  // a whitespace delimiter: a run of whitespace (quotes are transparent) holding it is one separator
+  int field = 0;
+  int64_t fs = b;
+  auto close = [&](int64_t fe) {
+#pragma unroll
     for (int k = 0; k < 4; ++k)
-      if (want[k] == field) got[k] = Field{x0, x1};
+      if (want[k] == field) got[k] = Field{fs, fe};
     ++field;
   };
-  if (!wsd) {
-    for (int64_t i = b; i < e; ++i)
-      if (s(i) == d) {
-        close(i, false);
-        fs = i + 1;
-      }
-  } else {  // a run of whitespace (quotes are transparent) holding a delimiter is one separator
+  {
     int64_t i = b;
     while (i < e) {
       const char c = s(i);
@@ -87,7 +116,7 @@ __device__ int split_line(const Src& s, int64_t b, int64_t e, char d, const int3
           ++j;
         }
         if (hd) {
-          close(i, false);
+          close(i);
           fs = j;
         }
         i = j;
@@ -96,7 +125,7 @@ __device__ int split_line(const Src& s, int64_t b, int64_t e, char d, const int3
       }
     }
   }
-  close(e, true);
+  close(e);
   return field;
 }
 

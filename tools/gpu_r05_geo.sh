@@ -1,13 +1,15 @@
 #!/bin/bash
-# round-5 GeoJSON locator (branch-free byte step): the GeoJSON GPU tests, the bench line, kernel stats
+# round-5 ingest kernels (branch-free GeoJSON locator, branch-free CSV field split): the ingest GPU
+# tests, the CSV and GeoJSON bench lines, kernel stats
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 S=tools/gpu_step.sh
 $S t_geo 600 python -u -m pytest -x -v --timeout 200 --timeout-method thread -p no:cacheprovider \
-  tests/test_gpu_geojson.py tests/test_shim_native.py -k "geojson or parse" || exit 1
+  tests/test_gpu_csv.py tests/test_gpu_geojson.py tests/test_shim_native.py -k "csv or geojson or parse" || exit 1
 grep -q " passed" gpurun_out/t_geo.log && ! grep -q "FAILED\|ERROR" gpurun_out/t_geo.log || exit 1
+$S geo_csv 300 python -u bench.py --workload csv --steps 20 --warmup 3 --no-cpu-baseline || exit 1
 $S geo_b1 300 python -u bench.py --workload geojson --steps 20 --warmup 3 --no-cpu-baseline || exit 1
-$S geo_prof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/geo_prof -o stats --output-format csv -- python -u bench.py --workload geojson --steps 10 --warmup 2 --no-cpu-baseline --no-verify || exit 1
-for f in gpurun_out/geo_b*.log; do
+$S geo_prof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/geo_prof -o stats --output-format csv -- python -u bench.py --workload csv --steps 20 --warmup 3 --no-cpu-baseline --no-verify || exit 1
+for f in gpurun_out/geo_b*.log gpurun_out/geo_csv.log; do
   echo "$f $(grep -h '^{' $f | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["ms_per_step"], d.get("verified_vs_oracle"), json.dumps(d.get("breakdown"))[:200])')"
 done
