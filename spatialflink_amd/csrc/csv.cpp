@@ -58,13 +58,12 @@ static int parse_text_lines(gf_ctx* ctx, gf_objid_dict* dict, const char* text, 
     const int64_t grid_lines = std::min<int64_t>(nl_cap + 1, cap);
     // the dictionary worklist: at most one String per line
     if (grid_lines > 0 && (st = dict_reserve_batch(dict, (uint64_t)grid_lines, (uint64_t)grid_lines))) return st;
-    GF_HIP_CHECK(ctx, hipMemsetAsync(dict->counters + 2, 0, 2 * sizeof(unsigned long long), ctx->stream));
     CsvErr* err = (CsvErr*)(base + o_err);
-    GF_HIP_CHECK(ctx, hipMemsetAsync(err, 0xFF, sizeof(CsvErr), ctx->stream));
     ExpandState es;
     if ((st = lookback_state(ctx, nseg, &es))) return st;
+    // (the index's first block also resets the error slot and the dictionary counters)
     GF_HIP_CHECK(ctx, launch_csv_nlindex(ctx->stream, text, len, nseg, (int64_t*)(base + o_nl), nl_cap,
-                                         (uint32_t*)(base + o_tot), es));
+                                         (uint32_t*)(base + o_tot), es, err, dict->counters + 2));
     ctx->expand_base += (unsigned long long)nseg;
     CsvArgs a = proto;
     a.text = text; a.len = len; a.nl = (int64_t*)(base + o_nl);

@@ -488,7 +488,7 @@ struct CsvArgs {
   int32_t value_lines;           // GeoJSON: 1 = each line is the record's value (else the record)
 };
 hipError_t launch_csv_nlindex(hipStream_t st, const char* text, int64_t len, int64_t nseg, int64_t* nl, int64_t nl_cap,
-                              uint32_t* total, const ExpandState& es);
+                              uint32_t* total, const ExpandState& es, CsvErr* err, unsigned long long* dict_counters);
 int lookback_state(gf_ctx* ctx, int64_t blocks, ExpandState* es);  // api.cpp
 hipError_t launch_csv_parse(gf_ctx* ctx, const CsvArgs& a);
 

@@ -321,13 +321,20 @@ __global__ void csv_error_kernel(CsvArgs a) {
 constexpr int kNlIters = (int)(kCsvSeg / (16 * kBlock));
 __global__ __launch_bounds__(kBlock) void csv_nlindex_kernel(const char* __restrict__ text, int64_t len,
                                                              int64_t* __restrict__ nl, int64_t nl_cap,
-                                                             uint32_t* __restrict__ total, ExpandState st) {
+                                                             uint32_t* __restrict__ total, ExpandState st,
+                                                             CsvErr* __restrict__ err,
+                                                             unsigned long long* __restrict__ dict_counters) {
   __shared__ unsigned long long s_bid, s_prefix;
   __shared__ uint32_t ws[kBlock / 64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   if (threadIdx.x == 0) s_bid = atomicAdd(st.ticket, 1ull) - st.base;
   __syncthreads();
   const uint64_t bid = s_bid;
+  if (bid == 0 && threadIdx.x == 0) {  // the parse's error slot and dictionary counters (no memset launches)
+    *err = CsvErr{~0ull, -1, -1};
+    dict_counters[0] = 0ull;
+    dict_counters[1] = 0ull;
+  }
   const int64_t s0 = (int64_t)bid * kCsvSeg;
   const int64_t s1 = s0 + kCsvSeg < len ? s0 + kCsvSeg : len;
   uint32_t m[kNlIters], c = 0;
@@ -410,8 +417,9 @@ __global__ __launch_bounds__(kBlock) void csv_nlindex_kernel(const char* __restr
 }
 
 hipError_t launch_csv_nlindex(hipStream_t st, const char* text, int64_t len, int64_t nseg, int64_t* nl, int64_t nl_cap,
-                              uint32_t* total, const ExpandState& es) {
-  hipLaunchKernelGGL(csv_nlindex_kernel, dim3((unsigned)nseg), dim3(kBlock), 0, st, text, len, nl, nl_cap, total, es);
+                              uint32_t* total, const ExpandState& es, CsvErr* err, unsigned long long* dict_counters) {
+  hipLaunchKernelGGL(csv_nlindex_kernel, dim3((unsigned)nseg), dim3(kBlock), 0, st, text, len, nl, nl_cap, total, es,
+                     err, dict_counters);
   return hipGetLastError();
 }
 
