@@ -695,6 +695,9 @@ GF_DHD inline int64_t jmember_value(const Src& s, int64_t k, int64_t e) {
 // accumulator while it is read, and its closing quote compares (length, accumulator) with the
 // looked-up names' packed constants.  Only literals (true / false / null) at a token's end and
 // property names longer than 16 bytes branch (rare).
+#ifndef GF_GEO_UNROLL
+#define GF_GEO_UNROLL 4  // byte steps of a word unrolled
+#endif
 GF_DHD inline bool geo_locate(const LBytes& s, int64_t p, int64_t e, const GeoTabs& gt, int vlines,
                                            GeoPos* g) {
   if (e - p >= INT32_MAX) return false;
@@ -718,7 +721,7 @@ GF_DHD inline bool geo_locate(const LBytes& s, int64_t p, int64_t e, const GeoTa
   const int32_t o0 = (int32_t)(p - s.base), o1 = (int32_t)(e - s.base);  // the line's LDS offsets
   for (int32_t w = o0 & ~3; w < o1 && !bad; w += 4) {
     const uint32_t word = *reinterpret_cast<const uint32_t*>(s.p + w);
-#pragma unroll
+#pragma unroll GF_GEO_UNROLL
     for (int k = 0; k < 4; ++k) {
       const int32_t i = w + k - o0;  // offset in the line
       const uint32_t byte = i < 0 || w + k >= o1 ? (uint32_t)' ' : (word >> (8 * k)) & 0xFFu;

@@ -1,6 +1,7 @@
 #!/bin/bash
 # round-5 ingest kernels (branch-free GeoJSON locator, branch-free CSV field split): the ingest GPU
-# tests, the CSV and GeoJSON bench lines, kernel stats
+# tests, the CSV and GeoJSON bench lines, kernel stats; A/B of the locator's byte-step unroll
+# (explibs/geo2: tools/build_exp.sh geo2 k_csv.hip "-DGF_GEO_UNROLL=2")
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 S=tools/gpu_step.sh
@@ -10,6 +11,7 @@ grep -q " passed" gpurun_out/t_geo.log && ! grep -q "FAILED\|ERROR" gpurun_out/t
 $S geo_csv 300 python -u bench.py --workload csv --steps 20 --warmup 3 --no-cpu-baseline || exit 1
 $S geo_b1 300 python -u bench.py --workload geojson --steps 20 --warmup 3 --no-cpu-baseline || exit 1
 $S geo_prof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/geo_prof -o stats --output-format csv -- python -u bench.py --workload csv --steps 20 --warmup 3 --no-cpu-baseline --no-verify || exit 1
+TAG=gu bash tools/gpu_ab.sh "--workload geojson --steps 10 --warmup 2" geo2 || exit 1
 for f in gpurun_out/geo_b*.log gpurun_out/geo_csv.log; do
   echo "$f $(grep -h '^{' $f | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["ms_per_step"], d.get("verified_vs_oracle"), json.dumps(d.get("breakdown"))[:200])')"
 done
