@@ -655,7 +655,7 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(1000.0 * elapsed / args.steps, 4),
+            "ms_per_step": round(1000.0 * elapsed / args.steps, 6),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,

@@ -23,7 +23,9 @@ def test_roofline_table_reproduces_lines(tmp_path, rnd):
     assert len(rows) >= 13
     for r in rows:
         if r["frac_line"] is not None and r["frac_recomputed"] is not None:
-            assert abs(r["frac_recomputed"] - r["frac_line"]) <= 0.01 * max(r["frac_line"], 1e-9) + 0.002, r
+            # (ms_per_step is printed to 4 decimals: a 3.3 us window carries 1.5 % of rounding)
+            rel = 0.01 + 0.00005 / max(r["ms_per_step"], 1e-9)
+            assert abs(r["frac_recomputed"] - r["frac_line"]) <= rel * max(r["frac_line"], 1e-9) + 0.002, r
     # every line with a committed PMC summary has its traffic ratio; streaming lines read each
     # byte about once
     covered = {r["workload"]: r["traffic_ratio"] for r in rows if r["pmc"]}

@@ -197,7 +197,7 @@ def _line(workload, value, unit, steps, warmup, elapsed, kernel, bytes_per_launc
         return
     achieved = bytes_per_launch / avg_s / 1e9 if avg_s > 0 else None
     d = {"metric": f"points/sec per window ({workload})", "value": round(value, 1), "unit": unit, "n_gpus": 1,
-         "steps": steps, "warmup": warmup, "ms_per_step": round(1000.0 * elapsed / steps, 4),
+         "steps": steps, "warmup": warmup, "ms_per_step": round(1000.0 * elapsed / steps, 6),
          "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
          "data": data_desc(),
          "roofline": {"bound": "hbm", "kernel": kernel, "achieved": round(achieved, 1) if achieved else None,
@@ -985,7 +985,7 @@ def bench_sliding(args):
         steps = args.steps
         d = {"metric": "points/sec per window (sliding-window kNN k=100)", "value": round(window_pts * steps / elapsed, 1),
              "unit": "window points/s", "n_gpus": world, "steps": steps, "warmup": args.warmup,
-             "ms_per_step": round(1000.0 * elapsed / steps, 4), "higher_is_better": True,
+             "ms_per_step": round(1000.0 * elapsed / steps, 6), "higher_is_better": True,
              "scaling": "strong" if world > 1 else "weak", "vs_baseline": None, "dtype": "f64",
              "data": f"synthetic: java.util.Random-compatible uniform points, Beijing bounds, {npanes} distinct "
                      "device-resident panes cycled",
