@@ -685,6 +685,164 @@ GF_DHD inline int64_t jmember_value(const Src& s, int64_t k, int64_t e) {
   return jskip(s, jskip(s, k + 1, e) + 1, e);
 }
 
+// The automaton's state over one line.  n[]: closing-quote positions (from p) of the last keys
+// noted: the record's "value"; in V: type, coordinates, geometry, properties; in V.geometry:
+// type, coordinates; in V.properties: the time and objID properties (-1: none).
+enum { GN_V, GN_TV, GN_CV, GN_GV, GN_PRV, GN_TG, GN_CG, GN_TP, GN_QP, kGeoNotes };
+struct GeoLoc {
+  int st, depth, pend;
+  uint32_t ts;
+  bool bad;
+  uint64_t kinds;  // bit d: the container at depth d is an object
+  uint32_t roles;  // 4 bits per depth 1..7
+  int32_t ks, tb;
+  uint64_t khi, klo;  // the current key's last 16 bytes
+  int32_t n[kGeoNotes];
+};
+GF_DHD inline void geo_loc_init(GeoLoc& L) {
+  L.st = JS_VAL;
+  L.depth = 0;
+  L.pend = JK_NONE;
+  L.ts = TS_IDLE;
+  L.bad = false;
+  L.kinds = 0;
+  L.roles = 0;
+  L.ks = 0;
+  L.tb = 0;
+  L.khi = 0;
+  L.klo = 0;
+  for (int k = 0; k < kGeoNotes; ++k) L.n[k] = -1;
+}
+// One byte step: `byte` at offset i of the line [p, e) (a blank for the word's bytes outside it).
+// top_role: JR_VAL for value lines, JR_TOP for Kafka records.
+GF_DHD inline void geo_step(GeoLoc& L, uint32_t byte, int32_t i, const LBytes& s, int64_t p, const GeoTabs& gt,
+                            int top_role) {
+  constexpr K16 kValue = geo_pack16("value", 5), kGeom = geo_pack16("geometry", 8);
+  constexpr K16 kProps = geo_pack16("properties", 10), kCoord = geo_pack16("coordinates", 11);
+  constexpr K16 kType = geo_pack16("type", 4);
+  const int32_t lts = gt.klen[4], lobj = gt.klen[5];
+  const int st = L.st;
+  const uint32_t ts = L.ts;
+  const uint32_t ent = (uint32_t)(gt.tab[byte] >> (7 * st)) & 0x7Fu;
+  const uint32_t nts = (uint32_t)(gt.ttab[byte] >> (4 * ts)) & 15u;
+  int nst = (int)(ent & 15u);
+  const int act = (int)(ent >> 4);
+  const bool in_tok = nst == JS_TOK, in_str = nst == JS_VSTR || nst == JS_KSTR;
+  // a token ended before this byte: its state decides (a literal's letters: the rare branch)
+  const bool tok_end = st == JS_TOK && !in_tok;
+  const bool lit = tok_end && ts == TS_LIT;
+  bool bad = L.bad;
+  bad |= tok_end && !lit && !(((kTsAccept >> ts) & 1u) && i - L.tb < 19);
+  if (lit) {  // true / false / null
+    const int n = i - L.tb;
+    const char c0 = s(p + L.tb);
+    bool ok = n == (c0 == 'f' ? 5 : 4);
+    const char* wd = c0 == 't' ? "true" : c0 == 'f' ? "false" : "null";
+    for (int q = 1; ok && q < n; ++q) ok = s(p + L.tb + q) == wd[q];
+    bad |= !ok;
+  }
+  L.tb = in_tok && st != JS_TOK ? i : L.tb;
+  // a string's bytes (its closing quote included) must leave the UTF-8 automaton accepting
+  bad |= (in_str || st == JS_VSTR || st == JS_KSTR) && nts == TS_ERR;
+  L.ts = in_tok || in_str ? nts : TS_IDLE;
+  // the key's bytes (between its quotes) into the accumulator; its opening quote resets it
+  const bool in_key = st == JS_KSTR && nst == JS_KSTR;
+  const uint64_t khi = L.khi, klo = L.klo;
+  const uint64_t nhi = (khi << 8) | (klo >> 56), nlo = (klo << 8) | byte;
+  const bool kb = act == JA_KEY_BEGIN;
+  L.khi = kb ? 0ull : in_key ? nhi : khi;
+  L.klo = kb ? 0ull : in_key ? nlo : klo;
+  L.ks = kb ? i + 1 : L.ks;
+  // containers: the role of the one we are in, a push's child role, the kind bits
+  const int depth = L.depth;
+  const int role = (unsigned)depth <= 7u ? (int)(L.roles >> (4 * depth)) & 15 : JR_NONE;
+  const bool push = act == JA_PUSH_OBJ || act == JA_PUSH_ARR, pop = act == JA_POP_OBJ || act == JA_POP_ARR;
+  int child = depth == 0 ? top_role
+            : role == JR_TOP ? (int)(0x0020u >> (4 * L.pend)) & 15   // value -> V
+            : role == JR_VAL ? (int)(0x4300u >> (4 * L.pend)) & 15   // geometry, properties
+            : JR_NONE;
+  child = act == JA_PUSH_ARR ? JR_NONE : child;
+  const int nd = depth + 1;
+  const uint64_t nbit = 1ull << (nd & 63);
+  L.kinds = push ? (act == JA_PUSH_OBJ ? L.kinds | nbit : L.kinds & ~nbit) : L.kinds;
+  const uint32_t rsh = 4u * (uint32_t)(nd & 7);
+  L.roles = push && nd <= 7 ? (L.roles & ~(15u << rsh)) | ((uint32_t)child << rsh) : L.roles;
+  const bool kobj = (L.kinds >> (depth & 63)) & 1;  // (a pop or comma does not change kinds)
+  bad |= push && nd > 63;
+  bad |= pop && (depth <= 0 || kobj != (act == JA_POP_OBJ));
+  bad |= act == JA_COMMA && depth <= 0;
+  nst = act == JA_COMMA ? (kobj ? JS_KEY : JS_VAL) : nst;
+  L.depth = depth + (int)push - (int)pop;
+  // a key's closing quote: note a looked-up member of a looked-up container
+  const bool kend = act == JA_KEY_END;
+  const int len = i - L.ks;
+  const uint64_t chi = L.khi, clo = L.klo;
+  // (a key of <= 8 bytes leaves khi 0: the short names compare klo only)
+  const bool e_type = len == 4 && clo == kType.lo, e_value = len == 5 && clo == kValue.lo;
+  const bool e_geom = len == 8 && clo == kGeom.lo;
+  const bool e_props = len == 10 && clo == kProps.lo && chi == kProps.hi;
+  const bool e_coord = len == 11 && clo == kCoord.lo && chi == kCoord.hi;
+  const bool top = kend && role == JR_TOP, val = kend && role == JR_VAL;
+  const bool geo = kend && role == JR_GEO, prop = kend && role == JR_PROP;
+  const bool m_value = top && e_value;
+  const bool v_type = val && e_type, v_coord = val && e_coord;
+  const bool v_geom = val && e_geom, v_props = val && e_props;
+  bool p_ts = prop && len == lts && lts <= 16 && clo == gt.pts.lo && chi == gt.pts.hi;
+  bool p_obj = prop && len == lobj && lobj <= 16 && clo == gt.pobj.lo && chi == gt.pobj.hi;
+  if ((lts > 16 || lobj > 16) && prop && len > 16) {  // (rare: a property name longer than 16 bytes)
+    p_ts = jkey_eq(s, p + L.ks, len, gt, 4);
+    p_obj = jkey_eq(s, p + L.ks, len, gt, 5);
+  }
+  L.pend = kend ? (m_value ? JK_VALUE : v_geom ? JK_GEO : v_props ? JK_PROP : JK_NONE) : L.pend;
+  L.n[GN_V] = m_value ? i : L.n[GN_V];
+  L.n[GN_TV] = v_type ? i : L.n[GN_TV];
+  L.n[GN_CV] = v_coord ? i : L.n[GN_CV];
+  L.n[GN_GV] = v_geom ? i : L.n[GN_GV];
+  L.n[GN_PRV] = v_props ? i : L.n[GN_PRV];
+  L.n[GN_TG] = geo && e_type ? i : L.n[GN_TG];
+  L.n[GN_CG] = geo && e_coord ? i : L.n[GN_CG];
+  L.n[GN_TP] = p_ts ? i : L.n[GN_TP];
+  L.n[GN_QP] = p_obj ? i : L.n[GN_QP];
+  bad |= nst == JS_ERR;
+  L.bad = bad;
+  L.st = nst == JS_ERR ? JS_AFT : nst;
+}
+// the line passed the automaton (valid, nothing the walk must check)
+GF_DHD inline bool geo_loc_ok(const GeoLoc& L) { return !L.bad && L.st == JS_AFT && L.depth == 0; }
+// The members the map reads from a passing line's notes n[] (positions from p; -1 none).
+template <class Src>
+GF_DHD inline void geo_notes_pos(const Src& s, int64_t p, int64_t e, int vlines, const int32_t* n, GeoPos* g) {
+  auto val = [&](int32_t k) { return k < 0 ? (int64_t)-1 : jmember_value(s, p + k, e); };
+  // notes inside an earlier "value" object, geometry or properties member are stale
+  const int32_t vb = vlines ? -1 : n[GN_V];
+  g->V = vlines ? p : val(n[GN_V]);
+  g->tV = val(n[GN_TV] > vb ? n[GN_TV] : -1);
+  g->cV = val(n[GN_CV] > vb ? n[GN_CV] : -1);
+  const int32_t gv = n[GN_GV] > vb ? n[GN_GV] : -1, pv = n[GN_PRV] > vb ? n[GN_PRV] : -1;
+  g->gV = val(gv);
+  g->tG = val(gv >= 0 && n[GN_TG] > gv ? n[GN_TG] : -1);
+  g->cG = val(gv >= 0 && n[GN_CG] > gv ? n[GN_CG] : -1);
+  g->prV = val(pv);
+  g->tsP = val(pv >= 0 && n[GN_TP] > pv ? n[GN_TP] : -1);
+  g->qP = val(pv >= 0 && n[GN_QP] > pv ? n[GN_QP] : -1);
+  g->escV = g->escG = g->escP = false;
+}
+// One word (4 LDS bytes at offset w from the staging base) of the line whose LDS offsets are
+// [o0, o1).  r05: the byte step is BRANCH-FREE (see geo_locate)
+#ifndef GF_GEO_UNROLL
+#define GF_GEO_UNROLL 2  // byte steps of a word unrolled (r05 A/B, parse us per 1M lines: 2 -> 3042-3048, 4 -> 3082-3086)
+#endif
+GF_DHD inline void geo_word(GeoLoc& L, int32_t w, int32_t o0, int32_t o1, const LBytes& s, int64_t p, const GeoTabs& gt,
+                            int top_role) {
+  const uint32_t word = *reinterpret_cast<const uint32_t*>(s.p + w);
+#pragma unroll GF_GEO_UNROLL
+  for (int k = 0; k < 4; ++k) {
+    const int32_t i = w + k - o0;  // offset in the line
+    const uint32_t byte = i < 0 || w + k >= o1 ? (uint32_t)' ' : (word >> (8 * k)) & 0xFFu;
+    geo_step(L, byte, i, s, p, gt, top_role);
+  }
+}
+
 // The automaton over the line [p, e) (s(p) == '{'), staged in LDS (lds + (pos - base)).  Returns
 // false when the line must take the walk; otherwise *g = the members the map reads.
 // r05: the byte step is BRANCH-FREE.  64 lanes walk 64 different lines, so some lane meets an
@@ -695,131 +853,16 @@ GF_DHD inline int64_t jmember_value(const Src& s, int64_t k, int64_t e) {
 // accumulator while it is read, and its closing quote compares (length, accumulator) with the
 // looked-up names' packed constants.  Only literals (true / false / null) at a token's end and
 // property names longer than 16 bytes branch (rare).
-#ifndef GF_GEO_UNROLL
-#define GF_GEO_UNROLL 2  // byte steps of a word unrolled (r05 A/B, parse us per 1M lines: 2 -> 3042-3048, 4 -> 3082-3086)
-#endif
 GF_DHD inline bool geo_locate(const LBytes& s, int64_t p, int64_t e, const GeoTabs& gt, int vlines,
                                            GeoPos* g) {
   if (e - p >= INT32_MAX) return false;
-  constexpr K16 kValue = geo_pack16("value", 5), kGeom = geo_pack16("geometry", 8);
-  constexpr K16 kProps = geo_pack16("properties", 10), kCoord = geo_pack16("coordinates", 11);
-  constexpr K16 kType = geo_pack16("type", 4);
-  int st = JS_VAL, depth = 0, pend = JK_NONE;
-  uint32_t ts = TS_IDLE;
-  bool bad = false;
-  uint64_t kinds = 0;  // bit d: the container at depth d is an object
-  uint32_t roles = 0;  // 4 bits per depth 1..7
-  int32_t ks = 0, tb = 0;
-  uint64_t khi = 0, klo = 0;  // the current key's last 16 bytes
-  // closing-quote positions (from p) of the last keys noted: the record's "value"; in V: type,
-  // coordinates, geometry, properties; in V.geometry: type, coordinates; in V.properties: the
-  // time and objID properties
-  int32_t v = -1, tV = -1, cV = -1, gV = -1, prV = -1, tG = -1, cG = -1, tP = -1, qP = -1;
-  const int32_t lts = gt.klen[4], lobj = gt.klen[5];
-  const bool long_props = lts > 16 || lobj > 16;  // (then their names are compared byte by byte)
+  GeoLoc L;
+  geo_loc_init(L);
   const int top_role = vlines ? JR_VAL : JR_TOP;
   const int32_t o0 = (int32_t)(p - s.base), o1 = (int32_t)(e - s.base);  // the line's LDS offsets
-  for (int32_t w = o0 & ~3; w < o1 && !bad; w += 4) {
-    const uint32_t word = *reinterpret_cast<const uint32_t*>(s.p + w);
-#pragma unroll GF_GEO_UNROLL
-    for (int k = 0; k < 4; ++k) {
-      const int32_t i = w + k - o0;  // offset in the line
-      const uint32_t byte = i < 0 || w + k >= o1 ? (uint32_t)' ' : (word >> (8 * k)) & 0xFFu;
-      const uint32_t ent = (uint32_t)(gt.tab[byte] >> (7 * st)) & 0x7Fu;
-      const uint32_t nts = (uint32_t)(gt.ttab[byte] >> (4 * ts)) & 15u;
-      int nst = (int)(ent & 15u);
-      const int act = (int)(ent >> 4);
-      const bool in_tok = nst == JS_TOK, in_str = nst == JS_VSTR || nst == JS_KSTR;
-      // a token ended before this byte: its state decides (a literal's letters: the rare branch)
-      const bool tok_end = st == JS_TOK && !in_tok;
-      const bool lit = tok_end && ts == TS_LIT;
-      bad |= tok_end && !lit && !(((kTsAccept >> ts) & 1u) && i - tb < 19);
-      if (lit) {  // true / false / null
-        const int n = i - tb;
-        const char c0 = s(p + tb);
-        bool ok = n == (c0 == 'f' ? 5 : 4);
-        const char* wd = c0 == 't' ? "true" : c0 == 'f' ? "false" : "null";
-        for (int q = 1; ok && q < n; ++q) ok = s(p + tb + q) == wd[q];
-        bad |= !ok;
-      }
-      tb = in_tok && st != JS_TOK ? i : tb;
-      // a string's bytes (its closing quote included) must leave the UTF-8 automaton accepting
-      bad |= (in_str || st == JS_VSTR || st == JS_KSTR) && nts == TS_ERR;
-      ts = in_tok || in_str ? nts : TS_IDLE;
-      // the key's bytes (between its quotes) into the accumulator; its opening quote resets it
-      const bool in_key = st == JS_KSTR && nst == JS_KSTR;
-      const uint64_t nhi = (khi << 8) | (klo >> 56), nlo = (klo << 8) | byte;
-      const bool kb = act == JA_KEY_BEGIN;
-      khi = kb ? 0ull : in_key ? nhi : khi;
-      klo = kb ? 0ull : in_key ? nlo : klo;
-      ks = kb ? i + 1 : ks;
-      // containers: the role of the one we are in, a push's child role, the kind bits
-      const int role = (unsigned)depth <= 7u ? (int)(roles >> (4 * depth)) & 15 : JR_NONE;
-      const bool push = act == JA_PUSH_OBJ || act == JA_PUSH_ARR, pop = act == JA_POP_OBJ || act == JA_POP_ARR;
-      int child = depth == 0 ? top_role
-                : role == JR_TOP ? (int)(0x0020u >> (4 * pend)) & 15   // value -> V
-                : role == JR_VAL ? (int)(0x4300u >> (4 * pend)) & 15   // geometry, properties
-                : JR_NONE;
-      child = act == JA_PUSH_ARR ? JR_NONE : child;
-      const int nd = depth + 1;
-      const uint64_t nbit = 1ull << (nd & 63);
-      kinds = push ? (act == JA_PUSH_OBJ ? kinds | nbit : kinds & ~nbit) : kinds;
-      const uint32_t rsh = 4u * (uint32_t)(nd & 7);
-      roles = push && nd <= 7 ? (roles & ~(15u << rsh)) | ((uint32_t)child << rsh) : roles;
-      const bool kobj = (kinds >> (depth & 63)) & 1;  // (a pop or comma does not change kinds)
-      bad |= push && nd > 63;
-      bad |= pop && (depth <= 0 || kobj != (act == JA_POP_OBJ));
-      bad |= act == JA_COMMA && depth <= 0;
-      nst = act == JA_COMMA ? (kobj ? JS_KEY : JS_VAL) : nst;
-      depth += (int)push - (int)pop;
-      // a key's closing quote: note a looked-up member of a looked-up container
-      const bool kend = act == JA_KEY_END;
-      const int len = i - ks;
-      // (a key of <= 8 bytes leaves khi 0: the short names compare klo only)
-      const bool e_type = len == 4 && klo == kType.lo, e_value = len == 5 && klo == kValue.lo;
-      const bool e_geom = len == 8 && klo == kGeom.lo;
-      const bool e_props = len == 10 && klo == kProps.lo && khi == kProps.hi;
-      const bool e_coord = len == 11 && klo == kCoord.lo && khi == kCoord.hi;
-      const bool top = kend && role == JR_TOP, val = kend && role == JR_VAL;
-      const bool geo = kend && role == JR_GEO, prop = kend && role == JR_PROP;
-      const bool m_value = top && e_value;
-      const bool v_type = val && e_type, v_coord = val && e_coord;
-      const bool v_geom = val && e_geom, v_props = val && e_props;
-      bool p_ts = prop && len == lts && lts <= 16 && klo == gt.pts.lo && khi == gt.pts.hi;
-      bool p_obj = prop && len == lobj && lobj <= 16 && klo == gt.pobj.lo && khi == gt.pobj.hi;
-      if (long_props && prop && len > 16) {  // (rare: a property name longer than 16 bytes)
-        p_ts = jkey_eq(s, p + ks, len, gt, 4);
-        p_obj = jkey_eq(s, p + ks, len, gt, 5);
-      }
-      pend = kend ? (m_value ? JK_VALUE : v_geom ? JK_GEO : v_props ? JK_PROP : JK_NONE) : pend;
-      v = m_value ? i : v;
-      tV = v_type ? i : tV;
-      cV = v_coord ? i : cV;
-      gV = v_geom ? i : gV;
-      prV = v_props ? i : prV;
-      tG = geo && e_type ? i : tG;
-      cG = geo && e_coord ? i : cG;
-      tP = p_ts ? i : tP;
-      qP = p_obj ? i : qP;
-      bad |= nst == JS_ERR;
-      st = nst == JS_ERR ? JS_AFT : nst;
-    }
-  }
-  if (bad || st != JS_AFT || depth != 0) return false;
-  auto val = [&](int32_t k) { return k < 0 ? (int64_t)-1 : jmember_value(s, p + k, e); };
-  // notes inside an earlier "value" object, geometry or properties member are stale
-  const int32_t vb = vlines ? -1 : v;
-  g->V = vlines ? p : val(v);
-  g->tV = val(tV > vb ? tV : -1);
-  g->cV = val(cV > vb ? cV : -1);
-  const int32_t gv = gV > vb ? gV : -1, pv = prV > vb ? prV : -1;
-  g->gV = val(gv);
-  g->tG = val(gv >= 0 && tG > gv ? tG : -1);
-  g->cG = val(gv >= 0 && cG > gv ? cG : -1);
-  g->prV = val(pv);
-  g->tsP = val(pv >= 0 && tP > pv ? tP : -1);
-  g->qP = val(pv >= 0 && qP > pv ? qP : -1);
-  g->escV = g->escG = g->escP = false;
+  for (int32_t w = o0 & ~3; w < o1 && !L.bad; w += 4) geo_word(L, w, o0, o1, s, p, gt, top_role);
+  if (!geo_loc_ok(L)) return false;
+  geo_notes_pos(s, p, e, vlines, L.n, g);
   return true;
 }
 

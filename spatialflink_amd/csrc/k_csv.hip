@@ -169,16 +169,26 @@ __device__ __forceinline__ void geo_tabs_fill(const CsvArgs& a, uint64_t* tab, u
   }
 }
 
+// line j's bytes [b, e) ('\r' dropped) and its first non-blank p; 0, or the error of a line that
+// is not an object
+template <class Src>
+__device__ __forceinline__ int geojson_bounds(const CsvArgs& a, const Src& s, int64_t j, int64_t newlines, int64_t& p,
+                                              int64_t& e) {
+  const int64_t b = j == 0 ? 0 : a.nl[j - 1] + 1;
+  e = j < newlines ? a.nl[j] : a.len;
+  if (e > b && s(e - 1) == '\r') --e;
+  if (e <= b) return kCsvEmptyLine;
+  p = jskip(s, b, e);
+  if (p >= e || s(p) != '{') return kCsvMissingField;  // not an object: malformed record
+  return kCsvOk;
+}
 // FAST: try the one-pass locator first (the LDS-staged path); otherwise the walk
 template <bool FAST, class Src>
 __device__ __forceinline__ int eval_geojson_line(const CsvArgs& a, const Src& s, int64_t j, int64_t newlines, LineOut* o,
                                                  const GeoTabs& gt) {
-  const int64_t b = j == 0 ? 0 : a.nl[j - 1] + 1;
-  int64_t e = j < newlines ? a.nl[j] : a.len;
-  if (e > b && s(e - 1) == '\r') --e;
-  if (e <= b) return kCsvEmptyLine;
-  const int64_t p = jskip(s, b, e);
-  if (p >= e || s(p) != '{') return kCsvMissingField;  // not an object: malformed record
+  int64_t p = 0, e = 0;
+  const int bs = geojson_bounds(a, s, j, newlines, p, e);
+  if (bs) return bs;
   const GeoProps gp{gt.keys + 4 * kGeoPropMax, gt.keys + 5 * kGeoPropMax, a.len_ts, a.len_obj, a.date_fmt, a.tz_off_ms,
                     kPow5Dev};
   if constexpr (FAST) return geojson_line(gt, gp, s, p, e, a.value_lines, true, o);
@@ -224,14 +234,34 @@ __device__ __forceinline__ bool csv_counts(const CsvArgs& a, int64_t& newlines, 
   lines = newlines + (a.text[a.len - 1] != '\n' ? 1 : 0);
   return newlines <= a.nl_cap && lines <= a.cap && lines <= a.grid_lines && lines <= (int64_t)UINT32_MAX;
 }
+// GeoJSON blocks hold 192 lines (GF_GEO_LINES), CSV blocks kBlock.  A block keeps its staged
+// lines in LDS until its slowest lane is done, and LDS is what bounds the residency: a block of 256
+// mean GeoJSON lines (~48 KB + 10 %, plus the locator's 4.5 KB of static tables) lets only two
+// share a CU (8 waves); three 192-line blocks fit (9 waves).  r05 A/B, parse kernel per 1M lines
+// (tools/gpu_r05_geo2.sh): 256 lines 3.05 ms, 192 lines 2.86, 128 lines 3.11 (four blocks, 8
+// waves).  Handing a block's lines to lanes in length order (so that each wave's byte loop runs
+// to a shorter longest line; the sum of the waves' longest lines drops 26 % on the bench lines)
+// measured slower (3.18 / 2.90 ms): the block's LDS is held until its longest line is done
+// either way, and the sort's ranks cost LDS.  So did lanes taking the block's next line from an
+// LDS queue when theirs ends (3.08 vs 2.89 ms): with as many lines as lanes there is nothing left
+// to take, and staging twice the lines per lane halves the resident waves instead (LDS).  The
+// lanes idle for ~40 % of a block's life (mean line 189 B, the longest of 192 ~330 B).
+#ifndef GF_GEO_LINES
+#define GF_GEO_LINES 192
+#endif
+constexpr int kGeoLines = GF_GEO_LINES;
+static_assert(kGeoLines % 64 == 0 && kGeoLines <= kBlock, "whole waves");
+template <int FMT>
+constexpr int parse_lines() { return FMT == 1 ? kGeoLines : kBlock; }
 template <int FMT>  // 0: CSV / TSV, 1: GeoJSON (a.format)
-__global__ __launch_bounds__(kBlock) void csv_parse_kernel(CsvArgs a) {
+__global__ __launch_bounds__(parse_lines<FMT>()) void csv_parse_kernel(CsvArgs a) {
+  constexpr int NB = parse_lines<FMT>();
   extern __shared__ __attribute__((aligned(16))) char lds[];
   int64_t newlines, lines;
   const bool ok = csv_counts(a, newlines, lines);
-  const int64_t L0 = (int64_t)blockIdx.x * kBlock;
+  const int64_t L0 = (int64_t)blockIdx.x * NB;
   if (!ok || L0 >= lines) return;  // block-uniform
-  const int64_t L1 = L0 + kBlock < lines ? L0 + kBlock : lines;  // exclusive
+  const int64_t L1 = L0 + NB < lines ? L0 + NB : lines;  // exclusive
   const int64_t b0 = L0 == 0 ? 0 : a.nl[L0 - 1] + 1;
   const int64_t b1 = L1 - 1 < newlines ? a.nl[L1 - 1] : a.len;     // the last line's '\n' (or end)
   const int64_t a0 = b0 & ~(int64_t)15;
@@ -249,7 +279,7 @@ __global__ __launch_bounds__(kBlock) void csv_parse_kernel(CsvArgs a) {
     __syncthreads();
   }
   if (b1 - a0 <= a.lds_cap) {  // block-uniform
-    for (int64_t off = a0 + 16 * threadIdx.x; off < b1; off += 16 * kBlock) {
+    for (int64_t off = a0 + 16 * threadIdx.x; off < b1; off += 16 * NB) {
       if (off + 16 <= a.len) {
         *reinterpret_cast<uint4*>(lds + (off - a0)) = *reinterpret_cast<const uint4*>(a.text + off);
       } else {
@@ -423,25 +453,23 @@ hipError_t launch_csv_nlindex(hipStream_t st, const char* text, int64_t len, int
   return hipGetLastError();
 }
 
-// Staging size: 256 mean-length lines plus a tenth for the spread of a block's sum, in 1-KB
-// steps between kCsvLds and kCsvLdsMax (CSV points ~55 B/line keep the 24 KB floor, so 6 blocks
-// share a CU).  GeoJSON features (~183 B/line, ~47 KB a block) are held to 50 KB when a mean
-// block fits it with 5% to spare, so that 3 blocks (with the locator's 2.4 KB of tables) share
-// a CU.  A block whose lines exceed the staging area parses from global memory with the walk
-// (same results, one dependent L2 read per byte).
+// Staging size: a block's mean-length lines plus a tenth for the spread of a block's sum, in
+// 1-KB steps between kCsvLds and kCsvLdsMax (CSV points ~55 B/line keep the 24 KB floor, so 6
+// blocks share a CU; GeoJSON features, ~189 B/line: ~40 KB for 192 lines, 3 blocks per CU with
+// the locator's tables).  A block whose lines exceed the staging area parses from global memory
+// with the walk (same results, one dependent L2 read per byte).
 hipError_t launch_csv_parse(gf_ctx* ctx, const CsvArgs& a0) {
   KTimer t(ctx, GF_K_CSV_PARSE);
   CsvArgs a = a0;
   const int64_t mean = a.mean_line;
-  const int64_t need = mean * kBlock;
+  const int NB = a.format == 1 ? kGeoLines : kBlock;
+  const int64_t need = mean * NB;
   int64_t cap = (need * 11 / 10 + 1023) & ~(int64_t)1023;
-  constexpr int64_t kGeoLds3 = 50 * 1024;
-  if (a.format == 1 && cap > kGeoLds3 && need * 20 <= kGeoLds3 * 19) cap = kGeoLds3;
   a.lds_cap = (int32_t)(cap < kCsvLds ? kCsvLds : cap > kCsvLdsMax ? kCsvLdsMax : cap);
   if (a.grid_lines > 0) {  // (blocks past the chunk's lines return at once)
-    const unsigned blocks = (unsigned)((a.grid_lines + kBlock - 1) / kBlock);
+    const unsigned blocks = (unsigned)((a.grid_lines + NB - 1) / NB);
     if (a.format == 1)
-      hipLaunchKernelGGL(csv_parse_kernel<1>, dim3(blocks), dim3(kBlock), (size_t)a.lds_cap, ctx->stream, a);
+      hipLaunchKernelGGL(csv_parse_kernel<1>, dim3(blocks), dim3(NB), (size_t)a.lds_cap, ctx->stream, a);
     else
       hipLaunchKernelGGL(csv_parse_kernel<0>, dim3(blocks), dim3(kBlock), (size_t)a.lds_cap, ctx->stream, a);
   }
