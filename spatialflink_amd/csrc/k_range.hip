@@ -304,7 +304,9 @@ __device__ __forceinline__ void waveq_round(const RangeArgs& a, const RangeLds& 
       bitmap_or(a.bitmap, i);
   }
   hits += (uint64_t)__popcll(__ballot(acc));
+#if GF_RANGE_EXP != 4
   queue_append2(cls == kTest, i, v.x, v.y, false, 0u, 0.0, 0.0, a, lcount);
+#endif
   // the ring's head moves past the round (r04 moved the rest [take, cnt) to the front instead: two
   // LDS reads and two writes per lane per round)
   q.head = (q.head + take) & (uint32_t)(kWaveQ - 1);
@@ -319,6 +321,8 @@ __device__ __forceinline__ void waveq_round(const RangeArgs& a, const RangeLds& 
 // C3 45.5 vs 45.0 us per window -- the 8-B layout stays.
 #ifndef GF_RANGE_EXP
 #define GF_RANGE_EXP 0  // experiment builds only (tools/build_exp.sh): 1 no span-queue rounds, 2 nothing queued
+                        // (the compiler then drops the loads: not a measurement), 3 no candidate tests at the
+                        // block's end, 4 nor their queue appends
 #endif
 #ifndef GF_RANGE_VEC
 #define GF_RANGE_VEC 0
@@ -716,7 +720,9 @@ __device__ __forceinline__ void range_body(const RangeArgs& a) {
     // the ring's tiles to global memory (before the block's candidate tests OR into them)
     const uint32_t lane = threadIdx.x & 63, held = wq.ntile < (uint32_t)kWaveRing ? wq.ntile : kWaveRing;
     if (lane < held) ring_store(a, wq, wq.ntile - held + lane);
+#if GF_RANGE_EXP != 3 && GF_RANGE_EXP != 4  // experiment builds: 3 no candidate tests, 4 nor their queue
     hits += drain_own_queue<POLY>(a, lcount);
+#endif
   }
   // per-block partial counts (plain stores; summed by range_finalize)
   const int wid = threadIdx.x >> 6;
