@@ -562,11 +562,18 @@ __device__ __forceinline__ bool test_object(const RangeArgs& a, double px, doubl
   return point_polygon_distance(px, py, a, o) <= a.r;
 }
 
-constexpr int kTestGroup = 8;
+#ifndef GF_RANGE_TEST_GROUP
+#define GF_RANGE_TEST_GROUP 2  // lanes per queued point in drain_own_queue (1, 2, 4, 8)
+// r05 A/B, C3 per window (tools/gpu_r05_c3g.sh, one box, twice): 8 lanes 45.9 / 45.5 us, 4 45.2 /
+// 45.4, 2 43.1 / 43.1, 1 44.1 / 44.4.  A block's ~60 queued points take one pass of 128 pairs
+// instead of two of 32 octets: each pass is a chain of dependent loads (entry, cell list,
+// polygon), so fewer passes shorten the block's tail; one lane per point walks lists serially.
+#endif
+constexpr int kTestGroup = GF_RANGE_TEST_GROUP;
 // DEFER 1: after its scan loop, a block drains its OWN queue segment (the candidate-cell points
 // it queued) -- no second launch, no grid-wide prefix of the segment counts.  A queued point is
-// a group of 8 lanes that test its candidate objects in parallel (8 at a time, stopping once one
-// hits), so the dependent chain per point is one object test, not the list length.  Hits are
+// a group of kTestGroup lanes that test its candidate objects in parallel (kTestGroup at a time,
+// stopping once one hits).  Hits are
 // OR-ed into the bitmap words this block stored during the scan: every wave drains its stores
 // (s_waitcnt vmcnt(0): acknowledged by L2) before the barrier, so the atomics land after them.
 // Returns this wave's added hits (wave-uniform).
