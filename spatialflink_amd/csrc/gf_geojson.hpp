@@ -830,7 +830,8 @@ GF_DHD inline void geo_notes_pos(const Src& s, int64_t p, int64_t e, int vlines,
 // One word (4 LDS bytes at offset w from the staging base) of the line whose LDS offsets are
 // [o0, o1).  r05: the byte step is BRANCH-FREE (see geo_locate)
 #ifndef GF_GEO_UNROLL
-#define GF_GEO_UNROLL 2  // byte steps of a word unrolled (r05 A/B, parse us per 1M lines: 2 -> 3042-3048, 4 -> 3082-3086)
+#define GF_GEO_UNROLL 2  // byte steps of a word unrolled (r05 A/B, parse us per 1M lines, 256-line blocks: 2 -> 3042-3048,
+                         // 4 -> 3082-3086; 192-line blocks (tools/gpu_r05_geo5.sh): 1 -> 2967-2977, 2 -> 2894-2903, 4 -> 2862-2864)
 #endif
 GF_DHD inline void geo_word(GeoLoc& L, int32_t w, int32_t o0, int32_t o1, const LBytes& s, int64_t p, const GeoTabs& gt,
                             int top_role) {
