@@ -1,7 +1,8 @@
 #!/bin/bash
-# round-5 GeoJSON parse occupancy / wave balance: lines handed to lanes in length order (the
-# product: GF_GEO_SORT=1) vs index order (explibs/nosort), and 192 / 128-line blocks (explibs/g192,
-# g128, g192ns = 192 without the sort) against 256 -- tools/build_exp.sh NAME k_csv.hip "-D..."
+# round-5 GeoJSON parse occupancy / wave balance, as run (the product then had 256-line blocks and
+# the length-order sort, GF_GEO_SORT=1, since removed): vs index order (explibs/nosort), 192 /
+# 128-line blocks (explibs/g192, g128, g192ns = 192 without the sort).  tools/build_exp.sh NAME
+# k_csv.hip "-DGF_GEO_LINES=N".  Result: 192 lines without the sort is the product.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 S=tools/gpu_step.sh
