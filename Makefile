@@ -11,7 +11,7 @@ LIB      := spatialflink_amd/libgeoflink_hip.so
 SOURCES  := $(SRC)/api.cpp $(SRC)/comm.cpp $(SRC)/sliding.cpp $(SRC)/csv.cpp $(SRC)/objid.cpp $(SRC)/k_points.hip $(SRC)/k_knn.hip \
             $(SRC)/k_range.hip $(SRC)/k_join.hip $(SRC)/k_csv.hip $(SRC)/k_objid.hip
 OBJECTS  := $(patsubst $(SRC)/%,$(OBJDIR)/%.o,$(SOURCES))
-HEADERS  := include/geoflink_hip.h $(SRC)/gf_internal.hpp $(SRC)/gf_text.hpp $(SRC)/gf_geojson.hpp $(SRC)/gf_numerics.hpp $(SRC)/gf_decimal.hpp $(SRC)/gf_pow5.hpp $(SRC)/gf_geom.hpp
+HEADERS  := include/geoflink_hip.h $(SRC)/gf_buildtag.hpp $(SRC)/gf_internal.hpp $(SRC)/gf_text.hpp $(SRC)/gf_geojson.hpp $(SRC)/gf_numerics.hpp $(SRC)/gf_decimal.hpp $(SRC)/gf_pow5.hpp $(SRC)/gf_geom.hpp
 
 all: $(LIB) oracle shim
 
@@ -24,9 +24,16 @@ $(SHIM): integration/jni/geoflink_shim.c integration/jni/geoflink_shim.h include
 	    -Wl,-rpath,'$$ORIGIN/../../spatialflink_amd' -Wl,-rpath,/opt/rocm/lib
 shim: $(SHIM)
 
-$(OBJDIR)/%.o: $(SRC)/% $(HEADERS)
+# The product rule takes no extra defines: experiments build only into
+# explibs/ through tools/build_exp.sh.  The flags stamp is rewritten at parse time whenever the
+# compile line differs from the last build's, so a changed HIPFLAGS (e.g. `make HIPFLAGS=...-DX`)
+# rebuilds every object, and the next plain `make` rebuilds them again as the product.
+FLAGS_STAMP := $(OBJDIR)/.hipflags
+$(shell mkdir -p $(OBJDIR); printf '%s\n' '$(HIPCC) $(HIPFLAGS)' | cmp -s - $(FLAGS_STAMP) || \
+        printf '%s\n' '$(HIPCC) $(HIPFLAGS)' > $(FLAGS_STAMP))
+$(OBJDIR)/%.o: $(SRC)/% $(HEADERS) $(FLAGS_STAMP)
 	@mkdir -p $(OBJDIR)
-	$(HIPCC) $(HIPFLAGS) $(GF_DEFS) -x hip -c $< -o $@
+	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
 
 $(LIB): $(OBJECTS)
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(OBJECTS) -ldl

@@ -703,6 +703,7 @@ def main():
             "breakdown": breakdown,
             "host_boundary": pcie,
             "verified_vs_oracle": verified,
+            "build": L.gf_build_info().decode(),
         }
         print(json.dumps(line), flush=True)
     if comm is not None:

@@ -110,6 +110,13 @@ typedef struct {
 
 /* ---- library / context ------------------------------------------------------------- */
 int         gf_abi_version(void);
+/* Build identity (no reference counterpart): the compile-time tuning / experiment defines every
+ * translation unit of this library was built with ("" per unit for the product build), and the
+ * GF_* run-time knobs set in the environment.  gf_build_is_product() == 1 iff no unit carries a
+ * command-line define -- the smoke and the GPU suite require it, so an experiment build
+ * (tools/build_exp.sh) can never be measured or tested as the product. */
+const char* gf_build_info(void);
+int         gf_build_is_product(void);
 const char* gf_status_string(int status);
 int         gf_device_count(int* n);
 /* One context per calling thread / Flink subtask; binds `device`, owns scratch + a stream. */

@@ -40,7 +40,7 @@ FLAG_JOIN_STREAM = 8
 
 # Every symbol include/geoflink_hip.h declares (checked by tests/test_abi.py).
 EXPORTS = [
-    "gf_abi_version", "gf_status_string", "gf_device_count", "gf_ctx_create", "gf_ctx_destroy",
+    "gf_abi_version", "gf_build_info", "gf_build_is_product", "gf_status_string", "gf_device_count", "gf_ctx_create", "gf_ctx_destroy",
     "gf_ctx_set_stream", "gf_ctx_stream", "gf_ctx_synchronize", "gf_ctx_join", "gf_ctx_fork", "gf_ctx_last_error", "gf_ctx_set_timing", "gf_ctx_set_timing_period", "gf_ctx_set_flag",
     "gf_ctx_timing", "gf_grid_make", "gf_grid_layers", "gf_cell_of", "gf_format_cell_id", "gf_parse_cell_id",
     "gf_assign_cells", "gf_bucket_by_cell", "gf_range_pp_plan_create", "gf_range_ppoly_plan_create",
@@ -121,6 +121,8 @@ def lib():
         pi32, pi64, pd = C.POINTER(i32), C.POINTER(i64), C.POINTER(d)
         sig = {
             "gf_abi_version": ([], C.c_int),
+            "gf_build_info": ([], C.c_char_p),
+            "gf_build_is_product": ([], C.c_int),
             "gf_status_string": ([C.c_int], C.c_char_p),
             "gf_device_count": ([C.POINTER(C.c_int)], C.c_int),
             "gf_ctx_create": ([C.c_int, C.POINTER(P)], C.c_int),

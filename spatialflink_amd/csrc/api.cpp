@@ -1,6 +1,9 @@
 // api.cpp -- C ABI of libgeoflink_hip.so (include/geoflink_hip.h): contexts, plans built once
 // per continuous query (the reference computes its guaranteed / candidate cell sets once per
 // operator, PointPointRangeQuery.java:119-125), and the per-window entry points.
+#define GF_TU_NAME api_cpp
+#include "gf_buildtag.hpp"  // first: records this unit's command-line defines
+
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -211,6 +214,64 @@ using namespace gf;
 // library / context
 // ---------------------------------------------------------------------------------------
 extern "C" int gf_abi_version(void) { return GF_ABI_VERSION; }
+
+namespace gf {  // one per translation unit (gf_buildtag.hpp)
+const char* build_tag_api_cpp();
+const char* build_tag_comm_cpp();
+const char* build_tag_sliding_cpp();
+const char* build_tag_csv_cpp();
+const char* build_tag_objid_cpp();
+const char* build_tag_k_points_hip();
+const char* build_tag_k_knn_hip();
+const char* build_tag_k_range_hip();
+const char* build_tag_k_join_hip();
+const char* build_tag_k_csv_hip();
+const char* build_tag_k_objid_hip();
+struct UnitTag {
+  const char* unit;
+  const char* (*tag)();
+};
+static const UnitTag kUnitTags[] = {
+    {"api.cpp", build_tag_api_cpp},         {"comm.cpp", build_tag_comm_cpp},
+    {"sliding.cpp", build_tag_sliding_cpp}, {"csv.cpp", build_tag_csv_cpp},
+    {"objid.cpp", build_tag_objid_cpp},     {"k_points.hip", build_tag_k_points_hip},
+    {"k_knn.hip", build_tag_k_knn_hip},     {"k_range.hip", build_tag_k_range_hip},
+    {"k_join.hip", build_tag_k_join_hip},   {"k_csv.hip", build_tag_k_csv_hip},
+    {"k_objid.hip", build_tag_k_objid_hip},
+};
+// run-time A/B knobs (valid alternative paths, never wrong results): reported, not refused
+static const char* const kEnvKnobs[] = {"GF_K2_LSD", "GF_JOIN_BAND_PER_CU", "GF_JOIN_ROWPROBE",
+                                        "GF_JOIN_CHUNK", "GF_RADIX_NT"};
+}  // namespace gf
+
+extern "C" int gf_build_is_product(void) {
+  for (const auto& u : kUnitTags)
+    if (u.tag()[0] != 0) return 0;
+  return 1;
+}
+
+extern "C" const char* gf_build_info(void) {
+  static std::string info = [] {
+    std::string s = "gfx950 abi " + std::to_string(GF_ABI_VERSION) + "; defines:";
+    bool any = false;
+    for (const auto& u : kUnitTags)
+      if (u.tag()[0]) {
+        s += std::string(" [") + u.unit + ":" + u.tag() + "]";
+        any = true;
+      }
+    if (!any) s += " none (product)";
+    s += "; env:";
+    bool anyenv = false;
+    for (const char* k : kEnvKnobs)
+      if (const char* v = std::getenv(k)) {
+        s += std::string(" ") + k + "=" + v;
+        anyenv = true;
+      }
+    if (!anyenv) s += " none";
+    return s;
+  }();
+  return info.c_str();
+}
 
 extern "C" const char* gf_status_string(int s) {
   switch (s) {

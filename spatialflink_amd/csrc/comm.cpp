@@ -14,6 +14,9 @@
 // control plane -- torch.distributed, Flink's broadcast, a shared file) or ncclCommInitAll (one
 // process driving every GPU).  Collectives are enqueued on the context's
 // stream; nothing here synchronises the host.
+#define GF_TU_NAME comm_cpp
+#include "gf_buildtag.hpp"  // first: records this unit's command-line defines
+
 #include <dlfcn.h>
 #include <rccl/rccl.h>
 

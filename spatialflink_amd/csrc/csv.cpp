@@ -5,6 +5,9 @@
 //   line parse + cell (the line count read on the device) -> the head (counts, first bad line,
 //   dictionary work) written into mapped pinned memory -> the call's one sync -> objID Strings
 //   that are not canonical decimals -> dictionary keys (objid.cpp)
+#define GF_TU_NAME csv_cpp
+#include "gf_buildtag.hpp"  // first: records this unit's command-line defines
+
 #include <cstring>
 #include <string>
 

@@ -9,6 +9,9 @@
 //               the objID String as its key (canonical decimals directly, the rest queued for
 //               the dictionary, k_objid.hip), Long.valueOf(time), Double.valueOf(x, y) correctly
 //               rounded on the device (gf_decimal.hpp), cell (cx, cy), SoA stores.
+#define GF_TU_NAME k_csv_hip
+#include "gf_buildtag.hpp"  // first: records this unit's command-line defines
+
 #include "gf_geojson.hpp"
 #include "gf_internal.hpp"
 

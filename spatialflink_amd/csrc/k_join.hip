@@ -8,6 +8,9 @@
 // query-grid cell within Chebyshev distance c of q's cell, exactly the replicated-key match.
 // Output: two passes over the ordinary side (count, then write at per-block scanned
 // offsets), so no global atomics and pairs come out grouped by ordinary point.
+#define GF_TU_NAME k_join_hip
+#include "gf_buildtag.hpp"  // first: records this unit's command-line defines
+
 #include <type_traits>
 
 #include "gf_internal.hpp"

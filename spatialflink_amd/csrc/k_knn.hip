@@ -18,6 +18,9 @@
 // below T (or T == r); otherwise it is flagged and gf_knn_decode re-evaluates the window
 // (sample path, then exhaustive T = r partitions).  Output: (d, objID) ascending, the
 // minimum-(d, idx) occurrence per objID.
+#define GF_TU_NAME k_knn_hip
+#include "gf_buildtag.hpp"  // first: records this unit's command-line defines
+
 #include <type_traits>
 
 #include "gf_geom.hpp"

@@ -17,6 +17,9 @@
 //   (scan)       rank = exclusive prefix of the flags
 //   dict_assign  id = dictionary size + rank; idmap[id] = the slot's arena (offset, length)
 //   dict_keys    key[line] = INT64_MIN + id of the line's slot
+#define GF_TU_NAME k_objid_hip
+#include "gf_buildtag.hpp"  // first: records this unit's command-line defines
+
 #include "gf_internal.hpp"
 
 namespace gf {

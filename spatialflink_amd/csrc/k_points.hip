@@ -1,6 +1,9 @@
 // k_points.hip -- per-point kernels: K1 cell assignment, K2 bucketing by cell (stable LSD
 // radix sort: per-wave LDS histograms, wave-ballot ranking), exclusive scan, and selection-
 // bitmap -> index expansion.  gfx950, wave64.
+#define GF_TU_NAME k_points_hip
+#include "gf_buildtag.hpp"  // first: records this unit's command-line defines
+
 #include <cstdlib>
 
 #include "gf_internal.hpp"

@@ -14,6 +14,9 @@
 //          class table (L1/L2 resident), out-of-grid cells against the g == 0 extra rects.
 // Testing a candidate-cell point walks that cell's object list (CSR built on the host over a
 // (c+2)-cell reach, a superset of every object that can be within r).
+#define GF_TU_NAME k_range_hip
+#include "gf_buildtag.hpp"  // first: records this unit's command-line defines
+
 #include "gf_geom.hpp"
 #include "gf_internal.hpp"
 

@@ -3,6 +3,9 @@
 // int64 keys the SoA carries.  Canonical decimals are their own key; every other String is
 // INT64_MIN + its id here.  One dictionary per stream of windows (the context's default one
 // serves gf_csv_parse), so a String gets the same key in every window.
+#define GF_TU_NAME objid_cpp
+#include "gf_buildtag.hpp"  // first: records this unit's command-line defines
+
 #include <algorithm>
 #include <cstring>
 #include <string>

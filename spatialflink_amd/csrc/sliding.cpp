@@ -13,6 +13,9 @@
 // Flink window assignment (TimeWindow.getWindowStartWithOffset, offset 0): an element with
 // timestamp t lies in pane floor(t / pane); window [s, s + size) (s a multiple of slide) closes
 // when the pane ending at s + size is complete; a window with no element never fires.
+#define GF_TU_NAME sliding_cpp
+#include "gf_buildtag.hpp"  // first: records this unit's command-line defines
+
 #include <algorithm>
 #include <climits>
 #include <numeric>

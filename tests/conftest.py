@@ -28,6 +28,31 @@ def oracle_mod():
     return oracle
 
 
+_BUILD_CHECKED = []
+
+
+def assert_product_build():
+    """The library under test must be the product build: no unit compiled with tuning or
+    experiment defines (gf_build_is_product).  GF_TEST_EXPERIMENT=1 lets
+    an A/B arm's experiment library be parity-checked explicitly (tools/gpu_ab.sh)."""
+    import spatialflink_amd._lib as L
+
+    lib = L.lib()
+    info = lib.gf_build_info().decode()
+    if os.environ.get("GF_TEST_EXPERIMENT") == "1":
+        return info
+    assert lib.gf_build_is_product() == 1, f"not the product build: {info} ({L.LIB_PATH})"
+    return info
+
+
+@pytest.fixture(autouse=True)
+def _product_build(request):
+    """Every gpu-marked test runs against the product library only."""
+    if request.node.get_closest_marker("gpu") is not None and not _BUILD_CHECKED:
+        _BUILD_CHECKED.append(assert_product_build())
+    yield
+
+
 @pytest.fixture(scope="session")
 def gpu():
     """Skip-free on the GPU box: a gpu-marked test must fail loudly if no device is visible."""

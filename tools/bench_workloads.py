@@ -205,6 +205,9 @@ def _line(workload, value, unit, steps, warmup, elapsed, kernel, bytes_per_launc
                       "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
                       "traffic": None, "bytes_per_launch": bytes_per_launch, "avg_launch_us": round(avg_s * 1e6, 2)}}
     d.update(extra)
+    from spatialflink_amd import _lib
+
+    d["build"] = _lib.lib().gf_build_info().decode()
     print(json.dumps(d), flush=True)
 
 
@@ -973,10 +976,22 @@ def bench_sliding(args):
     if rank == 0:  # HBM bytes per pane launch from the committed rocprofv3 PMC passes
         import glob
 
-        for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_sliding_knn_fused_pmc.json")), reverse=True):
+        # newest round first: r<NN>_sliding_pmc.json (tools/pmc_table.py layout) or the older
+        # r<NN>_sliding_knn_fused_pmc.json (one kernel, with its points per launch)
+        files = glob.glob(os.path.join(ROOT, "profiles", "r*_sliding_pmc.json")) + \
+            glob.glob(os.path.join(ROOT, "profiles", "r*_sliding_knn_fused_pmc.json"))
+        for f in sorted(files, key=lambda f: (os.path.basename(f).split("_")[0], "knn_fused" not in f), reverse=True):
             with open(f) as fh:
                 pm = json.load(fh)
-            if pm.get("points_per_launch") == pane_pts:
+            if "pmc" in pm:
+                ent = [v for k_, v in pm["pmc"].items() if "knn_fused_kernel" in k_]
+                # the campaign ran the default pane; take it only when it streamed this pane's bytes
+                if ent and abs(ent[0]["hbm_read_bytes_corrected"] - 16.0 * pane_pts) < 0.05 * 16.0 * pane_pts:
+                    traffic = ent[0]["hbm_read_bytes_corrected"] + ent[0].get("hbm_write_bytes", 0.0)
+                    traffic_src = (os.path.relpath(f, ROOT) + ": rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE passes, "
+                                   "median per knn_fused_kernel launch, FETCH_SIZE x2 (gfx950)")
+                    break
+            elif pm.get("points_per_launch") == pane_pts:
                 traffic = pm["traffic_bytes_per_launch"]
                 traffic_src = os.path.relpath(f, ROOT) + ": rocprofv3 FETCH_SIZE (x2, gfx950) + WRITE_SIZE, median per launch"
                 break
@@ -1003,7 +1018,8 @@ def bench_sliding(args):
              "scanned_points_per_s": round(pane_pts * world * steps / elapsed, 1),
              "breakdown": {"merge_us": round(1000.0 * merge_ms / max(merge_n, 1), 2),
                            "from_scratch_window_us": round(scratch_us, 2) if scratch_us else None},
-             "cpu_baseline": cpu, "verified_vs_whole_window_and_oracle": verified}
+             "cpu_baseline": cpu, "verified_vs_whole_window_and_oracle": verified,
+             "build": L.gf_build_info().decode()}
         print(json.dumps(d), flush=True)
     L.gf_knn_sliding_destroy(eng)
     if comm is not None:
