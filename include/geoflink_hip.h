@@ -343,8 +343,10 @@ int    gf_knn_merge_dev_batch(gf_ctx* ctx, int32_t k, const void* records, int32
  * entry of every String: rank independent.  (One rank's own select orders tied distances by
  * dictionary id; the cross-rank order differs from it only between different Strings at exactly
  * equal distances.)  The merged record's dictionary keys are the source ranks' and mean nothing
- * elsewhere: read its Strings with gf_knn_string_record_decode.  An input record with status != 0
- * or whose Strings did not fit gives status 2 (GF_KNN_STATUS_FOREIGN_KEYS) and no entries. */
+ * elsewhere: read its Strings with gf_knn_string_record_decode.  A flagged input record (status 1)
+ * gives a flagged merged record (status 1, no entries: re-evaluate the shard exactly and exchange
+ * again, as for gf_knn_exchange_batch); an input whose Strings did not fit its sidecar gives
+ * status 2 (GF_KNN_STATUS_FOREIGN_KEYS, no entries: retry with a larger cap_bytes). */
 size_t gf_knn_string_record_bytes(int32_t k, int64_t cap_bytes);
 /* Async: nrec consecutive records (gf_knn_result_bytes(k) apart, device or pinned memory) ->
  * nrec consecutive string records (gf_knn_string_record_bytes(k, cap_bytes) apart) with the
@@ -404,7 +406,11 @@ int gf_knn_exchange_batch(gf_comm* comm, gf_ctx* ctx, int32_t k, const void* rec
 int gf_knn_exchange_strings_batch(gf_comm* comm, gf_objid_dict* dict, int32_t k, int64_t cap_bytes,
                                   const void* records, int32_t nwin, void* merged);
 /* Async, one thread driving n communicators of one clique (gf_comm_create_all): the n
- * all-gathers as one RCCL group, then the n merges (comms[i] with ctxs[i], records[i], merged[i]). */
+ * all-gathers as one RCCL group, then the n merges (comms[i] with ctxs[i], records[i], merged[i]).
+ * comms must be the WHOLE clique (n == its size, each rank once; GF_ERR_ARG otherwise), checked
+ * with every other argument before the group starts.  Should RCCL still fail inside the group,
+ * the clique is aborted (ncclCommAbort: no all-gather is left waiting for a peer) and every later
+ * call on those communicators returns GF_ERR_COMM; destroy them and create a new clique. */
 int gf_knn_exchange_group(int32_t n, gf_comm* const* comms, gf_ctx* const* ctxs, int32_t k,
                           const void* const* records, int32_t nwin, void* const* merged);
 

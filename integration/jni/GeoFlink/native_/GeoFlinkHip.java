@@ -18,6 +18,8 @@
  *   knnWindow    PointPointKNNQuery.windowBased (PointPointKNNQuery.java:132-201) +
  *                KNNQuery.kNNWinAllEvaluationPointStream (KNNQuery.java:213-272)
  *   knnPolygonPlan  PointPolygonKNNQuery (PointPolygonKNNQuery.java:245-317)
+ *   knnWindowSharded / knnSharded*  the windowAll merge (PointPointKNNQuery.java:198-200) across the
+ *                GPUs of a node: an RCCL exchange of the bands' top-k records (HipShardedKnnFunction)
  *   knnSliding*  SlidingProcessingTimeWindows.of(size, slide) around the kNN apply
  *                (PointPointKNNQuery.java:158,198-200): panes evaluated once, windows merged
  *   rangeSliding*  the same apply under SlidingProcessingTimeWindows (PointPointRangeQuery.java:149)
@@ -113,6 +115,20 @@ public final class GeoFlinkHip {
   public static native int knnWindowSharded(long ctx, long plan, long comm, ByteBuffer x, ByteBuffer y,
                                             ByteBuffer objID, int n, long indexBase, long[] outObjID,
                                             double[] outDist, long[] outIdx, int k);
+  // The batched, asynchronous form (HipShardedKnnFunction; the path bench.py --gpus N times):
+  // knnShardedEnqueue queues this subtask's band of a window and returns its ticket; every
+  // batch-th enqueue issues ONE exchange of the batch's records by String (every rank must make
+  // the same calls in the same order); knnShardedResult(ticket) then gives the window's merged
+  // neighbours -- outDist, outIdx (global: indexBase + band position) and owned[j] = 1 for this
+  // band's Points -- and frees the ticket's slot (read a ticket before enqueueing 2 * batch more).
+  // knnShardedFlush exchanges an incomplete batch (end of input).  capBytes bounds the objID
+  // Strings of one record (e.g. 32 * k).
+  public static native void knnShardedBegin(long ctx, long plan, long comm, int batch, long capBytes);
+  public static native long knnShardedEnqueue(long ctx, long plan, ByteBuffer x, ByteBuffer y, ByteBuffer objID,
+                                              int n, long indexBase);
+  public static native void knnShardedFlush(long ctx, long plan);
+  public static native int knnShardedResult(long ctx, long plan, long ticket, double[] outDist, long[] outIdx,
+                                            int[] owned);
 
   // ---- sliding kNN (pane engine) ---------------------------------------------------------
   // size / gcd(size, slide) <= 64; the plan must outlive the sliding handle
@@ -138,6 +154,10 @@ public final class GeoFlinkHip {
   // their count -- larger than outCap: call again with a larger buffer
   public static native long rangeWindow(long ctx, long plan, ByteBuffer x, ByteBuffer y, int n, ByteBuffer out,
                                         int outCap);
+  // approximate point queries with |Q| > 1: the points of the last rangeWindow that the reference
+  // emits once per query point (PointPointRangeQuery.java:158-161) -- a subset of its list,
+  // ascending; same count / capacity convention; 0 for other plans
+  public static native long rangeWindowMulti(long ctx, long plan, ByteBuffer out, int outCap);
 
   // ---- sliding range (pane engine) ---------------------------------------------------------
   // SlidingProcessingTimeWindows.of(size, slide) around the range apply (PointPointRangeQuery.java:

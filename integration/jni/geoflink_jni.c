@@ -61,6 +61,19 @@ static int need_len(JNIEnv* env, jarray a, jsize n, const char* what) {
   return 1;
 }
 
+/* the three result arrays of a kNN call hold at least the PLAN's k entries (the shim writes up to
+ * that many, whatever k the Java caller passes) */
+static int need_knn_out(JNIEnv* env, const shim_knn* h, jarray oo, jarray od, jarray oi, const char* what) {
+  const jsize k = (jsize)shim_knn_k(h);
+  return need_len(env, oo, k, what) && need_len(env, od, k, what) && need_len(env, oi, k, what);
+}
+/* Get<Type>ArrayElements can fail (out of memory): NULL throws, release what was pinned */
+static int pinned_ok(JNIEnv* env, const void* a, const void* b, const void* c) {
+  if (a && b && c) return 1;
+  throw_msg(env, "java/lang/OutOfMemoryError", "pinning result arrays");
+  return 0;
+}
+
 /* UniformGrid(n, minX, maxX, minY, maxY) as double[5] */
 static int grid_of(JNIEnv* env, jdoubleArray jg, gf_grid* g) {
   if (!need_len(env, jg, 5, "grid: {n, minX, maxX, minY, maxY}")) return GF_ERR_ARG;
@@ -217,17 +230,18 @@ JNIEXPORT jint JNICALL Java_GeoFlink_native_1_GeoFlinkHip_knnWindow(JNIEnv* env,
   const double* x = direct(env, bx, 8 * (int64_t)n, "knnWindow: x");
   const double* y = direct(env, by, 8 * (int64_t)n, "knnWindow: y");
   const int64_t* o = direct(env, bo, 8 * (int64_t)n, "knnWindow: objID");
-  if ((*env)->ExceptionCheck(env) || !need_len(env, oo, k, "knnWindow: out") || !need_len(env, od, k, "knnWindow: out") ||
-      !need_len(env, oi, k, "knnWindow: out"))
+  (void)k;  /* the arrays are checked against the plan's own k */
+  if ((*env)->ExceptionCheck(env) || !need_knn_out(env, (shim_knn*)(intptr_t)plan, oo, od, oi, "knnWindow: out"))
     return 0;
   int32_t m = 0;
   jlong* po = (*env)->GetPrimitiveArrayCritical(env, oo, NULL);
-  jdouble* pd = (*env)->GetPrimitiveArrayCritical(env, od, NULL);
-  jlong* pi = (*env)->GetPrimitiveArrayCritical(env, oi, NULL);
-  int st = shim_knn_window((shim_knn*)(intptr_t)plan, x, y, o, n, (int64_t*)po, pd, (int64_t*)pi, &m);
-  (*env)->ReleasePrimitiveArrayCritical(env, oi, pi, 0);
-  (*env)->ReleasePrimitiveArrayCritical(env, od, pd, 0);
-  (*env)->ReleasePrimitiveArrayCritical(env, oo, po, 0);
+  jdouble* pd = po ? (*env)->GetPrimitiveArrayCritical(env, od, NULL) : NULL;
+  jlong* pi = pd ? (*env)->GetPrimitiveArrayCritical(env, oi, NULL) : NULL;
+  int st = pi ? shim_knn_window((shim_knn*)(intptr_t)plan, x, y, o, n, (int64_t*)po, pd, (int64_t*)pi, &m) : GF_ERR_NOMEM;
+  if (pi) (*env)->ReleasePrimitiveArrayCritical(env, oi, pi, 0);
+  if (pd) (*env)->ReleasePrimitiveArrayCritical(env, od, pd, 0);
+  if (po) (*env)->ReleasePrimitiveArrayCritical(env, oo, po, 0);
+  if (!pinned_ok(env, po, pd, pi)) return 0;
   throw_status(env, st, CTX(ctx));
   return m;
 }
@@ -281,19 +295,65 @@ JNIEXPORT jint JNICALL Java_GeoFlink_native_1_GeoFlinkHip_knnWindowSharded(JNIEn
   const double* x = direct(env, bx, 8 * (int64_t)n, "knnWindowSharded: x");
   const double* y = direct(env, by, 8 * (int64_t)n, "knnWindowSharded: y");
   const int64_t* o = direct(env, bo, 8 * (int64_t)n, "knnWindowSharded: objID");
-  if ((*env)->ExceptionCheck(env) || !need_len(env, oo, k, "knnWindowSharded: out") ||
-      !need_len(env, od, k, "knnWindowSharded: out") || !need_len(env, oi, k, "knnWindowSharded: out"))
+  (void)k;  /* the arrays are checked against the plan's own k */
+  if ((*env)->ExceptionCheck(env) || !need_knn_out(env, (shim_knn*)(intptr_t)plan, oo, od, oi, "knnWindowSharded: out"))
     return 0;
   /* not GetPrimitiveArrayCritical: the call blocks on a collective with the other ranks */
   int32_t m = 0;
   jlong* po = (*env)->GetLongArrayElements(env, oo, NULL);
   jdouble* pd = (*env)->GetDoubleArrayElements(env, od, NULL);
   jlong* pi = (*env)->GetLongArrayElements(env, oi, NULL);
-  int st = shim_knn_window_sharded((shim_knn*)(intptr_t)plan, (shim_comm*)(intptr_t)comm, x, y, o, n, indexBase,
-                                   (int64_t*)po, pd, (int64_t*)pi, &m);
-  (*env)->ReleaseLongArrayElements(env, oi, pi, st ? JNI_ABORT : 0);
-  (*env)->ReleaseDoubleArrayElements(env, od, pd, st ? JNI_ABORT : 0);
-  (*env)->ReleaseLongArrayElements(env, oo, po, st ? JNI_ABORT : 0);
+  int st = po && pd && pi ? shim_knn_window_sharded((shim_knn*)(intptr_t)plan, (shim_comm*)(intptr_t)comm, x, y, o, n,
+                                                    indexBase, (int64_t*)po, pd, (int64_t*)pi, &m)
+                          : GF_ERR_NOMEM;
+  if (pi) (*env)->ReleaseLongArrayElements(env, oi, pi, st ? JNI_ABORT : 0);
+  if (pd) (*env)->ReleaseDoubleArrayElements(env, od, pd, st ? JNI_ABORT : 0);
+  if (po) (*env)->ReleaseLongArrayElements(env, oo, po, st ? JNI_ABORT : 0);
+  if (!pinned_ok(env, po, pd, pi)) return 0;
+  throw_status(env, st, CTX(ctx));
+  return m;
+}
+
+/* ---- the batched sharded path: enqueue per window, one String exchange per B windows ---------- */
+JNIEXPORT void JNICALL Java_GeoFlink_native_1_GeoFlinkHip_knnShardedBegin(JNIEnv* env, jclass cls, jlong ctx,
+    jlong plan, jlong comm, jint batch, jlong capBytes) {
+  throw_status(env, shim_knn_sharded_begin((shim_knn*)(intptr_t)plan, (shim_comm*)(intptr_t)comm, batch, capBytes),
+               CTX(ctx));
+}
+/* this subtask's band of the next window -> its ticket (x, y, objID are copied before returning) */
+JNIEXPORT jlong JNICALL Java_GeoFlink_native_1_GeoFlinkHip_knnShardedEnqueue(JNIEnv* env, jclass cls, jlong ctx,
+    jlong plan, jobject bx, jobject by, jobject bo, jint n, jlong indexBase) {
+  const double* x = direct(env, bx, 8 * (int64_t)n, "knnShardedEnqueue: x");
+  const double* y = direct(env, by, 8 * (int64_t)n, "knnShardedEnqueue: y");
+  const int64_t* o = direct(env, bo, 8 * (int64_t)n, "knnShardedEnqueue: objID");
+  if ((*env)->ExceptionCheck(env)) return -1;
+  int64_t t = -1;
+  throw_status(env, shim_knn_sharded_enqueue((shim_knn*)(intptr_t)plan, x, y, o, n, indexBase, &t), CTX(ctx));
+  return t;
+}
+JNIEXPORT void JNICALL Java_GeoFlink_native_1_GeoFlinkHip_knnShardedFlush(JNIEnv* env, jclass cls, jlong ctx,
+    jlong plan) {
+  throw_status(env, shim_knn_sharded_flush((shim_knn*)(intptr_t)plan), CTX(ctx));
+}
+/* a ticket's merged neighbours: outDist, outIdx (global) and owned (1 = a Point of this band);
+ * returns their number; the arrays hold >= the plan's k */
+JNIEXPORT jint JNICALL Java_GeoFlink_native_1_GeoFlinkHip_knnShardedResult(JNIEnv* env, jclass cls, jlong ctx,
+    jlong plan, jlong ticket, jdoubleArray od, jlongArray oi, jintArray ow) {
+  shim_knn* h = (shim_knn*)(intptr_t)plan;
+  const jsize k = (jsize)shim_knn_k(h);
+  if (!need_len(env, od, k, "knnShardedResult: out") || !need_len(env, oi, k, "knnShardedResult: out") ||
+      !need_len(env, ow, k, "knnShardedResult: out"))
+    return 0;
+  /* not GetPrimitiveArrayCritical: a flagged window's second exchange waits on the other ranks */
+  int32_t m = 0;
+  jdouble* pd = (*env)->GetDoubleArrayElements(env, od, NULL);
+  jlong* pi = (*env)->GetLongArrayElements(env, oi, NULL);
+  jint* pw = (*env)->GetIntArrayElements(env, ow, NULL);
+  int st = pd && pi && pw ? shim_knn_sharded_result(h, ticket, pd, (int64_t*)pi, (int32_t*)pw, &m) : GF_ERR_NOMEM;
+  if (pw) (*env)->ReleaseIntArrayElements(env, ow, pw, st ? JNI_ABORT : 0);
+  if (pi) (*env)->ReleaseLongArrayElements(env, oi, pi, st ? JNI_ABORT : 0);
+  if (pd) (*env)->ReleaseDoubleArrayElements(env, od, pd, st ? JNI_ABORT : 0);
+  if (!pinned_ok(env, pd, pi, pw)) return 0;
   throw_status(env, st, CTX(ctx));
   return m;
 }
@@ -328,17 +388,18 @@ JNIEXPORT jlong JNICALL Java_GeoFlink_native_1_GeoFlinkHip_knnSlidingPush(JNIEnv
 }
 JNIEXPORT jint JNICALL Java_GeoFlink_native_1_GeoFlinkHip_knnSlidingDecode(JNIEnv* env, jclass cls, jlong ctx,
     jlong s, jlong window_end, jlongArray oo, jdoubleArray od, jlongArray oi, jint k) {
-  if (!need_len(env, oo, k, "knnSlidingDecode: out") || !need_len(env, od, k, "knnSlidingDecode: out") ||
-      !need_len(env, oi, k, "knnSlidingDecode: out"))
-    return 0;
+  (void)k;  /* the arrays are checked against the plan's own k */
+  if (!need_knn_out(env, shim_sliding_plan((shim_sliding*)(intptr_t)s), oo, od, oi, "knnSlidingDecode: out")) return 0;
   int32_t m = 0;
   jlong* po = (*env)->GetPrimitiveArrayCritical(env, oo, NULL);
-  jdouble* pd = (*env)->GetPrimitiveArrayCritical(env, od, NULL);
-  jlong* pi = (*env)->GetPrimitiveArrayCritical(env, oi, NULL);
-  int st = shim_sliding_decode((shim_sliding*)(intptr_t)s, window_end, (int64_t*)po, pd, (int64_t*)pi, &m);
-  (*env)->ReleasePrimitiveArrayCritical(env, oi, pi, 0);
-  (*env)->ReleasePrimitiveArrayCritical(env, od, pd, 0);
-  (*env)->ReleasePrimitiveArrayCritical(env, oo, po, 0);
+  jdouble* pd = po ? (*env)->GetPrimitiveArrayCritical(env, od, NULL) : NULL;
+  jlong* pi = pd ? (*env)->GetPrimitiveArrayCritical(env, oi, NULL) : NULL;
+  int st = pi ? shim_sliding_decode((shim_sliding*)(intptr_t)s, window_end, (int64_t*)po, pd, (int64_t*)pi, &m)
+              : GF_ERR_NOMEM;
+  if (pi) (*env)->ReleasePrimitiveArrayCritical(env, oi, pi, 0);
+  if (pd) (*env)->ReleasePrimitiveArrayCritical(env, od, pd, 0);
+  if (po) (*env)->ReleasePrimitiveArrayCritical(env, oo, po, 0);
+  if (!pinned_ok(env, po, pd, pi)) return 0;
   throw_status(env, st, CTX(ctx));
   return m;
 }
@@ -390,6 +451,19 @@ JNIEXPORT jlong JNICALL Java_GeoFlink_native_1_GeoFlinkHip_rangeWindow(JNIEnv* e
   if ((*env)->ExceptionCheck(env)) return 0;
   int64_t count = 0;
   int st = shim_range_window((shim_range*)(intptr_t)plan, x, y, n, out, out_cap, &count);
+  if (st != GF_ERR_CAPACITY) throw_status(env, st, CTX(ctx));
+  return count;
+}
+
+/* approximate point-point range with |Q| > 1: the points of the last rangeWindow the reference
+ * emits once per query point (PointPointRangeQuery.java:158-161); returns their count (> outCap:
+ * call again with a larger buffer), 0 for other plans */
+JNIEXPORT jlong JNICALL Java_GeoFlink_native_1_GeoFlinkHip_rangeWindowMulti(JNIEnv* env, jclass cls, jlong ctx,
+    jlong plan, jobject bout, jint out_cap) {
+  int32_t* out = direct(env, bout, 4 * (int64_t)out_cap, "rangeWindowMulti: out");
+  if ((*env)->ExceptionCheck(env)) return 0;
+  int64_t count = 0;
+  int st = shim_range_window_multi((shim_range*)(intptr_t)plan, out, out_cap, &count);
   if (st != GF_ERR_CAPACITY) throw_status(env, st, CTX(ctx));
   return count;
 }

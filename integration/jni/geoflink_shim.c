@@ -157,6 +157,26 @@ int shim_objid_decode(shim_ctx* c, const int64_t* keys, int64_t n, char* buf, in
 }
 
 /* ---- kNN -------------------------------------------------------------------------------- */
+/* the batched sharded path (shim_knn_sharded_*): 2B slots, groups of B consecutive tickets */
+#define SHIM_SHARD_MAX_BATCH 32
+typedef struct {
+  shim_comm* comm;
+  int32_t B;
+  int64_t cap_bytes;
+  size_t rb, sb;                 /* record / string record bytes */
+  cached_window win[2 * SHIM_SHARD_MAX_BATCH];
+  gf_points pts[2 * SHIM_SHARD_MAX_BATCH];
+  int64_t base[2 * SHIM_SHARD_MAX_BATCH], npts[2 * SHIM_SHARD_MAX_BATCH];
+  int64_t ticket[2 * SHIM_SHARD_MAX_BATCH];  /* the ticket in the slot, -1 when read (free) */
+  dbuf rec;                      /* 2B device records */
+  pbuf merged;                   /* 2B merged string records (mapped pinned) */
+  dbuf one;                      /* one exact record, for a flagged window's second exchange */
+  pbuf one_merged;
+  char* strbuf;                  /* decode scratch: the Strings of one merged record */
+  int64_t* strofs;
+  int64_t next, exchanged, synced;
+} shard_state;
+
 struct shim_knn {
   shim_ctx* c;
   gf_knn_plan* plan;
@@ -164,6 +184,7 @@ struct shim_knn {
   cached_window win;
   dbuf rec;     /* sharded windows: this rank's device record */
   pbuf merged;  /* ... and the merged record of all ranks (mapped pinned) */
+  shard_state* sh;
 };
 
 int shim_knn_plan(shim_ctx* c, const gf_grid* g, double qx, double qy, double r, int32_t k, shim_knn** out) {
@@ -197,15 +218,30 @@ int shim_knn_polygon_plan(shim_ctx* c, const gf_grid* g, const gf_polygons* poly
   return GF_OK;
 }
 
+static void shard_free(shard_state* sh) {
+  if (!sh) return;
+  for (int i = 0; i < 2 * SHIM_SHARD_MAX_BATCH; ++i) window_free(&sh->win[i]);
+  dbuf_free(&sh->rec);
+  pbuf_free(&sh->merged);
+  dbuf_free(&sh->one);
+  pbuf_free(&sh->one_merged);
+  free(sh->strbuf);
+  free(sh->strofs);
+  free(sh);
+}
+
 void shim_knn_destroy(shim_knn* h) {
   if (!h) return;
   gf_ctx_synchronize(h->c->ctx);
   window_free(&h->win);
   dbuf_free(&h->rec);
   pbuf_free(&h->merged);
+  shard_free(h->sh);
   gf_knn_plan_destroy(h->plan);
   free(h);
 }
+
+int32_t shim_knn_k(const shim_knn* h) { return h ? h->k : 0; }
 
 int shim_knn_window(shim_knn* h, const double* x, const double* y, const int64_t* objID, int64_t n, int64_t* out_objID,
                     double* out_dist, int64_t* out_idx, int32_t* m) {
@@ -316,8 +352,152 @@ int shim_knn_window_sharded(shim_knn* h, shim_comm* comm, const double* x, const
   }
   if (!st && ((const gf_knn_header*)h->merged.p)->status != 0) st = GF_ERR_ARG;  /* 2: dictionary keys */
   if (!st) st = gf_knn_decode(h->plan, &pts, h->merged.p, out_objID, out_dist, out_idx, m);
-  if (!st) st = gf_knn_plan_set_index_base(h->plan, 0);
-  return fail(h->c, st, "knnWindowSharded");
+  /* every exit path: the next knnWindow on this plan reports window-local indices */
+  const int st0 = gf_knn_plan_set_index_base(h->plan, 0);
+  return fail(h->c, st ? st : st0, "knnWindowSharded");
+}
+
+/* ---- the batched sharded path ------------------------------------------------------------ */
+int shim_knn_sharded_begin(shim_knn* h, shim_comm* comm, int32_t batch, int64_t cap_bytes) {
+  if (!h || !comm || batch < 1 || batch > SHIM_SHARD_MAX_BATCH || cap_bytes < 0 || cap_bytes > (1 << 24))
+    return fail(h ? h->c : NULL, GF_ERR_ARG, "knnShardedBegin: bad argument");
+  if (h->sh) return fail(h->c, GF_ERR_ARG, "knnShardedBegin: already begun on this plan");
+  shard_state* sh = (shard_state*)calloc(1, sizeof(shard_state));
+  if (!sh) return GF_ERR_NOMEM;
+  sh->comm = comm;
+  sh->B = batch;
+  sh->cap_bytes = cap_bytes;
+  sh->rb = gf_knn_result_bytes(h->k);
+  sh->sb = gf_knn_string_record_bytes(h->k, cap_bytes);
+  for (int i = 0; i < 2 * SHIM_SHARD_MAX_BATCH; ++i) sh->ticket[i] = -1;
+  int st = dbuf_need(&sh->rec, 2 * (size_t)batch * sh->rb);
+  if (!st) st = pbuf_need(&sh->merged, 2 * (size_t)batch * sh->sb);
+  if (!st) st = dbuf_need(&sh->one, sh->rb);
+  if (!st) st = pbuf_need(&sh->one_merged, sh->sb);
+  sh->strbuf = (char*)malloc((size_t)cap_bytes + 64);
+  sh->strofs = (int64_t*)malloc(sizeof(int64_t) * ((size_t)h->k + 1));
+  if (!st && (!sh->strbuf || !sh->strofs)) st = GF_ERR_NOMEM;
+  if (st) {
+    shard_free(sh);
+    return fail(h->c, st, "knnShardedBegin");
+  }
+  h->sh = sh;
+  return GF_OK;
+}
+
+/* one exchange of the enqueued, not yet exchanged windows (a group's slots are contiguous: groups
+ * start at multiples of B, and a flushed partial group skips the rest of its tickets) */
+static int shard_exchange(shim_knn* h) {
+  shard_state* sh = h->sh;
+  const int64_t n = sh->next - sh->exchanged;
+  if (n <= 0) return GF_OK;
+  gf_objid_dict* dict = NULL;
+  const size_t s0 = (size_t)(sh->exchanged % (2 * sh->B));
+  int st = gf_knn_plan_flush(h->plan);  /* pipelined plans: the group's last records complete */
+  if (!st) st = gf_ctx_objid_dict(h->c->ctx, &dict);
+  if (!st)
+    st = gf_knn_exchange_strings_batch(sh->comm->comm, dict, h->k, sh->cap_bytes, (char*)sh->rec.p + s0 * sh->rb,
+                                       (int32_t)n, (char*)sh->merged.p + s0 * sh->sb);
+  if (st) return st;
+  sh->exchanged = sh->next = (sh->next + sh->B - 1) / sh->B * sh->B;
+  return GF_OK;
+}
+
+int shim_knn_sharded_enqueue(shim_knn* h, const double* x, const double* y, const int64_t* objID, int64_t n,
+                             int64_t index_base, int64_t* ticket) {
+  shard_state* sh = h->sh;
+  *ticket = -1;
+  if (!sh) return fail(h->c, GF_ERR_ARG, "knnShardedEnqueue: knnShardedBegin first");
+  const int64_t t = sh->next;
+  const int s = (int)(t % (2 * sh->B));
+  if (sh->ticket[s] >= 0) return fail(h->c, GF_ERR_ARG, "knnShardedEnqueue: the result of the window 2B back is unread");
+  int st = upload(h->c->ctx, &sh->win[s], x, y, objID, n, &sh->pts[s]);
+  if (!st) st = gf_knn_plan_set_index_base(h->plan, index_base);
+  if (!st) st = gf_knn_enqueue(h->plan, &sh->pts[s], (char*)sh->rec.p + (size_t)s * sh->rb);
+  const int st0 = gf_knn_plan_set_index_base(h->plan, 0);
+  if (!st) st = st0;
+  if (st) return fail(h->c, st, "knnShardedEnqueue");
+  sh->ticket[s] = t;
+  sh->base[s] = index_base;
+  sh->npts[s] = n;
+  sh->next = t + 1;
+  *ticket = t;
+  if (sh->next % sh->B == 0) st = shard_exchange(h);  /* the group is complete: its exchange */
+  return fail(h->c, st, "knnShardedEnqueue");
+}
+
+int shim_knn_sharded_flush(shim_knn* h) {
+  if (!h->sh) return fail(h->c, GF_ERR_ARG, "knnShardedFlush: knnShardedBegin first");
+  return fail(h->c, shard_exchange(h), "knnShardedFlush");
+}
+
+/* a merged string record -> entries (dist, idx) and which of them this rank's band holds */
+static int shard_decode(shim_knn* h, const void* rec, int s, double* dist, int64_t* idx, int32_t* owned, int32_t* m,
+                        int32_t* status) {
+  shard_state* sh = h->sh;
+  int st = gf_knn_string_record_decode(rec, h->k, sh->cap_bytes, status, NULL, dist, idx, sh->strbuf,
+                                       sh->cap_bytes + 64, sh->strofs, m);
+  if (st || *status != 0) return st;
+  for (int32_t i = 0; i < *m; ++i) owned[i] = idx[i] >= sh->base[s] && idx[i] < sh->base[s] + sh->npts[s];
+  return GF_OK;
+}
+
+int shim_knn_sharded_result(shim_knn* h, int64_t ticket, double* out_dist, int64_t* out_idx, int32_t* owned,
+                            int32_t* m) {
+  shard_state* sh = h->sh;
+  *m = 0;
+  if (!sh) return fail(h->c, GF_ERR_ARG, "knnShardedResult: knnShardedBegin first");
+  const int s = (int)(ticket % (2 * sh->B));
+  if (ticket < 0 || ticket >= sh->exchanged || sh->ticket[s] != ticket)
+    return fail(h->c, GF_ERR_ARG, "knnShardedResult: ticket not exchanged yet (knnShardedFlush) or already read");
+  gf_ctx* ctx = h->c->ctx;
+  int st = GF_OK;
+  if (ticket >= sh->synced) {  /* one host wait per group */
+    st = gf_ctx_synchronize(ctx);
+    if (st) return fail(h->c, st, "knnShardedResult");
+    sh->synced = sh->exchanged;
+  }
+  int32_t status = 0;
+  st = shard_decode(h, (const char*)sh->merged.p + (size_t)s * sh->sb, s, out_dist, out_idx, owned, m, &status);
+  if (!st && status == 1) {
+    /* some rank's record needed the exact re-evaluation: every rank sees the same merged status,
+     * re-evaluates its band exactly (its local record, on the host) and the ranks exchange the
+     * exact records of this window once more */
+    gf_objid_dict* dict = NULL;
+    void* local = malloc(sh->rb);
+    int64_t* lo = (int64_t*)malloc(sizeof(int64_t) * (size_t)h->k);
+    double* ld = (double*)malloc(sizeof(double) * (size_t)h->k);
+    int64_t* li = (int64_t*)malloc(sizeof(int64_t) * (size_t)h->k);
+    int32_t lm = 0;
+    if (!local || !lo || !ld || !li) st = GF_ERR_NOMEM;
+    if (!st && copy(h->c, local, (char*)sh->rec.p + (size_t)s * sh->rb, sh->rb, hipMemcpyDeviceToHost)) st = GF_ERR_HIP;
+    if (!st) st = gf_ctx_synchronize(ctx);
+    if (!st) st = gf_knn_plan_set_index_base(h->plan, sh->base[s]);
+    if (!st) st = gf_knn_decode(h->plan, &sh->pts[s], local, lo, ld, li, &lm);
+    const int st0 = gf_knn_plan_set_index_base(h->plan, 0);
+    if (!st) st = st0;
+    if (!st) {
+      gf_knn_header* hd = (gf_knn_header*)local;
+      memset(local, 0, sh->rb);
+      hd->status = 0;
+      hd->n = lm;
+      hd->k = h->k;
+      double* rd = (double*)(hd + 1);
+      memcpy(rd, ld, sizeof(double) * (size_t)lm);
+      memcpy(rd + h->k, lo, sizeof(int64_t) * (size_t)lm);
+      memcpy((int64_t*)(rd + h->k) + h->k, li, sizeof(int64_t) * (size_t)lm);
+      if (copy(h->c, sh->one.p, local, sh->rb, hipMemcpyHostToDevice)) st = GF_ERR_HIP;
+    }
+    if (!st) st = gf_ctx_objid_dict(ctx, &dict);
+    if (!st) st = gf_knn_exchange_strings_batch(sh->comm->comm, dict, h->k, sh->cap_bytes, sh->one.p, 1, sh->one_merged.p);
+    if (!st) st = gf_ctx_synchronize(ctx);  /* (local is freed below) */
+    free(local); free(lo); free(ld); free(li);
+    if (!st) st = shard_decode(h, sh->one_merged.p, s, out_dist, out_idx, owned, m, &status);
+  }
+  if (!st && status != 0) st = status == GF_KNN_STATUS_FOREIGN_KEYS ? GF_ERR_CAPACITY : GF_ERR_ARG;
+  if (st) *m = 0;
+  else sh->ticket[s] = -1;  /* read: the slot may take window ticket + 2B */
+  return fail(h->c, st, "knnShardedResult");
 }
 
 /* ---- sliding kNN -------------------------------------------------------------------------- */
@@ -397,6 +577,8 @@ int shim_sliding_push(shim_sliding* s, int64_t pane_index, const double* x, cons
   return GF_OK;
 }
 
+shim_knn* shim_sliding_plan(shim_sliding* s) { return s ? s->plan : NULL; }
+
 int shim_sliding_flush(shim_sliding* s) {
   int st = gf_knn_sliding_flush(s->s);
   if (!st) s->pending_end = -1;
@@ -424,6 +606,10 @@ struct shim_range {
   cached_window win;
   dbuf bitmap;
   pbuf idx;      /* pinned: the index list written by the device, then the count */
+  int multi;     /* approximate point plan with |Q| > 1: candidate-cell points emitted |Q| times */
+  dbuf mbitmap;
+  pbuf midx;     /* pinned: the last window's multiplicity list, then its count */
+  int64_t mcount;
 };
 
 static int range_new(shim_ctx* c, gf_range_plan* plan, int st, shim_range** out, const char* what) {
@@ -443,7 +629,9 @@ int shim_range_plan(shim_ctx* c, const gf_grid* g, const double* qx, const doubl
                     int approximate, shim_range** out) {
   gf_range_plan* plan = NULL;
   int st = gf_range_pp_plan_create(c->ctx, g, qx, qy, nq, r, approximate, GF_METRIC_SQRT, &plan);
-  return range_new(c, plan, st, out, "rangePlan");
+  st = range_new(c, plan, st, out, "rangePlan");
+  if (!st) (*out)->multi = approximate && nq > 1;
+  return st;
 }
 
 int shim_range_polygon_plan(shim_ctx* c, const gf_grid* g, const gf_polygons* polys, double r, int approximate,
@@ -459,6 +647,8 @@ void shim_range_destroy(shim_range* h) {
   window_free(&h->win);
   dbuf_free(&h->bitmap);
   pbuf_free(&h->idx);
+  dbuf_free(&h->mbitmap);
+  pbuf_free(&h->midx);
   gf_range_plan_destroy(h->plan);
   free(h);
 }
@@ -467,17 +657,31 @@ int shim_range_window(shim_range* h, const double* x, const double* y, int64_t n
                       int64_t* count) {
   gf_points pts;
   *count = 0;
+  h->mcount = 0;
+  const size_t lcap = 4 * (size_t)(n > 0 ? n : 1) + 16;  /* an index list of n, then its count */
   int st = upload(h->c->ctx, &h->win, x, y, NULL, n, &pts);
   if (!st) st = dbuf_need(&h->bitmap, 8 * (size_t)((n + 63) / 64 + 1));
-  if (!st) st = pbuf_need(&h->idx, 4 * (size_t)(n > 0 ? n : 1) + 16);
-  if (!st) st = gf_range_run(h->plan, &pts, (uint64_t*)h->bitmap.p, NULL, NULL);
+  if (!st) st = pbuf_need(&h->idx, lcap);
+  if (!st && h->multi) st = dbuf_need(&h->mbitmap, 8 * (size_t)((n + 63) / 64 + 1));
+  if (!st && h->multi) st = pbuf_need(&h->midx, lcap);
+  if (!st) st = gf_range_run(h->plan, &pts, (uint64_t*)h->bitmap.p, h->multi ? (uint64_t*)h->mbitmap.p : NULL, NULL);
   /* the index list straight into pinned host memory, its count after it: one sync */
   int64_t* dcount = (int64_t*)((char*)h->idx.p + ((4 * (size_t)(n > 0 ? n : 1) + 7) / 8) * 8);
+  int64_t* mcount = h->multi ? (int64_t*)((char*)h->midx.p + ((4 * (size_t)(n > 0 ? n : 1) + 7) / 8) * 8) : NULL;
   if (!st) st = gf_bitmap_to_indices_async(h->c->ctx, (const uint64_t*)h->bitmap.p, n, (uint32_t*)h->idx.p, n, dcount);
+  if (!st && h->multi)
+    st = gf_bitmap_to_indices_async(h->c->ctx, (const uint64_t*)h->mbitmap.p, n, (uint32_t*)h->midx.p, n, mcount);
   if (!st) st = gf_ctx_synchronize(h->c->ctx);
   if (st) return fail(h->c, st, "rangeWindow");
+  if (mcount) h->mcount = *mcount;
   *count = *dcount;
   memcpy(out_idx, h->idx.p, 4 * (size_t)(*count < cap ? *count : cap));
+  return *count > cap ? GF_ERR_CAPACITY : GF_OK;
+}
+
+int shim_range_window_multi(shim_range* h, int32_t* out_idx, int64_t cap, int64_t* count) {
+  *count = h->multi ? h->mcount : 0;
+  if (*count > 0) memcpy(out_idx, h->midx.p, 4 * (size_t)(*count < cap ? *count : cap));
   return *count > cap ? GF_ERR_CAPACITY : GF_OK;
 }
 

@@ -53,6 +53,8 @@ int shim_pinned_alloc(int64_t bytes, void** out);
 void shim_pinned_free(void* p);
 int shim_knn_window(shim_knn* h, const double* x, const double* y, const int64_t* objID, int64_t n, int64_t* out_objID,
                     double* out_dist, int64_t* out_idx, int32_t* m);
+/* the plan's k: every kNN result array handed to the plan must hold at least this many entries */
+int32_t shim_knn_k(const shim_knn* h);
 
 /* ---- multi-GPU kNN: one subtask per GPU holds its cell-column band of every window; the
  * windowAll merge (PointPointKNNQuery.java:198-200, KNNQuery.java:213-272) becomes the RCCL
@@ -71,6 +73,27 @@ void shim_comm_destroy(shim_comm* comm);
 int shim_knn_window_sharded(shim_knn* h, shim_comm* comm, const double* x, const double* y, const int64_t* objID,
                             int64_t n, int64_t index_base, int64_t* out_objID, double* out_dist, int64_t* out_idx,
                             int32_t* m);
+/* The batched, asynchronous form (the path bench.py --gpus N times): windows are ENQUEUED (this
+ * rank's band uploaded into one of 2B device windows, its top-k record written on the device) and
+ * every B-th enqueue issues ONE exchange of the last B windows' records -- by String
+ * (gf_knn_exchange_strings_batch: the ranks' dictionaries differ, the windowAll merge dedupes by
+ * Point.objID, KNNQuery.java:232-251) -- without a host wait; results are read per window after
+ * its group's exchange.  Collective order: every rank makes the same begin / enqueue / flush /
+ * result calls in the same order (result of a flagged window re-exchanges it on every rank).
+ *   begin:   batch B (1..32), cap_bytes = the Strings of one record (e.g. 32 k)
+ *   enqueue: *ticket = the window's sequence number; GF_ERR_ARG when the window 2B tickets back
+ *            (same slot) was not read yet
+ *   flush:   exchange the enqueued windows of an incomplete group now (end of stream, a timer)
+ *   result:  a ticket whose group was exchanged -> *m entries, ascending (dist, String): dist,
+ *            global idx (index_base + window position); `owned` marks the entries of this rank's
+ *            band (index_base <= idx < index_base + n), so each rank emits its own Points.
+ *            GF_ERR_ARG for a ticket not exchanged (call flush) or already read. */
+int shim_knn_sharded_begin(shim_knn* h, shim_comm* comm, int32_t batch, int64_t cap_bytes);
+int shim_knn_sharded_enqueue(shim_knn* h, const double* x, const double* y, const int64_t* objID, int64_t n,
+                             int64_t index_base, int64_t* ticket);
+int shim_knn_sharded_flush(shim_knn* h);
+int shim_knn_sharded_result(shim_knn* h, int64_t ticket, double* out_dist, int64_t* out_idx, int32_t* owned,
+                            int32_t* m);
 
 /* ---- sliding kNN: SlidingProcessingTimeWindows.of(size, slide) around the kNN apply
  * (PointPointKNNQuery.java:158,198-200) -- the pane engine (gf_knn_sliding_*) ---------------- */
@@ -83,6 +106,7 @@ int shim_sliding_pane_ms(const shim_sliding* s, int64_t* pane_ms);
 int shim_sliding_push(shim_sliding* s, int64_t pane_index, const double* x, const double* y, const int64_t* objID,
                       int64_t n, int32_t* closed, int64_t* window_end);
 int shim_sliding_flush(shim_sliding* s);
+shim_knn* shim_sliding_plan(shim_sliding* s);  /* the kNN plan the engine runs (its k sizes decode's arrays) */
 int shim_sliding_decode(shim_sliding* s, int64_t window_end, int64_t* out_objID, double* out_dist, int64_t* out_idx,
                         int32_t* m);
 
@@ -97,6 +121,11 @@ void shim_range_destroy(shim_range* h);
  * > cap).  One device pass: bitmap, then the index list into pinned memory, one stream sync. */
 int shim_range_window(shim_range* h, const double* x, const double* y, int64_t n, int32_t* out_idx, int64_t cap,
                       int64_t* count);
+/* approximate point-point range with |Q| > 1: the reference's apply emits a candidate-cell point
+ * once per query point (PointPointRangeQuery.java:158-161), so those points of the LAST window
+ * (ascending, a subset of shim_range_window's list) are listed here -- emit each |Q| times in
+ * all.  *count = 0 for every other plan. */
+int shim_range_window_multi(shim_range* h, int32_t* out_idx, int64_t cap, int64_t* count);
 
 /* ---- sliding range: SlidingProcessingTimeWindows.of(size, slide) around the range apply
  * (PointPointRangeQuery.java:149-186) -- the pane engine (gf_range_sliding_*) ------------------ */

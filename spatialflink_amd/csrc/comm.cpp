@@ -20,6 +20,7 @@
 #include <dlfcn.h>
 #include <rccl/rccl.h>
 
+#include <atomic>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -39,6 +40,7 @@ struct Rccl {
   ncclResult_t (*CommInitRank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
   ncclResult_t (*CommInitAll)(ncclComm_t*, int, const int*) = nullptr;
   ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
+  ncclResult_t (*CommAbort)(ncclComm_t) = nullptr;
   ncclResult_t (*CommGetAsyncError)(ncclComm_t, ncclResult_t*) = nullptr;
   ncclResult_t (*AllGather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
   ncclResult_t (*GroupStart)() = nullptr;
@@ -67,6 +69,7 @@ Rccl& rccl_state() {
     sym(R.CommInitRank, "ncclCommInitRank");
     sym(R.CommInitAll, "ncclCommInitAll");
     sym(R.CommDestroy, "ncclCommDestroy");
+    sym(R.CommAbort, "ncclCommAbort");
     sym(R.CommGetAsyncError, "ncclCommGetAsyncError");
     sym(R.AllGather, "ncclAllGather");
     sym(R.GroupStart, "ncclGroupStart");
@@ -97,6 +100,11 @@ struct gf_comm {
   ncclComm_t comm = nullptr;
   int32_t nranks = 0, rank = 0;
   int device = 0;
+  // communicators created together by one gf_comm_create_all share a nonzero clique id (the
+  // group exchange needs one whole clique); gf_comm_create's are 0.  aborted: an exchange failed
+  // inside an RCCL group and the clique was aborted (every later call is refused)
+  uint64_t clique = 0;
+  bool aborted = false;
   std::string last_error;
   // device buffers of the exchange, grown on demand: the gathered records of every rank, and
   // this rank's string records (gf_knn_attach_strings' output) for the String exchange
@@ -186,12 +194,15 @@ extern "C" int gf_comm_create_all(int32_t ndev, const int* devices, gf_comm** ou
   std::vector<ncclComm_t> comms(ndev, nullptr);
   const ncclResult_t r = R->CommInitAll(comms.data(), ndev, devices);
   if (r != ncclSuccess) return fail(std::string("ncclCommInitAll: ") + R->GetErrorString(r));
+  static std::atomic<uint64_t> next_clique{1};
+  const uint64_t clique = next_clique.fetch_add(1);
   for (int32_t i = 0; i < ndev; ++i) {
     gf_comm* c = new gf_comm();
     c->comm = comms[i];
     c->nranks = ndev;
     c->rank = i;
     c->device = devices[i];
+    c->clique = clique;
     out[i] = c;
   }
   return GF_OK;
@@ -201,7 +212,7 @@ extern "C" void gf_comm_destroy(gf_comm* c) {
   if (!c) return;
   hipSetDevice(c->device);
   hipDeviceSynchronize();  // exchanges still queued read the buffers
-  if (c->comm)
+  if (c->comm && !c->aborted)
     if (Rccl* R = rccl()) R->CommDestroy(c->comm);
   if (c->gather) hipFree(c->gather);
   if (c->strings) hipFree(c->strings);
@@ -235,6 +246,7 @@ static int exchange_args_ok(gf_comm* c, gf_ctx* ctx, int32_t k, const void* reco
                             const char* what) {
   if (!c || !ctx || k < 1 || k > kMaxKLarge || nwin < 1 || nwin > 65535 || !records || !merged)
     return set_err(ctx, GF_ERR_ARG, std::string(what) + ": bad argument");
+  if (c->aborted) return comm_err(c, ctx, std::string(what) + ": the communicator was aborted after a failed group");
   if (ctx->device != c->device)
     return set_err(ctx, GF_ERR_ARG, std::string(what) + ": the context's device is not the communicator's");
   return bind(ctx);
@@ -283,8 +295,21 @@ extern "C" int gf_knn_exchange_group(int32_t n, gf_comm* const* comms, gf_ctx* c
   if (n < 1 || !comms || !ctxs || !records || !merged) return GF_ERR_ARG;
   const size_t rb = gf_knn_result_bytes(k);
   int st;
+  // Everything that can fail is checked BEFORE ncclGroupStart: the group must hold
+  // one all-gather for every rank of ONE clique -- issued for a subset, the launched kernels
+  // would wait forever for peers that never join, and the next sync would hang the device.
+  std::vector<uint8_t> seen((size_t)n, 0);
   for (int32_t i = 0; i < n; ++i) {
+    if (!comms[i] || !ctxs[i]) return GF_ERR_ARG;
     if ((st = exchange_args_ok(comms[i], ctxs[i], k, records[i], nwin, merged[i], "gf_knn_exchange_group"))) return st;
+    const gf_comm* c = comms[i];
+    const bool whole = c->nranks == n && (n == 1 || (c->clique != 0 && c->clique == comms[0]->clique)) &&
+                       c->rank >= 0 && c->rank < n && !seen[(size_t)c->rank];
+    if (!whole)
+      return set_err(ctxs[i], GF_ERR_ARG,
+                     "gf_knn_exchange_group: the communicators must be one whole gf_comm_create_all clique, "
+                     "each rank once");
+    seen[(size_t)c->rank] = 1;
     if ((st = comm_buffer(comms[i], ctxs[i], &comms[i]->gather, &comms[i]->gather_bytes,
                           rb * (size_t)nwin * (size_t)comms[i]->nranks)))
       return st;
@@ -296,14 +321,22 @@ extern "C" int gf_knn_exchange_group(int32_t n, gf_comm* const* comms, gf_ctx* c
   if ((st = nccl_check(comms[0], ctxs[0], R->GroupStart(), "ncclGroupStart"))) return st;
   int first_err = GF_OK;
   for (int32_t i = 0; i < n && !first_err; ++i) {
-    if (bind(ctxs[i])) { first_err = GF_ERR_HIP; break; }
+    if (hipSetDevice(ctxs[i]->device) != hipSuccess) { first_err = hip_err(ctxs[i], hipErrorInvalidDevice, "hipSetDevice"); break; }
     first_err = nccl_check(comms[i], ctxs[i],
                            R->AllGather(records[i], comms[i]->gather, rb * (size_t)nwin, ncclUint8, comms[i]->comm,
                                         ctxs[i]->stream),
                            "ncclAllGather");
   }
-  if ((st = nccl_check(comms[0], ctxs[0], R->GroupEnd(), "ncclGroupEnd"))) return st;
-  if (first_err) return first_err;
+  const int end_err = nccl_check(comms[0], ctxs[0], R->GroupEnd(), "ncclGroupEnd");
+  if (first_err || end_err) {
+    // a partial group may have launched some all-gathers whose peers never arrive: abort the
+    // whole clique so its kernels are torn down instead of spinning (every later call refused)
+    for (int32_t i = 0; i < n; ++i) {
+      if (!comms[i]->aborted) R->CommAbort(comms[i]->comm);
+      comms[i]->aborted = true;
+    }
+    return first_err ? first_err : end_err;
+  }
   for (int32_t i = 0; i < n; ++i)
     if ((st = gf_knn_merge_dev_batch(ctxs[i], k, comms[i]->gather, comms[i]->nranks, nwin, merge_layout(comms[i]),
                                      merged[i])))

@@ -205,8 +205,10 @@ __device__ __forceinline__ int32_t clamp_key(int32_t c, int32_t qn) { return (c 
 // in v, identical for both sides and gives every sub-cell a width > r serves (see the fine path
 // below); this one is within a few ulps of the cell split into f equal parts.
 __device__ __forceinline__ int32_t join_sub(double v, double mn, double cl, int32_t c, double fs, int32_t f) {
-  const int32_t j = jint((v - (mn + (double)c * cl)) * fs);
-  return j < 0 ? 0 : (j > f - 1 ? f - 1 : j);
+  // == clamp(jint(s), 0, f - 1): s < 1 (NaN included) -> 0, s >= f - 1 (+inf included) -> f - 1,
+  // else the truncation (in range) -- compares and one conversion, no saturation cases
+  const double s = (v - (mn + (double)c * cl)) * fs;
+  return !(s >= 1.0) ? 0 : (s >= (double)(f - 1) ? f - 1 : (int32_t)s);
 }
 
 // q_off index of a query point: its sub-cell (f sub-rows x f sub-columns per clamped cell) in

@@ -1577,9 +1577,12 @@ __global__ __launch_bounds__(kStrMergeT) void knn_merge_strings_kernel(int32_t k
       const gf_knn_header* h = (const gf_knn_header*)rec(r);
       s_off[r] = off;
       off += h->status == 0 ? h->n : 0;
-      // a flagged input (its rank's window needs the exact re-evaluation) or Strings that did not
-      // fit: the merged record holds other ranks' keys, so no caller could re-evaluate it -- 2
-      if (h->status != 0 || side_of(rec(r), k)->status != 0) st = GF_KNN_STATUS_FOREIGN_KEYS;
+      // a flagged input (status 1: its rank's window needs the exact re-evaluation) keeps the
+      // merged record flagged (1), as gf_knn_merge_dev does, so every rank re-evaluates its
+      // shard exactly and exchanges again; Strings that did not fit a sidecar cannot be merged
+      // by String at all -- 2 (GF_KNN_STATUS_FOREIGN_KEYS), which wins over 1
+      if (side_of(rec(r), k)->status != 0) st = GF_KNN_STATUS_FOREIGN_KEYS;
+      else if (h->status != 0 && st == 0) st = h->status;
     }
     s_off[nrec] = off;
     s_status = st;

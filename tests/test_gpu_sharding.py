@@ -275,6 +275,18 @@ def test_knn_merge_strings_across_dictionaries(sf, oracle_mod, k):
                                           out2.data_ptr()), ctx.handle, "merge strings small")
     st, strs, _, _ = sharding.decode_string_record(out2[0].cpu().numpy().tobytes(), k, 8)
     assert st == _lib.KNN_STATUS_FOREIGN_KEYS and strs == []
+    # a flagged input record (status 1) keeps the merged record flagged -- retryable by an exact
+    # re-evaluation and a second exchange, as gf_knn_merge_dev does -- while the
+    # other windows merge as before
+    flagged = ext.clone()
+    flagged[0, :4] = torch.tensor([1, 0, 0, 0], dtype=torch.uint8)  # shard 0, window 0: status 1
+    out3 = torch.zeros_like(out)
+    _lib.check(L.gf_knn_merge_dev_strings(ctx.handle, k, cap, flagged.data_ptr(), S, W, _lib.GF_MERGE_SHARD_MAJOR,
+                                          out3.data_ptr()), ctx.handle, "merge strings flagged")
+    st, strs, _, _ = sharding.decode_string_record(out3[0].cpu().numpy().tobytes(), k, cap)
+    assert st == 1 and strs == []
+    if W > 1:
+        np.testing.assert_array_equal(out3[1:].cpu().numpy(), out[1:].cpu().numpy())
 
 
 @pytest.mark.parametrize("nb", [1, 3, 8])

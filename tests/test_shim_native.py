@@ -554,3 +554,265 @@ def test_geojson_parse(shim, ctx, oracle_mod, date_fmt, tz, vl, props):
     np.testing.assert_array_equal(t, et)
     null = np.iinfo(np.int64).max  # GF_OBJID_NULL: the reference's null objID
     assert [None if k == null else s for k, s in zip(o.tolist(), _decode(shim, ctx, o))] == eo
+
+
+# ---- the Java window functions: their native call order, replayed through the C core ---------
+# Per class and method, the GeoFlinkHip natives in source order ("intern" = GeoFlinkHip.intern, the
+# Java helper over objidIntern that HipColumns.fill calls for objID columns).  Conditional calls
+# are listed as they appear in the source; GPU_SKIPPED names the ones the GPU replay does not take.
+JAVA_SEQ = {
+    "HipKnnWindowFunction": {"open": ["ctxCreate", "knnPlan"], "grow": ["pinnedFree", "pinnedBuffer"],
+                             "apply": ["intern", "knnWindow"],
+                             "close": ["pinnedFree", "knnPlanDestroy", "ctxDestroy"]},
+    "HipRangeWindowFunction": {"open": ["ctxCreate", "rangePlan", "rangePolygonPlan"],
+                               "apply": ["rangeWindow", "rangeWindow", "rangeWindowMulti"],
+                               "close": ["rangePlanDestroy", "ctxDestroy"]},
+    "HipJoinFunction": {"open": ["ctxCreate"], "coGroup": ["joinWindow"], "close": ["ctxDestroy"]},
+    "HipPolygonJoinFunction": {"open": ["ctxCreate"], "coGroup": ["polygonJoinWindow"], "close": ["ctxDestroy"]},
+    "HipShardedKnnFunction": {"open": ["ctxCreate", "knnPlan", "commUniqueId", "commCreate", "knnShardedBegin"],
+                              "apply": ["intern", "knnShardedEnqueue", "knnShardedResult"],
+                              "close": ["commDestroy", "knnPlanDestroy", "ctxDestroy"]},
+    "CommRendezvous": {"create": ["commUniqueId", "commCreate"]},
+}
+# helpers that only read state (not part of a native's action sequence)
+_SHIM_QUERIES = {"shim_last_error", "shim_knn_k", "shim_sliding_plan"}
+
+
+def _java_methods(cls):
+    """method name -> its body, for the class's top-level methods (brace matching)"""
+    src = re.sub(r"//[^\n]*|/\*.*?\*/", "", _read(os.path.join("GeoFlink", "native_", cls + ".java")), flags=re.S)
+    out = {}
+    for m in re.finditer(r"\n  (?:public |private |protected |static |final )*[\w<>\[\], ]+ (\w+)\([^)]*\)[^{;]*\{", src):
+        depth, i = 1, m.end()
+        while depth:
+            depth += {"{": 1, "}": -1}.get(src[i], 0)
+            i += 1
+        out[m.group(1)] = src[m.end():i]
+    return src, out
+
+
+def _java_native_calls(cls, method):
+    src, methods = _java_methods(cls)
+    objid_cols = "new HipColumns(true)" in src
+    calls = []
+    for m in re.finditer(r"GeoFlinkHip\.(\w+)\(|\b\w+\.fill\(|CommRendezvous\.create\(", methods[method]):
+        if m.group(1):
+            calls.append(m.group(1))
+        elif m.group(0).startswith("CommRendezvous"):
+            calls.extend(JAVA_SEQ["CommRendezvous"]["create"])
+        elif objid_cols:
+            calls.append("intern")
+    return calls
+
+
+def _jni_shim_map():
+    """native -> the shim_* functions its JNI wrapper calls, in order ("intern" -> objidIntern's)"""
+    src = _read("geoflink_jni.c")
+    out = {}
+    for m in re.finditer(r"Java_GeoFlink_native_1_GeoFlinkHip_(\w+)\(JNIEnv\* env[^{]*\{", src):
+        depth, i = 1, m.end()
+        while depth:
+            depth += {"{": 1, "}": -1}.get(src[i], 0)
+            i += 1
+        out[m.group(1)] = [f for f in re.findall(r"\b(shim_\w+)\(", src[m.end():i]) if f not in _SHIM_QUERIES]
+    out["intern"] = out["objidIntern"]
+    return out
+
+
+def test_java_functions_call_natives_in_order():
+    """Every Java window function's methods call the natives in the order JAVA_SEQ lists (the
+    order the GPU replay below drives through the C core), and every native exists with a JNI
+    wrapper that calls the shim."""
+    jn, jmap = _java_natives(), _jni_shim_map()
+    for cls, methods in JAVA_SEQ.items():
+        if cls == "CommRendezvous":
+            continue
+        for method, seq in methods.items():
+            assert _java_native_calls(cls, method) == seq, (cls, method, _java_native_calls(cls, method))
+            for nat in seq:
+                assert nat == "intern" or nat in jn, nat
+                assert jmap[nat], f"{nat}: its JNI wrapper calls no shim function"
+    assert _java_native_calls("CommRendezvous", "create") == JAVA_SEQ["CommRendezvous"]["create"]
+    # the reference's callers are range queries (StreamingJob.java:260,270, MN_Q1.java:63,
+    # Q1_HighRisk.java:74): the range function exists for point and polygon query sets
+    src, _ = _java_methods("HipRangeWindowFunction")
+    assert "Set<Point> queryPoints" in src and "forPolygons(" in src and "Set<Polygon> polygons" in src
+
+
+class _Recorder:
+    """the shim CDLL, recording the shim_* functions called (queries excluded)"""
+
+    def __init__(self, lib):
+        self._lib, self.calls = lib, []
+
+    def __getattr__(self, name):
+        f = getattr(self._lib, name)
+        if name in _SHIM_QUERIES:
+            return f
+
+        def rec(*a):
+            self.calls.append(name)
+            return f(*a)
+        return rec
+
+
+def _expect(cls, method, skip=()):
+    jmap = _jni_shim_map()
+    seq = [n for n in JAVA_SEQ[cls][method] if n not in skip]
+    return [f for n in seq for f in jmap[n]]
+
+
+def _intern(S, ctx, keys_str):
+    offs = np.zeros(len(keys_str) + 1, np.int64)
+    offs[1:] = np.cumsum([len(s) for s in keys_str])
+    keys = np.zeros(len(keys_str), np.int64)
+    _ok(S, ctx, S.shim_objid_intern(ctx, b"".join(keys_str), _a(offs), len(keys_str), _a(keys)), "intern")
+    return keys
+
+
+@pytest.mark.gpu
+def test_java_call_sequence_range(shim, oracle_mod):
+    """HipRangeWindowFunction, point queries, approximate with |Q| = 3 (the multiplicity list) and
+    exact: open / two windows / close replayed in the Java order; the emitted multiset == the
+    oracle's (PointPointRangeQuery.java:150-186, the reference's per-query-point emission)."""
+    g, og = grid(100), oracle_mod.grid(100, *BEIJING)
+    qx = np.array([QPOINT[0], 116.9, 117.3]); qy = np.array([QPOINT[1], 40.2, 40.9])
+    for approx in (1, 0):
+        S = _Recorder(shim)
+        ctx, plan = P(), P()
+        assert S.shim_ctx_create(0, C.byref(ctx)) == 0
+        _ok(S, ctx, S.shim_range_plan(ctx, C.byref(g), _a(qx), _a(qy), 3, 0.05, approx, C.byref(plan)), "plan")
+        assert S.calls == _expect("HipRangeWindowFunction", "open", skip=("rangePolygonPlan",))
+        for seed, n in ((21, 600_000), (22, 3000)):
+            S.calls.clear()
+            x, y = oracle_mod.java_random_points(seed, n, *BEIJING)
+            st, out, cnt = _range(S, plan, x, y, max(1, n // 8))  # the first, too-small buffer
+            if st == -2:
+                st, out, cnt = _range(S, plan, x, y, cnt)
+            _ok(S, ctx, st, "rangeWindow")
+            multi = np.zeros(max(cnt, 1), np.int32); mc = i64()
+            _ok(S, ctx, S.shim_range_window_multi(plan, _a(multi), len(multi), C.byref(mc)), "rangeWindowMulti")
+            # rangeWindow, its retry with a large enough buffer only when the first was too small
+            exp_calls = _expect("HipRangeWindowFunction", "apply")
+            assert S.calls == (exp_calls if cnt > max(1, n // 8) else exp_calls[1:]), S.calls
+            emitted = np.repeat(out[:cnt].astype(np.int64),
+                                np.where(np.isin(out[:cnt], multi[:mc.value]), 3, 1))
+            exp = oracle_mod.range_pp(og, x, y, qx, qy, 0.05, approximate=bool(approx))
+            np.testing.assert_array_equal(emitted, np.sort(exp))
+            assert (mc.value > 0) == bool(approx)
+        S.calls.clear()
+        S.shim_range_destroy(plan)
+        S.shim_ctx_destroy(ctx)
+        assert S.calls == _expect("HipRangeWindowFunction", "close")
+
+
+@pytest.mark.gpu
+def test_java_call_sequence_joins(shim, oracle_mod):
+    """HipJoinFunction / HipPolygonJoinFunction: open, one coGroup, close in the Java order; pairs
+    == the oracle's (PointPointJoinQuery.java:148-182, PointPolygonJoinQuery.java:154-213)."""
+    g, og = grid(100), oracle_mod.grid(100, *BEIJING)
+    ox, oy = oracle_mod.java_random_points(31, 300_000, *BEIJING)
+    qx, qy = oracle_mod.java_random_points(32, 30_000, *BEIJING)
+    OP = oracle_mod.Polygons(oracle_mod.generate_query_polygons(25, BEIJING[0], BEIJING[2], BEIJING[1], BEIJING[3]))
+    GP = gpolys(OP)
+    for cls in ("HipJoinFunction", "HipPolygonJoinFunction"):
+        S = _Recorder(shim)
+        ctx = P()
+        assert S.shim_ctx_create(0, C.byref(ctx)) == 0
+        assert S.calls == _expect(cls, "open")
+        S.calls.clear()
+        pairs, m = P(), i64()
+        if cls == "HipJoinFunction":
+            _ok(S, ctx, S.shim_join_window(ctx, C.byref(g), C.byref(g), _a(ox), _a(oy), len(ox), _a(qx), _a(qy),
+                                           len(qx), 0.01, 0, C.byref(pairs), C.byref(m)), "joinWindow")
+            est, exp = oracle_mod.join_pp(og, og, ox, oy, qx, qy, 0.01)
+        else:
+            _ok(S, ctx, S.shim_polygon_join_window(ctx, C.byref(g), _a(ox), _a(oy), len(ox), C.byref(GP), 0.005, 0,
+                                                   C.byref(pairs), C.byref(m)), "polygonJoinWindow")
+            exp = oracle_mod.join_ppoly(og, og, ox, oy, OP, 0.005)
+        assert S.calls == _expect(cls, "coGroup")
+        np.testing.assert_array_equal(_pairs(pairs, m.value), _sorted(exp))
+        S.calls.clear()
+        S.shim_ctx_destroy(ctx)
+        assert S.calls == _expect(cls, "close")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("batch", [1, 3])
+def test_java_call_sequence_sharded_knn(shim, oracle_mod, batch):
+    """HipShardedKnnFunction on a one-rank communicator (CommRendezvous: unique id + commCreate):
+    windows enqueued with String objIDs interned per window, their batch exchanged by String with
+    its last window, every window's result read -- == the oracle's kNN of the window (idx global:
+    rank << 32 + position; all owned on one rank); a window of 1.1M points stacked on the query
+    point overflows the candidate buffer, so its result takes the flagged path (exact
+    re-evaluation and a second exchange).  Then the slot-reuse guard and the flush."""
+    g, og = grid(500), oracle_mod.grid(500, *BEIJING)
+    S = _Recorder(shim)
+    S._lib.shim_knn_sharded_begin.argtypes = [P, P, i32, i64]
+    S._lib.shim_knn_sharded_enqueue.argtypes = [P, P, P, P, i64, i64, P]
+    S._lib.shim_knn_sharded_flush.argtypes = [P]
+    S._lib.shim_knn_sharded_result.argtypes = [P, i64, P, P, P, P]
+    ctx, plan, comm = P(), P(), P()
+    k, base = 50, 0  # rank 0
+    assert S.shim_ctx_create(0, C.byref(ctx)) == 0
+    _ok(S, ctx, S.shim_knn_plan(ctx, C.byref(g), QPOINT[0], QPOINT[1], 0.5, k, C.byref(plan)), "plan")
+    uid = (C.c_uint8 * 128)()
+    assert S.shim_comm_unique_id(uid) == 0
+    _ok(S, ctx, S.shim_comm_create(ctx, uid, 1, 0, C.byref(comm)), "commCreate")
+    _ok(S, ctx, S.shim_knn_sharded_begin(plan, comm, batch, 32 * k + 64), "begin")
+    assert S.calls == _expect("HipShardedKnnFunction", "open")  # (rank 0 of CommRendezvous)
+    try:
+        pending, wins = [], {}
+        rng = np.random.default_rng(5)
+        specs = [(41, 300_000, 0), (42, 250_000, 1_100_000), (43, 200_000, 0), (44, 5, 0), (45, 350_000, 0), (46, 0, 0)]
+        for w, (seed, n, stacked) in enumerate(specs):
+            x, y = oracle_mod.java_random_points(seed, n, *BEIJING)
+            if stacked:
+                x = np.concatenate([x, np.full(stacked, QPOINT[0])]); y = np.concatenate([y, np.full(stacked, QPOINT[1])])
+            ids = (rng.permutation(len(x)) % max(1, len(x) * 2 // 3)).astype(np.int64)
+            strs = [b"v%d" % i if i % 5 else b"%d" % i for i in ids.tolist()]
+            S.calls.clear()
+            keys = _intern(S, ctx, strs)
+            t = i64()
+            _ok(S, ctx, S.shim_knn_sharded_enqueue(plan, _a(x), _a(y), _a(keys), len(x), base, C.byref(t)), "enqueue")
+            assert t.value == w
+            wins[w] = (x, y, ids)
+            pending.append(w)
+            if (w + 1) % batch:
+                assert S.calls == _expect("HipShardedKnnFunction", "apply")[:2]
+                continue
+            for tw in pending:
+                od, oi, ow, m = np.zeros(k), np.zeros(k, np.int64), np.zeros(k, np.int32), i32()
+                _ok(S, ctx, S.shim_knn_sharded_result(plan, tw, _a(od), _a(oi), _a(ow), C.byref(m)), "result")
+                wx, wy, wid = wins.pop(tw)
+                est, eo, ed, ei = oracle_mod.knn(og, wx, wy, wid, *QPOINT, 0.5, k)
+                assert est == 0 and m.value == len(eo)
+                np.testing.assert_array_equal(od[:m.value].view(np.int64), ed.view(np.int64))
+                np.testing.assert_array_equal(wid[oi[:m.value] - base], eo)   # the window's own Points
+                assert ow[:m.value].all()
+            assert S.calls == _expect("HipShardedKnnFunction", "apply")[:2] + \
+                ["shim_knn_sharded_result"] * len(pending)
+            pending.clear()
+        if batch > 1:  # an unread window blocks its slot 2B tickets later; a flush exchanges a partial batch
+            x, y = oracle_mod.java_random_points(50, 1000, *BEIJING)
+            keys = np.arange(1000, dtype=np.int64)
+            t = i64()
+            for _ in range(2 * batch):
+                _ok(S, ctx, S.shim_knn_sharded_enqueue(plan, _a(x), _a(y), _a(keys), 1000, base, C.byref(t)), "fill")
+            assert S.shim_knn_sharded_enqueue(plan, _a(x), _a(y), _a(keys), 1000, base, C.byref(t)) == -1
+            first = t.value - 2 * batch + 1
+            od, oi, ow, m = np.zeros(k), np.zeros(k, np.int64), np.zeros(k, np.int32), i32()
+            for tw in range(first, first + 2 * batch):
+                _ok(S, ctx, S.shim_knn_sharded_result(plan, tw, _a(od), _a(oi), _a(ow), C.byref(m)), "drain")
+            _ok(S, ctx, S.shim_knn_sharded_enqueue(plan, _a(x), _a(y), _a(keys), 1000, base, C.byref(t)), "partial")
+            assert S.shim_knn_sharded_result(plan, t.value, _a(od), _a(oi), _a(ow), C.byref(m)) == -1  # not exchanged
+            _ok(S, ctx, S.shim_knn_sharded_flush(plan), "flush")
+            _ok(S, ctx, S.shim_knn_sharded_result(plan, t.value, _a(od), _a(oi), _a(ow), C.byref(m)), "after flush")
+            est, eo, ed, ei = oracle_mod.knn(og, x, y, keys, *QPOINT, 0.5, k)
+            np.testing.assert_array_equal(od[:m.value].view(np.int64), ed.view(np.int64))
+    finally:
+        S.calls.clear()
+        S.shim_comm_destroy(comm)
+        S.shim_knn_destroy(plan)
+        S.shim_ctx_destroy(ctx)
+        assert S.calls == _expect("HipShardedKnnFunction", "close")
