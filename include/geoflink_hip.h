@@ -141,12 +141,23 @@ const char* gf_ctx_last_error(gf_ctx* ctx);
  * GF_FLAG_GEOJSON_WALK: 1 = gf_geojson_parse takes the member-by-member walk on every line
  * (no one-pass locator); the results are the same.
  * GF_FLAG_JOIN_STREAM: 1 = gf_join_pp's fine path buckets only the query side and streams the
- * ordinary points in input order (an experiment the default path is measured against). */
+ * ordinary points in input order (an experiment the default path is measured against).
+ * GF_FLAG_GEOJSON_LANE: 1 = gf_geojson_parse locates members one line per lane (the r05 locator)
+ * instead of the wave-per-line scan; the results are the same.
+ * GF_FLAG_GEOJSON_CHECK: 1 = gf_geojson_parse runs the wave scan AND the lane locator on every
+ * staged line and counts their differences (gf_geojson_check_counts); results as the default. */
 #define GF_FLAG_JOIN_LEGACY 1
 #define GF_FLAG_JOIN_COARSE 2
 #define GF_FLAG_GEOJSON_WALK 4
 #define GF_FLAG_JOIN_STREAM 8
+#define GF_FLAG_GEOJSON_LANE 16
+#define GF_FLAG_GEOJSON_CHECK 32
 int gf_ctx_set_flag(gf_ctx* ctx, int flag, int value);
+/* GF_FLAG_GEOJSON_CHECK's counts since the last read (then zeroed), after a sync: out[0] lines
+ * both passed with the same member notes, out[1] the wave scan passed and the lane locator did not,
+ * out[2] both passed with different notes, out[3] the lane locator passed and the wave scan did not
+ * (a byte >= 0x80 sends a line to the walk).  out[1] and out[2] are defects. */
+int gf_geojson_check_counts(gf_ctx* ctx, unsigned long long out[4]);
 
 /* Record HIP events around launches of the kernels in `mask` (bit 1 << GF_K_*; 0 = off). */
 int         gf_ctx_set_timing(gf_ctx* ctx, int mask);
@@ -227,6 +238,10 @@ int  gf_range_plan_stats(const gf_range_plan* plan, int64_t* none_cells, int64_t
  * with the span prefilter (the scan only rules out points outside the class spans; every other
  * point is classified by the table at the block's end) -- table modes. */
 int  gf_range_plan_set_tuning(gf_range_plan* plan, int32_t scan_blocks, int32_t defer_mode);
+/* Testing: the deferred candidate tests at each scan block's end run on the first `lanes` lanes of
+ * every wave only (1..64; 0 = all, the default).  Results are identical for any value: the drain
+ * takes its points from a block cursor with whatever lanes are active (tests/test_gpu_parity.py). */
+int  gf_range_plan_set_drain_lanes(gf_range_plan* plan, int32_t lanes);
 /* Sync: selection bitmap -> ascending point indices (device uint32[cap]). */
 int  gf_bitmap_to_indices(gf_ctx* ctx, const uint64_t* bitmap, int64_t n, uint32_t* idx,
                           int64_t cap, int64_t* count);

@@ -34,6 +34,8 @@ METRIC_HYPOT = 1
 FLAG_JOIN_LEGACY = 1
 FLAG_JOIN_COARSE = 2
 FLAG_GEOJSON_WALK = 4
+FLAG_GEOJSON_LANE = 16
+FLAG_GEOJSON_CHECK = 32
 FLAG_JOIN_STREAM = 8
 (K_KNN_SCAN, K_KNN_SAMPLE, K_KNN_SELECT, K_RANGE_SCAN, K_ASSIGN, K_JOIN_PROBE, K_RANGE_TEST, K_JOIN_BUCKET,
  K_KNN_MERGE, K_CSV_PARSE, K_BUCKET, K_JOIN_COMPACT) = range(12)
@@ -42,9 +44,10 @@ FLAG_JOIN_STREAM = 8
 EXPORTS = [
     "gf_abi_version", "gf_build_info", "gf_build_is_product", "gf_status_string", "gf_device_count", "gf_ctx_create", "gf_ctx_destroy",
     "gf_ctx_set_stream", "gf_ctx_stream", "gf_ctx_synchronize", "gf_ctx_join", "gf_ctx_fork", "gf_ctx_last_error", "gf_ctx_set_timing", "gf_ctx_set_timing_period", "gf_ctx_set_flag",
+    "gf_geojson_check_counts",
     "gf_ctx_timing", "gf_grid_make", "gf_grid_layers", "gf_cell_of", "gf_format_cell_id", "gf_parse_cell_id",
     "gf_assign_cells", "gf_bucket_by_cell", "gf_range_pp_plan_create", "gf_range_ppoly_plan_create",
-    "gf_range_plan_destroy", "gf_range_run", "gf_range_run_batch", "gf_range_plan_stats", "gf_range_plan_set_tuning", "gf_bitmap_to_indices", "gf_bitmap_to_indices_async", "gf_knn_pp_plan_create",
+    "gf_range_plan_destroy", "gf_range_run", "gf_range_run_batch", "gf_range_plan_stats", "gf_range_plan_set_tuning", "gf_range_plan_set_drain_lanes", "gf_bitmap_to_indices", "gf_bitmap_to_indices_async", "gf_knn_pp_plan_create",
     "gf_knn_ppoly_plan_create",
     "gf_knn_plan_destroy", "gf_knn_plan_set_capacity", "gf_knn_plan_set_index_base", "gf_knn_plan_set_tuning", "gf_knn_plan_set_hint", "gf_knn_plan_set_pipeline", "gf_knn_plan_flush",
     "gf_knn_result_bytes", "gf_knn_enqueue",
@@ -135,6 +138,7 @@ def lib():
             "gf_ctx_last_error": ([P], C.c_char_p),
             "gf_ctx_set_timing": ([P, C.c_int], C.c_int),
             "gf_ctx_set_flag": ([P, C.c_int, C.c_int], C.c_int),
+            "gf_geojson_check_counts": ([P, P], C.c_int),
             "gf_ctx_set_timing_period": ([P, C.c_int], C.c_int),
             "gf_ctx_timing": ([P, C.c_int, pd, pi64], C.c_int),
             "gf_grid_make": ([i32, d, d, d, d, C.POINTER(GfGrid)], C.c_int),
@@ -153,6 +157,7 @@ def lib():
                                     C.POINTER(P)], C.c_int),
             "gf_range_plan_stats": ([P, pi64, pi64, pi64, pi64], C.c_int),
             "gf_range_plan_set_tuning": ([P, C.c_int32, C.c_int32], C.c_int),
+            "gf_range_plan_set_drain_lanes": ([P, i32], C.c_int),
             "gf_bitmap_to_indices": ([P, P, i64, P, i64, pi64], C.c_int),
             "gf_bitmap_to_indices_async": ([P, P, i64, P, i64, P], C.c_int),
             "gf_knn_pp_plan_create": ([P, C.POINTER(GfGrid), d, d, d, i32, C.c_int, C.POINTER(P)], C.c_int),

@@ -324,6 +324,7 @@ extern "C" void gf_ctx_destroy(gf_ctx* ctx) {
   if (ctx->csv_head) hipHostFree(ctx->csv_head);
   if (ctx->join_hist) hipFree(ctx->join_hist);
   if (ctx->join_ovf) hipFree(ctx->join_ovf);
+  if (ctx->geojson_check) hipFree(ctx->geojson_check);
   for (auto& e : ctx->pending) { hipEventDestroy(e.a); hipEventDestroy(e.b); }
   for (auto e : ctx->pool) hipEventDestroy(e);
   if (ctx->scratch) hipFree(ctx->scratch);
@@ -394,7 +395,29 @@ extern "C" int gf_ctx_set_flag(gf_ctx* ctx, int flag, int value) {
   if (flag == GF_FLAG_JOIN_COARSE) { ctx->join_coarse = value != 0; return GF_OK; }
   if (flag == GF_FLAG_GEOJSON_WALK) { ctx->geojson_walk = value != 0; return GF_OK; }
   if (flag == GF_FLAG_JOIN_STREAM) { ctx->join_stream = value != 0; return GF_OK; }
+  if (flag == GF_FLAG_GEOJSON_LANE) { ctx->geojson_lane = value != 0; return GF_OK; }
+  if (flag == GF_FLAG_GEOJSON_CHECK) {
+    if (value && !ctx->geojson_check) {
+      GF_HIP_CHECK(ctx, hipMalloc(&ctx->geojson_check, 4 * sizeof(unsigned long long)));
+      GF_HIP_CHECK(ctx, hipMemsetAsync(ctx->geojson_check, 0, 4 * sizeof(unsigned long long), ctx->stream));
+    } else if (!value && ctx->geojson_check) {
+      GF_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+      GF_HIP_CHECK(ctx, hipFree(ctx->geojson_check));
+      ctx->geojson_check = nullptr;
+    }
+    return GF_OK;
+  }
   return set_err(ctx, GF_ERR_ARG, "gf_ctx_set_flag: unknown flag");
+}
+
+extern "C" int gf_geojson_check_counts(gf_ctx* ctx, unsigned long long out[4]) {
+  if (!ctx || !out) return GF_ERR_ARG;
+  if (!ctx->geojson_check) return set_err(ctx, GF_ERR_ARG, "gf_geojson_check_counts: GF_FLAG_GEOJSON_CHECK is off");
+  GF_HIP_CHECK(ctx, hipMemcpyAsync(out, ctx->geojson_check, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                                   ctx->stream));
+  GF_HIP_CHECK(ctx, hipMemsetAsync(ctx->geojson_check, 0, 4 * sizeof(unsigned long long), ctx->stream));
+  GF_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
+  return GF_OK;
 }
 
 extern "C" int gf_ctx_set_timing(gf_ctx* ctx, int mask) {
@@ -510,7 +533,7 @@ static int bucket_rows(gf_ctx* ctx, const gf_grid* g, const gf_points* pts, uint
   const int64_t ub = n / kRowSeg + g->n + 2;  // segments <= sum over rows of (size / seg + 1)
   const int64_t matB = D * ub;
   Arena ar;
-  size_t o_k0 = ar.take<uint32_t>(n), o_k1 = ar.take<uint32_t>(n), o_v1 = ar.take<uint32_t>(n);
+  size_t o_k0 = ar.take<uint32_t>(n), o_k1 = ar.take<uint16_t>(n), o_v1 = ar.take<uint32_t>(n);
   size_t o_ma = ar.take<uint32_t>(matA), o_msa = ar.take<uint32_t>(matA + 1);
   size_t o_mb = ar.take<uint32_t>(matB), o_msb = ar.take<uint32_t>(matB + 1);
   int st = 0;
@@ -534,12 +557,16 @@ static int bucket_rows(gf_ctx* ctx, const gf_grid* g, const gf_points* pts, uint
   ctx->expand_base += (unsigned long long)scan1_blocks(matA);
   a.kin = U32(o_k0);
   a.vin = nullptr;
-  a.kout = U32(o_k1);
+  a.kout = nullptr;
+  a.kout16 = (uint16_t*)(base + o_k1);  // the columns (u16): the row is the position's
   a.vout = U32(o_v1);
   GF_HIP_CHECK(ctx, launch_radix(ctx, 1, a, blocks));
-  // pass B: per row segment column histograms, one scan, stable scatter by column (perm only)
+  // pass B: per row segment column histograms (one-segment rows count their own columns in the
+  // scatter), one scan, stable scatter by column (perm only)
   RadixArgs b = a;
-  b.kin = U32(o_k1);
+  b.kin = nullptr;
+  b.kin16 = (const uint16_t*)(base + o_k1);
+  b.kout16 = nullptr;
   b.vin = U32(o_v1);
   b.kout = nullptr;
   b.vout = perm;
@@ -1131,6 +1158,7 @@ int ensure_queue(gf_range_plan* P, RangeArgs& a, int blocks, bool with_counts) {
   gf_ctx* ctx = P->ctx;
   const int64_t tstride = (int64_t)blocks * kBlock * 2;
   a.seg_cap = 2 * kBlock * ((a.n + tstride - 1) / tstride);
+  a.drain_lanes = P->drain_lanes;
   const int64_t need = a.seg_cap * blocks;
   if (P->queue_cap < need || (with_counts && !P->jecnt)) {
     GF_HIP_CHECK(ctx, hipStreamSynchronize(ctx->stream));
@@ -1312,6 +1340,12 @@ extern "C" int gf_range_plan_set_tuning(gf_range_plan* P, int32_t scan_blocks, i
     return GF_ERR_ARG;
   P->scan_blocks = scan_blocks;
   P->defer_mode = defer_mode;
+  return GF_OK;
+}
+
+extern "C" int gf_range_plan_set_drain_lanes(gf_range_plan* P, int32_t lanes) {
+  if (!P || lanes < 0 || lanes > 64) return GF_ERR_ARG;
+  P->drain_lanes = lanes;
   return GF_OK;
 }
 

@@ -15,6 +15,11 @@
 
 using namespace gf;
 
+// staging sizes of a context's first chunk (no mean line length yet): a GeoJSON Feature record
+// (the bench's generated lines average 189 B; the reference's documented example line ~150 B) and
+// a CSV point line (~55 B)
+constexpr int64_t kGeoMeanLineDefault = 192, kCsvMeanLineDefault = 64;
+
 extern "C" int gf_csv_parse(gf_ctx* ctx, const char* text, int64_t len, const gf_csv_schema* sc, const gf_grid* g,
                             double* x, double* y, int64_t* objID, int64_t* ts, int32_t* cx, int32_t* cy, int64_t cap,
                             int64_t* n_out, int64_t* bad_line, int32_t* bad_kind) {
@@ -74,8 +79,12 @@ static int parse_text_lines(gf_ctx* ctx, gf_objid_dict* dict, const char* text, 
     a.nl_cap = nl_cap;
     a.cap = cap;
     a.grid_lines = grid_lines;
+    // LDS staging per block from the mean line length: the last call's on this context, else a
+    // per-format default (len / grid_lines undercounts it by the index's 1-line-per-32-B
+    // sizing, so a cold context's first chunk had ~32 B "lines", a 24 KB staging area, and every
+    // GeoJSON block fell back to the per-byte global-memory walk)
     const int64_t last_mean = ctx->csv_mean_line[proto.format == 1];
-    a.mean_line = last_mean > 0 ? last_mean : (grid_lines > 0 ? (len + grid_lines - 1) / grid_lines : len);
+    a.mean_line = last_mean > 0 ? last_mean : (proto.format == 1 ? kGeoMeanLineDefault : kCsvMeanLineDefault);
     a.head = (CsvHead*)ctx->csv_head;
     a.x = x; a.y = y; a.objID = objID; a.ts = ts; a.cx = cx; a.cy = cy;
     if (g) { a.minX = g->minX; a.minY = g->minY; a.cl = g->cellLength; }
@@ -156,6 +165,8 @@ extern "C" int gf_geojson_parse(gf_ctx* ctx, gf_objid_dict* dict, const char* te
   }
   a.date_fmt = sc->date_format;
   a.geo_fast = !ctx->geojson_walk;
+  a.geo_wave = !ctx->geojson_walk && !ctx->geojson_lane;
+  a.geo_check = ctx->geojson_check;
   a.value_lines = sc->value_lines;
   a.tz_off_ms = (int64_t)sc->tz_offset_minutes * 60000;
   return parse_text_lines(ctx, dict, text, len, a, g, x, y, objID, ts, cx, cy, cap, n_out, bad_line, bad_kind);

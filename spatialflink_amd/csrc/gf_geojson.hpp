@@ -854,8 +854,8 @@ GF_DHD inline void geo_word(GeoLoc& L, int32_t w, int32_t o0, int32_t o1, const 
 // accumulator while it is read, and its closing quote compares (length, accumulator) with the
 // looked-up names' packed constants.  Only literals (true / false / null) at a token's end and
 // property names longer than 16 bytes branch (rare).
-GF_DHD inline bool geo_locate(const LBytes& s, int64_t p, int64_t e, const GeoTabs& gt, int vlines,
-                                           GeoPos* g) {
+GF_DHD inline bool geo_locate_notes(const LBytes& s, int64_t p, int64_t e, const GeoTabs& gt, int vlines,
+                                    int32_t* n) {
   if (e - p >= INT32_MAX) return false;
   GeoLoc L;
   geo_loc_init(L);
@@ -863,7 +863,14 @@ GF_DHD inline bool geo_locate(const LBytes& s, int64_t p, int64_t e, const GeoTa
   const int32_t o0 = (int32_t)(p - s.base), o1 = (int32_t)(e - s.base);  // the line's LDS offsets
   for (int32_t w = o0 & ~3; w < o1 && !L.bad; w += 4) geo_word(L, w, o0, o1, s, p, gt, top_role);
   if (!geo_loc_ok(L)) return false;
-  geo_notes_pos(s, p, e, vlines, L.n, g);
+  for (int k = 0; k < kGeoNotes; ++k) n[k] = L.n[k];
+  return true;
+}
+GF_DHD inline bool geo_locate(const LBytes& s, int64_t p, int64_t e, const GeoTabs& gt, int vlines,
+                                           GeoPos* g) {
+  int32_t n[kGeoNotes];
+  if (!geo_locate_notes(s, p, e, gt, vlines, n)) return false;
+  geo_notes_pos(s, p, e, vlines, n, g);
   return true;
 }
 
@@ -890,6 +897,45 @@ GF_DHD inline int geojson_line(const GeoTabs& gt, const GeoProps& gp, const LByt
   const int st = eval_geojson_walk(gp, s, p, e, vlines, &w);
   *o = w;
   return st;
+}
+
+// ---------------------------------------------------------------------------------------
+// Byte classes of the wave-per-line scan (k_csv.hip geo_wave_scan): flags, and in bits 24..27 the
+// element a byte starts outside strings (a quote: a string, read as a value until its key-ness is
+// known; a token byte: a token, when the byte before it is not one).
+// ---------------------------------------------------------------------------------------
+enum : uint32_t {
+  WB_Q = 1u << 0,      // '"'
+  WB_BAD = 1u << 1,    // a backslash, a control byte other than \t \n \r, a byte >= 0x80: the walk decides
+  WB_WSC = 1u << 2,    // \t \n \r: whitespace outside strings, an error inside
+  WB_OTH = 1u << 3,    // no JSON token holds it (JC_OTHER): an error outside strings
+  WB_OB = 1u << 4, WB_CB = 1u << 5, WB_OA = 1u << 6, WB_CA = 1u << 7, WB_CO = 1u << 8, WB_CM = 1u << 9,
+  WB_TOK = 1u << 10,   // [0-9a-zA-Z+-.]
+  WB_DOT = 1u << 11, WB_E = 1u << 12
+};
+enum : uint32_t { WT_NONE, WT_OB, WT_OA, WT_CB, WT_CA, WT_CO, WT_CM, WT_SK, WT_SV, WT_TK };
+constexpr uint32_t kWtValueEnd = (1u << WT_CB) | (1u << WT_CA) | (1u << WT_SV) | (1u << WT_TK);
+GF_DHD inline uint32_t wave_class(int b) {
+  const int cl = jclass(b);
+  uint32_t f = 0, t = WT_NONE;
+  switch (cl) {
+    case JC_QUOTE: f = WB_Q; t = WT_SV; break;
+    case JC_BSL: case JC_CTRL: case JC_HIGH: f = WB_BAD; break;
+    case JC_WSC: f = WB_WSC; break;
+    case JC_OTHER: f = WB_OTH; break;
+    case JC_LBRACE: f = WB_OB; t = WT_OB; break;
+    case JC_RBRACE: f = WB_CB; t = WT_CB; break;
+    case JC_LBRACK: f = WB_OA; t = WT_OA; break;
+    case JC_RBRACK: f = WB_CA; t = WT_CA; break;
+    case JC_COLON: f = WB_CO; t = WT_CO; break;
+    case JC_COMMA: f = WB_CM; t = WT_CM; break;
+    case JC_TOK:
+      f = WB_TOK | (b == '.' ? WB_DOT : 0u) | (b == 'e' || b == 'E' ? WB_E : 0u);
+      t = WT_TK;
+      break;
+    default: break;  // JC_WS
+  }
+  return f | t << 24;
 }
 
 // one entry of the locator's two per-byte tables (geo_tabs_fill)

@@ -37,6 +37,8 @@ struct gf_ctx {
   int join_coarse = 0;  // testing: the row path without sub-cells
   int join_stream = 0;  // experiment: the fine path's streaming probe (query side bucketed only)
   int geojson_walk = 0; // testing: every GeoJSON line takes the member-by-member walk
+  int geojson_lane = 0; // GeoJSON: the r05 lane locator instead of the wave scan
+  unsigned long long* geojson_check = nullptr;  // GF_FLAG_GEOJSON_CHECK: the 4 counters (device; null: off)
   int64_t csv_mean_line[2] = {0, 0};  // per format (CSV, GeoJSON): the last call's mean line length (sizes the next one's LDS staging)
   int join_async_done = 0;  // gf_join_pp_async: the packing kernel wrote the count
   double join_ppp = 0.0;  // pairs per ordinary point of the last join (sizes the output chunks)
@@ -126,6 +128,26 @@ __device__ __forceinline__ void lds_barrier() {
   __builtin_amdgcn_s_waitcnt(0xC07F);  // vmcnt(63) expcnt(7) lgkmcnt(0)
   __builtin_amdgcn_s_barrier();
   __atomic_signal_fence(__ATOMIC_SEQ_CST);
+}
+
+// Intra-wave LDS hand-off (r06): lanes of ONE wave write LDS slots (ballot
+// compaction: a lane writes slot base + its rank among the writers) and lanes of the same wave
+// then read slots OTHER lanes wrote.  The hardware runs a wave's LDS instructions in order, so no
+// wait is needed -- but the compiler reasons per thread: a lane's write to slot p and its later
+// read of slot q != p are independent to it, so without a wave-scope fence it may move the read
+// above the write (or the write below the read) and the reading lane sees the slot's OLD contents.
+// That is the cause of round 5's lost C3 hits: the in-stream test variant read the queued points'
+// coordinates from a per-wave LDS ring, each point read by a group of 8 lanes that had not written
+// it.  Every debug build that removed the cross-lane read lost nothing -- coordinates read from
+// global memory (no LDS hand-off), a one-lane walk (each lane read the slot it had written itself:
+// a same-thread dependency the compiler keeps) -- and accepting every candidate only hid the stale
+// coordinates.  This marks every such hand-off: release + acquire at wavefront scope around a wave
+// barrier; the fences emit no instruction (wavefront scope), the barrier appears in the ISA as
+// "; wave barrier" (tests/test_isa_handoff.py checks the hand-offs carry it).
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 // single-query classification (exact, from host-side cell thresholds)
@@ -288,6 +310,8 @@ struct RangeArgs {
   uint32_t* queue_count;     // [blocks] entries per segment
   double* queue_xy;          // [2 * blocks * seg_cap] the queued points' coordinates
   int64_t seg_cap;           // points one scan block visits at most
+  int32_t drain_lanes;       // testing (gf_range_plan_set_drain_lanes): the block-end drain runs on the first
+                             // drain_lanes lanes of each wave only (0 = all) -- drain_own_queue takes any exec mask
   const uint8_t* rect;       // [npoly] axis-aligned rectangle shells without holes (nullable)
   // point-polygon join: bbox cells per polygon (x0, x1, y0, y1) and the layer counts
   const int32_t* brect;
@@ -333,6 +357,10 @@ struct RadixArgs {
   const uint32_t* MsA;      // pass B: pass A's scanned matrix (row r = [MsA[r nblkA], MsA[(r+1) nblkA]))
   int32_t nblkA;
   uint32_t* cstart;         // pass B: cell_start[0 .. gn*gn + 1], written by each row's first segment
+  // row mode (r06): pass A's scatter writes each point's COLUMN as u16 (kout16; the row is its
+  // position's row) and pass B reads those (kin16): 2 B instead of 4 per point written and read twice
+  uint16_t* kout16;
+  const uint16_t* kin16;
 };
 // scatter block size: 1024 threads (one 8192-point tile per block, one block per CU) or 512
 // (4096-point tiles, two blocks per CU: one block's LDS phases overlap the other's memory);
@@ -485,6 +513,8 @@ struct CsvArgs {
   char prop_ts[kGeoPropMax];
   int32_t lds_cap;               // set by launch_csv_parse: the block's dynamic LDS staging bytes
   int32_t geo_fast;              // GeoJSON: 1 = one-pass member location first (k_csv.hip geo_locate)
+  int32_t geo_wave;              // GeoJSON: 1 = the wave-per-line scan locates (k_csv.hip geo_wave_scan)
+  unsigned long long* geo_check; // GeoJSON, geo_wave: non-null = run the lane locator too and count differences
   int32_t value_lines;           // GeoJSON: 1 = each line is the record's value (else the record)
 };
 hipError_t launch_csv_nlindex(hipStream_t st, const char* text, int64_t len, int64_t nseg, int64_t* nl, int64_t nl_cap,
@@ -824,6 +854,7 @@ struct gf_range_plan {
   int64_t cls_cells[4] = {0, 0, 0, 0};  // in-grid cells per class (diagnostics)
   int32_t scan_blocks = 0;         // tuning: 0 = auto
   int32_t defer_mode = 0;          // tuning: 0 auto, 1 test inline, 2 defer
+  int32_t drain_lanes = 0;         // testing: lanes per wave running the block-end drain (0 = all)
   // point-polygon join plans (gf_join_ppoly_plan_create)
   int join = 0;
   int32_t* brect = nullptr;        // [npoly * 4] bbox cells x0, x1, y0, y1

@@ -198,6 +198,7 @@ __device__ __forceinline__ int eval_geojson_line(const CsvArgs& a, const Src& s,
   else return geojson_line(gt, gp, s, p, e, a.value_lines, o);
 }
 
+__device__ __forceinline__ bool store_line(const CsvArgs& a, int64_t j, int st, const LineOut& o, DictWork* w);
 // parse + store line j; returns true when its objID needs the dictionary (*w filled)
 template <int FMT, bool FAST, class Src>
 __device__ __forceinline__ bool parse_line(const CsvArgs& a, const Src& s, int64_t j, int64_t newlines, DictWork* w,
@@ -206,6 +207,10 @@ __device__ __forceinline__ bool parse_line(const CsvArgs& a, const Src& s, int64
   int st;
   if constexpr (FMT == 1) st = eval_geojson_line<FAST>(a, s, j, newlines, &o, gt);
   else st = eval_csv_line(a, s, j, newlines, &o);
+  return store_line(a, j, st, o, w);
+}
+// line j's outputs (or its error); true when its objID needs the dictionary (*w filled)
+__device__ __forceinline__ bool store_line(const CsvArgs& a, int64_t j, int st, const LineOut& o, DictWork* w) {
   if (st != kCsvOk) {
     atomicMin(&a.err->line, (unsigned long long)j);
     return false;
@@ -256,6 +261,7 @@ constexpr int kGeoLines = GF_GEO_LINES;
 static_assert(kGeoLines % 64 == 0 && kGeoLines <= kBlock, "whole waves");
 template <int FMT>
 constexpr int parse_lines() { return FMT == 1 ? kGeoLines : kBlock; }
+__device__ __forceinline__ void queue_dict(const CsvArgs& a, bool need, const DictWork& w);
 template <int FMT>  // 0: CSV / TSV, 1: GeoJSON (a.format)
 __global__ __launch_bounds__(parse_lines<FMT>()) void csv_parse_kernel(CsvArgs a) {
   constexpr int NB = parse_lines<FMT>();
@@ -297,6 +303,11 @@ __global__ __launch_bounds__(parse_lines<FMT>()) void csv_parse_kernel(CsvArgs a
   } else if (j < L1) {
     need = parse_line<FMT, false>(a, GBytes{a.text}, j, newlines, &w, gt);
   }
+  queue_dict(a, need, w);
+}
+
+// the wave's dictionary objIDs into the queue (one atomic per wave)
+__device__ __forceinline__ void queue_dict(const CsvArgs& a, bool need, const DictWork& w) {
   const uint64_t m = __ballot(need);
   if (m) {
     const int lane = threadIdx.x & 63;
@@ -311,6 +322,342 @@ __global__ __launch_bounds__(parse_lines<FMT>()) void csv_parse_kernel(CsvArgs a
     base = __shfl(base, 0, 64);
     if (need) a.dict_work[base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = w;
   }
+}
+
+// ---------------------------------------------------------------------------------------
+// r06: the wave-per-line structural scan (GeoJSON).  The lane locator above runs one line per
+// lane, a dependent byte chain per lane with ~1,500 instructions per line (r05 PMC).  Here the
+// whole wave reads ONE line, 64 bytes per step (one per lane, from the LDS-staged block), and
+// derives the line's structure from ballots:
+//   strings   a prefix XOR of the quote mask (a backslash anywhere sends the line to the walk, so
+//             every quote toggles) with the carried in-string bit;
+//   elements  brackets, ':' and ',' outside strings, opening quotes and token starts; the depth
+//             before each byte from mbcnt of the open / close masks; each element's predecessor
+//             (the highest element lane below it, or the last one of earlier steps);
+//   containers per depth level present in the step: the kind (object / array) and role (Kafka
+//             record, value, geometry, properties) of the innermost container from the last open
+//             at that level below the lane (or the carried level state); a string is a key when
+//             it follows '{' or ',' in an object;
+//   grammar   each element against its predecessor and container (the JSON grammar as the lane
+//             automaton's transitions state it, k_geojson.hpp jtrans);
+//   tokens    numbers by local rules over (previous, byte, next) plus the token's earlier '.'/'e'
+//             masks -- the lane automaton's number grammar -- literals by their first byte;
+//   keys      a looked-up container's key: its bytes from LDS (<= 16) against the packed names;
+//             the notes take the highest matching lane.
+// It accepts a subset of the lines the lane locator accepts (a byte >= 0x80 goes to the walk
+// too), with the same notes; GF_FLAG_GEOJSON_CHECK runs both and counts any difference
+// (tests/test_gpu_geojson.py::test_wave_scan_matches_lane_locator).  The evaluation of the
+// located members (geo_eval_body) stays one lane per line.
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ int32_t lanes_below(uint64_t m) {
+  return (int32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+__device__ __forceinline__ int top_lane(uint64_t m) { return 63 - __clzll((long long)m); }  // (m != 0)
+__device__ __forceinline__ uint32_t lane_val(uint32_t v, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, l); }
+__device__ __forceinline__ uint32_t from_lane(uint32_t v, int l) { return (uint32_t)__shfl((int)v, l, 64); }
+
+// The line lp[0, len) (lp[0] == '{') by the whole wave (a wave-uniform call).  false: the line
+// takes the walk; true: n[] = its notes (positions from lp, as geo_locate_notes).
+__device__ __forceinline__ bool geo_wave_scan(GF_LDS_PTR(char) lp, int32_t len, GF_LDS_PTR(uint32_t) wtab,
+                                              const GeoTabs& gt, int top_role, int32_t* n) {
+  constexpr K16 kValue = geo_pack16("value", 5), kGeom = geo_pack16("geometry", 8);
+  constexpr K16 kProps = geo_pack16("properties", 10), kCoord = geo_pack16("coordinates", 11);
+  constexpr K16 kType = geo_pack16("type", 4);
+  const int32_t lts = gt.klen[4], lobj = gt.klen[5];
+  const int lane = (int)(threadIdx.x & 63u);
+  const uint64_t below = (1ull << lane) - 1ull;
+  // carried from step to step (wave-uniform)
+  int32_t depth = 0, tok_start = 0, str_open = 0;
+  uint32_t instr = 0, tok_open = 0, tok_dot = 0, tok_e = 0, str_key = 0, last = WT_NONE, pend = JK_NONE;
+  uint32_t roles = 0;  // the open containers' roles at depths 1..3 (4 bits each)
+  uint64_t kinds = 0;  // bit d: the open container at depth d is an object
+  for (int k = 0; k < kGeoNotes; ++k) n[k] = -1;
+  for (int32_t c0 = 0; c0 < len; c0 += 64) {
+    const int32_t i = c0 + lane;
+    const uint32_t b = i < len ? (uint32_t)(uint8_t)lp[i] : 32u;
+    const uint32_t f = wtab[b];
+    const uint64_t Qm = __ballot(f & WB_Q);
+    uint64_t S = Qm;
+    S ^= S << 1;
+    S ^= S << 2;
+    S ^= S << 4;
+    S ^= S << 8;
+    S ^= S << 16;
+    S ^= S << 32;
+    S = instr ? ~S : S;
+    const uint64_t IN = (S << 1) | (uint64_t)instr;  // bit i: byte i is a string's content or closing quote
+    instr = (uint32_t)(S >> 63);
+    const bool in = (IN >> lane) & 1ull;
+    if (__ballot(f & (WB_BAD | (in ? WB_WSC : WB_OTH)))) return false;
+    const uint32_t fo = in ? 0u : f;  // the byte's classes outside strings (an opening quote included)
+    const uint64_t OPm = __ballot(fo & (WB_OB | WB_OA)), CLm = __ballot(fo & (WB_CB | WB_CA));
+    const uint64_t PUm = __ballot(fo & (WB_CO | WB_CM)), TKm = __ballot(fo & WB_TOK);
+    const uint64_t OQ = Qm & ~IN, CQ = Qm & IN;
+    const uint64_t TSm = TKm & ~((TKm << 1) | (uint64_t)tok_open);
+    const uint64_t ELm = OPm | CLm | PUm | OQ | TSm;
+    const bool el = (ELm >> lane) & 1ull, cq = (CQ >> lane) & 1ull;
+    const uint32_t traw = el ? fo >> 24 : (uint32_t)WT_NONE;
+    const bool isop = traw == WT_OB || traw == WT_OA;
+    const int32_t dbef = depth + lanes_below(OPm) - lanes_below(CLm);  // the depth before the byte
+    if (__ballot(((traw == WT_CB || traw == WT_CA || traw == WT_CM) && dbef <= 0) || (isop && dbef >= 63)))
+      return false;
+    const uint64_t pm = ELm & below;
+    const int pl = pm ? top_lane(pm) : 0;
+    const uint32_t praw0 = from_lane(traw, pl);
+    const uint32_t praw = pm ? praw0 : last;  // the predecessor (a string: key-ness not needed here)
+    // the depth levels the step's elements and closing quotes sit at, lowest first
+    const bool ctx = el || cq;
+    int32_t dl = depth, dh = depth;
+    while (__ballot(ctx && dbef < dl)) --dl;
+    while (__ballot(ctx && dbef > dh)) ++dh;
+    const uint64_t qb = Qm & below;
+    const int ql = qb ? top_lane(qb) : 0;  // a closing quote's opening quote (this step)
+    uint32_t K = 0, crole = JR_NONE, orole = JR_NONE, iskey = 0, kkind = JK_NONE;
+    for (int32_t D = dl; D <= dh + 1; ++D) {
+      const uint64_t OD = __ballot(isop && dbef == D - 1), BD = __ballot(traw == WT_OB && dbef == D - 1);
+      const bool at = ctx && dbef == D;
+      const uint64_t om = OD & below;
+      const int os = om ? top_lane(om) : 0;
+      const uint32_t rin = from_lane(orole, os);
+      const bool lowd = D >= 1 && D <= 3;
+      if (at) {  // the innermost container: the last open to depth D below, or the carried one
+        K = om ? (uint32_t)(BD >> os) & 1u : (uint32_t)(kinds >> (D & 63)) & 1u;
+        crole = om ? rin : lowd ? (roles >> (4 * D)) & 15u : (uint32_t)JR_NONE;
+        if (traw == WT_SV) iskey = praw == WT_OB || (praw == WT_CM && K);
+      }
+      const uint32_t kin = from_lane(iskey, ql);
+      if (at && cq) iskey = qb ? kin : str_key;
+      if (D <= 3) {  // (uniform) a looked-up container's keys; the roles of the containers opened here
+        const bool kend = at && cq && iskey;
+        const uint64_t KD = __ballot(kend);
+        if (lowd && __ballot(kend && crole != JR_NONE)) {
+          const int32_t kst = (qb ? c0 + ql : str_open) + 1, klen = i - kst;
+          uint64_t hi = 0, lo = 0;
+          if (kend && crole != JR_NONE && klen <= 16) {
+            for (int32_t q = kst; q < i; ++q) {
+              hi = (hi << 8) | (lo >> 56);
+              lo = (lo << 8) | (uint8_t)lp[q];
+            }
+          }
+          // (a key of <= 8 bytes leaves hi 0: the short names compare lo only)
+          const bool e_type = klen == 4 && lo == kType.lo, e_value = klen == 5 && lo == kValue.lo;
+          const bool e_geom = klen == 8 && lo == kGeom.lo;
+          const bool e_props = klen == 10 && lo == kProps.lo && hi == kProps.hi;
+          const bool e_coord = klen == 11 && lo == kCoord.lo && hi == kCoord.hi;
+          const bool top = kend && crole == JR_TOP, val = kend && crole == JR_VAL;
+          const bool geo = kend && crole == JR_GEO, prop = kend && crole == JR_PROP;
+          const bool m_value = top && e_value, v_geom = val && e_geom, v_props = val && e_props;
+          bool p_ts = prop && klen == lts && lts <= 16 && lo == gt.pts.lo && hi == gt.pts.hi;
+          bool p_obj = prop && klen == lobj && lobj <= 16 && lo == gt.pobj.lo && hi == gt.pobj.hi;
+          if ((lts > 16 || lobj > 16) && prop && klen > 16) {  // (rare: a property name longer than 16 bytes)
+            const LBytes s{lp, 0};
+            p_ts = jkey_eq(s, kst, klen, gt, 4);
+            p_obj = jkey_eq(s, kst, klen, gt, 5);
+          }
+          kkind = kend ? (m_value ? JK_VALUE : v_geom ? JK_GEO : v_props ? JK_PROP : JK_NONE) : kkind;
+          auto note = [&](int k, bool c) {
+            const uint64_t M = __ballot(c);
+            if (M) n[k] = c0 + top_lane(M);
+          };
+          note(GN_V, m_value);
+          note(GN_TV, val && e_type);
+          note(GN_CV, val && e_coord);
+          note(GN_GV, v_geom);
+          note(GN_PRV, v_props);
+          note(GN_TG, geo && e_type);
+          note(GN_CG, geo && e_coord);
+          note(GN_TP, p_ts);
+          note(GN_QP, p_obj);
+        }
+        if (D <= 2) {  // a container opened at depth D: its role from the key before it
+          const uint64_t pk = KD & below;
+          const uint32_t pin = from_lane(kkind, pk ? top_lane(pk) : 0);
+          const uint32_t pe = pk ? pin : pend;
+          if (at && isop)
+            orole = traw == WT_OA ? (uint32_t)JR_NONE
+                    : D == 0 ? (uint32_t)top_role
+                    : crole == JR_TOP ? (0x0020u >> (4 * pe)) & 15u   // value -> V
+                    : crole == JR_VAL ? (0x4300u >> (4 * pe)) & 15u   // geometry, properties
+                    : (uint32_t)JR_NONE;
+        }
+      }
+      if (OD) {  // the level's carried state: its last open of the step
+        const int s = top_lane(OD);
+        kinds = (kinds & ~(1ull << (D & 63))) | (((BD >> s) & 1ull) << (D & 63));
+        if (lowd) roles = (roles & ~(15u << (4 * D))) | (lane_val(orole, s) << (4 * D));
+      }
+    }
+    // the grammar: each element after its predecessor, in its container
+    const uint32_t tr = traw == WT_SV && iskey ? (uint32_t)WT_SK : traw;
+    const uint32_t pr0 = from_lane(tr, pl);
+    const uint32_t pr = pm ? pr0 : last;
+    const bool pve = (kWtValueEnd >> pr) & 1u;
+    const bool ok = tr == WT_NONE || tr == WT_SK ? true
+                    : tr == WT_CO ? pr == WT_SK
+                    : tr == WT_CM ? pve
+                    : tr == WT_CB ? K && (pr == WT_OB || pve)
+                    : tr == WT_CA ? !K && (pr == WT_OA || pve)
+                    : pr == WT_OA || pr == WT_CO || (pr == WT_CM && !K) || (pr == WT_NONE && tr == WT_OB);
+    if (__ballot(!ok)) return false;
+    // tokens: the number grammar by local rules, literals whole from their first byte
+    if (TKm) {
+      const uint64_t DOTm = __ballot(fo & WB_DOT), Em = __ballot(fo & WB_E);
+      const bool tk = (TKm >> lane) & 1ull;
+      const uint64_t tsb = TSm & (below | (1ull << lane));
+      const int32_t ts = tsb ? c0 + top_lane(tsb) : tok_start;  // the token's first byte
+      bool bad = false;
+      if (tk) {
+        const uint32_t fc = (uint8_t)lp[ts];
+        const uint32_t prv = i > ts ? (uint32_t)(uint8_t)lp[i - 1] : 0u;
+        const uint32_t nxt = i + 1 < len ? (uint32_t)(uint8_t)lp[i + 1] : 32u;
+        const bool num = fc == '-' || fc - '0' < 10u;
+        const bool ndig = nxt - '0' < 10u, pdig = prv - '0' < 10u, pexp = (prv | 0x20u) == 'e';
+        if (!num) {
+          if (i == ts) {  // true / false / null, and nothing else
+            const int wl = fc == 'f' ? 5 : 4;
+            const char* wd = fc == 't' ? "true" : fc == 'f' ? "false" : "null";
+            bool w = (fc == 't' || fc == 'f' || fc == 'n') && i + wl <= len;
+            for (int q = 1; w && q < wl; ++q) w = (uint8_t)lp[i + q] == (uint8_t)wd[q];
+            w = w && !(i + wl < len && (wtab[(uint8_t)lp[i + wl]] & WB_TOK));
+            bad = !w;
+          }
+        } else {  // -?(0|[1-9][0-9]*)(.[0-9]+)?([eE][+-]?[0-9]{1,2})?, shorter than 19 bytes
+          const uint32_t sh = ts > c0 ? (uint32_t)(ts - c0) : 0u;
+          const uint64_t rng = below & ~((1ull << sh) - 1ull);  // the token's bytes before this one (this step)
+          const bool carried = ts < c0;
+          if (b == '-') {
+            bad = !((i == ts || pexp) && ndig);
+          } else if (b == '+') {
+            bad = !(pexp && ndig);
+          } else if (b == '.') {
+            bad = !(pdig && ndig) || ((DOTm | Em) & rng) != 0 || (carried && (tok_dot | tok_e));
+          } else if ((b | 0x20u) == 'e') {
+            const bool sg = nxt == '+' || nxt == '-';
+            bad = !(pdig && (ndig || sg)) || (Em & rng) != 0 || (carried && tok_e);
+            const int32_t x = i + (sg ? 2 : 1);  // the exponent's first digit: a third one is the walk's
+            bad |= x + 2 < len && (uint32_t)(uint8_t)lp[x + 1] - '0' < 10u && (uint32_t)(uint8_t)lp[x + 2] - '0' < 10u;
+          } else if (b - '0' >= 10u) {
+            bad = true;  // a letter
+          } else {
+            bad = b == '0' && (i == ts || (i == ts + 1 && fc == '-')) && ndig;  // a leading zero
+          }
+          bad |= !(wtab[nxt] & WB_TOK) && i - ts + 1 >= 19;  // the token's last byte: its length
+        }
+      }
+      if (__ballot(bad)) return false;
+      const bool t63 = (TKm >> 63) & 1ull;
+      if (t63) {  // a token runs into the next step
+        const int32_t ts63 = (int32_t)lane_val((uint32_t)ts, 63);
+        const uint32_t sh = ts63 > c0 ? (uint32_t)(ts63 - c0) : 0u;
+        const uint64_t r = ~((1ull << sh) - 1ull);
+        const bool car = ts63 < c0;
+        tok_dot = (car && tok_dot) || (DOTm & r) != 0;
+        tok_e = (car && tok_e) || (Em & r) != 0;
+        tok_start = ts63;
+      }
+      tok_open = t63;
+    } else {
+      tok_open = 0;
+    }
+    if (ELm) last = lane_val(tr, top_lane(ELm));
+    depth += __popcll(OPm) - __popcll(CLm);
+    const uint64_t KCm = __ballot(cq && iskey);
+    if (KCm) pend = lane_val(kkind, top_lane(KCm));
+    if (instr && Qm) {  // a string runs into the next step
+      const int s = top_lane(Qm);
+      str_open = c0 + s;
+      str_key = lane_val(iskey, s);
+    }
+  }
+  return !instr && depth == 0 && last == WT_CB;
+}
+
+// GeoJSON blocks with the wave scan: the block's lines staged in LDS as csv_parse_kernel stages
+// them; each wave scans its 64 lines one after the other (all lanes on each), the line's lane
+// keeps the result, then every lane evaluates its own line from the notes (or walks it).
+// CHECK: the lane locator runs too, and a.geo_check counts [both pass, same notes; the scan
+// passes, the locator not; both pass, notes differ; the locator passes, the scan not].
+template <bool CHECK>
+__global__ __launch_bounds__(kGeoLines) void geojson_wave_kernel(CsvArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  int64_t newlines, lines;
+  const bool ok = csv_counts(a, newlines, lines);
+  const int64_t L0 = (int64_t)blockIdx.x * kGeoLines;
+  if (!ok || L0 >= lines) return;  // block-uniform
+  const int64_t L1 = L0 + kGeoLines < lines ? L0 + kGeoLines : lines;  // exclusive
+  const int64_t b0 = L0 == 0 ? 0 : a.nl[L0 - 1] + 1;
+  const int64_t b1 = L1 - 1 < newlines ? a.nl[L1 - 1] : a.len;
+  const int64_t a0 = b0 & ~(int64_t)15;
+  const int64_t j = L0 + threadIdx.x;
+  DictWork w{0, 0, 0};
+  bool need = false;
+  __shared__ uint64_t gtab[256], gttab[256];
+  __shared__ char gkeys[kGeoKeys * kGeoPropMax];
+  __shared__ uint32_t wtab[256];
+  const GeoTabs gt{(GF_LDS_PTR(uint64_t))gtab, (GF_LDS_PTR(uint64_t))gttab, (GF_LDS_PTR(char))gkeys,
+                   {5, 8, 10, 11, a.len_ts, a.len_obj, 4},
+                   geo_pack16(a.prop_ts, a.len_ts <= 16 ? a.len_ts : 0),
+                   geo_pack16(a.prop_obj, a.len_obj <= 16 ? a.len_obj : 0)};
+  geo_tabs_fill(a, gtab, gttab, gkeys);
+  for (int c = threadIdx.x; c < 256; c += blockDim.x) wtab[c] = wave_class(c);
+  const GeoProps gp{gt.keys + 4 * kGeoPropMax, gt.keys + 5 * kGeoPropMax, a.len_ts, a.len_obj, a.date_fmt,
+                    a.tz_off_ms, kPow5Dev};
+  if (b1 - a0 <= a.lds_cap) {  // block-uniform
+    for (int64_t off = a0 + 16 * threadIdx.x; off < b1; off += 16 * kGeoLines) {
+      if (off + 16 <= a.len) {
+        *reinterpret_cast<uint4*>(lds + (off - a0)) = *reinterpret_cast<const uint4*>(a.text + off);
+      } else {
+        for (int k = 0; k < 16 && off + k < a.len; ++k) lds[off - a0 + k] = a.text[off + k];
+      }
+    }
+    __syncthreads();
+    const LBytes s{(GF_LDS_PTR(char))lds, a0};
+    int64_t p = 0, e = 0;
+    const int bs = j < L1 ? geojson_bounds(a, s, j, newlines, p, e) : (int)kCsvEmptyLine;
+    const int32_t o0 = (int32_t)(p - a0), o1 = (int32_t)(e - a0);  // (staged: < 64 KB)
+    const int top_role = a.value_lines ? JR_VAL : JR_TOP;
+    const int lane = (int)(threadIdx.x & 63u);
+    bool wok = false;
+    int32_t wn[kGeoNotes];
+    for (int k = 0; k < kGeoNotes; ++k) wn[k] = -1;
+    for (uint64_t m = __ballot(j < L1 && bs == kCsvOk); m; m &= m - 1ull) {  // (wave-uniform)
+      const int q = __builtin_ctzll(m);
+      const int32_t q0 = __builtin_amdgcn_readlane(o0, q), q1 = __builtin_amdgcn_readlane(o1, q);
+      int32_t nq[kGeoNotes];
+      const bool okq = geo_wave_scan((GF_LDS_PTR(char))lds + q0, q1 - q0, (GF_LDS_PTR(uint32_t))wtab, gt, top_role, nq);
+      if (lane == q) {
+        wok = okq;
+        for (int k = 0; k < kGeoNotes; ++k) wn[k] = nq[k];
+      }
+    }
+    if (j < L1) {
+      LineOut o{0, 0, 0.0, 0.0, false, {0, 0}};
+      int st = bs;
+      if (bs == kCsvOk) {
+        if constexpr (CHECK) {
+          int32_t ln[kGeoNotes];
+          const bool lok = geo_locate_notes(s, p, e, gt, a.value_lines, ln);
+          bool same = true;
+          for (int k = 0; k < kGeoNotes; ++k) same = same && ln[k] == wn[k];
+          const int c = wok && lok ? (same ? 0 : 2) : wok ? 1 : lok ? 3 : -1;
+          if (c >= 0) atomicAdd(a.geo_check + c, 1ull);
+        }
+        if (wok) {
+          GeoPos g;
+          geo_notes_pos(s, p, e, a.value_lines, wn, &g);
+          st = geo_eval_body(gp, s, e, g, &o);
+        } else {
+          LineOut wo{0, 0, 0.0, 0.0, false, {0, 0}};
+          st = eval_geojson_walk(gp, s, p, e, a.value_lines, &wo);
+          o = wo;
+        }
+      }
+      need = store_line(a, j, st, o, &w);
+    }
+  } else if (j < L1) {
+    need = parse_line<1, false>(a, GBytes{a.text}, j, newlines, &w, gt);
+  }
+  queue_dict(a, need, w);
 }
 
 // The call's last kernel: the error kind of the first bad line (re-derived by a one-lane pass over
@@ -471,7 +818,11 @@ hipError_t launch_csv_parse(gf_ctx* ctx, const CsvArgs& a0) {
   a.lds_cap = (int32_t)(cap < kCsvLds ? kCsvLds : cap > kCsvLdsMax ? kCsvLdsMax : cap);
   if (a.grid_lines > 0) {  // (blocks past the chunk's lines return at once)
     const unsigned blocks = (unsigned)((a.grid_lines + NB - 1) / NB);
-    if (a.format == 1)
+    if (a.format == 1 && a.geo_wave && a.geo_check)
+      hipLaunchKernelGGL(geojson_wave_kernel<true>, dim3(blocks), dim3(NB), (size_t)a.lds_cap, ctx->stream, a);
+    else if (a.format == 1 && a.geo_wave)
+      hipLaunchKernelGGL(geojson_wave_kernel<false>, dim3(blocks), dim3(NB), (size_t)a.lds_cap, ctx->stream, a);
+    else if (a.format == 1)
       hipLaunchKernelGGL(csv_parse_kernel<1>, dim3(blocks), dim3(NB), (size_t)a.lds_cap, ctx->stream, a);
     else
       hipLaunchKernelGGL(csv_parse_kernel<0>, dim3(blocks), dim3(kBlock), (size_t)a.lds_cap, ctx->stream, a);

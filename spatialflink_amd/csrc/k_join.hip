@@ -720,6 +720,7 @@ struct JoinWaveBuf {
     const uint32_t g0 = hd.g0, gm = join_uni(hd.gm);
     const uint32_t* lq = reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(&hd) + hd.lqidx);
     const uint2* b = buf;
+    wave_lds_sync();  // the entries other lanes of this wave pushed (intra-wave LDS hand-off)
     auto get = [&](uint32_t i) {
       const uint2 v = b[i];
       const uint32_t qi = v.y & 0x80000000u ? v.y & 0x7fffffffu : (v.y - g0 < gm ? lq[v.y - g0] : a.sqidx[v.y]);
@@ -1172,6 +1173,7 @@ __global__ __launch_bounds__(kBlock) void join_stream_kernel(JoinRowArgs a) {
   const int32_t f = a.f, qn = a.qn;
   const int64_t fW = (int64_t)f * (qn + 2);
   auto flush = [&]() {
+    wave_lds_sync();  // the entries other lanes of this wave pushed (intra-wave LDS hand-off)
     join_emit(a.out, wo, cnt, [&](uint32_t i) {
       const uint2 v = buf[i];
       return make_uint2(v.x, a.sqidx[v.y]);
@@ -1684,6 +1686,7 @@ __global__ __launch_bounds__(kBandThreads, 4 * GF_BAND_MINBLK) void join_band_pr
         cnt = 0;
         return;
 #endif
+        wave_lds_sync();  // the entries other lanes of this wave pushed (intra-wave LDS hand-off)
         if (staged(st)) {
           band_emit(a.out, hd, cnt, [&](uint32_t i) {
             const uint2 v = buf[i];
@@ -1945,8 +1948,10 @@ __global__ __launch_bounds__(kBandThreads, 4 * GF_BAND_MINBLK) void join_band_pr
           if (act) wq[qc + __builtin_amdgcn_mbcnt_hi((uint32_t)(am >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)am, 0u))] = i;
           qc += (uint32_t)__popcll(am);
           if (qc >= 64) {
+            wave_lds_sync();  // positions other lanes queued (intra-wave LDS hand-off)
             const uint32_t k = wq[lane], rest = qc - 64;
             const uint32_t mv = lane < rest ? wq[64 + lane] : 0u;
+            wave_lds_sync();  // every lane read its slot before the tail moves to the front
             if (lane < rest) wq[lane] = mv;
             qc = rest;
             const double2 v = reinterpret_cast<const double2*>(a.soxy)[k];
@@ -1955,6 +1960,7 @@ __global__ __launch_bounds__(kBandThreads, 4 * GF_BAND_MINBLK) void join_band_pr
           }
         }
         if (qc > 0) {
+          wave_lds_sync();
           const uint32_t k = wq[lane < qc ? lane : 0];
           const double2 v = reinterpret_cast<const double2*>(a.soxy)[k];
           probe(st, v.x, v.y, a.soidx[k], lane < qc);

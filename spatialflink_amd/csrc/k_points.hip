@@ -254,13 +254,22 @@ __global__ __launch_bounds__(kRadixThreads) void radix_seg_hist_kernel(RadixArgs
     for (uint32_t d = threadIdx.x; d < D; d += kRadixThreads) a.M[(size_t)blockIdx.x * D + d] = 0u;
     return;
   }
+  if (rs.nseg == 1) {
+    // r06: a one-segment row (every row of a uniform 10M-point window on 500 x 500) is sorted by
+    // its own scatter block, which counts its columns itself (radix_scatter_kernel): no histogram
+    // read here.  Its entries only carry the row's total (column 0) so that the ONE scan of M still
+    // gives the later rows' segments their absolute slots.
+    for (uint32_t d = threadIdx.x; d < D; d += kRadixThreads)
+      a.M[(size_t)rs.base * D + d] = d == 0 ? (uint32_t)(rs.end - rs.beg) : 0u;
+    return;
+  }
   constexpr int U = 8;
   for (int64_t i0 = rs.beg + threadIdx.x; i0 < rs.end; i0 += (int64_t)kRadixThreads * U) {
     uint32_t k[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {  // clamped addresses (i0 < end): the U loads fly together
       const int64_t i = i0 + (int64_t)u * kRadixThreads;
-      k[u] = a.kin[i < rs.end ? i : rs.end - 1];
+      k[u] = a.kin16[i < rs.end ? i : rs.end - 1];
     }
 #pragma unroll
     for (int u = 0; u < U; ++u)
@@ -380,14 +389,54 @@ __global__ __launch_bounds__(NT, MINW) void radix_scatter_kernel(RadixArgs a) {
     beg = rs.beg;
     end = rs.end;
     const size_t m0 = (size_t)rs.base * D;
-    for (uint32_t d = threadIdx.x; d < D; d += NT) gc[d] = a.Ms[m0 + (size_t)d * rs.nseg + rs.j];
-    if (rs.j == 0) {  // the row's cells start at their columns' first slots
-      if (rs.r < (uint32_t)a.gn) {
-        for (int32_t c = threadIdx.x; c < a.gn; c += NT)
-          a.cstart[(size_t)rs.r * a.gn + c] = a.Ms[m0 + (size_t)c * rs.nseg];
+    if (rs.nseg == 1) {
+      // r06: a one-segment row counts its own columns (the histogram kernel skipped it): an LDS
+      // histogram of the row's u16 columns, a block scan -> each column's first slot
+      for (uint32_t d = threadIdx.x; d < D; d += NT) gc[d] = 0u;
+      lds_barrier();
+      constexpr int HU = 8;
+      for (int64_t i0 = beg + threadIdx.x; i0 < end; i0 += (int64_t)NT * HU) {
+        uint32_t c[HU];
+#pragma unroll
+        for (int u = 0; u < HU; ++u) {  // clamped addresses: the loads fly together
+          const int64_t i = i0 + (int64_t)u * NT;
+          c[u] = a.kin16[i < end ? i : end - 1];
+        }
+#pragma unroll
+        for (int u = 0; u < HU; ++u)
+          if (i0 + (int64_t)u * NT < end) atomicAdd(&gc[c[u] & mask], 1u);
+      }
+      lds_barrier();
+      // exclusive scan of gc[0 .. D) (D <= 512 <= NT: one entry per thread), plus the row's start
+      const uint32_t v = threadIdx.x < D ? gc[threadIdx.x] : 0u;
+      uint32_t inc = v;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = __shfl_up(inc, o, 64);
+        if (lane >= o) inc += t;
+      }
+      if (lane == 63) ws[w] = inc;
+      lds_barrier();
+      uint32_t before = inc - v + (uint32_t)beg;
+      for (int q = 0; q < w; ++q) before += ws[q];
+      if (threadIdx.x < D) gc[threadIdx.x] = before;
+      lds_barrier();
+      if (rs.r < (uint32_t)a.gn) {  // the row's cells start at their columns' first slots
+        for (int32_t c = threadIdx.x; c < a.gn; c += NT) a.cstart[(size_t)rs.r * a.gn + c] = gc[c];
       } else if (threadIdx.x == 0) {
-        a.cstart[(size_t)a.gn * a.gn] = a.Ms[m0];
+        a.cstart[(size_t)a.gn * a.gn] = (uint32_t)beg;
         a.cstart[(size_t)a.gn * a.gn + 1] = (uint32_t)a.n;
+      }
+    } else {
+      for (uint32_t d = threadIdx.x; d < D; d += NT) gc[d] = a.Ms[m0 + (size_t)d * rs.nseg + rs.j];
+      if (rs.j == 0) {  // the row's cells start at their columns' first slots
+        if (rs.r < (uint32_t)a.gn) {
+          for (int32_t c = threadIdx.x; c < a.gn; c += NT)
+            a.cstart[(size_t)rs.r * a.gn + c] = a.Ms[m0 + (size_t)c * rs.nseg];
+        } else if (threadIdx.x == 0) {
+          a.cstart[(size_t)a.gn * a.gn] = a.Ms[m0];
+          a.cstart[(size_t)a.gn * a.gn + 1] = (uint32_t)a.n;
+        }
       }
     }
   } else {
@@ -408,7 +457,7 @@ __global__ __launch_bounds__(NT, MINW) void radix_scatter_kernel(RadixArgs a) {
     for (int u = 0; u < U; ++u) {
       const uint32_t e = w * EPW + u * 64 + lane;
       idx[u] = t + (e < c ? e : c - 1);
-      k[u] = a.kin[idx[u]];
+      k[u] = a.kin16 ? (uint32_t)a.kin16[idx[u]] : a.kin[idx[u]];
     }
     if (a.vin) {  // kernel-uniform
 #pragma unroll
@@ -505,7 +554,8 @@ __global__ __launch_bounds__(NT, MINW) void radix_scatter_kernel(RadixArgs a) {
 #elif GF_RADIX_EXP >= 2
       if (o >= (uint32_t)a.n) continue;
 #endif
-      if (a.kout) a.kout[o] = kk;  // (pass B of row mode keeps only the permutation)
+      if (a.kout16) a.kout16[o] = (uint16_t)(kk & (uint32_t)(kRadixMaxDigits - 1));  // row mode pass A: the column
+      else if (a.kout) a.kout[o] = kk;  // (pass B of row mode keeps only the permutation)
       a.vout[o] = lv[p];
     }
     lds_barrier();

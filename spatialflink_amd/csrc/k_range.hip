@@ -289,6 +289,7 @@ __device__ __forceinline__ void waveq_round(const RangeArgs& a, const RangeLds& 
                                             uint64_t& hits, uint32_t* lcount) {
   const uint32_t lane = threadIdx.x & 63;
   const bool valid = lane < take;
+  wave_lds_sync();  // the entries other lanes of this wave queued (intra-wave LDS hand-off)
   const uint32_t slot_q = (q.head + (valid ? lane : 0u)) & (uint32_t)(kWaveQ - 1);
   const uint32_t i = q.idx[slot_q];
   const double2 v = q.xy[slot_q];
@@ -307,6 +308,7 @@ __device__ __forceinline__ void waveq_round(const RangeArgs& a, const RangeLds& 
       bitmap_or(a.bitmap, i);
   }
   hits += (uint64_t)__popcll(__ballot(acc));
+  wave_lds_sync();  // the ring words OR-ed by other lanes, before lane 0 stores a word that left the ring
 #if GF_RANGE_EXP != 4
   queue_append2(cls == kTest, i, v.x, v.y, false, 0u, 0.0, 0.0, a, lcount);
 #endif
@@ -573,27 +575,48 @@ __device__ __forceinline__ bool test_object(const RangeArgs& a, double px, doubl
 // polygon), so fewer passes shorten the block's tail; one lane per point walks lists serially.
 #endif
 constexpr int kTestGroup = GF_RANGE_TEST_GROUP;
-// DEFER 1: after its scan loop, a block drains its OWN queue segment (the candidate-cell points
-// it queued) -- no second launch, no grid-wide prefix of the segment counts.  A queued point is
-// a group of kTestGroup lanes that test its candidate objects in parallel (kTestGroup at a time,
-// stopping once one hits).  Hits are
-// OR-ed into the bitmap words this block stored during the scan: every wave drains its stores
-// (s_waitcnt vmcnt(0): acknowledged by L2) before the barrier, so the atomics land after them.
-// Returns this wave's added hits (wave-uniform).
+// DEFER 1 / 3: after its scan loop, a block drains its OWN queue segment (the candidate-cell points
+// it queued) -- no second launch, no grid-wide prefix of the segment counts.  A queued point is a
+// group of up to kTestGroup lanes that test its candidate objects in parallel (stopping once one
+// hits); hits are OR-ed into the bitmap words this block stored during the scan.
+// Hand-offs (r06), by construction rather than by the calling context:
+//  * the entries are GLOBAL memory stored by any wave of the block during its stream, the count
+//    is LDS: every wave drains its stores (s_waitcnt vmcnt(0): acknowledged by L2) and then meets
+//    the workgroup barrier (__syncthreads: release + acquire at workgroup scope, and no memory
+//    access moves across it), so every entry is complete before any lane reads one;
+//  * nothing else crosses lanes through memory: a group shares only ballot masks;
+//  * no full wave is assumed: each wave's ACTIVE lanes take points from a block cursor in LDS
+//    (one atomic per wave pass, its result broadcast by readfirstlane), form groups among
+//    themselves, and a point's hit is recorded by the lowest active lane of its group that found
+//    one -- a partially active wave drains every point it takes (tests: gf_range_plan_set_drain_lanes).
+// Returns this wave's added hits (uniform over the active lanes).
 template <int POLY>
-__device__ uint64_t drain_own_queue(const RangeArgs& a, const uint32_t& lcount) {
+__device__ uint64_t drain_own_queue(const RangeArgs& a, const uint32_t& lcount, uint32_t* cursor) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   const uint32_t total = lcount;
-  const int lane = threadIdx.x & 63, g = lane & (kTestGroup - 1);
-  constexpr int kGroups = kBlock / kTestGroup;
-  const int grp = threadIdx.x / kTestGroup;
-  const uint64_t gmask = ((1ull << kTestGroup) - 1) << (lane & ~(kTestGroup - 1));
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t act = __ballot(1);                     // the lanes running the drain
+  const uint32_t nact = (uint32_t)__popcll(act);
+  const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
+  const uint32_t G = nact < (uint32_t)kTestGroup ? nact : (uint32_t)kTestGroup;  // lanes per point
+  const uint32_t ng = nact / G;                          // groups in this wave (>= 1)
+  const uint32_t gi = rank / G, g = rank - gi * G;       // my group, my place in it
+  const bool grouped = gi < ng;                          // (the nact % G last lanes idle)
+  uint64_t gmask = 0;                                    // my group's lanes
+  for (uint32_t k = 0; k < ng; ++k) {
+    const uint64_t m = __ballot(grouped && gi == k);
+    if (gi == k) gmask = m;
+  }
   const size_t seg = (size_t)blockIdx.x * a.seg_cap;
   uint64_t hits = 0;
-  for (uint32_t e0 = 0; e0 < total; e0 += kGroups) {  // block-uniform
-    const uint32_t e = e0 + grp;
-    const bool valid = e < total;
+  for (;;) {  // uniform over the active lanes: this wave's next ng points
+    uint32_t e0 = 0;
+    if (rank == 0) e0 = atomicAdd(cursor, ng);
+    e0 = __builtin_amdgcn_readfirstlane(e0);
+    if (e0 >= total) break;
+    const uint32_t e = e0 + gi;
+    const bool valid = grouped && e < total;
     const size_t pos = seg + e;
     double px = 0.0, py = 0.0;
     int32_t b = 0, end = 0;
@@ -608,18 +631,16 @@ __device__ uint64_t drain_own_queue(const RangeArgs& a, const uint32_t& lcount) 
       }
     }
     bool hit = false;
-    for (int32_t t = b + g;; t += kTestGroup) {
-      const uint64_t hb = __ballot(hit);  // all lanes: the loop is wave-uniform
-      const bool mine = t < end && !(hb & gmask);
+    for (int32_t t = b + (int32_t)g;; t += (int32_t)G) {
+      const uint64_t hb = __ballot(hit);
+      const bool mine = valid && t < end && !(hb & gmask);
       if (!__ballot(mine)) break;  // every group of the wave is done
       if (mine) hit = test_object<POLY>(a, px, py, a.cand_off ? a.cand_list[t] : t);
     }
-    const bool ghit = (__ballot(hit) & gmask) != 0;
-    const uint64_t won = __ballot(valid && g == 0 && ghit);
-    if (valid && g == 0 && ghit) {
-      const uint32_t i = a.queue[pos];
-      bitmap_or(a.bitmap, i);
-    }
+    const uint64_t hm = __ballot(hit) & gmask;
+    const bool rec = hit && lane == (uint32_t)__builtin_ctzll(hm);  // one recorder per point
+    const uint64_t won = __ballot(rec);
+    if (rec) bitmap_or(a.bitmap, a.queue[pos]);
     hits += (uint64_t)__popcll(won);
   }
   return hits;
@@ -636,7 +657,7 @@ __device__ __forceinline__ bool span_maybe(const RangeArgs& a, double px, double
   return !in_grid || (px >= a.sx_lo && px < a.sx_hi && py >= a.sy_lo && py < a.sy_hi);
 }
 
-// dynamic-LDS header of range_kernel: lcount, pad, sh[kBlock/64], sm[kBlock/64] (16 B multiple)
+// dynamic-LDS header of range_kernel: lcount, pad, drain cursor, pad, sh[kBlock/64], sm[kBlock/64] (16 B multiple)
 constexpr int kRangeHdrWords = 4 + 2 * 2 * (kBlock / 64);
 #ifndef GF_RANGE_WAVES
 #define GF_RANGE_WAVES 1
@@ -657,7 +678,10 @@ __device__ __forceinline__ void range_body(const RangeArgs& a) {
   RangeLds L{nullptr, nullptr, nullptr, nullptr, nullptr};
   WaveQ wq{nullptr, nullptr, 0u, 0u, nullptr, 0u, (uint32_t)t0, (uint32_t)tstride};
   if (DEFER || TABLE) {
-    if (threadIdx.x == 0) lcount = 0u;
+    if (threadIdx.x == 0) {
+      lcount = 0u;
+      lds_base[2] = 0u;  // drain_own_queue's cursor
+    }
     if (TABLE) {
       const int n = a.grid_n;
       uint32_t* lr = lds;
@@ -724,14 +748,17 @@ __device__ __forceinline__ void range_body(const RangeArgs& a) {
     range_load<1, false>(T, a, nfull, tstride);
     range_stage<TABLE, POLY, DEFER, 1, false>(a, L, T, nfull, Tn, nfull, tstride, hits, mult, &lcount, wq);
   }
-  if (DEFER == 1) hits += drain_own_queue<POLY>(a, lcount);
+  const uint32_t dl = (uint32_t)a.drain_lanes;  // testing: 0 = every lane drains
+  const bool drainer = dl == 0 || (threadIdx.x & 63) < dl;
+  if (DEFER == 1 && drainer) hits += drain_own_queue<POLY>(a, lcount, &lds_base[2]);
   if (DEFER == 3) {
     if (wq.cnt > 0) waveq_round<POLY>(a, L, wq, wq.cnt, hits, &lcount);
     // the ring's tiles to global memory (before the block's candidate tests OR into them)
     const uint32_t lane = threadIdx.x & 63, held = wq.ntile < (uint32_t)kWaveRing ? wq.ntile : kWaveRing;
+    wave_lds_sync();  // ring words written by lane 0 and OR-ed by every lane, read by lane `held`
     if (lane < held) ring_store(a, wq, wq.ntile - held + lane);
 #if GF_RANGE_EXP != 3 && GF_RANGE_EXP != 4  // experiment builds: 3 no candidate tests, 4 nor their queue
-    hits += drain_own_queue<POLY>(a, lcount);
+    if (drainer) hits += drain_own_queue<POLY>(a, lcount, &lds_base[2]);
 #endif
   }
   // per-block partial counts (plain stores; summed by range_finalize)

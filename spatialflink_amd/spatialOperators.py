@@ -218,6 +218,10 @@ class _RangeBase(SpatialOperator):
             if tuning is not None:
                 _lib.check(_lib.lib().gf_range_plan_set_tuning(plan, int(tuning[0]), int(tuning[1])), None,
                            "gf_range_plan_set_tuning")
+            lanes = getattr(self, "drain_lanes", None)  # testing: gf_range_plan_set_drain_lanes
+            if lanes is not None:
+                _lib.check(_lib.lib().gf_range_plan_set_drain_lanes(plan, int(lanes)), None,
+                           "gf_range_plan_set_drain_lanes")
         return plan
 
     def __del__(self):

@@ -284,6 +284,38 @@ def test_range_table_defer_modes(sf, oracle_mod, mode):
     np.testing.assert_array_equal(res.indices().astype(np.int64), exp)
 
 
+@pytest.mark.parametrize("lanes", [1, 3, 37, 63])
+def test_range_drain_partial_waves(sf, oracle_mod, lanes):
+    """The block-end candidate drain (drain_own_queue, DEFER 1 and 3) run by only the first
+    `lanes` lanes of every wave (gf_range_plan_set_drain_lanes): its points come from a block
+    cursor taken by the active lanes, groups form among them and a point's hit is recorded by the
+    lowest active lane of its group that found it -- identical results for any exec mask
+    (safe by construction, not by its calling context).  The C3 shape
+    (generateQueryPolygons squares, PointPolygonRangeQuery.java:170-204) and a point query set."""
+    n = 500
+    g = sf.UniformGrid(n, *BEIJING)
+    og = oracle_mod.grid(n, *BEIJING)
+    raw = oracle_mod.generate_query_polygons(1000, 115.5, 39.6, 117.6, 41.1)
+    polys = [sf.Polygon(p, g) for p in raw]
+    x, y = oracle_mod.java_random_points(35, 600_000, 115.4, 117.7, 39.5, 41.2)
+    x[:5] = np.nan
+    w = win(sf, x, y)
+    exp = oracle_mod.range_ppoly(og, x, y, oracle_mod.Polygons(raw), 0.001)
+    for mode in (1, 3):
+        op = sf.PointPolygonRangeQuery(conf(sf), g)
+        op.tuning = (0, mode)
+        op.drain_lanes = lanes
+        res = op.run(w, polys, 0.001)
+        np.testing.assert_array_equal(res.indices().astype(np.int64), exp, err_msg=f"mode {mode}")
+        assert res.count() == len(exp)
+    qx, qy = oracle_mod.java_random_points(36, 300, 115.5, 115.6, 40.0, 40.4)
+    op = sf.PointPointRangeQuery(conf(sf), g)
+    op.tuning = (0, 3)
+    op.drain_lanes = lanes
+    res = op.run(w, [sf.Point(str(i), qx[i], qy[i], 0, g) for i in range(len(qx))], 0.004)
+    np.testing.assert_array_equal(res.indices().astype(np.int64), oracle_mod.range_pp(og, x, y, qx, qy, 0.004))
+
+
 def _ulps(v, k):
     for _ in range(abs(k)):
         v = np.nextafter(v, np.inf if k > 0 else -np.inf)

@@ -84,3 +84,56 @@ def test_range_finalize_handoff_is_write_through(tmp_path):
     asm = device_asm("k_range.hip", tmp_path)
     body = function_body(asm, "_ZN2gf12range_kernelILi1ELi1ELi3ELi2E")
     check_handoff(body, 2)  # the block's two partial counts
+
+
+def _after_barrier(body, k):
+    """index of the first s_barrier at or after k whose preceding non-comment lines (within 12)
+    hold s_waitcnt vmcnt(0)"""
+    for j in range(k, len(body)):
+        if body[j].startswith("s_barrier"):
+            prev = [b for b in body[max(0, j - 12):j] if b and not b.startswith(";")]
+            if any(b.startswith("s_waitcnt") and "vmcnt(0)" in b for b in prev):
+                return j
+    return None
+
+
+@pytest.mark.timeout(600)
+def test_range_drain_and_wave_queue_handoffs(tmp_path):
+    """VERDICT r05 item 2.  (a) drain_own_queue's hand-off is the block queue in GLOBAL memory:
+    s_waitcnt vmcnt(0) -> s_barrier, then the LDS cursor's atomic (ds_add_rtn, the active lanes'
+    points), and only then the queue's global loads -- in the C3 kernel (DEFER 3) and in the
+    deferred-test kernel (DEFER 1).  (b) Every intra-wave LDS hand-off of the C3 stream (the span
+    queue read by other lanes, the bitmap-word ring) carries a wave barrier (wave_lds_sync): the
+    compiler may not move a lane's read of a slot another lane wrote above that write."""
+    asm = device_asm("k_range.hip", tmp_path)
+    for name, min_wb in (("_ZN2gf12range_kernelILi1ELi1ELi3ELi2E", 3), ("_ZN2gf12range_kernelILi1ELi1ELi1E", 0)):
+        body = function_body(asm, name)
+        # the drain: the LAST vmcnt(0) + s_barrier pair followed by the cursor atomic
+        found = False
+        for k in range(len(body)):
+            j = _after_barrier(body, k)
+            if j is None:
+                break
+            rest = body[j + 1:]
+            cur = next((i for i, b in enumerate(rest) if b.startswith("ds_add_rtn_u32")), None)
+            if cur is not None and not any(b.startswith("global_load") for b in rest[:cur]):
+                glb = next((i for i, b in enumerate(rest) if b.startswith("global_load")), None)
+                assert glb is not None and glb > cur
+                found = True
+                break
+            k = j + 1
+        assert found, f"{name}: no vmcnt(0) -> s_barrier -> cursor atomic -> queue loads drain"
+        assert sum(ln == "; wave barrier" for ln in body) >= min_wb, name
+
+
+@pytest.mark.timeout(600)
+def test_join_pair_buffers_carry_wave_barriers(tmp_path):
+    """The join probes' per-wave pair buffers (written at ballot ranks, read by other lanes at the
+    flush) and the windowed band's point queue are intra-wave LDS hand-offs: wave barriers in
+    the band probe (both modes) and the row probe."""
+    asm = device_asm("k_join.hip", tmp_path)
+    for mode in (0, 1):
+        body = function_body(asm, f"_ZN2gf22join_band_probe_kernelILi{mode}E")
+        assert sum(ln == "; wave barrier" for ln in body) >= 3, mode
+    body = function_body(asm, "_ZN2gf21join_row_probe_kernelILi0ELi1E")
+    assert any(ln == "; wave barrier" for ln in body)

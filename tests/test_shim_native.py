@@ -771,6 +771,8 @@ def test_java_call_sequence_sharded_knn(shim, oracle_mod, batch):
                 x = np.concatenate([x, np.full(stacked, QPOINT[0])]); y = np.concatenate([y, np.full(stacked, QPOINT[1])])
             ids = (rng.permutation(len(x)) % max(1, len(x) * 2 // 3)).astype(np.int64)
             strs = [b"v%d" % i if i % 5 else b"%d" % i for i in ids.tolist()]
+            if stacked:  # exact distance ties: broken by dictionary id on a rank (arrival order, as the
+                strs = [b"%d" % i for i in ids.tolist()]  # reference's queue), so decimals here (by value)
             S.calls.clear()
             keys = _intern(S, ctx, strs)
             t = i64()

@@ -1101,6 +1101,9 @@ def bench_csv(args, geojson=False):
     geo_pool_lines = _geojson_pool_baseline(args, host_texts[(args.steps - 1) % 2][0]) if (
         geojson and not args.no_cpu_baseline) else None
     ctx = _lib.context(0)
+    if geojson:  # the member location: the wave-per-line scan (default) or the r05 lane locator
+        _lib.check(L.gf_ctx_set_flag(ctx.handle, _lib.FLAG_GEOJSON_LANE, int(args.geojson_locator == "lane")),
+                   ctx.handle, "flag")
     grid = sf.UniformGrid(100, *BEIJING)
     texts = [(t_[0], t_[1], t_[2], t_[3], device_text(t_[0])) for t_ in host_texts]
     nbytes = len(texts[0][0])
@@ -1130,6 +1133,13 @@ def bench_csv(args, geojson=False):
         parse(i)
         _lib.check(L.gf_range_run(h, C.byref(pts), bitmap.data_ptr(), None, counts.data_ptr()), ctx.handle, "range")
 
+    # the context's FIRST call (no mean line length yet: the staging is sized from the format's
+    # default -- ADVICE r05), timed on its own
+    torch.cuda.synchronize()
+    tcold = time.perf_counter()
+    parse(0)
+    torch.cuda.synchronize()
+    cold_ms = 1000.0 * (time.perf_counter() - tcold)
     for i in range(args.warmup):
         step(i)
     torch.cuda.synchronize()
@@ -1195,7 +1205,9 @@ def bench_csv(args, geojson=False):
             lambda R: all(np.array_equal(R[k_][0], ex) and np.array_equal(R[k_][1], ey) for k_ in R))
     avg_parse = pms / 1000.0 / max(pcnt, 1)
     _line(("GeoJSON" if geojson else "CSV") + " ingest + point-point range", n * args.steps / elapsed, "lines/s",
-          args.steps, args.warmup, elapsed, "csv_parse_kernel" + (" (GeoJSON lines)" if geojson else ""),
+          args.steps, args.warmup, elapsed,
+          ("geojson_wave_kernel" if args.geojson_locator == "wave" else "csv_parse_kernel (GeoJSON lines)")
+          if geojson else "csv_parse_kernel",
           float(nbytes + 40 * n), avg_parse,
           {"config": {"workload": f"{'geojson' if geojson else 'csv'}_{n // 1_000_000}Mlines_range_r{args.radius}_grid100",
                       "lines": n,
@@ -1204,7 +1216,9 @@ def bench_csv(args, geojson=False):
                          "range_kernel_us": round(rms * 1000.0 / max(rcnt, 1), 2),
                          "ingest_call_us": round(ingest_s * 1e6, 2),
                          "ingest_lines_per_s": round(n / ingest_s, 1),
-                         "ingest_text_GBps": round(nbytes / ingest_s / 1e9, 2)},
+                         "ingest_text_GBps": round(nbytes / ingest_s / 1e9, 2),
+                         "cold_first_call_ms": round(cold_ms, 3)},
+           **({"geojson_locator": args.geojson_locator} if geojson else {}),
            "cpu_baseline": cpu, "verified_vs_oracle": verified})
 
 
