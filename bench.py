@@ -218,7 +218,7 @@ def main():
     ap.add_argument("--clustered", action="store_true",
                     help="BASELINE.md section 3 clustered variant: 80%% of the points in 8 Gaussian hot spots (sigma 0.01)")
     ap.add_argument("--no-verify", action="store_true")
-    ap.add_argument("--geojson-locator", default="wave", choices=("wave", "lane"),
+    ap.add_argument("--geojson-locator", default="lane", choices=("lane", "wave"),
                     help="geojson: members located by the wave-per-line scan or the r05 one-lane-per-line locator")
     ap.add_argument("--windows", type=int, default=4, help="distinct resident windows cycled through")
     ap.add_argument("--timing-period", type=int, default=5,

@@ -142,15 +142,15 @@ const char* gf_ctx_last_error(gf_ctx* ctx);
  * (no one-pass locator); the results are the same.
  * GF_FLAG_JOIN_STREAM: 1 = gf_join_pp's fine path buckets only the query side and streams the
  * ordinary points in input order (an experiment the default path is measured against).
- * GF_FLAG_GEOJSON_LANE: 1 = gf_geojson_parse locates members one line per lane (the r05 locator)
- * instead of the wave-per-line scan; the results are the same.
+ * GF_FLAG_GEOJSON_WAVE: 1 = gf_geojson_parse locates members with the wave-per-line structural
+ * scan (r06, measured slower: DESIGN.md §3 GeoJSON) instead of one line per lane; same results.
  * GF_FLAG_GEOJSON_CHECK: 1 = gf_geojson_parse runs the wave scan AND the lane locator on every
  * staged line and counts their differences (gf_geojson_check_counts); results as the default. */
 #define GF_FLAG_JOIN_LEGACY 1
 #define GF_FLAG_JOIN_COARSE 2
 #define GF_FLAG_GEOJSON_WALK 4
 #define GF_FLAG_JOIN_STREAM 8
-#define GF_FLAG_GEOJSON_LANE 16
+#define GF_FLAG_GEOJSON_WAVE 16
 #define GF_FLAG_GEOJSON_CHECK 32
 int gf_ctx_set_flag(gf_ctx* ctx, int flag, int value);
 /* GF_FLAG_GEOJSON_CHECK's counts since the last read (then zeroed), after a sync: out[0] lines

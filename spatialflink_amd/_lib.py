@@ -34,7 +34,7 @@ METRIC_HYPOT = 1
 FLAG_JOIN_LEGACY = 1
 FLAG_JOIN_COARSE = 2
 FLAG_GEOJSON_WALK = 4
-FLAG_GEOJSON_LANE = 16
+FLAG_GEOJSON_WAVE = 16
 FLAG_GEOJSON_CHECK = 32
 FLAG_JOIN_STREAM = 8
 (K_KNN_SCAN, K_KNN_SAMPLE, K_KNN_SELECT, K_RANGE_SCAN, K_ASSIGN, K_JOIN_PROBE, K_RANGE_TEST, K_JOIN_BUCKET,
@@ -236,6 +236,8 @@ def lib():
             "gf_knn_exchange_group": ([i32, P, P, i32, P, i32, P], C.c_int),
         }
         for name, (argt, rest) in sig.items():
+            if os.environ.get("GF_LIB_PATH") and not hasattr(L, name):
+                continue  # an older build under A/B (tools/gpu_ab.sh): entries added since are absent
             fn = getattr(L, name)
             fn.argtypes = argt
             fn.restype = rest

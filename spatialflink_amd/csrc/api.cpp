@@ -395,7 +395,7 @@ extern "C" int gf_ctx_set_flag(gf_ctx* ctx, int flag, int value) {
   if (flag == GF_FLAG_JOIN_COARSE) { ctx->join_coarse = value != 0; return GF_OK; }
   if (flag == GF_FLAG_GEOJSON_WALK) { ctx->geojson_walk = value != 0; return GF_OK; }
   if (flag == GF_FLAG_JOIN_STREAM) { ctx->join_stream = value != 0; return GF_OK; }
-  if (flag == GF_FLAG_GEOJSON_LANE) { ctx->geojson_lane = value != 0; return GF_OK; }
+  if (flag == GF_FLAG_GEOJSON_WAVE) { ctx->geojson_wave = value != 0; return GF_OK; }
   if (flag == GF_FLAG_GEOJSON_CHECK) {
     if (value && !ctx->geojson_check) {
       GF_HIP_CHECK(ctx, hipMalloc(&ctx->geojson_check, 4 * sizeof(unsigned long long)));

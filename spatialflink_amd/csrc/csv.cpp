@@ -165,7 +165,7 @@ extern "C" int gf_geojson_parse(gf_ctx* ctx, gf_objid_dict* dict, const char* te
   }
   a.date_fmt = sc->date_format;
   a.geo_fast = !ctx->geojson_walk;
-  a.geo_wave = !ctx->geojson_walk && !ctx->geojson_lane;
+  a.geo_wave = !ctx->geojson_walk && (ctx->geojson_wave || ctx->geojson_check);
   a.geo_check = ctx->geojson_check;
   a.value_lines = sc->value_lines;
   a.tz_off_ms = (int64_t)sc->tz_offset_minutes * 60000;

@@ -107,6 +107,11 @@
 #else
 #define GF_BT_IF_GF_BAND_LDS_KB ""
 #endif
+#ifdef GF_BAND_THREADS
+#define GF_BT_IF_GF_BAND_THREADS " GF_BAND_THREADS=" GF_BT_STR(GF_BAND_THREADS)
+#else
+#define GF_BT_IF_GF_BAND_THREADS ""
+#endif
 #ifdef GF_BAND_MINBLK
 #define GF_BT_IF_GF_BAND_MINBLK " GF_BAND_MINBLK=" GF_BT_STR(GF_BAND_MINBLK)
 #else
@@ -155,7 +160,7 @@ const char* GF_BT_CAT(build_tag_, GF_TU_NAME)() {
       GF_BT_IF_GF_SCAT_EXP_NOSTORE GF_BT_IF_GF_BAND_EXP GF_BT_IF_GF_GEO_UNROLL GF_BT_IF_GF_GEO_LINES
           GF_BT_IF_GF_BUCKET_BITS GF_BT_IF_GF_JOIN_BUCKET_U GF_BT_IF_GF_BAND_BUF GF_BT_IF_GF_BAND_R
               GF_BT_IF_GF_BAND_R1 GF_BT_IF_GF_BAND_PAIR GF_BT_IF_GF_BAND_FLATSEL GF_BT_IF_GF_BAND_LDS_KB
-                  GF_BT_IF_GF_BAND_MINBLK GF_BT_IF_GF_BAND_QUEUE GF_BT_IF_GF_BAND_BALANCED
+                  GF_BT_IF_GF_BAND_MINBLK GF_BT_IF_GF_BAND_THREADS GF_BT_IF_GF_BAND_QUEUE GF_BT_IF_GF_BAND_BALANCED
                       GF_BT_IF_GF_RANGE_WAVEQ GF_BT_IF_GF_RANGE_VEC GF_BT_IF_GF_RANGE_TEST_GROUP
                           GF_BT_IF_GF_RANGE_WAVES GF_BT_IF_GF_RANGE_U;
 }

@@ -37,7 +37,7 @@ struct gf_ctx {
   int join_coarse = 0;  // testing: the row path without sub-cells
   int join_stream = 0;  // experiment: the fine path's streaming probe (query side bucketed only)
   int geojson_walk = 0; // testing: every GeoJSON line takes the member-by-member walk
-  int geojson_lane = 0; // GeoJSON: the r05 lane locator instead of the wave scan
+  int geojson_wave = 0; // GeoJSON: the wave-per-line scan instead of the lane locator (measured slower)
   unsigned long long* geojson_check = nullptr;  // GF_FLAG_GEOJSON_CHECK: the 4 counters (device; null: off)
   int64_t csv_mean_line[2] = {0, 0};  // per format (CSV, GeoJSON): the last call's mean line length (sizes the next one's LDS staging)
   int join_async_done = 0;  // gf_join_pp_async: the packing kernel wrote the count

@@ -433,10 +433,17 @@ __device__ __forceinline__ bool geo_wave_scan(GF_LDS_PTR(char) lp, int32_t len, 
         if (lowd && __ballot(kend && crole != JR_NONE)) {
           const int32_t kst = (qb ? c0 + ql : str_open) + 1, klen = i - kst;
           uint64_t hi = 0, lo = 0;
-          if (kend && crole != JR_NONE && klen <= 16) {
-            for (int32_t q = kst; q < i; ++q) {
+          if (kend && crole != JR_NONE && klen <= 16) {  // the key's last <= 16 bytes (16 independent reads)
+            uint32_t kb[16];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+              const int32_t x = i - 16 + q;
+              kb[q] = x >= kst ? (uint32_t)(uint8_t)lp[x] : 0u;
+            }
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
               hi = (hi << 8) | (lo >> 56);
-              lo = (lo << 8) | (uint8_t)lp[q];
+              lo = (lo << 8) | kb[q];
             }
           }
           // (a key of <= 8 bytes leaves hi 0: the short names compare lo only)
@@ -514,11 +521,15 @@ __device__ __forceinline__ bool geo_wave_scan(GF_LDS_PTR(char) lp, int32_t len, 
         const bool ndig = nxt - '0' < 10u, pdig = prv - '0' < 10u, pexp = (prv | 0x20u) == 'e';
         if (!num) {
           if (i == ts) {  // true / false / null, and nothing else
-            const int wl = fc == 'f' ? 5 : 4;
-            const char* wd = fc == 't' ? "true" : fc == 'f' ? "false" : "null";
-            bool w = (fc == 't' || fc == 'f' || fc == 'n') && i + wl <= len;
-            for (int q = 1; w && q < wl; ++q) w = (uint8_t)lp[i + q] == (uint8_t)wd[q];
-            w = w && !(i + wl < len && (wtab[(uint8_t)lp[i + wl]] & WB_TOK));
+            // the word's bytes after the first, and the byte after it (a blank past the line)
+            uint32_t wb[5];
+#pragma unroll
+            for (int q = 0; q < 5; ++q) wb[q] = i + 1 + q < len ? (uint32_t)(uint8_t)lp[i + 1 + q] : 32u;
+            const uint32_t w4 = wb[0] | wb[1] << 8 | wb[2] << 16, w5 = w4 | wb[3] << 24;  // little-endian
+            const bool w = fc == 't' ? w4 == ('r' | 'u' << 8 | 'e' << 16) && !(wtab[wb[3]] & WB_TOK)
+                         : fc == 'n' ? w4 == ('u' | 'l' << 8 | 'l' << 16) && !(wtab[wb[3]] & WB_TOK)
+                         : fc == 'f' ? w5 == ('a' | 'l' << 8 | 's' << 16 | (uint32_t)'e' << 24) && !(wtab[wb[4]] & WB_TOK)
+                         : false;
             bad = !w;
           }
         } else {  // -?(0|[1-9][0-9]*)(.[0-9]+)?([eE][+-]?[0-9]{1,2})?, shorter than 19 bytes

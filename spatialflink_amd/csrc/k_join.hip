@@ -1260,7 +1260,11 @@ hipError_t launch_join_stream(gf_ctx* ctx, const JoinRowArgs& a) {
 // no device atomic unless the region is full (then the dense overflow area).  Per-wave output
 // chunks cost one device atomic each on ONE counter: ~20K of them serialised at the memory side
 // (the row probe: 240 us with block chunks, 361 us with wave chunks).
-constexpr int kBandThreads = 1024, kBandWaves = kBandThreads / 64;
+#ifndef GF_BAND_THREADS  // experiment builds: a smaller block (with GF_BAND_LDS_KB / GF_BAND_MINBLK)
+#define GF_BAND_THREADS 1024
+#endif
+constexpr int kBandThreads = GF_BAND_THREADS, kBandWaves = kBandThreads / 64;
+static_assert(kBandThreads % 64 == 0 && kBandThreads <= 1024, "whole waves");
 typedef const uint32_t __attribute__((address_space(3)))* lds_u32;
 #ifndef GF_BAND_BUF
 #define GF_BAND_BUF 512
@@ -1554,7 +1558,7 @@ __device__ __forceinline__ void join_region_prep(const JoinFixup& f, uint64_t* w
 }
 
 template <int MODE>
-__global__ __launch_bounds__(kBandThreads, 4 * GF_BAND_MINBLK) void join_band_probe_kernel(JoinRowArgs a) {
+__global__ __launch_bounds__(kBandThreads, (kBandWaves * GF_BAND_MINBLK + 3) / 4) void join_band_probe_kernel(JoinRowArgs a) {
   extern __shared__ __attribute__((aligned(16))) char lds_base[];
   BandHdr& hd = *reinterpret_cast<BandHdr*>(lds_base);
   constexpr int kR = MODE == 0 ? kBandRound : kBandRound1;  // candidates per lane per walk round

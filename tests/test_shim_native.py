@@ -801,8 +801,8 @@ def test_java_call_sequence_sharded_knn(shim, oracle_mod, batch):
             t = i64()
             for _ in range(2 * batch):
                 _ok(S, ctx, S.shim_knn_sharded_enqueue(plan, _a(x), _a(y), _a(keys), 1000, base, C.byref(t)), "fill")
-            assert S.shim_knn_sharded_enqueue(plan, _a(x), _a(y), _a(keys), 1000, base, C.byref(t)) == -1
             first = t.value - 2 * batch + 1
+            assert S.shim_knn_sharded_enqueue(plan, _a(x), _a(y), _a(keys), 1000, base, C.byref(t)) == -1
             od, oi, ow, m = np.zeros(k), np.zeros(k, np.int64), np.zeros(k, np.int32), i32()
             for tw in range(first, first + 2 * batch):
                 _ok(S, ctx, S.shim_knn_sharded_result(plan, tw, _a(od), _a(oi), _a(ow), C.byref(m)), "drain")

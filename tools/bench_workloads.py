@@ -1101,8 +1101,8 @@ def bench_csv(args, geojson=False):
     geo_pool_lines = _geojson_pool_baseline(args, host_texts[(args.steps - 1) % 2][0]) if (
         geojson and not args.no_cpu_baseline) else None
     ctx = _lib.context(0)
-    if geojson:  # the member location: the wave-per-line scan (default) or the r05 lane locator
-        _lib.check(L.gf_ctx_set_flag(ctx.handle, _lib.FLAG_GEOJSON_LANE, int(args.geojson_locator == "lane")),
+    if geojson and args.geojson_locator == "wave":  # (default: one line per lane; older builds lack the flag)
+        _lib.check(L.gf_ctx_set_flag(ctx.handle, _lib.FLAG_GEOJSON_WAVE, int(args.geojson_locator == "wave")),
                    ctx.handle, "flag")
     grid = sf.UniformGrid(100, *BEIJING)
     texts = [(t_[0], t_[1], t_[2], t_[3], device_text(t_[0])) for t_ in host_texts]
