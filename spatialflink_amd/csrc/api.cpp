@@ -240,7 +240,7 @@ static const UnitTag kUnitTags[] = {
     {"k_objid.hip", build_tag_k_objid_hip},
 };
 // run-time A/B knobs (valid alternative paths, never wrong results): reported, not refused
-static const char* const kEnvKnobs[] = {"GF_K2_LSD", "GF_JOIN_BAND_PER_CU", "GF_JOIN_ROWPROBE",
+static const char* const kEnvKnobs[] = {"GF_K2_LSD", "GF_K2_SELFCOUNT", "GF_JOIN_BAND_PER_CU", "GF_JOIN_ROWPROBE",
                                         "GF_JOIN_CHUNK", "GF_RADIX_NT"};
 }  // namespace gf
 
@@ -577,6 +577,10 @@ static int bucket_rows(gf_ctx* ctx, const gf_grid* g, const gf_points* pts, uint
   b.M = U32(o_mb);
   b.Ms = U32(o_msb);
   b.cstart = cell_start;
+  // (GF_K2_SELFCOUNT=1, A/B only: a one-segment row's scatter block counts its own columns instead
+  // of the histogram kernel -- r06 A/B 0.2028 / 0.1997 vs 0.1988 / 0.1991 ms, profiles/r06_k2b_ab.jsonl)
+  const char* sce = std::getenv("GF_K2_SELFCOUNT");
+  b.self_count = sce && *sce == '1';
   GF_HIP_CHECK(ctx, launch_radix(ctx, 3, b, (int)ub));
   if ((st = lookback_state(ctx, scan1_blocks(matB), &es))) return st;
   GF_HIP_CHECK(ctx, launch_scan1(ctx->stream, U32(o_mb), matB, U32(o_msb), nullptr, 0, 0, es));

@@ -361,6 +361,7 @@ struct RadixArgs {
   // position's row) and pass B reads those (kin16): 2 B instead of 4 per point written and read twice
   uint16_t* kout16;
   const uint16_t* kin16;
+  int32_t self_count;       // pass B: a one-segment row's scatter block counts its columns (no histogram read)
 };
 // scatter block size: 1024 threads (one 8192-point tile per block, one block per CU) or 512
 // (4096-point tiles, two blocks per CU: one block's LDS phases overlap the other's memory);

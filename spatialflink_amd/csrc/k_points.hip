@@ -254,7 +254,7 @@ __global__ __launch_bounds__(kRadixThreads) void radix_seg_hist_kernel(RadixArgs
     for (uint32_t d = threadIdx.x; d < D; d += kRadixThreads) a.M[(size_t)blockIdx.x * D + d] = 0u;
     return;
   }
-  if (rs.nseg == 1) {
+  if (rs.nseg == 1 && a.self_count) {
     // r06: a one-segment row (every row of a uniform 10M-point window on 500 x 500) is sorted by
     // its own scatter block, which counts its columns itself (radix_scatter_kernel): no histogram
     // read here.  Its entries only carry the row's total (column 0) so that the ONE scan of M still
@@ -389,7 +389,7 @@ __global__ __launch_bounds__(NT, MINW) void radix_scatter_kernel(RadixArgs a) {
     beg = rs.beg;
     end = rs.end;
     const size_t m0 = (size_t)rs.base * D;
-    if (rs.nseg == 1) {
+    if (rs.nseg == 1 && a.self_count) {
       // r06: a one-segment row counts its own columns (the histogram kernel skipped it): an LDS
       // histogram of the row's u16 columns, a block scan -> each column's first slot
       for (uint32_t d = threadIdx.x; d < D; d += NT) gc[d] = 0u;
