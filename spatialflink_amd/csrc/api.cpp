@@ -240,7 +240,7 @@ static const UnitTag kUnitTags[] = {
     {"k_objid.hip", build_tag_k_objid_hip},
 };
 // run-time A/B knobs (valid alternative paths, never wrong results): reported, not refused
-static const char* const kEnvKnobs[] = {"GF_K2_LSD", "GF_K2_SELFCOUNT", "GF_JOIN_BAND_PER_CU", "GF_JOIN_ROWPROBE",
+static const char* const kEnvKnobs[] = {"GF_K2_LSD", "GF_K2_SELFCOUNT", "GF_K2_ROWSORT", "GF_JOIN_BAND_PER_CU", "GF_JOIN_ROWPROBE",
                                         "GF_JOIN_CHUNK", "GF_RADIX_NT"};
 }  // namespace gf
 
@@ -525,7 +525,8 @@ extern "C" int gf_assign_cells(gf_ctx* ctx, const gf_grid* g, const gf_points* p
 // row stably by column -- over row SEGMENTS, so each block's output lies inside its row's range
 // (row-local writes instead of 512 runs spread over the whole output), only the permutation is
 // written, and the cells' starts come from pass B's own scan (no key read-back, no bounds pass).
-constexpr int kRowSeg = 32768;  // points per row segment (a uniform 10M-point window on 500 x 500: one per row)
+constexpr int kRowSeg = 32768;  // points per row segment (a uniform 10M-point window on 500 x 500: one per row,
+                                // sorted whole by radix_row_sort_kernel, whose capacity this is)
 static int bucket_rows(gf_ctx* ctx, const gf_grid* g, const gf_points* pts, uint32_t* perm, uint32_t* cell_start,
                        int blocks) {
   const int64_t n = pts->n;
@@ -581,6 +582,11 @@ static int bucket_rows(gf_ctx* ctx, const gf_grid* g, const gf_points* pts, uint
   // of the histogram kernel -- r06 A/B 0.2028 / 0.1997 vs 0.1988 / 0.1991 ms, profiles/r06_k2b_ab.jsonl)
   const char* sce = std::getenv("GF_K2_SELFCOUNT");
   b.self_count = sce && *sce == '1';
+  // r06: one-segment rows sorted whole, each by one block with its output staged in LDS
+  // (radix_row_sort_kernel); GF_K2_ROWSORT=0 (A/B only) leaves them to the segment path
+  const char* rse = std::getenv("GF_K2_ROWSORT");
+  b.rowsort = !(rse && *rse == '0') && !b.self_count && kRowSeg <= radix_row_sort_cap();
+  if (b.rowsort) GF_HIP_CHECK(ctx, launch_radix(ctx, 4, b, g->n + 1));
   GF_HIP_CHECK(ctx, launch_radix(ctx, 3, b, (int)ub));
   if ((st = lookback_state(ctx, scan1_blocks(matB), &es))) return st;
   GF_HIP_CHECK(ctx, launch_scan1(ctx->stream, U32(o_mb), matB, U32(o_msb), nullptr, 0, 0, es));

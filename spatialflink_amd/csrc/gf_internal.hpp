@@ -362,6 +362,7 @@ struct RadixArgs {
   uint16_t* kout16;
   const uint16_t* kin16;
   int32_t self_count;       // pass B: a one-segment row's scatter block counts its columns (no histogram read)
+  int32_t rowsort;          // pass B: one-segment rows sorted whole by radix_row_sort_kernel (the others by segments)
 };
 // scatter block size: 1024 threads (one 8192-point tile per block, one block per CU) or 512
 // (4096-point tiles, two blocks per CU: one block's LDS phases overlap the other's memory);
@@ -369,6 +370,7 @@ struct RadixArgs {
 int radix_threads();
 inline int radix_tile() { return radix_threads() / 64 * 512; }
 inline int radix_max_blocks(int num_cus) { return num_cus * (1024 / radix_threads()); }
+int radix_row_sort_cap();  // k_points.hip: the largest row radix_row_sort_kernel sorts whole
 constexpr int kMaxShardBands = 64;
 size_t radix_scatter_lds_bytes();
 hipError_t launch_gather_points(hipStream_t s, const gf_points& in, const uint32_t* perm, int64_t begin, int64_t m,

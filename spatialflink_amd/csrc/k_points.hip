@@ -254,7 +254,7 @@ __global__ __launch_bounds__(kRadixThreads) void radix_seg_hist_kernel(RadixArgs
     for (uint32_t d = threadIdx.x; d < D; d += kRadixThreads) a.M[(size_t)blockIdx.x * D + d] = 0u;
     return;
   }
-  if (rs.nseg == 1 && a.self_count) {
+  if (rs.nseg == 1 && (a.self_count || a.rowsort)) {
     // r06: a one-segment row (every row of a uniform 10M-point window on 500 x 500) is sorted by
     // its own scatter block, which counts its columns itself (radix_scatter_kernel): no histogram
     // read here.  Its entries only carry the row's total (column 0) so that the ONE scan of M still
@@ -386,10 +386,11 @@ __global__ __launch_bounds__(NT, MINW) void radix_scatter_kernel(RadixArgs a) {
     __shared__ RowSeg rs;
     row_segment(a, rs);
     if (rs.r == 0xFFFFFFFFu) return;  // block-uniform
+    if (rs.nseg == 1 && a.rowsort) return;  // sorted whole by radix_row_sort_kernel
     beg = rs.beg;
     end = rs.end;
     const size_t m0 = (size_t)rs.base * D;
-    if (rs.nseg == 1 && a.self_count) {
+    if (rs.nseg == 1 && a.self_count) {  // (GF_K2_SELFCOUNT=1 A/B; rowsort off)
       // r06: a one-segment row counts its own columns (the histogram kernel skipped it): an LDS
       // histogram of the row's u16 columns, a block scan -> each column's first slot
       for (uint32_t d = threadIdx.x; d < D; d += NT) gc[d] = 0u;
@@ -564,6 +565,129 @@ __global__ __launch_bounds__(NT, MINW) void radix_scatter_kernel(RadixArgs a) {
   }
 }
 
+// ---- row mode pass B, one-segment rows (r06) ---------------------------------------------------
+// A row of <= a.seg points (<= kRowSortCap; the rows of the K2 bench window -- 10M points over
+// the 357 occupied rows of the 500 x 500 grid -- hold ~28K) is sorted by column inside ONE
+// 1024-thread block, the row's output staged whole in LDS.  Wave w takes the w-th contiguous part
+// of the row (<= 32 elements per lane, every load in flight at once) and ranks its elements stably
+// per 64-element step (9 ballots; the step's leader of each column advances the wave's u16 count
+// of it); one block scan in (column, wave) order gives every (column, wave) its first row-local
+// slot -- and the row's cell starts; each element lands in the LDS copy of the row's permutation
+// at slot + its rank, and the row is written out contiguously.  The tile scatter
+// (radix_scatter_kernel) wrote ~8-point column runs per 4096-point tile (partial lines, written
+// by blocks of every XCD) and scanned 4096 counts per tile.  r06 A/B (profiles/r06_k2c_ab.jsonl):
+// the window 0.189 vs 0.196-0.202 ms.  Measured and not kept: the permutation stored straight from
+// the registers into the row's range (no staging: 24 KB of LDS, two 768-thread blocks per CU,
+// every row in one round) 120 vs 61 us -- the scattered 4-B stores cost more than the second
+// round of blocks; the steps' counts taken with LDS atomics, broadcast after the last step (no
+// wait per step) 63 vs 61 us.
+constexpr int kRowSortNT = 1024, kRowSortW = kRowSortNT / 64, kRowSortU = 32;
+constexpr int kRowSortCap = kRowSortNT * kRowSortU;  // >= api.cpp kRowSeg (checked there)
+size_t radix_row_sort_lds_bytes() { return (size_t)kRowSortCap * 4 + (size_t)kRowSortW * kRadixMaxDigits * 2; }
+int radix_row_sort_cap() { return kRowSortCap; }
+
+__global__ __launch_bounds__(kRowSortNT, 4) void radix_row_sort_kernel(RadixArgs a) {
+  extern __shared__ uint32_t rsm[];
+  uint32_t* const out = rsm;                                              // [cap] the row's permutation
+  uint16_t* const wc = reinterpret_cast<uint16_t*>(out + kRowSortCap);     // [W][512] counts -> slots
+  __shared__ uint32_t ws[kRowSortW];
+  const uint32_t r = blockIdx.x;
+  if (r > (uint32_t)a.gn) return;  // block-uniform
+  const uint32_t lo = a.MsA[(size_t)r * a.nblkA], hi = a.MsA[(size_t)(r + 1) * a.nblkA];
+  const uint32_t nr = hi - lo;
+  if (nr > (uint32_t)a.seg) return;  // a multi-segment row: radix_seg_hist / radix_scatter sort it
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint64_t below = (1ull << lane) - 1ull;
+  const uint32_t per = (nr + kRowSortW - 1) / kRowSortW;  // <= 64 * kRowSortU
+  const uint32_t wb = w * per < nr ? w * per : nr, we = wb + per < nr ? wb + per : nr;
+  for (uint32_t d = lane; d < (uint32_t)kRadixMaxDigits; d += 64) wc[w * kRadixMaxDigits + d] = 0;
+  uint32_t cr[kRowSortU];  // column | rank within the wave's column << 16
+  uint32_t v[kRowSortU];
+  if (we > wb) {  // wave-uniform: the part's columns, clamped addresses (all loads in flight)
+#pragma unroll
+    for (int u = 0; u < kRowSortU; ++u) {
+      const uint32_t j = wb + u * 64 + lane;
+      cr[u] = a.kin16[lo + (j < we ? j : we - 1)];
+    }
+  }
+  wave_lds_sync();
+#pragma unroll
+  for (int u = 0; u < kRowSortU; ++u) {  // stable ranks per 64-element step
+    if (wb + u * 64 >= we) break;  // wave-uniform
+    const bool valid = wb + u * 64 + lane < we;
+    const uint32_t d = cr[u] & (uint32_t)(kRadixMaxDigits - 1);
+    uint64_t peers = __ballot(valid);
+#pragma unroll
+    for (int b = 0; b < kRadixMaxBits; ++b) {
+      const uint64_t bal = __ballot((d >> b) & 1u);
+      peers &= ((d >> b) & 1u) ? bal : ~bal;
+    }
+    const bool lead = valid && (peers & below) == 0;
+    uint32_t base = 0;
+    if (lead) {
+      base = wc[w * kRadixMaxDigits + d];
+      wc[w * kRadixMaxDigits + d] = (uint16_t)(base + (uint32_t)__popcll(peers));
+    }
+    base = __shfl(base, valid ? __ffsll((unsigned long long)peers) - 1 : lane, 64);
+    cr[u] = d | (base + (uint32_t)__popcll(peers & below)) << 16;
+    wave_lds_sync();  // the next step's leaders read the counts other lanes wrote
+  }
+  if (we > wb) {  // the permutation entries (in flight during the scan)
+#pragma unroll
+    for (int u = 0; u < kRowSortU; ++u) {
+      const uint32_t j = wb + u * 64 + lane;
+      v[u] = a.vin[lo + (j < we ? j : we - 1)];
+    }
+  }
+  __syncthreads();
+  {  // exclusive scan of the counts in (column, wave) order: thread t owns column t / 2, waves
+     // 8 (t % 2) .. + 8
+    constexpr int PT = kRowSortW * kRadixMaxDigits / kRowSortNT;  // 8
+    const uint32_t d = threadIdx.x / 2, w0 = (threadIdx.x % 2) * PT;
+    uint32_t cnt[PT], run = 0;
+#pragma unroll
+    for (int q = 0; q < PT; ++q) {
+      cnt[q] = wc[(w0 + q) * kRadixMaxDigits + d];
+      run += cnt[q];
+    }
+    uint32_t inc = run;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t t = __shfl_up(inc, o, 64);
+      if (lane >= o) inc += t;
+    }
+    if (lane == 63) ws[w] = inc;
+    __syncthreads();
+    uint32_t before = inc - run;
+    for (int q = 0; q < w; ++q) before += ws[q];
+    if (w0 == 0) {  // the row's cells start at their columns' first slots
+      if (r < (uint32_t)a.gn) {
+        if (d < (uint32_t)a.gn) a.cstart[(size_t)r * a.gn + d] = lo + before;
+      } else if (d == 0) {
+        a.cstart[(size_t)a.gn * a.gn] = lo;
+        a.cstart[(size_t)a.gn * a.gn + 1] = (uint32_t)a.n;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < PT; ++q) {
+      wc[(w0 + q) * kRadixMaxDigits + d] = (uint16_t)before;
+      before += cnt[q];
+    }
+  }
+  __syncthreads();
+  if (we > wb) {
+#pragma unroll
+    for (int u = 0; u < kRowSortU; ++u) {  // each element at its (column, wave) slot + rank
+      if (wb + u * 64 + lane < we) {
+        const uint32_t d = cr[u] & 0xFFFFu;
+        out[wc[w * kRadixMaxDigits + d] + (cr[u] >> 16)] = v[u];
+      }
+    }
+  }
+  __syncthreads();
+  for (uint32_t p = threadIdx.x; p < nr; p += kRowSortNT) a.vout[lo + p] = out[p];  // contiguous
+}
+
 // cell_start straight from the sorted keys (no histogram, no scan): cell_start[b] = the first
 // position whose key is >= b, so position i (key[-1] = -1, key[n] = bins as sentinels) starts
 // every bucket b in (key[i-1], key[i]].  One wave per 1024 consecutive positions (16 per lane,
@@ -636,6 +760,9 @@ hipError_t launch_radix(gf_ctx* ctx, int stage, const RadixArgs& a, int blocks) 
       break;
     case 3:
       hipLaunchKernelGGL(radix_seg_hist_kernel, dim3(blocks), dim3(kRadixThreads), 0, s, a);
+      break;
+    case 4:  // blocks = rows (gn + 1)
+      hipLaunchKernelGGL(radix_row_sort_kernel, dim3(blocks), dim3(kRowSortNT), radix_row_sort_lds_bytes(), s, a);
       break;
     default: {  // cell_start[0 .. gn*gn + 1] of the sorted kout into a.M: one wave per 256 positions
       const int64_t waves = (a.n + 1 + 64 * kBoundsPer - 1) / (64 * kBoundsPer);

@@ -93,6 +93,9 @@ def bucket_expected(oracle_mod, og, gn, x, y):
     (511, 800_000, (115.3, 117.8, 39.5, 41.2), True), (300, 100, BEIJING, False),
     (23, 50, (115.3, 117.8, 39.5, 41.2), False),            # the smallest two-pass grid: fewer points than rows
     (64, 70_000, (116.39, 116.41, 39.5, 41.2), False),      # one column: every row one cell
+    # r06 whole-row sort (radix_row_sort_kernel): the bench window (~20K-point rows), and rows
+    # around the one-segment bound (32768: some rows sorted whole, the others by segments)
+    (500, 10_000_000, BEIJING, False), (100, 2_340_500, BEIJING, False),  # (71.4 occupied rows)
 ])
 def test_bucket_by_cell_exact(sf, oracle_mod, gn, n, box, clustered):
     g = sf.UniformGrid(gn, *BEIJING)
@@ -111,6 +114,24 @@ def test_bucket_by_cell_exact(sf, oracle_mod, gn, n, box, clustered):
     ep, es = bucket_expected(oracle_mod, og, gn, x, y)
     np.testing.assert_array_equal(perm, ep)
     np.testing.assert_array_equal(start, es)
+
+
+@pytest.mark.parametrize("rowsort", ["0", "1"])
+def test_bucket_row_sort_matches_segments(sf, oracle_mod, rowsort, monkeypatch):
+    """GF_K2_ROWSORT=0 (A/B knob: every row by segments) and the default whole-row sort give the
+    same exact permutation on a clustered window with one- and multi-segment rows."""
+    monkeypatch.setenv("GF_K2_ROWSORT", rowsort)
+    gn, n = 200, 2_000_000
+    g = sf.UniformGrid(gn, *BEIJING)
+    og = oracle_mod.grid(gn, *BEIJING)
+    x, y = oracle_mod.java_random_points(5, n, *BEIJING)
+    rng = np.random.default_rng(1)
+    h = rng.random(n) < 0.3
+    y = np.where(h, 40.3 + 0.002 * rng.standard_normal(n), y)  # two hot rows: multi-segment
+    perm, start = sf.bucket_by_cell(win(sf, x, y), g)
+    ep, es = bucket_expected(oracle_mod, og, gn, x, y)
+    np.testing.assert_array_equal(perm.cpu().numpy().view(np.uint32).astype(np.int64), ep)
+    np.testing.assert_array_equal(start.cpu().numpy().view(np.uint32).astype(np.int64), es)
 
 
 @pytest.mark.parametrize("gn", [500, 2048])
