@@ -240,7 +240,7 @@ static const UnitTag kUnitTags[] = {
     {"k_objid.hip", build_tag_k_objid_hip},
 };
 // run-time A/B knobs (valid alternative paths, never wrong results): reported, not refused
-static const char* const kEnvKnobs[] = {"GF_K2_LSD", "GF_K2_SELFCOUNT", "GF_K2_ROWSORT", "GF_JOIN_BAND_PER_CU", "GF_JOIN_ROWPROBE",
+static const char* const kEnvKnobs[] = {"GF_K2_LSD", "GF_K2_SELFCOUNT", "GF_K2_ROWSORT", "GF_K2_MERGE", "GF_JOIN_BAND_PER_CU", "GF_JOIN_ROWPROBE",
                                         "GF_JOIN_CHUNK", "GF_RADIX_NT"};
 }  // namespace gf
 
@@ -537,6 +537,7 @@ static int bucket_rows(gf_ctx* ctx, const gf_grid* g, const gf_points* pts, uint
   size_t o_k0 = ar.take<uint32_t>(n), o_k1 = ar.take<uint16_t>(n), o_v1 = ar.take<uint32_t>(n);
   size_t o_ma = ar.take<uint32_t>(matA), o_msa = ar.take<uint32_t>(matA + 1);
   size_t o_mb = ar.take<uint32_t>(matB), o_msb = ar.take<uint32_t>(matB + 1);
+  size_t o_flag = ar.take<uint32_t>(1);
   int st = 0;
   char* base = (char*)ctx_scratch(ctx, ar.off, &st);
   if (st) return st;
@@ -546,6 +547,15 @@ static int bucket_rows(gf_ctx* ctx, const gf_grid* g, const gf_points* pts, uint
   a.x = pts->x; a.y = pts->y; a.n = n;
   a.minX = g->minX; a.minY = g->minY; a.cl = g->cellLength; a.gn = g->n;
   a.bits = kRadixMaxBits; a.nblk = blocks; a.rowmode = 1;
+  // (GF_K2_SELFCOUNT=1, A/B only: a one-segment row's scatter block counts its own columns instead
+  // of the histogram kernel -- r06 A/B 0.2028 / 0.1997 vs 0.1988 / 0.1991 ms, profiles/r06_k2b_ab.jsonl)
+  const char* sce = std::getenv("GF_K2_SELFCOUNT");
+  const bool self_count = sce && *sce == '1';
+  // r06: one-segment rows sorted whole, each by one block with its output staged in LDS
+  // (radix_row_sort_kernel); GF_K2_ROWSORT=0 (A/B only) leaves them to the segment path
+  const char* rse = std::getenv("GF_K2_ROWSORT");
+  const bool rowsort = !(rse && *rse == '0') && !self_count && kRowSeg <= radix_row_sort_cap();
+  a.multiseg = rowsort ? U32(o_flag) : nullptr;  // zeroed by pass A's histogram
   // pass A: row keys -> k0 with the histogram of rows, scan, stable scatter by row
   a.kout = U32(o_k0);
   a.shift = kRadixMaxBits;
@@ -578,19 +588,22 @@ static int bucket_rows(gf_ctx* ctx, const gf_grid* g, const gf_points* pts, uint
   b.M = U32(o_mb);
   b.Ms = U32(o_msb);
   b.cstart = cell_start;
-  // (GF_K2_SELFCOUNT=1, A/B only: a one-segment row's scatter block counts its own columns instead
-  // of the histogram kernel -- r06 A/B 0.2028 / 0.1997 vs 0.1988 / 0.1991 ms, profiles/r06_k2b_ab.jsonl)
-  const char* sce = std::getenv("GF_K2_SELFCOUNT");
-  b.self_count = sce && *sce == '1';
-  // r06: one-segment rows sorted whole, each by one block with its output staged in LDS
-  // (radix_row_sort_kernel); GF_K2_ROWSORT=0 (A/B only) leaves them to the segment path
-  const char* rse = std::getenv("GF_K2_ROWSORT");
-  b.rowsort = !(rse && *rse == '0') && !b.self_count && kRowSeg <= radix_row_sort_cap();
-  if (b.rowsort) GF_HIP_CHECK(ctx, launch_radix(ctx, 4, b, g->n + 1));
-  GF_HIP_CHECK(ctx, launch_radix(ctx, 3, b, (int)ub));
-  if ((st = lookback_state(ctx, scan1_blocks(matB), &es))) return st;
-  GF_HIP_CHECK(ctx, launch_scan1(ctx->stream, U32(o_mb), matB, U32(o_msb), nullptr, 0, 0, es));
-  ctx->expand_base += (unsigned long long)scan1_blocks(matB);
+  b.self_count = self_count;
+  b.rowsort = rowsort;
+  if (b.rowsort) {
+    // the rows sorted whole (blocks 0 .. gn) and the multi-segment rows' column histograms --
+    // in one launch (the blocks past the rows) or, GF_K2_MERGE=0 (A/B), a histogram launch of their
+    // own; the multi-segment rows' scatter blocks scan their own row's counts (no scan launch)
+    const char* me = std::getenv("GF_K2_MERGE");
+    const bool merge = !(me && *me == '0');
+    GF_HIP_CHECK(ctx, launch_radix(ctx, 4, b, g->n + 1 + (merge ? (int)ub : 0)));
+    if (!merge) GF_HIP_CHECK(ctx, launch_radix(ctx, 3, b, (int)ub));
+  } else {
+    GF_HIP_CHECK(ctx, launch_radix(ctx, 3, b, (int)ub));
+    if ((st = lookback_state(ctx, scan1_blocks(matB), &es))) return st;
+    GF_HIP_CHECK(ctx, launch_scan1(ctx->stream, U32(o_mb), matB, U32(o_msb), nullptr, 0, 0, es));
+    ctx->expand_base += (unsigned long long)scan1_blocks(matB);
+  }
   GF_HIP_CHECK(ctx, launch_radix(ctx, 1, b, (int)ub));
   return GF_OK;
 }

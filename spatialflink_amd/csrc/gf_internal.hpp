@@ -363,6 +363,9 @@ struct RadixArgs {
   const uint16_t* kin16;
   int32_t self_count;       // pass B: a one-segment row's scatter block counts its columns (no histogram read)
   int32_t rowsort;          // pass B: one-segment rows sorted whole by radix_row_sort_kernel (the others by segments)
+  // rowsort: a device word, zeroed by pass A's histogram, set by the row sort when some row has
+  // several segments; pass B's segment kernels (and its scan) return at once while it is 0
+  uint32_t* multiseg;
 };
 // scatter block size: 1024 threads (one 8192-point tile per block, one block per CU) or 512
 // (4096-point tiles, two blocks per CU: one block's LDS phases overlap the other's memory);
@@ -403,7 +406,7 @@ int64_t expand_blocks(int64_t words);
 // in / out / out2 16-byte aligned.
 int64_t scan1_blocks(int64_t L);
 hipError_t launch_scan1(hipStream_t s, uint32_t* in, int64_t L, uint32_t* out, uint32_t* out2, int64_t n2, int64_t nz,
-                        const ExpandState& st);
+                        const ExpandState& st, const uint32_t* skip_if_zero = nullptr);
 hipError_t launch_expand_bitmap_async(hipStream_t s, const uint64_t* bitmap, int64_t words, int64_t n, uint32_t* idx,
                                       int64_t cap, int64_t* count, const ExpandState& st);
 // a batch of windows (gf_range_run_batch): window w's expansion owns tickets [tile0[w], tile0[w+1])

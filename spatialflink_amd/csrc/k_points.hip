@@ -191,7 +191,7 @@ struct RowSeg {
   uint32_t total;             // segments of all rows (blocks >= total: none)
   uint32_t wsum[16];
 };
-__device__ __forceinline__ void row_segment(const RadixArgs& a, RowSeg& rs) {
+__device__ __forceinline__ void row_segment(const RadixArgs& a, RowSeg& rs, uint32_t b) {
   // rows t * RPT .. t * RPT + RPT - 1 per thread (RPT = 2 for 256-thread blocks, else 1)
   const uint32_t t = threadIdx.x, lane = t & 63, wid = t >> 6, R = (uint32_t)a.gn + 1u;
   const uint32_t RPT = blockDim.x >= 512 ? 1u : 2u, nw = blockDim.x / 64;
@@ -221,7 +221,6 @@ __device__ __forceinline__ void row_segment(const RadixArgs& a, RowSeg& rs) {
     before += w < wid ? rs.wsum[w] : 0u;
     tot += rs.wsum[w];
   }
-  const uint32_t b = blockIdx.x;
 #pragma unroll
   for (uint32_t q = 0; q < 2; ++q) {
     const uint32_t r = t * RPT + q;
@@ -244,17 +243,21 @@ __device__ __forceinline__ void row_segment(const RadixArgs& a, RowSeg& rs) {
 // every row the (column, segment) entries are consecutive and column-major, rows in order, so
 // ONE exclusive scan of M gives every (row, column, segment) its first output position.  Blocks
 // past the segments zero their D entries (the scan covers the launch's bound).
-__global__ __launch_bounds__(kRadixThreads) void radix_seg_hist_kernel(RadixArgs a) {
+// (rowsort: launched inside radix_row_sort_kernel's grid -- blocks past the rows -- for the
+// multi-segment rows only; their scatter blocks scan their own row's entries, no global scan)
+__device__ __forceinline__ void seg_hist_block(const RadixArgs& a, uint32_t bid) {
   __shared__ uint32_t h[kRadixMaxDigits];
   __shared__ RowSeg rs;
   const uint32_t D = 1u << a.bits, mask = D - 1u;
   for (uint32_t j = threadIdx.x; j < D; j += kRadixThreads) h[j] = 0u;
-  row_segment(a, rs);
+  row_segment(a, rs, bid);
   if (rs.r == 0xFFFFFFFFu) {  // block-uniform
-    for (uint32_t d = threadIdx.x; d < D; d += kRadixThreads) a.M[(size_t)blockIdx.x * D + d] = 0u;
+    if (!a.rowsort)
+      for (uint32_t d = threadIdx.x; d < D; d += kRadixThreads) a.M[(size_t)bid * D + d] = 0u;
     return;
   }
-  if (rs.nseg == 1 && (a.self_count || a.rowsort)) {
+  if (rs.nseg == 1 && a.rowsort) return;  // sorted whole by radix_row_sort_kernel
+  if (rs.nseg == 1 && a.self_count) {
     // r06: a one-segment row (every row of a uniform 10M-point window on 500 x 500) is sorted by
     // its own scatter block, which counts its columns itself (radix_scatter_kernel): no histogram
     // read here.  Its entries only carry the row's total (column 0) so that the ONE scan of M still
@@ -279,6 +282,7 @@ __global__ __launch_bounds__(kRadixThreads) void radix_seg_hist_kernel(RadixArgs
   for (uint32_t d = threadIdx.x; d < D; d += kRadixThreads)
     a.M[(size_t)rs.base * D + (size_t)d * rs.nseg + rs.j] = h[d];
 }
+__global__ __launch_bounds__(kRadixThreads) void radix_seg_hist_kernel(RadixArgs a) { seg_hist_block(a, blockIdx.x); }
 
 // block b's chunk [beg, end) of the a.nblk chunks (whole tiles except the last)
 __device__ __forceinline__ void radix_chunk(const RadixArgs& a, int64_t& beg, int64_t& end) {
@@ -299,6 +303,7 @@ __global__ __launch_bounds__(kRadixThreads) void radix_hist_kernel(RadixArgs a) 
   __syncthreads();
   int64_t beg, end;
   radix_chunk(a, beg, end);
+  if (FIRST && a.multiseg && blockIdx.x == 0 && threadIdx.x == 0) *a.multiseg = 0u;  // (pass B's row sort sets it)
   if (FIRST) {
     // pass 0: two points per lane (16-B loads of x and y; chunks start at whole tiles, so pairs
     // are 16-B aligned), keys stored as uint2
@@ -383,8 +388,9 @@ __global__ __launch_bounds__(NT, MINW) void radix_scatter_kernel(RadixArgs a) {
   const uint64_t below = (1ull << lane) - 1ull;
   int64_t beg, end;
   if (a.seg > 0) {  // row mode pass B: a row segment; its columns' first slots; cells' starts
+    if (a.multiseg && *a.multiseg == 0u) return;  // grid-uniform: every row was sorted whole
     __shared__ RowSeg rs;
-    row_segment(a, rs);
+    row_segment(a, rs, blockIdx.x);
     if (rs.r == 0xFFFFFFFFu) return;  // block-uniform
     if (rs.nseg == 1 && a.rowsort) return;  // sorted whole by radix_row_sort_kernel
     beg = rs.beg;
@@ -428,6 +434,39 @@ __global__ __launch_bounds__(NT, MINW) void radix_scatter_kernel(RadixArgs a) {
         a.cstart[(size_t)a.gn * a.gn] = (uint32_t)beg;
         a.cstart[(size_t)a.gn * a.gn + 1] = (uint32_t)a.n;
       }
+    } else if (a.rowsort) {
+      // r06: the row's own (column, segment) counts scanned by this block (column-major, as the
+      // global scan would order them; the row starts at pass A's row total): every segment block of
+      // the row reads the row's D x nseg entries, so no scan launch sits between the histograms and
+      // this scatter
+      const uint32_t E = D * rs.nseg, per = (E + NT - 1) / NT, e0 = threadIdx.x * per;
+      const uint32_t* Mr = a.M + m0;
+      uint32_t run = 0;
+      for (uint32_t e = e0; e < e0 + per && e < E; ++e) run += Mr[e];
+      uint32_t inc = run;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = __shfl_up(inc, o, 64);
+        if (lane >= o) inc += t;
+      }
+      if (lane == 63) ws[w] = inc;
+      lds_barrier();
+      uint32_t before = a.MsA[(size_t)rs.r * a.nblkA] + inc - run;
+      for (int q = 0; q < w; ++q) before += ws[q];
+      for (uint32_t e = e0; e < e0 + per && e < E; ++e) {
+        const uint32_t d = e / rs.nseg, s = e - d * rs.nseg;
+        if (s == rs.j) gc[d] = before;
+        if (rs.j == 0 && s == 0) {  // the row's cells start at their columns' first slots
+          if (rs.r < (uint32_t)a.gn) {
+            if (d < (uint32_t)a.gn) a.cstart[(size_t)rs.r * a.gn + d] = before;
+          } else if (d == 0) {
+            a.cstart[(size_t)a.gn * a.gn] = before;
+            a.cstart[(size_t)a.gn * a.gn + 1] = (uint32_t)a.n;
+          }
+        }
+        before += Mr[e];
+      }
+      lds_barrier();
     } else {
       for (uint32_t d = threadIdx.x; d < D; d += NT) gc[d] = a.Ms[m0 + (size_t)d * rs.nseg + rs.j];
       if (rs.j == 0) {  // the row's cells start at their columns' first slots
@@ -592,10 +631,16 @@ __global__ __launch_bounds__(kRowSortNT, 4) void radix_row_sort_kernel(RadixArgs
   uint16_t* const wc = reinterpret_cast<uint16_t*>(out + kRowSortCap);     // [W][512] counts -> slots
   __shared__ uint32_t ws[kRowSortW];
   const uint32_t r = blockIdx.x;
-  if (r > (uint32_t)a.gn) return;  // block-uniform
+  if (r > (uint32_t)a.gn) {  // block-uniform: the multi-segment rows' column histograms
+    seg_hist_block(a, r - (uint32_t)a.gn - 1u);
+    return;
+  }
   const uint32_t lo = a.MsA[(size_t)r * a.nblkA], hi = a.MsA[(size_t)(r + 1) * a.nblkA];
   const uint32_t nr = hi - lo;
-  if (nr > (uint32_t)a.seg) return;  // a multi-segment row: radix_seg_hist / radix_scatter sort it
+  if (nr > (uint32_t)a.seg) {  // a multi-segment row: radix_seg_hist / radix_scatter sort it
+    if (threadIdx.x == 0 && a.multiseg) atomicOr(a.multiseg, 1u);
+    return;
+  }
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const uint64_t below = (1ull << lane) - 1ull;
   const uint32_t per = (nr + kRowSortW - 1) / kRowSortW;  // <= 64 * kRowSortU
@@ -1105,11 +1150,13 @@ int64_t scan1_blocks(int64_t L) { return (L + kScan1Tile - 1) / kScan1Tile; }
 
 __global__ __launch_bounds__(kScanThreads) void scan1_kernel(uint32_t* __restrict__ in, int64_t L,
                                                              uint32_t* __restrict__ out, uint32_t* __restrict__ out2,
-                                                             int64_t n2, int64_t nz, ExpandState st) {
+                                                             int64_t n2, int64_t nz, ExpandState st,
+                                                             const uint32_t* __restrict__ skip_if_zero) {
   __shared__ unsigned long long s_bid, s_prefix;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  if (threadIdx.x == 0) s_bid = atomicAdd(st.ticket, 1ull) - st.base;
+  if (threadIdx.x == 0) s_bid = atomicAdd(st.ticket, 1ull) - st.base;  // (every block takes its ticket)
   __syncthreads();
+  if (skip_if_zero && *skip_if_zero == 0u) return;  // grid-uniform: nothing to scan (K2 pass B, no multi-segment row)
   const uint64_t bid = s_bid;
   const int64_t base = (int64_t)bid * kScan1Tile + (int64_t)threadIdx.x * kScan1Items;
   uint32_t v[kScan1Items];
@@ -1198,10 +1245,10 @@ __global__ __launch_bounds__(kScanThreads) void scan1_kernel(uint32_t* __restric
 }
 
 hipError_t launch_scan1(hipStream_t s, uint32_t* in, int64_t L, uint32_t* out, uint32_t* out2, int64_t n2, int64_t nz,
-                        const ExpandState& st) {
+                        const ExpandState& st, const uint32_t* skip_if_zero) {
   if (L <= 0) return hipMemsetAsync(out, 0, sizeof(uint32_t), s);
   hipLaunchKernelGGL(scan1_kernel, dim3((unsigned)scan1_blocks(L)), dim3(kScanThreads), 0, s, in, L, out, out2, n2, nz,
-                     st);
+                     st, skip_if_zero);
   return hipGetLastError();
 }
 
