@@ -57,3 +57,8 @@ extern "C" void geojson_core_parse(const char* buf, const int64_t* off, int64_t 
     oe[j] = o.f_obj.e;
   }
 }
+
+// The wave-per-line scan's byte classes (gf_geojson.hpp wave_class), for a CPU check of the table.
+extern "C" void geojson_core_wave_classes(uint32_t* out) {
+  for (int b = 0; b < 256; ++b) out[b] = gf::wave_class(b);
+}

@@ -110,3 +110,33 @@ def test_property_name_lengths(core, oracle_mod, obj_name, ts_name):
             ln = ln.replace(b'"properties":{', b'"properties":{"' + decoy_o + b'":"decoy","' + decoy_t + b'":7,', 1)
         out.append(ln)
     compare(core, oracle_mod, out, props=(obj_name, ts_name))
+
+
+def test_wave_scan_byte_classes(core):
+    """The wave-per-line scan's per-byte table (gf_geojson.hpp wave_class; k_csv.hip geo_wave_scan)
+    restated from the JSON lexical rules: every byte in exactly one class, the element it starts
+    outside strings, and the number-token sub-flags."""
+    import ctypes as C
+    out = (C.c_uint32 * 256)()
+    core.geojson_core_wave_classes(out)
+    WB = dict(Q=1, BAD=2, WSC=4, OTH=8, OB=16, CB=32, OA=64, CA=128, CO=256, CM=512, TOK=1024, DOT=2048, E=4096)
+    WT = dict(NONE=0, OB=1, OA=2, CB=3, CA=4, CO=5, CM=6, SK=7, SV=8, TK=9)
+    tok = set(b"0123456789abcdefghijklmnopqrstuvwxyzABCDEFGHIJKLMNOPQRSTUVWXYZ+-.")
+    single = {ord("{"): ("OB", "OB"), ord("}"): ("CB", "CB"), ord("["): ("OA", "OA"), ord("]"): ("CA", "CA"),
+              ord(":"): ("CO", "CO"), ord(","): ("CM", "CM"), ord('"'): ("Q", "SV")}
+    for b in range(256):
+        f, t = out[b] & 0xFFFFFF, out[b] >> 24
+        if b in single:
+            exp_f, exp_t = WB[single[b][0]], WT[single[b][1]]
+        elif b == ord(" "):
+            exp_f, exp_t = 0, 0
+        elif b in (9, 10, 13):
+            exp_f, exp_t = WB["WSC"], 0
+        elif b == ord("\\") or b < 0x20 or b >= 0x80:
+            exp_f, exp_t = WB["BAD"], 0
+        elif b in tok:
+            exp_f = WB["TOK"] | (WB["DOT"] if b == ord(".") else 0) | (WB["E"] if b in b"eE" else 0)
+            exp_t = WT["TK"]
+        else:
+            exp_f, exp_t = WB["OTH"], 0
+        assert (f, t) == (exp_f, exp_t), (b, f, t, exp_f, exp_t)
