@@ -197,7 +197,7 @@ constexpr int kScatThreads = 1024;
 constexpr int kHistSplit = 2;  // histogram chunks per scatter block
 // points per write-combining tile: 6144 where the row arrays leave room in LDS (6-point row
 // runs at C4's 1000 rows: scatter 121 -> 110 us), else 4096
-constexpr int kScatTileBig = 6144, kScatTileSmall = 4096;
+constexpr int kScatTileBig = 7168, kScatTileSmall = 4096;
 
 __device__ __forceinline__ int32_t clamp_key(int32_t c, int32_t qn) { return (c < -1 ? -1 : (c > qn ? qn : c)) + 1; }
 
@@ -298,7 +298,7 @@ __global__ __launch_bounds__(kScatThreads) void join_hist_kernel(JoinRowArgs a, 
 // same runs.  Destinations: the block's run start of each row (the matrix scan, minus `base`)
 // advanced tile by tile.
 size_t join_scatter_lds_bytes(int32_t nrows, int tile) {
-  return (size_t)tile * (16 + 4 + 4) + 2 * 4 * (size_t)nrows + 4 * (kScatThreads / 64);
+  return (size_t)tile * (16 + 2 + 2) + 2 * 4 * (size_t)nrows + 4 * (kScatThreads / 64);
 }
 int join_scatter_tile(int32_t nrows) {
   return join_scatter_lds_bytes(nrows, kScatTileBig) <= 160 * 1024 ? kScatTileBig : kScatTileSmall;
@@ -310,10 +310,13 @@ __device__ __forceinline__ void wc_row_scatter(const double* X, const double* Y,
                                                uint32_t* oidx, RowF rowf) {
   constexpr int kScatPer = kScatTile / kScatThreads;
   extern __shared__ __attribute__((aligned(16))) char sm[];
+  // per slot (r06: 20 B, was 24): the point, its tile-local input position, its row -- the
+  // destination is gd[row] + slot at write-out -- so a tile holds 7168 points instead of 6144
+  // (longer row runs: fewer partial lines per point written)
   double2* const sxy = reinterpret_cast<double2*>(sm);
-  uint32_t* const sidx = reinterpret_cast<uint32_t*>(sxy + kScatTile);
-  uint32_t* const sdst = sidx + kScatTile;
-  uint32_t* const th = sdst + kScatTile;  // [nrows] tile counts -> starts -> ends
+  uint16_t* const sloc = reinterpret_cast<uint16_t*>(sxy + kScatTile);
+  uint16_t* const srow = sloc + kScatTile;
+  uint32_t* const th = reinterpret_cast<uint32_t*>(srow + kScatTile);  // [nrows] tile counts -> starts -> ends
   uint32_t* const gd = th + nrows;        // [nrows] next global slot of the row (tile-local: minus start)
   uint32_t* const wsum = gd + nrows;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -382,17 +385,18 @@ __device__ __forceinline__ void wc_row_scatter(const double* X, const double* Y,
       if (row[u] < 0) continue;
       const uint32_t slot = atomicAdd(&th[row[u]], 1u);
       sxy[slot] = make_double2(x[u], y[u]);
-      sidx[slot] = (uint32_t)(t0 + threadIdx.x + u * kScatThreads);
-      sdst[slot] = gd[row[u]] + slot;
+      sloc[slot] = (uint16_t)(threadIdx.x + u * kScatThreads);
+      srow[slot] = (uint16_t)row[u];
     }
     lds_barrier();
 #ifndef GF_SCAT_EXP_NOSTORE  // experiment build: the tile is placed in LDS but not written out
     for (uint32_t k = threadIdx.x; k < kept; k += kScatThreads) {
-      const uint32_t d = sdst[k];
+      const uint32_t d = gd[srow[k]] + k;
       oxy[d] = sxy[k];
-      oidx[d] = sidx[k];
+      oidx[d] = (uint32_t)t0 + sloc[k];
     }
 #endif
+    lds_barrier();  // (the write-out read gd of any row)
     for (int r = r0; r < r0 + per && r < nrows; ++r) {  // th[r] = tile end of the row
       gd[r] += th[r];
       th[r] = 0u;
