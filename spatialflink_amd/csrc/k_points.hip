@@ -615,7 +615,8 @@ __global__ __launch_bounds__(NT, MINW) void radix_scatter_kernel(RadixArgs a) {
 // at slot + its rank, and the row is written out contiguously.  The tile scatter
 // (radix_scatter_kernel) wrote ~8-point column runs per 4096-point tile (partial lines, written
 // by blocks of every XCD) and scanned 4096 counts per tile.  r06 A/B (profiles/r06_k2c_ab.jsonl):
-// the window 0.189 vs 0.196-0.202 ms.  Measured and not kept: the permutation stored straight from
+// the window 0.189 vs 0.196-0.202 ms (0.170-0.172 once pass B's empty launches went: the
+// multiseg flag, the segment histograms as extra blocks of this launch).  Measured and not kept: the permutation stored straight from
 // the registers into the row's range (no staging: 24 KB of LDS, two 768-thread blocks per CU,
 // every row in one round) 120 vs 61 us -- the scattered 4-B stores cost more than the second
 // round of blocks; the steps' counts taken with LDS atomics, broadcast after the last step (no
